@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Benchmark: decoded values/s + GiB/s on device-resident int64 RLE_DICTIONARY pages
+(BASELINE.json configs[1]: 100M rows, 1k-cardinality dictionary, Zipf(1.5) run
+lengths truncated to [1, 4096], parquet-mr V1 pages of 20,000 values, uncompressed).
+
+A step = one decode of the whole 100M-value column chunk (5,000 pages) already
+resident in HBM, into a dense int64 column in HBM. With --gpus N (torch.distributed
+launcher) every rank decodes its own 100M-row row group (row groups shard
+one-per-GPU, no data-path collective: weak scaling); value = all ranks' values /
+max-over-ranks time.
+
+Prints ONE JSON line on rank 0. Extra objects: "roofline" (dominant kernel
+k_dict<8>, HBM-bound) and "cpu_baseline" (the oracle's value-at-a-time port of
+the reference reader, 1 thread, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "parquet-mr_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec)
+
+
+def make_c2(n_rows, seed_dict=42, seed_runs=43, a=1.5, card=1000, max_run=4096, page_rows=20000):
+    """Config 2 input: the dictionary column as parquet-mr would write it."""
+    from pqgpu import abi, writer
+    rng_d = np.random.default_rng(seed_dict)
+    dict_vals = rng_d.integers(-2**63, 2**63 - 1, size=card, dtype=np.int64, endpoint=True)
+    rng = np.random.default_rng(seed_runs)
+    runs = []
+    total = 0
+    while total < n_rows:
+        r = np.minimum(rng.zipf(a, size=1 << 20), max_run)
+        runs.append(r)
+        total += int(r.sum())
+    runs = np.concatenate(runs)
+    run_ids = rng.integers(0, card, size=runs.size)
+    cut = np.searchsorted(np.cumsum(runs), n_rows)
+    runs, run_ids = runs[:cut + 1], run_ids[:cut + 1]
+    ids = np.repeat(run_ids, runs)[:n_rows]
+    ids_fa, order = writer.first_appearance_ids(ids)
+    chunk = writer.write_dict_column_from_ids(abi.INT64, dict_vals[order], ids_fa, page_rows=page_rows)
+    return chunk, dict_vals, ids
+
+
+def cpu_baseline(batch, n_values, budget_s):
+    """The oracle (value-at-a-time C port of RunLengthBitPackingHybridDecoder.readInt ->
+    Dictionary.decodeToLong, 1 thread) on the same pages, repeated for ~budget_s."""
+    sys.path.insert(0, REPO)
+    from oracle import pqref
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        r = pqref.decode_batch(batch)
+        assert r.code == 0
+        reps += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": reps * n_values / dt, "unit": "values/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} x full {n_values / 1e6:.0f}M-value chunk ({batch.n_pages} pages), "
+                      f"{dt:.1f} s, oracle/pqref.c -O3, single thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--zipf", type=float, default=1.5)
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--verify", action="store_true", default=True)
+    ap.add_argument("--e2e", action="store_true", help="also time the host-bytes-in / host-array-out path")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from pqgpu import decoder as D, writer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    t_gen = time.perf_counter()
+    # each rank owns one row group: same dictionary seed, its own run stream
+    chunk, dict_vals, ids = make_c2(args.rows, seed_runs=43 + 1000 * rank, a=args.zipf)
+    batch = writer.build_batch([chunk])
+    t_gen = time.perf_counter() - t_gen
+    data_bytes = int(sum(len(p.body) for p in chunk.pages))
+
+    dec = D.Decoder(local)
+    dbatch = dec.upload(batch)
+    cols = dec.alloc_columns(batch)
+    plan = dec.plan(dbatch, cols)
+    stream = dec.stream
+    for _ in range(args.warmup):
+        plan.launch()
+    rc, st = plan.sync()
+    assert rc == 0, st.message
+    if args.verify:
+        got = cols[0].typed()
+        exp = torch.from_numpy(dict_vals[ids]).to(got.device)
+        assert torch.equal(got, exp), "decoded column differs from the generated values"
+        del exp
+
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        ev[0].record(stream)
+        for k in range(args.steps):
+            plan.launch()
+            ev[k + 1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    rc, st = plan.sync()
+    assert rc == 0, st.message
+    per_launch_ms = [ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)]
+    gpu_ms = sum(per_launch_ms)
+    t = torch.tensor([gpu_ms / 1e3, wall], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = float(t[0].item())
+
+    n = args.rows
+    total_values = n * world * args.steps
+    value = total_values / t_max
+    ms_per_step = t_max * 1e3 / args.steps
+    avg_launch_s = float(np.mean(per_launch_ms)) / 1e3
+    algo_bytes = n * 8 + data_bytes  # per launch: int64 out + encoded data-page bytes read
+    achieved = algo_bytes / avg_launch_s / 1e9
+
+    e2e = None
+    if args.e2e and rank == 0:
+        t1 = time.perf_counter()
+        rc2, st2, res, _ = dec.decode_host(batch)
+        e2e_s = time.perf_counter() - t1
+        assert rc2 == 0
+        e2e = {"values_per_s": n / e2e_s, "seconds": e2e_s}
+
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(batch, n, args.cpu_budget)
+
+    if rank == 0:
+        out = {
+            "metric": "decoded values/s, device-resident int64 RLE_DICTIONARY pages",
+            "value": value,
+            "unit": "values/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic",
+            "config": {"workload": "C2: int64 RLE_DICTIONARY, 1k-cardinality dictionary (w=10), "
+                                   f"Zipf(a={args.zipf}) run lengths in [1,4096], parquet-mr V1 pages of 20,000 values, "
+                                   "uncompressed, one 100M-row row group per GPU",
+                       "rows_per_gpu": n, "pages_per_gpu": batch.n_pages, "encoded_data_bytes_per_gpu": data_bytes,
+                       "parallelism": f"row-group shard x{world}"},
+            "gib_per_s": value * 8 / 2**30,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "pqg::k_dict<8>", "algorithmic_bytes_per_launch": algo_bytes,
+                         "avg_launch_ms": avg_launch_s * 1e3},
+            "cpu_baseline": cpu,
+            "input_gen_s": t_gen,
+        }
+        if e2e:
+            out["e2e_host_path"] = e2e
+        print(json.dumps(out), flush=True)
+    plan.close()
+    dec.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,236 @@
+/*
+ * pqgpu.h — C ABI of the MI355X-native Parquet column-page decoder.
+ *
+ * This is the drop-in boundary for parquet-mr's page-decode hot path
+ * (SURVEY.md §8b). Every entry point uses plain C types: pointers and sizes,
+ * no C++ or torch types. A JNI shim binds it the way
+ * parquet-mr would bind a native ValuesReader / ParquetReadRouter backend.
+ *
+ * Reference interfaces replaced (apache/parquet-mr 1.15.0-SNAPSHOT):
+ *   - ValuesReader.initFromPage / readX
+ *     parquet-column/src/main/java/org/apache/parquet/column/values/ValuesReader.java:36-203
+ *     -> pqg_decode (many pages per call; dense values + levels per column)
+ *   - ColumnReaderBase.readPageV1 / readPageV2 / newRLEIterator (page split, levels)
+ *     parquet-column/src/main/java/org/apache/parquet/column/impl/ColumnReaderBase.java:738-789
+ *     -> pqg_decode (levels decoded on device, data section located on device)
+ *   - Encoding.getValuesReader / getDictionaryBasedValuesReader / initDictionary
+ *     parquet-column/src/main/java/org/apache/parquet/column/Encoding.java:61-320
+ *     -> the (physical_type, encoding) dispatch inside pqg_decode
+ *   - ParquetReadRouter.read(bitWidth, in, currentCount, int[] out)
+ *     parquet-plugins/parquet-encoding-vector/src/main/java/org/apache/parquet/column/values/bitpacking/ParquetReadRouter.java:57-66
+ *     -> pqg_unpack_runs (device batch) / pqg_router_read (host buffers)
+ *
+ * Threading: a pqg_ctx owns one HIP stream and its device scratch; it is not
+ * shared between threads (one ctx per thread per GPU), like a ValuesReader.
+ * All pqg_decode / pqg_plan_launch work is asynchronous on the ctx stream
+ * until pqg_sync. No exception crosses this ABI: every function returns a
+ * pqg_error code and fills an optional pqg_status.
+ */
+#ifndef PQGPU_H
+#define PQGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PQG_ABI_VERSION 1
+
+/* parquet-format `Type` values (parquet.thrift). */
+enum pqg_physical_type {
+  PQG_BOOLEAN = 0,
+  PQG_INT32 = 1,
+  PQG_INT64 = 2,
+  PQG_INT96 = 3,
+  PQG_FLOAT = 4,
+  PQG_DOUBLE = 5,
+  PQG_BYTE_ARRAY = 6,
+  PQG_FIXED_LEN_BYTE_ARRAY = 7
+};
+
+/* parquet-format `Encoding` values (parquet.thrift); see Encoding.java:61-253. */
+enum pqg_encoding {
+  PQG_PLAIN = 0,
+  PQG_PLAIN_DICTIONARY = 2,
+  PQG_RLE = 3,
+  PQG_BIT_PACKED = 4,
+  PQG_DELTA_BINARY_PACKED = 5,
+  PQG_DELTA_LENGTH_BYTE_ARRAY = 6,
+  PQG_DELTA_BYTE_ARRAY = 7,
+  PQG_RLE_DICTIONARY = 8,
+  PQG_BYTE_STREAM_SPLIT = 9
+};
+
+/*
+ * Error codes. Each decode error names the Java exception the reference
+ * reader raises for the same bytes, so the JNI shim can rethrow it as
+ * ParquetDecodingException (io/ParquetDecodingException.java) with the same
+ * meaning. The first failing (page, value index) in page order is reported,
+ * which is the value at which the reference's lazy reader would throw.
+ */
+enum pqg_error {
+  PQG_OK = 0,
+  PQG_ERR_INVALID_ARG = 1,      /* API misuse (null pointer, bad count, capacity too small) */
+  PQG_ERR_UNSUPPORTED = 2,      /* (type, encoding) has no reader: Encoding.java:84,193; UnsupportedOperationException */
+  PQG_ERR_HIP = 3,              /* HIP runtime failure */
+  PQG_ERR_NO_DEVICE = 4,        /* no HIP device / extension unusable */
+  PQG_ERR_EOF = 10,             /* java.io.EOFException: read past the end of a page section
+                                   (SingleBufferInputStream.read :50-55, LittleEndianDataInputStream.readInt/readLong) */
+  PQG_ERR_RLE_PAST_END = 11,    /* IllegalArgumentException "Reading past RLE/BitPacking stream."
+                                   (RunLengthBitPackingHybridDecoder.java:81) */
+  PQG_ERR_BIT_WIDTH = 12,       /* IllegalArgumentException "bitWidth must be >= 0 and <= 32"
+                                   (RunLengthBitPackingHybridDecoder.java:55) */
+  PQG_ERR_DICT_ID = 13,         /* ArrayIndexOutOfBoundsException in Dictionary.decodeToX
+                                   (PlainValuesDictionary.java:159-161 etc.) */
+  PQG_ERR_EMPTY_PAGE = 14,      /* IOException "Attempt to read from empty page" (DictionaryValuesReader.java:57-62) */
+  PQG_ERR_EMPTY_PACKED_RUN = 15,/* bit-packed run header with 0 groups: AIOOBE on currentBuffer[] (:71) */
+  PQG_ERR_DELTA_CONFIG = 16,    /* IllegalArgumentException "miniBlockSize must be multiple of 8"
+                                   (DeltaBinaryPackingConfig.java:39) */
+  PQG_ERR_DELTA_PAST_END = 17,  /* ParquetDecodingException "no more value to read, total value count is N"
+                                   (DeltaBinaryPackingValuesReader.java:115-119) */
+  PQG_ERR_CORRUPT = 18,         /* section lengths inconsistent with the page (negative/oversized length prefix) */
+  PQG_ERR_NO_DICTIONARY = 19,   /* "could not read page ... as the dictionary was missing" (ColumnReaderBase.java:709-712) */
+  PQG_ERR_DICT_ENCODING = 20    /* "Dictionary data encoding type not supported" (PlainValuesDictionary.java:49-52) */
+};
+
+/*
+ * One data page, already decompressed, located inside the batch byte buffer.
+ * Mirrors DataPageV1 (DataPageV1.java:26-141) and DataPageV2 (DataPageV2.java:26-247).
+ */
+typedef struct pqg_page_desc {
+  uint64_t offset;         /* byte offset of the page body in the batch buffer (16-B aligned is fastest) */
+  uint32_t size;           /* page body length in bytes (V1: rl + dl + data sections; V2: rl + dl + data) */
+  uint32_t num_values;     /* header num_values: level slots including nulls */
+  int32_t column;          /* index into the pqg_column_desc table */
+  int32_t version;         /* 1 = DataPageV1, 2 = DataPageV2 */
+  int32_t encoding;        /* value encoding (pqg_encoding) */
+  int32_t rl_encoding;     /* V1 only: RLE or BIT_PACKED (ignored when max_rep == 0) */
+  int32_t dl_encoding;     /* V1 only: RLE or BIT_PACKED (ignored when max_def == 0) */
+  uint32_t rl_byte_length; /* V2 only: repetition_levels_byte_length */
+  uint32_t dl_byte_length; /* V2 only: definition_levels_byte_length */
+  uint32_t reserved;
+} pqg_page_desc;
+
+/*
+ * One column chunk: the ColumnDescriptor facts the decoder needs (physical
+ * type, type length, max rep/def level), its dictionary page (optional) and
+ * where its decoded output goes.
+ *
+ * Output layout (Java-equivalent "dense" form): `values` receives only the
+ * non-null values, in slot order, exactly the sequence the reference's
+ * ValuesReader returns for slots with dl == max_def (ColumnReaderBase.java:650-676).
+ * `def_levels` / `rep_levels` receive one byte per slot (the Java int level;
+ * level values above 255 are stored saturated to 255 and therefore never
+ * equal max_def, which is limited to <= 254). Element widths: INT32/FLOAT 4,
+ * INT64/DOUBLE 8, INT96 12, FIXED_LEN_BYTE_ARRAY type_length, BOOLEAN 1.
+ * For pqg_decode these are device pointers; the per-page value counts are
+ * written to `page_value_counts` (device, one uint32 per page of the batch, optional).
+ */
+typedef struct pqg_column_desc {
+  int32_t physical_type;     /* pqg_physical_type */
+  int32_t type_length;       /* FIXED_LEN_BYTE_ARRAY length */
+  int32_t max_rep;           /* ColumnDescriptor.getMaxRepetitionLevel() */
+  int32_t max_def;           /* ColumnDescriptor.getMaxDefinitionLevel() */
+  int64_t dict_offset;       /* byte offset of the dictionary page body in the batch buffer, -1 if none */
+  uint32_t dict_size;        /* dictionary page body bytes */
+  uint32_t dict_num_values;  /* DictionaryPageHeader.num_values */
+  int32_t dict_encoding;     /* PLAIN or PLAIN_DICTIONARY */
+  int32_t reserved0;
+  void* values;              /* dense output values */
+  uint64_t values_capacity;  /* capacity in elements */
+  uint8_t* def_levels;       /* per-slot definition levels (may be NULL) */
+  uint8_t* rep_levels;       /* per-slot repetition levels (may be NULL) */
+  uint64_t levels_capacity;  /* capacity in slots */
+  uint8_t* binary_data;      /* BYTE_ARRAY only: value bytes; `values` then holds int64 offsets[n+1] */
+  uint64_t binary_capacity;  /* BYTE_ARRAY only: capacity of binary_data in bytes */
+  uint64_t values_written;   /* OUT (after pqg_sync / host calls): non-null values decoded */
+} pqg_column_desc;
+
+/* First decode error of a call, in (page, value) order. */
+typedef struct pqg_status {
+  int32_t code;              /* pqg_error */
+  int32_t page;              /* index into the page table, -1 if not page-specific */
+  int64_t value_index;       /* value index inside the page (data values for value errors, slots for level errors) */
+  char message[240];
+} pqg_status;
+
+typedef struct pqg_ctx pqg_ctx;
+typedef struct pqg_plan pqg_plan;
+
+/* ---- context ------------------------------------------------------------ */
+
+/* Library / ABI version (PQG_ABI_VERSION). */
+int pqg_abi_version(void);
+
+/* Number of visible HIP devices (0 when none). */
+int pqg_device_count(void);
+
+/* Create a context on `device`. `hip_stream` may be NULL (the ctx creates its
+ * own non-blocking stream) or an existing hipStream_t to run on. */
+int pqg_ctx_create(int device, void* hip_stream, pqg_ctx** out);
+int pqg_ctx_destroy(pqg_ctx* ctx);
+/* The hipStream_t the ctx launches on. */
+void* pqg_ctx_stream(pqg_ctx* ctx);
+
+/* ---- device-resident batch decode ----------------------------------------
+ * `d_bytes` is a DEVICE buffer holding every page body (and dictionary page)
+ * the descriptors refer to, padded by at least 64 readable bytes after the
+ * last page. Column output pointers are DEVICE pointers. Pages of one column
+ * must appear in page order; pages of several columns may be interleaved.
+ * Asynchronous: errors are reported by pqg_sync. */
+int pqg_decode(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes,
+               pqg_column_desc* cols, int n_cols,
+               const pqg_page_desc* pages, int n_pages,
+               uint32_t* d_page_value_counts, pqg_status* st);
+
+/* Wait for all work on the ctx stream; returns the first decode error of the
+ * calls since the previous pqg_sync and fills cols[i].values_written for the
+ * most recent pqg_decode / plan launch. */
+int pqg_sync(pqg_ctx* ctx, pqg_status* st);
+
+/* ---- prepared plans (bench / steady-state) --------------------------------
+ * A plan uploads descriptors once; pqg_plan_launch re-runs the decode of the
+ * same page batch with no host work beyond the kernel launches. */
+int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes,
+                    const pqg_column_desc* cols, int n_cols,
+                    const pqg_page_desc* pages, int n_pages, pqg_plan** out, pqg_status* st);
+int pqg_plan_launch(pqg_plan* plan);
+/* Number of kernel launches one pqg_plan_launch issues, and the name of the dominant kernel. */
+int pqg_plan_kernel_count(pqg_plan* plan);
+int pqg_plan_destroy(pqg_plan* plan);
+
+/* ---- host-buffer decode (the JNI shim's entry: file bytes in, arrays out) --
+ * Copies `h_bytes` to the device through pinned staging (hipMemcpyAsync),
+ * decodes, and copies values / levels back into the HOST pointers of `cols`.
+ * Synchronous. */
+int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes,
+                    pqg_column_desc* cols, int n_cols,
+                    const pqg_page_desc* pages, int n_pages,
+                    uint32_t* h_page_value_counts, pqg_status* st);
+
+/* ---- ParquetReadRouter boundary --------------------------------------------
+ * Batch of bit-packed runs on the device: run r unpacks counts[r] (multiple of 8)
+ * LSB-first values of `bit_width` bits from d_in + in_offsets[r] into
+ * d_out + out_offsets[r] (int32). Bit-exact with Packer.LITTLE_ENDIAN
+ * BytePacker.unpack8Values (ByteBasedBitPackingGenerator.java:258-308). */
+int pqg_unpack_runs(pqg_ctx* ctx, int bit_width, const uint8_t* d_in,
+                    const uint64_t* d_in_offsets, const uint32_t* d_counts,
+                    const uint64_t* d_out_offsets, int32_t* d_out, int n_runs);
+
+/* ParquetReadRouter.read equivalent on host buffers: consumes
+ * count*bit_width/8 bytes of `in` (in_len must cover them, else PQG_ERR_EOF as
+ * SingleBufferInputStream.slice throws EOFException) and writes `count` ints.
+ * The unpack runs on the GPU (H2D, kernel, D2H); synchronous. */
+int pqg_router_read(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_len,
+                    int count, int32_t* out);
+
+/* Human-readable name of an error code. */
+const char* pqg_error_name(int code);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PQGPU_H */

@@ -1,0 +1,23 @@
+/* pqref.h — ORACLE (test infrastructure only): CPU restatement of parquet-mr's
+ * page readers. See pqref.c for the reference citations. Not part of the product. */
+#ifndef PQREF_H
+#define PQREF_H
+#include <stdint.h>
+#include "../include/pqgpu.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+int pqr_width_from_max_int(int32_t bound);
+void pqr_unpack8_int(int w, const uint8_t* in, int32_t* out);
+void pqr_unpack8_long(int w, const uint8_t* in, int64_t* out);
+int pqr_rle_decode(int bit_width, const uint8_t* buf, int64_t len, int64_t n, int32_t* out,
+                   int64_t* err_index, int64_t* consumed);
+int64_t pqr_router_read_batch(int bit_width, const uint8_t* in, int64_t in_len, int count, int32_t* out);
+int64_t pqr_delta_decode(const uint8_t* buf, int64_t len, int64_t* out, int64_t cap, int64_t* consumed);
+int pqr_decode(const uint8_t* bytes, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
+               const pqg_page_desc* pages, int n_pages, uint32_t* page_value_counts, pqg_status* st);
+const char* pqg_error_name_ref(int code);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,154 @@
+"""ORACLE binding — TEST INFRASTRUCTURE ONLY.
+
+ctypes wrapper around oracle/build/libpqref.so, the C restatement of
+parquet-mr's page readers (see pqref.c). Only tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg import this module; the product path never does.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_REPO = os.path.dirname(_HERE)
+sys.path.insert(0, os.path.join(_REPO, "parquet-mr_amd"))
+from pqgpu import abi  # noqa: E402  (struct layouts only)
+
+LIB_PATH = os.path.join(_HERE, "build", "libpqref.so")
+_LIB = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        vp, i64 = C.c_void_p, C.c_int64
+        L.pqr_width_from_max_int.argtypes = [C.c_int32]
+        L.pqr_unpack8_int.argtypes = [C.c_int, vp, vp]
+        L.pqr_unpack8_long.argtypes = [C.c_int, vp, vp]
+        L.pqr_rle_decode.argtypes = [C.c_int, vp, i64, i64, vp, C.POINTER(i64), C.POINTER(i64)]
+        L.pqr_rle_decode.restype = C.c_int
+        L.pqr_router_read_batch.argtypes = [C.c_int, vp, i64, C.c_int, vp]
+        L.pqr_router_read_batch.restype = i64
+        L.pqr_delta_decode.argtypes = [vp, i64, vp, i64, C.POINTER(i64)]
+        L.pqr_delta_decode.restype = i64
+        L.pqr_decode.argtypes = [vp, C.c_uint64, vp, C.c_int, vp, C.c_int, vp, C.POINTER(abi.Status)]
+        L.pqr_decode.restype = C.c_int
+        _LIB = L
+    return _LIB
+
+
+def _buf(b):
+    a = np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else b
+    return np.ascontiguousarray(a, dtype=np.uint8)
+
+
+def unpack8_int(w, data):
+    a = _buf(data)
+    out = np.zeros(8, dtype=np.int32)
+    lib().pqr_unpack8_int(w, a.ctypes.data, out.ctypes.data)
+    return out
+
+
+def unpack8_long(w, data):
+    a = _buf(data)
+    out = np.zeros(8, dtype=np.int64)
+    lib().pqr_unpack8_long(w, a.ctypes.data, out.ctypes.data)
+    return out
+
+
+def rle_decode(bit_width, data, n):
+    """n x RunLengthBitPackingHybridDecoder.readInt(). Returns (values, err, err_index, consumed)."""
+    a = _buf(data)
+    out = np.zeros(max(n, 1), dtype=np.int32)
+    ei, cons = C.c_int64(-1), C.c_int64(0)
+    rc = lib().pqr_rle_decode(bit_width, a.ctypes.data if len(a) else None, len(a), n, out.ctypes.data,
+                              C.byref(ei), C.byref(cons))
+    return out[:n], rc, ei.value, cons.value
+
+
+def router_read(bit_width, data, count):
+    """ParquetReadRouter.readBatch: returns (values, consumed) or raises EOFError."""
+    a = _buf(data)
+    out = np.zeros(max(count, 8), dtype=np.int32)
+    n = lib().pqr_router_read_batch(bit_width, a.ctypes.data if len(a) else None, len(a), count, out.ctypes.data)
+    if n < 0:
+        raise EOFError(abi.ERROR_NAMES.get(-n))
+    return out[:count], n
+
+
+def delta_decode(data, cap=1 << 22):
+    """DeltaBinaryPackingValuesReader.initFromPage + readLong x total. Returns (values, consumed) or (code, None)."""
+    a = _buf(data)
+    out = np.zeros(cap, dtype=np.int64)
+    cons = C.c_int64(0)
+    n = lib().pqr_delta_decode(a.ctypes.data if len(a) else None, len(a), out.ctypes.data, cap, C.byref(cons))
+    if n < 0:
+        return int(-n), None
+    return out[:n].copy(), cons.value
+
+
+class OracleResult:
+    def __init__(self, code, status, columns, page_value_counts):
+        self.code = code
+        self.status = status
+        self.columns = columns
+        self.page_value_counts = page_value_counts
+
+
+def decode_batch(batch, binary_capacity=None):
+    """Decode a writer.PageBatch with the oracle: per column dict(values, def_levels, rep_levels)."""
+    cols = (abi.ColumnDesc * max(1, len(batch.columns)))()
+    keep = []
+    for i, cd in enumerate(batch.columns):
+        c = cols[i]
+        for k, v in cd.items():
+            setattr(c, k, v)
+        n_slots = batch.column_slots[i]
+        n_cap = n_slots + 1
+        dt = abi.numpy_dtype(cd["physical_type"], cd["type_length"])
+        vals = np.zeros(n_cap + 1, dtype=dt)
+        dl = np.zeros(max(n_slots, 1), dtype=np.uint8)
+        rl = np.zeros(max(n_slots, 1), dtype=np.uint8)
+        keep += [vals, dl, rl]
+        c.values = vals.ctypes.data
+        c.values_capacity = n_cap + 1
+        c.def_levels = dl.ctypes.data if cd["max_def"] > 0 else None
+        c.rep_levels = rl.ctypes.data if cd["max_rep"] > 0 else None
+        c.levels_capacity = n_slots
+        if cd["physical_type"] == abi.BYTE_ARRAY:
+            cap = binary_capacity or int(len(batch.data))
+            bd = np.zeros(max(cap, 1), dtype=np.uint8)
+            keep.append(bd)
+            c.binary_data = bd.ctypes.data
+            c.binary_capacity = cap
+    counts = np.zeros(max(1, batch.n_pages), dtype=np.uint32)
+    st = abi.Status()
+    pages = np.ascontiguousarray(batch.pages)
+    rc = lib().pqr_decode(batch.data.ctypes.data, len(batch.data), C.addressof(cols), len(batch.columns),
+                          pages.ctypes.data if len(pages) else None, len(pages), counts.ctypes.data, C.byref(st))
+    out = []
+    for i, cd in enumerate(batch.columns):
+        n = int(cols[i].values_written)
+        res = {"n_values": n}
+        j = sum(4 if batch.columns[k]["physical_type"] == abi.BYTE_ARRAY else 3 for k in range(i))
+        vals, dl, rl = keep[j], keep[j + 1], keep[j + 2]
+        if cd["physical_type"] == abi.BYTE_ARRAY:
+            bd = keep[j + 3]
+            offs = vals[:n + 1] if n else np.zeros(1, dtype=np.int64)
+            res["values"] = [bd[offs[k]:offs[k + 1]].tobytes() for k in range(n)]
+            res["offsets"] = offs.copy()
+        else:
+            res["values"] = vals[:n].copy()
+        res["def_levels"] = dl[:batch.column_slots[i]].copy() if cd["max_def"] > 0 else None
+        res["rep_levels"] = rl[:batch.column_slots[i]].copy() if cd["max_rep"] > 0 else None
+        out.append(res)
+    return OracleResult(rc, st.as_tuple(), out, counts[:batch.n_pages].copy())

@@ -1,0 +1,688 @@
+// pqgpu_api.hip — the C ABI of include/pqgpu.h.
+//
+// Host work here is descriptor bookkeeping only (page tables, class lists,
+// prefix sums of header value counts, error resolution); every byte of page
+// data is decoded by the kernels in pqgpu_kernels.hip. There is no CPU decode
+// fallback: without a usable HIP device every entry point returns
+// PQG_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstddef>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "pqgpu_internal.h"
+
+using pqg::ColumnDev;
+using pqg::PageWork;
+
+namespace {
+
+const char* kNames[] = {"OK", "INVALID_ARG", "UNSUPPORTED", "HIP", "NO_DEVICE"};
+
+void set_status(pqg_status* st, int code, int page, int64_t idx, const char* what) {
+  if (!st) return;
+  st->code = code;
+  st->page = page;
+  st->value_index = idx;
+  std::snprintf(st->message, sizeof(st->message), "%s: %s (page %d, index %lld)", what, pqg_error_name(code), page,
+                (long long)idx);
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, n ? n : 16);
+    if (e == hipSuccess) cap = n ? n : 16;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(&p, n ? n : 16, hipHostMallocDefault);
+    if (e == hipSuccess) cap = n ? n : 16;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+int elem_width(int t, int tl) {
+  switch (t) {
+    case PQG_BOOLEAN: return 1;
+    case PQG_INT32: case PQG_FLOAT: return 4;
+    case PQG_INT64: case PQG_DOUBLE: return 8;
+    case PQG_INT96: return 12;
+    case PQG_FIXED_LEN_BYTE_ARRAY: return tl;
+    default: return 0;
+  }
+}
+
+// Kernel classes, in launch order after the level pass.
+enum Cls { C_DICT4 = 0, C_DICT8, C_PLAIN, C_BOOL, C_DELTA4, C_DELTA8, C_NCLS };
+
+struct HostErr {
+  int page;
+  int kind;  // 0 init, 2 value
+  int64_t index;
+  int code;
+};
+
+}  // namespace
+
+struct pqg_plan {
+  pqg_ctx* ctx = nullptr;
+  const uint8_t* d_bytes = nullptr;
+  uint64_t n_bytes = 0;
+  int n_pages = 0;
+  int n_cols = 0;
+  DevBuf work, cols, lists, col_pages, col_page_start, err, err_count;
+  std::vector<PageWork> h_work;
+  std::vector<int> cls_off, cls_n;  // into lists
+  int levels_off = 0, levels_n = 0;
+  int n_scan_cols = 0;
+  std::vector<int> page_cls;        // -1 if not launched
+  std::vector<uint8_t> col_nullable;
+  std::vector<uint64_t> col_required_values;
+  std::vector<HostErr> host_errs;
+  int kernels = 0;
+};
+
+struct pqg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  pqg_plan* last = nullptr;          // plan of the most recent pqg_decode (owned)
+  pqg_plan* last_launched = nullptr; // plan of the most recent launch (decode or plan_launch)
+  pqg_column_desc* last_cols = nullptr;
+  PinnedBuf pin_in, pin_out, pin_err;
+  DevBuf host_bytes, host_out, host_counts, host_runs;
+};
+
+extern "C" {
+
+int pqg_abi_version(void) { return PQG_ABI_VERSION; }
+
+const char* pqg_error_name(int code) {
+  switch (code) {
+    case PQG_OK: case PQG_ERR_INVALID_ARG: case PQG_ERR_UNSUPPORTED: case PQG_ERR_HIP: case PQG_ERR_NO_DEVICE:
+      return kNames[code];
+    case PQG_ERR_EOF: return "EOF";
+    case PQG_ERR_RLE_PAST_END: return "RLE_PAST_END";
+    case PQG_ERR_BIT_WIDTH: return "BIT_WIDTH";
+    case PQG_ERR_DICT_ID: return "DICT_ID";
+    case PQG_ERR_EMPTY_PAGE: return "EMPTY_PAGE";
+    case PQG_ERR_EMPTY_PACKED_RUN: return "EMPTY_PACKED_RUN";
+    case PQG_ERR_DELTA_CONFIG: return "DELTA_CONFIG";
+    case PQG_ERR_DELTA_PAST_END: return "DELTA_PAST_END";
+    case PQG_ERR_CORRUPT: return "CORRUPT";
+    case PQG_ERR_NO_DICTIONARY: return "NO_DICTIONARY";
+    case PQG_ERR_DICT_ENCODING: return "DICT_ENCODING";
+    default: return "UNKNOWN";
+  }
+}
+
+int pqg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int pqg_ctx_create(int device, void* hip_stream, pqg_ctx** out) {
+  if (!out) return PQG_ERR_INVALID_ARG;
+  *out = nullptr;
+  int n = pqg_device_count();
+  if (n <= 0) return PQG_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return PQG_ERR_INVALID_ARG;
+  if (hipSetDevice(device) != hipSuccess) return PQG_ERR_HIP;
+  pqg_ctx* c = new (std::nothrow) pqg_ctx();
+  if (!c) return PQG_ERR_INVALID_ARG;
+  c->device = device;
+  if (hip_stream) {
+    c->stream = (hipStream_t)hip_stream;
+  } else {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete c;
+      return PQG_ERR_HIP;
+    }
+    c->own_stream = true;
+  }
+  *out = c;
+  return PQG_OK;
+}
+
+void* pqg_ctx_stream(pqg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int pqg_plan_destroy(pqg_plan* p);
+
+int pqg_ctx_destroy(pqg_ctx* c) {
+  if (!c) return PQG_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (c->last) pqg_plan_destroy(c->last);
+  c->pin_in.release();
+  c->pin_out.release();
+  c->pin_err.release();
+  c->host_bytes.release();
+  c->host_out.release();
+  c->host_counts.release();
+  c->host_runs.release();
+  if (c->own_stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return PQG_OK;
+}
+
+int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, const pqg_column_desc* cols, int n_cols,
+                    const pqg_page_desc* pages, int n_pages, pqg_plan** out, pqg_status* st) {
+  if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
+  if (!ctx || !out || n_cols < 0 || n_pages < 0 || (n_cols && !cols) || (n_pages && !pages) || (n_bytes && !d_bytes)) {
+    set_status(st, PQG_ERR_INVALID_ARG, -1, -1, "plan arguments");
+    return PQG_ERR_INVALID_ARG;
+  }
+  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
+  pqg_plan* P = new (std::nothrow) pqg_plan();
+  if (!P) return PQG_ERR_INVALID_ARG;
+  P->ctx = ctx;
+  P->d_bytes = d_bytes;
+  P->n_bytes = n_bytes;
+  P->n_pages = n_pages;
+  P->n_cols = n_cols;
+  // ---- columns
+  std::vector<ColumnDev> hc((size_t)std::max(n_cols, 1));
+  std::vector<int> col_err((size_t)std::max(n_cols, 1), 0);
+  std::vector<int> col_first_page((size_t)std::max(n_cols, 1), -1);
+  P->col_nullable.assign((size_t)std::max(n_cols, 1), 0);
+  P->col_required_values.assign((size_t)std::max(n_cols, 1), 0);
+  for (int i = 0; i < n_cols; i++) {
+    const pqg_column_desc& c = cols[i];
+    ColumnDev& d = hc[(size_t)i];
+    std::memset(&d, 0, sizeof(d));
+    d.physical_type = c.physical_type;
+    d.type_length = c.type_length;
+    d.max_rep = c.max_rep;
+    d.max_def = c.max_def;
+    d.elem_width = elem_width(c.physical_type, c.type_length);
+    d.values = c.values;
+    d.def_levels = c.max_def > 0 ? c.def_levels : nullptr;
+    d.rep_levels = c.max_rep > 0 ? c.rep_levels : nullptr;
+    P->col_nullable[(size_t)i] = (c.max_def > 0 || c.max_rep > 0) ? 1 : 0;
+    if (c.max_def > 254 || c.max_rep > 254 || c.max_def < 0 || c.max_rep < 0) col_err[(size_t)i] = PQG_ERR_UNSUPPORTED;
+    if (c.dict_offset >= 0) {
+      // PlainValuesDictionary ctor :47-53 and the typed readers: validated from the descriptor
+      if (c.dict_encoding != PQG_PLAIN && c.dict_encoding != PQG_PLAIN_DICTIONARY) {
+        col_err[(size_t)i] = PQG_ERR_DICT_ENCODING;
+      } else if (c.physical_type == PQG_BOOLEAN) {
+        col_err[(size_t)i] = PQG_ERR_UNSUPPORTED;
+      } else if ((uint64_t)c.dict_offset + c.dict_size > n_bytes) {
+        col_err[(size_t)i] = PQG_ERR_INVALID_ARG;
+      } else if (d.elem_width > 0 && (uint64_t)c.dict_num_values * (uint64_t)d.elem_width > c.dict_size) {
+        col_err[(size_t)i] = PQG_ERR_EOF;
+      }
+      d.dict_n = c.dict_num_values;
+      d.dict_offset = (uint64_t)c.dict_offset;
+      d.dict_bytes = c.dict_size;
+    }
+  }
+  // ---- pages
+  P->h_work.resize((size_t)std::max(n_pages, 1));
+  P->page_cls.assign((size_t)std::max(n_pages, 1), -1);
+  std::vector<std::vector<int>> cls_lists(C_NCLS);
+  std::vector<int> lvl_list;
+  std::vector<std::vector<int>> col_pages((size_t)std::max(n_cols, 1));
+  std::vector<uint64_t> slot_acc((size_t)std::max(n_cols, 1), 0), val_acc((size_t)std::max(n_cols, 1), 0);
+  for (int p = 0; p < n_pages; p++) {
+    const pqg_page_desc& g = pages[p];
+    PageWork& w = P->h_work[(size_t)p];
+    std::memset(&w, 0, sizeof(w));
+    if (g.column < 0 || g.column >= n_cols || g.offset + g.size > n_bytes || (g.version != 1 && g.version != 2)) {
+      set_status(st, PQG_ERR_INVALID_ARG, p, -1, "page descriptor");
+      delete P;
+      return PQG_ERR_INVALID_ARG;
+    }
+    const int ci = g.column;
+    const pqg_column_desc& c = cols[ci];
+    if (col_first_page[(size_t)ci] < 0) {
+      col_first_page[(size_t)ci] = p;
+      if (col_err[(size_t)ci]) P->host_errs.push_back(HostErr{p, 0, -1, col_err[(size_t)ci]});
+    }
+    w.base = g.offset;
+    w.size = g.size;
+    w.num_slots = g.num_values;
+    w.column = ci;
+    w.version = g.version;
+    w.rl_encoding = g.rl_encoding;
+    w.dl_encoding = g.dl_encoding;
+    w.rl_len = g.rl_byte_length;
+    w.dl_len = g.dl_byte_length;
+    w.slot_offset = slot_acc[(size_t)ci];
+    slot_acc[(size_t)ci] += g.num_values;
+    const bool nullable = P->col_nullable[(size_t)ci] != 0;
+    if (!nullable) {
+      // required column: no level sections are consumed (ZeroIntegerValuesReader / BIT_PACKED
+      // width 0 / NullIntIterator), values = header num_values
+      if (g.version == 1 && ((g.rl_encoding != PQG_RLE && g.rl_encoding != PQG_BIT_PACKED) ||
+                             (g.dl_encoding != PQG_RLE && g.dl_encoding != PQG_BIT_PACKED))) {
+        P->host_errs.push_back(HostErr{p, 0, 0, PQG_ERR_UNSUPPORTED});
+        continue;
+      }
+      uint64_t lv = g.version == 2 ? (uint64_t)g.rl_byte_length + g.dl_byte_length : 0;
+      if (lv > g.size) {
+        P->host_errs.push_back(HostErr{p, 0, 0, PQG_ERR_CORRUPT});
+        continue;
+      }
+      w.data_begin = (uint32_t)lv;
+      w.n_values = g.num_values;
+      w.out_offset = val_acc[(size_t)ci];
+      val_acc[(size_t)ci] += g.num_values;
+    } else {
+      lvl_list.push_back(p);
+      col_pages[(size_t)ci].push_back(p);
+    }
+    if (col_err[(size_t)ci]) continue;  // dictionary page unusable: ColumnReaderBase ctor threw
+    // value class (Encoding.getValuesReader / getDictionaryBasedValuesReader dispatch)
+    const int t = c.physical_type;
+    const int ew = elem_width(t, c.type_length);
+    int cls = -1, herr = 0;
+    switch (g.encoding) {
+      case PQG_PLAIN_DICTIONARY:
+      case PQG_RLE_DICTIONARY:
+        if (c.dict_offset < 0) herr = PQG_ERR_NO_DICTIONARY;
+        else if (t == PQG_BOOLEAN) herr = PQG_ERR_UNSUPPORTED;
+        else if (ew == 8) cls = C_DICT8;
+        else if (ew == 4) cls = C_DICT4;
+        else herr = PQG_ERR_UNSUPPORTED;  // BYTE_ARRAY / INT96 / FLBA dictionaries: next row
+        break;
+      case PQG_PLAIN:
+        if (t == PQG_BOOLEAN) cls = C_BOOL;
+        else if (t == PQG_BYTE_ARRAY) herr = PQG_ERR_UNSUPPORTED;  // next row
+        else if (ew > 0) cls = C_PLAIN;
+        else herr = PQG_ERR_UNSUPPORTED;
+        break;
+      case PQG_DELTA_BINARY_PACKED:
+        if (t == PQG_INT64) cls = C_DELTA8;
+        else if (t == PQG_INT32) cls = C_DELTA4;
+        else herr = PQG_ERR_UNSUPPORTED;
+        break;
+      default:
+        herr = PQG_ERR_UNSUPPORTED;
+    }
+    if (herr) {
+      P->host_errs.push_back(HostErr{p, 0, 2, herr});
+      continue;
+    }
+    P->page_cls[(size_t)p] = cls;
+    cls_lists[(size_t)cls].push_back(p);
+  }
+  for (int i = 0; i < n_cols; i++) P->col_required_values[(size_t)i] = val_acc[(size_t)i];
+  // ---- flatten lists: [levels][class 0]...[class n]
+  std::vector<int32_t> flat(lvl_list.begin(), lvl_list.end());
+  P->levels_off = 0;
+  P->levels_n = (int)lvl_list.size();
+  P->cls_off.assign(C_NCLS, 0);
+  P->cls_n.assign(C_NCLS, 0);
+  for (int k = 0; k < C_NCLS; k++) {
+    P->cls_off[(size_t)k] = (int)flat.size();
+    P->cls_n[(size_t)k] = (int)cls_lists[(size_t)k].size();
+    flat.insert(flat.end(), cls_lists[(size_t)k].begin(), cls_lists[(size_t)k].end());
+  }
+  std::vector<int32_t> cp, cps;
+  cps.push_back(0);
+  for (int i = 0; i < n_cols; i++) {
+    if (col_pages[(size_t)i].empty()) continue;
+    cp.insert(cp.end(), col_pages[(size_t)i].begin(), col_pages[(size_t)i].end());
+    cps.push_back((int32_t)cp.size());
+  }
+  P->n_scan_cols = (int)cps.size() - 1;
+  // ---- upload
+  hipStream_t s = ctx->stream;
+  bool ok = P->work.ensure(sizeof(PageWork) * P->h_work.size()) == hipSuccess &&
+            P->cols.ensure(sizeof(ColumnDev) * hc.size()) == hipSuccess &&
+            P->lists.ensure(sizeof(int32_t) * std::max<size_t>(flat.size(), 1)) == hipSuccess &&
+            P->col_pages.ensure(sizeof(int32_t) * std::max<size_t>(cp.size(), 1)) == hipSuccess &&
+            P->col_page_start.ensure(sizeof(int32_t) * cps.size()) == hipSuccess &&
+            P->err.ensure(sizeof(uint64_t) * 3 * (size_t)std::max(n_pages, 1)) == hipSuccess &&
+            P->err_count.ensure(sizeof(uint32_t) * 4) == hipSuccess;
+  ok = ok && hipMemcpyAsync(P->work.p, P->h_work.data(), sizeof(PageWork) * P->h_work.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  ok = ok && hipMemcpyAsync(P->cols.p, hc.data(), sizeof(ColumnDev) * hc.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!flat.empty()) ok = ok && hipMemcpyAsync(P->lists.p, flat.data(), sizeof(int32_t) * flat.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!cp.empty()) ok = ok && hipMemcpyAsync(P->col_pages.p, cp.data(), sizeof(int32_t) * cp.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  ok = ok && hipMemcpyAsync(P->col_page_start.p, cps.data(), sizeof(int32_t) * cps.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  // the host vectors above die at return: wait for the copies
+  ok = ok && hipStreamSynchronize(s) == hipSuccess;
+  if (!ok) {
+    set_status(st, PQG_ERR_HIP, -1, -1, "plan upload");
+    pqg_plan_destroy(P);
+    return PQG_ERR_HIP;
+  }
+  P->kernels = (P->levels_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
+  for (int k = 0; k < C_NCLS; k++) P->kernels += P->cls_n[(size_t)k] ? 1 : 0;
+  *out = P;
+  return PQG_OK;
+}
+
+int pqg_plan_kernel_count(pqg_plan* P) { return P ? P->kernels : 0; }
+
+int pqg_plan_launch(pqg_plan* P) {
+  if (!P) return PQG_ERR_INVALID_ARG;
+  pqg_ctx* ctx = P->ctx;
+  hipStream_t s = ctx->stream;
+  uint64_t* err = (uint64_t*)P->err.p;
+  uint32_t* ecount = (uint32_t*)P->err_count.p;
+  PageWork* work = (PageWork*)P->work.p;
+  const ColumnDev* cols = (const ColumnDev*)P->cols.p;
+  const int32_t* lists = (const int32_t*)P->lists.p;
+  if (hipMemsetAsync(err, 0xFF, sizeof(uint64_t) * 3 * (size_t)std::max(P->n_pages, 1), s) != hipSuccess) return PQG_ERR_HIP;
+  if (hipMemsetAsync(ecount, 0, sizeof(uint32_t) * 4, s) != hipSuccess) return PQG_ERR_HIP;
+  hipError_t e = hipSuccess;
+  if (P->levels_n) {
+    e = pqg::launch_levels(s, P->d_bytes, P->n_bytes, work, cols, lists + P->levels_off, P->levels_n, err, ecount);
+    if (e == hipSuccess)
+      e = pqg::launch_scan(s, work, (const int32_t*)P->col_pages.p, (const int32_t*)P->col_page_start.p, P->n_scan_cols);
+  }
+  for (int k = 0; k < C_NCLS && e == hipSuccess; k++) {
+    int n = P->cls_n[(size_t)k];
+    if (!n) continue;
+    const int32_t* l = lists + P->cls_off[(size_t)k];
+    switch (k) {
+      case C_DICT4: e = pqg::launch_dict(4, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_DICT8: e = pqg::launch_dict(8, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_PLAIN: e = pqg::launch_plain(0, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_BOOL: e = pqg::launch_plain(1, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_DELTA4: e = pqg::launch_delta(4, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_DELTA8: e = pqg::launch_delta(8, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+    }
+  }
+  ctx->last_launched = P;
+  return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
+}
+
+int pqg_plan_destroy(pqg_plan* P) {
+  if (!P) return PQG_OK;
+  if (P->ctx) {
+    (void)hipStreamSynchronize(P->ctx->stream);
+    if (P->ctx->last_launched == P) P->ctx->last_launched = nullptr;
+    if (P->ctx->last == P) P->ctx->last = nullptr;
+  }
+  P->work.release();
+  P->cols.release();
+  P->lists.release();
+  P->col_pages.release();
+  P->col_page_start.release();
+  P->err.release();
+  P->err_count.release();
+  delete P;
+  return PQG_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Resolve the first error of a launched plan in (page, value) order.
+// Per page: init errors (rl init < dl init < data init) first; then value errors
+// (values are decoded only for slots before a level error, so a value error is
+// always earlier in the reference's read order); then level errors.
+int resolve_errors(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work_out) {
+  pqg_ctx* ctx = P->ctx;
+  hipStream_t s = ctx->stream;
+  if (ctx->pin_err.ensure(16) != hipSuccess) return PQG_ERR_HIP;
+  uint32_t* cnt = (uint32_t*)ctx->pin_err.p;
+  if (hipMemcpyAsync(cnt, P->err_count.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) return PQG_ERR_HIP;
+  bool need_work = false;
+  for (auto v : P->col_nullable) need_work = need_work || v;
+  if (need_work && work_out) {
+    work_out->resize(P->h_work.size());
+    if (hipMemcpyAsync(work_out->data(), P->work.p, sizeof(PageWork) * P->h_work.size(), hipMemcpyDeviceToHost, s) != hipSuccess)
+      return PQG_ERR_HIP;
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
+  std::vector<uint64_t> errs;
+  if (*cnt) {
+    errs.resize(3 * (size_t)std::max(P->n_pages, 1));
+    if (hipMemcpy(errs.data(), P->err.p, sizeof(uint64_t) * errs.size(), hipMemcpyDeviceToHost) != hipSuccess) return PQG_ERR_HIP;
+  }
+  if (P->host_errs.empty() && errs.empty()) return PQG_OK;
+  std::vector<const HostErr*> herr((size_t)std::max(P->n_pages, 1), nullptr);
+  for (const HostErr& h : P->host_errs)
+    if (!herr[(size_t)h.page]) herr[(size_t)h.page] = &h;
+  for (int p = 0; p < P->n_pages; p++) {
+    const HostErr* h = herr[(size_t)p];
+    uint64_t init = errs.empty() ? ~0ull : errs[3 * (size_t)p];
+    uint64_t lvl = errs.empty() ? ~0ull : errs[3 * (size_t)p + 1];
+    uint64_t val = errs.empty() ? ~0ull : errs[3 * (size_t)p + 2];
+    // host-detected errors are init-phase (descriptor) errors of this page
+    if (h && h->index == -1) {  // dictionary page: before any page is read
+      set_status(st, h->code, p, -1, "dictionary page");
+      return h->code;
+    }
+    if (h || init != ~0ull) {
+      uint64_t hkey = h ? (((uint64_t)h->index << 8) | (uint64_t)h->code) : ~0ull;
+      uint64_t k = std::min(hkey, init);
+      int code = (int)(k & 0xFF);
+      set_status(st, code, p, 0, (k >> 8) == 2 ? "data init" : "level init");
+      return code;
+    }
+    if (val != ~0ull) {
+      int code = (int)(val & 0xFF);
+      set_status(st, code, p, (int64_t)(val >> 8), "value decode");
+      return code;
+    }
+    if (lvl != ~0ull) {
+      int code = (int)(lvl & 0xFF);
+      set_status(st, code, p, (int64_t)(lvl >> 9), "level decode");
+      return code;
+    }
+  }
+  return PQG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pqg_sync(pqg_ctx* ctx, pqg_status* st) {
+  if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
+  if (!ctx) return PQG_ERR_INVALID_ARG;
+  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    set_status(st, PQG_ERR_HIP, -1, -1, hipGetErrorString(hipGetLastError()));
+    return PQG_ERR_HIP;
+  }
+  pqg_plan* P = ctx->last_launched;
+  if (!P) return PQG_OK;
+  std::vector<PageWork> work;
+  int rc = resolve_errors(P, st, &work);
+  if (ctx->last_cols && P == ctx->last) {
+    for (int i = 0; i < P->n_cols; i++) {
+      uint64_t n = P->col_required_values[(size_t)i];
+      if (P->col_nullable[(size_t)i] && !work.empty()) {
+        n = 0;
+        for (int p = 0; p < P->n_pages; p++)
+          if (work[(size_t)p].column == i) n += work[(size_t)p].n_values;
+      }
+      ctx->last_cols[i].values_written = n;
+    }
+  }
+  return rc;
+}
+
+int pqg_decode(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
+               const pqg_page_desc* pages, int n_pages, uint32_t* d_page_value_counts, pqg_status* st) {
+  if (!ctx) return PQG_ERR_INVALID_ARG;
+  // capacity checks (descriptor arithmetic)
+  {
+    std::vector<uint64_t> slots((size_t)std::max(n_cols, 1), 0);
+    for (int p = 0; p < n_pages; p++)
+      if (pages[p].column >= 0 && pages[p].column < n_cols) slots[(size_t)pages[p].column] += pages[p].num_values;
+    for (int i = 0; i < n_cols; i++) {
+      bool lv = cols[i].max_def > 0 || cols[i].max_rep > 0;
+      if (slots[(size_t)i] > cols[i].values_capacity || (slots[(size_t)i] && !cols[i].values) ||
+          (lv && ((cols[i].max_def > 0 && cols[i].def_levels) || (cols[i].max_rep > 0 && cols[i].rep_levels)) &&
+           slots[(size_t)i] > cols[i].levels_capacity)) {
+        set_status(st, PQG_ERR_INVALID_ARG, -1, i, "output capacity");
+        return PQG_ERR_INVALID_ARG;
+      }
+    }
+  }
+  if (ctx->last) {
+    pqg_plan_destroy(ctx->last);
+    ctx->last = nullptr;
+  }
+  pqg_plan* P = nullptr;
+  int rc = pqg_plan_create(ctx, d_bytes, n_bytes, cols, n_cols, pages, n_pages, &P, st);
+  if (rc) return rc;
+  ctx->last = P;
+  ctx->last_cols = cols;
+  rc = pqg_plan_launch(P);
+  if (rc == PQG_OK && d_page_value_counts && n_pages > 0) {
+    // n_values of every page (strided in PageWork) -> dense uint32 array
+    rc = hipMemcpy2DAsync(d_page_value_counts, sizeof(uint32_t), (const uint8_t*)P->work.p + offsetof(PageWork, n_values),
+                          sizeof(PageWork), sizeof(uint32_t), (size_t)n_pages, hipMemcpyDeviceToDevice,
+                          ctx->stream) == hipSuccess
+             ? PQG_OK
+             : PQG_ERR_HIP;
+  }
+  return rc;
+}
+
+int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
+                    const pqg_page_desc* pages, int n_pages, uint32_t* h_page_value_counts, pqg_status* st) {
+  if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
+  if (!ctx || (n_bytes && !h_bytes) || n_cols < 0 || n_pages < 0) return PQG_ERR_INVALID_ARG;
+  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
+  hipStream_t s = ctx->stream;
+  const uint64_t pad = 1024;
+  // device layout of outputs: per column values | def | rep, 256-B aligned
+  std::vector<uint64_t> off_v((size_t)std::max(n_cols, 1)), off_d((size_t)std::max(n_cols, 1)), off_r((size_t)std::max(n_cols, 1)),
+      nv((size_t)std::max(n_cols, 1), 0);
+  std::vector<uint64_t> slots((size_t)std::max(n_cols, 1), 0);
+  for (int p = 0; p < n_pages; p++)
+    if (pages[p].column >= 0 && pages[p].column < n_cols) slots[(size_t)pages[p].column] += pages[p].num_values;
+  uint64_t total = 0;
+  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  for (int i = 0; i < n_cols; i++) {
+    int w = elem_width(cols[i].physical_type, cols[i].type_length);
+    if (w <= 0) w = 8;
+    off_v[(size_t)i] = total;
+    total = al(total + slots[(size_t)i] * (uint64_t)w);
+    off_d[(size_t)i] = total;
+    if (cols[i].max_def > 0 && cols[i].def_levels) total = al(total + slots[(size_t)i]);
+    off_r[(size_t)i] = total;
+    if (cols[i].max_rep > 0 && cols[i].rep_levels) total = al(total + slots[(size_t)i]);
+  }
+  if (ctx->host_bytes.ensure(n_bytes + pad) != hipSuccess || ctx->host_out.ensure(total + 256) != hipSuccess ||
+      ctx->host_counts.ensure(sizeof(uint32_t) * (size_t)std::max(n_pages, 1)) != hipSuccess ||
+      ctx->pin_in.ensure(n_bytes + pad) != hipSuccess || ctx->pin_out.ensure(total + 256) != hipSuccess) {
+    set_status(st, PQG_ERR_HIP, -1, -1, "device buffers");
+    return PQG_ERR_HIP;
+  }
+  // host -> pinned -> device (the JNI shim hands heap bytes; the copy into pinned
+  // memory is what a production shim does with direct ByteBuffers too)
+  std::memcpy(ctx->pin_in.p, h_bytes, n_bytes);
+  std::memset((uint8_t*)ctx->pin_in.p + n_bytes, 0, pad);
+  if (hipMemcpyAsync(ctx->host_bytes.p, ctx->pin_in.p, n_bytes + pad, hipMemcpyHostToDevice, s) != hipSuccess) return PQG_ERR_HIP;
+  std::vector<pqg_column_desc> dcols(cols, cols + n_cols);
+  uint8_t* dout = (uint8_t*)ctx->host_out.p;
+  for (int i = 0; i < n_cols; i++) {
+    dcols[(size_t)i].values = dout + off_v[(size_t)i];
+    dcols[(size_t)i].values_capacity = slots[(size_t)i];
+    dcols[(size_t)i].def_levels = (cols[i].max_def > 0 && cols[i].def_levels) ? dout + off_d[(size_t)i] : nullptr;
+    dcols[(size_t)i].rep_levels = (cols[i].max_rep > 0 && cols[i].rep_levels) ? dout + off_r[(size_t)i] : nullptr;
+    dcols[(size_t)i].levels_capacity = slots[(size_t)i];
+  }
+  int rc = pqg_decode(ctx, (const uint8_t*)ctx->host_bytes.p, n_bytes, dcols.data(), n_cols, pages, n_pages,
+                      (uint32_t*)ctx->host_counts.p, st);
+  if (rc) return rc;
+  pqg_status st2;
+  rc = pqg_sync(ctx, &st2);
+  for (int i = 0; i < n_cols; i++) cols[i].values_written = dcols[(size_t)i].values_written;
+  if (rc && st) *st = st2;
+  // device -> pinned -> host arrays (decoded values are valid up to the first error)
+  if (hipMemcpyAsync(ctx->pin_out.p, dout, total, hipMemcpyDeviceToHost, s) != hipSuccess) return PQG_ERR_HIP;
+  std::vector<uint32_t> counts((size_t)std::max(n_pages, 1));
+  if (n_pages && hipMemcpyAsync(counts.data(), ctx->host_counts.p, sizeof(uint32_t) * (size_t)n_pages, hipMemcpyDeviceToHost, s) != hipSuccess)
+    return PQG_ERR_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
+  const uint8_t* po = (const uint8_t*)ctx->pin_out.p;
+  for (int i = 0; i < n_cols; i++) {
+    int w = elem_width(cols[i].physical_type, cols[i].type_length);
+    uint64_t n = std::min<uint64_t>(cols[i].values_written, cols[i].values_capacity);
+    if (cols[i].values && n) std::memcpy(cols[i].values, po + off_v[(size_t)i], n * (uint64_t)w);
+    if (cols[i].max_def > 0 && cols[i].def_levels)
+      std::memcpy(cols[i].def_levels, po + off_d[(size_t)i], std::min(slots[(size_t)i], cols[i].levels_capacity));
+    if (cols[i].max_rep > 0 && cols[i].rep_levels)
+      std::memcpy(cols[i].rep_levels, po + off_r[(size_t)i], std::min(slots[(size_t)i], cols[i].levels_capacity));
+  }
+  if (h_page_value_counts && n_pages) std::memcpy(h_page_value_counts, counts.data(), sizeof(uint32_t) * (size_t)n_pages);
+  return rc;
+}
+
+int pqg_unpack_runs(pqg_ctx* ctx, int bit_width, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                    const uint32_t* d_counts, const uint64_t* d_out_offsets, int32_t* d_out, int n_runs) {
+  if (!ctx || bit_width < 0 || bit_width > 32 || n_runs < 0) return PQG_ERR_INVALID_ARG;
+  if (n_runs == 0) return PQG_OK;
+  if (!d_in || !d_in_offsets || !d_counts || !d_out_offsets || !d_out) return PQG_ERR_INVALID_ARG;
+  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
+  // the kernel grid-strides inside each run; 64 blocks x 256 lanes per run
+  hipError_t e = pqg::launch_unpack_runs(ctx->stream, bit_width, d_in, ~0ull >> 1, d_in_offsets, d_counts, d_out_offsets,
+                                         d_out, n_runs, 1u << 14);
+  return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
+}
+
+int pqg_router_read(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_len, int count, int32_t* out) {
+  if (!ctx || bit_width < 0 || bit_width > 32 || count < 0 || (count && (!in || !out))) return PQG_ERR_INVALID_ARG;
+  if (count % 8 != 0) return PQG_ERR_INVALID_ARG;  // currentCount of a bit-packed run is a multiple of 8
+  const uint64_t need = (uint64_t)count * (uint64_t)bit_width / 8u;
+  if (need > in_len) return PQG_ERR_EOF;  // in.slice(count * bitWidth / 8) -> EOFException
+  if (count == 0) return PQG_OK;
+  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
+  hipStream_t s = ctx->stream;
+  const uint64_t in_al = (need + 16 + 255) & ~uint64_t(255);
+  const uint64_t tail = 32;  // [in_off, counts, out_off]
+  if (ctx->host_runs.ensure(in_al + (uint64_t)count * 4 + 256 + tail) != hipSuccess ||
+      ctx->pin_in.ensure(in_al + tail) != hipSuccess || ctx->pin_out.ensure((uint64_t)count * 4) != hipSuccess)
+    return PQG_ERR_HIP;
+  uint8_t* pin = (uint8_t*)ctx->pin_in.p;
+  std::memcpy(pin, in, need);
+  std::memset(pin + need, 0, in_al - need);
+  uint64_t* meta = (uint64_t*)(pin + in_al);
+  meta[0] = 0;                               // in offset
+  ((uint32_t*)&meta[1])[0] = (uint32_t)count; // count
+  meta[2] = 0;                               // out offset
+  uint8_t* d = (uint8_t*)ctx->host_runs.p;
+  int32_t* dout = (int32_t*)(d + in_al + tail + 256 - ((uintptr_t)(d + in_al + tail) & 255));
+  if (hipMemcpyAsync(d, pin, in_al + tail, hipMemcpyHostToDevice, s) != hipSuccess) return PQG_ERR_HIP;
+  hipError_t e = pqg::launch_unpack_runs(s, bit_width, d, need + 16, (const uint64_t*)(d + in_al),
+                                         (const uint32_t*)(d + in_al + 8), (const uint64_t*)(d + in_al + 16), dout, 1,
+                                         (uint32_t)count);
+  if (e != hipSuccess) return PQG_ERR_HIP;
+  if (hipMemcpyAsync(ctx->pin_out.p, dout, (size_t)count * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return PQG_ERR_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
+  std::memcpy(out, ctx->pin_out.p, (size_t)count * 4);
+  return PQG_OK;
+}
+
+}  // extern "C"

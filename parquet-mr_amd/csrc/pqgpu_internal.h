@@ -1,0 +1,57 @@
+// pqgpu_internal.h — device-side tables shared by the kernels and the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pqgpu.h"
+
+namespace pqg {
+
+// Per output column, on the device.
+struct ColumnDev {
+  int32_t physical_type;
+  int32_t type_length;
+  int32_t max_rep;
+  int32_t max_def;
+  int32_t elem_width;   // bytes per dense value
+  uint32_t dict_n;      // dictionary entries (0 if none)
+  uint64_t dict_offset; // dictionary page body offset in the batch
+  uint64_t dict_bytes;  // dictionary page body bytes
+  void* values;
+  uint8_t* def_levels;
+  uint8_t* rep_levels;
+};
+
+// Per page, on the device. The host fills the descriptor facts; for nullable
+// columns k_levels fills data_begin / n_values and k_scan_offsets fills out_offset.
+struct PageWork {
+  uint64_t base;        // page body offset in the batch
+  uint32_t size;        // page body bytes
+  uint32_t num_slots;   // header num_values
+  uint32_t data_begin;  // data section start (page-relative)
+  uint32_t n_values;    // non-null values to decode
+  uint64_t out_offset;  // first dense value index of the page in its column
+  uint64_t slot_offset; // first level slot of the page in its column
+  int32_t column;
+  int32_t version;
+  int32_t rl_encoding;
+  int32_t dl_encoding;
+  uint32_t rl_len;      // V2
+  uint32_t dl_len;      // V2
+};
+
+hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                       const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
+                         const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+hipError_t launch_scan(hipStream_t st, PageWork* work, const int32_t* col_pages, const int32_t* col_page_start,
+                       int n_cols);
+hipError_t launch_plain(int kind, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+hipError_t launch_unpack_runs(hipStream_t st, int w, const uint8_t* in, uint64_t in_bytes, const uint64_t* in_off,
+                              const uint32_t* counts, const uint64_t* out_off, int32_t* out, int n_runs,
+                              uint32_t max_count);
+
+}  // namespace pqg

@@ -1,0 +1,962 @@
+// pqgpu_kernels.hip — CDNA4 (gfx950) kernels of the MI355X Parquet page decoder.
+//
+// Hot path: RLE/bit-packed hybrid decode of dictionary ids and
+// levels, dictionary gather, PLAIN copy, DELTA_BINARY_PACKED. All integer /
+// byte work: no MFMA. One 64-lane wave decodes one page:
+//
+//   walk    — the wave reads the page section through a 512-byte register
+//             window (one dword per lane, two halves) and follows the run
+//             headers with v_readlane on the scalar unit. Each walked run
+//             lands in one lane's registers (run r -> lane r % 64), so a batch
+//             of 64 runs is a register-resident run table; no LDS.
+//   resolve — lanes holding RLE runs fetch their dictionary entry (one gather
+//             per run, not per value).
+//   expand  — lanes sweep the batch's output range in 16-byte stores; for each
+//             chunk a ballot finds the runs overlapping it and a uniform loop
+//             over those runs selects each element's run. Bit-packed elements
+//             are unpacked from the page bytes (buffer loads hit L1/L2: the
+//             walk just touched them) and gathered from the dictionary.
+//
+// Semantics follow the reference reader value for value:
+//   RunLengthBitPackingHybridDecoder.readInt/readNext (rle/…Decoder.java:61-109),
+//   DictionaryValuesReader.initFromPage/read* (dictionary/DictionaryValuesReader.java:48-118),
+//   PlainValuesReader (plain/PlainValuesReader.java:32-138),
+//   DeltaBinaryPackingValuesReader (delta/DeltaBinaryPackingValuesReader.java:59-172),
+//   ColumnReaderBase.readPageV1/V2 + levels (impl/ColumnReaderBase.java:650-789).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pqgpu_internal.h"
+
+namespace pqg {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+// Buffer resource over [base, base + n) with hardware range checking: loads past
+// n return 0 (never fault), so a window may overhang the end of the batch.
+__device__ __forceinline__ rsrc_t make_rsrc(const uint8_t* base, uint64_t n) {
+  uint64_t b = uni64((uint64_t)(uintptr_t)base);
+  uint32_t nr = n > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)n;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)b, (short)0, (int)uni(nr), 0x00020000);
+}
+
+__device__ __forceinline__ uint32_t ld32(rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
+
+// 8 bytes at any byte offset (little endian).
+__device__ __forceinline__ uint64_t ld8_any(rsrc_t r, uint32_t off) {
+  uint32_t a = off & ~3u, sh = (off & 3u) * 8u;
+  uint64_t x = (uint64_t)ld32(r, a) | ((uint64_t)ld32(r, a + 4) << 32);
+  if (sh) x = (x >> sh) | ((uint64_t)ld32(r, a + 8) << (64u - sh));
+  return x;
+}
+
+__device__ __forceinline__ uint32_t ld4_any(rsrc_t r, uint32_t off) {
+  uint32_t a = off & ~3u, sh = (off & 3u) * 8u;
+  uint32_t x = ld32(r, a);
+  if (sh) x = (x >> sh) | (ld32(r, a + 4) << (32u - sh));
+  return x;
+}
+
+// Record an error: smallest (index << 8 | code) per (page, kind) wins.
+__device__ __forceinline__ void report(uint64_t* err, uint32_t* err_count, int page, int kind, uint64_t index,
+                                       int code) {
+  atomicMin((unsigned long long*)&err[3 * (uint64_t)page + kind], (unsigned long long)((index << 8) | (uint64_t)code));
+  atomicAdd(err_count, 1u);
+}
+
+// ---------------------------------------------------------------------------
+// Register window over a page: lane l holds bytes [B + 4l, B + 4l + 4) in wa and
+// [B + 256 + 4l, ...) in wb. B is wave-uniform; reads are v_readlane.
+struct Window {
+  rsrc_t rs;
+  uint32_t B;
+  uint32_t wa, wb;
+
+  __device__ __forceinline__ void seek(uint32_t p) {
+    B = p & ~3u;
+    wa = ld32(rs, B + 4u * lane_id());
+    wb = ld32(rs, B + 256u + 4u * lane_id());
+  }
+  // Make [p, p + 12) resident. p never moves backwards.
+  __device__ __forceinline__ void ensure(uint32_t p) {
+    uint32_t k = p - B;
+    if (k > 496u) {
+      if (k <= 752u) {
+        B += 256u;
+        wa = wb;
+        wb = ld32(rs, B + 256u + 4u * lane_id());
+      } else {
+        seek(p);
+      }
+    }
+  }
+  __device__ __forceinline__ uint32_t dword(uint32_t i) {
+    uint32_t a = rdl(wa, i & 63u), b = rdl(wb, i & 63u);
+    return i < 64u ? a : b;
+  }
+  __device__ __forceinline__ uint64_t read8(uint32_t p) {
+    ensure(p);
+    uint32_t k = p - B, i = k >> 2, sh = (k & 3u) * 8u;
+    uint64_t x = (uint64_t)dword(i) | ((uint64_t)dword(i + 1) << 32);
+    if (sh) x = (x >> sh) | ((uint64_t)dword(i + 2) << (64u - sh));
+    return x;
+  }
+  __device__ __forceinline__ uint32_t byte(uint32_t p) {
+    ensure(p);
+    uint32_t k = p - B;
+    return (dword(k >> 2) >> ((k & 3u) * 8u)) & 0xFFu;
+  }
+};
+
+// readUnsignedVarInt (BytesUtils.java:202-211) at p. Sets len; Java int shift masking.
+// `lim` = bytes readable before the section end; a varint not terminated within
+// them gets len = lim + 1 (the caller's EOF check fails it, as read() would).
+__device__ __forceinline__ uint32_t read_uvarint(Window& w, uint32_t p, uint32_t lim, uint32_t& len) {
+  uint64_t x = w.read8(p);
+  uint32_t b0 = (uint32_t)x & 0xFFu;
+  if (!(b0 & 0x80u)) { len = 1; return b0; }
+  uint32_t b1 = (uint32_t)(x >> 8) & 0xFFu;
+  if (!(b1 & 0x80u)) { len = 2; return (b0 & 0x7Fu) | (b1 << 7); }
+  uint32_t value = 0, i = 0, k = 0, b;
+  for (;;) {
+    b = (k < 8u) ? (uint32_t)(x >> (8u * k)) & 0xFFu : w.byte(p + k);
+    if (!(b & 0x80u)) break;
+    value |= (b & 0x7Fu) << (i & 31u);
+    i += 7;
+    k++;
+    if (k >= lim) break;
+  }
+  len = k + 1;
+  return value | (b << (i & 31u));
+}
+
+// readUnsignedVarLong (BytesUtils.java:260-269), Java long shift masking.
+__device__ __forceinline__ uint64_t read_uvarlong(Window& w, uint32_t p, uint32_t lim, uint32_t& len) {
+  uint64_t value = 0;
+  uint32_t i = 0, k = 0, b;
+  uint64_t x = w.read8(p);
+  for (;;) {
+    b = (k < 8u) ? (uint32_t)(x >> (8u * k)) & 0xFFu : w.byte(p + k);
+    if (!(b & 0x80u)) break;
+    value |= (uint64_t)(b & 0x7Fu) << (i & 63u);
+    i += 7;
+    k++;
+    if (k >= lim) break;
+  }
+  len = k + 1;
+  return value | ((uint64_t)b << (i & 63u));
+}
+
+// readZigZagVarLong (BytesUtils.java:254-258)
+__device__ __forceinline__ int64_t zigzag64(uint64_t r) {
+  int64_t sign = -(int64_t)(r & 1);
+  int64_t temp = ((int64_t)((uint64_t)sign ^ r)) >> 1;
+  return (int64_t)((uint64_t)temp ^ (r & 0x8000000000000000ull));
+}
+
+// ---------------------------------------------------------------------------
+// RLE / bit-packed hybrid walker (RunLengthBitPackingHybridDecoder.readNext :80-109).
+
+struct RleWalk {
+  uint32_t pos;       // uniform: next header byte (page-relative)
+  uint32_t sec_end;   // uniform
+  uint32_t produced;  // uniform: values covered by the runs walked so far
+  uint32_t N;         // uniform: values wanted
+  int w;              // uniform: bit width
+};
+
+// One batch of up to 64 runs; lane r holds run r.
+struct RunBatch {
+  uint32_t start;   // first value index of the run
+  uint32_t meta;    // 0 = RLE, 1 = PACKED
+  uint32_t lo, hi;  // RLE: lo = raw value; PACKED: [lo, hi) = bytes read for the run
+  uint32_t nr;      // uniform
+  uint32_t first;   // uniform: value index of the batch start
+  uint32_t end;     // uniform: value index after the batch
+};
+
+// Walk up to 64 runs. Returns 0 or an error code; on error s.N is cut to the
+// error's value index (s.produced) so the caller stops after this batch.
+__device__ __forceinline__ int walk_batch(Window& win, RleWalk& s, RunBatch& rb) {
+  const uint32_t lane = lane_id();
+  rb.nr = 0;
+  rb.first = s.produced;
+  rb.start = 0xFFFFFFFFu;
+  rb.meta = 0;
+  rb.lo = 0;
+  rb.hi = 0;
+  int code = 0;
+  const uint32_t nb = ((uint32_t)s.w + 7u) >> 3;
+  while (rb.nr < 64u && s.produced < s.N) {
+    if (s.pos >= s.sec_end) { code = PQG_ERR_RLE_PAST_END; break; }     // :81
+    uint32_t hl;
+    uint32_t header = read_uvarint(win, s.pos, s.sec_end - s.pos, hl);
+    if ((uint64_t)s.pos + hl > s.sec_end) { code = PQG_ERR_EOF; break; }  // EOFException in read()
+    s.pos += hl;
+    uint64_t count;
+    uint32_t m, lo, hi = 0;
+    if ((header & 1u) == 0) {                                              // RLE :85-89
+      count = header >> 1;
+      if ((uint64_t)s.pos + nb > s.sec_end) { code = PQG_ERR_EOF; break; }
+      uint32_t v = 0;
+      if (nb) {
+        uint64_t x = win.read8(s.pos);
+        v = nb == 4 ? (uint32_t)x : (uint32_t)x & ((1u << (8u * nb)) - 1u);
+      }
+      s.pos += nb;
+      if (count == 0) count = s.N - s.produced;  // Java: currentCount goes negative, value repeats forever
+      m = 0;
+      lo = v;
+    } else {                                                               // PACKED :90-104
+      uint32_t groups = header >> 1;
+      if (groups == 0) { code = PQG_ERR_EMPTY_PACKED_RUN; break; }
+      if (groups >= (1u << 28)) { code = PQG_ERR_CORRUPT; break; }
+      count = (uint64_t)groups * 8u;
+      uint64_t need = (uint64_t)groups * (uint32_t)s.w;
+      uint32_t avail = s.sec_end - s.pos;
+      uint32_t rd = need < avail ? (uint32_t)need : avail;                 // :97-99
+      m = 1;
+      lo = s.pos;
+      hi = s.pos + rd;
+      s.pos += rd;
+    }
+    const bool me = lane == rb.nr;
+    rb.start = me ? s.produced : rb.start;
+    rb.meta = me ? m : rb.meta;
+    rb.lo = me ? lo : rb.lo;
+    rb.hi = me ? hi : rb.hi;
+    rb.nr++;
+    uint64_t np = (uint64_t)s.produced + count;
+    s.produced = np < s.N ? (uint32_t)np : s.N;
+  }
+  if (code) s.N = s.produced;
+  rb.end = s.produced;
+  return code;
+}
+
+// Value of element i (page-relative) of a PACKED run [lo, hi) starting at s_r.
+__device__ __forceinline__ uint32_t packed_elem(rsrc_t rs, uint32_t lo, uint32_t hi, uint32_t s_r, uint32_t i, int w) {
+  if (w == 0) return 0;
+  uint64_t bit = (uint64_t)(i - s_r) * (uint32_t)w;
+  uint32_t byte = lo + (uint32_t)(bit >> 3);
+  uint32_t a = byte & ~3u;
+  uint64_t x = (uint64_t)ld32(rs, a) | ((uint64_t)ld32(rs, a + 4) << 32);
+  if (a + 8u > hi) {  // truncated final group: bytes past what readFully got are 0 (:96-99)
+    int64_t keep = (int64_t)hi - (int64_t)a;
+    x = keep <= 0 ? 0 : (x & ((1ull << (8 * keep)) - 1ull));
+  }
+  x >>= (byte - a) * 8u + (uint32_t)(bit & 7u);
+  return w == 32 ? (uint32_t)x : (uint32_t)x & ((1u << w) - 1u);
+}
+
+// For lane element index i, select the run (among `mask`) covering it.
+struct Sel {
+  uint32_t s, meta, lo, hi;
+};
+
+__device__ __forceinline__ void select_runs(const RunBatch& rb, uint64_t mask, const uint32_t* idx, Sel* sel, int E) {
+  while (mask) {
+    uint32_t r = (uint32_t)__builtin_ctzll(mask);
+    mask &= mask - 1;
+    uint32_t s = rdl(rb.start, r), m = rdl(rb.meta, r), lo = rdl(rb.lo, r), hi = rdl(rb.hi, r);
+#pragma unroll
+    for (int k = 0; k < E; k++) {
+      bool t = idx[k] >= s;
+      sel[k].s = t ? s : sel[k].s;
+      sel[k].meta = t ? m : sel[k].meta;
+      sel[k].lo = t ? lo : sel[k].lo;
+      sel[k].hi = t ? hi : sel[k].hi;
+    }
+  }
+}
+
+// Runs of the batch that overlap value range [c_lo, c_hi).
+__device__ __forceinline__ uint64_t overlap_mask(const RunBatch& rb, uint32_t run_end, uint32_t c_lo, uint32_t c_hi) {
+  bool ov = lane_id() < rb.nr && rb.start < c_hi && run_end > c_lo;
+  return __ballot(ov);
+}
+
+// ---------------------------------------------------------------------------
+// Dictionary pages (DictionaryValuesReader): W = 4 or 8 byte values.
+
+template <int W>
+struct DictVal;
+template <>
+struct DictVal<8> {
+  typedef uint64_t T;
+};
+template <>
+struct DictVal<4> {
+  typedef uint32_t T;
+};
+
+template <int W>
+__device__ __forceinline__ typename DictVal<W>::T load_dict(rsrc_t d, uint32_t id) {
+  if constexpr (W == 8) return ld8_any(d, id * 8u);
+  else return ld4_any(d, id * 4u);
+}
+
+// One wave per page. Page list = pages of this class; PageWork holds data
+// section bounds, value count and output offset.
+template <int W>
+__global__ __launch_bounds__(64) void k_dict(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                              const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                              const int32_t* __restrict__ list, int n_list, uint64_t* err,
+                                              uint32_t* err_count) {
+  typedef typename DictVal<W>::T T;
+  constexpr int E = 16 / W;  // elements per lane per 16-byte store
+  const int page = list[blockIdx.x];
+  const PageWork pw = work[page];
+  const ColumnDev cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint32_t N = uni(pw.n_values);
+  const uint32_t sec_beg = uni(pw.data_begin), sec_end = uni(pw.size);
+  if (N == 0 && sec_beg >= sec_end) return;
+
+  Window win;
+  win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
+  const uint32_t dict_n = uni(cd.dict_n);
+
+  // DictionaryValuesReader.initFromPage :48-64
+  RleWalk s;
+  s.produced = 0;
+  s.N = N;
+  s.sec_end = sec_end;
+  if (sec_beg >= sec_end) {  // empty data section: every read throws "Attempt to read from empty page"
+    if (N) report(err, err_count, page, 2 /*value*/, 0, PQG_ERR_EMPTY_PAGE);
+    return;
+  }
+  win.seek(sec_beg);
+  const uint32_t bw = win.byte(sec_beg);
+  if (bw > 32u) {  // RunLengthBitPackingHybridDecoder ctor :55 (thrown at initFromPage)
+    report(err, err_count, page, 0 /*init*/, 2, PQG_ERR_BIT_WIDTH);
+    return;
+  }
+  s.w = (int)bw;
+  s.pos = sec_beg + 1;
+  T* out = (T*)cd.values;
+  const uint64_t obase = pw.out_offset;
+  const bool out16 = ((uintptr_t)out & 15u) == 0;
+
+  while (s.produced < s.N) {
+    RunBatch rb;
+    int code = walk_batch(win, s, rb);
+    if (code) report(err, err_count, page, 2, rb.end, code);
+    // resolve RLE runs through the dictionary (one gather per run)
+    uint32_t rlo = rb.lo, rhi = rb.hi;
+    if (lane < rb.nr && rb.meta == 0) {
+      if (rb.lo >= dict_n) {
+        if (rb.start < rb.end) report(err, err_count, page, 2, rb.start, PQG_ERR_DICT_ID);
+        rlo = 0;
+        rhi = 0;
+      } else {
+        uint64_t v = (uint64_t)load_dict<W>(drs, rb.lo);
+        rlo = (uint32_t)v;
+        rhi = (uint32_t)(v >> 32);
+      }
+    }
+    rb.lo = rlo;
+    rb.hi = rhi;
+    // run end = next run's start (or batch end)
+    uint32_t nxt = __shfl_down(rb.start, 1);
+    const uint32_t run_end = (lane + 1 < rb.nr) ? nxt : rb.end;
+    if (rb.end <= rb.first) break;
+    // expand [rb.first, rb.end): global element range
+    const uint64_t g_lo = obase + rb.first, g_hi = obase + rb.end;
+    for (uint64_t c0 = g_lo & ~(uint64_t)(E - 1); c0 < g_hi; c0 += (uint64_t)E * WAVE) {
+      const uint64_t cg = c0 + (uint64_t)E * lane;
+      // chunk range (page-relative), clamped
+      uint64_t cl = c0 > g_lo ? c0 - obase : rb.first;
+      uint64_t ch = c0 + (uint64_t)E * WAVE;
+      ch = (ch < g_hi ? ch : g_hi) - obase;
+      uint64_t mask = overlap_mask(rb, run_end, (uint32_t)cl, (uint32_t)ch);
+      uint32_t idx[E];
+      bool valid[E];
+      Sel sel[E];
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        uint64_t g = cg + k;
+        valid[k] = g >= g_lo && g < g_hi;
+        idx[k] = (uint32_t)(g - obase);
+        sel[k] = Sel{0, 0, 0, 0};
+      }
+      select_runs(rb, mask, idx, sel, E);
+      T vals[E];
+#pragma unroll
+      for (int k = 0; k < E; k++) {
+        T v;
+        if (sel[k].meta == 0) {
+          v = (T)(((uint64_t)sel[k].hi << 32) | sel[k].lo);
+        } else {
+          uint32_t id = packed_elem(win.rs, sel[k].lo, sel[k].hi, sel[k].s, idx[k], s.w);
+          if (id >= dict_n) {
+            if (valid[k]) report(err, err_count, page, 2, idx[k], PQG_ERR_DICT_ID);
+            v = 0;
+          } else {
+            v = valid[k] ? load_dict<W>(drs, id) : (T)0;
+          }
+        }
+        vals[k] = v;
+      }
+      bool all = true;
+#pragma unroll
+      for (int k = 0; k < E; k++) all = all && valid[k];
+      if (all && out16) {
+        if constexpr (W == 8) {
+          typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+          v2 st = {vals[0], vals[1]};
+          __builtin_nontemporal_store(st, (v2*)(out + cg));
+        } else {
+          typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+          v4 st = {vals[0], vals[1], vals[2], vals[3]};
+          __builtin_nontemporal_store(st, (v4*)(out + cg));
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < E; k++)
+          if (valid[k]) out[cg + k] = vals[k];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Levels (def/rep) of nullable columns: ColumnReaderBase.readPageV1/readPageV2,
+// RunLengthBitPackingHybridValuesReader.initFromPage (4-byte length prefix),
+// newRLEIterator (V2, no prefix). Writes u8 levels, the page's non-null count
+// and the data section start; value kernels run afterwards.
+
+// Decode one level section into out[slot_base + i], i < N. Returns the number of
+// slots decoded before an error (N when none) and sets *err_code.
+__device__ uint32_t decode_levels(Window& win, uint32_t beg, uint32_t end, int w, uint32_t N, uint8_t* out,
+                                  uint32_t max_def, bool count_nonnull, uint32_t* nonnull, int* err_code) {
+  const uint32_t lane = lane_id();
+  RleWalk s;
+  s.pos = beg;
+  s.sec_end = end;
+  s.produced = 0;
+  s.N = N;
+  s.w = w;
+  uint32_t cnt = 0;
+  int first_err = 0;
+  uint32_t done = N;
+  if (N) win.seek(beg);
+  while (s.produced < s.N) {
+    RunBatch rb;
+    int code = walk_batch(win, s, rb);
+    if (code && !first_err) { first_err = code; done = rb.end; }
+    if (lane < rb.nr && rb.meta == 0) rb.lo = rb.lo > 255u ? 255u : rb.lo;  // saturate (pqgpu.h)
+    uint32_t nxt = __shfl_down(rb.start, 1);
+    const uint32_t run_end = (lane + 1 < rb.nr) ? nxt : rb.end;
+    for (uint32_t c0 = rb.first; c0 < rb.end; c0 += WAVE) {
+      uint32_t i = c0 + lane;
+      uint32_t ch = c0 + WAVE < rb.end ? c0 + WAVE : rb.end;
+      uint64_t mask = overlap_mask(rb, run_end, c0, ch);
+      Sel sel = {0, 0, 0, 0};
+      select_runs(rb, mask, &i, &sel, 1);
+      uint32_t v = sel.meta == 0 ? sel.lo : packed_elem(win.rs, sel.lo, sel.hi, sel.s, i, w);
+      v = v > 255u ? 255u : v;
+      if (i < rb.end) {
+        if (out) out[i] = (uint8_t)v;
+        if (count_nonnull && v == max_def) cnt++;
+      }
+    }
+  }
+  // wave reduce
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if (nonnull) *nonnull = cnt;
+  *err_code = first_err;
+  return done;
+}
+
+__global__ __launch_bounds__(64) void k_levels(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                                const int32_t* __restrict__ list, int n_list, uint64_t* err,
+                                                uint32_t* err_count) {
+  const int page = list[blockIdx.x];
+  PageWork pw = work[page];
+  const ColumnDev cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  Window win;
+  win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  const uint32_t size = uni(pw.size);
+  const uint32_t nslots = uni(pw.num_slots);
+  const int wr = cd.max_rep ? 32 - __builtin_clz((uint32_t)cd.max_rep) : 0;
+  const int wd = cd.max_def ? 32 - __builtin_clz((uint32_t)cd.max_def) : 0;
+  uint32_t rl_beg = 0, rl_end = 0, dl_beg = 0, dl_end = 0, data_beg = 0;
+  int init_err = 0, init_phase = 0;
+  if (pw.version == 2) {
+    rl_beg = 0;
+    rl_end = pw.rl_len;
+    dl_beg = rl_end;
+    dl_end = rl_end + pw.dl_len;
+    data_beg = dl_end;
+    if ((uint64_t)pw.rl_len + pw.dl_len > size) { init_err = PQG_ERR_CORRUPT; init_phase = 0; }
+  } else {
+    uint32_t p = 0;
+    win.seek(0);
+    // rl section (RunLengthBitPackingHybridValuesReader.initFromPage :40-46) when max_rep > 0
+    for (int which = 0; which < 2 && !init_err; which++) {
+      int maxl = which == 0 ? cd.max_rep : cd.max_def;
+      int enc = which == 0 ? pw.rl_encoding : pw.dl_encoding;
+      uint32_t b = p, e = p;
+      if (maxl > 0) {
+        if (enc != PQG_RLE) { init_err = PQG_ERR_UNSUPPORTED; init_phase = which; break; }
+        if (p + 4u > size) { init_err = PQG_ERR_EOF; init_phase = which; break; }
+        int32_t len = (int32_t)(uint32_t)win.read8(p);
+        if (len < 0) { init_err = PQG_ERR_CORRUPT; init_phase = which; break; }
+        if ((uint64_t)p + 4u + (uint32_t)len > size) { init_err = PQG_ERR_EOF; init_phase = which; break; }
+        b = p + 4u;
+        e = b + (uint32_t)len;
+        p = e;
+      } else if (enc != PQG_RLE && enc != PQG_BIT_PACKED) {
+        init_err = PQG_ERR_UNSUPPORTED;
+        init_phase = which;
+        break;
+      }
+      if (which == 0) { rl_beg = b; rl_end = e; } else { dl_beg = b; dl_end = e; }
+    }
+    data_beg = p;
+  }
+  if (init_err) {
+    if (lane == 0) {
+      report(err, err_count, page, 0, (uint64_t)init_phase, init_err);
+      work[page].n_values = 0;
+      work[page].data_begin = size;
+    }
+    return;
+  }
+  // repetition levels first (ColumnReaderBase.checkRead reads rl then dl per slot)
+  uint32_t limit = nslots;
+  int code = 0;
+  uint8_t* rep_out = cd.rep_levels ? cd.rep_levels + pw.slot_offset : nullptr;
+  uint8_t* def_out = cd.def_levels ? cd.def_levels + pw.slot_offset : nullptr;
+  uint64_t lvl_err_key = ~0ull;
+  if (wr > 0) {
+    uint32_t done = decode_levels(win, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code);
+    if (code) {
+      limit = done;
+      lvl_err_key = ((uint64_t)done << 1) << 8 | (uint64_t)code;
+    }
+  } else if (rep_out) {
+    for (uint32_t i = lane; i < nslots; i += WAVE) rep_out[i] = 0;
+  }
+  uint32_t nonnull = 0;
+  if (wd > 0) {
+    int code2 = 0;
+    uint32_t done = decode_levels(win, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true, &nonnull, &code2);
+    if (code2) {
+      uint64_t key = (((uint64_t)done << 1) | 1ull) << 8 | (uint64_t)code2;
+      if (key < lvl_err_key) lvl_err_key = key;
+    }
+  } else {
+    nonnull = limit;  // max_def == 0: every slot holds a value
+    if (def_out)
+      for (uint32_t i = lane; i < limit; i += WAVE) def_out[i] = 0;
+  }
+  if (lane == 0) {
+    if (lvl_err_key != ~0ull) {
+      // level error key: slot << 1 | (0 = rl, 1 = dl) — host decodes it
+      atomicMin((unsigned long long*)&err[3 * (uint64_t)page + 1], (unsigned long long)lvl_err_key);
+      atomicAdd(err_count, 1u);
+    }
+    work[page].n_values = nonnull;
+    work[page].data_begin = data_beg;
+  }
+}
+
+// Exclusive scan of non-null counts per column (one workgroup per column).
+__global__ __launch_bounds__(256) void k_scan_offsets(PageWork* __restrict__ work, const int32_t* __restrict__ col_pages,
+                                                      const int32_t* __restrict__ col_page_start, int n_cols) {
+  const int c = blockIdx.x;
+  const int b = col_page_start[c], e = col_page_start[c + 1];
+  __shared__ uint64_t warp_sums[4];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = b; base < e; base += 256) {
+    int i = base + (int)threadIdx.x;
+    uint64_t v = i < e ? work[col_pages[i]].n_values : 0;
+    // inclusive wave scan
+    uint64_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      uint64_t y = __shfl_up(x, o);
+      if ((int)lane_id() >= o) x += y;
+    }
+    if (lane_id() == 63) warp_sums[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint64_t pre = carry;
+    for (int wv = 0; wv < (int)(threadIdx.x >> 6); wv++) pre += warp_sums[wv];
+    if (i < e) work[col_pages[i]].out_offset = pre + x - v;
+    __syncthreads();
+    if (threadIdx.x == 255) carry = pre + x;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// PLAIN fixed width (PlainValuesReader / FixedLenByteArrayPlainValuesReader):
+// byte copy of n_values * W bytes from the data section, EOF at the first
+// value that does not fit.
+__global__ __launch_bounds__(64) void k_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                              const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                              const int32_t* __restrict__ list, int n_list, uint64_t* err,
+                                              uint32_t* err_count) {
+  const int page = list[blockIdx.x];
+  const PageWork pw = work[page];
+  const ColumnDev cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint32_t W = uni((uint32_t)cd.elem_width);
+  const uint32_t beg = uni(pw.data_begin), end = uni(pw.size);
+  uint32_t n = uni(pw.n_values);
+  const uint32_t avail = end > beg ? end - beg : 0;
+  if ((uint64_t)n * W > avail) {
+    uint32_t fit = avail / W;
+    if (lane == 0) report(err, err_count, page, 2, fit, PQG_ERR_EOF);
+    n = fit;
+  }
+  rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  uint8_t* dst = (uint8_t*)cd.values + pw.out_offset * W;
+  const uint64_t nb = (uint64_t)n * W;
+  const uint32_t src0 = beg;
+  // destination-aligned 16-byte chunks
+  const uintptr_t d0 = (uintptr_t)dst, d1 = d0 + nb;
+  const uintptr_t a0 = (d0 + 15u) & ~(uintptr_t)15u, a1 = d1 & ~(uintptr_t)15u;
+  if (a0 >= a1) {  // tiny: bytewise
+    for (uint64_t i = lane; i < nb; i += WAVE) dst[i] = (uint8_t)(ld32(rs, (src0 + (uint32_t)i) & ~3u) >> (((src0 + (uint32_t)i) & 3u) * 8u));
+    return;
+  }
+  const uint32_t head = (uint32_t)(a0 - d0), tail = (uint32_t)(d1 - a1);
+  if (lane < head) {
+    uint32_t o = src0 + lane;
+    dst[lane] = (uint8_t)(ld32(rs, o & ~3u) >> ((o & 3u) * 8u));
+  }
+  if (lane < tail) {
+    uint64_t i = (a1 - d0) + lane;
+    uint32_t o = src0 + (uint32_t)i;
+    dst[i] = (uint8_t)(ld32(rs, o & ~3u) >> ((o & 3u) * 8u));
+  }
+  typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+  const uint64_t nchunks = (a1 - a0) >> 4;
+  const uint32_t sbase = src0 + head;           // source offset of the first aligned chunk
+  const uint32_t mis = sbase & 3u;
+  for (uint64_t c = lane; c < nchunks; c += WAVE) {
+    uint32_t so = sbase + (uint32_t)(c << 4);
+    v4 v;
+    if (mis == 0) {
+      v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)so, 0, 0);
+    } else {
+      uint32_t a = so & ~3u, sh = mis * 8u;
+      uint32_t x0 = ld32(rs, a), x1 = ld32(rs, a + 4), x2 = ld32(rs, a + 8), x3 = ld32(rs, a + 12), x4 = ld32(rs, a + 16);
+      v.x = (x0 >> sh) | (x1 << (32u - sh));
+      v.y = (x1 >> sh) | (x2 << (32u - sh));
+      v.z = (x2 >> sh) | (x3 << (32u - sh));
+      v.w = (x3 >> sh) | (x4 << (32u - sh));
+    }
+    __builtin_nontemporal_store(v, (v4*)(a0 + (c << 4)));
+  }
+}
+
+// PLAIN BOOLEAN (BooleanPlainValuesReader -> ByteBitPackingValuesReader(1, LE)):
+// bit i of the section (bytes past the section read as 0) -> one byte 0/1.
+__global__ __launch_bounds__(64) void k_plain_bool(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                   const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                                   const int32_t* __restrict__ list, int n_list, uint64_t* err,
+                                                   uint32_t* err_count) {
+  const int page = list[blockIdx.x];
+  const PageWork pw = work[page];
+  const ColumnDev cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint32_t beg = uni(pw.data_begin), end = uni(pw.size);
+  const uint32_t n = uni(pw.n_values);
+  // ByteBitPackingValuesReader.initFromPage :77-88: min(ceil(num_values/8), available) bytes
+  uint64_t want = ((uint64_t)pw.num_slots + 7u) / 8u;
+  uint32_t avail = end > beg ? end - beg : 0;
+  uint32_t lim = beg + (uint32_t)(want < avail ? want : avail);
+  rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  uint8_t* dst = (uint8_t*)cd.values + pw.out_offset;
+  for (uint32_t i = lane; i < n; i += WAVE) {
+    uint32_t o = beg + (i >> 3);
+    uint32_t b = o < lim ? (ld32(rs, o & ~3u) >> ((o & 3u) * 8u)) & 0xFFu : 0u;
+    dst[i] = (uint8_t)((b >> (i & 7u)) & 1u);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// DELTA_BINARY_PACKED (DeltaBinaryPackingValuesReader.initFromPage :59-77, eager):
+// the wave walks block headers (min delta, miniblock widths) into registers
+// (block b -> lane b % 64), then per block each lane unpacks its deltas, a
+// wave-wide inclusive scan (wrapping int64) turns them into values. INT32 =
+// (int) of the long (readInteger :103-107).
+template <int W>
+__global__ __launch_bounds__(64) void k_delta(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                              const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                              const int32_t* __restrict__ list, int n_list, uint64_t* err,
+                                              uint32_t* err_count) {
+  const int page = list[blockIdx.x];
+  const PageWork pw = work[page];
+  const ColumnDev cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint32_t beg = uni(pw.data_begin), end = uni(pw.size);
+  const uint32_t want = uni(pw.n_values);
+  Window win;
+  win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  win.seek(beg);
+  uint32_t p = beg, len;
+  // header (DeltaBinaryPackingConfig.readConfig :43-45, totalValueCount, first value)
+#define DELTA_FAIL(code_)                                              \
+  do {                                                                 \
+    if (lane == 0) report(err, err_count, page, 0, 2, (code_));        \
+    return;                                                            \
+  } while (0)
+  if (p >= end) DELTA_FAIL(PQG_ERR_EOF);
+  uint32_t block = read_uvarint(win, p, end - p, len);
+  if ((uint64_t)p + len > end) DELTA_FAIL(PQG_ERR_EOF);
+  p += len;
+  if (p >= end) DELTA_FAIL(PQG_ERR_EOF);
+  uint32_t mbn = read_uvarint(win, p, end - p, len);
+  if ((uint64_t)p + len > end) DELTA_FAIL(PQG_ERR_EOF);
+  p += len;
+  // DeltaBinaryPackingConfig ctor :34-41 (double division, % 8)
+  if (mbn == 0 || (int32_t)mbn < 0 || (int32_t)block < 0) DELTA_FAIL(mbn == 0 ? PQG_ERR_DELTA_CONFIG : PQG_ERR_CORRUPT);
+  if ((block % mbn) != 0 || ((block / mbn) % 8u) != 0) DELTA_FAIL(PQG_ERR_DELTA_CONFIG);
+  const uint32_t mbs = block / mbn;
+  if (mbs == 0) DELTA_FAIL(PQG_ERR_CORRUPT);
+  // register budget of this kernel: block <= 512 values, <= 8 miniblocks (parquet-mr default 128 / 4)
+  if (block > 512u || mbn > 8u) DELTA_FAIL(PQG_ERR_UNSUPPORTED);
+  if (p >= end) DELTA_FAIL(PQG_ERR_EOF);
+  uint32_t total = read_uvarint(win, p, end - p, len);
+  if ((uint64_t)p + len > end) DELTA_FAIL(PQG_ERR_EOF);
+  p += len;
+  if ((int32_t)total < 0) DELTA_FAIL(PQG_ERR_CORRUPT);
+  if (p >= end) DELTA_FAIL(PQG_ERR_EOF);
+  uint64_t fraw = read_uvarlong(win, p, end - p, len);
+  if ((uint64_t)p + len > end) DELTA_FAIL(PQG_ERR_EOF);
+  p += len;
+  const int64_t first = zigzag64(fraw);
+  // values to emit: min(want, total); want > total -> "no more value to read" at index total
+  uint32_t n_out = want;
+  if (want > total) {
+    n_out = total;
+  }
+  typedef typename DictVal<W>::T T;
+  T* out = (T*)cd.values + pw.out_offset;
+  // Value index k (0-based) of the page: k = 0 is `first`; block b covers
+  // k in [1 + b*block, 1 + (b+1)*block).
+  uint64_t carry = (uint64_t)first;
+  if (lane == 0 && n_out > 0) out[0] = (T)carry;
+  uint32_t buffered = 1;  // Java valuesBuffered (includes the first value)
+  const uint32_t E = (block + WAVE - 1) / WAVE;  // deltas per lane per block
+  bool fail = false;
+  int fail_code = 0;
+  while (buffered < total) {
+    // ---- walk up to 64 blocks (headers + data offsets)
+    uint32_t b_data = 0, b_wpos = 0, b_lo = 0, b_hi = 0, b_nmb = 0;
+    uint32_t nb = 0;
+    uint32_t blk_first = buffered;
+    while (nb < 64u && buffered < total) {
+      if (p >= end) { fail = true; fail_code = PQG_ERR_EOF; break; }
+      uint64_t mraw = read_uvarlong(win, p, end - p, len);               // loadNewBlockToBuffer :122-126
+      if ((uint64_t)p + len > end) { fail = true; fail_code = PQG_ERR_EOF; break; }
+      p += len;
+      int64_t mind = zigzag64(mraw);
+      if ((uint64_t)p + mbn > end) { fail = true; fail_code = PQG_ERR_EOF; break; }  // readBitWidthsForMiniBlocks
+      uint32_t wpos = p;
+      p += mbn;
+      // miniblocks unpacked while buffered < total (:131-135)
+      uint32_t used = 0;
+      uint64_t dbytes = 0;
+      uint32_t bufd = buffered;
+      for (uint32_t m = 0; m < mbn && bufd < total; m++) {
+        uint32_t wm = win.byte(wpos + m);
+        if (wm > 64u) { fail = true; fail_code = PQG_ERR_CORRUPT; break; }
+        dbytes += (uint64_t)wm * (mbs / 8u);
+        bufd += mbs;
+        used++;
+      }
+      if (fail) break;
+      if ((uint64_t)p + dbytes > end) { fail = true; fail_code = PQG_ERR_EOF; break; }  // in.slice EOF
+      const bool me = lane == nb;
+      b_data = me ? p : b_data;
+      b_wpos = me ? wpos : b_wpos;
+      b_lo = me ? (uint32_t)(uint64_t)mind : b_lo;
+      b_hi = me ? (uint32_t)((uint64_t)mind >> 32) : b_hi;
+      b_nmb = me ? used : b_nmb;
+      p += (uint32_t)dbytes;
+      win.ensure(p);
+      buffered = bufd;
+      nb++;
+    }
+    if (fail) break;
+    // ---- expand the walked blocks
+    for (uint32_t b = 0; b < nb; b++) {
+      const uint32_t data = rdl(b_data, b), wpos = rdl(b_wpos, b), nmb = rdl(b_nmb, b);
+      const uint64_t mind = ((uint64_t)rdl(b_hi, b) << 32) | rdl(b_lo, b);
+      const uint32_t k0 = blk_first + b * block;  // value index of the block's first delta
+      uint64_t loc[8];
+      uint64_t sum = 0;
+      // miniblock widths of this block (≤ 8 miniblocks handled in registers)
+      uint32_t wmb[8], offmb[8];
+      {
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t mm = 0; mm < 8; mm++) {
+          uint32_t wm = mm < nmb ? (ld32(win.rs, (wpos + mm) & ~3u) >> (((wpos + mm) & 3u) * 8u)) & 0xFFu : 0u;
+          wmb[mm] = wm;
+          offmb[mm] = acc;
+          acc += wm * (mbs / 8u);
+        }
+      }
+      // lane handles deltas j in [lane*E, lane*E + E), E <= 8
+#pragma unroll
+      for (uint32_t q = 0; q < 8; q++) {
+        uint64_t d = 0;
+        uint32_t j = lane * E + q;
+        if (q < E && j < block) {
+          uint32_t m = j / mbs;
+          if (m < nmb) {
+            uint32_t wm = 0, off = 0;
+#pragma unroll
+            for (uint32_t mm = 0; mm < 8; mm++)
+              if (mm == m) { wm = wmb[mm]; off = offmb[mm]; }
+            if (wm) {
+              uint64_t bit = (uint64_t)(j % mbs) * wm;
+              uint32_t byte = data + off + (uint32_t)(bit >> 3);
+              uint32_t a = byte & ~3u;
+              uint32_t x0 = ld32(win.rs, a), x1 = ld32(win.rs, a + 4), x2 = ld32(win.rs, a + 8);
+              uint32_t sh = (byte - a) * 8u + (uint32_t)(bit & 7u);  // < 32
+              uint64_t lo64 = (uint64_t)x0 | ((uint64_t)x1 << 32);
+              uint64_t v = sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)));
+              d = wm == 64 ? v : (v & ((1ull << wm) - 1ull));
+            }
+          }
+          d += mind;  // wrapping: minDelta + unpacked (loadNewBlockToBuffer :139-142)
+        }
+        sum += d;
+        loc[q] = sum;
+      }
+      // wave exclusive scan of lane sums (wrapping 64-bit)
+      uint64_t x = sum;
+      for (int o = 1; o < 64; o <<= 1) {
+        uint64_t y = __shfl_up(x, o);
+        if ((int)lane >= o) x += y;
+      }
+      uint64_t excl = x - sum;
+      uint64_t base_v = carry + excl;
+      // write values k0 + j for j in this lane's range, k < n_out
+#pragma unroll
+      for (uint32_t q = 0; q < 8; q++) {
+        uint32_t j = lane * E + q;
+        uint64_t k = (uint64_t)k0 + j;
+        if (q < E && j < block && k < n_out) out[k] = (T)(base_v + loc[q]);
+      }
+      carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
+    }
+  }
+  if (fail) {
+    if (lane == 0) report(err, err_count, page, 0, 2, fail_code);
+    return;
+  }
+  if (want > total && lane == 0) report(err, err_count, page, 2, total, PQG_ERR_DELTA_PAST_END);
+#undef DELTA_FAIL
+}
+
+// ---------------------------------------------------------------------------
+// ParquetReadRouter batch: run r unpacks counts[r] LSB-first values of width w.
+__global__ __launch_bounds__(256) void k_unpack_runs(int w, const uint8_t* __restrict__ in, uint64_t in_bytes,
+                                                     const uint64_t* __restrict__ in_off, const uint32_t* __restrict__ counts,
+                                                     const uint64_t* __restrict__ out_off, int32_t* __restrict__ out,
+                                                     int n_runs) {
+  const int r = blockIdx.y;
+  if (r >= n_runs) return;
+  const uint32_t cnt = counts[r];
+  rsrc_t rs = make_rsrc(in + in_off[r], in_bytes - in_off[r]);
+  int32_t* o = out + out_off[r];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+    uint32_t v = 0;
+    if (w) {
+      uint64_t bit = (uint64_t)i * (uint32_t)w;
+      uint32_t byte = (uint32_t)(bit >> 3), a = byte & ~3u;
+      uint64_t x = (uint64_t)ld32(rs, a) | ((uint64_t)ld32(rs, a + 4) << 32);
+      x >>= (byte - a) * 8u + (uint32_t)(bit & 7u);
+      v = w == 32 ? (uint32_t)x : (uint32_t)x & ((1u << w) - 1u);
+    }
+    o[i] = (int32_t)v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers (host side of this translation unit)
+
+#define PQG_LAUNCH_ARGS bytes, n_bytes, work, cols, list, n, err, err_count
+
+hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                       const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+  if (n <= 0) return hipSuccess;
+  if (width == 8) hipLaunchKernelGGL(k_dict<8>, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
+  else hipLaunchKernelGGL(k_dict<4>, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
+  return hipGetLastError();
+}
+
+hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
+                         const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_levels, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan(hipStream_t st, PageWork* work, const int32_t* col_pages, const int32_t* col_page_start,
+                       int n_cols) {
+  if (n_cols <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scan_offsets, dim3(n_cols), dim3(256), 0, st, work, col_pages, col_page_start, n_cols);
+  return hipGetLastError();
+}
+
+hipError_t launch_plain(int kind, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+  if (n <= 0) return hipSuccess;
+  if (kind == 1) hipLaunchKernelGGL(k_plain_bool, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
+  else hipLaunchKernelGGL(k_plain, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+  if (n <= 0) return hipSuccess;
+  if (width == 8) hipLaunchKernelGGL(k_delta<8>, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
+  else hipLaunchKernelGGL(k_delta<4>, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
+  return hipGetLastError();
+}
+
+hipError_t launch_unpack_runs(hipStream_t st, int w, const uint8_t* in, uint64_t in_bytes, const uint64_t* in_off,
+                              const uint32_t* counts, const uint64_t* out_off, int32_t* out, int n_runs,
+                              uint32_t max_count) {
+  if (n_runs <= 0) return hipSuccess;
+  uint32_t gx = (max_count + 255u) / 256u;
+  if (gx == 0) gx = 1;
+  if (gx > 64) gx = 64;
+  hipLaunchKernelGGL(k_unpack_runs, dim3(gx, n_runs), dim3(256), 0, st, w, in, in_bytes, in_off, counts, out_off, out,
+                     n_runs);
+  return hipGetLastError();
+}
+
+}  // namespace pqg

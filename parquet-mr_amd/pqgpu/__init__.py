@@ -1,0 +1,12 @@
+"""pqgpu — MI355X-native Parquet column-page decoder (drop-in for parquet-mr's page-decode path).
+
+Layout:
+  abi      ctypes mirror of include/pqgpu.h (the C ABI)
+  native   loader of libpqgpu.so (HIP kernels + C ABI); no CPU fallback
+  decoder  device-resident batch decode (Decoder, Plan)
+  writer   parquet-mr-identical page synthesis (bench / test inputs)
+  dist     row-group sharding across GPUs + RCCL gather
+"""
+from . import abi  # noqa: F401
+
+__all__ = ["abi", "native", "decoder", "writer", "dist"]

@@ -1,0 +1,137 @@
+"""ctypes mirror of include/pqgpu.h (the C ABI).
+
+Only data layout and constants live here; `native.py` binds the functions of
+libpqgpu.so and the oracle binds the same structs for the CPU checker.
+"""
+import ctypes as C
+
+import numpy as np
+
+ABI_VERSION = 1
+
+# parquet-format Type
+BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY = range(8)
+TYPE_NAMES = {BOOLEAN: "BOOLEAN", INT32: "INT32", INT64: "INT64", INT96: "INT96", FLOAT: "FLOAT",
+              DOUBLE: "DOUBLE", BYTE_ARRAY: "BYTE_ARRAY", FIXED_LEN_BYTE_ARRAY: "FIXED_LEN_BYTE_ARRAY"}
+
+# parquet-format Encoding
+PLAIN = 0
+PLAIN_DICTIONARY = 2
+RLE = 3
+BIT_PACKED = 4
+DELTA_BINARY_PACKED = 5
+DELTA_LENGTH_BYTE_ARRAY = 6
+DELTA_BYTE_ARRAY = 7
+RLE_DICTIONARY = 8
+BYTE_STREAM_SPLIT = 9
+
+# pqg_error
+OK = 0
+ERR_INVALID_ARG = 1
+ERR_UNSUPPORTED = 2
+ERR_HIP = 3
+ERR_NO_DEVICE = 4
+ERR_EOF = 10
+ERR_RLE_PAST_END = 11
+ERR_BIT_WIDTH = 12
+ERR_DICT_ID = 13
+ERR_EMPTY_PAGE = 14
+ERR_EMPTY_PACKED_RUN = 15
+ERR_DELTA_CONFIG = 16
+ERR_DELTA_PAST_END = 17
+ERR_CORRUPT = 18
+ERR_NO_DICTIONARY = 19
+ERR_DICT_ENCODING = 20
+
+ERROR_NAMES = {
+    OK: "OK", ERR_INVALID_ARG: "INVALID_ARG", ERR_UNSUPPORTED: "UNSUPPORTED", ERR_HIP: "HIP",
+    ERR_NO_DEVICE: "NO_DEVICE", ERR_EOF: "EOF", ERR_RLE_PAST_END: "RLE_PAST_END",
+    ERR_BIT_WIDTH: "BIT_WIDTH", ERR_DICT_ID: "DICT_ID", ERR_EMPTY_PAGE: "EMPTY_PAGE",
+    ERR_EMPTY_PACKED_RUN: "EMPTY_PACKED_RUN", ERR_DELTA_CONFIG: "DELTA_CONFIG",
+    ERR_DELTA_PAST_END: "DELTA_PAST_END", ERR_CORRUPT: "CORRUPT", ERR_NO_DICTIONARY: "NO_DICTIONARY",
+    ERR_DICT_ENCODING: "DICT_ENCODING",
+}
+
+
+class PageDesc(C.Structure):
+    """pqg_page_desc (48 bytes)."""
+    _fields_ = [
+        ("offset", C.c_uint64),
+        ("size", C.c_uint32),
+        ("num_values", C.c_uint32),
+        ("column", C.c_int32),
+        ("version", C.c_int32),
+        ("encoding", C.c_int32),
+        ("rl_encoding", C.c_int32),
+        ("dl_encoding", C.c_int32),
+        ("rl_byte_length", C.c_uint32),
+        ("dl_byte_length", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
+PAGE_DTYPE = np.dtype([
+    ("offset", "<u8"), ("size", "<u4"), ("num_values", "<u4"), ("column", "<i4"), ("version", "<i4"),
+    ("encoding", "<i4"), ("rl_encoding", "<i4"), ("dl_encoding", "<i4"), ("rl_byte_length", "<u4"),
+    ("dl_byte_length", "<u4"), ("reserved", "<u4"),
+])
+assert PAGE_DTYPE.itemsize == C.sizeof(PageDesc) == 48
+
+
+class ColumnDesc(C.Structure):
+    """pqg_column_desc."""
+    _fields_ = [
+        ("physical_type", C.c_int32),
+        ("type_length", C.c_int32),
+        ("max_rep", C.c_int32),
+        ("max_def", C.c_int32),
+        ("dict_offset", C.c_int64),
+        ("dict_size", C.c_uint32),
+        ("dict_num_values", C.c_uint32),
+        ("dict_encoding", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("values", C.c_void_p),
+        ("values_capacity", C.c_uint64),
+        ("def_levels", C.c_void_p),
+        ("rep_levels", C.c_void_p),
+        ("levels_capacity", C.c_uint64),
+        ("binary_data", C.c_void_p),
+        ("binary_capacity", C.c_uint64),
+        ("values_written", C.c_uint64),
+    ]
+
+
+class Status(C.Structure):
+    """pqg_status."""
+    _fields_ = [
+        ("code", C.c_int32),
+        ("page", C.c_int32),
+        ("value_index", C.c_int64),
+        ("message", C.c_char * 240),
+    ]
+
+    def as_tuple(self):
+        return (int(self.code), int(self.page), int(self.value_index))
+
+
+def elem_width(physical_type, type_length=0):
+    """Width in bytes of one dense output element (pqgpu.h, pqg_column_desc)."""
+    return {BOOLEAN: 1, INT32: 4, FLOAT: 4, INT64: 8, DOUBLE: 8, INT96: 12,
+            FIXED_LEN_BYTE_ARRAY: type_length, BYTE_ARRAY: 8}[physical_type]
+
+
+def numpy_dtype(physical_type, type_length=0):
+    """numpy dtype of the dense output for a physical type."""
+    if physical_type == BOOLEAN:
+        return np.dtype(np.uint8)
+    if physical_type == INT32:
+        return np.dtype("<i4")
+    if physical_type == INT64:
+        return np.dtype("<i8")
+    if physical_type == FLOAT:
+        return np.dtype("<f4")
+    if physical_type == DOUBLE:
+        return np.dtype("<f8")
+    if physical_type == BYTE_ARRAY:
+        return np.dtype("<i8")  # offsets
+    return np.dtype((np.void, elem_width(physical_type, type_length)))

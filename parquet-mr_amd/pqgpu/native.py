@@ -1,0 +1,68 @@
+"""ctypes binding of libpqgpu.so (the C ABI in include/pqgpu.h).
+
+The HIP library is the only decode path: if it is missing or has no device,
+the calls below raise — there is no CPU fallback in the product.
+"""
+import ctypes as C
+import os
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpqgpu.so")
+_LIB = None
+
+EXPORTS = [
+    "pqg_abi_version", "pqg_device_count", "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_stream", "pqg_decode",
+    "pqg_sync", "pqg_plan_create", "pqg_plan_launch", "pqg_plan_kernel_count", "pqg_plan_destroy",
+    "pqg_decode_host", "pqg_unpack_runs", "pqg_router_read", "pqg_error_name",
+]
+
+
+class PqgError(RuntimeError):
+    """A decode error; mirrors org.apache.parquet.io.ParquetDecodingException."""
+
+    def __init__(self, code, status=None, what=""):
+        self.code = int(code)
+        self.status = status
+        name = abi.ERROR_NAMES.get(self.code, str(self.code))
+        msg = f"{what}: {name}" if what else name
+        if status is not None:
+            msg += f" (page {status.page}, index {status.value_index}): {status.message.decode(errors='replace')}"
+        super().__init__(msg)
+
+
+def lib():
+    """Load libpqgpu.so; raises if the HIP extension was not built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"HIP extension missing: {LIB_PATH} (run __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        vp, i32, u64 = C.c_void_p, C.c_int, C.c_uint64
+        L.pqg_abi_version.restype = i32
+        L.pqg_device_count.restype = i32
+        L.pqg_ctx_create.argtypes = [i32, vp, C.POINTER(vp)]
+        L.pqg_ctx_destroy.argtypes = [vp]
+        L.pqg_ctx_stream.argtypes = [vp]
+        L.pqg_ctx_stream.restype = vp
+        L.pqg_decode.argtypes = [vp, vp, u64, vp, i32, vp, i32, vp, C.POINTER(abi.Status)]
+        L.pqg_sync.argtypes = [vp, C.POINTER(abi.Status)]
+        L.pqg_plan_create.argtypes = [vp, vp, u64, vp, i32, vp, i32, C.POINTER(vp), C.POINTER(abi.Status)]
+        L.pqg_plan_launch.argtypes = [vp]
+        L.pqg_plan_kernel_count.argtypes = [vp]
+        L.pqg_plan_destroy.argtypes = [vp]
+        L.pqg_decode_host.argtypes = [vp, vp, u64, vp, i32, vp, i32, vp, C.POINTER(abi.Status)]
+        L.pqg_unpack_runs.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32]
+        L.pqg_router_read.argtypes = [vp, i32, vp, C.c_size_t, i32, vp]
+        L.pqg_error_name.argtypes = [i32]
+        L.pqg_error_name.restype = C.c_char_p
+        if L.pqg_abi_version() != abi.ABI_VERSION:
+            raise RuntimeError("libpqgpu.so ABI version mismatch")
+        _LIB = L
+    return _LIB
+
+
+def check(rc, status=None, what=""):
+    if rc != abi.OK:
+        raise PqgError(rc, status, what)

@@ -1,0 +1,341 @@
+"""Page writer: synthesizes parquet-mr-identical column chunks (test / bench input).
+
+The encoders are restated in C++ (csrc/pqwriter.cpp -> libpqwriter.so) from
+parquet-mr's writers; this module assembles their output into data pages the
+way parquet-mr's column writers do:
+
+  * V1 pages: [rl section][dl section][data]; RLE level sections carry the
+    4-byte little-endian length prefix written by
+    RunLengthBitPackingHybridValuesWriter.getBytes (rle/RunLengthBitPackingHybridValuesWriter.java:62-72);
+    max level 0 writes nothing (ParquetProperties.java:162-190, ColumnWriterV1.java:60-78).
+  * V2 pages: levels without length prefix, byte lengths in the header
+    (ColumnWriterV2.java:42-110).
+  * Dictionary: ids assigned in first-appearance order (DictionaryValuesWriter.java:
+    Plain*DictionaryValuesWriter.write*), data section = 1-byte bit width +
+    RLE/bit-packed ids (DictionaryValuesWriter.getBytes :159-186); dictionary
+    page = PLAIN values.
+
+The writer is input synthesis only; it is not part of the decode path.
+"""
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "libpqwriter.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
+        lib = C.CDLL(path)
+        i64, vp = C.c_int64, C.c_void_p
+        lib.pqw_rle_encode.argtypes = [C.c_int, vp, i64, vp, i64]
+        lib.pqw_rle_encode.restype = i64
+        lib.pqw_rle_encode_u8.argtypes = [C.c_int, vp, i64, vp, i64]
+        lib.pqw_rle_encode_u8.restype = i64
+        lib.pqw_delta_encode_long.argtypes = [vp, i64, C.c_int, C.c_int, vp, i64]
+        lib.pqw_delta_encode_long.restype = i64
+        lib.pqw_delta_encode_int.argtypes = [vp, i64, C.c_int, C.c_int, vp, i64]
+        lib.pqw_delta_encode_int.restype = i64
+        _LIB = lib
+    return _LIB
+
+
+def width_from_max_int(bound):
+    """BytesUtils.getWidthFromMaxInt (BytesUtils.java:49-51)."""
+    return int(bound).bit_length() if bound >= 0 else 32
+
+
+def _call_with_buffer(fn, *args, cap):
+    out = np.empty(max(cap, 16), dtype=np.uint8)
+    n = fn(*args, out.ctypes.data, out.size)
+    if n < 0:
+        out = np.empty(-n, dtype=np.uint8)
+        n = fn(*args, out.ctypes.data, out.size)
+    return out[:n].tobytes()
+
+
+def rle_encode(values, bit_width):
+    """RunLengthBitPackingHybridEncoder: <encoded-data> of `values` (no length prefix)."""
+    v = np.ascontiguousarray(values, dtype=np.int32)
+    cap = 64 + (len(v) // 8 + 2) * (max(bit_width, 9) + 2)
+    return _call_with_buffer(_lib().pqw_rle_encode, bit_width, v.ctypes.data, len(v), cap=cap)
+
+
+def rle_encode_levels(levels, bit_width):
+    v = np.ascontiguousarray(levels, dtype=np.uint8)
+    cap = 64 + (len(v) // 8 + 2) * (max(bit_width, 9) + 2)
+    return _call_with_buffer(_lib().pqw_rle_encode_u8, bit_width, v.ctypes.data, len(v), cap=cap)
+
+
+def delta_encode(values, physical_type, block=128, miniblocks=4):
+    """DeltaBinaryPackingValuesWriterFor{Long,Integer}.getBytes."""
+    if physical_type == abi.INT64:
+        v = np.ascontiguousarray(values, dtype=np.int64)
+        fn = _lib().pqw_delta_encode_long
+    else:
+        v = np.ascontiguousarray(values, dtype=np.int32)
+        fn = _lib().pqw_delta_encode_int
+    cap = 64 + len(v) * 9 + (len(v) // block + 1) * (miniblocks + 12)
+    return _call_with_buffer(fn, v.ctypes.data, len(v), block, miniblocks, cap=cap)
+
+
+def plain_encode(values, physical_type, type_length=0):
+    """PlainValuesWriter / BooleanPlainValuesWriter / FixedLenByteArrayPlainValuesWriter."""
+    if physical_type == abi.BOOLEAN:
+        bits = np.ascontiguousarray(values, dtype=np.uint8) & 1
+        return np.packbits(bits, bitorder="little").tobytes()
+    if physical_type == abi.BYTE_ARRAY:
+        out = bytearray()
+        for b in values:
+            out += len(b).to_bytes(4, "little") + bytes(b)
+        return bytes(out)
+    if physical_type in (abi.INT96, abi.FIXED_LEN_BYTE_ARRAY):
+        w = abi.elem_width(physical_type, type_length)
+        return b"".join(bytes(b)[:w].ljust(w, b"\0") for b in values)
+    return np.ascontiguousarray(values, dtype=abi.numpy_dtype(physical_type)).tobytes()
+
+
+def dictionary_encode(values):
+    """Ids in first-appearance order, as DictionaryValuesWriter assigns them."""
+    values = np.asarray(values)
+    uniq, first, inverse = np.unique(values, return_index=True, return_inverse=True)
+    order = np.argsort(first, kind="stable")
+    rank = np.empty_like(order)
+    rank[order] = np.arange(len(order))
+    ids = rank[inverse.reshape(-1)].astype(np.int32)
+    return ids, uniq[order]
+
+
+@dataclass
+class Page:
+    body: bytes
+    num_values: int
+    encoding: int
+    version: int = 1
+    rl_encoding: int = abi.RLE
+    dl_encoding: int = abi.RLE
+    rl_byte_length: int = 0
+    dl_byte_length: int = 0
+    num_nulls: int = 0
+    num_rows: int = 0
+
+
+@dataclass
+class ColumnChunk:
+    physical_type: int
+    max_rep: int = 0
+    max_def: int = 0
+    type_length: int = 0
+    pages: List[Page] = field(default_factory=list)
+    dict_page: Optional[bytes] = None
+    dict_num_values: int = 0
+    dict_encoding: int = abi.PLAIN
+    # expected decode (what the reference reader returns), for tests
+    values: Optional[object] = None
+    def_levels: Optional[np.ndarray] = None
+    rep_levels: Optional[np.ndarray] = None
+
+    @property
+    def num_slots(self):
+        return sum(p.num_values for p in self.pages)
+
+
+def _level_section(levels, max_level, version):
+    if max_level == 0:
+        return b""
+    body = rle_encode_levels(levels, width_from_max_int(max_level))
+    if version == 1:
+        return len(body).to_bytes(4, "little") + body
+    return body
+
+
+def _page_bounds(n_slots, page_rows, rep_levels):
+    """Slot ranges of each page: `page_rows` slots, closed at record boundaries."""
+    bounds = []
+    start = 0
+    while start < n_slots:
+        end = min(start + page_rows, n_slots)
+        if rep_levels is not None and end < n_slots:
+            while end < n_slots and rep_levels[end] != 0:
+                end += 1
+        bounds.append((start, end))
+        start = end
+    if not bounds:
+        bounds.append((0, 0))
+    return bounds
+
+
+def write_column_chunk(physical_type, values, encoding, *, def_levels=None, rep_levels=None, max_def=0,
+                       max_rep=0, page_rows=20000, version=1, type_length=0, delta_block=128,
+                       delta_miniblocks=4, dict_page_encoding=abi.PLAIN):
+    """Encode one column chunk. `values` are the non-null values (dense, in slot order)."""
+    values = values if physical_type == abi.BYTE_ARRAY or physical_type in (abi.INT96, abi.FIXED_LEN_BYTE_ARRAY) \
+        else np.asarray(values)
+    n_values = len(values)
+    if def_levels is None:
+        n_slots = n_values
+        dl = np.full(n_slots, max_def, dtype=np.uint8)
+    else:
+        dl = np.asarray(def_levels, dtype=np.uint8)
+        n_slots = len(dl)
+    rl = np.zeros(n_slots, dtype=np.uint8) if rep_levels is None else np.asarray(rep_levels, dtype=np.uint8)
+    nonnull = (dl == max_def)
+    assert int(nonnull.sum()) == n_values, "def levels disagree with the value count"
+    chunk = ColumnChunk(physical_type=physical_type, max_rep=max_rep, max_def=max_def, type_length=type_length,
+                        values=values, def_levels=dl if max_def else None, rep_levels=rl if max_rep else None)
+    ids = None
+    if encoding in (abi.RLE_DICTIONARY, abi.PLAIN_DICTIONARY):
+        if physical_type == abi.BYTE_ARRAY:
+            seen = {}
+            ids = np.empty(n_values, dtype=np.int32)
+            dict_vals = []
+            for i, b in enumerate(values):
+                b = bytes(b)
+                if b not in seen:
+                    seen[b] = len(dict_vals)
+                    dict_vals.append(b)
+                ids[i] = seen[b]
+        else:
+            ids, dict_vals = dictionary_encode(values)
+        chunk.dict_page = plain_encode(dict_vals, physical_type, type_length)
+        chunk.dict_num_values = len(dict_vals)
+        chunk.dict_encoding = dict_page_encoding
+        bit_width = width_from_max_int(len(dict_vals) - 1)
+    value_pos = np.concatenate([[0], np.cumsum(nonnull)]).astype(np.int64)
+    for (s, e) in _page_bounds(n_slots, page_rows, rl if max_rep else None):
+        v0, v1 = int(value_pos[s]), int(value_pos[e])
+        if encoding in (abi.RLE_DICTIONARY, abi.PLAIN_DICTIONARY):
+            data = bytes([bit_width]) + rle_encode(ids[v0:v1], bit_width)
+        elif encoding == abi.PLAIN:
+            data = plain_encode(values[v0:v1], physical_type, type_length)
+        elif encoding == abi.DELTA_BINARY_PACKED:
+            data = delta_encode(values[v0:v1], physical_type, delta_block, delta_miniblocks)
+        else:
+            raise ValueError(f"writer does not support encoding {encoding}")
+        rls = _level_section(rl[s:e], max_rep, version)
+        dls = _level_section(dl[s:e], max_def, version)
+        page = Page(body=rls + dls + data, num_values=e - s, encoding=encoding, version=version,
+                    num_nulls=int((e - s) - (v1 - v0)),
+                    num_rows=int((rl[s:e] == 0).sum()) if max_rep else e - s)
+        if version == 2:
+            page.rl_byte_length, page.dl_byte_length = len(rls), len(dls)
+        chunk.pages.append(page)
+    return chunk
+
+
+def write_dict_column_from_ids(physical_type, dict_values, ids, page_rows=20000, encoding=abi.RLE_DICTIONARY):
+    """Required dictionary column from ids already numbered in first-appearance order
+    (fast path for large synthetic inputs; same bytes as write_column_chunk)."""
+    ids = np.ascontiguousarray(ids, dtype=np.int32)
+    bit_width = width_from_max_int(len(dict_values) - 1)
+    chunk = ColumnChunk(physical_type=physical_type, values=None)
+    chunk.dict_page = plain_encode(dict_values, physical_type)
+    chunk.dict_num_values = len(dict_values)
+    for s in range(0, max(len(ids), 1), page_rows):
+        e = min(s + page_rows, len(ids))
+        data = bytes([bit_width]) + rle_encode(ids[s:e], bit_width)
+        chunk.pages.append(Page(body=data, num_values=e - s, encoding=encoding, num_rows=e - s))
+    chunk.n_values_hint = len(ids)
+    return chunk
+
+
+def first_appearance_ids(ids):
+    """Renumber ids in order of first appearance (DictionaryValuesWriter id assignment)."""
+    ids = np.asarray(ids)
+    uniq, first = np.unique(ids, return_index=True)
+    order = uniq[np.argsort(first, kind="stable")]
+    remap = np.empty(int(ids.max()) + 1 if ids.size else 1, dtype=np.int32)
+    remap[order] = np.arange(order.size, dtype=np.int32)
+    return remap[ids], order
+
+
+@dataclass
+class PageBatch:
+    """All pages of several column chunks in one byte buffer + descriptor tables."""
+    data: np.ndarray            # uint8, padded
+    pages: np.ndarray           # PAGE_DTYPE
+    columns: List[dict]         # pqg_column_desc fields without output pointers
+    chunks: List[ColumnChunk]
+    page_slot_offsets: np.ndarray  # per page: first slot within its column
+    column_slots: List[int]
+    column_values: List[int]
+
+    @property
+    def n_pages(self):
+        return len(self.pages)
+
+
+ALIGN = 16
+PAD = 256
+
+
+def build_batch(chunks, align=ALIGN):
+    """Lay chunks out in one buffer (each page 16-B aligned), build the descriptor tables.
+
+    Several chunks may belong to the same output column (row groups of one column):
+    pass `column_of` on the chunk objects via attribute `column_index` to merge.
+    """
+    pieces = []
+    pos = 0
+
+    def place(b):
+        nonlocal pos
+        off = (pos + align - 1) // align * align
+        pieces.append((off, b))
+        pos = off + len(b)
+        return off
+
+    # output columns: chunks with the same column_index share one output column
+    col_index = []
+    columns = []
+    seen = {}
+    for i, ch in enumerate(chunks):
+        key = getattr(ch, "column_index", i)
+        if key not in seen:
+            seen[key] = len(columns)
+            columns.append(None)
+        col_index.append(seen[key])
+    page_rows = []
+    slot_off = []
+    col_slots = [0] * len(columns)
+    col_vals = [0] * len(columns)
+    dict_info = {}
+    for ci, ch in enumerate(chunks):
+        oc = col_index[ci]
+        doff = -1
+        if ch.dict_page is not None:
+            doff = place(ch.dict_page)
+        dict_info.setdefault(oc, []).append(doff)
+        if columns[oc] is None:
+            columns[oc] = dict(physical_type=ch.physical_type, type_length=ch.type_length, max_rep=ch.max_rep,
+                               max_def=ch.max_def, dict_offset=doff,
+                               dict_size=len(ch.dict_page) if ch.dict_page is not None else 0,
+                               dict_num_values=ch.dict_num_values, dict_encoding=ch.dict_encoding)
+        elif ch.dict_page is not None:
+            raise ValueError("a pqg_column_desc has one dictionary: decode row groups with separate "
+                             "dictionaries as separate columns (one per row group)")
+        for pg in ch.pages:
+            off = place(pg.body)
+            page_rows.append((off, len(pg.body), pg.num_values, oc, pg.version, pg.encoding, pg.rl_encoding,
+                              pg.dl_encoding, pg.rl_byte_length, pg.dl_byte_length, 0))
+            slot_off.append(col_slots[oc])
+            col_slots[oc] += pg.num_values
+        col_vals[oc] += len(ch.values) if ch.values is not None else getattr(ch, "n_values_hint", 0)
+    total = pos + PAD
+    data = np.zeros((total + align - 1) // align * align, dtype=np.uint8)
+    for off, b in pieces:
+        data[off:off + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    pages = np.array(page_rows, dtype=abi.PAGE_DTYPE) if page_rows else np.zeros(0, dtype=abi.PAGE_DTYPE)
+    return PageBatch(data=data, pages=pages, columns=columns, chunks=list(chunks),
+                     page_slot_offsets=np.array(slot_off, dtype=np.int64), column_slots=col_slots,
+                     column_values=col_vals)

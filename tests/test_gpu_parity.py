@@ -1,0 +1,278 @@
+"""GPU parity: libpqgpu.so (through the C ABI) vs the oracle on the same pages.
+
+Bit-exact on values (floats compared as bit patterns), levels, per-page value
+counts and the first error (code, page, index). Cases follow the reference's
+tests and BASELINE.json's configs at oracle-friendly sizes.
+"""
+import numpy as np
+import pytest
+
+from oracle import pqref
+from pqgpu import abi, writer
+
+from helpers import assert_same, make, nulls, zipf_dict_column
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(decoder, chunks, expect_error=False):
+    batch = writer.build_batch(chunks)
+    ref = pqref.decode_batch(batch)
+    dcols, st = decoder.decode(decoder.upload(batch), check=False)
+    assert (int(st.code), int(st.page), int(st.value_index)) == ref.status, \
+        f"gpu status {st.code, st.page, st.value_index} {st.message} vs oracle {ref.status}"
+    if expect_error:
+        assert ref.code != 0
+        return batch, ref, dcols
+    assert ref.code == 0, ref.status
+    for i, cd in enumerate(batch.columns):
+        col = dcols[i]
+        assert col.n_values == ref.columns[i]["n_values"]
+        assert_same(col.numpy(), ref.columns[i]["values"], cd["physical_type"])
+        if cd["max_def"] > 0:
+            assert np.array_equal(col.def_levels[:batch.column_slots[i]].cpu().numpy(), ref.columns[i]["def_levels"])
+        if cd["max_rep"] > 0:
+            assert np.array_equal(col.rep_levels[:batch.column_slots[i]].cpu().numpy(), ref.columns[i]["rep_levels"])
+    return batch, ref, dcols
+
+
+# ---- config 2 shape: RLE_DICTIONARY int64, Zipf run lengths --------------------------------------------
+
+@pytest.mark.parametrize("a", [1.5, 2.0, 3.0])
+@pytest.mark.parametrize("card", [1, 2, 1000, 70000])
+def test_dict_int64_zipf(decoder, a, card):
+    vals = zipf_dict_column(200_000, card=card, a=a, seed=int(a * 10) + card)
+    run_both(decoder, [make(abi.INT64, vals, abi.RLE_DICTIONARY)])
+
+
+@pytest.mark.parametrize("ptype", [abi.INT32, abi.FLOAT, abi.DOUBLE])
+def test_dict_other_types(decoder, ptype):
+    vals = zipf_dict_column(120_000, card=300, a=1.7, seed=3, physical_type=ptype)
+    run_both(decoder, [make(ptype, vals, abi.PLAIN_DICTIONARY, dict_page_encoding=abi.PLAIN_DICTIONARY)])
+
+
+@pytest.mark.parametrize("page_rows", [1, 7, 8, 9, 504, 505, 20000])
+def test_dict_page_sizes(decoder, page_rows):
+    vals = zipf_dict_column(30_000, card=50, a=1.3, seed=page_rows)
+    run_both(decoder, [make(abi.INT64, vals, abi.RLE_DICTIONARY, page_rows=page_rows)])
+
+
+def test_dict_multiple_columns_interleaved(decoder):
+    chunks = []
+    for k in range(4):
+        v = zipf_dict_column(50_000, card=10 + k * 200, a=1.5 + 0.2 * k, seed=k,
+                             physical_type=abi.INT64 if k % 2 == 0 else abi.INT32)
+        chunks.append(make(abi.INT64 if k % 2 == 0 else abi.INT32, v, abi.RLE_DICTIONARY, page_rows=7000))
+    batch = writer.build_batch(chunks)
+    # interleave pages of the 4 columns (page order within a column kept)
+    order = np.argsort(np.arange(batch.n_pages) % 7, kind="stable")
+    cols = batch.pages["column"][order]
+    for c in range(4):  # keep per-column order
+        idx = np.nonzero(cols == c)[0]
+        order[idx] = np.sort(order[idx])
+    batch.pages = batch.pages[order]
+    batch.page_slot_offsets = batch.page_slot_offsets[order]
+    ref = pqref.decode_batch(batch)
+    dcols, st = decoder.decode(decoder.upload(batch), check=False)
+    assert st.code == 0 and ref.code == 0
+    for i in range(4):
+        assert_same(dcols[i].numpy(), ref.columns[i]["values"], batch.columns[i]["physical_type"])
+
+
+def test_dict_known_answer_pages(decoder):
+    """TestDictionary.testLongDictionary (:285-317): 1000 x (i % 50), then 2000 descending."""
+    v1 = np.arange(1000, dtype=np.int64) % 50
+    v2 = np.arange(2000, 0, -1, dtype=np.int64) % 50
+    ch = make(abi.INT64, np.concatenate([v1, v2]), abi.PLAIN_DICTIONARY, page_rows=1000)
+    batch, ref, dcols = run_both(decoder, [ch])
+    assert np.array_equal(dcols[0].numpy(), np.concatenate([v1, v2]))
+
+
+# ---- nulls / levels (configs 3 and 5) -------------------------------------------------------------------
+
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("enc,ptype", [(abi.RLE_DICTIONARY, abi.INT64), (abi.PLAIN, abi.DOUBLE),
+                                       (abi.PLAIN, abi.INT32), (abi.DELTA_BINARY_PACKED, abi.INT64),
+                                       (abi.DELTA_BINARY_PACKED, abi.INT32), (abi.PLAIN, abi.BOOLEAN)])
+@pytest.mark.parametrize("null_frac", [0.0, 0.1, 0.9, 1.0])
+def test_optional_columns(decoder, version, enc, ptype, null_frac):
+    n_slots = 50_000
+    dl = nulls(n_slots, null_frac, seed=5)
+    n = int(dl.sum())
+    rng = np.random.default_rng(11)
+    if enc == abi.RLE_DICTIONARY:
+        vals = zipf_dict_column(max(n, 1), card=500, seed=2)[:n]
+    elif ptype == abi.DOUBLE:
+        vals = rng.standard_normal(n)
+    elif ptype == abi.BOOLEAN:
+        vals = rng.integers(0, 2, size=n).astype(np.uint8)
+    elif enc == abi.DELTA_BINARY_PACKED and ptype == abi.INT64:
+        vals = np.cumsum(rng.integers(-1000, 100000, size=n)).astype(np.int64)
+    else:
+        vals = rng.integers(-2**31, 2**31 - 1, size=n).astype(np.int32)
+    ch = make(ptype, vals, enc, def_levels=dl, max_def=1, version=version, page_rows=20000)
+    run_both(decoder, [ch])
+
+
+@pytest.mark.parametrize("version", [1, 2])
+def test_nested_list_levels(decoder, version):
+    """Config 5 shape: optional group (LIST) { repeated group list { optional int64 element } }:
+    max_rep 1, max_def 3. Lists ~ Poisson(3), 10% null lists, 10% null elements."""
+    rng = np.random.default_rng(11)
+    recs = 20_000
+    lens = rng.poisson(3, size=recs)
+    null_list = rng.random(recs) < 0.1
+    rl, dl = [], []
+    for L, nl in zip(lens, null_list):
+        if nl:
+            rl.append(0); dl.append(0)
+        elif L == 0:
+            rl.append(0); dl.append(1)
+        else:
+            for j in range(L):
+                rl.append(0 if j == 0 else 1)
+                dl.append(3 if rng.random() >= 0.1 else 2)
+    rl = np.array(rl, dtype=np.uint8)
+    dl = np.array(dl, dtype=np.uint8)
+    n = int((dl == 3).sum())
+    vals = rng.integers(-2**40, 2**40, size=n).astype(np.int64)
+    ch = make(abi.INT64, vals, abi.PLAIN, def_levels=dl, rep_levels=rl, max_def=3, max_rep=1, version=version,
+              page_rows=5000)
+    run_both(decoder, [ch])
+
+
+# ---- PLAIN (config 1 shape) and DELTA (config 3 shape) ----------------------------------------------------
+
+@pytest.mark.parametrize("ptype", [abi.INT32, abi.INT64, abi.FLOAT, abi.DOUBLE, abi.BOOLEAN])
+@pytest.mark.parametrize("n", [0, 1, 15, 1_000_000])
+def test_plain_required(decoder, ptype, n):
+    rng = np.random.default_rng(n)
+    dt = abi.numpy_dtype(ptype)
+    if ptype == abi.BOOLEAN:
+        vals = rng.integers(0, 2, size=n).astype(np.uint8)
+    else:
+        vals = rng.integers(0, 255, size=n * dt.itemsize, dtype=np.uint8).view(dt)
+    run_both(decoder, [make(ptype, vals, abi.PLAIN, page_rows=20000)])
+
+
+@pytest.mark.parametrize("ptype,w", [(abi.FIXED_LEN_BYTE_ARRAY, 3), (abi.FIXED_LEN_BYTE_ARRAY, 16),
+                                     (abi.INT96, 12)])
+def test_plain_fixed_len(decoder, ptype, w):
+    rng = np.random.default_rng(w)
+    vals = [rng.integers(0, 255, size=w, dtype=np.uint8).tobytes() for _ in range(5000)]
+    run_both(decoder, [make(ptype, vals, abi.PLAIN, type_length=w if ptype == abi.FIXED_LEN_BYTE_ARRAY else 0,
+                            page_rows=999)])
+
+
+@pytest.mark.parametrize("ptype", [abi.INT32, abi.INT64])
+@pytest.mark.parametrize("kind", ["walk", "random", "minmax", "const", "short"])
+def test_delta(decoder, ptype, kind):
+    rng = np.random.default_rng(7)
+    n = 100_003
+    info = np.iinfo(np.int64 if ptype == abi.INT64 else np.int32)
+    if kind == "walk":
+        vals = np.cumsum(rng.integers(-50, 500, size=n))
+    elif kind == "random":
+        vals = rng.integers(info.min, info.max, size=n, dtype=np.int64)
+    elif kind == "minmax":  # DeltaBinaryPackingValuesWriterForLongTest.shouldReadMaxMinValue (:130-141)
+        vals = np.where(np.arange(n) % 2 == 0, info.min, info.max)
+    elif kind == "const":
+        vals = np.full(n, 3)
+    else:
+        n = 29
+        vals = rng.integers(-10, 10, size=n)
+    vals = vals.astype(np.int64 if ptype == abi.INT64 else np.int32)
+    run_both(decoder, [make(ptype, vals, abi.DELTA_BINARY_PACKED, page_rows=20000)])
+
+
+@pytest.mark.parametrize("block,mb", [(128, 4), (64, 8), (256, 8), (512, 8), (32, 1)])
+def test_delta_configs(decoder, block, mb):
+    rng = np.random.default_rng(block)
+    vals = np.cumsum(rng.integers(-3, 1 << 20, size=40_000)).astype(np.int64)
+    run_both(decoder, [make(abi.INT64, vals, abi.DELTA_BINARY_PACKED, delta_block=block, delta_miniblocks=mb)])
+
+
+# ---- error classification ----------------------------------------------------------------------------
+
+def _dict_chunk(n=5000, card=100, seed=1):
+    return make(abi.INT64, zipf_dict_column(n, card=card, a=1.5, seed=seed), abi.RLE_DICTIONARY, page_rows=1000)
+
+
+def test_error_dict_id_out_of_range(decoder):
+    ch = _dict_chunk()
+    ch.dict_num_values = 10  # ids >= 10 now out of range (AIOOBE in decodeToLong)
+    run_both(decoder, [ch], expect_error=True)
+
+
+def test_error_bit_width(decoder):
+    ch = _dict_chunk()
+    pg = ch.pages[2]
+    pg.body = bytes([33]) + pg.body[1:]
+    run_both(decoder, [ch], expect_error=True)
+
+
+@pytest.mark.parametrize("cut", [1, 2, 5, 40])
+def test_error_truncated_page(decoder, cut):
+    ch = _dict_chunk(card=1000, seed=4)
+    pg = ch.pages[3]
+    pg.body = pg.body[:max(1, len(pg.body) - cut)]
+    batch, ref, _ = run_both(decoder, [ch], expect_error=ref_errors(ch))
+
+
+def ref_errors(ch):
+    return pqref.decode_batch(writer.build_batch([ch])).code != 0
+
+
+def test_error_empty_page(decoder):
+    ch = _dict_chunk()
+    ch.pages[1].body = b""
+    run_both(decoder, [ch], expect_error=True)
+
+
+def test_error_plain_eof(decoder):
+    ch = make(abi.INT64, np.arange(5000, dtype=np.int64), abi.PLAIN, page_rows=1000)
+    ch.pages[2].body = ch.pages[2].body[:-12]
+    run_both(decoder, [ch], expect_error=True)
+
+
+def test_error_delta_past_end(decoder):
+    ch = make(abi.INT64, np.arange(3000, dtype=np.int64), abi.DELTA_BINARY_PACKED, page_rows=1000)
+    ch.pages[1].num_values = 1500  # header total is 1000
+    run_both(decoder, [ch], expect_error=True)
+
+
+def test_error_missing_dictionary(decoder):
+    ch = _dict_chunk()
+    ch.dict_page = None
+    run_both(decoder, [ch], expect_error=True)
+
+
+def test_error_level_section_length(decoder):
+    dl = nulls(4000, 0.2, seed=1)
+    ch = make(abi.DOUBLE, np.random.default_rng(0).standard_normal(int(dl.sum())), abi.PLAIN, def_levels=dl,
+              max_def=1, version=1, page_rows=1000)
+    body = bytearray(ch.pages[1].body)
+    body[0:4] = (len(body) + 10).to_bytes(4, "little")
+    ch.pages[1].body = bytes(body)
+    run_both(decoder, [ch], expect_error=True)
+
+
+# ---- ParquetReadRouter -------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("w", list(range(0, 33)))
+def test_router_read(decoder, w):
+    rng = np.random.default_rng(w)
+    count = 2048
+    data = rng.integers(0, 256, size=count * w // 8 + 3, dtype=np.uint8)
+    got = decoder.router_read(w, data, count)
+    ref, _ = pqref.router_read(w, data, count)
+    assert np.array_equal(got, ref)
+
+
+def test_host_path_roundtrip(decoder):
+    vals = zipf_dict_column(100_000, card=1000, seed=9)
+    batch = writer.build_batch([make(abi.INT64, vals, abi.RLE_DICTIONARY)])
+    rc, st, res, counts = decoder.decode_host(batch)
+    assert rc == 0, st.message
+    assert np.array_equal(res[0]["values"], vals)
+    assert counts.sum() == vals.size
