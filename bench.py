@@ -120,11 +120,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    with torch.cuda.stream(stream):
-        ev[0].record(stream)
-        for k in range(args.steps):
-            plan.launch()
-            ev[k + 1].record(stream)
+    ev[0].record(stream)
+    for k in range(args.steps):
+        plan.launch()
+        ev[k + 1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -31,6 +31,37 @@
 namespace pqg {
 
 constexpr int WAVE = 64;
+// Pages per workgroup: one page per wave, 4 waves per 256-lane workgroup. One-wave
+// workgroups cap residency by the per-CU workgroup limit (measured: ~2.3k of 5k
+// waves resident), so pages are packed 4 to a workgroup.
+constexpr int WPB = 4;
+
+__device__ __forceinline__ uint32_t wave_id() {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+}
+// Page of this wave, or -1 when the grid's last workgroup has fewer pages.
+__device__ __forceinline__ int wave_page(const int32_t* list, int n_list) {
+  const int i = (int)(blockIdx.x * WPB + wave_id());
+  return i < n_list ? list[i] : -1;
+}
+#ifdef PQG_DIAG
+// Diagnostic build only (libpqgpu_diag.so, tools/diag_timeline.py): per-wave
+// stamps. Never compiled into the product library.
+__device__ uint64_t* pqg_diag_buf;
+#define DIAG_T(v) uint64_t v = __builtin_amdgcn_s_memtime()
+#define DIAG_ADD(acc, t0) acc += __builtin_amdgcn_s_memtime() - (t0)
+#else
+#define DIAG_T(v)
+#define DIAG_ADD(acc, t0)
+#endif
+
+// Intra-wave ordering of LDS writes before reads by other lanes (no s_barrier:
+// the waves of a workgroup work on different pages and do not meet).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
@@ -47,6 +78,18 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 }
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+// Stores through address_space(1) pointers: global_store_* count only in vmcnt.
+// (Generic pointers give flat_store_*, which also count in lgkmcnt, so every
+// s_waitcnt lgkmcnt(0) for an LDS read would wait for all stores in flight.)
+template <class T>
+__device__ __forceinline__ void gst(T* p, T v) {
+  *(__attribute__((address_space(1))) T*)p = v;
+}
+template <class T>
+__device__ __forceinline__ void gst_nt(T* p, T v) {
+  __builtin_nontemporal_store(v, (__attribute__((address_space(1))) T*)p);
+}
 
 // Buffer resource over [base, base + n) with hardware range checking: loads past
 // n return 0 (never fault), so a window may overhang the end of the batch.
@@ -174,6 +217,76 @@ __device__ __forceinline__ int64_t zigzag64(uint64_t r) {
 
 // ---------------------------------------------------------------------------
 // RLE / bit-packed hybrid walker (RunLengthBitPackingHybridDecoder.readNext :80-109).
+//
+// Parallel pre-decode: a 256-byte window [B, B + 256) is held one dword per
+// lane (plus the next two dwords), and every lane decodes a run header at each
+// of its 4 byte positions as if a run started there (varint, count, RLE value or
+// packed data start, next header position). The serial part — following the
+// chain of headers from the section start — is then 4 v_readlane per run.
+
+struct PreWin {
+  rsrc_t rs;
+  uint32_t B;          // uniform: window start (4-aligned, page-relative)
+  uint32_t nxt[4];     // per lane, byte b: next header position (0xFFFFFFFF: overflow)
+  uint32_t cnt[4];     // run count (values)
+  uint32_t val[4];     // RLE: raw value; PACKED: data start
+  uint32_t flg;        // byte b: bit0 packed, bit1 slow path, bits 2..4 header length
+};
+
+__device__ __forceinline__ void predecode(PreWin& pw, uint32_t B, int w) {
+  pw.B = B;
+  const uint32_t base = B + 4u * lane_id();
+  const uint32_t d0 = ld32(pw.rs, base), d1 = ld32(pw.rs, base + 4), d2 = ld32(pw.rs, base + 8);
+  const uint64_t lo = (uint64_t)d0 | ((uint64_t)d1 << 32);
+  const uint32_t nb = ((uint32_t)w + 7u) >> 3;
+  uint32_t flg = 0;
+#pragma unroll
+  for (uint32_t b = 0; b < 4; b++) {
+    const uint32_t p = base + b;
+    // bytes p .. p+7 in x, byte p+8 .. in hi8
+    const uint64_t x = b ? ((lo >> (8 * b)) | ((uint64_t)d2 << (64 - 8 * b))) : lo;
+    const uint32_t hi8 = d2 >> (8 * b);
+    const uint32_t b0 = (uint32_t)x & 0xFFu, b1 = (uint32_t)(x >> 8) & 0xFFu, b2 = (uint32_t)(x >> 16) & 0xFFu,
+                   b3 = (uint32_t)(x >> 24) & 0xFFu, b4 = (uint32_t)(x >> 32) & 0xFFu;
+    // readUnsignedVarInt, Java int semantics, up to 5 bytes here (longer: slow path)
+    uint32_t v = b0 & 0x7Fu, hl = 1, slow = 0;
+    if (b0 & 0x80u) {
+      v |= (b1 & 0x7Fu) << 7; hl = 2;
+      if (b1 & 0x80u) {
+        v |= (b2 & 0x7Fu) << 14; hl = 3;
+        if (b2 & 0x80u) {
+          v |= (b3 & 0x7Fu) << 21; hl = 4;
+          if (b3 & 0x80u) {
+            v |= b4 << 28; hl = 5;
+            if (b4 & 0x80u) slow = 1;
+          }
+        }
+      }
+    }
+    uint32_t nx, c, vv, pk;
+    if ((v & 1u) == 0) {  // RLE: count, then ceil(w/8) little-endian bytes, not masked
+      const uint32_t sh = 8u * hl;
+      const uint64_t y = (x >> sh) | ((uint64_t)hi8 << (64u - sh));
+      vv = nb == 4 ? (uint32_t)y : (uint32_t)y & ((1u << (8u * nb)) - 1u);
+      c = v >> 1;
+      nx = p + hl + nb;
+      pk = 0;
+    } else {              // PACKED: (header >>> 1) groups of 8 values, groups * w bytes
+      const uint32_t groups = v >> 1;
+      if (groups == 0 || groups >= (1u << 28)) slow = 1;
+      c = groups * 8u;
+      vv = p + hl;
+      const uint64_t e = (uint64_t)p + hl + (uint64_t)groups * (uint32_t)w;
+      nx = e > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)e;
+      pk = 1;
+    }
+    pw.nxt[b] = nx;
+    pw.cnt[b] = c;
+    pw.val[b] = vv;
+    flg |= (pk | (slow << 1) | (hl << 2)) << (8 * b);
+  }
+  pw.flg = flg;
+}
 
 struct RleWalk {
   uint32_t pos;       // uniform: next header byte (page-relative)
@@ -181,6 +294,10 @@ struct RleWalk {
   uint32_t produced;  // uniform: values covered by the runs walked so far
   uint32_t N;         // uniform: values wanted
   int w;              // uniform: bit width
+  // remainder of a bit-packed run split at a batch boundary (multiple of 8 values:
+  // the split point is byte aligned, 8 values = w bytes)
+  uint32_t pend_count;
+  uint32_t pend_lo, pend_hi;
 };
 
 // One batch of up to 64 runs; lane r holds run r.
@@ -193,9 +310,61 @@ struct RunBatch {
   uint32_t end;     // uniform: value index after the batch
 };
 
+// Scalar re-decode of one header at `pos` (rare: varints longer than 5 bytes,
+// 0 or >= 2^28 groups). Bytes come through uniform buffer loads.
+__device__ __forceinline__ uint32_t sbyte(rsrc_t rs, uint32_t p) {
+  return uni((ld32(rs, p & ~3u) >> ((p & 3u) * 8u)) & 0xFFu);
+}
+
+__device__ int slow_header(rsrc_t rs, uint32_t pos, uint32_t sec_end, int w, uint32_t& hl, uint32_t& m, uint64_t& count,
+                           uint32_t& val, uint32_t& next) {
+  uint32_t value = 0, i = 0, k = 0, bb;
+  for (;;) {
+    if (pos + k >= sec_end) return PQG_ERR_EOF;
+    bb = sbyte(rs, pos + k);
+    if (!(bb & 0x80u)) break;
+    value |= (bb & 0x7Fu) << (i & 31u);
+    i += 7;
+    k++;
+  }
+  const uint32_t header = value | (bb << (i & 31u));
+  hl = k + 1;
+  if ((header & 1u) == 0) {
+    const uint32_t nb = ((uint32_t)w + 7u) >> 3;
+    if ((uint64_t)pos + hl + nb > sec_end) return PQG_ERR_EOF;
+    uint32_t v = 0;
+    for (uint32_t j = 0; j < nb; j++) v |= sbyte(rs, pos + hl + j) << (8u * j);
+    m = 0;
+    count = header >> 1;
+    val = v;
+    next = pos + hl + nb;
+    return 0;
+  }
+  const uint32_t groups = header >> 1;
+  if (groups == 0) return PQG_ERR_EMPTY_PACKED_RUN;
+  if (groups >= (1u << 28)) return PQG_ERR_CORRUPT;
+  m = 1;
+  count = (uint64_t)groups * 8u;
+  val = pos + hl;
+  const uint64_t e = (uint64_t)pos + hl + (uint64_t)groups * (uint32_t)w;
+  next = e > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)e;
+  return 0;
+}
+
+__device__ __forceinline__ uint32_t pick4(const uint32_t (&a)[4], uint32_t b, uint32_t l) {
+  switch (b) {
+    case 0: return rdl(a[0], l);
+    case 1: return rdl(a[1], l);
+    case 2: return rdl(a[2], l);
+    default: return rdl(a[3], l);
+  }
+}
+
 // Walk up to 64 runs. Returns 0 or an error code; on error s.N is cut to the
 // error's value index (s.produced) so the caller stops after this batch.
-__device__ __forceinline__ int walk_batch(Window& win, RleWalk& s, RunBatch& rb) {
+// `cap` > 0 limits the bit-packed values one batch may cover (they are staged in
+// LDS); a packed run that does not fit is split at a multiple of 8 values.
+__device__ __forceinline__ int walk_batch(PreWin& win, RleWalk& s, RunBatch& rb, uint32_t cap = 0) {
   const uint32_t lane = lane_id();
   rb.nr = 0;
   rb.first = s.produced;
@@ -204,39 +373,62 @@ __device__ __forceinline__ int walk_batch(Window& win, RleWalk& s, RunBatch& rb)
   rb.lo = 0;
   rb.hi = 0;
   int code = 0;
-  const uint32_t nb = ((uint32_t)s.w + 7u) >> 3;
+  uint32_t packed = 0;
   while (rb.nr < 64u && s.produced < s.N) {
-    if (s.pos >= s.sec_end) { code = PQG_ERR_RLE_PAST_END; break; }     // :81
-    uint32_t hl;
-    uint32_t header = read_uvarint(win, s.pos, s.sec_end - s.pos, hl);
-    if ((uint64_t)s.pos + hl > s.sec_end) { code = PQG_ERR_EOF; break; }  // EOFException in read()
-    s.pos += hl;
     uint64_t count;
     uint32_t m, lo, hi = 0;
-    if ((header & 1u) == 0) {                                              // RLE :85-89
-      count = header >> 1;
-      if ((uint64_t)s.pos + nb > s.sec_end) { code = PQG_ERR_EOF; break; }
-      uint32_t v = 0;
-      if (nb) {
-        uint64_t x = win.read8(s.pos);
-        v = nb == 4 ? (uint32_t)x : (uint32_t)x & ((1u << (8u * nb)) - 1u);
-      }
-      s.pos += nb;
-      if (count == 0) count = s.N - s.produced;  // Java: currentCount goes negative, value repeats forever
-      m = 0;
-      lo = v;
-    } else {                                                               // PACKED :90-104
-      uint32_t groups = header >> 1;
-      if (groups == 0) { code = PQG_ERR_EMPTY_PACKED_RUN; break; }
-      if (groups >= (1u << 28)) { code = PQG_ERR_CORRUPT; break; }
-      count = (uint64_t)groups * 8u;
-      uint64_t need = (uint64_t)groups * (uint32_t)s.w;
-      uint32_t avail = s.sec_end - s.pos;
-      uint32_t rd = need < avail ? (uint32_t)need : avail;                 // :97-99
+    if (s.pend_count) {
       m = 1;
-      lo = s.pos;
-      hi = s.pos + rd;
-      s.pos += rd;
+      count = s.pend_count;
+      lo = s.pend_lo;
+      hi = s.pend_hi;
+      s.pend_count = 0;
+    } else {
+      if (s.pos >= s.sec_end) { code = PQG_ERR_RLE_PAST_END; break; }     // :81
+      const uint32_t k = s.pos - win.B;
+      if (k >= 256u) {
+        predecode(win, s.pos & ~3u, s.w);
+      }
+      const uint32_t kk = s.pos - win.B, l = kk >> 2, b = kk & 3u;
+      const uint32_t f = (rdl(win.flg, l) >> (8u * b)) & 0xFFu;
+      uint32_t hl, nx, vv;
+      if (f & 2u) {
+        code = slow_header(win.rs, s.pos, s.sec_end, s.w, hl, m, count, vv, nx);
+        if (code) break;
+      } else {
+        hl = f >> 2;
+        m = f & 1u;
+        nx = pick4(win.nxt, b, l);
+        vv = pick4(win.val, b, l);
+        count = pick4(win.cnt, b, l);
+        if ((uint64_t)s.pos + hl > s.sec_end) { code = PQG_ERR_EOF; break; }   // EOFException in read()
+      }
+      if (m == 0) {                                                          // RLE :85-89
+        if (nx > s.sec_end) { code = PQG_ERR_EOF; break; }
+        if (count == 0) count = s.N - s.produced;  // Java: currentCount goes negative, value repeats forever
+        lo = vv;
+        s.pos = nx;
+      } else {                                                               // PACKED :90-104
+        const uint32_t rd_end = nx < s.sec_end ? nx : s.sec_end;             // :97-99
+        lo = vv;
+        hi = rd_end;
+        s.pos = rd_end;
+      }
+    }
+    if (m == 1 && cap) {
+      uint64_t left = s.N - s.produced;
+      uint64_t eff = count < left ? count : left;
+      uint32_t room = cap - packed;
+      if (eff > room) {
+        uint32_t take = room & ~7u;
+        s.pend_count = (uint32_t)(count - take);
+        s.pend_lo = lo + (take >> 3) * (uint32_t)s.w;
+        s.pend_hi = hi;
+        if (take == 0) break;
+        count = take;
+        eff = take;
+      }
+      packed += (uint32_t)eff;
     }
     const bool me = lane == rb.nr;
     rb.start = me ? s.produced : rb.start;
@@ -314,16 +506,40 @@ __device__ __forceinline__ typename DictVal<W>::T load_dict(rsrc_t d, uint32_t i
   else return ld4_any(d, id * 4u);
 }
 
+constexpr uint32_t STAGE = 512;  // bit-packed values staged per batch (LDS, per wave)
+
+// Exclusive prefix sum over the wave (u32); *total = sum over all lanes.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o);
+    if ((int)lane_id() >= o) x += y;
+  }
+  *total = rdl(x, 63);
+  return x - v;
+}
+
 // One wave per page. Page list = pages of this class; PageWork holds data
 // section bounds, value count and output offset.
+//
+// Per batch of <= 64 runs: (1) walk, (2) resolve RLE runs through the
+// dictionary (one gather per run), (3) stage every bit-packed value of the
+// batch (unpack + dictionary gather, <= STAGE values, all loads of a round in
+// flight together) into LDS, (4) expand: 16-byte non-temporal stores, RLE
+// values from registers, packed values from LDS. The expansion issues no
+// global loads.
 template <int W>
-__global__ __launch_bounds__(64) void k_dict(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) void k_dict(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                               const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                               const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                               uint32_t* err_count) {
   typedef typename DictVal<W>::T T;
   constexpr int E = 16 / W;  // elements per lane per 16-byte store
-  const int page = list[blockIdx.x];
+  __shared__ T stage_all[WPB][STAGE];
+  T* stage = stage_all[wave_id()];
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
   const PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
   const uint32_t lane = lane_id();
@@ -331,7 +547,7 @@ __global__ __launch_bounds__(64) void k_dict(const uint8_t* __restrict__ bytes, 
   const uint32_t sec_beg = uni(pw.data_begin), sec_end = uni(pw.size);
   if (N == 0 && sec_beg >= sec_end) return;
 
-  Window win;
+  PreWin win;
   win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
   rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
   const uint32_t dict_n = uni(cd.dict_n);
@@ -339,33 +555,53 @@ __global__ __launch_bounds__(64) void k_dict(const uint8_t* __restrict__ bytes, 
   // DictionaryValuesReader.initFromPage :48-64
   RleWalk s;
   s.produced = 0;
+  s.pend_count = 0;
   s.N = N;
   s.sec_end = sec_end;
   if (sec_beg >= sec_end) {  // empty data section: every read throws "Attempt to read from empty page"
-    if (N) report(err, err_count, page, 2 /*value*/, 0, PQG_ERR_EMPTY_PAGE);
+    if (N && lane == 0) report(err, err_count, page, 2 /*value*/, 0, PQG_ERR_EMPTY_PAGE);
     return;
   }
-  win.seek(sec_beg);
-  const uint32_t bw = win.byte(sec_beg);
+  // warm L2 with the whole data section (up to 8 KiB) while the first window decodes;
+  // the loaded words are consumed only at the end of the kernel
+  const uint32_t pf0 = ld32(win.rs, (sec_beg & ~63u) + 64u * lane);
+  const uint32_t pf1 = ld32(win.rs, (sec_beg & ~63u) + 4096u + 64u * lane);
+  const uint32_t bw = sbyte(win.rs, sec_beg);
   if (bw > 32u) {  // RunLengthBitPackingHybridDecoder ctor :55 (thrown at initFromPage)
-    report(err, err_count, page, 0 /*init*/, 2, PQG_ERR_BIT_WIDTH);
+    if (lane == 0) report(err, err_count, page, 0 /*init*/, 2, PQG_ERR_BIT_WIDTH);
     return;
   }
   s.w = (int)bw;
   s.pos = sec_beg + 1;
+  predecode(win, s.pos & ~3u, s.w);
   T* out = (T*)cd.values;
   const uint64_t obase = pw.out_offset;
   const bool out16 = ((uintptr_t)out & 15u) == 0;
+  const uint32_t sh = (uint32_t)(obase % (uint64_t)E);  // page start inside its 16-byte output group
+  T* pal = out + (obase - sh);
+#ifdef PQG_DIAG
+  const uint64_t d_start = __builtin_amdgcn_s_memrealtime();
+  uint64_t d_walk = 0, d_stage = 0, d_exp = 0, d_nb = 0;
+#endif
 
   while (s.produced < s.N) {
     RunBatch rb;
-    int code = walk_batch(win, s, rb);
-    if (code) report(err, err_count, page, 2, rb.end, code);
-    // resolve RLE runs through the dictionary (one gather per run)
+    DIAG_T(t_w);
+    int code = walk_batch(win, s, rb, STAGE);
+    DIAG_ADD(d_walk, t_w);
+#ifdef PQG_DIAG
+    d_nb++;
+#endif
+    DIAG_T(t_s);
+    if (code && lane == 0) report(err, err_count, page, 2, rb.end, code);
+    if (rb.end <= rb.first) break;
+    uint32_t nxt = __shfl_down(rb.start, 1);
+    const uint32_t run_end = (lane + 1 < rb.nr) ? nxt : rb.end;
+    // (2) RLE runs through the dictionary
     uint32_t rlo = rb.lo, rhi = rb.hi;
     if (lane < rb.nr && rb.meta == 0) {
       if (rb.lo >= dict_n) {
-        if (rb.start < rb.end) report(err, err_count, page, 2, rb.start, PQG_ERR_DICT_ID);
+        report(err, err_count, page, 2, rb.start, PQG_ERR_DICT_ID);
         rlo = 0;
         rhi = 0;
       } else {
@@ -374,69 +610,146 @@ __global__ __launch_bounds__(64) void k_dict(const uint8_t* __restrict__ bytes, 
         rhi = (uint32_t)(v >> 32);
       }
     }
-    rb.lo = rlo;
-    rb.hi = rhi;
-    // run end = next run's start (or batch end)
-    uint32_t nxt = __shfl_down(rb.start, 1);
-    const uint32_t run_end = (lane + 1 < rb.nr) ? nxt : rb.end;
-    if (rb.end <= rb.first) break;
-    // expand [rb.first, rb.end): global element range
-    const uint64_t g_lo = obase + rb.first, g_hi = obase + rb.end;
-    for (uint64_t c0 = g_lo & ~(uint64_t)(E - 1); c0 < g_hi; c0 += (uint64_t)E * WAVE) {
-      const uint64_t cg = c0 + (uint64_t)E * lane;
-      // chunk range (page-relative), clamped
-      uint64_t cl = c0 > g_lo ? c0 - obase : rb.first;
-      uint64_t ch = c0 + (uint64_t)E * WAVE;
-      ch = (ch < g_hi ? ch : g_hi) - obase;
-      uint64_t mask = overlap_mask(rb, run_end, (uint32_t)cl, (uint32_t)ch);
-      uint32_t idx[E];
-      bool valid[E];
-      Sel sel[E];
+    // (3) stage bit-packed values: lane r's packed run gets stage slots [soff, soff + pc)
+    const bool is_packed = lane < rb.nr && rb.meta == 1;
+    const uint32_t pc = is_packed ? run_end - rb.start : 0u;
+    uint32_t P;
+    const uint32_t soff = wave_excl_scan(pc, &P);
+    if (P) {
+      for (uint32_t q0 = 0; q0 < P; q0 += 4u * WAVE) {
+        uint32_t ids[4];
+        uint32_t vidx[4];
+        bool ok[4];
 #pragma unroll
-      for (int k = 0; k < E; k++) {
-        uint64_t g = cg + k;
-        valid[k] = g >= g_lo && g < g_hi;
-        idx[k] = (uint32_t)(g - obase);
-        sel[k] = Sel{0, 0, 0, 0};
-      }
-      select_runs(rb, mask, idx, sel, E);
-      T vals[E];
+        for (int u = 0; u < 4; u++) {
+          const uint32_t q = q0 + (uint32_t)u * WAVE + lane;
+          // run holding stage slot q: the last lane r with soff_r <= q (soff is non-decreasing)
+          uint32_t r = 0;
 #pragma unroll
-      for (int k = 0; k < E; k++) {
-        T v;
-        if (sel[k].meta == 0) {
-          v = (T)(((uint64_t)sel[k].hi << 32) | sel[k].lo);
-        } else {
-          uint32_t id = packed_elem(win.rs, sel[k].lo, sel[k].hi, sel[k].s, idx[k], s.w);
-          if (id >= dict_n) {
-            if (valid[k]) report(err, err_count, page, 2, idx[k], PQG_ERR_DICT_ID);
-            v = 0;
-          } else {
-            v = valid[k] ? load_dict<W>(drs, id) : (T)0;
+          for (uint32_t st = 32; st > 0; st >>= 1) {
+            const uint32_t c = r + st;
+            const uint32_t so_c = __shfl(soff, (int)c);
+            r = (c < 64u && so_c <= q) ? c : r;
           }
+          const uint32_t so = __shfl(soff, (int)r), st = __shfl(rb.start, (int)r);
+          const uint32_t lo = __shfl(rb.lo, (int)r), hi = __shfl(rb.hi, (int)r);
+          ok[u] = q < P;
+          vidx[u] = st + (q - so);
+          ids[u] = ok[u] ? packed_elem(win.rs, lo, hi, 0, q - so, s.w) : 0u;
         }
-        vals[k] = v;
-      }
-      bool all = true;
 #pragma unroll
-      for (int k = 0; k < E; k++) all = all && valid[k];
-      if (all && out16) {
-        if constexpr (W == 8) {
-          typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-          v2 st = {vals[0], vals[1]};
-          __builtin_nontemporal_store(st, (v2*)(out + cg));
-        } else {
-          typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-          v4 st = {vals[0], vals[1], vals[2], vals[3]};
-          __builtin_nontemporal_store(st, (v4*)(out + cg));
+        for (int u = 0; u < 4; u++) {
+          const uint32_t q = q0 + (uint32_t)u * WAVE + lane;
+          if (!ok[u]) continue;
+          T v = 0;
+          if (ids[u] >= dict_n) report(err, err_count, page, 2, vidx[u], PQG_ERR_DICT_ID);
+          else v = load_dict<W>(drs, ids[u]);
+          stage[q] = v;
         }
-      } else {
-#pragma unroll
-        for (int k = 0; k < E; k++)
-          if (valid[k]) out[cg + k] = vals[k];
       }
     }
+    rb.lo = is_packed ? soff : rlo;
+    rb.hi = is_packed ? 0u : rhi;
+    wave_sync();
+    DIAG_ADD(d_stage, t_s);
+    DIAG_T(t_e);
+    // (4) expand [rb.first, rb.end). Page-relative 32-bit indices, shifted by `sh`
+    // so that chunk boundaries fall on 16-byte boundaries of the output.
+    {
+      constexpr uint32_t U = 2;                      // 16-byte stores per lane per chunk
+      constexpr uint32_t CH = (uint32_t)E * U * WAVE; // values per chunk
+      const uint32_t r_lo = rb.first + sh, r_hi = rb.end + sh;
+      for (uint32_t c0 = r_lo & ~(CH - 1); c0 < r_hi; c0 += CH) {
+        const uint32_t cl = (c0 > r_lo ? c0 : r_lo) - sh;
+        const uint32_t ch = (c0 + CH < r_hi ? c0 + CH : r_hi) - sh;
+        const uint64_t mask = overlap_mask(rb, run_end, cl, ch);
+        const uint32_t r0 = (uint32_t)__builtin_ctzll(mask);
+        if (__builtin_popcountll(mask) == 1 && rdl(rb.meta, r0) == 0) {
+          // the whole chunk lies in one RLE run: one value for every lane
+          const uint64_t v64 = ((uint64_t)rdl(rb.hi, r0) << 32) | rdl(rb.lo, r0);
+          const T v = (T)v64;
+#pragma unroll
+          for (uint32_t u = 0; u < U; u++) {
+            const uint32_t r = c0 + (u * WAVE + lane) * (uint32_t)E;  // shifted index of element 0
+            if (r >= r_lo && r + E <= r_hi && out16) {
+              if constexpr (W == 8) {
+                typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+                gst_nt((v2*)(pal + r), v2{v, v});
+              } else {
+                typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+                gst_nt((v4*)(pal + r), v4{v, v, v, v});
+              }
+            } else {
+#pragma unroll
+              for (int k = 0; k < E; k++)
+                if (r + k >= r_lo && r + k < r_hi) gst(pal + r + k, v);
+            }
+          }
+          continue;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+          const uint32_t r = c0 + (u * WAVE + lane) * (uint32_t)E;
+          uint32_t idx[E];
+          bool valid[E];
+          Sel sel[E];
+#pragma unroll
+          for (int k = 0; k < E; k++) {
+            valid[k] = r + k >= r_lo && r + k < r_hi;
+            idx[k] = r + k - sh;
+            sel[k] = Sel{0, 0, 0, 0};
+          }
+          select_runs(rb, mask, idx, sel, E);
+          T vals[E];
+#pragma unroll
+          for (int k = 0; k < E; k++) {
+            if (sel[k].meta == 0) {
+              vals[k] = (T)(((uint64_t)sel[k].hi << 32) | sel[k].lo);
+            } else {
+              uint32_t q = sel[k].lo + (idx[k] - sel[k].s);
+              vals[k] = stage[q < STAGE ? q : 0];
+            }
+          }
+          bool all = out16;
+#pragma unroll
+          for (int k = 0; k < E; k++) all = all && valid[k];
+          if (all) {
+            if constexpr (W == 8) {
+              typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+              gst_nt((v2*)(pal + r), v2{vals[0], vals[1]});
+            } else {
+              typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+              gst_nt((v4*)(pal + r), v4{vals[0], vals[1], vals[2], vals[3]});
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < E; k++)
+              if (valid[k]) gst(pal + r + k, vals[k]);
+          }
+        }
+      }
+    }
+    wave_sync();  // stage is rewritten by the next batch
+    DIAG_ADD(d_exp, t_e);
   }
+  asm volatile("; prefetch sink" ::"v"(pf0), "v"(pf1));
+#ifdef PQG_DIAG
+  if (lane == 0 && pqg_diag_buf) {
+    uint64_t* d = pqg_diag_buf + 8 * (uint64_t)page;
+    d[0] = d_start;
+    d[1] = __builtin_amdgcn_s_memrealtime();
+    d[2] = d_walk;
+    d[3] = d_stage;
+    d[4] = d_exp;
+    d[5] = d_nb;
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    d[6] = ((uint64_t)xcc << 32) | hw;
+    d[7] = blockIdx.x;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -447,19 +760,22 @@ __global__ __launch_bounds__(64) void k_dict(const uint8_t* __restrict__ bytes, 
 
 // Decode one level section into out[slot_base + i], i < N. Returns the number of
 // slots decoded before an error (N when none) and sets *err_code.
-__device__ uint32_t decode_levels(Window& win, uint32_t beg, uint32_t end, int w, uint32_t N, uint8_t* out,
+__device__ uint32_t decode_levels(rsrc_t rs, uint32_t beg, uint32_t end, int w, uint32_t N, uint8_t* out,
                                   uint32_t max_def, bool count_nonnull, uint32_t* nonnull, int* err_code) {
   const uint32_t lane = lane_id();
   RleWalk s;
   s.pos = beg;
   s.sec_end = end;
   s.produced = 0;
+  s.pend_count = 0;
   s.N = N;
   s.w = w;
+  PreWin win;
+  win.rs = rs;
+  if (N) predecode(win, beg & ~3u, w);
   uint32_t cnt = 0;
   int first_err = 0;
   uint32_t done = N;
-  if (N) win.seek(beg);
   while (s.produced < s.N) {
     RunBatch rb;
     int code = walk_batch(win, s, rb);
@@ -476,7 +792,7 @@ __device__ uint32_t decode_levels(Window& win, uint32_t beg, uint32_t end, int w
       uint32_t v = sel.meta == 0 ? sel.lo : packed_elem(win.rs, sel.lo, sel.hi, sel.s, i, w);
       v = v > 255u ? 255u : v;
       if (i < rb.end) {
-        if (out) out[i] = (uint8_t)v;
+        if (out) gst(out + i, (uint8_t)v);
         if (count_nonnull && v == max_def) cnt++;
       }
     }
@@ -488,11 +804,12 @@ __device__ uint32_t decode_levels(Window& win, uint32_t beg, uint32_t end, int w
   return done;
 }
 
-__global__ __launch_bounds__(64) void k_levels(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                 PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                 const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                                 uint32_t* err_count) {
-  const int page = list[blockIdx.x];
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
   PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
   const uint32_t lane = lane_id();
@@ -552,18 +869,18 @@ __global__ __launch_bounds__(64) void k_levels(const uint8_t* __restrict__ bytes
   uint8_t* def_out = cd.def_levels ? cd.def_levels + pw.slot_offset : nullptr;
   uint64_t lvl_err_key = ~0ull;
   if (wr > 0) {
-    uint32_t done = decode_levels(win, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code);
+    uint32_t done = decode_levels(win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code);
     if (code) {
       limit = done;
       lvl_err_key = ((uint64_t)done << 1) << 8 | (uint64_t)code;
     }
   } else if (rep_out) {
-    for (uint32_t i = lane; i < nslots; i += WAVE) rep_out[i] = 0;
+    for (uint32_t i = lane; i < nslots; i += WAVE) gst(rep_out + i, (uint8_t)0);
   }
   uint32_t nonnull = 0;
   if (wd > 0) {
     int code2 = 0;
-    uint32_t done = decode_levels(win, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true, &nonnull, &code2);
+    uint32_t done = decode_levels(win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true, &nonnull, &code2);
     if (code2) {
       uint64_t key = (((uint64_t)done << 1) | 1ull) << 8 | (uint64_t)code2;
       if (key < lvl_err_key) lvl_err_key = key;
@@ -571,7 +888,7 @@ __global__ __launch_bounds__(64) void k_levels(const uint8_t* __restrict__ bytes
   } else {
     nonnull = limit;  // max_def == 0: every slot holds a value
     if (def_out)
-      for (uint32_t i = lane; i < limit; i += WAVE) def_out[i] = 0;
+      for (uint32_t i = lane; i < limit; i += WAVE) gst(def_out + i, (uint8_t)0);
   }
   if (lane == 0) {
     if (lvl_err_key != ~0ull) {
@@ -606,7 +923,7 @@ __global__ __launch_bounds__(256) void k_scan_offsets(PageWork* __restrict__ wor
     __syncthreads();
     uint64_t pre = carry;
     for (int wv = 0; wv < (int)(threadIdx.x >> 6); wv++) pre += warp_sums[wv];
-    if (i < e) work[col_pages[i]].out_offset = pre + x - v;
+    if (i < e) gst(&work[col_pages[i]].out_offset, (uint64_t)(pre + x - v));
     __syncthreads();
     if (threadIdx.x == 255) carry = pre + x;
     __syncthreads();
@@ -617,11 +934,12 @@ __global__ __launch_bounds__(256) void k_scan_offsets(PageWork* __restrict__ wor
 // PLAIN fixed width (PlainValuesReader / FixedLenByteArrayPlainValuesReader):
 // byte copy of n_values * W bytes from the data section, EOF at the first
 // value that does not fit.
-__global__ __launch_bounds__(64) void k_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) void k_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                               const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                               const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                               uint32_t* err_count) {
-  const int page = list[blockIdx.x];
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
   const PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
   const uint32_t lane = lane_id();
@@ -642,18 +960,18 @@ __global__ __launch_bounds__(64) void k_plain(const uint8_t* __restrict__ bytes,
   const uintptr_t d0 = (uintptr_t)dst, d1 = d0 + nb;
   const uintptr_t a0 = (d0 + 15u) & ~(uintptr_t)15u, a1 = d1 & ~(uintptr_t)15u;
   if (a0 >= a1) {  // tiny: bytewise
-    for (uint64_t i = lane; i < nb; i += WAVE) dst[i] = (uint8_t)(ld32(rs, (src0 + (uint32_t)i) & ~3u) >> (((src0 + (uint32_t)i) & 3u) * 8u));
+    for (uint64_t i = lane; i < nb; i += WAVE) gst(dst + i, (uint8_t)(ld32(rs, (src0 + (uint32_t)i) & ~3u) >> (((src0 + (uint32_t)i) & 3u) * 8u)));
     return;
   }
   const uint32_t head = (uint32_t)(a0 - d0), tail = (uint32_t)(d1 - a1);
   if (lane < head) {
     uint32_t o = src0 + lane;
-    dst[lane] = (uint8_t)(ld32(rs, o & ~3u) >> ((o & 3u) * 8u));
+    gst(dst + lane, (uint8_t)(ld32(rs, o & ~3u) >> ((o & 3u) * 8u)));
   }
   if (lane < tail) {
     uint64_t i = (a1 - d0) + lane;
     uint32_t o = src0 + (uint32_t)i;
-    dst[i] = (uint8_t)(ld32(rs, o & ~3u) >> ((o & 3u) * 8u));
+    gst(dst + i, (uint8_t)(ld32(rs, o & ~3u) >> ((o & 3u) * 8u)));
   }
   typedef uint32_t v4 __attribute__((ext_vector_type(4)));
   const uint64_t nchunks = (a1 - a0) >> 4;
@@ -672,17 +990,18 @@ __global__ __launch_bounds__(64) void k_plain(const uint8_t* __restrict__ bytes,
       v.z = (x2 >> sh) | (x3 << (32u - sh));
       v.w = (x3 >> sh) | (x4 << (32u - sh));
     }
-    __builtin_nontemporal_store(v, (v4*)(a0 + (c << 4)));
+    gst_nt((v4*)(a0 + (c << 4)), v);
   }
 }
 
 // PLAIN BOOLEAN (BooleanPlainValuesReader -> ByteBitPackingValuesReader(1, LE)):
 // bit i of the section (bytes past the section read as 0) -> one byte 0/1.
-__global__ __launch_bounds__(64) void k_plain_bool(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) void k_plain_bool(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                    const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                    const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                                    uint32_t* err_count) {
-  const int page = list[blockIdx.x];
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
   const PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
   const uint32_t lane = lane_id();
@@ -697,7 +1016,7 @@ __global__ __launch_bounds__(64) void k_plain_bool(const uint8_t* __restrict__ b
   for (uint32_t i = lane; i < n; i += WAVE) {
     uint32_t o = beg + (i >> 3);
     uint32_t b = o < lim ? (ld32(rs, o & ~3u) >> ((o & 3u) * 8u)) & 0xFFu : 0u;
-    dst[i] = (uint8_t)((b >> (i & 7u)) & 1u);
+    gst(dst + i, (uint8_t)((b >> (i & 7u)) & 1u));
   }
 }
 
@@ -708,11 +1027,12 @@ __global__ __launch_bounds__(64) void k_plain_bool(const uint8_t* __restrict__ b
 // wave-wide inclusive scan (wrapping int64) turns them into values. INT32 =
 // (int) of the long (readInteger :103-107).
 template <int W>
-__global__ __launch_bounds__(64) void k_delta(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                               const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                               const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                               uint32_t* err_count) {
-  const int page = list[blockIdx.x];
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
   const PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
   const uint32_t lane = lane_id();
@@ -763,7 +1083,7 @@ __global__ __launch_bounds__(64) void k_delta(const uint8_t* __restrict__ bytes,
   // Value index k (0-based) of the page: k = 0 is `first`; block b covers
   // k in [1 + b*block, 1 + (b+1)*block).
   uint64_t carry = (uint64_t)first;
-  if (lane == 0 && n_out > 0) out[0] = (T)carry;
+  if (lane == 0 && n_out > 0) gst(out, (T)carry);
   uint32_t buffered = 1;  // Java valuesBuffered (includes the first value)
   const uint32_t E = (block + WAVE - 1) / WAVE;  // deltas per lane per block
   bool fail = false;
@@ -867,7 +1187,7 @@ __global__ __launch_bounds__(64) void k_delta(const uint8_t* __restrict__ bytes,
       for (uint32_t q = 0; q < 8; q++) {
         uint32_t j = lane * E + q;
         uint64_t k = (uint64_t)k0 + j;
-        if (q < E && j < block && k < n_out) out[k] = (T)(base_v + loc[q]);
+        if (q < E && j < block && k < n_out) gst(out + k, (T)(base_v + loc[q]));
       }
       carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
     }
@@ -900,9 +1220,17 @@ __global__ __launch_bounds__(256) void k_unpack_runs(int w, const uint8_t* __res
       x >>= (byte - a) * 8u + (uint32_t)(bit & 7u);
       v = w == 32 ? (uint32_t)x : (uint32_t)x & ((1u << w) - 1u);
     }
-    o[i] = (int32_t)v;
+    gst(o + i, (int32_t)v);
   }
 }
+
+#ifdef PQG_DIAG
+}  // namespace pqg
+extern "C" int pqg_diag_set(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(pqg::pqg_diag_buf), &p, sizeof(p)) == hipSuccess ? 0 : 3;
+}
+namespace pqg {
+#endif
 
 // ---------------------------------------------------------------------------
 // Launchers (host side of this translation unit)
@@ -912,15 +1240,15 @@ __global__ __launch_bounds__(256) void k_unpack_runs(int w, const uint8_t* __res
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
   if (n <= 0) return hipSuccess;
-  if (width == 8) hipLaunchKernelGGL(k_dict<8>, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
-  else hipLaunchKernelGGL(k_dict<4>, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
+  if (width == 8) hipLaunchKernelGGL(k_dict<8>, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
+  else hipLaunchKernelGGL(k_dict<4>, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   return hipGetLastError();
 }
 
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                          const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_levels, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
+  hipLaunchKernelGGL(k_levels, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   return hipGetLastError();
 }
 
@@ -934,16 +1262,16 @@ hipError_t launch_scan(hipStream_t st, PageWork* work, const int32_t* col_pages,
 hipError_t launch_plain(int kind, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                         const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
   if (n <= 0) return hipSuccess;
-  if (kind == 1) hipLaunchKernelGGL(k_plain_bool, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
-  else hipLaunchKernelGGL(k_plain, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
+  if (kind == 1) hipLaunchKernelGGL(k_plain_bool, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
+  else hipLaunchKernelGGL(k_plain, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   return hipGetLastError();
 }
 
 hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                         const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
   if (n <= 0) return hipSuccess;
-  if (width == 8) hipLaunchKernelGGL(k_delta<8>, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
-  else hipLaunchKernelGGL(k_delta<4>, dim3(n), dim3(64), 0, st, PQG_LAUNCH_ARGS);
+  if (width == 8) hipLaunchKernelGGL(k_delta<8>, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
+  else hipLaunchKernelGGL(k_delta<4>, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   return hipGetLastError();
 }
 

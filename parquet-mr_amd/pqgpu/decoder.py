@@ -90,7 +90,9 @@ class Decoder:
         self.device = torch.device("cuda", device)
         torch.cuda.set_device(self.device)
         if stream is None:
-            stream = torch.cuda.current_stream(self.device)
+            # a dedicated stream: the default stream's handle is 0, which the C ABI reads as
+            # "create your own", and events must be recorded on the stream the kernels run on
+            stream = torch.cuda.Stream(self.device)
         self.stream = stream
         h = C.c_void_p()
         native.check(L.pqg_ctx_create(device, C.c_void_p(stream.cuda_stream), C.byref(h)), what="pqg_ctx_create")
@@ -142,6 +144,7 @@ class Decoder:
         """Decode every page of `dbatch` into device columns. Returns (columns, status)."""
         batch = dbatch.batch
         cols = cols if cols is not None else self.alloc_columns(batch)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))  # uploads / allocations first
         descs = self._descs(batch, cols)
         pages = np.ascontiguousarray(batch.pages)
         st = abi.Status()
@@ -160,6 +163,7 @@ class Decoder:
     def plan(self, dbatch, cols=None):
         batch = dbatch.batch
         cols = cols if cols is not None else self.alloc_columns(batch)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
         descs = self._descs(batch, cols)
         pages = np.ascontiguousarray(batch.pages)
         st = abi.Status()

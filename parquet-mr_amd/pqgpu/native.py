@@ -9,7 +9,8 @@ import os
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpqgpu.so")
+# PQGPU_LIB selects a diagnostic build (tools/); the product is libpqgpu.so
+LIB_PATH = os.environ.get("PQGPU_LIB") or os.path.join(_HERE, "libpqgpu.so")
 _LIB = None
 
 EXPORTS = [
