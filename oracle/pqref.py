@@ -125,7 +125,7 @@ def decode_batch(batch, binary_capacity=None):
         c.rep_levels = rl.ctypes.data if cd["max_rep"] > 0 else None
         c.levels_capacity = n_slots
         if cd["physical_type"] == abi.BYTE_ARRAY:
-            cap = binary_capacity or int(len(batch.data))
+            cap = binary_capacity or max(1 << 24, 8 * int(len(batch.data)))
             bd = np.zeros(max(cap, 1), dtype=np.uint8)
             keep.append(bd)
             c.binary_data = bd.ctypes.data

@@ -1,0 +1,160 @@
+"""Regenerate the golden fixtures under tests/golden/ (run in the dev container).
+
+Two sources, both DATA (inputs + expected outputs), no reference source:
+
+1. parquet-mr-written (and Arrow-written) fixture files that the reference's
+   own tests hold (parquet-hadoop/src/test/resources/*.parquet,
+   parquet-avro/src/test/resources/strings-2.parquet) are copied verbatim.
+2. Files written here by pyarrow (Arrow C++ parquet writer, an independent
+   third-party writer) with the encodings on the hot path: dictionary
+   (RLE_DICTIONARY / PLAIN_DICTIONARY), PLAIN, DELTA_BINARY_PACKED, V1 and V2
+   data pages, nulls and nested lists.
+
+For every leaf column chunk the manifest records what the decoder needs
+(offsets, physical type, max levels) and the expected dense non-null values as
+read back by pyarrow (saved to <file>.npz, so the tests need no pyarrow).
+"""
+import json
+import os
+import shutil
+import sys
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.compute as pc
+import pyarrow.parquet as pq
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+REF_FILES = [
+    "parquet-hadoop/src/test/resources/test-file-with-no-column-indexes-1.parquet",
+    "parquet-hadoop/src/test/resources/test-append_1.parquet",
+    "parquet-hadoop/src/test/resources/test-append_2.parquet",
+    "parquet-hadoop/src/test/resources/test-empty-row-group_1.parquet",
+    "parquet-hadoop/src/test/resources/test-empty-row-group_2.parquet",
+    "parquet-hadoop/src/test/resources/test-empty-row-group_3.parquet",
+    "parquet-avro/src/test/resources/strings-2.parquet",
+]
+
+
+def leaf_values(arr):
+    """Dense non-null leaf values of a (possibly nested) arrow column, in slot order."""
+    t = arr.type
+    if pa.types.is_list(t) or pa.types.is_large_list(t):
+        return leaf_values(pc.list_flatten(arr))
+    if pa.types.is_struct(t):
+        raise ValueError("struct: select a field first")
+    return arr.drop_null()
+
+
+def field_path_array(table, path):
+    """Arrow array of the leaf at dotted `path` with parent nulls/lists preserved."""
+    parts = path.split(".")
+    arr = table.column(parts[0]).combine_chunks()
+    for p in parts[1:]:
+        while pa.types.is_list(arr.type):
+            arr = pc.list_flatten(arr)
+        if pa.types.is_struct(arr.type):
+            # propagate struct-level nulls to the child
+            child = pc.struct_field(arr, p)
+            arr = child
+    while pa.types.is_list(arr.type):
+        arr = pc.list_flatten(arr)
+    return arr
+
+
+def describe(path_in, name, rg_table_reader):
+    pf = pq.ParquetFile(path_in)
+    md = pf.metadata
+    schema = pf.schema
+    chunks = []
+    expected = {}
+    for rg in range(md.num_row_groups):
+        t = pf.read_row_group(rg)
+        for c in range(md.num_columns):
+            cc = md.row_group(rg).column(c)
+            col = schema.column(c)
+            path = cc.path_in_schema
+            start = cc.dictionary_page_offset if cc.dictionary_page_offset is not None else cc.data_page_offset
+            if cc.dictionary_page_offset is not None:
+                start = min(cc.dictionary_page_offset, cc.data_page_offset)
+            arr = field_path_array(t, path)
+            vals = arr.drop_null()
+            key = f"rg{rg}_c{c}"
+            ptype = col.physical_type
+            if ptype == "BYTE_ARRAY":
+                b = [bytes(x.as_py() if isinstance(x.as_py(), bytes) else str(x.as_py()).encode()) for x in vals]
+                lens = np.array([len(x) for x in b], dtype=np.int64)
+                expected[key + "_lens"] = lens
+                expected[key + "_bytes"] = np.frombuffer(b"".join(b), dtype=np.uint8) if b else np.zeros(0, np.uint8)
+            elif ptype == "BOOLEAN":
+                expected[key] = np.array(vals.to_pylist(), dtype=np.uint8)
+            else:
+                np_dt = {"INT32": np.int32, "INT64": np.int64, "FLOAT": np.float32, "DOUBLE": np.float64}[ptype]
+                expected[key] = np.array(vals.to_numpy(zero_copy_only=False), dtype=np_dt) if len(vals) else \
+                    np.zeros(0, np_dt)
+            chunks.append({"key": key, "row_group": rg, "column": c, "path": path, "physical_type": ptype,
+                           "max_def": col.max_definition_level, "max_rep": col.max_repetition_level,
+                           "type_length": col.length or 0, "start": start,
+                           "length": cc.total_compressed_size, "num_values": cc.num_values,
+                           "encodings": list(cc.encodings), "compression": cc.compression,
+                           "created_by": md.created_by})
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **expected)
+    return chunks
+
+
+def write_arrow_fixtures():
+    rng = np.random.default_rng(2024)
+    out = []
+    n = 30000
+    runs = np.minimum(rng.zipf(1.6, size=n), 300)
+    ids = np.repeat(rng.integers(0, 500, size=n), runs)[:n]
+    d_i64 = rng.integers(-2**62, 2**62, size=500)[ids]
+    walk = np.cumsum(rng.integers(-100, 10000, size=n)).astype(np.int64)
+    valid = rng.random(n) > 0.1
+    t = pa.table({
+        "dict_i64": pa.array(d_i64, type=pa.int64()),
+        "dict_i32": pa.array((ids * 7 - 1000).astype(np.int32)),
+        "dict_f64": pa.array(rng.standard_normal(500)[ids]),
+        "opt_dict_i64": pa.array(d_i64, mask=~valid),
+        "plain_f32": pa.array(rng.standard_normal(n).astype(np.float32)),
+        "opt_plain_f64": pa.array(rng.standard_normal(n), mask=~valid),
+        "delta_i64": pa.array(walk),
+        "delta_i32": pa.array((walk % 100000).astype(np.int32)),
+        "opt_delta_i64": pa.array(walk, mask=~valid),
+        "bool": pa.array(rng.random(n) > 0.3),
+        "list_i64": pa.array([None if rng.random() < 0.1 else
+                              [None if rng.random() < 0.1 else int(x) for x in rng.integers(-50, 50, size=rng.poisson(3))]
+                              for _ in range(n // 3)] + [[]] * (n - n // 3)),
+    })
+    enc = {"delta_i64": "DELTA_BINARY_PACKED", "delta_i32": "DELTA_BINARY_PACKED",
+           "opt_delta_i64": "DELTA_BINARY_PACKED", "plain_f32": "PLAIN", "opt_plain_f64": "PLAIN", "bool": "PLAIN"}
+    for ver in ("1.0", "2.0"):
+        name = f"arrow_encodings_v{ver[0]}"
+        path = os.path.join(HERE, name + ".parquet")
+        pq.write_table(t, path, data_page_version=ver, compression="NONE",
+                       use_dictionary=["dict_i64", "dict_i32", "dict_f64", "opt_dict_i64", "list_i64"],
+                       column_encoding=enc, data_page_size=16 * 1024, row_group_size=20000,
+                       write_page_index=False)
+        out.append(name)
+    return out
+
+
+def main():
+    manifest = {}
+    for rel in REF_FILES:
+        src = os.path.join(REF, rel)
+        name = os.path.splitext(os.path.basename(rel))[0]
+        dst = os.path.join(HERE, name + ".parquet")
+        shutil.copyfile(src, dst)
+        manifest[name] = {"source": f"reference:{rel}", "chunks": describe(dst, name, None)}
+    for name in write_arrow_fixtures():
+        manifest[name] = {"source": "pyarrow " + pa.__version__, "chunks": describe(os.path.join(HERE, name + ".parquet"),
+                                                                                   name, None)}
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+    print("wrote", len(manifest), "fixtures")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,78 @@
+"""Multi-rank path on CPU (gloo, world_size 2): row-group sharding + the all-gather
+concatenation. The per-rank decode here is the oracle (the GPU decode runs in the
+-m gpu tests); what is tested is the sharding / offset / gather logic."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pqgpu import abi, dist as pdist, writer
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _row_groups():
+    rng = np.random.default_rng(3)
+    rgs = []
+    for k in range(7):
+        n = int(rng.integers(1000, 20000))
+        vals = rng.integers(0, 300, size=n)[np.repeat(np.arange(n // 10 + 1), 10)[:n]].astype(np.int64) * (k + 1)
+        rgs.append(writer.write_column_chunk(abi.INT64, vals, abi.RLE_DICTIONARY, page_rows=4000))
+    return rgs
+
+
+def _worker(rank, world, port, q):
+    import sys
+    from oracle import pqref
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rgs = _row_groups()
+    sizes = [sum(len(p.body) for p in ch.pages) for ch in rgs]
+    rows = [len(ch.values) for ch in rgs]
+    shards = pdist.shard_row_groups(sizes, world)
+    mine = shards[rank]
+    local = []
+    for i in mine:
+        res = pqref.decode_batch(writer.build_batch([rgs[i]]))
+        assert res.code == 0
+        local.append(res.columns[0]["values"])
+    local = torch.from_numpy(np.concatenate(local) if local else np.zeros(0, np.int64))
+    full = pdist.gather_column(local, mine, shards, rows)
+    expect = np.concatenate([ch.values for ch in rgs])
+    q.put((rank, bool(np.array_equal(full.numpy(), expect)), [len(s) for s in shards]))
+    dist.destroy_process_group()
+
+
+def test_shard_row_groups_balanced():
+    sh = pdist.shard_row_groups([10, 9, 8, 1, 1, 1, 7, 3], 3)
+    assert sorted(sum(sh, [])) == list(range(8))
+    loads = [sum([10, 9, 8, 1, 1, 1, 7, 3][i] for i in s) for s in sh]
+    assert max(loads) - min(loads) <= 3
+
+
+def test_row_group_offsets():
+    assert list(pdist.row_group_offsets([5, 0, 7])) == [0, 5, 5]
+
+
+def test_gather_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    assert all(p.exitcode == 0 for p in procs)
