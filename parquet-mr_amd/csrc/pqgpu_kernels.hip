@@ -82,13 +82,19 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 // Stores through address_space(1) pointers: global_store_* count only in vmcnt.
 // (Generic pointers give flat_store_*, which also count in lgkmcnt, so every
 // s_waitcnt lgkmcnt(0) for an LDS read would wait for all stores in flight.)
+#ifdef PQG_DIAG
+__device__ int pqg_diag_nostore;  // diagnostic ablation: skip output stores (set by pqg_diag_nostore_set)
+#define PQG_STORE_GUARD if (!pqg_diag_nostore)
+#else
+#define PQG_STORE_GUARD
+#endif
 template <class T>
 __device__ __forceinline__ void gst(T* p, T v) {
-  *(__attribute__((address_space(1))) T*)p = v;
+  PQG_STORE_GUARD *(__attribute__((address_space(1))) T*)p = v;
 }
 template <class T>
 __device__ __forceinline__ void gst_nt(T* p, T v) {
-  __builtin_nontemporal_store(v, (__attribute__((address_space(1))) T*)p);
+  PQG_STORE_GUARD __builtin_nontemporal_store(v, (__attribute__((address_space(1))) T*)p);
 }
 
 // Buffer resource over [base, base + n) with hardware range checking: loads past
@@ -226,6 +232,11 @@ __device__ __forceinline__ int64_t zigzag64(uint64_t r) {
 
 struct PreWin {
   rsrc_t rs;
+  // Optional LDS copy of page bytes [seg_lo, seg_lo + SEG_BYTES): windows inside it are read
+  // from LDS. (A global load issued after this wave's stores waits for all of them: vmcnt
+  // counts stores on CDNA, so the bytes are staged before the first store.)
+  uint8_t* seg;
+  uint32_t seg_lo;
   uint32_t B;          // uniform: window start (4-aligned, page-relative)
   uint32_t nxt[4];     // per lane, byte b: next header position (0xFFFFFFFF: overflow)
   uint32_t cnt[4];     // run count (values)
@@ -233,10 +244,49 @@ struct PreWin {
   uint32_t flg;        // byte b: bit0 packed, bit1 slow path, bits 2..4 header length
 };
 
+constexpr uint32_t SEG_BYTES = 1536;   // LDS page segment per wave (budget: 5 workgroups per CU)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Fill the wave's LDS segment with page bytes [lo, lo + SEG_BYTES) (lo 16-aligned).
+__device__ __forceinline__ void seg_fill(PreWin& pw, uint32_t lo) {
+  pw.seg_lo = lo;
+#pragma unroll
+  for (uint32_t i = 0; i < SEG_BYTES; i += 16u * WAVE) {
+    const uint32_t o = i + 16u * lane_id();
+    if (o < SEG_BYTES) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(pw.rs, (int)(lo + o), 0, 0);
+      *(u32x4*)(pw.seg + o) = v;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// True when bytes [a, a + n) of the page are in the segment.
+__device__ __forceinline__ bool seg_has(const PreWin& pw, uint32_t a, uint32_t n) {
+  return pw.seg && a >= pw.seg_lo && a + n <= pw.seg_lo + SEG_BYTES;
+}
+
+__device__ __forceinline__ uint32_t seg32(const PreWin& pw, uint32_t a) {  // a 4-aligned, inside
+  return *(const uint32_t*)(pw.seg + (a - pw.seg_lo));
+}
+
 __device__ __forceinline__ void predecode(PreWin& pw, uint32_t B, int w) {
   pw.B = B;
   const uint32_t base = B + 4u * lane_id();
-  const uint32_t d0 = ld32(pw.rs, base), d1 = ld32(pw.rs, base + 4), d2 = ld32(pw.rs, base + 8);
+  if (pw.seg && !seg_has(pw, B, 264u)) seg_fill(pw, B & ~15u);
+  uint32_t d0, d1, d2;
+  if (pw.seg) {
+    d0 = seg32(pw, base);
+    d1 = seg32(pw, base + 4);
+    d2 = seg32(pw, base + 8);
+  } else {
+    d0 = ld32(pw.rs, base);
+    d1 = ld32(pw.rs, base + 4);
+    d2 = ld32(pw.rs, base + 8);
+  }
   const uint64_t lo = (uint64_t)d0 | ((uint64_t)d1 << 32);
   const uint32_t nb = ((uint32_t)w + 7u) >> 3;
   uint32_t flg = 0;
@@ -351,6 +401,11 @@ __device__ int slow_header(rsrc_t rs, uint32_t pos, uint32_t sec_end, int w, uin
   return 0;
 }
 
+__device__ __forceinline__ uint32_t wbyte(const PreWin& pw, uint32_t p) {
+  if (seg_has(pw, p & ~3u, 4)) return uni((seg32(pw, p & ~3u) >> ((p & 3u) * 8u)) & 0xFFu);
+  return sbyte(pw.rs, p);
+}
+
 __device__ __forceinline__ uint32_t pick4(const uint32_t (&a)[4], uint32_t b, uint32_t l) {
   switch (b) {
     case 0: return rdl(a[0], l);
@@ -459,6 +514,23 @@ __device__ __forceinline__ uint32_t packed_elem(rsrc_t rs, uint32_t lo, uint32_t
   return w == 32 ? (uint32_t)x : (uint32_t)x & ((1u << w) - 1u);
 }
 
+// packed_elem reading the LDS segment when the 8 bytes are there.
+__device__ __forceinline__ uint32_t packed_elem_w(const PreWin& pw, uint32_t lo, uint32_t hi, uint32_t j, int w) {
+  if (w == 0) return 0;
+  const uint64_t bit = (uint64_t)j * (uint32_t)w;
+  const uint32_t byte = lo + (uint32_t)(bit >> 3);
+  const uint32_t a = byte & ~3u;
+  uint64_t x;
+  if (seg_has(pw, a, 8)) x = (uint64_t)seg32(pw, a) | ((uint64_t)seg32(pw, a + 4) << 32);
+  else x = (uint64_t)ld32(pw.rs, a) | ((uint64_t)ld32(pw.rs, a + 4) << 32);
+  if (a + 8u > hi) {
+    const int64_t keep = (int64_t)hi - (int64_t)a;
+    x = keep <= 0 ? 0 : (x & ((1ull << (8 * keep)) - 1ull));
+  }
+  x >>= (byte - a) * 8u + (uint32_t)(bit & 7u);
+  return w == 32 ? (uint32_t)x : (uint32_t)x & ((1u << w) - 1u);
+}
+
 // For lane element index i, select the run (among `mask`) covering it.
 struct Sel {
   uint32_t s, meta, lo, hi;
@@ -506,7 +578,17 @@ __device__ __forceinline__ typename DictVal<W>::T load_dict(rsrc_t d, uint32_t i
   else return ld4_any(d, id * 4u);
 }
 
-constexpr uint32_t STAGE = 512;  // bit-packed values staged per batch (LDS, per wave)
+constexpr uint32_t DICT_LDS_BYTES = 8192;   // dictionary staged in LDS per workgroup when it fits
+constexpr uint32_t RT_MAX = 24;             // run records per expansion batch (LDS, per wave): small, so stores start early
+constexpr uint32_t NX_SENTINEL = 0xFFFFFFFFu;
+
+// Per-wave LDS of k_dict.
+struct DictWaveLds {
+  uint8_t seg[SEG_BYTES];  // page bytes [seg_lo, seg_lo + SEG_BYTES)
+  uint64_t ent[256];       // window position k: next header position | (count | packed << 31) << 32
+  uint32_t val[256];       // window position k: RLE raw value, or packed data start
+  uint64_t rt[RT_MAX + 1]; // run records: start | payload << 32 (payload: RLE id (<2^31) or 2^31 | data start)
+};
 
 // Exclusive prefix sum over the wave (u32); *total = sum over all lanes.
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
@@ -520,219 +602,235 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) 
   return x - v;
 }
 
-// One wave per page. Page list = pages of this class; PageWork holds data
-// section bounds, value count and output offset.
+template <int W>
+__device__ __forceinline__ void store_run16(typename DictVal<W>::T* pal, uint32_t a, uint32_t b, typename DictVal<W>::T v,
+                                            bool out16) {
+  typedef typename DictVal<W>::T T;
+  constexpr uint32_t E = 16 / W;
+  const uint32_t lane = lane_id();
+  const uint32_t a16 = out16 ? (a + E - 1) & ~(E - 1) : b;
+  const uint32_t b16 = out16 ? b & ~(E - 1) : b;
+  if (a16 < b16) {
+    if (lane < a16 - a) gst(pal + a + lane, v);
+    if (lane < b - b16) gst(pal + b16 + lane, v);
+    constexpr uint32_t STEP = E * WAVE;
+    uint32_t g = a16 + E * lane;
+    for (; g + 3 * STEP < b16; g += 4 * STEP) {
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        if constexpr (W == 8) {
+          typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+          gst_nt((v2*)(pal + g + u * STEP), v2{v, v});
+        } else {
+          gst_nt((u32x4*)(pal + g + u * STEP), u32x4{v, v, v, v});
+        }
+      }
+    }
+    for (; g < b16; g += STEP) {
+      if constexpr (W == 8) {
+        typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+        gst_nt((v2*)(pal + g), v2{v, v});
+      } else {
+        gst_nt((u32x4*)(pal + g), u32x4{v, v, v, v});
+      }
+    }
+  } else {
+    for (uint32_t i = a + lane; i < b; i += WAVE) gst(pal + i, v);
+  }
+}
+
+// One wave per page (4 per workgroup).
 //
-// Per batch of <= 64 runs: (1) walk, (2) resolve RLE runs through the
-// dictionary (one gather per run), (3) stage every bit-packed value of the
-// batch (unpack + dictionary gather, <= STAGE values, all loads of a round in
-// flight together) into LDS, (4) expand: 16-byte non-temporal stores, RLE
-// values from registers, packed values from LDS. The expansion issues no
-// global loads.
+//   stage   the workgroup's dictionary (when its pages share one that fits) and each
+//           wave's page data section into LDS, before any store: on CDNA vmcnt counts
+//           stores, so a global load issued after stores waits for all of them.
+//   window  a 256-byte window of the section is pre-decoded in parallel (every lane
+//           parses a run header at each of its 4 byte positions) into LDS tables.
+//   chain   the serial part — following headers from the section start — is one
+//           ds_read_b64 + ds_read_b32 per run, appending an 8-byte run record.
+//   expand  per run record: RLE -> dictionary value (LDS) stored with 16-byte
+//           non-temporal stores; bit-packed -> lanes unpack ids from the LDS page
+//           bytes and gather from the LDS dictionary.
 template <int W>
 __global__ __launch_bounds__(64 * WPB) void k_dict(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                              const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
-                                              const int32_t* __restrict__ list, int n_list, uint64_t* err,
-                                              uint32_t* err_count) {
+                                                    const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                                    const int32_t* __restrict__ list, int n_list, uint64_t* err,
+                                                    uint32_t* err_count) {
   typedef typename DictVal<W>::T T;
-  constexpr int E = 16 / W;  // elements per lane per 16-byte store
-  __shared__ T stage_all[WPB][STAGE];
-  T* stage = stage_all[wave_id()];
+  constexpr uint32_t E = 16 / W;
+  __shared__ __attribute__((aligned(16))) uint8_t dict_lds[DICT_LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) DictWaveLds wl_all[WPB];
+  __shared__ int wg_col[WPB];
+  DictWaveLds& L = wl_all[wave_id()];
   const int page = wave_page(list, n_list);
+  const uint32_t lane = lane_id();
+
+  if (lane == 0) wg_col[wave_id()] = page >= 0 ? work[page].column : -1;
+  __syncthreads();
+  int c0 = -1;
+  bool same = true;
+#pragma unroll
+  for (int k = 0; k < WPB; k++) {
+    const int c = wg_col[k];
+    if (c >= 0) {
+      if (c0 < 0) c0 = c;
+      else if (c != c0) same = false;
+    }
+  }
+  bool dict_in_lds = false;
+  if (same && c0 >= 0) {
+    const ColumnDev& cd0 = cols[c0];
+    const uint64_t need = (uint64_t)cd0.dict_n * W;
+    dict_in_lds = need <= DICT_LDS_BYTES && need <= cd0.dict_bytes;
+    if (dict_in_lds) {
+      rsrc_t d0 = make_rsrc(bytes + cd0.dict_offset, cd0.dict_bytes);
+      const bool al = (cd0.dict_offset & 3u) == 0;
+      for (uint32_t o = 16u * threadIdx.x; o < (uint32_t)need; o += 16u * 64u * WPB) {
+        u32x4 v;
+        if (al) v = __builtin_amdgcn_raw_buffer_load_b128(d0, (int)o, 0, 0);
+        else v = u32x4{ld4_any(d0, o), ld4_any(d0, o + 4), ld4_any(d0, o + 8), ld4_any(d0, o + 12)};
+        *(u32x4*)(dict_lds + o) = v;
+      }
+    }
+  }
+  __syncthreads();
   if (page < 0) return;
   const PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
-  const uint32_t lane = lane_id();
-  const uint32_t N = uni(pw.n_values);
+  uint32_t N = uni(pw.n_values);
   const uint32_t sec_beg = uni(pw.data_begin), sec_end = uni(pw.size);
   if (N == 0 && sec_beg >= sec_end) return;
 
   PreWin win;
   win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  win.seg = L.seg;
   rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
   const uint32_t dict_n = uni(cd.dict_n);
+  const T* dict_l = (const T*)dict_lds;
+  auto dict_get = [&](uint32_t id) -> T { return dict_in_lds ? dict_l[id] : load_dict<W>(drs, id); };
 
   // DictionaryValuesReader.initFromPage :48-64
-  RleWalk s;
-  s.produced = 0;
-  s.pend_count = 0;
-  s.N = N;
-  s.sec_end = sec_end;
   if (sec_beg >= sec_end) {  // empty data section: every read throws "Attempt to read from empty page"
     if (N && lane == 0) report(err, err_count, page, 2 /*value*/, 0, PQG_ERR_EMPTY_PAGE);
     return;
   }
-  // warm L2 with the whole data section (up to 8 KiB) while the first window decodes;
-  // the loaded words are consumed only at the end of the kernel
-  const uint32_t pf0 = ld32(win.rs, (sec_beg & ~63u) + 64u * lane);
-  const uint32_t pf1 = ld32(win.rs, (sec_beg & ~63u) + 4096u + 64u * lane);
-  const uint32_t bw = sbyte(win.rs, sec_beg);
+  seg_fill(win, sec_beg & ~15u);
+  const uint32_t bw = wbyte(win, sec_beg);
   if (bw > 32u) {  // RunLengthBitPackingHybridDecoder ctor :55 (thrown at initFromPage)
     if (lane == 0) report(err, err_count, page, 0 /*init*/, 2, PQG_ERR_BIT_WIDTH);
     return;
   }
-  s.w = (int)bw;
-  s.pos = sec_beg + 1;
-  predecode(win, s.pos & ~3u, s.w);
+  const int w = (int)bw;
+  const uint32_t nb = (bw + 7u) >> 3;
   T* out = (T*)cd.values;
   const uint64_t obase = pw.out_offset;
   const bool out16 = ((uintptr_t)out & 15u) == 0;
-  const uint32_t sh = (uint32_t)(obase % (uint64_t)E);  // page start inside its 16-byte output group
+  const uint32_t sh = (uint32_t)(obase % (uint64_t)E);
   T* pal = out + (obase - sh);
 #ifdef PQG_DIAG
   const uint64_t d_start = __builtin_amdgcn_s_memrealtime();
   uint64_t d_walk = 0, d_stage = 0, d_exp = 0, d_nb = 0;
 #endif
 
-  while (s.produced < s.N) {
-    RunBatch rb;
+  uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
+  uint32_t produced = 0;       // values covered by the runs read so far
+  uint32_t B = pos - 260u;     // current window: none yet (pos - B >= 256 forces a pre-decode)
+  while (produced < N) {
     DIAG_T(t_w);
-    int code = walk_batch(win, s, rb, STAGE);
+    // ---- chain: read runs into the run table (up to RT_MAX)
+    uint32_t nrun = 0;
+    const uint32_t first = produced;
+    int code = 0;
+    while (produced < N && nrun < RT_MAX) {
+      if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }           // readNext :81
+      if (pos - B >= 256u) {
+        // new window: pre-decode 256 positions into LDS
+        B = pos & ~3u;
+        predecode(win, B, w);
+#pragma unroll
+        for (uint32_t bb = 0; bb < 4; bb++) {
+          const uint32_t p = B + 4u * lane + bb;
+          const uint32_t f = (win.flg >> (8u * bb)) & 0xFFu;
+          const uint32_t hl = f >> 2;
+          uint32_t nx = win.nxt[bb];
+          // the slow scalar path handles: long varints, 0 / huge group counts, and any
+          // header or RLE value that crosses the section end (EOF semantics)
+          const bool slow = (f & 2u) || p + hl > sec_end || (!(f & 1u) && nx > sec_end);
+          if (slow) nx = NX_SENTINEL;
+          L.ent[4u * lane + bb] = (uint64_t)nx | ((uint64_t)(win.cnt[bb] | ((f & 1u) << 31)) << 32);
+          L.val[4u * lane + bb] = win.val[bb];
+        }
+        wave_sync();
+      }
+      const uint32_t k = pos - B;
+      const uint64_t e = L.ent[k];
+      uint32_t nx = uni((uint32_t)e);
+      uint32_t cw = uni((uint32_t)(e >> 32));
+      uint32_t v = uni(L.val[k]);
+      if (nx == NX_SENTINEL) {
+        uint32_t hl, m, nxs, vv;
+        uint64_t cnt64;
+        code = slow_header(win.rs, pos, sec_end, w, hl, m, cnt64, vv, nxs);
+        if (code) break;
+        if (m == 0 && nxs > sec_end) { code = PQG_ERR_EOF; break; }
+        nx = nxs;
+        v = vv;
+        cw = (uint32_t)(cnt64 > 0x7FFFFFFFull ? 0x7FFFFFFFu : cnt64) | (m << 31);
+      }
+      const uint32_t packed = cw >> 31;
+      uint64_t cnt = cw & 0x7FFFFFFFu;
+      uint32_t payload;
+      if (!packed) {
+        if (cnt == 0) cnt = N - produced;  // Java: currentCount goes negative, value repeats forever
+        payload = v > 0x7FFFFFFFu ? 0x7FFFFFFFu : v;  // ids >= 2^31 are out of range anyway
+        pos = nx;
+      } else {
+        payload = 0x80000000u | v;
+        pos = nx < sec_end ? nx : sec_end;  // truncated final group: readFully of what is left
+      }
+      L.rt[nrun] = (uint64_t)produced | ((uint64_t)payload << 32);
+      nrun++;
+      const uint64_t np = (uint64_t)produced + cnt;
+      produced = np < N ? (uint32_t)np : N;
+    }
+    if (code) {
+      if (lane == 0) report(err, err_count, page, 2, produced, code);
+      N = produced;
+    }
+    L.rt[nrun] = (uint64_t)produced;  // end sentinel
+    wave_sync();
     DIAG_ADD(d_walk, t_w);
 #ifdef PQG_DIAG
     d_nb++;
 #endif
-    DIAG_T(t_s);
-    if (code && lane == 0) report(err, err_count, page, 2, rb.end, code);
-    if (rb.end <= rb.first) break;
-    uint32_t nxt = __shfl_down(rb.start, 1);
-    const uint32_t run_end = (lane + 1 < rb.nr) ? nxt : rb.end;
-    // (2) RLE runs through the dictionary
-    uint32_t rlo = rb.lo, rhi = rb.hi;
-    if (lane < rb.nr && rb.meta == 0) {
-      if (rb.lo >= dict_n) {
-        report(err, err_count, page, 2, rb.start, PQG_ERR_DICT_ID);
-        rlo = 0;
-        rhi = 0;
-      } else {
-        uint64_t v = (uint64_t)load_dict<W>(drs, rb.lo);
-        rlo = (uint32_t)v;
-        rhi = (uint32_t)(v >> 32);
-      }
-    }
-    // (3) stage bit-packed values: lane r's packed run gets stage slots [soff, soff + pc)
-    const bool is_packed = lane < rb.nr && rb.meta == 1;
-    const uint32_t pc = is_packed ? run_end - rb.start : 0u;
-    uint32_t P;
-    const uint32_t soff = wave_excl_scan(pc, &P);
-    if (P) {
-      for (uint32_t q0 = 0; q0 < P; q0 += 4u * WAVE) {
-        uint32_t ids[4];
-        uint32_t vidx[4];
-        bool ok[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const uint32_t q = q0 + (uint32_t)u * WAVE + lane;
-          // run holding stage slot q: the last lane r with soff_r <= q (soff is non-decreasing)
-          uint32_t r = 0;
-#pragma unroll
-          for (uint32_t st = 32; st > 0; st >>= 1) {
-            const uint32_t c = r + st;
-            const uint32_t so_c = __shfl(soff, (int)c);
-            r = (c < 64u && so_c <= q) ? c : r;
-          }
-          const uint32_t so = __shfl(soff, (int)r), st = __shfl(rb.start, (int)r);
-          const uint32_t lo = __shfl(rb.lo, (int)r), hi = __shfl(rb.hi, (int)r);
-          ok[u] = q < P;
-          vidx[u] = st + (q - so);
-          ids[u] = ok[u] ? packed_elem(win.rs, lo, hi, 0, q - so, s.w) : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const uint32_t q = q0 + (uint32_t)u * WAVE + lane;
-          if (!ok[u]) continue;
-          T v = 0;
-          if (ids[u] >= dict_n) report(err, err_count, page, 2, vidx[u], PQG_ERR_DICT_ID);
-          else v = load_dict<W>(drs, ids[u]);
-          stage[q] = v;
-        }
-      }
-    }
-    rb.lo = is_packed ? soff : rlo;
-    rb.hi = is_packed ? 0u : rhi;
-    wave_sync();
-    DIAG_ADD(d_stage, t_s);
     DIAG_T(t_e);
-    // (4) expand [rb.first, rb.end). Page-relative 32-bit indices, shifted by `sh`
-    // so that chunk boundaries fall on 16-byte boundaries of the output.
-    {
-      constexpr uint32_t U = 2;                      // 16-byte stores per lane per chunk
-      constexpr uint32_t CH = (uint32_t)E * U * WAVE; // values per chunk
-      const uint32_t r_lo = rb.first + sh, r_hi = rb.end + sh;
-      for (uint32_t c0 = r_lo & ~(CH - 1); c0 < r_hi; c0 += CH) {
-        const uint32_t cl = (c0 > r_lo ? c0 : r_lo) - sh;
-        const uint32_t ch = (c0 + CH < r_hi ? c0 + CH : r_hi) - sh;
-        const uint64_t mask = overlap_mask(rb, run_end, cl, ch);
-        const uint32_t r0 = (uint32_t)__builtin_ctzll(mask);
-        if (__builtin_popcountll(mask) == 1 && rdl(rb.meta, r0) == 0) {
-          // the whole chunk lies in one RLE run: one value for every lane
-          const uint64_t v64 = ((uint64_t)rdl(rb.hi, r0) << 32) | rdl(rb.lo, r0);
-          const T v = (T)v64;
-#pragma unroll
-          for (uint32_t u = 0; u < U; u++) {
-            const uint32_t r = c0 + (u * WAVE + lane) * (uint32_t)E;  // shifted index of element 0
-            if (r >= r_lo && r + E <= r_hi && out16) {
-              if constexpr (W == 8) {
-                typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-                gst_nt((v2*)(pal + r), v2{v, v});
-              } else {
-                typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-                gst_nt((v4*)(pal + r), v4{v, v, v, v});
-              }
-            } else {
-#pragma unroll
-              for (int k = 0; k < E; k++)
-                if (r + k >= r_lo && r + k < r_hi) gst(pal + r + k, v);
-            }
-          }
-          continue;
+    // ---- expand the run records [first, produced)
+    for (uint32_t r = 0; r < nrun; r++) {
+      const uint64_t e0 = L.rt[r], e1 = L.rt[r + 1];
+      const uint32_t s0 = uni((uint32_t)e0), pl = uni((uint32_t)(e0 >> 32)), s1 = uni((uint32_t)e1);
+      if (!(pl & 0x80000000u)) {
+        T v = 0;
+        if (pl >= dict_n) {
+          if (lane == 0) report(err, err_count, page, 2, s0, PQG_ERR_DICT_ID);
+        } else {
+          v = dict_get(pl);
         }
-#pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-          const uint32_t r = c0 + (u * WAVE + lane) * (uint32_t)E;
-          uint32_t idx[E];
-          bool valid[E];
-          Sel sel[E];
-#pragma unroll
-          for (int k = 0; k < E; k++) {
-            valid[k] = r + k >= r_lo && r + k < r_hi;
-            idx[k] = r + k - sh;
-            sel[k] = Sel{0, 0, 0, 0};
-          }
-          select_runs(rb, mask, idx, sel, E);
-          T vals[E];
-#pragma unroll
-          for (int k = 0; k < E; k++) {
-            if (sel[k].meta == 0) {
-              vals[k] = (T)(((uint64_t)sel[k].hi << 32) | sel[k].lo);
-            } else {
-              uint32_t q = sel[k].lo + (idx[k] - sel[k].s);
-              vals[k] = stage[q < STAGE ? q : 0];
-            }
-          }
-          bool all = out16;
-#pragma unroll
-          for (int k = 0; k < E; k++) all = all && valid[k];
-          if (all) {
-            if constexpr (W == 8) {
-              typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-              gst_nt((v2*)(pal + r), v2{vals[0], vals[1]});
-            } else {
-              typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-              gst_nt((v4*)(pal + r), v4{vals[0], vals[1], vals[2], vals[3]});
-            }
-          } else {
-#pragma unroll
-            for (int k = 0; k < E; k++)
-              if (valid[k]) gst(pal + r + k, vals[k]);
-          }
+        store_run16<W>(pal, s0 + sh, s1 + sh, v, out16);
+      } else {
+        const uint32_t lo = pl & 0x7FFFFFFFu;
+        for (uint32_t i = lane; i < s1 - s0; i += WAVE) {
+          const uint32_t id = packed_elem_w(win, lo, sec_end, i, w);
+          T v = 0;
+          if (id >= dict_n) report(err, err_count, page, 2, s0 + i, PQG_ERR_DICT_ID);
+          else v = dict_get(id);
+          gst(pal + s0 + sh + i, v);
         }
       }
     }
-    wave_sync();  // stage is rewritten by the next batch
+    (void)first;
+    wave_sync();  // the run table is rewritten by the next batch
     DIAG_ADD(d_exp, t_e);
   }
-  asm volatile("; prefetch sink" ::"v"(pf0), "v"(pf1));
 #ifdef PQG_DIAG
   if (lane == 0 && pqg_diag_buf) {
     uint64_t* d = pqg_diag_buf + 8 * (uint64_t)page;
@@ -772,6 +870,8 @@ __device__ uint32_t decode_levels(rsrc_t rs, uint32_t beg, uint32_t end, int w, 
   s.w = w;
   PreWin win;
   win.rs = rs;
+  win.seg = nullptr;
+  win.seg_lo = 0;
   if (N) predecode(win, beg & ~3u, w);
   uint32_t cnt = 0;
   int first_err = 0;
@@ -1226,6 +1326,9 @@ __global__ __launch_bounds__(256) void k_unpack_runs(int w, const uint8_t* __res
 
 #ifdef PQG_DIAG
 }  // namespace pqg
+extern "C" int pqg_diag_nostore_set(int v) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(pqg::pqg_diag_nostore), &v, sizeof(v)) == hipSuccess ? 0 : 3;
+}
 extern "C" int pqg_diag_set(void* p) {
   return hipMemcpyToSymbol(HIP_SYMBOL(pqg::pqg_diag_buf), &p, sizeof(p)) == hipSuccess ? 0 : 3;
 }

@@ -17,6 +17,7 @@ from pqgpu import decoder as D, native, writer  # noqa: E402
 
 zipf = float(sys.argv[1]) if len(sys.argv) > 1 else 1.5
 out = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/diag.json"
+nostore = len(sys.argv) > 3 and sys.argv[3] == "nostore"
 chunk, dv, ids = bench.make_c2(100_000_000, a=zipf)
 batch = writer.build_batch([chunk])
 dec = D.Decoder(0)
@@ -25,6 +26,8 @@ buf = torch.zeros(batch.n_pages * 8, dtype=torch.int64, device="cuda")
 L = native.lib()
 L.pqg_diag_set.argtypes = [C.c_void_p]
 assert L.pqg_diag_set(buf.data_ptr()) == 0
+L.pqg_diag_nostore_set.argtypes = [C.c_int]
+assert L.pqg_diag_nostore_set(1 if nostore else 0) == 0
 for _ in range(3):
     plan.launch()
 torch.cuda.synchronize()
@@ -37,7 +40,7 @@ d = buf.view(-1, 8).cpu().numpy().astype(np.float64)
 start, end = d[:, 0], d[:, 1]
 t0 = start.min()
 res = {
-    "zipf": zipf, "kernel_ms_event": ev0.elapsed_time(ev1),
+    "zipf": zipf, "nostore": nostore, "kernel_ms_event": ev0.elapsed_time(ev1),
     "span_us": (end.max() - t0) / 100.0,  # s_memrealtime: 100 MHz
     "start_us_pct": np.percentile((start - t0) / 100.0, [0, 10, 50, 90, 99, 100]).tolist(),
     "dur_us_pct": np.percentile((end - start) / 100.0, [0, 10, 50, 90, 99, 100]).tolist(),
