@@ -579,7 +579,7 @@ __device__ __forceinline__ typename DictVal<W>::T load_dict(rsrc_t d, uint32_t i
 }
 
 constexpr uint32_t DICT_LDS_BYTES = 8192;   // dictionary staged in LDS per workgroup when it fits
-constexpr uint32_t RT_MAX = 24;             // run records per expansion batch (LDS, per wave): small, so stores start early
+constexpr uint32_t RT_MAX = 32;             // runs per expansion batch (lane r holds run r): small, so stores start early
 constexpr uint32_t NX_SENTINEL = 0xFFFFFFFFu;
 
 // Per-wave LDS of k_dict.
@@ -587,7 +587,6 @@ struct DictWaveLds {
   uint8_t seg[SEG_BYTES];  // page bytes [seg_lo, seg_lo + SEG_BYTES)
   uint64_t ent[256];       // window position k: next header position | (count | packed << 31) << 32
   uint32_t val[256];       // window position k: RLE raw value, or packed data start
-  uint64_t rt[RT_MAX + 1]; // run records: start | payload << 32 (payload: RLE id (<2^31) or 2^31 | data start)
 };
 
 // Exclusive prefix sum over the wave (u32); *total = sum over all lanes.
@@ -737,10 +736,11 @@ __global__ __launch_bounds__(64 * WPB) void k_dict(const uint8_t* __restrict__ b
   uint32_t B = pos - 260u;     // current window: none yet (pos - B >= 256 forces a pre-decode)
   while (produced < N) {
     DIAG_T(t_w);
-    // ---- chain: read runs into the run table (up to RT_MAX)
+    // ---- chain: read runs; run r's record lands in lane r (start, payload)
     uint32_t nrun = 0;
     const uint32_t first = produced;
     int code = 0;
+    uint32_t r_start = 0, r_pl = 0;
     while (produced < N && nrun < RT_MAX) {
       if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }           // readNext :81
       if (pos - B >= 256u) {
@@ -788,7 +788,9 @@ __global__ __launch_bounds__(64 * WPB) void k_dict(const uint8_t* __restrict__ b
         payload = 0x80000000u | v;
         pos = nx < sec_end ? nx : sec_end;  // truncated final group: readFully of what is left
       }
-      L.rt[nrun] = (uint64_t)produced | ((uint64_t)payload << 32);
+      const bool me = lane == nrun;
+      r_start = me ? produced : r_start;
+      r_pl = me ? payload : r_pl;
       nrun++;
       const uint64_t np = (uint64_t)produced + cnt;
       produced = np < N ? (uint32_t)np : N;
@@ -797,24 +799,29 @@ __global__ __launch_bounds__(64 * WPB) void k_dict(const uint8_t* __restrict__ b
       if (lane == 0) report(err, err_count, page, 2, produced, code);
       N = produced;
     }
-    L.rt[nrun] = (uint64_t)produced;  // end sentinel
-    wave_sync();
     DIAG_ADD(d_walk, t_w);
 #ifdef PQG_DIAG
     d_nb++;
 #endif
     DIAG_T(t_e);
-    // ---- expand the run records [first, produced)
+    // ---- resolve every RLE run of the batch through the dictionary in one gather
+    const uint32_t r_end_n = __shfl_down(r_start, 1);
+    const uint32_t r_end = lane + 1 < nrun ? r_end_n : produced;
+    uint32_t r_lo = 0, r_hi = 0;
+    if (lane < nrun && !(r_pl & 0x80000000u)) {
+      if (r_pl >= dict_n) {
+        report(err, err_count, page, 2, r_start, PQG_ERR_DICT_ID);
+      } else {
+        const uint64_t v = (uint64_t)dict_get(r_pl);
+        r_lo = (uint32_t)v;
+        r_hi = (uint32_t)(v >> 32);
+      }
+    }
+    // ---- expand [first, produced): a uniform loop over the runs, no LDS waits for RLE runs
     for (uint32_t r = 0; r < nrun; r++) {
-      const uint64_t e0 = L.rt[r], e1 = L.rt[r + 1];
-      const uint32_t s0 = uni((uint32_t)e0), pl = uni((uint32_t)(e0 >> 32)), s1 = uni((uint32_t)e1);
+      const uint32_t s0 = rdl(r_start, r), s1 = rdl(r_end, r), pl = rdl(r_pl, r);
       if (!(pl & 0x80000000u)) {
-        T v = 0;
-        if (pl >= dict_n) {
-          if (lane == 0) report(err, err_count, page, 2, s0, PQG_ERR_DICT_ID);
-        } else {
-          v = dict_get(pl);
-        }
+        const T v = (T)(((uint64_t)rdl(r_hi, r) << 32) | rdl(r_lo, r));
         store_run16<W>(pal, s0 + sh, s1 + sh, v, out16);
       } else {
         const uint32_t lo = pl & 0x7FFFFFFFu;
@@ -828,7 +835,6 @@ __global__ __launch_bounds__(64 * WPB) void k_dict(const uint8_t* __restrict__ b
       }
     }
     (void)first;
-    wave_sync();  // the run table is rewritten by the next batch
     DIAG_ADD(d_exp, t_e);
   }
 #ifdef PQG_DIAG
