@@ -100,6 +100,8 @@ struct pqg_plan {
   int n_pages = 0;
   int n_cols = 0;
   DevBuf work, cols, lists, col_pages, col_page_start, err, err_count;
+  DevBuf rec, chunk_run, chunks;      // dictionary pages: run records, chunk -> record, chunk work list
+  uint32_t chunk_off[2] = {0, 0}, chunk_n[2] = {0, 0};  // C_DICT4, C_DICT8 ranges in `chunks`
   std::vector<PageWork> h_work;
   std::vector<int> cls_off, cls_n;  // into lists
   int levels_off = 0, levels_n = 0;
@@ -337,6 +339,26 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     cls_lists[(size_t)cls].push_back(p);
   }
   for (int i = 0; i < n_cols; i++) P->col_required_values[(size_t)i] = val_acc[(size_t)i];
+  // ---- dictionary pages: run-record capacity (a run covers >= 1 value and its header takes
+  // >= 1 byte) and output chunks (slots [j*CH, (j+1)*CH) of the page, upper bound from the slot count)
+  std::vector<uint64_t> chunk_list;
+  uint64_t rec_total = 0;
+  uint32_t chunk_total = 0;
+  for (int k = C_DICT4; k <= C_DICT8; k++) {
+    P->chunk_off[k - C_DICT4] = (uint32_t)chunk_list.size();
+    for (int p : cls_lists[(size_t)k]) {
+      PageWork& w = P->h_work[(size_t)p];
+      const int ew = k == C_DICT8 ? 8 : 4;
+      const uint32_t ch = pqg::dict_chunk_values(ew);
+      w.rec_base = rec_total;
+      rec_total += (uint64_t)std::min<uint32_t>(w.num_slots, w.size) + 1;
+      w.chunk_base = chunk_total;
+      const uint32_t nch = (uint32_t)(((uint64_t)w.num_slots + (uint32_t)(16 / ew) - 1 + ch - 1) / ch);
+      for (uint32_t j = 0; j < nch; j++) chunk_list.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
+      chunk_total += nch;
+    }
+    P->chunk_n[k - C_DICT4] = (uint32_t)chunk_list.size() - P->chunk_off[k - C_DICT4];
+  }
   // ---- flatten lists: [levels][class 0]...[class n]
   std::vector<int32_t> flat(lvl_list.begin(), lvl_list.end());
   P->levels_off = 0;
@@ -364,7 +386,12 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
             P->col_pages.ensure(sizeof(int32_t) * std::max<size_t>(cp.size(), 1)) == hipSuccess &&
             P->col_page_start.ensure(sizeof(int32_t) * cps.size()) == hipSuccess &&
             P->err.ensure(sizeof(uint64_t) * 3 * (size_t)std::max(n_pages, 1)) == hipSuccess &&
-            P->err_count.ensure(sizeof(uint32_t) * 4) == hipSuccess;
+            P->err_count.ensure(sizeof(uint32_t) * 4) == hipSuccess &&
+            P->rec.ensure(sizeof(uint64_t) * std::max<uint64_t>(rec_total, 1)) == hipSuccess &&
+            P->chunk_run.ensure(sizeof(uint32_t) * std::max<uint32_t>(chunk_total, 1)) == hipSuccess &&
+            P->chunks.ensure(sizeof(uint64_t) * std::max<size_t>(chunk_list.size(), 1)) == hipSuccess;
+  if (!chunk_list.empty())
+    ok = ok && hipMemcpyAsync(P->chunks.p, chunk_list.data(), sizeof(uint64_t) * chunk_list.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   ok = ok && hipMemcpyAsync(P->work.p, P->h_work.data(), sizeof(PageWork) * P->h_work.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   ok = ok && hipMemcpyAsync(P->cols.p, hc.data(), sizeof(ColumnDev) * hc.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   if (!flat.empty()) ok = ok && hipMemcpyAsync(P->lists.p, flat.data(), sizeof(int32_t) * flat.size(), hipMemcpyHostToDevice, s) == hipSuccess;
@@ -379,6 +406,7 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
   }
   P->kernels = (P->levels_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
   for (int k = 0; k < C_NCLS; k++) P->kernels += P->cls_n[(size_t)k] ? 1 : 0;
+  for (int i = 0; i < 2; i++) P->kernels += P->chunk_n[i] ? 1 : 0;  // k_dict_expand
   *out = P;
   return PQG_OK;
 }
@@ -407,8 +435,14 @@ int pqg_plan_launch(pqg_plan* P) {
     if (!n) continue;
     const int32_t* l = lists + P->cls_off[(size_t)k];
     switch (k) {
-      case C_DICT4: e = pqg::launch_dict(4, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
-      case C_DICT8: e = pqg::launch_dict(8, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_DICT4:
+      case C_DICT8: {
+        const int i = k - C_DICT4;
+        e = pqg::launch_dict(k == C_DICT8 ? 8 : 4, s, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
+                             (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->chunk_off[i], P->chunk_n[i],
+                             err, ecount);
+        break;
+      }
       case C_PLAIN: e = pqg::launch_plain(0, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_BOOL: e = pqg::launch_plain(1, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_DELTA4: e = pqg::launch_delta(4, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
@@ -433,6 +467,9 @@ int pqg_plan_destroy(pqg_plan* P) {
   P->col_page_start.release();
   P->err.release();
   P->err_count.release();
+  P->rec.release();
+  P->chunk_run.release();
+  P->chunks.release();
   delete P;
   return PQG_OK;
 }

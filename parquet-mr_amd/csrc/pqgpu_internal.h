@@ -38,10 +38,24 @@ struct PageWork {
   int32_t dl_encoding;
   uint32_t rl_len;      // V2
   uint32_t dl_len;      // V2
+  // dictionary pages: run records (k_dict_runs -> k_dict_expand)
+  uint64_t rec_base;    // first run record of the page
+  uint32_t chunk_base;  // first output chunk of the page
+  uint32_t n_rec;       // run records written (device)
+  uint32_t n_ok;        // values covered before a run-walk error (device)
+  uint32_t reserved;
 };
 
+// Output chunk of k_dict_expand: CH_TILES x 64 lanes x 16 bytes.
+#ifndef PQG_CHUNK_TILES
+#define PQG_CHUNK_TILES 8
+#endif
+constexpr uint32_t DICT_CHUNK_TILES = PQG_CHUNK_TILES;
+inline uint32_t dict_chunk_values(int elem_width) { return DICT_CHUNK_TILES * 64u * (16u / (uint32_t)elem_width); }
+
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                       const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+                       const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
+                       const uint64_t* chunks, uint32_t n_chunks, uint64_t* err, uint32_t* err_count);
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                          const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
 hipError_t launch_scan(hipStream_t st, PageWork* work, const int32_t* col_pages, const int32_t* col_page_start,

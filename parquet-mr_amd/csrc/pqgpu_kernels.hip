@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "pqgpu_internal.h"
 
 namespace pqg {
@@ -109,19 +111,18 @@ __device__ __forceinline__ uint32_t ld32(rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
 }
 
-// 8 bytes at any byte offset (little endian).
+// 8 bytes at any byte offset (little endian). Branch-free (v_alignbyte): a load issued on
+// only one path leaves the waitcnt pass a "maybe pending" load at every later merge point,
+// and it then answers with s_waitcnt vmcnt(0) — draining all stores — in unrelated loops.
 __device__ __forceinline__ uint64_t ld8_any(rsrc_t r, uint32_t off) {
-  uint32_t a = off & ~3u, sh = (off & 3u) * 8u;
-  uint64_t x = (uint64_t)ld32(r, a) | ((uint64_t)ld32(r, a + 4) << 32);
-  if (sh) x = (x >> sh) | ((uint64_t)ld32(r, a + 8) << (64u - sh));
-  return x;
+  const uint32_t a = off & ~3u, sb = off & 3u;
+  const uint32_t w0 = ld32(r, a), w1 = ld32(r, a + 4), w2 = ld32(r, a + 8);
+  return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sb) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sb) << 32);
 }
 
 __device__ __forceinline__ uint32_t ld4_any(rsrc_t r, uint32_t off) {
-  uint32_t a = off & ~3u, sh = (off & 3u) * 8u;
-  uint32_t x = ld32(r, a);
-  if (sh) x = (x >> sh) | (ld32(r, a + 4) << (32u - sh));
-  return x;
+  const uint32_t a = off & ~3u, sb = off & 3u;
+  return __builtin_amdgcn_alignbyte(ld32(r, a + 4), ld32(r, a), sb);
 }
 
 // Record an error: smallest (index << 8 | code) per (page, kind) wins.
@@ -244,7 +245,7 @@ struct PreWin {
   uint32_t flg;        // byte b: bit0 packed, bit1 slow path, bits 2..4 header length
 };
 
-constexpr uint32_t SEG_BYTES = 1536;   // LDS page segment per wave (budget: 5 workgroups per CU)
+constexpr uint32_t SEG_BYTES = 4096;   // LDS page segment per wave of k_dict_runs (5 workgroups per CU)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -273,12 +274,15 @@ __device__ __forceinline__ uint32_t seg32(const PreWin& pw, uint32_t a) {  // a 
   return *(const uint32_t*)(pw.seg + (a - pw.seg_lo));
 }
 
+// LDS_ONLY: the caller guarantees the whole section is in the segment (no refill,
+// no global load: the hot loop then never waits on vmcnt, which would drain stores).
+template <bool LDS_ONLY = false>
 __device__ __forceinline__ void predecode(PreWin& pw, uint32_t B, int w) {
   pw.B = B;
   const uint32_t base = B + 4u * lane_id();
-  if (pw.seg && !seg_has(pw, B, 264u)) seg_fill(pw, B & ~15u);
+  if (!LDS_ONLY && pw.seg && !seg_has(pw, B, 264u)) seg_fill(pw, B & ~15u);
   uint32_t d0, d1, d2;
-  if (pw.seg) {
+  if (LDS_ONLY || pw.seg) {
     d0 = seg32(pw, base);
     d1 = seg32(pw, base + 4);
     d2 = seg32(pw, base + 8);
@@ -366,12 +370,22 @@ __device__ __forceinline__ uint32_t sbyte(rsrc_t rs, uint32_t p) {
   return uni((ld32(rs, p & ~3u) >> ((p & 3u) * 8u)) & 0xFFu);
 }
 
+template <class ByteAt>
+__device__ int slow_header_g(ByteAt sbyte_at, uint32_t pos, uint32_t sec_end, int w, uint32_t& hl, uint32_t& m,
+                             uint64_t& count, uint32_t& val, uint32_t& next);
+
 __device__ int slow_header(rsrc_t rs, uint32_t pos, uint32_t sec_end, int w, uint32_t& hl, uint32_t& m, uint64_t& count,
                            uint32_t& val, uint32_t& next) {
+  return slow_header_g([&](uint32_t p) { return sbyte(rs, p); }, pos, sec_end, w, hl, m, count, val, next);
+}
+
+template <class ByteAt>
+__device__ int slow_header_g(ByteAt sbyte_at, uint32_t pos, uint32_t sec_end, int w, uint32_t& hl, uint32_t& m,
+                             uint64_t& count, uint32_t& val, uint32_t& next) {
   uint32_t value = 0, i = 0, k = 0, bb;
   for (;;) {
     if (pos + k >= sec_end) return PQG_ERR_EOF;
-    bb = sbyte(rs, pos + k);
+    bb = sbyte_at(pos + k);
     if (!(bb & 0x80u)) break;
     value |= (bb & 0x7Fu) << (i & 31u);
     i += 7;
@@ -383,7 +397,7 @@ __device__ int slow_header(rsrc_t rs, uint32_t pos, uint32_t sec_end, int w, uin
     const uint32_t nb = ((uint32_t)w + 7u) >> 3;
     if ((uint64_t)pos + hl + nb > sec_end) return PQG_ERR_EOF;
     uint32_t v = 0;
-    for (uint32_t j = 0; j < nb; j++) v |= sbyte(rs, pos + hl + j) << (8u * j);
+    for (uint32_t j = 0; j < nb; j++) v |= sbyte_at(pos + hl + j) << (8u * j);
     m = 0;
     count = header >> 1;
     val = v;
@@ -515,13 +529,14 @@ __device__ __forceinline__ uint32_t packed_elem(rsrc_t rs, uint32_t lo, uint32_t
 }
 
 // packed_elem reading the LDS segment when the 8 bytes are there.
+template <bool LDS_ONLY = false>
 __device__ __forceinline__ uint32_t packed_elem_w(const PreWin& pw, uint32_t lo, uint32_t hi, uint32_t j, int w) {
   if (w == 0) return 0;
   const uint64_t bit = (uint64_t)j * (uint32_t)w;
   const uint32_t byte = lo + (uint32_t)(bit >> 3);
   const uint32_t a = byte & ~3u;
   uint64_t x;
-  if (seg_has(pw, a, 8)) x = (uint64_t)seg32(pw, a) | ((uint64_t)seg32(pw, a + 4) << 32);
+  if (LDS_ONLY || seg_has(pw, a, 8)) x = (uint64_t)seg32(pw, a) | ((uint64_t)seg32(pw, a + 4) << 32);
   else x = (uint64_t)ld32(pw.rs, a) | ((uint64_t)ld32(pw.rs, a + 4) << 32);
   if (a + 8u > hi) {
     const int64_t keep = (int64_t)hi - (int64_t)a;
@@ -579,7 +594,7 @@ __device__ __forceinline__ typename DictVal<W>::T load_dict(rsrc_t d, uint32_t i
 }
 
 constexpr uint32_t DICT_LDS_BYTES = 8192;   // dictionary staged in LDS per workgroup when it fits
-constexpr uint32_t RT_MAX = 32;             // runs per expansion batch (lane r holds run r): small, so stores start early
+constexpr uint32_t RT_MAX = 64;             // runs per expansion batch (lane r holds run r)
 constexpr uint32_t NX_SENTINEL = 0xFFFFFFFFu;
 
 // Per-wave LDS of k_dict.
@@ -601,152 +616,57 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) 
   return x - v;
 }
 
-template <int W>
-__device__ __forceinline__ void store_run16(typename DictVal<W>::T* pal, uint32_t a, uint32_t b, typename DictVal<W>::T v,
-                                            bool out16) {
-  typedef typename DictVal<W>::T T;
-  constexpr uint32_t E = 16 / W;
-  const uint32_t lane = lane_id();
-  const uint32_t a16 = out16 ? (a + E - 1) & ~(E - 1) : b;
-  const uint32_t b16 = out16 ? b & ~(E - 1) : b;
-  if (a16 < b16) {
-    if (lane < a16 - a) gst(pal + a + lane, v);
-    if (lane < b - b16) gst(pal + b16 + lane, v);
-    constexpr uint32_t STEP = E * WAVE;
-    uint32_t g = a16 + E * lane;
-    for (; g + 3 * STEP < b16; g += 4 * STEP) {
-#pragma unroll
-      for (uint32_t u = 0; u < 4; u++) {
-        if constexpr (W == 8) {
-          typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-          gst_nt((v2*)(pal + g + u * STEP), v2{v, v});
-        } else {
-          gst_nt((u32x4*)(pal + g + u * STEP), u32x4{v, v, v, v});
-        }
-      }
-    }
-    for (; g < b16; g += STEP) {
-      if constexpr (W == 8) {
-        typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-        gst_nt((v2*)(pal + g), v2{v, v});
-      } else {
-        gst_nt((u32x4*)(pal + g), u32x4{v, v, v, v});
-      }
-    }
-  } else {
-    for (uint32_t i = a + lane; i < b; i += WAVE) gst(pal + i, v);
-  }
-}
-
-// One wave per page (4 per workgroup).
+// ---------------------------------------------------------------------------
+// Dictionary pages in two launches.
 //
-//   stage   the workgroup's dictionary (when its pages share one that fits) and each
-//           wave's page data section into LDS, before any store: on CDNA vmcnt counts
-//           stores, so a global load issued after stores waits for all of them.
-//   window  a 256-byte window of the section is pre-decoded in parallel (every lane
-//           parses a run header at each of its 4 byte positions) into LDS tables.
-//   chain   the serial part — following headers from the section start — is one
-//           ds_read_b64 + ds_read_b32 per run, appending an 8-byte run record.
-//   expand  per run record: RLE -> dictionary value (LDS) stored with 16-byte
-//           non-temporal stores; bit-packed -> lanes unpack ids from the LDS page
-//           bytes and gather from the LDS dictionary.
-template <int W>
-__global__ __launch_bounds__(64 * WPB) void k_dict(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                                    const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
-                                                    const int32_t* __restrict__ list, int n_list, uint64_t* err,
-                                                    uint32_t* err_count) {
-  typedef typename DictVal<W>::T T;
-  constexpr uint32_t E = 16 / W;
-  __shared__ __attribute__((aligned(16))) uint8_t dict_lds[DICT_LDS_BYTES];
-  __shared__ __attribute__((aligned(16))) DictWaveLds wl_all[WPB];
-  __shared__ int wg_col[WPB];
-  DictWaveLds& L = wl_all[wave_id()];
-  const int page = wave_page(list, n_list);
+//   k_dict_runs    one wave per page: follows the run headers of the page's data
+//                  section and writes one 8-byte record per run (first value index,
+//                  payload: raw RLE id, or 0x80000000 | packed data position), plus,
+//                  per output chunk, the record holding the chunk's first value.
+//                  No dictionary access, no value stores: latency-bound LDS work.
+//   k_dict_expand  one wave per output chunk (CH_TILES x 64 lanes x 16 bytes), a
+//                  persistent grid over all chunks of all pages, so the expansion
+//                  is balanced regardless of how runs are spread over pages. All
+//                  loads of a chunk (records, packed bytes, dictionary) come before
+//                  its stores: on CDNA vmcnt counts stores, and a load issued after
+//                  stores would wait for all of them.
+constexpr uint32_t CH_TILES = DICT_CHUNK_TILES;
+
+__device__ __forceinline__ uint32_t chunk_values(uint32_t E) { return CH_TILES * WAVE * E; }
+
+template <bool SMALL>
+__device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg, uint32_t sec_end,
+                                          int w, uint64_t* rec, uint32_t* chunk_run, uint32_t CH, uint32_t sh, int page,
+                                          uint64_t* err, uint32_t* err_count, uint32_t& n_rec, uint32_t& n_ok) {
   const uint32_t lane = lane_id();
-
-  if (lane == 0) wg_col[wave_id()] = page >= 0 ? work[page].column : -1;
-  __syncthreads();
-  int c0 = -1;
-  bool same = true;
-#pragma unroll
-  for (int k = 0; k < WPB; k++) {
-    const int c = wg_col[k];
-    if (c >= 0) {
-      if (c0 < 0) c0 = c;
-      else if (c != c0) same = false;
-    }
-  }
-  bool dict_in_lds = false;
-  if (same && c0 >= 0) {
-    const ColumnDev& cd0 = cols[c0];
-    const uint64_t need = (uint64_t)cd0.dict_n * W;
-    dict_in_lds = need <= DICT_LDS_BYTES && need <= cd0.dict_bytes;
-    if (dict_in_lds) {
-      rsrc_t d0 = make_rsrc(bytes + cd0.dict_offset, cd0.dict_bytes);
-      const bool al = (cd0.dict_offset & 3u) == 0;
-      for (uint32_t o = 16u * threadIdx.x; o < (uint32_t)need; o += 16u * 64u * WPB) {
-        u32x4 v;
-        if (al) v = __builtin_amdgcn_raw_buffer_load_b128(d0, (int)o, 0, 0);
-        else v = u32x4{ld4_any(d0, o), ld4_any(d0, o + 4), ld4_any(d0, o + 8), ld4_any(d0, o + 12)};
-        *(u32x4*)(dict_lds + o) = v;
-      }
-    }
-  }
-  __syncthreads();
-  if (page < 0) return;
-  const PageWork pw = work[page];
-  const ColumnDev cd = cols[pw.column];
-  uint32_t N = uni(pw.n_values);
-  const uint32_t sec_beg = uni(pw.data_begin), sec_end = uni(pw.size);
-  if (N == 0 && sec_beg >= sec_end) return;
-
-  PreWin win;
-  win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
-  win.seg = L.seg;
-  rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
-  const uint32_t dict_n = uni(cd.dict_n);
-  const T* dict_l = (const T*)dict_lds;
-  auto dict_get = [&](uint32_t id) -> T { return dict_in_lds ? dict_l[id] : load_dict<W>(drs, id); };
-
-  // DictionaryValuesReader.initFromPage :48-64
-  if (sec_beg >= sec_end) {  // empty data section: every read throws "Attempt to read from empty page"
-    if (N && lane == 0) report(err, err_count, page, 2 /*value*/, 0, PQG_ERR_EMPTY_PAGE);
-    return;
-  }
-  seg_fill(win, sec_beg & ~15u);
-  const uint32_t bw = wbyte(win, sec_beg);
-  if (bw > 32u) {  // RunLengthBitPackingHybridDecoder ctor :55 (thrown at initFromPage)
-    if (lane == 0) report(err, err_count, page, 0 /*init*/, 2, PQG_ERR_BIT_WIDTH);
-    return;
-  }
-  const int w = (int)bw;
-  const uint32_t nb = (bw + 7u) >> 3;
-  T* out = (T*)cd.values;
-  const uint64_t obase = pw.out_offset;
-  const bool out16 = ((uintptr_t)out & 15u) == 0;
-  const uint32_t sh = (uint32_t)(obase % (uint64_t)E);
-  T* pal = out + (obase - sh);
-#ifdef PQG_DIAG
-  const uint64_t d_start = __builtin_amdgcn_s_memrealtime();
-  uint64_t d_walk = 0, d_stage = 0, d_exp = 0, d_nb = 0;
-#endif
-
   uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
   uint32_t produced = 0;       // values covered by the runs read so far
   uint32_t B = pos - 260u;     // current window: none yet (pos - B >= 256 forces a pre-decode)
-  while (produced < N) {
-    DIAG_T(t_w);
+  uint32_t k = 0;              // records written
+  while (true) {
+    // loop-carried scalars re-asserted wave-uniform (readfirstlane): without this the
+    // divergence analysis keeps them in VGPRs and runs the chain as masked vector code
+    produced = uni(produced);
+    N = uni(N);
+    pos = uni(pos);
+    B = uni(B);
+    k = uni(k);
+    if (produced >= N) break;
     // ---- chain: read runs; run r's record lands in lane r (start, payload)
     uint32_t nrun = 0;
-    const uint32_t first = produced;
     int code = 0;
     uint32_t r_start = 0, r_pl = 0;
-    while (produced < N && nrun < RT_MAX) {
+    while (true) {
+      produced = uni(produced);
+      pos = uni(pos);
+      nrun = uni(nrun);
+      B = uni(B);
+      if (produced >= N || nrun >= RT_MAX) break;
       if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }           // readNext :81
       if (pos - B >= 256u) {
         // new window: pre-decode 256 positions into LDS
         B = pos & ~3u;
-        predecode(win, B, w);
+        predecode<SMALL>(win, B, w);
 #pragma unroll
         for (uint32_t bb = 0; bb < 4; bb++) {
           const uint32_t p = B + 4u * lane + bb;
@@ -762,15 +682,19 @@ __global__ __launch_bounds__(64 * WPB) void k_dict(const uint8_t* __restrict__ b
         }
         wave_sync();
       }
-      const uint32_t k = pos - B;
-      const uint64_t e = L.ent[k];
+      const uint32_t kk = pos - B;
+      const uint64_t e = L.ent[kk];
       uint32_t nx = uni((uint32_t)e);
       uint32_t cw = uni((uint32_t)(e >> 32));
-      uint32_t v = uni(L.val[k]);
+      uint32_t v = uni(L.val[kk]);
       if (nx == NX_SENTINEL) {
         uint32_t hl, m, nxs, vv;
         uint64_t cnt64;
-        code = slow_header(win.rs, pos, sec_end, w, hl, m, cnt64, vv, nxs);
+        if constexpr (SMALL)
+          code = slow_header_g([&](uint32_t p) { return uni((seg32(win, p & ~3u) >> ((p & 3u) * 8u)) & 0xFFu); }, pos,
+                               sec_end, w, hl, m, cnt64, vv, nxs);
+        else
+          code = slow_header(win.rs, pos, sec_end, w, hl, m, cnt64, vv, nxs);
         if (code) break;
         if (m == 0 && nxs > sec_end) { code = PQG_ERR_EOF; break; }
         nx = nxs;
@@ -799,61 +723,310 @@ __global__ __launch_bounds__(64 * WPB) void k_dict(const uint8_t* __restrict__ b
       if (lane == 0) report(err, err_count, page, 2, produced, code);
       N = produced;
     }
-    DIAG_ADD(d_walk, t_w);
-#ifdef PQG_DIAG
-    d_nb++;
-#endif
-    DIAG_T(t_e);
-    // ---- resolve every RLE run of the batch through the dictionary in one gather
+    // ---- records, and the record holding each chunk's first value
+    // (chunk j covers output slots [j*CH, (j+1)*CH); its first value is max(0, j*CH - sh))
     const uint32_t r_end_n = __shfl_down(r_start, 1);
-    const uint32_t r_end = lane + 1 < nrun ? r_end_n : produced;
-    uint32_t r_lo = 0, r_hi = 0;
-    if (lane < nrun && !(r_pl & 0x80000000u)) {
-      if (r_pl >= dict_n) {
-        report(err, err_count, page, 2, r_start, PQG_ERR_DICT_ID);
+    if (lane < nrun) {
+      const uint32_t r_end = lane + 1 < nrun ? r_end_n : produced;
+      gst(rec + k + lane, (uint64_t)r_start | ((uint64_t)r_pl << 32));
+      uint32_t j = r_start == 0 ? 0 : (r_start + sh + CH - 1) / CH;
+      for (; j * CH < r_end + sh; j++) gst(chunk_run + j, k + lane);
+    }
+    k += nrun;
+  }
+  n_rec = k;
+  n_ok = N;
+}
+
+// One wave per page (4 per workgroup): the run records of RLE_DICTIONARY / PLAIN_DICTIONARY
+// pages (DictionaryValuesReader.initFromPage :48-64 + RunLengthBitPackingHybridDecoder.readNext
+// :80-109). The page section is staged in LDS; a 256-byte window is pre-decoded in parallel
+// (every lane parses a run header at each of its 4 byte positions) into LDS tables, and the
+// serial chain is one ds_read_b64 + ds_read_b32 per run.
+__global__ __launch_bounds__(64 * WPB) void k_dict_runs(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                        PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                                        const int32_t* __restrict__ list, int n_list, uint64_t* rec,
+                                                        uint32_t* chunk_run, uint64_t* err, uint32_t* err_count) {
+  __shared__ __attribute__((aligned(16))) DictWaveLds wl_all[WPB];
+  DictWaveLds& L = wl_all[wave_id()];
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
+  const uint32_t lane = lane_id();
+  const PageWork pw = work[page];
+  const ColumnDev cd = cols[pw.column];
+  uint32_t N = uni(pw.n_values);
+  const uint32_t sec_beg = uni(pw.data_begin), sec_end = uni(pw.size);
+  const uint32_t E = 16u / (uint32_t)cd.elem_width;
+  const uint32_t CH = chunk_values(E);
+  const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
+  uint32_t n_rec = 0, n_ok = 0;
+  if (N > 0) {
+    PreWin win;
+    win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+    win.seg = L.seg;
+    if (sec_beg >= sec_end) {
+      // empty data section: every read throws "Attempt to read from empty page"
+      if (lane == 0) report(err, err_count, page, 2 /*value*/, 0, PQG_ERR_EMPTY_PAGE);
+    } else {
+      seg_fill(win, sec_beg & ~15u);
+      const uint32_t bw = wbyte(win, sec_beg);
+      if (bw > 32u) {  // RunLengthBitPackingHybridDecoder ctor :55 (thrown at initFromPage)
+        if (lane == 0) report(err, err_count, page, 0 /*init*/, 2, PQG_ERR_BIT_WIDTH);
       } else {
-        const uint64_t v = (uint64_t)dict_get(r_pl);
-        r_lo = (uint32_t)v;
-        r_hi = (uint32_t)(v >> 32);
+        uint64_t* prec = rec + pw.rec_base;
+        uint32_t* pcr = chunk_run + pw.chunk_base;
+        // SMALL: the whole data section sits in the LDS segment: the walk has no global load
+        if (sec_end - win.seg_lo <= SEG_BYTES)
+          dict_walk<true>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
+        else
+          dict_walk<false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
       }
     }
-    // ---- expand [first, produced): a uniform loop over the runs, no LDS waits for RLE runs
-    for (uint32_t r = 0; r < nrun; r++) {
-      const uint32_t s0 = rdl(r_start, r), s1 = rdl(r_end, r), pl = rdl(r_pl, r);
-      if (!(pl & 0x80000000u)) {
-        const T v = (T)(((uint64_t)rdl(r_hi, r) << 32) | rdl(r_lo, r));
-        store_run16<W>(pal, s0 + sh, s1 + sh, v, out16);
-      } else {
-        const uint32_t lo = pl & 0x7FFFFFFFu;
-        for (uint32_t i = lane; i < s1 - s0; i += WAVE) {
-          const uint32_t id = packed_elem_w(win, lo, sec_end, i, w);
-          T v = 0;
-          if (id >= dict_n) report(err, err_count, page, 2, s0 + i, PQG_ERR_DICT_ID);
-          else v = dict_get(id);
-          gst(pal + s0 + sh + i, v);
+  }
+  if (lane == 0) {
+    work[page].n_rec = n_rec;
+    work[page].n_ok = n_ok;
+  }
+}
+
+// Persistent grid over output chunks; workgroup g takes chunks [g*per_wg, (g+1)*per_wg),
+// its waves stride through them. chunks[c] = page | (chunk index within the page) << 32.
+//
+// Per chunk: load the run records (lane r = run r), gather the RLE runs' dictionary
+// entries, stage the page bytes of the chunk's bit-packed values in LDS — all before the
+// first store — then sweep the chunk's tiles: a ballot finds the runs overlapping a tile,
+// each element picks its run in a uniform loop over those runs, one 16-byte store per lane.
+constexpr uint32_t XSEG_BYTES = 2048;  // per-wave LDS for the packed bytes of one chunk
+
+template <int W>
+__global__ __launch_bounds__(64 * WPB) void k_dict_expand(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                          const PageWork* __restrict__ work,
+                                                          const ColumnDev* __restrict__ cols,
+                                                          const uint64_t* __restrict__ rec,
+                                                          const uint32_t* __restrict__ chunk_run,
+                                                          const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                          uint32_t per_wg, uint64_t* err, uint32_t* err_count) {
+  typedef typename DictVal<W>::T T;
+  constexpr uint32_t E = 16 / W;
+  constexpr uint32_t CH = CH_TILES * WAVE * E;
+  __shared__ __attribute__((aligned(16))) uint8_t dict_lds[DICT_LDS_BYTES];
+  __shared__ __attribute__((aligned(16))) uint8_t xseg_all[WPB][XSEG_BYTES];
+  __shared__ __attribute__((aligned(16))) u32x4 rt_all[WPB][WAVE];
+  const uint32_t c_beg = blockIdx.x * per_wg;
+  const uint32_t c_end = c_beg + per_wg < n_chunks ? c_beg + per_wg : n_chunks;
+  if (c_beg >= c_end) return;
+  // stage the dictionary when every chunk of this workgroup reads the same one and it fits
+  const int col0 = work[(uint32_t)chunks[c_beg]].column;
+  const int col1 = work[(uint32_t)chunks[c_end - 1]].column;
+  bool dict_in_lds = false;
+  if (col0 == col1) {
+    const ColumnDev& cd0 = cols[col0];
+    const uint64_t need = (uint64_t)cd0.dict_n * W;
+    dict_in_lds = need <= DICT_LDS_BYTES && need <= cd0.dict_bytes;
+    if (dict_in_lds) {
+      rsrc_t d0 = make_rsrc(bytes + cd0.dict_offset, cd0.dict_bytes);
+      const bool al = (cd0.dict_offset & 3u) == 0;
+      for (uint32_t o = 16u * threadIdx.x; o < (uint32_t)need; o += 16u * 64u * WPB) {
+        u32x4 v;
+        if (al) v = __builtin_amdgcn_raw_buffer_load_b128(d0, (int)o, 0, 0);
+        else v = u32x4{ld4_any(d0, o), ld4_any(d0, o + 4), ld4_any(d0, o + 8), ld4_any(d0, o + 12)};
+        *(u32x4*)(dict_lds + o) = v;
+      }
+    }
+  }
+  __syncthreads();
+  const T* dict_l = (const T*)dict_lds;
+  uint8_t* xseg = xseg_all[wave_id()];
+  u32x4* rt = rt_all[wave_id()];
+  const uint32_t lane = lane_id();
+
+  for (uint32_t c = c_beg + wave_id(); c < c_end; c += WPB) {
+    c = uni(c);
+    const uint64_t cj = chunks[c];
+    const int page = (int)(uint32_t)cj;
+    const uint32_t j = (uint32_t)(cj >> 32);
+    const PageWork& pw = work[page];
+    const uint32_t N = uni(pw.n_ok);
+    const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
+    // output slots of this chunk, and the values they hold
+    const uint32_t s_lo = j * CH > sh ? j * CH : sh;
+    const uint32_t s_hi = (j + 1) * CH < N + sh ? (j + 1) * CH : N + sh;
+    if (s_lo >= s_hi) continue;
+    const uint32_t v_lo = s_lo - sh, v_hi = s_hi - sh;
+    const ColumnDev& cd = cols[pw.column];
+    const bool own_dict = dict_in_lds && pw.column == col0;
+    const uint32_t dict_n = uni(cd.dict_n);
+    rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
+    rsrc_t prs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+    const uint32_t sec_end = uni(pw.size);
+    const uint32_t n_rec = uni(pw.n_rec);
+    const uint32_t db = uni(pw.data_begin);
+    const int w = (int)uni((ld32(prs, db & ~3u) >> ((db & 3u) * 8u)) & 0xFFu);
+    const uint64_t* prec = rec + pw.rec_base;
+    uint32_t k = uni(chunk_run[pw.chunk_base + j]);
+    T* out = (T*)cd.values;
+    T* pal = out + (pw.out_offset - sh) + (uint64_t)j * CH;  // slot j*CH of the page
+    const bool out16 = ((uintptr_t)out & 15u) == 0;
+    auto dict_get = [&](uint32_t id) -> T { return own_dict ? dict_l[id] : load_dict<W>(drs, id); };
+
+    uint32_t b_lo = v_lo;
+    while (true) {
+      k = uni(k);
+      b_lo = uni(b_lo);
+      // records k .. k+63: lane r holds run k + r
+      const bool has = k + lane < n_rec;
+      const uint64_t rr = has ? prec[k + lane] : 0;
+      uint32_t r_start = has ? (uint32_t)rr : 0xFFFFFFFFu;
+      uint32_t r_pl = (uint32_t)(rr >> 32);
+      const uint32_t nxt = k + WAVE < n_rec ? uni((uint32_t)prec[k + WAVE]) : N;
+      const uint32_t r_end_n = __shfl_down(r_start, 1);
+      uint32_t r_end = lane == WAVE - 1 ? nxt : (k + lane + 1 < n_rec ? r_end_n : N);
+      const uint32_t e63 = rdl(r_end, WAVE - 1);
+      const uint32_t b_hi = uni(e63 < v_hi ? e63 : v_hi);  // this batch: values [b_lo, b_hi)
+      const bool live = has && r_start < b_hi && r_end > b_lo;
+      const bool pk = (r_pl & 0x80000000u) != 0;
+      // RLE runs: one dictionary gather per run
+      uint32_t r_lo = 0, r_hi = 0;
+      if (live && !pk) {
+        if (r_pl >= dict_n) {
+          report(err, err_count, page, 2, r_start > b_lo ? r_start : b_lo, PQG_ERR_DICT_ID);
+        } else {
+          const uint64_t x = (uint64_t)dict_get(r_pl);
+          r_lo = (uint32_t)x;
+          r_hi = (uint32_t)(x >> 32);
         }
       }
+      // Every register loaded from global memory is consumed here, before the tile loop:
+      // otherwise the waitcnt pass sees a load possibly pending at the loop head and puts
+      // s_waitcnt vmcnt(0) in front of every store, draining the stores one tile at a time.
+      asm volatile("" : "+v"(r_lo), "+v"(r_hi), "+v"(r_end), "+v"(r_start), "+v"(r_pl));
+      // packed runs: page bytes [x_lo, x_hi) of the values in [b_lo, b_hi), staged in LDS
+      const uint64_t pmask = __ballot(live && pk);
+      uint32_t x_lo = 0;
+      bool x_lds = false;
+      if (pmask) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(pmask), l = 63u - (uint32_t)__builtin_clzll(pmask);
+        const uint32_t fs = rdl(r_start, f), ls = rdl(r_start, l), le = rdl(r_end, l);
+        const uint32_t fa = b_lo > fs ? b_lo : fs, lb = b_hi < le ? b_hi : le;
+        x_lo = uni(((rdl(r_pl, f) & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)(fa - fs) * (uint32_t)w) >> 3)) & ~15u);
+        const uint32_t x_hi =
+            uni((rdl(r_pl, l) & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)(lb - ls) * (uint32_t)w + 7) >> 3) + 8u);
+        x_lds = x_hi - x_lo <= XSEG_BYTES;
+        if (x_lds) {
+#pragma unroll
+          for (uint32_t i = 0; i < XSEG_BYTES; i += 16u * WAVE) {
+            const uint32_t o = i + 16u * lane;
+            if (o < x_hi - x_lo) *(u32x4*)(xseg + o) = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(x_lo + o), 0, 0);
+          }
+          wave_sync();
+        }
+      }
+      // run table of the batch in LDS (16 bytes per run) for the tiles that mix runs
+      rt[lane] = u32x4{r_start, r_pl, r_lo, r_hi};
+      // all loads of this batch are complete here (one wait, before the first store of
+      // the batch); the waitcnt pass then has nothing pending inside the tile loop
+      __builtin_amdgcn_s_waitcnt(0);
+      // tiles of the batch. FAST: dictionary and packed bytes in LDS, so the loop has no
+      // global load — a load there would make every store's data wait for vmcnt(0), i.e.
+      // for all of this wave's stores in flight.
+      auto tiles = [&](auto fast_tag) {
+        constexpr bool FAST = decltype(fast_tag)::value;
+        uint32_t cur_s = 1, cur_e = 0;  // RLE run [cur_s, cur_e) of the previous tile (none)
+        uint32_t cur_lo = 0, cur_hi = 0;
+        const uint32_t t_first = (b_lo + sh) / (WAVE * E) - j * CH_TILES;
+        for (uint32_t t = t_first; t < CH_TILES; t++) {
+          t = uni(t);
+          const uint32_t ts = j * CH + t * WAVE * E;  // first slot of tile t
+          const uint32_t t_lo = ts > sh ? ts - sh : 0;
+          if (t_lo >= b_hi) break;
+          const uint32_t t_hi = ts + WAVE * E - sh;
+          const uint32_t c_lo = t_lo > b_lo ? t_lo : b_lo;  // values of the tile in this batch
+          const uint32_t c_hi = t_hi < b_hi ? t_hi : b_hi;
+          const bool interior = out16 && ts >= sh && c_lo == ts - sh && c_hi == t_hi;
+          const uint32_t i0 = ts + E * lane - sh;  // value index of the lane's first element (wraps below 0)
+          T v[E];
+          cur_s = uni(cur_s);
+          cur_e = uni(cur_e);
+          if (!(c_lo >= cur_s && c_hi <= cur_e)) {
+            // the run holding the tile's first value
+            const uint64_t m = __ballot(live && r_start <= c_lo && r_end > c_lo);
+            const uint32_t r = (uint32_t)__builtin_ctzll(m);
+            if (!(rdl(r_pl, r) & 0x80000000u)) {
+              cur_s = rdl(r_start, r);
+              cur_e = rdl(r_end, r);
+              cur_lo = rdl(r_lo, r);
+              cur_hi = rdl(r_hi, r);
+            } else {
+              cur_s = 1;
+              cur_e = 0;
+            }
+          }
+          if (c_lo >= cur_s && c_hi <= cur_e) {
+            // one RLE run covers the tile
+#pragma unroll
+            for (uint32_t e = 0; e < E; e++) v[e] = (T)(((uint64_t)cur_hi << 32) | cur_lo);
+          } else {
+            // mixed tile: element i takes run ra + #{runs r in (ra, rb] with start <= i}
+            const uint64_t ov = __ballot(live && r_start < c_hi && r_end > c_lo);
+            uint32_t idx[E];
+#pragma unroll
+            for (uint32_t e = 0; e < E; e++) idx[e] = (uint32_t)__builtin_ctzll(ov);
+            for (uint64_t m = ov & (ov - 1); m; m &= m - 1) {
+              const uint32_t s0 = rdl(r_start, (uint32_t)__builtin_ctzll(m));
+#pragma unroll
+              for (uint32_t e = 0; e < E; e++) idx[e] += i0 + e >= s0 ? 1u : 0u;
+            }
+#pragma unroll
+            for (uint32_t e = 0; e < E; e++) {
+              const u32x4 q = rt[idx[e]];
+              T x = (T)(((uint64_t)q.w << 32) | q.z);
+              const uint32_t i = i0 + e;
+              if ((q.y & 0x80000000u) && i >= c_lo && i < c_hi) {
+                // packed element: LSB-first bits at (i - run start) * w from the run's data start
+                const uint64_t bit = (uint64_t)(i - q.x) * (uint32_t)w;
+                const uint32_t byte = (q.y & 0x7FFFFFFFu) + (uint32_t)(bit >> 3);
+                const uint32_t a = byte & ~3u;
+                uint64_t y;
+                if (FAST || x_lds)
+                  y = (uint64_t)*(const uint32_t*)(xseg + (a - x_lo)) |
+                      ((uint64_t)*(const uint32_t*)(xseg + (a - x_lo) + 4) << 32);
+                else
+                  y = (uint64_t)ld32(prs, a) | ((uint64_t)ld32(prs, a + 4) << 32);
+                if (a + 8u > sec_end) {  // truncated final group: bytes past the section are 0 (:96-99)
+                  const int64_t keep = (int64_t)sec_end - (int64_t)a;
+                  y = keep <= 0 ? 0 : (y & ((1ull << (8 * keep)) - 1ull));
+                }
+                y >>= (byte - a) * 8u + (uint32_t)(bit & 7u);
+                const uint32_t id = w == 0 ? 0 : (w == 32 ? (uint32_t)y : (uint32_t)y & ((1u << w) - 1u));
+                x = 0;
+                if (id >= dict_n) report(err, err_count, page, 2, i, PQG_ERR_DICT_ID);
+                else x = FAST ? dict_l[id] : dict_get(id);
+              }
+              v[e] = x;
+            }
+          }
+          T* tp = pal + t * WAVE * E + E * lane;
+          if (interior) {
+            if constexpr (W == 8) {
+              typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+              gst_nt((v2*)tp, v2{v[0], v[1]});
+            } else {
+              gst_nt((u32x4*)tp, u32x4{v[0], v[1], v[2], v[3]});
+            }
+          } else {
+#pragma unroll
+            for (uint32_t e = 0; e < E; e++)
+              if (i0 + e >= c_lo && i0 + e < c_hi) gst(tp + e, v[e]);
+          }
+        }
+      };
+      if (own_dict && (x_lds || !pmask)) tiles(std::true_type{});
+      else tiles(std::false_type{});
+      if (b_hi >= v_hi) break;
+      k += WAVE;
+      b_lo = b_hi;
     }
-    (void)first;
-    DIAG_ADD(d_exp, t_e);
   }
-#ifdef PQG_DIAG
-  if (lane == 0 && pqg_diag_buf) {
-    uint64_t* d = pqg_diag_buf + 8 * (uint64_t)page;
-    d[0] = d_start;
-    d[1] = __builtin_amdgcn_s_memrealtime();
-    d[2] = d_walk;
-    d[3] = d_stage;
-    d[4] = d_exp;
-    d[5] = d_nb;
-    uint32_t xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    uint32_t hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    d[6] = ((uint64_t)xcc << 32) | hw;
-    d[7] = blockIdx.x;
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1347,10 +1520,23 @@ namespace pqg {
 #define PQG_LAUNCH_ARGS bytes, n_bytes, work, cols, list, n, err, err_count
 
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                       const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+                       const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
+                       const uint64_t* chunks, uint32_t n_chunks, uint64_t* err, uint32_t* err_count) {
   if (n <= 0) return hipSuccess;
-  if (width == 8) hipLaunchKernelGGL(k_dict<8>, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
-  else hipLaunchKernelGGL(k_dict<4>, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
+  hipLaunchKernelGGL(k_dict_runs, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, list, n,
+                     rec, chunk_run, err, err_count);
+  if (n_chunks == 0) return hipGetLastError();
+  // persistent expansion grid: about 8 workgroups per CU, contiguous chunk ranges
+  const uint32_t max_wg = 2048;
+  uint32_t per_wg = (n_chunks + max_wg - 1) / max_wg;
+  if (per_wg < WPB) per_wg = WPB;
+  const uint32_t n_wg = (n_chunks + per_wg - 1) / per_wg;
+  if (width == 8)
+    hipLaunchKernelGGL(k_dict_expand<8>, dim3(n_wg), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, rec, chunk_run,
+                       chunks, n_chunks, per_wg, err, err_count);
+  else
+    hipLaunchKernelGGL(k_dict_expand<4>, dim3(n_wg), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, rec, chunk_run,
+                       chunks, n_chunks, per_wg, err, err_count);
   return hipGetLastError();
 }
 

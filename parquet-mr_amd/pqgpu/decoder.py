@@ -83,7 +83,11 @@ class Plan:
 
 
 class Decoder:
-    def __init__(self, device=0, stream=None):
+    def __init__(self, device=0, stream=None, poison=None):
+        """poison: byte value written over freshly allocated output columns (tests use it so an
+        element the kernels never write, or write twice with different values, cannot pass by
+        reusing memory that already holds the right answer)."""
+        self.poison = poison
         L = native.lib()
         if L.pqg_device_count() <= 0:
             raise native.PqgError(abi.ERR_NO_DEVICE, what="no HIP device")
@@ -121,6 +125,10 @@ class Decoder:
             vals = torch.empty(max(n * w, 16), dtype=torch.uint8, device=self.device)
             dl = torch.zeros(max(n, 1), dtype=torch.uint8, device=self.device) if cd["max_def"] > 0 else None
             rl = torch.zeros(max(n, 1), dtype=torch.uint8, device=self.device) if cd["max_rep"] > 0 else None
+            if self.poison is not None:
+                for t in (vals, dl, rl):
+                    if t is not None:
+                        t.fill_(self.poison)
             cols.append(DeviceColumn(cd["physical_type"], vals, dl, rl, cd["type_length"]))
         return cols
 

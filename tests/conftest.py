@@ -34,6 +34,6 @@ def pytest_collection_modifyitems(config, items):
 @pytest.fixture(scope="session")
 def decoder():
     from pqgpu import decoder as D
-    dec = D.Decoder(0)
+    dec = D.Decoder(0, poison=0xA5)  # unwritten output elements show up as 0xA5A5...
     yield dec
     dec.close()
