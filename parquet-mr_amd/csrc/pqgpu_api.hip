@@ -200,7 +200,8 @@ int pqg_ctx_destroy(pqg_ctx* c) {
 int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, const pqg_column_desc* cols, int n_cols,
                     const pqg_page_desc* pages, int n_pages, pqg_plan** out, pqg_status* st) {
   if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
-  if (!ctx || !out || n_cols < 0 || n_pages < 0 || (n_cols && !cols) || (n_pages && !pages) || (n_bytes && !d_bytes)) {
+  if (!ctx || !out || n_cols < 0 || n_pages < 0 || (n_cols && !cols) || (n_pages && !pages) || (n_bytes && !d_bytes) ||
+      ((uintptr_t)d_bytes & 3u)) {  // the batch buffer is read as dwords (scalar loads): 4-byte aligned
     set_status(st, PQG_ERR_INVALID_ARG, -1, -1, "plan arguments");
     return PQG_ERR_INVALID_ARG;
   }
@@ -387,7 +388,7 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
             P->col_page_start.ensure(sizeof(int32_t) * cps.size()) == hipSuccess &&
             P->err.ensure(sizeof(uint64_t) * 3 * (size_t)std::max(n_pages, 1)) == hipSuccess &&
             P->err_count.ensure(sizeof(uint32_t) * 4) == hipSuccess &&
-            P->rec.ensure(sizeof(uint64_t) * std::max<uint64_t>(rec_total, 1)) == hipSuccess &&
+            P->rec.ensure(sizeof(uint64_t) * (rec_total + 16)) == hipSuccess &&  // k_dict_fill reads 9 ahead
             P->chunk_run.ensure(sizeof(uint32_t) * std::max<uint32_t>(chunk_total, 1)) == hipSuccess &&
             P->chunks.ensure(sizeof(uint64_t) * std::max<size_t>(chunk_list.size(), 1)) == hipSuccess;
   if (!chunk_list.empty())

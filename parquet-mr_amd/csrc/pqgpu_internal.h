@@ -48,7 +48,7 @@ struct PageWork {
 
 // Output chunk of k_dict_expand: CH_TILES x 64 lanes x 16 bytes.
 #ifndef PQG_CHUNK_TILES
-#define PQG_CHUNK_TILES 8
+#define PQG_CHUNK_TILES 16
 #endif
 constexpr uint32_t DICT_CHUNK_TILES = PQG_CHUNK_TILES;
 inline uint32_t dict_chunk_values(int elem_width) { return DICT_CHUNK_TILES * 64u * (16u / (uint32_t)elem_width); }

@@ -245,7 +245,7 @@ struct PreWin {
   uint32_t flg;        // byte b: bit0 packed, bit1 slow path, bits 2..4 header length
 };
 
-constexpr uint32_t SEG_BYTES = 4096;   // LDS page segment per wave of k_dict_runs (5 workgroups per CU)
+constexpr uint32_t SEG_BYTES = 3072;   // LDS page segment per wave of k_dict_runs (5 workgroups per CU)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -270,8 +270,12 @@ __device__ __forceinline__ bool seg_has(const PreWin& pw, uint32_t a, uint32_t n
   return pw.seg && a >= pw.seg_lo && a + n <= pw.seg_lo + SEG_BYTES;
 }
 
+// LDS byte buffers are written as u32x4 and read as u32: may_alias keeps TBAA from
+// reordering the two.
+typedef uint32_t __attribute__((may_alias)) u32_alias;
+
 __device__ __forceinline__ uint32_t seg32(const PreWin& pw, uint32_t a) {  // a 4-aligned, inside
-  return *(const uint32_t*)(pw.seg + (a - pw.seg_lo));
+  return *(const u32_alias*)(pw.seg + (a - pw.seg_lo));
 }
 
 // LDS_ONLY: the caller guarantees the whole section is in the segment (no refill,
@@ -634,10 +638,42 @@ constexpr uint32_t CH_TILES = DICT_CHUNK_TILES;
 
 __device__ __forceinline__ uint32_t chunk_values(uint32_t E) { return CH_TILES * WAVE * E; }
 
-template <bool SMALL>
+// Bit-packed runs of a dictionary page can be expanded by the walking wave itself (the page
+// bytes are in its LDS segment): lanes unpack one element each and gather the dictionary.
+// Off by default: k_dict_tiles writes whole 1 KB tiles (full cache lines) instead.
+constexpr bool PACKED_IN_WALK = false;
+template <int W>
+struct PackedSink {
+  typedef typename DictVal<W>::T T;
+  T* out;             // value 0 of the page
+  const T* dict_l;    // LDS dictionary (when dict_in_lds)
+  bool dict_in_lds;
+  rsrc_t drs;         // dictionary page bytes
+  uint32_t dict_n;
+  uint32_t sec_end;
+  int w;
+  int page;
+  uint64_t* err;
+  uint32_t* err_count;
+
+  // values [s_abs, s_abs + cnt) from packed data starting at page byte d0
+  template <bool LDS_ONLY>
+  __device__ __forceinline__ void put(const PreWin& win, uint32_t d0, uint32_t s_abs, uint32_t cnt) const {
+    for (uint32_t i = lane_id(); i < cnt; i += WAVE) {
+      const uint32_t id = packed_elem_w<LDS_ONLY>(win, d0, sec_end, i, w);
+      T x = 0;
+      if (id >= dict_n) report(err, err_count, page, 2, s_abs + i, PQG_ERR_DICT_ID);
+      else x = dict_in_lds ? dict_l[id] : load_dict<W>(drs, id);
+      gst(out + s_abs + i, x);
+    }
+  }
+};
+
+template <int W, bool SMALL>
 __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg, uint32_t sec_end,
                                           int w, uint64_t* rec, uint32_t* chunk_run, uint32_t CH, uint32_t sh, int page,
-                                          uint64_t* err, uint32_t* err_count, uint32_t& n_rec, uint32_t& n_ok) {
+                                          uint64_t* err, uint32_t* err_count, uint32_t& n_rec, uint32_t& n_ok,
+                                          const PackedSink<W>& ps) {
   const uint32_t lane = lane_id();
   uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
   uint32_t produced = 0;       // values covered by the runs read so far
@@ -732,7 +768,213 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
       uint32_t j = r_start == 0 ? 0 : (r_start + sh + CH - 1) / CH;
       for (; j * CH < r_end + sh; j++) gst(chunk_run + j, k + lane);
     }
+    for (uint64_t m = __ballot(lane < nrun && (r_pl & 0x80000000u)); m; m &= m - 1) {
+      const uint32_t r = (uint32_t)__builtin_ctzll(m);
+      const uint32_t s0 = rdl(r_start, r), e0 = rdl(lane + 1 < nrun ? r_end_n : produced, r);
+      if constexpr (PACKED_IN_WALK) ps.template put<SMALL>(win, rdl(r_pl, r) & 0x7FFFFFFFu, s0, e0 - s0);
+    }
     k += nrun;
+  }
+  n_rec = k;
+  n_ok = N;
+}
+
+// Pointer-jumping walk (SMALL pages: the whole data section sits in the LDS segment).
+//
+// The serial part of the hybrid decoder — each header's position depends on the previous
+// header — is replaced per 256-byte window by list ranking: every position p of the window
+// gets its successor J(p) (the next header position if a run header started at p; 256 if it
+// leaves the window or needs the scalar slow path), and 8 rounds of pointer doubling mark
+// the positions reachable from the chain start. The marked positions, in order, are the
+// window's runs; a saturating prefix sum of their counts gives each run's first value.
+// Cost per window is fixed (~8 LDS round trips) instead of one round trip per run.
+template <int W>
+__device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg,
+                                             uint32_t sec_end, int w, uint64_t* rec, uint32_t* chunk_run,
+                                             uint32_t CH, uint32_t sh, int page, uint64_t* err, uint32_t* err_count,
+                                             uint32_t& n_rec, uint32_t& n_ok, const PackedSink<W>& ps) {
+  const uint32_t lane = lane_id();
+  // successor table (256 x u16) and reached flags (256 x u8) over L.ent; every access goes
+  // through may_alias types (u16 gathers vs u64 row writes must not be reordered)
+  typedef uint16_t __attribute__((may_alias)) u16a;
+  typedef uint32_t __attribute__((may_alias)) u32a;
+  typedef uint64_t __attribute__((may_alias)) u64a;
+  u16a* Jt = (u16a*)L.ent;
+  uint8_t* Rt = (uint8_t*)L.ent + 512;
+  uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
+  uint32_t produced = 0, k = 0;
+  int code = 0;
+  // one record at lane 0 (the scalar slow path) and the chunk entries it owns
+  auto put_record = [&](uint32_t start, uint32_t end, uint32_t payload) {
+    if (lane == 0) {
+      gst(rec + k, (uint64_t)start | ((uint64_t)payload << 32));
+      uint32_t j = start == 0 ? 0 : (start + sh + CH - 1) / CH;
+      for (; j * CH < end + sh; j++) gst(chunk_run + j, k);
+    }
+    k++;
+  };
+  while (true) {
+    pos = uni(pos);
+    produced = uni(produced);
+    k = uni(k);
+    if (produced >= N) break;
+    if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
+    const uint32_t B = pos & ~3u;
+    predecode<true>(win, B, w);
+    // successors of this lane's 4 positions
+    uint32_t jv[4], nn[4], slowm = 0, inm = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const uint32_t p = B + 4u * lane + b;
+      const uint32_t f = (win.flg >> (8u * b)) & 0xFFu;
+      const uint32_t hl = f >> 2;
+      const uint32_t nx = win.nxt[b];
+      const bool in = p < sec_end;
+      // slow: long varints, 0 / huge group counts, a header or RLE value crossing the end
+      const bool slow = in && ((f & 2u) || p + hl > sec_end || (!(f & 1u) && nx > sec_end));
+      nn[b] = (f & 1u) ? (nx < sec_end ? nx : sec_end) : nx;  // packed: readFully of what is left
+      jv[b] = (!in || slow || nn[b] - B >= 256u) ? 256u : nn[b] - B;
+      slowm |= (slow ? 1u : 0u) << b;
+      inm |= (in ? 1u : 0u) << b;
+    }
+    const uint32_t s0 = pos - B;
+    *(u64a*)(Jt + 4u * lane) =
+        (uint64_t)jv[0] | ((uint64_t)jv[1] << 16) | ((uint64_t)jv[2] << 32) | ((uint64_t)jv[3] << 48);
+    *(u32a*)(Rt + 4u * lane) = (4u * lane <= s0 && s0 < 4u * lane + 4u) ? (1u << (8u * (s0 & 3u))) : 0u;
+    // pointer doubling: after round r the positions reached within 2^(r+1) steps are marked
+#pragma unroll 1
+    for (int r = 0; r < 8; r++) {
+      const uint32_t r4 = *(const u32a*)(Rt + 4u * lane);
+      uint32_t jn[4];
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++) {
+        if (((r4 >> (8u * b)) & 1u) && jv[b] < 256u) Rt[jv[b]] = 1;
+        jn[b] = jv[b] < 256u ? Jt[jv[b]] : 256u;
+      }
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++) jv[b] = jn[b];
+      *(u64a*)(Jt + 4u * lane) =
+          (uint64_t)jv[0] | ((uint64_t)jv[1] << 16) | ((uint64_t)jv[2] << 32) | ((uint64_t)jv[3] << 48);
+      // done when no marked position can still reach further (all its jumps are terminal);
+      // positions marked in this round have not been examined yet, so look at them too
+      const uint32_t r4n = *(const u32a*)(Rt + 4u * lane);
+      bool more = false;
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++) more |= ((r4n >> (8u * b)) & 1u) && jv[b] < 256u;
+      if (!__ballot(more)) break;
+    }
+    const uint32_t r4 = *(const u32a*)(Rt + 4u * lane);
+    uint32_t mk = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) mk |= ((r4 >> (8u * b)) & 1u) << b;
+    // last chain position of the window (its successor is terminal)
+    uint32_t q_last = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const uint64_t m = __ballot((mk >> b) & 1u);
+      if (m) {
+        const uint32_t q = 4u * (63u - (uint32_t)__builtin_clzll(m)) + b;
+        q_last = q > q_last ? q : q_last;
+      }
+    }
+    q_last = uni(q_last);
+    // runs of the window: marked, inside the section, fast-path headers
+    const uint32_t cap = N - produced;
+    uint32_t cc[4], lsum = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const bool v = ((mk & inm & ~slowm) >> b) & 1u;
+      const bool pk = (win.flg >> (8u * b)) & 1u;
+      uint32_t c = win.cnt[b];
+      if (!pk && c == 0) c = cap;  // Java: currentCount goes negative, the value repeats forever
+      c = v ? (c < cap ? c : cap) : 0u;
+      cc[b] = c;
+      lsum = lsum + c < cap ? lsum + c : cap;
+    }
+    // saturating inclusive scan of the lane sums
+    uint32_t inc = lsum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if ((int)lane >= o) inc = inc + y < cap ? inc + y : cap;
+    }
+    uint32_t st = __shfl_up(inc, 1);
+    if (lane == 0) st = 0;
+    const uint32_t total = uni(rdl(inc, WAVE - 1));
+    // record index of each emitted run (emitted: a run that starts before the cap)
+    uint32_t em = 0, stb[4];
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      stb[b] = st;
+      if (cc[b] && st < cap) em |= 1u << b;
+      st = st + cc[b] < cap ? st + cc[b] : cap;
+    }
+    uint32_t base = 0, n_em = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const uint64_t m = __ballot((em >> b) & 1u);
+      base += (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+      n_em += (uint32_t)__builtin_popcountll(m);
+    }
+    uint32_t idx = base;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      if ((em >> b) & 1u) {
+        const bool pk = (win.flg >> (8u * b)) & 1u;
+        const uint32_t vv = win.val[b];
+        const uint32_t payload = pk ? (0x80000000u | vv) : (vv > 0x7FFFFFFFu ? 0x7FFFFFFFu : vv);
+        const uint32_t s_abs = produced + stb[b];
+        const uint32_t e_abs = produced + (stb[b] + cc[b] < cap ? stb[b] + cc[b] : cap);
+        gst(rec + k + idx, (uint64_t)s_abs | ((uint64_t)payload << 32));
+        uint32_t j = s_abs == 0 ? 0 : (s_abs + sh + CH - 1) / CH;
+        for (; j * CH < e_abs + sh; j++) gst(chunk_run + j, k + idx);
+        idx++;
+      }
+    }
+    // bit-packed runs of the window, one at a time across the wave
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const bool pk = (win.flg >> (8u * b)) & 1u;
+      for (uint64_t m = __ballot(((em >> b) & 1u) && pk); m; m &= m - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        const uint32_t s_rel = rdl(stb[b], l);
+        const uint32_t e_rel = rdl(stb[b] + cc[b] < cap ? stb[b] + cc[b] : cap, l);
+        if constexpr (PACKED_IN_WALK) ps.template put<true>(win, rdl(win.val[b], l), produced + s_rel, e_rel - s_rel);
+      }
+    }
+    k += uni(n_em);
+    produced += total;
+    if (produced >= N) break;
+    // continue after the window's last chain position
+    const uint32_t ql = q_last >> 2, qb = q_last & 3u;
+    const uint32_t q_slow = (rdl(slowm, ql) >> qb) & 1u;
+    const uint32_t q_in = (rdl(inm, ql) >> qb) & 1u;
+    if (!q_in) {
+      pos = B + q_last;  // at or past the section end: RLE_PAST_END on the next iteration
+    } else if (!q_slow) {
+      pos = pick4(nn, qb, ql);  // leaves the window
+    } else {
+      // scalar re-decode of the header at q_last (readNext :80-109)
+      pos = B + q_last;
+      uint32_t hl, m, nxs, vv;
+      uint64_t cnt64;
+      code = slow_header_g([&](uint32_t p) { return uni((seg32(win, p & ~3u) >> ((p & 3u) * 8u)) & 0xFFu); }, pos,
+                           sec_end, w, hl, m, cnt64, vv, nxs);
+      if (code) break;
+      if (m == 0 && nxs > sec_end) { code = PQG_ERR_EOF; break; }
+      uint64_t cnt = cnt64;
+      const uint32_t left = N - produced;
+      if (m == 0 && cnt == 0) cnt = left;
+      const uint32_t take = cnt < left ? (uint32_t)cnt : left;
+      put_record(produced, produced + take, m ? (0x80000000u | vv) : (vv > 0x7FFFFFFFu ? 0x7FFFFFFFu : vv));
+      if constexpr (PACKED_IN_WALK) if (m) ps.template put<true>(win, vv, produced, take);
+      produced += take;
+      pos = m ? (nxs < sec_end ? nxs : sec_end) : nxs;
+    }
+  }
+  if (code) {
+    if (lane == 0) report(err, err_count, page, 2, produced, code);
+    N = produced;
   }
   n_rec = k;
   n_ok = N;
@@ -743,20 +985,50 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
 // :80-109). The page section is staged in LDS; a 256-byte window is pre-decoded in parallel
 // (every lane parses a run header at each of its 4 byte positions) into LDS tables, and the
 // serial chain is one ds_read_b64 + ds_read_b32 per run.
+template <int W>
 __global__ __launch_bounds__(64 * WPB) void k_dict_runs(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                         PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                         const int32_t* __restrict__ list, int n_list, uint64_t* rec,
                                                         uint32_t* chunk_run, uint64_t* err, uint32_t* err_count) {
+  typedef typename DictVal<W>::T T;
+  __shared__ __attribute__((aligned(16))) uint8_t dict_lds[PACKED_IN_WALK ? DICT_LDS_BYTES : 16];
   __shared__ __attribute__((aligned(16))) DictWaveLds wl_all[WPB];
+  int* wg_col = (int*)dict_lds;  // scratch before the dictionary is staged
   DictWaveLds& L = wl_all[wave_id()];
   const int page = wave_page(list, n_list);
-  if (page < 0) return;
   const uint32_t lane = lane_id();
+  // the workgroup's dictionary in LDS when its pages share one that fits (packed values)
+  if (lane == 0) wg_col[wave_id()] = page >= 0 ? work[page].column : -1;
+  __syncthreads();
+  int c0 = -1;
+  bool same = true;
+#pragma unroll
+  for (int q = 0; q < WPB; q++) {
+    const int c = wg_col[q];
+    if (c >= 0) {
+      if (c0 < 0) c0 = c;
+      else if (c != c0) same = false;
+    }
+  }
+  bool dict_in_lds = false;
+  __syncthreads();  // wg_col read by every wave before the dictionary overwrites it
+  if (PACKED_IN_WALK && same && c0 >= 0) {
+    const ColumnDev& cd0 = cols[c0];
+    const uint64_t need = (uint64_t)cd0.dict_n * W;
+    dict_in_lds = need <= DICT_LDS_BYTES && need <= cd0.dict_bytes;
+    if (dict_in_lds) {
+      rsrc_t d0 = make_rsrc(bytes + cd0.dict_offset, cd0.dict_bytes);
+      for (uint32_t o = 16u * threadIdx.x; o < (uint32_t)need; o += 16u * 64u * WPB)
+        *(u32x4*)(dict_lds + o) = u32x4{ld4_any(d0, o), ld4_any(d0, o + 4), ld4_any(d0, o + 8), ld4_any(d0, o + 12)};
+    }
+  }
+  __syncthreads();
+  if (page < 0) return;
   const PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
   uint32_t N = uni(pw.n_values);
   const uint32_t sec_beg = uni(pw.data_begin), sec_end = uni(pw.size);
-  const uint32_t E = 16u / (uint32_t)cd.elem_width;
+  constexpr uint32_t E = 16u / W;
   const uint32_t CH = chunk_values(E);
   const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
   uint32_t n_rec = 0, n_ok = 0;
@@ -775,11 +1047,27 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_runs(const uint8_t* __restric
       } else {
         uint64_t* prec = rec + pw.rec_base;
         uint32_t* pcr = chunk_run + pw.chunk_base;
+        PackedSink<W> ps;
+        ps.out = (T*)cd.values + pw.out_offset;
+        ps.dict_l = (const T*)dict_lds;
+        ps.dict_in_lds = dict_in_lds && pw.column == c0;
+        ps.drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
+        ps.dict_n = uni(cd.dict_n);
+        ps.sec_end = sec_end;
+        ps.w = (int)bw;
+        ps.page = page;
+        ps.err = err;
+        ps.err_count = err_count;
         // SMALL: the whole data section sits in the LDS segment: the walk has no global load
-        if (sec_end - win.seg_lo <= SEG_BYTES)
-          dict_walk<true>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
+        if (sec_end - win.seg_lo + 264u <= SEG_BYTES)  // every window inside the segment
+          dict_walk_pj<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok,
+                          ps);
+        else if (sec_end - win.seg_lo <= SEG_BYTES)
+          dict_walk<W, true>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec,
+                             n_ok, ps);
         else
-          dict_walk<false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
+          dict_walk<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec,
+                              n_ok, ps);
       }
     }
   }
@@ -789,245 +1077,278 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_runs(const uint8_t* __restric
   }
 }
 
-// Persistent grid over output chunks; workgroup g takes chunks [g*per_wg, (g+1)*per_wg),
-// its waves stride through them. chunks[c] = page | (chunk index within the page) << 32.
-//
-// Per chunk: load the run records (lane r = run r), gather the RLE runs' dictionary
-// entries, stage the page bytes of the chunk's bit-packed values in LDS — all before the
-// first store — then sweep the chunk's tiles: a ballot finds the runs overlapping a tile,
-// each element picks its run in a uniform loop over those runs, one 16-byte store per lane.
-constexpr uint32_t XSEG_BYTES = 2048;  // per-wave LDS for the packed bytes of one chunk
+// RLE runs of dictionary pages: one wave per output chunk (CH_TILES x 64 lanes x 16 bytes).
+// Everything the fill needs — chunk and page descriptors, run records, dictionary entries —
+// comes through scalar loads (s_load: lgkmcnt only), so no store of the wave is ever waited
+// on: the kernel is a memset driven by run records. Bit-packed runs were written by
+// k_dict_runs (they need the page bytes, which it has in LDS).
+template <int W>
+__device__ __forceinline__ typename DictVal<W>::T sload_dict(const uint32_t* __restrict__ words, uint64_t dict_offset,
+                                                             uint32_t id) {
+  // dictionary entry id through scalar loads, any byte alignment of the dictionary page:
+  // aligned dwords of the (16-byte aligned) batch buffer + v_alignbyte
+  const uint64_t o = dict_offset + (uint64_t)id * W;
+  const uint32_t* p = words + (o >> 2);
+  const uint32_t sb = (uint32_t)(o & 3u);
+  if constexpr (W == 8) {
+    const uint32_t w0 = p[0], w1 = p[1], w2 = sb ? p[2] : 0u;  // no read past the entry when aligned
+    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sb) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sb) << 32);
+  } else {
+    const uint32_t w0 = p[0], w1 = sb ? p[1] : 0u;
+    return __builtin_amdgcn_alignbyte(w1, w0, sb);
+  }
+}
 
 template <int W>
-__global__ __launch_bounds__(64 * WPB) void k_dict_expand(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                                          const PageWork* __restrict__ work,
-                                                          const ColumnDev* __restrict__ cols,
-                                                          const uint64_t* __restrict__ rec,
-                                                          const uint32_t* __restrict__ chunk_run,
-                                                          const uint64_t* __restrict__ chunks, uint32_t n_chunks,
-                                                          uint32_t per_wg, uint64_t* err, uint32_t* err_count) {
+__device__ __forceinline__ typename DictVal<W>::T dict_get_g(bool in_lds, const typename DictVal<W>::T* dict_l,
+                                                             rsrc_t drs, uint32_t id) {
+  return in_lds ? dict_l[id] : load_dict<W>(drs, id);
+}
+
+// One wave per output chunk (CH_TILES tiles of 64 lanes x 16 bytes, i.e. full 1 KB lines).
+//
+//   load phase  run records of the chunk -> LDS run table {start, payload, value}, RLE
+//               values gathered from the dictionary, page bytes of the bit-packed runs ->
+//               LDS. Vector loads happen only here, before the wave's first store (on CDNA
+//               vmcnt counts stores: a load after stores would wait for all of them).
+//   tile sweep  every lane tracks the run holding its element: per tile it advances past
+//               the run starts it crossed (usually none), reads the value (RLE) or unpacks
+//               the id and gathers (packed), and the wave stores one full 1 KB tile.
+constexpr uint32_t XT_RUNS = 128;   // run table entries per wave
+constexpr uint32_t XT_SEG = 2560;   // LDS bytes for the packed data of one round
+
+template <int W>
+__global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                         const PageWork* __restrict__ work,
+                                                         const ColumnDev* __restrict__ cols,
+                                                         const uint64_t* __restrict__ rec,
+                                                         const uint32_t* __restrict__ chunk_run,
+                                                         const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                         uint64_t* err, uint32_t* err_count) {
   typedef typename DictVal<W>::T T;
   constexpr uint32_t E = 16 / W;
-  constexpr uint32_t CH = CH_TILES * WAVE * E;
+  constexpr uint32_t TV = WAVE * E;  // values per tile
+  constexpr uint32_t CH = CH_TILES * TV;
   __shared__ __attribute__((aligned(16))) uint8_t dict_lds[DICT_LDS_BYTES];
-  __shared__ __attribute__((aligned(16))) uint8_t xseg_all[WPB][XSEG_BYTES];
-  __shared__ __attribute__((aligned(16))) u32x4 rt_all[WPB][WAVE];
-  const uint32_t c_beg = blockIdx.x * per_wg;
-  const uint32_t c_end = c_beg + per_wg < n_chunks ? c_beg + per_wg : n_chunks;
-  if (c_beg >= c_end) return;
-  // stage the dictionary when every chunk of this workgroup reads the same one and it fits
-  const int col0 = work[(uint32_t)chunks[c_beg]].column;
-  const int col1 = work[(uint32_t)chunks[c_end - 1]].column;
+  __shared__ __attribute__((aligned(16))) u32x4 tab_all[WPB][XT_RUNS];
+  __shared__ __attribute__((aligned(16))) uint8_t xseg_all[WPB][XT_SEG];
+  const uint32_t lane = lane_id();
+  const uint32_t c = blockIdx.x * WPB + wave_id();
+  const int page = c < n_chunks ? (int)(uint32_t)chunks[c] : -1;
+  // the workgroup's dictionary in LDS when its chunks share one that fits
+  int* wg_col = (int*)dict_lds;
+  if (lane == 0) wg_col[wave_id()] = page >= 0 ? work[page].column : -1;
+  __syncthreads();
+  int c0 = -1;
+  bool same = true;
+#pragma unroll
+  for (int q = 0; q < WPB; q++) {
+    const int cq = wg_col[q];
+    if (cq >= 0) {
+      if (c0 < 0) c0 = cq;
+      else if (cq != c0) same = false;
+    }
+  }
+  __syncthreads();
   bool dict_in_lds = false;
-  if (col0 == col1) {
-    const ColumnDev& cd0 = cols[col0];
+  if (same && c0 >= 0) {
+    const ColumnDev& cd0 = cols[c0];
     const uint64_t need = (uint64_t)cd0.dict_n * W;
     dict_in_lds = need <= DICT_LDS_BYTES && need <= cd0.dict_bytes;
     if (dict_in_lds) {
       rsrc_t d0 = make_rsrc(bytes + cd0.dict_offset, cd0.dict_bytes);
-      const bool al = (cd0.dict_offset & 3u) == 0;
-      for (uint32_t o = 16u * threadIdx.x; o < (uint32_t)need; o += 16u * 64u * WPB) {
-        u32x4 v;
-        if (al) v = __builtin_amdgcn_raw_buffer_load_b128(d0, (int)o, 0, 0);
-        else v = u32x4{ld4_any(d0, o), ld4_any(d0, o + 4), ld4_any(d0, o + 8), ld4_any(d0, o + 12)};
-        *(u32x4*)(dict_lds + o) = v;
-      }
+      for (uint32_t o = 16u * threadIdx.x; o < (uint32_t)need; o += 16u * 64u * WPB)
+        *(u32x4*)(dict_lds + o) = u32x4{ld4_any(d0, o), ld4_any(d0, o + 4), ld4_any(d0, o + 8), ld4_any(d0, o + 12)};
     }
   }
   __syncthreads();
+  if (page < 0) return;
   const T* dict_l = (const T*)dict_lds;
+  u32x4* tab = tab_all[wave_id()];
   uint8_t* xseg = xseg_all[wave_id()];
-  u32x4* rt = rt_all[wave_id()];
-  const uint32_t lane = lane_id();
 
-  for (uint32_t c = c_beg + wave_id(); c < c_end; c += WPB) {
-    c = uni(c);
-    const uint64_t cj = chunks[c];
-    const int page = (int)(uint32_t)cj;
-    const uint32_t j = (uint32_t)(cj >> 32);
-    const PageWork& pw = work[page];
-    const uint32_t N = uni(pw.n_ok);
-    const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
-    // output slots of this chunk, and the values they hold
-    const uint32_t s_lo = j * CH > sh ? j * CH : sh;
-    const uint32_t s_hi = (j + 1) * CH < N + sh ? (j + 1) * CH : N + sh;
-    if (s_lo >= s_hi) continue;
-    const uint32_t v_lo = s_lo - sh, v_hi = s_hi - sh;
-    const ColumnDev& cd = cols[pw.column];
-    const bool own_dict = dict_in_lds && pw.column == col0;
-    const uint32_t dict_n = uni(cd.dict_n);
-    rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
-    rsrc_t prs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
-    const uint32_t sec_end = uni(pw.size);
-    const uint32_t n_rec = uni(pw.n_rec);
-    const uint32_t db = uni(pw.data_begin);
-    const int w = (int)uni((ld32(prs, db & ~3u) >> ((db & 3u) * 8u)) & 0xFFu);
-    const uint64_t* prec = rec + pw.rec_base;
-    uint32_t k = uni(chunk_run[pw.chunk_base + j]);
-    T* out = (T*)cd.values;
-    T* pal = out + (pw.out_offset - sh) + (uint64_t)j * CH;  // slot j*CH of the page
-    const bool out16 = ((uintptr_t)out & 15u) == 0;
-    auto dict_get = [&](uint32_t id) -> T { return own_dict ? dict_l[id] : load_dict<W>(drs, id); };
+  const uint32_t j = (uint32_t)(chunks[c] >> 32);
+  const PageWork& pw = work[page];
+  const uint32_t N = uni(pw.n_ok);
+  const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
+  const uint32_t s_lo = j * CH > sh ? j * CH : sh;
+  const uint32_t s_hi = (j + 1) * CH < N + sh ? (j + 1) * CH : N + sh;
+  if (s_lo >= s_hi) return;
+  const uint32_t v_lo = s_lo - sh, v_hi = s_hi - sh;
+  const ColumnDev& cd = cols[pw.column];
+  const bool own_dict = dict_in_lds && pw.column == c0;
+  const uint32_t dict_n = uni(cd.dict_n);
+  rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
+  rsrc_t prs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  const uint32_t sec_end = uni(pw.size);
+  const uint32_t n_rec = uni(pw.n_rec);
+  const uint32_t db = uni(pw.data_begin);
+  const int w = (int)uni((ld32(prs, db & ~3u) >> ((db & 3u) * 8u)) & 0xFFu);
+  const uint64_t* prec = rec + pw.rec_base;
+  T* const pag = (T*)cd.values + (pw.out_offset - sh);  // slot 0 of the page
+  const bool out16 = ((uintptr_t)cd.values & 15u) == 0;
+  const uint32_t wmask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
 
-    uint32_t b_lo = v_lo;
-    while (true) {
-      k = uni(k);
-      b_lo = uni(b_lo);
-      // records k .. k+63: lane r holds run k + r
-      const bool has = k + lane < n_rec;
-      const uint64_t rr = has ? prec[k + lane] : 0;
-      uint32_t r_start = has ? (uint32_t)rr : 0xFFFFFFFFu;
-      uint32_t r_pl = (uint32_t)(rr >> 32);
-      const uint32_t nxt = k + WAVE < n_rec ? uni((uint32_t)prec[k + WAVE]) : N;
-      const uint32_t r_end_n = __shfl_down(r_start, 1);
-      uint32_t r_end = lane == WAVE - 1 ? nxt : (k + lane + 1 < n_rec ? r_end_n : N);
-      const uint32_t e63 = rdl(r_end, WAVE - 1);
-      const uint32_t b_hi = uni(e63 < v_hi ? e63 : v_hi);  // this batch: values [b_lo, b_hi)
-      const bool live = has && r_start < b_hi && r_end > b_lo;
-      const bool pk = (r_pl & 0x80000000u) != 0;
-      // RLE runs: one dictionary gather per run
-      uint32_t r_lo = 0, r_hi = 0;
-      if (live && !pk) {
-        if (r_pl >= dict_n) {
-          report(err, err_count, page, 2, r_start > b_lo ? r_start : b_lo, PQG_ERR_DICT_ID);
-        } else {
-          const uint64_t x = (uint64_t)dict_get(r_pl);
-          r_lo = (uint32_t)x;
-          r_hi = (uint32_t)(x >> 32);
+  uint32_t k = uni(chunk_run[pw.chunk_base + j]);  // first run of this round
+  uint32_t b_lo = v_lo;
+  while (true) {
+    k = uni(k);
+    b_lo = uni(b_lo);
+    // ---- load phase: runs k .. k + n_tab - 1 into the table (entry n_tab: end sentinel)
+    uint32_t n_tab = 0, b_hi = v_hi, px_lo = 0xFFFFFFFFu, px_hi = 0;
+    for (uint32_t t0 = 0; t0 < XT_RUNS; t0 += WAVE) {
+      const uint32_t r = k + t0 + lane;
+      const bool has = r < n_rec && t0 + lane < XT_RUNS - 1;  // a run of this round
+      const uint64_t rr = r < n_rec ? prec[r] : 0;
+      const uint32_t st = r < n_rec ? (uint32_t)rr : N;        // (past the runs: end sentinel)
+      const uint32_t pl = (uint32_t)(rr >> 32);
+      const uint32_t nx63 = uni(k + t0 + WAVE < n_rec ? (uint32_t)prec[k + t0 + WAVE] : N);
+      const uint32_t en_n = __shfl_down(st, 1);
+      const uint32_t en = lane == WAVE - 1 ? nx63 : en_n;  // end of this lane's run
+      const bool live = has && st < v_hi;
+      uint32_t vlo = 0, vhi = 0;
+      if (live && !(pl & 0x80000000u)) {
+        if (pl < dict_n) {
+          const uint64_t x = (uint64_t)(own_dict ? dict_l[pl] : load_dict<W>(drs, pl));
+          vlo = (uint32_t)x;
+          vhi = (uint32_t)(x >> 32);
         }
       }
-      // Every register loaded from global memory is consumed here, before the tile loop:
-      // otherwise the waitcnt pass sees a load possibly pending at the loop head and puts
-      // s_waitcnt vmcnt(0) in front of every store, draining the stores one tile at a time.
-      asm volatile("" : "+v"(r_lo), "+v"(r_hi), "+v"(r_end), "+v"(r_start), "+v"(r_pl));
-      // packed runs: page bytes [x_lo, x_hi) of the values in [b_lo, b_hi), staged in LDS
-      const uint64_t pmask = __ballot(live && pk);
-      uint32_t x_lo = 0;
-      bool x_lds = false;
-      if (pmask) {
-        const uint32_t f = (uint32_t)__builtin_ctzll(pmask), l = 63u - (uint32_t)__builtin_clzll(pmask);
-        const uint32_t fs = rdl(r_start, f), ls = rdl(r_start, l), le = rdl(r_end, l);
-        const uint32_t fa = b_lo > fs ? b_lo : fs, lb = b_hi < le ? b_hi : le;
-        x_lo = uni(((rdl(r_pl, f) & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)(fa - fs) * (uint32_t)w) >> 3)) & ~15u);
-        const uint32_t x_hi =
-            uni((rdl(r_pl, l) & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)(lb - ls) * (uint32_t)w + 7) >> 3) + 8u);
-        x_lds = x_hi - x_lo <= XSEG_BYTES;
-        if (x_lds) {
-#pragma unroll
-          for (uint32_t i = 0; i < XSEG_BYTES; i += 16u * WAVE) {
-            const uint32_t o = i + 16u * lane;
-            if (o < x_hi - x_lo) *(u32x4*)(xseg + o) = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(x_lo + o), 0, 0);
-          }
-          wave_sync();
-        }
+      tab[t0 + lane] = u32x4{st, pl, vlo, vhi};
+      // packed bytes needed by this round: [first packed byte, last packed byte + 8)
+      if (live && (pl & 0x80000000u)) {
+        const uint32_t e_run = en;
+        const uint32_t lo = (pl & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)((st > b_lo ? st : b_lo) - st) * (uint32_t)w) >> 3);
+        const uint32_t hi_v = (e_run < v_hi ? e_run : v_hi);
+        const uint32_t hi = (pl & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)(hi_v > st ? hi_v - st : 0) * (uint32_t)w + 7) >> 3) + 8u;
+        px_lo = lo < px_lo ? lo : px_lo;
+        px_hi = hi > px_hi ? hi : px_hi;
       }
-      // run table of the batch in LDS (16 bytes per run) for the tiles that mix runs
-      rt[lane] = u32x4{r_start, r_pl, r_lo, r_hi};
-      // all loads of this batch are complete here (one wait, before the first store of
-      // the batch); the waitcnt pass then has nothing pending inside the tile loop
-      __builtin_amdgcn_s_waitcnt(0);
-      // tiles of the batch. FAST: dictionary and packed bytes in LDS, so the loop has no
-      // global load — a load there would make every store's data wait for vmcnt(0), i.e.
-      // for all of this wave's stores in flight.
-      auto tiles = [&](auto fast_tag) {
-        constexpr bool FAST = decltype(fast_tag)::value;
-        uint32_t cur_s = 1, cur_e = 0;  // RLE run [cur_s, cur_e) of the previous tile (none)
-        uint32_t cur_lo = 0, cur_hi = 0;
-        const uint32_t t_first = (b_lo + sh) / (WAVE * E) - j * CH_TILES;
-        for (uint32_t t = t_first; t < CH_TILES; t++) {
-          t = uni(t);
-          const uint32_t ts = j * CH + t * WAVE * E;  // first slot of tile t
-          const uint32_t t_lo = ts > sh ? ts - sh : 0;
-          if (t_lo >= b_hi) break;
-          const uint32_t t_hi = ts + WAVE * E - sh;
-          const uint32_t c_lo = t_lo > b_lo ? t_lo : b_lo;  // values of the tile in this batch
-          const uint32_t c_hi = t_hi < b_hi ? t_hi : b_hi;
-          const bool interior = out16 && ts >= sh && c_lo == ts - sh && c_hi == t_hi;
-          const uint32_t i0 = ts + E * lane - sh;  // value index of the lane's first element (wraps below 0)
-          T v[E];
-          cur_s = uni(cur_s);
-          cur_e = uni(cur_e);
-          if (!(c_lo >= cur_s && c_hi <= cur_e)) {
-            // the run holding the tile's first value
-            const uint64_t m = __ballot(live && r_start <= c_lo && r_end > c_lo);
-            const uint32_t r = (uint32_t)__builtin_ctzll(m);
-            if (!(rdl(r_pl, r) & 0x80000000u)) {
-              cur_s = rdl(r_start, r);
-              cur_e = rdl(r_end, r);
-              cur_lo = rdl(r_lo, r);
-              cur_hi = rdl(r_hi, r);
-            } else {
-              cur_s = 1;
-              cur_e = 0;
-            }
-          }
-          if (c_lo >= cur_s && c_hi <= cur_e) {
-            // one RLE run covers the tile
-#pragma unroll
-            for (uint32_t e = 0; e < E; e++) v[e] = (T)(((uint64_t)cur_hi << 32) | cur_lo);
-          } else {
-            // mixed tile: element i takes run ra + #{runs r in (ra, rb] with start <= i}
-            const uint64_t ov = __ballot(live && r_start < c_hi && r_end > c_lo);
-            uint32_t idx[E];
-#pragma unroll
-            for (uint32_t e = 0; e < E; e++) idx[e] = (uint32_t)__builtin_ctzll(ov);
-            for (uint64_t m = ov & (ov - 1); m; m &= m - 1) {
-              const uint32_t s0 = rdl(r_start, (uint32_t)__builtin_ctzll(m));
-#pragma unroll
-              for (uint32_t e = 0; e < E; e++) idx[e] += i0 + e >= s0 ? 1u : 0u;
-            }
-#pragma unroll
-            for (uint32_t e = 0; e < E; e++) {
-              const u32x4 q = rt[idx[e]];
-              T x = (T)(((uint64_t)q.w << 32) | q.z);
-              const uint32_t i = i0 + e;
-              if ((q.y & 0x80000000u) && i >= c_lo && i < c_hi) {
-                // packed element: LSB-first bits at (i - run start) * w from the run's data start
-                const uint64_t bit = (uint64_t)(i - q.x) * (uint32_t)w;
-                const uint32_t byte = (q.y & 0x7FFFFFFFu) + (uint32_t)(bit >> 3);
-                const uint32_t a = byte & ~3u;
-                uint64_t y;
-                if (FAST || x_lds)
-                  y = (uint64_t)*(const uint32_t*)(xseg + (a - x_lo)) |
-                      ((uint64_t)*(const uint32_t*)(xseg + (a - x_lo) + 4) << 32);
-                else
-                  y = (uint64_t)ld32(prs, a) | ((uint64_t)ld32(prs, a + 4) << 32);
-                if (a + 8u > sec_end) {  // truncated final group: bytes past the section are 0 (:96-99)
-                  const int64_t keep = (int64_t)sec_end - (int64_t)a;
-                  y = keep <= 0 ? 0 : (y & ((1ull << (8 * keep)) - 1ull));
-                }
-                y >>= (byte - a) * 8u + (uint32_t)(bit & 7u);
-                const uint32_t id = w == 0 ? 0 : (w == 32 ? (uint32_t)y : (uint32_t)y & ((1u << w) - 1u));
-                x = 0;
-                if (id >= dict_n) report(err, err_count, page, 2, i, PQG_ERR_DICT_ID);
-                else x = FAST ? dict_l[id] : dict_get(id);
-              }
-              v[e] = x;
-            }
-          }
-          T* tp = pal + t * WAVE * E + E * lane;
-          if (interior) {
-            if constexpr (W == 8) {
-              typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-              gst_nt((v2*)tp, v2{v[0], v[1]});
-            } else {
-              gst_nt((u32x4*)tp, u32x4{v[0], v[1], v[2], v[3]});
-            }
-          } else {
-#pragma unroll
-            for (uint32_t e = 0; e < E; e++)
-              if (i0 + e >= c_lo && i0 + e < c_hi) gst(tp + e, v[e]);
-          }
-        }
-      };
-      if (own_dict && (x_lds || !pmask)) tiles(std::true_type{});
-      else tiles(std::false_type{});
-      if (b_hi >= v_hi) break;
-      k += WAVE;
-      b_lo = b_hi;
+      const uint64_t inb = __ballot(has && st < v_hi);
+      n_tab += (uint32_t)__builtin_popcountll(inb);
+      if (!(inb >> 63)) break;  // this batch ends the round
     }
+    n_tab = uni(n_tab);
+    // wave min / max of the packed byte range
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const uint32_t a = __shfl_xor(px_lo, o), b = __shfl_xor(px_hi, o);
+      px_lo = a < px_lo ? a : px_lo;
+      px_hi = b > px_hi ? b : px_hi;
+    }
+    px_lo = uni(px_lo) & ~15u;
+    px_hi = uni(px_hi);
+    // round end: the start of the first run not in the table
+    if (n_tab >= XT_RUNS - 1) {
+      const u32x4 q = tab[XT_RUNS - 1];
+      b_hi = uni(q.x) < v_hi ? uni(q.x) : v_hi;
+    }
+    bool x_lds = true;
+    if (px_hi > px_lo) {
+      x_lds = px_hi - px_lo <= XT_SEG;
+      if (x_lds) {
+#pragma unroll
+        for (uint32_t i = 0; i < XT_SEG; i += 16u * WAVE) {
+          const uint32_t o = i + 16u * lane;
+          if (o < px_hi - px_lo) *(u32x4*)(xseg + o) = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(px_lo + o), 0, 0);
+        }
+      }
+    }
+    // DICT_ID: RLE runs of the round with an id past the dictionary (reported at the first
+    // value of the run inside the chunk)
+    for (uint32_t t0 = 0; t0 < n_tab; t0 += WAVE) {
+      const u32x4 q = tab[t0 + lane];
+      const uint32_t en = tab[t0 + lane + 1].x;
+      if (t0 + lane < n_tab && !(q.y & 0x80000000u) && q.y >= dict_n && en > b_lo && q.x < b_hi)
+        report(err, err_count, page, 2, q.x > b_lo ? q.x : b_lo, PQG_ERR_DICT_ID);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // load phase complete (the wave has not stored yet this round)
+
+    // ---- tile sweep
+    auto sweep = [&](auto fast_tag) {
+      constexpr bool FAST = decltype(fast_tag)::value;
+      auto value = [&](uint32_t ci, uint32_t i, const u32x4& q) -> T {
+        if (!(q.y & 0x80000000u)) return (T)(((uint64_t)q.w << 32) | q.z);
+        const uint64_t bit = (uint64_t)(i - q.x) * (uint32_t)w;
+        const uint32_t byte = (q.y & 0x7FFFFFFFu) + (uint32_t)(bit >> 3);
+        const uint32_t a4 = byte & ~3u;
+        uint64_t y;
+        if (FAST)
+          y = (uint64_t)*(const u32_alias*)(xseg + (a4 - px_lo)) |
+              ((uint64_t)*(const u32_alias*)(xseg + (a4 - px_lo) + 4) << 32);
+        else
+          y = (uint64_t)ld32(prs, a4) | ((uint64_t)ld32(prs, a4 + 4) << 32);
+        if (a4 + 8u > sec_end) {  // truncated final group: bytes past the section are 0 (:96-99)
+          const int64_t keep = (int64_t)sec_end - (int64_t)a4;
+          y = keep <= 0 ? 0 : (y & ((1ull << (8 * keep)) - 1ull));
+        }
+        y >>= (byte - a4) * 8u + (uint32_t)(bit & 7u);
+        const uint32_t id = w == 0 ? 0u : (uint32_t)y & wmask;
+        if (id >= dict_n) {
+          report(err, err_count, page, 2, i, PQG_ERR_DICT_ID);
+          return 0;
+        }
+        return FAST ? dict_l[id] : dict_get_g<W>(own_dict, dict_l, drs, id);
+        (void)ci;
+      };
+      const uint32_t t_beg = (b_lo + sh) / TV, t_end = (b_hi + sh + TV - 1) / TV;  // page tiles
+      // run of the lane's first element: binary search of the table
+      uint32_t p0 = t_beg * TV + E * lane - sh;
+      uint32_t pe = p0 < b_lo || p0 > 0x7FFFFFFFu ? b_lo : (p0 >= b_hi ? b_hi - 1 : p0);
+      uint32_t ci = 0;
+#pragma unroll
+      for (uint32_t step = XT_RUNS / 2; step >= 1; step >>= 1)
+        if (ci + step < n_tab && tab[ci + step].x <= pe) ci += step;
+      u32x4 cq = tab[ci];
+      uint32_t ce = tab[ci + 1].x;
+      for (uint32_t t = t_beg; t < t_end; t++) {
+        t = uni(t);
+        const uint32_t ts = t * TV;  // first slot of the tile
+        p0 = ts + E * lane - sh;
+        pe = p0 < b_lo || p0 > 0x7FFFFFFFu ? b_lo : (p0 >= b_hi ? b_hi - 1 : p0);
+        while (pe >= ce) {  // crossed run starts (divergent, usually no lane)
+          ci++;
+          cq = tab[ci];
+          ce = tab[ci + 1].x;
+        }
+        // elements outside [b_lo, b_hi) are not stored; they are evaluated at a clamped index
+        T v[E];
+        v[0] = value(ci, pe, cq);
+#pragma unroll
+        for (uint32_t e = 1; e < E; e++) {
+          const uint32_t x = p0 + e;  // value index of element e (wraps below 0)
+          const uint32_t i = x < b_lo || x > 0x7FFFFFFFu ? b_lo : (x >= b_hi ? b_hi - 1 : x);
+          if (i < ce) {
+            v[e] = value(ci, i, cq);
+          } else {  // the element starts a later run
+            uint32_t cj = ci + 1;
+            while (cj + 1 < n_tab && tab[cj + 1].x <= i) cj++;
+            v[e] = value(cj, i, tab[cj]);
+          }
+        }
+        T* tp = pag + ts + E * lane;
+        if (out16 && ts >= b_lo + sh && ts + TV <= b_hi + sh) {
+          if constexpr (W == 8) {
+            typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+            gst_nt((v2*)tp, v2{v[0], v[1]});
+          } else {
+            gst_nt((u32x4*)tp, u32x4{v[0], v[1], v[2], v[3]});
+          }
+        } else {
+#pragma unroll
+          for (uint32_t e = 0; e < E; e++)
+            if (ts + E * lane + e >= b_lo + sh && ts + E * lane + e < b_hi + sh) gst(tp + e, v[e]);
+        }
+      }
+    };
+    if (own_dict && x_lds) sweep(std::true_type{});
+    else sweep(std::false_type{});
+    if (b_hi >= v_hi) break;
+    k += XT_RUNS - 1;
+    b_lo = b_hi;
   }
 }
+
 
 // ---------------------------------------------------------------------------
 // Levels (def/rep) of nullable columns: ColumnReaderBase.readPageV1/readPageV2,
@@ -1523,20 +1844,16 @@ hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                        const uint64_t* chunks, uint32_t n_chunks, uint64_t* err, uint32_t* err_count) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_dict_runs, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, list, n,
-                     rec, chunk_run, err, err_count);
-  if (n_chunks == 0) return hipGetLastError();
-  // persistent expansion grid: about 8 workgroups per CU, contiguous chunk ranges
-  const uint32_t max_wg = 2048;
-  uint32_t per_wg = (n_chunks + max_wg - 1) / max_wg;
-  if (per_wg < WPB) per_wg = WPB;
-  const uint32_t n_wg = (n_chunks + per_wg - 1) / per_wg;
-  if (width == 8)
-    hipLaunchKernelGGL(k_dict_expand<8>, dim3(n_wg), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, rec, chunk_run,
-                       chunks, n_chunks, per_wg, err, err_count);
-  else
-    hipLaunchKernelGGL(k_dict_expand<4>, dim3(n_wg), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, rec, chunk_run,
-                       chunks, n_chunks, per_wg, err, err_count);
+  const dim3 g1((n + WPB - 1) / WPB), g2((n_chunks + WPB - 1) / WPB), blk(64 * WPB);
+  if (width == 8) {
+    hipLaunchKernelGGL(k_dict_runs<8>, g1, blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run, err, err_count);
+    if (n_chunks)
+      hipLaunchKernelGGL(k_dict_tiles<8>, g2, blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, err, err_count);
+  } else {
+    hipLaunchKernelGGL(k_dict_runs<4>, g1, blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run, err, err_count);
+    if (n_chunks)
+      hipLaunchKernelGGL(k_dict_tiles<4>, g2, blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, err, err_count);
+  }
   return hipGetLastError();
 }
 
