@@ -179,7 +179,7 @@ def main():
             "gib_per_s": value * 8 / 2**30,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "pqg::k_dict_runs + pqg::k_dict_tiles<8> (whole plan launch)", "algorithmic_bytes_per_launch": algo_bytes,
+                         "kernel": "pqg::k_dict_fused<8> (whole plan launch)", "algorithmic_bytes_per_launch": algo_bytes,
                          "avg_launch_ms": avg_launch_s * 1e3},
             "cpu_baseline": cpu,
             "input_gen_s": t_gen,

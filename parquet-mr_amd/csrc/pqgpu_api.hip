@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -101,6 +102,9 @@ struct pqg_plan {
   int n_cols = 0;
   DevBuf work, cols, lists, col_pages, col_page_start, err, err_count;
   DevBuf rec, chunk_run, chunks;      // dictionary pages: run records, chunk -> record, chunk work list
+  DevBuf pstat, flags;                // per page: {records, values} and ready epoch (fused dictionary kernel)
+  uint32_t epoch = 0;
+  bool dict_fused = true;
   uint32_t chunk_off[2] = {0, 0}, chunk_n[2] = {0, 0};  // C_DICT4, C_DICT8 ranges in `chunks`
   std::vector<PageWork> h_work;
   std::vector<int> cls_off, cls_n;  // into lists
@@ -390,7 +394,14 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
             P->err_count.ensure(sizeof(uint32_t) * 4) == hipSuccess &&
             P->rec.ensure(sizeof(uint64_t) * (rec_total + 16)) == hipSuccess &&  // k_dict_fill reads 9 ahead
             P->chunk_run.ensure(sizeof(uint32_t) * std::max<uint32_t>(chunk_total, 1)) == hipSuccess &&
-            P->chunks.ensure(sizeof(uint64_t) * std::max<size_t>(chunk_list.size(), 1)) == hipSuccess;
+            P->chunks.ensure(sizeof(uint64_t) * std::max<size_t>(chunk_list.size(), 1)) == hipSuccess &&
+            P->pstat.ensure(sizeof(uint64_t) * (size_t)std::max(n_pages, 1)) == hipSuccess &&
+            P->flags.ensure(sizeof(uint32_t) * (size_t)std::max(n_pages, 1)) == hipSuccess;
+  ok = ok && hipMemsetAsync(P->flags.p, 0, sizeof(uint32_t) * (size_t)std::max(n_pages, 1), s) == hipSuccess;
+  {
+    const char* e = getenv("PQG_DICT_SPLIT");  // A/B switch: walk and tiles as two launches
+    P->dict_fused = !(e && e[0] == '1');
+  }
   if (!chunk_list.empty())
     ok = ok && hipMemcpyAsync(P->chunks.p, chunk_list.data(), sizeof(uint64_t) * chunk_list.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   ok = ok && hipMemcpyAsync(P->work.p, P->h_work.data(), sizeof(PageWork) * P->h_work.size(), hipMemcpyHostToDevice, s) == hipSuccess;
@@ -425,6 +436,11 @@ int pqg_plan_launch(pqg_plan* P) {
   const int32_t* lists = (const int32_t*)P->lists.p;
   if (hipMemsetAsync(err, 0xFF, sizeof(uint64_t) * 3 * (size_t)std::max(P->n_pages, 1), s) != hipSuccess) return PQG_ERR_HIP;
   if (hipMemsetAsync(ecount, 0, sizeof(uint32_t) * 4, s) != hipSuccess) return PQG_ERR_HIP;
+  if (++P->epoch == 0) {  // page ready flags compare against the launch epoch; reset on wrap
+    P->epoch = 1;
+    if (hipMemsetAsync(P->flags.p, 0, sizeof(uint32_t) * (size_t)std::max(P->n_pages, 1), s) != hipSuccess)
+      return PQG_ERR_HIP;
+  }
   hipError_t e = hipSuccess;
   if (P->levels_n) {
     e = pqg::launch_levels(s, P->d_bytes, P->n_bytes, work, cols, lists + P->levels_off, P->levels_n, err, ecount);
@@ -441,7 +457,7 @@ int pqg_plan_launch(pqg_plan* P) {
         const int i = k - C_DICT4;
         e = pqg::launch_dict(k == C_DICT8 ? 8 : 4, s, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
                              (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->chunk_off[i], P->chunk_n[i],
-                             err, ecount);
+                             (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused, err, ecount);
         break;
       }
       case C_PLAIN: e = pqg::launch_plain(0, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
@@ -471,6 +487,8 @@ int pqg_plan_destroy(pqg_plan* P) {
   P->rec.release();
   P->chunk_run.release();
   P->chunks.release();
+  P->pstat.release();
+  P->flags.release();
   delete P;
   return PQG_OK;
 }

@@ -38,12 +38,10 @@ struct PageWork {
   int32_t dl_encoding;
   uint32_t rl_len;      // V2
   uint32_t dl_len;      // V2
-  // dictionary pages: run records (k_dict_runs -> k_dict_expand)
+  // dictionary pages: run records (walk -> tiles)
   uint64_t rec_base;    // first run record of the page
   uint32_t chunk_base;  // first output chunk of the page
-  uint32_t n_rec;       // run records written (device)
-  uint32_t n_ok;        // values covered before a run-walk error (device)
-  uint32_t reserved;
+  uint32_t reserved[3];
 };
 
 // Output chunk of k_dict_expand: CH_TILES x 64 lanes x 16 bytes.
@@ -55,7 +53,8 @@ inline uint32_t dict_chunk_values(int elem_width) { return DICT_CHUNK_TILES * 64
 
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
-                       const uint64_t* chunks, uint32_t n_chunks, uint64_t* err, uint32_t* err_count);
+                       const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
+                       bool fused, uint64_t* err, uint32_t* err_count);
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                          const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
 hipError_t launch_scan(hipStream_t st, PageWork* work, const int32_t* col_pages, const int32_t* col_page_start,

@@ -99,6 +99,19 @@ __device__ __forceinline__ void gst_nt(T* p, T v) {
   PQG_STORE_GUARD __builtin_nontemporal_store(v, (__attribute__((address_space(1))) T*)p);
 }
 
+// Run records, chunk entries and page status are produced and consumed inside one launch
+// by the fused dictionary kernel (different CUs, possibly different XCDs, whose L2s are not
+// coherent): they are written and read with system-scope relaxed accesses (sc0 sc1: through
+// to memory), ordered by s_waitcnt vmcnt(0) before the page's ready flag is set.
+template <class T>
+__device__ __forceinline__ void sst(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <class T>
+__device__ __forceinline__ T sld(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Buffer resource over [base, base + n) with hardware range checking: loads past
 // n return 0 (never fault), so a window may overhang the end of the batch.
 __device__ __forceinline__ rsrc_t make_rsrc(const uint8_t* base, uint64_t n) {
@@ -638,42 +651,10 @@ constexpr uint32_t CH_TILES = DICT_CHUNK_TILES;
 
 __device__ __forceinline__ uint32_t chunk_values(uint32_t E) { return CH_TILES * WAVE * E; }
 
-// Bit-packed runs of a dictionary page can be expanded by the walking wave itself (the page
-// bytes are in its LDS segment): lanes unpack one element each and gather the dictionary.
-// Off by default: k_dict_tiles writes whole 1 KB tiles (full cache lines) instead.
-constexpr bool PACKED_IN_WALK = false;
-template <int W>
-struct PackedSink {
-  typedef typename DictVal<W>::T T;
-  T* out;             // value 0 of the page
-  const T* dict_l;    // LDS dictionary (when dict_in_lds)
-  bool dict_in_lds;
-  rsrc_t drs;         // dictionary page bytes
-  uint32_t dict_n;
-  uint32_t sec_end;
-  int w;
-  int page;
-  uint64_t* err;
-  uint32_t* err_count;
-
-  // values [s_abs, s_abs + cnt) from packed data starting at page byte d0
-  template <bool LDS_ONLY>
-  __device__ __forceinline__ void put(const PreWin& win, uint32_t d0, uint32_t s_abs, uint32_t cnt) const {
-    for (uint32_t i = lane_id(); i < cnt; i += WAVE) {
-      const uint32_t id = packed_elem_w<LDS_ONLY>(win, d0, sec_end, i, w);
-      T x = 0;
-      if (id >= dict_n) report(err, err_count, page, 2, s_abs + i, PQG_ERR_DICT_ID);
-      else x = dict_in_lds ? dict_l[id] : load_dict<W>(drs, id);
-      gst(out + s_abs + i, x);
-    }
-  }
-};
-
 template <int W, bool SMALL>
 __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg, uint32_t sec_end,
                                           int w, uint64_t* rec, uint32_t* chunk_run, uint32_t CH, uint32_t sh, int page,
-                                          uint64_t* err, uint32_t* err_count, uint32_t& n_rec, uint32_t& n_ok,
-                                          const PackedSink<W>& ps) {
+                                          uint64_t* err, uint32_t* err_count, uint32_t& n_rec, uint32_t& n_ok) {
   const uint32_t lane = lane_id();
   uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
   uint32_t produced = 0;       // values covered by the runs read so far
@@ -764,14 +745,9 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
     const uint32_t r_end_n = __shfl_down(r_start, 1);
     if (lane < nrun) {
       const uint32_t r_end = lane + 1 < nrun ? r_end_n : produced;
-      gst(rec + k + lane, (uint64_t)r_start | ((uint64_t)r_pl << 32));
+      sst(rec + k + lane, (uint64_t)r_start | ((uint64_t)r_pl << 32));
       uint32_t j = r_start == 0 ? 0 : (r_start + sh + CH - 1) / CH;
-      for (; j * CH < r_end + sh; j++) gst(chunk_run + j, k + lane);
-    }
-    for (uint64_t m = __ballot(lane < nrun && (r_pl & 0x80000000u)); m; m &= m - 1) {
-      const uint32_t r = (uint32_t)__builtin_ctzll(m);
-      const uint32_t s0 = rdl(r_start, r), e0 = rdl(lane + 1 < nrun ? r_end_n : produced, r);
-      if constexpr (PACKED_IN_WALK) ps.template put<SMALL>(win, rdl(r_pl, r) & 0x7FFFFFFFu, s0, e0 - s0);
+      for (; j * CH < r_end + sh; j++) sst(chunk_run + j, k + lane);
     }
     k += nrun;
   }
@@ -792,7 +768,7 @@ template <int W>
 __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg,
                                              uint32_t sec_end, int w, uint64_t* rec, uint32_t* chunk_run,
                                              uint32_t CH, uint32_t sh, int page, uint64_t* err, uint32_t* err_count,
-                                             uint32_t& n_rec, uint32_t& n_ok, const PackedSink<W>& ps) {
+                                             uint32_t& n_rec, uint32_t& n_ok) {
   const uint32_t lane = lane_id();
   // successor table (256 x u16) and reached flags (256 x u8) over L.ent; every access goes
   // through may_alias types (u16 gathers vs u64 row writes must not be reordered)
@@ -804,12 +780,16 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
   uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
   uint32_t produced = 0, k = 0;
   int code = 0;
+#ifdef PQG_DIAG
+  uint64_t d_pre = 0, d_dbl = 0, d_emit = 0, d_win = 0;
+  const uint64_t d_start = __builtin_amdgcn_s_memtime();
+#endif
   // one record at lane 0 (the scalar slow path) and the chunk entries it owns
   auto put_record = [&](uint32_t start, uint32_t end, uint32_t payload) {
     if (lane == 0) {
-      gst(rec + k, (uint64_t)start | ((uint64_t)payload << 32));
+      sst(rec + k, (uint64_t)start | ((uint64_t)payload << 32));
       uint32_t j = start == 0 ? 0 : (start + sh + CH - 1) / CH;
-      for (; j * CH < end + sh; j++) gst(chunk_run + j, k);
+      for (; j * CH < end + sh; j++) sst(chunk_run + j, k);
     }
     k++;
   };
@@ -820,6 +800,7 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
     if (produced >= N) break;
     if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
     const uint32_t B = pos & ~3u;
+    DIAG_T(t_pre);
     predecode<true>(win, B, w);
     // successors of this lane's 4 positions
     uint32_t jv[4], nn[4], slowm = 0, inm = 0;
@@ -837,6 +818,8 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
       slowm |= (slow ? 1u : 0u) << b;
       inm |= (in ? 1u : 0u) << b;
     }
+    DIAG_ADD(d_pre, t_pre);
+    DIAG_T(t_dbl);
     const uint32_t s0 = pos - B;
     *(u64a*)(Jt + 4u * lane) =
         (uint64_t)jv[0] | ((uint64_t)jv[1] << 16) | ((uint64_t)jv[2] << 32) | ((uint64_t)jv[3] << 48);
@@ -864,6 +847,8 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
       if (!__ballot(more)) break;
     }
     const uint32_t r4 = *(const u32a*)(Rt + 4u * lane);
+    DIAG_ADD(d_dbl, t_dbl);
+    DIAG_T(t_emit);
     uint32_t mk = 0;
 #pragma unroll
     for (uint32_t b = 0; b < 4; b++) mk |= ((r4 >> (8u * b)) & 1u) << b;
@@ -925,25 +910,18 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
         const uint32_t payload = pk ? (0x80000000u | vv) : (vv > 0x7FFFFFFFu ? 0x7FFFFFFFu : vv);
         const uint32_t s_abs = produced + stb[b];
         const uint32_t e_abs = produced + (stb[b] + cc[b] < cap ? stb[b] + cc[b] : cap);
-        gst(rec + k + idx, (uint64_t)s_abs | ((uint64_t)payload << 32));
+        sst(rec + k + idx, (uint64_t)s_abs | ((uint64_t)payload << 32));
         uint32_t j = s_abs == 0 ? 0 : (s_abs + sh + CH - 1) / CH;
-        for (; j * CH < e_abs + sh; j++) gst(chunk_run + j, k + idx);
+        for (; j * CH < e_abs + sh; j++) sst(chunk_run + j, k + idx);
         idx++;
-      }
-    }
-    // bit-packed runs of the window, one at a time across the wave
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      const bool pk = (win.flg >> (8u * b)) & 1u;
-      for (uint64_t m = __ballot(((em >> b) & 1u) && pk); m; m &= m - 1) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(m);
-        const uint32_t s_rel = rdl(stb[b], l);
-        const uint32_t e_rel = rdl(stb[b] + cc[b] < cap ? stb[b] + cc[b] : cap, l);
-        if constexpr (PACKED_IN_WALK) ps.template put<true>(win, rdl(win.val[b], l), produced + s_rel, e_rel - s_rel);
       }
     }
     k += uni(n_em);
     produced += total;
+    DIAG_ADD(d_emit, t_emit);
+#ifdef PQG_DIAG
+    d_win++;
+#endif
     if (produced >= N) break;
     // continue after the window's last chain position
     const uint32_t ql = q_last >> 2, qb = q_last & 3u;
@@ -967,7 +945,6 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
       if (m == 0 && cnt == 0) cnt = left;
       const uint32_t take = cnt < left ? (uint32_t)cnt : left;
       put_record(produced, produced + take, m ? (0x80000000u | vv) : (vv > 0x7FFFFFFFu ? 0x7FFFFFFFu : vv));
-      if constexpr (PACKED_IN_WALK) if (m) ps.template put<true>(win, vv, produced, take);
       produced += take;
       pos = m ? (nxs < sec_end ? nxs : sec_end) : nxs;
     }
@@ -978,6 +955,18 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
   }
   n_rec = k;
   n_ok = N;
+#ifdef PQG_DIAG
+  if (lane == 0 && pqg_diag_buf) {
+    uint64_t* d = pqg_diag_buf + 8 * (uint64_t)page;
+    d[0] = d_start;
+    d[1] = __builtin_amdgcn_s_memtime();
+    d[2] = d_pre;
+    d[3] = d_dbl;
+    d[4] = d_emit;
+    d[5] = d_win;
+    d[6] = k;
+  }
+#endif
 }
 
 // One wave per page (4 per workgroup): the run records of RLE_DICTIONARY / PLAIN_DICTIONARY
@@ -985,45 +974,18 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
 // :80-109). The page section is staged in LDS; a 256-byte window is pre-decoded in parallel
 // (every lane parses a run header at each of its 4 byte positions) into LDS tables, and the
 // serial chain is one ds_read_b64 + ds_read_b32 per run.
+// One wave per page (4 per workgroup; `group` is the workgroup's index among the walkers).
 template <int W>
-__global__ __launch_bounds__(64 * WPB) void k_dict_runs(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                                        PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
-                                                        const int32_t* __restrict__ list, int n_list, uint64_t* rec,
-                                                        uint32_t* chunk_run, uint64_t* err, uint32_t* err_count) {
-  typedef typename DictVal<W>::T T;
-  __shared__ __attribute__((aligned(16))) uint8_t dict_lds[PACKED_IN_WALK ? DICT_LDS_BYTES : 16];
-  __shared__ __attribute__((aligned(16))) DictWaveLds wl_all[WPB];
-  int* wg_col = (int*)dict_lds;  // scratch before the dictionary is staged
-  DictWaveLds& L = wl_all[wave_id()];
-  const int page = wave_page(list, n_list);
+__device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                               const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                               const int32_t* __restrict__ list, int n_list, uint64_t* rec,
+                                               uint32_t* chunk_run, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
+                                               uint64_t* err, uint32_t* err_count, uint8_t* lds, uint32_t group) {
+  DictWaveLds& L = ((DictWaveLds*)lds)[wave_id()];
+  const int i_page = (int)(group * WPB + wave_id());
+  if (i_page >= n_list) return;
+  const int page = list[i_page];
   const uint32_t lane = lane_id();
-  // the workgroup's dictionary in LDS when its pages share one that fits (packed values)
-  if (lane == 0) wg_col[wave_id()] = page >= 0 ? work[page].column : -1;
-  __syncthreads();
-  int c0 = -1;
-  bool same = true;
-#pragma unroll
-  for (int q = 0; q < WPB; q++) {
-    const int c = wg_col[q];
-    if (c >= 0) {
-      if (c0 < 0) c0 = c;
-      else if (c != c0) same = false;
-    }
-  }
-  bool dict_in_lds = false;
-  __syncthreads();  // wg_col read by every wave before the dictionary overwrites it
-  if (PACKED_IN_WALK && same && c0 >= 0) {
-    const ColumnDev& cd0 = cols[c0];
-    const uint64_t need = (uint64_t)cd0.dict_n * W;
-    dict_in_lds = need <= DICT_LDS_BYTES && need <= cd0.dict_bytes;
-    if (dict_in_lds) {
-      rsrc_t d0 = make_rsrc(bytes + cd0.dict_offset, cd0.dict_bytes);
-      for (uint32_t o = 16u * threadIdx.x; o < (uint32_t)need; o += 16u * 64u * WPB)
-        *(u32x4*)(dict_lds + o) = u32x4{ld4_any(d0, o), ld4_any(d0, o + 4), ld4_any(d0, o + 8), ld4_any(d0, o + 12)};
-    }
-  }
-  __syncthreads();
-  if (page < 0) return;
   const PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
   uint32_t N = uni(pw.n_values);
@@ -1032,6 +994,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_runs(const uint8_t* __restric
   const uint32_t CH = chunk_values(E);
   const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
   uint32_t n_rec = 0, n_ok = 0;
+  (void)cd;
   if (N > 0) {
     PreWin win;
     win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
@@ -1047,56 +1010,33 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_runs(const uint8_t* __restric
       } else {
         uint64_t* prec = rec + pw.rec_base;
         uint32_t* pcr = chunk_run + pw.chunk_base;
-        PackedSink<W> ps;
-        ps.out = (T*)cd.values + pw.out_offset;
-        ps.dict_l = (const T*)dict_lds;
-        ps.dict_in_lds = dict_in_lds && pw.column == c0;
-        ps.drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
-        ps.dict_n = uni(cd.dict_n);
-        ps.sec_end = sec_end;
-        ps.w = (int)bw;
-        ps.page = page;
-        ps.err = err;
-        ps.err_count = err_count;
         // SMALL: the whole data section sits in the LDS segment: the walk has no global load
         if (sec_end - win.seg_lo + 264u <= SEG_BYTES)  // every window inside the segment
-          dict_walk_pj<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok,
-                          ps);
+          dict_walk_pj<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
         else if (sec_end - win.seg_lo <= SEG_BYTES)
-          dict_walk<W, true>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec,
-                             n_ok, ps);
+          dict_walk<W, true>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
         else
-          dict_walk<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec,
-                              n_ok, ps);
+          dict_walk<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
       }
     }
   }
   if (lane == 0) {
-    work[page].n_rec = n_rec;
-    work[page].n_ok = n_ok;
+    sst(pstat + page, (uint64_t)n_rec | ((uint64_t)n_ok << 32));
+    __builtin_amdgcn_s_waitcnt(0);  // records, chunk entries and status are in memory
+    sst(flags + page, epoch);
   }
 }
 
-// RLE runs of dictionary pages: one wave per output chunk (CH_TILES x 64 lanes x 16 bytes).
-// Everything the fill needs — chunk and page descriptors, run records, dictionary entries —
-// comes through scalar loads (s_load: lgkmcnt only), so no store of the wave is ever waited
-// on: the kernel is a memset driven by run records. Bit-packed runs were written by
-// k_dict_runs (they need the page bytes, which it has in LDS).
 template <int W>
-__device__ __forceinline__ typename DictVal<W>::T sload_dict(const uint32_t* __restrict__ words, uint64_t dict_offset,
-                                                             uint32_t id) {
-  // dictionary entry id through scalar loads, any byte alignment of the dictionary page:
-  // aligned dwords of the (16-byte aligned) batch buffer + v_alignbyte
-  const uint64_t o = dict_offset + (uint64_t)id * W;
-  const uint32_t* p = words + (o >> 2);
-  const uint32_t sb = (uint32_t)(o & 3u);
-  if constexpr (W == 8) {
-    const uint32_t w0 = p[0], w1 = p[1], w2 = sb ? p[2] : 0u;  // no read past the entry when aligned
-    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sb) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sb) << 32);
-  } else {
-    const uint32_t w0 = p[0], w1 = sb ? p[1] : 0u;
-    return __builtin_amdgcn_alignbyte(w1, w0, sb);
-  }
+__global__ __launch_bounds__(64 * WPB) void k_dict_runs(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                        const PageWork* __restrict__ work,
+                                                        const ColumnDev* __restrict__ cols,
+                                                        const int32_t* __restrict__ list, int n_list, uint64_t* rec,
+                                                        uint32_t* chunk_run, uint64_t* pstat, uint32_t* flags,
+                                                        uint32_t epoch, uint64_t* err, uint32_t* err_count) {
+  __shared__ __attribute__((aligned(16))) DictWaveLds wl_all[WPB];
+  dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
+                    (uint8_t*)wl_all, blockIdx.x);
 }
 
 template <int W>
@@ -1117,23 +1057,28 @@ __device__ __forceinline__ typename DictVal<W>::T dict_get_g(bool in_lds, const 
 constexpr uint32_t XT_RUNS = 128;   // run table entries per wave
 constexpr uint32_t XT_SEG = 2560;   // LDS bytes for the packed data of one round
 
-template <int W>
-__global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                                         const PageWork* __restrict__ work,
-                                                         const ColumnDev* __restrict__ cols,
-                                                         const uint64_t* __restrict__ rec,
-                                                         const uint32_t* __restrict__ chunk_run,
-                                                         const uint64_t* __restrict__ chunks, uint32_t n_chunks,
-                                                         uint64_t* err, uint32_t* err_count) {
+constexpr uint32_t XT_LDS_BYTES = DICT_LDS_BYTES + WPB * (XT_RUNS * 16 + XT_SEG);
+constexpr uint32_t SPIN_LIMIT = 1u << 20;  // ~55 ms of s_sleep 2: a walker that never publishes
+
+// FUSED: launched in the same grid as the walkers (after them in workgroup order, so every
+// walker this wave waits for was dispatched first); the page's records are ready once its
+// flag holds this launch's epoch.
+template <int W, bool FUSED>
+__device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                                const uint64_t* rec, const uint32_t* chunk_run,
+                                                const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                const uint64_t* pstat, const uint32_t* flags, uint32_t epoch,
+                                                uint64_t* err, uint32_t* err_count, uint8_t* lds, uint32_t group) {
   typedef typename DictVal<W>::T T;
   constexpr uint32_t E = 16 / W;
   constexpr uint32_t TV = WAVE * E;  // values per tile
   constexpr uint32_t CH = CH_TILES * TV;
-  __shared__ __attribute__((aligned(16))) uint8_t dict_lds[DICT_LDS_BYTES];
-  __shared__ __attribute__((aligned(16))) u32x4 tab_all[WPB][XT_RUNS];
-  __shared__ __attribute__((aligned(16))) uint8_t xseg_all[WPB][XT_SEG];
+  uint8_t* dict_lds = lds;
+  u32x4* tab = (u32x4*)(lds + DICT_LDS_BYTES) + wave_id() * XT_RUNS;
+  uint8_t* xseg = lds + DICT_LDS_BYTES + WPB * XT_RUNS * 16 + wave_id() * XT_SEG;
   const uint32_t lane = lane_id();
-  const uint32_t c = blockIdx.x * WPB + wave_id();
+  const uint32_t c = group * WPB + wave_id();
   const int page = c < n_chunks ? (int)(uint32_t)chunks[c] : -1;
   // the workgroup's dictionary in LDS when its chunks share one that fits
   int* wg_col = (int*)dict_lds;
@@ -1164,12 +1109,21 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restri
   __syncthreads();
   if (page < 0) return;
   const T* dict_l = (const T*)dict_lds;
-  u32x4* tab = tab_all[wave_id()];
-  uint8_t* xseg = xseg_all[wave_id()];
+  if (FUSED) {
+    uint32_t spins = 0;
+    while (uni(sld(flags + page)) != epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins >= SPIN_LIMIT) {
+        if (lane == 0) report(err, err_count, page, 2, 0, PQG_ERR_HIP);
+        return;
+      }
+    }
+  }
+  const uint64_t pst = uni64(sld(pstat + page));
 
   const uint32_t j = (uint32_t)(chunks[c] >> 32);
   const PageWork& pw = work[page];
-  const uint32_t N = uni(pw.n_ok);
+  const uint32_t N = (uint32_t)(pst >> 32);  // values covered before a walk error
   const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
   const uint32_t s_lo = j * CH > sh ? j * CH : sh;
   const uint32_t s_hi = (j + 1) * CH < N + sh ? (j + 1) * CH : N + sh;
@@ -1181,7 +1135,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restri
   rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
   rsrc_t prs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
   const uint32_t sec_end = uni(pw.size);
-  const uint32_t n_rec = uni(pw.n_rec);
+  const uint32_t n_rec = (uint32_t)pst;
   const uint32_t db = uni(pw.data_begin);
   const int w = (int)uni((ld32(prs, db & ~3u) >> ((db & 3u) * 8u)) & 0xFFu);
   const uint64_t* prec = rec + pw.rec_base;
@@ -1189,7 +1143,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restri
   const bool out16 = ((uintptr_t)cd.values & 15u) == 0;
   const uint32_t wmask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
 
-  uint32_t k = uni(chunk_run[pw.chunk_base + j]);  // first run of this round
+  uint32_t k = uni(sld(chunk_run + pw.chunk_base + j));  // first run of this round
   uint32_t b_lo = v_lo;
   while (true) {
     k = uni(k);
@@ -1199,10 +1153,10 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restri
     for (uint32_t t0 = 0; t0 < XT_RUNS; t0 += WAVE) {
       const uint32_t r = k + t0 + lane;
       const bool has = r < n_rec && t0 + lane < XT_RUNS - 1;  // a run of this round
-      const uint64_t rr = r < n_rec ? prec[r] : 0;
+      const uint64_t rr = r < n_rec ? sld(prec + r) : 0;
       const uint32_t st = r < n_rec ? (uint32_t)rr : N;        // (past the runs: end sentinel)
       const uint32_t pl = (uint32_t)(rr >> 32);
-      const uint32_t nx63 = uni(k + t0 + WAVE < n_rec ? (uint32_t)prec[k + t0 + WAVE] : N);
+      const uint32_t nx63 = uni(k + t0 + WAVE < n_rec ? (uint32_t)sld(prec + k + t0 + WAVE) : N);
       const uint32_t en_n = __shfl_down(st, 1);
       const uint32_t en = lane == WAVE - 1 ? nx63 : en_n;  // end of this lane's run
       const bool live = has && st < v_hi;
@@ -1347,6 +1301,39 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restri
     k += XT_RUNS - 1;
     b_lo = b_hi;
   }
+}
+
+template <int W>
+__global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                         const PageWork* __restrict__ work,
+                                                         const ColumnDev* __restrict__ cols, const uint64_t* rec,
+                                                         const uint32_t* chunk_run, const uint64_t* __restrict__ chunks,
+                                                         uint32_t n_chunks, const uint64_t* pstat, uint64_t* err,
+                                                         uint32_t* err_count) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[XT_LDS_BYTES];
+  dict_tiles_body<W, false>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, nullptr, 0, err,
+                            err_count, lds, blockIdx.x);
+}
+
+// Walkers and tiles in one grid: workgroups [0, n_walk) walk pages, the rest expand chunks
+// as soon as their page is published, so the expansion overlaps the walk.
+template <int W>
+__global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                         const PageWork* __restrict__ work,
+                                                         const ColumnDev* __restrict__ cols,
+                                                         const int32_t* __restrict__ list, int n_list,
+                                                         uint32_t n_walk, uint64_t* rec, uint32_t* chunk_run,
+                                                         const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                         uint64_t* pstat, uint32_t* flags, uint32_t epoch,
+                                                         uint64_t* err, uint32_t* err_count) {
+  constexpr uint32_t LB = sizeof(DictWaveLds) * WPB > XT_LDS_BYTES ? sizeof(DictWaveLds) * WPB : XT_LDS_BYTES;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LB];
+  if (blockIdx.x < n_walk)
+    dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
+                      lds, blockIdx.x);
+  else
+    dict_tiles_body<W, true>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err,
+                             err_count, lds, blockIdx.x - n_walk);
 }
 
 
@@ -1842,17 +1829,32 @@ namespace pqg {
 
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
-                       const uint64_t* chunks, uint32_t n_chunks, uint64_t* err, uint32_t* err_count) {
+                       const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
+                       bool fused, uint64_t* err, uint32_t* err_count) {
   if (n <= 0) return hipSuccess;
-  const dim3 g1((n + WPB - 1) / WPB), g2((n_chunks + WPB - 1) / WPB), blk(64 * WPB);
+  const uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
+  const dim3 blk(64 * WPB);
+  if (fused) {
+    if (width == 8)
+      hipLaunchKernelGGL(k_dict_fused<8>, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n, n_walk,
+                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count);
+    else
+      hipLaunchKernelGGL(k_dict_fused<4>, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n, n_walk,
+                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count);
+    return hipGetLastError();
+  }
   if (width == 8) {
-    hipLaunchKernelGGL(k_dict_runs<8>, g1, blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run, err, err_count);
-    if (n_chunks)
-      hipLaunchKernelGGL(k_dict_tiles<8>, g2, blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, err, err_count);
+    hipLaunchKernelGGL(k_dict_runs<8>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,
+                       pstat, flags, epoch, err, err_count);
+    if (n_tile)
+      hipLaunchKernelGGL(k_dict_tiles<8>, dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks,
+                         n_chunks, pstat, err, err_count);
   } else {
-    hipLaunchKernelGGL(k_dict_runs<4>, g1, blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run, err, err_count);
-    if (n_chunks)
-      hipLaunchKernelGGL(k_dict_tiles<4>, g2, blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, err, err_count);
+    hipLaunchKernelGGL(k_dict_runs<4>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,
+                       pstat, flags, epoch, err, err_count);
+    if (n_tile)
+      hipLaunchKernelGGL(k_dict_tiles<4>, dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks,
+                         n_chunks, pstat, err, err_count);
   }
   return hipGetLastError();
 }
