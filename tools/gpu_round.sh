@@ -1,0 +1,49 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench (with CPU baseline), rocprofv3 kernel stats,
+# then separate PMC passes for HBM traffic. Every GPU step has its own time limit and
+# the script stops at the first failure (no retries).
+# Usage (from the repo root, via gpurun): bash tools/gpu_round.sh <tag> [steps...]
+#   steps: tests smoke bench bench2 prof pmc   (default: tests smoke bench prof pmc)
+set -euo pipefail
+TAG=${1:-run}; shift || true
+STEPS=${*:-tests smoke bench prof pmc}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+        > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
+      tail -3 "$OUT/pytest_gpu.log" ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+        || { tail -30 "$OUT/smoke.log"; exit 1; }
+      tail -2 "$OUT/smoke.log" ;;
+    bench)
+      timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
+        || { tail -30 "$OUT/bench.err"; exit 1; }
+      cat "$OUT/bench.json" ;;
+    bench2)
+      timeout -k 10 400 python -u bench.py --no-cpu --zipf 2.0 > "$OUT/bench_zipf2.json" 2> "$OUT/bench_zipf2.err" \
+        || { tail -30 "$OUT/bench_zipf2.err"; exit 1; }
+      cat "$OUT/bench_zipf2.json" ;;
+    prof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+        python3 bench.py --no-cpu > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
+        || { tail -30 "$OUT/prof.err"; exit 1; }
+      python3 tools/kstats.py "$OUT/prof" ;;
+    pmc)
+      i=0
+      mkdir -p "$OUT/pmc"
+      for grp in "FETCH_SIZE" "WRITE_SIZE" \
+                 "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU"; do
+        timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc/pass$i" -o run -- \
+          python3 bench.py --no-cpu --steps 5 --warmup 1 > "$OUT/pmc/pass$i.log" 2>&1 \
+          || { tail -20 "$OUT/pmc/pass$i.log"; exit 1; }
+        i=$((i+1))
+      done
+      python3 tools/pmc_summary.py "$OUT/pmc" || true ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
