@@ -396,7 +396,14 @@ static int emit_binary(colstate* cs, const uint8_t* src, int32_t len) {
 /* ------------------------------------------------------------------------ */
 /* Value readers: one struct with a tagged union of the reference's readers. */
 
-enum { VR_DICT = 1, VR_PLAIN_FIXED, VR_PLAIN_BOOL, VR_PLAIN_BINARY, VR_DELTA };
+enum { VR_DICT = 1, VR_PLAIN_FIXED, VR_PLAIN_BOOL, VR_PLAIN_BINARY, VR_DELTA, VR_DLBA, VR_DBA, VR_BSS };
+
+/* DeltaBinaryPackingValuesReader state: the eagerly decoded page (valuesBuffer). */
+typedef struct {
+  int64_t* buf;
+  int32_t total;
+  int32_t read;
+} jdelta;
 
 typedef struct {
   int kind;
@@ -407,16 +414,21 @@ typedef struct {
   const jdict* dict;
   /* boolean (ByteBitPackingValuesReader(1, LITTLE_ENDIAN), ByteBitPackingValuesReader.java:41-89) */
   int64_t bool_read;
-  /* delta */
-  int64_t* delta_buf;
-  int32_t delta_total;
-  int32_t delta_read;
+  /* DELTA_BINARY_PACKED values; DELTA_LENGTH_BYTE_ARRAY lengths; DELTA_BYTE_ARRAY suffix lengths */
+  jdelta delta;
+  /* DELTA_BYTE_ARRAY prefix lengths and the previous value (DeltaByteArrayReader.previous) */
+  jdelta prefix;
+  uint8_t* prev;
+  int64_t prev_len;
+  /* BYTE_STREAM_SPLIT: encoded stream count and index (ByteStreamSplitValuesReader :32-50) */
+  int64_t bss_count;
+  int64_t bss_index;
 } vreader;
 
 /* DeltaBinaryPackingValuesReader.initFromPage :59-77 (eager), allocateValuesBuffer :83-87,
  * loadNewBlockToBuffer :121-143, unpack8Values :156-162, readBitWidthsForMiniBlocks :164-172,
  * DeltaBinaryPackingConfig :30-51. */
-static int delta_init(vreader* r, jstream* s) {
+static int delta_init(jdelta* r, jstream* s) {
   int32_t block_size, mb_num, total;
   int e;
   if ((e = read_uvarint(s, &block_size))) return e;
@@ -431,12 +443,12 @@ static int delta_init(vreader* r, jstream* s) {
   if (total < 0) return PQG_ERR_CORRUPT;
   int64_t mb_count = ((int64_t)total + mb_size - 1) / mb_size;   /* Math.ceil :84 */
   int64_t cap = mb_count * mb_size + 1;
-  r->delta_buf = (int64_t*)calloc((size_t)cap, sizeof(int64_t));
-  r->delta_total = total;
-  r->delta_read = 0;
+  r->buf = (int64_t*)calloc((size_t)cap, sizeof(int64_t));
+  r->total = total;
+  r->read = 0;
   int32_t* widths = (int32_t*)calloc((size_t)mb_num, sizeof(int32_t));
   int64_t buffered = 0;
-  if ((e = read_zigzag_varlong(s, &r->delta_buf[buffered]))) { free(widths); return e; }
+  if ((e = read_zigzag_varlong(s, &r->buf[buffered]))) { free(widths); return e; }
   buffered++;
   while (buffered < total) {
     int64_t min_delta;
@@ -453,15 +465,37 @@ static int delta_init(vreader* r, jstream* s) {
       for (int32_t j = 0; j < mb_size; j += 8) {
         jstream sl;
         if ((e = js_slice(s, w, &sl))) { free(widths); return e; }
-        pqr_unpack8_long(w, sl.buf + sl.pos, &r->delta_buf[buffered]);
+        pqr_unpack8_long(w, sl.buf + sl.pos, &r->buf[buffered]);
         buffered += 8;
       }
     }
     int64_t unpacked = (int64_t)i * mb_size;
     for (int64_t j = buffered - unpacked; j < buffered; j++)
-      r->delta_buf[j] = (int64_t)((uint64_t)r->delta_buf[j] + (uint64_t)min_delta + (uint64_t)r->delta_buf[j - 1]);
+      r->buf[j] = (int64_t)((uint64_t)r->buf[j] + (uint64_t)min_delta + (uint64_t)r->buf[j - 1]);
   }
   free(widths);
+  return PQG_OK;
+}
+
+/* readLong :109-113 with checkRead :115-119 ("no more value to read"). */
+static int delta_next(jdelta* r, int64_t* v) {
+  if (r->read >= r->total) return PQG_ERR_DELTA_PAST_END;
+  *v = r->buf[r->read++];
+  return PQG_OK;
+}
+
+/* DeltaLengthByteArrayValuesReader.readBytes :51-58: length = lengthReader.readInteger()
+ * ((int) of the long), then in.slice(length): negative -> IllegalArgumentException from
+ * ByteBuffer.limit (CORRUPT), short -> EOFException ("Failed to read N bytes"). */
+static int dlba_next(vreader* r, const uint8_t** p, int32_t* len) {
+  int64_t l64;
+  int e = delta_next(&r->delta, &l64);
+  if (e) return e;
+  int32_t l = (int32_t)(uint32_t)(uint64_t)l64;
+  jstream sl;
+  if ((e = js_slice(&r->in, l, &sl))) return e;
+  *p = sl.buf + sl.pos;
+  *len = l;
   return PQG_OK;
 }
 
@@ -513,14 +547,60 @@ static int vreader_init(vreader* r, const pqg_page_desc* pg, colstate* cs, jstre
   if (enc == PQG_DELTA_BINARY_PACKED) {
     if (t != PQG_INT32 && t != PQG_INT64) return PQG_ERR_UNSUPPORTED;   /* Encoding.java :190-193 */
     r->kind = VR_DELTA;
-    return delta_init(r, s);
+    return delta_init(&r->delta, s);
+  }
+  if (enc == PQG_DELTA_LENGTH_BYTE_ARRAY) {
+    if (t != PQG_BYTE_ARRAY) return PQG_ERR_UNSUPPORTED;                /* Encoding.java :204-207 */
+    /* DeltaLengthByteArrayValuesReader.initFromPage :44-48: lengths (eager), then remainingStream() */
+    r->kind = VR_DLBA;
+    int e = delta_init(&r->delta, s);
+    if (e) return e;
+    r->in = *s;
+    s->pos = s->end;
+    return PQG_OK;
+  }
+  if (enc == PQG_DELTA_BYTE_ARRAY) {
+    /* Encoding.java :219-222 allows FIXED_LEN_BYTE_ARRAY too; the FLBA output here is fixed width,
+     * so a decoded value of another length is reported (DeltaByteArray on FLBA: next row) */
+    if (t != PQG_BYTE_ARRAY) return PQG_ERR_UNSUPPORTED;
+    /* DeltaByteArrayReader.initFromPage :45-48: prefix lengths, then the suffixes' DLBA reader */
+    r->kind = VR_DBA;
+    int e = delta_init(&r->prefix, s);
+    if (e) return e;
+    if ((e = delta_init(&r->delta, s))) return e;
+    r->in = *s;
+    s->pos = s->end;
+    r->prev = NULL;     /* previous = empty (:41); PARQUET-246 carry-over is not applied (:89-94) */
+    r->prev_len = 0;
+    return PQG_OK;
+  }
+  if (enc == PQG_BYTE_STREAM_SPLIT) {
+    /* Encoding.java :127-145; ByteStreamSplitValuesReader.initFromPage :67-97 */
+    if (t != PQG_FLOAT && t != PQG_DOUBLE && t != PQG_INT32 && t != PQG_INT64 && t != PQG_FIXED_LEN_BYTE_ARRAY)
+      return PQG_ERR_UNSUPPORTED;
+    int w = elem_width_of(t, c->type_length);
+    if (w <= 0) return PQG_ERR_UNSUPPORTED;
+    int64_t avail = js_available(s);
+    if (avail % w != 0) return PQG_ERR_CORRUPT;               /* "Invalid ByteStreamSplit stream" :74-79 */
+    if ((int64_t)value_count < avail / w) return PQG_ERR_CORRUPT;  /* upper bound check :83-88 */
+    r->kind = VR_BSS;
+    r->width = w;
+    r->in = *s;
+    s->pos = s->end;
+    r->bss_count = avail / w;
+    r->bss_index = 0;
+    return PQG_OK;
   }
   return PQG_ERR_UNSUPPORTED;
 }
 
 static void vreader_free(vreader* r) {
-  free(r->delta_buf);
-  r->delta_buf = NULL;
+  free(r->delta.buf);
+  free(r->prefix.buf);
+  free(r->prev);
+  r->delta.buf = NULL;
+  r->prefix.buf = NULL;
+  r->prev = NULL;
 }
 
 /* Reads one value through the reader and emits it (readLong/readInteger/...). */
@@ -562,14 +642,58 @@ static int vreader_read(vreader* r, colstate* cs) {
     }
     case VR_DELTA: {
       /* readLong :109-113, checkRead :115-119; readInteger :103-107 = (int) readLong() */
-      if (r->delta_read >= r->delta_total) return PQG_ERR_DELTA_PAST_END;
-      int64_t v = r->delta_buf[r->delta_read];
-      r->delta_read++;
+      int64_t v;
+      if ((e = delta_next(&r->delta, &v))) return e;
       if (c->physical_type == PQG_INT32) {
         int32_t i32 = (int32_t)(uint32_t)(uint64_t)v;
         return emit_fixed(cs, (const uint8_t*)&i32);
       }
       return emit_fixed(cs, (const uint8_t*)&v);
+    }
+    case VR_DLBA: {
+      const uint8_t* p;
+      int32_t len;
+      if ((e = dlba_next(r, &p, &len))) return e;
+      return emit_binary(cs, p, len);
+    }
+    case VR_DBA: {
+      /* DeltaByteArrayReader.readBytes :57-79 */
+      int64_t pl64;
+      if ((e = delta_next(&r->prefix, &pl64))) return e;
+      int32_t prefix = (int32_t)(uint32_t)(uint64_t)pl64;
+      const uint8_t* sp;
+      int32_t slen;
+      if ((e = dlba_next(r, &sp, &slen))) return e;
+      int64_t length = (int64_t)(int32_t)((uint32_t)prefix + (uint32_t)slen);  /* int addition */
+      if (prefix != 0) {
+        /* new byte[length] (NegativeArraySizeException), arraycopy(previous, 0, out, 0, prefix)
+         * (IndexOutOfBounds when prefix < 0 or prefix > previous.length) */
+        if (length < 0 || prefix < 0 || prefix > r->prev_len) return PQG_ERR_CORRUPT;
+        uint8_t* out = (uint8_t*)malloc((size_t)(length ? length : 1));
+        memcpy(out, r->prev, (size_t)prefix);
+        memcpy(out + prefix, sp, (size_t)slen);
+        free(r->prev);
+        r->prev = out;
+        r->prev_len = length;
+      } else {
+        uint8_t* out = (uint8_t*)malloc((size_t)(slen ? slen : 1));
+        memcpy(out, sp, (size_t)slen);
+        free(r->prev);
+        r->prev = out;
+        r->prev_len = slen;
+      }
+      return emit_binary(cs, r->prev, (int32_t)r->prev_len);
+    }
+    case VR_BSS: {
+      /* nextElementByteOffset :43-50; value bytes k = stream k at index i (decodeData :53-64) */
+      if (r->bss_index >= r->bss_count) return PQG_ERR_EOF;   /* "Byte-stream data was already exhausted." */
+      uint8_t tmp[64];
+      uint8_t* buf = r->width <= 64 ? tmp : (uint8_t*)malloc((size_t)r->width);
+      for (int k = 0; k < r->width; k++) buf[k] = r->in.buf[r->in.pos + r->bss_index + (int64_t)k * r->bss_count];
+      r->bss_index++;
+      e = emit_fixed(cs, buf);
+      if (buf != tmp) free(buf);
+      return e;
     }
   }
   return PQG_ERR_UNSUPPORTED;
@@ -717,11 +841,11 @@ int64_t pqr_delta_decode(const uint8_t* buf, int64_t len, int64_t* out, int64_t 
   jstream s = {buf, 0, len};
   vreader r;
   memset(&r, 0, sizeof(r));
-  int e = delta_init(&r, &s);
+  int e = delta_init(&r.delta, &s);
   if (e) { vreader_free(&r); return -e; }
-  int64_t n = r.delta_total;
+  int64_t n = r.delta.total;
   if (n > cap) { vreader_free(&r); return -PQG_ERR_INVALID_ARG; }
-  memcpy(out, r.delta_buf, (size_t)n * sizeof(int64_t));
+  memcpy(out, r.delta.buf, (size_t)n * sizeof(int64_t));
   if (consumed) *consumed = s.pos;
   vreader_free(&r);
   return n;

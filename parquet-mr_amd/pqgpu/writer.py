@@ -105,6 +105,42 @@ def plain_encode(values, physical_type, type_length=0):
     return np.ascontiguousarray(values, dtype=abi.numpy_dtype(physical_type)).tobytes()
 
 
+def dlba_encode(values):
+    """DeltaLengthByteArrayValuesWriter.getBytes (deltalengthbytearray/DeltaLengthByteArrayValuesWriter.java:77-86):
+    DELTA_BINARY_PACKED int lengths (128 / 4), then the concatenated bytes."""
+    vals = [bytes(b) for b in values]
+    lens = np.array([len(b) for b in vals], dtype=np.int32)
+    return delta_encode(lens, abi.INT32) + b"".join(vals)
+
+
+def dba_encode(values):
+    """DeltaByteArrayWriter.writeBytes / getBytes (deltastrings/DeltaByteArrayWriter.java:56-58, 90-100):
+    prefix lengths shared with the previous value (DELTA_BINARY_PACKED), then the suffixes as
+    DELTA_LENGTH_BYTE_ARRAY. `previous` starts empty on every page (reset :65-70)."""
+    prev = b""
+    prefixes, suffixes = [], []
+    for b in values:
+        b = bytes(b)
+        n = min(len(prev), len(b))
+        i = 0
+        while i < n and prev[i] == b[i]:
+            i += 1
+        prefixes.append(i)
+        suffixes.append(b[i:])
+        prev = b
+    return delta_encode(np.array(prefixes, dtype=np.int32), abi.INT32) + dlba_encode(suffixes)
+
+
+def bss_encode(values, physical_type, type_length=0):
+    """ByteStreamSplitValuesWriter: byte k of value i goes to stream k at index i."""
+    w = abi.elem_width(physical_type, type_length)
+    if physical_type in (abi.FIXED_LEN_BYTE_ARRAY, abi.INT96):
+        raw = np.frombuffer(b"".join(bytes(b)[:w].ljust(w, b"\0") for b in values), dtype=np.uint8)
+    else:
+        raw = np.ascontiguousarray(values, dtype=abi.numpy_dtype(physical_type)).view(np.uint8)
+    return np.ascontiguousarray(raw.reshape(-1, w).T).tobytes()
+
+
 def dictionary_encode(values):
     """Ids in first-appearance order, as DictionaryValuesWriter assigns them."""
     values = np.asarray(values)
@@ -220,6 +256,12 @@ def write_column_chunk(physical_type, values, encoding, *, def_levels=None, rep_
             data = plain_encode(values[v0:v1], physical_type, type_length)
         elif encoding == abi.DELTA_BINARY_PACKED:
             data = delta_encode(values[v0:v1], physical_type, delta_block, delta_miniblocks)
+        elif encoding == abi.DELTA_LENGTH_BYTE_ARRAY:
+            data = dlba_encode(values[v0:v1])
+        elif encoding == abi.DELTA_BYTE_ARRAY:
+            data = dba_encode(values[v0:v1])
+        elif encoding == abi.BYTE_STREAM_SPLIT:
+            data = bss_encode(values[v0:v1], physical_type, type_length)
         else:
             raise ValueError(f"writer does not support encoding {encoding}")
         rls = _level_section(rl[s:e], max_rep, version)

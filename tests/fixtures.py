@@ -33,6 +33,9 @@ def load_chunk(name, c):
         data = exp[key + "_bytes"].tobytes()
         offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
         expected = [data[offs[i]:offs[i + 1]] for i in range(len(lens))]
+    elif ptype in (abi.FIXED_LEN_BYTE_ARRAY, abi.INT96):
+        w = abi.elem_width(ptype, c["type_length"])
+        expected = np.ascontiguousarray(exp[key]).reshape(-1, w).view((np.void, w)).reshape(-1)
     else:
         expected = exp[key]
     ch.values = expected

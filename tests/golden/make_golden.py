@@ -87,6 +87,10 @@ def describe(path_in, name, rg_table_reader):
                 lens = np.array([len(x) for x in b], dtype=np.int64)
                 expected[key + "_lens"] = lens
                 expected[key + "_bytes"] = np.frombuffer(b"".join(b), dtype=np.uint8) if b else np.zeros(0, np.uint8)
+            elif ptype in ("FIXED_LEN_BYTE_ARRAY", "INT96"):
+                w = col.length if ptype == "FIXED_LEN_BYTE_ARRAY" else 12
+                b = b"".join(bytes(x.as_py()) for x in vals)
+                expected[key] = np.frombuffer(b, dtype=np.uint8).reshape(-1, w) if b else np.zeros((0, w), np.uint8)
             elif ptype == "BOOLEAN":
                 expected[key] = np.array(vals.to_pylist(), dtype=np.uint8)
             else:
@@ -140,6 +144,54 @@ def write_arrow_fixtures():
     return out
 
 
+def write_arrow_binary_fixtures():
+    """BYTE_ARRAY / FIXED_LEN_BYTE_ARRAY columns and the remaining value encodings:
+    PLAIN and dictionary strings, DELTA_LENGTH_BYTE_ARRAY, DELTA_BYTE_ARRAY (sorted keys with
+    shared prefixes), BYTE_STREAM_SPLIT (float/double/int32/int64/FLBA), FLBA dictionary."""
+    rng = np.random.default_rng(2025)
+    out = []
+    n = 8000
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", dtype=np.uint8)
+    def rand_str(lo, hi):
+        return alpha[rng.integers(0, alpha.size, size=rng.integers(lo, hi + 1))].tobytes().decode()
+    words = [rand_str(0, 24) for _ in range(300)]
+    runs = np.minimum(rng.zipf(1.5, size=n), 200)
+    ids = np.repeat(rng.integers(0, len(words), size=n), runs)[:n]
+    valid = rng.random(n) > 0.1
+    keys = sorted(f"https://example.org/item/{rng.integers(0, 10**6):07d}/{rand_str(0, 6)}" for _ in range(n))
+    fl = [rng.integers(0, 256, size=16, dtype=np.uint8).tobytes() for _ in range(50)]
+    t = pa.table({
+        "plain_str": pa.array([rand_str(4, 32) for _ in range(n)]),
+        "opt_plain_str": pa.array([rand_str(0, 40) if v else None for v in valid]),
+        "dict_str": pa.array([words[i] for i in ids]),
+        "opt_dict_str": pa.array([words[i] if v else None for i, v in zip(ids, valid)]),
+        "dlba_str": pa.array([rand_str(0, 60) for _ in range(n)]),
+        "dba_keys": pa.array(keys),
+        "opt_dba_str": pa.array([words[i] if v else None for i, v in zip(ids, valid)]),
+        "bss_f32": pa.array(rng.standard_normal(n).astype(np.float32)),
+        "bss_f64": pa.array(rng.standard_normal(n)),
+        "opt_bss_f64": pa.array(rng.standard_normal(n), mask=~valid),
+        "bss_i32": pa.array(rng.integers(-2**31, 2**31, size=n).astype(np.int32)),
+        "bss_i64": pa.array(rng.integers(-2**40, 2**40, size=n)),
+        "bss_flba": pa.array([fl[i % 50] for i in ids], type=pa.binary(16)),
+        "dict_flba": pa.array([fl[i % 50] for i in ids], type=pa.binary(16)),
+        "plain_flba": pa.array([rng.integers(0, 256, size=5, dtype=np.uint8).tobytes() for _ in range(n)],
+                               type=pa.binary(5)),
+    })
+    enc = {"plain_str": "PLAIN", "opt_plain_str": "PLAIN", "dlba_str": "DELTA_LENGTH_BYTE_ARRAY",
+           "dba_keys": "DELTA_BYTE_ARRAY", "opt_dba_str": "DELTA_BYTE_ARRAY", "bss_f32": "BYTE_STREAM_SPLIT",
+           "bss_f64": "BYTE_STREAM_SPLIT", "opt_bss_f64": "BYTE_STREAM_SPLIT", "bss_i32": "BYTE_STREAM_SPLIT",
+           "bss_i64": "BYTE_STREAM_SPLIT", "bss_flba": "BYTE_STREAM_SPLIT", "plain_flba": "PLAIN"}
+    for ver in ("1.0", "2.0"):
+        name = f"arrow_binary_v{ver[0]}"
+        path = os.path.join(HERE, name + ".parquet")
+        pq.write_table(t, path, data_page_version=ver, compression="NONE",
+                       use_dictionary=["dict_str", "opt_dict_str", "dict_flba"], column_encoding=enc,
+                       data_page_size=16 * 1024, row_group_size=n, write_page_index=False)
+        out.append(name)
+    return out
+
+
 def main():
     manifest = {}
     for rel in REF_FILES:
@@ -148,7 +200,7 @@ def main():
         dst = os.path.join(HERE, name + ".parquet")
         shutil.copyfile(src, dst)
         manifest[name] = {"source": f"reference:{rel}", "chunks": describe(dst, name, None)}
-    for name in write_arrow_fixtures():
+    for name in write_arrow_fixtures() + write_arrow_binary_fixtures():
         manifest[name] = {"source": "pyarrow " + pa.__version__, "chunks": describe(os.path.join(HERE, name + ".parquet"),
                                                                                    name, None)}
     with open(os.path.join(HERE, "manifest.json"), "w") as f:

@@ -33,3 +33,8 @@ class JavaRandom:
         v = (self.next(32) << 32) + self.next(32)
         v &= (1 << 64) - 1
         return v - (1 << 64) if v >> 63 else v
+
+    def nextFloat(self):
+        """next(24) / (float)(1 << 24) (JDK 8+)."""
+        import numpy as np
+        return np.float32(self.next(24)) / np.float32(1 << 24)

@@ -294,3 +294,99 @@ def test_dictionary_page_encoding_must_be_plain():  # PlainValuesDictionary.java
     ch.dict_encoding = abi.RLE
     res = pqref.decode_batch(writer.build_batch([ch]))
     assert res.code == abi.ERR_DICT_ENCODING
+
+
+# ---- TestDeltaLengthByteArray / TestDeltaByteArray (deltalengthbytearray/, deltastrings/) ------------------------
+
+def _decode_bytes(enc, values, ptype=abi.BYTE_ARRAY, **kw):
+    ch = writer.write_column_chunk(ptype, values, enc, **kw)
+    return pqref.decode_batch(writer.build_batch([ch]))
+
+
+def test_dlba_serialization():  # TestDeltaLengthByteArray.testSerialization / testLengths
+    vals = [b"parquet", b"hadoop", b"mapreduce"]
+    data = writer.dlba_encode(vals)
+    lens, consumed = pqref.delta_decode(data)
+    assert list(lens) == [7, 6, 9] and data[consumed:] == b"parquethadoopmapreduce"
+    res = _decode_bytes(abi.DELTA_LENGTH_BYTE_ARRAY, vals)
+    assert res.code == 0 and res.columns[0]["values"] == vals
+
+
+def test_dba_serialization_and_lengths():  # TestDeltaByteArray.testSerialization / testLengths (:35-90)
+    vals = [b"parquet-mr", b"parquet", b"parquet-format"]
+    data = writer.dba_encode(vals)
+    prefix, c1 = pqref.delta_decode(data)
+    assert list(prefix) == [0, 7, 7]
+    suffix, _ = pqref.delta_decode(data[c1:])
+    assert list(suffix) == [10, 0, 7]
+    res = _decode_bytes(abi.DELTA_BYTE_ARRAY, vals)
+    assert res.code == 0 and res.columns[0]["values"] == vals
+
+
+@pytest.mark.parametrize("enc", [abi.DELTA_LENGTH_BYTE_ARRAY, abi.DELTA_BYTE_ARRAY, abi.PLAIN])
+def test_binary_random_strings(enc):  # testRandomStrings: 10,000 strings of <= 32 chars
+    rng = np.random.default_rng(10)
+    vals = [bytes(rng.integers(97, 123, size=rng.integers(0, 33), dtype=np.uint8)) for _ in range(10000)]
+    vals.sort()
+    res = _decode_bytes(enc, vals, page_rows=3000)
+    assert res.code == 0 and res.columns[0]["values"] == vals
+
+
+def test_dba_prefix_longer_than_previous_fails():
+    """arraycopy(previous, 0, out, 0, prefixLength) with prefixLength > previous.length (:70-73)."""
+    data = writer.delta_encode(np.array([3], dtype=np.int32), abi.INT32) + writer.dlba_encode([b"x"])
+    ch = writer.write_column_chunk(abi.BYTE_ARRAY, [b"abcx"], abi.DELTA_BYTE_ARRAY)
+    ch.pages[0].body = data
+    res = pqref.decode_batch(writer.build_batch([ch]))
+    assert res.status == (abi.ERR_CORRUPT, 0, 0)
+
+
+def test_dlba_short_data_is_eof():  # in.slice(length) past the end: "Failed to read N bytes"
+    ch = writer.write_column_chunk(abi.BYTE_ARRAY, [b"abc", b"defgh"], abi.DELTA_LENGTH_BYTE_ARRAY)
+    ch.pages[0].body = ch.pages[0].body[:-2]
+    res = pqref.decode_batch(writer.build_batch([ch]))
+    assert res.status == (abi.ERR_EOF, 0, 1)
+
+
+# ---- ByteStreamSplitValuesReaderTest (bytestreamsplit/ByteStreamSplitValuesReaderTest.java) ------------------------
+
+def _bss_page(ptype, body, n, type_length=0):
+    ch = writer.write_column_chunk(ptype, np.zeros(n, dtype=abi.numpy_dtype(ptype)) if ptype != abi.FIXED_LEN_BYTE_ARRAY
+                                   else [b"\0" * type_length] * n, abi.BYTE_STREAM_SPLIT, type_length=type_length)
+    ch.pages[0].body = bytes(body)
+    return pqref.decode_batch(writer.build_batch([ch]))
+
+
+def test_bss_float_small_buffer():  # FloatTest.testSmallBuffer (:64-81)
+    body = [0x40, 0x00, 0x80, 0x40, 0x05, 0x84, 0xc5, 0xbd, 0x32, 0xc2, 0x41, 0x42]
+    res = _bss_page(abi.FLOAT, body, 3)
+    assert res.code == 0
+    assert list(res.columns[0]["values"]) == [np.float32(-98.62548828125), np.float32(23.62744140625),
+                                              np.float32(44.62939453125)]
+
+
+def test_bss_double_single_element():  # DoubleTest.testSingleElement
+    res = _bss_page(abi.DOUBLE, [0xFE, 0xFF, 0xFF, 0x0D, 0xA8, 0x77, 0xD2, 0x40], 1)
+    assert res.code == 0 and float(res.columns[0]["values"][0]) == 18910.62585449218
+
+
+def test_bss_int_single_element():  # IntegerTest.testSingleElement
+    res = _bss_page(abi.INT32, [0x12, 0x34, 0x56, 0x78], 1)
+    assert res.code == 0 and int(res.columns[0]["values"][0]) == 0x78563412
+
+
+def test_bss_float_random_java(  # FloatTest.testRandomInput: java.util.Random(1337).nextFloat() * 1024
+):
+    r = JavaRandom(1337)
+    vals = np.array([r.nextFloat() * np.float32(1024.0) for _ in range(256)], dtype=np.float32)
+    res = _decode_bytes(abi.BYTE_STREAM_SPLIT, vals, ptype=abi.FLOAT)
+    assert res.code == 0 and np.array_equal(res.columns[0]["values"].view(np.uint32), vals.view(np.uint32))
+
+
+def test_bss_errors():
+    # available % elementSize != 0 -> "Invalid ByteStreamSplit stream" at init (:74-79)
+    assert _bss_page(abi.FLOAT, [0] * 7, 2).status == (abi.ERR_CORRUPT, 0, 0)
+    # more encoded values than the page's value count (:83-88)
+    assert _bss_page(abi.FLOAT, [0] * 12, 2).status == (abi.ERR_CORRUPT, 0, 0)
+    # reading past the encoded values: "Byte-stream data was already exhausted." (:43-46)
+    assert _bss_page(abi.FLOAT, [0] * 4, 2).status == (abi.ERR_EOF, 0, 1)
