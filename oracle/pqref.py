@@ -105,7 +105,19 @@ class OracleResult:
 
 
 def decode_batch(batch, binary_capacity=None):
-    """Decode a writer.PageBatch with the oracle: per column dict(values, def_levels, rep_levels)."""
+    """Decode a writer.PageBatch with the oracle: per column dict(values, def_levels, rep_levels).
+    BYTE_ARRAY columns get `binary_capacity` bytes (default: 8x the batch, at least 16 MiB); when
+    that is short (dictionary expansion) the decode is repeated with 8x more, up to 1 GiB."""
+    cap = binary_capacity or max(1 << 24, 8 * int(len(batch.data)))
+    while True:
+        res = _decode_batch(batch, cap)
+        if res.code != abi.ERR_INVALID_ARG or binary_capacity or cap >= (1 << 30) or \
+                not any(cd["physical_type"] == abi.BYTE_ARRAY for cd in batch.columns):
+            return res
+        cap *= 8
+
+
+def _decode_batch(batch, binary_capacity):
     cols = (abi.ColumnDesc * max(1, len(batch.columns)))()
     keep = []
     for i, cd in enumerate(batch.columns):
@@ -125,7 +137,7 @@ def decode_batch(batch, binary_capacity=None):
         c.rep_levels = rl.ctypes.data if cd["max_rep"] > 0 else None
         c.levels_capacity = n_slots
         if cd["physical_type"] == abi.BYTE_ARRAY:
-            cap = binary_capacity or max(1 << 24, 8 * int(len(batch.data)))
+            cap = binary_capacity
             bd = np.zeros(max(cap, 1), dtype=np.uint8)
             keep.append(bd)
             c.binary_data = bd.ctypes.data

@@ -83,7 +83,10 @@ int elem_width(int t, int tl) {
 }
 
 // Kernel classes, in launch order after the level pass.
-enum Cls { C_DICT4 = 0, C_DICT8, C_PLAIN, C_BOOL, C_DELTA4, C_DELTA8, C_NCLS };
+//   C_IDS   dictionary pages whose values are not 4 / 8 bytes (BYTE_ARRAY, FLBA, INT96): ids first
+//   C_BINP  PLAIN BYTE_ARRAY          C_DLBA  DELTA_LENGTH_BYTE_ARRAY      C_BSS  BYTE_STREAM_SPLIT
+enum Cls { C_DICT4 = 0, C_DICT8, C_IDS, C_PLAIN, C_BOOL, C_DELTA4, C_DELTA8, C_BSS, C_BINP, C_DLBA, C_NCLS };
+constexpr int N_DICT_CLS = 3;  // C_DICT4, C_DICT8, C_IDS: run-record walk + chunk expansion
 
 struct HostErr {
   int page;
@@ -105,7 +108,18 @@ struct pqg_plan {
   DevBuf pstat, flags;                // per page: {records, values} and ready epoch (fused dictionary kernel)
   uint32_t epoch = 0;
   bool dict_fused = true;
-  uint32_t chunk_off[2] = {0, 0}, chunk_n[2] = {0, 0};  // C_DICT4, C_DICT8 ranges in `chunks`
+  uint32_t chunk_off[N_DICT_CLS] = {0, 0, 0}, chunk_n[N_DICT_CLS] = {0, 0, 0};  // ranges in `chunks`
+  // BYTE_ARRAY / fixed-width-dictionary scratch (ColumnDev::blen, bsrc, dict_len, dict_src, block_sums,
+  // bin_total), dictionary walks, post-passes, offset-scan blocks, copy chunks
+  DevBuf bscratch, bin_lists, bin_blocks, bin_chunks;
+  uint64_t blen_bytes = 0;            // leading part of bscratch cleared before every launch
+  int n_dict_walk = 0, n_bind = 0, n_fixd = 0, n_bin_cols = 0;
+  int off_dict_walk = 0, off_bind = 0, off_fixd = 0, off_bin_cols = 0;  // into bin_lists
+  uint32_t n_bin_blocks = 0, n_bin_chunks = 0;
+  std::vector<uint64_t> bin_total_off;  // per column: byte offset of its bin_total in bscratch (or ~0)
+  std::vector<uint64_t> bin_capacity;
+  std::vector<int> col_first_page;
+  std::vector<void*> empty_bin_values; // BYTE_ARRAY columns without slots: offsets[0] = 0
   std::vector<PageWork> h_work;
   std::vector<int> cls_off, cls_n;  // into lists
   int levels_off = 0, levels_n = 0;
@@ -233,6 +247,8 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     d.max_def = c.max_def;
     d.elem_width = elem_width(c.physical_type, c.type_length);
     d.values = c.values;
+    d.binary_data = c.binary_data;
+    d.binary_capacity = c.physical_type == PQG_BYTE_ARRAY ? c.binary_capacity : 0;
     d.def_levels = c.max_def > 0 ? c.def_levels : nullptr;
     d.rep_levels = c.max_rep > 0 ? c.rep_levels : nullptr;
     P->col_nullable[(size_t)i] = (c.max_def > 0 || c.max_rep > 0) ? 1 : 0;
@@ -243,6 +259,8 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
         col_err[(size_t)i] = PQG_ERR_DICT_ENCODING;
       } else if (c.physical_type == PQG_BOOLEAN) {
         col_err[(size_t)i] = PQG_ERR_UNSUPPORTED;
+      } else if (c.physical_type == PQG_FIXED_LEN_BYTE_ARRAY && c.type_length <= 0) {
+        col_err[(size_t)i] = PQG_ERR_CORRUPT;  // PlainBinaryDictionary :106 checkArgument(length > 0)
       } else if ((uint64_t)c.dict_offset + c.dict_size > n_bytes) {
         col_err[(size_t)i] = PQG_ERR_INVALID_ARG;
       } else if (d.elem_width > 0 && (uint64_t)c.dict_num_values * (uint64_t)d.elem_width > c.dict_size) {
@@ -318,13 +336,15 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
       case PQG_RLE_DICTIONARY:
         if (c.dict_offset < 0) herr = PQG_ERR_NO_DICTIONARY;
         else if (t == PQG_BOOLEAN) herr = PQG_ERR_UNSUPPORTED;
+        else if (t == PQG_BYTE_ARRAY) { cls = C_IDS; w.bin_kind = pqg::BIN_DICT; }
         else if (ew == 8) cls = C_DICT8;
         else if (ew == 4) cls = C_DICT4;
-        else herr = PQG_ERR_UNSUPPORTED;  // BYTE_ARRAY / INT96 / FLBA dictionaries: next row
+        else if (ew > 0) cls = C_IDS;      // FLBA / INT96: ids, then k_gather_fixed
+        else herr = PQG_ERR_UNSUPPORTED;
         break;
       case PQG_PLAIN:
         if (t == PQG_BOOLEAN) cls = C_BOOL;
-        else if (t == PQG_BYTE_ARRAY) herr = PQG_ERR_UNSUPPORTED;  // next row
+        else if (t == PQG_BYTE_ARRAY) { cls = C_BINP; w.bin_kind = pqg::BIN_PLAIN; }
         else if (ew > 0) cls = C_PLAIN;
         else herr = PQG_ERR_UNSUPPORTED;
         break;
@@ -333,8 +353,19 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
         else if (t == PQG_INT32) cls = C_DELTA4;
         else herr = PQG_ERR_UNSUPPORTED;
         break;
+      case PQG_DELTA_LENGTH_BYTE_ARRAY:
+        if (t == PQG_BYTE_ARRAY) { cls = C_DLBA; w.bin_kind = pqg::BIN_DLBA; }
+        else herr = PQG_ERR_UNSUPPORTED;   // Encoding.java :204-207
+        break;
+      case PQG_BYTE_STREAM_SPLIT:
+        if (t == PQG_FLOAT || t == PQG_DOUBLE || t == PQG_INT32 || t == PQG_INT64 ||
+            (t == PQG_FIXED_LEN_BYTE_ARRAY && ew > 0))
+          cls = C_BSS;
+        else
+          herr = PQG_ERR_UNSUPPORTED;      // Encoding.java :130-143
+        break;
       default:
-        herr = PQG_ERR_UNSUPPORTED;
+        herr = PQG_ERR_UNSUPPORTED;        // DELTA_BYTE_ARRAY: next row
     }
     if (herr) {
       P->host_errs.push_back(HostErr{p, 0, 2, herr});
@@ -344,12 +375,56 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     cls_lists[(size_t)cls].push_back(p);
   }
   for (int i = 0; i < n_cols; i++) P->col_required_values[(size_t)i] = val_acc[(size_t)i];
+  P->col_first_page = col_first_page;
+  // ---- BYTE_ARRAY and fixed-width dictionary columns: scratch layout, dictionary walks,
+  // post-passes, offset-scan blocks and copy chunks
+  std::vector<int32_t> dict_walk, bind, fixd, bin_cols;
+  std::vector<uint64_t> bin_blocks, bin_chunks;
+  std::vector<uint64_t> blen_off((size_t)std::max(n_cols, 1), ~0ull), bsrc_off = blen_off, dlen_off = blen_off,
+      dsrc_off = blen_off, bsum_off = blen_off;
+  P->bin_total_off.assign((size_t)std::max(n_cols, 1), ~0ull);
+  P->bin_capacity.assign((size_t)std::max(n_cols, 1), 0);
+  uint64_t sc = 0;
+  auto take = [&](uint64_t bytes) { uint64_t o = sc; sc = (sc + bytes + 255) & ~uint64_t(255); return o; };
+  std::vector<uint8_t> needs_ids((size_t)std::max(n_cols, 1), 0);
+  for (int p : cls_lists[C_IDS]) needs_ids[(size_t)P->h_work[(size_t)p].column] = 1;
+  for (int i = 0; i < n_cols; i++) {  // blen first: the part cleared before every launch
+    if (cols[i].physical_type == PQG_BYTE_ARRAY || needs_ids[(size_t)i]) blen_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
+  }
+  P->blen_bytes = sc;
+  for (int i = 0; i < n_cols; i++) {
+    if (cols[i].physical_type != PQG_BYTE_ARRAY) continue;
+    bin_cols.push_back(i);
+    P->bin_capacity[(size_t)i] = cols[i].binary_capacity;
+    bsrc_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
+    const uint64_t nb = (slot_acc[(size_t)i] + pqg::SCAN_BLOCK - 1) / pqg::SCAN_BLOCK;
+    bsum_off[(size_t)i] = take(8 * (nb + 1));
+    P->bin_total_off[(size_t)i] = take(8);
+    for (uint64_t b = 0; b < nb; b++) bin_blocks.push_back(((uint64_t)(uint32_t)i << 32) | b);
+    if (nb == 0 && cols[i].values) P->empty_bin_values.push_back(cols[i].values);
+    if (cols[i].dict_offset >= 0 && !col_err[(size_t)i]) {
+      dict_walk.push_back(i);
+      dlen_off[(size_t)i] = take(4 * ((uint64_t)cols[i].dict_num_values + 1));
+      dsrc_off[(size_t)i] = take(4 * ((uint64_t)cols[i].dict_num_values + 1));
+    }
+  }
+  for (int k : {C_IDS, C_BINP, C_DLBA})
+    for (int p : cls_lists[(size_t)k]) {
+      const PageWork& w = P->h_work[(size_t)p];
+      if (k == C_IDS && cols[w.column].physical_type != PQG_BYTE_ARRAY) {
+        fixd.push_back(p);
+        continue;
+      }
+      if (k == C_IDS) bind.push_back(p);
+      const uint32_t nch = (w.num_slots + pqg::BIN_CHUNK - 1) / pqg::BIN_CHUNK;
+      for (uint32_t j = 0; j < nch; j++) bin_chunks.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
+    }
   // ---- dictionary pages: run-record capacity (a run covers >= 1 value and its header takes
   // >= 1 byte) and output chunks (slots [j*CH, (j+1)*CH) of the page, upper bound from the slot count)
   std::vector<uint64_t> chunk_list;
   uint64_t rec_total = 0;
   uint32_t chunk_total = 0;
-  for (int k = C_DICT4; k <= C_DICT8; k++) {
+  for (int k = C_DICT4; k < C_DICT4 + N_DICT_CLS; k++) {
     P->chunk_off[k - C_DICT4] = (uint32_t)chunk_list.size();
     for (int p : cls_lists[(size_t)k]) {
       PageWork& w = P->h_work[(size_t)p];
@@ -383,6 +458,14 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     cps.push_back((int32_t)cp.size());
   }
   P->n_scan_cols = (int)cps.size() - 1;
+  // bin_lists: [dictionary walks (columns)][BYTE_ARRAY dictionary pages][FLBA/INT96 dictionary pages][BYTE_ARRAY columns]
+  std::vector<int32_t> bl;
+  P->off_dict_walk = (int)bl.size(); P->n_dict_walk = (int)dict_walk.size(); bl.insert(bl.end(), dict_walk.begin(), dict_walk.end());
+  P->off_bind = (int)bl.size(); P->n_bind = (int)bind.size(); bl.insert(bl.end(), bind.begin(), bind.end());
+  P->off_fixd = (int)bl.size(); P->n_fixd = (int)fixd.size(); bl.insert(bl.end(), fixd.begin(), fixd.end());
+  P->off_bin_cols = (int)bl.size(); P->n_bin_cols = (int)bin_cols.size(); bl.insert(bl.end(), bin_cols.begin(), bin_cols.end());
+  P->n_bin_blocks = (uint32_t)bin_blocks.size();
+  P->n_bin_chunks = (uint32_t)bin_chunks.size();
   // ---- upload
   hipStream_t s = ctx->stream;
   bool ok = P->work.ensure(sizeof(PageWork) * P->h_work.size()) == hipSuccess &&
@@ -390,7 +473,11 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
             P->lists.ensure(sizeof(int32_t) * std::max<size_t>(flat.size(), 1)) == hipSuccess &&
             P->col_pages.ensure(sizeof(int32_t) * std::max<size_t>(cp.size(), 1)) == hipSuccess &&
             P->col_page_start.ensure(sizeof(int32_t) * cps.size()) == hipSuccess &&
-            P->err.ensure(sizeof(uint64_t) * 3 * (size_t)std::max(n_pages, 1)) == hipSuccess &&
+            P->err.ensure(sizeof(uint64_t) * 3 * (size_t)(n_pages + std::max(n_cols, 1))) == hipSuccess &&
+            P->bscratch.ensure(std::max<uint64_t>(sc, 256)) == hipSuccess &&
+            P->bin_lists.ensure(sizeof(int32_t) * std::max<size_t>(bl.size(), 1)) == hipSuccess &&
+            P->bin_blocks.ensure(sizeof(uint64_t) * std::max<size_t>(bin_blocks.size(), 1)) == hipSuccess &&
+            P->bin_chunks.ensure(sizeof(uint64_t) * std::max<size_t>(bin_chunks.size(), 1)) == hipSuccess &&
             P->err_count.ensure(sizeof(uint32_t) * 4) == hipSuccess &&
             P->rec.ensure(sizeof(uint64_t) * (rec_total + 16)) == hipSuccess &&  // k_dict_fill reads 9 ahead
             P->chunk_run.ensure(sizeof(uint32_t) * std::max<uint32_t>(chunk_total, 1)) == hipSuccess &&
@@ -402,6 +489,26 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     const char* e = getenv("PQG_DICT_SPLIT");  // A/B switch: walk and tiles as two launches
     P->dict_fused = !(e && e[0] == '1');
   }
+  {
+    uint8_t* scb = (uint8_t*)P->bscratch.p;
+    auto at = [&](uint64_t o) -> void* { return o == ~0ull ? nullptr : (void*)(scb + o); };
+    for (int i = 0; i < n_cols; i++) {
+      ColumnDev& d = hc[(size_t)i];
+      d.blen = (uint32_t*)at(blen_off[(size_t)i]);
+      d.bsrc = (uint32_t*)at(bsrc_off[(size_t)i]);
+      d.dict_len = (uint32_t*)at(dlen_off[(size_t)i]);
+      d.dict_src = (uint32_t*)at(dsrc_off[(size_t)i]);
+      d.block_sums = (uint64_t*)at(bsum_off[(size_t)i]);
+      d.bin_total = (uint64_t*)at(P->bin_total_off[(size_t)i]);
+      d.n_slots = slot_acc[(size_t)i];
+    }
+  }
+  if (!bl.empty())
+    ok = ok && hipMemcpyAsync(P->bin_lists.p, bl.data(), sizeof(int32_t) * bl.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!bin_blocks.empty())
+    ok = ok && hipMemcpyAsync(P->bin_blocks.p, bin_blocks.data(), sizeof(uint64_t) * bin_blocks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!bin_chunks.empty())
+    ok = ok && hipMemcpyAsync(P->bin_chunks.p, bin_chunks.data(), sizeof(uint64_t) * bin_chunks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   if (!chunk_list.empty())
     ok = ok && hipMemcpyAsync(P->chunks.p, chunk_list.data(), sizeof(uint64_t) * chunk_list.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   ok = ok && hipMemcpyAsync(P->work.p, P->h_work.data(), sizeof(PageWork) * P->h_work.size(), hipMemcpyHostToDevice, s) == hipSuccess;
@@ -418,7 +525,8 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
   }
   P->kernels = (P->levels_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
   for (int k = 0; k < C_NCLS; k++) P->kernels += P->cls_n[(size_t)k] ? 1 : 0;
-  for (int i = 0; i < 2; i++) P->kernels += P->chunk_n[i] ? 1 : 0;  // k_dict_expand
+  P->kernels += (P->n_dict_walk ? 1 : 0) + (P->n_bind ? 1 : 0) + (P->n_fixd ? 1 : 0) + (P->n_bin_blocks ? 3 : 0) +
+                (P->n_bin_chunks ? 1 : 0);
   *out = P;
   return PQG_OK;
 }
@@ -434,7 +542,11 @@ int pqg_plan_launch(pqg_plan* P) {
   PageWork* work = (PageWork*)P->work.p;
   const ColumnDev* cols = (const ColumnDev*)P->cols.p;
   const int32_t* lists = (const int32_t*)P->lists.p;
-  if (hipMemsetAsync(err, 0xFF, sizeof(uint64_t) * 3 * (size_t)std::max(P->n_pages, 1), s) != hipSuccess) return PQG_ERR_HIP;
+  if (hipMemsetAsync(err, 0xFF, sizeof(uint64_t) * 3 * (size_t)(P->n_pages + std::max(P->n_cols, 1)), s) != hipSuccess)
+    return PQG_ERR_HIP;
+  if (P->blen_bytes && hipMemsetAsync(P->bscratch.p, 0, P->blen_bytes, s) != hipSuccess) return PQG_ERR_HIP;
+  for (void* v : P->empty_bin_values)
+    if (hipMemsetAsync(v, 0, sizeof(int64_t), s) != hipSuccess) return PQG_ERR_HIP;
   if (hipMemsetAsync(ecount, 0, sizeof(uint32_t) * 4, s) != hipSuccess) return PQG_ERR_HIP;
   if (++P->epoch == 0) {  // page ready flags compare against the launch epoch; reset on wrap
     P->epoch = 1;
@@ -447,6 +559,10 @@ int pqg_plan_launch(pqg_plan* P) {
     if (e == hipSuccess)
       e = pqg::launch_scan(s, work, (const int32_t*)P->col_pages.p, (const int32_t*)P->col_page_start.p, P->n_scan_cols);
   }
+  const int32_t* bl = (const int32_t*)P->bin_lists.p;
+  if (e == hipSuccess && P->n_dict_walk)  // BYTE_ARRAY dictionary entries (PlainBinaryDictionary ctor)
+    e = pqg::launch_bin_walk(s, P->d_bytes, P->n_bytes, work, cols, bl + P->off_dict_walk, P->n_dict_walk, 1, P->n_pages,
+                             err, ecount);
   for (int k = 0; k < C_NCLS && e == hipSuccess; k++) {
     int n = P->cls_n[(size_t)k];
     if (!n) continue;
@@ -460,12 +576,35 @@ int pqg_plan_launch(pqg_plan* P) {
                              (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused, err, ecount);
         break;
       }
+      case C_IDS: {
+        const int i = k - C_DICT4;
+        e = pqg::launch_dict_ids(s, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
+                                 (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->chunk_off[i],
+                                 P->chunk_n[i], (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused,
+                                 err, ecount);
+        break;
+      }
+      case C_BSS: e = pqg::launch_bss(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_BINP:
+        e = pqg::launch_bin_walk(s, P->d_bytes, P->n_bytes, work, cols, l, n, 0, P->n_pages, err, ecount);
+        break;
+      case C_DLBA: e = pqg::launch_dlba_lengths(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_PLAIN: e = pqg::launch_plain(0, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_BOOL: e = pqg::launch_plain(1, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_DELTA4: e = pqg::launch_delta(4, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_DELTA8: e = pqg::launch_delta(8, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
     }
   }
+  // post-passes: dictionary ids -> BYTE_ARRAY entries / fixed-width entries; offsets; value bytes
+  if (e == hipSuccess && P->n_bind) e = pqg::launch_bin_dict_map(s, work, cols, bl + P->off_bind, P->n_bind);
+  if (e == hipSuccess && P->n_fixd)
+    e = pqg::launch_gather_fixed(s, P->d_bytes, P->n_bytes, work, cols, bl + P->off_fixd, P->n_fixd);
+  if (e == hipSuccess && P->n_bin_blocks)
+    e = pqg::launch_bin_scan(s, cols, bl + P->off_bin_cols, P->n_bin_cols, (const uint64_t*)P->bin_blocks.p,
+                             P->n_bin_blocks);
+  if (e == hipSuccess && P->n_bin_chunks)
+    e = pqg::launch_bin_copy(s, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->bin_chunks.p, P->n_bin_chunks,
+                             err, ecount);
   ctx->last_launched = P;
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }
@@ -489,6 +628,10 @@ int pqg_plan_destroy(pqg_plan* P) {
   P->chunks.release();
   P->pstat.release();
   P->flags.release();
+  P->bscratch.release();
+  P->bin_lists.release();
+  P->bin_blocks.release();
+  P->bin_chunks.release();
   delete P;
   return PQG_OK;
 }
@@ -496,6 +639,8 @@ int pqg_plan_destroy(pqg_plan* P) {
 }  // extern "C"
 
 namespace {
+
+int resolve_page_errors(pqg_plan* P, pqg_status* st, const std::vector<uint64_t>& errs);
 
 // Resolve the first error of a launched plan in (page, value) order.
 // Per page: init errors (rl init < dl init < data init) first; then value errors
@@ -517,15 +662,51 @@ int resolve_errors(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work_out)
   if (hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
   std::vector<uint64_t> errs;
   if (*cnt) {
-    errs.resize(3 * (size_t)std::max(P->n_pages, 1));
+    errs.resize(3 * (size_t)(P->n_pages + std::max(P->n_cols, 1)));
     if (hipMemcpy(errs.data(), P->err.p, sizeof(uint64_t) * errs.size(), hipMemcpyDeviceToHost) != hipSuccess) return PQG_ERR_HIP;
   }
+  int rc = resolve_page_errors(P, st, errs);
+  if (rc) return rc;
+  // BYTE_ARRAY output capacity (API misuse, after the decode errors: values past a decode error
+  // are not meaningful and may inflate the byte count)
+  for (int i = 0; i < P->n_cols; i++) {
+    if (P->bin_total_off[(size_t)i] == ~0ull) continue;
+    uint64_t total = 0;
+    if (hipMemcpy(&total, (uint8_t*)P->bscratch.p + P->bin_total_off[(size_t)i], sizeof(total), hipMemcpyDeviceToHost) !=
+        hipSuccess)
+      return PQG_ERR_HIP;
+    if (total > P->bin_capacity[(size_t)i]) {
+      if (st) {
+        st->code = PQG_ERR_INVALID_ARG;
+        st->page = -1;
+        st->value_index = (int64_t)total;
+        std::snprintf(st->message, sizeof(st->message),
+                      "binary capacity: column %d needs %llu bytes of binary_data (capacity %llu)", i,
+                      (unsigned long long)total, (unsigned long long)P->bin_capacity[(size_t)i]);
+      }
+      return PQG_ERR_INVALID_ARG;
+    }
+  }
+  return PQG_OK;
+}
+
+int resolve_page_errors(pqg_plan* P, pqg_status* st, const std::vector<uint64_t>& errs) {
   if (P->host_errs.empty() && errs.empty()) return PQG_OK;
   std::vector<const HostErr*> herr((size_t)std::max(P->n_pages, 1), nullptr);
   for (const HostErr& h : P->host_errs)
     if (!herr[(size_t)h.page]) herr[(size_t)h.page] = &h;
   for (int p = 0; p < P->n_pages; p++) {
     const HostErr* h = herr[(size_t)p];
+    // device-detected dictionary page errors (BYTE_ARRAY dictionary walk, pseudo page n_pages + column):
+    // the ColumnReaderBase ctor reads the dictionary before the column's first page
+    const int col = P->h_work[(size_t)p].column;
+    if (!errs.empty() && col >= 0 && col < P->n_cols && P->col_first_page[(size_t)col] == p) {
+      const uint64_t d = errs[3 * (size_t)(P->n_pages + col)];
+      if (d != ~0ull) {
+        set_status(st, (int)(d & 0xFF), p, -1, "dictionary page");
+        return (int)(d & 0xFF);
+      }
+    }
     uint64_t init = errs.empty() ? ~0ull : errs[3 * (size_t)p];
     uint64_t lvl = errs.empty() ? ~0ull : errs[3 * (size_t)p + 1];
     uint64_t val = errs.empty() ? ~0ull : errs[3 * (size_t)p + 2];
@@ -595,7 +776,8 @@ int pqg_decode(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, pqg_colum
       if (pages[p].column >= 0 && pages[p].column < n_cols) slots[(size_t)pages[p].column] += pages[p].num_values;
     for (int i = 0; i < n_cols; i++) {
       bool lv = cols[i].max_def > 0 || cols[i].max_rep > 0;
-      if (slots[(size_t)i] > cols[i].values_capacity || (slots[(size_t)i] && !cols[i].values) ||
+      const uint64_t need = slots[(size_t)i] + (cols[i].physical_type == PQG_BYTE_ARRAY ? 1 : 0);  // offsets[n + 1]
+      if (need > cols[i].values_capacity || (need && !cols[i].values) ||
           (lv && ((cols[i].max_def > 0 && cols[i].def_levels) || (cols[i].max_rep > 0 && cols[i].rep_levels)) &&
            slots[(size_t)i] > cols[i].levels_capacity)) {
         set_status(st, PQG_ERR_INVALID_ARG, -1, i, "output capacity");
@@ -631,27 +813,22 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
   hipStream_t s = ctx->stream;
   const uint64_t pad = 1024;
-  // device layout of outputs: per column values | def | rep, 256-B aligned
-  std::vector<uint64_t> off_v((size_t)std::max(n_cols, 1)), off_d((size_t)std::max(n_cols, 1)), off_r((size_t)std::max(n_cols, 1)),
-      nv((size_t)std::max(n_cols, 1), 0);
-  std::vector<uint64_t> slots((size_t)std::max(n_cols, 1), 0);
+  const size_t nc = (size_t)std::max(n_cols, 1);
+  std::vector<uint64_t> slots(nc, 0), page_bytes(nc, 0);
   for (int p = 0; p < n_pages; p++)
-    if (pages[p].column >= 0 && pages[p].column < n_cols) slots[(size_t)pages[p].column] += pages[p].num_values;
-  uint64_t total = 0;
-  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
-  for (int i = 0; i < n_cols; i++) {
-    int w = elem_width(cols[i].physical_type, cols[i].type_length);
-    if (w <= 0) w = 8;
-    off_v[(size_t)i] = total;
-    total = al(total + slots[(size_t)i] * (uint64_t)w);
-    off_d[(size_t)i] = total;
-    if (cols[i].max_def > 0 && cols[i].def_levels) total = al(total + slots[(size_t)i]);
-    off_r[(size_t)i] = total;
-    if (cols[i].max_rep > 0 && cols[i].rep_levels) total = al(total + slots[(size_t)i]);
-  }
-  if (ctx->host_bytes.ensure(n_bytes + pad) != hipSuccess || ctx->host_out.ensure(total + 256) != hipSuccess ||
-      ctx->host_counts.ensure(sizeof(uint32_t) * (size_t)std::max(n_pages, 1)) != hipSuccess ||
-      ctx->pin_in.ensure(n_bytes + pad) != hipSuccess || ctx->pin_out.ensure(total + 256) != hipSuccess) {
+    if (pages[p].column >= 0 && pages[p].column < n_cols) {
+      slots[(size_t)pages[p].column] += pages[p].num_values;
+      page_bytes[(size_t)pages[p].column] += pages[p].size;
+    }
+  // BYTE_ARRAY bytes on the device: PLAIN / DELTA_LENGTH values fit in their pages; dictionary
+  // columns may expand, so the first attempt may come back short and is then re-run once at the
+  // exact size the device counted
+  std::vector<uint64_t> bin_cap(nc, 0);
+  for (int i = 0; i < n_cols; i++)
+    if (cols[i].physical_type == PQG_BYTE_ARRAY)
+      bin_cap[(size_t)i] = page_bytes[(size_t)i] + (cols[i].dict_offset >= 0 ? 2 * (uint64_t)cols[i].dict_size : 0) + 64;
+  if (ctx->host_bytes.ensure(n_bytes + pad) != hipSuccess || ctx->pin_in.ensure(n_bytes + pad) != hipSuccess ||
+      ctx->host_counts.ensure(sizeof(uint32_t) * (size_t)std::max(n_pages, 1)) != hipSuccess) {
     set_status(st, PQG_ERR_HIP, -1, -1, "device buffers");
     return PQG_ERR_HIP;
   }
@@ -660,23 +837,63 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   std::memcpy(ctx->pin_in.p, h_bytes, n_bytes);
   std::memset((uint8_t*)ctx->pin_in.p + n_bytes, 0, pad);
   if (hipMemcpyAsync(ctx->host_bytes.p, ctx->pin_in.p, n_bytes + pad, hipMemcpyHostToDevice, s) != hipSuccess) return PQG_ERR_HIP;
+  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  std::vector<uint64_t> off_v(nc), off_d(nc), off_r(nc), off_b(nc);
   std::vector<pqg_column_desc> dcols(cols, cols + n_cols);
-  uint8_t* dout = (uint8_t*)ctx->host_out.p;
-  for (int i = 0; i < n_cols; i++) {
-    dcols[(size_t)i].values = dout + off_v[(size_t)i];
-    dcols[(size_t)i].values_capacity = slots[(size_t)i];
-    dcols[(size_t)i].def_levels = (cols[i].max_def > 0 && cols[i].def_levels) ? dout + off_d[(size_t)i] : nullptr;
-    dcols[(size_t)i].rep_levels = (cols[i].max_rep > 0 && cols[i].rep_levels) ? dout + off_r[(size_t)i] : nullptr;
-    dcols[(size_t)i].levels_capacity = slots[(size_t)i];
-  }
-  int rc = pqg_decode(ctx, (const uint8_t*)ctx->host_bytes.p, n_bytes, dcols.data(), n_cols, pages, n_pages,
-                      (uint32_t*)ctx->host_counts.p, st);
-  if (rc) return rc;
+  uint64_t total = 0;
+  int rc = PQG_OK;
   pqg_status st2;
-  rc = pqg_sync(ctx, &st2);
+  for (int attempt = 0; attempt < 2; attempt++) {
+    // device layout of outputs: per column values | def | rep | binary bytes, 256-B aligned
+    total = 0;
+    for (int i = 0; i < n_cols; i++) {
+      const bool bin = cols[i].physical_type == PQG_BYTE_ARRAY;
+      int w = elem_width(cols[i].physical_type, cols[i].type_length);
+      if (w <= 0) w = 8;
+      off_v[(size_t)i] = total;
+      total = al(total + (slots[(size_t)i] + (bin ? 1 : 0)) * (uint64_t)w);
+      off_d[(size_t)i] = total;
+      if (cols[i].max_def > 0 && cols[i].def_levels) total = al(total + slots[(size_t)i]);
+      off_r[(size_t)i] = total;
+      if (cols[i].max_rep > 0 && cols[i].rep_levels) total = al(total + slots[(size_t)i]);
+      off_b[(size_t)i] = total;
+      if (bin) total = al(total + bin_cap[(size_t)i]);
+    }
+    if (ctx->host_out.ensure(total + 256) != hipSuccess || ctx->pin_out.ensure(total + 256) != hipSuccess) {
+      set_status(st, PQG_ERR_HIP, -1, -1, "device buffers");
+      return PQG_ERR_HIP;
+    }
+    uint8_t* dout = (uint8_t*)ctx->host_out.p;
+    for (int i = 0; i < n_cols; i++) {
+      const bool bin = cols[i].physical_type == PQG_BYTE_ARRAY;
+      dcols[(size_t)i].values = dout + off_v[(size_t)i];
+      dcols[(size_t)i].values_capacity = slots[(size_t)i] + (bin ? 1 : 0);
+      dcols[(size_t)i].def_levels = (cols[i].max_def > 0 && cols[i].def_levels) ? dout + off_d[(size_t)i] : nullptr;
+      dcols[(size_t)i].rep_levels = (cols[i].max_rep > 0 && cols[i].rep_levels) ? dout + off_r[(size_t)i] : nullptr;
+      dcols[(size_t)i].levels_capacity = slots[(size_t)i];
+      dcols[(size_t)i].binary_data = bin ? dout + off_b[(size_t)i] : nullptr;
+      dcols[(size_t)i].binary_capacity = bin_cap[(size_t)i];
+    }
+    rc = pqg_decode(ctx, (const uint8_t*)ctx->host_bytes.p, n_bytes, dcols.data(), n_cols, pages, n_pages,
+                    (uint32_t*)ctx->host_counts.p, st);
+    if (rc) return rc;
+    rc = pqg_sync(ctx, &st2);
+    if (rc != PQG_ERR_INVALID_ARG || st2.page != -1 || !ctx->last || attempt == 1) break;
+    // binary capacity: size every BYTE_ARRAY column to the byte count the device produced
+    bool grew = false;
+    for (int i = 0; i < n_cols; i++) {
+      const uint64_t o = ctx->last->bin_total_off[(size_t)i];
+      if (o == ~0ull) continue;
+      uint64_t t = 0;
+      if (hipMemcpy(&t, (uint8_t*)ctx->last->bscratch.p + o, sizeof(t), hipMemcpyDeviceToHost) != hipSuccess) return PQG_ERR_HIP;
+      if (t > bin_cap[(size_t)i]) { bin_cap[(size_t)i] = t; grew = true; }
+    }
+    if (!grew) break;
+  }
   for (int i = 0; i < n_cols; i++) cols[i].values_written = dcols[(size_t)i].values_written;
   if (rc && st) *st = st2;
   // device -> pinned -> host arrays (decoded values are valid up to the first error)
+  uint8_t* dout = (uint8_t*)ctx->host_out.p;
   if (hipMemcpyAsync(ctx->pin_out.p, dout, total, hipMemcpyDeviceToHost, s) != hipSuccess) return PQG_ERR_HIP;
   std::vector<uint32_t> counts((size_t)std::max(n_pages, 1));
   if (n_pages && hipMemcpyAsync(counts.data(), ctx->host_counts.p, sizeof(uint32_t) * (size_t)n_pages, hipMemcpyDeviceToHost, s) != hipSuccess)
@@ -686,7 +903,29 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   for (int i = 0; i < n_cols; i++) {
     int w = elem_width(cols[i].physical_type, cols[i].type_length);
     uint64_t n = std::min<uint64_t>(cols[i].values_written, cols[i].values_capacity);
-    if (cols[i].values && n) std::memcpy(cols[i].values, po + off_v[(size_t)i], n * (uint64_t)w);
+    if (cols[i].physical_type == PQG_BYTE_ARRAY) {
+      // offsets[n + 1] and the bytes they span
+      n = std::min<uint64_t>(cols[i].values_written, cols[i].values_capacity ? cols[i].values_capacity - 1 : 0);
+      const int64_t* offs = (const int64_t*)(po + off_v[(size_t)i]);
+      if (cols[i].values && cols[i].values_capacity) std::memcpy(cols[i].values, offs, (n + 1) * sizeof(int64_t));
+      const uint64_t nb = (uint64_t)offs[n];
+      if (nb > cols[i].binary_capacity) {
+        if (rc == PQG_OK) {
+          rc = PQG_ERR_INVALID_ARG;
+          if (st) {
+            st->code = rc;
+            st->page = -1;
+            st->value_index = (int64_t)nb;
+            std::snprintf(st->message, sizeof(st->message), "binary capacity: column %d needs %llu bytes", i,
+                          (unsigned long long)nb);
+          }
+        }
+      } else if (cols[i].binary_data && nb) {
+        std::memcpy(cols[i].binary_data, po + off_b[(size_t)i], nb);
+      }
+    } else if (cols[i].values && n) {
+      std::memcpy(cols[i].values, po + off_v[(size_t)i], n * (uint64_t)w);
+    }
     if (cols[i].max_def > 0 && cols[i].def_levels)
       std::memcpy(cols[i].def_levels, po + off_d[(size_t)i], std::min(slots[(size_t)i], cols[i].levels_capacity));
     if (cols[i].max_rep > 0 && cols[i].rep_levels)

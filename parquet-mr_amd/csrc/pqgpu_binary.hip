@@ -1,0 +1,530 @@
+// pqgpu_binary.hip — CDNA4 (gfx950) kernels for variable-length and byte-transposed values:
+//
+//   k_bss            BYTE_STREAM_SPLIT (ByteStreamSplitValuesReader.java:30-114): byte k of value i
+//                    sits in stream k; lanes read 4 consecutive values of every stream as dwords
+//                    and transpose them in registers.
+//   k_bin_walk       PLAIN BYTE_ARRAY (BinaryPlainValuesReader.java:35-61) and the entries of a
+//                    BYTE_ARRAY dictionary page (PlainBinaryDictionary, PlainValuesDictionary.java:87-113):
+//                    the chain of 4-byte length prefixes, followed in parallel (below).
+//   k_bin_dict_map   RLE_DICTIONARY BYTE_ARRAY pages: dictionary id -> (length, source) of the entry.
+//   k_gather_fixed   FIXED_LEN_BYTE_ARRAY / INT96 dictionary pages: id -> fixed-width entry bytes.
+//   k_bin_scan_*     exclusive scan of value lengths -> int64 offsets of every BYTE_ARRAY column.
+//   k_bin_copy       value bytes -> the column's byte buffer, one wave per 256-value chunk,
+//                    output-dword parallel (every lane stores whole dwords).
+//
+// Output of a BYTE_ARRAY column (include/pqgpu.h): offsets[n + 1] (int64) + the concatenated
+// bytes — the Binary values the reference's ValuesReader.readBytes returns, in slot order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pqgpu_device.h"
+
+namespace pqg {
+
+// ---------------------------------------------------------------------------
+// BYTE_STREAM_SPLIT. initFromPage :67-97: available % W != 0 and "more encoded values than the
+// page's value count" fail at init; reading past the encoded values fails at that value
+// (nextElementByteOffset :43-50).
+__global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                  const PageWork* __restrict__ work,
+                                                  const ColumnDev* __restrict__ cols,
+                                                  const int32_t* __restrict__ list, int n_list, uint64_t* err,
+                                                  uint32_t* err_count) {
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
+  const PageWork pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint32_t W = uni((uint32_t)cd.elem_width);
+  const uint32_t beg = uni(pw.data_begin), end = uni(pw.size);
+  const uint32_t avail = end > beg ? end - beg : 0;
+  if (W == 0 || avail % W != 0 || pw.num_slots < avail / W) {
+    if (lane == 0) report(err, err_count, page, 0, 2, PQG_ERR_CORRUPT);
+    return;
+  }
+  const uint32_t count = avail / W;
+  uint32_t n = uni(pw.n_values);
+  if (n > count) {
+    if (lane == 0) report(err, err_count, page, 2, count, PQG_ERR_EOF);
+    n = count;
+  }
+  const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  uint8_t* out = (uint8_t*)cd.values + pw.out_offset * W;
+  if (W == 4 || W == 8) {
+    // lane: values [i0, i0 + 4); stream k -> one dword holding byte k of those 4 values
+    for (uint32_t i0 = 4u * lane; i0 < n; i0 += 4u * WAVE) {
+      uint32_t d[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) d[k] = k < W ? ld4_any(rs, beg + k * count + i0) : 0u;
+      uint32_t lo[4], hi[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t sh = 8u * j;
+        lo[j] = ((d[0] >> sh) & 0xFFu) | (((d[1] >> sh) & 0xFFu) << 8) | (((d[2] >> sh) & 0xFFu) << 16) |
+                (((d[3] >> sh) & 0xFFu) << 24);
+        hi[j] = ((d[4] >> sh) & 0xFFu) | (((d[5] >> sh) & 0xFFu) << 8) | (((d[6] >> sh) & 0xFFu) << 16) |
+                (((d[7] >> sh) & 0xFFu) << 24);
+      }
+      if (W == 4) {
+        uint32_t* o = (uint32_t*)out + i0;
+        if (i0 + 4 <= n && ((uintptr_t)o & 15u) == 0) {
+          gst_nt((u32x4*)o, u32x4{lo[0], lo[1], lo[2], lo[3]});
+        } else {
+#pragma unroll
+          for (uint32_t j = 0; j < 4; j++)
+            if (i0 + j < n) gst(o + j, lo[j]);
+        }
+      } else {
+        uint32_t* o = (uint32_t*)out + 2 * i0;
+        if (i0 + 4 <= n && ((uintptr_t)o & 15u) == 0) {
+          gst_nt((u32x4*)o, u32x4{lo[0], hi[0], lo[1], hi[1]});
+          gst_nt((u32x4*)(o + 4), u32x4{lo[2], hi[2], lo[3], hi[3]});
+        } else {
+#pragma unroll
+          for (uint32_t j = 0; j < 4; j++)
+            if (i0 + j < n) {
+              gst(o + 2 * j, lo[j]);
+              gst(o + 2 * j + 1, hi[j]);
+            }
+        }
+      }
+    }
+  } else {
+    // FIXED_LEN_BYTE_ARRAY of any width: one output byte per lane and step
+    const uint64_t nb = (uint64_t)n * W;
+    for (uint64_t o = lane; o < nb; o += WAVE) {
+      const uint32_t i = (uint32_t)(o / W), k = (uint32_t)(o % W);
+      const uint32_t a = beg + k * count + i;
+      gst(out + o, (uint8_t)(ld32(rs, a & ~3u) >> ((a & 3u) * 8u)));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Length-prefixed values: [len: 4 bytes LE][len bytes] repeated (BinaryPlainValuesReader.readBytes
+// :35-42: readIntLittleEndian, then in.slice(len)).
+//
+// The chain of positions is serial (each length gives the next position). It is followed a
+// 1 KiB window at a time without a serial step per value:
+//   1. every lane tests its 16 byte positions p of the window: p is a CANDIDATE when a value
+//      could start there (4 length bytes inside the section, 0 <= len, p + 4 + len <= end);
+//   2. the candidates are compacted in position order into LDS with their successor p + 4 + len;
+//   3. every true value start is a candidate, and the first candidate is the current position.
+//      Candidate i is followed by the true chain exactly when succ(i) == pos(i + 1); a batch of
+//      64 candidates whose successors all match is accepted in one step. A mismatch (a false
+//      candidate inside a value's bytes — rare: a length prefix read from string bytes is
+//      almost always larger than the section) is resolved by a search for succ(i) in the list.
+// So the per-value work is parallel; the serial steps are one per 64 values plus one per
+// false candidate that sits between two true ones.
+constexpr uint32_t BW_WIN = 1024;  // window bytes (16 positions per lane)
+
+struct BinWalkLds {
+  uint32_t pos[BW_WIN];
+  uint32_t nxt[BW_WIN];
+};
+
+// Error of a value whose length prefix starts at p (not a candidate).
+__device__ __forceinline__ int bin_value_error(rsrc_t rs, uint32_t p, uint32_t end, bool dict) {
+  if ((uint64_t)p + 4u > end) return PQG_ERR_EOF;  // readIntLittleEndian: EOFException
+  const int32_t len = (int32_t)ld4_any(rs, p);
+  if (len < 0) return PQG_ERR_CORRUPT;             // slice(negative): IllegalArgumentException
+  return dict ? PQG_ERR_CORRUPT : PQG_ERR_EOF;     // slice past the end: EOFException (dictionary: CORRUPT)
+}
+
+__device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, uint32_t N, uint32_t* out_len,
+                         uint32_t* out_src, bool dict, int page, int kind, uint64_t* err, uint32_t* err_count) {
+  const uint32_t lane = lane_id();
+  uint32_t pos = beg, produced = 0;
+  int code = 0;
+  while (true) {
+    pos = uni(pos);
+    produced = uni(produced);
+    if (produced >= N) break;
+    if ((uint64_t)pos + 4u > end) { code = PQG_ERR_EOF; break; }
+    // ---- candidates of the window [B, B + BW_WIN)
+    const uint32_t B = pos & ~3u;
+    const uint32_t base = B + 16u * lane;
+    const u32x4 d4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)base, 0, 0);
+    const uint32_t d[5] = {d4.x, d4.y, d4.z, d4.w, ld32(rs, base + 16u)};
+    uint32_t m = 0;
+    uint32_t nx[16];
+#pragma unroll
+    for (uint32_t q = 0; q < 16; q++) {
+      const uint32_t p = base + q;
+      const uint32_t len = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
+      const uint64_t e = (uint64_t)p + 4u + len;
+      const bool c = p >= pos && (int32_t)len >= 0 && e <= end;
+      nx[q] = (uint32_t)e;
+      m |= (c ? 1u : 0u) << q;
+    }
+    uint32_t total;
+    const uint32_t rank = wave_excl_scan_u32((uint32_t)__builtin_popcount(m), &total);
+    {
+      uint32_t r = rank;
+#pragma unroll
+      for (uint32_t q = 0; q < 16; q++)
+        if ((m >> q) & 1u) {
+          L.pos[r] = base + q;
+          L.nxt[r] = nx[q];
+          r++;
+        }
+    }
+    wave_sync();
+    total = uni(total);
+    if (total == 0 || L.pos[0] != pos) {  // the current position cannot hold a value
+      code = bin_value_error(rs, pos, end, dict);
+      break;
+    }
+    // ---- follow the chain through the candidate list
+    uint32_t i0 = 0;
+    bool leave = false;  // next position lies past the window
+    while (true) {
+      i0 = uni(i0);
+      const uint32_t k = i0 + lane;
+      const uint32_t p = k < total ? L.pos[k] : 0xFFFFFFFFu;
+      const uint32_t s = k < total ? L.nxt[k] : 0xFFFFFFFFu;
+      const uint32_t pn = k + 1 < total ? L.pos[k + 1] : 0xFFFFFFFFu;
+      // lanes [0, f] are values: f = first lane whose successor is not the next candidate
+      const uint64_t bad = __ballot(k >= total || s != pn);
+      const uint32_t f = (uint32_t)__builtin_ctzll(bad | (1ull << 63));
+      const uint32_t take = uni(f + 1 < N - produced ? f + 1 : N - produced);
+      if (lane < take) {
+        gst(out_len + produced + lane, s - p - 4u);
+        gst(out_src + produced + lane, p + 4u);
+      }
+      produced += take;
+      if (produced >= N) break;
+      const uint32_t cur = rdl(s, f);  // true successor of the last accepted value
+      pos = cur;
+      if (cur >= B + BW_WIN) { leave = true; break; }
+      // find cur among the candidates after i0 + f (false candidates in between)
+      uint32_t lo = i0 + f + 1, hi = total;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.pos[mid] < cur) lo = mid + 1;
+        else hi = mid;
+      }
+      lo = uni(lo);
+      if (lo >= total || L.pos[lo] != cur) {  // every position of the window was tested
+        code = bin_value_error(rs, cur, end, dict);
+        break;
+      }
+      i0 = lo;
+    }
+    if (code || !leave) break;
+    wave_sync();  // the next window overwrites the list
+  }
+  if (code && lane == 0) report(err, err_count, page, kind, produced, code);
+}
+
+// One wave per page. dict_walk = 0: PLAIN BYTE_ARRAY data pages (values -> blen / bsrc at the
+// page's value offset). dict_walk = 1: `list` holds column indices of BYTE_ARRAY dictionaries;
+// the dictionary page's entries -> dict_len / dict_src; an error is recorded on the column's
+// pseudo page (n_pages + column) as an init error.
+__global__ __launch_bounds__(64 * WPB) void k_bin_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                       const PageWork* __restrict__ work,
+                                                       const ColumnDev* __restrict__ cols,
+                                                       const int32_t* __restrict__ list, int n_list, int dict_walk,
+                                                       int n_pages, uint64_t* err, uint32_t* err_count) {
+  __shared__ BinWalkLds lds_all[WPB];
+  const int item = wave_page(list, n_list);
+  if (item < 0) return;
+  BinWalkLds& L = lds_all[wave_id()];
+  if (dict_walk) {
+    const ColumnDev& cd = cols[item];
+    const rsrc_t rs = make_rsrc(bytes + cd.dict_offset, n_bytes - cd.dict_offset);
+    bin_walk(L, rs, 0, (uint32_t)cd.dict_bytes, cd.dict_n, cd.dict_len, cd.dict_src, true, n_pages + item, 0, err,
+             err_count);
+    return;
+  }
+  const PageWork& pw = work[item];
+  const ColumnDev& cd = cols[pw.column];
+  const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  bin_walk(L, rs, uni(pw.data_begin), uni(pw.size), uni(pw.n_values), cd.blen + pw.out_offset,
+           cd.bsrc + pw.out_offset, false, item, 2, err, err_count);
+}
+
+// RLE_DICTIONARY BYTE_ARRAY pages: ids (in blen, written by the dictionary kernel) -> entry
+// length and offset in the dictionary page. Invalid ids were reported by the dictionary kernel.
+__global__ __launch_bounds__(256) void k_bin_dict_map(const PageWork* __restrict__ work,
+                                                      const ColumnDev* __restrict__ cols,
+                                                      const int32_t* __restrict__ list, int n_list) {
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
+  const PageWork& pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t n = uni(pw.n_values), dn = uni(cd.dict_n);
+  uint32_t* len = cd.blen + pw.out_offset;
+  uint32_t* src = cd.bsrc + pw.out_offset;
+  for (uint32_t i = lane_id(); i < n; i += WAVE) {
+    const uint32_t id = len[i];
+    const bool ok = id < dn;
+    gst(len + i, ok ? cd.dict_len[id] : 0u);
+    gst(src + i, ok ? cd.dict_src[id] : 0u);
+  }
+}
+
+// FIXED_LEN_BYTE_ARRAY / INT96 dictionary pages: ids (in blen) -> W-byte entries, one output
+// byte per lane and step (the dictionary is small and L2-resident).
+__global__ __launch_bounds__(256) void k_gather_fixed(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                      const PageWork* __restrict__ work,
+                                                      const ColumnDev* __restrict__ cols,
+                                                      const int32_t* __restrict__ list, int n_list) {
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
+  const PageWork& pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t W = uni((uint32_t)cd.elem_width), dn = uni(cd.dict_n);
+  const uint64_t nb = (uint64_t)uni(pw.n_values) * W;
+  const uint32_t* ids = cd.blen + pw.out_offset;
+  uint8_t* out = (uint8_t*)cd.values + pw.out_offset * W;
+  const rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
+  for (uint64_t o = lane_id(); o < nb; o += WAVE) {
+    const uint32_t i = (uint32_t)(o / W), k = (uint32_t)(o % W);
+    const uint32_t id = ids[i];
+    if (id >= dn) continue;
+    const uint32_t a = id * W + k;
+    gst(out + o, (uint8_t)(ld32(drs, a & ~3u) >> ((a & 3u) * 8u)));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Offsets of BYTE_ARRAY columns: exclusive scan of blen over [0, n_slots) (entries past the
+// column's decoded values hold 0: blen is cleared before every launch), written as int64
+// offsets[0 .. n_slots]. blocks[b] = (column << 32) | block index within the column.
+
+__device__ __forceinline__ uint64_t block_reduce_u64(uint64_t v, uint64_t* red) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t t = 0;
+  for (uint32_t w = 0; w < blockDim.x / WAVE; w++) t += red[w];
+  __syncthreads();
+  return t;
+}
+
+__global__ __launch_bounds__(256) void k_bin_block_sums(const ColumnDev* __restrict__ cols,
+                                                        const uint64_t* __restrict__ blocks) {
+  __shared__ uint64_t red[4];
+  const uint64_t b = blocks[blockIdx.x];
+  const ColumnDev& cd = cols[(uint32_t)(b >> 32)];
+  const uint64_t v0 = (uint64_t)(uint32_t)b * SCAN_BLOCK;
+  uint64_t s = 0;
+  for (uint32_t i = threadIdx.x; i < SCAN_BLOCK; i += 256) {
+    const uint64_t v = v0 + i;
+    if (v < cd.n_slots) s += cd.blen[v];
+  }
+  s = block_reduce_u64(s, red);
+  if (threadIdx.x == 0) cd.block_sums[(uint32_t)b] = s;
+}
+
+// One workgroup per BYTE_ARRAY column: exclusive scan of its block sums (in place) + total.
+__global__ __launch_bounds__(256) void k_bin_block_bases(const ColumnDev* __restrict__ cols,
+                                                         const int32_t* __restrict__ bin_cols) {
+  __shared__ uint64_t wsum[4];
+  __shared__ uint64_t carry;
+  const ColumnDev& cd = cols[bin_cols[blockIdx.x]];
+  const uint32_t nb = (uint32_t)((cd.n_slots + SCAN_BLOCK - 1) / SCAN_BLOCK);
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+    const uint32_t b = b0 + threadIdx.x;
+    const uint64_t v = b < nb ? cd.block_sums[b] : 0;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o);
+      if ((int)lane_id() >= o) x += y;
+    }
+    if (lane_id() == 63) wsum[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint64_t pre = carry;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) pre += wsum[w];
+    if (b < nb) cd.block_sums[b] = pre + x - v;
+    __syncthreads();
+    if (threadIdx.x == 255) carry = pre + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *cd.bin_total = carry;
+}
+
+__global__ __launch_bounds__(256) void k_bin_offsets(const ColumnDev* __restrict__ cols,
+                                                     const uint64_t* __restrict__ blocks) {
+  __shared__ uint64_t wsum[4];
+  __shared__ uint64_t carry;
+  const uint64_t b = blocks[blockIdx.x];
+  const ColumnDev& cd = cols[(uint32_t)(b >> 32)];
+  const uint64_t v0 = (uint64_t)(uint32_t)b * SCAN_BLOCK;
+  int64_t* off = (int64_t*)cd.values;
+  if (threadIdx.x == 0) carry = cd.block_sums[(uint32_t)b];
+  __syncthreads();
+  for (uint32_t i0 = 0; i0 < SCAN_BLOCK; i0 += 256) {
+    const uint64_t v = v0 + i0 + threadIdx.x;
+    const uint64_t len = v < cd.n_slots ? cd.blen[v] : 0;
+    uint64_t x = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o);
+      if ((int)lane_id() >= o) x += y;
+    }
+    if (lane_id() == 63) wsum[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint64_t pre = carry;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) pre += wsum[w];
+    if (v < cd.n_slots) gst(off + v, (int64_t)(pre + x - len));
+    if (v + 1 == cd.n_slots) gst(off + v + 1, (int64_t)(pre + x));
+    __syncthreads();
+    if (threadIdx.x == 255) carry = pre + x;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Value bytes. One wave per chunk of BIN_CHUNK values of one page (chunks[c] = page | j << 32).
+// The chunk's offsets and sources are staged in LDS; every lane owns output dwords of the
+// chunk's byte range and finds the value of its first byte by binary search (then walks
+// forward). A dword inside one value is one unaligned 4-byte source read; a dword that straddles
+// values (or the chunk ends, which other waves share) is assembled and stored byte by byte.
+// DELTA_LENGTH_BYTE_ARRAY sources are the page's value bytes (PageWork::aux) + the in-page offset;
+// a value running past the page is the reference's "Failed to read N bytes" (EOF) at that value.
+__global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                       const PageWork* __restrict__ work,
+                                                       const ColumnDev* __restrict__ cols,
+                                                       const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                       uint64_t* err, uint32_t* err_count) {
+  __shared__ uint64_t off_all[WPB][BIN_CHUNK + 1];
+  __shared__ uint32_t src_all[WPB][BIN_CHUNK];
+  const uint32_t c = blockIdx.x * WPB + wave_id();
+  if (c >= n_chunks) return;
+  uint64_t* off = off_all[wave_id()];
+  uint32_t* src = src_all[wave_id()];
+  const uint32_t lane = lane_id();
+  const uint64_t ch = chunks[c];
+  const int page = (int)(uint32_t)ch;
+  const uint32_t j = (uint32_t)(ch >> 32);
+  const PageWork& pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t nv = uni(pw.n_values);
+  const uint32_t i_lo = j * BIN_CHUNK;
+  if (i_lo >= nv) return;
+  const uint32_t i_hi = i_lo + BIN_CHUNK < nv ? i_lo + BIN_CHUNK : nv;
+  const uint32_t n = i_hi - i_lo;
+  const int64_t* offs = (const int64_t*)cd.values + pw.out_offset;
+  const bool dlba = uni(pw.bin_kind) == BIN_DLBA;
+  const bool from_dict = uni(pw.bin_kind) == BIN_DICT;
+  const uint64_t sbase = from_dict ? cd.dict_offset : pw.base;
+  const uint64_t slim = from_dict ? cd.dict_bytes : pw.size;
+  const rsrc_t rs = make_rsrc(bytes + sbase, n_bytes - sbase);
+  const uint64_t page0 = (uint64_t)offs[0];
+  for (uint32_t k = lane; k <= n; k += WAVE) off[k] = (uint64_t)offs[i_lo + k];
+  wave_sync();
+  for (uint32_t k = lane; k < n; k += WAVE) {
+    uint32_t s;
+    if (dlba) {
+      const uint64_t rel = off[k] - page0, len = off[k + 1] - off[k];
+      const uint64_t avail = pw.size > pw.aux ? pw.size - pw.aux : 0;
+      if (rel + len > avail) report(err, err_count, page, 2, i_lo + k, PQG_ERR_EOF);
+      s = (uint32_t)(pw.aux + rel);
+    } else {
+      s = cd.bsrc[pw.out_offset + i_lo + k];
+    }
+    src[k] = s;
+  }
+  wave_sync();
+  const uint64_t o_lo = off[0], o_hi0 = off[n];
+  const uint64_t o_hi = o_hi0 < cd.binary_capacity ? o_hi0 : cd.binary_capacity;  // overflow: reported at sync
+  if (o_lo >= o_hi) return;
+  uint8_t* dst = cd.binary_data;
+  const uint64_t a0 = o_lo & ~3ull;
+  uint32_t kv = 0;  // value of this lane's current byte (monotone across iterations)
+  for (uint64_t a = a0 + 4u * lane; a < o_hi; a += 4u * WAVE) {
+    const uint64_t b0 = a > o_lo ? a : o_lo;
+    // value holding byte b0: last k with off[k] <= b0
+    uint32_t lo = kv, hi = n;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (off[mid] <= b0) lo = mid;
+      else hi = mid;
+    }
+    kv = lo;
+    const uint64_t e = a + 4u;
+    if (a >= o_lo && e <= o_hi && e <= off[kv + 1]) {
+      const uint64_t sp = (uint64_t)src[kv] + (a - off[kv]);
+      const uint32_t x = sp + 4u <= slim ? ld4_any(rs, (uint32_t)sp) : 0u;
+      gst((uint32_t*)(dst + a), x);
+    } else {
+      uint32_t k = kv, x = 0, have = 0;
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint64_t bb = a + q;
+        if (bb < o_lo || bb >= o_hi) continue;
+        while (k + 1 < n && bb >= off[k + 1]) k++;
+        const uint64_t sp = (uint64_t)src[k] + (bb - off[k]);
+        const uint32_t v = sp < slim ? (ld32(rs, (uint32_t)sp & ~3u) >> (((uint32_t)sp & 3u) * 8u)) & 0xFFu : 0u;
+        x |= v << (8u * q);
+        have |= 1u << q;
+      }
+      if (have == 0xFu) {
+        gst((uint32_t*)(dst + a), x);
+      } else {
+        for (uint32_t q = 0; q < 4; q++)
+          if ((have >> q) & 1u) gst(dst + a + q, (uint8_t)(x >> (8u * q)));
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers
+
+#define PQG_BIN_ARGS bytes, n_bytes, work, cols, list, n, err, err_count
+
+hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
+                      const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bss, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_BIN_ARGS);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                           const ColumnDev* cols, const int32_t* list, int n, int dict_walk, int n_pages,
+                           uint64_t* err, uint32_t* err_count) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bin_walk, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, list, n,
+                     dict_walk, n_pages, err, err_count);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin_dict_map(hipStream_t st, PageWork* work, const ColumnDev* cols, const int32_t* list, int n) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bin_dict_map, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, work, cols, list, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_fixed(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                               const ColumnDev* cols, const int32_t* list, int n) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_fixed, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols,
+                     list, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin_scan(hipStream_t st, const ColumnDev* cols, const int32_t* bin_cols, int n_bin_cols,
+                           const uint64_t* blocks, uint32_t n_blocks) {
+  if (n_bin_cols <= 0 || n_blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bin_block_sums, dim3(n_blocks), dim3(256), 0, st, cols, blocks);
+  hipLaunchKernelGGL(k_bin_block_bases, dim3(n_bin_cols), dim3(256), 0, st, cols, bin_cols);
+  hipLaunchKernelGGL(k_bin_offsets, dim3(n_blocks), dim3(256), 0, st, cols, blocks);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                           const ColumnDev* cols, const uint64_t* chunks, uint32_t n_chunks, uint64_t* err,
+                           uint32_t* err_count) {
+  if (n_chunks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bin_copy, dim3((n_chunks + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols,
+                     chunks, n_chunks, err, err_count);
+  return hipGetLastError();
+}
+
+}  // namespace pqg

@@ -20,6 +20,19 @@ struct ColumnDev {
   void* values;
   uint8_t* def_levels;
   uint8_t* rep_levels;
+  // BYTE_ARRAY columns: `values` = int64 offsets[n_slots + 1] into binary_data; per value
+  // scratch: blen (length; dictionary ids of RLE_DICTIONARY pages until k_bin_dict_map) and
+  // bsrc (source byte offset relative to the page body, or to the dictionary page body)
+  uint8_t* binary_data;
+  uint64_t binary_capacity;
+  uint32_t* blen;
+  uint32_t* bsrc;
+  // BYTE_ARRAY dictionary entries (PlainBinaryDictionary): length and offset in the dictionary page
+  uint32_t* dict_len;
+  uint32_t* dict_src;
+  uint64_t n_slots;        // level slots of the column in the batch (offsets span n_slots + 1)
+  uint64_t* block_sums;    // BYTE_ARRAY offset scan: per 4096-value block
+  uint64_t* bin_total;     // BYTE_ARRAY: bytes of the decoded values (device, one u64)
 };
 
 // Per page, on the device. The host fills the descriptor facts; for nullable
@@ -41,8 +54,12 @@ struct PageWork {
   // dictionary pages: run records (walk -> tiles)
   uint64_t rec_base;    // first run record of the page
   uint32_t chunk_base;  // first output chunk of the page
-  uint32_t reserved[3];
+  uint32_t aux;         // DELTA_LENGTH_BYTE_ARRAY: start of the value bytes (end of the length stream)
+  uint32_t bin_kind;    // BYTE_ARRAY pages: BIN_PLAIN / BIN_DLBA / BIN_DICT (source of the value bytes)
+  uint32_t reserved;
 };
+
+enum BinKind : uint32_t { BIN_PLAIN = 0, BIN_DLBA = 1, BIN_DICT = 2 };
 
 // Output chunk of k_dict_expand: CH_TILES x 64 lanes x 16 bytes.
 #ifndef PQG_CHUNK_TILES
@@ -63,6 +80,31 @@ hipError_t launch_plain(int kind, hipStream_t st, const uint8_t* bytes, uint64_t
                         const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
 hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                         const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+// dictionary kernels: MODE 0 = values of a 4/8-byte dictionary; MODE 1 = the ids themselves
+// (u32, into ColumnDev::blen) for BYTE_ARRAY / FIXED_LEN_BYTE_ARRAY / INT96 dictionaries
+hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                           const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
+                           const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
+                           uint32_t epoch, bool fused, uint64_t* err, uint32_t* err_count);
+// DELTA_LENGTH_BYTE_ARRAY lengths (k_delta into blen, records PageWork::aux)
+hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                               const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+// pqgpu_binary.hip
+constexpr uint32_t BIN_CHUNK = 256;     // values per k_bin_copy chunk
+constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block
+hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
+                      const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                           const ColumnDev* cols, const int32_t* list, int n, int dict_walk, int n_pages,
+                           uint64_t* err, uint32_t* err_count);
+hipError_t launch_bin_dict_map(hipStream_t st, PageWork* work, const ColumnDev* cols, const int32_t* list, int n);
+hipError_t launch_gather_fixed(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                               const ColumnDev* cols, const int32_t* list, int n);
+hipError_t launch_bin_scan(hipStream_t st, const ColumnDev* cols, const int32_t* bin_cols, int n_bin_cols,
+                           const uint64_t* blocks, uint32_t n_blocks);
+hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                           const ColumnDev* cols, const uint64_t* chunks, uint32_t n_chunks, uint64_t* err,
+                           uint32_t* err_count);
 hipError_t launch_unpack_runs(hipStream_t st, int w, const uint8_t* in, uint64_t in_bytes, const uint64_t* in_off,
                               const uint32_t* counts, const uint64_t* out_off, int32_t* out, int n_runs,
                               uint32_t max_count);

@@ -28,212 +28,9 @@
 
 #include <type_traits>
 
-#include "pqgpu_internal.h"
+#include "pqgpu_device.h"
 
 namespace pqg {
-
-constexpr int WAVE = 64;
-// Pages per workgroup: one page per wave, 4 waves per 256-lane workgroup. One-wave
-// workgroups cap residency by the per-CU workgroup limit (measured: ~2.3k of 5k
-// waves resident), so pages are packed 4 to a workgroup.
-constexpr int WPB = 4;
-
-__device__ __forceinline__ uint32_t wave_id() {
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-}
-// Page of this wave, or -1 when the grid's last workgroup has fewer pages.
-__device__ __forceinline__ int wave_page(const int32_t* list, int n_list) {
-  const int i = (int)(blockIdx.x * WPB + wave_id());
-  return i < n_list ? list[i] : -1;
-}
-#ifdef PQG_DIAG
-// Diagnostic build only (libpqgpu_diag.so, tools/diag_timeline.py): per-wave
-// stamps. Never compiled into the product library.
-__device__ uint64_t* pqg_diag_buf;
-#define DIAG_T(v) uint64_t v = __builtin_amdgcn_s_memtime()
-#define DIAG_ADD(acc, t0) acc += __builtin_amdgcn_s_memtime() - (t0)
-#else
-#define DIAG_T(v)
-#define DIAG_ADD(acc, t0)
-#endif
-
-// Intra-wave ordering of LDS writes before reads by other lanes (no s_barrier:
-// the waves of a workgroup work on different pages and do not meet).
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
-
-__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
-}
-
-__device__ __forceinline__ uint32_t uni(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-}
-
-__device__ __forceinline__ uint64_t uni64(uint64_t v) {
-  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
-}
-
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-
-// Stores through address_space(1) pointers: global_store_* count only in vmcnt.
-// (Generic pointers give flat_store_*, which also count in lgkmcnt, so every
-// s_waitcnt lgkmcnt(0) for an LDS read would wait for all stores in flight.)
-#ifdef PQG_DIAG
-__device__ int pqg_diag_nostore;  // diagnostic ablation: skip output stores (set by pqg_diag_nostore_set)
-#define PQG_STORE_GUARD if (!pqg_diag_nostore)
-#else
-#define PQG_STORE_GUARD
-#endif
-template <class T>
-__device__ __forceinline__ void gst(T* p, T v) {
-  PQG_STORE_GUARD *(__attribute__((address_space(1))) T*)p = v;
-}
-template <class T>
-__device__ __forceinline__ void gst_nt(T* p, T v) {
-  PQG_STORE_GUARD __builtin_nontemporal_store(v, (__attribute__((address_space(1))) T*)p);
-}
-
-// Run records, chunk entries and page status are produced and consumed inside one launch
-// by the fused dictionary kernel (different CUs, possibly different XCDs, whose L2s are not
-// coherent): they are written and read with system-scope relaxed accesses (sc0 sc1: through
-// to memory), ordered by s_waitcnt vmcnt(0) before the page's ready flag is set.
-template <class T>
-__device__ __forceinline__ void sst(T* p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-template <class T>
-__device__ __forceinline__ T sld(const T* p) {
-  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Buffer resource over [base, base + n) with hardware range checking: loads past
-// n return 0 (never fault), so a window may overhang the end of the batch.
-__device__ __forceinline__ rsrc_t make_rsrc(const uint8_t* base, uint64_t n) {
-  uint64_t b = uni64((uint64_t)(uintptr_t)base);
-  uint32_t nr = n > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)n;
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)b, (short)0, (int)uni(nr), 0x00020000);
-}
-
-__device__ __forceinline__ uint32_t ld32(rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
-}
-
-// 8 bytes at any byte offset (little endian). Branch-free (v_alignbyte): a load issued on
-// only one path leaves the waitcnt pass a "maybe pending" load at every later merge point,
-// and it then answers with s_waitcnt vmcnt(0) — draining all stores — in unrelated loops.
-__device__ __forceinline__ uint64_t ld8_any(rsrc_t r, uint32_t off) {
-  const uint32_t a = off & ~3u, sb = off & 3u;
-  const uint32_t w0 = ld32(r, a), w1 = ld32(r, a + 4), w2 = ld32(r, a + 8);
-  return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sb) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sb) << 32);
-}
-
-__device__ __forceinline__ uint32_t ld4_any(rsrc_t r, uint32_t off) {
-  const uint32_t a = off & ~3u, sb = off & 3u;
-  return __builtin_amdgcn_alignbyte(ld32(r, a + 4), ld32(r, a), sb);
-}
-
-// Record an error: smallest (index << 8 | code) per (page, kind) wins.
-__device__ __forceinline__ void report(uint64_t* err, uint32_t* err_count, int page, int kind, uint64_t index,
-                                       int code) {
-  atomicMin((unsigned long long*)&err[3 * (uint64_t)page + kind], (unsigned long long)((index << 8) | (uint64_t)code));
-  atomicAdd(err_count, 1u);
-}
-
-// ---------------------------------------------------------------------------
-// Register window over a page: lane l holds bytes [B + 4l, B + 4l + 4) in wa and
-// [B + 256 + 4l, ...) in wb. B is wave-uniform; reads are v_readlane.
-struct Window {
-  rsrc_t rs;
-  uint32_t B;
-  uint32_t wa, wb;
-
-  __device__ __forceinline__ void seek(uint32_t p) {
-    B = p & ~3u;
-    wa = ld32(rs, B + 4u * lane_id());
-    wb = ld32(rs, B + 256u + 4u * lane_id());
-  }
-  // Make [p, p + 12) resident. p never moves backwards.
-  __device__ __forceinline__ void ensure(uint32_t p) {
-    uint32_t k = p - B;
-    if (k > 496u) {
-      if (k <= 752u) {
-        B += 256u;
-        wa = wb;
-        wb = ld32(rs, B + 256u + 4u * lane_id());
-      } else {
-        seek(p);
-      }
-    }
-  }
-  __device__ __forceinline__ uint32_t dword(uint32_t i) {
-    uint32_t a = rdl(wa, i & 63u), b = rdl(wb, i & 63u);
-    return i < 64u ? a : b;
-  }
-  __device__ __forceinline__ uint64_t read8(uint32_t p) {
-    ensure(p);
-    uint32_t k = p - B, i = k >> 2, sh = (k & 3u) * 8u;
-    uint64_t x = (uint64_t)dword(i) | ((uint64_t)dword(i + 1) << 32);
-    if (sh) x = (x >> sh) | ((uint64_t)dword(i + 2) << (64u - sh));
-    return x;
-  }
-  __device__ __forceinline__ uint32_t byte(uint32_t p) {
-    ensure(p);
-    uint32_t k = p - B;
-    return (dword(k >> 2) >> ((k & 3u) * 8u)) & 0xFFu;
-  }
-};
-
-// readUnsignedVarInt (BytesUtils.java:202-211) at p. Sets len; Java int shift masking.
-// `lim` = bytes readable before the section end; a varint not terminated within
-// them gets len = lim + 1 (the caller's EOF check fails it, as read() would).
-__device__ __forceinline__ uint32_t read_uvarint(Window& w, uint32_t p, uint32_t lim, uint32_t& len) {
-  uint64_t x = w.read8(p);
-  uint32_t b0 = (uint32_t)x & 0xFFu;
-  if (!(b0 & 0x80u)) { len = 1; return b0; }
-  uint32_t b1 = (uint32_t)(x >> 8) & 0xFFu;
-  if (!(b1 & 0x80u)) { len = 2; return (b0 & 0x7Fu) | (b1 << 7); }
-  uint32_t value = 0, i = 0, k = 0, b;
-  for (;;) {
-    b = (k < 8u) ? (uint32_t)(x >> (8u * k)) & 0xFFu : w.byte(p + k);
-    if (!(b & 0x80u)) break;
-    value |= (b & 0x7Fu) << (i & 31u);
-    i += 7;
-    k++;
-    if (k >= lim) break;
-  }
-  len = k + 1;
-  return value | (b << (i & 31u));
-}
-
-// readUnsignedVarLong (BytesUtils.java:260-269), Java long shift masking.
-__device__ __forceinline__ uint64_t read_uvarlong(Window& w, uint32_t p, uint32_t lim, uint32_t& len) {
-  uint64_t value = 0;
-  uint32_t i = 0, k = 0, b;
-  uint64_t x = w.read8(p);
-  for (;;) {
-    b = (k < 8u) ? (uint32_t)(x >> (8u * k)) & 0xFFu : w.byte(p + k);
-    if (!(b & 0x80u)) break;
-    value |= (uint64_t)(b & 0x7Fu) << (i & 63u);
-    i += 7;
-    k++;
-    if (k >= lim) break;
-  }
-  len = k + 1;
-  return value | ((uint64_t)b << (i & 63u));
-}
-
-// readZigZagVarLong (BytesUtils.java:254-258)
-__device__ __forceinline__ int64_t zigzag64(uint64_t r) {
-  int64_t sign = -(int64_t)(r & 1);
-  int64_t temp = ((int64_t)((uint64_t)sign ^ r)) >> 1;
-  return (int64_t)((uint64_t)temp ^ (r & 0x8000000000000000ull));
-}
 
 // ---------------------------------------------------------------------------
 // RLE / bit-packed hybrid walker (RunLengthBitPackingHybridDecoder.readNext :80-109).
@@ -260,7 +57,6 @@ struct PreWin {
 
 constexpr uint32_t SEG_BYTES = 3072;   // LDS page segment per wave of k_dict_runs (5 workgroups per CU)
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Fill the wave's LDS segment with page bytes [lo, lo + SEG_BYTES) (lo 16-aligned).
 __device__ __forceinline__ void seg_fill(PreWin& pw, uint32_t lo) {
@@ -1063,7 +859,10 @@ constexpr uint32_t SPIN_LIMIT = 1u << 20;  // ~55 ms of s_sleep 2: a walker that
 // FUSED: launched in the same grid as the walkers (after them in workgroup order, so every
 // walker this wave waits for was dispatched first); the page's records are ready once its
 // flag holds this launch's epoch.
-template <int W, bool FUSED>
+// IDS: the expansion writes the dictionary ids themselves (u32, into ColumnDev::blen) instead
+// of dictionary values: BYTE_ARRAY / FIXED_LEN_BYTE_ARRAY / INT96 dictionaries, whose values
+// are materialized by later kernels (k_bin_dict_map + k_bin_copy, k_gather_fixed).
+template <int W, bool FUSED, bool IDS = false>
 __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                 const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                 const uint64_t* rec, const uint32_t* chunk_run,
@@ -1096,7 +895,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
   }
   __syncthreads();
   bool dict_in_lds = false;
-  if (same && c0 >= 0) {
+  if (!IDS && same && c0 >= 0) {
     const ColumnDev& cd0 = cols[c0];
     const uint64_t need = (uint64_t)cd0.dict_n * W;
     dict_in_lds = need <= DICT_LDS_BYTES && need <= cd0.dict_bytes;
@@ -1139,8 +938,9 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
   const uint32_t db = uni(pw.data_begin);
   const int w = (int)uni((ld32(prs, db & ~3u) >> ((db & 3u) * 8u)) & 0xFFu);
   const uint64_t* prec = rec + pw.rec_base;
-  T* const pag = (T*)cd.values + (pw.out_offset - sh);  // slot 0 of the page
-  const bool out16 = ((uintptr_t)cd.values & 15u) == 0;
+  T* const out_base = IDS ? (T*)cd.blen : (T*)cd.values;
+  T* const pag = out_base + (pw.out_offset - sh);  // slot 0 of the page
+  const bool out16 = ((uintptr_t)out_base & 15u) == 0;
   const uint32_t wmask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
 
   uint32_t k = uni(sld(chunk_run + pw.chunk_base + j));  // first run of this round
@@ -1163,9 +963,13 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       uint32_t vlo = 0, vhi = 0;
       if (live && !(pl & 0x80000000u)) {
         if (pl < dict_n) {
-          const uint64_t x = (uint64_t)(own_dict ? dict_l[pl] : load_dict<W>(drs, pl));
-          vlo = (uint32_t)x;
-          vhi = (uint32_t)(x >> 32);
+          if constexpr (IDS) {
+            vlo = pl;
+          } else {
+            const uint64_t x = (uint64_t)(own_dict ? dict_l[pl] : load_dict<W>(drs, pl));
+            vlo = (uint32_t)x;
+            vhi = (uint32_t)(x >> 32);
+          }
         }
       }
       tab[t0 + lane] = u32x4{st, pl, vlo, vhi};
@@ -1242,7 +1046,8 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
           report(err, err_count, page, 2, i, PQG_ERR_DICT_ID);
           return 0;
         }
-        return FAST ? dict_l[id] : dict_get_g<W>(own_dict, dict_l, drs, id);
+        if constexpr (IDS) return (T)id;
+        else return FAST ? dict_l[id] : dict_get_g<W>(own_dict, dict_l, drs, id);
         (void)ci;
       };
       const uint32_t t_beg = (b_lo + sh) / TV, t_end = (b_hi + sh + TV - 1) / TV;  // page tiles
@@ -1295,7 +1100,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
         }
       }
     };
-    if (own_dict && x_lds) sweep(std::true_type{});
+    if ((IDS || own_dict) && x_lds) sweep(std::true_type{});
     else sweep(std::false_type{});
     if (b_hi >= v_hi) break;
     k += XT_RUNS - 1;
@@ -1303,7 +1108,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
   }
 }
 
-template <int W>
+template <int W, bool IDS = false>
 __global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                          const PageWork* __restrict__ work,
                                                          const ColumnDev* __restrict__ cols, const uint64_t* rec,
@@ -1311,13 +1116,13 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restri
                                                          uint32_t n_chunks, const uint64_t* pstat, uint64_t* err,
                                                          uint32_t* err_count) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[XT_LDS_BYTES];
-  dict_tiles_body<W, false>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, nullptr, 0, err,
-                            err_count, lds, blockIdx.x);
+  dict_tiles_body<W, false, IDS>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, nullptr, 0,
+                                 err, err_count, lds, blockIdx.x);
 }
 
 // Walkers and tiles in one grid: workgroups [0, n_walk) walk pages, the rest expand chunks
 // as soon as their page is published, so the expansion overlaps the walk.
-template <int W>
+template <int W, bool IDS = false>
 __global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                          const PageWork* __restrict__ work,
                                                          const ColumnDev* __restrict__ cols,
@@ -1332,8 +1137,8 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restri
     dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
                       lds, blockIdx.x);
   else
-    dict_tiles_body<W, true>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err,
-                             err_count, lds, blockIdx.x - n_walk);
+    dict_tiles_body<W, true, IDS>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch,
+                                  err, err_count, lds, blockIdx.x - n_walk);
 }
 
 
@@ -1613,9 +1418,14 @@ __global__ __launch_bounds__(64 * WPB) void k_plain_bool(const uint8_t* __restri
 // (block b -> lane b % 64), then per block each lane unpacks its deltas, a
 // wave-wide inclusive scan (wrapping int64) turns them into values. INT32 =
 // (int) of the long (readInteger :103-107).
-template <int W>
+//
+// DLBA: the lengths of DELTA_LENGTH_BYTE_ARRAY pages (DeltaLengthByteArrayValuesReader.initFromPage
+// :44-48 reads them with this reader, then takes the remaining stream as the value bytes): the
+// lengths go to ColumnDev::blen, the stream position after the length stream to PageWork::aux,
+// and a negative length (in.slice(negative) -> IllegalArgumentException) is reported at its value.
+template <int W, bool DLBA = false>
 __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                              const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                              PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                               const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                               uint32_t* err_count) {
   const int page = wave_page(list, n_list);
@@ -1666,11 +1476,18 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
     n_out = total;
   }
   typedef typename DictVal<W>::T T;
-  T* out = (T*)cd.values + pw.out_offset;
+  T* out = (DLBA ? (T*)cd.blen : (T*)cd.values) + pw.out_offset;
   // Value index k (0-based) of the page: k = 0 is `first`; block b covers
   // k in [1 + b*block, 1 + (b+1)*block).
   uint64_t carry = (uint64_t)first;
-  if (lane == 0 && n_out > 0) gst(out, (T)carry);
+  if (lane == 0 && n_out > 0) {
+    if (DLBA && (int32_t)(uint32_t)carry < 0) {
+      report(err, err_count, page, 2, 0, PQG_ERR_CORRUPT);
+      gst(out, (T)0);
+    } else {
+      gst(out, (T)carry);
+    }
+  }
   uint32_t buffered = 1;  // Java valuesBuffered (includes the first value)
   const uint32_t E = (block + WAVE - 1) / WAVE;  // deltas per lane per block
   bool fail = false;
@@ -1774,7 +1591,14 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
       for (uint32_t q = 0; q < 8; q++) {
         uint32_t j = lane * E + q;
         uint64_t k = (uint64_t)k0 + j;
-        if (q < E && j < block && k < n_out) gst(out + k, (T)(base_v + loc[q]));
+        if (q < E && j < block && k < n_out) {
+          T v = (T)(base_v + loc[q]);
+          if (DLBA && (int32_t)(uint32_t)v < 0) {
+            report(err, err_count, page, 2, k, PQG_ERR_CORRUPT);
+            v = 0;
+          }
+          gst(out + k, v);
+        }
       }
       carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
     }
@@ -1784,6 +1608,7 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
     return;
   }
   if (want > total && lane == 0) report(err, err_count, page, 2, total, PQG_ERR_DELTA_PAST_END);
+  if (DLBA && lane == 0) work[page].aux = p;
 #undef DELTA_FAIL
 }
 
@@ -1859,6 +1684,26 @@ hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t
   return hipGetLastError();
 }
 
+hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                           const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
+                           const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
+                           uint32_t epoch, bool fused, uint64_t* err, uint32_t* err_count) {
+  if (n <= 0) return hipSuccess;
+  const uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
+  const dim3 blk(64 * WPB);
+  if (fused) {
+    hipLaunchKernelGGL((k_dict_fused<4, true>), dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n,
+                       n_walk, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_dict_runs<4>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,
+                     pstat, flags, epoch, err, err_count);
+  if (n_tile)
+    hipLaunchKernelGGL((k_dict_tiles<4, true>), dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run,
+                       chunks, n_chunks, pstat, err, err_count);
+  return hipGetLastError();
+}
+
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                          const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
   if (n <= 0) return hipSuccess;
@@ -1886,6 +1731,13 @@ hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_
   if (n <= 0) return hipSuccess;
   if (width == 8) hipLaunchKernelGGL(k_delta<8>, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   else hipLaunchKernelGGL(k_delta<4>, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
+  return hipGetLastError();
+}
+
+hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                               const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL((k_delta<4, true>), dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   return hipGetLastError();
 }
 

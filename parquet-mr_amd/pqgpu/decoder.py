@@ -32,13 +32,18 @@ class DeviceBatch:
 
 
 class DeviceColumn:
-    def __init__(self, physical_type, values, def_levels=None, rep_levels=None, type_length=0):
+    def __init__(self, physical_type, values, def_levels=None, rep_levels=None, type_length=0, binary_data=None):
         self.physical_type = physical_type
         self.type_length = type_length
-        self.values = values          # torch uint8 buffer viewed per type by `typed()`
+        self.values = values          # torch uint8 buffer viewed per type by `typed()` (BYTE_ARRAY: int64 offsets)
         self.def_levels = def_levels
         self.rep_levels = rep_levels
+        self.binary_data = binary_data  # BYTE_ARRAY: the values' bytes (offsets index into it)
         self.n_values = 0
+
+    def offsets(self):
+        """BYTE_ARRAY: int64 offsets[n_values + 1] (device tensor)."""
+        return self.values[: (self.n_values + 1) * 8].view(torch.int64)
 
     def typed(self):
         dt = {abi.INT32: torch.int32, abi.INT64: torch.int64, abi.FLOAT: torch.float32,
@@ -48,7 +53,12 @@ class DeviceColumn:
         return v.view(dt) if dt is not None else v.view(-1, w)
 
     def numpy(self):
-        """Host copy of the decoded values (numpy, the reference's Java array analogue)."""
+        """Host copy of the decoded values (numpy, the reference's Java array analogue;
+        BYTE_ARRAY: a list of bytes, the reference's Binary values)."""
+        if self.physical_type == abi.BYTE_ARRAY:
+            offs = self.offsets().cpu().numpy()
+            data = self.binary_data[: int(offs[-1])].cpu().numpy().tobytes() if offs[-1] > 0 else b""
+            return [data[offs[i]:offs[i + 1]] for i in range(self.n_values)]
         w = abi.elem_width(self.physical_type, self.type_length)
         raw = self.values[: self.n_values * w].cpu().numpy()
         return raw.view(abi.numpy_dtype(self.physical_type, self.type_length))
@@ -117,19 +127,33 @@ class Decoder:
     def upload(self, batch):
         return DeviceBatch(batch, self.device)
 
+    @staticmethod
+    def binary_estimate(batch, i):
+        """Bytes a BYTE_ARRAY column is first given: its page bytes (PLAIN / DELTA_LENGTH values fit
+        in them) + twice its dictionary page; decode() grows it when the device counts more."""
+        cd = batch.columns[i]
+        pages = batch.pages[batch.pages["column"] == i]
+        return int(pages["size"].sum()) + 2 * int(cd["dict_size"] if cd["dict_offset"] >= 0 else 0) + 64
+
     def alloc_columns(self, batch):
         cols = []
         for i, cd in enumerate(batch.columns):
             n = batch.column_slots[i]
             w = abi.elem_width(cd["physical_type"], cd["type_length"])
-            vals = torch.empty(max(n * w, 16), dtype=torch.uint8, device=self.device)
+            binary = None
+            if cd["physical_type"] == abi.BYTE_ARRAY:
+                n_off = n + 1  # offsets[n + 1]
+                binary = torch.empty(self.binary_estimate(batch, i), dtype=torch.uint8, device=self.device)
+                vals = torch.empty(max(n_off * 8, 16), dtype=torch.uint8, device=self.device)
+            else:
+                vals = torch.empty(max(n * w, 16), dtype=torch.uint8, device=self.device)
             dl = torch.zeros(max(n, 1), dtype=torch.uint8, device=self.device) if cd["max_def"] > 0 else None
             rl = torch.zeros(max(n, 1), dtype=torch.uint8, device=self.device) if cd["max_rep"] > 0 else None
             if self.poison is not None:
                 for t in (vals, dl, rl):
                     if t is not None:
                         t.fill_(self.poison)
-            cols.append(DeviceColumn(cd["physical_type"], vals, dl, rl, cd["type_length"]))
+            cols.append(DeviceColumn(cd["physical_type"], vals, dl, rl, cd["type_length"], binary))
         return cols
 
     def _descs(self, batch, cols):
@@ -142,6 +166,10 @@ class Decoder:
             n = batch.column_slots[i]
             c.values = col.values.data_ptr()
             c.values_capacity = n
+            if cd["physical_type"] == abi.BYTE_ARRAY:
+                c.values_capacity = n + 1
+                c.binary_data = col.binary_data.data_ptr()
+                c.binary_capacity = col.binary_data.numel()
             c.def_levels = col.def_levels.data_ptr() if col.def_levels is not None else None
             c.rep_levels = col.rep_levels.data_ptr() if col.rep_levels is not None else None
             c.levels_capacity = n
@@ -149,9 +177,25 @@ class Decoder:
 
     # -- decode --------------------------------------------------------------------
     def decode(self, dbatch, cols=None, page_counts=None, check=True):
-        """Decode every page of `dbatch` into device columns. Returns (columns, status)."""
+        """Decode every page of `dbatch` into device columns. Returns (columns, status).
+        A BYTE_ARRAY column whose byte buffer turns out short (the status names the bytes it
+        needs) is given that many bytes and the batch is decoded again."""
         batch = dbatch.batch
         cols = cols if cols is not None else self.alloc_columns(batch)
+        for _ in range(len(batch.columns) + 1):
+            rc, st, descs = self._decode_once(dbatch, cols, page_counts)
+            if not (rc == abi.ERR_INVALID_ARG and st.page == -1 and st.message.startswith(b"binary capacity")):
+                break
+            i = int(st.message.split()[3])
+            cols[i].binary_data = torch.empty(int(st.value_index) + 64, dtype=torch.uint8, device=self.device)
+        for i, col in enumerate(cols):
+            col.n_values = int(descs[i].values_written)
+        if check:
+            native.check(rc, st, "pqg_decode")
+        return cols, st
+
+    def _decode_once(self, dbatch, cols, page_counts):
+        batch = dbatch.batch
         self.stream.wait_stream(torch.cuda.current_stream(self.device))  # uploads / allocations first
         descs = self._descs(batch, cols)
         pages = np.ascontiguousarray(batch.pages)
@@ -162,11 +206,7 @@ class Decoder:
                           pages.ctypes.data if len(pages) else None, len(pages), counts_ptr, C.byref(st))
         if rc == abi.OK:
             rc = L.pqg_sync(self.ctx, C.byref(st))
-        for i, col in enumerate(cols):
-            col.n_values = int(descs[i].values_written)
-        if check:
-            native.check(rc, st, "pqg_decode")
-        return cols, st
+        return rc, st, descs
 
     def plan(self, dbatch, cols=None):
         batch = dbatch.batch
@@ -184,8 +224,20 @@ class Decoder:
             col.n_values = batch.column_values[i]
         return Plan(self, h, cols, descs, (pages, dbatch))
 
-    def decode_host(self, batch):
-        """File bytes in, host arrays out (pqg_decode_host): the JNI shim's path."""
+    def decode_host(self, batch, binary_capacity=None):
+        """File bytes in, host arrays out (pqg_decode_host): the JNI shim's path. BYTE_ARRAY
+        columns come back as lists of bytes (plus "offsets"); a short host byte buffer is
+        grown to the size the library reports and the call repeated once."""
+        caps = {i: binary_capacity or self.binary_estimate(batch, i) for i, cd in enumerate(batch.columns)
+                if cd["physical_type"] == abi.BYTE_ARRAY}
+        for _ in range(2):
+            rc, st, res, counts, need = self._decode_host_once(batch, caps)
+            if not need:
+                break
+            caps.update(need)
+        return rc, st, res, counts
+
+    def _decode_host_once(self, batch, caps):
         descs = (abi.ColumnDesc * max(1, len(batch.columns)))()
         outs = []
         for i, cd in enumerate(batch.columns):
@@ -193,29 +245,42 @@ class Decoder:
             for k, v in cd.items():
                 setattr(c, k, v)
             n = batch.column_slots[i]
-            vals = np.zeros(max(n, 1), dtype=abi.numpy_dtype(cd["physical_type"], cd["type_length"]))
+            binary = cd["physical_type"] == abi.BYTE_ARRAY
+            vals = np.zeros(max(n + 1, 1), dtype=abi.numpy_dtype(cd["physical_type"], cd["type_length"]))
             dl = np.zeros(max(n, 1), dtype=np.uint8)
             rl = np.zeros(max(n, 1), dtype=np.uint8)
+            bd = np.zeros(max(caps.get(i, 0), 1), dtype=np.uint8) if binary else None
             c.values = vals.ctypes.data
-            c.values_capacity = n
+            c.values_capacity = n + 1 if binary else n
             c.def_levels = dl.ctypes.data if cd["max_def"] > 0 else None
             c.rep_levels = rl.ctypes.data if cd["max_rep"] > 0 else None
             c.levels_capacity = n
-            outs.append((vals, dl, rl))
+            if binary:
+                c.binary_data = bd.ctypes.data
+                c.binary_capacity = caps[i]
+            outs.append((vals, dl, rl, bd))
         counts = np.zeros(max(1, batch.n_pages), dtype=np.uint32)
         pages = np.ascontiguousarray(batch.pages)
         st = abi.Status()
         rc = native.lib().pqg_decode_host(self.ctx, batch.data.ctypes.data, batch.data.size, C.addressof(descs),
                                           len(batch.columns), pages.ctypes.data if len(pages) else None, len(pages),
                                           counts.ctypes.data, C.byref(st))
+        need = {}
+        if rc == abi.ERR_INVALID_ARG and st.page == -1 and st.message.startswith(b"binary capacity"):
+            need[int(st.message.split()[3])] = int(st.value_index)
         res = []
         for i, cd in enumerate(batch.columns):
             n = int(descs[i].values_written)
-            vals, dl, rl = outs[i]
-            res.append({"values": vals[:n], "n_values": n,
-                        "def_levels": dl[:batch.column_slots[i]] if cd["max_def"] > 0 else None,
-                        "rep_levels": rl[:batch.column_slots[i]] if cd["max_rep"] > 0 else None})
-        return rc, st, res, counts[:batch.n_pages]
+            vals, dl, rl, bd = outs[i]
+            r = {"values": vals[:n], "n_values": n,
+                 "def_levels": dl[:batch.column_slots[i]] if cd["max_def"] > 0 else None,
+                 "rep_levels": rl[:batch.column_slots[i]] if cd["max_rep"] > 0 else None}
+            if bd is not None:
+                offs = vals[:n + 1].copy()
+                r["offsets"] = offs
+                r["values"] = [bd[offs[k]:offs[k + 1]].tobytes() for k in range(n)] if not need else []
+            res.append(r)
+        return rc, st, res, counts[:batch.n_pages], need
 
     # -- ParquetReadRouter ---------------------------------------------------------
     def router_read(self, bit_width, data, count):

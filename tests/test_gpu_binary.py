@@ -1,0 +1,150 @@
+"""GPU parity for BYTE_ARRAY (PLAIN, dictionary, DELTA_LENGTH_BYTE_ARRAY), BYTE_STREAM_SPLIT and
+FIXED_LEN_BYTE_ARRAY / INT96 dictionaries: libpqgpu.so through the C ABI vs the oracle, bit-exact
+(values, offsets, levels, first error)."""
+import numpy as np
+import pytest
+
+from oracle import pqref
+from pqgpu import abi, writer
+
+from helpers import make, nulls, zipf_dict_column
+from test_gpu_parity import run_both
+
+pytestmark = pytest.mark.gpu
+
+
+def _strings(n, seed, lo=0, hi=32, alphabet=b"abcdefghijklmnopqrstuvwxyz0123456789"):
+    rng = np.random.default_rng(seed)
+    a = np.frombuffer(alphabet, dtype=np.uint8)
+    return [a[rng.integers(0, a.size, size=rng.integers(lo, hi + 1))].tobytes() for _ in range(n)]
+
+
+def _binary_vals(kind, n, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "ascii":
+        return _strings(n, seed, 4, 32)
+    if kind == "empty":      # zero-length values: every length prefix is 00 00 00 00
+        return [b""] * n
+    if kind == "zeros":      # value bytes that look like small lengths: many false candidates
+        return [bytes(int(x)) for x in rng.integers(0, 12, size=n)]
+    if kind == "smallints":  # little-endian small ints as values
+        return [int(x).to_bytes(4, "little") for x in rng.integers(0, 64, size=n)]
+    if kind == "random":
+        return [rng.integers(0, 256, size=rng.integers(0, 40), dtype=np.uint8).tobytes() for _ in range(n)]
+    if kind == "long":       # values longer than the walker's 1 KiB window
+        return [rng.integers(0, 256, size=rng.integers(0, 3000), dtype=np.uint8).tobytes() for _ in range(n)]
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["ascii", "empty", "zeros", "smallints", "random", "long"])
+@pytest.mark.parametrize("enc", [abi.PLAIN, abi.DELTA_LENGTH_BYTE_ARRAY, abi.RLE_DICTIONARY])
+def test_binary_required(decoder, kind, enc):
+    n = 600 if kind == "long" else 30_000
+    vals = _binary_vals(kind, n, seed=len(kind))
+    if enc == abi.RLE_DICTIONARY:  # few distinct values
+        vals = [vals[i] for i in np.random.default_rng(1).integers(0, min(len(vals), 400), size=len(vals))]
+    run_both(decoder, [make(abi.BYTE_ARRAY, vals, enc, page_rows=7000)])
+
+
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("enc", [abi.PLAIN, abi.DELTA_LENGTH_BYTE_ARRAY, abi.PLAIN_DICTIONARY])
+@pytest.mark.parametrize("null_frac", [0.0, 0.3, 1.0])
+def test_binary_optional(decoder, version, enc, null_frac):
+    dl = nulls(20_000, null_frac, seed=3)
+    vals = _strings(int(dl.sum()), seed=4, lo=0, hi=48)
+    if enc == abi.PLAIN_DICTIONARY:
+        vals = [vals[i % 97] for i in range(len(vals))]
+    run_both(decoder, [make(abi.BYTE_ARRAY, vals, enc, def_levels=dl, max_def=1, version=version, page_rows=6000,
+                            dict_page_encoding=abi.PLAIN_DICTIONARY)])
+
+
+def test_binary_many_columns_one_batch(decoder):
+    chunks = [make(abi.BYTE_ARRAY, _strings(9000, s), e, page_rows=2500)
+              for s, e in enumerate([abi.PLAIN, abi.DELTA_LENGTH_BYTE_ARRAY, abi.RLE_DICTIONARY, abi.PLAIN])]
+    chunks.append(make(abi.INT64, zipf_dict_column(9000, card=50, seed=1), abi.RLE_DICTIONARY))
+    run_both(decoder, chunks)
+
+
+def test_binary_dictionary_expands_past_estimate(decoder):
+    """A dictionary of long entries: the decoded bytes exceed the first byte-buffer estimate,
+    the status reports the size needed and decode() retries."""
+    words = [bytes([65 + i]) * 5000 for i in range(4)]
+    vals = [words[i % 4] for i in range(4000)]
+    batch, ref, dcols = run_both(decoder, [make(abi.BYTE_ARRAY, vals, abi.RLE_DICTIONARY)])
+    assert dcols[0].binary_data.numel() >= 4000 * 5000
+
+
+def _err_case(which):
+    if which == "plain_eof":      # a value's length runs past the page (EOF at that value)
+        ch = make(abi.BYTE_ARRAY, _strings(3000, 1), abi.PLAIN, page_rows=1000)
+        ch.pages[1].body = ch.pages[1].body[:-3]
+    elif which == "plain_negative":  # slice(negative)
+        ch = make(abi.BYTE_ARRAY, _strings(3000, 2), abi.PLAIN, page_rows=1000)
+        b = bytearray(ch.pages[2].body)
+        b[0:4] = (0xFFFFFFF0).to_bytes(4, "little")
+        ch.pages[2].body = bytes(b)
+    elif which == "dlba_eof":     # DELTA_LENGTH: value bytes missing at the end
+        ch = make(abi.BYTE_ARRAY, _strings(3000, 3), abi.DELTA_LENGTH_BYTE_ARRAY, page_rows=1000)
+        ch.pages[0].body = ch.pages[0].body[:-10]
+    elif which == "dict_short":   # dictionary page shorter than its entries (PlainBinaryDictionary ctor)
+        ch = make(abi.BYTE_ARRAY, _strings(3000, 4), abi.RLE_DICTIONARY, page_rows=1000)
+        ch.dict_page = ch.dict_page[:-5]
+    elif which == "dict_id":      # dictionary id out of range
+        ch = make(abi.BYTE_ARRAY, _strings(3000, 5, 1, 3), abi.RLE_DICTIONARY, page_rows=1000)
+        ch.dict_num_values = 3
+    return ch
+
+
+@pytest.mark.parametrize("which", ["plain_eof", "plain_negative", "dlba_eof", "dict_short", "dict_id"])
+def test_binary_errors(decoder, which):
+    run_both(decoder, [_err_case(which)], expect_error=True)
+
+
+@pytest.mark.parametrize("ptype,tl", [(abi.FLOAT, 0), (abi.DOUBLE, 0), (abi.INT32, 0), (abi.INT64, 0),
+                                      (abi.FIXED_LEN_BYTE_ARRAY, 3), (abi.FIXED_LEN_BYTE_ARRAY, 16)])
+@pytest.mark.parametrize("null_frac", [0.0, 0.2])
+def test_byte_stream_split(decoder, ptype, tl, null_frac):
+    rng = np.random.default_rng(tl + 1)
+    dl = nulls(30_001, null_frac, seed=9)
+    n = int(dl.sum())
+    if ptype == abi.FIXED_LEN_BYTE_ARRAY:
+        vals = [rng.integers(0, 256, size=tl, dtype=np.uint8).tobytes() for _ in range(n)]
+    else:
+        dt = abi.numpy_dtype(ptype)
+        vals = rng.integers(0, 256, size=n * dt.itemsize, dtype=np.uint8).view(dt)
+    run_both(decoder, [make(ptype, vals, abi.BYTE_STREAM_SPLIT, def_levels=dl, max_def=1, type_length=tl,
+                            page_rows=7001)])
+
+
+def test_byte_stream_split_errors(decoder):
+    ch = make(abi.FLOAT, np.arange(3000, dtype=np.float32), abi.BYTE_STREAM_SPLIT, page_rows=1000)
+    ch.pages[1].body = ch.pages[1].body[:-1]   # length not a multiple of 4
+    run_both(decoder, [ch], expect_error=True)
+    ch = make(abi.DOUBLE, np.arange(3000, dtype=np.float64), abi.BYTE_STREAM_SPLIT, page_rows=1000)
+    ch.pages[2].body = ch.pages[2].body[:-16]  # fewer encoded values than the page reads
+    run_both(decoder, [ch], expect_error=True)
+
+
+@pytest.mark.parametrize("ptype,tl", [(abi.FIXED_LEN_BYTE_ARRAY, 16), (abi.FIXED_LEN_BYTE_ARRAY, 5),
+                                      (abi.FIXED_LEN_BYTE_ARRAY, 8), (abi.INT96, 0)])
+def test_fixed_len_dictionary(decoder, ptype, tl):
+    rng = np.random.default_rng(tl)
+    w = abi.elem_width(ptype, tl)
+    words = [rng.integers(0, 256, size=w, dtype=np.uint8).tobytes() for _ in range(300)]
+    runs = np.minimum(rng.zipf(1.5, size=20000), 500)
+    ids = np.repeat(rng.integers(0, 300, size=runs.size), runs)[:20000]
+    run_both(decoder, [make(ptype, [words[i] for i in ids], abi.RLE_DICTIONARY, type_length=tl, page_rows=6000)])
+
+
+def test_host_path_binary(decoder):
+    """pqg_decode_host with BYTE_ARRAY columns (offsets + bytes back in host memory), including
+    a dictionary column that needs more bytes than the first estimate."""
+    words = [bytes([97 + i % 26]) * (100 + i) for i in range(50)]
+    chunks = [make(abi.BYTE_ARRAY, _strings(20000, 7), abi.PLAIN),
+              make(abi.BYTE_ARRAY, [words[i % 50] for i in range(20000)], abi.RLE_DICTIONARY)]
+    batch = writer.build_batch(chunks)
+    ref = pqref.decode_batch(batch, binary_capacity=1 << 23)
+    rc, st, res, counts = decoder.decode_host(batch)
+    assert rc == 0, st.message
+    for i in range(2):
+        assert res[i]["values"] == ref.columns[i]["values"]

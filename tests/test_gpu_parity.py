@@ -29,6 +29,8 @@ def run_both(decoder, chunks, expect_error=False):
         col = dcols[i]
         assert col.n_values == ref.columns[i]["n_values"]
         assert_same(col.numpy(), ref.columns[i]["values"], cd["physical_type"])
+        if cd["physical_type"] == abi.BYTE_ARRAY:
+            assert np.array_equal(col.offsets().cpu().numpy(), ref.columns[i]["offsets"][:col.n_values + 1])
         if cd["max_def"] > 0:
             assert np.array_equal(col.def_levels[:batch.column_slots[i]].cpu().numpy(), ref.columns[i]["def_levels"])
         if cd["max_rep"] > 0:
@@ -276,3 +278,4 @@ def test_host_path_roundtrip(decoder):
     assert rc == 0, st.message
     assert np.array_equal(res[0]["values"], vals)
     assert counts.sum() == vals.size
+
