@@ -85,7 +85,8 @@ int elem_width(int t, int tl) {
 // Kernel classes, in launch order after the level pass.
 //   C_IDS   dictionary pages whose values are not 4 / 8 bytes (BYTE_ARRAY, FLBA, INT96): ids first
 //   C_BINP  PLAIN BYTE_ARRAY          C_DLBA  DELTA_LENGTH_BYTE_ARRAY      C_BSS  BYTE_STREAM_SPLIT
-enum Cls { C_DICT4 = 0, C_DICT8, C_IDS, C_PLAIN, C_BOOL, C_DELTA4, C_DELTA8, C_BSS, C_BINP, C_DLBA, C_NCLS };
+//   C_DBA   DELTA_BYTE_ARRAY (lengths here; values by k_dba_copy after the offset scan)
+enum Cls { C_DICT4 = 0, C_DICT8, C_IDS, C_PLAIN, C_BOOL, C_DELTA4, C_DELTA8, C_BSS, C_BINP, C_DLBA, C_DBA, C_NCLS };
 constexpr int N_DICT_CLS = 3;  // C_DICT4, C_DICT8, C_IDS: run-record walk + chunk expansion
 
 struct HostErr {
@@ -364,8 +365,14 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
         else
           herr = PQG_ERR_UNSUPPORTED;      // Encoding.java :130-143
         break;
+      case PQG_DELTA_BYTE_ARRAY:
+        // Encoding.java :219-222 also allows FIXED_LEN_BYTE_ARRAY; its fixed-width output form has
+        // no room for the variable lengths the reader may return (next row)
+        if (t == PQG_BYTE_ARRAY) { cls = C_DBA; w.bin_kind = pqg::BIN_DBA; }
+        else herr = PQG_ERR_UNSUPPORTED;
+        break;
       default:
-        herr = PQG_ERR_UNSUPPORTED;        // DELTA_BYTE_ARRAY: next row
+        herr = PQG_ERR_UNSUPPORTED;
     }
     if (herr) {
       P->host_errs.push_back(HostErr{p, 0, 2, herr});
@@ -589,6 +596,7 @@ int pqg_plan_launch(pqg_plan* P) {
         e = pqg::launch_bin_walk(s, P->d_bytes, P->n_bytes, work, cols, l, n, 0, P->n_pages, err, ecount);
         break;
       case C_DLBA: e = pqg::launch_dlba_lengths(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_DBA: e = pqg::launch_dba_lengths(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_PLAIN: e = pqg::launch_plain(0, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_BOOL: e = pqg::launch_plain(1, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_DELTA4: e = pqg::launch_delta(4, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
@@ -605,6 +613,8 @@ int pqg_plan_launch(pqg_plan* P) {
   if (e == hipSuccess && P->n_bin_chunks)
     e = pqg::launch_bin_copy(s, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->bin_chunks.p, P->n_bin_chunks,
                              err, ecount);
+  if (e == hipSuccess && P->cls_n[C_DBA])
+    e = pqg::launch_dba_copy(s, P->d_bytes, P->n_bytes, work, cols, lists + P->cls_off[C_DBA], P->cls_n[C_DBA]);
   ctx->last_launched = P;
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }

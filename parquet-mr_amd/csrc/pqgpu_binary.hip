@@ -475,6 +475,94 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
 }
 
 // ---------------------------------------------------------------------------
+// DELTA_BYTE_ARRAY values (DeltaByteArrayReader.readBytes :57-79): value i = the first prefix_i
+// bytes of value i - 1, then suffix i. The dependency is serial across values, so one wave walks
+// a page's values in order with the previous value in LDS: per batch of 64 values the suffix
+// bytes are staged into LDS in one coalesced pass, then each value is assembled byte-parallel
+// (prefix from the previous value's LDS copy, suffix from the staging buffer) and stored. k_delta
+// MODE 2 left bsrc = prefix length, blen = value length (0 from the first invalid value on; the
+// errors are reported there) and PageWork::aux = start of the suffix bytes. A value longer than
+// the LDS buffer takes its prefix from the previous value's output in global memory.
+constexpr uint32_t DBA_VB = 2048;  // LDS bytes per value buffer (previous / current)
+constexpr uint32_t DBA_SB = 4096;  // LDS suffix staging bytes per batch
+
+__global__ __launch_bounds__(64 * WPB) void k_dba_copy(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                       const PageWork* __restrict__ work,
+                                                       const ColumnDev* __restrict__ cols,
+                                                       const int32_t* __restrict__ list, int n_list) {
+  __shared__ uint8_t vbuf_all[WPB][2][DBA_VB];
+  __shared__ uint32_t sbuf_all[WPB][DBA_SB / 4 + 1];
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
+  const PageWork& pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint32_t N = uni(pw.n_values);
+  const uint64_t v0 = pw.out_offset;
+  const int64_t* offs = (const int64_t*)cd.values + v0;
+  uint8_t* dst = cd.binary_data;
+  const uint64_t cap = cd.binary_capacity;
+  const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  uint8_t(*vbuf)[DBA_VB] = vbuf_all[wave_id()];
+  uint32_t* sbuf = sbuf_all[wave_id()];
+  const uint8_t* sb8 = (const uint8_t*)sbuf;
+  uint32_t sp = uni(pw.aux);  // next suffix byte (page-relative)
+  uint32_t cur = 0;
+  bool prev_lds = true;       // the previous value is in vbuf[cur ^ 1]
+  uint64_t prev_off = 0;      // its output offset
+  for (uint32_t i0 = 0; i0 < N; i0 += WAVE) {
+    const uint32_t i = i0 + lane;
+    const bool in = i < N;
+    const uint32_t L = in ? cd.blen[v0 + i] : 0u;
+    uint32_t P = in ? cd.bsrc[v0 + i] : 0u;
+    P = P < L ? P : L;
+    const uint32_t S = L - P;
+    uint32_t stot;
+    const uint32_t sx = wave_excl_scan_u32(S, &stot);
+    const uint64_t off = in ? (uint64_t)offs[i] : 0;
+    const bool staged = stot <= DBA_SB;
+    if (staged) {
+      for (uint32_t o = 4u * lane; o < stot; o += 4u * WAVE) sbuf[o >> 2] = ld4_any(rs, sp + o);
+      wave_sync();
+    }
+    const uint32_t nb = N - i0 < WAVE ? N - i0 : WAVE;
+    for (uint32_t t = 0; t < nb; t++) {
+      const uint32_t len = rdl(L, t), pre = rdl(P, t), so = rdl(sx, t);
+      const uint64_t o = ((uint64_t)rdl((uint32_t)(off >> 32), t) << 32) | rdl((uint32_t)off, t);
+      if (len == 0) {  // empty value (or past an error)
+        prev_lds = true;
+        cur ^= 1;
+        continue;
+      }
+      const bool fits = len <= DBA_VB;
+      if (pre && !prev_lds) __builtin_amdgcn_s_waitcnt(0);  // the previous value's stores, read below
+      for (uint32_t j = lane; j < len; j += WAVE) {
+        uint32_t b;
+        if (j < pre) {
+          if (prev_lds) {
+            b = vbuf[cur ^ 1][j];
+          } else {
+            const uint64_t a = prev_off + j;
+            b = a < cap ? (sld((const uint32_t*)(dst + (a & ~3ull))) >> ((a & 3u) * 8u)) & 0xFFu : 0u;
+          }
+        } else {
+          const uint32_t q = so + j - pre;
+          b = staged ? sb8[q] : (ld32(rs, (sp + q) & ~3u) >> (((sp + q) & 3u) * 8u)) & 0xFFu;
+        }
+        if (fits) vbuf[cur][j] = (uint8_t)b;
+        if (o + j < cap) gst(dst + o + j, (uint8_t)b);
+      }
+      wave_sync();
+      prev_lds = fits;
+      prev_off = o;
+      cur ^= 1;
+    }
+    sp += stot;
+    wave_sync();  // the next batch overwrites the staging buffer
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Launchers
 
 #define PQG_BIN_ARGS bytes, n_bytes, work, cols, list, n, err, err_count
@@ -515,6 +603,13 @@ hipError_t launch_bin_scan(hipStream_t st, const ColumnDev* cols, const int32_t*
   hipLaunchKernelGGL(k_bin_block_sums, dim3(n_blocks), dim3(256), 0, st, cols, blocks);
   hipLaunchKernelGGL(k_bin_block_bases, dim3(n_bin_cols), dim3(256), 0, st, cols, bin_cols);
   hipLaunchKernelGGL(k_bin_offsets, dim3(n_blocks), dim3(256), 0, st, cols, blocks);
+  return hipGetLastError();
+}
+
+hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                           const ColumnDev* cols, const int32_t* list, int n) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dba_copy, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, list, n);
   return hipGetLastError();
 }
 

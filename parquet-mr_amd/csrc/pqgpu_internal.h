@@ -59,7 +59,7 @@ struct PageWork {
   uint32_t reserved;
 };
 
-enum BinKind : uint32_t { BIN_PLAIN = 0, BIN_DLBA = 1, BIN_DICT = 2 };
+enum BinKind : uint32_t { BIN_PLAIN = 0, BIN_DLBA = 1, BIN_DICT = 2, BIN_DBA = 3 };
 
 // Output chunk of k_dict_expand: CH_TILES x 64 lanes x 16 bytes.
 #ifndef PQG_CHUNK_TILES
@@ -89,6 +89,11 @@ hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
 // DELTA_LENGTH_BYTE_ARRAY lengths (k_delta into blen, records PageWork::aux)
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+// DELTA_BYTE_ARRAY prefix / suffix lengths (k_delta MODE 2: bsrc = prefix, blen = value length, aux)
+hipError_t launch_dba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                              const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                           const ColumnDev* cols, const int32_t* list, int n);
 // pqgpu_binary.hip
 constexpr uint32_t BIN_CHUNK = 256;     // values per k_bin_copy chunk
 constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block

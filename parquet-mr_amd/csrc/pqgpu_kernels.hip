@@ -1419,69 +1419,51 @@ __global__ __launch_bounds__(64 * WPB) void k_plain_bool(const uint8_t* __restri
 // wave-wide inclusive scan (wrapping int64) turns them into values. INT32 =
 // (int) of the long (readInteger :103-107).
 //
-// DLBA: the lengths of DELTA_LENGTH_BYTE_ARRAY pages (DeltaLengthByteArrayValuesReader.initFromPage
-// :44-48 reads them with this reader, then takes the remaining stream as the value bytes): the
-// lengths go to ColumnDev::blen, the stream position after the length stream to PageWork::aux,
-// and a negative length (in.slice(negative) -> IllegalArgumentException) is reported at its value.
-template <int W, bool DLBA = false>
-__global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                              PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
-                                              const int32_t* __restrict__ list, int n_list, uint64_t* err,
-                                              uint32_t* err_count) {
-  const int page = wave_page(list, n_list);
-  if (page < 0) return;
-  const PageWork pw = work[page];
-  const ColumnDev cd = cols[pw.column];
+// One stream [p, end) -> out[0 .. min(want, total)). Returns 0 or the init error code (the
+// reader decodes eagerly in initFromPage); *p_end = stream position after the used miniblocks,
+// *total_out = the header's value count. NEG: a negative (int) value is reported as CORRUPT at
+// its index and written as 0 (DELTA_LENGTH_BYTE_ARRAY lengths: in.slice(negative)).
+template <int W, bool NEG>
+__device__ int delta_stream(Window& win, uint32_t p, uint32_t end, uint32_t want, typename DictVal<W>::T* out,
+                            int page, uint64_t* err, uint32_t* err_count, uint32_t* p_end, uint32_t* total_out) {
+  typedef typename DictVal<W>::T T;
   const uint32_t lane = lane_id();
-  const uint32_t beg = uni(pw.data_begin), end = uni(pw.size);
-  const uint32_t want = uni(pw.n_values);
-  Window win;
-  win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
-  win.seek(beg);
-  uint32_t p = beg, len;
+  uint32_t len;
+  win.seek(p);
   // header (DeltaBinaryPackingConfig.readConfig :43-45, totalValueCount, first value)
-#define DELTA_FAIL(code_)                                              \
-  do {                                                                 \
-    if (lane == 0) report(err, err_count, page, 0, 2, (code_));        \
-    return;                                                            \
-  } while (0)
-  if (p >= end) DELTA_FAIL(PQG_ERR_EOF);
+  if (p >= end) return PQG_ERR_EOF;
   uint32_t block = read_uvarint(win, p, end - p, len);
-  if ((uint64_t)p + len > end) DELTA_FAIL(PQG_ERR_EOF);
+  if ((uint64_t)p + len > end) return PQG_ERR_EOF;
   p += len;
-  if (p >= end) DELTA_FAIL(PQG_ERR_EOF);
+  if (p >= end) return PQG_ERR_EOF;
   uint32_t mbn = read_uvarint(win, p, end - p, len);
-  if ((uint64_t)p + len > end) DELTA_FAIL(PQG_ERR_EOF);
+  if ((uint64_t)p + len > end) return PQG_ERR_EOF;
   p += len;
   // DeltaBinaryPackingConfig ctor :34-41 (double division, % 8)
-  if (mbn == 0 || (int32_t)mbn < 0 || (int32_t)block < 0) DELTA_FAIL(mbn == 0 ? PQG_ERR_DELTA_CONFIG : PQG_ERR_CORRUPT);
-  if ((block % mbn) != 0 || ((block / mbn) % 8u) != 0) DELTA_FAIL(PQG_ERR_DELTA_CONFIG);
+  if (mbn == 0 || (int32_t)mbn < 0 || (int32_t)block < 0) return mbn == 0 ? PQG_ERR_DELTA_CONFIG : PQG_ERR_CORRUPT;
+  if ((block % mbn) != 0 || ((block / mbn) % 8u) != 0) return PQG_ERR_DELTA_CONFIG;
   const uint32_t mbs = block / mbn;
-  if (mbs == 0) DELTA_FAIL(PQG_ERR_CORRUPT);
+  if (mbs == 0) return PQG_ERR_CORRUPT;
   // register budget of this kernel: block <= 512 values, <= 8 miniblocks (parquet-mr default 128 / 4)
-  if (block > 512u || mbn > 8u) DELTA_FAIL(PQG_ERR_UNSUPPORTED);
-  if (p >= end) DELTA_FAIL(PQG_ERR_EOF);
+  if (block > 512u || mbn > 8u) return PQG_ERR_UNSUPPORTED;
+  if (p >= end) return PQG_ERR_EOF;
   uint32_t total = read_uvarint(win, p, end - p, len);
-  if ((uint64_t)p + len > end) DELTA_FAIL(PQG_ERR_EOF);
+  if ((uint64_t)p + len > end) return PQG_ERR_EOF;
   p += len;
-  if ((int32_t)total < 0) DELTA_FAIL(PQG_ERR_CORRUPT);
-  if (p >= end) DELTA_FAIL(PQG_ERR_EOF);
+  if ((int32_t)total < 0) return PQG_ERR_CORRUPT;
+  if (p >= end) return PQG_ERR_EOF;
   uint64_t fraw = read_uvarlong(win, p, end - p, len);
-  if ((uint64_t)p + len > end) DELTA_FAIL(PQG_ERR_EOF);
+  if ((uint64_t)p + len > end) return PQG_ERR_EOF;
   p += len;
   const int64_t first = zigzag64(fraw);
-  // values to emit: min(want, total); want > total -> "no more value to read" at index total
-  uint32_t n_out = want;
-  if (want > total) {
-    n_out = total;
-  }
-  typedef typename DictVal<W>::T T;
-  T* out = (DLBA ? (T*)cd.blen : (T*)cd.values) + pw.out_offset;
+  *total_out = total;
+  // values to emit: min(want, total); want > total -> "no more value to read" at index total (caller)
+  const uint32_t n_out = want > total ? total : want;
   // Value index k (0-based) of the page: k = 0 is `first`; block b covers
   // k in [1 + b*block, 1 + (b+1)*block).
   uint64_t carry = (uint64_t)first;
   if (lane == 0 && n_out > 0) {
-    if (DLBA && (int32_t)(uint32_t)carry < 0) {
+    if (NEG && (int32_t)(uint32_t)carry < 0) {
       report(err, err_count, page, 2, 0, PQG_ERR_CORRUPT);
       gst(out, (T)0);
     } else {
@@ -1490,20 +1472,18 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
   }
   uint32_t buffered = 1;  // Java valuesBuffered (includes the first value)
   const uint32_t E = (block + WAVE - 1) / WAVE;  // deltas per lane per block
-  bool fail = false;
-  int fail_code = 0;
   while (buffered < total) {
     // ---- walk up to 64 blocks (headers + data offsets)
     uint32_t b_data = 0, b_wpos = 0, b_lo = 0, b_hi = 0, b_nmb = 0;
     uint32_t nb = 0;
     uint32_t blk_first = buffered;
     while (nb < 64u && buffered < total) {
-      if (p >= end) { fail = true; fail_code = PQG_ERR_EOF; break; }
+      if (p >= end) return PQG_ERR_EOF;
       uint64_t mraw = read_uvarlong(win, p, end - p, len);               // loadNewBlockToBuffer :122-126
-      if ((uint64_t)p + len > end) { fail = true; fail_code = PQG_ERR_EOF; break; }
+      if ((uint64_t)p + len > end) return PQG_ERR_EOF;
       p += len;
       int64_t mind = zigzag64(mraw);
-      if ((uint64_t)p + mbn > end) { fail = true; fail_code = PQG_ERR_EOF; break; }  // readBitWidthsForMiniBlocks
+      if ((uint64_t)p + mbn > end) return PQG_ERR_EOF;                  // readBitWidthsForMiniBlocks
       uint32_t wpos = p;
       p += mbn;
       // miniblocks unpacked while buffered < total (:131-135)
@@ -1512,13 +1492,12 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
       uint32_t bufd = buffered;
       for (uint32_t m = 0; m < mbn && bufd < total; m++) {
         uint32_t wm = win.byte(wpos + m);
-        if (wm > 64u) { fail = true; fail_code = PQG_ERR_CORRUPT; break; }
+        if (wm > 64u) return PQG_ERR_CORRUPT;
         dbytes += (uint64_t)wm * (mbs / 8u);
         bufd += mbs;
         used++;
       }
-      if (fail) break;
-      if ((uint64_t)p + dbytes > end) { fail = true; fail_code = PQG_ERR_EOF; break; }  // in.slice EOF
+      if ((uint64_t)p + dbytes > end) return PQG_ERR_EOF;               // in.slice EOF
       const bool me = lane == nb;
       b_data = me ? p : b_data;
       b_wpos = me ? wpos : b_wpos;
@@ -1530,7 +1509,6 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
       buffered = bufd;
       nb++;
     }
-    if (fail) break;
     // ---- expand the walked blocks
     for (uint32_t b = 0; b < nb; b++) {
       const uint32_t data = rdl(b_data, b), wpos = rdl(b_wpos, b), nmb = rdl(b_nmb, b);
@@ -1593,7 +1571,7 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
         uint64_t k = (uint64_t)k0 + j;
         if (q < E && j < block && k < n_out) {
           T v = (T)(base_v + loc[q]);
-          if (DLBA && (int32_t)(uint32_t)v < 0) {
+          if (NEG && (int32_t)(uint32_t)v < 0) {
             report(err, err_count, page, 2, k, PQG_ERR_CORRUPT);
             v = 0;
           }
@@ -1603,13 +1581,95 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
       carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
     }
   }
-  if (fail) {
-    if (lane == 0) report(err, err_count, page, 0, 2, fail_code);
+  *p_end = p;
+  return 0;
+}
+
+// MODE 0: DELTA_BINARY_PACKED values. MODE 1 (DLBA): the lengths of DELTA_LENGTH_BYTE_ARRAY
+// pages (DeltaLengthByteArrayValuesReader.initFromPage :44-48 reads them with this reader, then
+// takes the remaining stream as the value bytes) -> ColumnDev::blen, value bytes start ->
+// PageWork::aux. MODE 2 (DBA): DELTA_BYTE_ARRAY pages (DeltaByteArrayReader.initFromPage :45-48):
+// prefix lengths -> bsrc, suffix lengths -> blen, suffix bytes start -> aux; then per value the
+// checks of readBytes :57-79 in the reference's order and blen <- prefix + suffix length.
+template <int W, int MODE = 0>
+__global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                              PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                              const int32_t* __restrict__ list, int n_list, uint64_t* err,
+                                              uint32_t* err_count) {
+  typedef typename DictVal<W>::T T;
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
+  const PageWork pw = work[page];
+  const ColumnDev cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint32_t beg = uni(pw.data_begin), end = uni(pw.size);
+  const uint32_t want = uni(pw.n_values);
+  Window win;
+  win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  uint32_t p_end = beg, total = 0;
+  T* out = (MODE == 0 ? (T*)cd.values : MODE == 1 ? (T*)cd.blen : (T*)cd.bsrc) + pw.out_offset;
+  int code = delta_stream<W, MODE == 1>(win, beg, end, want, out, page, err, err_count, &p_end, &total);
+  if (code) {
+    if (lane == 0) report(err, err_count, page, 0, 2, code);
     return;
   }
-  if (want > total && lane == 0) report(err, err_count, page, 2, total, PQG_ERR_DELTA_PAST_END);
-  if (DLBA && lane == 0) work[page].aux = p;
-#undef DELTA_FAIL
+  uint32_t past_end = want > total ? total : 0xFFFFFFFFu;  // first index with no value
+  if constexpr (MODE == 2) {
+    uint32_t total2 = 0, p2 = p_end;
+    code = delta_stream<4, false>(win, p_end, end, want, cd.blen + pw.out_offset, page, err, err_count, &p2, &total2);
+    if (code) {
+      if (lane == 0) report(err, err_count, page, 0, 2, code);
+      return;
+    }
+    p_end = p2;
+    if (want > total2 && total2 < past_end) past_end = total2;
+    // readBytes checks per value i, in order: prefix / suffix length past the streams
+    // (DELTA_PAST_END), suffix length < 0 (slice(negative)), suffix bytes past the page (EOF),
+    // then for prefix != 0: new byte[prefix + suffix] < 0, arraycopy(previous, 0, out, 0, prefix)
+    // with prefix < 0 or > previous.length. blen becomes the value length (0 past an error).
+    const uint32_t n_chk = want < past_end ? want : past_end;
+    const uint32_t avail = end > p_end ? end - p_end : 0;
+    uint32_t* pl = cd.bsrc + pw.out_offset;
+    uint32_t* sl = cd.blen + pw.out_offset;
+    uint64_t s_carry = 0;
+    uint32_t prev_len = 0;  // previous value of the page (empty before the first, :41)
+    uint32_t first_bad = 0xFFFFFFFFu;
+    // the lengths were just stored by this wave: wait for them, then read past the L1 (a line
+    // shared with a neighbouring page may sit in this CU's L1 from before those stores)
+    __builtin_amdgcn_s_waitcnt(0);
+    for (uint32_t i0 = 0; i0 < n_chk; i0 += WAVE) {
+      const uint32_t i = i0 + lane;
+      const bool in = i < n_chk;
+      const int32_t pre = in ? (int32_t)sld(pl + i) : 0;
+      const int32_t suf = in ? (int32_t)sld(sl + i) : 0;
+      const uint64_t sv = suf > 0 ? (uint64_t)suf : 0;
+      uint64_t incl = sv;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(incl, o);
+        if ((int)lane >= o) incl += y;
+      }
+      const int32_t full = (int32_t)((uint32_t)pre + (uint32_t)suf);
+      uint32_t prev = __shfl_up((uint32_t)(full < 0 ? 0 : full), 1);
+      if (lane == 0) prev = prev_len;
+      int c = 0;
+      if (in) {
+        if (suf < 0) c = PQG_ERR_CORRUPT;
+        else if (s_carry + incl > avail) c = PQG_ERR_EOF;
+        else if (pre != 0 && (full < 0 || pre < 0 || (uint32_t)pre > prev)) c = PQG_ERR_CORRUPT;
+      }
+      if (c) report(err, err_count, page, 2, i, c);
+      const uint64_t bad = __ballot(c != 0);
+      if (bad && first_bad == 0xFFFFFFFFu) first_bad = i0 + (uint32_t)__builtin_ctzll(bad);
+      const uint32_t fb = uni(first_bad);
+      if (in) gst(sl + i, (c || i >= fb) ? 0u : (uint32_t)full);
+      prev_len = rdl((uint32_t)(full < 0 ? 0 : full), WAVE - 1);
+      s_carry += rdl((uint32_t)incl, WAVE - 1) | ((uint64_t)rdl((uint32_t)(incl >> 32), WAVE - 1) << 32);
+    }
+    // values past an error or past the streams hold length 0 (blen was cleared before the launch)
+  }
+  if (past_end != 0xFFFFFFFFu && lane == 0) report(err, err_count, page, 2, past_end, PQG_ERR_DELTA_PAST_END);
+  if (MODE != 0 && lane == 0) work[page].aux = p_end;
 }
 
 // ---------------------------------------------------------------------------
@@ -1737,7 +1797,14 @@ hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL((k_delta<4, true>), dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
+  hipLaunchKernelGGL((k_delta<4, 1>), dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
+  return hipGetLastError();
+}
+
+hipError_t launch_dba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                              const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL((k_delta<4, 2>), dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   return hipGetLastError();
 }
 

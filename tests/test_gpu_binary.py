@@ -148,3 +148,55 @@ def test_host_path_binary(decoder):
     assert rc == 0, st.message
     for i in range(2):
         assert res[i]["values"] == ref.columns[i]["values"]
+
+
+# ---- DELTA_BYTE_ARRAY (DeltaByteArrayReader) -----------------------------------------------------------------
+
+def _dba_vals(kind, n, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "urls":      # sorted keys sharing long prefixes (the encoding's use case)
+        return sorted(f"https://example.org/{rng.integers(0, 50)}/item/{rng.integers(0, 10**6):07d}".encode()
+                      for _ in range(n))
+    if kind == "random":
+        return _strings(n, seed, 0, 24, alphabet=b"ab")
+    if kind == "long":      # values past the kernel's 2 KiB LDS value buffer, with shared prefixes
+        base = rng.integers(97, 123, size=6000, dtype=np.uint8).tobytes()
+        return [base[:rng.integers(0, 6000)] + bytes([97 + i % 26]) * int(rng.integers(0, 40)) for i in range(n)]
+    if kind == "growing":   # prefix i + 1 of value i + 1 = all of value i
+        return [b"x" * i for i in range(n)]
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind,n", [("urls", 30000), ("random", 30000), ("long", 400), ("growing", 700)])
+def test_delta_byte_array(decoder, kind, n):
+    run_both(decoder, [make(abi.BYTE_ARRAY, _dba_vals(kind, n, 5), abi.DELTA_BYTE_ARRAY, page_rows=5000)])
+
+
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("null_frac", [0.2, 1.0])
+def test_delta_byte_array_optional(decoder, version, null_frac):
+    dl = nulls(20_000, null_frac, seed=8)
+    vals = _dba_vals("urls", int(dl.sum()), 6)
+    run_both(decoder, [make(abi.BYTE_ARRAY, vals, abi.DELTA_BYTE_ARRAY, def_levels=dl, max_def=1, version=version,
+                            page_rows=6000)])
+
+
+def _dba_err(which):
+    from pqgpu import writer as W
+    if which == "prefix_too_long":   # prefix > previous.length (arraycopy IndexOutOfBounds)
+        body = W.delta_encode(np.array([0, 9], dtype=np.int32), abi.INT32) + W.dlba_encode([b"abc", b"x"])
+    elif which == "suffix_short":    # suffix bytes missing: "Failed to read N bytes"
+        body = W.dba_encode([b"abcdef", b"abcxyz", b"q"])[:-2]
+    elif which == "negative_suffix":  # slice(negative)
+        body = W.delta_encode(np.array([0, 0], dtype=np.int32), abi.INT32) + \
+            W.delta_encode(np.array([2, -5], dtype=np.int32), abi.INT32) + b"ab"
+    elif which == "prefix_stream_short":  # fewer prefix lengths than values: DELTA_PAST_END
+        body = W.delta_encode(np.array([0], dtype=np.int32), abi.INT32) + W.dlba_encode([b"abc", b"de"])
+    ch = make(abi.BYTE_ARRAY, [b"a", b"b"] if which != "suffix_short" else [b"a", b"b", b"c"], abi.DELTA_BYTE_ARRAY)
+    ch.pages[0].body = body
+    return ch
+
+
+@pytest.mark.parametrize("which", ["prefix_too_long", "suffix_short", "negative_suffix", "prefix_stream_short"])
+def test_delta_byte_array_errors(decoder, which):
+    run_both(decoder, [_dba_err(which)], expect_error=True)

@@ -11,7 +11,7 @@ from helpers import assert_same
 
 pytestmark = pytest.mark.gpu
 CASES = list(chunk_cases())
-GPU_DBA = False  # DELTA_BYTE_ARRAY on the device
+GPU_DBA = True  # DELTA_BYTE_ARRAY on the device
 
 
 @pytest.mark.parametrize("name,c", CASES, ids=[f"{n}:{c['key']}:{c['path']}" for n, c in CASES])
