@@ -89,11 +89,62 @@ def delta_encode(values, physical_type, block=128, miniblocks=4):
     return _call_with_buffer(fn, v.ctypes.data, len(v), block, miniblocks, cap=cap)
 
 
+class BinaryValues:
+    """BYTE_ARRAY values as numpy arrays (offsets[n + 1], data) for large synthetic inputs; slices
+    like a list of bytes."""
+
+    def __init__(self, offsets, data):
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        self.data = np.ascontiguousarray(data, dtype=np.uint8)
+
+    @classmethod
+    def random(cls, n, min_len, max_len, seed, alphabet=b"abcdefghijklmnopqrstuvwxyz0123456789"):
+        rng = np.random.default_rng(seed)
+        lens = rng.integers(min_len, max_len + 1, size=n)
+        offs = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        a = np.frombuffer(alphabet, dtype=np.uint8)
+        return cls(offs, a[rng.integers(0, a.size, size=int(offs[-1]), dtype=np.uint8)])
+
+    def __len__(self):
+        return self.offsets.size - 1
+
+    def lengths(self):
+        return np.diff(self.offsets)
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            a, b, _ = k.indices(len(self))
+            o = self.offsets[a:b + 1]
+            return BinaryValues(o - o[0], self.data[o[0]:o[-1]])
+        return self.data[self.offsets[k]:self.offsets[k + 1]].tobytes()
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield self[i]
+
+
+def _plain_binary_np(v):
+    """[4-byte LE length][bytes] per value, vectorized (BinaryValues)."""
+    n = len(v)
+    lens = v.lengths()
+    out = np.empty(4 * n + v.data.size, dtype=np.uint8)
+    starts = v.offsets[:-1] + 4 * np.arange(n, dtype=np.int64)  # where each length prefix goes
+    lb = lens.astype("<u4").view(np.uint8).reshape(n, 4)
+    for k in range(4):
+        out[starts + k] = lb[:, k]
+    owner = np.repeat(np.arange(n, dtype=np.int64), lens)
+    out[np.arange(v.data.size, dtype=np.int64) + 4 * (owner + 1)] = v.data
+    return out.tobytes()
+
+
 def plain_encode(values, physical_type, type_length=0):
     """PlainValuesWriter / BooleanPlainValuesWriter / FixedLenByteArrayPlainValuesWriter."""
     if physical_type == abi.BOOLEAN:
         bits = np.ascontiguousarray(values, dtype=np.uint8) & 1
         return np.packbits(bits, bitorder="little").tobytes()
+    if physical_type == abi.BYTE_ARRAY and isinstance(values, BinaryValues):
+        return _plain_binary_np(values)
     if physical_type == abi.BYTE_ARRAY:
         out = bytearray()
         for b in values:
@@ -108,6 +159,8 @@ def plain_encode(values, physical_type, type_length=0):
 def dlba_encode(values):
     """DeltaLengthByteArrayValuesWriter.getBytes (deltalengthbytearray/DeltaLengthByteArrayValuesWriter.java:77-86):
     DELTA_BINARY_PACKED int lengths (128 / 4), then the concatenated bytes."""
+    if isinstance(values, BinaryValues):
+        return delta_encode(values.lengths().astype(np.int32), abi.INT32) + values.data.tobytes()
     vals = [bytes(b) for b in values]
     lens = np.array([len(b) for b in vals], dtype=np.int32)
     return delta_encode(lens, abi.INT32) + b"".join(vals)
@@ -117,6 +170,23 @@ def dba_encode(values):
     """DeltaByteArrayWriter.writeBytes / getBytes (deltastrings/DeltaByteArrayWriter.java:56-58, 90-100):
     prefix lengths shared with the previous value (DELTA_BINARY_PACKED), then the suffixes as
     DELTA_LENGTH_BYTE_ARRAY. `previous` starts empty on every page (reset :65-70)."""
+    if isinstance(values, BinaryValues) and len(values) > 1:
+        # vectorized: values padded into rows, prefix = first mismatch with the previous row
+        lens = values.lengths()
+        L = int(lens.max()) + 1
+        n = len(values)
+        rows = np.zeros((n, L), dtype=np.int16) - 1
+        owner = np.repeat(np.arange(n), lens)
+        col = np.arange(values.data.size) - np.repeat(values.offsets[:-1], lens)
+        rows[owner, col] = values.data
+        neq = rows[1:] != rows[:-1]
+        pre = np.zeros(n, dtype=np.int32)
+        pre[1:] = np.where(neq.any(axis=1), np.argmax(neq, axis=1), L)
+        pre[1:] = np.minimum(pre[1:], np.minimum(lens[1:], lens[:-1]))
+        keep = np.arange(values.data.size) - np.repeat(values.offsets[:-1], lens) >= np.repeat(pre, lens)
+        sfx_lens = (lens - pre).astype(np.int64)
+        sfx = BinaryValues(np.concatenate([[0], np.cumsum(sfx_lens)]), values.data[keep])
+        return delta_encode(pre, abi.INT32) + dlba_encode(sfx)
     prev = b""
     prefixes, suffixes = [], []
     for b in values:

@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Decode throughput of every BASELINE.json config and encoding family beside the headline.
+
+bench.py prints the ONE headline line (C2). This suite times the other configs and the widened
+§8 rows on one GPU, inputs resident in HBM, one JSON line per workload:
+
+  c1_plain_i32   C1: 1M int32 PLAIN, required (plus the host-buffers-in / arrays-out path)
+  c2_zipf2       C2 stress variant: Zipf(2.0) run lengths (26 % of ids in bit-packed runs)
+  c3_mixed       C3: 8 optional columns (2 int32 + 2 int64 DELTA_BINARY_PACKED, 2 double PLAIN,
+                 2 BYTE_ARRAY PLAIN of 4-32 bytes), 10 % nulls, RLE def levels, V2 pages
+  c5_levels      C5: LIST<int64> records (Poisson(3) lengths, 10 % null lists / elements),
+                 rep + def levels and values (record assembly is the next row)
+  str_plain / str_dict / str_dlba / str_dba   BYTE_ARRAY encodings, 4-32 byte strings
+  bss_f64        BYTE_STREAM_SPLIT doubles
+  delta_i64      DELTA_BINARY_PACKED int64 random walk
+
+value = non-null values decoded per second; gbps = algorithmic bytes (encoded page bytes read +
+decoded values / offsets / bytes written + level bytes written) / launch time. cpu = the oracle
+(value-at-a-time restatement of the reference readers, 1 thread) on a bounded page sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "parquet-mr_amd"), REPO]
+
+from pqgpu import abi, writer  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+
+
+def nulls(n, frac, seed):
+    return (np.random.default_rng(seed).random(n) >= frac).astype(np.uint8)
+
+
+def gen(name, rows):
+    """-> list of ColumnChunk"""
+    rng = np.random.default_rng(7)
+    if name == "c1_plain_i32":
+        v = np.random.default_rng(1).integers(-2**31, 2**31 - 1, size=rows, dtype=np.int64).astype(np.int32)
+        return [writer.write_column_chunk(abi.INT32, v, abi.PLAIN)]
+    if name == "c2_zipf2":
+        import bench
+        ch, _, _ = bench.make_c2(rows, a=2.0)
+        return [ch]
+    if name == "c3_mixed":
+        dl = nulls(rows, 0.1, 8)
+        n = int(dl.sum())
+        out = []
+        for k in range(2):
+            walk = np.cumsum(rng.integers(-100, 1000, size=n)).astype(np.int64)
+            out.append(writer.write_column_chunk(abi.INT32, (walk % (1 << 30)).astype(np.int32), abi.DELTA_BINARY_PACKED,
+                                                 def_levels=dl, max_def=1, version=2))
+            out.append(writer.write_column_chunk(abi.INT64, walk * 1000 + k, abi.DELTA_BINARY_PACKED,
+                                                 def_levels=dl, max_def=1, version=2))
+            out.append(writer.write_column_chunk(abi.DOUBLE, rng.standard_normal(n), abi.PLAIN, def_levels=dl,
+                                                 max_def=1, version=2))
+            out.append(writer.write_column_chunk(abi.BYTE_ARRAY, writer.BinaryValues.random(n, 4, 32, seed=k), abi.PLAIN,
+                                                 def_levels=dl, max_def=1, version=2))
+            print(f"[gen c3_mixed] {len(out)} of 8 columns", file=sys.stderr, flush=True)
+        return out
+    if name == "c5_levels":
+        recs = rows
+        lens = rng.poisson(3, size=recs)
+        null_list = rng.random(recs) < 0.1
+        slots = np.where(null_list | (lens == 0), 1, lens)
+        n_slots = int(slots.sum())
+        starts = np.concatenate([[0], np.cumsum(slots)[:-1]])
+        rl = np.ones(n_slots, dtype=np.uint8)
+        rl[starts] = 0
+        dl = np.full(n_slots, 3, dtype=np.uint8)
+        dl[rng.random(n_slots) < 0.1] = 2
+        dl[starts[null_list]] = 0
+        dl[starts[~null_list & (lens == 0)]] = 1
+        n = int((dl == 3).sum())
+        vals = rng.integers(-2**40, 2**40, size=n)
+        return [writer.write_column_chunk(abi.INT64, vals, abi.PLAIN, def_levels=dl, rep_levels=rl, max_def=3, max_rep=1,
+                                          page_rows=20000)]
+    if name.startswith("str_"):
+        enc = {"str_plain": abi.PLAIN, "str_dict": abi.RLE_DICTIONARY, "str_dlba": abi.DELTA_LENGTH_BYTE_ARRAY,
+               "str_dba": abi.DELTA_BYTE_ARRAY}[name]
+        if enc == abi.RLE_DICTIONARY:
+            words = writer.BinaryValues.random(1000, 4, 32, seed=3)
+            runs = np.minimum(rng.zipf(1.5, size=rows), 4096)
+            ids = np.repeat(rng.integers(0, 1000, size=runs.size), runs)[:rows]
+            ids_fa, order = writer.first_appearance_ids(ids)
+            lens = words.lengths()[order]
+            offs = np.concatenate([[0], np.cumsum(lens)])
+            dwords = writer.BinaryValues(offs, np.concatenate([words.data[words.offsets[o]:words.offsets[o + 1]]
+                                                               for o in order]))
+            ch = writer.write_dict_column_from_ids(abi.BYTE_ARRAY, dwords, ids_fa)
+            return [ch]
+        if enc == abi.DELTA_BYTE_ARRAY:
+            # sorted keys with shared prefixes
+            keys = np.sort(rng.integers(0, 10**12, size=rows))
+            s = np.char.add(b"https://example.org/item/", np.char.zfill(keys.astype("S12"), 12))
+            lens = np.char.str_len(s)
+            offs = np.concatenate([[0], np.cumsum(lens)])
+            data = np.frombuffer(b"".join(s.tolist()), dtype=np.uint8)
+            return [writer.write_column_chunk(abi.BYTE_ARRAY, writer.BinaryValues(offs, data), enc)]
+        return [writer.write_column_chunk(abi.BYTE_ARRAY, writer.BinaryValues.random(rows, 4, 32, seed=5), enc)]
+    if name == "bss_f64":
+        return [writer.write_column_chunk(abi.DOUBLE, rng.standard_normal(rows), abi.BYTE_STREAM_SPLIT)]
+    if name == "delta_i64":
+        walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
+        return [writer.write_column_chunk(abi.INT64, walk, abi.DELTA_BINARY_PACKED)]
+    raise ValueError(name)
+
+
+def algo_bytes(batch, cols):
+    enc = int(batch.pages["size"].sum()) + sum(int(c["dict_size"]) for c in batch.columns if c["dict_offset"] >= 0)
+    out = 0
+    for i, cd in enumerate(batch.columns):
+        n = cols[i].n_values
+        if cd["physical_type"] == abi.BYTE_ARRAY:
+            out += 8 * (n + 1) + int(cols[i].offsets()[-1].item())
+        else:
+            out += n * abi.elem_width(cd["physical_type"], cd["type_length"])
+        out += batch.column_slots[i] * ((cd["max_def"] > 0) + (cd["max_rep"] > 0))
+    return enc, out
+
+
+def cpu_sample(chunks, max_pages, budget_s):
+    from oracle import pqref
+    sub = []
+    for ch in chunks:
+        c = writer.ColumnChunk(**{k: getattr(ch, k) for k in ("physical_type", "max_rep", "max_def", "type_length",
+                                                               "dict_page", "dict_num_values", "dict_encoding")})
+        c.pages = ch.pages[:max_pages]
+        sub.append(c)
+    b = writer.build_batch(sub)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        r = pqref.decode_batch(b)
+        assert r.code == 0, r.status
+        reps += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    nv = sum(c["n_values"] for c in r.columns)
+    return {"values_per_s": reps * nv / dt, "cores": 1, "kind": "port",
+            "sample": f"first {max_pages} pages of every column, {reps} reps, {dt:.1f} s"}
+
+
+def run(name, rows, steps, warmup, cpu_budget):
+    import torch
+    from pqgpu import decoder as D
+    t0 = time.perf_counter()
+    chunks = gen(name, rows)
+    batch = writer.build_batch(chunks)
+    t_gen = time.perf_counter() - t0
+    dec = D.Decoder(0)
+    dbatch = dec.upload(batch)
+    cols, st = dec.decode(dbatch)  # sizes BYTE_ARRAY buffers, first full decode
+    plan = dec.plan(dbatch, cols)
+    for _ in range(warmup):
+        plan.launch()
+    rc, st = plan.sync()
+    assert rc == 0, st.message
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    torch.cuda.synchronize()
+    ev[0].record(dec.stream)
+    for k in range(steps):
+        plan.launch()
+        ev[k + 1].record(dec.stream)
+    torch.cuda.synchronize()
+    rc, st = plan.sync()
+    assert rc == 0, st.message
+    ms = float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(steps)]))
+    nvals = sum(c.n_values for c in cols)
+    nslots = sum(batch.column_slots)
+    enc, out = algo_bytes(batch, cols)
+    gbps = (enc + out) / (ms / 1e3) / 1e9
+    res = {"workload": name, "rows": rows, "columns": len(batch.columns), "pages": batch.n_pages,
+           "values": nvals, "slots": nslots, "ms_per_launch": ms, "values_per_s": nvals / (ms / 1e3),
+           "encoded_bytes": enc, "output_bytes": out, "gbps": gbps, "hbm_frac": gbps / HBM_PEAK_GBS,
+           "kernels_per_launch": plan.kernel_count, "input_gen_s": t_gen}
+    if name == "c1_plain_i32":
+        t1 = time.perf_counter()
+        rc2, st2, res2, _ = dec.decode_host(batch)
+        e2e = time.perf_counter() - t1
+        assert rc2 == 0
+        res["e2e_host_values_per_s"] = nvals / e2e
+    if cpu_budget > 0:
+        res["cpu"] = cpu_sample(chunks, 50, cpu_budget)
+    plan.close()
+    dec.close()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("workloads", nargs="*", default=["c1_plain_i32", "c2_zipf2", "c3_mixed", "c5_levels", "str_plain",
+                                                     "str_dict", "str_dlba", "str_dba", "bss_f64", "delta_i64"])
+    ap.add_argument("--rows", type=int, default=None, help="override the per-workload row count")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cpu-budget", type=float, default=2.0)
+    ap.add_argument("--gen-only", action="store_true")
+    args = ap.parse_args()
+    default_rows = {"c1_plain_i32": 1_000_000, "c2_zipf2": 100_000_000, "c3_mixed": 100_000_000,
+                    "c5_levels": 100_000_000, "str_plain": 20_000_000, "str_dict": 20_000_000,
+                    "str_dlba": 20_000_000, "str_dba": 20_000_000, "bss_f64": 100_000_000, "delta_i64": 100_000_000}
+    for w in args.workloads:
+        rows = args.rows or default_rows[w]
+        if args.gen_only:
+            t0 = time.perf_counter()
+            b = writer.build_batch(gen(w, rows))
+            print(json.dumps({"workload": w, "rows": rows, "pages": b.n_pages, "bytes": int(b.data.size),
+                              "gen_s": time.perf_counter() - t0}), flush=True)
+            continue
+        print(json.dumps(run(w, rows, args.steps, args.warmup, args.cpu_budget)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -28,6 +28,15 @@ for s in $STEPS; do
       timeout -k 10 400 python -u bench.py --no-cpu --zipf 2.0 > "$OUT/bench_zipf2.json" 2> "$OUT/bench_zipf2.err" \
         || { tail -30 "$OUT/bench_zipf2.err"; exit 1; }
       cat "$OUT/bench_zipf2.json" ;;
+    suite)
+      timeout -k 10 900 python -u tools/bench_suite.py > "$OUT/suite.jsonl" 2> "$OUT/suite.err" \
+        || { tail -30 "$OUT/suite.err"; exit 1; }
+      cat "$OUT/suite.jsonl" ;;
+    suiteprof)
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/suiteprof" -o run -- \
+        python3 tools/bench_suite.py --cpu-budget 0 > "$OUT/suiteprof.jsonl" 2> "$OUT/suiteprof.err" \
+        || { tail -30 "$OUT/suiteprof.err"; exit 1; }
+      python3 tools/kstats.py "$OUT/suiteprof" ;;
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
         python3 bench.py --no-cpu > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
