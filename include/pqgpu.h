@@ -226,6 +226,38 @@ int pqg_unpack_runs(pqg_ctx* ctx, int bit_width, const uint8_t* d_in,
 int pqg_router_read(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_len,
                     int count, int32_t* out);
 
+/* ---- record assembly ---------------------------------------------------------
+ * Dremel assembly of ONE leaf column into the columnar form of its records: the
+ * Arrow-style equivalent of the converter events parquet-mr's automaton emits
+ * (RecordReaderImplementation.read, parquet-column/src/main/java/org/apache/parquet/io/RecordReaderImplementation.java:409-446,
+ * built by MessageColumnIO.getRecordReader, io/MessageColumnIO.java:77-130).
+ *
+ * `path` lists the schema nodes from the root's child down to the leaf. Entries of
+ * repetition depth r are the records (r = 0) or the elements of the r-th REPEATED node.
+ * A non-REPEATED node has one entry per entry of its depth (the number of REPEATED nodes
+ * at or above it); a REPEATED node's entries are its elements. Outputs (device pointers):
+ *   OPTIONAL node: validity[entry] = 1 when the node is present (a group the automaton opens,
+ *                  or a non-null leaf value);
+ *   REPEATED node: offsets[e] for every entry e of the enclosing depth, plus offsets[n] =
+ *                  this node's entry count (a list's elements are offsets[e] .. offsets[e+1]).
+ * The leaf's non-null values are the dense values pqg_decode wrote for the column.
+ * d_def_levels / d_rep_levels: the u8 levels pqg_decode wrote (NULL when the max level is 0).
+ * Synchronous. When an output is too small, returns PQG_ERR_INVALID_ARG with every
+ * n_entries filled in (nothing written). */
+enum pqg_repetition { PQG_REQUIRED = 0, PQG_OPTIONAL = 1, PQG_REPEATED = 2 };
+
+typedef struct pqg_assembly_node {
+  int32_t repetition;      /* pqg_repetition (parquet-format FieldRepetitionType) */
+  int32_t reserved;
+  uint8_t* validity;       /* OPTIONAL: 1 byte per entry; may be NULL */
+  int64_t* offsets;        /* REPEATED: offsets[n_enclosing_entries + 1]; may be NULL */
+  uint64_t capacity;       /* elements the validity / offsets array holds */
+  uint64_t n_entries;      /* OUT: entries of this node */
+} pqg_assembly_node;
+
+int pqg_assemble(pqg_ctx* ctx, const uint8_t* d_def_levels, const uint8_t* d_rep_levels, uint64_t n_slots,
+                 pqg_assembly_node* path, int depth, uint64_t* n_records, pqg_status* st);
+
 /* Human-readable name of an error code. */
 const char* pqg_error_name(int code);
 

@@ -141,6 +141,7 @@ struct pqg_ctx {
   pqg_column_desc* last_cols = nullptr;
   PinnedBuf pin_in, pin_out, pin_err;
   DevBuf host_bytes, host_out, host_counts, host_runs;
+  DevBuf asm_scratch;                // pqg_assemble: block counts + totals
 };
 
 extern "C" {
@@ -211,6 +212,7 @@ int pqg_ctx_destroy(pqg_ctx* c) {
   c->host_out.release();
   c->host_counts.release();
   c->host_runs.release();
+  c->asm_scratch.release();
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return PQG_OK;
@@ -943,6 +945,95 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   }
   if (h_page_value_counts && n_pages) std::memcpy(h_page_value_counts, counts.data(), sizeof(uint32_t) * (size_t)n_pages);
   return rc;
+}
+
+int pqg_assemble(pqg_ctx* ctx, const uint8_t* d_def_levels, const uint8_t* d_rep_levels, uint64_t n_slots,
+                 pqg_assembly_node* path, int depth, uint64_t* n_records, pqg_status* st) {
+  if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
+  if (!ctx || !path || depth <= 0 || depth > (int)pqg::ASM_MAX_NODES) {
+    set_status(st, PQG_ERR_INVALID_ARG, -1, -1, "assembly arguments");
+    return PQG_ERR_INVALID_ARG;
+  }
+  // levels of every node (ColumnIO repetition / definition level)
+  pqg::AsmParams P;
+  std::memset(&P, 0, sizeof(P));
+  P.n_nodes = (uint32_t)depth;
+  uint32_t r = 0, d = 0;
+  for (int k = 0; k < depth; k++) {
+    const int rp = path[k].repetition;
+    if (rp != PQG_REQUIRED && rp != PQG_OPTIONAL && rp != PQG_REPEATED) {
+      set_status(st, PQG_ERR_INVALID_ARG, -1, k, "assembly node repetition");
+      return PQG_ERR_INVALID_ARG;
+    }
+    if (rp == PQG_REPEATED) {
+      r++;
+      d++;
+      if (r >= pqg::ASM_MAX_DEPTHS) {
+        set_status(st, PQG_ERR_UNSUPPORTED, -1, k, "assembly: more than 7 repetition levels");
+        return PQG_ERR_UNSUPPORTED;
+      }
+      P.DR[r] = d;
+    } else if (rp == PQG_OPTIONAL) {
+      d++;
+    }
+    P.kind[k] = rp;
+    P.depth[k] = r;
+    P.D[k] = d;
+    P.validity[k] = rp == PQG_OPTIONAL ? path[k].validity : nullptr;
+    P.offsets[k] = rp == PQG_REPEATED ? path[k].offsets : nullptr;
+  }
+  P.max_rep = r;
+  if (d > 254) {
+    set_status(st, PQG_ERR_UNSUPPORTED, -1, -1, "assembly: definition level above 254");
+    return PQG_ERR_UNSUPPORTED;
+  }
+  if (n_slots && ((d > 0 && !d_def_levels) || (r > 0 && !d_rep_levels))) {
+    set_status(st, PQG_ERR_INVALID_ARG, -1, -1, "assembly levels");
+    return PQG_ERR_INVALID_ARG;
+  }
+  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
+  hipStream_t s = ctx->stream;
+  const uint32_t n_blocks = (uint32_t)((n_slots + 4095) / 4096);
+  const size_t cnt_bytes = sizeof(uint64_t) * pqg::ASM_MAX_DEPTHS * (size_t)std::max<uint32_t>(n_blocks, 1);
+  if (ctx->asm_scratch.ensure(cnt_bytes + 256) != hipSuccess || ctx->pin_err.ensure(256) != hipSuccess) return PQG_ERR_HIP;
+  uint64_t* counts = (uint64_t*)ctx->asm_scratch.p;
+  uint64_t* totals = (uint64_t*)((uint8_t*)ctx->asm_scratch.p + cnt_bytes);
+  hipError_t e = pqg::launch_assemble(s, d > 0 ? d_def_levels : nullptr, r > 0 ? d_rep_levels : nullptr, n_slots, P,
+                                      counts, n_blocks, totals, 0);
+  uint64_t* h_tot = (uint64_t*)ctx->pin_err.p;
+  if (e == hipSuccess) e = hipMemcpyAsync(h_tot, totals, sizeof(uint64_t) * pqg::ASM_MAX_DEPTHS, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    set_status(st, PQG_ERR_HIP, -1, -1, hipGetErrorString(e));
+    return PQG_ERR_HIP;
+  }
+  if (n_records) *n_records = h_tot[0];
+  int bad = -1;
+  for (int k = 0; k < depth; k++) {
+    path[k].n_entries = h_tot[P.depth[k]];
+    uint64_t need = 0;
+    if (P.kind[k] == PQG_OPTIONAL && P.validity[k]) need = h_tot[P.depth[k]];
+    if (P.kind[k] == PQG_REPEATED && P.offsets[k]) need = h_tot[P.depth[k] - 1] + 1;
+    if (need > path[k].capacity && bad < 0) bad = k;
+  }
+  if (bad >= 0) {
+    set_status(st, PQG_ERR_INVALID_ARG, -1, bad, "assembly output capacity");
+    return PQG_ERR_INVALID_ARG;
+  }
+  bool any_out = false;
+  for (int k = 0; k < depth; k++) any_out = any_out || P.validity[k] || P.offsets[k];
+  if (!any_out) return PQG_OK;  // counts only
+  e = pqg::launch_assemble(s, d > 0 ? d_def_levels : nullptr, r > 0 ? d_rep_levels : nullptr, n_slots, P, counts,
+                           n_blocks, totals, 1);
+  if (e == hipSuccess && n_blocks == 0)  // no slots: closing offsets only (offsets[0] = 0)
+    for (int k = 0; k < depth && e == hipSuccess; k++)
+      if (P.kind[k] == PQG_REPEATED && P.offsets[k]) e = hipMemsetAsync(P.offsets[k], 0, sizeof(int64_t), s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    set_status(st, PQG_ERR_HIP, -1, -1, hipGetErrorString(e));
+    return PQG_ERR_HIP;
+  }
+  return PQG_OK;
 }
 
 int pqg_unpack_runs(pqg_ctx* ctx, int bit_width, const uint8_t* d_in, const uint64_t* d_in_offsets,

@@ -175,7 +175,11 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
       code = bin_value_error(rs, pos, end, dict);
       break;
     }
-    // ---- follow the chain through the candidate list
+    // ---- follow the chain through the candidate list, 64 candidates at a time: every lane
+    // finds the lane holding its successor (vector binary search over the batch's sorted
+    // positions), then the chain is walked from lane 0 with one v_readlane per value; false
+    // candidates (a length read from a shifted prefix, e.g. the byte before a small length)
+    // are simply never reached.
     uint32_t i0 = 0;
     bool leave = false;  // next position lies past the window
     while (true) {
@@ -183,33 +187,45 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
       const uint32_t k = i0 + lane;
       const uint32_t p = k < total ? L.pos[k] : 0xFFFFFFFFu;
       const uint32_t s = k < total ? L.nxt[k] : 0xFFFFFFFFu;
-      const uint32_t pn = k + 1 < total ? L.pos[k + 1] : 0xFFFFFFFFu;
-      // lanes [0, f] are values: f = first lane whose successor is not the next candidate
-      const uint64_t bad = __ballot(k >= total || s != pn);
-      const uint32_t f = (uint32_t)__builtin_ctzll(bad | (1ull << 63));
-      const uint32_t take = uni(f + 1 < N - produced ? f + 1 : N - produced);
-      if (lane < take) {
-        gst(out_len + produced + lane, s - p - 4u);
-        gst(out_src + produced + lane, p + 4u);
+      uint32_t lo = 0;
+#pragma unroll
+      for (uint32_t step = 32; step >= 1; step >>= 1) {
+        const uint32_t c = lo + step;
+        if (c < WAVE && (uint32_t)__shfl((int)p, (int)c) <= s) lo = c;
+      }
+      const uint32_t J = ((uint32_t)__shfl((int)p, (int)lo) == s && lo > lane) ? lo : WAVE;
+      uint64_t mask = 0;
+      uint32_t j = 0, last = 0;
+      while (j < WAVE) {  // lane 0 holds the current position (a value start)
+        mask |= 1ull << j;
+        last = j;
+        j = rdl(J, j);
+      }
+      const uint32_t n_acc = (uint32_t)__builtin_popcountll(mask);
+      const uint32_t take = uni(n_acc < N - produced ? n_acc : N - produced);
+      const uint32_t rank = (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1ull));
+      if (((mask >> lane) & 1ull) && rank < take) {
+        gst(out_len + produced + rank, s - p - 4u);
+        gst(out_src + produced + rank, p + 4u);
       }
       produced += take;
       if (produced >= N) break;
-      const uint32_t cur = rdl(s, f);  // true successor of the last accepted value
+      const uint32_t cur = rdl(s, last);  // true successor of the last value of the batch
       pos = cur;
       if (cur >= B + BW_WIN) { leave = true; break; }
-      // find cur among the candidates after i0 + f (false candidates in between)
-      uint32_t lo = i0 + f + 1, hi = total;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (L.pos[mid] < cur) lo = mid + 1;
-        else hi = mid;
+      // find cur among the candidates after the batch's last value
+      uint32_t a = i0 + last + 1, b = total;
+      while (a < b) {
+        const uint32_t mid = (a + b) >> 1;
+        if (L.pos[mid] < cur) a = mid + 1;
+        else b = mid;
       }
-      lo = uni(lo);
-      if (lo >= total || L.pos[lo] != cur) {  // every position of the window was tested
+      a = uni(a);
+      if (a >= total || L.pos[a] != cur) {  // every position of the window was tested
         code = bin_value_error(rs, cur, end, dict);
         break;
       }
-      i0 = lo;
+      i0 = a;
     }
     if (code || !leave) break;
     wave_sync();  // the next window overwrites the list

@@ -110,6 +110,21 @@ hipError_t launch_bin_scan(hipStream_t st, const ColumnDev* cols, const int32_t*
 hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const uint64_t* chunks, uint32_t n_chunks, uint64_t* err,
                            uint32_t* err_count);
+// pqgpu_assembly.hip: levels -> offsets / validity of one leaf column's path
+constexpr uint32_t ASM_MAX_DEPTHS = 8;  // repetition depths 0..7 (max_rep <= 7)
+constexpr uint32_t ASM_MAX_NODES = 16;  // path length
+struct AsmParams {
+  uint32_t n_nodes;
+  uint32_t max_rep;
+  uint32_t DR[ASM_MAX_DEPTHS];          // definition level of the r-th REPEATED node (DR[0] = 0)
+  int32_t kind[ASM_MAX_NODES];          // pqg_repetition
+  uint32_t depth[ASM_MAX_NODES];        // repetition depth of the node's entries
+  uint32_t D[ASM_MAX_NODES];            // definition level of the node
+  uint8_t* validity[ASM_MAX_NODES];
+  int64_t* offsets[ASM_MAX_NODES];
+};
+hipError_t launch_assemble(hipStream_t st, const uint8_t* def, const uint8_t* rep, uint64_t n, const AsmParams& P,
+                           uint64_t* block_counts, uint32_t n_blocks, uint64_t* totals, int phase);
 hipError_t launch_unpack_runs(hipStream_t st, int w, const uint8_t* in, uint64_t in_bytes, const uint64_t* in_off,
                               const uint32_t* counts, const uint64_t* out_off, int32_t* out, int n_runs,
                               uint32_t max_count);

@@ -114,6 +114,22 @@ class Status(C.Structure):
         return (int(self.code), int(self.page), int(self.value_index))
 
 
+# FieldRepetitionType (pqg_repetition)
+REQUIRED, OPTIONAL, REPEATED = 0, 1, 2
+
+
+class AssemblyNode(C.Structure):
+    """pqg_assembly_node."""
+    _fields_ = [
+        ("repetition", C.c_int32),
+        ("reserved", C.c_int32),
+        ("validity", C.c_void_p),
+        ("offsets", C.c_void_p),
+        ("capacity", C.c_uint64),
+        ("n_entries", C.c_uint64),
+    ]
+
+
 def elem_width(physical_type, type_length=0):
     """Width in bytes of one dense output element (pqgpu.h, pqg_column_desc)."""
     return {BOOLEAN: 1, INT32: 4, FLOAT: 4, INT64: 8, DOUBLE: 8, INT96: 12,

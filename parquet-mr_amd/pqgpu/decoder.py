@@ -282,6 +282,56 @@ class Decoder:
             res.append(r)
         return rc, st, res, counts[:batch.n_pages], need
 
+    # -- record assembly -------------------------------------------------------------
+    def assemble(self, path, n_slots, def_levels=None, rep_levels=None):
+        """Dremel record assembly of one leaf column (pqg_assemble): `path` = repetitions of the
+        schema nodes from the root's child to the leaf; levels = the u8 device tensors decode()
+        wrote. Returns {"records": n, "nodes": [{"validity": tensor|None, "offsets": tensor|None,
+        "n_entries": n}, ...]} with device tensors (RecordReaderImplementation.read's records in
+        columnar form)."""
+        depth = len(path)
+        nodes = (abi.AssemblyNode * depth)()
+        for k, rp in enumerate(path):
+            nodes[k].repetition = rp
+        L = native.lib()
+        n_rec = C.c_uint64(0)
+        st = abi.Status()
+        dptr = def_levels.data_ptr() if def_levels is not None else None
+        rptr = rep_levels.data_ptr() if rep_levels is not None else None
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        # first call: entry counts (capacities 0 -> INVALID_ARG with every n_entries filled in)
+        rc = L.pqg_assemble(self.ctx, dptr, rptr, n_slots, C.addressof(nodes), depth, C.byref(n_rec), C.byref(st))
+        need_alloc = rc == abi.ERR_INVALID_ARG and st.page == -1 and st.message.startswith(b"assembly output capacity")
+        if rc != abi.OK and not need_alloc:
+            native.check(rc, st, "pqg_assemble")
+        out = []
+        counts = [int(nodes[k].n_entries) for k in range(depth)]
+        # entries of repetition depth r: records (r = 0), elements of the r-th REPEATED node
+        at_depth = [int(n_rec.value)]
+        for k, rp in enumerate(path):
+            if rp == abi.REPEATED:
+                at_depth.append(counts[k])
+        keep = []
+        r = 0
+        for k, rp in enumerate(path):
+            v = o = None
+            if rp == abi.OPTIONAL:
+                v = torch.empty(max(counts[k], 1), dtype=torch.uint8, device=self.device)
+                nodes[k].validity = v.data_ptr()
+                nodes[k].capacity = counts[k]
+            elif rp == abi.REPEATED:
+                o = torch.empty(at_depth[r] + 1, dtype=torch.int64, device=self.device)  # one list per enclosing entry
+                nodes[k].offsets = o.data_ptr()
+                nodes[k].capacity = at_depth[r] + 1
+                r += 1
+            keep.append((v, o))
+        rc = L.pqg_assemble(self.ctx, dptr, rptr, n_slots, C.addressof(nodes), depth, C.byref(n_rec), C.byref(st))
+        native.check(rc, st, "pqg_assemble")
+        for k in range(depth):
+            v, o = keep[k]
+            out.append({"validity": v[:counts[k]] if v is not None else None, "offsets": o, "n_entries": counts[k]})
+        return {"records": int(n_rec.value), "nodes": out}
+
     # -- ParquetReadRouter ---------------------------------------------------------
     def router_read(self, bit_width, data, count):
         """ParquetReadRouter.read(bitWidth, in, currentCount, int[]) on the GPU."""
