@@ -191,7 +191,8 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
 #pragma unroll
       for (uint32_t step = 32; step >= 1; step >>= 1) {
         const uint32_t c = lo + step;
-        if (c < WAVE && (uint32_t)__shfl((int)p, (int)c) <= s) lo = c;
+        const uint32_t pv = (uint32_t)__shfl((int)p, (int)(c & 63u));  // convergent: every lane
+        if (c < WAVE && pv <= s) lo = c;
       }
       const uint32_t J = ((uint32_t)__shfl((int)p, (int)lo) == s && lo > lane) ? lo : WAVE;
       uint64_t mask = 0;

@@ -256,7 +256,17 @@ __device__ __forceinline__ int walk_batch(PreWin& win, RleWalk& s, RunBatch& rb,
   rb.hi = 0;
   int code = 0;
   uint32_t packed = 0;
-  while (rb.nr < 64u && s.produced < s.N) {
+  while (true) {
+    // loop-carried scalars re-asserted wave-uniform (readfirstlane): otherwise the divergence
+    // analysis keeps them in VGPRs and the serial chain runs as masked vector code
+    rb.nr = uni(rb.nr);
+    s.produced = uni(s.produced);
+    s.pos = uni(s.pos);
+    s.N = uni(s.N);
+    s.pend_count = uni(s.pend_count);
+    win.B = uni(win.B);
+    packed = uni(packed);
+    if (rb.nr >= 64u || s.produced >= s.N) break;
     uint64_t count;
     uint32_t m, lo, hi = 0;
     if (s.pend_count) {
@@ -1148,6 +1158,261 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restri
 // newRLEIterator (V2, no prefix). Writes u8 levels, the page's non-null count
 // and the data section start; value kernels run afterwards.
 
+// Per-wave LDS of the level decoder: the page segment and pre-decode tables of the pointer-
+// jumping walk (as in the dictionary walk) plus the run table of one window.
+struct LevelWaveLds {
+  DictWaveLds w;
+  uint32_t r_start[256];  // first slot of run k of the window
+  uint32_t r_pay[256];    // RLE: value (saturated to 255); PACKED: 0x80000000 | data byte position
+  uint32_t r_end[256];    // PACKED: end of the bytes read for the run (truncated final group)
+};
+
+// Levels of the runs rs[0 .. n_run) covering slots [s_lo, s_hi) -> out (u8), 16 slots per lane
+// with 16-byte stores where the tile is inside [s_lo, s_hi); counts slots == max_def.
+__device__ __forceinline__ void expand_level_runs(const LevelWaveLds& L, rsrc_t rs, uint32_t n_run, uint32_t s_lo,
+                                                  uint32_t s_hi, int w, uint8_t* out, uint32_t max_def,
+                                                  bool count_nonnull, uint32_t& cnt) {
+  const uint32_t lane = lane_id();
+  const int64_t mis = out ? (int64_t)((uintptr_t)out & 15u) : 0;
+  const uint32_t wmask = w >= 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
+  for (int64_t t = (((int64_t)s_lo + mis) & ~(int64_t)15) - mis; t < (int64_t)s_hi; t += 16 * WAVE) {
+    const int64_t s0 = t + 16 * (int64_t)lane;
+    if (s0 + 16 <= (int64_t)s_lo || s0 >= (int64_t)s_hi) continue;
+    const uint32_t lo_s = (uint32_t)(s0 > (int64_t)s_lo ? s0 : (int64_t)s_lo);
+    const uint32_t hi_s = (uint32_t)(s0 + 16 < (int64_t)s_hi ? s0 + 16 : (int64_t)s_hi);
+    // run holding lo_s: last k with r_start[k] <= lo_s
+    uint32_t a = 0, b = n_run;
+    while (b - a > 1) {
+      const uint32_t mid = (a + b) >> 1;
+      if (L.r_start[mid] <= lo_s) a = mid;
+      else b = mid;
+    }
+    uint64_t wlo = 0, whi = 0;
+    uint32_t cur = lo_s, k = a;
+    while (cur < hi_s) {
+      const uint32_t st = L.r_start[k], pay = L.r_pay[k];
+      const uint32_t re = k + 1 < n_run ? L.r_start[k + 1] : s_hi;
+      const uint32_t stop = hi_s < re ? hi_s : re;
+      if (!(pay & 0x80000000u)) {
+        for (uint32_t q = cur; q < stop; q++) {
+          const uint32_t j = q - (uint32_t)s0;
+          if (j < 8) wlo |= (uint64_t)pay << (8 * j);
+          else whi |= (uint64_t)pay << (8 * (j - 8));
+        }
+      } else if (w > 0) {
+        const uint32_t rlo = pay & 0x7FFFFFFFu, rhi = L.r_end[k];
+        const uint64_t bit0 = (uint64_t)(cur - st) * (uint32_t)w;
+        const uint32_t a0 = rlo + (uint32_t)(bit0 >> 3);
+        uint64_t x[3];
+#pragma unroll
+        for (uint32_t c = 0; c < 3; c++) {
+          const uint32_t ac = a0 + 8u * c;
+          const uint64_t v = ld8_any(rs, ac);
+          const int64_t keep = (int64_t)rhi - (int64_t)ac;  // bytes past the run's read end are 0 (:96-99)
+          x[c] = keep >= 8 ? v : (keep <= 0 ? 0 : (v & ((1ull << (8 * keep)) - 1ull)));
+        }
+        for (uint32_t q = cur; q < stop; q++) {
+          const uint32_t sh = (uint32_t)(bit0 & 7u) + (q - cur) * (uint32_t)w;
+          const uint32_t c = sh >> 6, o = sh & 63u;
+          const uint64_t lo64 = c == 0 ? x[0] : (c == 1 ? x[1] : x[2]);
+          const uint64_t hi64 = c == 0 ? x[1] : (c == 1 ? x[2] : 0ull);
+          const uint64_t f = o ? ((lo64 >> o) | (hi64 << (64u - o))) : lo64;
+          uint32_t v = (uint32_t)f & wmask;
+          v = v > 255u ? 255u : v;
+          const uint32_t j = q - (uint32_t)s0;
+          if (j < 8) wlo |= (uint64_t)v << (8 * j);
+          else whi |= (uint64_t)v << (8 * (j - 8));
+        }
+      }
+      cur = stop;
+      k++;
+    }
+    const uint32_t j0 = lo_s - (uint32_t)s0, j1 = hi_s - (uint32_t)s0;
+    if (count_nonnull)
+      for (uint32_t j = j0; j < j1; j++)
+        cnt += (uint32_t)((j < 8 ? wlo >> (8 * j) : whi >> (8 * (j - 8))) & 0xFFu) == max_def ? 1u : 0u;
+    if (out) {
+      uint8_t* o = out + s0;
+      if (j0 == 0 && j1 == 16) {
+        typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+        gst((v2*)o, v2{wlo, whi});
+      } else {
+        for (uint32_t j = j0; j < j1; j++) gst(o + j, (uint8_t)((j < 8 ? wlo >> (8 * j) : whi >> (8 * (j - 8))) & 0xFFu));
+      }
+    }
+  }
+}
+
+// RLE / bit-packed level section [beg, end) (RunLengthBitPackingHybridDecoder over the section)
+// -> out[0 .. N): the pointer-jumping walk of the dictionary path (one 256-byte window at a time:
+// every byte position pre-decoded as a run header, 8 rounds of pointer doubling mark the chain),
+// the window's runs in an LDS table, then tile expansion of the slots they cover.
+// Returns the slots decoded before an error (N when none) and sets *err_code.
+__device__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs, uint32_t beg, uint32_t end, int w, uint32_t N,
+                                     uint8_t* out, uint32_t max_def, bool count_nonnull, uint32_t* nonnull,
+                                     int* err_code) {
+  const uint32_t lane = lane_id();
+  typedef uint16_t __attribute__((may_alias)) u16a;
+  typedef uint32_t __attribute__((may_alias)) u32a;
+  typedef uint64_t __attribute__((may_alias)) u64a;
+  u16a* Jt = (u16a*)L.w.ent;
+  uint8_t* Rt = (uint8_t*)L.w.ent + 512;
+  PreWin win;
+  win.rs = rs;
+  win.seg = L.w.seg;
+  win.seg_lo = 0xFFFFF000u;  // nothing staged yet
+  uint32_t pos = beg, produced = 0, cnt = 0;
+  int code = 0;
+  while (true) {
+    pos = uni(pos);
+    produced = uni(produced);
+    if (produced >= N) break;
+    if (pos >= end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
+    const uint32_t B = pos & ~3u;
+    predecode<false>(win, B, w);  // stages [B, B + 264) in the segment when needed
+    uint32_t jv[4], nn[4], slowm = 0, inm = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const uint32_t p = B + 4u * lane + b;
+      const uint32_t f = (win.flg >> (8u * b)) & 0xFFu;
+      const uint32_t hl = f >> 2;
+      const uint32_t nx = win.nxt[b];
+      const bool in = p < end;
+      const bool slow = in && ((f & 2u) || p + hl > end || (!(f & 1u) && nx > end));
+      nn[b] = (f & 1u) ? (nx < end ? nx : end) : nx;  // packed: readFully of what is left
+      jv[b] = (!in || slow || nn[b] - B >= 256u) ? 256u : nn[b] - B;
+      slowm |= (slow ? 1u : 0u) << b;
+      inm |= (in ? 1u : 0u) << b;
+    }
+    const uint32_t s0 = pos - B;
+    *(u64a*)(Jt + 4u * lane) =
+        (uint64_t)jv[0] | ((uint64_t)jv[1] << 16) | ((uint64_t)jv[2] << 32) | ((uint64_t)jv[3] << 48);
+    *(u32a*)(Rt + 4u * lane) = (4u * lane <= s0 && s0 < 4u * lane + 4u) ? (1u << (8u * (s0 & 3u))) : 0u;
+#pragma unroll 1
+    for (int r = 0; r < 8; r++) {
+      const uint32_t r4 = *(const u32a*)(Rt + 4u * lane);
+      uint32_t jn[4];
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++) {
+        if (((r4 >> (8u * b)) & 1u) && jv[b] < 256u) Rt[jv[b]] = 1;
+        jn[b] = jv[b] < 256u ? Jt[jv[b]] : 256u;
+      }
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++) jv[b] = jn[b];
+      *(u64a*)(Jt + 4u * lane) =
+          (uint64_t)jv[0] | ((uint64_t)jv[1] << 16) | ((uint64_t)jv[2] << 32) | ((uint64_t)jv[3] << 48);
+      const uint32_t r4n = *(const u32a*)(Rt + 4u * lane);
+      bool more = false;
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++) more |= ((r4n >> (8u * b)) & 1u) && jv[b] < 256u;
+      if (!__ballot(more)) break;
+    }
+    const uint32_t r4 = *(const u32a*)(Rt + 4u * lane);
+    uint32_t mk = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) mk |= ((r4 >> (8u * b)) & 1u) << b;
+    uint32_t q_last = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const uint64_t m = __ballot((mk >> b) & 1u);
+      if (m) {
+        const uint32_t q = 4u * (63u - (uint32_t)__builtin_clzll(m)) + b;
+        q_last = q > q_last ? q : q_last;
+      }
+    }
+    q_last = uni(q_last);
+    // runs of the window: marked, inside the section, fast-path headers; counts capped at N
+    const uint32_t cap = N - produced;
+    uint32_t cc[4], lsum = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const bool v = ((mk & inm & ~slowm) >> b) & 1u;
+      const bool pk = (win.flg >> (8u * b)) & 1u;
+      uint32_t c = win.cnt[b];
+      if (!pk && c == 0) c = cap;  // Java: currentCount goes negative, the value repeats forever
+      c = v ? (c < cap ? c : cap) : 0u;
+      cc[b] = c;
+      lsum = lsum + c < cap ? lsum + c : cap;
+    }
+    uint32_t inc = lsum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if ((int)lane >= o) inc = inc + y < cap ? inc + y : cap;
+    }
+    uint32_t st = __shfl_up(inc, 1);
+    if (lane == 0) st = 0;
+    const uint32_t total = uni(rdl(inc, WAVE - 1));
+    uint32_t em = 0, stb[4];
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      stb[b] = st;
+      if (cc[b] && st < cap) em |= 1u << b;
+      st = st + cc[b] < cap ? st + cc[b] : cap;
+    }
+    uint32_t base = 0, n_em = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const uint64_t m = __ballot((em >> b) & 1u);
+      base += (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+      n_em += (uint32_t)__builtin_popcountll(m);
+    }
+    n_em = uni(n_em);
+    wave_sync();  // the previous window's expansion read the run table
+    uint32_t idx = base;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      if ((em >> b) & 1u) {
+        const bool pk = (win.flg >> (8u * b)) & 1u;
+        const uint32_t vv = win.val[b];
+        L.r_start[idx] = produced + stb[b];
+        L.r_pay[idx] = pk ? (0x80000000u | vv) : (vv > 255u ? 255u : vv);
+        L.r_end[idx] = nn[b];
+        idx++;
+      }
+    }
+    wave_sync();
+    if (n_em) expand_level_runs(L, rs, n_em, produced, produced + total, w, out, max_def, count_nonnull, cnt);
+    produced += total;
+    if (produced >= N) break;
+    const uint32_t ql = q_last >> 2, qb = q_last & 3u;
+    const uint32_t q_slow = (rdl(slowm, ql) >> qb) & 1u;
+    const uint32_t q_in = (rdl(inm, ql) >> qb) & 1u;
+    if (!q_in) {
+      pos = B + q_last;  // at or past the section end: RLE_PAST_END next
+    } else if (!q_slow) {
+      pos = pick4(nn, qb, ql);  // leaves the window
+    } else {
+      // scalar re-decode of the header at q_last (readNext :80-109)
+      pos = B + q_last;
+      uint32_t hl, m, nxs, vv;
+      uint64_t cnt64;
+      code = slow_header_g([&](uint32_t p) { return wbyte(win, p); }, pos, end, w, hl, m, cnt64, vv, nxs);
+      if (code) break;
+      if (m == 0 && nxs > end) { code = PQG_ERR_EOF; break; }
+      uint64_t c64 = cnt64;
+      const uint32_t left = N - produced;
+      if (m == 0 && c64 == 0) c64 = left;
+      const uint32_t take = c64 < left ? (uint32_t)c64 : left;
+      const uint32_t rd_end = m ? (nxs < end ? nxs : end) : nxs;
+      wave_sync();
+      if (lane == 0) {
+        L.r_start[0] = produced;
+        L.r_pay[0] = m ? (0x80000000u | vv) : (vv > 255u ? 255u : vv);
+        L.r_end[0] = rd_end;
+      }
+      wave_sync();
+      expand_level_runs(L, rs, 1, produced, produced + take, w, out, max_def, count_nonnull, cnt);
+      produced += take;
+      pos = rd_end;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if (nonnull) *nonnull = cnt;
+  *err_code = code;
+  return code ? produced : N;
+}
+
 // Decode one level section into out[slot_base + i], i < N. Returns the number of
 // slots decoded before an error (N when none) and sets *err_code.
 __device__ uint32_t decode_levels(rsrc_t rs, uint32_t beg, uint32_t end, int w, uint32_t N, uint8_t* out,
@@ -1173,19 +1438,89 @@ __device__ uint32_t decode_levels(rsrc_t rs, uint32_t beg, uint32_t end, int w, 
     int code = walk_batch(win, s, rb);
     if (code && !first_err) { first_err = code; done = rb.end; }
     if (lane < rb.nr && rb.meta == 0) rb.lo = rb.lo > 255u ? 255u : rb.lo;  // saturate (pqgpu.h)
-    uint32_t nxt = __shfl_down(rb.start, 1);
-    const uint32_t run_end = (lane + 1 < rb.nr) ? nxt : rb.end;
-    for (uint32_t c0 = rb.first; c0 < rb.end; c0 += WAVE) {
-      uint32_t i = c0 + lane;
-      uint32_t ch = c0 + WAVE < rb.end ? c0 + WAVE : rb.end;
-      uint64_t mask = overlap_mask(rb, run_end, c0, ch);
-      Sel sel = {0, 0, 0, 0};
-      select_runs(rb, mask, &i, &sel, 1);
-      uint32_t v = sel.meta == 0 ? sel.lo : packed_elem(win.rs, sel.lo, sel.hi, sel.s, i, w);
-      v = v > 255u ? 255u : v;
-      if (i < rb.end) {
-        if (out) gst(out + i, (uint8_t)v);
-        if (count_nonnull && v == max_def) cnt++;
+    const uint32_t nxt_start = (uint32_t)__shfl_down((int)rb.start, 1);  // convergent: every lane
+    const uint32_t run_end = (lane + 1 < rb.nr) ? nxt_start : rb.end;
+    const uint32_t nr = uni(rb.nr), first = uni(rb.first), endv = uni(rb.end);
+#ifdef PQG_ABLATE_LVL_EXPAND
+    if (endv != 0xFFFFFFFFu) continue;  // diagnostic ablation: walk only
+#endif
+    // tiles of 64 lanes x 16 slots; tile boundaries where out + slot is 16-byte aligned
+    const int64_t mis = out ? (int64_t)((uintptr_t)out & 15u) : 0;
+    for (int64_t t = (((int64_t)first + mis) & ~(int64_t)15) - mis; t < (int64_t)endv; t += 16 * WAVE) {
+      const int64_t s0 = t + 16 * (int64_t)lane;
+      const uint32_t lo_s = (uint32_t)(s0 > (int64_t)first ? s0 : (int64_t)first);
+      const uint32_t hi_s = (uint32_t)(s0 + 16 < (int64_t)endv ? s0 + 16 : (int64_t)endv);
+      const bool act = s0 + 16 > (int64_t)first && s0 < (int64_t)endv;
+      // run holding the lane's first slot: largest r < nr with start[r] <= lo_s
+      uint32_t r = 0;
+#pragma unroll
+      for (uint32_t step = 32; step >= 1; step >>= 1) {
+        const uint32_t c = r + step;
+        const uint32_t v = (uint32_t)__shfl((int)rb.start, (int)(c & 63u));
+        if (c < nr && v <= lo_s) r = c;
+      }
+      uint64_t wlo = 0, whi = 0;  // the lane's 16 level bytes
+      uint32_t cur = act ? lo_s : hi_s;
+      while (__ballot(cur < hi_s)) {  // one run of each lane per pass (usually one pass)
+        const uint32_t st = (uint32_t)__shfl((int)rb.start, (int)r), m = (uint32_t)__shfl((int)rb.meta, (int)r);
+        const uint32_t rlo = (uint32_t)__shfl((int)rb.lo, (int)r), rhi = (uint32_t)__shfl((int)rb.hi, (int)r);
+        const uint32_t re = (uint32_t)__shfl((int)run_end, (int)r);
+        if (cur < hi_s) {
+          const uint32_t stop = hi_s < re ? hi_s : re;
+          if (m == 0) {
+            for (uint32_t q = cur; q < stop; q++) {
+              const uint32_t j = q - (uint32_t)s0;
+              if (j < 8) wlo |= (uint64_t)rlo << (8 * j);
+              else whi |= (uint64_t)rlo << (8 * (j - 8));
+            }
+          } else if (w > 0) {
+            // bits [(cur - st) * w, (stop - st) * w) of the run's bytes [rlo, rhi); past rhi: 0
+            const uint64_t bit0 = (uint64_t)(cur - st) * (uint32_t)w;
+            const uint32_t a0 = rlo + (uint32_t)(bit0 >> 3);
+            uint64_t x[3];
+#pragma unroll
+            for (uint32_t c = 0; c < 3; c++) {
+              const uint32_t ac = a0 + 8u * c;
+              uint64_t v = ld8_any(win.rs, ac);
+              const int64_t keep = (int64_t)rhi - (int64_t)ac;
+              x[c] = keep >= 8 ? v : (keep <= 0 ? 0 : (v & ((1ull << (8 * keep)) - 1ull)));
+            }
+            const uint32_t wmask = w >= 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
+            for (uint32_t q = cur; q < stop; q++) {
+              const uint32_t sh = (uint32_t)(bit0 & 7u) + (q - cur) * (uint32_t)w;  // < 8 + 15 * 32
+              const uint32_t c = sh >> 6, o = sh & 63u;
+              const uint64_t lo64 = c == 0 ? x[0] : (c == 1 ? x[1] : x[2]);
+              const uint64_t hi64 = c == 0 ? x[1] : (c == 1 ? x[2] : 0ull);
+              const uint64_t f = o ? ((lo64 >> o) | (hi64 << (64u - o))) : lo64;
+              uint32_t v = (uint32_t)f & wmask;
+              v = v > 255u ? 255u : v;
+              const uint32_t j = q - (uint32_t)s0;
+              if (j < 8) wlo |= (uint64_t)v << (8 * j);
+              else whi |= (uint64_t)v << (8 * (j - 8));
+            }
+          }
+          cur = stop;
+          r++;
+        }
+      }
+      if (act) {
+        const uint32_t j0 = lo_s - (uint32_t)s0, j1 = hi_s - (uint32_t)s0;
+        if (count_nonnull) {
+          for (uint32_t j = j0; j < j1; j++) {
+            const uint32_t v = (uint32_t)((j < 8 ? wlo >> (8 * j) : whi >> (8 * (j - 8))) & 0xFFu);
+            cnt += v == max_def ? 1u : 0u;
+          }
+        }
+        if (out) {
+          uint8_t* o = out + s0;
+          if (j0 == 0 && j1 == 16) {
+            typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+            gst((v2*)o, v2{wlo, whi});
+          } else {
+            for (uint32_t j = j0; j < j1; j++)
+              gst(o + j, (uint8_t)((j < 8 ? wlo >> (8 * j) : whi >> (8 * (j - 8))) & 0xFFu));
+          }
+        }
       }
     }
   }
@@ -1200,8 +1535,10 @@ __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__
                                                 PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                 const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                                 uint32_t* err_count) {
+  __shared__ __attribute__((aligned(16))) LevelWaveLds lvl_lds[WPB];
   const int page = wave_page(list, n_list);
   if (page < 0) return;
+  LevelWaveLds& LL = lvl_lds[wave_id()];
   PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
   const uint32_t lane = lane_id();
@@ -1261,7 +1598,7 @@ __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__
   uint8_t* def_out = cd.def_levels ? cd.def_levels + pw.slot_offset : nullptr;
   uint64_t lvl_err_key = ~0ull;
   if (wr > 0) {
-    uint32_t done = decode_levels(win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code);
+    uint32_t done = decode_levels_pj(LL, win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code);
     if (code) {
       limit = done;
       lvl_err_key = ((uint64_t)done << 1) << 8 | (uint64_t)code;
@@ -1272,7 +1609,8 @@ __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__
   uint32_t nonnull = 0;
   if (wd > 0) {
     int code2 = 0;
-    uint32_t done = decode_levels(win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true, &nonnull, &code2);
+    uint32_t done = decode_levels_pj(LL, win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true, &nonnull,
+                                     &code2);
     if (code2) {
       uint64_t key = (((uint64_t)done << 1) | 1ull) << 8 | (uint64_t)code2;
       if (key < lvl_err_key) lvl_err_key = key;
