@@ -453,11 +453,14 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
   const uint64_t o_hi = o_hi0 < cd.binary_capacity ? o_hi0 : cd.binary_capacity;  // overflow: reported at sync
   if (o_lo >= o_hi) return;
   uint8_t* dst = cd.binary_data;
-  const uint64_t a0 = o_lo & ~3ull;
+  // every lane fills 16-byte blocks of the output: the value holding the block's first byte by
+  // binary search, then per dword the value pieces it contains (one unaligned 4-byte source
+  // read per piece, usually one piece per dword)
+  const uint64_t a0 = o_lo & ~15ull;
+  const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
   uint32_t kv = 0;  // value of this lane's current byte (monotone across iterations)
-  for (uint64_t a = a0 + 4u * lane; a < o_hi; a += 4u * WAVE) {
+  for (uint64_t a = a0 + 16u * lane; a < o_hi; a += 16u * WAVE) {
     const uint64_t b0 = a > o_lo ? a : o_lo;
-    // value holding byte b0: last k with off[k] <= b0
     uint32_t lo = kv, hi = n;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
@@ -465,27 +468,41 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
       else hi = mid;
     }
     kv = lo;
-    const uint64_t e = a + 4u;
-    if (a >= o_lo && e <= o_hi && e <= off[kv + 1]) {
-      const uint64_t sp = (uint64_t)src[kv] + (a - off[kv]);
-      const uint32_t x = sp + 4u <= slim ? ld4_any(rs, (uint32_t)sp) : 0u;
-      gst((uint32_t*)(dst + a), x);
-    } else {
-      uint32_t k = kv, x = 0, have = 0;
-      for (uint32_t q = 0; q < 4; q++) {
-        const uint64_t bb = a + q;
-        if (bb < o_lo || bb >= o_hi) continue;
-        while (k + 1 < n && bb >= off[k + 1]) k++;
-        const uint64_t sp = (uint64_t)src[k] + (bb - off[k]);
-        const uint32_t v = sp < slim ? (ld32(rs, (uint32_t)sp & ~3u) >> (((uint32_t)sp & 3u) * 8u)) & 0xFFu : 0u;
-        x |= v << (8u * q);
-        have |= 1u << q;
+    uint32_t wd[4];
+    uint32_t have = 0;  // bit q: dword q fully inside [o_lo, o_hi)
+    uint32_t k = kv;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      const uint64_t d0 = a + 4u * q;
+      const uint64_t x0 = d0 > o_lo ? d0 : o_lo, x1 = d0 + 4u < o_hi ? d0 + 4u : o_hi;
+      uint32_t word = 0;
+      for (uint64_t cur = x0; cur < x1;) {
+        while (k + 1 < n && cur >= off[k + 1]) k++;
+        const uint64_t vend = off[k + 1];
+        const uint64_t seg_end = x1 < vend ? x1 : vend;
+        const uint32_t nbytes = (uint32_t)(seg_end - cur);
+        const uint64_t sp = (uint64_t)src[k] + (cur - off[k]);
+        const uint32_t v = sp < slim ? ld4_any(rs, (uint32_t)sp) : 0u;
+        const uint32_t m = nbytes >= 4 ? 0xFFFFFFFFu : ((1u << (8u * nbytes)) - 1u);
+        word |= (v & m) << (8u * (uint32_t)(cur - d0));
+        cur = seg_end;
       }
-      if (have == 0xFu) {
-        gst((uint32_t*)(dst + a), x);
-      } else {
-        for (uint32_t q = 0; q < 4; q++)
-          if ((have >> q) & 1u) gst(dst + a + q, (uint8_t)(x >> (8u * q)));
+      wd[q] = word;
+      if (x0 == d0 && x1 == d0 + 4u) have |= 1u << q;
+    }
+    if (!dst_al4) have = 0;  // unaligned byte buffer (C ABI caller): byte stores only
+    if (have == 0xFu && dst_al16) {
+      gst_nt((u32x4*)(dst + a), u32x4{wd[0], wd[1], wd[2], wd[3]});
+    } else {
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint64_t d0 = a + 4u * q;
+        if ((have >> q) & 1u) {
+          gst((uint32_t*)(dst + d0), wd[q]);
+        } else {
+          for (uint32_t j = 0; j < 4; j++)
+            if (d0 + j >= o_lo && d0 + j < o_hi) gst(dst + d0 + j, (uint8_t)(wd[q] >> (8u * j)));
+        }
       }
     }
   }
