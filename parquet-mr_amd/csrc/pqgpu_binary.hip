@@ -119,8 +119,9 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
 constexpr uint32_t BW_WIN = 1024;  // window bytes (16 positions per lane)
 
 struct BinWalkLds {
-  uint32_t pos[BW_WIN];
-  uint32_t nxt[BW_WIN];
+  uint32_t pos[BW_WIN];   // candidate positions, ascending
+  uint32_t nxt[BW_WIN];   // their successors (p + 4 + len)
+  uint16_t idx[BW_WIN];   // window offset -> candidate index (valid where pos[idx] matches)
 };
 
 // Error of a value whose length prefix starts at p (not a candidate).
@@ -166,6 +167,7 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
         if ((m >> q) & 1u) {
           L.pos[r] = base + q;
           L.nxt[r] = nx[q];
+          L.idx[16u * lane + q] = (uint16_t)r;
           r++;
         }
     }
@@ -176,10 +178,10 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
       break;
     }
     // ---- follow the chain through the candidate list, 64 candidates at a time: every lane
-    // finds the lane holding its successor (vector binary search over the batch's sorted
-    // positions), then the chain is walked from lane 0 with one v_readlane per value; false
-    // candidates (a length read from a shifted prefix, e.g. the byte before a small length)
-    // are simply never reached.
+    // looks up the candidate index of its successor (window offset -> index table), then the
+    // chain is walked from lane 0 (the current value start) with one v_readlane per value;
+    // false candidates (a length read from a shifted prefix, e.g. the byte before a small
+    // length) are simply never reached.
     uint32_t i0 = 0;
     bool leave = false;  // next position lies past the window
     while (true) {
@@ -187,14 +189,10 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
       const uint32_t k = i0 + lane;
       const uint32_t p = k < total ? L.pos[k] : 0xFFFFFFFFu;
       const uint32_t s = k < total ? L.nxt[k] : 0xFFFFFFFFu;
-      uint32_t lo = 0;
-#pragma unroll
-      for (uint32_t step = 32; step >= 1; step >>= 1) {
-        const uint32_t c = lo + step;
-        const uint32_t pv = (uint32_t)__shfl((int)p, (int)(c & 63u));  // convergent: every lane
-        if (c < WAVE && pv <= s) lo = c;
-      }
-      const uint32_t J = ((uint32_t)__shfl((int)p, (int)lo) == s && lo > lane) ? lo : WAVE;
+      const uint32_t so = s - B;
+      const uint32_t t = so < BW_WIN ? L.idx[so] : 0xFFFFu;
+      const bool hit = t < total && t > k && t - i0 < WAVE && L.pos[t < total ? t : 0] == s;
+      const uint32_t J = hit ? t - i0 : WAVE;
       uint64_t mask = 0;
       uint32_t j = 0, last = 0;
       while (j < WAVE) {  // lane 0 holds the current position (a value start)
@@ -214,15 +212,8 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
       const uint32_t cur = rdl(s, last);  // true successor of the last value of the batch
       pos = cur;
       if (cur >= B + BW_WIN) { leave = true; break; }
-      // find cur among the candidates after the batch's last value
-      uint32_t a = i0 + last + 1, b = total;
-      while (a < b) {
-        const uint32_t mid = (a + b) >> 1;
-        if (L.pos[mid] < cur) a = mid + 1;
-        else b = mid;
-      }
-      a = uni(a);
-      if (a >= total || L.pos[a] != cur) {  // every position of the window was tested
+      const uint32_t a = uni((uint32_t)L.idx[cur - B]);
+      if (a >= total || L.pos[a] != cur || a <= i0 + last) {  // every position of the window was tested
         code = bin_value_error(rs, cur, end, dict);
         break;
       }
