@@ -709,16 +709,50 @@ static int vreader_read(vreader* r, colstate* cs) {
 typedef struct {
   int zero;
   rle_dec rle;
+  /* BIT_PACKED (BIG_ENDIAN) levels: ByteBitPackingValuesReader(maxLevel, BIG_ENDIAN) */
+  int be;
+  int be_width;
+  jstream be_in;
+  int64_t be_read;
 } lreader;
 
-static int lreader_init_v1(lreader* L, int enc, int max_level, jstream* s) {
+/* BE (MSB-first) unpack: Packer.BIG_ENDIAN, ByteBasedBitPackingGenerator getShift msbFirst branch
+ * (:153-159): value i = bits [i*w, (i+1)*w) of the stream, bit 0 = MSB of byte 0. */
+static uint32_t be_value(const uint8_t* buf, int64_t avail, int64_t idx, int w) {
+  uint32_t v = 0;
+  for (int k = 0; k < w; k++) {
+    int64_t bit = idx * w + k;
+    int64_t byte = bit >> 3;
+    uint32_t b = byte < avail ? buf[byte] : 0;   /* readMore :49-57: zero fill past the section */
+    v = (v << 1) | ((b >> (7 - (bit & 7))) & 1u);
+  }
+  return v;
+}
+
+void pqr_unpack8_int_be(int w, const uint8_t* in, int32_t* out) {
+  for (int i = 0; i < 8; i++) out[i] = (int32_t)be_value(in, w, i, w);
+}
+
+static int lreader_init_v1(lreader* L, int enc, int max_level, jstream* s, int32_t value_count) {
   memset(L, 0, sizeof(*L));
   int w = pqr_width_from_max_int(max_level);
   if (w == 0) {
     if (enc == PQG_RLE || enc == PQG_BIT_PACKED) { L->zero = 1; return PQG_OK; }
     return PQG_ERR_UNSUPPORTED;
   }
-  if (enc != PQG_RLE) return PQG_ERR_UNSUPPORTED;  /* BIT_PACKED (BE) levels with maxLevel > 0: next row */
+  if (enc == PQG_BIT_PACKED) {
+    /* ByteBitPackingValuesReader.initFromPage :77-88: min(ceil(valueCount * w / 8), available)
+     * bytes, valueCount = the page's num_values */
+    int64_t length = ((int64_t)value_count * w + 7) / 8;
+    if (length > js_available(s)) length = js_available(s);
+    jstream sl;
+    js_slice(s, length, &sl);
+    L->be = 1;
+    L->be_width = w;
+    L->be_in = sl;
+    return PQG_OK;
+  }
+  if (enc != PQG_RLE) return PQG_ERR_UNSUPPORTED;
   int32_t length;
   int e = read_int_le(s, &length);
   if (e) return e;
@@ -736,6 +770,10 @@ static int lreader_init_v2(lreader* L, int max_level, jstream sec) {
 
 static inline int lreader_next(lreader* L, int32_t* v) {
   if (L->zero) { *v = 0; return PQG_OK; }
+  if (L->be) {
+    *v = (int32_t)be_value(L->be_in.buf + L->be_in.pos, js_available(&L->be_in), L->be_read++, L->be_width);
+    return PQG_OK;
+  }
   return rle_read_int(&L->rle, v);
 }
 
@@ -798,8 +836,8 @@ int pqr_decode(const uint8_t* bytes, uint64_t n_bytes, pqg_column_desc* cols, in
         rc = e; set_status(st, rc, p, 0, "data init"); vreader_free(&vr); break;
       }
     } else {
-      if ((e = lreader_init_v1(&rl, pg->rl_encoding, c->max_rep, &page)) ||
-          (e = lreader_init_v1(&dl, pg->dl_encoding, c->max_def, &page))) {
+      if ((e = lreader_init_v1(&rl, pg->rl_encoding, c->max_rep, &page, nv)) ||
+          (e = lreader_init_v1(&dl, pg->dl_encoding, c->max_def, &page, nv))) {
         rc = e; set_status(st, rc, p, 0, "level init"); break;
       }
       if ((e = vreader_init(&vr, pg, C, &page, nv))) {

@@ -10,6 +10,7 @@ extern "C" {
 int pqr_width_from_max_int(int32_t bound);
 void pqr_unpack8_int(int w, const uint8_t* in, int32_t* out);
 void pqr_unpack8_long(int w, const uint8_t* in, int64_t* out);
+void pqr_unpack8_int_be(int w, const uint8_t* in, int32_t* out);
 int pqr_rle_decode(int bit_width, const uint8_t* buf, int64_t len, int64_t n, int32_t* out,
                    int64_t* err_index, int64_t* consumed);
 int64_t pqr_router_read_batch(int bit_width, const uint8_t* in, int64_t in_len, int count, int32_t* out);

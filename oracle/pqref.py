@@ -34,6 +34,7 @@ def lib():
         L.pqr_width_from_max_int.argtypes = [C.c_int32]
         L.pqr_unpack8_int.argtypes = [C.c_int, vp, vp]
         L.pqr_unpack8_long.argtypes = [C.c_int, vp, vp]
+        L.pqr_unpack8_int_be.argtypes = [C.c_int, vp, vp]
         L.pqr_rle_decode.argtypes = [C.c_int, vp, i64, i64, vp, C.POINTER(i64), C.POINTER(i64)]
         L.pqr_rle_decode.restype = C.c_int
         L.pqr_router_read_batch.argtypes = [C.c_int, vp, i64, C.c_int, vp]
@@ -55,6 +56,13 @@ def unpack8_int(w, data):
     a = _buf(data)
     out = np.zeros(8, dtype=np.int32)
     lib().pqr_unpack8_int(w, a.ctypes.data, out.ctypes.data)
+    return out
+
+
+def unpack8_int_be(w, data):
+    a = np.concatenate([_buf(data), np.zeros(8, np.uint8)])
+    out = np.zeros(8, dtype=np.int32)
+    lib().pqr_unpack8_int_be(w, a.ctypes.data, out.ctypes.data)
     return out
 
 

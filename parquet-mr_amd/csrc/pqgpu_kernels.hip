@@ -1158,6 +1158,40 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restri
 // newRLEIterator (V2, no prefix). Writes u8 levels, the page's non-null count
 // and the data section start; value kernels run afterwards.
 
+// BIT_PACKED (big-endian) level section [beg, end): level i = bits [i*w, (i+1)*w) MSB first
+// (Packer.BIG_ENDIAN, ByteBasedBitPackingGenerator getShift msbFirst :153-159); bytes past the
+// section read as 0 (ByteBitPackingValuesReader.readMore :49-57). 16 slots per lane, no errors.
+__device__ uint32_t decode_levels_be(rsrc_t rs, uint32_t beg, uint32_t end, int w, uint32_t N, uint8_t* out,
+                                     uint32_t max_def, bool count_nonnull, uint32_t* nonnull, int* err_code) {
+  const uint32_t lane = lane_id();
+  uint32_t cnt = 0;
+  const uint32_t mask = (1u << w) - 1u;  // w <= 8 (max level <= 254)
+  for (uint32_t s0 = 16u * lane; s0 < N; s0 += 16u * WAVE) {
+    uint64_t wlo = 0, whi = 0;
+    for (uint32_t j = 0; j < 16 && s0 + j < N; j++) {
+      const uint64_t bit = (uint64_t)(s0 + j) * (uint32_t)w;
+      const uint32_t a = beg + (uint32_t)(bit >> 3);
+      uint32_t x = 0;  // bytes a .. a+3, big endian, 0 past the section
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t bq = a + q < end ? (ld32(rs, (a + q) & ~3u) >> (((a + q) & 3u) * 8u)) & 0xFFu : 0u;
+        x = (x << 8) | bq;
+      }
+      const uint32_t v = (x >> (32u - (uint32_t)(bit & 7u) - (uint32_t)w)) & mask;
+      if (count_nonnull && v == max_def) cnt++;
+      if (j < 8) wlo |= (uint64_t)v << (8 * j);
+      else whi |= (uint64_t)v << (8 * (j - 8));
+    }
+    if (out)
+      for (uint32_t j = 0; j < 16 && s0 + j < N; j++)
+        gst(out + s0 + j, (uint8_t)((j < 8 ? wlo >> (8 * j) : whi >> (8 * (j - 8))) & 0xFFu));
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if (nonnull) *nonnull = cnt;
+  *err_code = 0;
+  return N;
+}
+
 // Per-wave LDS of the level decoder: the page segment and pre-decode tables of the pointer-
 // jumping walk (as in the dictionary walk) plus the run table of one window.
 struct LevelWaveLds {
@@ -1549,6 +1583,7 @@ __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__
   const int wr = cd.max_rep ? 32 - __builtin_clz((uint32_t)cd.max_rep) : 0;
   const int wd = cd.max_def ? 32 - __builtin_clz((uint32_t)cd.max_def) : 0;
   uint32_t rl_beg = 0, rl_end = 0, dl_beg = 0, dl_end = 0, data_beg = 0;
+  bool rl_be = false, dl_be = false;  // V1 BIT_PACKED (big-endian) level sections
   int init_err = 0, init_phase = 0;
   if (pw.version == 2) {
     rl_beg = 0;
@@ -1565,7 +1600,18 @@ __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__
       int maxl = which == 0 ? cd.max_rep : cd.max_def;
       int enc = which == 0 ? pw.rl_encoding : pw.dl_encoding;
       uint32_t b = p, e = p;
-      if (maxl > 0) {
+      if (maxl > 0 && enc == PQG_BIT_PACKED) {
+        // deprecated BIT_PACKED levels (ByteBitPackingValuesReader(maxLevel, BIG_ENDIAN).initFromPage
+        // :77-88): min(ceil(num_values * w / 8), available) bytes, no length prefix
+        const uint32_t wl = 32 - __builtin_clz((uint32_t)maxl);
+        const uint64_t want = ((uint64_t)nslots * wl + 7u) / 8u;
+        const uint32_t len = (uint32_t)(want < (uint64_t)(size - p) ? want : (uint64_t)(size - p));
+        b = p;
+        e = p + len;
+        p = e;
+        if (which == 0) rl_be = true;
+        else dl_be = true;
+      } else if (maxl > 0) {
         if (enc != PQG_RLE) { init_err = PQG_ERR_UNSUPPORTED; init_phase = which; break; }
         if (p + 4u > size) { init_err = PQG_ERR_EOF; init_phase = which; break; }
         int32_t len = (int32_t)(uint32_t)win.read8(p);
@@ -1598,7 +1644,8 @@ __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__
   uint8_t* def_out = cd.def_levels ? cd.def_levels + pw.slot_offset : nullptr;
   uint64_t lvl_err_key = ~0ull;
   if (wr > 0) {
-    uint32_t done = decode_levels_pj(LL, win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code);
+    uint32_t done = rl_be ? decode_levels_be(win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code)
+                          : decode_levels_pj(LL, win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code);
     if (code) {
       limit = done;
       lvl_err_key = ((uint64_t)done << 1) << 8 | (uint64_t)code;
@@ -1609,8 +1656,10 @@ __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__
   uint32_t nonnull = 0;
   if (wd > 0) {
     int code2 = 0;
-    uint32_t done = decode_levels_pj(LL, win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true, &nonnull,
-                                     &code2);
+    uint32_t done = dl_be ? decode_levels_be(win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true,
+                                             &nonnull, &code2)
+                          : decode_levels_pj(LL, win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true,
+                                             &nonnull, &code2);
     if (code2) {
       uint64_t key = (((uint64_t)done << 1) | 1ull) << 8 | (uint64_t)code2;
       if (key < lvl_err_key) lvl_err_key = key;

@@ -256,9 +256,22 @@ class ColumnChunk:
         return sum(p.num_values for p in self.pages)
 
 
-def _level_section(levels, max_level, version):
+def be_pack(values, bit_width):
+    """Deprecated BIT_PACKED level encoding (BitPacking / Packer.BIG_ENDIAN): MSB-first bit
+    stream, ceil(n * w / 8) bytes."""
+    v = np.asarray(values, dtype=np.uint32)
+    if bit_width == 0 or v.size == 0:
+        return b""
+    bits = ((v[:, None] >> np.arange(bit_width - 1, -1, -1, dtype=np.uint32)) & 1).astype(np.uint8).ravel()
+    return np.packbits(bits).tobytes()
+
+
+def _level_section(levels, max_level, version, encoding=abi.RLE):
     if max_level == 0:
         return b""
+    if encoding == abi.BIT_PACKED:
+        assert version == 1, "BIT_PACKED levels exist only in V1 pages"
+        return be_pack(levels, width_from_max_int(max_level))
     body = rle_encode_levels(levels, width_from_max_int(max_level))
     if version == 1:
         return len(body).to_bytes(4, "little") + body
@@ -283,7 +296,7 @@ def _page_bounds(n_slots, page_rows, rep_levels):
 
 def write_column_chunk(physical_type, values, encoding, *, def_levels=None, rep_levels=None, max_def=0,
                        max_rep=0, page_rows=20000, version=1, type_length=0, delta_block=128,
-                       delta_miniblocks=4, dict_page_encoding=abi.PLAIN):
+                       delta_miniblocks=4, dict_page_encoding=abi.PLAIN, level_encoding=abi.RLE):
     """Encode one column chunk. `values` are the non-null values (dense, in slot order)."""
     values = values if physical_type == abi.BYTE_ARRAY or physical_type in (abi.INT96, abi.FIXED_LEN_BYTE_ARRAY) \
         else np.asarray(values)
@@ -334,9 +347,10 @@ def write_column_chunk(physical_type, values, encoding, *, def_levels=None, rep_
             data = bss_encode(values[v0:v1], physical_type, type_length)
         else:
             raise ValueError(f"writer does not support encoding {encoding}")
-        rls = _level_section(rl[s:e], max_rep, version)
-        dls = _level_section(dl[s:e], max_def, version)
+        rls = _level_section(rl[s:e], max_rep, version, level_encoding)
+        dls = _level_section(dl[s:e], max_def, version, level_encoding)
         page = Page(body=rls + dls + data, num_values=e - s, encoding=encoding, version=version,
+                    rl_encoding=level_encoding, dl_encoding=level_encoding,
                     num_nulls=int((e - s) - (v1 - v0)),
                     num_rows=int((rl[s:e] == 0).sum()) if max_rep else e - s)
         if version == 2:

@@ -279,3 +279,20 @@ def test_host_path_roundtrip(decoder):
     assert np.array_equal(res[0]["values"], vals)
     assert counts.sum() == vals.size
 
+
+
+@pytest.mark.parametrize("max_def,max_rep", [(1, 0), (2, 0), (3, 1), (7, 0)])
+def test_v1_bit_packed_levels(decoder, max_def, max_rep):
+    """Deprecated BIT_PACKED (big-endian) level sections of old parquet-mr V1 pages
+    (ByteBitPackingValuesReader(maxLevel, BIG_ENDIAN))."""
+    rng = np.random.default_rng(max_def * 10 + max_rep)
+    n = 30_000
+    dl = rng.integers(0, max_def + 1, size=n).astype(np.uint8)
+    rl = None
+    if max_rep:
+        rl = (rng.random(n) < 0.6).astype(np.uint8) * max_rep
+        rl[0] = 0
+    vals = rng.integers(-2**40, 2**40, size=int((dl == max_def).sum())).astype(np.int64)
+    ch = make(abi.INT64, vals, abi.PLAIN, def_levels=dl, rep_levels=rl, max_def=max_def, max_rep=max_rep, version=1,
+              level_encoding=abi.BIT_PACKED, page_rows=7000)
+    run_both(decoder, [ch])

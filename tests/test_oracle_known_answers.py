@@ -390,3 +390,38 @@ def test_bss_errors():
     assert _bss_page(abi.FLOAT, [0] * 12, 2).status == (abi.ERR_CORRUPT, 0, 0)
     # reading past the encoded values: "Byte-stream data was already exhausted." (:43-46)
     assert _bss_page(abi.FLOAT, [0] * 4, 2).status == (abi.ERR_EOF, 0, 1)
+
+
+# ---- TestBitPacking (parquet-encoding/src/test/.../bitpacking/TestBitPacking.java:36-...): BIG_ENDIAN --------------
+
+BE_CASES = [  # (bit width, values, expected bit string)
+    (1, [0], "00000000"), (1, [1], "10000000"), (1, [0, 0], "00000000"), (1, [1, 1], "11000000"),
+    (1, [1] * 9, "11111111 10000000"), (1, [0] * 9, "00000000 00000000"),
+    (1, [0, 0, 0, 0, 0, 0, 0, 1], "00000001"), (1, [0] * 9 + [1], "00000000 01000000"),
+    (1, [0, 1, 0, 0, 1, 1, 1, 0, 0, 1], "01001110 01000000"),
+    (2, [0, 1, 2, 3, 3, 3, 2, 1, 1, 0, 0, 0, 1], "00011011 11111001 01000000 01000000"),
+]
+
+
+@pytest.mark.parametrize("w,vals,bits", BE_CASES)
+def test_be_bit_packing_known_answers(w, vals, bits):
+    expected = bytes(int(b, 2) for b in bits.split())
+    assert writer.be_pack(vals, w) == expected
+    padded = expected + b"\0" * 16
+    got = []
+    for g in range(0, len(vals), 8):
+        got += list(pqref.unpack8_int_be(w, padded[g * w // 8:]))
+    assert got[:len(vals)] == vals
+
+
+@pytest.mark.parametrize("max_def", [1, 2, 3, 7])
+def test_v1_bit_packed_def_levels(max_def):
+    """Old parquet-mr V1 pages: BIT_PACKED (big-endian) definition levels, no length prefix."""
+    rng = np.random.default_rng(max_def)
+    dl = rng.integers(0, max_def + 1, size=5000).astype(np.uint8)
+    vals = np.arange(int((dl == max_def).sum()), dtype=np.int64)
+    ch = writer.write_column_chunk(abi.INT64, vals, abi.PLAIN, def_levels=dl, max_def=max_def, version=1,
+                                   level_encoding=abi.BIT_PACKED, page_rows=1000)
+    res = pqref.decode_batch(writer.build_batch([ch]))
+    assert res.code == 0, res.status
+    assert np.array_equal(res.columns[0]["def_levels"], dl) and np.array_equal(res.columns[0]["values"], vals)
