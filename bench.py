@@ -74,6 +74,60 @@ def cpu_baseline(batch, n_values, budget_s):
                       f"{dt:.1f} s, oracle/pqref.c -O3, single thread"}
 
 
+def cpu_baseline_mt(chunk, n_values, threads, budget_s):
+    """The same oracle on `threads` host threads, pages split into contiguous groups (pages of a
+    required dictionary column are independent once the dictionary is read; ctypes releases the
+    GIL during the C decode)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from pqgpu import writer
+    sys.path.insert(0, REPO)
+    from oracle import pqref
+    groups = np.array_split(np.arange(len(chunk.pages)), threads)
+    subs = []
+    for g in groups:
+        c = writer.ColumnChunk(physical_type=chunk.physical_type, dict_page=chunk.dict_page,
+                               dict_num_values=chunk.dict_num_values, dict_encoding=chunk.dict_encoding)
+        c.pages = [chunk.pages[i] for i in g]
+        subs.append(writer.build_batch([c]))
+    with ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        reps = 0
+        while True:
+            for r in ex.map(pqref.decode_batch, subs):
+                assert r.code == 0
+            reps += 1
+            if time.perf_counter() - t0 >= budget_s:
+                break
+        dt = time.perf_counter() - t0
+    return {"value": reps * n_values / dt, "unit": "values/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x full chunk, {threads} threads over page groups, {dt:.1f} s"}
+
+
+def pyarrow_baseline(values, budget_s, threads):
+    """Third-party reference point (not the reference): Arrow C++ (pyarrow) reading the same
+    values written by pyarrow as one dictionary-encoded int64 column, uncompressed, V1 pages."""
+    try:
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+    except Exception as e:  # pyarrow absent on the host
+        return {"unavailable": str(e)}
+    sink = pa.BufferOutputStream()
+    pq.write_table(pa.table({"c2": pa.array(values)}), sink, compression="NONE", use_dictionary=True,
+                   data_page_version="1.0", row_group_size=len(values))
+    buf = sink.getvalue()
+    pa.set_cpu_count(threads)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        t = pq.read_table(pa.BufferReader(buf), use_threads=True)
+        reps += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": reps * len(values) / dt, "unit": "values/s", "cores": threads, "kind": "third-party",
+            "sample": f"pyarrow {pa.__version__} read_table of the same 100M values (its own pages), {reps} reps"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,6 +218,9 @@ def main():
     cpu = None
     if rank == 0 and not args.no_cpu:
         cpu = cpu_baseline(batch, n, args.cpu_budget)
+        threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 cores
+        cpu["multi_thread"] = cpu_baseline_mt(chunk, n, threads, args.cpu_budget / 2)
+        cpu["pyarrow"] = pyarrow_baseline(dict_vals[ids], args.cpu_budget / 2, threads)
 
     traffic, traffic_bytes, traffic_src = None, None, None
     if os.path.exists(args.traffic_json):
