@@ -82,6 +82,12 @@ int elem_width(int t, int tl) {
   }
 }
 
+// Error words: 3 per page + 3 per column (dictionary pages), padded to 16 bytes; the error
+// counter follows them in the same allocation.
+size_t err_region_bytes(int n_pages, int n_cols) {
+  return (sizeof(uint64_t) * 3 * (size_t)(n_pages + std::max(n_cols, 1)) + 15) & ~(size_t)15;
+}
+
 // Kernel classes, in launch order after the level pass.
 //   C_IDS   dictionary pages whose values are not 4 / 8 bytes (BYTE_ARRAY, FLBA, INT96): ids first
 //   C_BINP  PLAIN BYTE_ARRAY          C_DLBA  DELTA_LENGTH_BYTE_ARRAY      C_BSS  BYTE_STREAM_SPLIT
@@ -104,7 +110,7 @@ struct pqg_plan {
   uint64_t n_bytes = 0;
   int n_pages = 0;
   int n_cols = 0;
-  DevBuf work, cols, lists, col_pages, col_page_start, err, err_count;
+  DevBuf work, cols, lists, col_pages, col_page_start, err;
   DevBuf rec, chunk_run, chunks;      // dictionary pages: run records, chunk -> record, chunk work list
   DevBuf pstat, flags;                // per page: {records, values} and ready epoch (fused dictionary kernel)
   uint32_t epoch = 0;
@@ -482,12 +488,12 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
             P->lists.ensure(sizeof(int32_t) * std::max<size_t>(flat.size(), 1)) == hipSuccess &&
             P->col_pages.ensure(sizeof(int32_t) * std::max<size_t>(cp.size(), 1)) == hipSuccess &&
             P->col_page_start.ensure(sizeof(int32_t) * cps.size()) == hipSuccess &&
-            P->err.ensure(sizeof(uint64_t) * 3 * (size_t)(n_pages + std::max(n_cols, 1))) == hipSuccess &&
+            P->err.ensure(err_region_bytes(n_pages, n_cols) + 16) == hipSuccess &&
             P->bscratch.ensure(std::max<uint64_t>(sc, 256)) == hipSuccess &&
             P->bin_lists.ensure(sizeof(int32_t) * std::max<size_t>(bl.size(), 1)) == hipSuccess &&
             P->bin_blocks.ensure(sizeof(uint64_t) * std::max<size_t>(bin_blocks.size(), 1)) == hipSuccess &&
             P->bin_chunks.ensure(sizeof(uint64_t) * std::max<size_t>(bin_chunks.size(), 1)) == hipSuccess &&
-            P->err_count.ensure(sizeof(uint32_t) * 4) == hipSuccess &&
+
             P->rec.ensure(sizeof(uint64_t) * (rec_total + 16)) == hipSuccess &&  // k_dict_fill reads 9 ahead
             P->chunk_run.ensure(sizeof(uint32_t) * std::max<uint32_t>(chunk_total, 1)) == hipSuccess &&
             P->chunks.ensure(sizeof(uint64_t) * std::max<size_t>(chunk_list.size(), 1)) == hipSuccess &&
@@ -547,16 +553,17 @@ int pqg_plan_launch(pqg_plan* P) {
   pqg_ctx* ctx = P->ctx;
   hipStream_t s = ctx->stream;
   uint64_t* err = (uint64_t*)P->err.p;
-  uint32_t* ecount = (uint32_t*)P->err_count.p;
+  // error words and the error counter share one allocation and one 0xFF memset per launch: the
+  // counter starts at 0xFFFFFFFF and report() increments it (wraps), so "no error" is 0xFFFFFFFF
+  const size_t err_bytes = err_region_bytes(P->n_pages, P->n_cols);
+  uint32_t* ecount = (uint32_t*)((uint8_t*)P->err.p + err_bytes);
   PageWork* work = (PageWork*)P->work.p;
   const ColumnDev* cols = (const ColumnDev*)P->cols.p;
   const int32_t* lists = (const int32_t*)P->lists.p;
-  if (hipMemsetAsync(err, 0xFF, sizeof(uint64_t) * 3 * (size_t)(P->n_pages + std::max(P->n_cols, 1)), s) != hipSuccess)
-    return PQG_ERR_HIP;
+  if (hipMemsetAsync(err, 0xFF, err_bytes + 16, s) != hipSuccess) return PQG_ERR_HIP;
   if (P->blen_bytes && hipMemsetAsync(P->bscratch.p, 0, P->blen_bytes, s) != hipSuccess) return PQG_ERR_HIP;
   for (void* v : P->empty_bin_values)
     if (hipMemsetAsync(v, 0, sizeof(int64_t), s) != hipSuccess) return PQG_ERR_HIP;
-  if (hipMemsetAsync(ecount, 0, sizeof(uint32_t) * 4, s) != hipSuccess) return PQG_ERR_HIP;
   if (++P->epoch == 0) {  // page ready flags compare against the launch epoch; reset on wrap
     P->epoch = 1;
     if (hipMemsetAsync(P->flags.p, 0, sizeof(uint32_t) * (size_t)std::max(P->n_pages, 1), s) != hipSuccess)
@@ -634,7 +641,6 @@ int pqg_plan_destroy(pqg_plan* P) {
   P->col_pages.release();
   P->col_page_start.release();
   P->err.release();
-  P->err_count.release();
   P->rec.release();
   P->chunk_run.release();
   P->chunks.release();
@@ -663,7 +669,9 @@ int resolve_errors(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work_out)
   hipStream_t s = ctx->stream;
   if (ctx->pin_err.ensure(16) != hipSuccess) return PQG_ERR_HIP;
   uint32_t* cnt = (uint32_t*)ctx->pin_err.p;
-  if (hipMemcpyAsync(cnt, P->err_count.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) return PQG_ERR_HIP;
+  if (hipMemcpyAsync(cnt, (uint8_t*)P->err.p + err_region_bytes(P->n_pages, P->n_cols), sizeof(uint32_t),
+                     hipMemcpyDeviceToHost, s) != hipSuccess)
+    return PQG_ERR_HIP;
   bool need_work = false;
   for (auto v : P->col_nullable) need_work = need_work || v;
   if (need_work && work_out) {
@@ -673,7 +681,7 @@ int resolve_errors(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work_out)
   }
   if (hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
   std::vector<uint64_t> errs;
-  if (*cnt) {
+  if (*cnt != 0xFFFFFFFFu) {  // the counter starts at 0xFFFFFFFF (see pqg_plan_launch)
     errs.resize(3 * (size_t)(P->n_pages + std::max(P->n_cols, 1)));
     if (hipMemcpy(errs.data(), P->err.p, sizeof(uint64_t) * errs.size(), hipMemcpyDeviceToHost) != hipSuccess) return PQG_ERR_HIP;
   }
