@@ -389,6 +389,27 @@ __global__ __launch_bounds__(256) void k_bin_offsets(const ColumnDev* __restrict
 }
 
 // ---------------------------------------------------------------------------
+// Store the 16-byte output block at `a` (dwords wd) clipped to [o_lo, o_hi): one 16-byte store
+// when the block is whole and aligned, dword stores for whole dwords, byte stores at the edges
+// (which neighbouring chunks / pages share). have: bit q = dword q whole (0 for an unaligned dst).
+__device__ __forceinline__ void store_block16(uint8_t* dst, uint64_t a, uint64_t o_lo, uint64_t o_hi,
+                                              const uint32_t (&wd)[4], uint32_t have, bool dst_al16) {
+  if (have == 0xFu && dst_al16) {
+    gst_nt((u32x4*)(dst + a), u32x4{wd[0], wd[1], wd[2], wd[3]});
+    return;
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    const uint64_t d0 = a + 4u * q;
+    if ((have >> q) & 1u) {
+      gst((uint32_t*)(dst + d0), wd[q]);
+    } else {
+      for (uint32_t j = 0; j < 4; j++)
+        if (d0 + j >= o_lo && d0 + j < o_hi) gst(dst + d0 + j, (uint8_t)(wd[q] >> (8u * j)));
+    }
+  }
+}
+
 // Value bytes. One wave per chunk of BIN_CHUNK values of one page (chunks[c] = page | j << 32).
 // The chunk's offsets and sources are staged in LDS; every lane owns output dwords of the
 // chunk's byte range and finds the value of its first byte by binary search (then walks
@@ -449,52 +470,53 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
   // read per piece, usually one piece per dword)
   const uint64_t a0 = o_lo & ~15ull;
   const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
+  // Blocks are gathered G at a time before any of them is stored: a source load issued
+  // after a store waits for that store (vmcnt counts both), so loads and stores are not interleaved.
+  constexpr uint32_t G = 4;
   uint32_t kv = 0;  // value of this lane's current byte (monotone across iterations)
-  for (uint64_t a = a0 + 16u * lane; a < o_hi; a += 16u * WAVE) {
-    const uint64_t b0 = a > o_lo ? a : o_lo;
-    uint32_t lo = kv, hi = n;
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (off[mid] <= b0) lo = mid;
-      else hi = mid;
-    }
-    kv = lo;
-    uint32_t wd[4];
-    uint32_t have = 0;  // bit q: dword q fully inside [o_lo, o_hi)
-    uint32_t k = kv;
+  for (uint64_t ag = a0 + 16u * lane; ag < o_hi; ag += 16u * WAVE * G) {
+    uint32_t wd[G][4];
+    uint32_t have[G];  // bit q: dword q fully inside [o_lo, o_hi)
 #pragma unroll
-    for (uint32_t q = 0; q < 4; q++) {
-      const uint64_t d0 = a + 4u * q;
-      const uint64_t x0 = d0 > o_lo ? d0 : o_lo, x1 = d0 + 4u < o_hi ? d0 + 4u : o_hi;
-      uint32_t word = 0;
-      for (uint64_t cur = x0; cur < x1;) {
-        while (k + 1 < n && cur >= off[k + 1]) k++;
-        const uint64_t vend = off[k + 1];
-        const uint64_t seg_end = x1 < vend ? x1 : vend;
-        const uint32_t nbytes = (uint32_t)(seg_end - cur);
-        const uint64_t sp = (uint64_t)src[k] + (cur - off[k]);
-        const uint32_t v = sp < slim ? ld4_any(rs, (uint32_t)sp) : 0u;
-        const uint32_t m = nbytes >= 4 ? 0xFFFFFFFFu : ((1u << (8u * nbytes)) - 1u);
-        word |= (v & m) << (8u * (uint32_t)(cur - d0));
-        cur = seg_end;
+    for (uint32_t g = 0; g < G; g++) {
+      const uint64_t a = ag + 16u * WAVE * g;
+      have[g] = 0;
+      wd[g][0] = wd[g][1] = wd[g][2] = wd[g][3] = 0;
+      if (a >= o_hi) continue;
+      const uint64_t b0 = a > o_lo ? a : o_lo;
+      uint32_t lo = kv, hi = n;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= b0) lo = mid;
+        else hi = mid;
       }
-      wd[q] = word;
-      if (x0 == d0 && x1 == d0 + 4u) have |= 1u << q;
-    }
-    if (!dst_al4) have = 0;  // unaligned byte buffer (C ABI caller): byte stores only
-    if (have == 0xFu && dst_al16) {
-      gst_nt((u32x4*)(dst + a), u32x4{wd[0], wd[1], wd[2], wd[3]});
-    } else {
+      kv = lo;
+      uint32_t k = kv;
 #pragma unroll
       for (uint32_t q = 0; q < 4; q++) {
         const uint64_t d0 = a + 4u * q;
-        if ((have >> q) & 1u) {
-          gst((uint32_t*)(dst + d0), wd[q]);
-        } else {
-          for (uint32_t j = 0; j < 4; j++)
-            if (d0 + j >= o_lo && d0 + j < o_hi) gst(dst + d0 + j, (uint8_t)(wd[q] >> (8u * j)));
+        const uint64_t x0 = d0 > o_lo ? d0 : o_lo, x1 = d0 + 4u < o_hi ? d0 + 4u : o_hi;
+        uint32_t word = 0;
+        for (uint64_t cur = x0; cur < x1;) {
+          while (k + 1 < n && cur >= off[k + 1]) k++;
+          const uint64_t vend = off[k + 1];
+          const uint64_t seg_end = x1 < vend ? x1 : vend;
+          const uint32_t nbytes = (uint32_t)(seg_end - cur);
+          const uint64_t sp = (uint64_t)src[k] + (cur - off[k]);
+          const uint32_t v = sp < slim ? ld4_any(rs, (uint32_t)sp) : 0u;
+          const uint32_t m = nbytes >= 4 ? 0xFFFFFFFFu : ((1u << (8u * nbytes)) - 1u);
+          word |= (v & m) << (8u * (uint32_t)(cur - d0));
+          cur = seg_end;
         }
+        wd[g][q] = word;
+        if (x0 == d0 && x1 == d0 + 4u) have[g] |= 1u << q;
       }
+      if (!dst_al4) have[g] = 0;  // unaligned byte buffer (C ABI caller): byte stores only
+    }
+#pragma unroll
+    for (uint32_t g = 0; g < G; g++) {
+      const uint64_t a = ag + 16u * WAVE * g;
+      if (a < o_hi) store_block16(dst, a, o_lo, o_hi, wd[g], have[g], dst_al16);
     }
   }
 }

@@ -72,6 +72,16 @@ __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v, uint32_t* tot
   return x - v;
 }
 
+// Maximum over the wave (u32), in every lane.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t y = __shfl_xor(v, o);
+    v = v > y ? v : y;
+  }
+  return v;
+}
+
 // Stores through address_space(1) pointers: global_store_* count only in vmcnt.
 // (Generic pointers give flat_store_*, which also count in lgkmcnt, so every
 // s_waitcnt lgkmcnt(0) for an LDS read would wait for all stores in flight.)

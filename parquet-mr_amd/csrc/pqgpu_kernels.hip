@@ -1806,24 +1806,77 @@ __global__ __launch_bounds__(64 * WPB) void k_plain_bool(const uint8_t* __restri
 // wave-wide inclusive scan (wrapping int64) turns them into values. INT32 =
 // (int) of the long (readInteger :103-107).
 //
+// LDS segment of the page bytes for the delta decoder: the serial header chain and the
+// miniblocks are read from LDS, and the segment is refilled (one coalesced 8 KiB load) only
+// every few dozen blocks. Reading the page with global loads between the blocks' stores costs
+// a full store drain per block (vmcnt counts stores on CDNA).
+constexpr uint32_t DSEG = 8192;
+
+struct DSeg {
+  rsrc_t rs;
+  uint8_t* seg;
+  uint32_t lo;  // segment = page bytes [lo, lo + DSEG), lo 16-aligned (uniform)
+
+  __device__ __forceinline__ void fill(uint32_t p) {
+    lo = uni(p & ~15u);
+#pragma unroll
+    for (uint32_t i = 0; i < DSEG; i += 16u * WAVE) {
+      const uint32_t o = i + 16u * lane_id();
+      *(u32x4*)(seg + o) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lo + o), 0, 0);
+    }
+    wave_sync();
+  }
+  __device__ __forceinline__ bool has(uint32_t a, uint32_t n) const {
+    return a >= lo && (uint64_t)a + n <= (uint64_t)lo + DSEG;
+  }
+  __device__ __forceinline__ uint32_t w32(uint32_t a4) const { return *(const u32_alias*)(seg + (a4 - lo)); }
+  // 8 bytes at uniform p (refills the segment when they are not staged)
+  __device__ __forceinline__ uint64_t read8u(uint32_t p) {
+    const uint32_t a = p & ~3u, sb = p & 3u;
+    if (!has(a, 12)) fill(p);
+    const uint32_t x0 = w32(a), x1 = w32(a + 4), x2 = w32(a + 8);
+    return (uint64_t)__builtin_amdgcn_alignbyte(x1, x0, sb) |
+           ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sb) << 32);
+  }
+};
+
+// readUnsignedVarInt / readUnsignedVarLong (BytesUtils.java:202-211, 260-269) at uniform p with
+// Java shift masking; a varint not terminated within `lim` bytes gets len = lim + 1.
+template <bool INT>
+__device__ __forceinline__ uint64_t seg_uvar(DSeg& S, uint32_t p, uint32_t lim, uint32_t& len) {
+  uint64_t value = 0, x = S.read8u(p);
+  uint32_t i = 0, k = 0, b;
+  for (;;) {
+    b = (k < 8u) ? (uint32_t)(x >> (8u * k)) & 0xFFu : (uint32_t)S.read8u(p + k) & 0xFFu;
+    if (!(b & 0x80u)) break;
+    value |= (uint64_t)(b & 0x7Fu) << (i & (INT ? 31u : 63u));
+    i += 7;
+    k++;
+    if (k >= lim) break;
+  }
+  len = k + 1;
+  if (INT) return (uint32_t)value | (b << (i & 31u));
+  return value | ((uint64_t)b << (i & 63u));
+}
+
 // One stream [p, end) -> out[0 .. min(want, total)). Returns 0 or the init error code (the
 // reader decodes eagerly in initFromPage); *p_end = stream position after the used miniblocks,
 // *total_out = the header's value count. NEG: a negative (int) value is reported as CORRUPT at
 // its index and written as 0 (DELTA_LENGTH_BYTE_ARRAY lengths: in.slice(negative)).
 template <int W, bool NEG>
-__device__ int delta_stream(Window& win, uint32_t p, uint32_t end, uint32_t want, typename DictVal<W>::T* out,
+__device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, typename DictVal<W>::T* out,
                             int page, uint64_t* err, uint32_t* err_count, uint32_t* p_end, uint32_t* total_out) {
   typedef typename DictVal<W>::T T;
   const uint32_t lane = lane_id();
   uint32_t len;
-  win.seek(p);
+  p = uni(p);
   // header (DeltaBinaryPackingConfig.readConfig :43-45, totalValueCount, first value)
   if (p >= end) return PQG_ERR_EOF;
-  uint32_t block = read_uvarint(win, p, end - p, len);
+  const uint32_t block = (uint32_t)seg_uvar<true>(S, p, end - p, len);
   if ((uint64_t)p + len > end) return PQG_ERR_EOF;
   p += len;
   if (p >= end) return PQG_ERR_EOF;
-  uint32_t mbn = read_uvarint(win, p, end - p, len);
+  const uint32_t mbn = (uint32_t)seg_uvar<true>(S, p, end - p, len);
   if ((uint64_t)p + len > end) return PQG_ERR_EOF;
   p += len;
   // DeltaBinaryPackingConfig ctor :34-41 (double division, % 8)
@@ -1834,12 +1887,12 @@ __device__ int delta_stream(Window& win, uint32_t p, uint32_t end, uint32_t want
   // register budget of this kernel: block <= 512 values, <= 8 miniblocks (parquet-mr default 128 / 4)
   if (block > 512u || mbn > 8u) return PQG_ERR_UNSUPPORTED;
   if (p >= end) return PQG_ERR_EOF;
-  uint32_t total = read_uvarint(win, p, end - p, len);
+  const uint32_t total = (uint32_t)seg_uvar<true>(S, p, end - p, len);
   if ((uint64_t)p + len > end) return PQG_ERR_EOF;
   p += len;
   if ((int32_t)total < 0) return PQG_ERR_CORRUPT;
   if (p >= end) return PQG_ERR_EOF;
-  uint64_t fraw = read_uvarlong(win, p, end - p, len);
+  const uint64_t fraw = seg_uvar<false>(S, p, end - p, len);
   if ((uint64_t)p + len > end) return PQG_ERR_EOF;
   p += len;
   const int64_t first = zigzag64(fraw);
@@ -1859,57 +1912,74 @@ __device__ int delta_stream(Window& win, uint32_t p, uint32_t end, uint32_t want
   }
   uint32_t buffered = 1;  // Java valuesBuffered (includes the first value)
   const uint32_t E = (block + WAVE - 1) / WAVE;  // deltas per lane per block
-  while (buffered < total) {
-    // ---- walk up to 64 blocks (headers + data offsets)
+  // bytes a block header may touch: varint (<= 10) + widths (<= 8) + read slack
+  constexpr uint32_t HDR_SPAN = 40;
+  while (true) {
+    buffered = uni(buffered);
+    p = uni(p);
+    if (buffered >= total) break;
+    // a batch starts with its first block fully staged (a block is <= 4126 bytes)
+    if (!S.has(p, DSEG / 2 + 64)) S.fill(p);
+    // ---- walk up to 64 blocks whose bytes lie in the segment (headers + data offsets)
     uint32_t b_data = 0, b_wpos = 0, b_lo = 0, b_hi = 0, b_nmb = 0;
     uint32_t nb = 0;
-    uint32_t blk_first = buffered;
-    while (nb < 64u && buffered < total) {
+    const uint32_t blk_first = buffered;
+    while (true) {
+      nb = uni(nb);
+      p = uni(p);
+      buffered = uni(buffered);
+      if (nb >= 64u || buffered >= total) break;
       if (p >= end) return PQG_ERR_EOF;
-      uint64_t mraw = read_uvarlong(win, p, end - p, len);               // loadNewBlockToBuffer :122-126
+      if (!S.has(p, HDR_SPAN)) break;  // nb > 0 here: the batch ends, the next one refills
+      const uint64_t mraw = seg_uvar<false>(S, p, end - p, len);  // loadNewBlockToBuffer :122-126
       if ((uint64_t)p + len > end) return PQG_ERR_EOF;
-      p += len;
-      int64_t mind = zigzag64(mraw);
-      if ((uint64_t)p + mbn > end) return PQG_ERR_EOF;                  // readBitWidthsForMiniBlocks
-      uint32_t wpos = p;
-      p += mbn;
+      const int64_t mind = zigzag64(mraw);
+      const uint32_t wpos = p + len;
+      if ((uint64_t)wpos + mbn > end) return PQG_ERR_EOF;  // readBitWidthsForMiniBlocks
       // miniblocks unpacked while buffered < total (:131-135)
-      uint32_t used = 0;
+      uint32_t used = 0, bufd = buffered;
       uint64_t dbytes = 0;
-      uint32_t bufd = buffered;
+      const uint64_t wbytes = S.read8u(wpos);  // the <= 8 width bytes
       for (uint32_t m = 0; m < mbn && bufd < total; m++) {
-        uint32_t wm = win.byte(wpos + m);
+        const uint32_t wm = (uint32_t)(wbytes >> (8u * m)) & 0xFFu;
         if (wm > 64u) return PQG_ERR_CORRUPT;
         dbytes += (uint64_t)wm * (mbs / 8u);
         bufd += mbs;
         used++;
       }
-      if ((uint64_t)p + dbytes > end) return PQG_ERR_EOF;               // in.slice EOF
+      const uint32_t dpos = wpos + mbn;
+      if ((uint64_t)dpos + dbytes > end) return PQG_ERR_EOF;  // in.slice EOF
+      // the block's data (+ read slack) must be staged, else the block starts the next batch
+      if (!S.has(dpos, (uint32_t)dbytes + 12u)) break;
       const bool me = lane == nb;
-      b_data = me ? p : b_data;
+      b_data = me ? dpos : b_data;
       b_wpos = me ? wpos : b_wpos;
       b_lo = me ? (uint32_t)(uint64_t)mind : b_lo;
       b_hi = me ? (uint32_t)((uint64_t)mind >> 32) : b_hi;
       b_nmb = me ? used : b_nmb;
-      p += (uint32_t)dbytes;
-      win.ensure(p);
+      p = dpos + (uint32_t)dbytes;
       buffered = bufd;
       nb++;
     }
-    // ---- expand the walked blocks
+    if (nb == 0) return PQG_ERR_CORRUPT;  // unreachable: the first block of a batch always fits
+    // ---- expand the walked blocks (every read from the LDS segment)
     for (uint32_t b = 0; b < nb; b++) {
       const uint32_t data = rdl(b_data, b), wpos = rdl(b_wpos, b), nmb = rdl(b_nmb, b);
       const uint64_t mind = ((uint64_t)rdl(b_hi, b) << 32) | rdl(b_lo, b);
       const uint32_t k0 = blk_first + b * block;  // value index of the block's first delta
       uint64_t loc[8];
       uint64_t sum = 0;
-      // miniblock widths of this block (≤ 8 miniblocks handled in registers)
+      // miniblock widths of this block (<= 8 miniblocks handled in registers)
       uint32_t wmb[8], offmb[8];
       {
+        const uint32_t wa = wpos & ~3u, sb = wpos & 3u;
+        const uint32_t y0 = S.w32(wa), y1 = S.w32(wa + 4), y2 = S.w32(wa + 8);
+        const uint64_t wb = (uint64_t)__builtin_amdgcn_alignbyte(y1, y0, sb) |
+                            ((uint64_t)__builtin_amdgcn_alignbyte(y2, y1, sb) << 32);
         uint32_t acc = 0;
 #pragma unroll
         for (uint32_t mm = 0; mm < 8; mm++) {
-          uint32_t wm = mm < nmb ? (ld32(win.rs, (wpos + mm) & ~3u) >> (((wpos + mm) & 3u) * 8u)) & 0xFFu : 0u;
+          const uint32_t wm = mm < nmb ? (uint32_t)(wb >> (8u * mm)) & 0xFFu : 0u;
           wmb[mm] = wm;
           offmb[mm] = acc;
           acc += wm * (mbs / 8u);
@@ -1931,7 +2001,7 @@ __device__ int delta_stream(Window& win, uint32_t p, uint32_t end, uint32_t want
               uint64_t bit = (uint64_t)(j % mbs) * wm;
               uint32_t byte = data + off + (uint32_t)(bit >> 3);
               uint32_t a = byte & ~3u;
-              uint32_t x0 = ld32(win.rs, a), x1 = ld32(win.rs, a + 4), x2 = ld32(win.rs, a + 8);
+              uint32_t x0 = S.w32(a), x1 = S.w32(a + 4), x2 = S.w32(a + 8);
               uint32_t sh = (byte - a) * 8u + (uint32_t)(bit & 7u);  // < 32
               uint64_t lo64 = (uint64_t)x0 | ((uint64_t)x1 << 32);
               uint64_t v = sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)));
@@ -1984,6 +2054,7 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
                                               const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                               uint32_t* err_count) {
   typedef typename DictVal<W>::T T;
+  __shared__ __attribute__((aligned(16))) uint8_t dseg_all[WPB][DSEG];
   const int page = wave_page(list, n_list);
   if (page < 0) return;
   const PageWork pw = work[page];
@@ -1991,11 +2062,13 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
   const uint32_t lane = lane_id();
   const uint32_t beg = uni(pw.data_begin), end = uni(pw.size);
   const uint32_t want = uni(pw.n_values);
-  Window win;
-  win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  DSeg S;
+  S.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  S.seg = dseg_all[wave_id()];
+  S.lo = 0x80000000u;  // nothing staged yet (pages are < 2 GiB)
   uint32_t p_end = beg, total = 0;
   T* out = (MODE == 0 ? (T*)cd.values : MODE == 1 ? (T*)cd.blen : (T*)cd.bsrc) + pw.out_offset;
-  int code = delta_stream<W, MODE == 1>(win, beg, end, want, out, page, err, err_count, &p_end, &total);
+  int code = delta_stream<W, MODE == 1>(S, beg, end, want, out, page, err, err_count, &p_end, &total);
   if (code) {
     if (lane == 0) report(err, err_count, page, 0, 2, code);
     return;
@@ -2003,7 +2076,7 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
   uint32_t past_end = want > total ? total : 0xFFFFFFFFu;  // first index with no value
   if constexpr (MODE == 2) {
     uint32_t total2 = 0, p2 = p_end;
-    code = delta_stream<4, false>(win, p_end, end, want, cd.blen + pw.out_offset, page, err, err_count, &p2, &total2);
+    code = delta_stream<4, false>(S, p_end, end, want, cd.blen + pw.out_offset, page, err, err_count, &p2, &total2);
     if (code) {
       if (lane == 0) report(err, err_count, page, 0, 2, code);
       return;
