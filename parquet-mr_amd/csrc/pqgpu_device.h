@@ -72,6 +72,25 @@ __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v, uint32_t* tot
   return x - v;
 }
 
+// Inclusive prefix sum over the wave (u64, wrapping) with DPP row shifts and row broadcasts
+// (no LDS round trips). Call with all 64 lanes active.
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t x) {
+#define PQG_DPP_STEP(ctrl, rmask)                                                                        \
+  {                                                                                                      \
+    const uint32_t lo_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, ctrl, rmask, 0xf, true);         \
+    const uint32_t hi_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), ctrl, rmask, 0xf, true); \
+    x += ((uint64_t)hi_ << 32) | lo_;                                                                    \
+  }
+  PQG_DPP_STEP(0x111, 0xf)  // row_shr:1
+  PQG_DPP_STEP(0x112, 0xf)  // row_shr:2
+  PQG_DPP_STEP(0x114, 0xf)  // row_shr:4
+  PQG_DPP_STEP(0x118, 0xf)  // row_shr:8
+  PQG_DPP_STEP(0x142, 0xa)  // row_bcast:15 -> rows 1, 3
+  PQG_DPP_STEP(0x143, 0xc)  // row_bcast:31 -> rows 2, 3
+#undef PQG_DPP_STEP
+  return x;
+}
+
 // Maximum over the wave (u32), in every lane.
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll

@@ -1859,6 +1859,72 @@ __device__ __forceinline__ uint64_t seg_uvar(DSeg& S, uint32_t p, uint32_t lim, 
   return value | ((uint64_t)b << (i & 63u));
 }
 
+// Expansion of nb walked blocks (block b's facts in lane b of b_*): lane l owns deltas
+// [l*E, l*E + E) of every block, all in one miniblock m (the lane's miniblock index and its
+// position in it are the same for every block). Unpacked deltas + minDelta (wrapping, as
+// loadNewBlockToBuffer :139-142), a DPP scan of the lanes' sums, then the lane's E values.
+template <int W, bool NEG, uint32_t E>
+__device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_t b_data, uint32_t b_wpos,
+                                             uint32_t b_lo, uint32_t b_hi, uint32_t b_nmb, uint32_t blk_first,
+                                             uint32_t block, uint32_t mbs, uint32_t n_out, uint64_t& carry,
+                                             typename DictVal<W>::T* out, int page, uint64_t* err,
+                                             uint32_t* err_count) {
+  typedef typename DictVal<W>::T T;
+  const uint32_t lane = lane_id();
+  const uint32_t j0 = lane * E;
+  const bool lane_in = j0 < block;
+  const uint32_t m = lane_in ? j0 / mbs : 0u;
+  const uint32_t jm = j0 - m * mbs;
+  const uint32_t mb_bytes = mbs / 8u;  // bytes per bit of width
+  for (uint32_t b = 0; b < nb; b++) {
+    const uint32_t data = rdl(b_data, b), wpos = rdl(b_wpos, b), nmb = rdl(b_nmb, b);
+    const uint64_t mind = ((uint64_t)rdl(b_hi, b) << 32) | rdl(b_lo, b);
+    const uint32_t k0 = blk_first + b * block;  // value index of the block's first delta
+    // the block's miniblock widths (<= 8 bytes at wpos)
+    const uint32_t wa = wpos & ~3u, sb = wpos & 3u;
+    const uint32_t y0 = S.w32(wa), y1 = S.w32(wa + 4), y2 = S.w32(wa + 8);
+    const uint32_t wlo = __builtin_amdgcn_alignbyte(y1, y0, sb), whi = __builtin_amdgcn_alignbyte(y2, y1, sb);
+    // width of the lane's miniblock and the byte offset of its data (sum of the widths before it)
+    const uint32_t wl = m < nmb ? ((m < 4u ? wlo >> (8u * m) : whi >> (8u * (m - 4u))) & 0xFFu) : 0u;
+    const uint32_t blo = m >= 4u ? wlo : (m ? wlo & ((1u << (8u * m)) - 1u) : 0u);
+    const uint32_t bhi = m <= 4u ? 0u : whi & ((1u << (8u * (m - 4u))) - 1u);
+    const uint32_t off = (__builtin_amdgcn_sad_u8(blo, 0u, 0u) + __builtin_amdgcn_sad_u8(bhi, 0u, 0u)) * mb_bytes;
+    uint64_t loc[E];
+    uint64_t sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < E; q++) {
+      uint64_t d = 0;
+      if (wl) {
+        const uint32_t bit = (jm + q) * wl;
+        const uint32_t byte = data + off + (bit >> 3);
+        const uint32_t a = byte & ~3u;
+        const uint32_t x0 = S.w32(a), x1 = S.w32(a + 4), x2 = S.w32(a + 8);
+        const uint32_t sh = (byte - a) * 8u + (bit & 7u);  // < 32
+        const uint64_t lo64 = (uint64_t)x0 | ((uint64_t)x1 << 32);
+        const uint64_t v = sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)));
+        d = wl == 64 ? v : (v & ((1ull << wl) - 1ull));
+      }
+      sum += lane_in ? d + mind : 0ull;
+      loc[q] = sum;
+    }
+    const uint64_t x = wave_incl_scan_u64(sum);
+    const uint64_t base_v = carry + (x - sum);
+#pragma unroll
+    for (uint32_t q = 0; q < E; q++) {
+      const uint64_t k = (uint64_t)k0 + j0 + q;
+      if (lane_in && k < n_out) {
+        T v = (T)(base_v + loc[q]);
+        if (NEG && (int32_t)(uint32_t)v < 0) {
+          report(err, err_count, page, 2, k, PQG_ERR_CORRUPT);
+          v = 0;
+        }
+        gst(out + k, v);
+      }
+    }
+    carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
+  }
+}
+
 // One stream [p, end) -> out[0 .. min(want, total)). Returns 0 or the init error code (the
 // reader decodes eagerly in initFromPage); *p_end = stream position after the used miniblocks,
 // *total_out = the header's value count. NEG: a negative (int) value is reported as CORRUPT at
@@ -1911,7 +1977,9 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     }
   }
   uint32_t buffered = 1;  // Java valuesBuffered (includes the first value)
-  const uint32_t E = (block + WAVE - 1) / WAVE;  // deltas per lane per block
+  // deltas per lane per block: the power of two >= block / 64 (it divides the block, a multiple
+  // of 8, so a lane's deltas never straddle a miniblock)
+  const uint32_t E = block <= 64u ? 1u : block <= 128u ? 2u : block <= 256u ? 4u : 8u;
   // bytes a block header may touch: varint (<= 10) + widths (<= 8) + read slack
   constexpr uint32_t HDR_SPAN = 40;
   while (true) {
@@ -1963,80 +2031,10 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     }
     if (nb == 0) return PQG_ERR_CORRUPT;  // unreachable: the first block of a batch always fits
     // ---- expand the walked blocks (every read from the LDS segment)
-    for (uint32_t b = 0; b < nb; b++) {
-      const uint32_t data = rdl(b_data, b), wpos = rdl(b_wpos, b), nmb = rdl(b_nmb, b);
-      const uint64_t mind = ((uint64_t)rdl(b_hi, b) << 32) | rdl(b_lo, b);
-      const uint32_t k0 = blk_first + b * block;  // value index of the block's first delta
-      uint64_t loc[8];
-      uint64_t sum = 0;
-      // miniblock widths of this block (<= 8 miniblocks handled in registers)
-      uint32_t wmb[8], offmb[8];
-      {
-        const uint32_t wa = wpos & ~3u, sb = wpos & 3u;
-        const uint32_t y0 = S.w32(wa), y1 = S.w32(wa + 4), y2 = S.w32(wa + 8);
-        const uint64_t wb = (uint64_t)__builtin_amdgcn_alignbyte(y1, y0, sb) |
-                            ((uint64_t)__builtin_amdgcn_alignbyte(y2, y1, sb) << 32);
-        uint32_t acc = 0;
-#pragma unroll
-        for (uint32_t mm = 0; mm < 8; mm++) {
-          const uint32_t wm = mm < nmb ? (uint32_t)(wb >> (8u * mm)) & 0xFFu : 0u;
-          wmb[mm] = wm;
-          offmb[mm] = acc;
-          acc += wm * (mbs / 8u);
-        }
-      }
-      // lane handles deltas j in [lane*E, lane*E + E), E <= 8
-#pragma unroll
-      for (uint32_t q = 0; q < 8; q++) {
-        uint64_t d = 0;
-        uint32_t j = lane * E + q;
-        if (q < E && j < block) {
-          uint32_t m = j / mbs;
-          if (m < nmb) {
-            uint32_t wm = 0, off = 0;
-#pragma unroll
-            for (uint32_t mm = 0; mm < 8; mm++)
-              if (mm == m) { wm = wmb[mm]; off = offmb[mm]; }
-            if (wm) {
-              uint64_t bit = (uint64_t)(j % mbs) * wm;
-              uint32_t byte = data + off + (uint32_t)(bit >> 3);
-              uint32_t a = byte & ~3u;
-              uint32_t x0 = S.w32(a), x1 = S.w32(a + 4), x2 = S.w32(a + 8);
-              uint32_t sh = (byte - a) * 8u + (uint32_t)(bit & 7u);  // < 32
-              uint64_t lo64 = (uint64_t)x0 | ((uint64_t)x1 << 32);
-              uint64_t v = sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)));
-              d = wm == 64 ? v : (v & ((1ull << wm) - 1ull));
-            }
-          }
-          d += mind;  // wrapping: minDelta + unpacked (loadNewBlockToBuffer :139-142)
-        }
-        sum += d;
-        loc[q] = sum;
-      }
-      // wave exclusive scan of lane sums (wrapping 64-bit)
-      uint64_t x = sum;
-      for (int o = 1; o < 64; o <<= 1) {
-        uint64_t y = __shfl_up(x, o);
-        if ((int)lane >= o) x += y;
-      }
-      uint64_t excl = x - sum;
-      uint64_t base_v = carry + excl;
-      // write values k0 + j for j in this lane's range, k < n_out
-#pragma unroll
-      for (uint32_t q = 0; q < 8; q++) {
-        uint32_t j = lane * E + q;
-        uint64_t k = (uint64_t)k0 + j;
-        if (q < E && j < block && k < n_out) {
-          T v = (T)(base_v + loc[q]);
-          if (NEG && (int32_t)(uint32_t)v < 0) {
-            report(err, err_count, page, 2, k, PQG_ERR_CORRUPT);
-            v = 0;
-          }
-          gst(out + k, v);
-        }
-      }
-      carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
-    }
+    if (E == 1) delta_expand<W, NEG, 1>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
+    else if (E == 2) delta_expand<W, NEG, 2>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
+    else if (E == 4) delta_expand<W, NEG, 4>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
+    else delta_expand<W, NEG, 8>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
   }
   *p_end = p;
   return 0;
