@@ -1859,10 +1859,34 @@ __device__ __forceinline__ uint64_t seg_uvar(DSeg& S, uint32_t p, uint32_t lim, 
   return value | ((uint64_t)b << (i & 63u));
 }
 
-// Expansion of nb walked blocks (block b's facts in lane b of b_*): lane l owns deltas
+// Expansion of nb walked blocks (block b's facts in lane b of b_*): lane l unpacks deltas
 // [l*E, l*E + E) of every block, all in one miniblock m (the lane's miniblock index and its
-// position in it are the same for every block). Unpacked deltas + minDelta (wrapping, as
-// loadNewBlockToBuffer :139-142), a DPP scan of the lanes' sums, then the lane's E values.
+// position in it are the same for every block): unpacked + minDelta (wrapping, as
+// loadNewBlockToBuffer :139-142), a DPP scan of the lanes' sums. The value after delta j has
+// index blk_first + b*block + j; lane l STORES the E values ending one delta earlier
+// (indices blk_first - 1 + b*block + l*E + q, the first taken from lane l - 1 / the carry), so
+// that every lane's run is E-aligned and goes out as wide stores. The value after a stream's
+// last full block is written by the caller (delta_stream).
+template <class T, uint32_t E>
+__device__ __forceinline__ void store_run(T* p, const T (&u)[E]) {
+  constexpr uint32_t BYTES = E * sizeof(T);
+  if constexpr (BYTES >= 16) {
+#pragma unroll
+    for (uint32_t i = 0; i < BYTES / 16; i++) {
+      u32x4 v;
+      __builtin_memcpy(&v, (const uint8_t*)u + 16 * i, 16);
+      gst((u32x4*)p + i, v);
+    }
+  } else if constexpr (BYTES == 8) {
+    uint64_t v;
+    __builtin_memcpy(&v, u, 8);
+    gst((uint64_t*)p, v);
+  } else {
+#pragma unroll
+    for (uint32_t q = 0; q < E; q++) gst(p + q, u[q]);
+  }
+}
+
 template <int W, bool NEG, uint32_t E>
 __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_t b_data, uint32_t b_wpos,
                                              uint32_t b_lo, uint32_t b_hi, uint32_t b_nmb, uint32_t blk_first,
@@ -1876,10 +1900,13 @@ __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_
   const uint32_t m = lane_in ? j0 / mbs : 0u;
   const uint32_t jm = j0 - m * mbs;
   const uint32_t mb_bytes = mbs / 8u;  // bytes per bit of width
+  // wide stores need the run's first value E*W-aligned (runs start at multiples of E from `out`)
+  constexpr uint32_t RUN = E * (uint32_t)sizeof(T);
+  const bool wide = RUN >= 8 && (((uintptr_t)out + ((uint64_t)(blk_first - 1) * sizeof(T))) % (RUN >= 16 ? 16 : 8)) == 0 &&
+                    ((uint64_t)block * sizeof(T)) % (RUN >= 16 ? 16 : 8) == 0;
   for (uint32_t b = 0; b < nb; b++) {
     const uint32_t data = rdl(b_data, b), wpos = rdl(b_wpos, b), nmb = rdl(b_nmb, b);
     const uint64_t mind = ((uint64_t)rdl(b_hi, b) << 32) | rdl(b_lo, b);
-    const uint32_t k0 = blk_first + b * block;  // value index of the block's first delta
     // the block's miniblock widths (<= 8 bytes at wpos)
     const uint32_t wa = wpos & ~3u, sb = wpos & 3u;
     const uint32_t y0 = S.w32(wa), y1 = S.w32(wa + 4), y2 = S.w32(wa + 8);
@@ -1889,6 +1916,7 @@ __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_
     const uint32_t blo = m >= 4u ? wlo : (m ? wlo & ((1u << (8u * m)) - 1u) : 0u);
     const uint32_t bhi = m <= 4u ? 0u : whi & ((1u << (8u * (m - 4u))) - 1u);
     const uint32_t off = (__builtin_amdgcn_sad_u8(blo, 0u, 0u) + __builtin_amdgcn_sad_u8(bhi, 0u, 0u)) * mb_bytes;
+    const uint64_t mask = wl == 64 ? ~0ull : ((1ull << wl) - 1ull);
     uint64_t loc[E];
     uint64_t sum = 0;
 #pragma unroll
@@ -1902,23 +1930,37 @@ __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_
         const uint32_t sh = (byte - a) * 8u + (bit & 7u);  // < 32
         const uint64_t lo64 = (uint64_t)x0 | ((uint64_t)x1 << 32);
         const uint64_t v = sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)));
-        d = wl == 64 ? v : (v & ((1ull << wl) - 1ull));
+        d = v & mask;
       }
       sum += lane_in ? d + mind : 0ull;
       loc[q] = sum;
     }
     const uint64_t x = wave_incl_scan_u64(sum);
     const uint64_t base_v = carry + (x - sum);
+    // value before this lane's first delta: the previous lane's last value (lane 0: the carry)
+    const uint64_t last = base_v + loc[E - 1];
+    const uint32_t plo = (uint32_t)__shfl_up((int)(uint32_t)last, 1), phi = (uint32_t)__shfl_up((int)(uint32_t)(last >> 32), 1);
+    const uint64_t prev = lane == 0 ? carry : (((uint64_t)phi << 32) | plo);
+    const uint64_t k0 = (uint64_t)blk_first - 1u + (uint64_t)b * block + j0;  // index of the run's first value
+    T u[E];
 #pragma unroll
-    for (uint32_t q = 0; q < E; q++) {
-      const uint64_t k = (uint64_t)k0 + j0 + q;
-      if (lane_in && k < n_out) {
-        T v = (T)(base_v + loc[q]);
-        if (NEG && (int32_t)(uint32_t)v < 0) {
-          report(err, err_count, page, 2, k, PQG_ERR_CORRUPT);
-          v = 0;
+    for (uint32_t q = 0; q < E; q++) u[q] = (T)(q == 0 ? prev : base_v + loc[q - 1]);
+    if (lane_in) {
+      if (!NEG && wide && k0 + E <= n_out) {
+        store_run<T, E>(out + k0, u);
+      } else {
+#pragma unroll
+        for (uint32_t q = 0; q < E; q++) {
+          const uint64_t k = k0 + q;
+          if (k < n_out) {
+            T v = u[q];
+            if (NEG && k > 0 && (int32_t)(uint32_t)v < 0) {
+              report(err, err_count, page, 2, k, PQG_ERR_CORRUPT);
+              v = 0;
+            }
+            if (!NEG || k > 0) gst(out + k, v);
+          }
         }
-        gst(out + k, v);
       }
     }
     carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
@@ -1977,6 +2019,7 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     }
   }
   uint32_t buffered = 1;  // Java valuesBuffered (includes the first value)
+  uint32_t n_blocks = 0;
   // deltas per lane per block: the power of two >= block / 64 (it divides the block, a multiple
   // of 8, so a lane's deltas never straddle a miniblock)
   const uint32_t E = block <= 64u ? 1u : block <= 128u ? 2u : block <= 256u ? 4u : 8u;
@@ -2035,6 +2078,20 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     else if (E == 2) delta_expand<W, NEG, 2>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else if (E == 4) delta_expand<W, NEG, 4>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else delta_expand<W, NEG, 8>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
+    n_blocks += nb;
+  }
+  // the value after the last delta of the last block (the expansion stores values up to the one
+  // before each block's last delta); only needed when that block was full
+  {
+    const uint64_t k = (uint64_t)n_blocks * block;
+    if (n_blocks && k < n_out && lane == 0) {
+      T v = (T)carry;
+      if (NEG && (int32_t)(uint32_t)v < 0) {
+        report(err, err_count, page, 2, k, PQG_ERR_CORRUPT);
+        v = 0;
+      }
+      gst(out + k, v);
+    }
   }
   *p_end = p;
   return 0;

@@ -187,11 +187,16 @@ def test_delta(decoder, ptype, kind):
     run_both(decoder, [make(ptype, vals, abi.DELTA_BINARY_PACKED, page_rows=20000)])
 
 
-@pytest.mark.parametrize("block,mb", [(128, 4), (64, 8), (256, 8), (512, 8), (32, 1)])
-def test_delta_configs(decoder, block, mb):
+@pytest.mark.parametrize("block,mb", [(128, 4), (64, 8), (256, 8), (512, 8), (32, 1), (8, 1),
+                                      (192, 3), (24, 3), (320, 5)])
+@pytest.mark.parametrize("ptype", [abi.INT64, abi.INT32])
+def test_delta_configs(decoder, block, mb, ptype):
+    # blocks of 8 * 2^k values take the several-blocks-per-step expansion, the others one block per step
     rng = np.random.default_rng(block)
     vals = np.cumsum(rng.integers(-3, 1 << 20, size=40_000)).astype(np.int64)
-    run_both(decoder, [make(abi.INT64, vals, abi.DELTA_BINARY_PACKED, delta_block=block, delta_miniblocks=mb)])
+    if ptype == abi.INT32:
+        vals = vals.astype(np.int32)
+    run_both(decoder, [make(ptype, vals, abi.DELTA_BINARY_PACKED, delta_block=block, delta_miniblocks=mb)])
 
 
 # ---- error classification ----------------------------------------------------------------------------
