@@ -132,21 +132,26 @@ __device__ __forceinline__ int bin_value_error(rsrc_t rs, uint32_t p, uint32_t e
   return dict ? PQG_ERR_CORRUPT : PQG_ERR_EOF;     // slice past the end: EOFException (dictionary: CORRUPT)
 }
 
+// The window's accepted values are marked in the candidate list (bit 31 of pos) during the walk
+// and stored after it, once the next window's bytes have been requested: a load issued after
+// stores would wait for them (vmcnt counts stores), so every window costs one memory latency,
+// not two.
 __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, uint32_t N, uint32_t* out_len,
                          uint32_t* out_src, bool dict, int page, int kind, uint64_t* err, uint32_t* err_count) {
   const uint32_t lane = lane_id();
-  uint32_t pos = beg, produced = 0;
+  uint32_t pos = uni(beg), produced = 0;
   int code = 0;
+  u32x4 d4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((pos & ~3u) + 16u * lane), 0, 0);
+  uint32_t d5 = ld32(rs, (pos & ~3u) + 16u * lane + 16u);
   while (true) {
     pos = uni(pos);
     produced = uni(produced);
     if (produced >= N) break;
     if ((uint64_t)pos + 4u > end) { code = PQG_ERR_EOF; break; }
-    // ---- candidates of the window [B, B + BW_WIN)
+    // ---- candidates of the window [B, B + BW_WIN) (its bytes are in d4 / d5)
     const uint32_t B = pos & ~3u;
     const uint32_t base = B + 16u * lane;
-    const u32x4 d4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)base, 0, 0);
-    const uint32_t d[5] = {d4.x, d4.y, d4.z, d4.w, ld32(rs, base + 16u)};
+    const uint32_t d[5] = {d4.x, d4.y, d4.z, d4.w, d5};
     uint32_t m = 0;
     uint32_t nx[16];
 #pragma unroll
@@ -182,12 +187,12 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
     // chain is walked from lane 0 (the current value start) with one v_readlane per value;
     // false candidates (a length read from a shifted prefix, e.g. the byte before a small
     // length) are simply never reached.
-    uint32_t i0 = 0;
+    uint32_t i0 = 0, got = 0;
     bool leave = false;  // next position lies past the window
     while (true) {
       i0 = uni(i0);
+      got = uni(got);
       const uint32_t k = i0 + lane;
-      const uint32_t p = k < total ? L.pos[k] : 0xFFFFFFFFu;
       const uint32_t s = k < total ? L.nxt[k] : 0xFFFFFFFFu;
       const uint32_t so = s - B;
       const uint32_t t = so < BW_WIN ? L.idx[so] : 0xFFFFu;
@@ -201,14 +206,12 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
         j = rdl(J, j);
       }
       const uint32_t n_acc = (uint32_t)__builtin_popcountll(mask);
-      const uint32_t take = uni(n_acc < N - produced ? n_acc : N - produced);
+      const uint32_t room = N - produced - got;
+      const uint32_t take = uni(n_acc < room ? n_acc : room);
       const uint32_t rank = (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1ull));
-      if (((mask >> lane) & 1ull) && rank < take) {
-        gst(out_len + produced + rank, s - p - 4u);
-        gst(out_src + produced + rank, p + 4u);
-      }
-      produced += take;
-      if (produced >= N) break;
+      if (((mask >> lane) & 1ull) && rank < take) L.pos[k] |= 0x80000000u;  // accepted (k < total)
+      got += take;
+      if (take == room) break;
       const uint32_t cur = rdl(s, last);  // true successor of the last value of the batch
       pos = cur;
       if (cur >= B + BW_WIN) { leave = true; break; }
@@ -219,6 +222,28 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
       }
       i0 = a;
     }
+    // ---- request the next window, then store this window's values
+    if (leave) {
+      const uint32_t nb = (pos & ~3u) + 16u * lane;
+      d4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)nb, 0, 0);
+      d5 = ld32(rs, nb + 16u);
+    }
+    wave_sync();
+    got = uni(got);
+    for (uint32_t k0 = 0, done = 0; done < got; k0 += WAVE) {
+      const uint32_t k = k0 + lane;
+      const uint32_t pk = k < total ? L.pos[k] : 0u;
+      const bool acc = (pk >> 31) != 0;
+      const uint64_t am = __ballot(acc);
+      if (acc) {
+        const uint32_t o = produced + done + (uint32_t)__builtin_popcountll(am & ((1ull << lane) - 1ull));
+        const uint32_t p = pk & 0x7FFFFFFFu;
+        gst(out_len + o, L.nxt[k] - p - 4u);
+        gst(out_src + o, p + 4u);
+      }
+      done += (uint32_t)__builtin_popcountll(am);
+    }
+    produced += got;
     if (code || !leave) break;
     wave_sync();  // the next window overwrites the list
   }

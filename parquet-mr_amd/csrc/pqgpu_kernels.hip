@@ -1203,9 +1203,137 @@ struct LevelWaveLds {
 
 // Levels of the runs rs[0 .. n_run) covering slots [s_lo, s_hi) -> out (u8), 16 slots per lane
 // with 16-byte stores where the tile is inside [s_lo, s_hi); counts slots == max_def.
-__device__ __forceinline__ void expand_level_runs(const LevelWaveLds& L, rsrc_t rs, uint32_t n_run, uint32_t s_lo,
-                                                  uint32_t s_hi, int w, uint8_t* out, uint32_t max_def,
-                                                  bool count_nonnull, uint32_t& cnt) {
+// Packed bytes come from the wave's LDS segment of the page when it holds them (a global load
+// here would wait for the tile stores before it: vmcnt counts stores).
+// Byte mask of bytes [jb, je) (clamped to the tile) in dword i of a 16-byte tile.
+__device__ __forceinline__ uint32_t tile_byte_mask(int32_t jb, int32_t je, int32_t i) {
+  const int32_t lo = jb - 4 * i < 0 ? 0 : (jb - 4 * i > 4 ? 4 : jb - 4 * i);
+  const int32_t hi = je - 4 * i < 0 ? 0 : (je - 4 * i > 4 ? 4 : je - 4 * i);
+  const uint32_t mh = hi >= 4 ? 0xFFFFFFFFu : (1u << (8 * hi)) - 1u;
+  const uint32_t ml = lo >= 4 ? 0xFFFFFFFFu : (1u << (8 * lo)) - 1u;
+  return mh & ~ml;
+}
+
+// Bit width WB (1..8) specialisation of expand_level_runs: per tile piece (the part of one run
+// inside the lane's 16 slots) the 16 levels are formed without a per-slot loop: an RLE piece is
+// its value replicated, a packed piece is 24 bytes at the piece's bit offset, shifted once, then
+// 16 bit fields at compile-time positions; a byte mask merges the piece into the tile.
+template <int WB>
+__device__ __forceinline__ void expand_level_tiles(const LevelWaveLds& L, const PreWin& win, uint32_t n_run,
+                                                   uint32_t s_lo, uint32_t s_hi, uint8_t* out, uint32_t max_def,
+                                                   bool count_nonnull, uint32_t& cnt) {
+  const rsrc_t rs = win.rs;
+  const uint32_t lane = lane_id();
+  const int64_t mis = out ? (int64_t)((uintptr_t)out & 15u) : 0;
+  for (int64_t t = (((int64_t)s_lo + mis) & ~(int64_t)15) - mis; t < (int64_t)s_hi; t += 16 * WAVE) {
+    const int64_t s0 = t + 16 * (int64_t)lane;
+    if (s0 + 16 <= (int64_t)s_lo || s0 >= (int64_t)s_hi) continue;
+    const uint32_t lo_s = (uint32_t)(s0 > (int64_t)s_lo ? s0 : (int64_t)s_lo);
+    const uint32_t hi_s = (uint32_t)(s0 + 16 < (int64_t)s_hi ? s0 + 16 : (int64_t)s_hi);
+    uint32_t a = 0, b = n_run;
+    while (b - a > 1) {
+      const uint32_t mid = (a + b) >> 1;
+      if (L.r_start[mid] <= lo_s) a = mid;
+      else b = mid;
+    }
+    uint32_t acc[4] = {0u, 0u, 0u, 0u};
+    uint32_t cur = lo_s, k = a;
+    while (cur < hi_s) {
+      const uint32_t st = L.r_start[k], pay = L.r_pay[k];
+      const uint32_t re = k + 1 < n_run ? L.r_start[k + 1] : s_hi;
+      const uint32_t stop = hi_s < re ? hi_s : re;
+      const int32_t jb = (int32_t)(cur - (uint32_t)s0), je = (int32_t)(stop - (uint32_t)s0);
+      uint32_t v[4];
+      if (!(pay & 0x80000000u)) {
+        const uint32_t rep = pay * 0x01010101u;  // pay <= 255 (saturated)
+        v[0] = v[1] = v[2] = v[3] = rep;
+      } else {
+        // bit offset of tile slot 0 from the run's data start (negative when the run starts
+        // inside the tile: those slots are masked off below)
+        const uint32_t rlo = pay & 0x7FFFFFFFu, rhi = L.r_end[k];
+        const int64_t base = ((int64_t)cur - (int64_t)st - (int64_t)jb) * WB;
+        const int64_t byte0 = (int64_t)rlo + (base >> 3);
+        const uint32_t bsh = (uint32_t)(base & 7);
+        const int64_t a4 = byte0 & ~(int64_t)3;  // may be < 0 near the page start (masked slots only)
+        const uint32_t sb = (uint32_t)(byte0 & 3);
+        uint32_t y[6];
+        if (a4 >= 0 && seg_has(win, (uint32_t)a4, 24u)) {
+#pragma unroll
+          for (uint32_t c = 0; c < 6; c++) y[c] = seg32(win, (uint32_t)a4 + 4u * c);
+        } else {
+#pragma unroll
+          for (uint32_t c = 0; c < 6; c++) y[c] = a4 + 4 * (int64_t)c >= 0 ? ld32(rs, (uint32_t)(a4 + 4 * (int64_t)c)) : 0u;
+        }
+        // bytes at or past the run's read end are 0 (readNext :96-99: truncated final group)
+#pragma unroll
+        for (uint32_t c = 0; c < 6; c++) {
+          const int64_t kp = (int64_t)rhi - (a4 + 4 * (int64_t)c);
+          y[c] &= kp >= 4 ? 0xFFFFFFFFu : (kp <= 0 ? 0u : (1u << (8 * kp)) - 1u);
+        }
+        uint32_t z[5], D[5];
+#pragma unroll
+        for (uint32_t c = 0; c < 5; c++) z[c] = __builtin_amdgcn_alignbyte(y[c + 1], y[c], sb);
+#pragma unroll
+        for (uint32_t c = 0; c < 4; c++) D[c] = __builtin_amdgcn_alignbit(z[c + 1], z[c], bsh);
+        D[4] = z[4] >> bsh;
+        v[0] = v[1] = v[2] = v[3] = 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < 16; q++) {
+          constexpr uint32_t M = (1u << WB) - 1u;
+          const uint32_t bp = q * WB, wi = bp >> 5, bo = bp & 31u;
+          const uint32_t f = (bo + WB <= 32u ? (D[wi] >> bo) : __builtin_amdgcn_alignbit(D[wi + 1], D[wi], bo)) & M;
+          v[q >> 2] |= f << (8u * (q & 3u));
+        }
+      }
+#pragma unroll
+      for (int32_t c = 0; c < 4; c++) {
+        const uint32_t m = tile_byte_mask(jb, je, c);
+        acc[c] = (acc[c] & ~m) | (v[c] & m);
+      }
+      cur = stop;
+      k++;
+    }
+    const int32_t j0 = (int32_t)(lo_s - (uint32_t)s0), j1 = (int32_t)(hi_s - (uint32_t)s0);
+    if (count_nonnull) {
+      // bytes == max_def inside [j0, j1): zero bytes of acc ^ max_def (per-byte test, no carries)
+      const uint32_t rep = max_def * 0x01010101u;
+#pragma unroll
+      for (int32_t c = 0; c < 4; c++) {
+        const uint32_t y = acc[c] ^ rep;
+        const uint32_t nz = ((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y;  // bit 7 of a byte: byte != 0
+        cnt += (uint32_t)__builtin_popcount(~nz & 0x80808080u & tile_byte_mask(j0, j1, c));
+      }
+    }
+    if (out) {
+      uint8_t* o = out + s0;
+      if (j0 == 0 && j1 == 16) {
+        gst((u32x4*)o, u32x4{acc[0], acc[1], acc[2], acc[3]});
+      } else {
+#pragma unroll
+        for (int32_t j = 0; j < 16; j++)
+          if (j >= j0 && j < j1) gst(o + j, (uint8_t)(acc[j >> 2] >> (8 * (j & 3))));
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void expand_level_runs_generic(const LevelWaveLds& L, const PreWin& win, uint32_t n_run,
+                                                          uint32_t s_lo, uint32_t s_hi, int w, uint8_t* out,
+                                                          uint32_t max_def, bool count_nonnull, uint32_t& cnt);
+
+// WB = 1..4: the specialised tile expansion; WB = 0: any width.
+template <int WB>
+__device__ __forceinline__ void expand_level_runs(const LevelWaveLds& L, const PreWin& win, uint32_t n_run,
+                                                  uint32_t s_lo, uint32_t s_hi, int w, uint8_t* out,
+                                                  uint32_t max_def, bool count_nonnull, uint32_t& cnt) {
+  if constexpr (WB > 0) expand_level_tiles<WB>(L, win, n_run, s_lo, s_hi, out, max_def, count_nonnull, cnt);
+  else expand_level_runs_generic(L, win, n_run, s_lo, s_hi, w, out, max_def, count_nonnull, cnt);
+}
+
+__device__ __forceinline__ void expand_level_runs_generic(const LevelWaveLds& L, const PreWin& win, uint32_t n_run,
+                                                          uint32_t s_lo, uint32_t s_hi, int w, uint8_t* out,
+                                                          uint32_t max_def, bool count_nonnull, uint32_t& cnt) {
+  const rsrc_t rs = win.rs;
   const uint32_t lane = lane_id();
   const int64_t mis = out ? (int64_t)((uintptr_t)out & 15u) : 0;
   const uint32_t wmask = w >= 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
@@ -1238,10 +1366,19 @@ __device__ __forceinline__ void expand_level_runs(const LevelWaveLds& L, rsrc_t 
         const uint64_t bit0 = (uint64_t)(cur - st) * (uint32_t)w;
         const uint32_t a0 = rlo + (uint32_t)(bit0 >> 3);
         uint64_t x[3];
+        const bool in_seg = seg_has(win, a0 & ~3u, 28u);
+        uint32_t dw[7];
+        if (in_seg) {
+#pragma unroll
+          for (uint32_t c = 0; c < 7; c++) dw[c] = seg32(win, (a0 & ~3u) + 4u * c);
+        }
 #pragma unroll
         for (uint32_t c = 0; c < 3; c++) {
           const uint32_t ac = a0 + 8u * c;
-          const uint64_t v = ld8_any(rs, ac);
+          const uint32_t sb = a0 & 3u;
+          const uint64_t v = in_seg ? ((uint64_t)__builtin_amdgcn_alignbyte(dw[2 * c + 1], dw[2 * c], sb) |
+                                       ((uint64_t)__builtin_amdgcn_alignbyte(dw[2 * c + 2], dw[2 * c + 1], sb) << 32))
+                                    : ld8_any(rs, ac);
           const int64_t keep = (int64_t)rhi - (int64_t)ac;  // bytes past the run's read end are 0 (:96-99)
           x[c] = keep >= 8 ? v : (keep <= 0 ? 0 : (v & ((1ull << (8 * keep)) - 1ull)));
         }
@@ -1282,7 +1419,8 @@ __device__ __forceinline__ void expand_level_runs(const LevelWaveLds& L, rsrc_t 
 // every byte position pre-decoded as a run header, 8 rounds of pointer doubling mark the chain),
 // the window's runs in an LDS table, then tile expansion of the slots they cover.
 // Returns the slots decoded before an error (N when none) and sets *err_code.
-__device__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs, uint32_t beg, uint32_t end, int w, uint32_t N,
+template <int WB>
+__device__ __forceinline__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs, uint32_t beg, uint32_t end, int w, uint32_t N,
                                      uint8_t* out, uint32_t max_def, bool count_nonnull, uint32_t* nonnull,
                                      int* err_code) {
   const uint32_t lane = lane_id();
@@ -1406,7 +1544,7 @@ __device__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs, uint32_t beg, u
       }
     }
     wave_sync();
-    if (n_em) expand_level_runs(L, rs, n_em, produced, produced + total, w, out, max_def, count_nonnull, cnt);
+    if (n_em) expand_level_runs<WB>(L, win, n_em, produced, produced + total, w, out, max_def, count_nonnull, cnt);
     produced += total;
     if (produced >= N) break;
     const uint32_t ql = q_last >> 2, qb = q_last & 3u;
@@ -1436,7 +1574,7 @@ __device__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs, uint32_t beg, u
         L.r_end[0] = rd_end;
       }
       wave_sync();
-      expand_level_runs(L, rs, 1, produced, produced + take, w, out, max_def, count_nonnull, cnt);
+      expand_level_runs<WB>(L, win, 1, produced, produced + take, w, out, max_def, count_nonnull, cnt);
       produced += take;
       pos = rd_end;
     }
@@ -1565,6 +1703,19 @@ __device__ uint32_t decode_levels(rsrc_t rs, uint32_t beg, uint32_t end, int w, 
   return done;
 }
 
+// decode_levels_pj with the tile expansion specialised for the section's bit width.
+__device__ __forceinline__ uint32_t decode_levels_w(LevelWaveLds& L, rsrc_t rs, uint32_t beg, uint32_t end, int w,
+                                                    uint32_t N, uint8_t* out, uint32_t max_def, bool count_nonnull,
+                                                    uint32_t* nonnull, int* err_code) {
+  switch (w) {
+    case 1: return decode_levels_pj<1>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
+    case 2: return decode_levels_pj<2>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
+    case 3: return decode_levels_pj<3>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
+    case 4: return decode_levels_pj<4>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
+    default: return decode_levels_pj<0>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
+  }
+}
+
 __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                 PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                 const int32_t* __restrict__ list, int n_list, uint64_t* err,
@@ -1645,7 +1796,7 @@ __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__
   uint64_t lvl_err_key = ~0ull;
   if (wr > 0) {
     uint32_t done = rl_be ? decode_levels_be(win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code)
-                          : decode_levels_pj(LL, win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code);
+                          : decode_levels_w(LL, win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code);
     if (code) {
       limit = done;
       lvl_err_key = ((uint64_t)done << 1) << 8 | (uint64_t)code;
@@ -1658,7 +1809,7 @@ __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__
     int code2 = 0;
     uint32_t done = dl_be ? decode_levels_be(win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true,
                                              &nonnull, &code2)
-                          : decode_levels_pj(LL, win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true,
+                          : decode_levels_w(LL, win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true,
                                              &nonnull, &code2);
     if (code2) {
       uint64_t key = (((uint64_t)done << 1) | 1ull) << 8 | (uint64_t)code2;

@@ -286,6 +286,27 @@ def test_host_path_roundtrip(decoder):
 
 
 
+@pytest.mark.parametrize("max_def", [1, 2, 5, 12, 20, 40])
+@pytest.mark.parametrize("shape", ["random", "runs"])
+@pytest.mark.parametrize("version", [1, 2])
+def test_rle_level_widths(decoder, max_def, shape, version):
+    """RLE / bit-packed hybrid definition levels of bit widths 1..6 (the level expansion is
+    specialised per width up to 4), random (mostly bit-packed) and run-heavy (mostly RLE with
+    short bit-packed stretches) sequences."""
+    rng = np.random.default_rng(max_def * 7 + version)
+    n = 50_000
+    if shape == "random":
+        dl = rng.integers(0, max_def + 1, size=n)
+    else:
+        runs = rng.integers(1, 40, size=n // 8)
+        dl = np.repeat(rng.integers(0, max_def + 1, size=runs.size), runs)[:n]
+        n = dl.size
+    dl = dl.astype(np.uint8)
+    vals = rng.integers(-2**40, 2**40, size=int((dl == max_def).sum())).astype(np.int64)
+    ch = make(abi.INT64, vals, abi.PLAIN, def_levels=dl, max_def=max_def, version=version, page_rows=6007)
+    run_both(decoder, [ch])
+
+
 @pytest.mark.parametrize("max_def,max_rep", [(1, 0), (2, 0), (3, 1), (7, 0)])
 def test_v1_bit_packed_levels(decoder, max_def, max_rep):
     """Deprecated BIT_PACKED (big-endian) level sections of old parquet-mr V1 pages
