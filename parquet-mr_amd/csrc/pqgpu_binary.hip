@@ -119,8 +119,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
 constexpr uint32_t BW_WIN = 1024;  // window bytes (16 positions per lane)
 
 struct BinWalkLds {
-  uint32_t pos[BW_WIN];   // candidate positions, ascending
-  uint32_t nxt[BW_WIN];   // their successors (p + 4 + len)
+  uint2 pn[BW_WIN];       // candidate positions (ascending; bit 31: accepted) and successors (p + 4 + len)
   uint16_t idx[BW_WIN];   // window offset -> candidate index (valid where pos[idx] matches)
 };
 
@@ -136,49 +135,52 @@ __device__ __forceinline__ int bin_value_error(rsrc_t rs, uint32_t p, uint32_t e
 // and stored after it, once the next window's bytes have been requested: a load issued after
 // stores would wait for them (vmcnt counts stores), so every window costs one memory latency,
 // not two.
-__device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, uint32_t N, uint32_t* out_len,
+__device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, uint32_t N, uint32_t* out_len,
                          uint32_t* out_src, bool dict, int page, int kind, uint64_t* err, uint32_t* err_count) {
   const uint32_t lane = lane_id();
   uint32_t pos = uni(beg), produced = 0;
   int code = 0;
-  u32x4 d4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((pos & ~3u) + 16u * lane), 0, 0);
-  uint32_t d5 = ld32(rs, (pos & ~3u) + 16u * lane + 16u);
+  // fixed 1 KiB tiles of the page; the tile after the current one is always in flight
+  uint32_t B = pos & ~(BW_WIN - 1u);
+  u32x4 d4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(B + 16u * lane), 0, 0);
+  uint32_t d5 = ld32(rs, B + 16u * lane + 16u);
+  u32x4 n4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(B + BW_WIN + 16u * lane), 0, 0);
+  uint32_t n5 = ld32(rs, B + BW_WIN + 16u * lane + 16u);
   while (true) {
     pos = uni(pos);
     produced = uni(produced);
+    B = uni(B);
     if (produced >= N) break;
     if ((uint64_t)pos + 4u > end) { code = PQG_ERR_EOF; break; }
-    // ---- candidates of the window [B, B + BW_WIN) (its bytes are in d4 / d5)
-    const uint32_t B = pos & ~3u;
+    // ---- candidates of the tile [B, B + BW_WIN) holding pos (its bytes are in d4 / d5)
     const uint32_t base = B + 16u * lane;
     const uint32_t d[5] = {d4.x, d4.y, d4.z, d4.w, d5};
     uint32_t m = 0;
     uint32_t nx[16];
+    // 32-bit test (pages < 2 GiB): 0 <= len <= end - (p + 4), i.e. rem = end - 4 - p >= 0 and
+    // len <= rem as unsigned (a negative len is >= 2^31 > rem)
+    const int32_t rem0 = (int32_t)(end - 4u - base);
 #pragma unroll
     for (uint32_t q = 0; q < 16; q++) {
-      const uint32_t p = base + q;
       const uint32_t len = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
-      const uint64_t e = (uint64_t)p + 4u + len;
-      const bool c = p >= pos && (int32_t)len >= 0 && e <= end;
-      nx[q] = (uint32_t)e;
+      const int32_t rem = rem0 - (int32_t)q;
+      const bool c = rem >= 0 && len <= (uint32_t)rem;
+      nx[q] = base + q + 4u + len;
       m |= (c ? 1u : 0u) << q;
     }
+    if (base < pos) m &= pos - base >= 16u ? 0u : ~((1u << (pos - base)) - 1u);
     uint32_t total;
     const uint32_t rank = wave_excl_scan_u32((uint32_t)__builtin_popcount(m), &total);
-    {
-      uint32_t r = rank;
 #pragma unroll
-      for (uint32_t q = 0; q < 16; q++)
-        if ((m >> q) & 1u) {
-          L.pos[r] = base + q;
-          L.nxt[r] = nx[q];
-          L.idx[16u * lane + q] = (uint16_t)r;
-          r++;
-        }
-    }
+    for (uint32_t q = 0; q < 16; q++)
+      if ((m >> q) & 1u) {
+        const uint32_t r = rank + (uint32_t)__builtin_popcount(m & ((1u << q) - 1u));
+        *(uint64_t*)&L.pn[r] = (uint64_t)(base + q) | ((uint64_t)nx[q] << 32);
+        L.idx[16u * lane + q] = (uint16_t)r;
+      }
     wave_sync();
     total = uni(total);
-    if (total == 0 || L.pos[0] != pos) {  // the current position cannot hold a value
+    if (total == 0 || L.pn[0].x != pos) {  // the current position cannot hold a value
       code = bin_value_error(rs, pos, end, dict);
       break;
     }
@@ -193,10 +195,10 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
       i0 = uni(i0);
       got = uni(got);
       const uint32_t k = i0 + lane;
-      const uint32_t s = k < total ? L.nxt[k] : 0xFFFFFFFFu;
+      const uint32_t s = k < total ? L.pn[k].y : 0xFFFFFFFFu;
       const uint32_t so = s - B;
       const uint32_t t = so < BW_WIN ? L.idx[so] : 0xFFFFu;
-      const bool hit = t < total && t > k && t - i0 < WAVE && L.pos[t < total ? t : 0] == s;
+      const bool hit = t < total && t > k && t - i0 < WAVE && L.pn[t < total ? t : 0].x == s;
       const uint32_t J = hit ? t - i0 : WAVE;
       uint64_t mask = 0;
       uint32_t j = 0, last = 0;
@@ -209,36 +211,45 @@ __device__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, u
       const uint32_t room = N - produced - got;
       const uint32_t take = uni(n_acc < room ? n_acc : room);
       const uint32_t rank = (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1ull));
-      if (((mask >> lane) & 1ull) && rank < take) L.pos[k] |= 0x80000000u;  // accepted (k < total)
+      if (((mask >> lane) & 1ull) && rank < take) L.pn[k].x |= 0x80000000u;  // accepted (k < total)
       got += take;
       if (take == room) break;
       const uint32_t cur = rdl(s, last);  // true successor of the last value of the batch
       pos = cur;
       if (cur >= B + BW_WIN) { leave = true; break; }
       const uint32_t a = uni((uint32_t)L.idx[cur - B]);
-      if (a >= total || L.pos[a] != cur || a <= i0 + last) {  // every position of the window was tested
+      if (a >= total || L.pn[a].x != cur || a <= i0 + last) {  // every position of the window was tested
         code = bin_value_error(rs, cur, end, dict);
         break;
       }
       i0 = a;
     }
-    // ---- request the next window, then store this window's values
+    // ---- advance to the tile holding the next value (requesting the one after it), then
+    // store this tile's values
     if (leave) {
-      const uint32_t nb = (pos & ~3u) + 16u * lane;
-      d4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)nb, 0, 0);
-      d5 = ld32(rs, nb + 16u);
+      const uint32_t nB = pos & ~(BW_WIN - 1u);
+      if (nB == B + BW_WIN) {
+        d4 = n4;
+        d5 = n5;
+      } else {  // a value longer than a tile: the prefetch missed
+        d4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(nB + 16u * lane), 0, 0);
+        d5 = ld32(rs, nB + 16u * lane + 16u);
+      }
+      n4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(nB + BW_WIN + 16u * lane), 0, 0);
+      n5 = ld32(rs, nB + BW_WIN + 16u * lane + 16u);
+      B = nB;
     }
     wave_sync();
     got = uni(got);
     for (uint32_t k0 = 0, done = 0; done < got; k0 += WAVE) {
       const uint32_t k = k0 + lane;
-      const uint32_t pk = k < total ? L.pos[k] : 0u;
-      const bool acc = (pk >> 31) != 0;
+      const uint2 e = k < total ? L.pn[k] : uint2{0u, 0u};
+      const bool acc = (e.x >> 31) != 0;
       const uint64_t am = __ballot(acc);
       if (acc) {
         const uint32_t o = produced + done + (uint32_t)__builtin_popcountll(am & ((1ull << lane) - 1ull));
-        const uint32_t p = pk & 0x7FFFFFFFu;
-        gst(out_len + o, L.nxt[k] - p - 4u);
+        const uint32_t p = e.x & 0x7FFFFFFFu;
+        gst(out_len + o, e.y - p - 4u);
         gst(out_src + o, p + 4u);
       }
       done += (uint32_t)__builtin_popcountll(am);
