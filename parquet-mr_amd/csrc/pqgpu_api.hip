@@ -118,11 +118,15 @@ struct pqg_plan {
   uint32_t chunk_off[N_DICT_CLS] = {0, 0, 0}, chunk_n[N_DICT_CLS] = {0, 0, 0};  // ranges in `chunks`
   // BYTE_ARRAY / fixed-width-dictionary scratch (ColumnDev::blen, bsrc, dict_len, dict_src, block_sums,
   // bin_total), dictionary walks, post-passes, offset-scan blocks, copy chunks
-  DevBuf bscratch, bin_lists, bin_blocks, bin_chunks;
+  DevBuf bscratch, bin_lists, bin_blocks, bin_chunks, dba_chunks;
   uint64_t blen_bytes = 0;            // leading part of bscratch cleared before every launch
   int n_dict_walk = 0, n_bind = 0, n_fixd = 0, n_bin_cols = 0;
   int off_dict_walk = 0, off_bind = 0, off_fixd = 0, off_bin_cols = 0;  // into bin_lists
-  uint32_t n_bin_blocks = 0, n_bin_chunks = 0;
+  uint32_t n_bin_blocks = 0, n_bin_chunks = 0, n_dba_chunks = 0;
+  uint64_t dba_meta_off = ~0ull;  // DELTA_BYTE_ARRAY per-chunk {suffix base, smallest prefix} in bscratch
+  uint32_t* dba_meta() const {
+    return dba_meta_off == ~0ull ? nullptr : (uint32_t*)((uint8_t*)bscratch.p + dba_meta_off);
+  }
   std::vector<uint64_t> bin_total_off;  // per column: byte offset of its bin_total in bscratch (or ~0)
   std::vector<uint64_t> bin_capacity;
   std::vector<int> col_first_page;
@@ -434,6 +438,17 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
       const uint32_t nch = (w.num_slots + pqg::BIN_CHUNK - 1) / pqg::BIN_CHUNK;
       for (uint32_t j = 0; j < nch; j++) bin_chunks.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
     }
+  // ---- DELTA_BYTE_ARRAY pages: BIN_CHUNK-value chunks (upper bound from the slot count)
+  std::vector<uint64_t> dba_chunks;
+  for (int p : cls_lists[C_DBA]) {
+    PageWork& w = P->h_work[(size_t)p];
+    w.chunk_base = (uint32_t)dba_chunks.size();
+    w.reserved = 0;
+    const uint32_t nch = (w.num_slots + pqg::BIN_CHUNK - 1) / pqg::BIN_CHUNK;
+    for (uint32_t j = 0; j < nch; j++) dba_chunks.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
+  }
+  if (!dba_chunks.empty()) P->dba_meta_off = take(8 * dba_chunks.size());
+  P->n_dba_chunks = (uint32_t)dba_chunks.size();
   // ---- dictionary pages: run-record capacity (a run covers >= 1 value and its header takes
   // >= 1 byte) and output chunks (slots [j*CH, (j+1)*CH) of the page, upper bound from the slot count)
   std::vector<uint64_t> chunk_list;
@@ -493,6 +508,7 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
             P->bin_lists.ensure(sizeof(int32_t) * std::max<size_t>(bl.size(), 1)) == hipSuccess &&
             P->bin_blocks.ensure(sizeof(uint64_t) * std::max<size_t>(bin_blocks.size(), 1)) == hipSuccess &&
             P->bin_chunks.ensure(sizeof(uint64_t) * std::max<size_t>(bin_chunks.size(), 1)) == hipSuccess &&
+            P->dba_chunks.ensure(sizeof(uint64_t) * std::max<size_t>(dba_chunks.size(), 1)) == hipSuccess &&
 
             P->rec.ensure(sizeof(uint64_t) * (rec_total + 16)) == hipSuccess &&  // k_dict_fill reads 9 ahead
             P->chunk_run.ensure(sizeof(uint32_t) * std::max<uint32_t>(chunk_total, 1)) == hipSuccess &&
@@ -524,6 +540,8 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     ok = ok && hipMemcpyAsync(P->bin_blocks.p, bin_blocks.data(), sizeof(uint64_t) * bin_blocks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   if (!bin_chunks.empty())
     ok = ok && hipMemcpyAsync(P->bin_chunks.p, bin_chunks.data(), sizeof(uint64_t) * bin_chunks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!dba_chunks.empty())
+    ok = ok && hipMemcpyAsync(P->dba_chunks.p, dba_chunks.data(), sizeof(uint64_t) * dba_chunks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   if (!chunk_list.empty())
     ok = ok && hipMemcpyAsync(P->chunks.p, chunk_list.data(), sizeof(uint64_t) * chunk_list.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   ok = ok && hipMemcpyAsync(P->work.p, P->h_work.data(), sizeof(PageWork) * P->h_work.size(), hipMemcpyHostToDevice, s) == hipSuccess;
@@ -541,7 +559,7 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
   P->kernels = (P->levels_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
   for (int k = 0; k < C_NCLS; k++) P->kernels += P->cls_n[(size_t)k] ? 1 : 0;
   P->kernels += (P->n_dict_walk ? 1 : 0) + (P->n_bind ? 1 : 0) + (P->n_fixd ? 1 : 0) + (P->n_bin_blocks ? 3 : 0) +
-                (P->n_bin_chunks ? 1 : 0);
+                (P->n_bin_chunks ? 1 : 0) + (P->cls_n[C_DBA] ? (P->n_dba_chunks ? 4 : 1) : 0);
   *out = P;
   return PQG_OK;
 }
@@ -605,7 +623,9 @@ int pqg_plan_launch(pqg_plan* P) {
         e = pqg::launch_bin_walk(s, P->d_bytes, P->n_bytes, work, cols, l, n, 0, P->n_pages, err, ecount);
         break;
       case C_DLBA: e = pqg::launch_dlba_lengths(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
-      case C_DBA: e = pqg::launch_dba_lengths(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_DBA:
+        e = pqg::launch_dba_lengths(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount, P->dba_meta());
+        break;
       case C_PLAIN: e = pqg::launch_plain(0, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_BOOL: e = pqg::launch_plain(1, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_DELTA4: e = pqg::launch_delta(4, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
@@ -623,7 +643,8 @@ int pqg_plan_launch(pqg_plan* P) {
     e = pqg::launch_bin_copy(s, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->bin_chunks.p, P->n_bin_chunks,
                              err, ecount);
   if (e == hipSuccess && P->cls_n[C_DBA])
-    e = pqg::launch_dba_copy(s, P->d_bytes, P->n_bytes, work, cols, lists + P->cls_off[C_DBA], P->cls_n[C_DBA]);
+    e = pqg::launch_dba_copy(s, P->d_bytes, P->n_bytes, work, cols, lists + P->cls_off[C_DBA], P->cls_n[C_DBA],
+                             (const uint64_t*)P->dba_chunks.p, P->n_dba_chunks, P->dba_meta());
   ctx->last_launched = P;
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }
@@ -650,6 +671,7 @@ int pqg_plan_destroy(pqg_plan* P) {
   P->bin_lists.release();
   P->bin_blocks.release();
   P->bin_chunks.release();
+  P->dba_chunks.release();
   delete P;
   return PQG_OK;
 }

@@ -559,43 +559,39 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
 
 // ---------------------------------------------------------------------------
 // DELTA_BYTE_ARRAY values (DeltaByteArrayReader.readBytes :57-79): value i = the first prefix_i
-// bytes of value i - 1, then suffix i. The dependency is serial across values, so one wave walks
-// a page's values in order with the previous value in LDS: per batch of 64 values the suffix
-// bytes are staged into LDS in one coalesced pass, then each value is assembled byte-parallel
-// (prefix from the previous value's LDS copy, suffix from the staging buffer) and stored. k_delta
-// MODE 2 left bsrc = prefix length, blen = value length (0 from the first invalid value on; the
-// errors are reported there) and PageWork::aux = start of the suffix bytes. A value longer than
-// the LDS buffer takes its prefix from the previous value's output in global memory.
-constexpr uint32_t DBA_VB = 2048;  // LDS bytes per value buffer (previous / current)
+// bytes of value i - 1, then suffix i. k_delta MODE 2 left bsrc = prefix length, blen = value
+// length (0 from the first invalid value on; the errors are reported there), PageWork::aux = start
+// of the suffix bytes and, per chunk of BIN_CHUNK values, {suffix bytes before the chunk, smallest
+// prefix length m_c in the chunk} (dba_meta).
+//
+// The dependency is serial across values, but only through the LAST value of each chunk: value
+// i of chunk c needs nothing from before the chunk except the chunk's previous value, i.e. the
+// last value T_{c-1} of chunk c - 1, and T_c = the first m_c bytes of T_{c-1}, then bytes that
+// come from chunk c's own suffixes. So:
+//   k_dba_tail    (one wave per chunk)  writes the own bytes [m_c, |T_c|) of T_c into the output:
+//                 value y of the chunk supplies bytes [P_y, min P_{y+1..last}) (suffix minimum);
+//   k_dba_chain   (one wave per page)   follows T_0, T_1, ... with T in LDS and writes the
+//                 inherited bytes [0, m_c) of every T_c: one short step per chunk;
+//   k_dba_chunks  (one wave per chunk)  with T_{c-1} read back as the previous value, assembles
+//                 the chunk's values one after another (LDS, byte-parallel per value).
+// A page with a value longer than DBA_VB (PageWork::reserved, set by k_delta) is copied by
+// k_dba_copy, the same per-value loop over the whole page with long previous values read back
+// from the output.
 constexpr uint32_t DBA_SB = 4096;  // LDS suffix staging bytes per batch
 
-__global__ __launch_bounds__(64 * WPB) void k_dba_copy(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                                       const PageWork* __restrict__ work,
-                                                       const ColumnDev* __restrict__ cols,
-                                                       const int32_t* __restrict__ list, int n_list) {
-  __shared__ uint8_t vbuf_all[WPB][2][DBA_VB];
-  __shared__ uint32_t sbuf_all[WPB][DBA_SB / 4 + 1];
-  const int page = wave_page(list, n_list);
-  if (page < 0) return;
-  const PageWork& pw = work[page];
-  const ColumnDev& cd = cols[pw.column];
+// Values [i_beg, i_end) of a page, in order. The previous value is in vbuf[cur ^ 1] when
+// prev_lds; otherwise at output offset prev_off. sp: page-relative position of value i_beg's suffix.
+__device__ __forceinline__ void dba_values(const ColumnDev& cd, uint64_t v0, rsrc_t rs, uint32_t i_beg, uint32_t i_end,
+                                           uint32_t sp, uint8_t (*vbuf)[DBA_VB], uint32_t* sbuf, uint32_t cur,
+                                           bool prev_lds, uint64_t prev_off) {
   const uint32_t lane = lane_id();
-  const uint32_t N = uni(pw.n_values);
-  const uint64_t v0 = pw.out_offset;
   const int64_t* offs = (const int64_t*)cd.values + v0;
   uint8_t* dst = cd.binary_data;
   const uint64_t cap = cd.binary_capacity;
-  const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
-  uint8_t(*vbuf)[DBA_VB] = vbuf_all[wave_id()];
-  uint32_t* sbuf = sbuf_all[wave_id()];
   const uint8_t* sb8 = (const uint8_t*)sbuf;
-  uint32_t sp = uni(pw.aux);  // next suffix byte (page-relative)
-  uint32_t cur = 0;
-  bool prev_lds = true;       // the previous value is in vbuf[cur ^ 1]
-  uint64_t prev_off = 0;      // its output offset
-  for (uint32_t i0 = 0; i0 < N; i0 += WAVE) {
+  for (uint32_t i0 = i_beg; i0 < i_end; i0 += WAVE) {
     const uint32_t i = i0 + lane;
-    const bool in = i < N;
+    const bool in = i < i_end;
     const uint32_t L = in ? cd.blen[v0 + i] : 0u;
     uint32_t P = in ? cd.bsrc[v0 + i] : 0u;
     P = P < L ? P : L;
@@ -608,7 +604,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_copy(const uint8_t* __restrict
       for (uint32_t o = 4u * lane; o < stot; o += 4u * WAVE) sbuf[o >> 2] = ld4_any(rs, sp + o);
       wave_sync();
     }
-    const uint32_t nb = N - i0 < WAVE ? N - i0 : WAVE;
+    const uint32_t nb = i_end - i0 < WAVE ? i_end - i0 : WAVE;
     for (uint32_t t = 0; t < nb; t++) {
       const uint32_t len = rdl(L, t), pre = rdl(P, t), so = rdl(sx, t);
       const uint64_t o = ((uint64_t)rdl((uint32_t)(off >> 32), t) << 32) | rdl((uint32_t)off, t);
@@ -643,6 +639,201 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_copy(const uint8_t* __restrict
     sp += stot;
     wave_sync();  // the next batch overwrites the staging buffer
   }
+}
+
+// Serial copy of the pages with a value longer than DBA_VB (PageWork::reserved).
+__global__ __launch_bounds__(64 * WPB) void k_dba_copy(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                       const PageWork* __restrict__ work,
+                                                       const ColumnDev* __restrict__ cols,
+                                                       const int32_t* __restrict__ list, int n_list) {
+  __shared__ uint8_t vbuf_all[WPB][2][DBA_VB];
+  __shared__ uint32_t sbuf_all[WPB][DBA_SB / 4 + 1];
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
+  const PageWork& pw = work[page];
+  if (!uni(pw.reserved)) return;
+  const ColumnDev& cd = cols[pw.column];
+  const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  dba_values(cd, pw.out_offset, rs, 0, uni(pw.n_values), uni(pw.aux), vbuf_all[wave_id()], sbuf_all[wave_id()], 0,
+             true, 0);
+}
+
+// Chunk (page, j) of the chunk list -> its value range; false when the chunk holds no value or
+// its page takes the serial copy.
+__device__ __forceinline__ bool dba_chunk(const PageWork* work, const uint64_t* chunks, uint32_t c, int& page,
+                                          uint32_t& j, uint32_t& i_lo, uint32_t& i_hi) {
+  const uint64_t ch = chunks[c];
+  page = (int)(uint32_t)ch;
+  j = (uint32_t)(ch >> 32);
+  const PageWork& pw = work[page];
+  const uint32_t nv = uni(pw.n_values);
+  i_lo = j * BIN_CHUNK;
+  if (uni(pw.reserved) || i_lo >= nv) return false;
+  i_hi = i_lo + BIN_CHUNK < nv ? i_lo + BIN_CHUNK : nv;
+  return true;
+}
+
+// Own bytes of the chunk's last value: value y supplies bytes [P_y, R_y), R_y = min(P_{y+1..last})
+// (R_last = its length); those intervals tile [m_c, L_last).
+__global__ __launch_bounds__(64 * WPB) void k_dba_tail(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                       const PageWork* __restrict__ work,
+                                                       const ColumnDev* __restrict__ cols,
+                                                       const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                       const uint32_t* __restrict__ meta) {
+  const uint32_t c = blockIdx.x * WPB + wave_id();
+  if (c >= n_chunks) return;
+  int page;
+  uint32_t j, i_lo, i_hi;
+  if (!dba_chunk(work, chunks, c, page, j, i_lo, i_hi)) return;
+  const PageWork& pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint64_t v0 = pw.out_offset;
+  const uint32_t n = i_hi - i_lo;
+  // lane holds values y = 4 * lane + q of the chunk
+  uint32_t Lq[4], Pq[4], Sq[4], s_lane = 0, m_lane = 0xFFFFFFFFu;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    const uint32_t y = 4u * lane + q;
+    const bool in = y < n;
+    Lq[q] = in ? cd.blen[v0 + i_lo + y] : 0u;
+    const uint32_t p = in ? cd.bsrc[v0 + i_lo + y] : 0u;
+    Pq[q] = in ? (p < Lq[q] ? p : Lq[q]) : 0xFFFFFFFFu;
+    Sq[q] = in ? Lq[q] - Pq[q] : 0u;
+    s_lane += Sq[q];
+  }
+  const uint32_t last = n - 1;
+  const uint32_t L_last = uni(cd.blen[v0 + i_lo + last]);
+  if (L_last == 0) return;
+  uint32_t stot;
+  const uint32_t sx_lane = wave_excl_scan_u32(s_lane, &stot);
+  // suffix minimum of P over the following values: within the lane, then over the later lanes
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) m_lane = Pq[q] < m_lane ? Pq[q] : m_lane;
+  uint32_t after = 0xFFFFFFFFu;  // min over lanes > this lane
+  {
+    uint32_t x = m_lane;  // inclusive suffix min over lanes >= this one
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_down(x, o);
+      if ((int)lane + o < 64) x = y < x ? y : x;
+    }
+    after = __shfl_down(x, 1);
+    if (lane == 63) after = 0xFFFFFFFFu;
+  }
+  const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  const uint32_t sp = uni(pw.aux) + meta[2u * ((uint64_t)pw.chunk_base + j)];
+  const int64_t* offs = (const int64_t*)cd.values + v0;
+  const uint64_t o_last = (uint64_t)offs[i_lo + last];
+  uint8_t* dst = cd.binary_data;
+  const uint64_t cap = cd.binary_capacity;
+  uint32_t R = after, sx = sx_lane;
+  uint32_t sxq[4];
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) { sxq[q] = sx; sx += Sq[q]; }
+#pragma unroll
+  for (int q = 3; q >= 0; q--) {
+    const uint32_t y = 4u * lane + (uint32_t)q;
+    if (y < n) {
+      const uint32_t hi = y == last ? L_last : (R < Lq[q] ? R : Lq[q]);
+      for (uint32_t b = Pq[q]; b < hi; b++) {
+        const uint32_t a = sp + sxq[q] + (b - Pq[q]);
+        const uint32_t v = (ld32(rs, a & ~3u) >> ((a & 3u) * 8u)) & 0xFFu;
+        if (o_last + b < cap) gst(dst + o_last + b, (uint8_t)v);
+      }
+    }
+    R = Pq[q] < R ? Pq[q] : R;
+  }
+}
+
+// Inherited bytes of every chunk's last value, chunk after chunk of one page: T_c[0, m_c) =
+// T_{c-1}[0, m_c), with T kept in LDS (the own bytes come from k_dba_tail's output).
+__global__ __launch_bounds__(64 * WPB) void k_dba_chain(const PageWork* __restrict__ work,
+                                                        const ColumnDev* __restrict__ cols,
+                                                        const int32_t* __restrict__ list, int n_list,
+                                                        const uint32_t* __restrict__ meta) {
+  __shared__ uint8_t tbuf_all[WPB][DBA_VB];
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
+  const PageWork& pw = work[page];
+  if (uni(pw.reserved)) return;
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint32_t nv = uni(pw.n_values);
+  const uint32_t nch = (nv + BIN_CHUNK - 1) / BIN_CHUNK;
+  if (nch <= 1) return;
+  const uint64_t v0 = pw.out_offset;
+  const int64_t* offs = (const int64_t*)cd.values + v0;
+  uint8_t* dst = cd.binary_data;
+  const uint64_t cap = cd.binary_capacity;
+  uint8_t* T = tbuf_all[wave_id()];
+  const uint32_t* m = meta + 2u * (uint64_t)pw.chunk_base;
+  // T_0 = chunk 0's last value (all own bytes: its first value has prefix 0)
+  uint32_t tl = uni(cd.blen[v0 + BIN_CHUNK - 1]);
+  {
+    const uint64_t o = (uint64_t)offs[BIN_CHUNK - 1];
+    for (uint32_t b = lane; b < tl; b += WAVE) T[b] = o + b < cap ? dst[o + b] : 0;
+  }
+  wave_sync();
+  for (uint32_t c = 1; c < nch; c++) {
+    const uint32_t il = (c + 1) * BIN_CHUNK < nv ? (c + 1) * BIN_CHUNK - 1 : nv - 1;
+    const uint32_t Ll = uni(cd.blen[v0 + il]);
+    const uint32_t mc = uni(m[2u * c + 1u]);
+    const uint64_t o = (uint64_t)offs[il];
+    const uint32_t k = mc < Ll ? mc : Ll;  // inherited bytes (<= |T_{c-1}| for a valid page)
+    // own bytes [k, Ll) were written by k_dba_tail (an earlier launch): load them first
+    uint8_t own[DBA_VB / WAVE];
+#pragma unroll
+    for (uint32_t r = 0; r < DBA_VB / WAVE; r++) {
+      const uint32_t b = lane + r * WAVE;
+      own[r] = (b >= k && b < Ll && o + b < cap) ? dst[o + b] : 0;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < DBA_VB / WAVE; r++) {
+      const uint32_t b = lane + r * WAVE;
+      if (b < k && o + b < cap) gst(dst + o + b, T[b]);
+    }
+    wave_sync();
+#pragma unroll
+    for (uint32_t r = 0; r < DBA_VB / WAVE; r++) {
+      const uint32_t b = lane + r * WAVE;
+      if (b >= k && b < Ll) T[b] = own[r];
+    }
+    wave_sync();
+    tl = Ll;
+  }
+  (void)tl;
+}
+
+// The chunk's values in order, the previous value being T_{c-1} (complete in the output after
+// k_dba_tail and k_dba_chain).
+__global__ __launch_bounds__(64 * WPB) void k_dba_chunks(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                         const PageWork* __restrict__ work,
+                                                         const ColumnDev* __restrict__ cols,
+                                                         const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                         const uint32_t* __restrict__ meta) {
+  __shared__ uint8_t vbuf_all[WPB][2][DBA_VB];
+  __shared__ uint32_t sbuf_all[WPB][DBA_SB / 4 + 1];
+  const uint32_t c = blockIdx.x * WPB + wave_id();
+  if (c >= n_chunks) return;
+  int page;
+  uint32_t j, i_lo, i_hi;
+  if (!dba_chunk(work, chunks, c, page, j, i_lo, i_hi)) return;
+  const PageWork& pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint64_t v0 = pw.out_offset;
+  uint8_t(*vbuf)[DBA_VB] = vbuf_all[wave_id()];
+  if (i_lo) {  // previous value -> vbuf[1]
+    const int64_t* offs = (const int64_t*)cd.values + v0;
+    const uint32_t lp = uni(cd.blen[v0 + i_lo - 1]);
+    const uint64_t o = (uint64_t)offs[i_lo - 1];
+    for (uint32_t b = lane; b < lp; b += WAVE) vbuf[1][b] = o + b < cd.binary_capacity ? cd.binary_data[o + b] : 0;
+    wave_sync();
+  }
+  const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  const uint32_t sp = uni(pw.aux) + meta[2u * ((uint64_t)pw.chunk_base + j)];
+  dba_values(cd, v0, rs, i_lo, i_hi, uni(sp), vbuf, sbuf_all[wave_id()], 0, true, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -690,8 +881,15 @@ hipError_t launch_bin_scan(hipStream_t st, const ColumnDev* cols, const int32_t*
 }
 
 hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                           const ColumnDev* cols, const int32_t* list, int n) {
+                           const ColumnDev* cols, const int32_t* list, int n, const uint64_t* chunks,
+                           uint32_t n_chunks, const uint32_t* dba_meta) {
   if (n <= 0) return hipSuccess;
+  if (n_chunks) {
+    const dim3 gc((n_chunks + WPB - 1) / WPB);
+    hipLaunchKernelGGL(k_dba_tail, gc, dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, chunks, n_chunks, dba_meta);
+    hipLaunchKernelGGL(k_dba_chain, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, work, cols, list, n, dba_meta);
+    hipLaunchKernelGGL(k_dba_chunks, gc, dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, chunks, n_chunks, dba_meta);
+  }
   hipLaunchKernelGGL(k_dba_copy, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, list, n);
   return hipGetLastError();
 }

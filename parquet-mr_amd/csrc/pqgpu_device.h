@@ -91,6 +91,16 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t x) {
   return x;
 }
 
+// Minimum over the wave (u32), in every lane.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t y = __shfl_xor(v, o);
+    v = v < y ? v : y;
+  }
+  return v;
+}
+
 // Maximum over the wave (u32), in every lane.
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll

@@ -89,11 +89,18 @@ hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
 // DELTA_LENGTH_BYTE_ARRAY lengths (k_delta into blen, records PageWork::aux)
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
-// DELTA_BYTE_ARRAY prefix / suffix lengths (k_delta MODE 2: bsrc = prefix, blen = value length, aux)
+// DELTA_BYTE_ARRAY prefix / suffix lengths (k_delta MODE 2: bsrc = prefix, blen = value length, aux;
+// dba_meta: per BIN_CHUNK-value chunk {suffix bytes before it, smallest prefix in it};
+// PageWork::reserved = 1 when a value is longer than DBA_VB: that page takes the serial copy)
+constexpr uint32_t DBA_VB = 2048;  // LDS bytes of one value buffer of the DELTA_BYTE_ARRAY copy
 hipError_t launch_dba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                              const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+                              const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count,
+                              uint32_t* dba_meta);
+// DELTA_BYTE_ARRAY value bytes: chunk tails, per-page chain of chunk tails, chunk copies, serial
+// copy of the pages with long values
 hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                           const ColumnDev* cols, const int32_t* list, int n);
+                           const ColumnDev* cols, const int32_t* list, int n, const uint64_t* chunks,
+                           uint32_t n_chunks, const uint32_t* dba_meta);
 // pqgpu_binary.hip
 constexpr uint32_t BIN_CHUNK = 256;     // values per k_bin_copy chunk
 constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block

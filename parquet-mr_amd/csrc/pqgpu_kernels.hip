@@ -2258,7 +2258,7 @@ template <int W, int MODE = 0>
 __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                               PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                               const int32_t* __restrict__ list, int n_list, uint64_t* err,
-                                              uint32_t* err_count) {
+                                              uint32_t* err_count, uint32_t* __restrict__ dba_meta = nullptr) {
   typedef typename DictVal<W>::T T;
   __shared__ __attribute__((aligned(16))) uint8_t dseg_all[WPB][DSEG];
   const int page = wave_page(list, n_list);
@@ -2300,6 +2300,10 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
     uint64_t s_carry = 0;
     uint32_t prev_len = 0;  // previous value of the page (empty before the first, :41)
     uint32_t first_bad = 0xFFFFFFFFu;
+    // per BIN_CHUNK-value chunk of the page, for the chunk-parallel value copy (k_dba_tail /
+    // k_dba_chain / k_dba_chunks): suffix bytes before the chunk, smallest prefix length in it
+    uint32_t* meta = dba_meta + 2u * (uint64_t)pw.chunk_base;
+    uint32_t cmin = 0xFFFFFFFFu, lmax = 0;
     // the lengths were just stored by this wave: wait for them, then read past the L1 (a line
     // shared with a neighbouring page may sit in this CU's L1 from before those stores)
     __builtin_amdgcn_s_waitcnt(0);
@@ -2328,10 +2332,30 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
       const uint64_t bad = __ballot(c != 0);
       if (bad && first_bad == 0xFFFFFFFFu) first_bad = i0 + (uint32_t)__builtin_ctzll(bad);
       const uint32_t fb = uni(first_bad);
-      if (in) gst(sl + i, (c || i >= fb) ? 0u : (uint32_t)full);
+      const uint32_t Lf = (c || i >= fb) ? 0u : (uint32_t)full;
+      if (in) gst(sl + i, Lf);
+      if ((i0 % BIN_CHUNK) == 0 && lane == 0) gst(meta + 2u * (i0 / BIN_CHUNK), (uint32_t)s_carry);
+      {
+        const uint32_t pf = !in ? 0xFFFFFFFFu : (Lf ? (uint32_t)pre : 0u);  // the copy's prefix: min(prefix, length)
+        const uint32_t mn = wave_min_u32(pf), mx = wave_max_u32(in ? Lf : 0u);
+        cmin = mn < cmin ? mn : cmin;
+        lmax = mx > lmax ? mx : lmax;
+      }
+      if (((i0 + WAVE) % BIN_CHUNK) == 0 || i0 + WAVE >= n_chk) {
+        if (lane == 0) gst(meta + 2u * (i0 / BIN_CHUNK) + 1u, cmin);
+        cmin = 0xFFFFFFFFu;
+      }
       prev_len = rdl((uint32_t)(full < 0 ? 0 : full), WAVE - 1);
       s_carry += rdl((uint32_t)incl, WAVE - 1) | ((uint64_t)rdl((uint32_t)(incl >> 32), WAVE - 1) << 32);
     }
+    // chunks past the checked values hold no bytes
+    const uint32_t nch = (uint32_t)(((uint64_t)pw.num_slots + BIN_CHUNK - 1) / BIN_CHUNK);
+    for (uint32_t j = (n_chk + BIN_CHUNK - 1) / BIN_CHUNK + lane; j < nch; j += WAVE) {
+      gst(meta + 2u * j, (uint32_t)s_carry);
+      gst(meta + 2u * j + 1u, 0u);
+    }
+    // a value longer than the LDS value buffers sends the page to the serial copy
+    if (lane == 0) work[page].reserved = lmax > DBA_VB ? 1u : 0u;
     // values past an error or past the streams hold length 0 (blen was cleared before the launch)
   }
   if (past_end != 0xFFFFFFFFu && lane == 0) report(err, err_count, page, 2, past_end, PQG_ERR_DELTA_PAST_END);
@@ -2468,9 +2492,10 @@ hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_
 }
 
 hipError_t launch_dba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                              const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+                              const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count,
+                              uint32_t* dba_meta) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL((k_delta<4, 2>), dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
+  hipLaunchKernelGGL((k_delta<4, 2>), dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS, dba_meta);
   return hipGetLastError();
 }
 

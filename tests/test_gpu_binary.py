@@ -1,6 +1,8 @@
 """GPU parity for BYTE_ARRAY (PLAIN, dictionary, DELTA_LENGTH_BYTE_ARRAY), BYTE_STREAM_SPLIT and
 FIXED_LEN_BYTE_ARRAY / INT96 dictionaries: libpqgpu.so through the C ABI vs the oracle, bit-exact
 (values, offsets, levels, first error)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -200,3 +202,25 @@ def _dba_err(which):
 @pytest.mark.parametrize("which", ["prefix_too_long", "suffix_short", "negative_suffix", "prefix_stream_short"])
 def test_delta_byte_array_errors(decoder, which):
     run_both(decoder, [_dba_err(which)], expect_error=True)
+
+
+def test_delta_byte_array_mixed_pages(decoder):
+    """One chunk of pages whose values stay under the 2 KiB LDS value buffer (chunk-parallel copy:
+    tails, chain of chunk tails, chunks) next to pages with longer values (serial copy)."""
+    short = [b"x" * (i % 1900) + bytes([97 + i % 26]) for i in range(3000)]
+    grow = [b"y" * min(i * 3, 2600) for i in range(1200)]
+    run_both(decoder, [make(abi.BYTE_ARRAY, short + grow + short, abi.DELTA_BYTE_ARRAY, page_rows=1700)])
+
+
+@pytest.mark.parametrize("at", [300, 1000, 1279])
+def test_delta_byte_array_error_mid_page(decoder, at):
+    """An invalid prefix length (longer than the previous value) inside a page of several
+    256-value chunks: values before it decode, the error is reported at its index."""
+    from pqgpu import writer as W
+    vals = _dba_vals("urls", 1280, 9)
+    pre = [0] + [len(os.path.commonprefix([vals[i - 1], vals[i]])) for i in range(1, len(vals))]
+    pre[at] = len(vals[at - 1]) + 5
+    suf = [v[min(p, len(v)):] for v, p in zip(vals, pre)]
+    ch = make(abi.BYTE_ARRAY, vals, abi.DELTA_BYTE_ARRAY)
+    ch.pages[0].body = W.delta_encode(np.array(pre, dtype=np.int32), abi.INT32) + W.dlba_encode(suf)
+    run_both(decoder, [ch], expect_error=True)
