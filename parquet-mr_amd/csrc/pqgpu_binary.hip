@@ -578,12 +578,25 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
 // k_dba_copy, the same per-value loop over the whole page with long previous values read back
 // from the output.
 constexpr uint32_t DBA_SB = 4096;  // LDS suffix staging bytes per batch
+constexpr uint32_t DBA_OB = 4096;  // LDS output bytes of a byte-parallel batch
+
+// LDS of the byte-parallel batch (k_dba_chunks): the batch's values are assembled in obuf, lane
+// k writing value k as segments: its suffix [P_k, L_k), then [P_y, P_prev) from the suffix of
+// y = the previous value with a strictly smaller prefix length (the bytes every value between
+// them inherits unchanged), and so on down to prefix 0 or, past the batch start, the previous
+// batch's last value.
+struct DbaPar {
+  uint8_t obuf_raw[16 + DBA_OB + 32];  // obuf = obuf_raw + 16 (slack for unaligned dword reads)
+  uint32_t pmin[6][WAVE];              // pmin[s][x] = min prefix length over values (x - 2^s, x]
+  uint32_t sx[WAVE];                   // suffix offset of value x in the staging buffer
+  uint8_t pse[WAVE];                   // previous value with a smaller prefix length (255: none)
+};
 
 // Values [i_beg, i_end) of a page, in order. The previous value is in vbuf[cur ^ 1] when
 // prev_lds; otherwise at output offset prev_off. sp: page-relative position of value i_beg's suffix.
 __device__ __forceinline__ void dba_values(const ColumnDev& cd, uint64_t v0, rsrc_t rs, uint32_t i_beg, uint32_t i_end,
                                            uint32_t sp, uint8_t (*vbuf)[DBA_VB], uint32_t* sbuf, uint32_t cur,
-                                           bool prev_lds, uint64_t prev_off) {
+                                           bool prev_lds, uint64_t prev_off, DbaPar* par = nullptr) {
   const uint32_t lane = lane_id();
   const int64_t* offs = (const int64_t*)cd.values + v0;
   uint8_t* dst = cd.binary_data;
@@ -604,7 +617,89 @@ __device__ __forceinline__ void dba_values(const ColumnDev& cd, uint64_t v0, rsr
       for (uint32_t o = 4u * lane; o < stot; o += 4u * WAVE) sbuf[o >> 2] = ld4_any(rs, sp + o);
       wave_sync();
     }
+    // the batch's loads are complete before the value loop: otherwise the compiler cannot tell
+    // at the loop head whether `off` has arrived and waits with vmcnt(0) — for every store of
+    // the previous value — once per value
+    __builtin_amdgcn_s_waitcnt(0);
     const uint32_t nb = i_end - i0 < WAVE ? i_end - i0 : WAVE;
+    if (par && staged && prev_lds) {
+      const uint32_t lmax = uni(wave_max_u32(L));
+      uint32_t ltot;
+      const uint32_t lx = wave_excl_scan_u32(L, &ltot);
+      ltot = uni(ltot);
+      if (lmax <= DBA_VB && ltot <= DBA_OB) {
+        uint32_t mv = in ? P : 0xFFFFFFFFu;
+#pragma unroll
+        for (uint32_t st = 0; st < 6; st++) {
+          if (st) {
+            const uint32_t y = __shfl_up(mv, 1u << (st - 1));
+            if (lane >= (1u << (st - 1))) mv = y < mv ? y : mv;
+          }
+          par->pmin[st][lane] = mv;
+        }
+        par->sx[lane] = sx;
+        wave_sync();
+        uint32_t ps = 255u;
+        if (in && P > 0) {  // max{y < lane : P_y <= P - 1}
+          int y = (int)lane - 1;
+          const uint32_t th = P - 1u;
+#pragma unroll
+          for (int st = 5; st >= 0; st--)
+            if (y >= (1 << st) - 1 && par->pmin[st][y] > th) y -= 1 << st;
+          ps = y < 0 ? 255u : (uint32_t)y;
+        }
+        par->pse[lane] = (uint8_t)ps;
+        wave_sync();
+        uint8_t* obuf = par->obuf_raw + 16;
+        const uint8_t* prevb = vbuf[cur ^ 1];
+        if (in) {
+          uint8_t* ob = obuf + lx;
+          uint32_t y = lane, hi = L, lo = P, sxy = sx;
+          while (true) {
+            for (uint32_t b = lo; b < hi; b++) ob[b] = sb8[sxy + (b - lo)];  // suffix of y
+            if (lo == 0) break;
+            hi = lo;
+            y = par->pse[y];
+            if (y == 255u) {  // inherited from before the batch
+              for (uint32_t b = 0; b < hi; b++) ob[b] = prevb[b];
+              break;
+            }
+            lo = par->pmin[0][y];
+            sxy = par->sx[y];
+          }
+        }
+        wave_sync();
+        // the batch's bytes -> output, 16-byte blocks (edges shared with the neighbouring
+        // batches / chunks are stored bytewise)
+        const uint64_t o_lo = ((uint64_t)rdl((uint32_t)(off >> 32), 0) << 32) | rdl((uint32_t)off, 0);
+        const uint64_t o_end = o_lo + ltot;
+        const uint64_t o_hi = o_end < cap ? o_end : cap;
+        const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
+        typedef uint32_t __attribute__((may_alias)) u32a;
+        for (uint64_t a = (o_lo & ~15ull) + 16u * lane; a < o_hi; a += 16u * WAVE) {
+          const int32_t rel = (int32_t)(int64_t)(a - o_lo);  // >= -15
+          const int32_t rb = rel & ~3;
+          const uint32_t sb = (uint32_t)rel & 3u;
+          uint32_t w[5], wd[4], have = 0;
+#pragma unroll
+          for (uint32_t c = 0; c < 5; c++) w[c] = *(const u32a*)(obuf + rb + 4 * (int32_t)c);
+#pragma unroll
+          for (uint32_t c = 0; c < 4; c++) {
+            wd[c] = __builtin_amdgcn_alignbyte(w[c + 1], w[c], sb);
+            const uint64_t d0 = a + 4u * c;
+            if (d0 >= o_lo && d0 + 4u <= o_hi) have |= 1u << c;
+          }
+          store_block16(dst, a, o_lo, o_hi, wd, dst_al4 ? have : 0u, dst_al16);
+        }
+        // the batch's last value becomes the previous value
+        const uint32_t ll = rdl(L, nb - 1), lxl = rdl(lx, nb - 1);
+        for (uint32_t b = lane; b < ll; b += WAVE) vbuf[cur][b] = obuf[lxl + b];
+        cur ^= 1;
+        sp += stot;
+        wave_sync();  // the next batch overwrites the staging buffers
+        continue;
+      }
+    }
     for (uint32_t t = 0; t < nb; t++) {
       const uint32_t len = rdl(L, t), pre = rdl(P, t), so = rdl(sx, t);
       const uint64_t o = ((uint64_t)rdl((uint32_t)(off >> 32), t) << 32) | rdl((uint32_t)off, t);
@@ -814,6 +909,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chunks(const uint8_t* __restri
                                                          const uint32_t* __restrict__ meta) {
   __shared__ uint8_t vbuf_all[WPB][2][DBA_VB];
   __shared__ uint32_t sbuf_all[WPB][DBA_SB / 4 + 1];
+  __shared__ __attribute__((aligned(16))) DbaPar par_all[WPB];
   const uint32_t c = blockIdx.x * WPB + wave_id();
   if (c >= n_chunks) return;
   int page;
@@ -833,7 +929,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chunks(const uint8_t* __restri
   }
   const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
   const uint32_t sp = uni(pw.aux) + meta[2u * ((uint64_t)pw.chunk_base + j)];
-  dba_values(cd, v0, rs, i_lo, i_hi, uni(sp), vbuf, sbuf_all[wave_id()], 0, true, 0);
+  dba_values(cd, v0, rs, i_lo, i_hi, uni(sp), vbuf, sbuf_all[wave_id()], 0, true, 0, &par_all[wave_id()]);
 }
 
 // ---------------------------------------------------------------------------
