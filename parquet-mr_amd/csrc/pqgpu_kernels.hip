@@ -2307,18 +2307,28 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
     // the lengths were just stored by this wave: wait for them, then read past the L1 (a line
     // shared with a neighbouring page may sit in this CU's L1 from before those stores)
     __builtin_amdgcn_s_waitcnt(0);
-    for (uint32_t i0 = 0; i0 < n_chk; i0 += WAVE) {
+    // DG batches of lengths are loaded before the stores of any of them (a load issued after
+    // stores waits for them: one drain per DG batches, not per batch)
+    constexpr uint32_t DG = 8;
+    for (uint32_t g0 = 0; g0 < n_chk; g0 += DG * WAVE) {
+    int32_t pre_g[DG], suf_g[DG];
+#pragma unroll
+    for (uint32_t q = 0; q < DG; q++) {
+      const uint32_t i = g0 + q * WAVE + lane;
+      pre_g[q] = i < n_chk ? (int32_t)sld(pl + i) : 0;
+      suf_g[q] = i < n_chk ? (int32_t)sld(sl + i) : 0;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+    for (uint32_t q = 0; q < DG; q++) {
+      const uint32_t i0 = g0 + q * WAVE;
+      if (i0 >= n_chk) break;
       const uint32_t i = i0 + lane;
       const bool in = i < n_chk;
-      const int32_t pre = in ? (int32_t)sld(pl + i) : 0;
-      const int32_t suf = in ? (int32_t)sld(sl + i) : 0;
+      const int32_t pre = pre_g[q];
+      const int32_t suf = suf_g[q];
       const uint64_t sv = suf > 0 ? (uint64_t)suf : 0;
-      uint64_t incl = sv;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(incl, o);
-        if ((int)lane >= o) incl += y;
-      }
+      const uint64_t incl = wave_incl_scan_u64(sv);
       const int32_t full = (int32_t)((uint32_t)pre + (uint32_t)suf);
       uint32_t prev = __shfl_up((uint32_t)(full < 0 ? 0 : full), 1);
       if (lane == 0) prev = prev_len;
@@ -2347,6 +2357,7 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
       }
       prev_len = rdl((uint32_t)(full < 0 ? 0 : full), WAVE - 1);
       s_carry += rdl((uint32_t)incl, WAVE - 1) | ((uint64_t)rdl((uint32_t)(incl >> 32), WAVE - 1) << 32);
+    }
     }
     // chunks past the checked values hold no bytes
     const uint32_t nch = (uint32_t)(((uint64_t)pw.num_slots + BIN_CHUNK - 1) / BIN_CHUNK);
