@@ -118,9 +118,12 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
 // false candidate that sits between two true ones.
 constexpr uint32_t BW_WIN = 1024;  // window bytes (16 positions per lane)
 
+constexpr uint32_t BW_CAP = 256;   // candidates per pass over a tile (more: the tile is taken in parts)
+
 struct BinWalkLds {
-  uint2 pn[BW_WIN];       // candidate positions (ascending; bit 31: accepted) and successors (p + 4 + len)
+  uint2 pn[BW_CAP];       // candidate positions (ascending; bit 31: accepted) and successors (p + 4 + len)
   uint16_t idx[BW_WIN];   // window offset -> candidate index (valid where pos[idx] matches)
+  uint32_t cut;           // position of candidate BW_CAP (the end of this pass) when there are more
 };
 
 // Error of a value whose length prefix starts at p (not a candidate).
@@ -175,11 +178,18 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
     for (uint32_t q = 0; q < 16; q++)
       if ((m >> q) & 1u) {
         const uint32_t r = rank + (uint32_t)__builtin_popcount(m & ((1u << q) - 1u));
-        *(uint64_t*)&L.pn[r] = (uint64_t)(base + q) | ((uint64_t)nx[q] << 32);
-        L.idx[16u * lane + q] = (uint16_t)r;
+        if (r < BW_CAP) {
+          *(uint64_t*)&L.pn[r] = (uint64_t)(base + q) | ((uint64_t)nx[q] << 32);
+          L.idx[16u * lane + q] = (uint16_t)r;
+        } else if (r == BW_CAP) {
+          L.cut = base + q;
+        }
       }
     wave_sync();
     total = uni(total);
+    // this pass covers [pos, eff_end): the whole tile, or up to the first candidate past the cap
+    const uint32_t eff_end = total > BW_CAP ? uni(L.cut) : B + BW_WIN;
+    if (total > BW_CAP) total = BW_CAP;
     if (total == 0 || L.pn[0].x != pos) {  // the current position cannot hold a value
       code = bin_value_error(rs, pos, end, dict);
       break;
@@ -216,7 +226,7 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
       if (take == room) break;
       const uint32_t cur = rdl(s, last);  // true successor of the last value of the batch
       pos = cur;
-      if (cur >= B + BW_WIN) { leave = true; break; }
+      if (cur >= eff_end) { leave = true; break; }
       const uint32_t a = uni((uint32_t)L.idx[cur - B]);
       if (a >= total || L.pn[a].x != cur || a <= i0 + last) {  // every position of the window was tested
         code = bin_value_error(rs, cur, end, dict);
@@ -226,8 +236,10 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
     }
     // ---- advance to the tile holding the next value (requesting the one after it), then
     // store this tile's values
-    if (leave) {
-      const uint32_t nB = pos & ~(BW_WIN - 1u);
+    // (nB == B: the rest of the same tile after a pass cut at BW_CAP candidates; its bytes are
+    // still in d4 / d5)
+    const uint32_t nB = pos & ~(BW_WIN - 1u);
+    if (leave && nB != B) {
       if (nB == B + BW_WIN) {
         d4 = n4;
         d5 = n5;
