@@ -91,6 +91,15 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t x) {
   return x;
 }
 
+// Mask of bytes [jb, je) (clamped) within dword i of a 16-byte block.
+__device__ __forceinline__ uint32_t block_byte_mask(int32_t jb, int32_t je, int32_t i) {
+  const int32_t lo = jb - 4 * i < 0 ? 0 : (jb - 4 * i > 4 ? 4 : jb - 4 * i);
+  const int32_t hi = je - 4 * i < 0 ? 0 : (je - 4 * i > 4 ? 4 : je - 4 * i);
+  const uint32_t mh = hi >= 4 ? 0xFFFFFFFFu : (1u << (8 * hi)) - 1u;
+  const uint32_t ml = lo >= 4 ? 0xFFFFFFFFu : (1u << (8 * lo)) - 1u;
+  return mh & ~ml;
+}
+
 // Minimum over the wave (u32), in every lane.
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
