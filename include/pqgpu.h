@@ -258,6 +258,28 @@ typedef struct pqg_assembly_node {
 int pqg_assemble(pqg_ctx* ctx, const uint8_t* d_def_levels, const uint8_t* d_rep_levels, uint64_t n_slots,
                  pqg_assembly_node* path, int depth, uint64_t* n_records, pqg_status* st);
 
+/* ---- page decompression (codec SNAPPY) --------------------------------------
+ * Replaces the decompression step between the page reader and the value readers:
+ * ColumnChunkPageReadStore.readPage (parquet-hadoop/src/main/java/org/apache/parquet/hadoop/ColumnChunkPageReadStore.java:144-172
+ * for V1 pages, :218-247 for the data section of compressed V2 pages) calling
+ * BytesInputDecompressor.decompress -> SnappyDecompressor (parquet-hadoop/.../hadoop/codec/SnappyDecompressor.java),
+ * i.e. xerial Snappy.uncompress of one raw Snappy block into a buffer of the header's
+ * uncompressed size. Job j decompresses d_src[src_offset, src_offset + src_size) into
+ * d_dst[dst_offset, dst_offset + dst_size); a block whose length varint differs from dst_size
+ * or that is malformed fails with PQG_ERR_CORRUPT. d_jobs is a DEVICE array; d_status (device,
+ * n_jobs int32, may be NULL) receives each job's code. Asynchronous on the context's stream;
+ * pqg_snappy_sync reports the first failing job (st->page = job index). */
+typedef struct pqg_snappy_job {
+  uint64_t src_offset;
+  uint64_t dst_offset;
+  uint32_t src_size;
+  uint32_t dst_size;
+} pqg_snappy_job;
+
+int pqg_snappy_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, uint8_t* d_dst, uint64_t dst_bytes,
+                          const pqg_snappy_job* d_jobs, int n_jobs, int32_t* d_status);
+int pqg_snappy_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_status* st);
+
 /* Human-readable name of an error code. */
 const char* pqg_error_name(int code);
 

@@ -910,3 +910,72 @@ const char* pqg_error_name_ref(int code) {
     default: return "UNKNOWN";
   }
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Snappy raw block decompression (ORACLE). parquet-mr decompresses a SNAPPY page with
+ * SnappyDecompressor.decompress (parquet-hadoop/.../hadoop/codec/SnappyDecompressor.java), which
+ * calls Snappy.uncompress of xerial snappy-java (a third-party library absent here, pinned in
+ * parquet-mr's pom as org.xerial.snappy:snappy-java); the page is decompressed into a buffer of
+ * the header's uncompressed size (ColumnChunkPageReadStore.java:150-172 V1, :223-247 V2 data
+ * section). This restates the published Snappy block format (google/snappy
+ * format_description.txt): varint uncompressed length, then elements — literal (tag & 3 == 0,
+ * length - 1 in the tag or 1..4 following bytes), copy with 1-, 2- or 4-byte offset — where a
+ * copy may overlap its own output (byte-at-a-time semantics). Returns 0 and *out_len, or
+ * PQG_ERR_CORRUPT for malformed input or a length different from `expect`.
+ * ------------------------------------------------------------------------------------------ */
+int pqr_snappy_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expect, int64_t* out_len) {
+  int64_t p = 0;
+  uint64_t ulen = 0;
+  int shift = 0;
+  for (;;) {
+    if (p >= n || shift > 28) return PQG_ERR_CORRUPT;
+    uint8_t b = src[p++];
+    ulen |= (uint64_t)(b & 0x7F) << shift;
+    if (!(b & 0x80)) break;
+    shift += 7;
+  }
+  if (ulen > 0xFFFFFFFFull || (int64_t)ulen != expect) return PQG_ERR_CORRUPT;
+  int64_t op = 0;
+  while (op < (int64_t)ulen) {
+    if (p >= n) return PQG_ERR_CORRUPT;
+    const uint8_t tag = src[p++];
+    if ((tag & 3) == 0) {
+      int64_t len = tag >> 2;
+      if (len >= 60) {
+        const int nb = (int)len - 59;
+        if (p + nb > n) return PQG_ERR_CORRUPT;
+        len = 0;
+        for (int i = 0; i < nb; i++) len |= (int64_t)src[p + i] << (8 * i);
+        p += nb;
+      }
+      len += 1;
+      if (p + len > n || op + len > (int64_t)ulen) return PQG_ERR_CORRUPT;
+      memcpy(dst + op, src + p, (size_t)len);
+      p += len;
+      op += len;
+    } else {
+      int64_t len, off;
+      if ((tag & 3) == 1) {
+        if (p + 1 > n) return PQG_ERR_CORRUPT;
+        len = 4 + ((tag >> 2) & 7);
+        off = ((int64_t)(tag >> 5) << 8) | src[p];
+        p += 1;
+      } else if ((tag & 3) == 2) {
+        if (p + 2 > n) return PQG_ERR_CORRUPT;
+        len = 1 + (tag >> 2);
+        off = (int64_t)src[p] | ((int64_t)src[p + 1] << 8);
+        p += 2;
+      } else {
+        if (p + 4 > n) return PQG_ERR_CORRUPT;
+        len = 1 + (tag >> 2);
+        off = (int64_t)src[p] | ((int64_t)src[p + 1] << 8) | ((int64_t)src[p + 2] << 16) | ((int64_t)src[p + 3] << 24);
+        p += 4;
+      }
+      if (off == 0 || off > op || op + len > (int64_t)ulen) return PQG_ERR_CORRUPT;
+      for (int64_t i = 0; i < len; i++) dst[op + i] = dst[op - off + i];
+      op += len;
+    }
+  }
+  *out_len = op;
+  return 0;
+}

@@ -40,6 +40,8 @@ def lib():
         L.pqr_router_read_batch.argtypes = [C.c_int, vp, i64, C.c_int, vp]
         L.pqr_router_read_batch.restype = i64
         L.pqr_delta_decode.argtypes = [vp, i64, vp, i64, C.POINTER(i64)]
+        L.pqr_snappy_decompress.argtypes = [vp, i64, vp, i64, C.POINTER(i64)]
+        L.pqr_snappy_decompress.restype = C.c_int
         L.pqr_delta_decode.restype = i64
         L.pqr_decode.argtypes = [vp, C.c_uint64, vp, C.c_int, vp, C.c_int, vp, C.POINTER(abi.Status)]
         L.pqr_decode.restype = C.c_int
@@ -172,3 +174,15 @@ def _decode_batch(batch, binary_capacity):
         res["rep_levels"] = rl[:batch.column_slots[i]].copy() if cd["max_rep"] > 0 else None
         out.append(res)
     return OracleResult(rc, st.as_tuple(), out, counts[:batch.n_pages].copy())
+
+
+def snappy_decompress(data, uncompressed_size):
+    """Snappy raw block -> bytes (ORACLE; pqr_snappy_decompress). Raises ValueError with the
+    error code on malformed input or a length different from uncompressed_size."""
+    src = np.frombuffer(bytes(data), dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    out = np.zeros(max(int(uncompressed_size), 1), dtype=np.uint8)
+    n = C.c_int64(0)
+    rc = lib().pqr_snappy_decompress(src.ctypes.data, len(data), out.ctypes.data, int(uncompressed_size), C.byref(n))
+    if rc:
+        raise ValueError(f"snappy: error {rc}")
+    return out[:n.value].tobytes()

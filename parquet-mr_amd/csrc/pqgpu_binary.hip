@@ -159,7 +159,6 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
     const uint32_t base = B + 16u * lane;
     const uint32_t d[5] = {d4.x, d4.y, d4.z, d4.w, d5};
     uint32_t m = 0;
-    uint32_t nx[16];
     // 32-bit test (pages < 2 GiB): 0 <= len <= end - (p + 4), i.e. rem = end - 4 - p >= 0 and
     // len <= rem as unsigned (a negative len is >= 2^31 > rem)
     const int32_t rem0 = (int32_t)(end - 4u - base);
@@ -168,7 +167,6 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
       const uint32_t len = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
       const int32_t rem = rem0 - (int32_t)q;
       const bool c = rem >= 0 && len <= (uint32_t)rem;
-      nx[q] = base + q + 4u + len;
       m |= (c ? 1u : 0u) << q;
     }
     if (base < pos) m &= pos - base >= 16u ? 0u : ~((1u << (pos - base)) - 1u);
@@ -179,7 +177,8 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
       if ((m >> q) & 1u) {
         const uint32_t r = rank + (uint32_t)__builtin_popcount(m & ((1u << q) - 1u));
         if (r < BW_CAP) {
-          *(uint64_t*)&L.pn[r] = (uint64_t)(base + q) | ((uint64_t)nx[q] << 32);
+          const uint32_t nx = base + q + 4u + __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
+          *(uint64_t*)&L.pn[r] = (uint64_t)(base + q) | ((uint64_t)nx << 32);
           L.idx[16u * lane + q] = (uint16_t)r;
         } else if (r == BW_CAP) {
           L.cut = base + q;

@@ -89,6 +89,9 @@ hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
 // DELTA_LENGTH_BYTE_ARRAY lengths (k_delta into blen, records PageWork::aux)
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+// pqgpu_snappy.hip: one wave per raw Snappy block (jobs: pqg_snappy_job, device array)
+hipError_t launch_snappy(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
+                         const void* jobs, int n_jobs, int32_t* status);
 // DELTA_BYTE_ARRAY prefix / suffix lengths (k_delta MODE 2: bsrc = prefix, blen = value length, aux;
 // dba_meta: per BIN_CHUNK-value chunk {suffix bytes before it, smallest prefix in it};
 // PageWork::reserved = 1 when a value is longer than DBA_VB: that page takes the serial copy)

@@ -15,7 +15,7 @@ import ctypes as C
 import numpy as np
 import torch
 
-from . import abi, native
+from . import abi, native, writer
 
 
 class DeviceBatch:
@@ -126,6 +126,100 @@ class Decoder:
     # -- buffers -----------------------------------------------------------------
     def upload(self, batch):
         return DeviceBatch(batch, self.device)
+
+    def upload_chunks(self, chunks):
+        """Column chunks whose pages may be SNAPPY-compressed -> a DeviceBatch of uncompressed pages.
+
+        The batch is laid out for the uncompressed pages (writer.build_batch over placeholders of
+        the uncompressed sizes), the compressed blocks are uploaded once, and
+        pqg_snappy_decompress writes every block straight into its page's place in the batch on
+        the GPU (ColumnChunkPageReadStore.readPage's decompress step). Raises PqgError(CORRUPT)
+        with the failing block when a block is malformed or its length differs from the header."""
+        import copy
+        placeholders, blocks = [], []   # blocks: (payload, ("dict", output column) | ("page", page index), prefix)
+        n_page = 0
+        for ch in chunks:
+            ph = copy.copy(ch)
+            ph.pages = []
+            if ch.dict_page is not None and ch.dict_codec == writer.SNAPPY:
+                ph.dict_page = bytes(ch.dict_uncompressed_size)
+                blocks.append((ch.dict_page, ("dict", len(placeholders)), 0))
+            for pg in ch.pages:
+                q = copy.copy(pg)
+                if pg.codec == writer.SNAPPY:
+                    lv = pg.rl_byte_length + pg.dl_byte_length if pg.version == 2 else 0
+                    q.body = pg.body[:lv] + bytes(pg.uncompressed_size - lv)
+                    blocks.append((pg.body[lv:], ("page", n_page), lv))
+                elif pg.codec != writer.UNCOMPRESSED:
+                    raise native.PqgError(abi.ERR_UNSUPPORTED, what=f"page codec {pg.codec}")
+                ph.pages.append(q)
+                n_page += 1
+            placeholders.append(ph)
+        batch = writer.build_batch(placeholders)
+        dbatch = DeviceBatch(batch, self.device)
+        if not blocks:
+            return dbatch
+        col_of_chunk = []
+        seen = {}
+        for i, ch in enumerate(placeholders):
+            seen.setdefault(getattr(ch, "column_index", i), len(seen))
+            col_of_chunk.append(seen[getattr(ch, "column_index", i)])
+        src, jobs, pos = [], np.zeros((len(blocks), 3), dtype=np.uint64), 0
+        sizes = np.zeros((len(blocks), 2), dtype=np.uint32)
+        for j, (payload, (kind, idx), prefix) in enumerate(blocks):
+            if kind == "dict":
+                dst = int(batch.columns[col_of_chunk[idx]]["dict_offset"])
+                n_out = int(batch.columns[col_of_chunk[idx]]["dict_size"])
+            else:
+                dst = int(batch.pages["offset"][idx]) + prefix
+                n_out = int(batch.pages["size"][idx]) - prefix
+            jobs[j, 0], jobs[j, 1] = pos, dst
+            sizes[j] = (len(payload), n_out)
+            src.append(payload + bytes((-len(payload)) % 16))
+            pos += len(src[-1])
+        table = np.zeros(len(blocks), dtype=np.dtype([("src_offset", "<u8"), ("dst_offset", "<u8"),
+                                                      ("src_size", "<u4"), ("dst_size", "<u4")]))
+        table["src_offset"], table["dst_offset"] = jobs[:, 0], jobs[:, 1]
+        table["src_size"], table["dst_size"] = sizes[:, 0], sizes[:, 1]
+        d_src = torch.from_numpy(np.frombuffer(b"".join(src) + bytes(16), dtype=np.uint8).copy()).to(self.device)
+        d_jobs = torch.from_numpy(table.view(np.uint8).copy()).to(self.device)
+        d_status = torch.zeros(len(blocks), dtype=torch.int32, device=self.device)
+        torch.cuda.current_stream(self.device).synchronize()  # the uploads above, before the decoder's stream
+        L = native.lib()
+        rc = L.pqg_snappy_decompress(self.ctx, d_src.data_ptr(), d_src.numel(), dbatch.bytes.data_ptr(),
+                                     dbatch.n_bytes, d_jobs.data_ptr(), len(blocks), d_status.data_ptr())
+        native.check(rc, what="pqg_snappy_decompress")
+        st = abi.Status()
+        rc = L.pqg_snappy_sync(self.ctx, d_status.data_ptr(), len(blocks), C.byref(st))
+        native.check(rc, st, what="snappy block")
+        return dbatch
+
+    def snappy_decompress(self, blocks, sizes):
+        """Raw Snappy blocks (host bytes) -> device tensor of the concatenated outputs (each at a
+        16-byte aligned offset) + the offsets, decompressed by pqg_snappy_decompress.
+        Returns (out_tensor, offsets, status_codes)."""
+        src, soff, pos = [], [], 0
+        for b in blocks:
+            soff.append(pos)
+            src.append(bytes(b) + bytes((-len(b)) % 16))
+            pos += len(src[-1])
+        doff = np.concatenate([[0], np.cumsum([(s + 15) // 16 * 16 for s in sizes])]).astype(np.int64)
+        table = np.zeros(len(blocks), dtype=np.dtype([("src_offset", "<u8"), ("dst_offset", "<u8"),
+                                                      ("src_size", "<u4"), ("dst_size", "<u4")]))
+        table["src_offset"], table["dst_offset"] = soff, doff[:-1]
+        table["src_size"], table["dst_size"] = [len(b) for b in blocks], sizes
+        d_src = torch.from_numpy(np.frombuffer(b"".join(src) + bytes(16), dtype=np.uint8).copy()).to(self.device)
+        d_dst = torch.zeros(int(doff[-1]) + 16, dtype=torch.uint8, device=self.device)
+        d_jobs = torch.from_numpy(table.view(np.uint8).copy()).to(self.device)
+        d_status = torch.full((max(len(blocks), 1),), -1, dtype=torch.int32, device=self.device)
+        torch.cuda.current_stream(self.device).synchronize()
+        L = native.lib()
+        native.check(L.pqg_snappy_decompress(self.ctx, d_src.data_ptr(), d_src.numel(), d_dst.data_ptr(), d_dst.numel(),
+                                             d_jobs.data_ptr(), len(blocks), d_status.data_ptr()),
+                     what="pqg_snappy_decompress")
+        st = abi.Status()
+        L.pqg_snappy_sync(self.ctx, d_status.data_ptr(), len(blocks), C.byref(st))
+        return d_dst, doff, d_status[:len(blocks)].cpu().numpy()
 
     @staticmethod
     def binary_estimate(batch, i):

@@ -3,9 +3,10 @@
 Restates what parquet-mr's ParquetFileReader.Chunk.readAllPages does for one
 column chunk (parquet-hadoop/.../ParquetFileReader.java:1824-1979) with the
 header read by Util.readPageHeader (parquet-format-structures/.../Util.java:127-131,
-Thrift TCompactProtocol). Only uncompressed chunks are supported (codecs are
-out of scope). The result is a writer.ColumnChunk whose pages
-feed writer.build_batch -> the device decoder.
+Thrift TCompactProtocol). Chunks are UNCOMPRESSED or SNAPPY (ColumnMetaData.codec):
+SNAPPY pages keep their compressed bodies (codec / uncompressed_size on the Page) and are
+decompressed on the GPU by Decoder.upload_chunks (pqg_snappy_decompress). The result is a
+writer.ColumnChunk whose pages feed writer.build_batch -> the device decoder.
 
 This is host-side metadata handling (headers, offsets); no page data is decoded
 here.
@@ -152,7 +153,8 @@ def read_page_header(buf, pos):
     return h, r.pos
 
 
-def read_column_chunk(buf, start, length, physical_type, max_def=0, max_rep=0, type_length=0, num_values=None):
+def read_column_chunk(buf, start, length, physical_type, max_def=0, max_rep=0, type_length=0, num_values=None,
+                      codec=0):
     """Split an uncompressed column chunk [start, start+length) into a ColumnChunk.
 
     Mirrors ParquetFileReader.Chunk.readAllPages (:1824-1979): DICTIONARY_PAGE ->
@@ -165,8 +167,11 @@ def read_column_chunk(buf, start, length, physical_type, max_def=0, max_rep=0, t
     while pos < end and (num_values is None or seen < num_values):
         h, body = read_page_header(buf, pos)
         size = h["compressed_page_size"]
-        if h.get("uncompressed_page_size", size) != size and h["type"] != DATA_PAGE_V2:
-            raise ThriftError("compressed pages are not supported (codecs are out of scope)")
+        usize = h.get("uncompressed_page_size", size)
+        if codec not in (0, 1):
+            raise ThriftError(f"codec {codec} is not supported (UNCOMPRESSED and SNAPPY are)")
+        if not codec and usize != size and h["type"] != DATA_PAGE_V2:
+            raise ThriftError("compressed page in an UNCOMPRESSED chunk")
         data = bytes(buf[body:body + size])
         if len(data) != size:
             raise ThriftError("page body truncated")
@@ -175,18 +180,23 @@ def read_column_chunk(buf, start, length, physical_type, max_def=0, max_rep=0, t
             chunk.dict_page = data
             chunk.dict_num_values = h["num_values"]
             chunk.dict_encoding = h["encoding"]
+            if codec:
+                chunk.dict_codec, chunk.dict_uncompressed_size = codec, usize
         elif t == DATA_PAGE:
             chunk.pages.append(Page(body=data, num_values=h["num_values"], encoding=h["encoding"], version=1,
                                     rl_encoding=h["repetition_level_encoding"],
-                                    dl_encoding=h["definition_level_encoding"]))
+                                    dl_encoding=h["definition_level_encoding"], codec=codec,
+                                    uncompressed_size=usize if codec else 0))
             seen += h["num_values"]
         elif t == DATA_PAGE_V2:
-            if h.get("is_compressed", True) and h.get("uncompressed_page_size", size) != size:
-                raise ThriftError("compressed V2 pages are not supported")
+            compressed = bool(codec) and h.get("is_compressed", True)
+            if not compressed and usize != size:
+                raise ThriftError("V2 page sizes differ but the page is not compressed")
             chunk.pages.append(Page(body=data, num_values=h["num_values"], encoding=h["encoding"], version=2,
                                     rl_byte_length=h["repetition_levels_byte_length"],
                                     dl_byte_length=h["definition_levels_byte_length"],
-                                    num_nulls=h.get("num_nulls", 0), num_rows=h.get("num_rows", 0)))
+                                    num_nulls=h.get("num_nulls", 0), num_rows=h.get("num_rows", 0),
+                                    codec=codec if compressed else 0, uncompressed_size=usize if compressed else 0))
             seen += h["num_values"]
         pos = body + size
     return chunk

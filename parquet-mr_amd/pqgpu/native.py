@@ -17,6 +17,7 @@ EXPORTS = [
     "pqg_abi_version", "pqg_device_count", "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_stream", "pqg_decode",
     "pqg_sync", "pqg_plan_create", "pqg_plan_launch", "pqg_plan_kernel_count", "pqg_plan_destroy",
     "pqg_decode_host", "pqg_unpack_runs", "pqg_router_read", "pqg_error_name", "pqg_assemble",
+    "pqg_snappy_decompress", "pqg_snappy_sync",
 ]
 
 
@@ -57,6 +58,8 @@ def lib():
         L.pqg_unpack_runs.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32]
         L.pqg_router_read.argtypes = [vp, i32, vp, C.c_size_t, i32, vp]
         L.pqg_assemble.argtypes = [vp, vp, vp, u64, vp, i32, C.POINTER(u64), C.POINTER(abi.Status)]
+        L.pqg_snappy_decompress.argtypes = [vp, vp, u64, vp, u64, vp, i32, vp]
+        L.pqg_snappy_sync.argtypes = [vp, vp, i32, C.POINTER(abi.Status)]
         L.pqg_error_name.argtypes = [i32]
         L.pqg_error_name.restype = C.c_char_p
         if L.pqg_abi_version() != abi.ABI_VERSION:

@@ -234,6 +234,12 @@ class Page:
     dl_byte_length: int = 0
     num_nulls: int = 0
     num_rows: int = 0
+    # page codec (parquet CompressionCodec: 0 UNCOMPRESSED, 1 SNAPPY). A compressed V1 body is
+    # one Snappy block of the whole page; a compressed V2 body is the level sections as they
+    # are, then one Snappy block of the data section. uncompressed_size: the header's
+    # uncompressed_page_size (V2: levels included).
+    codec: int = 0
+    uncompressed_size: int = 0
 
 
 @dataclass
@@ -246,6 +252,8 @@ class ColumnChunk:
     dict_page: Optional[bytes] = None
     dict_num_values: int = 0
     dict_encoding: int = abi.PLAIN
+    dict_codec: int = 0               # codec of the dictionary page (its uncompressed size below)
+    dict_uncompressed_size: int = 0
     # expected decode (what the reference reader returns), for tests
     values: Optional[object] = None
     def_levels: Optional[np.ndarray] = None
@@ -465,3 +473,26 @@ def build_batch(chunks, align=ALIGN):
     return PageBatch(data=data, pages=pages, columns=columns, chunks=list(chunks),
                      page_slot_offsets=np.array(slot_off, dtype=np.int64), column_slots=col_slots,
                      column_values=col_vals)
+
+
+UNCOMPRESSED, SNAPPY = 0, 1
+
+
+def snappy_chunk(chunk):
+    """A copy of `chunk` with every page (and the dictionary page) Snappy-compressed the way
+    parquet-mr writes SNAPPY column chunks (V1: the whole body; V2: the data section after the
+    level sections). Compression by pyarrow's libsnappy (test-data synthesis only)."""
+    import copy
+
+    import pyarrow as pa
+    out = copy.deepcopy(chunk)
+    if out.dict_page is not None:
+        out.dict_uncompressed_size = len(out.dict_page)
+        out.dict_page = pa.compress(out.dict_page, codec="snappy", asbytes=True)
+        out.dict_codec = SNAPPY
+    for pg in out.pages:
+        pg.uncompressed_size = len(pg.body)
+        lv = pg.rl_byte_length + pg.dl_byte_length if pg.version == 2 else 0
+        pg.body = pg.body[:lv] + pa.compress(pg.body[lv:], codec="snappy", asbytes=True)
+        pg.codec = SNAPPY
+    return out

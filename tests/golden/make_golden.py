@@ -192,6 +192,46 @@ def write_arrow_binary_fixtures():
     return out
 
 
+def write_arrow_snappy_fixtures():
+    """SNAPPY-compressed chunks (the codec parquet-mr writes by default): dictionary, PLAIN,
+    DELTA and string columns, optional with nulls, V1 and V2 pages."""
+    rng = np.random.default_rng(77)
+    n = 12000
+    runs = np.minimum(rng.zipf(1.6, size=n), 200)
+    ids = np.repeat(rng.integers(0, 300, size=n), runs)[:n]
+    valid = rng.random(n) > 0.15
+    words = [f"w{i:04d}-{'x' * (i % 17)}" for i in range(300)]
+    t = pa.table({
+        "dict_i64": pa.array(rng.integers(-2**60, 2**60, size=300)[ids], type=pa.int64()),
+        "opt_plain_f64": pa.array(rng.standard_normal(n), mask=~valid),
+        "delta_i64": pa.array(np.cumsum(rng.integers(-50, 5000, size=n)).astype(np.int64)),
+        "dict_str": pa.array([words[i] for i in ids]),
+        "opt_plain_str": pa.array([words[i][: 3 + i % 9] for i in rng.integers(0, 300, size=n)], mask=~valid),
+    })
+    out = []
+    for ver in ("1.0", "2.0"):
+        name = f"arrow_snappy_v{ver[0]}"
+        pq.write_table(t, os.path.join(HERE, name + ".parquet"), data_page_version=ver, compression="SNAPPY",
+                       use_dictionary=["dict_i64", "dict_str"],
+                       column_encoding={"opt_plain_f64": "PLAIN", "delta_i64": "DELTA_BINARY_PACKED",
+                                        "opt_plain_str": "PLAIN"},
+                       data_page_size=8 * 1024, row_group_size=n, write_page_index=False)
+        out.append(name)
+    return out
+
+
+def add_snappy_fixtures():
+    """Append the SNAPPY fixtures to an existing manifest (the other fixtures untouched)."""
+    with open(os.path.join(HERE, "manifest.json")) as f:
+        manifest = json.load(f)
+    for name in write_arrow_snappy_fixtures():
+        manifest[name] = {"source": "pyarrow " + pa.__version__, "chunks": describe(os.path.join(HERE, name + ".parquet"),
+                                                                                   name, None)}
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+    print("manifest:", len(manifest), "fixtures")
+
+
 def main():
     manifest = {}
     for rel in REF_FILES:
@@ -200,7 +240,7 @@ def main():
         dst = os.path.join(HERE, name + ".parquet")
         shutil.copyfile(src, dst)
         manifest[name] = {"source": f"reference:{rel}", "chunks": describe(dst, name, None)}
-    for name in write_arrow_fixtures() + write_arrow_binary_fixtures():
+    for name in write_arrow_fixtures() + write_arrow_binary_fixtures() + write_arrow_snappy_fixtures():
         manifest[name] = {"source": "pyarrow " + pa.__version__, "chunks": describe(os.path.join(HERE, name + ".parquet"),
                                                                                    name, None)}
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
@@ -209,4 +249,4 @@ def main():
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(add_snappy_fixtures() if "--snappy" in sys.argv else main())

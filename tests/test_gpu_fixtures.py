@@ -35,7 +35,6 @@ def test_gpu_decodes_fixture(decoder, name, c):
 
 def test_gpu_all_fixtures_one_batch(decoder):
     """Every fixture chunk decoded in ONE pqg_decode call (many columns, mixed encodings)."""
-    from pqgpu import writer
     chunks, exp = [], []
     for name, c in CASES:
         ch, e = load_chunk(name, c)
@@ -43,7 +42,7 @@ def test_gpu_all_fixtures_one_batch(decoder):
             continue
         chunks.append(ch)
         exp.append(e)
-    batch = writer.build_batch(chunks)
-    cols, st = decoder.decode(decoder.upload(batch))
+    # SNAPPY chunks are decompressed on the device straight into the batch (pqg_snappy_decompress)
+    cols, st = decoder.decode(decoder.upload_chunks(chunks))
     for col, e, ch in zip(cols, exp, chunks):
         assert_same(col.numpy(), e, ch.physical_type)
