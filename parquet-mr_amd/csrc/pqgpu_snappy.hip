@@ -9,9 +9,9 @@
 //
 // One wave per block. The element stream is serial, so the wave parses tags as uniform scalars
 // from an LDS segment of the compressed bytes and moves each element's bytes with all lanes:
-// literals from the segment, copies from a 32 KiB LDS ring of the most recent output (offsets
-// beyond it — rare: the reference compressor's offsets stay inside 64 KiB blocks — are read back
-// from the output after a store drain). Output bytes go to HBM as they are produced.
+// literals from the segment, copies from an 8 KiB LDS ring of the most recent output (older
+// offsets are read back from the output after a store drain). Each element's tag and its
+// length / offset bytes come from ONE 8-byte LDS read. Output bytes go to HBM as produced.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -19,9 +19,10 @@
 
 namespace pqg {
 
-constexpr uint32_t SN_RING = 32768;  // LDS window of the most recent output bytes
+// LDS per wave (one-wave workgroups): 8 KiB ring + 2 KiB segment -> 16 blocks in flight per CU
+constexpr uint32_t SN_RING = 8192;   // LDS window of the most recent output bytes
 constexpr uint32_t SN_RMASK = SN_RING - 1;
-constexpr uint32_t SN_SEG = 4096;    // LDS segment of the compressed block
+constexpr uint32_t SN_SEG = 2048;    // LDS segment of the compressed block
 
 struct SnappyJobDev {  // = pqg_snappy_job
   uint64_t src_offset;
@@ -67,6 +68,14 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
     if (p < lo || p >= lo + SN_SEG) fill(p);
     return uni(seg[p - lo]);
   };
+  typedef uint32_t __attribute__((may_alias)) u32a;
+  // bytes p .. p + 7 of the block (uniform p), one LDS round trip
+  auto peek8 = [&](uint32_t p) -> uint64_t {
+    if (p < lo || p + 12u > lo + SN_SEG) fill(p);
+    const uint32_t a = (p - lo) & ~3u, sb = p & 3u;  // lo is 16-aligned
+    const uint32_t x0 = *(const u32a*)(seg + a), x1 = *(const u32a*)(seg + a + 4), x2 = *(const u32a*)(seg + a + 8);
+    return ((uint64_t)uni(__builtin_amdgcn_alignbyte(x2, x1, sb)) << 32) | uni(__builtin_amdgcn_alignbyte(x1, x0, sb));
+  };
   // uncompressed length (varint, <= 32 bits)
   uint32_t p = 0, ulen = 0;
   {
@@ -86,15 +95,16 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
     op = uni(op);
     p = uni(p);
     if (p >= n) { code = PQG_ERR_CORRUPT; break; }
-    const uint32_t tag = byte_at(p);
+    const uint64_t w8 = peek8(p);  // tag + up to 4 length / offset bytes
+    const uint32_t tag = (uint32_t)w8 & 0xFFu;
+    const uint32_t x = (uint32_t)(w8 >> 8);  // the 4 bytes after the tag
     p++;
     if ((tag & 3u) == 0u) {  // literal
       uint64_t len = tag >> 2;
       if (len >= 60u) {
         const uint32_t nb = (uint32_t)len - 59u;
         if ((uint64_t)p + nb > n) { code = PQG_ERR_CORRUPT; break; }
-        len = 0;
-        for (uint32_t i = 0; i < nb; i++) len |= (uint64_t)byte_at(p + i) << (8u * i);
+        len = nb == 4u ? x : (x & ((1u << (8u * nb)) - 1u));
         p += nb;
       }
       len += 1;
@@ -111,7 +121,7 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
           gst(out + op + done + i, b);
         }
         done += piece;
-        wave_sync();
+        __builtin_amdgcn_wave_barrier();
       }
       p += L;
       op += L;
@@ -120,24 +130,24 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
       if ((tag & 3u) == 1u) {
         if (p + 1u > n) { code = PQG_ERR_CORRUPT; break; }
         len = 4u + ((tag >> 2) & 7u);
-        off = ((tag >> 5) << 8) | byte_at(p);
+        off = ((tag >> 5) << 8) | (x & 0xFFu);
         p += 1;
       } else if ((tag & 3u) == 2u) {
         if (p + 2u > n) { code = PQG_ERR_CORRUPT; break; }
         len = 1u + (tag >> 2);
-        off = byte_at(p) | (byte_at(p + 1) << 8);
+        off = x & 0xFFFFu;
         p += 2;
       } else {
         if (p + 4u > n) { code = PQG_ERR_CORRUPT; break; }
         len = 1u + (tag >> 2);
-        off = byte_at(p) | (byte_at(p + 1) << 8) | (byte_at(p + 2) << 16) | (byte_at(p + 3) << 24);
+        off = x;
         p += 4;
       }
       if (off == 0u || off > op || (uint64_t)op + len > ulen) { code = PQG_ERR_CORRUPT; break; }
       uint32_t b = 0;
       if (off <= SN_RING - WAVE) {
         // byte op + i = byte op - off + (i mod off): the pattern of the last `off` bytes repeats
-        if (lane < len) b = ring[(op - off + (lane % off)) & SN_RMASK];
+        if (lane < len) b = ring[(op - off + (off >= len ? lane : lane % off)) & SN_RMASK];
       } else {
         // older than the ring (off > len here): this wave's own stores, drained, read back
         __builtin_amdgcn_s_waitcnt(0);
@@ -145,12 +155,14 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
         const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(a & ~3u), 0, 0);
         b = lane < len ? (w >> ((a & 3u) * 8u)) & 0xFFu : 0u;
       }
-      wave_sync();  // every lane has read before any lane writes the ring
+      // (the ring positions read, < op, and written, >= op, never alias: off <= SN_RING - 64;
+      // LDS operations of one wave complete in order, so the next element reads these writes)
+      __builtin_amdgcn_wave_barrier();
       if (lane < len) {
         ring[(op + lane) & SN_RMASK] = (uint8_t)b;
         gst(out + op + lane, (uint8_t)b);
       }
-      wave_sync();
+      __builtin_amdgcn_wave_barrier();
       op += len;
     }
   }

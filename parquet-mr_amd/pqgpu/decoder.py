@@ -25,6 +25,7 @@ class DeviceBatch:
         self.batch = batch
         self.device = device
         self.bytes = torch.from_numpy(batch.data).to(device)
+        self.snappy = None  # (compressed blocks, job table, status) when built by Decoder.upload_chunks
 
     @property
     def n_bytes(self):
@@ -185,14 +186,22 @@ class Decoder:
         d_jobs = torch.from_numpy(table.view(np.uint8).copy()).to(self.device)
         d_status = torch.zeros(len(blocks), dtype=torch.int32, device=self.device)
         torch.cuda.current_stream(self.device).synchronize()  # the uploads above, before the decoder's stream
-        L = native.lib()
-        rc = L.pqg_snappy_decompress(self.ctx, d_src.data_ptr(), d_src.numel(), dbatch.bytes.data_ptr(),
-                                     dbatch.n_bytes, d_jobs.data_ptr(), len(blocks), d_status.data_ptr())
-        native.check(rc, what="pqg_snappy_decompress")
+        dbatch.snappy = (d_src, d_jobs, d_status, len(blocks))
+        self.decompress(dbatch)
         st = abi.Status()
-        rc = L.pqg_snappy_sync(self.ctx, d_status.data_ptr(), len(blocks), C.byref(st))
+        rc = native.lib().pqg_snappy_sync(self.ctx, d_status.data_ptr(), len(blocks), C.byref(st))
         native.check(rc, st, what="snappy block")
         return dbatch
+
+    def decompress(self, dbatch):
+        """(Re)issue the SNAPPY decompression of an upload_chunks batch on the decoder's stream
+        (asynchronous; the benchmarks time it together with the decode)."""
+        if getattr(dbatch, "snappy", None) is None:
+            return
+        d_src, d_jobs, d_status, n = dbatch.snappy
+        rc = native.lib().pqg_snappy_decompress(self.ctx, d_src.data_ptr(), d_src.numel(), dbatch.bytes.data_ptr(),
+                                                dbatch.n_bytes, d_jobs.data_ptr(), n, d_status.data_ptr())
+        native.check(rc, what="pqg_snappy_decompress")
 
     def snappy_decompress(self, blocks, sizes):
         """Raw Snappy blocks (host bytes) -> device tensor of the concatenated outputs (each at a

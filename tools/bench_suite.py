@@ -106,6 +106,13 @@ def gen(name, rows):
         return [writer.write_column_chunk(abi.BYTE_ARRAY, writer.BinaryValues.random(rows, 4, 32, seed=5), enc)]
     if name == "bss_f64":
         return [writer.write_column_chunk(abi.DOUBLE, rng.standard_normal(rows), abi.BYTE_STREAM_SPLIT)]
+    if name == "c2_snappy":   # the headline pages, SNAPPY-compressed (parquet-mr's default codec)
+        import bench
+        ch, _, _ = bench.make_c2(rows)
+        return [writer.snappy_chunk(ch)]
+    if name == "plain_i64_snappy":  # int64 random walk, PLAIN pages, SNAPPY
+        walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
+        return [writer.snappy_chunk(writer.write_column_chunk(abi.INT64, walk, abi.PLAIN))]
     if name == "delta_i64":
         walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
         return [writer.write_column_chunk(abi.INT64, walk, abi.DELTA_BINARY_PACKED)]
@@ -132,7 +139,32 @@ def cpu_sample(chunks, max_pages, budget_s):
         c = writer.ColumnChunk(**{k: getattr(ch, k) for k in ("physical_type", "max_rep", "max_def", "type_length",
                                                                "dict_page", "dict_num_values", "dict_encoding")})
         c.pages = ch.pages[:max_pages]
+        c.dict_codec, c.dict_uncompressed_size = ch.dict_codec, ch.dict_uncompressed_size
         sub.append(c)
+    t_unz, label = 0.0, ""
+    if any(p.codec for c in sub for p in c.pages):
+        # SNAPPY: the oracle decompresses the pages (C restatement of the block format), timed too
+        import copy
+
+        def unz(c):
+            c = copy.deepcopy(c)
+            if c.dict_codec:
+                c.dict_page = pqref.snappy_decompress(c.dict_page, c.dict_uncompressed_size)
+                c.dict_codec = 0
+            for p in c.pages:
+                if p.codec:
+                    lv = p.rl_byte_length + p.dl_byte_length if p.version == 2 else 0
+                    p.body = p.body[:lv] + pqref.snappy_decompress(p.body[lv:], p.uncompressed_size - lv)
+                    p.codec = 0
+            return c
+        t0, zr = time.perf_counter(), 0
+        while True:
+            plain = [unz(c) for c in sub]
+            zr += 1
+            if time.perf_counter() - t0 >= budget_s / 2:
+                break
+        t_unz = (time.perf_counter() - t0) / zr
+        sub, label = plain, f" + Snappy decompression {t_unz * 1e3:.1f} ms per rep"
     b = writer.build_batch(sub)
     t0 = time.perf_counter()
     reps = 0
@@ -144,8 +176,8 @@ def cpu_sample(chunks, max_pages, budget_s):
             break
     dt = time.perf_counter() - t0
     nv = sum(c["n_values"] for c in r.columns)
-    return {"values_per_s": reps * nv / dt, "cores": 1, "kind": "port",
-            "sample": f"first {max_pages} pages of every column, {reps} reps, {dt:.1f} s"}
+    return {"values_per_s": nv / (dt / reps + t_unz), "cores": 1, "kind": "port",
+            "sample": f"first {max_pages} pages of every column, {reps} reps, {dt:.1f} s{label}"}
 
 
 def run(name, rows, steps, warmup, cpu_budget):
@@ -153,10 +185,15 @@ def run(name, rows, steps, warmup, cpu_budget):
     from pqgpu import decoder as D
     t0 = time.perf_counter()
     chunks = gen(name, rows)
-    batch = writer.build_batch(chunks)
+    compressed = any(p.codec for ch in chunks for p in ch.pages)
     t_gen = time.perf_counter() - t0
     dec = D.Decoder(0)
-    dbatch = dec.upload(batch)
+    if compressed:  # SNAPPY: every timed step decompresses on the GPU, then decodes
+        dbatch = dec.upload_chunks(chunks)
+        batch = dbatch.batch
+    else:
+        batch = writer.build_batch(chunks)
+        dbatch = dec.upload(batch)
     cols, st = dec.decode(dbatch)  # sizes BYTE_ARRAY buffers, first full decode
     plan = dec.plan(dbatch, cols)
     for _ in range(warmup):
@@ -167,6 +204,7 @@ def run(name, rows, steps, warmup, cpu_budget):
     torch.cuda.synchronize()
     ev[0].record(dec.stream)
     for k in range(steps):
+        dec.decompress(dbatch)
         plan.launch()
         ev[k + 1].record(dec.stream)
     torch.cuda.synchronize()
@@ -181,6 +219,18 @@ def run(name, rows, steps, warmup, cpu_budget):
            "values": nvals, "slots": nslots, "ms_per_launch": ms, "values_per_s": nvals / (ms / 1e3),
            "encoded_bytes": enc, "output_bytes": out, "gbps": gbps, "hbm_frac": gbps / HBM_PEAK_GBS,
            "kernels_per_launch": plan.kernel_count, "input_gen_s": t_gen}
+    if compressed:
+        comp = sum(len(p.body) for ch in chunks for p in ch.pages) + sum(len(ch.dict_page or b"") for ch in chunks)
+        ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        torch.cuda.synchronize()
+        ev2[0].record(dec.stream)
+        for _ in range(steps):
+            dec.decompress(dbatch)
+        ev2[1].record(dec.stream)
+        torch.cuda.synchronize()
+        sms = ev2[0].elapsed_time(ev2[1]) / steps
+        res.update({"compressed_bytes": comp, "snappy_ms": sms,
+                    "snappy_gbps_uncompressed": enc / (sms / 1e3) / 1e9})
     if name == "c1_plain_i32":
         t1 = time.perf_counter()
         rc2, st2, res2, _ = dec.decode_host(batch)
@@ -206,7 +256,8 @@ def main():
     args = ap.parse_args()
     default_rows = {"c1_plain_i32": 1_000_000, "c2_zipf2": 100_000_000, "c3_mixed": 100_000_000,
                     "c5_levels": 100_000_000, "str_plain": 20_000_000, "str_dict": 20_000_000,
-                    "str_dlba": 20_000_000, "str_dba": 20_000_000, "bss_f64": 100_000_000, "delta_i64": 100_000_000}
+                    "str_dlba": 20_000_000, "str_dba": 20_000_000, "bss_f64": 100_000_000, "delta_i64": 100_000_000,
+                    "c2_snappy": 100_000_000, "plain_i64_snappy": 100_000_000}
     for w in args.workloads:
         rows = args.rows or default_rows[w]
         if args.gen_only:
