@@ -23,6 +23,7 @@ namespace pqg {
 constexpr uint32_t SN_RING = 8192;   // LDS window of the most recent output bytes
 constexpr uint32_t SN_RMASK = SN_RING - 1;
 constexpr uint32_t SN_SEG = 2048;    // LDS segment of the compressed block
+constexpr uint32_t SN_OB = 2048;     // output bytes per batch of elements
 
 struct SnappyJobDev {  // = pqg_snappy_job
   uint64_t src_offset;
@@ -69,13 +70,6 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
     return uni(seg[p - lo]);
   };
   typedef uint32_t __attribute__((may_alias)) u32a;
-  // bytes p .. p + 7 of the block (uniform p), one LDS round trip
-  auto peek8 = [&](uint32_t p) -> uint64_t {
-    if (p < lo || p + 12u > lo + SN_SEG) fill(p);
-    const uint32_t a = (p - lo) & ~3u, sb = p & 3u;  // lo is 16-aligned
-    const uint32_t x0 = *(const u32a*)(seg + a), x1 = *(const u32a*)(seg + a + 4), x2 = *(const u32a*)(seg + a + 8);
-    return ((uint64_t)uni(__builtin_amdgcn_alignbyte(x2, x1, sb)) << 32) | uni(__builtin_amdgcn_alignbyte(x1, x0, sb));
-  };
   // uncompressed length (varint, <= 32 bits)
   uint32_t p = 0, ulen = 0;
   {
@@ -90,81 +84,152 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
     if ((b & 0x80u) || (k == 5u && b > 15u)) code = PQG_ERR_CORRUPT;
   }
   if (!code && ulen != ulen_exp) code = PQG_ERR_CORRUPT;
+  // Elements are taken a 256-byte window of the compressed block at a time: every lane parses
+  // an element header at each of its 4 byte positions (as if an element started there), the
+  // true chain of element starts is then followed from the current position with one
+  // v_readlane per element, and the batch (<= 64 elements, <= SN_OB output bytes) is executed:
+  // literals by their own lanes in parallel (long ones cooperatively), then the copies in order,
+  // each by all lanes from the LDS ring.
   uint32_t op = 0;
+  auto sel4 = [](const uint32_t (&v)[4], uint32_t b) { return b == 0 ? v[0] : b == 1 ? v[1] : b == 2 ? v[2] : v[3]; };
+  auto read8 = [&](uint32_t q) -> uint64_t {  // bytes q .. q + 7 from the segment (per lane)
+    const uint32_t a = (q - lo) & ~3u, sb = q & 3u;
+    const uint32_t x0 = *(const u32a*)(seg + a), x1 = *(const u32a*)(seg + a + 4), x2 = *(const u32a*)(seg + a + 8);
+    return ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sb) << 32) | __builtin_amdgcn_alignbyte(x1, x0, sb);
+  };
+  // element header at q: header bytes, output length, and (literals) data length
+  auto header = [](uint64_t x, uint32_t& hl, uint32_t& olen, uint32_t& off, uint32_t& type) {
+    const uint32_t tag = (uint32_t)x & 0xFFu, y = (uint32_t)(x >> 8);
+    type = tag & 3u;
+    off = 0;
+    if (type == 0u) {
+      const uint32_t lf = tag >> 2;
+      if (lf < 60u) {
+        hl = 1u;
+        olen = lf + 1u;
+      } else {
+        const uint32_t nb = lf - 59u;
+        hl = 1u + nb;
+        const uint32_t v = nb == 4u ? y : (y & ((1u << (8u * nb)) - 1u));
+        olen = v == 0xFFFFFFFFu ? 0xFFFFFFFFu : v + 1u;  // (a 2^32-byte literal cannot fit: invalid below)
+      }
+    } else if (type == 1u) {
+      hl = 2u;
+      olen = 4u + ((tag >> 2) & 7u);
+      off = ((tag >> 5) << 8) | (y & 0xFFu);
+    } else if (type == 2u) {
+      hl = 3u;
+      olen = 1u + (tag >> 2);
+      off = y & 0xFFFFu;
+    } else {
+      hl = 5u;
+      olen = 1u + (tag >> 2);
+      off = y;
+    }
+  };
   while (!code && op < ulen) {
     op = uni(op);
     p = uni(p);
     if (p >= n) { code = PQG_ERR_CORRUPT; break; }
-    const uint64_t w8 = peek8(p);  // tag + up to 4 length / offset bytes
-    const uint32_t tag = (uint32_t)w8 & 0xFFu;
-    const uint32_t x = (uint32_t)(w8 >> 8);  // the 4 bytes after the tag
-    p++;
-    if ((tag & 3u) == 0u) {  // literal
-      uint64_t len = tag >> 2;
-      if (len >= 60u) {
-        const uint32_t nb = (uint32_t)len - 59u;
-        if ((uint64_t)p + nb > n) { code = PQG_ERR_CORRUPT; break; }
-        len = nb == 4u ? x : (x & ((1u << (8u * nb)) - 1u));
-        p += nb;
+    const uint32_t B = p & ~3u;
+    if (B < lo || B + 256u + 16u > lo + SN_SEG) fill(B);
+    // ---- every position of the window as an element start
+    uint32_t nx[4], ol[4];
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const uint32_t q = B + 4u * lane + b;
+      uint32_t hl, olen, off, type;
+      header(read8(q), hl, olen, off, type);
+      const uint64_t e = (uint64_t)q + hl + (type == 0u ? olen : 0u);
+      nx[b] = e > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)e;
+      ol[b] = olen;
+    }
+    // ---- the true chain from p (one v_readlane per element)
+    uint32_t epos = 0, m = 0, ob = 0, cur = p;
+    while (true) {
+      cur = uni(cur);
+      if (m >= WAVE || cur >= B + 256u || cur >= n) break;
+      const uint32_t d = cur - B, l = d >> 2, bb = d & 3u;
+      const uint32_t nn = rdl(sel4(nx, bb), l), oo = rdl(sel4(ol, bb), l);
+      if (m > 0 && (uint64_t)ob + oo > SN_OB) break;
+      epos = lane == m ? cur : epos;
+      m++;
+      ob = (uint64_t)ob + oo > 0xFFFFFFFFull ? 0xFFFFFFFFu : ob + oo;
+      cur = nn;
+      if (ob > SN_OB) break;  // one long literal is a batch of its own
+    }
+    // ---- the batch: lane k < m holds element k
+    const bool in = lane < m;
+    const uint32_t q = in ? epos : B;
+    uint32_t hl, len, off, type;
+    header(read8(q), hl, len, off, type);
+    if (!in) len = 0;
+    uint32_t btot;
+    const uint32_t ox = wave_excl_scan_u32(len < 0x80000000u ? len : 0x80000000u, &btot);
+    const uint64_t ok = (uint64_t)op + ox;  // output position of the element
+    bool valid = true;
+    if (in) {
+      if (type == 0u) valid = (uint64_t)q + hl + len <= n && ok + len <= ulen;
+      else valid = (uint64_t)q + hl <= n && off != 0u && off <= ok && ok + len <= ulen;
+    }
+    if (__ballot(!valid)) { code = PQG_ERR_CORRUPT; break; }
+    const uint32_t o32 = (uint32_t)ok;
+    uint64_t lm = __ballot(in && type == 0u && len > (uint32_t)WAVE);  // literals over 64 bytes
+    // literals of <= 64 bytes: each by its own lane (the data lies inside the segment)
+    if (in && type == 0u && len <= (uint32_t)WAVE) {
+      const uint32_t s0 = q + hl - lo;
+      for (uint32_t i = 0; i < len; i++) {
+        const uint8_t v = seg[s0 + i];
+        ring[(o32 + i) & SN_RMASK] = v;
+        gst(out + o32 + i, v);
       }
-      len += 1;
-      if ((uint64_t)p + len > n || (uint64_t)op + len > ulen) { code = PQG_ERR_CORRUPT; break; }
-      const uint32_t L = (uint32_t)len;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // longer literals: all lanes, from refilled segments
+    while (lm) {
+      const uint32_t k = (uint32_t)__builtin_ctzll(lm);
+      lm &= lm - 1;
+      const uint32_t L = rdl(len, k), ls = rdl(q + hl, k), lo_out = rdl(o32, k);
       for (uint32_t done = 0; done < L;) {
-        const uint32_t q = uni(p + done);
-        if (q < lo || q + 16u > lo + SN_SEG) fill(q);
-        uint32_t piece = lo + SN_SEG - q;
+        const uint32_t qq = uni(ls + done);
+        if (qq < lo || qq + 16u > lo + SN_SEG) fill(qq);
+        uint32_t piece = lo + SN_SEG - qq;
         piece = uni(piece < L - done ? piece : L - done);
         for (uint32_t i = lane; i < piece; i += WAVE) {
-          const uint8_t b = seg[q - lo + i];
-          ring[(op + done + i) & SN_RMASK] = b;
-          gst(out + op + done + i, b);
+          const uint8_t v = seg[qq - lo + i];
+          ring[(lo_out + done + i) & SN_RMASK] = v;
+          gst(out + lo_out + done + i, v);
         }
         done += piece;
         __builtin_amdgcn_wave_barrier();
       }
-      p += L;
-      op += L;
-    } else {  // copy
-      uint32_t len, off;
-      if ((tag & 3u) == 1u) {
-        if (p + 1u > n) { code = PQG_ERR_CORRUPT; break; }
-        len = 4u + ((tag >> 2) & 7u);
-        off = ((tag >> 5) << 8) | (x & 0xFFu);
-        p += 1;
-      } else if ((tag & 3u) == 2u) {
-        if (p + 2u > n) { code = PQG_ERR_CORRUPT; break; }
-        len = 1u + (tag >> 2);
-        off = x & 0xFFFFu;
-        p += 2;
-      } else {
-        if (p + 4u > n) { code = PQG_ERR_CORRUPT; break; }
-        len = 1u + (tag >> 2);
-        off = x;
-        p += 4;
-      }
-      if (off == 0u || off > op || (uint64_t)op + len > ulen) { code = PQG_ERR_CORRUPT; break; }
-      uint32_t b = 0;
-      if (off <= SN_RING - WAVE) {
-        // byte op + i = byte op - off + (i mod off): the pattern of the last `off` bytes repeats
-        if (lane < len) b = ring[(op - off + (off >= len ? lane : lane % off)) & SN_RMASK];
-      } else {
-        // older than the ring (off > len here): this wave's own stores, drained, read back
-        __builtin_amdgcn_s_waitcnt(0);
-        const uint32_t a = op - off + lane;
-        const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(a & ~3u), 0, 0);
-        b = lane < len ? (w >> ((a & 3u) * 8u)) & 0xFFu : 0u;
-      }
-      // (the ring positions read, < op, and written, >= op, never alias: off <= SN_RING - 64;
-      // LDS operations of one wave complete in order, so the next element reads these writes)
-      __builtin_amdgcn_wave_barrier();
-      if (lane < len) {
-        ring[(op + lane) & SN_RMASK] = (uint8_t)b;
-        gst(out + op + lane, (uint8_t)b);
-      }
-      __builtin_amdgcn_wave_barrier();
-      op += len;
     }
+    // copies, in element order, all lanes (ring positions read < o, written >= o: no aliasing
+    // while off <= SN_RING - SN_OB - 64; older offsets read the drained output back)
+    uint64_t cm = __ballot(in && type != 0u);
+    while (cm) {
+      const uint32_t k = (uint32_t)__builtin_ctzll(cm);
+      cm &= cm - 1;
+      const uint32_t L = rdl(len, k), F = rdl(off, k), O = rdl(o32, k);
+      uint32_t v = 0;
+      if (F <= SN_RING - SN_OB - WAVE) {
+        if (lane < L) v = ring[(O - F + (F >= L ? lane : lane % F)) & SN_RMASK];
+      } else {
+        __builtin_amdgcn_s_waitcnt(0);
+        const uint32_t a = O - F + lane;
+        const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(a & ~3u), 0, 0);
+        v = lane < L ? (w >> ((a & 3u) * 8u)) & 0xFFu : 0u;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (lane < L) {
+        ring[(O + lane) & SN_RMASK] = (uint8_t)v;
+        gst(out + O + lane, (uint8_t)v);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    btot = uni(btot);
+    op += btot;
+    p = cur;
   }
   if (lane == 0 && status) status[jb] = code;
 }
