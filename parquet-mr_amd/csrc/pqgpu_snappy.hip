@@ -204,9 +204,33 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
         __builtin_amdgcn_wave_barrier();
       }
     }
-    // copies, in element order, all lanes (ring positions read < o, written >= o: no aliasing
-    // while off <= SN_RING - SN_OB - 64; older offsets read the drained output back)
-    uint64_t cm = __ballot(in && type != 0u);
+    // copies whose source starts at or after the end of every earlier copy's output read only
+    // literal bytes and bytes from before the batch (all in the ring now): each by its own lane,
+    // in parallel (an overlapping copy re-reads its own earlier bytes, in order)
+    const bool is_copy = in && type != 0u;
+    uint32_t pend;
+    {
+      uint32_t x = is_copy ? o32 + len : 0u;  // inclusive prefix max of the copies' output ends
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+        if ((int)lane >= d) x = y > x ? y : x;
+      }
+      pend = (uint32_t)__shfl_up((int)x, 1);
+      if (lane == 0) pend = 0;
+    }
+    const bool indep = is_copy && off <= SN_RING - SN_OB - WAVE && o32 - off >= pend;
+    if (indep) {
+      for (uint32_t i = 0; i < len; i++) {
+        const uint8_t v = ring[(o32 - off + i) & SN_RMASK];
+        ring[(o32 + i) & SN_RMASK] = v;
+        gst(out + o32 + i, v);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // the other copies, in element order, all lanes (ring positions read < o, written >= o: no
+    // aliasing while off <= SN_RING - SN_OB - 64; older offsets read the drained output back)
+    uint64_t cm = __ballot(is_copy && !indep);
     while (cm) {
       const uint32_t k = (uint32_t)__builtin_ctzll(cm);
       cm &= cm - 1;
