@@ -23,7 +23,7 @@ namespace pqg {
 constexpr uint32_t SN_RING = 8192;   // LDS window of the most recent output bytes
 constexpr uint32_t SN_RMASK = SN_RING - 1;
 constexpr uint32_t SN_SEG = 2048;    // LDS segment of the compressed block
-constexpr uint32_t SN_OB = 2048;     // output bytes per batch of elements
+constexpr uint32_t SN_W = 128;       // window of element starts per batch (<= 64 elements)
 
 struct SnappyJobDev {  // = pqg_snappy_job
   uint64_t src_offset;
@@ -38,6 +38,8 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
                                                  int32_t* __restrict__ status) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[SN_RING];
   __shared__ __attribute__((aligned(16))) uint8_t seg[SN_SEG];
+  __shared__ uint8_t sJ[SN_W], sM[SN_W];  // window successor table, chain marks
+  __shared__ uint32_t elist[WAVE];          // the batch's element starts
   const int jb = (int)blockIdx.x;
   if (jb >= n_jobs) return;
   const uint32_t lane = lane_id();
@@ -91,7 +93,6 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
   // literals by their own lanes in parallel (long ones cooperatively), then the copies in order,
   // each by all lanes from the LDS ring.
   uint32_t op = 0;
-  auto sel4 = [](const uint32_t (&v)[4], uint32_t b) { return b == 0 ? v[0] : b == 1 ? v[1] : b == 2 ? v[2] : v[3]; };
   auto read8 = [&](uint32_t q) -> uint64_t {  // bytes q .. q + 7 from the segment (per lane)
     const uint32_t a = (q - lo) & ~3u, sb = q & 3u;
     const uint32_t x0 = *(const u32a*)(seg + a), x1 = *(const u32a*)(seg + a + 4), x2 = *(const u32a*)(seg + a + 8);
@@ -131,48 +132,76 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
     op = uni(op);
     p = uni(p);
     if (p >= n) { code = PQG_ERR_CORRUPT; break; }
-    const uint32_t B = p & ~3u;
-    if (B < lo || B + 256u + 16u > lo + SN_SEG) fill(B);
-    // ---- every position of the window as an element start
-    uint32_t nx[4], ol[4];
+    const uint32_t B = p & ~1u;  // window [B, B + SN_W): 2 byte positions per lane
+    if (B < lo || B + SN_W + 80u > lo + SN_SEG) fill(B);
+    // ---- every position of the window as an element start: its successor's window offset
+    uint32_t jv[2];
 #pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      const uint32_t q = B + 4u * lane + b;
+    for (uint32_t b = 0; b < 2; b++) {
+      const uint32_t q = B + 2u * lane + b;
       uint32_t hl, olen, off, type;
       header(read8(q), hl, olen, off, type);
-      const uint64_t e = (uint64_t)q + hl + (type == 0u ? olen : 0u);
-      nx[b] = e > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)e;
-      ol[b] = olen;
+      const uint64_t e = (uint64_t)q + hl + (type == 0u ? olen : 0u) - B;
+      jv[b] = e < SN_W ? (uint32_t)e : SN_W;
+      sJ[2u * lane + b] = (uint8_t)jv[b];
+      sM[2u * lane + b] = q == p ? 1u : 0u;
     }
-    // ---- the true chain from p (one v_readlane per element)
-    uint32_t epos = 0, m = 0, ob = 0, cur = p;
-    while (true) {
-      cur = uni(cur);
-      if (m >= WAVE || cur >= B + 256u || cur >= n) break;
-      const uint32_t d = cur - B, l = d >> 2, bb = d & 3u;
-      const uint32_t nn = rdl(sel4(nx, bb), l), oo = rdl(sel4(ol, bb), l);
-      if (m > 0 && (uint64_t)ob + oo > SN_OB) break;
-      epos = lane == m ? cur : epos;
-      m++;
-      ob = (uint64_t)ob + oo > 0xFFFFFFFFull ? 0xFFFFFFFFu : ob + oo;
-      cur = nn;
-      if (ob > SN_OB) break;  // one long literal is a batch of its own
+    wave_sync();
+    // ---- pointer doubling marks the chain of element starts from p (list ranking: <= 7 rounds
+    // of LDS work per window instead of one scalar step per element)
+#pragma unroll 1
+    for (uint32_t r = 0; r < 7; r++) {
+      uint32_t jn[2];
+      bool more = false;
+#pragma unroll
+      for (uint32_t b = 0; b < 2; b++)
+        if (sM[2u * lane + b] && jv[b] < SN_W) sM[jv[b]] = 1u;
+#pragma unroll
+      for (uint32_t b = 0; b < 2; b++) jn[b] = jv[b] < SN_W ? sJ[jv[b]] : SN_W;
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (uint32_t b = 0; b < 2; b++) {
+        jv[b] = jn[b];
+        sJ[2u * lane + b] = (uint8_t)jn[b];
+      }
+      wave_sync();
+#pragma unroll
+      for (uint32_t b = 0; b < 2; b++) more |= sM[2u * lane + b] && jv[b] < SN_W;
+      if (!__ballot(more)) break;
     }
+    // ---- marked positions in order = the batch's elements (<= 64: an element has >= 2 bytes)
+    const uint32_t mk0 = sM[2u * lane], mk1 = sM[2u * lane + 1u];
+    uint32_t m;
+    const uint32_t eb = wave_excl_scan_u32(mk0 + mk1, &m);
+    if (mk0) elist[eb] = B + 2u * lane;
+    if (mk1) elist[eb + mk0] = B + 2u * lane + 1u;
+    wave_sync();
+    m = uni(m);
     // ---- the batch: lane k < m holds element k
-    const bool in = lane < m;
-    const uint32_t q = in ? epos : B;
+    const uint32_t q = lane < m ? elist[lane] : B;
     uint32_t hl, len, off, type;
     header(read8(q), hl, len, off, type);
-    if (!in) len = 0;
+    if (lane >= m) len = 0;
     uint32_t btot;
     const uint32_t ox = wave_excl_scan_u32(len < 0x80000000u ? len : 0x80000000u, &btot);
     const uint64_t ok = (uint64_t)op + ox;  // output position of the element
+    // the stream ends at the element that completes the output (trailing input is ignored) or at
+    // the end of the input
+    {
+      const uint64_t stop = __ballot(lane < m && (q >= n || ok >= ulen));
+      if (stop) m = (uint32_t)__builtin_ctzll(stop);
+    }
+    const bool in = lane < m;
+    if (!in) len = 0;
+    btot = m ? uni(rdl(ox, m - 1) + rdl(len, m - 1)) : 0u;
     bool valid = true;
     if (in) {
       if (type == 0u) valid = (uint64_t)q + hl + len <= n && ok + len <= ulen;
       else valid = (uint64_t)q + hl <= n && off != 0u && off <= ok && ok + len <= ulen;
     }
     if (__ballot(!valid)) { code = PQG_ERR_CORRUPT; break; }
+    const uint32_t cur = m ? uni(rdl(q + hl + (type == 0u ? len : 0u), m - 1)) : p;  // next element start
+    const uint64_t bend = (uint64_t)op + btot;  // the ring holds output [bend - SN_RING, bend) once the literals are in
     const uint32_t o32 = (uint32_t)ok;
     uint64_t lm = __ballot(in && type == 0u && len > (uint32_t)WAVE);  // literals over 64 bytes
     // literals of <= 64 bytes: each by its own lane (the data lies inside the segment)
@@ -219,7 +248,7 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
       pend = (uint32_t)__shfl_up((int)x, 1);
       if (lane == 0) pend = 0;
     }
-    const bool indep = is_copy && off <= SN_RING - SN_OB - WAVE && o32 - off >= pend;
+    const bool indep = is_copy && (uint64_t)(o32 - off) + SN_RING >= bend + WAVE && o32 - off >= pend;
     if (indep) {
       for (uint32_t i = 0; i < len; i++) {
         const uint8_t v = ring[(o32 - off + i) & SN_RMASK];
@@ -236,7 +265,7 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
       cm &= cm - 1;
       const uint32_t L = rdl(len, k), F = rdl(off, k), O = rdl(o32, k);
       uint32_t v = 0;
-      if (F <= SN_RING - SN_OB - WAVE) {
+      if ((uint64_t)(O - F) + SN_RING >= bend + WAVE) {
         if (lane < L) v = ring[(O - F + (F >= L ? lane : lane % F)) & SN_RMASK];
       } else {
         __builtin_amdgcn_s_waitcnt(0);
@@ -251,7 +280,6 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
       }
       __builtin_amdgcn_wave_barrier();
     }
-    btot = uni(btot);
     op += btot;
     p = cur;
   }
