@@ -7,11 +7,15 @@
 // size. Format (google/snappy format_description.txt): varint length, then elements — literal
 // (tag & 3 == 0) or copy (1-, 2-, 4-byte offset, length 1..64) that may overlap its own output.
 //
-// One wave per block. The element stream is serial, so the wave parses tags as uniform scalars
-// from an LDS segment of the compressed bytes and moves each element's bytes with all lanes:
-// literals from the segment, copies from an 8 KiB LDS ring of the most recent output (older
-// offsets are read back from the output after a store drain). Each element's tag and its
-// length / offset bytes come from ONE 8-byte LDS read. Output bytes go to HBM as produced.
+// One wave per block, elements taken a 128-byte window of the compressed bytes (staged in an LDS
+// segment) at a time: every lane parses an element header at its 2 byte positions as if an
+// element started there, and pointer doubling over the window's successor table marks the true
+// chain of element starts. The batch (<= 64 elements, <= 512 output bytes) is then resolved byte
+// by byte: every output byte gets its source (a literal byte in the segment, or the output
+// position it copies), and pointer jumping follows chains of dependent copies in log2(depth)
+// rounds until each source is a literal byte or lies before the batch (in an 8 KiB LDS ring of
+// the most recent output, or, older, in HBM). The batch's bytes go to the ring and from there to
+// HBM with aligned dword stores; a long literal that ends a batch is streamed to HBM directly.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -19,11 +23,13 @@
 
 namespace pqg {
 
-// LDS per wave (one-wave workgroups): 8 KiB ring + 2 KiB segment -> 16 blocks in flight per CU
+// LDS per wave (one-wave workgroups): 8 KiB ring + 2 KiB segment + 2 KiB byte sources
 constexpr uint32_t SN_RING = 8192;   // LDS window of the most recent output bytes
 constexpr uint32_t SN_RMASK = SN_RING - 1;
 constexpr uint32_t SN_SEG = 2048;    // LDS segment of the compressed block
 constexpr uint32_t SN_W = 128;       // window of element starts per batch (<= 64 elements)
+constexpr uint32_t SN_CAP = 512;     // output bytes per batch (a longer first element: a literal, streamed)
+constexpr uint32_t SN_LIT = 0x80000000u;  // source tag of a literal byte (| its segment offset)
 
 struct SnappyJobDev {  // = pqg_snappy_job
   uint64_t src_offset;
@@ -40,6 +46,7 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
   __shared__ __attribute__((aligned(16))) uint8_t seg[SN_SEG];
   __shared__ uint8_t sJ[SN_W], sM[SN_W];  // window successor table, chain marks
   __shared__ uint32_t elist[WAVE];          // the batch's element starts
+  __shared__ uint32_t sS[SN_CAP];           // source of every output byte of the batch
   const int jb = (int)blockIdx.x;
   if (jb >= n_jobs) return;
   const uint32_t lane = lane_id();
@@ -86,12 +93,7 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
     if ((b & 0x80u) || (k == 5u && b > 15u)) code = PQG_ERR_CORRUPT;
   }
   if (!code && ulen != ulen_exp) code = PQG_ERR_CORRUPT;
-  // Elements are taken a 256-byte window of the compressed block at a time: every lane parses
-  // an element header at each of its 4 byte positions (as if an element started there), the
-  // true chain of element starts is then followed from the current position with one
-  // v_readlane per element, and the batch (<= 64 elements, <= SN_OB output bytes) is executed:
-  // literals by their own lanes in parallel (long ones cooperatively), then the copies in order,
-  // each by all lanes from the LDS ring.
+  if (!code && ulen >= SN_LIT) code = PQG_ERR_INVALID_ARG;  // page sizes are int32 (PageHeader)
   uint32_t op = 0;
   auto read8 = [&](uint32_t q) -> uint64_t {  // bytes q .. q + 7 from the segment (per lane)
     const uint32_t a = (q - lo) & ~3u, sb = q & 3u;
@@ -126,6 +128,31 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
       hl = 5u;
       olen = 1u + (tag >> 2);
       off = y;
+    }
+  };
+  const u32a* ring32 = (const u32a*)ring;
+  // ring bytes of output positions t .. t + 3 (per lane; the ring wraps)
+  auto ring4 = [&](uint32_t t) -> uint32_t {
+    const uint32_t r = t & SN_RMASK & ~3u;
+    return __builtin_amdgcn_alignbyte(ring32[((r + 4u) & SN_RMASK) >> 2], ring32[r >> 2], t & 3u);
+  };
+  // output [a, e) (uniform, e - a <= SN_RING, all in the ring) to HBM: aligned dwords, bytes at the ends
+  const uint32_t oal = (uint32_t)(uintptr_t)out & 3u;
+  auto flush = [&](uint32_t a, uint32_t e) {
+    const uint32_t base = ((a + oal) & ~3u) - oal;  // out + base is dword aligned (base <= a, may wrap)
+    const uint32_t skip = a - base, span = e - base;
+    for (uint32_t d0 = 0; d0 < span; d0 += 4u * WAVE) {
+      const uint32_t d = d0 + 4u * lane;
+      if (d < span) {
+        const uint32_t t = base + d, v = ring4(t);
+        if (d >= skip && d + 4u <= span) {
+          gst((uint32_t*)(out + t), v);
+        } else {
+#pragma unroll
+          for (uint32_t j = 0; j < 4u; j++)
+            if (d + j >= skip && d + j < span) gst(out + (t + j), (uint8_t)(v >> (8u * j)));
+        }
+      }
     }
   };
   while (!code && op < ulen) {
@@ -190,6 +217,9 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
     {
       const uint64_t stop = __ballot(lane < m && (q >= n || ok >= ulen));
       if (stop) m = (uint32_t)__builtin_ctzll(stop);
+      // at most SN_CAP output bytes (an element longer than that is a literal: a batch of its own)
+      const uint64_t over = __ballot(lane < m && lane > 0u && (uint64_t)ox + len > SN_CAP);
+      if (over) m = (uint32_t)__builtin_ctzll(over);
     }
     const bool in = lane < m;
     if (!in) len = 0;
@@ -201,24 +231,78 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
     }
     if (__ballot(!valid)) { code = PQG_ERR_CORRUPT; break; }
     const uint32_t cur = m ? uni(rdl(q + hl + (type == 0u ? len : 0u), m - 1)) : p;  // next element start
-    const uint64_t bend = (uint64_t)op + btot;  // the ring holds output [bend - SN_RING, bend) once the literals are in
     const uint32_t o32 = (uint32_t)ok;
-    uint64_t lm = __ballot(in && type == 0u && len > (uint32_t)WAVE);  // literals over 64 bytes
-    // literals of <= 64 bytes: each by its own lane (the data lies inside the segment)
-    if (in && type == 0u && len <= (uint32_t)WAVE) {
-      const uint32_t s0 = q + hl - lo;
-      for (uint32_t i = 0; i < len; i++) {
-        const uint8_t v = seg[s0 + i];
-        ring[(o32 + i) & SN_RMASK] = v;
-        gst(out + o32 + i, v);
+    // a literal of over 64 bytes that ends the batch (it may be longer than the ring) goes to HBM
+    // straight from the segment; the batch's other output, [op, fend), goes via the ring
+    const bool tail_lit = m && rdl(type, m - 1) == 0u && rdl(len, m - 1) > (uint32_t)WAVE;
+    const uint32_t fend = tail_lit ? uni(rdl(o32, m - 1)) : uni(op + btot);
+    const uint32_t T = fend - op;  // <= SN_CAP
+    // ---- the source of every output byte: its literal byte in the segment, or the output position
+    // it copies (an overlapping copy's later bytes copy its own earlier ones)
+    if (in && !(tail_lit && lane == m - 1)) {
+      const uint32_t s0 = type == 0u ? SN_LIT | (q + hl - lo) : o32 - off, b0 = o32 - op;
+      for (uint32_t i = 0; i < len; i++) sS[b0 + i] = s0 + i;
+    }
+    wave_sync();
+    // ---- pointer jumping until every source is a literal byte or a byte from before the batch
+    // (chains of dependent copies resolve in log2(depth) rounds instead of one copy at a time)
+    constexpr uint32_t NB = SN_CAP / WAVE;
+    uint32_t sv[NB];
+#pragma unroll
+    for (uint32_t j = 0; j < NB; j++) {
+      const uint32_t b = lane + WAVE * j;
+      sv[j] = b < T ? sS[b] : SN_LIT;
+    }
+#pragma unroll 1
+    for (uint32_t r = 0; r < 12u; r++) {
+      bool more = false, hop = false;
+#pragma unroll
+      for (uint32_t j = 0; j < NB; j++) {
+        if (!(sv[j] & SN_LIT) && sv[j] >= op) {
+          sv[j] = sS[sv[j] - op];
+          hop = true;
+          more |= !(sv[j] & SN_LIT) && sv[j] >= op;
+        }
+      }
+      if (!__ballot(hop)) break;
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (uint32_t j = 0; j < NB; j++) {
+        const uint32_t b = lane + WAVE * j;
+        if (b < T) sS[b] = sv[j];
+      }
+      wave_sync();
+      if (!__ballot(more)) break;
+    }
+    // ---- the bytes: literal bytes from the segment, earlier output from the ring, or (older than
+    // the ring) from HBM after the earlier batches' stores have drained
+    bool far = false;
+#pragma unroll
+    for (uint32_t j = 0; j < NB; j++) far |= !(sv[j] & SN_LIT) && (uint64_t)sv[j] + SN_RING < (uint64_t)fend + WAVE;
+    if (__ballot(far)) __builtin_amdgcn_s_waitcnt(0);
+    uint32_t bv[NB];
+#pragma unroll
+    for (uint32_t j = 0; j < NB; j++) {
+      const uint32_t v = sv[j];
+      if (v & SN_LIT) {
+        bv[j] = seg[v & (SN_SEG - 1u)];
+      } else if ((uint64_t)v + SN_RING < (uint64_t)fend + WAVE) {
+        const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(v & ~3u), 0, 0);
+        bv[j] = (w >> ((v & 3u) * 8u)) & 0xFFu;
+      } else {
+        bv[j] = ring[v & SN_RMASK];
       }
     }
     __builtin_amdgcn_wave_barrier();
-    // longer literals: all lanes, from refilled segments
-    while (lm) {
-      const uint32_t k = (uint32_t)__builtin_ctzll(lm);
-      lm &= lm - 1;
-      const uint32_t L = rdl(len, k), ls = rdl(q + hl, k), lo_out = rdl(o32, k);
+#pragma unroll
+    for (uint32_t j = 0; j < NB; j++) {
+      const uint32_t b = lane + WAVE * j;
+      if (b < T) ring[(op + b) & SN_RMASK] = (uint8_t)bv[j];
+    }
+    wave_sync();
+    flush(op, fend);
+    if (tail_lit) {  // all lanes, from refilled segments, to the ring and to HBM
+      const uint32_t k = m - 1u, L = rdl(len, k), ls = rdl(q + hl, k);
       for (uint32_t done = 0; done < L;) {
         const uint32_t qq = uni(ls + done);
         if (qq < lo || qq + 16u > lo + SN_SEG) fill(qq);
@@ -226,59 +310,12 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
         piece = uni(piece < L - done ? piece : L - done);
         for (uint32_t i = lane; i < piece; i += WAVE) {
           const uint8_t v = seg[qq - lo + i];
-          ring[(lo_out + done + i) & SN_RMASK] = v;
-          gst(out + lo_out + done + i, v);
+          ring[(fend + done + i) & SN_RMASK] = v;
+          gst(out + fend + done + i, v);
         }
         done += piece;
         __builtin_amdgcn_wave_barrier();
       }
-    }
-    // copies whose source starts at or after the end of every earlier copy's output read only
-    // literal bytes and bytes from before the batch (all in the ring now): each by its own lane,
-    // in parallel (an overlapping copy re-reads its own earlier bytes, in order)
-    const bool is_copy = in && type != 0u;
-    uint32_t pend;
-    {
-      uint32_t x = is_copy ? o32 + len : 0u;  // inclusive prefix max of the copies' output ends
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-        if ((int)lane >= d) x = y > x ? y : x;
-      }
-      pend = (uint32_t)__shfl_up((int)x, 1);
-      if (lane == 0) pend = 0;
-    }
-    const bool indep = is_copy && (uint64_t)(o32 - off) + SN_RING >= bend + WAVE && o32 - off >= pend;
-    if (indep) {
-      for (uint32_t i = 0; i < len; i++) {
-        const uint8_t v = ring[(o32 - off + i) & SN_RMASK];
-        ring[(o32 + i) & SN_RMASK] = v;
-        gst(out + o32 + i, v);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    // the other copies, in element order, all lanes (ring positions read < o, written >= o: no
-    // aliasing while off <= SN_RING - SN_OB - 64; older offsets read the drained output back)
-    uint64_t cm = __ballot(is_copy && !indep);
-    while (cm) {
-      const uint32_t k = (uint32_t)__builtin_ctzll(cm);
-      cm &= cm - 1;
-      const uint32_t L = rdl(len, k), F = rdl(off, k), O = rdl(o32, k);
-      uint32_t v = 0;
-      if ((uint64_t)(O - F) + SN_RING >= bend + WAVE) {
-        if (lane < L) v = ring[(O - F + (F >= L ? lane : lane % F)) & SN_RMASK];
-      } else {
-        __builtin_amdgcn_s_waitcnt(0);
-        const uint32_t a = O - F + lane;
-        const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(a & ~3u), 0, 0);
-        v = lane < L ? (w >> ((a & 3u) * 8u)) & 0xFFu : 0u;
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (lane < L) {
-        ring[(O + lane) & SN_RMASK] = (uint8_t)v;
-        gst(out + O + lane, (uint8_t)v);
-      }
-      __builtin_amdgcn_wave_barrier();
     }
     op += btot;
     p = cur;

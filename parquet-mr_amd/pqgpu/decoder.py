@@ -203,16 +203,18 @@ class Decoder:
                                                 dbatch.n_bytes, d_jobs.data_ptr(), n, d_status.data_ptr())
         native.check(rc, what="pqg_snappy_decompress")
 
-    def snappy_decompress(self, blocks, sizes):
+    def snappy_decompress(self, blocks, sizes, skew=False):
         """Raw Snappy blocks (host bytes) -> device tensor of the concatenated outputs (each at a
-        16-byte aligned offset) + the offsets, decompressed by pqg_snappy_decompress.
-        Returns (out_tensor, offsets, status_codes)."""
+        16-byte aligned offset, or with skew=True at offsets of every residue mod 16) + the
+        offsets, decompressed by pqg_snappy_decompress. Returns (out_tensor, offsets, status_codes)."""
         src, soff, pos = [], [], 0
         for b in blocks:
             soff.append(pos)
             src.append(bytes(b) + bytes((-len(b)) % 16))
             pos += len(src[-1])
-        doff = np.concatenate([[0], np.cumsum([(s + 15) // 16 * 16 for s in sizes])]).astype(np.int64)
+        doff = np.concatenate([[0], np.cumsum([(s + 15) // 16 * 16 + 16 for s in sizes])]).astype(np.int64)
+        if skew:  # block i starts i % 16 bytes into its slot (V2 data sections follow their levels)
+            doff[:-1] += np.arange(len(sizes)) % 16
         table = np.zeros(len(blocks), dtype=np.dtype([("src_offset", "<u8"), ("dst_offset", "<u8"),
                                                       ("src_size", "<u4"), ("dst_size", "<u4")]))
         table["src_offset"], table["dst_offset"] = soff, doff[:-1]

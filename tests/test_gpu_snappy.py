@@ -77,8 +77,8 @@ def _handmade():
     return cases
 
 
-def _run(decoder, blocks, sizes):
-    out, offs, status = decoder.snappy_decompress(blocks, sizes)
+def _run(decoder, blocks, sizes, skew=False):
+    out, offs, status = decoder.snappy_decompress(blocks, sizes, skew=skew)
     host = out.cpu().numpy()
     return [host[offs[i]:offs[i] + sizes[i]].tobytes() for i in range(len(blocks))], status
 
@@ -93,15 +93,17 @@ def test_golden_vectors(decoder):
         assert g == r, n
 
 
-def test_handmade_blocks(decoder):
+@pytest.mark.parametrize("skew", [False, True])
+def test_handmade_blocks(decoder, skew):
     cases = _handmade()
-    got, status = _run(decoder, [c[0] for c in cases], [len(c[1]) for c in cases])
+    got, status = _run(decoder, [c[0] for c in cases], [len(c[1]) for c in cases], skew=skew)
     assert list(status) == [0] * len(cases)
     for i, (g, (_, out)) in enumerate(zip(got, cases)):
         assert g == out, i
 
 
-def test_many_pyarrow_blocks(decoder):
+@pytest.mark.parametrize("skew", [False, True])
+def test_many_pyarrow_blocks(decoder, skew):
     pa = pytest.importorskip("pyarrow")
     rng = np.random.default_rng(4)
     raws = []
@@ -115,7 +117,7 @@ def test_many_pyarrow_blocks(decoder):
         else:
             raws.append(np.cumsum(rng.integers(-5, 500, size=n // 8)).astype(np.int64).tobytes())
     comps = [pa.compress(r, codec="snappy", asbytes=True) for r in raws]
-    got, status = _run(decoder, comps, [len(r) for r in raws])
+    got, status = _run(decoder, comps, [len(r) for r in raws], skew=skew)
     assert list(status) == [0] * len(raws)
     assert got == raws
 
