@@ -10,10 +10,10 @@
 // One wave per block, elements taken a 128-byte window of the compressed bytes (staged in an LDS
 // segment) at a time: every lane parses an element header at its 2 byte positions as if an
 // element started there, and pointer doubling over the window's successor table marks the true
-// chain of element starts. The batch (<= 64 elements, <= 512 output bytes) is then resolved byte
+// chain of element starts. The batch (<= 64 elements, <= 256 output bytes) is then resolved byte
 // by byte: every output byte gets its source (a literal byte in the segment, or the output
 // position it copies), and pointer jumping follows chains of dependent copies in log2(depth)
-// rounds until each source is a literal byte or lies before the batch (in an 8 KiB LDS ring of
+// rounds until each source is a literal byte or lies before the batch (in an 4 KiB LDS ring of
 // the most recent output, or, older, in HBM). The batch's bytes go to the ring and from there to
 // HBM with aligned dword stores; a long literal that ends a batch is streamed to HBM directly.
 #include <hip/hip_runtime.h>
@@ -23,12 +23,13 @@
 
 namespace pqg {
 
-// LDS per wave (one-wave workgroups): 8 KiB ring + 2 KiB segment + 2 KiB byte sources
-constexpr uint32_t SN_RING = 8192;   // LDS window of the most recent output bytes
+// LDS per wave (one-wave workgroups): 4 KiB ring + 2 KiB segment + 1 KiB byte sources + 0.5 KiB
+// chain tables = 7.7 KiB -> 20 blocks per CU: all 5,000 pages of a 100 M-value chunk at once
+constexpr uint32_t SN_RING = 4096;   // LDS window of the most recent output bytes
 constexpr uint32_t SN_RMASK = SN_RING - 1;
 constexpr uint32_t SN_SEG = 2048;    // LDS segment of the compressed block
 constexpr uint32_t SN_W = 128;       // window of element starts per batch (<= 64 elements)
-constexpr uint32_t SN_CAP = 512;     // output bytes per batch (a longer first element: a literal, streamed)
+constexpr uint32_t SN_CAP = 256;     // output bytes per batch (a longer first element: a literal, streamed)
 constexpr uint32_t SN_LIT = 0x80000000u;  // source tag of a literal byte (| its segment offset)
 
 struct SnappyJobDev {  // = pqg_snappy_job
