@@ -2118,6 +2118,90 @@ __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_
   }
 }
 
+// Any other DeltaBinaryPackingConfig the reference accepts (blocks of more than 512 values or more
+// than 8 miniblocks; DuckDB writes 2048 / 8): block by block, miniblock by miniblock, 64 deltas
+// per step, page bytes read with buffer loads. Same checks, in the same order, as the batched walk
+// below (loadNewBlockToBuffer :118-143): widths of the used miniblocks (> 64: CORRUPT), then
+// their bytes (EOF). p = position after the header; the first value is already stored.
+template <int W, bool NEG>
+__device__ int delta_generic(const rsrc_t rs, uint32_t p, uint32_t end, uint32_t block, uint32_t mbn, uint32_t mbs,
+                             uint32_t total, uint32_t n_out, uint64_t carry, typename DictVal<W>::T* out, int page,
+                             uint64_t* err, uint32_t* err_count, uint32_t* p_end) {
+  typedef typename DictVal<W>::T T;
+  const uint32_t lane = lane_id();
+  auto byte_at = [&](uint32_t a) -> uint32_t { return uni((ld32(rs, a & ~3u) >> (8u * (a & 3u))) & 0xFFu); };
+  uint32_t buffered = 1;
+  uint64_t k_next = 1;  // value index after the next delta
+  while (true) {
+    p = uni(p);
+    buffered = uni(buffered);
+    if (buffered >= total) break;
+    if (p >= end) return PQG_ERR_EOF;
+    // min delta (readZigZagVarLong, Java shift masking)
+    uint64_t mraw = 0;
+    uint32_t i = 0, k = 0, b;
+    for (;;) {
+      b = byte_at(p + k);
+      if (!(b & 0x80u)) break;
+      mraw |= (uint64_t)(b & 0x7Fu) << (i & 63u);
+      i += 7;
+      k++;
+      if (k >= end - p) break;
+    }
+    mraw |= (uint64_t)b << (i & 63u);
+    if ((uint64_t)p + k + 1u > end) return PQG_ERR_EOF;
+    const uint64_t mind = (uint64_t)zigzag64(mraw);
+    const uint32_t wpos = p + k + 1u;
+    if ((uint64_t)wpos + mbn > end) return PQG_ERR_EOF;  // readBitWidthsForMiniBlocks
+    uint32_t used = 0, bufd = buffered;
+    uint64_t dbytes = 0;
+    for (uint32_t m = 0; m < mbn && bufd < total; m++) {
+      const uint32_t wm = byte_at(wpos + m);
+      if (wm > 64u) return PQG_ERR_CORRUPT;
+      dbytes += (uint64_t)wm * (mbs / 8u);
+      bufd += mbs;
+      used++;
+    }
+    const uint32_t dpos = wpos + mbn;
+    if ((uint64_t)dpos + dbytes > end) return PQG_ERR_EOF;  // in.slice EOF
+    uint32_t mo = dpos;  // data of miniblock m
+    for (uint32_t m = 0; m < used; m++) {
+      const uint32_t w = byte_at(wpos + m);
+      const uint64_t mask = w == 64u ? ~0ull : ((1ull << w) - 1ull);
+      for (uint32_t c = 0; c < mbs; c += WAVE) {
+        const uint32_t q = c + lane;
+        const bool in = q < mbs;
+        uint64_t d = 0;
+        if (in && w) {
+          const uint32_t bit = q * w, byte = mo + (bit >> 3), a = byte & ~3u;
+          const uint32_t x0 = ld32(rs, a), x1 = ld32(rs, a + 4), x2 = ld32(rs, a + 8);
+          const uint32_t sh = (byte - a) * 8u + (bit & 7u);
+          const uint64_t lo64 = (uint64_t)x0 | ((uint64_t)x1 << 32);
+          d = (sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)))) & mask;
+        }
+        const uint64_t x = wave_incl_scan_u64(in ? d + mind : 0ull);
+        const uint64_t kk = k_next + q;
+        if (in && kk < n_out) {
+          T v = (T)(carry + x);
+          if (NEG && (int32_t)(uint32_t)v < 0) {
+            report(err, err_count, page, 2, kk, PQG_ERR_CORRUPT);
+            v = 0;
+          }
+          gst(out + kk, v);
+        }
+        carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
+      }
+      k_next += mbs;
+      mo += w * (mbs / 8u);
+    }
+    p = dpos + (uint32_t)dbytes;
+    buffered = bufd;
+  }
+  (void)block;
+  *p_end = p;
+  return 0;
+}
+
 // One stream [p, end) -> out[0 .. min(want, total)). Returns 0 or the init error code (the
 // reader decodes eagerly in initFromPage); *p_end = stream position after the used miniblocks,
 // *total_out = the header's value count. NEG: a negative (int) value is reported as CORRUPT at
@@ -2143,8 +2227,6 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
   if ((block % mbn) != 0 || ((block / mbn) % 8u) != 0) return PQG_ERR_DELTA_CONFIG;
   const uint32_t mbs = block / mbn;
   if (mbs == 0) return PQG_ERR_CORRUPT;
-  // register budget of this kernel: block <= 512 values, <= 8 miniblocks (parquet-mr default 128 / 4)
-  if (block > 512u || mbn > 8u) return PQG_ERR_UNSUPPORTED;
   if (p >= end) return PQG_ERR_EOF;
   const uint32_t total = (uint32_t)seg_uvar<true>(S, p, end - p, len);
   if ((uint64_t)p + len > end) return PQG_ERR_EOF;
@@ -2169,6 +2251,10 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
       gst(out, (T)carry);
     }
   }
+  // register budget of the batched expansion: block <= 512 values, <= 8 miniblocks (parquet-mr
+  // and Arrow write 128 / 4); other configurations take the block-by-block path
+  if (block > 512u || mbn > 8u)
+    return delta_generic<W, NEG>(S.rs, p, end, block, mbn, mbs, total, n_out, carry, out, page, err, err_count, p_end);
   uint32_t buffered = 1;  // Java valuesBuffered (includes the first value)
   uint32_t n_blocks = 0;
   // deltas per lane per block: the power of two >= block / 64 (it divides the block, a multiple

@@ -188,10 +188,13 @@ def test_delta(decoder, ptype, kind):
 
 
 @pytest.mark.parametrize("block,mb", [(128, 4), (64, 8), (256, 8), (512, 8), (32, 1), (8, 1),
-                                      (192, 3), (24, 3), (320, 5)])
+                                      (192, 3), (24, 3), (320, 5),
+                                      # block-by-block path: > 512 values or > 8 miniblocks (DuckDB: 2048 / 8)
+                                      (1024, 4), (2048, 8), (128, 16), (1024, 128), (40000, 5), (8192, 64)])
 @pytest.mark.parametrize("ptype", [abi.INT64, abi.INT32])
 def test_delta_configs(decoder, block, mb, ptype):
-    # blocks of 8 * 2^k values take the several-blocks-per-step expansion, the others one block per step
+    # blocks of 8 * 2^k values take the several-blocks-per-step expansion, the others one block per
+    # step; blocks of more than 512 values or more than 8 miniblocks the block-by-block path
     rng = np.random.default_rng(block)
     vals = np.cumsum(rng.integers(-3, 1 << 20, size=40_000)).astype(np.int64)
     if ptype == abi.INT32:
@@ -245,6 +248,28 @@ def test_error_plain_eof(decoder):
 def test_error_delta_past_end(decoder):
     ch = make(abi.INT64, np.arange(3000, dtype=np.int64), abi.DELTA_BINARY_PACKED, page_rows=1000)
     ch.pages[1].num_values = 1500  # header total is 1000
+    run_both(decoder, [ch], expect_error=True)
+
+
+@pytest.mark.parametrize("block,mb", [(128, 4), (2048, 8), (256, 32)])
+@pytest.mark.parametrize("cut", [1, 3, 17, 300, 1500])
+def test_error_delta_truncated(decoder, block, mb, cut):
+    # truncated DELTA pages: the batched and the block-by-block paths classify like the oracle
+    vals = np.cumsum(np.random.default_rng(cut).integers(-3, 1 << 30, size=6000)).astype(np.int64)
+    ch = make(abi.INT64, vals, abi.DELTA_BINARY_PACKED, page_rows=3000, delta_block=block, delta_miniblocks=mb)
+    ch.pages[1].body = ch.pages[1].body[:len(ch.pages[1].body) - cut]
+    run_both(decoder, [ch], expect_error=ref_errors(ch))
+
+
+def test_error_delta_wide_miniblock(decoder):
+    # a miniblock width over 64 (CORRUPT) in a block of the block-by-block path
+    ch = make(abi.INT64, np.arange(5000, dtype=np.int64) * 7, abi.DELTA_BINARY_PACKED, page_rows=5000,
+              delta_block=1024, delta_miniblocks=8)
+    body = bytearray(ch.pages[0].body)
+    # header varints: block, miniblocks, total, first (zigzag 0 = 1 byte); then block 0: min delta (1 byte), widths
+    hdr = 2 + 1 + 2 + 1
+    body[hdr + 1 + 2] = 65
+    ch.pages[0].body = bytes(body)
     run_both(decoder, [ch], expect_error=True)
 
 
