@@ -396,7 +396,7 @@ static int emit_binary(colstate* cs, const uint8_t* src, int32_t len) {
 /* ------------------------------------------------------------------------ */
 /* Value readers: one struct with a tagged union of the reference's readers. */
 
-enum { VR_DICT = 1, VR_PLAIN_FIXED, VR_PLAIN_BOOL, VR_PLAIN_BINARY, VR_DELTA, VR_DLBA, VR_DBA, VR_BSS };
+enum { VR_DICT = 1, VR_PLAIN_FIXED, VR_PLAIN_BOOL, VR_PLAIN_BINARY, VR_DELTA, VR_DLBA, VR_DBA, VR_BSS, VR_RLE_BOOL };
 
 /* DeltaBinaryPackingValuesReader state: the eagerly decoded page (valuesBuffer). */
 typedef struct {
@@ -591,6 +591,19 @@ static int vreader_init(vreader* r, const pqg_page_desc* pg, colstate* cs, jstre
     r->bss_index = 0;
     return PQG_OK;
   }
+  if (enc == PQG_RLE) {
+    /* Encoding.RLE.getValuesReader :116-124: VALUES only for BOOLEAN (getMaxLevel :255-271, width 1;
+     * parquet-mr's V2 writer, DefaultV2ValuesWriterFactory.getBooleanValuesWriter :77-84).
+     * RunLengthBitPackingHybridValuesReader.initFromPage :40-46: 4-byte LE length, sliceStream */
+    if (t != PQG_BOOLEAN) return PQG_ERR_UNSUPPORTED;
+    int32_t length;
+    int e = read_int_le(s, &length);
+    if (e) return e;
+    jstream sl;
+    if ((e = js_slice(s, length, &sl))) return e;
+    r->kind = VR_RLE_BOOL;
+    return rle_init(&r->rle, 1, sl);
+  }
   return PQG_ERR_UNSUPPORTED;
 }
 
@@ -630,6 +643,13 @@ static int vreader_read(vreader* r, colstate* cs) {
       int64_t byte = bit >> 3;
       uint8_t v = 0;
       if (byte < js_available(&r->in)) v = (r->in.buf[r->in.pos + byte] >> (bit & 7)) & 1;
+      return emit_fixed(cs, &v);
+    }
+    case VR_RLE_BOOL: {
+      /* RunLengthBitPackingHybridValuesReader.readBoolean :58-60: readInteger() != 0 */
+      int32_t x;
+      if ((e = rle_read_int(&r->rle, &x))) return e;
+      uint8_t v = x != 0;
       return emit_fixed(cs, &v);
     }
     case VR_PLAIN_BINARY: {

@@ -92,7 +92,7 @@ size_t err_region_bytes(int n_pages, int n_cols) {
 //   C_IDS   dictionary pages whose values are not 4 / 8 bytes (BYTE_ARRAY, FLBA, INT96): ids first
 //   C_BINP  PLAIN BYTE_ARRAY          C_DLBA  DELTA_LENGTH_BYTE_ARRAY      C_BSS  BYTE_STREAM_SPLIT
 //   C_DBA   DELTA_BYTE_ARRAY (lengths here; values by k_dba_copy after the offset scan)
-enum Cls { C_DICT4 = 0, C_DICT8, C_IDS, C_PLAIN, C_BOOL, C_DELTA4, C_DELTA8, C_BSS, C_BINP, C_DLBA, C_DBA, C_NCLS };
+enum Cls { C_DICT4 = 0, C_DICT8, C_IDS, C_PLAIN, C_BOOL, C_DELTA4, C_DELTA8, C_BSS, C_BINP, C_DLBA, C_DBA, C_RLEBOOL, C_NCLS };
 constexpr int N_DICT_CLS = 3;  // C_DICT4, C_DICT8, C_IDS: run-record walk + chunk expansion
 
 struct HostErr {
@@ -359,6 +359,10 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
         if (t == PQG_BOOLEAN) cls = C_BOOL;
         else if (t == PQG_BYTE_ARRAY) { cls = C_BINP; w.bin_kind = pqg::BIN_PLAIN; }
         else if (ew > 0) cls = C_PLAIN;
+        else herr = PQG_ERR_UNSUPPORTED;
+        break;
+      case PQG_RLE:  // Encoding.RLE values: BOOLEAN only (getMaxLevel :255-271)
+        if (t == PQG_BOOLEAN) cls = C_RLEBOOL;
         else herr = PQG_ERR_UNSUPPORTED;
         break;
       case PQG_DELTA_BINARY_PACKED:
@@ -628,6 +632,7 @@ int pqg_plan_launch(pqg_plan* P) {
         break;
       case C_PLAIN: e = pqg::launch_plain(0, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_BOOL: e = pqg::launch_plain(1, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_RLEBOOL: e = pqg::launch_plain(2, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_DELTA4: e = pqg::launch_delta(4, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_DELTA8: e = pqg::launch_delta(8, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
     }

@@ -1950,6 +1950,50 @@ __global__ __launch_bounds__(64 * WPB) void k_plain_bool(const uint8_t* __restri
   }
 }
 
+// BOOLEAN values with encoding RLE (Encoding.RLE.getValuesReader :116-124, getMaxLevel :255-271:
+// width 1 for BOOLEAN values; parquet-mr's V2 writer, DefaultV2ValuesWriterFactory
+// .getBooleanValuesWriter :77-84): RunLengthBitPackingHybridValuesReader.initFromPage :40-46 reads
+// a 4-byte LE length and slices the stream; readBoolean :58-60 = readInteger() != 0. The width-1
+// hybrid stream is decoded by the level-section decoder (same decoder class in the reference),
+// then an RLE run's unmasked repeated byte is folded to 0 / 1.
+__global__ __launch_bounds__(64 * WPB) void k_rle_bool(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                 const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                                 const int32_t* __restrict__ list, int n_list, uint64_t* err,
+                                                 uint32_t* err_count) {
+  __shared__ __attribute__((aligned(16))) LevelWaveLds lvl_lds[WPB];
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
+  const PageWork pw = work[page];
+  const ColumnDev cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint32_t beg = uni(pw.data_begin), size = uni(pw.size), n = uni(pw.n_values);
+  const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  int code = 0;
+  uint32_t b = 0, e = 0;
+  if ((uint64_t)beg + 4u > size) {
+    code = PQG_ERR_EOF;  // readIntLittleEndian
+  } else {
+    const int32_t len = (int32_t)uni(ld4_any(rs, beg));
+    if (len < 0) code = PQG_ERR_CORRUPT;  // sliceStream(negative)
+    else if ((uint64_t)beg + 4u + (uint32_t)len > size) code = PQG_ERR_EOF;
+    b = beg + 4u;
+    e = b + (uint32_t)len;
+  }
+  if (code) {
+    if (lane == 0) report(err, err_count, page, 0, 2, code);
+    return;
+  }
+  uint8_t* out = (uint8_t*)cd.values + pw.out_offset;
+  int c2 = 0;
+  const uint32_t done = decode_levels_w(lvl_lds[wave_id()], rs, b, e, 1, n, out, 1u, false, nullptr, &c2);
+  if (c2 && lane == 0) report(err, err_count, page, 2, done, c2);
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's stores are visible to its loads
+  for (uint32_t i = lane; i < done; i += WAVE) {
+    const uint8_t v = *(const volatile uint8_t*)(out + i);
+    if (v > 1u) gst(out + i, (uint8_t)1);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // DELTA_BINARY_PACKED (DeltaBinaryPackingValuesReader.initFromPage :59-77, eager):
 // the wave walks block headers (min delta, miniblock widths) into registers
@@ -2569,6 +2613,7 @@ hipError_t launch_plain(int kind, hipStream_t st, const uint8_t* bytes, uint64_t
                         const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
   if (n <= 0) return hipSuccess;
   if (kind == 1) hipLaunchKernelGGL(k_plain_bool, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
+  else if (kind == 2) hipLaunchKernelGGL(k_rle_bool, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   else hipLaunchKernelGGL(k_plain, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   return hipGetLastError();
 }

@@ -353,6 +353,10 @@ def write_column_chunk(physical_type, values, encoding, *, def_levels=None, rep_
             data = dba_encode(values[v0:v1])
         elif encoding == abi.BYTE_STREAM_SPLIT:
             data = bss_encode(values[v0:v1], physical_type, type_length)
+        elif encoding == abi.RLE and physical_type == abi.BOOLEAN:
+            # RunLengthBitPackingHybridValuesWriter(1).getBytes: 4-byte LE length + width-1 stream
+            rle = rle_encode(np.asarray(values[v0:v1], dtype=np.int32), 1)
+            data = len(rle).to_bytes(4, "little") + rle
         else:
             raise ValueError(f"writer does not support encoding {encoding}")
         rls = _level_section(rl[s:e], max_rep, version, level_encoding)

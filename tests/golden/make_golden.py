@@ -220,11 +220,38 @@ def write_arrow_snappy_fixtures():
     return out
 
 
-def add_snappy_fixtures():
-    """Append the SNAPPY fixtures to an existing manifest (the other fixtures untouched)."""
+def write_arrow_bool_rle_fixtures():
+    """BOOLEAN values with the RLE encoding (4-byte length + width-1 hybrid stream; what
+    parquet-mr's V2 writer emits for booleans, DefaultV2ValuesWriterFactory.getBooleanValuesWriter):
+    runs, random bits, optional with nulls, inside a list; V1 and V2 pages."""
+    rng = np.random.default_rng(91)
+    n = 20000
+    runs = np.minimum(rng.zipf(1.4, size=n), 3000)
+    runbits = np.repeat(rng.random(n) < 0.5, runs)[:n]
+    valid = rng.random(n) > 0.2
+    t = pa.table({
+        "bool_runs": pa.array(runbits),
+        "bool_rand": pa.array(rng.random(n) < 0.3),
+        "opt_bool": pa.array(rng.random(n) < 0.6, mask=~valid),
+        "list_bool": pa.array([None if rng.random() < 0.1 else
+                               [None if rng.random() < 0.1 else bool(x) for x in rng.random(rng.poisson(2)) < 0.5]
+                               for _ in range(n)]),
+    })
+    out = []
+    for ver in ("1.0", "2.0"):
+        name = f"arrow_bool_rle_v{ver[0]}"
+        pq.write_table(t, os.path.join(HERE, name + ".parquet"), data_page_version=ver, compression="NONE",
+                       use_dictionary=False, column_encoding={c: "RLE" for c in t.column_names},
+                       data_page_size=2 * 1024, row_group_size=n, write_page_index=False)
+        out.append(name)
+    return out
+
+
+def add_fixtures(writer_fn):
+    """Append the fixtures of one writer function to an existing manifest (the others untouched)."""
     with open(os.path.join(HERE, "manifest.json")) as f:
         manifest = json.load(f)
-    for name in write_arrow_snappy_fixtures():
+    for name in writer_fn():
         manifest[name] = {"source": "pyarrow " + pa.__version__, "chunks": describe(os.path.join(HERE, name + ".parquet"),
                                                                                    name, None)}
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
@@ -240,7 +267,8 @@ def main():
         dst = os.path.join(HERE, name + ".parquet")
         shutil.copyfile(src, dst)
         manifest[name] = {"source": f"reference:{rel}", "chunks": describe(dst, name, None)}
-    for name in write_arrow_fixtures() + write_arrow_binary_fixtures() + write_arrow_snappy_fixtures():
+    for name in (write_arrow_fixtures() + write_arrow_binary_fixtures() + write_arrow_snappy_fixtures() +
+                 write_arrow_bool_rle_fixtures()):
         manifest[name] = {"source": "pyarrow " + pa.__version__, "chunks": describe(os.path.join(HERE, name + ".parquet"),
                                                                                    name, None)}
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
@@ -249,4 +277,8 @@ def main():
 
 
 if __name__ == "__main__":
-    sys.exit(add_snappy_fixtures() if "--snappy" in sys.argv else main())
+    if "--snappy" in sys.argv:
+        sys.exit(add_fixtures(write_arrow_snappy_fixtures))
+    if "--bool-rle" in sys.argv:
+        sys.exit(add_fixtures(write_arrow_bool_rle_fixtures))
+    sys.exit(main())

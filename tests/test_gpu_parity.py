@@ -273,6 +273,50 @@ def test_error_delta_wide_miniblock(decoder):
     run_both(decoder, [ch], expect_error=True)
 
 
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("kind", ["runs", "random", "nulls"])
+def test_rle_boolean(decoder, version, kind):
+    # BOOLEAN values with encoding RLE (parquet-mr's V2 writer for booleans)
+    rng = np.random.default_rng(len(kind) * 10 + version)
+    n = 50_000
+    if kind == "runs":
+        vals = np.repeat(rng.random(2000) < 0.5, np.minimum(rng.zipf(1.3, size=2000), 5000))[:n]
+    else:
+        vals = rng.random(n) < 0.4
+    dl = nulls(len(vals), 0.25, seed=3) if kind == "nulls" else None
+    v = vals[dl.astype(bool)] if dl is not None else vals
+    ch = make(abi.BOOLEAN, v.astype(np.uint8), abi.RLE, def_levels=dl, max_def=1 if dl is not None else 0,
+              version=version, page_rows=7000)
+    run_both(decoder, [ch])
+
+
+def test_rle_boolean_unmasked_run_value(decoder):
+    # an RLE run's repeated byte is not masked to the width: readBoolean = (value != 0)
+    rle = bytes([20 << 1, 0x02, 10 << 1, 0x00, 5 << 1, 0xFF, 1 << 1 | 1, 0b10110010])  # 20 x 2, 10 x 0, 5 x 255, 8 bits
+    ch = make(abi.BOOLEAN, np.zeros(43, dtype=np.uint8), abi.RLE)
+    ch.pages[0].body = len(rle).to_bytes(4, "little") + rle
+    _, ref, _ = run_both(decoder, [ch])
+    assert list(ref.columns[0]["values"]) == [1] * 20 + [0] * 10 + [1] * 5 + [0, 1, 0, 0, 1, 1, 0, 1]
+
+
+@pytest.mark.parametrize("cut", [1, 2, 4, 9, 60])
+def test_error_rle_boolean_truncated(decoder, cut):
+    vals = (np.random.default_rng(cut).random(9000) < 0.5).astype(np.uint8)
+    ch = make(abi.BOOLEAN, vals, abi.RLE, page_rows=3000)
+    ch.pages[1].body = ch.pages[1].body[:max(0, len(ch.pages[1].body) - cut)]
+    run_both(decoder, [ch], expect_error=ref_errors(ch))
+
+
+def test_error_rle_boolean_length(decoder):
+    vals = (np.arange(3000) % 3 == 0).astype(np.uint8)
+    for bad in (-5, 10**6, 2):  # negative length, past the page, shorter than the values need
+        ch = make(abi.BOOLEAN, vals, abi.RLE, page_rows=1000)
+        body = bytearray(ch.pages[1].body)
+        body[0:4] = int(bad).to_bytes(4, "little", signed=True)
+        ch.pages[1].body = bytes(body)
+        run_both(decoder, [ch], expect_error=True)
+
+
 def test_error_missing_dictionary(decoder):
     ch = _dict_chunk()
     ch.dict_page = None
