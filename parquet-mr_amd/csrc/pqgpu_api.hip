@@ -8,11 +8,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "pqgpu_internal.h"
@@ -853,12 +855,56 @@ int pqg_decode(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, pqg_colum
   return rc;
 }
 
+// ---- host copies of the host path (pinned staging <-> caller arrays): one thread moves ~10 GB/s,
+// so large copies are spread over up to 8 threads, and the D2H of the outputs is issued in chunks
+// whose copies out of pinned memory start as each chunk lands.
+namespace {
+struct HostCopy {
+  uint8_t* dst;
+  uint64_t src;  // offset in the pinned buffer
+  uint64_t len;
+};
+constexpr uint64_t HOST_CHUNK = 32ull << 20;
+inline int host_threads(uint64_t bytes) {
+  const unsigned hw = std::thread::hardware_concurrency();
+  const uint64_t want = bytes / (8ull << 20) + 1;
+  return (int)std::min<uint64_t>({want, 8ull, hw ? (uint64_t)hw : 1ull});
+}
+// the parts of `jobs` inside [lo, hi) of the pinned buffer `base`
+void copy_range(const std::vector<HostCopy>& jobs, const uint8_t* base, uint64_t lo, uint64_t hi) {
+  for (const HostCopy& j : jobs) {
+    const uint64_t a = std::max(lo, j.src), b = std::min(hi, j.src + j.len);
+    if (a < b) std::memcpy(j.dst + (a - j.src), base + a, b - a);
+  }
+}
+void par_memcpy(void* dst, const void* src, uint64_t n) {
+  const int t = host_threads(n);
+  if (t <= 1) { std::memcpy(dst, src, n); return; }
+  std::vector<std::thread> th;
+  const uint64_t per = (n / (uint64_t)t + 4095) & ~4095ull;
+  for (int k = 0; k < t; k++) {
+    const uint64_t a = std::min(n, per * (uint64_t)k), b = std::min(n, a + per);
+    if (a < b) th.emplace_back([=] { std::memcpy((uint8_t*)dst + a, (const uint8_t*)src + a, b - a); });
+  }
+  for (auto& x : th) x.join();
+}
+}  // namespace
+
 int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
                     const pqg_page_desc* pages, int n_pages, uint32_t* h_page_value_counts, pqg_status* st) {
   if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
   if (!ctx || (n_bytes && !h_bytes) || n_cols < 0 || n_pages < 0) return PQG_ERR_INVALID_ARG;
   if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
   hipStream_t s = ctx->stream;
+  // PQG_HOST_TIMING=1: phase times of this call on stderr (diagnostics)
+  static const bool timing = std::getenv("PQG_HOST_TIMING") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char* what) {
+    if (!timing) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "pqg_decode_host %-10s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+    t_last = now;
+  };
   const uint64_t pad = 1024;
   const size_t nc = (size_t)std::max(n_cols, 1);
   std::vector<uint64_t> slots(nc, 0), page_bytes(nc, 0);
@@ -881,8 +927,9 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   }
   // host -> pinned -> device (the JNI shim hands heap bytes; the copy into pinned
   // memory is what a production shim does with direct ByteBuffers too)
-  std::memcpy(ctx->pin_in.p, h_bytes, n_bytes);
+  par_memcpy(ctx->pin_in.p, h_bytes, n_bytes);
   std::memset((uint8_t*)ctx->pin_in.p + n_bytes, 0, pad);
+  phase("stage-in");
   if (hipMemcpyAsync(ctx->host_bytes.p, ctx->pin_in.p, n_bytes + pad, hipMemcpyHostToDevice, s) != hipSuccess) return PQG_ERR_HIP;
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
   std::vector<uint64_t> off_v(nc), off_d(nc), off_r(nc), off_b(nc);
@@ -939,46 +986,78 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   }
   for (int i = 0; i < n_cols; i++) cols[i].values_written = dcols[(size_t)i].values_written;
   if (rc && st) *st = st2;
-  // device -> pinned -> host arrays (decoded values are valid up to the first error)
+  phase("h2d+decode");
+  // device -> pinned -> host arrays (decoded values are valid up to the first error): the D2H goes
+  // in HOST_CHUNK pieces, each followed by an event; worker threads copy the fixed-width values
+  // and levels out of each piece as it lands
   uint8_t* dout = (uint8_t*)ctx->host_out.p;
-  if (hipMemcpyAsync(ctx->pin_out.p, dout, total, hipMemcpyDeviceToHost, s) != hipSuccess) return PQG_ERR_HIP;
-  std::vector<uint32_t> counts((size_t)std::max(n_pages, 1));
-  if (n_pages && hipMemcpyAsync(counts.data(), ctx->host_counts.p, sizeof(uint32_t) * (size_t)n_pages, hipMemcpyDeviceToHost, s) != hipSuccess)
-    return PQG_ERR_HIP;
-  if (hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
   const uint8_t* po = (const uint8_t*)ctx->pin_out.p;
+  std::vector<HostCopy> jobs;
   for (int i = 0; i < n_cols; i++) {
-    int w = elem_width(cols[i].physical_type, cols[i].type_length);
-    uint64_t n = std::min<uint64_t>(cols[i].values_written, cols[i].values_capacity);
-    if (cols[i].physical_type == PQG_BYTE_ARRAY) {
-      // offsets[n + 1] and the bytes they span
-      n = std::min<uint64_t>(cols[i].values_written, cols[i].values_capacity ? cols[i].values_capacity - 1 : 0);
-      const int64_t* offs = (const int64_t*)(po + off_v[(size_t)i]);
-      if (cols[i].values && cols[i].values_capacity) std::memcpy(cols[i].values, offs, (n + 1) * sizeof(int64_t));
-      const uint64_t nb = (uint64_t)offs[n];
-      if (nb > cols[i].binary_capacity) {
-        if (rc == PQG_OK) {
-          rc = PQG_ERR_INVALID_ARG;
-          if (st) {
-            st->code = rc;
-            st->page = -1;
-            st->value_index = (int64_t)nb;
-            std::snprintf(st->message, sizeof(st->message), "binary capacity: column %d needs %llu bytes", i,
-                          (unsigned long long)nb);
-          }
-        }
-      } else if (cols[i].binary_data && nb) {
-        std::memcpy(cols[i].binary_data, po + off_b[(size_t)i], nb);
-      }
-    } else if (cols[i].values && n) {
-      std::memcpy(cols[i].values, po + off_v[(size_t)i], n * (uint64_t)w);
-    }
+    const int w = elem_width(cols[i].physical_type, cols[i].type_length);
+    const uint64_t n = std::min<uint64_t>(cols[i].values_written, cols[i].values_capacity);
+    if (cols[i].physical_type != PQG_BYTE_ARRAY && cols[i].values && n)
+      jobs.push_back({(uint8_t*)cols[i].values, off_v[(size_t)i], n * (uint64_t)w});
     if (cols[i].max_def > 0 && cols[i].def_levels)
-      std::memcpy(cols[i].def_levels, po + off_d[(size_t)i], std::min(slots[(size_t)i], cols[i].levels_capacity));
+      jobs.push_back({cols[i].def_levels, off_d[(size_t)i], std::min(slots[(size_t)i], cols[i].levels_capacity)});
     if (cols[i].max_rep > 0 && cols[i].rep_levels)
-      std::memcpy(cols[i].rep_levels, po + off_r[(size_t)i], std::min(slots[(size_t)i], cols[i].levels_capacity));
+      jobs.push_back({cols[i].rep_levels, off_r[(size_t)i], std::min(slots[(size_t)i], cols[i].levels_capacity)});
+  }
+  const uint64_t n_chunks = (total + HOST_CHUNK - 1) / HOST_CHUNK;
+  std::vector<hipEvent_t> ev((size_t)n_chunks, nullptr);
+  bool ok = true;
+  for (uint64_t k = 0; k < n_chunks && ok; k++) {
+    const uint64_t a = k * HOST_CHUNK, len = std::min(HOST_CHUNK, total - a);
+    ok = hipMemcpyAsync((uint8_t*)ctx->pin_out.p + a, dout + a, len, hipMemcpyDeviceToHost, s) == hipSuccess &&
+         hipEventCreateWithFlags(&ev[(size_t)k], hipEventDisableTiming) == hipSuccess &&
+         hipEventRecord(ev[(size_t)k], s) == hipSuccess;
+  }
+  std::vector<uint32_t> counts((size_t)std::max(n_pages, 1));
+  if (ok && n_pages)
+    ok = hipMemcpyAsync(counts.data(), ctx->host_counts.p, sizeof(uint32_t) * (size_t)n_pages, hipMemcpyDeviceToHost, s) == hipSuccess;
+  if (ok) {
+    const int T = std::max(1, std::min<int>(host_threads(total), (int)n_chunks));
+    std::vector<int> wok((size_t)T, 1);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+      th.emplace_back([&, t] {
+        if (hipSetDevice(ctx->device) != hipSuccess) { wok[(size_t)t] = 0; return; }
+        for (uint64_t k = (uint64_t)t; k < n_chunks; k += (uint64_t)T) {
+          if (hipEventSynchronize(ev[(size_t)k]) != hipSuccess) { wok[(size_t)t] = 0; return; }
+          copy_range(jobs, po, k * HOST_CHUNK, std::min(total, (k + 1) * HOST_CHUNK));
+        }
+      });
+    for (auto& x : th) x.join();
+    for (int v : wok) ok = ok && v;
+  }
+  for (hipEvent_t e : ev)
+    if (e) (void)hipEventDestroy(e);
+  if (!ok || hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
+  phase("d2h+copy");
+  for (int i = 0; i < n_cols; i++) {
+    if (cols[i].physical_type != PQG_BYTE_ARRAY) continue;
+    // offsets[n + 1] and the bytes they span
+    const uint64_t n = std::min<uint64_t>(cols[i].values_written, cols[i].values_capacity ? cols[i].values_capacity - 1 : 0);
+    const int64_t* offs = (const int64_t*)(po + off_v[(size_t)i]);
+    if (cols[i].values && cols[i].values_capacity) par_memcpy(cols[i].values, offs, (n + 1) * sizeof(int64_t));
+    const uint64_t nb = (uint64_t)offs[n];
+    if (nb > cols[i].binary_capacity) {
+      if (rc == PQG_OK) {
+        rc = PQG_ERR_INVALID_ARG;
+        if (st) {
+          st->code = rc;
+          st->page = -1;
+          st->value_index = (int64_t)nb;
+          std::snprintf(st->message, sizeof(st->message), "binary capacity: column %d needs %llu bytes", i,
+                        (unsigned long long)nb);
+        }
+      }
+    } else if (cols[i].binary_data && nb) {
+      par_memcpy(cols[i].binary_data, po + off_b[(size_t)i], nb);
+    }
   }
   if (h_page_value_counts && n_pages) std::memcpy(h_page_value_counts, counts.data(), sizeof(uint32_t) * (size_t)n_pages);
+  phase("binary");
   return rc;
 }
 

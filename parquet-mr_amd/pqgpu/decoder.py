@@ -11,6 +11,7 @@ the same sequence the reference's ValuesReader / ColumnReader return
 torch is used only for device memory and the stream handle.
 """
 import ctypes as C
+import time
 
 import numpy as np
 import torch
@@ -329,20 +330,22 @@ class Decoder:
             col.n_values = batch.column_values[i]
         return Plan(self, h, cols, descs, (pages, dbatch))
 
-    def decode_host(self, batch, binary_capacity=None):
+    def decode_host(self, batch, binary_capacity=None, prefault=False):
         """File bytes in, host arrays out (pqg_decode_host): the JNI shim's path. BYTE_ARRAY
         columns come back as lists of bytes (plus "offsets"); a short host byte buffer is
-        grown to the size the library reports and the call repeated once."""
+        grown to the size the library reports and the call repeated once. prefault=True writes
+        the output arrays before the call (a Java `new long[n]` is zeroed, i.e. touched, when it
+        is allocated); self.last_native_s = seconds inside the last pqg_decode_host call."""
         caps = {i: binary_capacity or self.binary_estimate(batch, i) for i, cd in enumerate(batch.columns)
                 if cd["physical_type"] == abi.BYTE_ARRAY}
         for _ in range(2):
-            rc, st, res, counts, need = self._decode_host_once(batch, caps)
+            rc, st, res, counts, need = self._decode_host_once(batch, caps, prefault)
             if not need:
                 break
             caps.update(need)
         return rc, st, res, counts
 
-    def _decode_host_once(self, batch, caps):
+    def _decode_host_once(self, batch, caps, prefault=False):
         descs = (abi.ColumnDesc * max(1, len(batch.columns)))()
         outs = []
         for i, cd in enumerate(batch.columns):
@@ -355,6 +358,10 @@ class Decoder:
             dl = np.zeros(max(n, 1), dtype=np.uint8)
             rl = np.zeros(max(n, 1), dtype=np.uint8)
             bd = np.zeros(max(caps.get(i, 0), 1), dtype=np.uint8) if binary else None
+            if prefault:
+                for a in (vals, dl if cd["max_def"] > 0 else None, rl if cd["max_rep"] > 0 else None, bd):
+                    if a is not None:
+                        a.view(np.uint8)[::4096] = 0
             c.values = vals.ctypes.data
             c.values_capacity = n + 1 if binary else n
             c.def_levels = dl.ctypes.data if cd["max_def"] > 0 else None
@@ -367,9 +374,11 @@ class Decoder:
         counts = np.zeros(max(1, batch.n_pages), dtype=np.uint32)
         pages = np.ascontiguousarray(batch.pages)
         st = abi.Status()
+        t0 = time.perf_counter()
         rc = native.lib().pqg_decode_host(self.ctx, batch.data.ctypes.data, batch.data.size, C.addressof(descs),
                                           len(batch.columns), pages.ctypes.data if len(pages) else None, len(pages),
                                           counts.ctypes.data, C.byref(st))
+        self.last_native_s = time.perf_counter() - t0
         need = {}
         if rc == abi.ERR_INVALID_ARG and st.page == -1 and st.message.startswith(b"binary capacity"):
             need[int(st.message.split()[3])] = int(st.value_index)

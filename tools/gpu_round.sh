@@ -3,7 +3,7 @@
 # then separate PMC passes for HBM traffic. Every GPU step has its own time limit and
 # the script stops at the first failure (no retries).
 # Usage (from the repo root, via gpurun): bash tools/gpu_round.sh <tag> [steps...]
-#   steps: tests smoke bench bench2 prof pmc   (default: tests smoke bench prof pmc)
+#   steps: tests smoke bench e2e bench2 suite suiteprof prof pmc   (default: tests smoke bench prof pmc)
 set -euo pipefail
 TAG=${1:-run}; shift || true
 STEPS=${*:-tests smoke bench prof pmc}
@@ -24,6 +24,10 @@ for s in $STEPS; do
       timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
         || { tail -30 "$OUT/bench.err"; exit 1; }
       cat "$OUT/bench.json" ;;
+    e2e)
+      timeout -k 10 400 python -u bench.py --no-cpu --e2e --steps 5 > "$OUT/bench_e2e.json" 2> "$OUT/bench_e2e.err" \
+        || { tail -30 "$OUT/bench_e2e.err"; exit 1; }
+      cat "$OUT/bench_e2e.json" ;;
     bench2)
       timeout -k 10 400 python -u bench.py --no-cpu --zipf 2.0 > "$OUT/bench_zipf2.json" 2> "$OUT/bench_zipf2.err" \
         || { tail -30 "$OUT/bench_zipf2.err"; exit 1; }
