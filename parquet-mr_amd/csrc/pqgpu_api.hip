@@ -154,6 +154,7 @@ struct pqg_ctx {
   PinnedBuf pin_in, pin_out, pin_err;
   DevBuf host_bytes, host_out, host_counts, host_runs;
   DevBuf asm_scratch;                // pqg_assemble: block counts + totals
+  hipStream_t copy_stream = nullptr; // pqg_decode_host: second D2H queue (odd output chunks)
 };
 
 extern "C" {
@@ -225,6 +226,10 @@ int pqg_ctx_destroy(pqg_ctx* c) {
   c->host_counts.release();
   c->host_runs.release();
   c->asm_scratch.release();
+  if (c->copy_stream) {
+    (void)hipStreamSynchronize(c->copy_stream);
+    (void)hipStreamDestroy(c->copy_stream);
+  }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return PQG_OK;
@@ -1006,11 +1011,22 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   const uint64_t n_chunks = (total + HOST_CHUNK - 1) / HOST_CHUNK;
   std::vector<hipEvent_t> ev((size_t)n_chunks, nullptr);
   bool ok = true;
+  // odd chunks on a second stream (a second DMA queue), after the decode
+  hipStream_t s2 = s;
+  hipEvent_t dec_done = nullptr;
+  if (n_chunks > 1) {
+    if (!ctx->copy_stream && hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess)
+      ctx->copy_stream = nullptr;
+    if (ctx->copy_stream && hipEventCreateWithFlags(&dec_done, hipEventDisableTiming) == hipSuccess &&
+        hipEventRecord(dec_done, s) == hipSuccess && hipStreamWaitEvent(ctx->copy_stream, dec_done, 0) == hipSuccess)
+      s2 = ctx->copy_stream;
+  }
   for (uint64_t k = 0; k < n_chunks && ok; k++) {
     const uint64_t a = k * HOST_CHUNK, len = std::min(HOST_CHUNK, total - a);
-    ok = hipMemcpyAsync((uint8_t*)ctx->pin_out.p + a, dout + a, len, hipMemcpyDeviceToHost, s) == hipSuccess &&
+    hipStream_t sk = (k & 1) ? s2 : s;
+    ok = hipMemcpyAsync((uint8_t*)ctx->pin_out.p + a, dout + a, len, hipMemcpyDeviceToHost, sk) == hipSuccess &&
          hipEventCreateWithFlags(&ev[(size_t)k], hipEventDisableTiming) == hipSuccess &&
-         hipEventRecord(ev[(size_t)k], s) == hipSuccess;
+         hipEventRecord(ev[(size_t)k], sk) == hipSuccess;
   }
   std::vector<uint32_t> counts((size_t)std::max(n_pages, 1));
   if (ok && n_pages)
@@ -1030,8 +1046,10 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
     for (auto& x : th) x.join();
     for (int v : wok) ok = ok && v;
   }
+  if (s2 != s && hipStreamSynchronize(s2) != hipSuccess) ok = false;
   for (hipEvent_t e : ev)
     if (e) (void)hipEventDestroy(e);
+  if (dec_done) (void)hipEventDestroy(dec_done);
   if (!ok || hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
   phase("d2h+copy");
   for (int i = 0; i < n_cols; i++) {
