@@ -255,43 +255,43 @@ __global__ __launch_bounds__(WAVE) void k_snappy(const uint8_t* __restrict__ src
       sv[j] = b < T ? sS[b] : SN_LIT;
     }
 #pragma unroll 1
-    for (uint32_t r = 0; r < 12u; r++) {
+    for (uint32_t r = 0; r < 12u; r++) {  // branch-free rounds (the index is clamped to the table)
       bool more = false, hop = false;
 #pragma unroll
       for (uint32_t j = 0; j < NB; j++) {
-        if (!(sv[j] & SN_LIT) && sv[j] >= op) {
-          sv[j] = sS[sv[j] - op];
-          hop = true;
-          more |= !(sv[j] & SN_LIT) && sv[j] >= op;
-        }
+        const bool inb = !(sv[j] & SN_LIT) && sv[j] >= op;
+        const uint32_t nv = sS[(sv[j] - op) & (SN_CAP - 1u)];
+        sv[j] = inb ? nv : sv[j];
+        hop |= inb;
+        more |= inb && !(nv & SN_LIT) && nv >= op;
       }
       if (!__ballot(hop)) break;
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (uint32_t j = 0; j < NB; j++) {
-        const uint32_t b = lane + WAVE * j;
-        if (b < T) sS[b] = sv[j];
-      }
+      for (uint32_t j = 0; j < NB; j++) sS[lane + WAVE * j] = sv[j];  // entries >= T hold SN_LIT
       wave_sync();
       if (!__ballot(more)) break;
     }
     // ---- the bytes: literal bytes from the segment, earlier output from the ring, or (older than
     // the ring) from HBM after the earlier batches' stores have drained
-    bool far = false;
-#pragma unroll
-    for (uint32_t j = 0; j < NB; j++) far |= !(sv[j] & SN_LIT) && (uint64_t)sv[j] + SN_RING < (uint64_t)fend + WAVE;
-    if (__ballot(far)) __builtin_amdgcn_s_waitcnt(0);
     uint32_t bv[NB];
+    bool far = false;
 #pragma unroll
     for (uint32_t j = 0; j < NB; j++) {
       const uint32_t v = sv[j];
-      if (v & SN_LIT) {
-        bv[j] = seg[v & (SN_SEG - 1u)];
-      } else if ((uint64_t)v + SN_RING < (uint64_t)fend + WAVE) {
-        const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(v & ~3u), 0, 0);
-        bv[j] = (w >> ((v & 3u) * 8u)) & 0xFFu;
-      } else {
-        bv[j] = ring[v & SN_RMASK];
+      const uint32_t lit = seg[v & (SN_SEG - 1u)], rg = ring[v & SN_RMASK];
+      bv[j] = (v & SN_LIT) ? lit : rg;
+      far |= !(v & SN_LIT) && (uint64_t)v + SN_RING < (uint64_t)fend + WAVE;
+    }
+    if (__ballot(far)) {
+      __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+      for (uint32_t j = 0; j < NB; j++) {
+        const uint32_t v = sv[j];
+        if (!(v & SN_LIT) && (uint64_t)v + SN_RING < (uint64_t)fend + WAVE) {
+          const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(v & ~3u), 0, 0);
+          bv[j] = (w >> ((v & 3u) * 8u)) & 0xFFu;
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
