@@ -264,7 +264,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_bytes_per_launch": traffic_bytes, "traffic_source": traffic_src,
-                         "kernel": "pqg::k_dict_fused<8> (avg_launch_ms: whole plan launch incl. error-word memsets)", "algorithmic_bytes_per_launch": algo_bytes,
+                         "kernel": "pqg::k_dict_fused<8> (avg_launch_ms: whole plan launch, one dispatch, incl. the ~6 us dispatch-to-dispatch gap)", "algorithmic_bytes_per_launch": algo_bytes,
                          "avg_launch_ms": avg_launch_s * 1e3},
             "cpu_baseline": cpu,
             "input_gen_s": t_gen,

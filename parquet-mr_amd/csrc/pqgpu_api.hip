@@ -116,6 +116,7 @@ struct pqg_plan {
   DevBuf rec, chunk_run, chunks;      // dictionary pages: run records, chunk -> record, chunk work list
   DevBuf pstat, flags;                // per page: {records, values} and ready epoch (fused dictionary kernel)
   uint32_t epoch = 0;
+  uint32_t err_epoch = pqg::ERR_EPOCH_MAX;  // error-word epoch of the last launch (first launch wraps: zeroes the region)
   bool dict_fused = true;
   uint32_t chunk_off[N_DICT_CLS] = {0, 0, 0}, chunk_n[N_DICT_CLS] = {0, 0, 0};  // ranges in `chunks`
   // BYTE_ARRAY / fixed-width-dictionary scratch (ColumnDev::blen, bsrc, dict_len, dict_src, block_sums,
@@ -582,14 +583,17 @@ int pqg_plan_launch(pqg_plan* P) {
   pqg_ctx* ctx = P->ctx;
   hipStream_t s = ctx->stream;
   uint64_t* err = (uint64_t*)P->err.p;
-  // error words and the error counter share one allocation and one 0xFF memset per launch: the
-  // counter starts at 0xFFFFFFFF and report() increments it (wraps), so "no error" is 0xFFFFFFFF
+  // error words and the error counter share one allocation; both are tagged with the launch's
+  // error epoch (pqg::ErrCount), so the region is zeroed only when the epoch wraps
   const size_t err_bytes = err_region_bytes(P->n_pages, P->n_cols);
-  uint32_t* ecount = (uint32_t*)((uint8_t*)P->err.p + err_bytes);
+  if (++P->err_epoch > pqg::ERR_EPOCH_MAX) {
+    P->err_epoch = 1;
+    if (hipMemsetAsync(P->err.p, 0, err_bytes + 16, s) != hipSuccess) return PQG_ERR_HIP;
+  }
+  const pqg::ErrCount ecount{(uint32_t*)((uint8_t*)P->err.p + err_bytes), P->err_epoch};
   PageWork* work = (PageWork*)P->work.p;
   const ColumnDev* cols = (const ColumnDev*)P->cols.p;
   const int32_t* lists = (const int32_t*)P->lists.p;
-  if (hipMemsetAsync(err, 0xFF, err_bytes + 16, s) != hipSuccess) return PQG_ERR_HIP;
   if (P->blen_bytes && hipMemsetAsync(P->bscratch.p, 0, P->blen_bytes, s) != hipSuccess) return PQG_ERR_HIP;
   for (void* v : P->empty_bin_values)
     if (hipMemsetAsync(v, 0, sizeof(int64_t), s) != hipSuccess) return PQG_ERR_HIP;
@@ -715,9 +719,11 @@ int resolve_errors(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work_out)
   }
   if (hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
   std::vector<uint64_t> errs;
-  if (*cnt != 0xFFFFFFFFu) {  // the counter starts at 0xFFFFFFFF (see pqg_plan_launch)
+  if (*cnt == P->err_epoch) {  // a kernel of the last launch reported (see pqg::ErrCount)
     errs.resize(3 * (size_t)(P->n_pages + std::max(P->n_cols, 1)));
     if (hipMemcpy(errs.data(), P->err.p, sizeof(uint64_t) * errs.size(), hipMemcpyDeviceToHost) != hipSuccess) return PQG_ERR_HIP;
+    for (uint64_t& w : errs)  // words of earlier launches are stale: no error in this one
+      w = (w >> 48) == P->err_epoch ? (~w & pqg::ERR_KEY_MASK) : ~0ull;
   }
   int rc = resolve_page_errors(P, st, errs);
   if (rc) return rc;

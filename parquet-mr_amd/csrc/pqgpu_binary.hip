@@ -29,7 +29,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
                                                   const PageWork* __restrict__ work,
                                                   const ColumnDev* __restrict__ cols,
                                                   const int32_t* __restrict__ list, int n_list, uint64_t* err,
-                                                  uint32_t* err_count) {
+                                                  ErrCount err_count) {
   const int page = wave_page(list, n_list);
   if (page < 0) return;
   const PageWork pw = work[page];
@@ -139,7 +139,7 @@ __device__ __forceinline__ int bin_value_error(rsrc_t rs, uint32_t p, uint32_t e
 // stores would wait for them (vmcnt counts stores), so every window costs one memory latency,
 // not two.
 __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, uint32_t N, uint32_t* out_len,
-                         uint32_t* out_src, bool dict, int page, int kind, uint64_t* err, uint32_t* err_count) {
+                         uint32_t* out_src, bool dict, int page, int kind, uint64_t* err, ErrCount err_count) {
   const uint32_t lane = lane_id();
   uint32_t pos = uni(beg), produced = 0;
   int code = 0;
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_walk(const uint8_t* __restrict
                                                        const PageWork* __restrict__ work,
                                                        const ColumnDev* __restrict__ cols,
                                                        const int32_t* __restrict__ list, int n_list, int dict_walk,
-                                                       int n_pages, uint64_t* err, uint32_t* err_count) {
+                                                       int n_pages, uint64_t* err, ErrCount err_count) {
   __shared__ BinWalkLds lds_all[WPB];
   const int item = wave_page(list, n_list);
   if (item < 0) return;
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
                                                        const PageWork* __restrict__ work,
                                                        const ColumnDev* __restrict__ cols,
                                                        const uint64_t* __restrict__ chunks, uint32_t n_chunks,
-                                                       uint64_t* err, uint32_t* err_count) {
+                                                       uint64_t* err, ErrCount err_count) {
   __shared__ uint64_t off_all[WPB][BIN_CHUNK + 1];
   __shared__ uint32_t src_all[WPB][BIN_CHUNK];
   const uint32_t c = blockIdx.x * WPB + wave_id();
@@ -949,7 +949,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chunks(const uint8_t* __restri
 #define PQG_BIN_ARGS bytes, n_bytes, work, cols, list, n, err, err_count
 
 hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
-                      const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+                      const int32_t* list, int n, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_bss, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_BIN_ARGS);
   return hipGetLastError();
@@ -957,7 +957,7 @@ hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, Pa
 
 hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, int dict_walk, int n_pages,
-                           uint64_t* err, uint32_t* err_count) {
+                           uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_bin_walk, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, list, n,
                      dict_walk, n_pages, err, err_count);
@@ -1003,7 +1003,7 @@ hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
 
 hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const uint64_t* chunks, uint32_t n_chunks, uint64_t* err,
-                           uint32_t* err_count) {
+                           ErrCount err_count) {
   if (n_chunks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_bin_copy, dim3((n_chunks + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols,
                      chunks, n_chunks, err, err_count);

@@ -182,11 +182,14 @@ __device__ __forceinline__ uint32_t ld4_any(rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_alignbyte(ld32(r, a + 4), ld32(r, a), sb);
 }
 
-// Record an error: smallest (index << 8 | code) per (page, kind) wins.
-__device__ __forceinline__ void report(uint64_t* err, uint32_t* err_count, int page, int kind, uint64_t index,
+// Record an error: smallest (index << 8 | code) per (page, kind) wins (epoch-tagged, see ErrCount).
+__device__ __forceinline__ void report_key(uint64_t* word, ErrCount err_count, uint64_t key) {
+  atomicMax((unsigned long long*)word, (unsigned long long)(((uint64_t)err_count.epoch << 48) | (~key & ERR_KEY_MASK)));
+  atomicMax(err_count.p, err_count.epoch);
+}
+__device__ __forceinline__ void report(uint64_t* err, ErrCount err_count, int page, int kind, uint64_t index,
                                        int code) {
-  atomicMin((unsigned long long*)&err[3 * (uint64_t)page + kind], (unsigned long long)((index << 8) | (uint64_t)code));
-  atomicAdd(err_count, 1u);
+  report_key(&err[3 * (uint64_t)page + kind], err_count, (index << 8) | (uint64_t)code);
 }
 
 // ---------------------------------------------------------------------------

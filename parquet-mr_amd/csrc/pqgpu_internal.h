@@ -59,6 +59,18 @@ struct PageWork {
   uint32_t reserved;
 };
 
+// Error counter handle passed to every kernel. Error words and the counter are tagged with the
+// plan's launch epoch (1..ERR_EPOCH_MAX) instead of being re-initialised each launch: a word
+// holds (epoch << 48) | (~key & ERR_KEY_MASK) and is raised with atomicMax, so the newest epoch
+// wins and, inside one epoch, the smallest key (index << 8 | code); the counter holds the epoch
+// of the last launch that reported. The region is zeroed only when the epoch wraps.
+struct ErrCount {
+  uint32_t* p;
+  uint32_t epoch;
+};
+constexpr uint32_t ERR_EPOCH_MAX = 0xFFFFu;
+constexpr uint64_t ERR_KEY_MASK = (1ull << 48) - 1;
+
 enum BinKind : uint32_t { BIN_PLAIN = 0, BIN_DLBA = 1, BIN_DICT = 2, BIN_DBA = 3 };
 
 // Output chunk of k_dict_expand: CH_TILES x 64 lanes x 16 bytes.
@@ -71,24 +83,24 @@ inline uint32_t dict_chunk_values(int elem_width) { return DICT_CHUNK_TILES * 64
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                        const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                       bool fused, uint64_t* err, uint32_t* err_count);
+                       bool fused, uint64_t* err, ErrCount err_count);
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
-                         const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+                         const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_scan(hipStream_t st, PageWork* work, const int32_t* col_pages, const int32_t* col_page_start,
                        int n_cols);
 hipError_t launch_plain(int kind, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 // dictionary kernels: MODE 0 = values of a 4/8-byte dictionary; MODE 1 = the ids themselves
 // (u32, into ColumnDev::blen) for BYTE_ARRAY / FIXED_LEN_BYTE_ARRAY / INT96 dictionaries
 hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                            const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
-                           uint32_t epoch, bool fused, uint64_t* err, uint32_t* err_count);
+                           uint32_t epoch, bool fused, uint64_t* err, ErrCount err_count);
 // DELTA_LENGTH_BYTE_ARRAY lengths (k_delta into blen, records PageWork::aux)
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                               const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+                               const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 // pqgpu_snappy.hip: one wave per raw Snappy block (jobs: pqg_snappy_job, device array)
 hipError_t launch_snappy(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
                          const void* jobs, int n_jobs, int32_t* status);
@@ -97,7 +109,7 @@ hipError_t launch_snappy(hipStream_t st, const uint8_t* src, uint64_t src_bytes,
 // PageWork::reserved = 1 when a value is longer than DBA_VB: that page takes the serial copy)
 constexpr uint32_t DBA_VB = 2048;  // LDS bytes of one value buffer of the DELTA_BYTE_ARRAY copy
 hipError_t launch_dba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                              const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count,
+                              const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count,
                               uint32_t* dba_meta);
 // DELTA_BYTE_ARRAY value bytes: chunk tails, per-page chain of chunk tails, chunk copies, serial
 // copy of the pages with long values
@@ -108,10 +120,10 @@ hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
 constexpr uint32_t BIN_CHUNK = 256;     // values per k_bin_copy chunk
 constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block
 hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
-                      const int32_t* list, int n, uint64_t* err, uint32_t* err_count);
+                      const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, int dict_walk, int n_pages,
-                           uint64_t* err, uint32_t* err_count);
+                           uint64_t* err, ErrCount err_count);
 hipError_t launch_bin_dict_map(hipStream_t st, PageWork* work, const ColumnDev* cols, const int32_t* list, int n);
 hipError_t launch_gather_fixed(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n);
@@ -119,7 +131,7 @@ hipError_t launch_bin_scan(hipStream_t st, const ColumnDev* cols, const int32_t*
                            const uint64_t* blocks, uint32_t n_blocks);
 hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const uint64_t* chunks, uint32_t n_chunks, uint64_t* err,
-                           uint32_t* err_count);
+                           ErrCount err_count);
 // pqgpu_assembly.hip: levels -> offsets / validity of one leaf column's path
 constexpr uint32_t ASM_MAX_DEPTHS = 8;  // repetition depths 0..7 (max_rep <= 7)
 constexpr uint32_t ASM_MAX_NODES = 16;  // path length

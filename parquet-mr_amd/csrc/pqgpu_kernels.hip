@@ -460,7 +460,7 @@ __device__ __forceinline__ uint32_t chunk_values(uint32_t E) { return CH_TILES *
 template <int W, bool SMALL>
 __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg, uint32_t sec_end,
                                           int w, uint64_t* rec, uint32_t* chunk_run, uint32_t CH, uint32_t sh, int page,
-                                          uint64_t* err, uint32_t* err_count, uint32_t& n_rec, uint32_t& n_ok) {
+                                          uint64_t* err, ErrCount err_count, uint32_t& n_rec, uint32_t& n_ok) {
   const uint32_t lane = lane_id();
   uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
   uint32_t produced = 0;       // values covered by the runs read so far
@@ -573,7 +573,7 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
 template <int W>
 __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg,
                                              uint32_t sec_end, int w, uint64_t* rec, uint32_t* chunk_run,
-                                             uint32_t CH, uint32_t sh, int page, uint64_t* err, uint32_t* err_count,
+                                             uint32_t CH, uint32_t sh, int page, uint64_t* err, ErrCount err_count,
                                              uint32_t& n_rec, uint32_t& n_ok) {
   const uint32_t lane = lane_id();
   // successor table (256 x u16) and reached flags (256 x u8) over L.ent; every access goes
@@ -786,7 +786,7 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
                                                const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                const int32_t* __restrict__ list, int n_list, uint64_t* rec,
                                                uint32_t* chunk_run, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                                               uint64_t* err, uint32_t* err_count, uint8_t* lds, uint32_t group) {
+                                               uint64_t* err, ErrCount err_count, uint8_t* lds, uint32_t group) {
   DictWaveLds& L = ((DictWaveLds*)lds)[wave_id()];
   const int i_page = (int)(group * WPB + wave_id());
   if (i_page >= n_list) return;
@@ -839,7 +839,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_runs(const uint8_t* __restric
                                                         const ColumnDev* __restrict__ cols,
                                                         const int32_t* __restrict__ list, int n_list, uint64_t* rec,
                                                         uint32_t* chunk_run, uint64_t* pstat, uint32_t* flags,
-                                                        uint32_t epoch, uint64_t* err, uint32_t* err_count) {
+                                                        uint32_t epoch, uint64_t* err, ErrCount err_count) {
   __shared__ __attribute__((aligned(16))) DictWaveLds wl_all[WPB];
   dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
                     (uint8_t*)wl_all, blockIdx.x);
@@ -878,7 +878,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
                                                 const uint64_t* rec, const uint32_t* chunk_run,
                                                 const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                 const uint64_t* pstat, const uint32_t* flags, uint32_t epoch,
-                                                uint64_t* err, uint32_t* err_count, uint8_t* lds, uint32_t group) {
+                                                uint64_t* err, ErrCount err_count, uint8_t* lds, uint32_t group) {
   typedef typename DictVal<W>::T T;
   constexpr uint32_t E = 16 / W;
   constexpr uint32_t TV = WAVE * E;  // values per tile
@@ -1124,7 +1124,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restri
                                                          const ColumnDev* __restrict__ cols, const uint64_t* rec,
                                                          const uint32_t* chunk_run, const uint64_t* __restrict__ chunks,
                                                          uint32_t n_chunks, const uint64_t* pstat, uint64_t* err,
-                                                         uint32_t* err_count) {
+                                                         ErrCount err_count) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[XT_LDS_BYTES];
   dict_tiles_body<W, false, IDS>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, nullptr, 0,
                                  err, err_count, lds, blockIdx.x);
@@ -1140,7 +1140,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restri
                                                          uint32_t n_walk, uint64_t* rec, uint32_t* chunk_run,
                                                          const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                          uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                                                         uint64_t* err, uint32_t* err_count) {
+                                                         uint64_t* err, ErrCount err_count) {
   constexpr uint32_t LB = sizeof(DictWaveLds) * WPB > XT_LDS_BYTES ? sizeof(DictWaveLds) * WPB : XT_LDS_BYTES;
   __shared__ __attribute__((aligned(16))) uint8_t lds[LB];
   if (blockIdx.x < n_walk)
@@ -1719,7 +1719,7 @@ __device__ __forceinline__ uint32_t decode_levels_w(LevelWaveLds& L, rsrc_t rs, 
 __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                 PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                 const int32_t* __restrict__ list, int n_list, uint64_t* err,
-                                                uint32_t* err_count) {
+                                                ErrCount err_count) {
   __shared__ __attribute__((aligned(16))) LevelWaveLds lvl_lds[WPB];
   const int page = wave_page(list, n_list);
   if (page < 0) return;
@@ -1823,8 +1823,7 @@ __global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__
   if (lane == 0) {
     if (lvl_err_key != ~0ull) {
       // level error key: slot << 1 | (0 = rl, 1 = dl) — host decodes it
-      atomicMin((unsigned long long*)&err[3 * (uint64_t)page + 1], (unsigned long long)lvl_err_key);
-      atomicAdd(err_count, 1u);
+      report_key(&err[3 * (uint64_t)page + 1], err_count, lvl_err_key);
     }
     work[page].n_values = nonnull;
     work[page].data_begin = data_beg;
@@ -1867,7 +1866,7 @@ __global__ __launch_bounds__(256) void k_scan_offsets(PageWork* __restrict__ wor
 __global__ __launch_bounds__(64 * WPB) void k_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                               const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                               const int32_t* __restrict__ list, int n_list, uint64_t* err,
-                                              uint32_t* err_count) {
+                                              ErrCount err_count) {
   const int page = wave_page(list, n_list);
   if (page < 0) return;
   const PageWork pw = work[page];
@@ -1929,7 +1928,7 @@ __global__ __launch_bounds__(64 * WPB) void k_plain(const uint8_t* __restrict__ 
 __global__ __launch_bounds__(64 * WPB) void k_plain_bool(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                    const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                    const int32_t* __restrict__ list, int n_list, uint64_t* err,
-                                                   uint32_t* err_count) {
+                                                   ErrCount err_count) {
   const int page = wave_page(list, n_list);
   if (page < 0) return;
   const PageWork pw = work[page];
@@ -1959,7 +1958,7 @@ __global__ __launch_bounds__(64 * WPB) void k_plain_bool(const uint8_t* __restri
 __global__ __launch_bounds__(64 * WPB) void k_rle_bool(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                  const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                  const int32_t* __restrict__ list, int n_list, uint64_t* err,
-                                                 uint32_t* err_count) {
+                                                 ErrCount err_count) {
   __shared__ __attribute__((aligned(16))) LevelWaveLds lvl_lds[WPB];
   const int page = wave_page(list, n_list);
   if (page < 0) return;
@@ -2087,7 +2086,7 @@ __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_
                                              uint32_t b_lo, uint32_t b_hi, uint32_t b_nmb, uint32_t blk_first,
                                              uint32_t block, uint32_t mbs, uint32_t n_out, uint64_t& carry,
                                              typename DictVal<W>::T* out, int page, uint64_t* err,
-                                             uint32_t* err_count) {
+                                             ErrCount err_count) {
   typedef typename DictVal<W>::T T;
   const uint32_t lane = lane_id();
   const uint32_t j0 = lane * E;
@@ -2170,7 +2169,7 @@ __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_
 template <int W, bool NEG>
 __device__ int delta_generic(const rsrc_t rs, uint32_t p, uint32_t end, uint32_t block, uint32_t mbn, uint32_t mbs,
                              uint32_t total, uint32_t n_out, uint64_t carry, typename DictVal<W>::T* out, int page,
-                             uint64_t* err, uint32_t* err_count, uint32_t* p_end) {
+                             uint64_t* err, ErrCount err_count, uint32_t* p_end) {
   typedef typename DictVal<W>::T T;
   const uint32_t lane = lane_id();
   auto byte_at = [&](uint32_t a) -> uint32_t { return uni((ld32(rs, a & ~3u) >> (8u * (a & 3u))) & 0xFFu); };
@@ -2252,7 +2251,7 @@ __device__ int delta_generic(const rsrc_t rs, uint32_t p, uint32_t end, uint32_t
 // its index and written as 0 (DELTA_LENGTH_BYTE_ARRAY lengths: in.slice(negative)).
 template <int W, bool NEG>
 __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, typename DictVal<W>::T* out,
-                            int page, uint64_t* err, uint32_t* err_count, uint32_t* p_end, uint32_t* total_out) {
+                            int page, uint64_t* err, ErrCount err_count, uint32_t* p_end, uint32_t* total_out) {
   typedef typename DictVal<W>::T T;
   const uint32_t lane = lane_id();
   uint32_t len;
@@ -2388,7 +2387,7 @@ template <int W, int MODE = 0>
 __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                               PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                               const int32_t* __restrict__ list, int n_list, uint64_t* err,
-                                              uint32_t* err_count, uint32_t* __restrict__ dba_meta = nullptr) {
+                                              ErrCount err_count, uint32_t* __restrict__ dba_meta = nullptr) {
   typedef typename DictVal<W>::T T;
   __shared__ __attribute__((aligned(16))) uint8_t dseg_all[WPB][DSEG];
   const int page = wave_page(list, n_list);
@@ -2546,7 +2545,7 @@ namespace pqg {
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                        const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                       bool fused, uint64_t* err, uint32_t* err_count) {
+                       bool fused, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
   const uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
   const dim3 blk(64 * WPB);
@@ -2578,7 +2577,7 @@ hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t
 hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                            const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
-                           uint32_t epoch, bool fused, uint64_t* err, uint32_t* err_count) {
+                           uint32_t epoch, bool fused, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
   const uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
   const dim3 blk(64 * WPB);
@@ -2596,7 +2595,7 @@ hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
 }
 
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
-                         const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+                         const int32_t* list, int n, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_levels, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   return hipGetLastError();
@@ -2610,7 +2609,7 @@ hipError_t launch_scan(hipStream_t st, PageWork* work, const int32_t* col_pages,
 }
 
 hipError_t launch_plain(int kind, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
   if (kind == 1) hipLaunchKernelGGL(k_plain_bool, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   else if (kind == 2) hipLaunchKernelGGL(k_rle_bool, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
@@ -2619,7 +2618,7 @@ hipError_t launch_plain(int kind, hipStream_t st, const uint8_t* bytes, uint64_t
 }
 
 hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
   if (width == 8) hipLaunchKernelGGL(k_delta<8>, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   else hipLaunchKernelGGL(k_delta<4>, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
@@ -2627,14 +2626,14 @@ hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_
 }
 
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                               const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count) {
+                               const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL((k_delta<4, 1>), dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   return hipGetLastError();
 }
 
 hipError_t launch_dba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                              const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, uint32_t* err_count,
+                              const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count,
                               uint32_t* dba_meta) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL((k_delta<4, 2>), dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS, dba_meta);
