@@ -912,7 +912,14 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
     if (dict_in_lds) {
       rsrc_t d0 = make_rsrc(bytes + cd0.dict_offset, cd0.dict_bytes);
       for (uint32_t o = 16u * threadIdx.x; o < (uint32_t)need; o += 16u * 64u * WPB)
+#ifdef PQG_DICT_STAGE_DWORDS
         *(u32x4*)(dict_lds + o) = u32x4{ld4_any(d0, o), ld4_any(d0, o + 4), ld4_any(d0, o + 8), ld4_any(d0, o + 12)};
+#else
+        *(u32x4*)(dict_lds + o) =  // any byte alignment; the piece at the buffer's end dword by dword
+            o + 16u <= cd0.dict_bytes
+                ? __builtin_amdgcn_raw_buffer_load_b128(d0, (int)o, 0, 0)
+                : u32x4{ld4_any(d0, o), ld4_any(d0, o + 4), ld4_any(d0, o + 8), ld4_any(d0, o + 12)};
+#endif
     }
   }
   __syncthreads();
