@@ -864,7 +864,10 @@ constexpr uint32_t XT_RUNS = 128;   // run table entries per wave
 constexpr uint32_t XT_SEG = 2560;   // LDS bytes for the packed data of one round
 
 constexpr uint32_t XT_LDS_BYTES = DICT_LDS_BYTES + WPB * (XT_RUNS * 16 + XT_SEG);
-constexpr uint32_t SPIN_LIMIT = 1u << 20;  // ~55 ms of s_sleep 2: a walker that never publishes
+#ifndef PQG_SPIN_SLEEP
+#define PQG_SPIN_SLEEP 2
+#endif
+constexpr uint32_t SPIN_LIMIT = (3u << 20) / (PQG_SPIN_SLEEP + 1);  // ~55 ms: a walker that never publishes
 
 // FUSED: launched in the same grid as the walkers (after them in workgroup order, so every
 // walker this wave waits for was dispatched first); the page's records are ready once its
@@ -928,7 +931,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
   if (FUSED) {
     uint32_t spins = 0;
     while (uni(sld(flags + page)) != epoch) {
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(PQG_SPIN_SLEEP);
       if (++spins >= SPIN_LIMIT) {
         if (lane == 0) report(err, err_count, page, 2, 0, PQG_ERR_HIP);
         return;
