@@ -574,7 +574,7 @@ template <int W>
 __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg,
                                              uint32_t sec_end, int w, uint64_t* rec, uint32_t* chunk_run,
                                              uint32_t CH, uint32_t sh, int page, uint64_t* err, ErrCount err_count,
-                                             uint32_t& n_rec, uint32_t& n_ok) {
+                                             uint32_t& n_rec, uint32_t& n_ok, uint64_t* prog) {
   const uint32_t lane = lane_id();
   // successor table (256 x u16) and reached flags (256 x u8) over L.ent; every access goes
   // through may_alias types (u16 gathers vs u64 row writes must not be reordered)
@@ -724,6 +724,14 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
     }
     k += uni(n_em);
     produced += total;
+#ifdef PQG_WALK_PROGRESS  // experimental: fails test_dict_page_sizes[8], see DESIGN.md §9
+    // progress for the fused expansion: records [0, k) cover values [0, produced) and are in
+    // memory (chunks inside that range may start before the page's flag is set)
+    if (prog && produced < N) {
+      __builtin_amdgcn_s_waitcnt(0);
+      if (lane == 0) sst(prog, (uint64_t)k | ((uint64_t)produced << 32));
+    }
+#endif
     DIAG_ADD(d_emit, t_emit);
 #ifdef PQG_DIAG
     d_win++;
@@ -818,7 +826,8 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
         uint32_t* pcr = chunk_run + pw.chunk_base;
         // SMALL: the whole data section sits in the LDS segment: the walk has no global load
         if (sec_end - win.seg_lo + 264u <= SEG_BYTES)  // every window inside the segment
-          dict_walk_pj<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
+          dict_walk_pj<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok,
+                          pstat + page);
         else if (sec_end - win.seg_lo <= SEG_BYTES)
           dict_walk<W, true>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
         else
@@ -826,9 +835,10 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
       }
     }
   }
-  if (lane == 0) {
+  __builtin_amdgcn_s_waitcnt(0);  // records and chunk entries are in memory before the status:
+  if (lane == 0) {                // the fused expansion may act on the status before the flag
     sst(pstat + page, (uint64_t)n_rec | ((uint64_t)n_ok << 32));
-    __builtin_amdgcn_s_waitcnt(0);  // records, chunk entries and status are in memory
+    __builtin_amdgcn_s_waitcnt(0);  // status in memory before the flag
     sst(flags + page, epoch);
   }
 }
@@ -928,20 +938,37 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
   __syncthreads();
   if (page < 0) return;
   const T* dict_l = (const T*)dict_lds;
+  const uint32_t j = (uint32_t)(chunks[c] >> 32);
+  const PageWork& pw = work[page];
+  uint64_t pst;
   if (FUSED) {
+    // the page's walk is done (flag), or its progress word ({records, values} zeroed per launch)
+    // already covers this chunk's values: records [0, k) and their chunk entries are in memory
     uint32_t spins = 0;
-    while (uni(sld(flags + page)) != epoch) {
+    while (true) {
+      if (uni(sld(flags + page)) == epoch) {
+        pst = uni64(sld(pstat + page));
+        break;
+      }
+#ifdef PQG_WALK_PROGRESS  // experimental: fails test_dict_page_sizes[8], see DESIGN.md §9
+      const uint32_t sh0 = (uint32_t)(pw.out_offset % (uint64_t)E), nv = uni(pw.n_values);
+      const uint32_t need = ((j + 1) * CH < nv + sh0 ? (j + 1) * CH : nv + sh0) - sh0;
+      const uint64_t pp = uni64(sld(pstat + page));
+      if ((uint32_t)(pp >> 32) >= need) {
+        pst = pp;
+        break;
+      }
+#endif
       __builtin_amdgcn_s_sleep(PQG_SPIN_SLEEP);
       if (++spins >= SPIN_LIMIT) {
         if (lane == 0) report(err, err_count, page, 2, 0, PQG_ERR_HIP);
         return;
       }
     }
+  } else {
+    pst = uni64(sld(pstat + page));
   }
-  const uint64_t pst = uni64(sld(pstat + page));
 
-  const uint32_t j = (uint32_t)(chunks[c] >> 32);
-  const PageWork& pw = work[page];
   const uint32_t N = (uint32_t)(pst >> 32);  // values covered before a walk error
   const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
   const uint32_t s_lo = j * CH > sh ? j * CH : sh;
