@@ -724,7 +724,7 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
     }
     k += uni(n_em);
     produced += total;
-#ifdef PQG_WALK_PROGRESS  // experimental: fails test_dict_page_sizes[8], see DESIGN.md §9
+#ifdef PQG_WALK_PROGRESS  // experimental, off: correct but slower in the A/B
     // progress for the fused expansion: records [0, k) cover values [0, produced) and are in
     // memory (chunks inside that range may start before the page's flag is set)
     if (prog && produced < N) {
@@ -950,11 +950,12 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
         pst = uni64(sld(pstat + page));
         break;
       }
-#ifdef PQG_WALK_PROGRESS  // experimental: fails test_dict_page_sizes[8], see DESIGN.md §9
+#ifdef PQG_WALK_PROGRESS  // experimental, off: correct but slower in the A/B
       const uint32_t sh0 = (uint32_t)(pw.out_offset % (uint64_t)E), nv = uni(pw.n_values);
       const uint32_t need = ((j + 1) * CH < nv + sh0 ? (j + 1) * CH : nv + sh0) - sh0;
       const uint64_t pp = uni64(sld(pstat + page));
       if ((uint32_t)(pp >> 32) >= need) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // record loads after the status load
         pst = pp;
         break;
       }
