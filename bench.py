@@ -22,7 +22,7 @@ import time
 import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(REPO, "parquet-mr_amd"))
+sys.path[:0] = [os.path.join(REPO, "parquet-mr_amd"), os.path.join(REPO, "tools")]
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md: 8.0 TB/s spec)
 DOMINANT_KERNEL = "void pqg::k_dict_fused<8>"
@@ -34,25 +34,9 @@ def workload_key(rows, zipf):
 
 
 def make_c2(n_rows, seed_dict=42, seed_runs=43, a=1.5, card=1000, max_run=4096, page_rows=20000):
-    """Config 2 input: the dictionary column as parquet-mr would write it."""
-    from pqgpu import abi, writer
-    rng_d = np.random.default_rng(seed_dict)
-    dict_vals = rng_d.integers(-2**63, 2**63 - 1, size=card, dtype=np.int64, endpoint=True)
-    rng = np.random.default_rng(seed_runs)
-    runs = []
-    total = 0
-    while total < n_rows:
-        r = np.minimum(rng.zipf(a, size=1 << 20), max_run)
-        runs.append(r)
-        total += int(r.sum())
-    runs = np.concatenate(runs)
-    run_ids = rng.integers(0, card, size=runs.size)
-    cut = np.searchsorted(np.cumsum(runs), n_rows)
-    runs, run_ids = runs[:cut + 1], run_ids[:cut + 1]
-    ids = np.repeat(run_ids, runs)[:n_rows]
-    ids_fa, order = writer.first_appearance_ids(ids)
-    chunk = writer.write_dict_column_from_ids(abi.INT64, dict_vals[order], ids_fa, page_rows=page_rows)
-    return chunk, dict_vals, ids
+    """Config 2 input: the dictionary column as parquet-mr would write it (tools/workloads.py)."""
+    import workloads
+    return workloads.make_c2(n_rows, seed_dict, seed_runs, a, card, max_run, page_rows)
 
 
 def cpu_baseline(batch, n_values, budget_s):
@@ -128,6 +112,47 @@ def pyarrow_baseline(values, budget_s, threads):
             "sample": f"pyarrow {pa.__version__} read_table of the same 100M values (its own pages), {reps} reps"}
 
 
+def launch_ranks(n):
+    """`--gpus N` run without a launcher: start N ranks under torch.distributed.run (one process per
+    GPU, rendezvous on 127.0.0.1) as a CHILD process and exit with its code. Nothing here touches
+    the GPU, so no process that initialised HIP is replaced."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, PQG_BENCH_LAUNCHED="1")
+    return subprocess.call(cmd, env=env)
+
+
+def init_ranks(args):
+    """-> (world, rank, local_rank, device index). World size is what the process group reports."""
+    import torch
+    import torch.distributed as dist
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_env != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world_env} ranks; reporting {world_env}",
+              file=sys.stderr)
+    ndev = torch.cuda.device_count()
+    dev = local % max(ndev, 1)
+    torch.cuda.set_device(dev)
+    world = 1
+    if world_env > 1:
+        backend = args.backend or ("nccl" if ndev >= world_env else "gloo")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:  # fewer GPUs than ranks (rehearsal on a 1-GPU box): ranks share the GPU, gloo collectives
+            dist.init_process_group("gloo")
+        world = dist.get_world_size()
+        rank = dist.get_rank()
+    return world, rank, local, dev
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,23 +162,21 @@ def main():
     ap.add_argument("--zipf", type=float, default=1.5)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--verify", action="store_true", default=True)
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the timed RCCL all-gather of the column")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default=None)
     ap.add_argument("--e2e", action="store_true", help="also time the host-bytes-in / host-array-out path")
     ap.add_argument("--traffic-json", default=TRAFFIC_JSON,
                     help="rocprofv3 PMC traffic summary of this kernel (tools/pmc_summary.py --json)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
     from pqgpu import decoder as D, writer
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
+    world, rank, local, devi = init_ranks(args)
 
     t_gen = time.perf_counter()
     # each rank owns one row group: same dictionary seed, its own run stream
@@ -162,20 +185,22 @@ def main():
     t_gen = time.perf_counter() - t_gen
     data_bytes = int(sum(len(p.body) for p in chunk.pages))
 
-    dec = D.Decoder(local)
+    dec = D.Decoder(devi, poison=0xA5)
     dbatch = dec.upload(batch)
-    cols = dec.alloc_columns(batch)
+    cols = dec.alloc_columns(batch)  # poisoned: an element no launch writes cannot pass the check
     plan = dec.plan(dbatch, cols)
     stream = dec.stream
+    exp = None
+    if not args.no_verify:
+        exp = torch.from_numpy(dict_vals[ids]).to(dec.device)
+        plan.launch()  # the FIRST launch of a fresh plan is checked (not one after warm-up rewrites)
+        rc, st = plan.sync()
+        assert rc == 0, st.message
+        assert torch.equal(cols[0].typed(), exp), "first launch: decoded column differs from the generated values"
     for _ in range(args.warmup):
         plan.launch()
     rc, st = plan.sync()
     assert rc == 0, st.message
-    if args.verify:
-        got = cols[0].typed()
-        exp = torch.from_numpy(dict_vals[ids]).to(got.device)
-        assert torch.equal(got, exp), "decoded column differs from the generated values"
-        del exp
 
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     if world > 1:
@@ -192,12 +217,45 @@ def main():
     wall = time.perf_counter() - t0
     rc, st = plan.sync()
     assert rc == 0, st.message
+    if exp is not None:
+        assert torch.equal(cols[0].typed(), exp), "after the timed launches: decoded column differs"
     per_launch_ms = [ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)]
     gpu_ms = sum(per_launch_ms)
-    t = torch.tensor([gpu_ms / 1e3, wall], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([gpu_ms / 1e3, wall], dtype=torch.float64)
     if world > 1:
+        t = t.to(f"cuda:{devi}") if dist.get_backend() == "nccl" else t
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = float(t[0].item())
+
+    gather = None
+    if world > 1 and not args.no_gather:
+        # the final column concatenation (north_star: RCCL/xGMI gather only for it), timed on its own:
+        # every rank ends with the full world x rows column; checked by a checksum of checksums
+        from pqgpu import dist as pdist
+        shards = [[r] for r in range(world)]
+        counts = [args.rows] * world
+        local_col = cols[0].typed()
+        full = pdist.gather_column(local_col, [rank], shards, counts)  # warm-up (communicator setup)
+        del full
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        full = pdist.gather_column(local_col, [rank], shards, counts)
+        torch.cuda.synchronize()
+        dist.barrier()
+        g_s = torch.tensor([time.perf_counter() - tg], dtype=torch.float64)
+        csum = torch.tensor([int(local_col.sum().item()) & (2**63 - 1)], dtype=torch.int64)
+        g_s = g_s.to(f"cuda:{devi}") if dist.get_backend() == "nccl" else g_s
+        csum = csum.to(g_s.device)
+        dist.all_reduce(g_s, op=dist.ReduceOp.MAX)
+        dist.all_reduce(csum)
+        ok = (int(full.sum().item()) & (2**63 - 1)) == (int(csum.item()) & (2**63 - 1)) and full.numel() == world * args.rows
+        g = float(g_s.item())
+        recv = (world - 1) * args.rows * 8
+        gather = {"collective": f"all_gather ({dist.get_backend()})", "bytes_received_per_rank": recv,
+                  "seconds": g, "gb_per_s_per_rank": recv / g / 1e9, "checksum_ok": bool(ok),
+                  "note": "timed separately; not part of value (decode-only rate)"}
+        del full
 
     n = args.rows
     total_values = n * world * args.steps
@@ -223,7 +281,7 @@ def main():
                        "chunked D2H -> caller's int64 array); output array allocated and touched beforehand"}
 
     cpu = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(batch, n, args.cpu_budget)
         threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 cores
         cpu["multi_thread"] = cpu_baseline_mt(chunk, n, threads, args.cpu_budget / 2)
@@ -261,6 +319,8 @@ def main():
                        "rows_per_gpu": n, "pages_per_gpu": batch.n_pages, "encoded_data_bytes_per_gpu": data_bytes,
                        "parallelism": f"row-group shard x{world}"},
             "gib_per_s": value * 8 / 2**30,
+            "verified": "first launch of a fresh plan and the state after the timed launches == generated values"
+                        if exp is not None else None,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_bytes_per_launch": traffic_bytes, "traffic_source": traffic_src,
@@ -269,6 +329,8 @@ def main():
             "cpu_baseline": cpu,
             "input_gen_s": t_gen,
         }
+        if gather:
+            out["gather"] = gather
         if e2e:
             out["e2e_host_path"] = e2e
         print(json.dumps(out), flush=True)

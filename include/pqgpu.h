@@ -76,6 +76,9 @@ enum pqg_error {
   PQG_ERR_UNSUPPORTED = 2,      /* (type, encoding) has no reader: Encoding.java:84,193; UnsupportedOperationException */
   PQG_ERR_HIP = 3,              /* HIP runtime failure */
   PQG_ERR_NO_DEVICE = 4,        /* no HIP device / extension unusable */
+  PQG_ERR_TIMEOUT = 5,          /* a fused-kernel wave waited > 2 s of wall time for its page's walk (the
+                                   walker was descheduled or starved); not a decode error: the chunk's
+                                   output is incomplete, relaunch the plan */
   PQG_ERR_EOF = 10,             /* java.io.EOFException: read past the end of a page section
                                    (SingleBufferInputStream.read :50-55, LittleEndianDataInputStream.readInt/readLong) */
   PQG_ERR_RLE_PAST_END = 11,    /* IllegalArgumentException "Reading past RLE/BitPacking stream."

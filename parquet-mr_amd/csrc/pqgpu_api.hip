@@ -166,6 +166,7 @@ const char* pqg_error_name(int code) {
   switch (code) {
     case PQG_OK: case PQG_ERR_INVALID_ARG: case PQG_ERR_UNSUPPORTED: case PQG_ERR_HIP: case PQG_ERR_NO_DEVICE:
       return kNames[code];
+    case PQG_ERR_TIMEOUT: return "TIMEOUT";
     case PQG_ERR_EOF: return "EOF";
     case PQG_ERR_RLE_PAST_END: return "RLE_PAST_END";
     case PQG_ERR_BIT_WIDTH: return "BIT_WIDTH";

@@ -561,6 +561,39 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
   n_ok = N;
 }
 
+// Walk -> expansion hand-off inside one launch (walkers and expansion waves on any CU / XCD).
+//
+// Every datum handed off — run records, chunk -> record entries, page status, page flag — is
+// written and read ONLY with system-scope atomics (sst / sld: global_store / global_load with
+// sc0 sc1). On gfx950 those bypass the non-coherent per-XCD L2 (stores write through, loads
+// miss), so no cache write-back or invalidate is needed for them; what the hand-off needs is
+// ORDER:
+//   release (walker): the wave's record stores are complete before the status store, and the
+//     status before the flag — s_waitcnt vmcnt(0) (stores count in vmcnt; the wait returns once
+//     the write-through stores are acknowledged), plus a compiler barrier so no store is moved
+//     across it;
+//   acquire (expansion): the status / record loads are issued after the flag load returned the
+//     epoch — the flag value feeds the loop's scalar branch, so its load has completed (vmcnt)
+//     before any later load issues; a compiler barrier keeps those loads below the branch.
+// The memory model's agent-scope fences (buffer_wbl2 sc1 on release, buffer_inv sc1 on acquire)
+// would also write back / invalidate the L2 lines of the expansion's own output and input; both
+// were measured (PQG_HANDOFF = 1: release store, 2: acquire fence, 3: both) and
+// cost 2.6x on C2, while every hand-off datum already bypasses those caches.
+#ifndef PQG_HANDOFF
+#define PQG_HANDOFF 0
+#endif
+__device__ __forceinline__ void handoff_release() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+__device__ __forceinline__ void handoff_acquire() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#if PQG_HANDOFF & 2
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+}
+
 // Pointer-jumping walk (SMALL pages: the whole data section sits in the LDS segment).
 //
 // The serial part of the hybrid decoder — each header's position depends on the previous
@@ -728,8 +761,9 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
     // progress for the fused expansion: records [0, k) cover values [0, produced) and are in
     // memory (chunks inside that range may start before the page's flag is set)
     if (prog && produced < N) {
-      __builtin_amdgcn_s_waitcnt(0);
-      if (lane == 0) sst(prog, (uint64_t)k | ((uint64_t)produced << 32));
+      wave_sync();
+      if (lane == 0)
+        __hip_atomic_store(prog, (uint64_t)k | ((uint64_t)produced << 32), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 #endif
     DIAG_ADD(d_emit, t_emit);
@@ -835,11 +869,18 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
       }
     }
   }
-  __builtin_amdgcn_s_waitcnt(0);  // records and chunk entries are in memory before the status:
-  if (lane == 0) {                // the fused expansion may act on the status before the flag
+  // Publish (see handoff_release): every lane's record / chunk-entry stores, then lane 0's
+  // status, then the flag.
+  wave_sync();
+  handoff_release();
+  if (lane == 0) {
     sst(pstat + page, (uint64_t)n_rec | ((uint64_t)n_ok << 32));
-    __builtin_amdgcn_s_waitcnt(0);  // status in memory before the flag
+    handoff_release();
+#if PQG_HANDOFF & 1
+    __hip_atomic_store(flags + page, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#else
     sst(flags + page, epoch);
+#endif
   }
 }
 
@@ -877,7 +918,9 @@ constexpr uint32_t XT_LDS_BYTES = DICT_LDS_BYTES + WPB * (XT_RUNS * 16 + XT_SEG)
 #ifndef PQG_SPIN_SLEEP
 #define PQG_SPIN_SLEEP 2
 #endif
-constexpr uint32_t SPIN_LIMIT = (3u << 20) / (PQG_SPIN_SLEEP + 1);  // ~55 ms: a walker that never publishes
+constexpr uint64_t SPIN_TIMEOUT_TICKS = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+
+
 
 // FUSED: launched in the same grid as the walkers (after them in workgroup order, so every
 // walker this wave waits for was dispatched first); the page's records are ready once its
@@ -939,14 +982,25 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
   if (page < 0) return;
   const T* dict_l = (const T*)dict_lds;
   const uint32_t j = (uint32_t)(chunks[c] >> 32);
-  const PageWork& pw = work[page];
+  // page / column facts and the page's bit width do not depend on the walk: loaded before the
+  // hand-off, so the compiler barrier there does not serialize them behind the flag
+  const PageWork pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t dict_n = uni(cd.dict_n);
+  rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
+  rsrc_t prs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  const uint32_t sec_end = uni(pw.size);
+  const uint32_t db = uni(pw.data_begin);
+  const int w = (int)uni((ld32(prs, db & ~3u) >> ((db & 3u) * 8u)) & 0xFFu);
+  T* const out_base = IDS ? (T*)cd.blen : (T*)cd.values;
   uint64_t pst;
   if (FUSED) {
-    // the page's walk is done (flag), or its progress word ({records, values} zeroed per launch)
-    // already covers this chunk's values: records [0, k) and their chunk entries are in memory
-    uint32_t spins = 0;
+    // The flag is polled; once it holds this launch's epoch, handoff_acquire orders the status /
+    // record / chunk-entry loads below after it (once per chunk, not per poll).
+    uint64_t t_wait = 0;
     while (true) {
       if (uni(sld(flags + page)) == epoch) {
+        handoff_acquire();
         pst = uni64(sld(pstat + page));
         break;
       }
@@ -955,14 +1009,18 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       const uint32_t need = ((j + 1) * CH < nv + sh0 ? (j + 1) * CH : nv + sh0) - sh0;
       const uint64_t pp = uni64(sld(pstat + page));
       if ((uint32_t)(pp >> 32) >= need) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // record loads after the status load
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // record loads after the status load
         pst = pp;
         break;
       }
 #endif
       __builtin_amdgcn_s_sleep(PQG_SPIN_SLEEP);
-      if (++spins >= SPIN_LIMIT) {
-        if (lane == 0) report(err, err_count, page, 2, 0, PQG_ERR_HIP);
+      // wall-clock bound (s_memrealtime: constant 100 MHz): a walker that never publishes
+      // (descheduled, starved) turns into PQG_ERR_TIMEOUT after SPIN_TIMEOUT_TICKS, not a hang
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (t_wait == 0) t_wait = now;
+      else if (now - t_wait > SPIN_TIMEOUT_TICKS) {
+        if (lane == 0) report(err, err_count, page, 2, 0, PQG_ERR_TIMEOUT);
         return;
       }
     }
@@ -976,17 +1034,9 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
   const uint32_t s_hi = (j + 1) * CH < N + sh ? (j + 1) * CH : N + sh;
   if (s_lo >= s_hi) return;
   const uint32_t v_lo = s_lo - sh, v_hi = s_hi - sh;
-  const ColumnDev& cd = cols[pw.column];
   const bool own_dict = dict_in_lds && pw.column == c0;
-  const uint32_t dict_n = uni(cd.dict_n);
-  rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
-  rsrc_t prs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
-  const uint32_t sec_end = uni(pw.size);
   const uint32_t n_rec = (uint32_t)pst;
-  const uint32_t db = uni(pw.data_begin);
-  const int w = (int)uni((ld32(prs, db & ~3u) >> ((db & 3u) * 8u)) & 0xFFu);
   const uint64_t* prec = rec + pw.rec_base;
-  T* const out_base = IDS ? (T*)cd.blen : (T*)cd.values;
   T* const pag = out_base + (pw.out_offset - sh);  // slot 0 of the page
   const bool out16 = ((uintptr_t)out_base & 15u) == 0;
   const uint32_t wmask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;

@@ -31,6 +31,7 @@ ERR_INVALID_ARG = 1
 ERR_UNSUPPORTED = 2
 ERR_HIP = 3
 ERR_NO_DEVICE = 4
+ERR_TIMEOUT = 5
 ERR_EOF = 10
 ERR_RLE_PAST_END = 11
 ERR_BIT_WIDTH = 12
@@ -45,7 +46,7 @@ ERR_DICT_ENCODING = 20
 
 ERROR_NAMES = {
     OK: "OK", ERR_INVALID_ARG: "INVALID_ARG", ERR_UNSUPPORTED: "UNSUPPORTED", ERR_HIP: "HIP",
-    ERR_NO_DEVICE: "NO_DEVICE", ERR_EOF: "EOF", ERR_RLE_PAST_END: "RLE_PAST_END",
+    ERR_NO_DEVICE: "NO_DEVICE", ERR_TIMEOUT: "TIMEOUT", ERR_EOF: "EOF", ERR_RLE_PAST_END: "RLE_PAST_END",
     ERR_BIT_WIDTH: "BIT_WIDTH", ERR_DICT_ID: "DICT_ID", ERR_EMPTY_PAGE: "EMPTY_PAGE",
     ERR_EMPTY_PACKED_RUN: "EMPTY_PACKED_RUN", ERR_DELTA_CONFIG: "DELTA_CONFIG",
     ERR_DELTA_PAST_END: "DELTA_PAST_END", ERR_CORRUPT: "CORRUPT", ERR_NO_DICTIONARY: "NO_DICTIONARY",

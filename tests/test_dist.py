@@ -49,8 +49,38 @@ def _worker(rank, world, port, q):
     local = torch.from_numpy(np.concatenate(local) if local else np.zeros(0, np.int64))
     full = pdist.gather_column(local, mine, shards, rows)
     expect = np.concatenate([ch.values for ch in rgs])
-    q.put((rank, bool(np.array_equal(full.numpy(), expect)), [len(s) for s in shards]))
+    ok = bool(np.array_equal(full.numpy(), expect))
+    # BYTE_ARRAY: byte-total all-gather + offset rebase (PLAIN strings of 0-40 bytes per row group)
+    brgs = _binary_row_groups()
+    bshards = pdist.shard_row_groups([sum(len(p.body) for p in ch.pages) for ch in brgs], world)
+    offs, data = [np.zeros(1, np.int64)], []
+    for i in bshards[rank]:
+        res = pqref.decode_batch(writer.build_batch([brgs[i]]))
+        assert res.code == 0
+        vals = res.columns[0]["values"]
+        lens = np.array([len(v) for v in vals], dtype=np.int64)
+        offs.append(offs[-1][-1] + np.cumsum(lens))
+        data.append(np.frombuffer(b"".join(vals), dtype=np.uint8))
+    loff = torch.from_numpy(np.concatenate(offs))
+    ldata = torch.from_numpy(np.concatenate(data) if data else np.zeros(0, np.uint8))
+    foff, fdata = pdist.gather_binary(loff, ldata, bshards[rank], bshards, [len(ch.values) for ch in brgs])
+    allv = [bytes(v) for ch in brgs for v in ch.values]
+    exp_off = np.concatenate([[0], np.cumsum([len(v) for v in allv])])
+    ok_b = bool(np.array_equal(foff.numpy(), exp_off)) and fdata.numpy().tobytes() == b"".join(allv)
+    q.put((rank, ok and ok_b, [len(s) for s in shards], [len(s) for s in bshards]))
     dist.destroy_process_group()
+
+
+def _binary_row_groups():
+    rng = np.random.default_rng(5)
+    rgs = []
+    for k in range(5):
+        n = int(rng.integers(0 if k == 2 else 100, 3000))
+        vals = writer.BinaryValues.random(n, 0, 40, seed=100 + k)
+        ch = writer.write_column_chunk(abi.BYTE_ARRAY, vals, abi.PLAIN, page_rows=700)
+        ch.values = [vals[i] for i in range(n)]
+        rgs.append(ch)
+    return rgs
 
 
 def test_shard_row_groups_balanced():
@@ -74,5 +104,5 @@ def test_gather_world2_gloo():
     res = [q.get(timeout=240) for _ in procs]
     for p in procs:
         p.join(timeout=60)
-    assert all(ok for _, ok, _ in res), res
+    assert all(r[1] for r in res), res
     assert all(p.exitcode == 0 for p in procs)
