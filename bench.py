@@ -153,12 +153,210 @@ def init_ranks(args):
     return world, rank, local, dev
 
 
+def run_c4(args, world, rank, devi):
+    """C4 (BASELINE configs[3]): TPC-H lineitem-shaped 16 columns, `--rows` rows in total (default 1 B)
+    in row groups of 1M rows, sharded over the ranks by encoded bytes (dist.shard_row_groups, the
+    Hadoop row-group split); strong scaling. A step = one plan launch decoding every page of the
+    rank's row groups (16 columns: DELTA int64 keys / int32 dates, PLAIN doubles, dictionary int32
+    and strings, PLAIN comment strings) into the rank's slice of each column. The inputs are
+    `--c4-templates` distinct synthetic row groups laid out repeatedly (row group g = template
+    g mod T): every copy's pages are decoded, none is skipped or cached."""
+    import copy
+
+    import torch
+    import torch.distributed as dist
+    import lineitem as LI
+    from pqgpu import abi, decoder as D, dist as pdist, writer
+
+    rg_rows = 1_000_000
+    n_rg = max(1, args.rows // rg_rows)
+    T = min(args.c4_templates, n_rg)
+    t_gen = time.perf_counter()
+    templates, base = [], 0
+    for t in range(T):
+        ch, ex, n_ord = LI.make_row_group(rg_rows, 1000 + t, base)
+        base += n_ord
+        templates.append((ch, ex))
+    tsize = [sum(len(p.body) for c in ch for p in c.pages) for ch, _ in templates]
+    shards = pdist.shard_row_groups([tsize[g % T] for g in range(n_rg)], world)
+    mine = shards[rank]
+    chunks = []
+    for g in mine:
+        for k, c in enumerate(templates[g % T][0]):
+            cc = copy.copy(c)
+            # dictionary columns: one pqg column per row group (its own dictionary); the others
+            # decode every row group into one rank-wide column, back to back
+            cc.column_index = (k, g) if c.dict_page is not None else (k, -1)
+            chunks.append(cc)
+    batch = writer.build_batch(chunks)
+    t_gen = time.perf_counter() - t_gen
+    enc_bytes = int(batch.pages["size"].sum()) + sum(int(c["dict_size"]) for c in batch.columns if c["dict_offset"] >= 0)
+
+    dec = D.Decoder(devi, poison=0xA5)
+    dbatch = dec.upload(batch)
+    cols, st = dec.decode(dbatch)  # sizes the BYTE_ARRAY buffers
+    plan = dec.plan(dbatch, cols)
+    keys = [getattr(c, "column_index") for c in chunks]
+    col_of = {}
+    for key in keys:
+        col_of.setdefault(key, len(col_of))
+
+    def verify(what):
+        # every row group's slice of every column == its template's values
+        exp_dev = {}
+        pos = {k: 0 for k in range(16)}
+        bpos = 0
+        for g in mine:
+            t = g % T
+            for k in range(16):
+                ci = col_of[(k, g)] if (k, g) in col_of else col_of[(k, -1)]
+                col = cols[ci]
+                ex = templates[t][1][k]
+                key = (t, k)
+                if key not in exp_dev:
+                    if isinstance(ex.values, writer.BinaryValues):
+                        exp_dev[key] = (torch.from_numpy(ex.values.offsets).to(dec.device),
+                                        torch.from_numpy(ex.values.data).to(dec.device))
+                    else:
+                        exp_dev[key] = torch.from_numpy(np.ascontiguousarray(ex.values).view(np.uint8)).to(dec.device)
+                e = exp_dev[key]
+                merged = (k, -1) in col_of
+                r0 = pos[k] if merged else 0
+                n = rg_rows
+                if isinstance(e, tuple):
+                    offs = col.offsets()[r0:r0 + n + 1]
+                    b0 = int(offs[0].item())
+                    assert torch.equal(offs - b0, e[0]), f"{what}: row group {g} column {k} offsets"
+                    assert torch.equal(col.binary_data[b0:b0 + e[1].numel()], e[1]), f"{what}: rg {g} col {k} bytes"
+                else:
+                    w = e.numel() // n
+                    assert torch.equal(col.values[r0 * w:(r0 + n) * w], e), f"{what}: row group {g} column {k}"
+                if merged:
+                    pos[k] += n
+        del exp_dev
+
+    plan.launch()  # first launch of the fresh plan, checked
+    rc, st = plan.sync()
+    assert rc == 0, st.message
+    if not args.no_verify:
+        verify("first launch")
+    for _ in range(args.warmup):
+        plan.launch()
+    rc, st = plan.sync()
+    assert rc == 0, st.message
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record(dec.stream)
+    for _ in range(args.steps):
+        plan.launch()
+    ev[1].record(dec.stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    rc, st = plan.sync()
+    assert rc == 0, st.message
+    if not args.no_verify:
+        verify("after the timed launches")
+    gpu_s = ev[0].elapsed_time(ev[1]) / 1e3
+    out_bytes = 0
+    for i, cd in enumerate(batch.columns):
+        n = cols[i].n_values
+        out_bytes += 8 * (n + 1) + int(cols[i].offsets()[-1].item()) if cd["physical_type"] == abi.BYTE_ARRAY \
+            else n * abi.elem_width(cd["physical_type"], cd["type_length"])
+    t = torch.tensor([gpu_s, wall, float(len(mine) * rg_rows), float(enc_bytes + out_bytes)], dtype=torch.float64)
+    rows_all = torch.tensor([float(len(mine) * rg_rows), float(enc_bytes + out_bytes)], dtype=torch.float64)
+    if world > 1:
+        dev = f"cuda:{devi}" if dist.get_backend() == "nccl" else "cpu"
+        t, rows_all = t.to(dev), rows_all.to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(rows_all)
+    t_max = float(t[0].item())
+    total_rows, total_bytes = float(rows_all[0].item()), float(rows_all[1].item())
+
+    gather = None
+    if world > 1 and not args.no_gather:
+        # final concatenation of two representative columns over RCCL: l_orderkey (int64, fixed width)
+        # and l_comment (BYTE_ARRAY: byte-total all-gather + offset rebase), timed separately
+        counts = [rg_rows] * n_rg
+        ok_col, cm_col = cols[col_of[(0, -1)]], cols[col_of[(15, -1)]]
+        res = {}
+        for name, fn in (("l_orderkey", lambda: pdist.gather_column(ok_col.typed(), mine, shards, counts)),
+                         ("l_comment", lambda: pdist.gather_binary(cm_col.offsets(), cm_col.binary_data, mine, shards,
+                                                                  counts))):
+            fn()
+            dist.barrier()
+            torch.cuda.synchronize()
+            tg = time.perf_counter()
+            r = fn()
+            torch.cuda.synchronize()
+            dist.barrier()
+            nbytes = r.numel() * r.element_size() if not isinstance(r, tuple) else sum(x.numel() * x.element_size() for x in r)
+            gs = torch.tensor([time.perf_counter() - tg], dtype=torch.float64)
+            gs = gs.to(f"cuda:{devi}") if dist.get_backend() == "nccl" else gs
+            dist.all_reduce(gs, op=dist.ReduceOp.MAX)
+            res[name] = {"full_column_bytes": nbytes, "seconds": float(gs.item()),
+                         "gb_per_s": nbytes / float(gs.item()) / 1e9}
+            del r
+        gather = {"collective": f"all_gather ({dist.get_backend()})", "columns": res,
+                  "note": "timed separately; not part of value (decode-only rate)"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, REPO)
+        from oracle import pqref
+        b1 = writer.build_batch(templates[0][0])
+        t1, reps = time.perf_counter(), 0
+        while True:
+            r = pqref.decode_batch(b1)
+            assert r.code == 0
+            reps += 1
+            if time.perf_counter() - t1 >= args.cpu_budget:
+                break
+        dt = time.perf_counter() - t1
+        cpu = {"value": reps * rg_rows * 16 / dt, "unit": "values/s", "cores": 1, "kind": "port",
+               "sample": f"{reps} x one 1M-row, 16-column row group, oracle/pqref.c single thread, {dt:.1f} s"}
+    if rank == 0:
+        value = total_rows * 16 * args.steps / t_max
+        out = {
+            "metric": "decoded values/s, device-resident C4 lineitem 16 columns",
+            "value": value, "unit": "values/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": t_max * 1e3 / args.steps, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "mixed (int32/int64/f64/bytes)", "data": "synthetic",
+            "config": {"workload": "C4: TPC-H lineitem-shaped 16 required columns (DELTA int64 keys / int32 dates, "
+                                   "PLAIN doubles, RLE_DICTIONARY int32 + strings, PLAIN comment), parquet-mr V1 "
+                                   "pages of 20,000 values, uncompressed, 1M-row row groups sharded over ranks",
+                       "rows_total": int(total_rows), "row_groups_total": n_rg, "row_groups_this_rank": len(mine),
+                       "distinct_row_groups": T, "pages_this_rank": batch.n_pages,
+                       "pqg_columns_this_rank": len(batch.columns), "parallelism": f"row-group shard x{world}"},
+            "gb_per_s": total_bytes * args.steps / t_max / 1e9,
+            "hbm_frac_per_gpu": total_bytes * args.steps / t_max / 1e9 / world / HBM_PEAK_GBS,
+            "kernels_per_launch": plan.kernel_count,
+            "verified": None if args.no_verify else "every row group x column slice == its generated values, first launch "
+                                                    "of a fresh plan and after the timed launches",
+            "cpu_baseline": cpu, "input_gen_s": t_gen,
+        }
+        if gather:
+            out["gather"] = gather
+        print(json.dumps(out), flush=True)
+    plan.close()
+    dec.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--workload", choices=["c2", "c4"], default="c2",
+                    help="c2: the headline (BASELINE metric); c4: lineitem 16 columns, strong scaling")
+    ap.add_argument("--rows", type=int, default=None, help="c2: rows per GPU (100M); c4: rows in total (1B)")
+    ap.add_argument("--c4-templates", type=int, default=4, help="c4: distinct synthetic row groups")
     ap.add_argument("--zipf", type=float, default=1.5)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -177,6 +375,10 @@ def main():
     from pqgpu import decoder as D, writer
 
     world, rank, local, devi = init_ranks(args)
+    if args.workload == "c4":
+        args.rows = args.rows or 1_000_000_000
+        return run_c4(args, world, rank, devi)
+    args.rows = args.rows or 100_000_000
 
     t_gen = time.perf_counter()
     # each rank owns one row group: same dictionary seed, its own run stream

@@ -239,7 +239,19 @@ class Decoder:
         in them) + twice its dictionary page; decode() grows it when the device counts more."""
         cd = batch.columns[i]
         pages = batch.pages[batch.pages["column"] == i]
-        return int(pages["size"].sum()) + 2 * int(cd["dict_size"] if cd["dict_offset"] >= 0 else 0) + 64
+        est = int(pages["size"].sum()) + 2 * int(cd["dict_size"] if cd["dict_offset"] >= 0 else 0) + 64
+        if cd["dict_offset"] >= 0 and 0 < cd["dict_num_values"] <= 1 << 16:
+            # dictionary column: at most slots x the longest dictionary entry ([u32 length][bytes] each)
+            d = batch.data[int(cd["dict_offset"]): int(cd["dict_offset"]) + int(cd["dict_size"])].tobytes()
+            pos, longest = 0, 0
+            for _ in range(int(cd["dict_num_values"])):
+                if pos + 4 > len(d):
+                    break
+                n = int.from_bytes(d[pos:pos + 4], "little")
+                longest = max(longest, n)
+                pos += 4 + n
+            est = max(est, batch.column_slots[i] * longest + 64)
+        return est
 
     def alloc_columns(self, batch):
         cols = []

@@ -120,3 +120,22 @@ def test_c5_full_with_assembly(decoder):
     dl = work.expect[0].def_levels
     elem_valid = (dl[dl >= 2] == 3).astype(np.uint8)
     assert torch.equal(got["nodes"][2]["validity"], torch.from_numpy(elem_valid).to(dev)), "element validity"
+
+
+def test_c4_lineitem_row_groups(decoder):
+    """C4: four 1M-row lineitem row groups (64 column chunks: DELTA keys / dates, PLAIN doubles,
+    dictionary int32 + strings, PLAIN comments) in one batch, each chunk == its generated values;
+    an oracle sample of every column first."""
+    import lineitem as LI
+    work = LI.make_c4(4_000_000)
+    oracle_sample(WL.Workload("c4 rg0", work.chunks[:16], work.expect[:16]), 5)
+    batch = writer.build_batch(work.chunks)
+    dbatch = decoder.upload(batch)
+    cols, st = decoder.decode(dbatch)
+    WL.verify(cols, work, "decode")
+    plan = decoder.plan(dbatch, cols)
+    plan.launch()
+    rc, st = plan.sync()
+    assert rc == 0, st.message
+    WL.verify(cols, work, "plan")
+    plan.close()

@@ -31,56 +31,21 @@ sys.path[:0] = [os.path.join(REPO, "parquet-mr_amd"), REPO]
 
 from pqgpu import abi, writer  # noqa: E402
 
+sys.path.insert(0, os.path.join(REPO, "tools"))
+import workloads as WL  # noqa: E402
+
 HBM_PEAK_GBS = 8000.0
 
 
-def nulls(n, frac, seed):
-    return (np.random.default_rng(seed).random(n) >= frac).astype(np.uint8)
-
-
 def gen(name, rows):
-    """-> list of ColumnChunk"""
+    """-> workloads.Workload (column chunks + the values written, for verification)."""
+    if name in ("c2_zipf2", "c3_mixed", "c5_levels", "c4_lineitem"):
+        return WL.generate(name, rows)
     rng = np.random.default_rng(7)
+    E = WL.Expected
     if name == "c1_plain_i32":
         v = np.random.default_rng(1).integers(-2**31, 2**31 - 1, size=rows, dtype=np.int64).astype(np.int32)
-        return [writer.write_column_chunk(abi.INT32, v, abi.PLAIN)]
-    if name == "c2_zipf2":
-        import bench
-        ch, _, _ = bench.make_c2(rows, a=2.0)
-        return [ch]
-    if name == "c3_mixed":
-        dl = nulls(rows, 0.1, 8)
-        n = int(dl.sum())
-        out = []
-        for k in range(2):
-            walk = np.cumsum(rng.integers(-100, 1000, size=n)).astype(np.int64)
-            out.append(writer.write_column_chunk(abi.INT32, (walk % (1 << 30)).astype(np.int32), abi.DELTA_BINARY_PACKED,
-                                                 def_levels=dl, max_def=1, version=2))
-            out.append(writer.write_column_chunk(abi.INT64, walk * 1000 + k, abi.DELTA_BINARY_PACKED,
-                                                 def_levels=dl, max_def=1, version=2))
-            out.append(writer.write_column_chunk(abi.DOUBLE, rng.standard_normal(n), abi.PLAIN, def_levels=dl,
-                                                 max_def=1, version=2))
-            out.append(writer.write_column_chunk(abi.BYTE_ARRAY, writer.BinaryValues.random(n, 4, 32, seed=k), abi.PLAIN,
-                                                 def_levels=dl, max_def=1, version=2))
-            print(f"[gen c3_mixed] {len(out)} of 8 columns", file=sys.stderr, flush=True)
-        return out
-    if name == "c5_levels":
-        recs = rows
-        lens = rng.poisson(3, size=recs)
-        null_list = rng.random(recs) < 0.1
-        slots = np.where(null_list | (lens == 0), 1, lens)
-        n_slots = int(slots.sum())
-        starts = np.concatenate([[0], np.cumsum(slots)[:-1]])
-        rl = np.ones(n_slots, dtype=np.uint8)
-        rl[starts] = 0
-        dl = np.full(n_slots, 3, dtype=np.uint8)
-        dl[rng.random(n_slots) < 0.1] = 2
-        dl[starts[null_list]] = 0
-        dl[starts[~null_list & (lens == 0)]] = 1
-        n = int((dl == 3).sum())
-        vals = rng.integers(-2**40, 2**40, size=n)
-        return [writer.write_column_chunk(abi.INT64, vals, abi.PLAIN, def_levels=dl, rep_levels=rl, max_def=3, max_rep=1,
-                                          page_rows=20000)]
+        return WL.Workload(name, [writer.write_column_chunk(abi.INT32, v, abi.PLAIN)], [E(v)])
     if name.startswith("str_"):
         enc = {"str_plain": abi.PLAIN, "str_dict": abi.RLE_DICTIONARY, "str_dlba": abi.DELTA_LENGTH_BYTE_ARRAY,
                "str_dba": abi.DELTA_BYTE_ARRAY}[name]
@@ -89,12 +54,11 @@ def gen(name, rows):
             runs = np.minimum(rng.zipf(1.5, size=rows), 4096)
             ids = np.repeat(rng.integers(0, 1000, size=runs.size), runs)[:rows]
             ids_fa, order = writer.first_appearance_ids(ids)
-            lens = words.lengths()[order]
-            offs = np.concatenate([[0], np.cumsum(lens)])
-            dwords = writer.BinaryValues(offs, np.concatenate([words.data[words.offsets[o]:words.offsets[o + 1]]
-                                                               for o in order]))
+            wl = [words[int(o)] for o in order]
+            dwords = writer.BinaryValues(np.concatenate([[0], np.cumsum([len(x) for x in wl])]),
+                                         np.frombuffer(b"".join(wl), dtype=np.uint8))
             ch = writer.write_dict_column_from_ids(abi.BYTE_ARRAY, dwords, ids_fa)
-            return [ch]
+            return WL.Workload(name, [ch], [E(WL.binary_take(wl, ids_fa))])
         if enc == abi.DELTA_BYTE_ARRAY:
             # sorted keys with shared prefixes
             keys = np.sort(rng.integers(0, 10**12, size=rows))
@@ -102,20 +66,22 @@ def gen(name, rows):
             lens = np.char.str_len(s)
             offs = np.concatenate([[0], np.cumsum(lens)])
             data = np.frombuffer(b"".join(s.tolist()), dtype=np.uint8)
-            return [writer.write_column_chunk(abi.BYTE_ARRAY, writer.BinaryValues(offs, data), enc)]
-        return [writer.write_column_chunk(abi.BYTE_ARRAY, writer.BinaryValues.random(rows, 4, 32, seed=5), enc)]
+            v = writer.BinaryValues(offs, data)
+            return WL.Workload(name, [writer.write_column_chunk(abi.BYTE_ARRAY, v, enc)], [E(v)])
+        v = writer.BinaryValues.random(rows, 4, 32, seed=5)
+        return WL.Workload(name, [writer.write_column_chunk(abi.BYTE_ARRAY, v, enc)], [E(v)])
     if name == "bss_f64":
-        return [writer.write_column_chunk(abi.DOUBLE, rng.standard_normal(rows), abi.BYTE_STREAM_SPLIT)]
+        v = rng.standard_normal(rows)
+        return WL.Workload(name, [writer.write_column_chunk(abi.DOUBLE, v, abi.BYTE_STREAM_SPLIT)], [E(v)])
     if name == "c2_snappy":   # the headline pages, SNAPPY-compressed (parquet-mr's default codec)
-        import bench
-        ch, _, _ = bench.make_c2(rows)
-        return [writer.snappy_chunk(ch)]
+        w = WL.c2(rows)
+        return WL.Workload(name, [writer.snappy_chunk(w.chunks[0])], w.expect)
     if name == "plain_i64_snappy":  # int64 random walk, PLAIN pages, SNAPPY
         walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
-        return [writer.snappy_chunk(writer.write_column_chunk(abi.INT64, walk, abi.PLAIN))]
+        return WL.Workload(name, [writer.snappy_chunk(writer.write_column_chunk(abi.INT64, walk, abi.PLAIN))], [E(walk)])
     if name == "delta_i64":
         walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
-        return [writer.write_column_chunk(abi.INT64, walk, abi.DELTA_BINARY_PACKED)]
+        return WL.Workload(name, [writer.write_column_chunk(abi.INT64, walk, abi.DELTA_BINARY_PACKED)], [E(walk)])
     raise ValueError(name)
 
 
@@ -184,7 +150,8 @@ def run(name, rows, steps, warmup, cpu_budget):
     import torch
     from pqgpu import decoder as D
     t0 = time.perf_counter()
-    chunks = gen(name, rows)
+    work = gen(name, rows)
+    chunks = work.chunks
     compressed = any(p.codec for ch in chunks for p in ch.pages)
     t_gen = time.perf_counter() - t0
     dec = D.Decoder(0)
@@ -195,7 +162,12 @@ def run(name, rows, steps, warmup, cpu_budget):
         batch = writer.build_batch(chunks)
         dbatch = dec.upload(batch)
     cols, st = dec.decode(dbatch)  # sizes BYTE_ARRAY buffers, first full decode
+    WL.verify(cols, work, "decode")
     plan = dec.plan(dbatch, cols)
+    plan.launch()
+    rc, st = plan.sync()
+    assert rc == 0, st.message
+    WL.verify(cols, work, "first plan launch")
     for _ in range(warmup):
         plan.launch()
     rc, st = plan.sync()
@@ -210,6 +182,7 @@ def run(name, rows, steps, warmup, cpu_budget):
     torch.cuda.synchronize()
     rc, st = plan.sync()
     assert rc == 0, st.message
+    WL.verify(cols, work, "after the timed launches")
     ms = float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(steps)]))
     nvals = sum(c.n_values for c in cols)
     nslots = sum(batch.column_slots)
@@ -218,7 +191,8 @@ def run(name, rows, steps, warmup, cpu_budget):
     res = {"workload": name, "rows": rows, "columns": len(batch.columns), "pages": batch.n_pages,
            "values": nvals, "slots": nslots, "ms_per_launch": ms, "values_per_s": nvals / (ms / 1e3),
            "encoded_bytes": enc, "output_bytes": out, "gbps": gbps, "hbm_frac": gbps / HBM_PEAK_GBS,
-           "kernels_per_launch": plan.kernel_count, "input_gen_s": t_gen}
+           "kernels_per_launch": plan.kernel_count, "input_gen_s": t_gen,
+           "verified": "decoded columns == generated values (decode, first plan launch, after the timed launches)"}
     if compressed:
         comp = sum(len(p.body) for ch in chunks for p in ch.pages) + sum(len(ch.dict_page or b"") for ch in chunks)
         ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -257,12 +231,13 @@ def main():
     default_rows = {"c1_plain_i32": 1_000_000, "c2_zipf2": 100_000_000, "c3_mixed": 100_000_000,
                     "c5_levels": 100_000_000, "str_plain": 20_000_000, "str_dict": 20_000_000,
                     "str_dlba": 20_000_000, "str_dba": 20_000_000, "bss_f64": 100_000_000, "delta_i64": 100_000_000,
-                    "c2_snappy": 100_000_000, "plain_i64_snappy": 100_000_000}
+                    "c2_snappy": 100_000_000, "plain_i64_snappy": 100_000_000,
+                    "c4_lineitem": 8_000_000}
     for w in args.workloads:
         rows = args.rows or default_rows[w]
         if args.gen_only:
             t0 = time.perf_counter()
-            b = writer.build_batch(gen(w, rows))
+            b = writer.build_batch(gen(w, rows).chunks)
             print(json.dumps({"workload": w, "rows": rows, "pages": b.n_pages, "bytes": int(b.data.size),
                               "gen_s": time.perf_counter() - t0}), flush=True)
             continue

@@ -69,6 +69,17 @@ def make_c2(n_rows, seed_dict=42, seed_runs=43, a=1.5, card=1000, max_run=4096, 
     return chunk, dict_vals, ids
 
 
+def binary_take(words, ids):
+    """BinaryValues of words[ids] (words: list of bytes; vectorized)."""
+    lens = np.array([len(w) for w in words], dtype=np.int64)
+    starts = np.concatenate([[0], np.cumsum(lens)])[:-1]
+    blob = np.frombuffer(b"".join(words), dtype=np.uint8)
+    vl = lens[ids]
+    offs = np.concatenate([[0], np.cumsum(vl)]).astype(np.int64)
+    pos = np.arange(int(offs[-1]), dtype=np.int64) - np.repeat(offs[:-1], vl) + np.repeat(starts[ids], vl)
+    return writer.BinaryValues(offs, blob[pos])
+
+
 def c2(rows, a=1.5, seed_runs=43):
     ch, dv, ids = make_c2(rows, a=a, seed_runs=seed_runs)
     return Workload(f"c2 zipf={a}", [ch], [Expected(dv[ids])])
