@@ -95,7 +95,9 @@ enum pqg_error {
                                    (DeltaBinaryPackingValuesReader.java:115-119) */
   PQG_ERR_CORRUPT = 18,         /* section lengths inconsistent with the page (negative/oversized length prefix) */
   PQG_ERR_NO_DICTIONARY = 19,   /* "could not read page ... as the dictionary was missing" (ColumnReaderBase.java:709-712) */
-  PQG_ERR_DICT_ENCODING = 20    /* "Dictionary data encoding type not supported" (PlainValuesDictionary.java:49-52) */
+  PQG_ERR_DICT_ENCODING = 20,   /* "Dictionary data encoding type not supported" (PlainValuesDictionary.java:49-52) */
+  PQG_ERR_CRC = 21              /* ParquetDecodingException "could not verify page integrity, CRC checksum
+                                   verification failed" (ParquetFileReader.java:1805-1813) */
 };
 
 /*
@@ -131,6 +133,14 @@ typedef struct pqg_page_desc {
  * For pqg_decode these are device pointers; the per-page value counts are
  * written to `page_value_counts` (device, one uint32 per page of the batch, optional).
  */
+/* pqg_column_desc.flags: PQG_COLUMN_DICTIONARY_IDS — `values` receives the uint32 dictionary id of
+ * every non-null value instead of the value (DictionaryValuesReader.readValueDictionaryId,
+ * parquet-column/src/main/java/org/apache/parquet/column/values/dictionary/DictionaryValuesReader.java:67-73),
+ * any physical type; a page of the column that is not dictionary-encoded fails with
+ * PQG_ERR_UNSUPPORTED (ValuesReader.readValueDictionaryId throws UnsupportedOperationException,
+ * ValuesReader.java:142-144). */
+#define PQG_COLUMN_DICTIONARY_IDS 1
+
 typedef struct pqg_column_desc {
   int32_t physical_type;     /* pqg_physical_type */
   int32_t type_length;       /* FIXED_LEN_BYTE_ARRAY length */
@@ -140,7 +150,7 @@ typedef struct pqg_column_desc {
   uint32_t dict_size;        /* dictionary page body bytes */
   uint32_t dict_num_values;  /* DictionaryPageHeader.num_values */
   int32_t dict_encoding;     /* PLAIN or PLAIN_DICTIONARY */
-  int32_t reserved0;
+  int32_t flags;             /* PQG_COLUMN_* (0: decode values) */
   void* values;              /* dense output values */
   uint64_t values_capacity;  /* capacity in elements */
   uint8_t* def_levels;       /* per-slot definition levels (may be NULL) */
@@ -282,6 +292,57 @@ typedef struct pqg_snappy_job {
 int pqg_snappy_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, uint8_t* d_dst, uint64_t dst_bytes,
                           const pqg_snappy_job* d_jobs, int n_jobs, int32_t* d_status);
 int pqg_snappy_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_status* st);
+
+/* ---- page framing (host) ----------------------------------------------------
+ * File bytes in: the page headers of one raw column chunk, as
+ * ParquetFileReader.Chunk.readAllPages reads them
+ * (parquet-hadoop/src/main/java/org/apache/parquet/hadoop/ParquetFileReader.java:1824-1979;
+ * header = Thrift compact PageHeader, Util.readPageHeader,
+ * parquet-format-structures/src/main/java/org/apache/parquet/format/Util.java:127-131).
+ * Host code: no device needed. */
+enum pqg_page_type { PQG_DATA_PAGE = 0, PQG_INDEX_PAGE = 1, PQG_DICTIONARY_PAGE = 2, PQG_DATA_PAGE_V2 = 3 };
+
+typedef struct pqg_page_header {
+  int32_t type;                          /* pqg_page_type */
+  int32_t uncompressed_page_size;
+  int32_t compressed_page_size;
+  int32_t has_crc;
+  uint32_t crc;
+  int32_t num_values;                    /* data pages: slots; dictionary page: entries */
+  int32_t encoding;                      /* values encoding / dictionary page encoding */
+  int32_t definition_level_encoding;     /* DataPageHeader (V1) */
+  int32_t repetition_level_encoding;     /* DataPageHeader (V1) */
+  int32_t num_nulls;                     /* DataPageHeaderV2 */
+  int32_t num_rows;                      /* DataPageHeaderV2 */
+  int32_t definition_levels_byte_length; /* DataPageHeaderV2 */
+  int32_t repetition_levels_byte_length; /* DataPageHeaderV2 */
+  int32_t is_compressed;                 /* DataPageHeaderV2 (default 1) */
+  int32_t is_sorted;                     /* DictionaryPageHeader */
+  int32_t reserved;
+  uint64_t header_offset;                /* offset of the header in the chunk buffer */
+  uint64_t body_offset;                  /* offset of the page body (compressed_page_size bytes) */
+} pqg_page_header;
+
+/* CRC-32 (java.util.zip.CRC32) of n bytes, continuing from `crc` (0 to start). */
+uint32_t pqg_crc32(uint32_t crc, const uint8_t* data, uint64_t n);
+
+/* Walk the page headers of the chunk bytes [chunk, chunk + chunk_len) until `value_count` data
+ * values have been read (ColumnMetaData.num_values; < 0: every header up to the end).
+ * DICTIONARY_PAGE, DATA_PAGE and DATA_PAGE_V2 headers go to `headers` in order; other page types
+ * are skipped (as readAllPages does). verify_crc != 0: pages whose header has a crc are checked
+ * (CRC-32 of the page's compressed bytes) -> PQG_ERR_CRC with st->page = the page.
+ * Errors: a second dictionary page, unreadable header, V2 level lengths past the page -> CORRUPT;
+ * a body past the chunk -> EOF; value count mismatch at the end -> CORRUPT ("Expected N values in
+ * column chunk ..."). *n_headers = headers found; capacity too small -> INVALID_ARG with
+ * st->value_index = the count needed. */
+int pqg_frame_chunk(const uint8_t* chunk, uint64_t chunk_len, int64_t value_count, int verify_crc,
+                    pqg_page_header* headers, int capacity, int* n_headers, pqg_status* st);
+
+/* Headers of an UNCOMPRESSED chunk placed at byte `chunk_offset` of a batch buffer -> the
+ * pqg_page_desc entries of its data pages (column index `column`) and the dictionary fields of
+ * `col` (may be NULL). A compressed page -> PQG_ERR_UNSUPPORTED (decompress first). */
+int pqg_pages_from_headers(const pqg_page_header* headers, int n_headers, uint64_t chunk_offset, int column,
+                           pqg_column_desc* col, pqg_page_desc* pages, int capacity, int* n_pages, pqg_status* st);
 
 /* Human-readable name of an error code. */
 const char* pqg_error_name(int code);

@@ -84,6 +84,11 @@ int elem_width(int t, int tl) {
   }
 }
 
+// PQG_COLUMN_DICTIONARY_IDS columns write uint32 ids; BYTE_ARRAY columns otherwise write offsets + bytes
+bool ids_mode(const pqg_column_desc& c) { return (c.flags & PQG_COLUMN_DICTIONARY_IDS) != 0; }
+bool bin_out(const pqg_column_desc& c) { return c.physical_type == PQG_BYTE_ARRAY && !ids_mode(c); }
+int out_width(const pqg_column_desc& c) { return ids_mode(c) ? 4 : elem_width(c.physical_type, c.type_length); }
+
 // Error words: 3 per page + 3 per column (dictionary pages), padded to 16 bytes; the error
 // counter follows them in the same allocation.
 size_t err_region_bytes(int n_pages, int n_cols) {
@@ -178,6 +183,7 @@ const char* pqg_error_name(int code) {
     case PQG_ERR_CORRUPT: return "CORRUPT";
     case PQG_ERR_NO_DICTIONARY: return "NO_DICTIONARY";
     case PQG_ERR_DICT_ENCODING: return "DICT_ENCODING";
+    case PQG_ERR_CRC: return "CRC";
     default: return "UNKNOWN";
   }
 }
@@ -270,7 +276,7 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     d.elem_width = elem_width(c.physical_type, c.type_length);
     d.values = c.values;
     d.binary_data = c.binary_data;
-    d.binary_capacity = c.physical_type == PQG_BYTE_ARRAY ? c.binary_capacity : 0;
+    d.binary_capacity = bin_out(c) ? c.binary_capacity : 0;
     d.def_levels = c.max_def > 0 ? c.def_levels : nullptr;
     d.rep_levels = c.max_rep > 0 ? c.rep_levels : nullptr;
     P->col_nullable[(size_t)i] = (c.max_def > 0 || c.max_rep > 0) ? 1 : 0;
@@ -353,6 +359,14 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     const int t = c.physical_type;
     const int ew = elem_width(t, c.type_length);
     int cls = -1, herr = 0;
+    if (ids_mode(c)) {
+      // readValueDictionaryId: dictionary pages give their ids (any physical type, k_dict_fused<4, IDS>
+      // writing straight into the column's uint32 values); other readers throw (ValuesReader.java:123-125)
+      if (g.encoding != PQG_PLAIN_DICTIONARY && g.encoding != PQG_RLE_DICTIONARY) herr = PQG_ERR_UNSUPPORTED;
+      else if (c.dict_offset < 0) herr = PQG_ERR_NO_DICTIONARY;
+      else if (t == PQG_BOOLEAN) herr = PQG_ERR_UNSUPPORTED;
+      else cls = C_IDS;
+    } else
     switch (g.encoding) {
       case PQG_PLAIN_DICTIONARY:
       case PQG_RLE_DICTIONARY:
@@ -421,11 +435,12 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
   std::vector<uint8_t> needs_ids((size_t)std::max(n_cols, 1), 0);
   for (int p : cls_lists[C_IDS]) needs_ids[(size_t)P->h_work[(size_t)p].column] = 1;
   for (int i = 0; i < n_cols; i++) {  // blen first: the part cleared before every launch
-    if (cols[i].physical_type == PQG_BYTE_ARRAY || needs_ids[(size_t)i]) blen_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
+    if (ids_mode(cols[i])) continue;  // ids go straight to the column's values
+    if (bin_out(cols[i]) || needs_ids[(size_t)i]) blen_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
   }
   P->blen_bytes = sc;
   for (int i = 0; i < n_cols; i++) {
-    if (cols[i].physical_type != PQG_BYTE_ARRAY) continue;
+    if (!bin_out(cols[i])) continue;
     bin_cols.push_back(i);
     P->bin_capacity[(size_t)i] = cols[i].binary_capacity;
     bsrc_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
@@ -443,6 +458,7 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
   for (int k : {C_IDS, C_BINP, C_DLBA})
     for (int p : cls_lists[(size_t)k]) {
       const PageWork& w = P->h_work[(size_t)p];
+      if (k == C_IDS && ids_mode(cols[w.column])) continue;  // the ids are the output
       if (k == C_IDS && cols[w.column].physical_type != PQG_BYTE_ARRAY) {
         fixd.push_back(p);
         continue;
@@ -538,7 +554,7 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     auto at = [&](uint64_t o) -> void* { return o == ~0ull ? nullptr : (void*)(scb + o); };
     for (int i = 0; i < n_cols; i++) {
       ColumnDev& d = hc[(size_t)i];
-      d.blen = (uint32_t*)at(blen_off[(size_t)i]);
+      d.blen = ids_mode(cols[i]) ? (uint32_t*)cols[i].values : (uint32_t*)at(blen_off[(size_t)i]);
       d.bsrc = (uint32_t*)at(bsrc_off[(size_t)i]);
       d.dict_len = (uint32_t*)at(dlen_off[(size_t)i]);
       d.dict_src = (uint32_t*)at(dsrc_off[(size_t)i]);
@@ -844,7 +860,7 @@ int pqg_decode(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, pqg_colum
       if (pages[p].column >= 0 && pages[p].column < n_cols) slots[(size_t)pages[p].column] += pages[p].num_values;
     for (int i = 0; i < n_cols; i++) {
       bool lv = cols[i].max_def > 0 || cols[i].max_rep > 0;
-      const uint64_t need = slots[(size_t)i] + (cols[i].physical_type == PQG_BYTE_ARRAY ? 1 : 0);  // offsets[n + 1]
+      const uint64_t need = slots[(size_t)i] + (bin_out(cols[i]) ? 1 : 0);  // offsets[n + 1]
       if (need > cols[i].values_capacity || (need && !cols[i].values) ||
           (lv && ((cols[i].max_def > 0 && cols[i].def_levels) || (cols[i].max_rep > 0 && cols[i].rep_levels)) &&
            slots[(size_t)i] > cols[i].levels_capacity)) {
@@ -937,7 +953,7 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   // exact size the device counted
   std::vector<uint64_t> bin_cap(nc, 0);
   for (int i = 0; i < n_cols; i++)
-    if (cols[i].physical_type == PQG_BYTE_ARRAY)
+    if (bin_out(cols[i]))
       bin_cap[(size_t)i] = page_bytes[(size_t)i] + (cols[i].dict_offset >= 0 ? 2 * (uint64_t)cols[i].dict_size : 0) + 64;
   if (ctx->host_bytes.ensure(n_bytes + pad) != hipSuccess || ctx->pin_in.ensure(n_bytes + pad) != hipSuccess ||
       ctx->host_counts.ensure(sizeof(uint32_t) * (size_t)std::max(n_pages, 1)) != hipSuccess) {
@@ -960,8 +976,8 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
     // device layout of outputs: per column values | def | rep | binary bytes, 256-B aligned
     total = 0;
     for (int i = 0; i < n_cols; i++) {
-      const bool bin = cols[i].physical_type == PQG_BYTE_ARRAY;
-      int w = elem_width(cols[i].physical_type, cols[i].type_length);
+      const bool bin = bin_out(cols[i]);
+      int w = out_width(cols[i]);
       if (w <= 0) w = 8;
       off_v[(size_t)i] = total;
       total = al(total + (slots[(size_t)i] + (bin ? 1 : 0)) * (uint64_t)w);
@@ -978,7 +994,7 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
     }
     uint8_t* dout = (uint8_t*)ctx->host_out.p;
     for (int i = 0; i < n_cols; i++) {
-      const bool bin = cols[i].physical_type == PQG_BYTE_ARRAY;
+      const bool bin = bin_out(cols[i]);
       dcols[(size_t)i].values = dout + off_v[(size_t)i];
       dcols[(size_t)i].values_capacity = slots[(size_t)i] + (bin ? 1 : 0);
       dcols[(size_t)i].def_levels = (cols[i].max_def > 0 && cols[i].def_levels) ? dout + off_d[(size_t)i] : nullptr;
@@ -1013,9 +1029,9 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   const uint8_t* po = (const uint8_t*)ctx->pin_out.p;
   std::vector<HostCopy> jobs;
   for (int i = 0; i < n_cols; i++) {
-    const int w = elem_width(cols[i].physical_type, cols[i].type_length);
+    const int w = out_width(cols[i]);
     const uint64_t n = std::min<uint64_t>(cols[i].values_written, cols[i].values_capacity);
-    if (cols[i].physical_type != PQG_BYTE_ARRAY && cols[i].values && n)
+    if (!bin_out(cols[i]) && cols[i].values && n)
       jobs.push_back({(uint8_t*)cols[i].values, off_v[(size_t)i], n * (uint64_t)w});
     if (cols[i].max_def > 0 && cols[i].def_levels)
       jobs.push_back({cols[i].def_levels, off_d[(size_t)i], std::min(slots[(size_t)i], cols[i].levels_capacity)});
@@ -1067,7 +1083,7 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   if (!ok || hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
   phase("d2h+copy");
   for (int i = 0; i < n_cols; i++) {
-    if (cols[i].physical_type != PQG_BYTE_ARRAY) continue;
+    if (!bin_out(cols[i])) continue;
     // offsets[n + 1] and the bytes they span
     const uint64_t n = std::min<uint64_t>(cols[i].values_written, cols[i].values_capacity ? cols[i].values_capacity - 1 : 0);
     const int64_t* offs = (const int64_t*)(po + off_v[(size_t)i]);

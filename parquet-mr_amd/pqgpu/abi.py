@@ -43,6 +43,9 @@ ERR_DELTA_PAST_END = 17
 ERR_CORRUPT = 18
 ERR_NO_DICTIONARY = 19
 ERR_DICT_ENCODING = 20
+ERR_CRC = 21
+
+COLUMN_DICTIONARY_IDS = 1  # pqg_column_desc.flags: values <- uint32 dictionary ids
 
 ERROR_NAMES = {
     OK: "OK", ERR_INVALID_ARG: "INVALID_ARG", ERR_UNSUPPORTED: "UNSUPPORTED", ERR_HIP: "HIP",
@@ -50,7 +53,7 @@ ERROR_NAMES = {
     ERR_BIT_WIDTH: "BIT_WIDTH", ERR_DICT_ID: "DICT_ID", ERR_EMPTY_PAGE: "EMPTY_PAGE",
     ERR_EMPTY_PACKED_RUN: "EMPTY_PACKED_RUN", ERR_DELTA_CONFIG: "DELTA_CONFIG",
     ERR_DELTA_PAST_END: "DELTA_PAST_END", ERR_CORRUPT: "CORRUPT", ERR_NO_DICTIONARY: "NO_DICTIONARY",
-    ERR_DICT_ENCODING: "DICT_ENCODING",
+    ERR_DICT_ENCODING: "DICT_ENCODING", ERR_CRC: "CRC",
 }
 
 
@@ -90,7 +93,7 @@ class ColumnDesc(C.Structure):
         ("dict_size", C.c_uint32),
         ("dict_num_values", C.c_uint32),
         ("dict_encoding", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("flags", C.c_int32),
         ("values", C.c_void_p),
         ("values_capacity", C.c_uint64),
         ("def_levels", C.c_void_p),
@@ -100,6 +103,19 @@ class ColumnDesc(C.Structure):
         ("binary_capacity", C.c_uint64),
         ("values_written", C.c_uint64),
     ]
+
+
+class PageHeader(C.Structure):
+    """pqg_page_header (parquet.thrift PageHeader fields the reader uses)."""
+    _fields_ = [("type", C.c_int32), ("uncompressed_page_size", C.c_int32), ("compressed_page_size", C.c_int32),
+                ("has_crc", C.c_int32), ("crc", C.c_uint32), ("num_values", C.c_int32), ("encoding", C.c_int32),
+                ("definition_level_encoding", C.c_int32), ("repetition_level_encoding", C.c_int32),
+                ("num_nulls", C.c_int32), ("num_rows", C.c_int32), ("definition_levels_byte_length", C.c_int32),
+                ("repetition_levels_byte_length", C.c_int32), ("is_compressed", C.c_int32), ("is_sorted", C.c_int32),
+                ("reserved", C.c_int32), ("header_offset", C.c_uint64), ("body_offset", C.c_uint64)]
+
+
+DATA_PAGE, INDEX_PAGE, DICTIONARY_PAGE, DATA_PAGE_V2 = 0, 1, 2, 3
 
 
 class Status(C.Structure):

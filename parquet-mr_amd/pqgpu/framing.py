@@ -209,3 +209,26 @@ def read_footer_length(buf):
 
 
 TYPE_BY_NAME = {v: k for k, v in abi.TYPE_NAMES.items()}
+
+
+def frame_chunk_native(chunk_bytes, value_count=-1, verify_crc=True):
+    """The C-ABI page framing (pqg_frame_chunk, host code of libpqgpu.so) over raw chunk bytes.
+    Returns (rc, status, [abi.PageHeader, ...])."""
+    import ctypes as C
+
+    import numpy as np
+
+    from . import native
+    buf = np.frombuffer(bytes(chunk_bytes), dtype=np.uint8)
+    L = native.lib()
+    n = C.c_int(0)
+    st = abi.Status()
+    cap = 64
+    while True:
+        hdrs = (abi.PageHeader * cap)()
+        rc = L.pqg_frame_chunk(buf.ctypes.data if buf.size else None, buf.size, value_count, int(bool(verify_crc)),
+                               C.addressof(hdrs), cap, C.byref(n), C.byref(st))
+        if rc == abi.ERR_INVALID_ARG and n.value > cap:
+            cap = n.value
+            continue
+        return rc, st, [hdrs[i] for i in range(min(n.value, cap))]

@@ -1,0 +1,116 @@
+/*
+ * ValuesReader over one page's slice of a GPU-decoded column
+ * (parquet-column/src/main/java/org/apache/parquet/column/values/ValuesReader.java:36-203).
+ * Same state machine as pqg_values_reader (include/pqgpu_reader.h, parquet-mr_amd/csrc/pqgpu_reader.cpp),
+ * which tests/c/harness.c pins: reads of another type throw UnsupportedOperationException, a decode
+ * error surfaces at the read of the failing value, a read past the page's values throws
+ * ParquetDecodingException (the readers' wrapped EOFException).
+ */
+package org.apache.parquet.column.values.gpu;
+
+import java.io.IOException;
+import org.apache.parquet.bytes.ByteBufferInputStream;
+import org.apache.parquet.column.values.ValuesReader;
+import org.apache.parquet.io.ParquetDecodingException;
+import org.apache.parquet.io.api.Binary;
+
+public final class GpuValuesReader extends ValuesReader {
+  private static final int BOOLEAN = 0, INT32 = 1, INT64 = 2, INT96 = 3, FLOAT = 4, DOUBLE = 5, BYTE_ARRAY = 6,
+      FIXED_LEN_BYTE_ARRAY = 7;
+  private final GpuPageBatch batch;
+  private final int column;
+  private final int type;
+  private final boolean ids;
+  private final long end;
+  private final long errorAt;
+  private long pos;
+
+  GpuValuesReader(GpuPageBatch batch, int column, long first, long end, long errorAt) {
+    this.batch = batch;
+    this.column = column;
+    this.type = batch.physicalType[column];
+    this.ids = (batch.flags[column] & PqGpu.COLUMN_DICTIONARY_IDS) != 0;
+    this.pos = first;
+    this.end = end;
+    this.errorAt = errorAt;
+  }
+
+  /** The page was decoded on the device: its section is consumed as a whole (:107-114 contract). */
+  @Override
+  public void initFromPage(int valueCount, ByteBufferInputStream in) throws IOException {
+    in.skipFully(in.available());
+  }
+
+  public long remaining() {
+    return Math.max(0, end - pos);
+  }
+
+  private int next() {
+    if (errorAt >= 0 && pos >= errorAt) throw batch.exception(batch.code, "value " + pos + " of column " + column);
+    if (pos >= end) throw new ParquetDecodingException("no more values in the page (column " + column + ")");
+    return (int) pos++;
+  }
+
+  private void require(boolean ok) {
+    if (!ok) throw new UnsupportedOperationException();
+  }
+
+  @Override
+  public int readValueDictionaryId() {
+    require(ids);
+    return ((int[]) batch.values[column])[next()];
+  }
+
+  @Override
+  public boolean readBoolean() {
+    require(!ids && type == BOOLEAN);
+    return ((byte[]) batch.values[column])[next()] != 0;
+  }
+
+  @Override
+  public int readInteger() {
+    require(!ids && type == INT32);
+    return ((int[]) batch.values[column])[next()];
+  }
+
+  @Override
+  public long readLong() {
+    require(!ids && type == INT64);
+    return ((long[]) batch.values[column])[next()];
+  }
+
+  @Override
+  public float readFloat() {
+    require(!ids && type == FLOAT);
+    return ((float[]) batch.values[column])[next()];
+  }
+
+  @Override
+  public double readDouble() {
+    require(!ids && type == DOUBLE);
+    return ((double[]) batch.values[column])[next()];
+  }
+
+  @Override
+  public Binary readBytes() {
+    require(!ids && (type == BYTE_ARRAY || type == FIXED_LEN_BYTE_ARRAY || type == INT96));
+    int i = next();
+    if (type == BYTE_ARRAY) {
+      long[] offsets = (long[]) batch.values[column];
+      int a = (int) offsets[i], b = (int) offsets[i + 1];
+      return Binary.fromConstantByteArray(batch.binary[column], a, b - a);
+    }
+    int w = type == INT96 ? 12 : batch.typeLength[column];
+    return Binary.fromConstantByteArray((byte[]) batch.values[column], i * w, w);
+  }
+
+  @Override
+  public void skip() {
+    next();
+  }
+
+  @Override
+  public void skip(int n) {
+    for (int k = 0; k < n; k++) next();
+  }
+}

@@ -12,10 +12,11 @@ from pqgpu import abi, native
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "pqgpu.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in sorted(os.listdir(os.path.join(REPO, "include"))) if h.endswith(".h")]
 
 
 def declared_functions():
-    text = open(HEADER).read()
+    text = "".join(open(h).read() for h in HEADERS)
     return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\*\s]+?\b(pqg_\w+)\s*\(", text, re.M)))
 
 
