@@ -190,7 +190,11 @@ void* pqg_ctx_stream(pqg_ctx* ctx);
 /* ---- device-resident batch decode ----------------------------------------
  * `d_bytes` is a 4-byte aligned DEVICE buffer holding every page body (and
  * dictionary page) the descriptors refer to, padded by at least 64 readable
- * bytes after the last page. Column output pointers are DEVICE pointers. Pages of one column
+ * bytes after the last page; `n_bytes` is its readable size INCLUDING that
+ * padding (device loads are range-checked per dword against it, so a page that
+ * ends at an unaligned offset needs the padding inside n_bytes). Page offsets may
+ * have any alignment (raw file bytes); 16-B aligned is fastest. Column output
+ * pointers are DEVICE pointers. Pages of one column
  * must appear in page order; pages of several columns may be interleaved.
  * Asynchronous: errors are reported by pqg_sync. */
 int pqg_decode(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes,

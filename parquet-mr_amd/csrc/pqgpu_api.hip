@@ -1003,7 +1003,9 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
       dcols[(size_t)i].binary_data = bin ? dout + off_b[(size_t)i] : nullptr;
       dcols[(size_t)i].binary_capacity = bin_cap[(size_t)i];
     }
-    rc = pqg_decode(ctx, (const uint8_t*)ctx->host_bytes.p, n_bytes, dcols.data(), n_cols, pages, n_pages,
+    // the zero padding is part of the readable range: loads are range-checked per dword against it, and
+    // a page ending at an unaligned offset close to n_bytes (raw file bytes) needs its last dword whole
+    rc = pqg_decode(ctx, (const uint8_t*)ctx->host_bytes.p, n_bytes + pad, dcols.data(), n_cols, pages, n_pages,
                     (uint32_t*)ctx->host_counts.p, st);
     if (rc) return rc;
     rc = pqg_sync(ctx, &st2);
