@@ -116,15 +116,34 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
 //      almost always larger than the section) is resolved by a search for succ(i) in the list.
 // So the per-value work is parallel; the serial steps are one per 64 values plus one per
 // false candidate that sits between two true ones.
-constexpr uint32_t BW_WIN = 1024;  // window bytes (16 positions per lane)
-
-constexpr uint32_t BW_CAP = 256;   // candidates per pass over a tile (more: the tile is taken in parts)
+#ifndef PQG_BW_WIN
+#define PQG_BW_WIN 2048
+#endif
+constexpr uint32_t BW_WIN = PQG_BW_WIN;    // window bytes
+constexpr uint32_t BW_Q = BW_WIN / 64;     // positions per lane (16 or 32)
+constexpr uint32_t BW_CAP = BW_WIN / 4;    // candidates per pass over a tile (more: the tile is taken in parts)
+static_assert(BW_Q == 16 || BW_Q == 32, "window of 1 or 2 KiB");
 
 struct BinWalkLds {
   uint2 pn[BW_CAP];       // candidate positions (ascending; bit 31: accepted) and successors (p + 4 + len)
   uint16_t idx[BW_WIN];   // window offset -> candidate index (valid where pos[idx] matches)
   uint32_t cut;           // position of candidate BW_CAP (the end of this pass) when there are more
 };
+
+// Window bytes of one lane: [B + BW_Q * lane, + BW_Q + 4) as BW_Q / 4 + 1 dwords.
+struct BwBytes {
+  u32x4 a, b;  // b unused for 16 positions
+  uint32_t x;
+};
+__device__ __forceinline__ BwBytes bw_load(rsrc_t rs, uint32_t B) {
+  const uint32_t o = B + BW_Q * lane_id();
+  BwBytes r;
+  r.a = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0);
+  if constexpr (BW_Q == 32) r.b = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(o + 16u), 0, 0);
+  else r.b = u32x4{0, 0, 0, 0};
+  r.x = ld32(rs, o + BW_Q);
+  return r;
+}
 
 // Error of a value whose length prefix starts at p (not a candidate).
 __device__ __forceinline__ int bin_value_error(rsrc_t rs, uint32_t p, uint32_t end, bool dict) {
@@ -143,43 +162,46 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
   const uint32_t lane = lane_id();
   uint32_t pos = uni(beg), produced = 0;
   int code = 0;
-  // fixed 1 KiB tiles of the page; the tile after the current one is always in flight
+  // fixed BW_WIN tiles of the page; the tile after the current one is always in flight
   uint32_t B = pos & ~(BW_WIN - 1u);
-  u32x4 d4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(B + 16u * lane), 0, 0);
-  uint32_t d5 = ld32(rs, B + 16u * lane + 16u);
-  u32x4 n4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(B + BW_WIN + 16u * lane), 0, 0);
-  uint32_t n5 = ld32(rs, B + BW_WIN + 16u * lane + 16u);
+  BwBytes cur_b = bw_load(rs, B);
+  BwBytes nxt_b = bw_load(rs, B + BW_WIN);
   while (true) {
     pos = uni(pos);
     produced = uni(produced);
     B = uni(B);
     if (produced >= N) break;
     if ((uint64_t)pos + 4u > end) { code = PQG_ERR_EOF; break; }
-    // ---- candidates of the tile [B, B + BW_WIN) holding pos (its bytes are in d4 / d5)
-    const uint32_t base = B + 16u * lane;
-    const uint32_t d[5] = {d4.x, d4.y, d4.z, d4.w, d5};
+    // ---- candidates of the tile [B, B + BW_WIN) holding pos (its bytes are in cur_b)
+    const uint32_t base = B + BW_Q * lane;
+    uint32_t d[BW_Q / 4 + 1];
+    d[0] = cur_b.a.x; d[1] = cur_b.a.y; d[2] = cur_b.a.z; d[3] = cur_b.a.w;
+    if constexpr (BW_Q == 32) {
+      d[4] = cur_b.b.x; d[5] = cur_b.b.y; d[6] = cur_b.b.z; d[7] = cur_b.b.w;
+    }
+    d[BW_Q / 4] = cur_b.x;
     uint32_t m = 0;
     // 32-bit test (pages < 2 GiB): 0 <= len <= end - (p + 4), i.e. rem = end - 4 - p >= 0 and
     // len <= rem as unsigned (a negative len is >= 2^31 > rem)
     const int32_t rem0 = (int32_t)(end - 4u - base);
 #pragma unroll
-    for (uint32_t q = 0; q < 16; q++) {
+    for (uint32_t q = 0; q < BW_Q; q++) {
       const uint32_t len = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
       const int32_t rem = rem0 - (int32_t)q;
       const bool c = rem >= 0 && len <= (uint32_t)rem;
       m |= (c ? 1u : 0u) << q;
     }
-    if (base < pos) m &= pos - base >= 16u ? 0u : ~((1u << (pos - base)) - 1u);
+    if (base < pos) m &= pos - base >= BW_Q ? 0u : ~((1u << (pos - base)) - 1u);
     uint32_t total;
     const uint32_t rank = wave_excl_scan_u32((uint32_t)__builtin_popcount(m), &total);
 #pragma unroll
-    for (uint32_t q = 0; q < 16; q++)
+    for (uint32_t q = 0; q < BW_Q; q++)
       if ((m >> q) & 1u) {
         const uint32_t r = rank + (uint32_t)__builtin_popcount(m & ((1u << q) - 1u));
         if (r < BW_CAP) {
           const uint32_t nx = base + q + 4u + __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
           *(uint64_t*)&L.pn[r] = (uint64_t)(base + q) | ((uint64_t)nx << 32);
-          L.idx[16u * lane + q] = (uint16_t)r;
+          L.idx[BW_Q * lane + q] = (uint16_t)r;
         } else if (r == BW_CAP) {
           L.cut = base + q;
         }
@@ -194,10 +216,11 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
       break;
     }
     // ---- follow the chain through the candidate list, 64 candidates at a time: every lane
-    // looks up the candidate index of its successor (window offset -> index table), then the
-    // chain is walked from lane 0 (the current value start) with one v_readlane per value;
-    // false candidates (a length read from a shifted prefix, e.g. the byte before a small
-    // length) are simply never reached.
+    // looks up the candidate index of its successor (window offset -> index table). Where the
+    // candidates link one to the next (the usual case: every candidate is a value start), the
+    // batch's chain is the run of consecutive links from lane 0, found by one ballot; otherwise
+    // the chain is walked from lane 0 with one v_readlane per value (false candidates — a length
+    // read from a shifted prefix, e.g. the byte before a small length — are never reached).
     uint32_t i0 = 0, got = 0;
     bool leave = false;  // next position lies past the window
     while (true) {
@@ -210,11 +233,17 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
       const bool hit = t < total && t > k && t - i0 < WAVE && L.pn[t < total ? t : 0].x == s;
       const uint32_t J = hit ? t - i0 : WAVE;
       uint64_t mask = 0;
-      uint32_t j = 0, last = 0;
-      while (j < WAVE) {  // lane 0 holds the current position (a value start)
+      uint32_t last = 0;
+      // lanes 0 .. run are the chain: lane l < run links to lane l + 1 (lane 63 never "links":
+      // its successor is outside the batch); from lane run the chain continues by readlanes only
+      // when its successor is a later lane of the batch (a false candidate in between)
+      const uint64_t next1 = __ballot(hit && t == k + 1);
+      const uint32_t run = ~next1 ? (uint32_t)__builtin_ctzll(~next1) : WAVE - 1u;
+      last = run;
+      mask = last == WAVE - 1u ? ~0ull : ((1ull << (last + 1u)) - 1ull);
+      for (uint32_t j = rdl(J, last); j < WAVE; j = rdl(J, j)) {
         mask |= 1ull << j;
         last = j;
-        j = rdl(J, j);
       }
       const uint32_t n_acc = (uint32_t)__builtin_popcountll(mask);
       const uint32_t room = N - produced - got;
@@ -236,18 +265,11 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
     // ---- advance to the tile holding the next value (requesting the one after it), then
     // store this tile's values
     // (nB == B: the rest of the same tile after a pass cut at BW_CAP candidates; its bytes are
-    // still in d4 / d5)
+    // still in cur_b)
     const uint32_t nB = pos & ~(BW_WIN - 1u);
     if (leave && nB != B) {
-      if (nB == B + BW_WIN) {
-        d4 = n4;
-        d5 = n5;
-      } else {  // a value longer than a tile: the prefetch missed
-        d4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(nB + 16u * lane), 0, 0);
-        d5 = ld32(rs, nB + 16u * lane + 16u);
-      }
-      n4 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(nB + BW_WIN + 16u * lane), 0, 0);
-      n5 = ld32(rs, nB + BW_WIN + 16u * lane + 16u);
+      cur_b = nB == B + BW_WIN ? nxt_b : bw_load(rs, nB);  // else: a value longer than a tile, the prefetch missed
+      nxt_b = bw_load(rs, nB + BW_WIN);
       B = nB;
     }
     wave_sync();

@@ -79,11 +79,17 @@ enum BinKind : uint32_t { BIN_PLAIN = 0, BIN_DLBA = 1, BIN_DICT = 2, BIN_DBA = 3
 #endif
 constexpr uint32_t DICT_CHUNK_TILES = PQG_CHUNK_TILES;
 inline uint32_t dict_chunk_values(int elem_width) { return DICT_CHUNK_TILES * 64u * (16u / (uint32_t)elem_width); }
+// output chunks of a dictionary page of n slots (slots shifted by up to 16 / width - 1 for 16-B alignment)
+inline uint32_t dict_page_chunks(uint32_t n, int elem_width) {
+  const uint32_t ch = dict_chunk_values(elem_width);
+  return (uint32_t)(((uint64_t)n + (uint32_t)(16 / elem_width) - 1 + ch - 1) / ch);
+}
+constexpr int DICT_WPB = 4;  // pages (walkers) / chunks (tiles) per workgroup of the dictionary kernels
 
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                        const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                       bool fused, uint64_t* err, ErrCount err_count);
+                       bool fused, uint32_t walk_wg, uint32_t tile_wg, uint64_t* err, ErrCount err_count);
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                          const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_scan(hipStream_t st, PageWork* work, const int32_t* col_pages, const int32_t* col_page_start,
@@ -97,7 +103,7 @@ hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_
 hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                            const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
-                           uint32_t epoch, bool fused, uint64_t* err, ErrCount err_count);
+                           uint32_t epoch, bool fused, uint32_t walk_wg, uint32_t tile_wg, uint64_t* err, ErrCount err_count);
 // DELTA_LENGTH_BYTE_ARRAY lengths (k_delta into blen, records PageWork::aux)
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count);

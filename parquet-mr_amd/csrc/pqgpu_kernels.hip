@@ -575,17 +575,18 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
 //   acquire (expansion): the status / record loads are issued after the flag load returned the
 //     epoch — the flag value feeds the loop's scalar branch, so its load has completed (vmcnt)
 //     before any later load issues; a compiler barrier keeps those loads below the branch.
-// The memory model's agent-scope fences (buffer_wbl2 sc1 on release, buffer_inv sc1 on acquire)
-// would also write back / invalidate the L2 lines of the expansion's own output and input; both
-// were measured (PQG_HANDOFF = 1: release store, 2: acquire fence, 3: both) and
-// cost 2.6x on C2, while every hand-off datum already bypasses those caches.
+// This is the "{sc0 sc1 stores and loads both sides}" hand-off of MI355X_MICROARCH.md
+// (inter-workgroup visibility: every handed-off byte stored sc1 and loaded sc1, every storing wave's
+// vmcnt(0) before its flag, the polling wave loads only after its poll matched), which needs no
+// agent-scope fence. The memory model's fences (buffer_wbl2 sc1 on release, buffer_inv sc1 on
+// acquire) write back / invalidate the caches for the expansion's own traffic too; measured on C2
+// (PQG_HANDOFF = 1 release store: 1.30x the time, 2 acquire fence: 2.45x, 3 both: 2.8x;
+// profiles/r02/r02_b/ab).
 #ifndef PQG_HANDOFF
 #define PQG_HANDOFF 0
 #endif
 __device__ __forceinline__ void handoff_release() {
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  __builtin_amdgcn_s_waitcnt(0);
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a compiler barrier too (invisible to the waitcnt pass)
 }
 __device__ __forceinline__ void handoff_acquire() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -934,7 +935,8 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
                                                 const uint64_t* rec, const uint32_t* chunk_run,
                                                 const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                 const uint64_t* pstat, const uint32_t* flags, uint32_t epoch,
-                                                uint64_t* err, ErrCount err_count, uint8_t* lds, uint32_t group) {
+                                                uint64_t* err, ErrCount err_count, uint8_t* lds, uint32_t group,
+                                                uint32_t tile_stride = 0) {
   typedef typename DictVal<W>::T T;
   constexpr uint32_t E = 16 / W;
   constexpr uint32_t TV = WAVE * E;  // values per tile
@@ -979,230 +981,239 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
     }
   }
   __syncthreads();
-  if (page < 0) return;
   const T* dict_l = (const T*)dict_lds;
-  const uint32_t j = (uint32_t)(chunks[c] >> 32);
-  // page / column facts and the page's bit width do not depend on the walk: loaded before the
-  // hand-off, so the compiler barrier there does not serialize them behind the flag
-  const PageWork pw = work[page];
-  const ColumnDev& cd = cols[pw.column];
-  const uint32_t dict_n = uni(cd.dict_n);
-  rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
-  rsrc_t prs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
-  const uint32_t sec_end = uni(pw.size);
-  const uint32_t db = uni(pw.data_begin);
-  const int w = (int)uni((ld32(prs, db & ~3u) >> ((db & 3u) * 8u)) & 0xFFu);
-  T* const out_base = IDS ? (T*)cd.blen : (T*)cd.values;
-  uint64_t pst;
-  if (FUSED) {
-    // The flag is polled; once it holds this launch's epoch, handoff_acquire orders the status /
-    // record / chunk-entry loads below after it (once per chunk, not per poll).
-    uint64_t t_wait = 0;
+  // one output chunk (c < n_chunks); false when the wave must stop (a walker timed out)
+  auto one_chunk = [&](uint32_t c) -> bool {
+    const int page = (int)(uint32_t)chunks[c];
+      const uint32_t j = (uint32_t)(chunks[c] >> 32);
+    // page / column facts and the page's bit width do not depend on the walk: loaded before the
+    // hand-off, so the compiler barrier there does not serialize them behind the flag
+    const PageWork pw = work[page];
+    const ColumnDev& cd = cols[pw.column];
+    const uint32_t dict_n = uni(cd.dict_n);
+    rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes);
+    rsrc_t prs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+    const uint32_t sec_end = uni(pw.size);
+    const uint32_t db = uni(pw.data_begin);
+    const int w = (int)uni((ld32(prs, db & ~3u) >> ((db & 3u) * 8u)) & 0xFFu);
+    T* const out_base = IDS ? (T*)cd.blen : (T*)cd.values;
+    uint64_t pst;
+    if (FUSED) {
+      // The flag is polled; once it holds this launch's epoch, handoff_acquire orders the status /
+      // record / chunk-entry loads below after it (once per chunk, not per poll).
+      uint64_t t_wait = 0;
+      while (true) {
+        if (uni(sld(flags + page)) == epoch) {
+          handoff_acquire();
+          pst = uni64(sld(pstat + page));
+          break;
+        }
+  #ifdef PQG_WALK_PROGRESS  // experimental, off: correct but slower in the A/B
+        const uint32_t sh0 = (uint32_t)(pw.out_offset % (uint64_t)E), nv = uni(pw.n_values);
+        const uint32_t need = ((j + 1) * CH < nv + sh0 ? (j + 1) * CH : nv + sh0) - sh0;
+        const uint64_t pp = uni64(sld(pstat + page));
+        if ((uint32_t)(pp >> 32) >= need) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // record loads after the status load
+          pst = pp;
+          break;
+        }
+  #endif
+        __builtin_amdgcn_s_sleep(PQG_SPIN_SLEEP);
+        // wall-clock bound (s_memrealtime: constant 100 MHz): a walker that never publishes
+        // (descheduled, starved) turns into PQG_ERR_TIMEOUT after SPIN_TIMEOUT_TICKS, not a hang
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (t_wait == 0) t_wait = now;
+        else if (now - t_wait > SPIN_TIMEOUT_TICKS) {
+          if (lane == 0) report(err, err_count, page, 2, 0, PQG_ERR_TIMEOUT);
+          return false;
+        }
+      }
+    } else {
+      pst = uni64(sld(pstat + page));
+    }
+
+    const uint32_t N = (uint32_t)(pst >> 32);  // values covered before a walk error
+    const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
+    const uint32_t s_lo = j * CH > sh ? j * CH : sh;
+    const uint32_t s_hi = (j + 1) * CH < N + sh ? (j + 1) * CH : N + sh;
+    if (s_lo >= s_hi) return true;
+    const uint32_t v_lo = s_lo - sh, v_hi = s_hi - sh;
+    const bool own_dict = dict_in_lds && pw.column == c0;
+    const uint32_t n_rec = (uint32_t)pst;
+    const uint64_t* prec = rec + pw.rec_base;
+    T* const pag = out_base + (pw.out_offset - sh);  // slot 0 of the page
+    const bool out16 = ((uintptr_t)out_base & 15u) == 0;
+    const uint32_t wmask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
+
+    uint32_t k = uni(sld(chunk_run + pw.chunk_base + j));  // first run of this round
+    uint32_t b_lo = v_lo;
     while (true) {
-      if (uni(sld(flags + page)) == epoch) {
-        handoff_acquire();
-        pst = uni64(sld(pstat + page));
-        break;
+      k = uni(k);
+      b_lo = uni(b_lo);
+      // ---- load phase: runs k .. k + n_tab - 1 into the table (entry n_tab: end sentinel)
+      uint32_t n_tab = 0, b_hi = v_hi, px_lo = 0xFFFFFFFFu, px_hi = 0;
+      for (uint32_t t0 = 0; t0 < XT_RUNS; t0 += WAVE) {
+        const uint32_t r = k + t0 + lane;
+        const bool has = r < n_rec && t0 + lane < XT_RUNS - 1;  // a run of this round
+        const uint64_t rr = r < n_rec ? sld(prec + r) : 0;
+        const uint32_t st = r < n_rec ? (uint32_t)rr : N;        // (past the runs: end sentinel)
+        const uint32_t pl = (uint32_t)(rr >> 32);
+        const uint32_t nx63 = uni(k + t0 + WAVE < n_rec ? (uint32_t)sld(prec + k + t0 + WAVE) : N);
+        const uint32_t en_n = __shfl_down(st, 1);
+        const uint32_t en = lane == WAVE - 1 ? nx63 : en_n;  // end of this lane's run
+        const bool live = has && st < v_hi;
+        uint32_t vlo = 0, vhi = 0;
+        if (live && !(pl & 0x80000000u)) {
+          if (pl < dict_n) {
+            if constexpr (IDS) {
+              vlo = pl;
+            } else {
+              const uint64_t x = (uint64_t)(own_dict ? dict_l[pl] : load_dict<W>(drs, pl));
+              vlo = (uint32_t)x;
+              vhi = (uint32_t)(x >> 32);
+            }
+          }
+        }
+        tab[t0 + lane] = u32x4{st, pl, vlo, vhi};
+        // packed bytes needed by this round: [first packed byte, last packed byte + 8)
+        if (live && (pl & 0x80000000u)) {
+          const uint32_t e_run = en;
+          const uint32_t lo = (pl & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)((st > b_lo ? st : b_lo) - st) * (uint32_t)w) >> 3);
+          const uint32_t hi_v = (e_run < v_hi ? e_run : v_hi);
+          const uint32_t hi = (pl & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)(hi_v > st ? hi_v - st : 0) * (uint32_t)w + 7) >> 3) + 8u;
+          px_lo = lo < px_lo ? lo : px_lo;
+          px_hi = hi > px_hi ? hi : px_hi;
+        }
+        const uint64_t inb = __ballot(has && st < v_hi);
+        n_tab += (uint32_t)__builtin_popcountll(inb);
+        if (!(inb >> 63)) break;  // this batch ends the round
       }
-#ifdef PQG_WALK_PROGRESS  // experimental, off: correct but slower in the A/B
-      const uint32_t sh0 = (uint32_t)(pw.out_offset % (uint64_t)E), nv = uni(pw.n_values);
-      const uint32_t need = ((j + 1) * CH < nv + sh0 ? (j + 1) * CH : nv + sh0) - sh0;
-      const uint64_t pp = uni64(sld(pstat + page));
-      if ((uint32_t)(pp >> 32) >= need) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // record loads after the status load
-        pst = pp;
-        break;
+      n_tab = uni(n_tab);
+      // wave min / max of the packed byte range
+  #pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t a = __shfl_xor(px_lo, o), b = __shfl_xor(px_hi, o);
+        px_lo = a < px_lo ? a : px_lo;
+        px_hi = b > px_hi ? b : px_hi;
       }
-#endif
-      __builtin_amdgcn_s_sleep(PQG_SPIN_SLEEP);
-      // wall-clock bound (s_memrealtime: constant 100 MHz): a walker that never publishes
-      // (descheduled, starved) turns into PQG_ERR_TIMEOUT after SPIN_TIMEOUT_TICKS, not a hang
-      const uint64_t now = __builtin_amdgcn_s_memrealtime();
-      if (t_wait == 0) t_wait = now;
-      else if (now - t_wait > SPIN_TIMEOUT_TICKS) {
-        if (lane == 0) report(err, err_count, page, 2, 0, PQG_ERR_TIMEOUT);
-        return;
+      px_lo = uni(px_lo) & ~15u;
+      px_hi = uni(px_hi);
+      // round end: the start of the first run not in the table
+      if (n_tab >= XT_RUNS - 1) {
+        const u32x4 q = tab[XT_RUNS - 1];
+        b_hi = uni(q.x) < v_hi ? uni(q.x) : v_hi;
       }
-    }
-  } else {
-    pst = uni64(sld(pstat + page));
-  }
-
-  const uint32_t N = (uint32_t)(pst >> 32);  // values covered before a walk error
-  const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
-  const uint32_t s_lo = j * CH > sh ? j * CH : sh;
-  const uint32_t s_hi = (j + 1) * CH < N + sh ? (j + 1) * CH : N + sh;
-  if (s_lo >= s_hi) return;
-  const uint32_t v_lo = s_lo - sh, v_hi = s_hi - sh;
-  const bool own_dict = dict_in_lds && pw.column == c0;
-  const uint32_t n_rec = (uint32_t)pst;
-  const uint64_t* prec = rec + pw.rec_base;
-  T* const pag = out_base + (pw.out_offset - sh);  // slot 0 of the page
-  const bool out16 = ((uintptr_t)out_base & 15u) == 0;
-  const uint32_t wmask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
-
-  uint32_t k = uni(sld(chunk_run + pw.chunk_base + j));  // first run of this round
-  uint32_t b_lo = v_lo;
-  while (true) {
-    k = uni(k);
-    b_lo = uni(b_lo);
-    // ---- load phase: runs k .. k + n_tab - 1 into the table (entry n_tab: end sentinel)
-    uint32_t n_tab = 0, b_hi = v_hi, px_lo = 0xFFFFFFFFu, px_hi = 0;
-    for (uint32_t t0 = 0; t0 < XT_RUNS; t0 += WAVE) {
-      const uint32_t r = k + t0 + lane;
-      const bool has = r < n_rec && t0 + lane < XT_RUNS - 1;  // a run of this round
-      const uint64_t rr = r < n_rec ? sld(prec + r) : 0;
-      const uint32_t st = r < n_rec ? (uint32_t)rr : N;        // (past the runs: end sentinel)
-      const uint32_t pl = (uint32_t)(rr >> 32);
-      const uint32_t nx63 = uni(k + t0 + WAVE < n_rec ? (uint32_t)sld(prec + k + t0 + WAVE) : N);
-      const uint32_t en_n = __shfl_down(st, 1);
-      const uint32_t en = lane == WAVE - 1 ? nx63 : en_n;  // end of this lane's run
-      const bool live = has && st < v_hi;
-      uint32_t vlo = 0, vhi = 0;
-      if (live && !(pl & 0x80000000u)) {
-        if (pl < dict_n) {
-          if constexpr (IDS) {
-            vlo = pl;
-          } else {
-            const uint64_t x = (uint64_t)(own_dict ? dict_l[pl] : load_dict<W>(drs, pl));
-            vlo = (uint32_t)x;
-            vhi = (uint32_t)(x >> 32);
+      bool x_lds = true;
+      if (px_hi > px_lo) {
+        x_lds = px_hi - px_lo <= XT_SEG;
+        if (x_lds) {
+  #pragma unroll
+          for (uint32_t i = 0; i < XT_SEG; i += 16u * WAVE) {
+            const uint32_t o = i + 16u * lane;
+            if (o < px_hi - px_lo) *(u32x4*)(xseg + o) = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(px_lo + o), 0, 0);
           }
         }
       }
-      tab[t0 + lane] = u32x4{st, pl, vlo, vhi};
-      // packed bytes needed by this round: [first packed byte, last packed byte + 8)
-      if (live && (pl & 0x80000000u)) {
-        const uint32_t e_run = en;
-        const uint32_t lo = (pl & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)((st > b_lo ? st : b_lo) - st) * (uint32_t)w) >> 3);
-        const uint32_t hi_v = (e_run < v_hi ? e_run : v_hi);
-        const uint32_t hi = (pl & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)(hi_v > st ? hi_v - st : 0) * (uint32_t)w + 7) >> 3) + 8u;
-        px_lo = lo < px_lo ? lo : px_lo;
-        px_hi = hi > px_hi ? hi : px_hi;
+      // DICT_ID: RLE runs of the round with an id past the dictionary (reported at the first
+      // value of the run inside the chunk)
+      for (uint32_t t0 = 0; t0 < n_tab; t0 += WAVE) {
+        const u32x4 q = tab[t0 + lane];
+        const uint32_t en = tab[t0 + lane + 1].x;
+        if (t0 + lane < n_tab && !(q.y & 0x80000000u) && q.y >= dict_n && en > b_lo && q.x < b_hi)
+          report(err, err_count, page, 2, q.x > b_lo ? q.x : b_lo, PQG_ERR_DICT_ID);
       }
-      const uint64_t inb = __ballot(has && st < v_hi);
-      n_tab += (uint32_t)__builtin_popcountll(inb);
-      if (!(inb >> 63)) break;  // this batch ends the round
-    }
-    n_tab = uni(n_tab);
-    // wave min / max of the packed byte range
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const uint32_t a = __shfl_xor(px_lo, o), b = __shfl_xor(px_hi, o);
-      px_lo = a < px_lo ? a : px_lo;
-      px_hi = b > px_hi ? b : px_hi;
-    }
-    px_lo = uni(px_lo) & ~15u;
-    px_hi = uni(px_hi);
-    // round end: the start of the first run not in the table
-    if (n_tab >= XT_RUNS - 1) {
-      const u32x4 q = tab[XT_RUNS - 1];
-      b_hi = uni(q.x) < v_hi ? uni(q.x) : v_hi;
-    }
-    bool x_lds = true;
-    if (px_hi > px_lo) {
-      x_lds = px_hi - px_lo <= XT_SEG;
-      if (x_lds) {
-#pragma unroll
-        for (uint32_t i = 0; i < XT_SEG; i += 16u * WAVE) {
-          const uint32_t o = i + 16u * lane;
-          if (o < px_hi - px_lo) *(u32x4*)(xseg + o) = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(px_lo + o), 0, 0);
-        }
-      }
-    }
-    // DICT_ID: RLE runs of the round with an id past the dictionary (reported at the first
-    // value of the run inside the chunk)
-    for (uint32_t t0 = 0; t0 < n_tab; t0 += WAVE) {
-      const u32x4 q = tab[t0 + lane];
-      const uint32_t en = tab[t0 + lane + 1].x;
-      if (t0 + lane < n_tab && !(q.y & 0x80000000u) && q.y >= dict_n && en > b_lo && q.x < b_hi)
-        report(err, err_count, page, 2, q.x > b_lo ? q.x : b_lo, PQG_ERR_DICT_ID);
-    }
-    __builtin_amdgcn_s_waitcnt(0);  // load phase complete (the wave has not stored yet this round)
+      __builtin_amdgcn_s_waitcnt(0);  // load phase complete (the wave has not stored yet this round)
 
-    // ---- tile sweep
-    auto sweep = [&](auto fast_tag) {
-      constexpr bool FAST = decltype(fast_tag)::value;
-      auto value = [&](uint32_t ci, uint32_t i, const u32x4& q) -> T {
-        if (!(q.y & 0x80000000u)) return (T)(((uint64_t)q.w << 32) | q.z);
-        const uint64_t bit = (uint64_t)(i - q.x) * (uint32_t)w;
-        const uint32_t byte = (q.y & 0x7FFFFFFFu) + (uint32_t)(bit >> 3);
-        const uint32_t a4 = byte & ~3u;
-        uint64_t y;
-        if (FAST)
-          y = (uint64_t)*(const u32_alias*)(xseg + (a4 - px_lo)) |
-              ((uint64_t)*(const u32_alias*)(xseg + (a4 - px_lo) + 4) << 32);
-        else
-          y = (uint64_t)ld32(prs, a4) | ((uint64_t)ld32(prs, a4 + 4) << 32);
-        if (a4 + 8u > sec_end) {  // truncated final group: bytes past the section are 0 (:96-99)
-          const int64_t keep = (int64_t)sec_end - (int64_t)a4;
-          y = keep <= 0 ? 0 : (y & ((1ull << (8 * keep)) - 1ull));
+      // ---- tile sweep
+      auto sweep = [&](auto fast_tag) {
+        constexpr bool FAST = decltype(fast_tag)::value;
+        auto value = [&](uint32_t ci, uint32_t i, const u32x4& q) -> T {
+          if (!(q.y & 0x80000000u)) return (T)(((uint64_t)q.w << 32) | q.z);
+          const uint64_t bit = (uint64_t)(i - q.x) * (uint32_t)w;
+          const uint32_t byte = (q.y & 0x7FFFFFFFu) + (uint32_t)(bit >> 3);
+          const uint32_t a4 = byte & ~3u;
+          uint64_t y;
+          if (FAST)
+            y = (uint64_t)*(const u32_alias*)(xseg + (a4 - px_lo)) |
+                ((uint64_t)*(const u32_alias*)(xseg + (a4 - px_lo) + 4) << 32);
+          else
+            y = (uint64_t)ld32(prs, a4) | ((uint64_t)ld32(prs, a4 + 4) << 32);
+          if (a4 + 8u > sec_end) {  // truncated final group: bytes past the section are 0 (:96-99)
+            const int64_t keep = (int64_t)sec_end - (int64_t)a4;
+            y = keep <= 0 ? 0 : (y & ((1ull << (8 * keep)) - 1ull));
+          }
+          y >>= (byte - a4) * 8u + (uint32_t)(bit & 7u);
+          const uint32_t id = w == 0 ? 0u : (uint32_t)y & wmask;
+          if (id >= dict_n) {
+            report(err, err_count, page, 2, i, PQG_ERR_DICT_ID);
+            return 0;
+          }
+          if constexpr (IDS) return (T)id;
+          else return FAST ? dict_l[id] : dict_get_g<W>(own_dict, dict_l, drs, id);
+          (void)ci;
+        };
+        const uint32_t t_beg = (b_lo + sh) / TV, t_end = (b_hi + sh + TV - 1) / TV;  // page tiles
+        // run of the lane's first element: binary search of the table
+        uint32_t p0 = t_beg * TV + E * lane - sh;
+        uint32_t pe = p0 < b_lo || p0 > 0x7FFFFFFFu ? b_lo : (p0 >= b_hi ? b_hi - 1 : p0);
+        uint32_t ci = 0;
+  #pragma unroll
+        for (uint32_t step = XT_RUNS / 2; step >= 1; step >>= 1)
+          if (ci + step < n_tab && tab[ci + step].x <= pe) ci += step;
+        u32x4 cq = tab[ci];
+        uint32_t ce = tab[ci + 1].x;
+        for (uint32_t t = t_beg; t < t_end; t++) {
+          t = uni(t);
+          const uint32_t ts = t * TV;  // first slot of the tile
+          p0 = ts + E * lane - sh;
+          pe = p0 < b_lo || p0 > 0x7FFFFFFFu ? b_lo : (p0 >= b_hi ? b_hi - 1 : p0);
+          while (pe >= ce) {  // crossed run starts (divergent, usually no lane)
+            ci++;
+            cq = tab[ci];
+            ce = tab[ci + 1].x;
+          }
+          // elements outside [b_lo, b_hi) are not stored; they are evaluated at a clamped index
+          T v[E];
+          v[0] = value(ci, pe, cq);
+  #pragma unroll
+          for (uint32_t e = 1; e < E; e++) {
+            const uint32_t x = p0 + e;  // value index of element e (wraps below 0)
+            const uint32_t i = x < b_lo || x > 0x7FFFFFFFu ? b_lo : (x >= b_hi ? b_hi - 1 : x);
+            if (i < ce) {
+              v[e] = value(ci, i, cq);
+            } else {  // the element starts a later run
+              uint32_t cj = ci + 1;
+              while (cj + 1 < n_tab && tab[cj + 1].x <= i) cj++;
+              v[e] = value(cj, i, tab[cj]);
+            }
+          }
+          T* tp = pag + ts + E * lane;
+          if (out16 && ts >= b_lo + sh && ts + TV <= b_hi + sh) {
+            if constexpr (W == 8) {
+              typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+              gst_nt((v2*)tp, v2{v[0], v[1]});
+            } else {
+              gst_nt((u32x4*)tp, u32x4{v[0], v[1], v[2], v[3]});
+            }
+          } else {
+  #pragma unroll
+            for (uint32_t e = 0; e < E; e++)
+              if (ts + E * lane + e >= b_lo + sh && ts + E * lane + e < b_hi + sh) gst(tp + e, v[e]);
+          }
         }
-        y >>= (byte - a4) * 8u + (uint32_t)(bit & 7u);
-        const uint32_t id = w == 0 ? 0u : (uint32_t)y & wmask;
-        if (id >= dict_n) {
-          report(err, err_count, page, 2, i, PQG_ERR_DICT_ID);
-          return 0;
-        }
-        if constexpr (IDS) return (T)id;
-        else return FAST ? dict_l[id] : dict_get_g<W>(own_dict, dict_l, drs, id);
-        (void)ci;
       };
-      const uint32_t t_beg = (b_lo + sh) / TV, t_end = (b_hi + sh + TV - 1) / TV;  // page tiles
-      // run of the lane's first element: binary search of the table
-      uint32_t p0 = t_beg * TV + E * lane - sh;
-      uint32_t pe = p0 < b_lo || p0 > 0x7FFFFFFFu ? b_lo : (p0 >= b_hi ? b_hi - 1 : p0);
-      uint32_t ci = 0;
-#pragma unroll
-      for (uint32_t step = XT_RUNS / 2; step >= 1; step >>= 1)
-        if (ci + step < n_tab && tab[ci + step].x <= pe) ci += step;
-      u32x4 cq = tab[ci];
-      uint32_t ce = tab[ci + 1].x;
-      for (uint32_t t = t_beg; t < t_end; t++) {
-        t = uni(t);
-        const uint32_t ts = t * TV;  // first slot of the tile
-        p0 = ts + E * lane - sh;
-        pe = p0 < b_lo || p0 > 0x7FFFFFFFu ? b_lo : (p0 >= b_hi ? b_hi - 1 : p0);
-        while (pe >= ce) {  // crossed run starts (divergent, usually no lane)
-          ci++;
-          cq = tab[ci];
-          ce = tab[ci + 1].x;
-        }
-        // elements outside [b_lo, b_hi) are not stored; they are evaluated at a clamped index
-        T v[E];
-        v[0] = value(ci, pe, cq);
-#pragma unroll
-        for (uint32_t e = 1; e < E; e++) {
-          const uint32_t x = p0 + e;  // value index of element e (wraps below 0)
-          const uint32_t i = x < b_lo || x > 0x7FFFFFFFu ? b_lo : (x >= b_hi ? b_hi - 1 : x);
-          if (i < ce) {
-            v[e] = value(ci, i, cq);
-          } else {  // the element starts a later run
-            uint32_t cj = ci + 1;
-            while (cj + 1 < n_tab && tab[cj + 1].x <= i) cj++;
-            v[e] = value(cj, i, tab[cj]);
-          }
-        }
-        T* tp = pag + ts + E * lane;
-        if (out16 && ts >= b_lo + sh && ts + TV <= b_hi + sh) {
-          if constexpr (W == 8) {
-            typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-            gst_nt((v2*)tp, v2{v[0], v[1]});
-          } else {
-            gst_nt((u32x4*)tp, u32x4{v[0], v[1], v[2], v[3]});
-          }
-        } else {
-#pragma unroll
-          for (uint32_t e = 0; e < E; e++)
-            if (ts + E * lane + e >= b_lo + sh && ts + E * lane + e < b_hi + sh) gst(tp + e, v[e]);
-        }
-      }
-    };
-    if ((IDS || own_dict) && x_lds) sweep(std::true_type{});
-    else sweep(std::false_type{});
-    if (b_hi >= v_hi) break;
-    k += XT_RUNS - 1;
-    b_lo = b_hi;
+      if ((IDS || own_dict) && x_lds) sweep(std::true_type{});
+      else sweep(std::false_type{});
+      if (b_hi >= v_hi) break;
+      k += XT_RUNS - 1;
+      b_lo = b_hi;
+    }
+    return true;
+  };
+  // tile_stride == 0: one chunk per wave; else persistent: this wave's chunks c, c + 4 * stride, ...
+  // (chunks in page order, so a wave's next chunk is a page walked later)
+  for (uint32_t cc = c; cc < n_chunks; cc += WPB * tile_stride) {
+    if (!one_chunk(cc) || !tile_stride) break;
   }
 }
 
@@ -1228,15 +1239,22 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restri
                                                          uint32_t n_walk, uint64_t* rec, uint32_t* chunk_run,
                                                          const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                          uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                                                         uint64_t* err, ErrCount err_count) {
+                                                         uint32_t walk_wg, uint32_t tile_wg, uint64_t* err,
+                                                         ErrCount err_count) {
   constexpr uint32_t LB = sizeof(DictWaveLds) * WPB > XT_LDS_BYTES ? sizeof(DictWaveLds) * WPB : XT_LDS_BYTES;
   __shared__ __attribute__((aligned(16))) uint8_t lds[LB];
-  if (blockIdx.x < n_walk)
-    dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
-                      lds, blockIdx.x);
-  else
+  // workgroups [0, n_walk) walk, the rest expand. walk_wg / tile_wg > 0: persistent workgroups
+  // that take every walk_wg-th group of 4 pages / every tile_wg-th group of 4 chunks, in page order
+  if (blockIdx.x < n_walk) {
+    for (uint32_t g = blockIdx.x; g * WPB < (uint32_t)n_list; g += walk_wg) {
+      dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
+                        lds, g);
+      if (!walk_wg) break;
+    }
+  } else {
     dict_tiles_body<W, true, IDS>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch,
-                                  err, err_count, lds, blockIdx.x - n_walk);
+                                  err, err_count, lds, blockIdx.x - n_walk, tile_wg);
+  }
 }
 
 
@@ -2633,17 +2651,19 @@ namespace pqg {
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                        const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                       bool fused, uint64_t* err, ErrCount err_count) {
+                       bool fused, uint32_t walk_wg, uint32_t tile_wg, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
-  const uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
+  uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
+  if (fused && walk_wg && walk_wg < n_walk) n_walk = walk_wg; else walk_wg = fused && walk_wg ? n_walk : walk_wg;
+  if (fused && tile_wg && tile_wg < n_tile) n_tile = tile_wg; else tile_wg = fused && tile_wg ? n_tile : tile_wg;
   const dim3 blk(64 * WPB);
   if (fused) {
     if (width == 8)
       hipLaunchKernelGGL(k_dict_fused<8>, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n, n_walk,
-                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count);
+                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, err, err_count);
     else
       hipLaunchKernelGGL(k_dict_fused<4>, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n, n_walk,
-                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count);
+                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, err, err_count);
     return hipGetLastError();
   }
   if (width == 8) {
@@ -2665,13 +2685,16 @@ hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t
 hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                            const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
-                           uint32_t epoch, bool fused, uint64_t* err, ErrCount err_count) {
+                           uint32_t epoch, bool fused, uint32_t walk_wg, uint32_t tile_wg, uint64_t* err,
+                           ErrCount err_count) {
   if (n <= 0) return hipSuccess;
-  const uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
+  uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
+  if (fused && walk_wg && walk_wg < n_walk) n_walk = walk_wg; else walk_wg = fused && walk_wg ? n_walk : walk_wg;
+  if (fused && tile_wg && tile_wg < n_tile) n_tile = tile_wg; else tile_wg = fused && tile_wg ? n_tile : tile_wg;
   const dim3 blk(64 * WPB);
   if (fused) {
     hipLaunchKernelGGL((k_dict_fused<4, true>), dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n,
-                       n_walk, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count);
+                       n_walk, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, err, err_count);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_dict_runs<4>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,

@@ -57,6 +57,24 @@ __global__ __launch_bounds__(256) void k_lane_contig(v2* out, u64 n16) {
       if (base + u < n16) st16<NT>(out + base + u, v2{base, (u64)u});
 }
 
+// Grid-stride, one 16-byte store per lane per step (the classic fill kernel).
+template <bool NT>
+__global__ __launch_bounds__(256) void k_gridstride(v2* out, u64 n16) {
+  const u64 t = (u64)blockIdx.x * 256 + threadIdx.x, nt = (u64)gridDim.x * 256;
+  for (u64 i = t; i < n16; i += nt) st16<NT>(out + i, v2{i, 1});
+}
+
+// XCD-aware: workgroup b runs on XCD (b % 8); give each XCD one contiguous eighth of the buffer and
+// deal that eighth's chunks to its workgroups in order.
+template <bool NT>
+__global__ __launch_bounds__(256) void k_xcd_chunks(v2* out, u64 n16, u64 chunk16) {
+  const u64 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const u64 xcd = blockIdx.x & 7, j = blockIdx.x >> 3, per_x = (gridDim.x + 7) >> 3;
+  const u64 n_ch = (n16 + chunk16 - 1) / chunk16, ch_x = (n_ch + 7) / 8;
+  for (u64 c = xcd * ch_x + j * 4 + wv; c < (xcd + 1) * ch_x && c < n_ch; c += per_x * 4)
+    for (u64 i = c * chunk16 + lane; i < (c + 1) * chunk16 && i < n16; i += 64) st16<NT>(out + i, v2{i, c});
+}
+
 template <class F>
 float timeit(F f, int reps) {
   hipEvent_t a, b;
@@ -111,6 +129,24 @@ int main() {
     t = timeit([&] { hipLaunchKernelGGL((k_lane_contig<false, 4>), dim3(g), dim3(256), 0, 0, out, n16); }, 20);
     snprintf(nm, sizeof nm, "lane-contig x4 plain grid=%llu", g);
     REPORT(nm);
+  }
+  for (u64 g : {1024ull, 2048ull, 4096ull, 16384ull, 65536ull}) {
+    t = timeit([&] { hipLaunchKernelGGL(k_gridstride<true>, dim3(g), dim3(256), 0, 0, out, n16); }, 20);
+    snprintf(nm, sizeof nm, "gridstride nt grid=%llu", g);
+    REPORT(nm);
+    t = timeit([&] { hipLaunchKernelGGL(k_gridstride<false>, dim3(g), dim3(256), 0, 0, out, n16); }, 20);
+    snprintf(nm, sizeof nm, "gridstride plain grid=%llu", g);
+    REPORT(nm);
+  }
+  for (u64 chunk : {16384ull, 65536ull}) {
+    for (u64 g : {2048ull, 8192ull}) {
+      t = timeit([&] { hipLaunchKernelGGL(k_xcd_chunks<true>, dim3(g), dim3(256), 0, 0, out, n16, chunk / 16); }, 20);
+      snprintf(nm, sizeof nm, "xcd-chunks nt chunk=%lluKB grid=%llu", chunk / 1024, g);
+      REPORT(nm);
+      t = timeit([&] { hipLaunchKernelGGL(k_xcd_chunks<false>, dim3(g), dim3(256), 0, 0, out, n16, chunk / 16); }, 20);
+      snprintf(nm, sizeof nm, "xcd-chunks plain chunk=%lluKB grid=%llu", chunk / 1024, g);
+      REPORT(nm);
+    }
   }
   t = timeit([&] { hipMemsetAsync(out, 0, bytes); }, 20);
   REPORT("hipMemset");
