@@ -297,6 +297,23 @@ int pqg_snappy_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes
                           const pqg_snappy_job* d_jobs, int n_jobs, int32_t* d_status);
 int pqg_snappy_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_status* st);
 
+/* ---- page decompression (codec ZSTD) ------------------------------------------
+ * The same step for ZSTD pages: ZstandardCodec -> ZstdDecompressorStream
+ * (parquet-hadoop/src/main/java/org/apache/parquet/hadoop/codec/ZstdDecompressorStream.java:31-46,
+ * zstd-jni's ZstdInputStream over libzstd) read for exactly the header's uncompressed size
+ * (ColumnChunkPageReadStore.java:144-172). Job j decodes the Zstandard frames (RFC 8878; skippable
+ * frames skipped, concatenated frames in order) in d_src[src_offset, + src_size) and keeps the first
+ * dst_size bytes at d_dst + dst_offset. Frames that end before dst_size -> PQG_ERR_EOF; a malformed
+ * frame, a frame content size or content checksum (XXH64) that does not match -> PQG_ERR_CORRUPT;
+ * dictionaries are not supported (a frame naming one -> CORRUPT). Asynchronous on the context's
+ * stream; the context keeps 128 KiB of device scratch per job. pqg_zstd_sync reports the first
+ * failing job (st->page = job index). */
+typedef pqg_snappy_job pqg_zstd_job;
+
+int pqg_zstd_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, uint8_t* d_dst, uint64_t dst_bytes,
+                        const pqg_zstd_job* d_jobs, int n_jobs, int32_t* d_status);
+int pqg_zstd_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_status* st);
+
 /* ---- page framing (host) ----------------------------------------------------
  * File bytes in: the page headers of one raw column chunk, as
  * ParquetFileReader.Chunk.readAllPages reads them

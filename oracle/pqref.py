@@ -42,6 +42,10 @@ def lib():
         L.pqr_delta_decode.argtypes = [vp, i64, vp, i64, C.POINTER(i64)]
         L.pqr_snappy_decompress.argtypes = [vp, i64, vp, i64, C.POINTER(i64)]
         L.pqr_snappy_decompress.restype = C.c_int
+        L.pqr_zstd_decompress.argtypes = [vp, i64, vp, i64, C.POINTER(i64)]
+        L.pqr_zstd_decompress.restype = C.c_int
+        L.pqr_xxh64.argtypes = [vp, C.c_uint64, C.c_uint64]
+        L.pqr_xxh64.restype = C.c_uint64
         L.pqr_delta_decode.restype = i64
         L.pqr_decode.argtypes = [vp, C.c_uint64, vp, C.c_int, vp, C.c_int, vp, C.POINTER(abi.Status)]
         L.pqr_decode.restype = C.c_int
@@ -186,3 +190,21 @@ def snappy_decompress(data, uncompressed_size):
     if rc:
         raise ValueError(f"snappy: error {rc}")
     return out[:n.value].tobytes()
+
+
+def zstd_decompress(data, uncompressed_size):
+    """Zstandard frames -> the first `uncompressed_size` bytes (ORACLE; pqr_zstd_decompress,
+    RFC 8878 restated). Raises ValueError(code) when malformed or short."""
+    src = _buf(data)
+    out = np.zeros(max(int(uncompressed_size), 1), dtype=np.uint8)
+    n = C.c_int64(0)
+    rc = lib().pqr_zstd_decompress(src.ctypes.data if src.size else None, src.size, out.ctypes.data,
+                                   int(uncompressed_size), C.byref(n))
+    if rc:
+        raise ValueError(f"zstd: error {rc}")
+    return out[:int(uncompressed_size)].tobytes()
+
+
+def xxh64(data, seed=0):
+    src = _buf(data)
+    return int(lib().pqr_xxh64(src.ctypes.data if src.size else None, src.size, seed))

@@ -163,6 +163,7 @@ struct pqg_ctx {
   DevBuf host_bytes, host_out, host_counts, host_runs;
   DevBuf asm_scratch;                // pqg_assemble: block counts + totals
   hipStream_t copy_stream = nullptr; // pqg_decode_host: second D2H queue (odd output chunks)
+  DevBuf zstd_scratch;               // pqg_zstd_decompress: literal buffers, ZSTD_LIT_SCRATCH per job
 };
 
 extern "C" {
@@ -1241,6 +1242,38 @@ int pqg_snappy_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_statu
   for (int j = 0; j < n_jobs; j++)
     if (h[(size_t)j]) {
       set_status(st, h[(size_t)j], j, -1, "snappy block");
+      return h[(size_t)j];
+    }
+  return PQG_OK;
+}
+
+int pqg_zstd_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, uint8_t* d_dst, uint64_t dst_bytes,
+                        const pqg_zstd_job* d_jobs, int n_jobs, int32_t* d_status) {
+  if (!ctx || n_jobs < 0) return PQG_ERR_INVALID_ARG;
+  if (n_jobs == 0) return PQG_OK;
+  if (!d_src || !d_dst || !d_jobs) return PQG_ERR_INVALID_ARG;
+  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
+  // the scratch may be in use by a previous call still queued on the stream: grow only after it
+  if (ctx->zstd_scratch.cap < pqg::ZSTD_LIT_SCRATCH * (uint64_t)n_jobs) {
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return PQG_ERR_HIP;
+    if (ctx->zstd_scratch.ensure(pqg::ZSTD_LIT_SCRATCH * (uint64_t)n_jobs) != hipSuccess) return PQG_ERR_HIP;
+  }
+  const hipError_t e = pqg::launch_zstd(ctx->stream, d_src, src_bytes, d_dst, dst_bytes, d_jobs, n_jobs, d_status,
+                                        (uint8_t*)ctx->zstd_scratch.p);
+  return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
+}
+
+int pqg_zstd_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_status* st) {
+  if (!ctx || n_jobs < 0) return PQG_ERR_INVALID_ARG;
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return PQG_ERR_HIP;
+  if (st) set_status(st, PQG_OK, -1, -1, "zstd");
+  if (!d_status || n_jobs == 0) return PQG_OK;
+  std::vector<int32_t> h((size_t)n_jobs);
+  if (hipMemcpy(h.data(), d_status, sizeof(int32_t) * (size_t)n_jobs, hipMemcpyDeviceToHost) != hipSuccess)
+    return PQG_ERR_HIP;
+  for (int j = 0; j < n_jobs; j++)
+    if (h[(size_t)j]) {
+      set_status(st, h[(size_t)j], j, -1, "zstd frame");
       return h[(size_t)j];
     }
   return PQG_OK;

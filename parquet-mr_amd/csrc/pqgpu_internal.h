@@ -108,6 +108,10 @@ hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 // pqgpu_snappy.hip: one wave per raw Snappy block (jobs: pqg_snappy_job, device array)
+// ZSTD frames per job (pqgpu_zstd.hip); scratch = n_jobs x ZSTD_LIT_SCRATCH bytes of literal buffers
+constexpr uint64_t ZSTD_LIT_SCRATCH = 131072;
+hipError_t launch_zstd(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
+                       const pqg_snappy_job* jobs, int n_jobs, int32_t* status, uint8_t* scratch);
 hipError_t launch_snappy(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
                          const void* jobs, int n_jobs, int32_t* status);
 // DELTA_BYTE_ARRAY prefix / suffix lengths (k_delta MODE 2: bsrc = prefix, blen = value length, aux;

@@ -1,0 +1,696 @@
+// pqgpu_zstd.hip — ZSTD page decompression on gfx950 (pqg_zstd_decompress).
+//
+// parquet-mr decompresses a ZSTD page through zstd-jni's streaming decoder (ZstandardCodec ->
+// ZstdDecompressorStream, parquet-hadoop/src/main/java/org/apache/parquet/hadoop/codec/
+// ZstdDecompressorStream.java:31-46; libzstd underneath) and keeps exactly the header's
+// uncompressed size (ColumnChunkPageReadStore.java:144-172). The format is RFC 8878; the CPU
+// restatement every test checks against is oracle/zstd_ref.c.
+//
+// One 64-lane wave per job (page). Decoding a ZSTD block has two serial parts and one parallel:
+//   * literals: Huffman streams decoded by lanes 0..3 (one stream each, 4-stream blocks) or lane 0,
+//     with the decoding table in LDS, into a per-job literal buffer in global scratch;
+//   * sequences: the three FSE state machines and the backward bitstream, wave-uniform code (the
+//     scalar unit does the bookkeeping), the bitstream read through a 1 KiB LDS window;
+//   * execution: each sequence's literal copy and match copy by all 64 lanes, the last 4 KiB of
+//     output mirrored in an LDS ring so that overlapping / near matches read LDS; older bytes
+//     are read back from the output with system-scope (L1-bypassing) loads after a store drain
+//     every 2 KiB of output.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pqgpu_device.h"
+
+namespace pqg {
+
+constexpr uint32_t ZS_RING = 4096;    // LDS mirror of the most recent output
+constexpr uint32_t ZS_WIN = 1024;     // LDS window of the sequence bitstream
+constexpr uint32_t ZS_HWIN = 256;     // LDS window per Huffman stream
+constexpr uint32_t ZS_LIT_MAX = 131072;
+
+struct ZWaveLds {
+  uint32_t ll[512], ml[512], of[256];  // FSE decoding entries: sym | nb << 8 | base << 16
+  uint16_t huf[2048];                  // Huffman decoding entries: sym | nb << 8
+  uint8_t ring[ZS_RING];
+  uint8_t win[ZS_WIN + 16];
+  uint8_t hwin[4][ZS_HWIN + 16];
+  int16_t norm[256];
+  uint8_t wts[256];
+  uint16_t nxt[256];
+  uint32_t flag;
+};
+
+__constant__ int16_t ZLL_DEF[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+__constant__ int16_t ZML_DEF[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                    1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+__constant__ int16_t ZOF_DEF[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+__constant__ uint32_t ZLL_BASE[36] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 18, 20, 22, 24, 28, 32, 40,
+                                      48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+__constant__ uint8_t ZLL_BITS[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ uint32_t ZML_BASE[53] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29,
+                                      30, 31, 32, 33, 34, 35, 37, 39, 41, 43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099,
+                                      8195, 16387, 32771, 65539};
+__constant__ uint8_t ZML_BITS[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                     0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+
+__device__ __forceinline__ int zhigh(uint32_t v) { return v ? 31 - __builtin_clz(v) : -1; }
+
+// one input byte at `o` of the job's input (uniform reads: every lane loads the same dword)
+__device__ __forceinline__ uint32_t zbyte(rsrc_t rs, uint32_t o) { return (ld32(rs, o & ~3u) >> ((o & 3u) * 8u)) & 0xFFu; }
+
+// Forward little-endian bit reader over the input (FSE table descriptions), uniform.
+struct FwdBits {
+  rsrc_t rs;
+  uint32_t lim;     // input bytes readable (the description's end)
+  uint64_t bitpos;  // absolute bit position
+  bool bad;
+  __device__ uint32_t get(int k) {
+    uint32_t v = 0;
+    const uint64_t b0 = bitpos;
+    if (((b0 + (uint64_t)k + 7) >> 3) > lim) { bad = true; bitpos += (uint64_t)k; return 0; }
+    const uint32_t byte = (uint32_t)(b0 >> 3);
+    const uint64_t w = ld8_any(rs, byte);
+    v = (uint32_t)((w >> (b0 & 7)) & ((1ull << k) - 1ull));
+    bitpos += (uint64_t)k;
+    return v;
+  }
+};
+
+// Backward bitstream (RFC 8878 §4.1) whose bytes [0, n) start at input offset `base`; read through
+// an LDS window (wave-uniform use: the whole wave refills it).
+struct BackBits {
+  rsrc_t rs;
+  uint32_t base, n;
+  int64_t bits;      // unread bits
+  uint32_t wlo;      // window covers stream bytes [wlo, wlo + ZS_WIN)
+  uint8_t* win;
+  __device__ bool init(rsrc_t r, uint32_t b, uint32_t len, uint8_t* w) {
+    rs = r; base = b; n = len; win = w; wlo = 0xFFFFFFFFu;
+    if (len == 0) return false;
+    const uint32_t last = zbyte(rs, base + len - 1);
+    if (!last) return false;
+    bits = (int64_t)(len - 1) * 8 + zhigh(last);
+    return true;
+  }
+  __device__ void refill(uint32_t need_end) {  // window ending at stream byte need_end
+    const uint32_t lo = need_end > ZS_WIN ? need_end - ZS_WIN : 0;
+    wlo = lo;
+    const uint32_t o = 16u * lane_id();
+    *(u32x4*)(win + o) = u32x4{ld4_any(rs, base + lo + o), ld4_any(rs, base + lo + o + 4),
+                               ld4_any(rs, base + lo + o + 8), ld4_any(rs, base + lo + o + 12)};
+    wave_sync();
+  }
+  // k <= 32 bits; bits below the stream start read as 0 (overflow: bits < 0 afterwards)
+  __device__ uint32_t read(int k) {
+    if (k == 0) return 0;
+    bits -= k;
+    int64_t a = bits;
+    int sh = 0;
+    if (a < 0) { sh = (int)-a; a = 0; }
+    const int kk = k - sh;
+    if (kk <= 0) return 0;
+    const uint32_t b0 = (uint32_t)(a >> 3), b1 = (uint32_t)((a + kk + 7) >> 3);  // bytes [b0, b1)
+    if (wlo == 0xFFFFFFFFu || b0 < wlo || b1 > wlo + ZS_WIN) refill(b1 < n ? b1 : n);
+    uint64_t w = 0;
+    const uint32_t rel = b0 - wlo;
+    typedef uint32_t __attribute__((may_alias)) u32a;
+    const uint32_t r4 = rel & ~3u;
+    const uint32_t d0 = *(const u32a*)(win + r4), d1 = *(const u32a*)(win + r4 + 4), d2 = *(const u32a*)(win + r4 + 8);
+    const uint32_t s = rel & 3u;
+    w = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
+    const uint32_t v = (uint32_t)((w >> (a & 7)) & ((1ull << kk) - 1ull));
+    return v << sh;
+  }
+};
+
+// Per-lane backward bitstream for one Huffman stream, its own LDS window (lane-private use).
+struct LaneBits {
+  uint32_t base, n, wlo;
+  int64_t bits;
+  uint8_t* win;
+  __device__ void refill(rsrc_t rs, uint32_t need_end) {
+    const uint32_t lo = need_end > ZS_HWIN ? need_end - ZS_HWIN : 0;
+    wlo = lo;
+    for (uint32_t o = 0; o < ZS_HWIN; o += 16)
+      *(u32x4*)(win + o) = u32x4{ld4_any(rs, base + lo + o), ld4_any(rs, base + lo + o + 4),
+                                 ld4_any(rs, base + lo + o + 8), ld4_any(rs, base + lo + o + 12)};
+  }
+  __device__ uint32_t peek(rsrc_t rs, int k) {  // the next k bits without consuming (zeros past the start)
+    int64_t a = bits - k;
+    int sh = 0;
+    if (a < 0) { sh = (int)-a; a = 0; }
+    const int kk = k - sh;
+    if (kk <= 0) return 0;
+    const uint32_t b0 = (uint32_t)(a >> 3), b1 = (uint32_t)((a + kk + 7) >> 3);
+    if (wlo == 0xFFFFFFFFu || b0 < wlo || b1 > wlo + ZS_HWIN) refill(rs, b1 < n ? b1 : n);
+    const uint32_t rel = b0 - wlo;
+    typedef uint32_t __attribute__((may_alias)) u32a;
+    const uint32_t r4 = rel & ~3u, s = rel & 3u;
+    const uint32_t d0 = *(const u32a*)(win + r4), d1 = *(const u32a*)(win + r4 + 4);
+    const uint32_t w = __builtin_amdgcn_alignbyte(d1, d0, s);
+    return ((w >> (a & 7)) & ((1u << kk) - 1u)) << sh;
+  }
+};
+
+// FSE decoding table from normalized counts (RFC 8878 §4.1.1), wave-uniform; entries in `tab`.
+__device__ bool zfse_build(ZWaveLds& L, uint32_t* tab, int nsym, int log) {
+  int16_t* norm = L.norm;
+  uint16_t* nxt = L.nxt;
+  const int size = 1 << log;
+  int high = size - 1;
+  const uint32_t lane = lane_id();
+  if (lane == 0) {
+    for (int s = 0; s < nsym; s++) {
+      if (norm[s] == -1) { tab[high--] = (uint32_t)s; nxt[s] = 1; }
+      else nxt[s] = (uint16_t)norm[s];
+    }
+    const int step = (size >> 1) + (size >> 3) + 3, mask = size - 1;
+    int pos = 0;
+    for (int s = 0; s < nsym; s++)
+      for (int i = 0; i < norm[s]; i++) {
+        tab[pos] = (uint32_t)s;
+        do { pos = (pos + step) & mask; } while (pos > high);
+      }
+    L.flag = pos != 0;  // the spread must end where it started
+    if (pos == 0)
+      for (int u = 0; u < size; u++) {
+        const uint32_t s = tab[u] & 0xFFu;
+        const uint32_t ns = nxt[s]++;
+        const int nb = log - zhigh(ns);
+        tab[u] = s | ((uint32_t)nb << 8) | (((ns << nb) - (uint32_t)size) << 16);
+      }
+  }
+  wave_sync();
+  return uni(L.flag) == 0;
+}
+
+// Normalized counts (FSE table description) at input offset `o`; returns bytes or -1.
+__device__ int64_t zread_ncount(rsrc_t rs, uint32_t o, uint32_t lim, int max_log, int max_sym, int16_t* norm, int* nsym,
+                                int* log) {
+  FwdBits f{rs, lim, (uint64_t)o * 8u, false};
+  const int accuracy = 5 + (int)f.get(4);
+  if (accuracy > max_log) return -1;
+  *log = accuracy;
+  int remaining = (1 << accuracy) + 1, sym = 0;
+  while (remaining > 1 && sym <= max_sym && !f.bad) {
+    const int nbits = zhigh((uint32_t)remaining) + 1;
+    const uint32_t maxv = (1u << nbits) - 1u - (uint32_t)remaining;
+    uint32_t v = f.get(nbits - 1);
+    if (v >= maxv) {
+      v |= f.get(1) << (nbits - 1);
+      if (v >= (1u << (nbits - 1))) v -= maxv;
+    }
+    const int prob = (int)v - 1;
+    if (lane_id() == 0) norm[sym] = (int16_t)prob;
+    sym++;
+    remaining -= prob < 0 ? -prob : prob;
+    if (prob == 0 && sym <= max_sym) {
+      uint32_t rep;
+      do {
+        rep = f.get(2);
+        for (uint32_t r = 0; r < rep && sym <= max_sym; r++) {
+          if (lane_id() == 0) norm[sym] = 0;
+          sym++;
+        }
+      } while (rep == 3 && !f.bad);
+    }
+  }
+  wave_sync();
+  if (f.bad || remaining != 1 || sym > max_sym + 1) return -1;
+  *nsym = sym;
+  return (int64_t)((f.bitpos + 7) >> 3) - o;
+}
+
+// Sequence table for one mode (RFC 8878 §3.1.1.3.2.1): predefined / RLE / FSE-compressed / repeat.
+__device__ bool zseq_table(ZWaveLds& L, uint32_t* tab, int* tlog, bool& have, int mode, rsrc_t rs, uint32_t& q,
+                           uint32_t lim, const int16_t* def, int def_n, int def_log, int max_log, int max_sym) {
+  if (mode == 0) {
+    if (lane_id() < (uint32_t)def_n) L.norm[lane_id()] = def[lane_id()];
+    wave_sync();
+    *tlog = def_log;
+    have = zfse_build(L, tab, def_n, def_log);
+    return have;
+  }
+  if (mode == 1) {
+    if (q >= lim) return false;
+    const uint32_t s = zbyte(rs, q);
+    q++;
+    if ((int)s > max_sym) return false;
+    if (lane_id() == 0) tab[0] = s;
+    wave_sync();
+    *tlog = 0;
+    have = true;
+    return true;
+  }
+  if (mode == 2) {
+    int ns, lg;
+    const int64_t u = zread_ncount(rs, q, lim, max_log, max_sym, L.norm, &ns, &lg);
+    if (u < 0) return false;
+    q += (uint32_t)u;
+    *tlog = lg;
+    have = zfse_build(L, tab, ns, lg);
+    return have;
+  }
+  return have;  // repeat
+}
+
+// Huffman decoding table from weights L.wts[0, nsym) (+ the implied last weight), RFC 8878 §4.2.1.
+__device__ int zhuf_build(ZWaveLds& L, int nsym) {
+  uint32_t total = 0;
+  for (int s = 0; s < nsym; s++) {
+    const uint32_t w = L.wts[s];
+    if (w > 11) return -1;
+    if (w) total += 1u << (w - 1);
+  }
+  if (!total) return -1;
+  const int max_bits = zhigh(total) + 1;
+  const uint32_t left = (1u << max_bits) - total;
+  if (max_bits > 11 || (left & (left - 1u))) return -1;
+  if (lane_id() == 0) L.wts[nsym] = (uint8_t)(zhigh(left) + 1);
+  wave_sync();
+  nsym++;
+  uint32_t next = 0;
+  for (int wt = 1; wt <= max_bits; wt++) {
+    const uint32_t nb = (uint32_t)(max_bits + 1 - wt), len = 1u << (wt - 1);
+    for (int s = 0; s < nsym; s++) {
+      if (L.wts[s] != wt) continue;
+      for (uint32_t e = lane_id(); e < len; e += WAVE) L.huf[next + e] = (uint16_t)(s | (nb << 8));
+      next += len;
+    }
+  }
+  wave_sync();
+  return next == (1u << max_bits) ? max_bits : -1;
+}
+
+// Huffman tree description at q; returns max_bits (> 0) and advances q, or -1.
+__device__ int zhuf_tree(ZWaveLds& L, rsrc_t rs, uint32_t& q, uint32_t lim) {
+  if (q >= lim) return -1;
+  const uint32_t hdr = zbyte(rs, q);
+  int nsym = 0;
+  if (hdr >= 128) {
+    nsym = (int)hdr - 127;
+    const uint32_t nb = (uint32_t)(nsym + 1) / 2;
+    if (q + 1 + nb > lim) return -1;
+    for (int s = (int)lane_id(); s < nsym; s += WAVE) {
+      const uint32_t b = zbyte(rs, q + 1 + (uint32_t)s / 2);
+      L.wts[s] = (uint8_t)((s & 1) ? (b & 15u) : (b >> 4));
+    }
+    wave_sync();
+    q += 1 + nb;
+  } else {
+    const uint32_t cs = hdr;
+    if (q + 1 + cs > lim) return -1;
+    int ns, lg;
+    const int64_t hb = zread_ncount(rs, q + 1, q + 1 + cs, 6, 255, L.norm, &ns, &lg);
+    if (hb < 0) return -1;
+    if (!zfse_build(L, L.ll, ns, lg)) return -1;  // L.ll as scratch: the sequence tables are read later
+    BackBits b;
+    if (!b.init(rs, q + 1 + (uint32_t)hb, cs - (uint32_t)hb, L.win)) return -1;
+    uint32_t s1 = b.read(lg), s2 = b.read(lg);
+    for (;;) {
+      if (nsym >= 254) return -1;
+      uint32_t e = L.ll[s1];
+      if (lane_id() == 0) L.wts[nsym] = (uint8_t)(e & 0xFFu);
+      nsym++;
+      s1 = (e >> 16) + b.read((int)((e >> 8) & 0xFFu));
+      if (b.bits < 0) {
+        if (lane_id() == 0) L.wts[nsym] = (uint8_t)(L.ll[s2] & 0xFFu);
+        nsym++;
+        break;
+      }
+      e = L.ll[s2];
+      if (lane_id() == 0) L.wts[nsym] = (uint8_t)(e & 0xFFu);
+      nsym++;
+      s2 = (e >> 16) + b.read((int)((e >> 8) & 0xFFu));
+      if (b.bits < 0) {
+        if (lane_id() == 0) L.wts[nsym] = (uint8_t)(L.ll[s1] & 0xFFu);
+        nsym++;
+        break;
+      }
+    }
+    wave_sync();
+    q += 1 + cs;
+  }
+  return zhuf_build(L, nsym);
+}
+
+// ---- output: global bytes + the LDS ring of the last ZS_RING bytes
+struct ZOut {
+  uint8_t* dst;
+  uint32_t cap;        // job's output size: bytes past it are dropped (the page reader stops there)
+  uint32_t pos;        // bytes produced
+  uint32_t frame0;     // output position of the current frame's start
+  uint32_t drained;    // every store below this position has completed
+};
+
+__device__ __forceinline__ void zput(ZOut& O, ZWaveLds& L, uint32_t p, uint32_t v) {
+  L.ring[p & (ZS_RING - 1u)] = (uint8_t)v;
+  if (p < O.cap) gst(O.dst + p, (uint8_t)v);
+}
+
+// output byte q (< pos): from the ring when recent, else from memory (system-scope load after a
+// drain; the line may sit in this CU's L1 from before it was written)
+__device__ __forceinline__ uint32_t zget(const ZOut& O, const ZWaveLds& L, uint32_t q, uint32_t pos) {
+  if (pos - q <= ZS_RING - WAVE) return L.ring[q & (ZS_RING - 1u)];
+  if (q >= O.cap) return 0;
+  const uint32_t w = sld((const uint32_t*)(O.dst + (q & ~3u)));
+  return (w >> ((q & 3u) * 8u)) & 0xFFu;
+}
+
+__device__ __forceinline__ void zdrain(ZOut& O) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  O.drained = O.pos;
+}
+
+// copy n literal bytes: from the input (raw literals), a single byte (RLE) or the literal buffer
+__device__ void zcopy_lits(ZOut& O, ZWaveLds& L, int kind, rsrc_t rs, uint32_t src, const uint8_t* litbuf,
+                           uint32_t n) {
+  for (uint32_t k0 = 0; k0 < n; k0 += WAVE) {
+    const uint32_t k = k0 + lane_id();
+    if (k < n) {
+      uint32_t v;
+      if (kind == 0) v = zbyte(rs, src + k);
+      else if (kind == 1) v = src;
+      else v = (sld((const uint32_t*)(litbuf + ((src + k) & ~3u))) >> (((src + k) & 3u) * 8u)) & 0xFFu;
+      zput(O, L, O.pos + k, v);
+    }
+  }
+  O.pos += n;
+  wave_sync();
+  if (O.pos - O.drained >= 2048u) zdrain(O);
+}
+
+// match: n bytes from `off` back; in rounds of min(off, 64) so a round only reads finished bytes
+__device__ void zcopy_match(ZOut& O, ZWaveLds& L, uint32_t off, uint32_t n) {
+  const uint32_t step = off < WAVE ? off : WAVE;
+  for (uint32_t k0 = 0; k0 < n; k0 += step) {
+    const uint32_t cur = O.pos + k0;
+    // a far match reads memory: every byte this round reads must have been stored
+    if (off > ZS_RING - WAVE && cur + step - off > O.drained) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      O.drained = cur;
+    }
+    const uint32_t k = k0 + lane_id();
+    if (lane_id() < step && k < n) {
+      const uint32_t q = O.pos + k - off;
+      zput(O, L, O.pos + k, zget(O, L, q, O.pos + k0));
+    }
+    wave_sync();
+  }
+  O.pos += n;
+  if (O.pos - O.drained >= 2048u) zdrain(O);
+}
+
+// One compressed block [q, q + bs) of the job's input. Returns 0 or an error code.
+__device__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t q, uint32_t bs, uint8_t* litbuf, bool& have_huf,
+                      int& huf_bits, bool* have_tab, int* tlog, uint32_t* rep) {
+  const uint32_t lim = q + bs;
+  if (bs < 1) return PQG_ERR_CORRUPT;
+  const uint32_t b0 = zbyte(rs, q);
+  const int lt = (int)(b0 & 3u), sf = (int)((b0 >> 2) & 3u);
+  uint32_t regen = 0, comp = 0, hl = 0;
+  if (lt <= 1) {
+    if (sf == 0 || sf == 2) { regen = b0 >> 3; hl = 1; }
+    else if (sf == 1) { regen = (b0 >> 4) + (zbyte(rs, q + 1) << 4); hl = 2; }
+    else { regen = (b0 >> 4) + (zbyte(rs, q + 1) << 4) + (zbyte(rs, q + 2) << 12); hl = 3; }
+  } else {
+    const uint64_t v = ld8_any(rs, q);
+    if (sf <= 1) { regen = (uint32_t)(v >> 4) & 0x3FFu; comp = (uint32_t)(v >> 14) & 0x3FFu; hl = 3; }
+    else if (sf == 2) { regen = (uint32_t)(v >> 4) & 0x3FFFu; comp = (uint32_t)(v >> 18) & 0x3FFFu; hl = 4; }
+    else { regen = (uint32_t)(v >> 4) & 0x3FFFFu; comp = (uint32_t)(v >> 22) & 0x3FFFFu; hl = 5; }
+  }
+  if (q + hl > lim || regen > ZS_LIT_MAX) return PQG_ERR_CORRUPT;
+  uint32_t p = q + hl;
+  int lit_kind;          // 0 raw (input at lit_src), 1 RLE (byte lit_src), 2 decoded into litbuf
+  uint32_t lit_src = 0;
+  if (lt == 0) {
+    if (p + regen > lim) return PQG_ERR_CORRUPT;
+    lit_kind = 0; lit_src = p; p += regen;
+  } else if (lt == 1) {
+    if (p + 1 > lim) return PQG_ERR_CORRUPT;
+    lit_kind = 1; lit_src = zbyte(rs, p); p += 1;
+  } else {
+    if (p + comp > lim) return PQG_ERR_CORRUPT;
+    uint32_t c = p;
+    const uint32_t cend = p + comp;
+    if (lt == 2) {
+      huf_bits = zhuf_tree(L, rs, c, cend);
+      if (huf_bits < 0) return PQG_ERR_CORRUPT;
+      have_huf = true;
+    } else if (!have_huf) {
+      return PQG_ERR_CORRUPT;
+    }
+    // streams: 1 (lane 0) or 4 (lanes 0..3), each decoded into its part of litbuf
+    uint32_t sb[4] = {c, 0, 0, 0}, sn[4] = {cend - c, 0, 0, 0}, cnt[4] = {regen, 0, 0, 0}, dst0[4] = {0, 0, 0, 0};
+    int ns = 1;
+    if (sf != 0) {
+      if (cend - c < 6) return PQG_ERR_CORRUPT;
+      const uint32_t s1 = zbyte(rs, c) | (zbyte(rs, c + 1) << 8), s2 = zbyte(rs, c + 2) | (zbyte(rs, c + 3) << 8),
+                     s3 = zbyte(rs, c + 4) | (zbyte(rs, c + 5) << 8);
+      const uint32_t tot = cend - c - 6;
+      if ((uint64_t)s1 + s2 + s3 > tot) return PQG_ERR_CORRUPT;
+      const uint32_t seg = (regen + 3) / 4;
+      if (3 * seg > regen) return PQG_ERR_CORRUPT;
+      sb[0] = c + 6; sn[0] = s1;
+      sb[1] = sb[0] + s1; sn[1] = s2;
+      sb[2] = sb[1] + s2; sn[2] = s3;
+      sb[3] = sb[2] + s3; sn[3] = tot - s1 - s2 - s3;
+      cnt[0] = cnt[1] = cnt[2] = seg; cnt[3] = regen - 3 * seg;
+      dst0[1] = seg; dst0[2] = 2 * seg; dst0[3] = 3 * seg;
+      ns = 4;
+    }
+    const uint32_t lane = lane_id();
+    int bad = 0;
+    if ((int)lane < ns) {
+      uint32_t mb = 0, mn = 0, mc = 0, md = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if ((int)lane == i) { mb = sb[i]; mn = sn[i]; mc = cnt[i]; md = dst0[i]; }
+      LaneBits lb{mb, mn, 0xFFFFFFFFu, 0, L.hwin[lane]};
+      const uint32_t last = mn ? zbyte(rs, mb + mn - 1) : 0u;
+      if (!last) {
+        bad = 1;
+      } else {
+        lb.bits = (int64_t)(mn - 1) * 8 + zhigh(last);
+        uint32_t acc = 0;
+        for (uint32_t i = 0; i < mc; i++) {
+          const uint32_t e = L.huf[lb.peek(rs, huf_bits)];
+          lb.bits -= (int64_t)(e >> 8);
+          if (lb.bits < 0) { bad = 1; break; }
+          const uint32_t o = md + i;
+          acc |= (e & 0xFFu) << ((o & 3u) * 8u);
+          if ((o & 3u) == 3u || i + 1 == mc) {  // flush a (partial) dword: byte stores keep neighbours
+            for (uint32_t j = (o & ~3u) > md ? (o & ~3u) : md; j <= o; j++) gst(litbuf + j, (uint8_t)(acc >> ((j & 3u) * 8u)));
+            acc = 0;
+          }
+        }
+        if (!bad && lb.bits != 0) bad = 1;
+      }
+    }
+    if (__ballot(bad)) return PQG_ERR_CORRUPT;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // literals in memory before they are read back
+    lit_kind = 2;
+    p += comp;
+  }
+  // ---- sequences
+  if (p >= lim) return PQG_ERR_CORRUPT;
+  uint32_t nseq = zbyte(rs, p);
+  if (nseq == 0) {
+    p += 1;
+    zcopy_lits(O, L, lit_kind, rs, lit_src, litbuf, regen);
+    return p == lim ? 0 : PQG_ERR_CORRUPT;
+  }
+  if (nseq < 128) { p += 1; }
+  else if (nseq < 255) { nseq = ((nseq - 128) << 8) + zbyte(rs, p + 1); p += 2; }
+  else { nseq = zbyte(rs, p + 1) + (zbyte(rs, p + 2) << 8) + 0x7F00u; p += 3; }
+  if (p >= lim) return PQG_ERR_CORRUPT;
+  const uint32_t modes = zbyte(rs, p++);
+  if (modes & 3u) return PQG_ERR_CORRUPT;
+  if (!zseq_table(L, L.ll, &tlog[0], have_tab[0], (int)(modes >> 6), rs, p, lim, ZLL_DEF, 36, 6, 9, 35)) return PQG_ERR_CORRUPT;
+  if (!zseq_table(L, L.of, &tlog[1], have_tab[1], (int)((modes >> 4) & 3u), rs, p, lim, ZOF_DEF, 29, 5, 8, 31)) return PQG_ERR_CORRUPT;
+  if (!zseq_table(L, L.ml, &tlog[2], have_tab[2], (int)((modes >> 2) & 3u), rs, p, lim, ZML_DEF, 53, 6, 9, 52)) return PQG_ERR_CORRUPT;
+  BackBits b;
+  if (!b.init(rs, p, lim - p, L.win)) return PQG_ERR_CORRUPT;
+  uint32_t sl = b.read(tlog[0]), so = b.read(tlog[1]), sm = b.read(tlog[2]);
+  uint32_t lit_pos = 0;
+  for (uint32_t i = 0; i < nseq; i++) {
+    const uint32_t el = L.ll[sl], eo = L.of[so], em = L.ml[sm];
+    const uint32_t llc = el & 0xFFu, ofc = eo & 0xFFu, mlc = em & 0xFFu;
+    if (llc > 35 || mlc > 52 || ofc > 31) return PQG_ERR_CORRUPT;
+    const uint64_t ofv = (1ull << ofc) + (ofc ? b.read((int)ofc) : 0u);
+    const uint32_t ml = ZML_BASE[mlc] + (ZML_BITS[mlc] ? b.read(ZML_BITS[mlc]) : 0u);
+    const uint32_t ll = ZLL_BASE[llc] + (ZLL_BITS[llc] ? b.read(ZLL_BITS[llc]) : 0u);
+    uint32_t off;
+    if (ofv > 3) {
+      off = (uint32_t)(ofv - 3);
+      rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = off;
+    } else {
+      uint32_t idx = (uint32_t)ofv - 1u;
+      if (ll == 0) idx++;
+      if (idx == 0) {
+        off = rep[0];
+      } else if (idx == 3) {
+        off = rep[0] - 1u;
+        if (off == 0) return PQG_ERR_CORRUPT;
+        rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = off;
+      } else {
+        off = idx == 1 ? rep[1] : rep[2];
+        if (idx == 2) rep[2] = rep[1];
+        rep[1] = rep[0];
+        rep[0] = off;
+      }
+    }
+    if (i + 1 < nseq) {
+      sl = (el >> 16) + b.read((int)((el >> 8) & 0xFFu));
+      sm = (em >> 16) + b.read((int)((em >> 8) & 0xFFu));
+      so = (eo >> 16) + b.read((int)((eo >> 8) & 0xFFu));
+    }
+    if (b.bits < 0 || lit_pos + ll > regen) return PQG_ERR_CORRUPT;
+    if (ll) zcopy_lits(O, L, lit_kind, rs, lit_kind == 1 ? lit_src : lit_src + lit_pos, litbuf, ll);
+    lit_pos += ll;
+    if (off == 0 || off > O.pos - O.frame0) return PQG_ERR_CORRUPT;
+    zcopy_match(O, L, off, ml);
+  }
+  if (b.bits != 0) return PQG_ERR_CORRUPT;
+  if (regen > lit_pos) zcopy_lits(O, L, lit_kind, rs, lit_kind == 1 ? lit_src : lit_src + lit_pos, litbuf, regen - lit_pos);
+  return 0;
+}
+
+// XXH64 of the frame's output [a, e) (content checksum), lane 0 alone: the output is re-read from
+// memory after a drain. Only for frames that carry a checksum.
+__device__ uint64_t zxxh64(const uint8_t* p, uint32_t n) {
+  constexpr uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull, P3 = 1609587929392839161ull,
+                     P4 = 9650029242287828579ull, P5 = 2870177450012600261ull;
+  auto rotl = [](uint64_t x, int r) { return (x << r) | (x >> (64 - r)); };
+  const uint32_t mis = (uint32_t)(uintptr_t)p & 3u;
+  const uint32_t* base = (const uint32_t*)(p - mis);
+  auto rd = [&](uint32_t o, int bytes) {  // little-endian bytes [o, o + bytes) of the output, bytes <= 8
+    const uint32_t a = o + mis, w = a >> 2, s = a & 3u;
+    const uint32_t d0 = sld(base + w), d1 = sld(base + w + 1), d2 = s ? sld(base + w + 2) : 0u;
+    uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
+    return bytes == 8 ? v : v & ((1ull << (8 * bytes)) - 1ull);
+  };
+  auto round = [&](uint64_t acc, uint64_t in) { acc += in * P2; acc = rotl(acc, 31); return acc * P1; };
+  uint32_t o = 0;
+  uint64_t h;
+  if (n >= 32) {
+    uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1;
+    for (; o + 32 <= n; o += 32) {
+      v1 = round(v1, rd(o, 8)); v2 = round(v2, rd(o + 8, 8)); v3 = round(v3, rd(o + 16, 8)); v4 = round(v4, rd(o + 24, 8));
+    }
+    h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+    for (uint64_t v : {v1, v2, v3, v4}) { h ^= round(0, v); h = h * P1 + P4; }
+  } else {
+    h = P5;
+  }
+  h += n;
+  for (; o + 8 <= n; o += 8) { h ^= round(0, rd(o, 8)); h = rotl(h, 27) * P1 + P4; }
+  if (o + 4 <= n) { h ^= rd(o, 4) * P1; h = rotl(h, 23) * P2 + P3; o += 4; }
+  for (; o < n; o++) { h ^= rd(o, 1) * P5; h = rotl(h, 11) * P1; }
+  h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+  return h;
+}
+
+// One wave per job: the frames of src[job] -> dst[job] (exactly dst_size bytes kept).
+__global__ __launch_bounds__(64) void k_zstd(const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
+                                             uint64_t dst_bytes, const pqg_snappy_job* __restrict__ jobs, int n_jobs,
+                                             int32_t* status, uint8_t* scratch, uint64_t lit_stride) {
+  __shared__ __attribute__((aligned(16))) ZWaveLds L;
+  const int j = (int)blockIdx.x;
+  if (j >= n_jobs) return;
+  const pqg_snappy_job jb = jobs[j];
+  const rsrc_t rs = make_rsrc(src + jb.src_offset, src_bytes - jb.src_offset);
+  const uint32_t n = uni(jb.src_size);
+  uint8_t* litbuf = scratch + (uint64_t)j * lit_stride;
+  ZOut O{dst + jb.dst_offset, uni(jb.dst_size), 0, 0, 0};
+  int code = 0;
+  uint32_t p = 0;
+  if (jb.dst_offset + jb.dst_size > dst_bytes || jb.src_offset + jb.src_size > src_bytes) code = PQG_ERR_INVALID_ARG;
+  while (!code && p < n && O.pos < O.cap) {
+    p = uni(p);
+    if (n - p < 4) { code = PQG_ERR_CORRUPT; break; }
+    const uint32_t magic = ld4_any(rs, p);
+    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
+      if (n - p < 8) { code = PQG_ERR_CORRUPT; break; }
+      const uint32_t sz = ld4_any(rs, p + 4);
+      if (sz > n - p - 8) { code = PQG_ERR_CORRUPT; break; }
+      p += 8 + sz;
+      continue;
+    }
+    if (magic != 0xFD2FB528u) { code = PQG_ERR_CORRUPT; break; }
+    p += 4;
+    if (p >= n) { code = PQG_ERR_CORRUPT; break; }
+    const uint32_t fhd = zbyte(rs, p++);
+    const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1u, checksum = (fhd >> 2) & 1u, did_flag = fhd & 3u;
+    if (fhd & 8u) { code = PQG_ERR_CORRUPT; break; }
+    if (!single) p++;  // Window_Descriptor: the whole frame is decoded in place
+    const uint32_t did_sz = did_flag == 3 ? 4u : did_flag;
+    uint32_t did = 0;
+    for (uint32_t i = 0; i < did_sz; i++) did |= zbyte(rs, p + i) << (8 * i);
+    p += did_sz;
+    if (did) { code = PQG_ERR_CORRUPT; break; }
+    const uint32_t fcs_sz = fcs_flag == 0 ? single : (fcs_flag == 1 ? 2u : fcs_flag == 2 ? 4u : 8u);
+    if (p + fcs_sz > n) { code = PQG_ERR_CORRUPT; break; }
+    uint64_t fcs = 0;
+    for (uint32_t i = 0; i < fcs_sz; i++) fcs |= (uint64_t)zbyte(rs, p + i) << (8 * i);
+    if (fcs_sz == 2) fcs += 256;
+    p += fcs_sz;
+    O.frame0 = O.pos;
+    uint32_t rep[3] = {1, 4, 8};
+    bool have_huf = false, have_tab[3] = {false, false, false};
+    int huf_bits = 0, tlog[3] = {0, 0, 0};
+    bool cut = false;
+    while (!code) {
+      if (O.pos >= O.cap) { cut = true; break; }  // the page reader stops at its size
+      if (p + 3 > n) { code = PQG_ERR_CORRUPT; break; }
+      const uint32_t bh = zbyte(rs, p) | (zbyte(rs, p + 1) << 8) | (zbyte(rs, p + 2) << 16);
+      p += 3;
+      const uint32_t last = bh & 1u, type = (bh >> 1) & 3u, bs = bh >> 3;
+      if (type == 3) { code = PQG_ERR_CORRUPT; break; }
+      if (type == 1) {
+        if (p + 1 > n) { code = PQG_ERR_CORRUPT; break; }
+        const uint32_t v = zbyte(rs, p);
+        for (uint32_t k0 = 0; k0 < bs; k0 += WAVE)
+          if (k0 + lane_id() < bs) zput(O, L, O.pos + k0 + lane_id(), v);
+        O.pos += bs;
+        p += 1;
+        wave_sync();
+      } else if (type == 0) {
+        if (p + bs > n) { code = PQG_ERR_CORRUPT; break; }
+        zcopy_lits(O, L, 0, rs, p, litbuf, bs);
+        p += bs;
+      } else {
+        if (p + bs > n) { code = PQG_ERR_CORRUPT; break; }
+        const uint32_t before = O.pos;
+        code = zblock(L, O, rs, p, bs, litbuf, have_huf, huf_bits, have_tab, tlog, rep);
+        if (!code && O.pos - before > ZS_LIT_MAX) code = PQG_ERR_CORRUPT;
+        p += bs;
+      }
+      if (O.pos - O.drained >= 2048u) zdrain(O);
+      if (last) break;
+    }
+    if (code || cut) break;
+    if ((fcs_flag || single) && (uint64_t)(O.pos - O.frame0) != fcs) { code = PQG_ERR_CORRUPT; break; }
+    if (checksum) {
+      if (p + 4 > n) { code = PQG_ERR_CORRUPT; break; }
+      const uint32_t want = ld4_any(rs, p);
+      p += 4;
+      if (O.pos <= O.cap) {
+        zdrain(O);
+        const uint32_t got = (uint32_t)zxxh64(O.dst + O.frame0, O.pos - O.frame0);
+        if (uni(got) != want) { code = PQG_ERR_CORRUPT; break; }
+      }
+    }
+  }
+  if (!code && O.pos < O.cap) code = PQG_ERR_EOF;  // the frames end before the page's size
+  if (lane_id() == 0 && status) status[j] = code;
+}
+
+hipError_t launch_zstd(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
+                       const pqg_snappy_job* jobs, int n_jobs, int32_t* status, uint8_t* scratch) {
+  if (n_jobs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_zstd, dim3(n_jobs), dim3(64), 0, st, src, src_bytes, dst, dst_bytes, jobs, n_jobs, status,
+                     scratch, (uint64_t)ZS_LIT_MAX);
+  return hipGetLastError();
+}
+
+}  // namespace pqg

@@ -26,7 +26,7 @@ class DeviceBatch:
         self.batch = batch
         self.device = device
         self.bytes = torch.from_numpy(batch.data).to(device)
-        self.snappy = None  # (compressed blocks, job table, status) when built by Decoder.upload_chunks
+        self.codec_jobs = None  # [(codec, compressed blocks, job table, status, n)] when built by Decoder.upload_chunks
 
     @property
     def n_bytes(self):
@@ -129,29 +129,36 @@ class Decoder:
     def upload(self, batch):
         return DeviceBatch(batch, self.device)
 
+    _CODEC_FN = {writer.SNAPPY: ("pqg_snappy_decompress", "pqg_snappy_sync", "snappy block"),
+                 writer.ZSTD: ("pqg_zstd_decompress", "pqg_zstd_sync", "zstd frame")}
+
     def upload_chunks(self, chunks):
-        """Column chunks whose pages may be SNAPPY-compressed -> a DeviceBatch of uncompressed pages.
+        """Column chunks whose pages may be SNAPPY- or ZSTD-compressed -> a DeviceBatch of
+        uncompressed pages.
 
         The batch is laid out for the uncompressed pages (writer.build_batch over placeholders of
         the uncompressed sizes), the compressed blocks are uploaded once, and
-        pqg_snappy_decompress writes every block straight into its page's place in the batch on
-        the GPU (ColumnChunkPageReadStore.readPage's decompress step). Raises PqgError(CORRUPT)
-        with the failing block when a block is malformed or its length differs from the header."""
+        pqg_snappy_decompress / pqg_zstd_decompress write every block straight into its page's
+        place in the batch on the GPU (ColumnChunkPageReadStore.readPage's decompress step).
+        Raises PqgError(CORRUPT / EOF) with the failing block when a block is malformed or its
+        length differs from the header."""
         import copy
-        placeholders, blocks = [], []   # blocks: (payload, ("dict", output column) | ("page", page index), prefix)
+        placeholders, blocks = [], []   # (codec, payload, ("dict", chunk) | ("page", page index), prefix)
         n_page = 0
         for ch in chunks:
             ph = copy.copy(ch)
             ph.pages = []
-            if ch.dict_page is not None and ch.dict_codec == writer.SNAPPY:
+            if ch.dict_page is not None and ch.dict_codec != writer.UNCOMPRESSED:
+                if ch.dict_codec not in self._CODEC_FN:
+                    raise native.PqgError(abi.ERR_UNSUPPORTED, what=f"dictionary page codec {ch.dict_codec}")
                 ph.dict_page = bytes(ch.dict_uncompressed_size)
-                blocks.append((ch.dict_page, ("dict", len(placeholders)), 0))
+                blocks.append((ch.dict_codec, ch.dict_page, ("dict", len(placeholders)), 0))
             for pg in ch.pages:
                 q = copy.copy(pg)
-                if pg.codec == writer.SNAPPY:
+                if pg.codec in self._CODEC_FN:
                     lv = pg.rl_byte_length + pg.dl_byte_length if pg.version == 2 else 0
                     q.body = pg.body[:lv] + bytes(pg.uncompressed_size - lv)
-                    blocks.append((pg.body[lv:], ("page", n_page), lv))
+                    blocks.append((pg.codec, pg.body[lv:], ("page", n_page), lv))
                 elif pg.codec != writer.UNCOMPRESSED:
                     raise native.PqgError(abi.ERR_UNSUPPORTED, what=f"page codec {pg.codec}")
                 ph.pages.append(q)
@@ -166,43 +173,71 @@ class Decoder:
         for i, ch in enumerate(placeholders):
             seen.setdefault(getattr(ch, "column_index", i), len(seen))
             col_of_chunk.append(seen[getattr(ch, "column_index", i)])
-        src, jobs, pos = [], np.zeros((len(blocks), 3), dtype=np.uint64), 0
-        sizes = np.zeros((len(blocks), 2), dtype=np.uint32)
-        for j, (payload, (kind, idx), prefix) in enumerate(blocks):
-            if kind == "dict":
-                dst = int(batch.columns[col_of_chunk[idx]]["dict_offset"])
-                n_out = int(batch.columns[col_of_chunk[idx]]["dict_size"])
-            else:
-                dst = int(batch.pages["offset"][idx]) + prefix
-                n_out = int(batch.pages["size"][idx]) - prefix
-            jobs[j, 0], jobs[j, 1] = pos, dst
-            sizes[j] = (len(payload), n_out)
-            src.append(payload + bytes((-len(payload)) % 16))
-            pos += len(src[-1])
-        table = np.zeros(len(blocks), dtype=np.dtype([("src_offset", "<u8"), ("dst_offset", "<u8"),
-                                                      ("src_size", "<u4"), ("dst_size", "<u4")]))
-        table["src_offset"], table["dst_offset"] = jobs[:, 0], jobs[:, 1]
-        table["src_size"], table["dst_size"] = sizes[:, 0], sizes[:, 1]
-        d_src = torch.from_numpy(np.frombuffer(b"".join(src) + bytes(16), dtype=np.uint8).copy()).to(self.device)
-        d_jobs = torch.from_numpy(table.view(np.uint8).copy()).to(self.device)
-        d_status = torch.zeros(len(blocks), dtype=torch.int32, device=self.device)
+        jobsets = []
+        for codec in sorted({b[0] for b in blocks}):
+            mine = [b for b in blocks if b[0] == codec]
+            src, pos = [], 0
+            table = np.zeros(len(mine), dtype=np.dtype([("src_offset", "<u8"), ("dst_offset", "<u8"),
+                                                        ("src_size", "<u4"), ("dst_size", "<u4")]))
+            for j, (_, payload, (kind, idx), prefix) in enumerate(mine):
+                if kind == "dict":
+                    dst = int(batch.columns[col_of_chunk[idx]]["dict_offset"])
+                    n_out = int(batch.columns[col_of_chunk[idx]]["dict_size"])
+                else:
+                    dst = int(batch.pages["offset"][idx]) + prefix
+                    n_out = int(batch.pages["size"][idx]) - prefix
+                table[j] = (pos, dst, len(payload), n_out)
+                src.append(payload + bytes((-len(payload)) % 16))
+                pos += len(src[-1])
+            d_src = torch.from_numpy(np.frombuffer(b"".join(src) + bytes(16), dtype=np.uint8).copy()).to(self.device)
+            d_jobs = torch.from_numpy(table.view(np.uint8).copy()).to(self.device)
+            d_status = torch.zeros(len(mine), dtype=torch.int32, device=self.device)
+            jobsets.append((codec, d_src, d_jobs, d_status, len(mine)))
         torch.cuda.current_stream(self.device).synchronize()  # the uploads above, before the decoder's stream
-        dbatch.snappy = (d_src, d_jobs, d_status, len(blocks))
+        dbatch.codec_jobs = jobsets
         self.decompress(dbatch)
-        st = abi.Status()
-        rc = native.lib().pqg_snappy_sync(self.ctx, d_status.data_ptr(), len(blocks), C.byref(st))
-        native.check(rc, st, what="snappy block")
+        for codec, _, _, d_status, n in jobsets:
+            st = abi.Status()
+            _, sync, what = self._CODEC_FN[codec]
+            rc = getattr(native.lib(), sync)(self.ctx, d_status.data_ptr(), n, C.byref(st))
+            native.check(rc, st, what=what)
         return dbatch
 
     def decompress(self, dbatch):
-        """(Re)issue the SNAPPY decompression of an upload_chunks batch on the decoder's stream
+        """(Re)issue the page decompression of an upload_chunks batch on the decoder's stream
         (asynchronous; the benchmarks time it together with the decode)."""
-        if getattr(dbatch, "snappy", None) is None:
-            return
-        d_src, d_jobs, d_status, n = dbatch.snappy
-        rc = native.lib().pqg_snappy_decompress(self.ctx, d_src.data_ptr(), d_src.numel(), dbatch.bytes.data_ptr(),
-                                                dbatch.n_bytes, d_jobs.data_ptr(), n, d_status.data_ptr())
-        native.check(rc, what="pqg_snappy_decompress")
+        for codec, d_src, d_jobs, d_status, n in getattr(dbatch, "codec_jobs", None) or ():
+            fn = getattr(native.lib(), self._CODEC_FN[codec][0])
+            rc = fn(self.ctx, d_src.data_ptr(), d_src.numel(), dbatch.bytes.data_ptr(), dbatch.n_bytes,
+                    d_jobs.data_ptr(), n, d_status.data_ptr())
+            native.check(rc, what=self._CODEC_FN[codec][0])
+
+    def zstd_decompress(self, frames, sizes):
+        """Raw Zstandard frames (host bytes) -> device tensor of the concatenated outputs (each at a
+        16-byte aligned offset) + the offsets, decompressed by pqg_zstd_decompress.
+        Returns (out_tensor, offsets, status_codes, status)."""
+        src, soff, pos = [], [], 0
+        for b in frames:
+            soff.append(pos)
+            src.append(bytes(b) + bytes((-len(b)) % 16))
+            pos += len(src[-1])
+        doff = np.concatenate([[0], np.cumsum([(s + 15) // 16 * 16 + 16 for s in sizes])]).astype(np.int64)
+        table = np.zeros(len(frames), dtype=np.dtype([("src_offset", "<u8"), ("dst_offset", "<u8"),
+                                                      ("src_size", "<u4"), ("dst_size", "<u4")]))
+        table["src_offset"], table["dst_offset"] = soff, doff[:-1]
+        table["src_size"], table["dst_size"] = [len(b) for b in frames], sizes
+        d_src = torch.from_numpy(np.frombuffer(b"".join(src) + bytes(16), dtype=np.uint8).copy()).to(self.device)
+        d_dst = torch.zeros(int(doff[-1]) + 16, dtype=torch.uint8, device=self.device)
+        d_jobs = torch.from_numpy(table.view(np.uint8).copy()).to(self.device)
+        d_status = torch.full((max(len(frames), 1),), -1, dtype=torch.int32, device=self.device)
+        torch.cuda.current_stream(self.device).synchronize()
+        L = native.lib()
+        native.check(L.pqg_zstd_decompress(self.ctx, d_src.data_ptr(), d_src.numel(), d_dst.data_ptr(), d_dst.numel(),
+                                           d_jobs.data_ptr(), len(frames), d_status.data_ptr()),
+                     what="pqg_zstd_decompress")
+        st = abi.Status()
+        L.pqg_zstd_sync(self.ctx, d_status.data_ptr(), len(frames), C.byref(st))
+        return d_dst, doff, d_status[:len(frames)].cpu().numpy(), st
 
     def snappy_decompress(self, blocks, sizes, skew=False):
         """Raw Snappy blocks (host bytes) -> device tensor of the concatenated outputs (each at a

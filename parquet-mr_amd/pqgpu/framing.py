@@ -3,9 +3,10 @@
 Restates what parquet-mr's ParquetFileReader.Chunk.readAllPages does for one
 column chunk (parquet-hadoop/.../ParquetFileReader.java:1824-1979) with the
 header read by Util.readPageHeader (parquet-format-structures/.../Util.java:127-131,
-Thrift TCompactProtocol). Chunks are UNCOMPRESSED or SNAPPY (ColumnMetaData.codec):
-SNAPPY pages keep their compressed bodies (codec / uncompressed_size on the Page) and are
-decompressed on the GPU by Decoder.upload_chunks (pqg_snappy_decompress). The result is a
+Thrift TCompactProtocol). Chunks are UNCOMPRESSED, SNAPPY or ZSTD (ColumnMetaData.codec):
+compressed pages keep their compressed bodies (codec / uncompressed_size on the Page) and are
+decompressed on the GPU by Decoder.upload_chunks (pqg_snappy_decompress / pqg_zstd_decompress).
+The C-ABI form of the same walk is pqg_frame_chunk (frame_chunk_native below). The result is a
 writer.ColumnChunk whose pages feed writer.build_batch -> the device decoder.
 
 This is host-side metadata handling (headers, offsets); no page data is decoded
@@ -168,8 +169,8 @@ def read_column_chunk(buf, start, length, physical_type, max_def=0, max_rep=0, t
         h, body = read_page_header(buf, pos)
         size = h["compressed_page_size"]
         usize = h.get("uncompressed_page_size", size)
-        if codec not in (0, 1):
-            raise ThriftError(f"codec {codec} is not supported (UNCOMPRESSED and SNAPPY are)")
+        if codec not in (0, 1, 6):
+            raise ThriftError(f"codec {codec} is not supported (UNCOMPRESSED, SNAPPY and ZSTD are)")
         if not codec and usize != size and h["type"] != DATA_PAGE_V2:
             raise ThriftError("compressed page in an UNCOMPRESSED chunk")
         data = bytes(buf[body:body + size])

@@ -479,7 +479,7 @@ def build_batch(chunks, align=ALIGN):
                      column_values=col_vals)
 
 
-UNCOMPRESSED, SNAPPY = 0, 1
+UNCOMPRESSED, SNAPPY, ZSTD = 0, 1, 6   # parquet.thrift CompressionCodec
 
 
 def snappy_chunk(chunk):
@@ -499,4 +499,25 @@ def snappy_chunk(chunk):
         lv = pg.rl_byte_length + pg.dl_byte_length if pg.version == 2 else 0
         pg.body = pg.body[:lv] + pa.compress(pg.body[lv:], codec="snappy", asbytes=True)
         pg.codec = SNAPPY
+    return out
+
+
+def zstd_chunk(chunk, level=3):
+    """A copy of `chunk` with every page (and the dictionary page) ZSTD-compressed the way
+    parquet-mr writes ZSTD column chunks (V1: the whole body; V2: the data section), at parquet-mr's
+    default level 3 (ZstandardCodec). Compression by pyarrow's libzstd (test-data synthesis only)."""
+    import copy
+
+    import pyarrow as pa
+    codec = pa.Codec("zstd", compression_level=level)
+    out = copy.deepcopy(chunk)
+    if out.dict_page is not None:
+        out.dict_uncompressed_size = len(out.dict_page)
+        out.dict_page = codec.compress(out.dict_page, asbytes=True)
+        out.dict_codec = ZSTD
+    for pg in out.pages:
+        pg.uncompressed_size = len(pg.body)
+        lv = pg.rl_byte_length + pg.dl_byte_length if pg.version == 2 else 0
+        pg.body = pg.body[:lv] + codec.compress(pg.body[lv:], asbytes=True)
+        pg.codec = ZSTD
     return out

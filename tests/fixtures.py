@@ -24,7 +24,7 @@ def chunk_cases():
 def load_chunk(name, c):
     buf = np.fromfile(os.path.join(GOLDEN, name + ".parquet"), dtype=np.uint8)
     ptype = framing.TYPE_BY_NAME[c["physical_type"]]
-    codec = writer.SNAPPY if c.get("compression") == "SNAPPY" else writer.UNCOMPRESSED
+    codec = {"SNAPPY": writer.SNAPPY, "ZSTD": writer.ZSTD}.get(c.get("compression"), writer.UNCOMPRESSED)
     ch = framing.read_column_chunk(buf, c["start"], c["length"], ptype, max_def=c["max_def"], max_rep=c["max_rep"],
                                    type_length=c["type_length"], num_values=c["num_values"], codec=codec)
     exp = np.load(os.path.join(GOLDEN, name + ".npz"))
@@ -48,22 +48,24 @@ def is_compressed(ch):
 
 
 def decompressed_on_host(ch):
-    """The chunk with every SNAPPY page decompressed by the ORACLE (test infrastructure)."""
+    """The chunk with every SNAPPY / ZSTD page decompressed by the ORACLE (test infrastructure)."""
     import copy
 
     from oracle import pqref
     out = copy.deepcopy(ch)
     if out.dict_codec:
-        out.dict_page = pqref.snappy_decompress(out.dict_page, out.dict_uncompressed_size)
+        unz = pqref.zstd_decompress if out.dict_codec == writer.ZSTD else pqref.snappy_decompress
+        out.dict_page = unz(out.dict_page, out.dict_uncompressed_size)
         out.dict_codec = writer.UNCOMPRESSED
     for p in out.pages:
         if p.codec:
             lv = p.rl_byte_length + p.dl_byte_length if p.version == 2 else 0
-            p.body = p.body[:lv] + pqref.snappy_decompress(p.body[lv:], p.uncompressed_size - lv)
+            unz = pqref.zstd_decompress if p.codec == writer.ZSTD else pqref.snappy_decompress
+            p.body = p.body[:lv] + unz(p.body[lv:], p.uncompressed_size - lv)
             p.codec = writer.UNCOMPRESSED
     return out
 
 
 def batch_of(ch):
-    """Host batch of a fixture chunk (SNAPPY pages decompressed by the oracle)."""
+    """Host batch of a fixture chunk (compressed pages decompressed by the oracle)."""
     return writer.build_batch([decompressed_on_host(ch) if is_compressed(ch) else ch])

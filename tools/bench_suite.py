@@ -79,6 +79,12 @@ def gen(name, rows):
     if name == "plain_i64_snappy":  # int64 random walk, PLAIN pages, SNAPPY
         walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
         return WL.Workload(name, [writer.snappy_chunk(writer.write_column_chunk(abi.INT64, walk, abi.PLAIN))], [E(walk)])
+    if name == "c2_zstd":     # the headline pages, ZSTD-compressed at parquet-mr's default level 3
+        w = WL.c2(rows)
+        return WL.Workload(name, [writer.zstd_chunk(w.chunks[0])], w.expect)
+    if name == "plain_i64_zstd":  # int64 random walk, PLAIN pages, ZSTD level 3
+        walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
+        return WL.Workload(name, [writer.zstd_chunk(writer.write_column_chunk(abi.INT64, walk, abi.PLAIN))], [E(walk)])
     if name == "delta_i64":
         walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
         return WL.Workload(name, [writer.write_column_chunk(abi.INT64, walk, abi.DELTA_BINARY_PACKED)], [E(walk)])
@@ -109,18 +115,20 @@ def cpu_sample(chunks, max_pages, budget_s):
         sub.append(c)
     t_unz, label = 0.0, ""
     if any(p.codec for c in sub for p in c.pages):
-        # SNAPPY: the oracle decompresses the pages (C restatement of the block format), timed too
+        # SNAPPY / ZSTD: the oracle decompresses the pages (C restatements of the formats), timed too
         import copy
+        fns = {writer.SNAPPY: pqref.snappy_decompress, writer.ZSTD: pqref.zstd_decompress}
+        codec_name = {writer.SNAPPY: "Snappy", writer.ZSTD: "ZSTD"}[next(p.codec for c in sub for p in c.pages if p.codec)]
 
         def unz(c):
             c = copy.deepcopy(c)
             if c.dict_codec:
-                c.dict_page = pqref.snappy_decompress(c.dict_page, c.dict_uncompressed_size)
+                c.dict_page = fns[c.dict_codec](c.dict_page, c.dict_uncompressed_size)
                 c.dict_codec = 0
             for p in c.pages:
                 if p.codec:
                     lv = p.rl_byte_length + p.dl_byte_length if p.version == 2 else 0
-                    p.body = p.body[:lv] + pqref.snappy_decompress(p.body[lv:], p.uncompressed_size - lv)
+                    p.body = p.body[:lv] + fns[p.codec](p.body[lv:], p.uncompressed_size - lv)
                     p.codec = 0
             return c
         t0, zr = time.perf_counter(), 0
@@ -130,7 +138,7 @@ def cpu_sample(chunks, max_pages, budget_s):
             if time.perf_counter() - t0 >= budget_s / 2:
                 break
         t_unz = (time.perf_counter() - t0) / zr
-        sub, label = plain, f" + Snappy decompression {t_unz * 1e3:.1f} ms per rep"
+        sub, label = plain, f" + {codec_name} decompression {t_unz * 1e3:.1f} ms per rep"
     b = writer.build_batch(sub)
     t0 = time.perf_counter()
     reps = 0
@@ -155,7 +163,7 @@ def run(name, rows, steps, warmup, cpu_budget):
     compressed = any(p.codec for ch in chunks for p in ch.pages)
     t_gen = time.perf_counter() - t0
     dec = D.Decoder(0)
-    if compressed:  # SNAPPY: every timed step decompresses on the GPU, then decodes
+    if compressed:  # SNAPPY / ZSTD: every timed step decompresses on the GPU, then decodes
         dbatch = dec.upload_chunks(chunks)
         batch = dbatch.batch
     else:
@@ -203,8 +211,9 @@ def run(name, rows, steps, warmup, cpu_budget):
         ev2[1].record(dec.stream)
         torch.cuda.synchronize()
         sms = ev2[0].elapsed_time(ev2[1]) / steps
-        res.update({"compressed_bytes": comp, "snappy_ms": sms,
-                    "snappy_gbps_uncompressed": enc / (sms / 1e3) / 1e9})
+        codec = {writer.SNAPPY: "snappy", writer.ZSTD: "zstd"}[next(p.codec for ch in chunks for p in ch.pages if p.codec)]
+        res.update({"compressed_bytes": comp, f"{codec}_ms": sms,
+                    f"{codec}_gbps_uncompressed": enc / (sms / 1e3) / 1e9})
     if name == "c1_plain_i32":
         t1 = time.perf_counter()
         rc2, st2, res2, _ = dec.decode_host(batch)
@@ -232,6 +241,7 @@ def main():
                     "c5_levels": 100_000_000, "str_plain": 20_000_000, "str_dict": 20_000_000,
                     "str_dlba": 20_000_000, "str_dba": 20_000_000, "bss_f64": 100_000_000, "delta_i64": 100_000_000,
                     "c2_snappy": 100_000_000, "plain_i64_snappy": 100_000_000,
+                    "c2_zstd": 100_000_000, "plain_i64_zstd": 100_000_000,
                     "c4_lineitem": 8_000_000}
     for w in args.workloads:
         rows = args.rows or default_rows[w]
