@@ -115,8 +115,22 @@ typedef struct pqg_page_desc {
   int32_t dl_encoding;     /* V1 only: RLE or BIT_PACKED (ignored when max_def == 0) */
   uint32_t rl_byte_length; /* V2 only: repetition_levels_byte_length */
   uint32_t dl_byte_length; /* V2 only: definition_levels_byte_length */
-  uint32_t reserved;
+  uint32_t flags;          /* PQG_PAGE_* (0 for a page written by a current writer) */
 } pqg_page_desc;
+
+/* pqg_page_desc.flags: PQG_PAGE_DBA_CARRY — a DELTA_BYTE_ARRAY page whose reader takes the previous
+ * page's last value as its starting `previous` (PARQUET-246: DeltaByteArrayWriter before parquet-mr
+ * 1.8.0 did not reset `previous` between pages, so the first value of every page after the first may
+ * carry a prefix of the previous page's last value). The reader side is
+ * ColumnReaderBase.initDataReader (parquet-column/.../column/impl/ColumnReaderBase.java:730-735) ->
+ * DeltaByteArrayReader.setPreviousReader (.../values/deltastrings/DeltaByteArrayReader.java:89-95),
+ * applied when CorruptDeltaByteArrays.requiresSequentialReads(created_by, DELTA_BYTE_ARRAY)
+ * (parquet-column/src/main/java/org/apache/parquet/CorruptDeltaByteArrays.java:31-84) holds: the caller
+ * sets the flag on every DELTA_BYTE_ARRAY page of such a column chunk except its first page. The
+ * previous page of the column in the batch must be a DELTA_BYTE_ARRAY page (the reference casts its
+ * reader to DeltaByteArrayReader), otherwise PQG_ERR_UNSUPPORTED. Flagged pages are decoded in page
+ * order, one column at a time. */
+#define PQG_PAGE_DBA_CARRY 1
 
 /*
  * One column chunk: the ColumnDescriptor facts the decoder needs (physical

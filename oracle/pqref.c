@@ -370,6 +370,11 @@ typedef struct {
   jdict dict;
   int dict_err;
   int dict_checked;
+  /* the previous page's data reader (ColumnReaderBase.initDataReader :702, previousReader): its kind and,
+   * for DELTA_BYTE_ARRAY, its `previous` value (PARQUET-246 carry-over, PQG_PAGE_DBA_CARRY) */
+  int last_kind;            /* 0: no page yet */
+  uint8_t* dba_prev;
+  int64_t dba_prev_len;
 } colstate;
 
 static int emit_fixed(colstate* cs, const uint8_t* src) {
@@ -560,9 +565,9 @@ static int vreader_init(vreader* r, const pqg_page_desc* pg, colstate* cs, jstre
     return PQG_OK;
   }
   if (enc == PQG_DELTA_BYTE_ARRAY) {
-    /* Encoding.java :219-222 allows FIXED_LEN_BYTE_ARRAY too; the FLBA output here is fixed width,
-     * so a decoded value of another length is reported (DeltaByteArray on FLBA: next row) */
-    if (t != PQG_BYTE_ARRAY) return PQG_ERR_UNSUPPORTED;
+    /* Encoding.java :219-222: BYTE_ARRAY and FIXED_LEN_BYTE_ARRAY; the FLBA output here is fixed
+     * width, so a decoded value of another length is reported as PQG_ERR_CORRUPT (vreader_read) */
+    if (t != PQG_BYTE_ARRAY && !(t == PQG_FIXED_LEN_BYTE_ARRAY && c->type_length > 0)) return PQG_ERR_UNSUPPORTED;
     /* DeltaByteArrayReader.initFromPage :45-48: prefix lengths, then the suffixes' DLBA reader */
     r->kind = VR_DBA;
     int e = delta_init(&r->prefix, s);
@@ -570,8 +575,18 @@ static int vreader_init(vreader* r, const pqg_page_desc* pg, colstate* cs, jstre
     if ((e = delta_init(&r->delta, s))) return e;
     r->in = *s;
     s->pos = s->end;
-    r->prev = NULL;     /* previous = empty (:41); PARQUET-246 carry-over is not applied (:89-94) */
+    r->prev = NULL;     /* previous = empty (:41) */
     r->prev_len = 0;
+    if (pg->flags & PQG_PAGE_DBA_CARRY) {
+      /* ColumnReaderBase.initDataReader :730-735 -> setPreviousReader :89-95 (PARQUET-246): previous =
+       * the previous page reader's previous; that reader must be a DeltaByteArrayReader (cast) */
+      if (cs->last_kind && cs->last_kind != VR_DBA) return PQG_ERR_UNSUPPORTED;
+      if (cs->last_kind && cs->dba_prev_len > 0) {
+        r->prev = (uint8_t*)malloc((size_t)cs->dba_prev_len);
+        memcpy(r->prev, cs->dba_prev, (size_t)cs->dba_prev_len);
+        r->prev_len = cs->dba_prev_len;
+      }
+    }
     return PQG_OK;
   }
   if (enc == PQG_BYTE_STREAM_SPLIT) {
@@ -701,6 +716,10 @@ static int vreader_read(vreader* r, colstate* cs) {
         free(r->prev);
         r->prev = out;
         r->prev_len = slen;
+      }
+      if (c->physical_type == PQG_FIXED_LEN_BYTE_ARRAY) {
+        if (r->prev_len != c->type_length) return PQG_ERR_CORRUPT;  /* no room in the fixed-width output */
+        return emit_fixed(cs, r->prev);
       }
       return emit_binary(cs, r->prev, (int32_t)r->prev_len);
     }
@@ -883,11 +902,19 @@ int pqr_decode(const uint8_t* bytes, uint64_t n_bytes, pqg_column_desc* cols, in
       }
     }
     if (page_value_counts) page_value_counts[p] = (uint32_t)(C->n_values - before);
+    C->last_kind = vr.kind;
+    if (vr.kind == VR_DBA) {  /* keep `previous` for the next page's setPreviousReader */
+      free(C->dba_prev);
+      C->dba_prev = vr.prev;
+      C->dba_prev_len = vr.prev_len;
+      vr.prev = NULL;
+    }
     vreader_free(&vr);
   }
   for (int i = 0; i < n_cols; i++) {
     cols[i].values_written = cs[i].n_values;
     dict_free(&cs[i].dict);
+    free(cs[i].dba_prev);
   }
   free(cs);
   return rc;

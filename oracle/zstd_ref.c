@@ -224,11 +224,11 @@ static int64_t huf_read_tree(HufTab* H, const uint8_t* p, int64_t n) {
       if (nsym >= 255) return -1;
       w[nsym++] = T.t[s1].sym;
       s1 = T.t[s1].base + bitb_read(&b, T.t[s1].nb);
-      if (b.bits < 0) { w[nsym++] = T.t[s2].sym; break; }
+      if (b.bits < 0) { if (nsym >= 255) return -1; w[nsym++] = T.t[s2].sym; break; }
       if (nsym >= 255) return -1;
       w[nsym++] = T.t[s2].sym;
       s2 = T.t[s2].base + bitb_read(&b, T.t[s2].nb);
-      if (b.bits < 0) { w[nsym++] = T.t[s1].sym; break; }
+      if (b.bits < 0) { if (nsym >= 255) return -1; w[nsym++] = T.t[s1].sym; break; }
     }
     used = 1 + cs;
   }

@@ -130,8 +130,8 @@ struct pqg_plan {
   // bin_total), dictionary walks, post-passes, offset-scan blocks, copy chunks
   DevBuf bscratch, bin_lists, bin_blocks, bin_chunks, dba_chunks;
   uint64_t blen_bytes = 0;            // leading part of bscratch cleared before every launch
-  int n_dict_walk = 0, n_bind = 0, n_fixd = 0, n_bin_cols = 0;
-  int off_dict_walk = 0, off_bind = 0, off_fixd = 0, off_bin_cols = 0;  // into bin_lists
+  int n_dict_walk = 0, n_bind = 0, n_fixd = 0, n_bin_cols = 0, n_carry = 0;
+  int off_dict_walk = 0, off_bind = 0, off_fixd = 0, off_bin_cols = 0, off_carry = 0;  // into bin_lists
   uint32_t n_bin_blocks = 0, n_bin_chunks = 0, n_dba_chunks = 0;
   uint64_t dba_meta_off = ~0ull;  // DELTA_BYTE_ARRAY per-chunk {suffix base, smallest prefix} in bscratch
   uint32_t* dba_meta() const {
@@ -309,6 +309,10 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
   std::vector<int> lvl_list;
   std::vector<std::vector<int>> col_pages((size_t)std::max(n_cols, 1));
   std::vector<uint64_t> slot_acc((size_t)std::max(n_cols, 1), 0), val_acc((size_t)std::max(n_cols, 1), 0);
+  // per column: class of its previous page (-2: none yet; PQG_PAGE_DBA_CARRY needs a DELTA_BYTE_ARRAY
+  // one), FIXED_LEN_BYTE_ARRAY with DELTA_BYTE_ARRAY pages, any carry page
+  std::vector<int> col_last_cls((size_t)std::max(n_cols, 1), -2);
+  std::vector<uint8_t> dba_fixed((size_t)std::max(n_cols, 1), 0), dba_carry((size_t)std::max(n_cols, 1), 0);
   for (int p = 0; p < n_pages; p++) {
     const pqg_page_desc& g = pages[p];
     PageWork& w = P->h_work[(size_t)p];
@@ -333,6 +337,7 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     w.dl_encoding = g.dl_encoding;
     w.rl_len = g.rl_byte_length;
     w.dl_len = g.dl_byte_length;
+    w.pflags = g.flags;
     w.slot_offset = slot_acc[(size_t)ci];
     slot_acc[(size_t)ci] += g.num_values;
     const bool nullable = P->col_nullable[(size_t)ci] != 0;
@@ -357,6 +362,8 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
       lvl_list.push_back(p);
       col_pages[(size_t)ci].push_back(p);
     }
+    const int last_cls = col_last_cls[(size_t)ci];
+    col_last_cls[(size_t)ci] = -1;
     if (col_err[(size_t)ci]) continue;  // dictionary page unusable: ColumnReaderBase ctor threw
     // value class (Encoding.getValuesReader / getDictionaryBasedValuesReader dispatch)
     const int t = c.physical_type;
@@ -408,10 +415,20 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
           herr = PQG_ERR_UNSUPPORTED;      // Encoding.java :130-143
         break;
       case PQG_DELTA_BYTE_ARRAY:
-        // Encoding.java :219-222 also allows FIXED_LEN_BYTE_ARRAY; its fixed-width output form has
-        // no room for the variable lengths the reader may return (next row)
-        if (t == PQG_BYTE_ARRAY) { cls = C_DBA; w.bin_kind = pqg::BIN_DBA; }
-        else herr = PQG_ERR_UNSUPPORTED;
+        // Encoding.java :219-222: BYTE_ARRAY and FIXED_LEN_BYTE_ARRAY (whose values must then be
+        // type_length bytes each: k_delta reports any other length as PQG_ERR_CORRUPT)
+        if (t == PQG_BYTE_ARRAY || (t == PQG_FIXED_LEN_BYTE_ARRAY && ew > 0)) {
+          cls = C_DBA;
+          w.bin_kind = pqg::BIN_DBA;
+          if (t == PQG_FIXED_LEN_BYTE_ARRAY) dba_fixed[(size_t)ci] = 1;
+          if (g.flags & PQG_PAGE_DBA_CARRY) {
+            // setPreviousReader casts the previous page's reader to DeltaByteArrayReader
+            if (last_cls != -2 && last_cls != C_DBA) { cls = -1; herr = PQG_ERR_UNSUPPORTED; }
+            else dba_carry[(size_t)ci] = 1;
+          }
+        } else {
+          herr = PQG_ERR_UNSUPPORTED;
+        }
         break;
       default:
         herr = PQG_ERR_UNSUPPORTED;
@@ -421,13 +438,14 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
       continue;
     }
     P->page_cls[(size_t)p] = cls;
+    col_last_cls[(size_t)ci] = cls;
     cls_lists[(size_t)cls].push_back(p);
   }
   for (int i = 0; i < n_cols; i++) P->col_required_values[(size_t)i] = val_acc[(size_t)i];
   P->col_first_page = col_first_page;
   // ---- BYTE_ARRAY and fixed-width dictionary columns: scratch layout, dictionary walks,
   // post-passes, offset-scan blocks and copy chunks
-  std::vector<int32_t> dict_walk, bind, fixd, bin_cols;
+  std::vector<int32_t> dict_walk, bind, fixd, bin_cols, carry_cols;
   std::vector<uint64_t> bin_blocks, bin_chunks;
   std::vector<uint64_t> blen_off((size_t)std::max(n_cols, 1), ~0ull), bsrc_off = blen_off, dlen_off = blen_off,
       dsrc_off = blen_off, bsum_off = blen_off;
@@ -439,9 +457,14 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
   for (int p : cls_lists[C_IDS]) needs_ids[(size_t)P->h_work[(size_t)p].column] = 1;
   for (int i = 0; i < n_cols; i++) {  // blen first: the part cleared before every launch
     if (ids_mode(cols[i])) continue;  // ids go straight to the column's values
-    if (bin_out(cols[i]) || needs_ids[(size_t)i]) blen_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
+    if (bin_out(cols[i]) || needs_ids[(size_t)i] || dba_fixed[(size_t)i])
+      blen_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
   }
   P->blen_bytes = sc;
+  for (int i = 0; i < n_cols; i++) {
+    if (dba_fixed[(size_t)i]) bsrc_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));  // prefix lengths
+    if (dba_carry[(size_t)i]) carry_cols.push_back(i);
+  }
   for (int i = 0; i < n_cols; i++) {
     if (!bin_out(cols[i])) continue;
     bin_cols.push_back(i);
@@ -526,6 +549,7 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
   P->off_bind = (int)bl.size(); P->n_bind = (int)bind.size(); bl.insert(bl.end(), bind.begin(), bind.end());
   P->off_fixd = (int)bl.size(); P->n_fixd = (int)fixd.size(); bl.insert(bl.end(), fixd.begin(), fixd.end());
   P->off_bin_cols = (int)bl.size(); P->n_bin_cols = (int)bin_cols.size(); bl.insert(bl.end(), bin_cols.begin(), bin_cols.end());
+  P->off_carry = (int)bl.size(); P->n_carry = (int)carry_cols.size(); bl.insert(bl.end(), carry_cols.begin(), carry_cols.end());
   P->n_bin_blocks = (uint32_t)bin_blocks.size();
   P->n_bin_chunks = (uint32_t)bin_chunks.size();
   // ---- upload
@@ -567,6 +591,10 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
       d.block_sums = (uint64_t*)at(bsum_off[(size_t)i]);
       d.bin_total = (uint64_t*)at(P->bin_total_off[(size_t)i]);
       d.n_slots = slot_acc[(size_t)i];
+      if (dba_fixed[(size_t)i]) {  // DELTA_BYTE_ARRAY values go straight to the fixed-width output
+        d.binary_data = (uint8_t*)cols[i].values;
+        d.binary_capacity = slot_acc[(size_t)i] * (uint64_t)d.elem_width;
+      }
     }
   }
   if (!bl.empty())
@@ -594,7 +622,8 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
   P->kernels = (P->levels_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
   for (int k = 0; k < C_NCLS; k++) P->kernels += P->cls_n[(size_t)k] ? 1 : 0;
   P->kernels += (P->n_dict_walk ? 1 : 0) + (P->n_bind ? 1 : 0) + (P->n_fixd ? 1 : 0) + (P->n_bin_blocks ? 3 : 0) +
-                (P->n_bin_chunks ? 1 : 0) + (P->cls_n[C_DBA] ? (P->n_dba_chunks ? 4 : 1) : 0);
+                (P->n_bin_chunks ? 1 : 0) + (P->cls_n[C_DBA] ? (P->n_dba_chunks ? 4 : 1) : 0) +
+                (P->n_carry ? 1 : 0);
   *out = P;
   return PQG_OK;
 }
@@ -691,7 +720,8 @@ int pqg_plan_launch(pqg_plan* P) {
                              err, ecount);
   if (e == hipSuccess && P->cls_n[C_DBA])
     e = pqg::launch_dba_copy(s, P->d_bytes, P->n_bytes, work, cols, lists + P->cls_off[C_DBA], P->cls_n[C_DBA],
-                             (const uint64_t*)P->dba_chunks.p, P->n_dba_chunks, P->dba_meta());
+                             (const uint64_t*)P->dba_chunks.p, P->n_dba_chunks, P->dba_meta(), bl + P->off_carry,
+                             P->n_carry, err, ecount);
   ctx->last_launched = P;
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }

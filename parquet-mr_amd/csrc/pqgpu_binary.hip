@@ -625,13 +625,19 @@ struct DbaPar {
   uint8_t pse[WAVE];                   // previous value with a smaller prefix length (255: none)
 };
 
+// Output byte offset of column value v: BYTE_ARRAY from the offset scan; FIXED_LEN_BYTE_ARRAY
+// (every value type_length bytes, checked by k_delta) at v * type_length of `values`.
+__device__ __forceinline__ uint64_t dba_off(const ColumnDev& cd, uint64_t v) {
+  return cd.physical_type == PQG_FIXED_LEN_BYTE_ARRAY ? v * (uint64_t)(uint32_t)cd.type_length
+                                                      : (uint64_t)((const int64_t*)cd.values)[v];
+}
+
 // Values [i_beg, i_end) of a page, in order. The previous value is in vbuf[cur ^ 1] when
 // prev_lds; otherwise at output offset prev_off. sp: page-relative position of value i_beg's suffix.
 __device__ __forceinline__ void dba_values(const ColumnDev& cd, uint64_t v0, rsrc_t rs, uint32_t i_beg, uint32_t i_end,
                                            uint32_t sp, uint8_t (*vbuf)[DBA_VB], uint32_t* sbuf, uint32_t cur,
                                            bool prev_lds, uint64_t prev_off, DbaPar* par = nullptr) {
   const uint32_t lane = lane_id();
-  const int64_t* offs = (const int64_t*)cd.values + v0;
   uint8_t* dst = cd.binary_data;
   const uint64_t cap = cd.binary_capacity;
   const uint8_t* sb8 = (const uint8_t*)sbuf;
@@ -644,7 +650,7 @@ __device__ __forceinline__ void dba_values(const ColumnDev& cd, uint64_t v0, rsr
     const uint32_t S = L - P;
     uint32_t stot;
     const uint32_t sx = wave_excl_scan_u32(S, &stot);
-    const uint64_t off = in ? (uint64_t)offs[i] : 0;
+    const uint64_t off = in ? dba_off(cd, v0 + i) : 0;
     const bool staged = stot <= DBA_SB;
     if (staged) {
       for (uint32_t o = 4u * lane; o < stot; o += 4u * WAVE) sbuf[o >> 2] = ld4_any(rs, sp + o);
@@ -779,7 +785,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_copy(const uint8_t* __restrict
   const int page = wave_page(list, n_list);
   if (page < 0) return;
   const PageWork& pw = work[page];
-  if (!uni(pw.reserved)) return;
+  if (uni(pw.reserved) != 1u) return;
   const ColumnDev& cd = cols[pw.column];
   const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
   dba_values(cd, pw.out_offset, rs, 0, uni(pw.n_values), uni(pw.aux), vbuf_all[wave_id()], sbuf_all[wave_id()], 0,
@@ -851,8 +857,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_tail(const uint8_t* __restrict
   }
   const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
   const uint32_t sp = uni(pw.aux) + meta[2u * ((uint64_t)pw.chunk_base + j)];
-  const int64_t* offs = (const int64_t*)cd.values + v0;
-  const uint64_t o_last = (uint64_t)offs[i_lo + last];
+  const uint64_t o_last = dba_off(cd, v0 + i_lo + last);
   uint8_t* dst = cd.binary_data;
   const uint64_t cap = cd.binary_capacity;
   uint32_t R = after, sx = sx_lane;
@@ -891,7 +896,6 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chain(const PageWork* __restri
   const uint32_t nch = (nv + BIN_CHUNK - 1) / BIN_CHUNK;
   if (nch <= 1) return;
   const uint64_t v0 = pw.out_offset;
-  const int64_t* offs = (const int64_t*)cd.values + v0;
   uint8_t* dst = cd.binary_data;
   const uint64_t cap = cd.binary_capacity;
   uint8_t* T = tbuf_all[wave_id()];
@@ -899,7 +903,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chain(const PageWork* __restri
   // T_0 = chunk 0's last value (all own bytes: its first value has prefix 0)
   uint32_t tl = uni(cd.blen[v0 + BIN_CHUNK - 1]);
   {
-    const uint64_t o = (uint64_t)offs[BIN_CHUNK - 1];
+    const uint64_t o = dba_off(cd, v0 + BIN_CHUNK - 1);
     for (uint32_t b = lane; b < tl; b += WAVE) T[b] = o + b < cap ? dst[o + b] : 0;
   }
   wave_sync();
@@ -907,7 +911,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chain(const PageWork* __restri
     const uint32_t il = (c + 1) * BIN_CHUNK < nv ? (c + 1) * BIN_CHUNK - 1 : nv - 1;
     const uint32_t Ll = uni(cd.blen[v0 + il]);
     const uint32_t mc = uni(m[2u * c + 1u]);
-    const uint64_t o = (uint64_t)offs[il];
+    const uint64_t o = dba_off(cd, v0 + il);
     const uint32_t k = mc < Ll ? mc : Ll;  // inherited bytes (<= |T_{c-1}| for a valid page)
     // own bytes [k, Ll) were written by k_dba_tail (an earlier launch): load them first
     uint8_t own[DBA_VB / WAVE];
@@ -954,15 +958,75 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chunks(const uint8_t* __restri
   const uint64_t v0 = pw.out_offset;
   uint8_t(*vbuf)[DBA_VB] = vbuf_all[wave_id()];
   if (i_lo) {  // previous value -> vbuf[1]
-    const int64_t* offs = (const int64_t*)cd.values + v0;
     const uint32_t lp = uni(cd.blen[v0 + i_lo - 1]);
-    const uint64_t o = (uint64_t)offs[i_lo - 1];
+    const uint64_t o = dba_off(cd, v0 + i_lo - 1);
     for (uint32_t b = lane; b < lp; b += WAVE) vbuf[1][b] = o + b < cd.binary_capacity ? cd.binary_data[o + b] : 0;
     wave_sync();
   }
   const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
   const uint32_t sp = uni(pw.aux) + meta[2u * ((uint64_t)pw.chunk_base + j)];
   dba_values(cd, v0, rs, i_lo, i_hi, uni(sp), vbuf, sbuf_all[wave_id()], 0, true, 0, &par_all[wave_id()]);
+}
+
+// PQG_PAGE_DBA_CARRY pages (PARQUET-246): one wave per column walks the column's DELTA_BYTE_ARRAY
+// pages in page order. A flagged page starts from the column's previous value (value out_offset - 1,
+// DeltaByteArrayReader.setPreviousReader :89-95) unless no value was decoded since the last unflagged
+// page (the start of a column chunk), whose reader starts empty; its first value's prefix is checked
+// against that previous value here (readBytes :72-74: arraycopy past previous.length), then the page
+// is copied value after value (dba_values). Unflagged pages were copied by the launches before.
+__global__ __launch_bounds__(64) void k_dba_carry(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                  const PageWork* __restrict__ work,
+                                                  const ColumnDev* __restrict__ cols,
+                                                  const int32_t* __restrict__ list, int n_list,
+                                                  const int32_t* __restrict__ carry_cols, uint64_t* err,
+                                                  ErrCount err_count) {
+  __shared__ uint8_t vbuf[2][DBA_VB];
+  __shared__ uint32_t sbuf[DBA_SB / 4 + 1];
+  const int col = carry_cols[blockIdx.x];
+  const ColumnDev& cd = cols[col];
+  const uint32_t lane = lane_id();
+  uint8_t* dst = cd.binary_data;
+  const uint64_t cap = cd.binary_capacity;
+  uint64_t chain_start = 0;  // first value of the current column chunk
+  for (int k = 0; k < n_list; k++) {
+    const int page = list[k];
+    const PageWork& pw = work[page];
+    if (uni(pw.column) != col) continue;
+    const uint64_t v0 = pw.out_offset;
+    if (uni(pw.reserved) != 2u) {
+      chain_start = v0;
+      continue;
+    }
+    const uint32_t nv = uni(pw.n_values);
+    if (nv == 0) continue;
+    bool prev_lds = true;
+    uint64_t prev_off = 0;
+    const uint32_t lp = v0 > chain_start ? uni(cd.blen[v0 - 1]) : 0u;  // the previous value's length
+    {
+      const int32_t pre0 = (int32_t)uni(cd.bsrc[v0]);
+      const uint32_t L0 = uni(cd.blen[v0]);
+      if (L0 != 0 && pre0 > 0 && (uint32_t)pre0 > lp) {
+        if (lane == 0) report(err, err_count, page, 2, 0, PQG_ERR_CORRUPT);
+        return;  // the reference throws here: nothing after this value is read
+      }
+    }
+    if (lp > 0) {
+      const uint64_t o = dba_off(cd, v0 - 1);
+      __builtin_amdgcn_s_waitcnt(0);  // this wave's stores of the previous page, read back below
+      if (lp <= DBA_VB) {
+        for (uint32_t b = lane; b < lp; b += WAVE) {
+          const uint64_t a = o + b;
+          vbuf[1][b] = a < cap ? (uint8_t)((sld((const uint32_t*)(dst + (a & ~3ull))) >> ((a & 3u) * 8u)) & 0xFFu) : 0;
+        }
+        wave_sync();
+      } else {
+        prev_lds = false;
+        prev_off = o;
+      }
+    }
+    const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+    dba_values(cd, v0, rs, 0, nv, uni(pw.aux), vbuf, sbuf, 0, prev_lds, prev_off);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1011,7 +1075,8 @@ hipError_t launch_bin_scan(hipStream_t st, const ColumnDev* cols, const int32_t*
 
 hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, const uint64_t* chunks,
-                           uint32_t n_chunks, const uint32_t* dba_meta) {
+                           uint32_t n_chunks, const uint32_t* dba_meta, const int32_t* carry_cols, int n_carry_cols,
+                           uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
   if (n_chunks) {
     const dim3 gc((n_chunks + WPB - 1) / WPB);
@@ -1020,6 +1085,9 @@ hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
     hipLaunchKernelGGL(k_dba_chunks, gc, dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, chunks, n_chunks, dba_meta);
   }
   hipLaunchKernelGGL(k_dba_copy, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, list, n);
+  if (n_carry_cols > 0)
+    hipLaunchKernelGGL(k_dba_carry, dim3(n_carry_cols), dim3(64), 0, st, bytes, n_bytes, work, cols, list, n, carry_cols,
+                       err, err_count);
   return hipGetLastError();
 }
 

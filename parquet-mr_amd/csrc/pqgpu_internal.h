@@ -56,7 +56,9 @@ struct PageWork {
   uint32_t chunk_base;  // first output chunk of the page
   uint32_t aux;         // DELTA_LENGTH_BYTE_ARRAY: start of the value bytes (end of the length stream)
   uint32_t bin_kind;    // BYTE_ARRAY pages: BIN_PLAIN / BIN_DLBA / BIN_DICT (source of the value bytes)
-  uint32_t reserved;
+  uint32_t reserved;    // DELTA_BYTE_ARRAY (set by k_delta): 0 chunk-parallel copy, 1 serial copy, 2 carry chain
+  uint32_t pflags;      // pqg_page_desc.flags (PQG_PAGE_DBA_CARRY)
+  uint32_t pad0;
 };
 
 // Error counter handle passed to every kernel. Error words and the counter are tagged with the
@@ -122,10 +124,13 @@ hipError_t launch_dba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_b
                               const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count,
                               uint32_t* dba_meta);
 // DELTA_BYTE_ARRAY value bytes: chunk tails, per-page chain of chunk tails, chunk copies, serial
-// copy of the pages with long values
+// copy of the pages with long values, and (carry_cols: one wave per column) the PQG_PAGE_DBA_CARRY
+// pages of each column in page order. FIXED_LEN_BYTE_ARRAY columns write value i at i * type_length
+// of `values` (dba_off).
 hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, const uint64_t* chunks,
-                           uint32_t n_chunks, const uint32_t* dba_meta);
+                           uint32_t n_chunks, const uint32_t* dba_meta, const int32_t* carry_cols, int n_carry_cols,
+                           uint64_t* err, ErrCount err_count);
 // pqgpu_binary.hip
 constexpr uint32_t BIN_CHUNK = 256;     // values per k_bin_copy chunk
 constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block

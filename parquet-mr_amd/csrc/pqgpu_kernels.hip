@@ -2534,6 +2534,13 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
     uint32_t* sl = cd.blen + pw.out_offset;
     uint64_t s_carry = 0;
     uint32_t prev_len = 0;  // previous value of the page (empty before the first, :41)
+    // PQG_PAGE_DBA_CARRY (PARQUET-246, setPreviousReader :89-95): the first value's previous is the
+    // column's value out_offset - 1, known only after the earlier pages: its prefix check is made by
+    // k_dba_carry, which copies the page in page order
+    const bool carry = (uni(pw.pflags) & PQG_PAGE_DBA_CARRY) != 0;
+    // FIXED_LEN_BYTE_ARRAY (Encoding.java :219-222): every value must be type_length bytes to fit the
+    // fixed-width output
+    const int32_t fixw = cd.physical_type == PQG_FIXED_LEN_BYTE_ARRAY ? cd.type_length : 0;
     uint32_t first_bad = 0xFFFFFFFFu;
     // per BIN_CHUNK-value chunk of the page, for the chunk-parallel value copy (k_dba_tail /
     // k_dba_chain / k_dba_chunks): suffix bytes before the chunk, smallest prefix length in it
@@ -2571,7 +2578,8 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
       if (in) {
         if (suf < 0) c = PQG_ERR_CORRUPT;
         else if (s_carry + incl > avail) c = PQG_ERR_EOF;
-        else if (pre != 0 && (full < 0 || pre < 0 || (uint32_t)pre > prev)) c = PQG_ERR_CORRUPT;
+        else if (pre != 0 && (full < 0 || pre < 0 || ((uint32_t)pre > prev && !(carry && i == 0)))) c = PQG_ERR_CORRUPT;
+        else if (fixw && full != fixw) c = PQG_ERR_CORRUPT;
       }
       if (c) report(err, err_count, page, 2, i, c);
       const uint64_t bad = __ballot(c != 0);
@@ -2601,7 +2609,7 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
       gst(meta + 2u * j + 1u, 0u);
     }
     // a value longer than the LDS value buffers sends the page to the serial copy
-    if (lane == 0) work[page].reserved = lmax > DBA_VB ? 1u : 0u;
+    if (lane == 0) work[page].reserved = carry ? 2u : lmax > DBA_VB ? 1u : 0u;
     // values past an error or past the streams hold length 0 (blen was cleared before the launch)
   }
   if (past_end != 0xFFFFFFFFu && lane == 0) report(err, err_count, page, 2, past_end, PQG_ERR_DELTA_PAST_END);

@@ -306,22 +306,26 @@ __device__ int zhuf_tree(ZWaveLds& L, rsrc_t rs, uint32_t& q, uint32_t lim) {
     BackBits b;
     if (!b.init(rs, q + 1 + (uint32_t)hb, cs - (uint32_t)hb, L.win)) return -1;
     uint32_t s1 = b.read(lg), s2 = b.read(lg);
+    // at most 255 decoded weights (libzstd HUF_readStats: FSE output capacity hwSize - 1)
     for (;;) {
-      if (nsym >= 254) return -1;
+      if (nsym >= 255) return -1;
       uint32_t e = L.ll[s1];
       if (lane_id() == 0) L.wts[nsym] = (uint8_t)(e & 0xFFu);
       nsym++;
       s1 = (e >> 16) + b.read((int)((e >> 8) & 0xFFu));
       if (b.bits < 0) {
+        if (nsym >= 255) return -1;
         if (lane_id() == 0) L.wts[nsym] = (uint8_t)(L.ll[s2] & 0xFFu);
         nsym++;
         break;
       }
+      if (nsym >= 255) return -1;
       e = L.ll[s2];
       if (lane_id() == 0) L.wts[nsym] = (uint8_t)(e & 0xFFu);
       nsym++;
       s2 = (e >> 16) + b.read((int)((e >> 8) & 0xFFu));
       if (b.bits < 0) {
+        if (nsym >= 255) return -1;
         if (lane_id() == 0) L.wts[nsym] = (uint8_t)(L.ll[s1] & 0xFFu);
         nsym++;
         break;

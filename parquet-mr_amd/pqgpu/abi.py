@@ -46,6 +46,7 @@ ERR_DICT_ENCODING = 20
 ERR_CRC = 21
 
 COLUMN_DICTIONARY_IDS = 1  # pqg_column_desc.flags: values <- uint32 dictionary ids
+PAGE_DBA_CARRY = 1  # pqg_page_desc.flags: DELTA_BYTE_ARRAY page continues the previous page's value (PARQUET-246)
 
 ERROR_NAMES = {
     OK: "OK", ERR_INVALID_ARG: "INVALID_ARG", ERR_UNSUPPORTED: "UNSUPPORTED", ERR_HIP: "HIP",
@@ -70,14 +71,14 @@ class PageDesc(C.Structure):
         ("dl_encoding", C.c_int32),
         ("rl_byte_length", C.c_uint32),
         ("dl_byte_length", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("flags", C.c_uint32),
     ]
 
 
 PAGE_DTYPE = np.dtype([
     ("offset", "<u8"), ("size", "<u4"), ("num_values", "<u4"), ("column", "<i4"), ("version", "<i4"),
     ("encoding", "<i4"), ("rl_encoding", "<i4"), ("dl_encoding", "<i4"), ("rl_byte_length", "<u4"),
-    ("dl_byte_length", "<u4"), ("reserved", "<u4"),
+    ("dl_byte_length", "<u4"), ("flags", "<u4"),
 ])
 assert PAGE_DTYPE.itemsize == C.sizeof(PageDesc) == 48
 

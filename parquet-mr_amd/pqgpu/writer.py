@@ -166,11 +166,12 @@ def dlba_encode(values):
     return delta_encode(lens, abi.INT32) + b"".join(vals)
 
 
-def dba_encode(values):
+def dba_encode(values, previous=b""):
     """DeltaByteArrayWriter.writeBytes / getBytes (deltastrings/DeltaByteArrayWriter.java:56-58, 90-100):
     prefix lengths shared with the previous value (DELTA_BINARY_PACKED), then the suffixes as
-    DELTA_LENGTH_BYTE_ARRAY. `previous` starts empty on every page (reset :65-70)."""
-    if isinstance(values, BinaryValues) and len(values) > 1:
+    DELTA_LENGTH_BYTE_ARRAY. `previous` starts empty on every page (reset :65-70); a non-empty
+    `previous` writes the page as parquet-mr < 1.8 did (PARQUET-246: reset kept the last value)."""
+    if isinstance(values, BinaryValues) and len(values) > 1 and not previous:
         # vectorized: values padded into rows, prefix = first mismatch with the previous row
         lens = values.lengths()
         L = int(lens.max()) + 1
@@ -187,7 +188,7 @@ def dba_encode(values):
         sfx_lens = (lens - pre).astype(np.int64)
         sfx = BinaryValues(np.concatenate([[0], np.cumsum(sfx_lens)]), values.data[keep])
         return delta_encode(pre, abi.INT32) + dlba_encode(sfx)
-    prev = b""
+    prev = bytes(previous)
     prefixes, suffixes = [], []
     for b in values:
         b = bytes(b)
@@ -258,6 +259,9 @@ class ColumnChunk:
     values: Optional[object] = None
     def_levels: Optional[np.ndarray] = None
     rep_levels: Optional[np.ndarray] = None
+    # CorruptDeltaByteArrays.requiresSequentialReads(created_by, DELTA_BYTE_ARRAY): build_batch flags
+    # the chunk's DELTA_BYTE_ARRAY pages after its first page PQG_PAGE_DBA_CARRY
+    dba_carry: bool = False
 
     @property
     def num_slots(self):
@@ -304,8 +308,12 @@ def _page_bounds(n_slots, page_rows, rep_levels):
 
 def write_column_chunk(physical_type, values, encoding, *, def_levels=None, rep_levels=None, max_def=0,
                        max_rep=0, page_rows=20000, version=1, type_length=0, delta_block=128,
-                       delta_miniblocks=4, dict_page_encoding=abi.PLAIN, level_encoding=abi.RLE):
-    """Encode one column chunk. `values` are the non-null values (dense, in slot order)."""
+                       delta_miniblocks=4, dict_page_encoding=abi.PLAIN, level_encoding=abi.RLE,
+                       dba_carry=False):
+    """Encode one column chunk. `values` are the non-null values (dense, in slot order).
+    dba_carry: DELTA_BYTE_ARRAY pages written like parquet-mr < 1.8 (PARQUET-246: each page's first
+    value may share a prefix with the previous page's last value); the chunk is marked so that
+    build_batch flags its pages PQG_PAGE_DBA_CARRY."""
     values = values if physical_type == abi.BYTE_ARRAY or physical_type in (abi.INT96, abi.FIXED_LEN_BYTE_ARRAY) \
         else np.asarray(values)
     n_values = len(values)
@@ -319,7 +327,8 @@ def write_column_chunk(physical_type, values, encoding, *, def_levels=None, rep_
     nonnull = (dl == max_def)
     assert int(nonnull.sum()) == n_values, "def levels disagree with the value count"
     chunk = ColumnChunk(physical_type=physical_type, max_rep=max_rep, max_def=max_def, type_length=type_length,
-                        values=values, def_levels=dl if max_def else None, rep_levels=rl if max_rep else None)
+                        values=values, def_levels=dl if max_def else None, rep_levels=rl if max_rep else None,
+                        dba_carry=dba_carry)
     ids = None
     if encoding in (abi.RLE_DICTIONARY, abi.PLAIN_DICTIONARY):
         if physical_type == abi.BYTE_ARRAY:
@@ -350,7 +359,7 @@ def write_column_chunk(physical_type, values, encoding, *, def_levels=None, rep_
         elif encoding == abi.DELTA_LENGTH_BYTE_ARRAY:
             data = dlba_encode(values[v0:v1])
         elif encoding == abi.DELTA_BYTE_ARRAY:
-            data = dba_encode(values[v0:v1])
+            data = dba_encode(values[v0:v1], bytes(values[v0 - 1]) if dba_carry and v0 > 0 else b"")
         elif encoding == abi.BYTE_STREAM_SPLIT:
             data = bss_encode(values[v0:v1], physical_type, type_length)
         elif encoding == abi.RLE and physical_type == abi.BOOLEAN:
@@ -462,10 +471,12 @@ def build_batch(chunks, align=ALIGN):
         elif ch.dict_page is not None:
             raise ValueError("a pqg_column_desc has one dictionary: decode row groups with separate "
                              "dictionaries as separate columns (one per row group)")
-        for pg in ch.pages:
+        for k, pg in enumerate(ch.pages):
             off = place(pg.body)
+            carry = abi.PAGE_DBA_CARRY if (getattr(ch, "dba_carry", False) and k > 0 and
+                                           pg.encoding == abi.DELTA_BYTE_ARRAY) else 0
             page_rows.append((off, len(pg.body), pg.num_values, oc, pg.version, pg.encoding, pg.rl_encoding,
-                              pg.dl_encoding, pg.rl_byte_length, pg.dl_byte_length, 0))
+                              pg.dl_encoding, pg.rl_byte_length, pg.dl_byte_length, carry))
             slot_off.append(col_slots[oc])
             col_slots[oc] += pg.num_values
         col_vals[oc] += len(ch.values) if ch.values is not None else getattr(ch, "n_values_hint", 0)
