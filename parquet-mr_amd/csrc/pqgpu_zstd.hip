@@ -29,6 +29,7 @@ constexpr uint32_t ZS_LIT_MAX = 131072;
 
 struct ZWaveLds {
   uint32_t ll[512], ml[512], of[256];  // FSE decoding entries: sym | nb << 8 | base << 16
+  uint32_t hw[64];                     // FSE table of compressed Huffman weights (accuracy <= 6)
   uint16_t huf[2048];                  // Huffman decoding entries: sym | nb << 8
   uint8_t ring[ZS_RING];
   uint8_t win[ZS_WIN + 16];
@@ -302,31 +303,32 @@ __device__ int zhuf_tree(ZWaveLds& L, rsrc_t rs, uint32_t& q, uint32_t lim) {
     int ns, lg;
     const int64_t hb = zread_ncount(rs, q + 1, q + 1 + cs, 6, 255, L.norm, &ns, &lg);
     if (hb < 0) return -1;
-    if (!zfse_build(L, L.ll, ns, lg)) return -1;  // L.ll as scratch: the sequence tables are read later
+    // its own table: a later block may repeat the sequence tables (LL / OF / ML mode 3)
+    if (!zfse_build(L, L.hw, ns, lg)) return -1;
     BackBits b;
     if (!b.init(rs, q + 1 + (uint32_t)hb, cs - (uint32_t)hb, L.win)) return -1;
     uint32_t s1 = b.read(lg), s2 = b.read(lg);
     // at most 255 decoded weights (libzstd HUF_readStats: FSE output capacity hwSize - 1)
     for (;;) {
       if (nsym >= 255) return -1;
-      uint32_t e = L.ll[s1];
+      uint32_t e = L.hw[s1];
       if (lane_id() == 0) L.wts[nsym] = (uint8_t)(e & 0xFFu);
       nsym++;
       s1 = (e >> 16) + b.read((int)((e >> 8) & 0xFFu));
       if (b.bits < 0) {
         if (nsym >= 255) return -1;
-        if (lane_id() == 0) L.wts[nsym] = (uint8_t)(L.ll[s2] & 0xFFu);
+        if (lane_id() == 0) L.wts[nsym] = (uint8_t)(L.hw[s2] & 0xFFu);
         nsym++;
         break;
       }
       if (nsym >= 255) return -1;
-      e = L.ll[s2];
+      e = L.hw[s2];
       if (lane_id() == 0) L.wts[nsym] = (uint8_t)(e & 0xFFu);
       nsym++;
       s2 = (e >> 16) + b.read((int)((e >> 8) & 0xFFu));
       if (b.bits < 0) {
         if (nsym >= 255) return -1;
-        if (lane_id() == 0) L.wts[nsym] = (uint8_t)(L.ll[s1] & 0xFFu);
+        if (lane_id() == 0) L.wts[nsym] = (uint8_t)(L.hw[s1] & 0xFFu);
         nsym++;
         break;
       }
