@@ -289,6 +289,35 @@ typedef struct pqg_assembly_node {
 int pqg_assemble(pqg_ctx* ctx, const uint8_t* d_def_levels, const uint8_t* d_rep_levels, uint64_t n_slots,
                  pqg_assembly_node* path, int depth, uint64_t* n_records, pqg_status* st);
 
+/* Record assembly of every leaf of a schema: the columnar form of what the automaton emits when it
+ * interleaves all leaves of each record (RecordReaderImplementation ctor :253-330 builds the
+ * transitions between leaves — nextColumnIdxForRepLevel, levelToClose — and read() :409-446 walks
+ * them). `nodes` is the schema below the message root in depth-first order, each naming its parent
+ * (-1: a child of the root); `leaves` gives the levels pqg_decode wrote for each leaf node. Every
+ * node's outputs (validity / offsets, as in pqg_assembly_node) come from the first leaf under it in
+ * schema order; the other leaves under a node must agree on its entry count, and all leaves on the
+ * record count, or the call fails with PQG_ERR_CORRUPT (st->page = the leaf, st->value_index = the
+ * node). Synchronous. */
+typedef struct pqg_schema_node {
+  int32_t parent;          /* index of the parent node (< this index), -1 for a child of the root */
+  int32_t repetition;      /* pqg_repetition */
+  uint8_t* validity;       /* OPTIONAL: 1 byte per entry; may be NULL */
+  int64_t* offsets;        /* REPEATED: offsets[n_enclosing_entries + 1]; may be NULL */
+  uint64_t capacity;       /* elements the validity / offsets array holds */
+  uint64_t n_entries;      /* OUT: entries of this node */
+} pqg_schema_node;
+
+typedef struct pqg_schema_leaf {
+  int32_t node;            /* index of the leaf in `nodes` */
+  int32_t reserved;
+  const uint8_t* d_def_levels;  /* device, NULL when the leaf's max definition level is 0 */
+  const uint8_t* d_rep_levels;  /* device, NULL when the leaf's max repetition level is 0 */
+  uint64_t n_slots;
+} pqg_schema_leaf;
+
+int pqg_assemble_schema(pqg_ctx* ctx, pqg_schema_node* nodes, int n_nodes, const pqg_schema_leaf* leaves, int n_leaves,
+                        uint64_t* n_records, pqg_status* st);
+
 /* ---- page decompression (codec SNAPPY) --------------------------------------
  * Replaces the decompression step between the page reader and the value readers:
  * ColumnChunkPageReadStore.readPage (parquet-hadoop/src/main/java/org/apache/parquet/hadoop/ColumnChunkPageReadStore.java:144-172

@@ -1237,6 +1237,79 @@ int pqg_assemble(pqg_ctx* ctx, const uint8_t* d_def_levels, const uint8_t* d_rep
   return PQG_OK;
 }
 
+int pqg_assemble_schema(pqg_ctx* ctx, pqg_schema_node* nodes, int n_nodes, const pqg_schema_leaf* leaves, int n_leaves,
+                        uint64_t* n_records, pqg_status* st) {
+  if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
+  if (!ctx || !nodes || n_nodes <= 0 || (n_leaves > 0 && !leaves) || n_leaves < 0) {
+    set_status(st, PQG_ERR_INVALID_ARG, -1, -1, "schema assembly arguments");
+    return PQG_ERR_INVALID_ARG;
+  }
+  for (int k = 0; k < n_nodes; k++)
+    if (nodes[k].parent >= k || nodes[k].parent < -1) {
+      set_status(st, PQG_ERR_INVALID_ARG, -1, k, "schema node parent");
+      return PQG_ERR_INVALID_ARG;
+    }
+  std::vector<int> owner((size_t)n_nodes, -1);  // leaf whose pass wrote the node's outputs
+  uint64_t records = 0;
+  for (int li = 0; li < n_leaves; li++) {
+    const pqg_schema_leaf& lf = leaves[li];
+    if (lf.node < 0 || lf.node >= n_nodes) {
+      set_status(st, PQG_ERR_INVALID_ARG, li, -1, "schema leaf node");
+      return PQG_ERR_INVALID_ARG;
+    }
+    for (int k = 0; k < n_nodes; k++)
+      if (nodes[k].parent == lf.node) {
+        set_status(st, PQG_ERR_INVALID_ARG, li, k, "schema leaf has children");
+        return PQG_ERR_INVALID_ARG;
+      }
+    // the leaf's path: root's child .. leaf
+    std::vector<int> chain;
+    for (int k = lf.node; k >= 0; k = nodes[k].parent) chain.push_back(k);
+    std::reverse(chain.begin(), chain.end());
+    if (chain.size() > pqg::ASM_MAX_NODES) {
+      set_status(st, PQG_ERR_UNSUPPORTED, li, -1, "schema assembly: path too deep");
+      return PQG_ERR_UNSUPPORTED;
+    }
+    std::vector<pqg_assembly_node> path(chain.size());
+    for (size_t q = 0; q < chain.size(); q++) {
+      const pqg_schema_node& n = nodes[chain[q]];
+      pqg_assembly_node& a = path[q];
+      std::memset(&a, 0, sizeof(a));
+      a.repetition = n.repetition;
+      if (owner[(size_t)chain[q]] < 0) {  // first leaf under this node: it writes the outputs
+        a.validity = n.validity;
+        a.offsets = n.offsets;
+        a.capacity = n.capacity;
+      }
+    }
+    uint64_t nrec = 0;
+    const int rc = pqg_assemble(ctx, lf.d_def_levels, lf.d_rep_levels, lf.n_slots, path.data(), (int)path.size(), &nrec, st);
+    if (rc) {
+      if (st) st->page = li;
+      if (st && rc == PQG_ERR_INVALID_ARG && st->value_index >= 0 && st->value_index < (int64_t)chain.size())
+        st->value_index = chain[(size_t)st->value_index];  // path position -> node index
+      return rc;
+    }
+    if (li > 0 && nrec != records) {
+      set_status(st, PQG_ERR_CORRUPT, li, -1, "schema assembly: leaves disagree on the record count");
+      return PQG_ERR_CORRUPT;
+    }
+    records = nrec;
+    for (size_t q = 0; q < chain.size(); q++) {
+      const int k = chain[q];
+      if (owner[(size_t)k] < 0) {
+        owner[(size_t)k] = li;
+        nodes[k].n_entries = path[q].n_entries;
+      } else if (nodes[k].n_entries != path[q].n_entries) {
+        set_status(st, PQG_ERR_CORRUPT, li, k, "schema assembly: leaves disagree on a node's entries");
+        return PQG_ERR_CORRUPT;
+      }
+    }
+  }
+  if (n_records) *n_records = records;
+  return PQG_OK;
+}
+
 int pqg_unpack_runs(pqg_ctx* ctx, int bit_width, const uint8_t* d_in, const uint64_t* d_in_offsets,
                     const uint32_t* d_counts, const uint64_t* d_out_offsets, int32_t* d_out, int n_runs) {
   if (!ctx || bit_width < 0 || bit_width > 32 || n_runs < 0) return PQG_ERR_INVALID_ARG;

@@ -1128,6 +1128,9 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       auto sweep = [&](auto fast_tag) {
         constexpr bool FAST = decltype(fast_tag)::value;
         auto value = [&](uint32_t ci, uint32_t i, const u32x4& q) -> T {
+#ifdef PQG_XT_NOVALUE  // A/B diagnostic: the sweep's loop and stores without the value computation
+          return (T)i;
+#endif
           if (!(q.y & 0x80000000u)) return (T)(((uint64_t)q.w << 32) | q.z);
           const uint64_t bit = (uint64_t)(i - q.x) * (uint32_t)w;
           const uint32_t byte = (q.y & 0x7FFFFFFFu) + (uint32_t)(bit >> 3);

@@ -136,6 +136,29 @@ class Status(C.Structure):
 REQUIRED, OPTIONAL, REPEATED = 0, 1, 2
 
 
+class SchemaNode(C.Structure):
+    """pqg_schema_node."""
+    _fields_ = [
+        ("parent", C.c_int32),
+        ("repetition", C.c_int32),
+        ("validity", C.c_void_p),
+        ("offsets", C.c_void_p),
+        ("capacity", C.c_uint64),
+        ("n_entries", C.c_uint64),
+    ]
+
+
+class SchemaLeaf(C.Structure):
+    """pqg_schema_leaf."""
+    _fields_ = [
+        ("node", C.c_int32),
+        ("reserved", C.c_int32),
+        ("d_def_levels", C.c_void_p),
+        ("d_rep_levels", C.c_void_p),
+        ("n_slots", C.c_uint64),
+    ]
+
+
 class AssemblyNode(C.Structure):
     """pqg_assembly_node."""
     _fields_ = [

@@ -493,6 +493,58 @@ class Decoder:
             out.append({"validity": v[:counts[k]] if v is not None else None, "offsets": o, "n_entries": counts[k]})
         return {"records": int(n_rec.value), "nodes": out}
 
+    def assemble_schema(self, nodes, leaves):
+        """Record assembly of every leaf of a schema (pqg_assemble_schema). nodes: [(parent index or
+        -1, repetition)] in depth-first order; leaves: [(node index, def tensor|None, rep tensor|None,
+        n_slots)] in schema order. Returns {"records": n, "nodes": [{"validity", "offsets",
+        "n_entries"}]} (device tensors; a node's outputs come from the first leaf under it)."""
+        arr = (abi.SchemaNode * len(nodes))()
+        first_slots = [None] * len(nodes)
+        for node, _, _, n in leaves:  # capacity bound: slots of the first leaf under the node (+ 1)
+            k = node
+            while k >= 0:
+                if first_slots[k] is None:
+                    first_slots[k] = n
+                k = nodes[k][0]
+        keep = []
+        for k, (parent, rp) in enumerate(nodes):
+            arr[k].parent, arr[k].repetition = parent, rp
+            cap = (first_slots[k] or 0) + 1
+            v = o = None
+            if rp == abi.OPTIONAL:
+                v = torch.empty(cap, dtype=torch.uint8, device=self.device)
+                arr[k].validity = v.data_ptr()
+            elif rp == abi.REPEATED:
+                o = torch.empty(cap, dtype=torch.int64, device=self.device)
+                arr[k].offsets = o.data_ptr()
+            arr[k].capacity = cap
+            keep.append((v, o))
+        lv = (abi.SchemaLeaf * max(1, len(leaves)))()
+        for i, (node, dl, rl, n) in enumerate(leaves):
+            lv[i].node = node
+            lv[i].d_def_levels = dl.data_ptr() if dl is not None else None
+            lv[i].d_rep_levels = rl.data_ptr() if rl is not None else None
+            lv[i].n_slots = n
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        n_rec = C.c_uint64(0)
+        st = abi.Status()
+        rc = native.lib().pqg_assemble_schema(self.ctx, C.addressof(arr), len(nodes), C.addressof(lv), len(leaves),
+                                              C.byref(n_rec), C.byref(st))
+        native.check(rc, st, "pqg_assemble_schema")
+        out = []
+        for k, (parent, rp) in enumerate(nodes):
+            v, o = keep[k]
+            cnt = int(arr[k].n_entries)
+            enc = None
+            if o is not None:  # offsets: one per entry of the enclosing repeated node (or record) + 1
+                q = parent
+                while q >= 0 and nodes[q][1] != abi.REPEATED:
+                    q = nodes[q][0]
+                enc = int(n_rec.value) if q < 0 else int(arr[q].n_entries)
+            out.append({"validity": v[:cnt] if v is not None else None,
+                        "offsets": o[:enc + 1] if o is not None else None, "n_entries": cnt})
+        return {"records": int(n_rec.value), "nodes": out}
+
     # -- ParquetReadRouter ---------------------------------------------------------
     def router_read(self, bit_width, data, count):
         """ParquetReadRouter.read(bitWidth, in, currentCount, int[]) on the GPU."""
