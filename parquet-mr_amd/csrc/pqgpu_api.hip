@@ -125,7 +125,7 @@ struct pqg_plan {
   bool dict_fused = true;
   uint32_t chunk_off[N_DICT_CLS] = {0, 0, 0}, chunk_n[N_DICT_CLS] = {0, 0, 0};  // ranges in `chunks`
   // fused dictionary kernel: persistent walker / tile workgroup counts (0: one page / 4 chunks per WG)
-  uint32_t dict_walk_wg = 0, dict_tile_wg = 0;
+  uint32_t dict_walk_wg = 0, dict_tile_wg = 0, dict_walk_pg = 0;
   // BYTE_ARRAY / fixed-width-dictionary scratch (ColumnDev::blen, bsrc, dict_len, dict_src, block_sums,
   // bin_total), dictionary walks, post-passes, offset-scan blocks, copy chunks
   DevBuf bscratch, bin_lists, bin_blocks, bin_chunks, dba_chunks;
@@ -578,6 +578,8 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     // persistent walker / tile workgroups of the fused kernel (A/B knobs; 0 = one unit per WG)
     if (const char* w = getenv("PQG_DICT_WALK_WG")) P->dict_walk_wg = (uint32_t)std::max(0, atoi(w));
     if (const char* t = getenv("PQG_DICT_TILE_WG")) P->dict_tile_wg = (uint32_t)std::max(0, atoi(t));
+    // dictionary walk: one workgroup per page (dict_page_wg, 1) or one wave per page (0)
+    if (const char* g = getenv("PQG_DICT_WALK_PG")) P->dict_walk_pg = (uint32_t)std::max(0, atoi(g));
   }
   {
     uint8_t* scb = (uint8_t*)P->bscratch.p;
@@ -682,7 +684,7 @@ int pqg_plan_launch(pqg_plan* P) {
         e = pqg::launch_dict(k == C_DICT8 ? 8 : 4, s, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
                              (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->chunk_off[i], P->chunk_n[i],
                              (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused,
-                             P->dict_walk_wg, P->dict_tile_wg, err, ecount);
+                             P->dict_walk_wg, P->dict_tile_wg, P->dict_walk_pg, err, ecount);
         break;
       }
       case C_IDS: {
@@ -690,7 +692,7 @@ int pqg_plan_launch(pqg_plan* P) {
         e = pqg::launch_dict_ids(s, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
                                  (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->chunk_off[i],
                                  P->chunk_n[i], (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused,
-                                 P->dict_walk_wg, P->dict_tile_wg, err, ecount);
+                                 P->dict_walk_wg, P->dict_tile_wg, P->dict_walk_pg, err, ecount);
         break;
       }
       case C_BSS: e = pqg::launch_bss(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;

@@ -28,6 +28,8 @@ __device__ __forceinline__ int wave_page(const int32_t* list, int n_list) {
 // Diagnostic build only (libpqgpu_diag.so, tools/diag_timeline.py): per-wave
 // stamps. Never compiled into the product library.
 static __device__ uint64_t* pqg_diag_buf;
+static __device__ uint64_t* pqg_diag_wrt;  // per page: s_memrealtime at walk start / publish
+static __device__ uint64_t* pqg_diag_xrt;  // per chunk: start, flag seen, end, (page | cu << 32)
 #define DIAG_T(v) uint64_t v = __builtin_amdgcn_s_memtime()
 #define DIAG_ADD(acc, t0) acc += __builtin_amdgcn_s_memtime() - (t0)
 #else

@@ -91,7 +91,8 @@ constexpr int DICT_WPB = 4;  // pages (walkers) / chunks (tiles) per workgroup o
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                        const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                       bool fused, uint32_t walk_wg, uint32_t tile_wg, uint64_t* err, ErrCount err_count);
+                       bool fused, uint32_t walk_wg, uint32_t tile_wg, uint32_t walk_pg, uint64_t* err,
+                       ErrCount err_count);
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                          const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_scan(hipStream_t st, PageWork* work, const int32_t* col_pages, const int32_t* col_page_start,
@@ -105,7 +106,8 @@ hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_
 hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                            const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
-                           uint32_t epoch, bool fused, uint32_t walk_wg, uint32_t tile_wg, uint64_t* err, ErrCount err_count);
+                           uint32_t epoch, bool fused, uint32_t walk_wg, uint32_t tile_wg, uint32_t walk_pg,
+                           uint64_t* err, ErrCount err_count);
 // DELTA_LENGTH_BYTE_ARRAY lengths (k_delta into blen, records PageWork::aux)
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count);

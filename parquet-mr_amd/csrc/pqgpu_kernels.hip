@@ -55,7 +55,10 @@ struct PreWin {
   uint32_t flg;        // byte b: bit0 packed, bit1 slow path, bits 2..4 header length
 };
 
-constexpr uint32_t SEG_BYTES = 3072;   // LDS page segment per wave of k_dict_runs (5 workgroups per CU)
+#ifndef PQG_SEG_BYTES
+#define PQG_SEG_BYTES 3072
+#endif
+constexpr uint32_t SEG_BYTES = PQG_SEG_BYTES;   // LDS page segment per wave of k_dict_runs (5 workgroups per CU)
 
 
 // Fill the wave's LDS segment with page bytes [lo, lo + SEG_BYTES) (lo 16-aligned).
@@ -585,6 +588,12 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
 #ifndef PQG_HANDOFF
 #define PQG_HANDOFF 0
 #endif
+#ifndef PQG_WALK_CHAIN
+#define PQG_WALK_CHAIN 1
+#endif
+#ifndef PQG_WALK_PRIO
+#define PQG_WALK_PRIO 0
+#endif
 __device__ __forceinline__ void handoff_release() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a compiler barrier too (invisible to the waitcnt pass)
 }
@@ -612,11 +621,13 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
   const uint32_t lane = lane_id();
   // successor table (256 x u16) and reached flags (256 x u8) over L.ent; every access goes
   // through may_alias types (u16 gathers vs u64 row writes must not be reordered)
+#if !PQG_WALK_CHAIN
   typedef uint16_t __attribute__((may_alias)) u16a;
   typedef uint32_t __attribute__((may_alias)) u32a;
   typedef uint64_t __attribute__((may_alias)) u64a;
   u16a* Jt = (u16a*)L.ent;
   uint8_t* Rt = (uint8_t*)L.ent + 512;
+#endif
   uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
   uint32_t produced = 0, k = 0;
   int code = 0;
@@ -660,6 +671,32 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
     }
     DIAG_ADD(d_pre, t_pre);
     DIAG_T(t_dbl);
+#if PQG_WALK_CHAIN
+    // the chain of run headers from pos, followed with one v_readlane per run (the successors
+    // stay in registers): ~20 dependent scalar steps per window on C2 pages, cheaper than the
+    // ~8 LDS rounds of pointer doubling (#else) unless a window holds very many runs
+    const uint32_t s0 = pos - B;
+    uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+    uint32_t q = s0, q_last = s0;
+    while (q < 256u) {
+      q = uni(q);
+      q_last = q;
+      const uint32_t ql = q >> 2, qb = q & 3u;
+      const uint64_t bit = 1ull << ql;
+      uint32_t nq;
+      switch (qb) {
+        case 0: m0 |= bit; nq = rdl(jv[0], ql); break;
+        case 1: m1 |= bit; nq = rdl(jv[1], ql); break;
+        case 2: m2 |= bit; nq = rdl(jv[2], ql); break;
+        default: m3 |= bit; nq = rdl(jv[3], ql); break;
+      }
+      q = nq;
+    }
+    DIAG_ADD(d_dbl, t_dbl);
+    DIAG_T(t_emit);
+    const uint32_t mk = (uint32_t)((m0 >> lane) & 1u) | ((uint32_t)((m1 >> lane) & 1u) << 1) |
+                        ((uint32_t)((m2 >> lane) & 1u) << 2) | ((uint32_t)((m3 >> lane) & 1u) << 3);
+#else
     const uint32_t s0 = pos - B;
     *(u64a*)(Jt + 4u * lane) =
         (uint64_t)jv[0] | ((uint64_t)jv[1] << 16) | ((uint64_t)jv[2] << 32) | ((uint64_t)jv[3] << 48);
@@ -702,6 +739,7 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
         q_last = q > q_last ? q : q_last;
       }
     }
+#endif
     q_last = uni(q_last);
     // runs of the window: marked, inside the section, fast-path headers
     const uint32_t cap = N - produced;
@@ -818,6 +856,320 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
 #endif
 }
 
+// ---- One WORKGROUP per page: the page's run headers ranked over 2048-byte super-windows.
+//
+// The same list ranking as dict_walk_pj, with the 256 threads of the workgroup sharing one page:
+// every byte position of a super-window (8 per thread) is parsed as a possible run header, its
+// successor goes to an LDS table, and pointer doubling over the whole super-window (<= 12 rounds,
+// workgroup barriers between them) marks the chain of headers from the window's first header. A
+// page's data section is then walked in ceil(bytes / ~2 KB) serial steps instead of one per 256
+// bytes (dict_walk_pj) or one per run (dict_walk): on Zipf(2.0) pages (~8.7 KB, ~1,500 headers) the
+// per-wave walk took ~140 us, the serial part the expansion waits for.
+constexpr uint32_t PW_SW = 2048;                   // header positions per super-window
+constexpr uint32_t PW_PER_T = PW_SW / (64u * WPB);  // positions per thread (8)
+constexpr uint32_t PW_SEG = PW_SW + 128;            // staged bytes: 16-aligned start + parse slack
+
+struct PageWgLds {
+  uint8_t seg[PW_SEG];    // section bytes [A0, A0 + PW_SEG), A0 = super-window start & ~15
+  uint16_t J[PW_SW];      // successor (window-relative; PW_SW: leaves the window / chain end / slow)
+  uint8_t M[PW_SW];       // on the chain from the window's first header
+  uint32_t red[2][WPB];   // per-wave partials of the workgroup scans / maxima
+};
+
+struct HdrAt {
+  uint32_t nx, cnt, val, flg;  // next header, values, RLE value or packed data start, pk | slow << 1 | hl << 2
+};
+
+// Run header at page position p (LDS offset o of the staged segment): the parse of predecode.
+__device__ __forceinline__ HdrAt hdr_parse(const uint8_t* seg, uint32_t o, uint32_t p, int w) {
+  typedef uint32_t __attribute__((may_alias)) u32a;
+  const uint32_t a = o & ~3u, s = o & 3u;
+  const uint32_t d0 = *(const u32a*)(seg + a), d1 = *(const u32a*)(seg + a + 4), d2 = *(const u32a*)(seg + a + 8),
+                 d3 = *(const u32a*)(seg + a + 12);
+  const uint64_t x = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) |
+                     ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
+  const uint32_t hi8 = __builtin_amdgcn_alignbyte(d3, d2, s);  // bytes p + 8 .. p + 11
+  const uint32_t b0 = (uint32_t)x & 0xFFu, b1 = (uint32_t)(x >> 8) & 0xFFu, b2 = (uint32_t)(x >> 16) & 0xFFu,
+                 b3 = (uint32_t)(x >> 24) & 0xFFu, b4 = (uint32_t)(x >> 32) & 0xFFu;
+  uint32_t v = b0 & 0x7Fu, hl = 1, slow = 0;
+  if (b0 & 0x80u) {
+    v |= (b1 & 0x7Fu) << 7; hl = 2;
+    if (b1 & 0x80u) {
+      v |= (b2 & 0x7Fu) << 14; hl = 3;
+      if (b2 & 0x80u) {
+        v |= (b3 & 0x7Fu) << 21; hl = 4;
+        if (b3 & 0x80u) {
+          v |= b4 << 28; hl = 5;
+          if (b4 & 0x80u) slow = 1;
+        }
+      }
+    }
+  }
+  HdrAt h;
+  const uint32_t nb = ((uint32_t)w + 7u) >> 3;
+  if ((v & 1u) == 0) {
+    const uint32_t shb = 8u * hl;
+    const uint64_t y = (x >> shb) | ((uint64_t)hi8 << (64u - shb));
+    h.val = nb == 4 ? (uint32_t)y : (uint32_t)y & ((1u << (8u * nb)) - 1u);
+    h.cnt = v >> 1;
+    h.nx = p + hl + nb;
+    h.flg = (slow << 1) | (hl << 2);
+  } else {
+    const uint32_t groups = v >> 1;
+    if (groups == 0 || groups >= (1u << 28)) slow = 1;
+    h.cnt = groups * 8u;
+    h.val = p + hl;
+    const uint64_t e = (uint64_t)p + hl + (uint64_t)groups * (uint32_t)w;
+    h.nx = e > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)e;
+    h.flg = 1u | (slow << 1) | (hl << 2);
+  }
+  return h;
+}
+
+// Workgroup exclusive prefix of v saturated at cap (min(sum, cap)); *total = the saturated sum.
+__device__ __forceinline__ uint32_t wg_excl_sat(uint32_t v, uint32_t cap, uint32_t* red, uint32_t* total) {
+  const uint32_t lane = lane_id(), wv = wave_id();
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if ((int)lane >= o) inc = inc + y < cap ? inc + y : cap;
+  }
+  uint32_t ex = __shfl_up(inc, 1);
+  if (lane == 0) ex = 0;
+  if (lane == WAVE - 1) red[wv] = inc;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < WPB; q++) {
+    const uint32_t sq = red[q];
+    if (q < wv) before = before + sq < cap ? before + sq : cap;
+    tot = tot + sq < cap ? tot + sq : cap;
+  }
+  __syncthreads();
+  *total = tot;
+  return before + ex < cap ? before + ex : cap;
+}
+
+__device__ __forceinline__ uint32_t wg_max(uint32_t v, uint32_t* red) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t y = __shfl_xor(v, o);
+    v = y > v ? y : v;
+  }
+  if (lane_id() == 0) red[wave_id()] = v;
+  __syncthreads();
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < WPB; q++) m = red[q] > m ? red[q] : m;
+  __syncthreads();
+  return m;
+}
+
+template <int W>
+__device__ void dict_page_wg(PageWgLds& L, rsrc_t rs, uint32_t N, uint32_t sec_beg, uint32_t sec_end, int w, uint64_t* rec,
+                             uint32_t* chunk_run, uint32_t CH, uint32_t sh, int page, uint64_t* err, ErrCount err_count,
+                             uint32_t& n_rec, uint32_t& n_ok) {
+  const uint32_t t = threadIdx.x;
+  uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position (after the bit width)
+  uint32_t produced = 0, k = 0;
+  int code = 0;
+  // a record written by one thread (the scalar slow path) and the chunk entries it owns
+  auto put_record = [&](uint32_t start, uint32_t end, uint32_t payload) {
+    if (t == 0) {
+      sst(rec + k, (uint64_t)start | ((uint64_t)payload << 32));
+      uint32_t j = start == 0 ? 0 : (start + sh + CH - 1) / CH;
+      for (; j * CH < end + sh; j++) sst(chunk_run + j, k);
+    }
+    k++;
+  };
+  while (true) {
+    // every quantity of this loop is workgroup-uniform
+    if (produced >= N) break;
+    if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
+    const uint32_t P0 = pos, A0 = P0 & ~15u;
+    __syncthreads();  // the previous super-window's LDS reads are done
+    for (uint32_t o = 16u * t; o < PW_SEG; o += 16u * 64u * WPB)
+      *(u32x4*)(L.seg + o) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(A0 + o), 0, 0);
+    __syncthreads();
+    uint32_t jv[PW_PER_T], slowm = 0, inm = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < PW_PER_T; b++) {
+      const uint32_t rel = PW_PER_T * t + b, p = P0 + rel;
+      const HdrAt h = hdr_parse(L.seg, p - A0, p, w);
+      const bool pk = h.flg & 1u, in = p < sec_end;
+      const uint32_t hl = h.flg >> 2;
+      // slow: long varints, 0 / huge group counts, a header or RLE value crossing the end
+      const bool slow = in && ((h.flg & 2u) || p + hl > sec_end || (!pk && h.nx > sec_end));
+      const uint32_t nn = pk ? (h.nx < sec_end ? h.nx : sec_end) : h.nx;
+      jv[b] = (!in || slow || nn - P0 >= PW_SW) ? PW_SW : nn - P0;
+      L.J[rel] = (uint16_t)jv[b];
+      L.M[rel] = rel == 0 ? 1 : 0;
+      slowm |= (slow ? 1u : 0u) << b;
+      inm |= (in ? 1u : 0u) << b;
+    }
+    __syncthreads();
+    // pointer doubling: after round r every chain position within 2^(r+1) steps is marked
+#pragma unroll 1
+    for (int r = 0; r < 12; r++) {
+      uint32_t jn[PW_PER_T];
+#pragma unroll
+      for (uint32_t b = 0; b < PW_PER_T; b++) {
+        const uint32_t rel = PW_PER_T * t + b;
+        if (jv[b] < PW_SW && L.M[rel]) L.M[jv[b]] = 1;
+        jn[b] = jv[b] < PW_SW ? L.J[jv[b]] : PW_SW;
+      }
+      __syncthreads();
+      bool more = false;
+#pragma unroll
+      for (uint32_t b = 0; b < PW_PER_T; b++) {
+        jv[b] = jn[b];
+        L.J[PW_PER_T * t + b] = (uint16_t)jn[b];
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t b = 0; b < PW_PER_T; b++) more |= jv[b] < PW_SW && L.M[PW_PER_T * t + b];
+      if (!__syncthreads_or(more)) break;
+    }
+    // the chain: marked positions in order (thread-major = position order)
+    uint32_t mk = 0, hi_rel = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < PW_PER_T; b++)
+      if (L.M[PW_PER_T * t + b]) {
+        mk |= 1u << b;
+        hi_rel = PW_PER_T * t + b;
+      }
+    const uint32_t q_last = wg_max(hi_rel, L.red[0]);
+    const uint32_t cap = N - produced;
+    uint32_t cc[PW_PER_T], pl[PW_PER_T], lsum = 0, n_run = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < PW_PER_T; b++) {
+      cc[b] = 0;
+      pl[b] = 0;
+      if (((mk & inm & ~slowm) >> b) & 1u) {
+        const uint32_t rel = PW_PER_T * t + b, p = P0 + rel;
+        const HdrAt h = hdr_parse(L.seg, p - A0, p, w);
+        uint32_t c = h.cnt;
+        if (!(h.flg & 1u) && c == 0) c = cap;  // Java: currentCount goes negative, the value repeats forever
+        cc[b] = c < cap ? c : cap;
+        pl[b] = (h.flg & 1u) ? (0x80000000u | h.val) : (h.val > 0x7FFFFFFFu ? 0x7FFFFFFFu : h.val);
+        lsum = lsum + cc[b] < cap ? lsum + cc[b] : cap;
+      }
+    }
+    uint32_t total;
+    uint32_t st = wg_excl_sat(lsum, cap, L.red[0], &total);
+    // emitted: a run that starts before the cap
+    uint32_t em = 0, stb[PW_PER_T];
+#pragma unroll
+    for (uint32_t b = 0; b < PW_PER_T; b++) {
+      stb[b] = st;
+      if (cc[b] && st < cap) em |= 1u << b;
+      st = st + cc[b] < cap ? st + cc[b] : cap;
+    }
+    n_run = (uint32_t)__builtin_popcount(em);
+    uint32_t n_em;
+    uint32_t idx = wg_excl_sat(n_run, 0xFFFFFFFFu, L.red[1], &n_em);
+#pragma unroll
+    for (uint32_t b = 0; b < PW_PER_T; b++) {
+      if ((em >> b) & 1u) {
+        const uint32_t s_abs = produced + stb[b];
+        const uint32_t e_abs = produced + (stb[b] + cc[b] < cap ? stb[b] + cc[b] : cap);
+        sst(rec + k + idx, (uint64_t)s_abs | ((uint64_t)pl[b] << 32));
+        uint32_t j = s_abs == 0 ? 0 : (s_abs + sh + CH - 1) / CH;
+        for (; j * CH < e_abs + sh; j++) sst(chunk_run + j, k + idx);
+        idx++;
+      }
+    }
+    k += n_em;
+    produced += total;
+    if (produced >= N) break;
+    // continue after the chain's last position (every thread parses it from LDS)
+    const uint32_t pq = P0 + q_last;
+    const HdrAt hq = hdr_parse(L.seg, pq - A0, pq, w);
+    const bool q_in = pq < sec_end;
+    const uint32_t q_hl = hq.flg >> 2;
+    const bool q_pk = hq.flg & 1u;
+    const bool q_slow = q_in && ((hq.flg & 2u) || pq + q_hl > sec_end || (!q_pk && hq.nx > sec_end));
+    if (!q_in) {
+      pos = pq;  // at the section end: RLE_PAST_END on the next step
+    } else if (!q_slow) {
+      pos = q_pk ? (hq.nx < sec_end ? hq.nx : sec_end) : hq.nx;  // leaves the super-window
+    } else {
+      // scalar re-decode of the header at pq (readNext :80-109), identical in every thread
+      uint32_t hl, m, nxs, vv;
+      uint64_t cnt64;
+      code = slow_header_g([&](uint32_t p) { return sbyte(rs, p); }, pq, sec_end, w, hl, m, cnt64, vv, nxs);
+      if (code) break;
+      if (m == 0 && nxs > sec_end) { code = PQG_ERR_EOF; break; }
+      uint64_t cnt = cnt64;
+      const uint32_t left = N - produced;
+      if (m == 0 && cnt == 0) cnt = left;
+      const uint32_t take = cnt < left ? (uint32_t)cnt : left;
+      put_record(produced, produced + take, m ? (0x80000000u | vv) : (vv > 0x7FFFFFFFu ? 0x7FFFFFFFu : vv));
+      produced += take;
+      pos = m ? (nxs < sec_end ? nxs : sec_end) : nxs;
+    }
+  }
+  if (code) {
+    if (t == 0) report(err, err_count, page, 2, produced, code);
+    N = produced;
+  }
+  n_rec = k;
+  n_ok = N;
+}
+
+// Walker workgroup for ONE page (dict_page_wg); publishes like dict_runs_body.
+template <int W>
+__device__ __forceinline__ void dict_runs_body_wg(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                  const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                                  const int32_t* __restrict__ list, int n_list, uint64_t* rec,
+                                                  uint32_t* chunk_run, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
+                                                  uint64_t* err, ErrCount err_count, uint8_t* lds, uint32_t i_page) {
+  PageWgLds& L = *(PageWgLds*)lds;
+  if (i_page >= (uint32_t)n_list) return;
+  const int page = list[i_page];
+#ifdef PQG_DIAG
+  const uint64_t rt_w0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  const PageWork pw = work[page];
+  uint32_t N = uni(pw.n_values);
+  const uint32_t sec_beg = uni(pw.data_begin), sec_end = uni(pw.size);
+  constexpr uint32_t E = 16u / W;
+  const uint32_t CH = chunk_values(E);
+  const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
+  uint32_t n_rec = 0, n_ok = 0;
+  if (N > 0) {
+    const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+    if (sec_beg >= sec_end) {
+      // empty data section: every read throws "Attempt to read from empty page"
+      if (threadIdx.x == 0) report(err, err_count, page, 2 /*value*/, 0, PQG_ERR_EMPTY_PAGE);
+    } else {
+      const uint32_t bw = sbyte(rs, sec_beg);
+      if (bw > 32u) {  // RunLengthBitPackingHybridDecoder ctor :55 (thrown at initFromPage)
+        if (threadIdx.x == 0) report(err, err_count, page, 0 /*init*/, 2, PQG_ERR_BIT_WIDTH);
+      } else {
+        dict_page_wg<W>(L, rs, N, sec_beg, sec_end, (int)bw, rec + pw.rec_base, chunk_run + pw.chunk_base, CH, sh, page,
+                        err, err_count, n_rec, n_ok);
+      }
+    }
+  }
+  // Publish (see handoff_release): every wave's record / chunk-entry stores are complete before the
+  // barrier, then thread 0 writes the status and the flag
+  handoff_release();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sst(pstat + page, (uint64_t)n_rec | ((uint64_t)n_ok << 32));
+    handoff_release();
+    sst(flags + page, epoch);
+#ifdef PQG_DIAG
+    if (pqg_diag_wrt) {
+      pqg_diag_wrt[2 * page] = rt_w0;
+      pqg_diag_wrt[2 * page + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+  }
+}
+
 // One wave per page (4 per workgroup): the run records of RLE_DICTIONARY / PLAIN_DICTIONARY
 // pages (DictionaryValuesReader.initFromPage :48-64 + RunLengthBitPackingHybridDecoder.readNext
 // :80-109). The page section is staged in LDS; a 256-byte window is pre-decoded in parallel
@@ -834,6 +1186,14 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
   const int i_page = (int)(group * WPB + wave_id());
   if (i_page >= n_list) return;
   const int page = list[i_page];
+#ifdef PQG_DIAG
+  const uint64_t rt_w0 = __builtin_amdgcn_s_memrealtime();
+#endif
+#if PQG_WALK_PRIO
+  // the walk is one serial chain per page that the page's expansion waits for: issue its
+  // instructions ahead of the expansion waves sharing the SIMD
+  __builtin_amdgcn_s_setprio(PQG_WALK_PRIO);
+#endif
   const uint32_t lane = lane_id();
   const PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
@@ -882,7 +1242,16 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
 #else
     sst(flags + page, epoch);
 #endif
+#ifdef PQG_DIAG
+    if (pqg_diag_wrt) {
+      pqg_diag_wrt[2 * page] = rt_w0;
+      pqg_diag_wrt[2 * page + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
   }
+#if PQG_WALK_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
 }
 
 template <int W>
@@ -891,10 +1260,16 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_runs(const uint8_t* __restric
                                                         const ColumnDev* __restrict__ cols,
                                                         const int32_t* __restrict__ list, int n_list, uint64_t* rec,
                                                         uint32_t* chunk_run, uint64_t* pstat, uint32_t* flags,
-                                                        uint32_t epoch, uint64_t* err, ErrCount err_count) {
+                                                        uint32_t epoch, uint32_t walk_pg, uint64_t* err,
+                                                        ErrCount err_count) {
   __shared__ __attribute__((aligned(16))) DictWaveLds wl_all[WPB];
-  dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
-                    (uint8_t*)wl_all, blockIdx.x);
+  static_assert(sizeof(DictWaveLds) * WPB >= sizeof(PageWgLds), "walker LDS");
+  if (walk_pg)
+    dict_runs_body_wg<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
+                         (uint8_t*)wl_all, blockIdx.x);
+  else
+    dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
+                      (uint8_t*)wl_all, blockIdx.x);
 }
 
 template <int W>
@@ -912,8 +1287,14 @@ __device__ __forceinline__ typename DictVal<W>::T dict_get_g(bool in_lds, const 
 //   tile sweep  every lane tracks the run holding its element: per tile it advances past
 //               the run starts it crossed (usually none), reads the value (RLE) or unpacks
 //               the id and gathers (packed), and the wave stores one full 1 KB tile.
-constexpr uint32_t XT_RUNS = 128;   // run table entries per wave
-constexpr uint32_t XT_SEG = 2560;   // LDS bytes for the packed data of one round
+#ifndef PQG_XT_RUNS
+#define PQG_XT_RUNS 128
+#endif
+#ifndef PQG_XT_SEG
+#define PQG_XT_SEG 2560
+#endif
+constexpr uint32_t XT_RUNS = PQG_XT_RUNS;  // run table entries per wave
+constexpr uint32_t XT_SEG = PQG_XT_SEG;    // LDS bytes for the packed data of one round
 
 constexpr uint32_t XT_LDS_BYTES = DICT_LDS_BYTES + WPB * (XT_RUNS * 16 + XT_SEG);
 #ifndef PQG_SPIN_SLEEP
@@ -984,6 +1365,24 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
   const T* dict_l = (const T*)dict_lds;
   // one output chunk (c < n_chunks); false when the wave must stop (a walker timed out)
   auto one_chunk = [&](uint32_t c) -> bool {
+#ifdef PQG_DIAG
+    const uint64_t rt_x0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t rt_x1 = 0;
+    struct XStamp {
+      uint64_t t0, *t1;
+      uint32_t c;
+      __device__ ~XStamp() {
+        if (pqg_diag_xrt && lane_id() == 0) {
+          uint32_t hw;
+          asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+          pqg_diag_xrt[4 * (uint64_t)c] = t0;
+          pqg_diag_xrt[4 * (uint64_t)c + 1] = *t1;
+          pqg_diag_xrt[4 * (uint64_t)c + 2] = __builtin_amdgcn_s_memrealtime();
+          pqg_diag_xrt[4 * (uint64_t)c + 3] = (uint64_t)hw;
+        }
+      }
+    } xstamp{rt_x0, &rt_x1, c};
+#endif
     const int page = (int)(uint32_t)chunks[c];
       const uint32_t j = (uint32_t)(chunks[c] >> 32);
     // page / column facts and the page's bit width do not depend on the walk: loaded before the
@@ -1005,6 +1404,9 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       while (true) {
         if (uni(sld(flags + page)) == epoch) {
           handoff_acquire();
+#ifdef PQG_DIAG
+          rt_x1 = __builtin_amdgcn_s_memrealtime();
+#endif
           pst = uni64(sld(pstat + page));
           break;
         }
@@ -1234,21 +1636,34 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restri
 
 // Walkers and tiles in one grid: workgroups [0, n_walk) walk pages, the rest expand chunks
 // as soon as their page is published, so the expansion overlaps the walk.
+#ifdef PQG_WAVES_PER_EU
+#define PQG_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(PQG_WAVES_PER_EU, PQG_WAVES_PER_EU)))
+#else
+#define PQG_FUSED_ATTR
+#endif
 template <int W, bool IDS = false>
-__global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) PQG_FUSED_ATTR void k_dict_fused(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                          const PageWork* __restrict__ work,
                                                          const ColumnDev* __restrict__ cols,
                                                          const int32_t* __restrict__ list, int n_list,
                                                          uint32_t n_walk, uint64_t* rec, uint32_t* chunk_run,
                                                          const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                          uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                                                         uint32_t walk_wg, uint32_t tile_wg, uint64_t* err,
+                                                         uint32_t walk_wg, uint32_t tile_wg, uint32_t walk_pg, uint64_t* err,
                                                          ErrCount err_count) {
   constexpr uint32_t LB = sizeof(DictWaveLds) * WPB > XT_LDS_BYTES ? sizeof(DictWaveLds) * WPB : XT_LDS_BYTES;
+  static_assert(LB >= sizeof(PageWgLds), "walker LDS");
   __shared__ __attribute__((aligned(16))) uint8_t lds[LB];
   // workgroups [0, n_walk) walk, the rest expand. walk_wg / tile_wg > 0: persistent workgroups
-  // that take every walk_wg-th group of 4 pages / every tile_wg-th group of 4 chunks, in page order
-  if (blockIdx.x < n_walk) {
+  // that take every walk_wg-th group of 4 pages / every tile_wg-th group of 4 chunks, in page order.
+  // walk_pg: a walker workgroup walks ONE page with all its threads (dict_page_wg)
+  if (blockIdx.x < n_walk && walk_pg) {
+    for (uint32_t g = blockIdx.x; g < (uint32_t)n_list; g += walk_wg) {
+      dict_runs_body_wg<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err,
+                           err_count, lds, g);
+      if (!walk_wg) break;
+    }
+  } else if (blockIdx.x < n_walk) {
     for (uint32_t g = blockIdx.x; g * WPB < (uint32_t)n_list; g += walk_wg) {
       dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
                         lds, g);
@@ -2651,6 +3066,12 @@ extern "C" int pqg_diag_nostore_set(int v) {
 extern "C" int pqg_diag_set(void* p) {
   return hipMemcpyToSymbol(HIP_SYMBOL(pqg::pqg_diag_buf), &p, sizeof(p)) == hipSuccess ? 0 : 3;
 }
+extern "C" int pqg_diag_rt_set(void* walk, void* chunk) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(pqg::pqg_diag_wrt), &walk, sizeof(walk)) == hipSuccess &&
+                 hipMemcpyToSymbol(HIP_SYMBOL(pqg::pqg_diag_xrt), &chunk, sizeof(chunk)) == hipSuccess
+             ? 0
+             : 3;
+}
 namespace pqg {
 #endif
 
@@ -2662,30 +3083,31 @@ namespace pqg {
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                        const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                       bool fused, uint32_t walk_wg, uint32_t tile_wg, uint64_t* err, ErrCount err_count) {
+                       bool fused, uint32_t walk_wg, uint32_t tile_wg, uint32_t walk_pg, uint64_t* err,
+                       ErrCount err_count) {
   if (n <= 0) return hipSuccess;
-  uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
+  uint32_t n_walk = walk_pg ? (uint32_t)n : (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
   if (fused && walk_wg && walk_wg < n_walk) n_walk = walk_wg; else walk_wg = fused && walk_wg ? n_walk : walk_wg;
   if (fused && tile_wg && tile_wg < n_tile) n_tile = tile_wg; else tile_wg = fused && tile_wg ? n_tile : tile_wg;
   const dim3 blk(64 * WPB);
   if (fused) {
     if (width == 8)
       hipLaunchKernelGGL(k_dict_fused<8>, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n, n_walk,
-                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, err, err_count);
+                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, walk_pg, err, err_count);
     else
       hipLaunchKernelGGL(k_dict_fused<4>, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n, n_walk,
-                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, err, err_count);
+                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, walk_pg, err, err_count);
     return hipGetLastError();
   }
   if (width == 8) {
     hipLaunchKernelGGL(k_dict_runs<8>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,
-                       pstat, flags, epoch, err, err_count);
+                       pstat, flags, epoch, walk_pg, err, err_count);
     if (n_tile)
       hipLaunchKernelGGL(k_dict_tiles<8>, dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks,
                          n_chunks, pstat, err, err_count);
   } else {
     hipLaunchKernelGGL(k_dict_runs<4>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,
-                       pstat, flags, epoch, err, err_count);
+                       pstat, flags, epoch, walk_pg, err, err_count);
     if (n_tile)
       hipLaunchKernelGGL(k_dict_tiles<4>, dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks,
                          n_chunks, pstat, err, err_count);
@@ -2696,20 +3118,20 @@ hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t
 hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                            const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
-                           uint32_t epoch, bool fused, uint32_t walk_wg, uint32_t tile_wg, uint64_t* err,
-                           ErrCount err_count) {
+                           uint32_t epoch, bool fused, uint32_t walk_wg, uint32_t tile_wg, uint32_t walk_pg,
+                           uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
-  uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
+  uint32_t n_walk = walk_pg ? (uint32_t)n : (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
   if (fused && walk_wg && walk_wg < n_walk) n_walk = walk_wg; else walk_wg = fused && walk_wg ? n_walk : walk_wg;
   if (fused && tile_wg && tile_wg < n_tile) n_tile = tile_wg; else tile_wg = fused && tile_wg ? n_tile : tile_wg;
   const dim3 blk(64 * WPB);
   if (fused) {
     hipLaunchKernelGGL((k_dict_fused<4, true>), dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n,
-                       n_walk, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, err, err_count);
+                       n_walk, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, walk_pg, err, err_count);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_dict_runs<4>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,
-                     pstat, flags, epoch, err, err_count);
+                     pstat, flags, epoch, walk_pg, err, err_count);
   if (n_tile)
     hipLaunchKernelGGL((k_dict_tiles<4, true>), dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run,
                        chunks, n_chunks, pstat, err, err_count);

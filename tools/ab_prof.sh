@@ -10,7 +10,7 @@ for spec in "$@"; do
   IFS=: read -r label envs lib <<< "$spec"
   if [ "$lib" = default ]; then unset PQGPU_LIB; else export PQGPU_LIB=$PWD/$lib; fi
   for e in $envs; do export "$e"; done
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/$label" -o run -- python3 -u bench.py --no-cpu --no-verify \
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$label" -o run -- python3 -u bench.py --no-cpu --no-verify \
     --steps 30 ${AB_ARGS:-} > "$OUT/$label.json" 2> "$OUT/$label.err" || { tail -20 "$OUT/$label.err"; exit 1; }
   for e in $envs; do unset "${e%%=*}"; done
   f=$(find "$OUT/$label" -name '*kernel_stats.csv' | head -1)
