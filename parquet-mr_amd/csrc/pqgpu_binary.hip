@@ -119,6 +119,9 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
 #ifndef PQG_BW_WIN
 #define PQG_BW_WIN 2048
 #endif
+#ifndef PQG_BW_AHEAD
+#define PQG_BW_AHEAD 1
+#endif
 constexpr uint32_t BW_WIN = PQG_BW_WIN;    // window bytes
 constexpr uint32_t BW_Q = BW_WIN / 64;     // positions per lane (16 or 32)
 constexpr uint32_t BW_CAP = BW_WIN / 4;    // candidates per pass over a tile (more: the tile is taken in parts)
@@ -162,10 +165,18 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
   const uint32_t lane = lane_id();
   uint32_t pos = uni(beg), produced = 0;
   int code = 0;
-  // fixed BW_WIN tiles of the page; the tile after the current one is always in flight
+  // fixed BW_WIN tiles of the page; the PQG_BW_AHEAD tiles after the current one are in flight
+  // (a page is one wave's serial chain: with few pages per CU the tile latency is not hidden by
+  // other waves, so the wave itself keeps several tiles in flight)
   uint32_t B = pos & ~(BW_WIN - 1u);
   BwBytes cur_b = bw_load(rs, B);
   BwBytes nxt_b = bw_load(rs, B + BW_WIN);
+#if PQG_BW_AHEAD >= 2
+  BwBytes nxt2_b = bw_load(rs, B + 2u * BW_WIN);
+#endif
+#if PQG_BW_AHEAD >= 3
+  BwBytes nxt3_b = bw_load(rs, B + 3u * BW_WIN);
+#endif
   while (true) {
     pos = uni(pos);
     produced = uni(produced);
@@ -268,8 +279,29 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
     // still in cur_b)
     const uint32_t nB = pos & ~(BW_WIN - 1u);
     if (leave && nB != B) {
-      cur_b = nB == B + BW_WIN ? nxt_b : bw_load(rs, nB);  // else: a value longer than a tile, the prefetch missed
-      nxt_b = bw_load(rs, nB + BW_WIN);
+      if (nB == B + BW_WIN) {
+        cur_b = nxt_b;
+#if PQG_BW_AHEAD >= 2
+        nxt_b = nxt2_b;
+#if PQG_BW_AHEAD >= 3
+        nxt2_b = nxt3_b;
+        nxt3_b = bw_load(rs, nB + 3u * BW_WIN);
+#else
+        nxt2_b = bw_load(rs, nB + 2u * BW_WIN);
+#endif
+#else
+        nxt_b = bw_load(rs, nB + BW_WIN);
+#endif
+      } else {  // a value longer than a tile: the prefetch missed
+        cur_b = bw_load(rs, nB);
+        nxt_b = bw_load(rs, nB + BW_WIN);
+#if PQG_BW_AHEAD >= 2
+        nxt2_b = bw_load(rs, nB + 2u * BW_WIN);
+#endif
+#if PQG_BW_AHEAD >= 3
+        nxt3_b = bw_load(rs, nB + 3u * BW_WIN);
+#endif
+      }
       B = nB;
     }
     wave_sync();
