@@ -253,7 +253,9 @@ int pqg_unpack_runs(pqg_ctx* ctx, int bit_width, const uint8_t* d_in,
 /* ParquetReadRouter.read equivalent on host buffers: consumes
  * count*bit_width/8 bytes of `in` (in_len must cover them, else PQG_ERR_EOF as
  * SingleBufferInputStream.slice throws EOFException) and writes `count` ints.
- * The unpack runs on the GPU (H2D, kernel, D2H); synchronous. */
+ * The unpack runs on the GPU (H2D, kernel, D2H); synchronous. A parity entry for the router's
+ * call shape: one call per run pays a PCIe round trip, so batch runs through pqg_unpack_runs
+ * (device buffers) or decode whole pages with pqg_decode. */
 int pqg_router_read(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_len,
                     int count, int32_t* out);
 

@@ -594,6 +594,9 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
 #ifndef PQG_WALK_PRIO
 #define PQG_WALK_PRIO 0
 #endif
+#ifndef PQG_PJ_LARGE
+#define PQG_PJ_LARGE 1
+#endif
 __device__ __forceinline__ void handoff_release() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a compiler barrier too (invisible to the waitcnt pass)
 }
@@ -613,7 +616,7 @@ __device__ __forceinline__ void handoff_acquire() {
 // the positions reachable from the chain start. The marked positions, in order, are the
 // window's runs; a saturating prefix sum of their counts gives each run's first value.
 // Cost per window is fixed (~8 LDS round trips) instead of one round trip per run.
-template <int W>
+template <int W, bool SMALL = true>
 __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg,
                                              uint32_t sec_end, int w, uint64_t* rec, uint32_t* chunk_run,
                                              uint32_t CH, uint32_t sh, int page, uint64_t* err, ErrCount err_count,
@@ -652,7 +655,7 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
     if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
     const uint32_t B = pos & ~3u;
     DIAG_T(t_pre);
-    predecode<true>(win, B, w);
+    predecode<SMALL>(win, B, w);  // !SMALL: the segment is refilled when the window leaves it
     // successors of this lane's 4 positions
     uint32_t jv[4], nn[4], slowm = 0, inm = 0;
 #pragma unroll
@@ -823,8 +826,9 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
       pos = B + q_last;
       uint32_t hl, m, nxs, vv;
       uint64_t cnt64;
-      code = slow_header_g([&](uint32_t p) { return uni((seg32(win, p & ~3u) >> ((p & 3u) * 8u)) & 0xFFu); }, pos,
-                           sec_end, w, hl, m, cnt64, vv, nxs);
+      code = SMALL ? slow_header_g([&](uint32_t p) { return uni((seg32(win, p & ~3u) >> ((p & 3u) * 8u)) & 0xFFu); },
+                                   pos, sec_end, w, hl, m, cnt64, vv, nxs)
+                   : slow_header_g([&](uint32_t p) { return wbyte(win, p); }, pos, sec_end, w, hl, m, cnt64, vv, nxs);
       if (code) break;
       if (m == 0 && nxs > sec_end) { code = PQG_ERR_EOF; break; }
       uint64_t cnt = cnt64;
@@ -1223,10 +1227,18 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
         if (sec_end - win.seg_lo + 264u <= SEG_BYTES)  // every window inside the segment
           dict_walk_pj<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok,
                           pstat + page);
+#if PQG_PJ_LARGE
+        // larger sections: the same window walk, the LDS segment refilled as the chain advances
+        // (windows inside long bit-packed runs are jumped over, not pre-decoded)
+        else
+          dict_walk_pj<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec,
+                                 n_ok, pstat + page);
+#else
         else if (sec_end - win.seg_lo <= SEG_BYTES)
           dict_walk<W, true>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
         else
           dict_walk<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
+#endif
       }
     }
   }

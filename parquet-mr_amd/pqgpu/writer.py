@@ -1,6 +1,6 @@
 """Page writer: synthesizes parquet-mr-identical column chunks (test / bench input).
 
-The encoders are restated in C++ (csrc/pqwriter.cpp -> libpqwriter.so) from
+The encoders are restated in C++ (tools/synth/pqwriter.cpp -> tools/synth/libpqwriter.so) from
 parquet-mr's writers; this module assembles their output into data pages the
 way parquet-mr's column writers do:
 
@@ -33,7 +33,8 @@ _LIB = None
 def _lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "libpqwriter.so")
+        # input synthesis only (the restated parquet-mr encoders), built outside the product package
+        path = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "tools", "synth", "libpqwriter.so")
         if not os.path.exists(path):
             raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
         lib = C.CDLL(path)
