@@ -122,6 +122,9 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
 #ifndef PQG_BW_AHEAD
 #define PQG_BW_AHEAD 1
 #endif
+#ifndef PQG_BW_COMPACT_LOOP
+#define PQG_BW_COMPACT_LOOP 1
+#endif
 constexpr uint32_t BW_WIN = PQG_BW_WIN;    // window bytes
 constexpr uint32_t BW_Q = BW_WIN / 64;     // positions per lane (16 or 32)
 constexpr uint32_t BW_CAP = BW_WIN / 4;    // candidates per pass over a tile (more: the tile is taken in parts)
@@ -205,6 +208,35 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
     if (base < pos) m &= pos - base >= BW_Q ? 0u : ~((1u << (pos - base)) - 1u);
     uint32_t total;
     const uint32_t rank = wave_excl_scan_u32((uint32_t)__builtin_popcount(m), &total);
+#if PQG_BW_COMPACT_LOOP
+    // one iteration per candidate of this lane (about BW_Q / average value size), not one per
+    // position: the per-position form spent most of the walk's scalar and vector instructions
+    // on exec-mask branches (profiles/r02/final1/strpmc)
+    {
+      uint32_t mm = m, r = rank;
+      while (mm) {
+        const uint32_t q = (uint32_t)__builtin_ctz(mm);
+        mm &= mm - 1u;
+        if (r < BW_CAP) {
+          // d[q / 4] and d[q / 4 + 1] by selects (no dynamic register indexing)
+          const uint32_t i = q >> 2;
+          uint32_t lo = d[0], hi = d[1];
+#pragma unroll
+          for (uint32_t t = 1; t < BW_Q / 4; t++) {
+            const bool s = i == t;
+            lo = s ? d[t] : lo;
+            hi = s ? d[t + 1] : hi;
+          }
+          const uint32_t nx = base + q + 4u + __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
+          *(uint64_t*)&L.pn[r] = (uint64_t)(base + q) | ((uint64_t)nx << 32);
+          L.idx[BW_Q * lane + q] = (uint16_t)r;
+        } else if (r == BW_CAP) {
+          L.cut = base + q;
+        }
+        r++;
+      }
+    }
+#else
 #pragma unroll
     for (uint32_t q = 0; q < BW_Q; q++)
       if ((m >> q) & 1u) {
@@ -217,6 +249,7 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
           L.cut = base + q;
         }
       }
+#endif
     wave_sync();
     total = uni(total);
     // this pass covers [pos, eff_end): the whole tile, or up to the first candidate past the cap
