@@ -125,6 +125,9 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
 #ifndef PQG_BW_COMPACT_LOOP
 #define PQG_BW_COMPACT_LOOP 1
 #endif
+#ifndef PQG_COPY_REL32
+#define PQG_COPY_REL32 1
+#endif
 constexpr uint32_t BW_WIN = PQG_BW_WIN;    // window bytes
 constexpr uint32_t BW_Q = BW_WIN / 64;     // positions per lane (16 or 32)
 constexpr uint32_t BW_CAP = BW_WIN / 4;    // candidates per pass over a tile (more: the tile is taken in parts)
@@ -558,10 +561,12 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
                                                        uint64_t* err, ErrCount err_count) {
   __shared__ uint64_t off_all[WPB][BIN_CHUNK + 1];
   __shared__ uint32_t src_all[WPB][BIN_CHUNK];
+  __shared__ uint32_t rel_all[WPB][BIN_CHUNK + 1];
   const uint32_t c = blockIdx.x * WPB + wave_id();
   if (c >= n_chunks) return;
   uint64_t* off = off_all[wave_id()];
   uint32_t* src = src_all[wave_id()];
+  uint32_t* rel = rel_all[wave_id()];
   const uint32_t lane = lane_id();
   const uint64_t ch = chunks[c];
   const int page = (int)(uint32_t)ch;
@@ -582,7 +587,15 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
   const uint64_t page0 = (uint64_t)offs[0];
   for (uint32_t k = lane; k <= n; k += WAVE) off[k] = (uint64_t)offs[i_lo + k];
   wave_sync();
-  for (uint32_t k = lane; k < n; k += WAVE) {
+#if PQG_COPY_REL32
+  // PLAIN / DLBA sources follow from the offsets (see below): only value 0's is needed
+  // (PLAIN only: DELTA_LENGTH sources are computed per value below for the EOF check)
+  const bool plain_small = !dlba && !from_dict && off[n] - off[0] < 0x7FFF0000ull - 16u;
+  const uint32_t n_src = plain_small ? 1u : n;
+#else
+  const uint32_t n_src = n;
+#endif
+  for (uint32_t k = lane; k < n_src; k += WAVE) {
     uint32_t s;
     if (dlba) {
       const uint64_t rel = off[k] - page0, len = off[k + 1] - off[k];
@@ -607,6 +620,70 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
   // Blocks are gathered G at a time before any of them is stored: a source load issued
   // after a store waits for that store (vmcnt counts both), so loads and stores are not interleaved.
   constexpr uint32_t G = 4;
+#if PQG_COPY_REL32
+  if (o_hi - a0 < 0x7FFF0000ull) {
+    // The usual case: the chunk's bytes span < 2 GiB, so offsets are kept chunk-relative in 32
+    // bits (relative to the first 16-byte block a0), and PLAIN / DELTA_LENGTH sources follow from
+    // them: value k starts at src0 + rel[k] (DLBA) or src0 + rel[k] + 4k (PLAIN: the 4-byte
+    // length prefixes); only dictionary entries need the per-value source table.
+    for (uint32_t k = lane; k <= n; k += WAVE) rel[k] = (uint32_t)(off[k] - a0);
+    wave_sync();
+    const uint32_t hole = dlba ? 0u : 4u;
+    const uint32_t src0 = src[0];
+    const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
+    uint32_t kv = 0;
+    for (uint32_t bg = 16u * lane; bg < r_hi; bg += 16u * WAVE * G) {
+      uint32_t wd[G][4];
+      uint32_t have[G];
+#pragma unroll
+      for (uint32_t g = 0; g < G; g++) {
+        const uint32_t b = bg + 16u * WAVE * g;  // block start (relative to a0)
+        have[g] = 0;
+        wd[g][0] = wd[g][1] = wd[g][2] = wd[g][3] = 0;
+        if (b >= r_hi) continue;
+        const uint32_t b0 = b > r_lo ? b : r_lo;
+        uint32_t lo = kv, hi = n;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (rel[mid] <= b0) lo = mid;
+          else hi = mid;
+        }
+        kv = lo;
+        uint32_t k = kv;
+        uint32_t k_end = rel[k + 1];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+          const uint32_t d0 = b + 4u * q;
+          const uint32_t x0 = d0 > r_lo ? d0 : r_lo, x1 = d0 + 4u < r_hi ? d0 + 4u : r_hi;
+          uint32_t word = 0;
+          for (uint32_t cur = x0; cur < x1;) {
+            while (k + 1 < n && cur >= k_end) {
+              k++;
+              k_end = rel[k + 1];
+            }
+            const uint32_t seg_end = x1 < k_end ? x1 : k_end;
+            const uint32_t sk = from_dict ? src[k] : src0 + (rel[k] - r_lo) + hole * k;
+            const uint32_t sp = sk + (cur - rel[k]);
+            const uint32_t v = sp < slim ? ld4_any(rs, sp) : 0u;
+            const uint32_t nb = seg_end - cur;
+            const uint32_t msk = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
+            word |= (v & msk) << (8u * (cur - d0));
+            cur = seg_end;
+          }
+          wd[g][q] = word;
+          if (x0 == d0 && x1 == d0 + 4u) have[g] |= 1u << q;
+        }
+        if (!dst_al4) have[g] = 0;  // unaligned byte buffer (C ABI caller): byte stores only
+      }
+#pragma unroll
+      for (uint32_t g = 0; g < G; g++) {
+        const uint32_t b = bg + 16u * WAVE * g;
+        if (b < r_hi) store_block16(dst, a0 + b, o_lo, o_hi, wd[g], have[g], dst_al16);
+      }
+    }
+    return;
+  }
+#endif
   uint32_t kv = 0;  // value of this lane's current byte (monotone across iterations)
   for (uint64_t ag = a0 + 16u * lane; ag < o_hi; ag += 16u * WAVE * G) {
     uint32_t wd[G][4];
