@@ -55,6 +55,21 @@ __constant__ uint8_t ZML_BITS[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0
 
 __device__ __forceinline__ int zhigh(uint32_t v) { return v ? 31 - __builtin_clz(v) : -1; }
 
+// Reads of bytes this wave stored earlier (literal buffer, output), after the s_waitcnt that
+// completed the stores: system-scope loads (L1 and L2 bypassed). A workgroup-scope load
+// (PQG_ZSTD_SLD=0) measured the same (71.7 ms on 100 M int64 PLAIN pages, profiles/r02/zstd_ab):
+// the kernel is not bound by these round trips.
+#ifndef PQG_ZSTD_SLD
+#define PQG_ZSTD_SLD 1
+#endif
+__device__ __forceinline__ uint32_t zld(const uint32_t* p) {
+#if PQG_ZSTD_SLD
+  return sld(p);
+#else
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+}
+
 // one input byte at `o` of the job's input (uniform reads: every lane loads the same dword)
 __device__ __forceinline__ uint32_t zbyte(rsrc_t rs, uint32_t o) { return (ld32(rs, o & ~3u) >> ((o & 3u) * 8u)) & 0xFFu; }
 
@@ -358,7 +373,7 @@ __device__ __forceinline__ void zput(ZOut& O, ZWaveLds& L, uint32_t p, uint32_t 
 __device__ __forceinline__ uint32_t zget(const ZOut& O, const ZWaveLds& L, uint32_t q, uint32_t pos) {
   if (pos - q <= ZS_RING - WAVE) return L.ring[q & (ZS_RING - 1u)];
   if (q >= O.cap) return 0;
-  const uint32_t w = sld((const uint32_t*)(O.dst + (q & ~3u)));
+  const uint32_t w = zld((const uint32_t*)(O.dst + (q & ~3u)));
   return (w >> ((q & 3u) * 8u)) & 0xFFu;
 }
 
@@ -376,7 +391,7 @@ __device__ void zcopy_lits(ZOut& O, ZWaveLds& L, int kind, rsrc_t rs, uint32_t s
       uint32_t v;
       if (kind == 0) v = zbyte(rs, src + k);
       else if (kind == 1) v = src;
-      else v = (sld((const uint32_t*)(litbuf + ((src + k) & ~3u))) >> (((src + k) & 3u) * 8u)) & 0xFFu;
+      else v = (zld((const uint32_t*)(litbuf + ((src + k) & ~3u))) >> (((src + k) & 3u) * 8u)) & 0xFFu;
       zput(O, L, O.pos + k, v);
     }
   }
@@ -571,7 +586,7 @@ __device__ uint64_t zxxh64(const uint8_t* p, uint32_t n) {
   const uint32_t* base = (const uint32_t*)(p - mis);
   auto rd = [&](uint32_t o, int bytes) {  // little-endian bytes [o, o + bytes) of the output, bytes <= 8
     const uint32_t a = o + mis, w = a >> 2, s = a & 3u;
-    const uint32_t d0 = sld(base + w), d1 = sld(base + w + 1), d2 = s ? sld(base + w + 2) : 0u;
+    const uint32_t d0 = zld(base + w), d1 = zld(base + w + 1), d2 = s ? zld(base + w + 2) : 0u;
     uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
     return bytes == 8 ? v : v & ((1ull << (8 * bytes)) - 1ull);
   };
