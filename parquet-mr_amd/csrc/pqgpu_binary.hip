@@ -128,6 +128,9 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
 #ifndef PQG_COPY_REL32
 #define PQG_COPY_REL32 1
 #endif
+#ifndef PQG_COPY_COMPOSE
+#define PQG_COPY_COMPOSE 1
+#endif
 constexpr uint32_t BW_WIN = PQG_BW_WIN;    // window bytes
 constexpr uint32_t BW_Q = BW_WIN / 64;     // positions per lane (16 or 32)
 constexpr uint32_t BW_CAP = BW_WIN / 4;    // candidates per pass over a tile (more: the tile is taken in parts)
@@ -649,6 +652,53 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
           else hi = mid;
         }
         kv = lo;
+        const uint32_t bend = b + 16u < r_hi ? b + 16u : r_hi;
+#if PQG_COPY_COMPOSE
+        // PLAIN / DLBA: the block's source is one stream with a 4-byte hole (PLAIN) at every value
+        // start inside the block; with at most 4 such starts the block is composed without loops:
+        // 9 aligned source dwords, the 8 dwords a_t at the block's byte alignment, and per output
+        // byte i the dword a_{q + cnt_i} (cnt_i = value starts at or before byte i).
+        // (not when block byte 0 would lie before the page start: its source offset cannot be
+        // expressed, and the block's stored bytes would read as 0)
+        const bool compose = !from_dict && !(kv + 5u < n && rel[kv + 5u] < bend) &&
+                             !(b < r_lo && src0 + hole * kv < r_lo - b);
+        if (compose) {
+          uint64_t prof = 0;  // nibble i: value starts at or before byte i of the block (PLAIN)
+#pragma unroll
+          for (uint32_t j = 1; j <= 4; j++) {
+            const uint32_t kk = kv + j;
+            const uint32_t pj = kk < n ? rel[kk] : 0xFFFFFFFFu;
+            if (pj < bend && hole) prof += 0x1111111111111111ull << (4u * (pj - b));
+          }
+          const uint32_t S = src0 + (b - r_lo) + hole * kv;  // source of block byte 0 (wraps below: not stored)
+          const uint32_t A = S & ~3u, sh = S & 3u;
+          const u32x4 w0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)A, 0, 0);
+          const u32x4 w1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(A + 16u), 0, 0);
+          const uint32_t w8 = ld32(rs, A + 32u);
+          const uint32_t wv[9] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w8};
+          uint32_t a[8];
+#pragma unroll
+          for (uint32_t t = 0; t < 8; t++) a[t] = __builtin_amdgcn_alignbyte(wv[t + 1], wv[t], sh);
+#pragma unroll
+          for (uint32_t q = 0; q < 4; q++) {
+            uint32_t word = 0;
+#pragma unroll
+            for (uint32_t e = 0; e < 4; e++) {
+              const uint32_t c = (uint32_t)(prof >> (4u * (4u * q + e))) & 0xFu;  // 0..4
+              uint32_t v = a[q];
+              v = c == 1u ? a[q + 1] : v;
+              v = c == 2u ? a[q + 2] : v;
+              v = c == 3u ? a[q + 3] : v;
+              v = c == 4u ? a[q + 4] : v;
+              word |= v & (0xFFu << (8u * e));
+            }
+            const uint32_t d0 = b + 4u * q;
+            wd[g][q] = word;
+            if (d0 >= r_lo && d0 + 4u <= r_hi) have[g] |= 1u << q;
+          }
+        } else
+#endif
+        {
         uint32_t k = kv;
         uint32_t k_end = rel[k + 1];
 #pragma unroll
@@ -673,6 +723,8 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
           wd[g][q] = word;
           if (x0 == d0 && x1 == d0 + 4u) have[g] |= 1u << q;
         }
+        }
+        (void)bend;
         if (!dst_al4) have[g] = 0;  // unaligned byte buffer (C ABI caller): byte stores only
       }
 #pragma unroll
