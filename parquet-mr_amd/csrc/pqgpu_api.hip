@@ -651,15 +651,11 @@ int pqg_plan_launch(pqg_plan* P) {
   if (P->blen_bytes && hipMemsetAsync(P->bscratch.p, 0, P->blen_bytes, s) != hipSuccess) return PQG_ERR_HIP;
   for (void* v : P->empty_bin_values)
     if (hipMemsetAsync(v, 0, sizeof(int64_t), s) != hipSuccess) return PQG_ERR_HIP;
-  // dictionary walk progress words ({records, values} per page, read by the fused expansion
-  // before the page's flag is set) start at zero in every launch
-#ifdef PQG_WALK_PROGRESS
-  if (P->dict_fused && (P->cls_n[C_DICT4] || P->cls_n[C_DICT8] || P->cls_n[C_IDS]) &&
-      hipMemsetAsync(P->pstat.p, 0, sizeof(uint64_t) * (size_t)std::max(P->n_pages, 1), s) != hipSuccess)
-    return PQG_ERR_HIP;
-#endif
-  if (++P->epoch == 0) {  // page ready flags compare against the launch epoch; reset on wrap
-    P->epoch = 1;
+  // page ready flags compare against the launch epoch (even); a walker's early partial status is
+  // flagged epoch - 1. Reset on wrap.
+  P->epoch += 2;
+  if (P->epoch == 0) {
+    P->epoch = 2;
     if (hipMemsetAsync(P->flags.p, 0, sizeof(uint32_t) * (size_t)std::max(P->n_pages, 1), s) != hipSuccess)
       return PQG_ERR_HIP;
   }

@@ -597,6 +597,11 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
 #ifndef PQG_PJ_LARGE
 #define PQG_PJ_LARGE 1
 #endif
+// early partial hand-off after the walker's first window (off: C2 181.5 vs 172.6 us per launch,
+// profiles/r02/early_ab — the extra wait on the walker's stores costs more than early chunks gain)
+#ifndef PQG_EARLY
+#define PQG_EARLY 0
+#endif
 __device__ __forceinline__ void handoff_release() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a compiler barrier too (invisible to the waitcnt pass)
 }
@@ -620,8 +625,12 @@ template <int W, bool SMALL = true>
 __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg,
                                              uint32_t sec_end, int w, uint64_t* rec, uint32_t* chunk_run,
                                              uint32_t CH, uint32_t sh, int page, uint64_t* err, ErrCount err_count,
-                                             uint32_t& n_rec, uint32_t& n_ok, uint64_t* prog) {
+                                             uint32_t& n_rec, uint32_t& n_ok, uint64_t* prog, uint32_t* pflag,
+                                             uint32_t pepoch) {
   const uint32_t lane = lane_id();
+#if PQG_EARLY
+  bool first = true;
+#endif
   // successor table (256 x u16) and reached flags (256 x u8) over L.ent; every access goes
   // through may_alias types (u16 gathers vs u64 row writes must not be reordered)
 #if !PQG_WALK_CHAIN
@@ -799,14 +808,19 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
     }
     k += uni(n_em);
     produced += total;
-#ifdef PQG_WALK_PROGRESS  // experimental, off: correct but slower in the A/B
-    // progress for the fused expansion: records [0, k) cover values [0, produced) and are in
-    // memory (chunks inside that range may start before the page's flag is set)
-    if (prog && produced < N) {
-      wave_sync();
-      if (lane == 0)
-        __hip_atomic_store(prog, (uint64_t)k | ((uint64_t)produced << 32), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#if PQG_EARLY
+    // early hand-off after the first window: records [0, k) cover values [0, produced); the page's
+    // flag goes to epoch - 1 (odd: never a full epoch, never the zeroed initial flag) with that
+    // partial status, so the expansion chunks inside [0, produced) start before the walk ends
+    if (first && pflag && produced < N) {
+      handoff_release();
+      if (lane == 0) {
+        sst(prog, (uint64_t)k | ((uint64_t)produced << 32));
+        handoff_release();
+        sst(pflag, pepoch - 1u);
+      }
     }
+    first = false;
 #endif
     DIAG_ADD(d_emit, t_emit);
 #ifdef PQG_DIAG
@@ -1226,13 +1240,13 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
         // SMALL: the whole data section sits in the LDS segment: the walk has no global load
         if (sec_end - win.seg_lo + 264u <= SEG_BYTES)  // every window inside the segment
           dict_walk_pj<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok,
-                          pstat + page);
+                          pstat + page, flags + page, epoch);
 #if PQG_PJ_LARGE
         // larger sections: the same window walk, the LDS segment refilled as the chain advances
         // (windows inside long bit-packed runs are jumped over, not pre-decoded)
         else
           dict_walk_pj<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec,
-                                 n_ok, pstat + page);
+                                 n_ok, pstat + page, flags + page, epoch);
 #else
         else if (sec_end - win.seg_lo <= SEG_BYTES)
           dict_walk<W, true>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
@@ -1422,16 +1436,23 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
           pst = uni64(sld(pstat + page));
           break;
         }
-  #ifdef PQG_WALK_PROGRESS  // experimental, off: correct but slower in the A/B
-        const uint32_t sh0 = (uint32_t)(pw.out_offset % (uint64_t)E), nv = uni(pw.n_values);
-        const uint32_t need = ((j + 1) * CH < nv + sh0 ? (j + 1) * CH : nv + sh0) - sh0;
-        const uint64_t pp = uni64(sld(pstat + page));
-        if ((uint32_t)(pp >> 32) >= need) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // record loads after the status load
-          pst = pp;
-          break;
+#if PQG_EARLY
+        // the walker's partial status (flag epoch - 1): go when it covers this chunk's values;
+        // the status may already be the final one (stored before the final flag), never an older one
+        if (uni(sld(flags + page)) == epoch - 1u) {
+          const uint32_t sh0 = (uint32_t)(pw.out_offset % (uint64_t)E), nv = uni(pw.n_values);
+          const uint32_t need = ((j + 1) * CH < nv + sh0 ? (j + 1) * CH : nv + sh0) - sh0;
+          handoff_acquire();
+          const uint64_t pp = uni64(sld(pstat + page));
+          if ((uint32_t)(pp >> 32) >= need) {
+#ifdef PQG_DIAG
+            rt_x1 = __builtin_amdgcn_s_memrealtime();
+#endif
+            pst = pp;
+            break;
+          }
         }
-  #endif
+#endif
         __builtin_amdgcn_s_sleep(PQG_SPIN_SLEEP);
         // wall-clock bound (s_memrealtime: constant 100 MHz): a walker that never publishes
         // (descheduled, starved) turns into PQG_ERR_TIMEOUT after SPIN_TIMEOUT_TICKS, not a hang
