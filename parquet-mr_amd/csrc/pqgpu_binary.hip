@@ -125,6 +125,9 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
 #ifndef PQG_BW_COMPACT_LOOP
 #define PQG_BW_COMPACT_LOOP 1
 #endif
+#ifndef PQG_BW_LIFT
+#define PQG_BW_LIFT 1
+#endif
 #ifndef PQG_COPY_REL32
 #define PQG_COPY_REL32 1
 #endif
@@ -291,10 +294,33 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
       const uint32_t run = ~next1 ? (uint32_t)__builtin_ctzll(~next1) : WAVE - 1u;
       last = run;
       mask = last == WAVE - 1u ? ~0ull : ((1ull << (last + 1u)) - 1ull);
+#if PQG_BW_LIFT
+      if (rdl(J, last) < WAVE) {
+        // the chain goes on past a false candidate (e.g. the byte before a length prefix, whose
+        // shifted "length" fits the page): successors increase, so lane l is on the chain from
+        // lane 0 iff binary lifting from lane 0 over the jump tables J^(2^r) stops exactly at l
+        uint32_t P[6];
+        P[0] = J;
+#pragma unroll
+        for (int r = 1; r < 6; r++) {
+          const uint32_t g = (uint32_t)__shfl((int)P[r - 1], (int)(P[r - 1] & (WAVE - 1u)));
+          P[r] = P[r - 1] < WAVE ? g : WAVE;
+        }
+        uint32_t x = 0;
+#pragma unroll
+        for (int r = 5; r >= 0; r--) {
+          const uint32_t y = (uint32_t)__shfl((int)P[r], (int)x);
+          if (y <= lane) x = y;
+        }
+        mask = __ballot(x == lane);
+        last = 63u - (uint32_t)__builtin_clzll(mask);
+      }
+#else
       for (uint32_t j = rdl(J, last); j < WAVE; j = rdl(J, j)) {
         mask |= 1ull << j;
         last = j;
       }
+#endif
       const uint32_t n_acc = (uint32_t)__builtin_popcountll(mask);
       const uint32_t room = N - produced - got;
       const uint32_t take = uni(n_acc < room ? n_acc : room);
@@ -452,34 +478,52 @@ __device__ __forceinline__ uint64_t block_reduce_u64(uint64_t v, uint64_t* red) 
   return t;
 }
 
+// A block of SCAN_BLOCK lengths is read as 4 rows of 1,024: in row i thread t holds lengths
+// [i * 1024 + 4t, i * 1024 + 4t + 4) (one 16-byte load when the lengths are 16-byte aligned).
+static_assert(SCAN_BLOCK == 4096, "scan block layout: 4 rows x 256 threads x 4 lengths");
+__device__ __forceinline__ u32x4 scan_row_load(const uint32_t* blen, uint64_t n_slots, uint64_t v) {
+  if (v + 4 <= n_slots && ((uintptr_t)(blen + v) & 15u) == 0)
+    return *(const __attribute__((address_space(1))) u32x4*)(blen + v);
+  u32x4 x;
+#pragma unroll
+  for (int k = 0; k < 4; k++) x[k] = v + k < n_slots ? blen[v + k] : 0u;
+  return x;
+}
+
 __global__ __launch_bounds__(256) void k_bin_block_sums(const ColumnDev* __restrict__ cols,
                                                         const uint64_t* __restrict__ blocks) {
   __shared__ uint64_t red[4];
   const uint64_t b = blocks[blockIdx.x];
   const ColumnDev& cd = cols[(uint32_t)(b >> 32)];
   const uint64_t v0 = (uint64_t)(uint32_t)b * SCAN_BLOCK;
+  u32x4 x[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) x[i] = scan_row_load(cd.blen, cd.n_slots, v0 + 1024u * i + 4u * threadIdx.x);
   uint64_t s = 0;
-  for (uint32_t i = threadIdx.x; i < SCAN_BLOCK; i += 256) {
-    const uint64_t v = v0 + i;
-    if (v < cd.n_slots) s += cd.blen[v];
-  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) s += (uint64_t)x[i][0] + x[i][1] + (uint64_t)x[i][2] + x[i][3];
   s = block_reduce_u64(s, red);
   if (threadIdx.x == 0) cd.block_sums[(uint32_t)b] = s;
 }
 
 // One workgroup per BYTE_ARRAY column: exclusive scan of its block sums (in place) + total.
+// Each thread scans 16 consecutive sums serially: one wave scan and one barrier pair per 4,096.
 __global__ __launch_bounds__(256) void k_bin_block_bases(const ColumnDev* __restrict__ cols,
                                                          const int32_t* __restrict__ bin_cols) {
   __shared__ uint64_t wsum[4];
-  __shared__ uint64_t carry;
   const ColumnDev& cd = cols[bin_cols[blockIdx.x]];
   const uint32_t nb = (uint32_t)((cd.n_slots + SCAN_BLOCK - 1) / SCAN_BLOCK);
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
-    const uint32_t b = b0 + threadIdx.x;
-    const uint64_t v = b < nb ? cd.block_sums[b] : 0;
-    uint64_t x = v;
+  uint64_t* bs = cd.block_sums;
+  uint64_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += 16u * 256u) {
+    const uint32_t bt = b0 + 16u * threadIdx.x;
+    uint64_t v[16], s = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      v[k] = bt + k < nb ? bs[bt + k] : 0;
+      s += v[k];
+    }
+    uint64_t x = s;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint64_t y = __shfl_up(x, o);
@@ -487,44 +531,85 @@ __global__ __launch_bounds__(256) void k_bin_block_bases(const ColumnDev* __rest
     }
     if (lane_id() == 63) wsum[threadIdx.x >> 6] = x;
     __syncthreads();
-    uint64_t pre = carry;
-    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) pre += wsum[w];
-    if (b < nb) cd.block_sums[b] = pre + x - v;
-    __syncthreads();
-    if (threadIdx.x == 255) carry = pre + x;
+    uint64_t pre = carry, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; w++) {
+      pre += w < (threadIdx.x >> 6) ? wsum[w] : 0;
+      tot += wsum[w];
+    }
+    pre += x - s;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      if (bt + k < nb) bs[bt + k] = pre;
+      pre += v[k];
+    }
+    carry += tot;
     __syncthreads();
   }
   if (threadIdx.x == 0) *cd.bin_total = carry;
 }
 
+// Offsets of one scan block: per row, a wave scan of the threads' 4-length sums and the wave
+// totals through LDS (4 rows scanned side by side: one barrier per block instead of two per
+// 256 lengths); offsets stored as two 16-byte stores per row and thread.
 __global__ __launch_bounds__(256) void k_bin_offsets(const ColumnDev* __restrict__ cols,
                                                      const uint64_t* __restrict__ blocks) {
-  __shared__ uint64_t wsum[4];
-  __shared__ uint64_t carry;
+  __shared__ uint64_t wsum[4][4];  // [row][wave]
   const uint64_t b = blocks[blockIdx.x];
   const ColumnDev& cd = cols[(uint32_t)(b >> 32)];
   const uint64_t v0 = (uint64_t)(uint32_t)b * SCAN_BLOCK;
+  const uint64_t n_slots = cd.n_slots;
   int64_t* off = (int64_t*)cd.values;
-  if (threadIdx.x == 0) carry = cd.block_sums[(uint32_t)b];
-  __syncthreads();
-  for (uint32_t i0 = 0; i0 < SCAN_BLOCK; i0 += 256) {
-    const uint64_t v = v0 + i0 + threadIdx.x;
-    const uint64_t len = v < cd.n_slots ? cd.blen[v] : 0;
-    uint64_t x = len;
+  const uint32_t t = threadIdx.x, wv = t >> 6, lane = lane_id();
+  u32x4 x[4];
+  uint64_t inc[4];
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint64_t y = __shfl_up(x, o);
-      if ((int)lane_id() >= o) x += y;
+  for (int i = 0; i < 4; i++) {
+    x[i] = scan_row_load(cd.blen, n_slots, v0 + 1024u * i + 4u * t);
+    inc[i] = (uint64_t)x[i][0] + x[i][1] + (uint64_t)x[i][2] + x[i][3];
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint64_t y = __shfl_up(inc[i], o);
+      if ((int)lane >= o) inc[i] += y;
     }
-    if (lane_id() == 63) wsum[threadIdx.x >> 6] = x;
-    __syncthreads();
-    uint64_t pre = carry;
-    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) pre += wsum[w];
-    if (v < cd.n_slots) gst(off + v, (int64_t)(pre + x - len));
-    if (v + 1 == cd.n_slots) gst(off + v + 1, (int64_t)(pre + x));
-    __syncthreads();
-    if (threadIdx.x == 255) carry = pre + x;
-    __syncthreads();
+  }
+  if (lane == 63) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) wsum[i][wv] = inc[i];
+  }
+  __syncthreads();
+  uint64_t base = cd.block_sums[(uint32_t)b];
+  const bool vec = ((uintptr_t)off & 15u) == 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint64_t pre = base;
+    uint64_t row = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; w++) {
+      pre += w < wv ? wsum[i][w] : 0;
+      row += wsum[i][w];
+    }
+    base += row;
+    // exclusive offsets of this thread's 4 lengths
+    uint64_t e0 = pre + inc[i] - ((uint64_t)x[i][0] + x[i][1] + (uint64_t)x[i][2] + x[i][3]);
+    const uint64_t e1 = e0 + x[i][0], e2 = e1 + x[i][1], e3 = e2 + x[i][2], e4 = e3 + x[i][3];
+    const uint64_t v = v0 + 1024u * i + 4u * t;
+    if (vec && v + 4 <= n_slots) {
+      typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+      gst((i64x2*)(off + v), i64x2{(int64_t)e0, (int64_t)e1});
+      gst((i64x2*)(off + v + 2), i64x2{(int64_t)e2, (int64_t)e3});
+    } else {
+      const uint64_t e[4] = {e0, e1, e2, e3};
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (v + k < n_slots) gst(off + v + k, (int64_t)e[k]);
+    }
+    // the final offset (the column's byte total) after the last slot
+    if (v < n_slots && n_slots <= v + 4) gst(off + n_slots, (int64_t)(n_slots - v == 1 ? e1 : n_slots - v == 2 ? e2
+                                                                     : n_slots - v == 3 ? e3 : e4));
   }
 }
 

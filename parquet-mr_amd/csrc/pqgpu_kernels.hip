@@ -599,6 +599,9 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
 #endif
 // early partial hand-off after the walker's first window (off: C2 181.5 vs 172.6 us per launch,
 // profiles/r02/early_ab — the extra wait on the walker's stores costs more than early chunks gain)
+#ifndef PQG_LEVELS_BITS
+#define PQG_LEVELS_BITS 1
+#endif
 #ifndef PQG_EARLY
 #define PQG_EARLY 0
 #endif
@@ -1782,6 +1785,19 @@ __device__ __forceinline__ void expand_level_tiles(const LevelWaveLds& L, const 
   const rsrc_t rs = win.rs;
   const uint32_t lane = lane_id();
   const int64_t mis = out ? (int64_t)((uintptr_t)out & 15u) : 0;
+#if PQG_LEVELS_BITS
+  // width 1 with every RLE value 0 or 1 (the usual flat optional column): the tile's 16 levels
+  // are built as a 16-bit mask (3 operations per piece) and spread to bytes once per tile
+  bool bits_ok = false;
+  if constexpr (WB == 1) {
+    bool bad = false;
+    for (uint32_t i = lane; i < n_run; i += WAVE) {
+      const uint32_t p = L.r_pay[i];
+      bad |= !(p & 0x80000000u) && p > 1u;
+    }
+    bits_ok = !__ballot(bad);
+  }
+#endif
   for (int64_t t = (((int64_t)s_lo + mis) & ~(int64_t)15) - mis; t < (int64_t)s_hi; t += 16 * WAVE) {
     const int64_t s0 = t + 16 * (int64_t)lane;
     if (s0 + 16 <= (int64_t)s_lo || s0 >= (int64_t)s_hi) continue;
@@ -1795,6 +1811,58 @@ __device__ __forceinline__ void expand_level_tiles(const LevelWaveLds& L, const 
     }
     uint32_t acc[4] = {0u, 0u, 0u, 0u};
     uint32_t cur = lo_s, k = a;
+#if PQG_LEVELS_BITS
+    if (WB == 1 && bits_ok) {
+      uint32_t m = 0;  // bit j: level of tile slot j
+      while (cur < hi_s) {
+        const uint32_t st = L.r_start[k], pay = L.r_pay[k];
+        const uint32_t re = k + 1 < n_run ? L.r_start[k + 1] : s_hi;
+        const uint32_t stop = hi_s < re ? hi_s : re;
+        const uint32_t jb = cur - (uint32_t)s0, je = stop - (uint32_t)s0;
+        const uint32_t pm = ((1u << je) - 1u) & ~((1u << jb) - 1u);
+        uint32_t bits;
+        if (!(pay & 0x80000000u)) {
+          bits = pay ? 0xFFFFu : 0u;
+        } else {
+          // 32 bits of the run's data from slot cur on (bytes at or past the read end are 0)
+          const uint32_t rlo = pay & 0x7FFFFFFFu, rhi = L.r_end[k];
+          const uint32_t bp = cur - st, byte0 = rlo + (bp >> 3), a4 = byte0 & ~3u;
+          uint32_t y0, y1;
+          if (seg_has(win, a4, 8u)) {
+            y0 = seg32(win, a4);
+            y1 = seg32(win, a4 + 4u);
+          } else {
+            y0 = ld32(rs, a4);
+            y1 = ld32(rs, a4 + 4u);
+          }
+          const int32_t k0 = (int32_t)rhi - (int32_t)a4, k1 = k0 - 4;
+          y0 &= k0 >= 4 ? 0xFFFFFFFFu : (k0 <= 0 ? 0u : (1u << (8 * k0)) - 1u);
+          y1 &= k1 >= 4 ? 0xFFFFFFFFu : (k1 <= 0 ? 0u : (1u << (8 * k1)) - 1u);
+          const uint32_t z = __builtin_amdgcn_alignbyte(y1, y0, byte0 & 3u);
+          bits = (z >> (bp & 7u)) << jb;
+        }
+        m = (m & ~pm) | (bits & pm);
+        cur = stop;
+        k++;
+      }
+#pragma unroll
+      for (uint32_t c = 0; c < 4; c++) acc[c] = (((m >> (4u * c)) & 0xFu) * 0x204081u) & 0x01010101u;
+      const uint32_t j0 = lo_s - (uint32_t)s0, j1 = hi_s - (uint32_t)s0;
+      const uint32_t jm = ((1u << j1) - 1u) & ~((1u << j0) - 1u);
+      if (count_nonnull) cnt += max_def == 1 ? __builtin_popcount(m & jm) : max_def == 0 ? __builtin_popcount(~m & jm) : 0;
+      if (out) {
+        uint8_t* o = out + s0;
+        if (j0 == 0 && j1 == 16) {
+          gst((u32x4*)o, u32x4{acc[0], acc[1], acc[2], acc[3]});
+        } else {
+#pragma unroll
+          for (uint32_t j = 0; j < 16; j++)
+            if (j >= j0 && j < j1) gst(o + j, (uint8_t)(acc[j >> 2] >> (8 * (j & 3))));
+        }
+      }
+      continue;
+    }
+#endif
     while (cur < hi_s) {
       const uint32_t st = L.r_start[k], pay = L.r_pay[k];
       const uint32_t re = k + 1 < n_run ? L.r_start[k + 1] : s_hi;
