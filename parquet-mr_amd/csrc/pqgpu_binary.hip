@@ -131,6 +131,15 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
 #ifndef PQG_COPY_REL32
 #define PQG_COPY_REL32 1
 #endif
+#ifndef PQG_COPY_BTAB
+#define PQG_COPY_BTAB 1
+#endif
+#if PQG_COPY_BTAB
+constexpr uint32_t COPY_BTAB = 320;  // block table entries per wave (chunks of up to 5 KiB)
+#endif
+#ifndef PQG_COPY_PERM
+#define PQG_COPY_PERM 1
+#endif
 #ifndef PQG_COPY_COMPOSE
 #define PQG_COPY_COMPOSE 1
 #endif
@@ -650,6 +659,9 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
   __shared__ uint64_t off_all[WPB][BIN_CHUNK + 1];
   __shared__ uint32_t src_all[WPB][BIN_CHUNK];
   __shared__ uint32_t rel_all[WPB][BIN_CHUNK + 1];
+#if PQG_COPY_BTAB
+  __shared__ uint32_t bt_all[WPB][COPY_BTAB];
+#endif
   const uint32_t c = blockIdx.x * WPB + wave_id();
   if (c >= n_chunks) return;
   uint64_t* off = off_all[wave_id()];
@@ -720,6 +732,37 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
     const uint32_t src0 = src[0];
     const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
     uint32_t kv = 0;
+#if PQG_COPY_BTAB
+    // value of every 16-byte block's first byte, when the chunk spans at most COPY_BTAB blocks:
+    // bt[j] = the last value starting at or before byte 16j (a value starting inside block j - 1
+    // is entered at index ceil(rel / 16), then a running maximum), instead of a binary search
+    // per block
+    uint32_t* bt = bt_all[wave_id()];
+    const uint32_t nblk = (r_hi + 15u) >> 4;
+    const bool btab = nblk <= COPY_BTAB;
+    if (btab) {
+      for (uint32_t i = lane; i < nblk; i += WAVE) bt[i] = 0;
+      wave_sync();
+      for (uint32_t k = lane; k < n; k += WAVE) {
+        const uint32_t blk = (rel[k] + 15u) >> 4;
+        if (blk < nblk) atomicMax(&bt[blk], k);
+      }
+      wave_sync();
+      uint32_t carry = 0;
+      for (uint32_t i0 = 0; i0 < nblk; i0 += WAVE) {
+        uint32_t v = i0 + lane < nblk ? bt[i0 + lane] : 0u;
+        v = v > carry ? v : carry;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(v, o);
+          if ((int)lane >= o) v = v > y ? v : y;
+        }
+        if (i0 + lane < nblk) bt[i0 + lane] = v;
+        carry = uni(rdl(v, WAVE - 1));
+      }
+      wave_sync();
+    }
+#endif
     for (uint32_t bg = 16u * lane; bg < r_hi; bg += 16u * WAVE * G) {
       uint32_t wd[G][4];
       uint32_t have[G];
@@ -730,6 +773,12 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
         wd[g][0] = wd[g][1] = wd[g][2] = wd[g][3] = 0;
         if (b >= r_hi) continue;
         const uint32_t b0 = b > r_lo ? b : r_lo;
+#if PQG_COPY_BTAB
+        if (btab) {
+          kv = bt[b >> 4];
+        } else
+#endif
+        {
         uint32_t lo = kv, hi = n;
         while (hi - lo > 1) {
           const uint32_t mid = (lo + hi) >> 1;
@@ -737,6 +786,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
           else hi = mid;
         }
         kv = lo;
+        }
         const uint32_t bend = b + 16u < r_hi ? b + 16u : r_hi;
 #if PQG_COPY_COMPOSE
         // PLAIN / DLBA: the block's source is one stream with a 4-byte hole (PLAIN) at every value
@@ -767,6 +817,24 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
 #pragma unroll
           for (uint32_t q = 0; q < 4; q++) {
             uint32_t word = 0;
+#if PQG_COPY_PERM
+            // the dword's bytes come from a[q + c0] and, after at most one value start inside
+            // it, a[q + c0 + 1]: one v_perm with the byte selector of the start
+            const uint32_t cq = (uint32_t)(prof >> (16u * q)) & 0xFFFFu;  // counts of bytes 4q .. 4q+3
+            const uint32_t c0 = cq & 0xFu;
+            const uint32_t dn = cq - c0 * 0x1111u;  // nibbles: 0, or 1 from the start on
+            if (dn <= 0x1111u && (dn & 0xEEEEu) == 0) {
+              uint32_t A0 = a[q], A1 = a[q + 1];
+#pragma unroll
+              for (uint32_t t = 1; t <= 4; t++) {
+                A0 = c0 == t ? a[q + t < 8 ? q + t : 7] : A0;
+                A1 = c0 == t ? a[q + t + 1 < 8 ? q + t + 1 : 7] : A1;
+              }
+              const uint32_t hb = (dn & 1u) | ((dn & 0x10u) << 4) | ((dn & 0x100u) << 8) | ((dn & 0x1000u) << 12);
+              word = __builtin_amdgcn_perm(A1, A0, 0x03020100u + 4u * hb);
+            } else
+#endif
+            {
 #pragma unroll
             for (uint32_t e = 0; e < 4; e++) {
               const uint32_t c = (uint32_t)(prof >> (4u * (4u * q + e))) & 0xFu;  // 0..4
@@ -776,6 +844,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
               v = c == 3u ? a[q + 3] : v;
               v = c == 4u ? a[q + 4] : v;
               word |= v & (0xFFu << (8u * e));
+            }
             }
             const uint32_t d0 = b + 4u * q;
             wd[g][q] = word;
