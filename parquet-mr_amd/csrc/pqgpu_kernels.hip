@@ -605,6 +605,10 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
 #ifndef PQG_EARLY
 #define PQG_EARLY 0
 #endif
+// list walk (dict_walk_ls) instead of the mark-word chain of dict_walk_pj
+#ifndef PQG_WALK_LIST
+#define PQG_WALK_LIST 1
+#endif
 __device__ __forceinline__ void handoff_release() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a compiler barrier too (invisible to the waitcnt pass)
 }
@@ -875,6 +879,170 @@ __device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32
     d[6] = k;
   }
 #endif
+}
+
+// Saturating inclusive scan over the wave: lane l gets min(v_0 + ... + v_l, cap) (every v <= cap <
+// 2^31). DPP row shifts and row broadcasts, no LDS round trip; call with all 64 lanes active.
+__device__ __forceinline__ uint32_t wave_incl_scan_sat(uint32_t x, uint32_t cap) {
+#define PQG_DPP_SAT(ctrl, rmask)                                                                \
+  {                                                                                             \
+    const uint32_t y_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, rmask, 0xf, true); \
+    x = x + y_ < cap ? x + y_ : cap;                                                            \
+  }
+  PQG_DPP_SAT(0x111, 0xf)  // row_shr:1
+  PQG_DPP_SAT(0x112, 0xf)  // row_shr:2
+  PQG_DPP_SAT(0x114, 0xf)  // row_shr:4
+  PQG_DPP_SAT(0x118, 0xf)  // row_shr:8
+  PQG_DPP_SAT(0x142, 0xa)  // row_bcast:15 -> rows 1, 3
+  PQG_DPP_SAT(0x143, 0xc)  // row_bcast:31 -> rows 2, 3
+#undef PQG_DPP_SAT
+  return x;
+}
+
+// List walk: the same windows and pre-decode as dict_walk_pj, with the window's chain and its
+// records built without per-position masks.
+//   chain    the successors of a lane's 4 positions are packed into one dword (byte b: window
+//            offset of the successor of position 4 * lane + b, 0 = the chain stops there — a
+//            successor is always past its header, so 0 is free); each step is one v_readlane, a
+//            byte extract and one lane select that appends the position to a list VGPR (lane t =
+//            t-th header of the batch): one loop branch per run, no per-position mark words.
+//   records  lane t reads its header's count / payload from an LDS table (one 8-byte entry per
+//            window position), a saturating DPP scan gives the first values, and lane t stores
+//            record k + t: one store per run instead of a ballot compaction over 256 positions.
+// A window with more than 64 headers on its chain is taken in several batches.
+// Semantics are those of dict_walk_pj (readNext :80-109, the scalar slow path for long varints,
+// 0 / huge group counts and headers crossing the section end).
+template <int W, bool SMALL = true>
+__device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg,
+                                             uint32_t sec_end, int w, uint64_t* rec, uint32_t* chunk_run,
+                                             uint32_t CH, uint32_t sh, int page, uint64_t* err, ErrCount err_count,
+                                             uint32_t& n_rec, uint32_t& n_ok) {
+  typedef uint64_t __attribute__((may_alias)) u64a;
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  typedef u64x2 __attribute__((may_alias)) u64x2a;
+  const uint32_t lane = lane_id();
+  uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
+  uint32_t produced = 0, k = 0;
+  int code = 0;
+  auto put_record = [&](uint32_t start, uint32_t end, uint32_t payload) {
+    if (lane == 0) {
+      sst(rec + k, (uint64_t)start | ((uint64_t)payload << 32));
+      uint32_t j = start == 0 ? 0 : (start + sh + CH - 1) / CH;
+      for (; j * CH < end + sh; j++) sst(chunk_run + j, k);
+    }
+    k++;
+  };
+  while (true) {
+    pos = uni(pos);
+    produced = uni(produced);
+    k = uni(k);
+    if (produced >= N) break;
+    if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
+    const uint32_t B = pos & ~3u;
+    predecode<SMALL>(win, B, w);
+    uint32_t js = 0, nn[4], slowm = 0, inm = 0;
+    uint64_t ent[4];
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const uint32_t p = B + 4u * lane + b;
+      const uint32_t f = (win.flg >> (8u * b)) & 0xFFu;
+      const uint32_t hl = f >> 2;
+      const uint32_t nx = win.nxt[b];
+      const bool in = p < sec_end;
+      const bool slow = in && ((f & 2u) || p + hl > sec_end || (!(f & 1u) && nx > sec_end));
+      nn[b] = (f & 1u) ? (nx < sec_end ? nx : sec_end) : nx;  // packed: readFully of what is left
+      const uint32_t j = (!in || slow || nn[b] - B >= 256u) ? 0u : nn[b] - B;
+      js |= j << (8u * b);
+      slowm |= (slow ? 1u : 0u) << b;
+      inm |= (in ? 1u : 0u) << b;
+      ent[b] = (uint64_t)win.val[b] | ((uint64_t)(win.cnt[b] | ((f & 1u) << 31)) << 32);
+    }
+    wave_sync();  // the previous window's table reads are done
+    ((u64x2a*)L.ent)[2u * lane] = u64x2{ent[0], ent[1]};
+    ((u64x2a*)L.ent)[2u * lane + 1u] = u64x2{ent[2], ent[3]};
+    wave_sync();
+    uint32_t q = pos - B, nq = 0;
+    while (true) {  // batches of at most 64 chain positions
+      uint32_t t = 0, lst = 0;
+      while (true) {
+        q = uni(q);
+        lst = lane == t ? q : lst;  // v_cmp + v_cndmask
+        nq = (rdl(js, q >> 2) >> ((q & 3u) << 3)) & 0xFFu;
+        t++;
+        if (nq == 0u || t == (uint32_t)WAVE) break;
+        q = nq;
+      }
+      t = uni(t);
+      nq = uni(nq);
+      // the batch's last position q ends the chain here (nq == 0): a run only when it is a
+      // fast-path header inside the section (otherwise the scalar path below takes it)
+      const uint32_t ql = q >> 2, qb = q & 3u;
+      const bool last_run = nq != 0u || (!((rdl(slowm, ql) >> qb) & 1u) && ((rdl(inm, ql) >> qb) & 1u));
+      const uint32_t n_v = last_run ? t : t - 1u;
+      const uint32_t cap = N - produced;
+      uint32_t c = 0, payload = 0;
+      if (lane < n_v) {
+        const uint64_t e = ((const u64a*)L.ent)[lst];
+        const uint32_t cw = (uint32_t)(e >> 32), vv = (uint32_t)e;
+        const bool pk = cw >> 31;
+        c = cw & 0x7FFFFFFFu;
+        if (!pk && c == 0) c = cap;  // Java: currentCount goes negative, the value repeats forever
+        c = c < cap ? c : cap;
+        payload = pk ? (0x80000000u | vv) : (vv > 0x7FFFFFFFu ? 0x7FFFFFFFu : vv);
+      }
+      const uint32_t inc = wave_incl_scan_sat(c, cap);
+      uint32_t st = __shfl_up(inc, 1);
+      if (lane == 0) st = 0;
+      const uint32_t total = uni(rdl(inc, WAVE - 1));
+      // emitted: the runs that start before the cap (a prefix of the lanes)
+      const bool em = c > 0u && st < cap;
+      const uint32_t n_em = uni((uint32_t)__builtin_popcountll(__ballot(em)));
+      if (em) {
+        const uint32_t s_abs = produced + st;
+        const uint32_t e_abs = produced + (st + c < cap ? st + c : cap);
+        sst(rec + k + lane, (uint64_t)s_abs | ((uint64_t)payload << 32));
+        uint32_t j = s_abs == 0 ? 0 : (s_abs + sh + CH - 1) / CH;
+        for (; j * CH < e_abs + sh; j++) sst(chunk_run + j, k + lane);
+      }
+      k = uni(k + n_em);
+      produced = uni(produced + total);
+      if (produced >= N || nq == 0u) break;
+      q = nq;  // the chain goes on inside this window: next batch
+    }
+    if (produced >= N) break;
+    // continue after the window's last chain position q
+    const uint32_t ql = q >> 2, qb = q & 3u;
+    const uint32_t q_slow = (rdl(slowm, ql) >> qb) & 1u;
+    const uint32_t q_in = (rdl(inm, ql) >> qb) & 1u;
+    if (!q_in) {
+      pos = B + q;  // at or past the section end: RLE_PAST_END on the next iteration
+    } else if (!q_slow) {
+      pos = pick4(nn, qb, ql);  // leaves the window
+    } else {
+      // scalar re-decode of the header at q (readNext :80-109)
+      pos = B + q;
+      uint32_t hl, m, nxs, vv;
+      uint64_t cnt64;
+      code = SMALL ? slow_header_g([&](uint32_t p) { return uni((seg32(win, p & ~3u) >> ((p & 3u) * 8u)) & 0xFFu); },
+                                   pos, sec_end, w, hl, m, cnt64, vv, nxs)
+                   : slow_header_g([&](uint32_t p) { return wbyte(win, p); }, pos, sec_end, w, hl, m, cnt64, vv, nxs);
+      if (code) break;
+      if (m == 0 && nxs > sec_end) { code = PQG_ERR_EOF; break; }
+      uint64_t cnt = cnt64;
+      const uint32_t left = N - produced;
+      if (m == 0 && cnt == 0) cnt = left;
+      const uint32_t take = cnt < left ? (uint32_t)cnt : left;
+      put_record(produced, produced + take, m ? (0x80000000u | vv) : (vv > 0x7FFFFFFFu ? 0x7FFFFFFFu : vv));
+      produced += take;
+      pos = m ? (nxs < sec_end ? nxs : sec_end) : nxs;
+    }
+  }
+  if (code) {
+    if (lane == 0) report(err, err_count, page, 2, produced, code);
+    N = produced;
+  }
+  n_rec = k;
+  n_ok = N;
 }
 
 // ---- One WORKGROUP per page: the page's run headers ranked over 2048-byte super-windows.
@@ -1241,6 +1409,13 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
         uint64_t* prec = rec + pw.rec_base;
         uint32_t* pcr = chunk_run + pw.chunk_base;
         // SMALL: the whole data section sits in the LDS segment: the walk has no global load
+#if PQG_WALK_LIST && !PQG_EARLY
+        if (sec_end - win.seg_lo + 264u <= SEG_BYTES)  // every window inside the segment
+          dict_walk_ls<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
+        else
+          dict_walk_ls<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec,
+                                 n_ok);
+#else
         if (sec_end - win.seg_lo + 264u <= SEG_BYTES)  // every window inside the segment
           dict_walk_pj<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok,
                           pstat + page, flags + page, epoch);
@@ -1255,6 +1430,7 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
           dict_walk<W, true>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
         else
           dict_walk<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
+#endif
 #endif
       }
     }
