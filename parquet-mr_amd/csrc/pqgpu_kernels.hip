@@ -92,7 +92,10 @@ __device__ __forceinline__ uint32_t seg32(const PreWin& pw, uint32_t a) {  // a 
 
 // LDS_ONLY: the caller guarantees the whole section is in the segment (no refill,
 // no global load: the hot loop then never waits on vmcnt, which would drain stores).
-template <bool LDS_ONLY = false>
+// FAST: headers of at most 4 bytes are parsed branch-free from the position's first dword; a
+// 5-byte header (a count / group number of 2^27 or more) is marked slow and left to the scalar
+// path, so an RLE value (<= 4 bytes) always lies inside the 8 bytes at the position.
+template <bool LDS_ONLY = false, bool FAST = false>
 __device__ __forceinline__ void predecode(PreWin& pw, uint32_t B, int w) {
   pw.B = B;
   const uint32_t base = B + 4u * lane_id();
@@ -120,7 +123,14 @@ __device__ __forceinline__ void predecode(PreWin& pw, uint32_t B, int w) {
                    b3 = (uint32_t)(x >> 24) & 0xFFu, b4 = (uint32_t)(x >> 32) & 0xFFu;
     // readUnsignedVarInt, Java int semantics, up to 5 bytes here (longer: slow path)
     uint32_t v = b0 & 0x7Fu, hl = 1, slow = 0;
-    if (b0 & 0x80u) {
+    if constexpr (FAST) {
+      const uint32_t d = (uint32_t)x, stop = ~d & 0x80808080u;  // stop bit of each of 4 bytes
+      slow = stop == 0u;
+      hl = stop ? ((uint32_t)__builtin_ctz(stop) >> 3) + 1u : 4u;
+      const uint32_t dm = d & (0xFFFFFFFFu >> (32u - 8u * hl));
+      v = (dm & 0x7Fu) | ((dm >> 1) & 0x3F80u) | ((dm >> 2) & 0x1FC000u) | ((dm >> 3) & 0xFE00000u);
+      (void)b1; (void)b2; (void)b3; (void)b4;
+    } else if (b0 & 0x80u) {
       v |= (b1 & 0x7Fu) << 7; hl = 2;
       if (b1 & 0x80u) {
         v |= (b2 & 0x7Fu) << 14; hl = 3;
@@ -136,7 +146,7 @@ __device__ __forceinline__ void predecode(PreWin& pw, uint32_t B, int w) {
     uint32_t nx, c, vv, pk;
     if ((v & 1u) == 0) {  // RLE: count, then ceil(w/8) little-endian bytes, not masked
       const uint32_t sh = 8u * hl;
-      const uint64_t y = (x >> sh) | ((uint64_t)hi8 << (64u - sh));
+      const uint64_t y = FAST ? x >> sh : (x >> sh) | ((uint64_t)hi8 << (64u - sh));
       vv = nb == 4 ? (uint32_t)y : (uint32_t)y & ((1u << (8u * nb)) - 1u);
       c = v >> 1;
       nx = p + hl + nb;
@@ -609,6 +619,14 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
 #ifndef PQG_WALK_LIST
 #define PQG_WALK_LIST 1
 #endif
+// list walk: two chain steps per iteration (successor-of-successor table, PQG_WALK_J2) and the
+// branch-free 4-byte header parse (PQG_PRE_FAST)
+#ifndef PQG_WALK_J2
+#define PQG_WALK_J2 0
+#endif
+#ifndef PQG_PRE_FAST
+#define PQG_PRE_FAST 0
+#endif
 __device__ __forceinline__ void handoff_release() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a compiler barrier too (invisible to the waitcnt pass)
 }
@@ -939,7 +957,7 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
     if (produced >= N) break;
     if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
     const uint32_t B = pos & ~3u;
-    predecode<SMALL>(win, B, w);
+    predecode<SMALL, (bool)PQG_PRE_FAST>(win, B, w);
     uint32_t js = 0, nn[4], slowm = 0, inm = 0;
     uint64_t ent[4];
 #pragma unroll
@@ -961,9 +979,35 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
     ((u64x2a*)L.ent)[2u * lane] = u64x2{ent[0], ent[1]};
     ((u64x2a*)L.ent)[2u * lane + 1u] = u64x2{ent[2], ent[3]};
     wave_sync();
+#if PQG_WALK_J2
+    // successor of the successor of each position (0: the chain stops within two steps)
+    uint32_t js2 = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const uint32_t j = (js >> (8u * b)) & 0xFFu;
+      const uint32_t src = (uint32_t)__shfl((int)js, (int)(j >> 2));
+      js2 |= (j ? (src >> ((j & 3u) << 3)) & 0xFFu : 0u) << (8u * b);
+    }
+#endif
     uint32_t q = pos - B, nq = 0;
     while (true) {  // batches of at most 64 chain positions
       uint32_t t = 0, lst = 0;
+#if PQG_WALK_J2
+      while (true) {  // two positions per step: q and its successor n1
+        q = uni(q);
+        t = uni(t);
+        const uint32_t l = q >> 2, sb = (q & 3u) << 3;
+        const uint32_t n1 = (rdl(js, l) >> sb) & 0xFFu;
+        const uint32_t n2 = (rdl(js2, l) >> sb) & 0xFFu;
+        lst = lane == t ? q : lst;
+        lst = lane == t + 1u ? n1 : lst;  // past the batch when n1 == 0 (not read)
+        if (n1 == 0u) { t += 1u; nq = 0u; break; }
+        if (n2 == 0u) { t += 2u; q = n1; nq = 0u; break; }
+        t += 2u;
+        if (t == (uint32_t)WAVE) { q = n1; nq = n2; break; }
+        q = n2;
+      }
+#else
       while (true) {
         q = uni(q);
         lst = lane == t ? q : lst;  // v_cmp + v_cndmask
@@ -972,6 +1016,7 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
         if (nq == 0u || t == (uint32_t)WAVE) break;
         q = nq;
       }
+#endif
       t = uni(t);
       nq = uni(nq);
       // the batch's last position q ends the chain here (nq == 0): a run only when it is a
@@ -2806,6 +2851,14 @@ __global__ __launch_bounds__(64 * WPB) void k_rle_bool(const uint8_t* __restrict
 // every few dozen blocks. Reading the page with global loads between the blocks' stores costs
 // a full store drain per block (vmcnt counts stores on CDNA).
 constexpr uint32_t DSEG = 8192;
+// segment expansion (delta_expand_seg) for miniblocks of a multiple of 16 deltas
+#ifndef PQG_DELTA_SEG
+#define PQG_DELTA_SEG 1
+#endif
+// block headers parsed by the vector unit (delta_hdr_v)
+#ifndef PQG_DELTA_VHDR
+#define PQG_DELTA_VHDR 1
+#endif
 
 struct DSeg {
   rsrc_t rs;
@@ -2962,6 +3015,92 @@ __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_
   }
 }
 
+// Segment expansion of nb walked blocks whose miniblocks hold a multiple of 16 deltas (parquet-mr
+// and Arrow write 128 / 4, i.e. 32 per miniblock): lane l of a step takes segment g = 64 * step + l
+// of the batch — 16 consecutive deltas of one miniblock of block g / (block / 16) — unpacks them
+// from the LDS segment at its own bit position, keeps their running sums in registers, and one
+// 64-bit DPP scan of the 64 segment sums gives every segment its base: 1,024 deltas per scan and
+// per carry step instead of one block (delta_expand: 64 * E). Values, the minDelta addition
+// (loadNewBlockToBuffer :139-142, also for the unread miniblocks of a last block, whose values lie
+// past the count and are not stored) and the store layout are those of delta_expand: lane l stores
+// the 16 values ending one delta earlier (the first from lane l - 1 / the carry), as wide stores
+// when the run is aligned. Not for NEG streams (DELTA_LENGTH lengths check every value).
+template <int W>
+__device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uint32_t b_data, uint32_t b_wpos,
+                                                 uint32_t b_lo, uint32_t b_hi, uint32_t b_nmb, uint32_t blk_first,
+                                                 uint32_t block, uint32_t mbs, uint32_t n_out, uint64_t& carry,
+                                                 typename DictVal<W>::T* out) {
+  typedef typename DictVal<W>::T T;
+  constexpr uint32_t L = 16;
+  const uint32_t lane = lane_id();
+  const uint32_t SB = block / L;  // segments per block
+  const uint32_t n_seg = nb * SB;
+  const uint32_t mb_bytes = mbs / 8u;  // bytes per bit of width
+  const bool wide = (((uintptr_t)out + (uint64_t)(blk_first - 1) * sizeof(T)) % 16) == 0 &&
+                    ((uint64_t)block * sizeof(T)) % 16 == 0;
+  for (uint32_t g0 = 0; g0 < n_seg; g0 += WAVE) {
+    const uint32_t g = g0 + lane;
+    const bool lane_in = g < n_seg;
+    const uint32_t bb = lane_in ? g / SB : 0u;
+    const uint32_t j0 = (g - bb * SB) * L;  // the segment's first delta in its block
+    const uint32_t m = j0 / mbs, jm = j0 - m * mbs;
+    const uint32_t data = (uint32_t)__shfl((int)b_data, (int)bb), wpos = (uint32_t)__shfl((int)b_wpos, (int)bb);
+    const uint32_t nmb = (uint32_t)__shfl((int)b_nmb, (int)bb);
+    const uint64_t mind = ((uint64_t)(uint32_t)__shfl((int)b_hi, (int)bb) << 32) | (uint32_t)__shfl((int)b_lo, (int)bb);
+    // the block's miniblock widths (<= 8 bytes at wpos), the lane's width and data offset
+    const uint32_t wa = wpos & ~3u, sb = wpos & 3u;
+    const uint32_t y0 = S.w32(wa), y1 = S.w32(wa + 4), y2 = S.w32(wa + 8);
+    const uint32_t wlo = __builtin_amdgcn_alignbyte(y1, y0, sb), whi = __builtin_amdgcn_alignbyte(y2, y1, sb);
+    const uint32_t wl = m < nmb ? ((m < 4u ? wlo >> (8u * m) : whi >> (8u * (m - 4u))) & 0xFFu) : 0u;
+    const uint32_t blo = m >= 4u ? wlo : (m ? wlo & ((1u << (8u * m)) - 1u) : 0u);
+    const uint32_t bhi = m <= 4u ? 0u : whi & ((1u << (8u * (m - 4u))) - 1u);
+    const uint32_t dbase = data + (__builtin_amdgcn_sad_u8(blo, 0u, 0u) + __builtin_amdgcn_sad_u8(bhi, 0u, 0u)) * mb_bytes;
+    const uint64_t mask = wl == 64 ? ~0ull : ((1ull << wl) - 1ull);
+    const bool narrow = !__ballot(lane_in && wl > 32u);  // every width <= 32: two dwords per delta
+    uint64_t loc[L];
+    uint64_t sum = 0;
+    uint32_t bit = jm * wl;
+#pragma unroll
+    for (uint32_t q = 0; q < L; q++) {
+      uint64_t d = 0;
+      if (wl) {
+        const uint32_t byte = dbase + (bit >> 3);
+        const uint32_t a = byte & ~3u;
+        const uint32_t sh = (byte - a) * 8u + (bit & 7u);  // < 32
+        const uint64_t lo64 = (uint64_t)S.w32(a) | ((uint64_t)S.w32(a + 4) << 32);
+        if (narrow) {
+          d = (lo64 >> sh) & mask;
+        } else {
+          const uint32_t x2 = S.w32(a + 8);
+          d = (sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)))) & mask;
+        }
+      }
+      sum += lane_in ? d + mind : 0ull;
+      loc[q] = sum;
+      bit += wl;
+    }
+    const uint64_t x = wave_incl_scan_u64(sum);
+    const uint64_t base_v = carry + (x - sum);
+    const uint64_t last = base_v + loc[L - 1];
+    const uint32_t plo = (uint32_t)__shfl_up((int)(uint32_t)last, 1), phi = (uint32_t)__shfl_up((int)(uint32_t)(last >> 32), 1);
+    const uint64_t prev = lane == 0 ? carry : (((uint64_t)phi << 32) | plo);
+    const uint64_t k0 = (uint64_t)blk_first - 1u + (uint64_t)bb * block + j0;  // index of the run's first value
+    T u[L];
+#pragma unroll
+    for (uint32_t q = 0; q < L; q++) u[q] = (T)(q == 0 ? prev : base_v + loc[q - 1]);
+    if (lane_in) {
+      if (wide && k0 + L <= n_out) {
+        store_run<T, L>(out + k0, u);
+      } else {
+#pragma unroll
+        for (uint32_t q = 0; q < L; q++)
+          if (k0 + q < n_out) gst(out + k0 + q, u[q]);
+      }
+    }
+    carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
+  }
+}
+
 // Any other DeltaBinaryPackingConfig the reference accepts (blocks of more than 512 values or more
 // than 8 miniblocks; DuckDB writes 2048 / 8): block by block, miniblock by miniblock, 64 deltas
 // per step, page bytes read with buffer loads. Same checks, in the same order, as the batched walk
@@ -3046,6 +3185,58 @@ __device__ int delta_generic(const rsrc_t rs, uint32_t p, uint32_t end, uint32_t
   return 0;
 }
 
+// Block header (loadNewBlockToBuffer :118-143: zigzag varlong min delta, readBitWidthsForMiniBlocks,
+// the used miniblocks' byte count) parsed by the VECTOR unit at uniform p: every lane computes the
+// same values from its LDS copy of 28 bytes (laundered into VGPRs so the compiler keeps the
+// arithmetic off the scalar unit, which the CU's four SIMDs share: the scalar walk issued ~230
+// SALU instructions per 128-value block and made k_delta scalar-issue bound). Covers the common
+// case — a min delta of at most 8 varint bytes, every used width <= 64, header and data inside the
+// section — and returns false otherwise, so the scalar walk raises the reference's error.
+struct DeltaHdr {
+  uint32_t wpos, dpos, next, used, dbytes;
+  uint64_t mind;
+};
+__device__ __forceinline__ bool delta_hdr_v(const DSeg& S, uint32_t p, uint32_t end, uint32_t mbn, uint32_t mbs,
+                                            uint32_t buffered, uint32_t total, DeltaHdr& h) {
+  const uint32_t a = p & ~3u, sb = p & 3u;
+  if (!S.has(a, 28)) return false;
+  uint32_t d[7];
+#pragma unroll
+  for (int i = 0; i < 7; i++) d[i] = S.w32(a + 4u * i);
+  asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]));
+  uint32_t x[6];
+#pragma unroll
+  for (int i = 0; i < 6; i++) x[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sb);  // bytes p + 4i ..
+  const uint64_t lo = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+  const uint64_t stop = ~lo & 0x8080808080808080ull;  // the varint's last byte has bit 7 clear
+  const uint32_t len = stop ? ((uint32_t)__builtin_ctzll(stop) >> 3) + 1u : 9u;
+  const uint64_t v = len >= 8u ? lo : lo & ((1ull << (8u * len)) - 1ull);
+  const uint64_t raw = (v & 0x7Full) | ((v >> 1) & (0x7Full << 7)) | ((v >> 2) & (0x7Full << 14)) |
+                       ((v >> 3) & (0x7Full << 21)) | ((v >> 4) & (0x7Full << 28)) | ((v >> 5) & (0x7Full << 35)) |
+                       ((v >> 6) & (0x7Full << 42)) | ((v >> 7) & (0x7Full << 49));
+  h.mind = (raw >> 1) ^ (0ull - (raw & 1ull));  // zigzag
+  h.wpos = p + len;
+  // the <= 8 width bytes: bytes [len, len + 8) of x
+  const uint32_t q = len >> 2, r = len & 3u;
+  const uint32_t xa = q == 0 ? x[0] : (q == 1 ? x[1] : x[2]);
+  const uint32_t xb = q == 0 ? x[1] : (q == 1 ? x[2] : x[3]);
+  const uint32_t xc = q == 0 ? x[2] : (q == 1 ? x[3] : x[4]);
+  uint32_t wl = __builtin_amdgcn_alignbyte(xb, xa, r), wh = __builtin_amdgcn_alignbyte(xc, xb, r);
+  // miniblocks unpacked while buffered < total (:131-135)
+  const uint32_t rem = total - buffered;  // > 0
+  const uint32_t used = rem >= mbn * mbs ? mbn : (rem + mbs - 1u) / mbs;  // a page's last block only
+  wl &= used >= 4u ? 0xFFFFFFFFu : (1u << (8u * used)) - 1u;
+  wh &= used <= 4u ? 0u : (used == 8u ? 0xFFFFFFFFu : (1u << (8u * (used - 4u))) - 1u);
+  // a used width > 64 (bit 7 set, or low 7 bits >= 65): the scalar walk reports CORRUPT
+  const uint32_t bad = (((wl & 0x7F7F7F7Fu) + 0x3F3F3F3Fu) | wl | ((wh & 0x7F7F7F7Fu) + 0x3F3F3F3Fu) | wh) & 0x80808080u;
+  h.used = used;
+  h.dbytes = (__builtin_amdgcn_sad_u8(wl, 0u, 0u) + __builtin_amdgcn_sad_u8(wh, 0u, 0u)) * (mbs / 8u);
+  h.dpos = h.wpos + mbn;
+  h.next = h.dpos + h.dbytes;
+  const bool ok = len <= 8u && !bad && (uint64_t)h.dpos + h.dbytes <= end;  // (implies p + len, wpos + mbn <= end)
+  return uni(ok ? 1u : 0u) != 0u;
+}
+
 // One stream [p, end) -> out[0 .. min(want, total)). Returns 0 or the init error code (the
 // reader decodes eagerly in initFromPage); *p_end = stream position after the used miniblocks,
 // *total_out = the header's value count. NEG: a negative (int) value is reported as CORRUPT at
@@ -3123,6 +3314,25 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
       if (nb >= 64u || buffered >= total) break;
       if (p >= end) return PQG_ERR_EOF;
       if (!S.has(p, HDR_SPAN)) break;  // nb > 0 here: the batch ends, the next one refills
+#if PQG_DELTA_VHDR
+      {
+        DeltaHdr h;
+        if (delta_hdr_v(S, p, end, mbn, mbs, buffered, total, h)) {
+          // the block's data (+ read slack) must be staged, else the block starts the next batch
+          if (!S.has(uni(h.dpos), uni(h.dbytes) + 12u)) break;
+          const bool me = lane == nb;
+          b_data = me ? h.dpos : b_data;
+          b_wpos = me ? h.wpos : b_wpos;
+          b_lo = me ? (uint32_t)h.mind : b_lo;
+          b_hi = me ? (uint32_t)(h.mind >> 32) : b_hi;
+          b_nmb = me ? h.used : b_nmb;
+          p = uni(h.next);
+          buffered = uni(buffered + h.used * mbs);
+          nb++;
+          continue;
+        }
+      }
+#endif
       const uint64_t mraw = seg_uvar<false>(S, p, end - p, len);  // loadNewBlockToBuffer :122-126
       if ((uint64_t)p + len > end) return PQG_ERR_EOF;
       const int64_t mind = zigzag64(mraw);
@@ -3155,7 +3365,9 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     }
     if (nb == 0) return PQG_ERR_CORRUPT;  // unreachable: the first block of a batch always fits
     // ---- expand the walked blocks (every read from the LDS segment)
-    if (E == 1) delta_expand<W, NEG, 1>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
+    if (PQG_DELTA_SEG && !NEG && (mbs % 16u) == 0)
+      delta_expand_seg<W>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out);
+    else if (E == 1) delta_expand<W, NEG, 1>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else if (E == 2) delta_expand<W, NEG, 2>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else if (E == 4) delta_expand<W, NEG, 4>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else delta_expand<W, NEG, 8>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
