@@ -627,6 +627,11 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
 #ifndef PQG_PRE_FAST
 #define PQG_PRE_FAST 0
 #endif
+// list walk: the chain followed by the vector unit (ds_bpermute per run) instead of v_readlane + SALU
+// (measured equal on C2 and 1 % slower on Zipf(2.0): profiles/r02/walk_ls/vchain; off)
+#ifndef PQG_WALK_VCHAIN
+#define PQG_WALK_VCHAIN 0
+#endif
 __device__ __forceinline__ void handoff_release() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a compiler barrier too (invisible to the waitcnt pass)
 }
@@ -1006,6 +1011,26 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
         t += 2u;
         if (t == (uint32_t)WAVE) { q = n1; nq = n2; break; }
         q = n2;
+      }
+#elif PQG_WALK_VCHAIN
+      {
+        // the chain on the vector unit: q stays in a VGPR (the same value in every lane) and each
+        // step is one ds_bpermute broadcast of the successor dword + a byte extract. The scalar
+        // form (v_readlane + ~15 SALU per run) made Zipf(2.0) walks (~40 runs per window)
+        // scalar-issue bound: the CU's walkers share one scalar unit
+        uint32_t qv = q, tv = 0, nqv = 0;
+        asm volatile("" : "+v"(qv));
+        while (true) {
+          lst = lane == tv ? qv : lst;
+          const uint32_t src = (uint32_t)__shfl((int)js, (int)(qv >> 2));
+          nqv = (src >> ((qv & 3u) << 3)) & 0xFFu;
+          tv++;
+          if (nqv == 0u || tv == (uint32_t)WAVE) break;
+          qv = nqv;
+        }
+        q = uni(qv);
+        t = uni(tv);
+        nq = uni(nqv);
       }
 #else
       while (true) {
@@ -3365,7 +3390,10 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     }
     if (nb == 0) return PQG_ERR_CORRUPT;  // unreachable: the first block of a batch always fits
     // ---- expand the walked blocks (every read from the LDS segment)
-    if (PQG_DELTA_SEG && !NEG && (mbs % 16u) == 0)
+    // (the segment path stores 16-value runs per lane: only where they are 16-byte aligned; a
+    // page of a nullable column starts at any value offset, and per-element stores of lane-private
+    // runs measured slower than delta_expand's lane-interleaved ones)
+    if (PQG_DELTA_SEG && !NEG && (mbs % 16u) == 0 && ((uintptr_t)out % 16u) == 0 && ((uint64_t)block * W) % 16u == 0)
       delta_expand_seg<W>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out);
     else if (E == 1) delta_expand<W, NEG, 1>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else if (E == 2) delta_expand<W, NEG, 2>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
