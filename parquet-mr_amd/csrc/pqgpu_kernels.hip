@@ -3131,13 +3131,19 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
 // per step, page bytes read with buffer loads. Same checks, in the same order, as the batched walk
 // below (loadNewBlockToBuffer :118-143): widths of the used miniblocks (> 64: CORRUPT), then
 // their bytes (EOF). p = position after the header; the first value is already stored.
+// Every byte comes from the wave's LDS segment (refilled when a header or a 64-delta step leaves
+// it): a global load between the steps' stores would wait for all of them (vmcnt counts stores),
+// one drain per 64 values; with the segment it is one drain per 8 KiB of page bytes.
 template <int W, bool NEG>
-__device__ int delta_generic(const rsrc_t rs, uint32_t p, uint32_t end, uint32_t block, uint32_t mbn, uint32_t mbs,
+__device__ int delta_generic(DSeg& S, uint32_t p, uint32_t end, uint32_t block, uint32_t mbn, uint32_t mbs,
                              uint32_t total, uint32_t n_out, uint64_t carry, typename DictVal<W>::T* out, int page,
                              uint64_t* err, ErrCount err_count, uint32_t* p_end) {
   typedef typename DictVal<W>::T T;
   const uint32_t lane = lane_id();
-  auto byte_at = [&](uint32_t a) -> uint32_t { return uni((ld32(rs, a & ~3u) >> (8u * (a & 3u))) & 0xFFu); };
+  auto byte_at = [&](uint32_t a) -> uint32_t {
+    if (!S.has(a & ~3u, 4)) S.fill(a);
+    return uni((S.w32(a & ~3u) >> (8u * (a & 3u))) & 0xFFu);
+  };
   uint32_t buffered = 1;
   uint64_t k_next = 1;  // value index after the next delta
   while (true) {
@@ -3179,10 +3185,13 @@ __device__ int delta_generic(const rsrc_t rs, uint32_t p, uint32_t end, uint32_t
       for (uint32_t c = 0; c < mbs; c += WAVE) {
         const uint32_t q = c + lane;
         const bool in = q < mbs;
+        // the step's bytes [mo + c*w/8, mo + (c+64)*w/8 + 12) staged (<= 524 bytes)
+        const uint32_t s_lo = (mo + ((c * w) >> 3)) & ~3u, s_hi = mo + (((c + WAVE) * w + 7u) >> 3) + 12u;
+        if (w && !S.has(s_lo, s_hi - s_lo)) S.fill(s_lo);
         uint64_t d = 0;
         if (in && w) {
           const uint32_t bit = q * w, byte = mo + (bit >> 3), a = byte & ~3u;
-          const uint32_t x0 = ld32(rs, a), x1 = ld32(rs, a + 4), x2 = ld32(rs, a + 8);
+          const uint32_t x0 = S.w32(a), x1 = S.w32(a + 4), x2 = S.w32(a + 8);
           const uint32_t sh = (byte - a) * 8u + (bit & 7u);
           const uint64_t lo64 = (uint64_t)x0 | ((uint64_t)x1 << 32);
           d = (sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)))) & mask;
@@ -3314,7 +3323,7 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
   // register budget of the batched expansion: block <= 512 values, <= 8 miniblocks (parquet-mr
   // and Arrow write 128 / 4); other configurations take the block-by-block path
   if (block > 512u || mbn > 8u)
-    return delta_generic<W, NEG>(S.rs, p, end, block, mbn, mbs, total, n_out, carry, out, page, err, err_count, p_end);
+    return delta_generic<W, NEG>(S, p, end, block, mbn, mbs, total, n_out, carry, out, page, err, err_count, p_end);
   uint32_t buffered = 1;  // Java valuesBuffered (includes the first value)
   uint32_t n_blocks = 0;
   // deltas per lane per block: the power of two >= block / 64 (it divides the block, a multiple

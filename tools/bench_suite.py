@@ -13,6 +13,7 @@ bench.py prints the ONE headline line (C2). This suite times the other configs a
   str_plain / str_dict / str_dlba / str_dba   BYTE_ARRAY encodings, 4-32 byte strings
   bss_f64        BYTE_STREAM_SPLIT doubles
   delta_i64      DELTA_BINARY_PACKED int64 random walk
+  delta_i64_2048 the same values with 2048-value blocks of 8 miniblocks (DuckDB's writer; the block-by-block path)
 
 value = non-null values decoded per second; gbps = algorithmic bytes (encoded page bytes read +
 decoded values / offsets / bytes written + level bytes written) / launch time. cpu = the oracle
@@ -88,6 +89,10 @@ def gen(name, rows):
     if name == "delta_i64":
         walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
         return WL.Workload(name, [writer.write_column_chunk(abi.INT64, walk, abi.DELTA_BINARY_PACKED)], [E(walk)])
+    if name == "delta_i64_2048":  # the same values in DuckDB's DELTA configuration (blocks of 2048, 8 miniblocks)
+        walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
+        return WL.Workload(name, [writer.write_column_chunk(abi.INT64, walk, abi.DELTA_BINARY_PACKED, delta_block=2048,
+                                                            delta_miniblocks=8)], [E(walk)])
     raise ValueError(name)
 
 
@@ -230,7 +235,8 @@ def run(name, rows, steps, warmup, cpu_budget):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("workloads", nargs="*", default=["c1_plain_i32", "c2_zipf2", "c3_mixed", "c5_levels", "str_plain",
-                                                     "str_dict", "str_dlba", "str_dba", "bss_f64", "delta_i64"])
+                                                     "str_dict", "str_dlba", "str_dba", "bss_f64", "delta_i64",
+                                                     "delta_i64_2048"])
     ap.add_argument("--rows", type=int, default=None, help="override the per-workload row count")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
@@ -240,6 +246,7 @@ def main():
     default_rows = {"c1_plain_i32": 1_000_000, "c2_zipf2": 100_000_000, "c3_mixed": 100_000_000,
                     "c5_levels": 100_000_000, "str_plain": 20_000_000, "str_dict": 20_000_000,
                     "str_dlba": 20_000_000, "str_dba": 20_000_000, "bss_f64": 100_000_000, "delta_i64": 100_000_000,
+                    "delta_i64_2048": 100_000_000,
                     "c2_snappy": 100_000_000, "plain_i64_snappy": 100_000_000,
                     "c2_zstd": 100_000_000, "plain_i64_zstd": 100_000_000,
                     "c4_lineitem": 8_000_000}
