@@ -3219,42 +3219,40 @@ __device__ int delta_generic(DSeg& S, uint32_t p, uint32_t end, uint32_t block, 
   return 0;
 }
 
-// Block header (loadNewBlockToBuffer :118-143: zigzag varlong min delta, readBitWidthsForMiniBlocks,
-// the used miniblocks' byte count) parsed by the VECTOR unit at uniform p: every lane computes the
-// same values from its LDS copy of 28 bytes (laundered into VGPRs so the compiler keeps the
-// arithmetic off the scalar unit, which the CU's four SIMDs share: the scalar walk issued ~230
-// SALU instructions per 128-value block and made k_delta scalar-issue bound). Covers the common
-// case — a min delta of at most 8 varint bytes, every used width <= 64, header and data inside the
+// Block header chain step (loadNewBlockToBuffer :118-143: zigzag varlong min delta,
+// readBitWidthsForMiniBlocks, the used miniblocks' byte count) on the VECTOR unit at uniform p:
+// every lane computes the same values from its LDS copy of 20 bytes (laundered into VGPRs so the
+// compiler keeps the arithmetic off the scalar unit, which the CU's four SIMDs share: the scalar
+// walk issued ~230 SALU instructions per 128-value block and made k_delta scalar-issue bound).
+// Only what the NEXT header's position needs is on this serial path — the varint's length (stop-bit
+// mask + ctz), the used widths' byte sum (v_sad_u8) — the min delta's value is decoded afterwards
+// by the block's own lane (delta_mind_v), all blocks of a batch at once. Covers the common case —
+// a min delta of at most 8 varint bytes, every used width <= 64, header and data inside the
 // section — and returns false otherwise, so the scalar walk raises the reference's error.
 struct DeltaHdr {
-  uint32_t wpos, dpos, next, used, dbytes;
-  uint64_t mind;
+  uint32_t len, wpos, dpos, next, used, dbytes;
 };
 __device__ __forceinline__ bool delta_hdr_v(const DSeg& S, uint32_t p, uint32_t end, uint32_t mbn, uint32_t mbs,
                                             uint32_t buffered, uint32_t total, DeltaHdr& h) {
   const uint32_t a = p & ~3u, sb = p & 3u;
-  if (!S.has(a, 28)) return false;
-  uint32_t d[7];
+  if (!S.has(a, 20)) return false;
+  uint32_t d[5];
 #pragma unroll
-  for (int i = 0; i < 7; i++) d[i] = S.w32(a + 4u * i);
-  asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]));
-  uint32_t x[6];
+  for (int i = 0; i < 5; i++) d[i] = S.w32(a + 4u * i);
+  asm volatile("" : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]));
+  uint32_t x[4];
 #pragma unroll
-  for (int i = 0; i < 6; i++) x[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sb);  // bytes p + 4i ..
+  for (int i = 0; i < 4; i++) x[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sb);  // bytes p + 4i ..
   const uint64_t lo = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
   const uint64_t stop = ~lo & 0x8080808080808080ull;  // the varint's last byte has bit 7 clear
   const uint32_t len = stop ? ((uint32_t)__builtin_ctzll(stop) >> 3) + 1u : 9u;
-  const uint64_t v = len >= 8u ? lo : lo & ((1ull << (8u * len)) - 1ull);
-  const uint64_t raw = (v & 0x7Full) | ((v >> 1) & (0x7Full << 7)) | ((v >> 2) & (0x7Full << 14)) |
-                       ((v >> 3) & (0x7Full << 21)) | ((v >> 4) & (0x7Full << 28)) | ((v >> 5) & (0x7Full << 35)) |
-                       ((v >> 6) & (0x7Full << 42)) | ((v >> 7) & (0x7Full << 49));
-  h.mind = (raw >> 1) ^ (0ull - (raw & 1ull));  // zigzag
+  h.len = len;
   h.wpos = p + len;
-  // the <= 8 width bytes: bytes [len, len + 8) of x
+  // the <= 8 width bytes: bytes [len, len + 8) of x (len == 8: x[2], x[3])
   const uint32_t q = len >> 2, r = len & 3u;
   const uint32_t xa = q == 0 ? x[0] : (q == 1 ? x[1] : x[2]);
   const uint32_t xb = q == 0 ? x[1] : (q == 1 ? x[2] : x[3]);
-  const uint32_t xc = q == 0 ? x[2] : (q == 1 ? x[3] : x[4]);
+  const uint32_t xc = q == 0 ? x[2] : x[3];
   uint32_t wl = __builtin_amdgcn_alignbyte(xb, xa, r), wh = __builtin_amdgcn_alignbyte(xc, xb, r);
   // miniblocks unpacked while buffered < total (:131-135)
   const uint32_t rem = total - buffered;  // > 0
@@ -3269,6 +3267,19 @@ __device__ __forceinline__ bool delta_hdr_v(const DSeg& S, uint32_t p, uint32_t 
   h.next = h.dpos + h.dbytes;
   const bool ok = len <= 8u && !bad && (uint64_t)h.dpos + h.dbytes <= end;  // (implies p + len, wpos + mbn <= end)
   return uni(ok ? 1u : 0u) != 0u;
+}
+
+// The min delta of a block whose header delta_hdr_v walked: zigzag varlong of `len` (<= 8) bytes at
+// hp (readZigZagVarLong), decoded by the block's lane from the LDS segment.
+__device__ __forceinline__ uint64_t delta_mind_v(const DSeg& S, uint32_t hp, uint32_t len) {
+  const uint32_t a = hp & ~3u, sb = hp & 3u;
+  const uint32_t d0 = S.w32(a), d1 = S.w32(a + 4), d2 = S.w32(a + 8);
+  const uint64_t lo = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sb) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sb) << 32);
+  const uint64_t v = len >= 8u ? lo : lo & ((1ull << (8u * len)) - 1ull);
+  const uint64_t raw = (v & 0x7Full) | ((v >> 1) & (0x7Full << 7)) | ((v >> 2) & (0x7Full << 14)) |
+                       ((v >> 3) & (0x7Full << 21)) | ((v >> 4) & (0x7Full << 28)) | ((v >> 5) & (0x7Full << 35)) |
+                       ((v >> 6) & (0x7Full << 42)) | ((v >> 7) & (0x7Full << 49));
+  return (raw >> 1) ^ (0ull - (raw & 1ull));  // zigzag
 }
 
 // One stream [p, end) -> out[0 .. min(want, total)). Returns 0 or the init error code (the
@@ -3338,7 +3349,7 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     // a batch starts with its first block fully staged (a block is <= 4126 bytes)
     if (!S.has(p, DSEG / 2 + 64)) S.fill(p);
     // ---- walk up to 64 blocks whose bytes lie in the segment (headers + data offsets)
-    uint32_t b_data = 0, b_wpos = 0, b_lo = 0, b_hi = 0, b_nmb = 0;
+    uint32_t b_data = 0, b_wpos = 0, b_lo = 0, b_hi = 0, b_nmb = 0, b_mv = 0;
     uint32_t nb = 0;
     const uint32_t blk_first = buffered;
     while (true) {
@@ -3357,8 +3368,9 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
           const bool me = lane == nb;
           b_data = me ? h.dpos : b_data;
           b_wpos = me ? h.wpos : b_wpos;
-          b_lo = me ? (uint32_t)h.mind : b_lo;
-          b_hi = me ? (uint32_t)(h.mind >> 32) : b_hi;
+          b_lo = me ? p : b_lo;  // header position and varint length: the min delta follows below
+          b_hi = me ? h.len : b_hi;
+          b_mv = me ? 1u : b_mv;
           b_nmb = me ? h.used : b_nmb;
           p = uni(h.next);
           buffered = uni(buffered + h.used * mbs);
@@ -3398,6 +3410,15 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
       nb++;
     }
     if (nb == 0) return PQG_ERR_CORRUPT;  // unreachable: the first block of a batch always fits
+#if PQG_DELTA_VHDR
+    // min deltas of the blocks delta_hdr_v walked, one lane per block (the segment holds them: it is
+    // refilled only at a batch start)
+    if (b_mv) {
+      const uint64_t md = delta_mind_v(S, b_lo, b_hi);
+      b_lo = (uint32_t)md;
+      b_hi = (uint32_t)(md >> 32);
+    }
+#endif
     // ---- expand the walked blocks (every read from the LDS segment)
     // (the segment path stores 16-value runs per lane: only where they are 16-byte aligned; a
     // page of a nullable column starts at any value offset, and per-element stores of lane-private
