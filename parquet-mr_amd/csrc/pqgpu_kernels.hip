@@ -2020,6 +2020,34 @@ __device__ __forceinline__ uint32_t tile_byte_mask(int32_t jb, int32_t je, int32
   return mh & ~ml;
 }
 
+// Run holding slot lo_s: the largest a < n_run (<= 256) with r_start[a] <= lo_s (r_start ascending,
+// r_start[0] <= lo_s). PQG_LEVELS_FIXED_SEARCH: eight fixed steps with unconditional LDS reads
+// instead of the divergent bisection loop (whose exec bookkeeping runs on the scalar unit):
+// measured C3 10.01 -> 10.10 ms, C5 2.17 -> 2.19 ms (profiles/r02/lv_ab), so off.
+#ifndef PQG_LEVELS_FIXED_SEARCH
+#define PQG_LEVELS_FIXED_SEARCH 0
+#endif
+__device__ __forceinline__ uint32_t level_run_of(const LevelWaveLds& L, uint32_t n_run, uint32_t lo_s) {
+#if PQG_LEVELS_FIXED_SEARCH
+  uint32_t a = 0;
+#pragma unroll
+  for (uint32_t step = 128; step >= 1; step >>= 1) {
+    const uint32_t i = a + step;
+    const uint32_t v = L.r_start[i < n_run ? i : n_run - 1u];
+    a = (i < n_run && v <= lo_s) ? i : a;
+  }
+  return a;
+#else
+  uint32_t a = 0, b = n_run;
+  while (b - a > 1) {
+    const uint32_t mid = (a + b) >> 1;
+    if (L.r_start[mid] <= lo_s) a = mid;
+    else b = mid;
+  }
+  return a;
+#endif
+}
+
 // Bit width WB (1..8) specialisation of expand_level_runs: per tile piece (the part of one run
 // inside the lane's 16 slots) the 16 levels are formed without a per-slot loop: an RLE piece is
 // its value replicated, a packed piece is 24 bytes at the piece's bit offset, shifted once, then
@@ -2049,12 +2077,7 @@ __device__ __forceinline__ void expand_level_tiles(const LevelWaveLds& L, const 
     if (s0 + 16 <= (int64_t)s_lo || s0 >= (int64_t)s_hi) continue;
     const uint32_t lo_s = (uint32_t)(s0 > (int64_t)s_lo ? s0 : (int64_t)s_lo);
     const uint32_t hi_s = (uint32_t)(s0 + 16 < (int64_t)s_hi ? s0 + 16 : (int64_t)s_hi);
-    uint32_t a = 0, b = n_run;
-    while (b - a > 1) {
-      const uint32_t mid = (a + b) >> 1;
-      if (L.r_start[mid] <= lo_s) a = mid;
-      else b = mid;
-    }
+    const uint32_t a = level_run_of(L, n_run, lo_s);
     uint32_t acc[4] = {0u, 0u, 0u, 0u};
     uint32_t cur = lo_s, k = a;
 #if PQG_LEVELS_BITS
@@ -2214,12 +2237,7 @@ __device__ __forceinline__ void expand_level_runs_generic(const LevelWaveLds& L,
     const uint32_t lo_s = (uint32_t)(s0 > (int64_t)s_lo ? s0 : (int64_t)s_lo);
     const uint32_t hi_s = (uint32_t)(s0 + 16 < (int64_t)s_hi ? s0 + 16 : (int64_t)s_hi);
     // run holding lo_s: last k with r_start[k] <= lo_s
-    uint32_t a = 0, b = n_run;
-    while (b - a > 1) {
-      const uint32_t mid = (a + b) >> 1;
-      if (L.r_start[mid] <= lo_s) a = mid;
-      else b = mid;
-    }
+    const uint32_t a = level_run_of(L, n_run, lo_s);
     uint64_t wlo = 0, whi = 0;
     uint32_t cur = lo_s, k = a;
     while (cur < hi_s) {
