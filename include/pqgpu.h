@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PQG_ABI_VERSION 1
+#define PQG_ABI_VERSION 2
 
 /* parquet-format `Type` values (parquet.thrift). */
 enum pqg_physical_type {
@@ -404,11 +404,26 @@ uint32_t pqg_crc32(uint32_t crc, const uint8_t* data, uint64_t n);
 int pqg_frame_chunk(const uint8_t* chunk, uint64_t chunk_len, int64_t value_count, int verify_crc,
                     pqg_page_header* headers, int capacity, int* n_headers, pqg_status* st);
 
-/* Headers of an UNCOMPRESSED chunk placed at byte `chunk_offset` of a batch buffer -> the
- * pqg_page_desc entries of its data pages (column index `column`) and the dictionary fields of
- * `col` (may be NULL). A compressed page -> PQG_ERR_UNSUPPORTED (decompress first). */
-int pqg_pages_from_headers(const pqg_page_header* headers, int n_headers, uint64_t chunk_offset, int column,
-                           pqg_column_desc* col, pqg_page_desc* pages, int capacity, int* n_pages, pqg_status* st);
+/* ColumnMetaData.codec (parquet.thrift CompressionCodec; CompressionCodecName in parquet-mr). */
+enum pqg_codec {
+  PQG_CODEC_UNCOMPRESSED = 0, PQG_CODEC_SNAPPY = 1, PQG_CODEC_GZIP = 2, PQG_CODEC_LZO = 3,
+  PQG_CODEC_BROTLI = 4, PQG_CODEC_LZ4 = 5, PQG_CODEC_ZSTD = 6, PQG_CODEC_LZ4_RAW = 7
+};
+
+/* Headers of a chunk placed at byte `chunk_offset` of a batch buffer -> the pqg_page_desc entries
+ * of its data pages (column index `column`) and the dictionary fields of `col` (may be NULL).
+ * `codec` is the chunk's ColumnMetaData.codec; it alone decides which pages are compressed, as
+ * ColumnChunkPageReadStore.readPage does (ColumnChunkPageReadStore.java:147-181, :218-257,
+ * readDictionaryPage :313-316): with a codec other than UNCOMPRESSED every V1 data page and the
+ * dictionary page are compressed whatever their sizes, a V2 page when its is_compressed flag is set.
+ * A compressed page -> PQG_ERR_UNSUPPORTED with st->page = its header index (decompress first:
+ * pqg_snappy_decompress / pqg_zstd_decompress, then describe the decompressed layout). An
+ * UNCOMPRESSED chunk's pages are taken as they are (CodecFactory.NO_OP_DECOMPRESSOR). A codec
+ * outside pqg_codec -> PQG_ERR_INVALID_ARG. Replaces the page loop of
+ * ParquetFileReader.Chunk.readAllPages (ParquetFileReader.java:1824-1979) + the decompressor choice. */
+int pqg_pages_from_headers(const pqg_page_header* headers, int n_headers, int codec, uint64_t chunk_offset,
+                           int column, pqg_column_desc* col, pqg_page_desc* pages, int capacity, int* n_pages,
+                           pqg_status* st);
 
 /* Human-readable name of an error code. */
 const char* pqg_error_name(int code);

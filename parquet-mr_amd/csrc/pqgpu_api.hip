@@ -246,8 +246,11 @@ int pqg_ctx_destroy(pqg_ctx* c) {
   return PQG_OK;
 }
 
-int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, const pqg_column_desc* cols, int n_cols,
-                    const pqg_page_desc* pages, int n_pages, pqg_plan** out, pqg_status* st) {
+// valid_bytes: the caller's data ends there (page and dictionary extents are checked against it); the
+// kernels may read up to n_bytes (pqg_decode_host's zero padding past the caller's bytes)
+static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, uint64_t valid_bytes,
+                            const pqg_column_desc* cols, int n_cols, const pqg_page_desc* pages, int n_pages,
+                            pqg_plan** out, pqg_status* st) {
   if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
   if (!ctx || !out || n_cols < 0 || n_pages < 0 || (n_cols && !cols) || (n_pages && !pages) || (n_bytes && !d_bytes) ||
       ((uintptr_t)d_bytes & 3u)) {  // the batch buffer is read as dwords (scalar loads): 4-byte aligned
@@ -292,7 +295,7 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
         col_err[(size_t)i] = PQG_ERR_UNSUPPORTED;
       } else if (c.physical_type == PQG_FIXED_LEN_BYTE_ARRAY && c.type_length <= 0) {
         col_err[(size_t)i] = PQG_ERR_CORRUPT;  // PlainBinaryDictionary :106 checkArgument(length > 0)
-      } else if ((uint64_t)c.dict_offset + c.dict_size > n_bytes) {
+      } else if ((uint64_t)c.dict_offset + c.dict_size > valid_bytes) {
         col_err[(size_t)i] = PQG_ERR_INVALID_ARG;
       } else if (d.elem_width > 0 && (uint64_t)c.dict_num_values * (uint64_t)d.elem_width > c.dict_size) {
         col_err[(size_t)i] = PQG_ERR_EOF;
@@ -317,7 +320,7 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, cons
     const pqg_page_desc& g = pages[p];
     PageWork& w = P->h_work[(size_t)p];
     std::memset(&w, 0, sizeof(w));
-    if (g.column < 0 || g.column >= n_cols || g.offset + g.size > n_bytes || (g.version != 1 && g.version != 2)) {
+    if (g.column < 0 || g.column >= n_cols || g.offset + g.size > valid_bytes || g.offset + g.size < g.offset || (g.version != 1 && g.version != 2)) {
       set_status(st, PQG_ERR_INVALID_ARG, p, -1, "page descriptor");
       delete P;
       return PQG_ERR_INVALID_ARG;
@@ -885,9 +888,15 @@ int pqg_sync(pqg_ctx* ctx, pqg_status* st) {
   return rc;
 }
 
-int pqg_decode(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
-               const pqg_page_desc* pages, int n_pages, uint32_t* d_page_value_counts, pqg_status* st) {
-  if (!ctx) return PQG_ERR_INVALID_ARG;
+int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, const pqg_column_desc* cols, int n_cols,
+                    const pqg_page_desc* pages, int n_pages, pqg_plan** out, pqg_status* st) {
+  return plan_create_impl(ctx, d_bytes, n_bytes, n_bytes, cols, n_cols, pages, n_pages, out, st);
+}
+
+static int decode_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, uint64_t valid_bytes,
+                       pqg_column_desc* cols, int n_cols, const pqg_page_desc* pages, int n_pages,
+                       uint32_t* d_page_value_counts, pqg_status* st) {
+  if (!ctx || n_cols < 0 || n_pages < 0 || (n_cols && !cols) || (n_pages && !pages)) return PQG_ERR_INVALID_ARG;
   // capacity checks (descriptor arithmetic)
   {
     std::vector<uint64_t> slots((size_t)std::max(n_cols, 1), 0);
@@ -909,7 +918,7 @@ int pqg_decode(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, pqg_colum
     ctx->last = nullptr;
   }
   pqg_plan* P = nullptr;
-  int rc = pqg_plan_create(ctx, d_bytes, n_bytes, cols, n_cols, pages, n_pages, &P, st);
+  int rc = plan_create_impl(ctx, d_bytes, n_bytes, valid_bytes, cols, n_cols, pages, n_pages, &P, st);
   if (rc) return rc;
   ctx->last = P;
   ctx->last_cols = cols;
@@ -923,6 +932,11 @@ int pqg_decode(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, pqg_colum
              : PQG_ERR_HIP;
   }
   return rc;
+}
+
+int pqg_decode(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
+               const pqg_page_desc* pages, int n_pages, uint32_t* d_page_value_counts, pqg_status* st) {
+  return decode_impl(ctx, d_bytes, n_bytes, n_bytes, cols, n_cols, pages, n_pages, d_page_value_counts, st);
 }
 
 // ---- host copies of the host path (pinned staging <-> caller arrays): one thread moves ~10 GB/s,
@@ -1040,8 +1054,8 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
     }
     // the zero padding is part of the readable range: loads are range-checked per dword against it, and
     // a page ending at an unaligned offset close to n_bytes (raw file bytes) needs its last dword whole
-    rc = pqg_decode(ctx, (const uint8_t*)ctx->host_bytes.p, n_bytes + pad, dcols.data(), n_cols, pages, n_pages,
-                    (uint32_t*)ctx->host_counts.p, st);
+    rc = decode_impl(ctx, (const uint8_t*)ctx->host_bytes.p, n_bytes + pad, n_bytes, dcols.data(), n_cols, pages,
+                     n_pages, (uint32_t*)ctx->host_counts.p, st);
     if (rc) return rc;
     rc = pqg_sync(ctx, &st2);
     if (rc != PQG_ERR_INVALID_ARG || st2.page != -1 || !ctx->last || attempt == 1) break;

@@ -296,22 +296,29 @@ int pqg_frame_chunk(const uint8_t* chunk, uint64_t chunk_len, int64_t value_coun
   return PQG_OK;
 }
 
-int pqg_pages_from_headers(const pqg_page_header* headers, int n_headers, uint64_t chunk_offset, int column,
-                           pqg_column_desc* col, pqg_page_desc* pages, int capacity, int* n_pages, pqg_status* st) {
+int pqg_pages_from_headers(const pqg_page_header* headers, int n_headers, int codec, uint64_t chunk_offset,
+                           int column, pqg_column_desc* col, pqg_page_desc* pages, int capacity, int* n_pages,
+                           pqg_status* st) {
   if (st) std::memset(st, 0, sizeof(*st));
-  if ((n_headers > 0 && !headers) || !n_pages || capacity < 0 || (capacity > 0 && !pages)) {
+  if ((n_headers > 0 && !headers) || !n_pages || capacity < 0 || (capacity > 0 && !pages) || codec < PQG_CODEC_UNCOMPRESSED ||
+      codec > PQG_CODEC_LZ4_RAW) {
     pqg_set_status(st, PQG_ERR_INVALID_ARG, -1, -1, "pqg_pages_from_headers: bad arguments");
     return PQG_ERR_INVALID_ARG;
   }
   int n = 0;
   for (int i = 0; i < n_headers; i++) {
     const pqg_page_header& h = headers[i];
-    // a compressed page must be decompressed first (pqg_snappy_decompress) into a layout of its own
-    const bool compressed = h.type == PQG_DATA_PAGE_V2 ? (h.is_compressed && h.uncompressed_page_size != h.compressed_page_size)
-                                                       : h.uncompressed_page_size != h.compressed_page_size;
-    if (compressed) {
+    // Whether the page body goes through the chunk's decompressor is decided by the codec, never by
+    // the sizes (ColumnChunkPageReadStore.readPage): a V1 data page (:147-181) and the dictionary
+    // page (readDictionaryPage :313-316) always do; a V2 page only when is_compressed (:218, :232,
+    // :253). UNCOMPRESSED is CodecFactory.NO_OP_DECOMPRESSOR (CodecFactory.java:60-83), whose
+    // BytesInput form returns the bytes as they are. A compressed page must be decompressed first
+    // (pqg_snappy_decompress / pqg_zstd_decompress) into a layout of its own.
+    const bool compressed = codec != PQG_CODEC_UNCOMPRESSED && (h.type != PQG_DATA_PAGE_V2 || h.is_compressed);
+    if (compressed && (h.type == PQG_DICTIONARY_PAGE || h.type == PQG_DATA_PAGE || h.type == PQG_DATA_PAGE_V2)) {
       pqg_set_status(st, PQG_ERR_UNSUPPORTED, i, -1,
-                     "compressed page: decompress the chunk (pqg_snappy_decompress) and describe the decompressed pages");
+                     "compressed page: decompress the chunk (pqg_snappy_decompress / pqg_zstd_decompress) and "
+                     "describe the decompressed pages");
       return PQG_ERR_UNSUPPORTED;
     }
     if (h.type == PQG_DICTIONARY_PAGE) {

@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # parquet-format Type
 BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY = range(8)
@@ -45,6 +45,8 @@ ERR_NO_DICTIONARY = 19
 ERR_DICT_ENCODING = 20
 ERR_CRC = 21
 
+# ColumnMetaData.codec (parquet.thrift CompressionCodec; pqg_codec)
+CODEC_UNCOMPRESSED, CODEC_SNAPPY, CODEC_GZIP, CODEC_LZO, CODEC_BROTLI, CODEC_LZ4, CODEC_ZSTD, CODEC_LZ4_RAW = range(8)
 COLUMN_DICTIONARY_IDS = 1  # pqg_column_desc.flags: values <- uint32 dictionary ids
 PAGE_DBA_CARRY = 1  # pqg_page_desc.flags: DELTA_BYTE_ARRAY page continues the previous page's value (PARQUET-246)
 

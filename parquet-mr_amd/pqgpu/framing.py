@@ -171,8 +171,8 @@ def read_column_chunk(buf, start, length, physical_type, max_def=0, max_rep=0, t
         usize = h.get("uncompressed_page_size", size)
         if codec not in (0, 1, 6):
             raise ThriftError(f"codec {codec} is not supported (UNCOMPRESSED, SNAPPY and ZSTD are)")
-        if not codec and usize != size and h["type"] != DATA_PAGE_V2:
-            raise ThriftError("compressed page in an UNCOMPRESSED chunk")
+        # UNCOMPRESSED: CodecFactory.NO_OP_DECOMPRESSOR hands the page bytes on as they are, whatever
+        # uncompressed_page_size says (CodecFactory.java:60-83); the codec alone decides (pqg_pages_from_headers)
         data = bytes(buf[body:body + size])
         if len(data) != size:
             raise ThriftError("page body truncated")
@@ -191,8 +191,6 @@ def read_column_chunk(buf, start, length, physical_type, max_def=0, max_rep=0, t
             seen += h["num_values"]
         elif t == DATA_PAGE_V2:
             compressed = bool(codec) and h.get("is_compressed", True)
-            if not compressed and usize != size:
-                raise ThriftError("V2 page sizes differ but the page is not compressed")
             chunk.pages.append(Page(body=data, num_values=h["num_values"], encoding=h["encoding"], version=2,
                                     rl_byte_length=h["repetition_levels_byte_length"],
                                     dl_byte_length=h["definition_levels_byte_length"],

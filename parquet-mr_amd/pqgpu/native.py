@@ -70,7 +70,7 @@ def lib():
         L.pqg_crc32.argtypes = [C.c_uint32, vp, u64]
         L.pqg_crc32.restype = C.c_uint32
         L.pqg_frame_chunk.argtypes = [vp, u64, C.c_int64, i32, vp, i32, C.POINTER(i32), C.POINTER(abi.Status)]
-        L.pqg_pages_from_headers.argtypes = [vp, i32, u64, i32, vp, vp, i32, C.POINTER(i32), C.POINTER(abi.Status)]
+        L.pqg_pages_from_headers.argtypes = [vp, i32, i32, u64, i32, vp, vp, i32, C.POINTER(i32), C.POINTER(abi.Status)]
         L.pqg_error_name.argtypes = [i32]
         L.pqg_error_name.restype = C.c_char_p
         if L.pqg_abi_version() != abi.ABI_VERSION:

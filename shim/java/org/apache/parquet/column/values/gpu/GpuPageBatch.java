@@ -24,9 +24,13 @@ public final class GpuPageBatch {
   final long errorIndex;
   final int errorKind;
   final long[] valuesWritten;
+  /** Per page: its column, and the index of its first value in that column's dense output. */
+  private final int[] pageColumn;
+  private final long[] pageFirst;
 
   /**
-   * @param pageBytes direct buffer: every page body (and dictionary page) the descriptors refer to
+   * @param pageBytes direct or heap buffer; [position, limit) holds every page body (and dictionary
+   *     page) the descriptors refer to (descriptor offsets are relative to position)
    * @param pageDescs packed pqg_page_desc[] (PqGpu.frameChunk output, concatenated per chunk)
    * @param columnDescs packed pqg_column_desc[] without output pointers
    */
@@ -57,19 +61,29 @@ public final class GpuPageBatch {
     errorKind = (int) r[3];
     valuesWritten = new long[nCols];
     System.arraycopy(r, 4, valuesWritten, 0, nCols);
-  }
-
-  int pageColumn(int page) {
-    return ByteBuffer.wrap(pageDescs).order(ByteOrder.LITTLE_ENDIAN).getInt(page * PqGpu.PAGE_DESC_BYTES + 16);
-  }
-
-  /** The reader of one data page (the ValuesReader ColumnReaderBase.initDataReader would create). */
-  public GpuValuesReader reader(int page) {
-    int column = pageColumn(page);
-    long first = 0;
-    for (int p = 0; p < page; p++) {
-      if (pageColumn(p) == column) first += pageCounts[p];
+    // one pass: each page's column and its first value (prefix sum of the value counts per column)
+    ByteBuffer pd = ByteBuffer.wrap(pageDescs).order(ByteOrder.LITTLE_ENDIAN);
+    pageColumn = new int[nPages];
+    pageFirst = new long[nPages];
+    long[] acc = new long[Math.max(nCols, 1)];
+    for (int p = 0; p < nPages; p++) {
+      int c = pd.getInt(p * PqGpu.PAGE_DESC_BYTES + 16);
+      pageColumn[p] = c;
+      if (c >= 0 && c < nCols) {
+        pageFirst[p] = acc[c];
+        acc[c] += pageCounts[p];
+      }
     }
+  }
+
+  public int pageCount() {
+    return pageColumn.length;
+  }
+
+  /** The reader of one data page (the ValuesReader ColumnReaderBase.initDataReader would create). O(1). */
+  public GpuValuesReader reader(int page) {
+    int column = pageColumn[page];
+    long first = pageFirst[page];
     long errorAt = -1;
     if (code != 0) {
       if (errorPage < 0 || page > errorPage || (page == errorPage && errorKind == 2)) {

@@ -1,5 +1,14 @@
 /*
- * Native entry points of the MI355X page decoder (libpqgpu.so via libpqgpu_jni.so).
+ * Entry points of the MI355X page decoder (libpqgpu.so via libpqgpu_jni.so) for parquet-mr code in
+ * other packages (ParquetReadRouter lives in org.apache.parquet.column.values.bitpacking,
+ * ColumnReaderBase in org.apache.parquet.column.impl): every method a caller needs is public.
+ *
+ * ByteBuffers may be direct or heap (parquet-mr's default allocator is HeapByteBufferAllocator,
+ * ParquetReadOptions.java:265): the bytes from position() to limit() are used in both cases. A heap
+ * buffer is passed as its backing array (array() + arrayOffset() + position()); a read-only heap
+ * buffer is copied once. The natives below take (buffer or array, offset, length) and never look at
+ * the buffer's position themselves.
+ *
  * JNI glue: shim/jni/pqgpu_jni.c; C ABI: include/pqgpu.h, include/pqgpu_reader.h.
  */
 package org.apache.parquet.column.values.gpu;
@@ -18,41 +27,126 @@ public final class PqGpu {
   public static final int COLUMN_DESC_BYTES = 104;
   /** pqg_column_desc.flags: decode dictionary ids (readValueDictionaryId) instead of values. */
   public static final int COLUMN_DICTIONARY_IDS = 1;
+  /** ColumnMetaData.codec values (parquet.thrift CompressionCodec; pqg_codec). */
+  public static final int CODEC_UNCOMPRESSED = 0, CODEC_SNAPPY = 1, CODEC_GZIP = 2, CODEC_LZO = 3,
+      CODEC_BROTLI = 4, CODEC_LZ4 = 5, CODEC_ZSTD = 6, CODEC_LZ4_RAW = 7;
 
   /** Number of visible MI355X devices (0: no GPU path; the caller keeps the CPU readers). */
-  static native int deviceCount();
+  public static native int deviceCount();
 
-  /** One decode context (HIP stream + device scratch) per reader thread, like ColumnReaderBase. */
-  static native long ctxCreate(int device);
+  /** One decode context (HIP stream + device scratch); not thread-safe: one per reader thread. */
+  public static native long ctxCreate(int device);
 
-  static native void ctxDestroy(long ctx);
-
-  /**
-   * Page headers of one raw column chunk (ParquetFileReader.Chunk.readAllPages): returns packed
-   * pqg_page_desc[] of its data pages, fills dictInfo = {dict offset, size, num_values, encoding}
-   * (offset -1: none). Throws ParquetDecodingException on a CRC mismatch / corrupt header.
-   */
-  static native byte[] frameChunk(ByteBuffer chunk, long valueCount, boolean verifyCrc, long chunkOffset, int column,
-      long[] dictInfo);
-
-  /**
-   * Decode every page of a batch in one call (pqg_decode_host). values[i]: long[] / int[] / float[] /
-   * double[] / byte[] (BOOLEAN, FIXED_LEN_BYTE_ARRAY, INT96 row-major) or long[] offsets for
-   * BYTE_ARRAY (binary[i] receives the bytes), int[] for COLUMN_DICTIONARY_IDS columns; defLevels /
-   * repLevels may hold null. pageCounts receives each page's value count. Returns {code, page,
-   * value_index, kind (0 none, 1 value error: lazily at that read, 2 page error: at initFromPage),
-   * values_written[0..nCols)}. Decode errors are returned, not thrown: the readers throw them where
-   * the reference readers would.
-   */
-  static native long[] decodeHost(long ctx, ByteBuffer pageBytes, byte[] pageDescs, byte[] columnDescs,
-      Object[] values, byte[][] defLevels, byte[][] repLevels, byte[][] binary, int[] pageCounts);
-
-  /**
-   * ParquetReadRouter.read on the GPU (pqg_router_read): unpack `count` LSB-first values of `bitWidth`
-   * bits from the direct buffer `in` (count * bitWidth / 8 bytes) into out[0..count).
-   */
-  static native void routerRead(long ctx, int bitWidth, ByteBuffer in, int count, int[] out);
+  public static native void ctxDestroy(long ctx);
 
   /** JNI class name of the exception for a pqg_error code (pqg_java_exception). */
-  static native String exceptionClass(int code);
+  public static native String exceptionClass(int code);
+
+  private static final ThreadLocal<long[]> THREAD_CTX = new ThreadLocal<long[]>();
+
+  /**
+   * The calling thread's context on device 0, created on first use (what a ParquetReadRouter branch
+   * or a column reader uses; parquet-mr reads a row group's columns on one thread). Released by
+   * {@link #releaseThreadContext()}.
+   */
+  public static long threadContext() {
+    long[] c = THREAD_CTX.get();
+    if (c == null) {
+      c = new long[] {ctxCreate(0)};
+      THREAD_CTX.set(c);
+    }
+    return c[0];
+  }
+
+  public static void releaseThreadContext() {
+    long[] c = THREAD_CTX.get();
+    if (c != null) {
+      ctxDestroy(c[0]);
+      THREAD_CTX.remove();
+    }
+  }
+
+  /**
+   * Page headers of one raw column chunk (ParquetFileReader.Chunk.readAllPages) in
+   * chunk[position, limit): returns packed pqg_page_desc[] of its data pages, fills dictInfo = {dict
+   * offset, size, num_values, encoding} (offset -1: none). codec = ColumnMetaData.codec: with a codec
+   * other than CODEC_UNCOMPRESSED a V1 / dictionary page, or a V2 page with is_compressed set, throws
+   * UnsupportedOperationException (decompress first). Throws ParquetDecodingException on a CRC
+   * mismatch / corrupt header. Descriptor offsets are chunkOffset + offset inside the chunk.
+   */
+  public static byte[] frameChunk(ByteBuffer chunk, long valueCount, boolean verifyCrc, int codec, long chunkOffset,
+      int column, long[] dictInfo) {
+    if (chunk.isDirect()) {
+      return frameChunkDirect(chunk, chunk.position(), chunk.remaining(), valueCount, verifyCrc, codec, chunkOffset,
+          column, dictInfo);
+    }
+    byte[] a = heapBytes(chunk);
+    int off = chunk.hasArray() && !chunk.isReadOnly() ? chunk.arrayOffset() + chunk.position() : 0;
+    return frameChunkArray(a, off, chunk.remaining(), valueCount, verifyCrc, codec, chunkOffset, column, dictInfo);
+  }
+
+  /**
+   * Decode every page of a batch in one call (pqg_decode_host); pageBytes[position, limit) holds
+   * the bytes the descriptors' offsets refer to. values[i]: long[] / int[] / float[] / double[] /
+   * byte[] (BOOLEAN, FIXED_LEN_BYTE_ARRAY, INT96 row-major) or long[] offsets (n + 1) for BYTE_ARRAY
+   * (binary[i] receives the bytes), int[] for COLUMN_DICTIONARY_IDS columns of any type;
+   * defLevels / repLevels may hold null. pageCounts receives each page's value count. Returns {code,
+   * page, value_index, kind (0 none, 1 value error: lazily at that read, 2 page error: at
+   * initFromPage), values_written[0..nCols)}. Decode errors are returned, not thrown: the readers
+   * throw them where the reference readers would.
+   */
+  public static long[] decodeHost(long ctx, ByteBuffer pageBytes, byte[] pageDescs, byte[] columnDescs, Object[] values,
+      byte[][] defLevels, byte[][] repLevels, byte[][] binary, int[] pageCounts) {
+    if (pageBytes.isDirect()) {
+      return decodeHostDirect(ctx, pageBytes, pageBytes.position(), pageBytes.remaining(), pageDescs, columnDescs,
+          values, defLevels, repLevels, binary, pageCounts);
+    }
+    byte[] a = heapBytes(pageBytes);
+    int off = pageBytes.hasArray() && !pageBytes.isReadOnly() ? pageBytes.arrayOffset() + pageBytes.position() : 0;
+    return decodeHostArray(ctx, a, off, pageBytes.remaining(), pageDescs, columnDescs, values, defLevels, repLevels,
+        binary, pageCounts);
+  }
+
+  /**
+   * ParquetReadRouter.read on the GPU (pqg_router_read): unpack `count` LSB-first values of
+   * `bitWidth` bits from in[position, limit) (count * bitWidth / 8 bytes; fewer -> EOFException)
+   * into out[0..count).
+   */
+  public static void routerRead(long ctx, int bitWidth, ByteBuffer in, int count, int[] out)
+      throws java.io.EOFException {
+    if (in.isDirect()) {
+      routerReadDirect(ctx, bitWidth, in, in.position(), in.remaining(), count, out);
+      return;
+    }
+    byte[] a = heapBytes(in);
+    int off = in.hasArray() && !in.isReadOnly() ? in.arrayOffset() + in.position() : 0;
+    routerReadArray(ctx, bitWidth, a, off, in.remaining(), count, out);
+  }
+
+  /** The backing array of a heap buffer, or a copy of [position, limit) of a read-only one. */
+  private static byte[] heapBytes(ByteBuffer b) {
+    if (b.hasArray() && !b.isReadOnly()) return b.array();
+    byte[] copy = new byte[b.remaining()];
+    b.duplicate().get(copy);
+    return copy;
+  }
+
+  private static native byte[] frameChunkDirect(ByteBuffer chunk, int offset, int length, long valueCount,
+      boolean verifyCrc, int codec, long chunkOffset, int column, long[] dictInfo);
+
+  private static native byte[] frameChunkArray(byte[] chunk, int offset, int length, long valueCount,
+      boolean verifyCrc, int codec, long chunkOffset, int column, long[] dictInfo);
+
+  private static native long[] decodeHostDirect(long ctx, ByteBuffer pageBytes, int offset, int length,
+      byte[] pageDescs, byte[] columnDescs, Object[] values, byte[][] defLevels, byte[][] repLevels, byte[][] binary,
+      int[] pageCounts);
+
+  private static native long[] decodeHostArray(long ctx, byte[] pageBytes, int offset, int length, byte[] pageDescs,
+      byte[] columnDescs, Object[] values, byte[][] defLevels, byte[][] repLevels, byte[][] binary, int[] pageCounts);
+
+  private static native void routerReadDirect(long ctx, int bitWidth, ByteBuffer in, int offset, int length, int count,
+      int[] out);
+
+  private static native void routerReadArray(long ctx, int bitWidth, byte[] in, int offset, int length, int count,
+      int[] out);
 }

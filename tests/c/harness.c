@@ -5,7 +5,7 @@
  * failure mapped to the Java exception class the shim throws (pqg_java_exception).
  *
  * usage: harness <case file> <mode>
- *   case file: "PQGC" | i32 physical_type, type_length, max_def, max_rep, flags | i64 num_values |
+ *   case file: "PQGC" | i32 physical_type, type_length, max_def, max_rep, flags, codec | i64 num_values |
  *              u64 chunk_len | chunk bytes            (written by tests/test_c_harness.py)
  *   mode:      all   read every value of every page with the column type's read call
  *              skip  per page: skip(3), read 2, repeated (ValuesReader.skip(int n))
@@ -109,10 +109,10 @@ int main(int argc, char** argv) {
   FILE* f = fopen(argv[1], "rb");
   if (!f) return 2;
   char magic[4];
-  int32_t hdr[5];
+  int32_t hdr[6];
   int64_t num_values;
   uint64_t chunk_len;
-  if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "PQGC", 4) || fread(hdr, 4, 5, f) != 5 ||
+  if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "PQGC", 4) || fread(hdr, 4, 6, f) != 6 ||
       fread(&num_values, 8, 1, f) != 1 || fread(&chunk_len, 8, 1, f) != 1)
     return 2;
   const uint64_t pad = 1024;
@@ -140,7 +140,8 @@ int main(int argc, char** argv) {
   col.dict_offset = -1;
   pqg_page_desc* pages = calloc((size_t)n_hdr + 1, sizeof(pqg_page_desc));
   int n_pages = 0;
-  rc = pqg_pages_from_headers(hdrs, n_hdr, 0, 0, &col, pages, n_hdr + 1, &n_pages, &st);
+  /* the chunk's ColumnMetaData.codec decides which pages are compressed (ColumnChunkPageReadStore) */
+  rc = pqg_pages_from_headers(hdrs, n_hdr, hdr[5], 0, 0, &col, pages, n_hdr + 1, &n_pages, &st);
   if (rc) {
     printf("FRAME_ERROR %d %s %d\n", rc, exc(rc), st.page);
     return 0;

@@ -29,9 +29,9 @@ def harness(tmp_path_factory):
     return exe
 
 
-def case_file(tmp_path, raw, ptype, num_values, type_length=0, max_def=0, max_rep=0, flags=0):
+def case_file(tmp_path, raw, ptype, num_values, type_length=0, max_def=0, max_rep=0, flags=0, codec=0):
     p = tmp_path / "case.bin"
-    p.write_bytes(b"PQGC" + struct.pack("<5i", ptype, type_length, max_def, max_rep, flags) +
+    p.write_bytes(b"PQGC" + struct.pack("<6i", ptype, type_length, max_def, max_rep, flags, codec) +
                   struct.pack("<qQ", num_values, len(raw)) + raw)
     return str(p)
 
@@ -216,3 +216,64 @@ def test_harness_value_error_surfaces_at_the_failing_read(harness, tmp_path):
     assert r["ends"][page] == (abi.ERR_DICT_ID, "java/lang/ArrayIndexOutOfBoundsException")
     for p in range(page + 1, 3):
         assert r["init"][p][0] == abi.ERR_DICT_ID
+
+
+# ---- the chunk codec decides compression (ColumnChunkPageReadStore.readPage) ---------------------
+
+def _chunk(version, n=3000, dict_enc=False):
+    vals = np.arange(n, dtype=np.int64) * 3 - 7
+    if dict_enc:
+        return vals % 50, writer.write_column_chunk(abi.INT64, vals % 50, abi.RLE_DICTIONARY, page_rows=1000,
+                                                    version=version)
+    return vals, writer.write_column_chunk(abi.INT64, vals, abi.PLAIN, page_rows=1000, version=version)
+
+
+@pytest.mark.parametrize("codec", [abi.CODEC_SNAPPY, abi.CODEC_ZSTD, abi.CODEC_GZIP])
+def test_codec_v1_page_with_equal_sizes_is_compressed(harness, tmp_path, codec):
+    """A V1 page of a compressed chunk goes through the decompressor whatever its header sizes say
+    (ColumnChunkPageReadStore.java:147-181): equal compressed / uncompressed sizes must not make
+    pqg_pages_from_headers describe its bytes as values. -> UNSUPPORTED (decompress first)."""
+    vals, ch = _chunk(1)
+    raw = thrift_compact.chunk_bytes(ch)
+    r = parse(run(harness, case_file(tmp_path, raw, abi.INT64, len(vals), codec=codec)))
+    assert r["FRAME_ERROR"][:3] == [str(abi.ERR_UNSUPPORTED), "java/lang/UnsupportedOperationException", "0"]
+
+
+def test_codec_dictionary_page_of_compressed_chunk(harness, tmp_path):
+    """The dictionary page is decompressed with the chunk codec (readDictionaryPage :313-316)."""
+    vals, ch = _chunk(2, dict_enc=True)
+    raw = thrift_compact.chunk_bytes(ch)
+    r = parse(run(harness, case_file(tmp_path, raw, abi.INT64, len(vals), codec=abi.CODEC_SNAPPY)))
+    assert r["FRAME_ERROR"][:3] == [str(abi.ERR_UNSUPPORTED), "java/lang/UnsupportedOperationException", "0"]
+
+
+def test_codec_v2_is_compressed_flag_decides(harness, tmp_path):
+    """V2: is_compressed=true with equal sizes in a SNAPPY chunk -> compressed (UNSUPPORTED here);
+    is_compressed=false in a SNAPPY chunk -> the page is taken as it is (:218)."""
+    vals, ch = _chunk(2)
+    raw = thrift_compact.chunk_bytes(ch, is_compressed=True)
+    r = parse(run(harness, case_file(tmp_path, raw, abi.INT64, len(vals), codec=abi.CODEC_SNAPPY)))
+    assert r["FRAME_ERROR"][:3] == [str(abi.ERR_UNSUPPORTED), "java/lang/UnsupportedOperationException", "0"]
+    raw = thrift_compact.chunk_bytes(ch, is_compressed=False)
+    r = parse(run(harness, case_file(tmp_path, raw, abi.INT64, len(vals), codec=abi.CODEC_SNAPPY)))
+    assert "FRAME_ERROR" not in r and int(r["FRAME"][0]) == len(ch.pages)
+
+
+def test_codec_out_of_range_is_invalid(harness, tmp_path):
+    vals, ch = _chunk(1)
+    r = parse(run(harness, case_file(tmp_path, thrift_compact.chunk_bytes(ch), abi.INT64, len(vals), codec=8)))
+    assert r["FRAME_ERROR"][0] == str(abi.ERR_INVALID_ARG)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("version", [1, 2])
+def test_codec_uncompressed_pages_decode(harness, tmp_path, version):
+    """UNCOMPRESSED chunk (V1 / V2) and a V2 page with is_compressed=false inside a SNAPPY chunk:
+    framed and decoded through the C ABI, values equal the written ones."""
+    vals, ch = _chunk(version)
+    for codec in ([abi.CODEC_UNCOMPRESSED] if version == 1 else [abi.CODEC_UNCOMPRESSED, abi.CODEC_SNAPPY]):
+        raw = thrift_compact.chunk_bytes(ch, is_compressed=False)
+        r = parse(run(harness, case_file(tmp_path, raw, abi.INT64, len(vals), codec=codec)))
+        assert r["DECODE"][0] == "0"
+        got = [int(v) for p in sorted(r["values"]) for _, v in r["values"][p]]
+        assert got == vals.tolist()

@@ -182,7 +182,7 @@ def test_pages_from_headers_match_build_batch():
         pages = (abi.PageDesc * max(1, len(hdrs)))()
         n = C.c_int(0)
         base = 4096
-        rc = L.pqg_pages_from_headers(C.addressof(arr), len(hdrs), base, 0, C.byref(col), C.addressof(pages),
+        rc = L.pqg_pages_from_headers(C.addressof(arr), len(hdrs), abi.CODEC_UNCOMPRESSED, base, 0, C.byref(col), C.addressof(pages),
                                       len(hdrs), C.byref(n), C.byref(st))
         assert rc == abi.OK, st.message
         assert n.value == len(ch.pages)

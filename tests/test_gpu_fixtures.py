@@ -74,7 +74,7 @@ def test_gpu_decodes_raw_chunk_bytes(decoder):
         col.dict_offset = -1
         pages = (abi.PageDesc * len(hdrs))()
         n = C.c_int(0)
-        rc = L.pqg_pages_from_headers(C.addressof(arr), len(hdrs), base, len(columns), C.byref(col),
+        rc = L.pqg_pages_from_headers(C.addressof(arr), len(hdrs), abi.CODEC_UNCOMPRESSED, base, len(columns), C.byref(col),
                                       C.addressof(pages), len(hdrs), C.byref(n), C.byref(st))
         assert rc == abi.OK, st.message
         descs += [bytes(pages[k]) for k in range(n.value)]

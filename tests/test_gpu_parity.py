@@ -354,6 +354,31 @@ def test_host_path_roundtrip(decoder):
     assert counts.sum() == vals.size
 
 
+@pytest.mark.parametrize("what", ["page", "dictionary"])
+@pytest.mark.parametrize("over", [1, 100, 1023])
+def test_host_path_extent_past_buffer(decoder, what, over):
+    """pqg_decode_host reads its staged bytes with 1 KiB of zero padding; a page or dictionary whose
+    extent runs past the CALLER's buffer by fewer than 1 KiB must still be rejected (INVALID_ARG),
+    as pqg_decode rejects it, not decoded against the padding (the reference would hit EOF)."""
+    import copy
+    vals = zipf_dict_column(40_000, card=300, seed=11)
+    batch = writer.build_batch([make(abi.INT64, vals, abi.RLE_DICTIONARY)])
+    b = copy.copy(batch)
+    b.pages = batch.pages.copy()
+    b.columns = [dict(c) for c in batch.columns]
+    n = batch.data.size
+    if what == "page":
+        p = b.n_pages - 1
+        b.pages["size"][p] = n - int(b.pages["offset"][p]) + over
+    else:
+        b.columns[0]["dict_size"] = n - int(b.columns[0]["dict_offset"]) + over
+    rc, st, res, counts = decoder.decode_host(b)
+    assert rc == abi.ERR_INVALID_ARG, (rc, st.message)
+    if what == "page":
+        assert st.page == b.n_pages - 1
+    rc, st, res, counts = decoder.decode_host(batch)
+    assert rc == 0 and np.array_equal(res[0]["values"], vals)
+
 
 @pytest.mark.parametrize("max_def", [1, 2, 5, 12, 20, 40])
 @pytest.mark.parametrize("shape", ["random", "runs"])

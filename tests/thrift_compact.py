@@ -33,8 +33,9 @@ def _struct(fields):
     return bytes(out + b"\x00")
 
 
-def page_header(ptype, size, num_values, enc=0, crc=None, v2=None, extra_field=False):
-    f = [(1, 5, _zz(ptype)), (2, 5, _zz(size)), (3, 5, _zz(size))]
+def page_header(ptype, size, num_values, enc=0, crc=None, v2=None, extra_field=False, usize=None, is_compressed=False):
+    """usize: uncompressed_page_size (default = size); is_compressed: the V2 header's flag."""
+    f = [(1, 5, _zz(ptype)), (2, 5, _zz(size if usize is None else usize)), (3, 5, _zz(size))]
     if crc is not None:
         f.append((4, 5, _zz(crc - (1 << 32) if crc >= 1 << 31 else crc)))
     if ptype == 0:
@@ -44,18 +45,20 @@ def page_header(ptype, size, num_values, enc=0, crc=None, v2=None, extra_field=F
     elif ptype == 3:
         rl, dl = v2
         f.append((8, 12, _struct([(1, 5, _zz(num_values)), (2, 5, _zz(0)), (3, 5, _zz(num_values)),
-                                  (4, 5, _zz(enc)), (5, 5, _zz(dl)), (6, 5, _zz(rl)), (7, 2, b"")])))
+                                  (4, 5, _zz(enc)), (5, 5, _zz(dl)), (6, 5, _zz(rl)),
+                                  (7, 1 if is_compressed else 2, b"")])))
     if extra_field:  # an unknown field id 20 (binary) the reader must skip
         f.append((20, 8, _varint(3) + b"xyz"))
     return _struct(f)
 
 
-def page_header_of(pg, crc=None):
-    """PageHeader of a writer.Page (uncompressed)."""
+def page_header_of(pg, crc=None, usize=None, is_compressed=False):
+    """PageHeader of a writer.Page (uncompressed unless the caller says otherwise: usize =
+    uncompressed_page_size to claim, is_compressed = the V2 flag)."""
     if pg.version == 2:
         return page_header(3, len(pg.body), pg.num_values, enc=pg.encoding, crc=crc,
-                           v2=(pg.rl_byte_length, pg.dl_byte_length))
-    f = [(1, 5, _zz(0)), (2, 5, _zz(len(pg.body))), (3, 5, _zz(len(pg.body)))]
+                           v2=(pg.rl_byte_length, pg.dl_byte_length), usize=usize, is_compressed=is_compressed)
+    f = [(1, 5, _zz(0)), (2, 5, _zz(len(pg.body) if usize is None else usize)), (3, 5, _zz(len(pg.body)))]
     if crc is not None:
         f.append((4, 5, _zz(crc - (1 << 32) if crc >= 1 << 31 else crc)))
     f.append((5, 12, _struct([(1, 5, _zz(pg.num_values)), (2, 5, _zz(pg.encoding)), (3, 5, _zz(pg.dl_encoding)),
@@ -63,14 +66,15 @@ def page_header_of(pg, crc=None):
     return _struct(f)
 
 
-def chunk_bytes(ch, with_crc=True, dict_num_values=None):
+def chunk_bytes(ch, with_crc=True, dict_num_values=None, is_compressed=False):
     """Raw bytes of an uncompressed writer.ColumnChunk: [dictionary page] data pages, each header
-    followed by its body (with page CRCs, as parquet-mr writes them by default)."""
+    followed by its body (with page CRCs, as parquet-mr writes them by default). is_compressed: the
+    V2 headers' flag (the bodies stay as they are)."""
     out = bytearray()
     if ch.dict_page is not None:
         crc = zlib.crc32(ch.dict_page) if with_crc else None
         n = ch.dict_num_values if dict_num_values is None else dict_num_values
         out += page_header(2, len(ch.dict_page), n, enc=ch.dict_encoding, crc=crc) + ch.dict_page
     for pg in ch.pages:
-        out += page_header_of(pg, zlib.crc32(pg.body) if with_crc else None) + pg.body
+        out += page_header_of(pg, zlib.crc32(pg.body) if with_crc else None, is_compressed=is_compressed) + pg.body
     return bytes(out)
