@@ -161,79 +161,29 @@ def run_c4(args, world, rank, devi):
     and strings, PLAIN comment strings) into the rank's slice of each column. The inputs are
     `--c4-templates` distinct synthetic row groups laid out repeatedly (row group g = template
     g mod T): every copy's pages are decoded, none is skipped or cached."""
-    import copy
-
     import torch
     import torch.distributed as dist
     import lineitem as LI
     from pqgpu import abi, decoder as D, dist as pdist, writer
 
-    rg_rows = 1_000_000
-    n_rg = max(1, args.rows // rg_rows)
-    T = min(args.c4_templates, n_rg)
     t_gen = time.perf_counter()
-    templates, base = [], 0
-    for t in range(T):
-        ch, ex, n_ord = LI.make_row_group(rg_rows, 1000 + t, base)
-        base += n_ord
-        templates.append((ch, ex))
-    tsize = [sum(len(p.body) for c in ch for p in c.pages) for ch, _ in templates]
-    shards = pdist.shard_row_groups([tsize[g % T] for g in range(n_rg)], world)
-    mine = shards[rank]
-    chunks = []
-    for g in mine:
-        for k, c in enumerate(templates[g % T][0]):
-            cc = copy.copy(c)
-            # dictionary columns: one pqg column per row group (its own dictionary); the others
-            # decode every row group into one rank-wide column, back to back
-            cc.column_index = (k, g) if c.dict_page is not None else (k, -1)
-            chunks.append(cc)
-    batch = writer.build_batch(chunks)
+    shard = LI.Shard(args.rows, world, rank, args.c4_templates)
+    rg_rows, n_rg, T, templates, shards, mine = shard.rg_rows, shard.n_rg, shard.T, shard.templates, shard.shards, shard.mine
+    batch, col_of = shard.batch, shard.col_of
     t_gen = time.perf_counter() - t_gen
     enc_bytes = int(batch.pages["size"].sum()) + sum(int(c["dict_size"]) for c in batch.columns if c["dict_offset"] >= 0)
 
     dec = D.Decoder(devi, poison=0xA5)
     dbatch = dec.upload(batch)
     cols, st = dec.decode(dbatch)  # sizes the BYTE_ARRAY buffers
+    for c in cols:  # poison: the plan's first launch must write every element itself
+        for t in (c.values, c.def_levels, c.rep_levels, c.binary_data):
+            if t is not None:
+                t.fill_(0xA5)
     plan = dec.plan(dbatch, cols)
-    keys = [getattr(c, "column_index") for c in chunks]
-    col_of = {}
-    for key in keys:
-        col_of.setdefault(key, len(col_of))
 
     def verify(what):
-        # every row group's slice of every column == its template's values
-        exp_dev = {}
-        pos = {k: 0 for k in range(16)}
-        bpos = 0
-        for g in mine:
-            t = g % T
-            for k in range(16):
-                ci = col_of[(k, g)] if (k, g) in col_of else col_of[(k, -1)]
-                col = cols[ci]
-                ex = templates[t][1][k]
-                key = (t, k)
-                if key not in exp_dev:
-                    if isinstance(ex.values, writer.BinaryValues):
-                        exp_dev[key] = (torch.from_numpy(ex.values.offsets).to(dec.device),
-                                        torch.from_numpy(ex.values.data).to(dec.device))
-                    else:
-                        exp_dev[key] = torch.from_numpy(np.ascontiguousarray(ex.values).view(np.uint8)).to(dec.device)
-                e = exp_dev[key]
-                merged = (k, -1) in col_of
-                r0 = pos[k] if merged else 0
-                n = rg_rows
-                if isinstance(e, tuple):
-                    offs = col.offsets()[r0:r0 + n + 1]
-                    b0 = int(offs[0].item())
-                    assert torch.equal(offs - b0, e[0]), f"{what}: row group {g} column {k} offsets"
-                    assert torch.equal(col.binary_data[b0:b0 + e[1].numel()], e[1]), f"{what}: rg {g} col {k} bytes"
-                else:
-                    w = e.numel() // n
-                    assert torch.equal(col.values[r0 * w:(r0 + n) * w], e), f"{what}: row group {g} column {k}"
-                if merged:
-                    pos[k] += n
-        del exp_dev
+        shard.verify(cols, dec.device, what)
 
     plan.launch()  # first launch of the fresh plan, checked
     rc, st = plan.sync()

@@ -228,8 +228,14 @@ int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes,
                     const pqg_column_desc* cols, int n_cols,
                     const pqg_page_desc* pages, int n_pages, pqg_plan** out, pqg_status* st);
 int pqg_plan_launch(pqg_plan* plan);
-/* Number of kernel launches one pqg_plan_launch issues, and the name of the dominant kernel. */
+/* Number of kernel launches one pqg_plan_launch issues. */
 int pqg_plan_kernel_count(pqg_plan* plan);
+/* Dictionary pages decode in one fused launch (walk + expansion, the expansion waiting for its
+ * page's walk). Should an expansion wait longer than 2 s (the GPU did not dispatch the walker it
+ * waits for), that launch reports PQG_ERR_TIMEOUT internally and pqg_sync re-runs the plan with the
+ * walk and the expansion as two launches; the plan keeps that mode and the caller sees the normal
+ * result. Returns how many launches of the plan were re-run that way. */
+int pqg_plan_timeout_fallbacks(pqg_plan* plan);
 int pqg_plan_destroy(pqg_plan* plan);
 
 /* ---- host-buffer decode (the JNI shim's entry: file bytes in, arrays out) --
@@ -276,7 +282,9 @@ int pqg_router_read(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_le
  * The leaf's non-null values are the dense values pqg_decode wrote for the column.
  * d_def_levels / d_rep_levels: the u8 levels pqg_decode wrote (NULL when the max level is 0).
  * Synchronous. When an output is too small, returns PQG_ERR_INVALID_ARG with every
- * n_entries filled in (nothing written). */
+ * n_entries filled in (nothing written). Outputs sized for the bound (validity: n_slots
+ * entries, offsets: n_slots + 1) are written in one pass with a single synchronisation;
+ * smaller ones are checked against the counted entries first (one extra round trip). */
 enum pqg_repetition { PQG_REQUIRED = 0, PQG_OPTIONAL = 1, PQG_REPEATED = 2 };
 
 typedef struct pqg_assembly_node {

@@ -150,6 +150,7 @@ struct pqg_plan {
   std::vector<uint64_t> col_required_values;
   std::vector<HostErr> host_errs;
   int kernels = 0;
+  int timeout_fallbacks = 0;           // launches re-run in split mode after PQG_ERR_TIMEOUT (pqg_sync)
 };
 
 struct pqg_ctx {
@@ -635,6 +636,8 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
 
 int pqg_plan_kernel_count(pqg_plan* P) { return P ? P->kernels : 0; }
 
+int pqg_plan_timeout_fallbacks(pqg_plan* P) { return P ? P->timeout_fallbacks : 0; }
+
 int pqg_plan_launch(pqg_plan* P) {
   if (!P) return PQG_ERR_INVALID_ARG;
   pqg_ctx* ctx = P->ctx;
@@ -874,6 +877,23 @@ int pqg_sync(pqg_ctx* ctx, pqg_status* st) {
   if (!P) return PQG_OK;
   std::vector<PageWork> work;
   int rc = resolve_errors(P, st, &work);
+  if (rc == PQG_ERR_TIMEOUT && P->dict_fused) {
+    // The fused dictionary kernel's hand-off relies on the walker workgroups being dispatched before
+    // the expansion workgroups that wait for them, which HIP does not promise. A launch in which an
+    // expansion waited past SPIN_TIMEOUT_TICKS (it then stops and reports PQG_ERR_TIMEOUT; the walkers
+    // still finish, so the grid drains) is re-run with the walk and the expansion as two launches,
+    // which have no inter-workgroup waits; the plan keeps that mode. Every output of the re-run is
+    // written again, so the result is the same bit for bit.
+    P->dict_fused = false;
+    for (int k : {C_DICT4, C_DICT8, C_IDS}) P->kernels += P->cls_n[(size_t)k] ? 1 : 0;
+    P->timeout_fallbacks++;
+    rc = pqg_plan_launch(P);
+    if (rc == PQG_OK) {
+      if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
+      work.clear();
+      rc = resolve_errors(P, st, &work);
+    }
+  }
   if (ctx->last_cols && P == ctx->last) {
     for (int i = 0; i < P->n_cols; i++) {
       uint64_t n = P->col_required_values[(size_t)i];
@@ -1211,10 +1231,22 @@ int pqg_assemble(pqg_ctx* ctx, const uint8_t* d_def_levels, const uint8_t* d_rep
   if (ctx->asm_scratch.ensure(cnt_bytes + 256) != hipSuccess || ctx->pin_err.ensure(256) != hipSuccess) return PQG_ERR_HIP;
   uint64_t* counts = (uint64_t*)ctx->asm_scratch.p;
   uint64_t* totals = (uint64_t*)((uint8_t*)ctx->asm_scratch.p + cnt_bytes);
+  bool any_out = false, bounded = true;
+  for (int k = 0; k < depth; k++) {
+    any_out = any_out || P.validity[k] || P.offsets[k];
+    // entries of any depth <= n_slots: outputs sized for that bound need no count round trip
+    if ((P.validity[k] && path[k].capacity < n_slots) || (P.offsets[k] && path[k].capacity < n_slots + 1)) bounded = false;
+  }
+  const bool one_pass = any_out && bounded;
   hipError_t e = pqg::launch_assemble(s, d > 0 ? d_def_levels : nullptr, r > 0 ? d_rep_levels : nullptr, n_slots, P,
                                       counts, n_blocks, totals, 0);
+  if (e == hipSuccess && one_pass) e = pqg::launch_assemble(s, d > 0 ? d_def_levels : nullptr, r > 0 ? d_rep_levels : nullptr,
+                                                            n_slots, P, counts, n_blocks, totals, 1);
   uint64_t* h_tot = (uint64_t*)ctx->pin_err.p;
   if (e == hipSuccess) e = hipMemcpyAsync(h_tot, totals, sizeof(uint64_t) * pqg::ASM_MAX_DEPTHS, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && one_pass && n_blocks == 0)  // no slots: closing offsets only (offsets[0] = 0)
+    for (int k = 0; k < depth && e == hipSuccess; k++)
+      if (P.kind[k] == PQG_REPEATED && P.offsets[k]) e = hipMemsetAsync(P.offsets[k], 0, sizeof(int64_t), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     set_status(st, PQG_ERR_HIP, -1, -1, hipGetErrorString(e));
@@ -1233,9 +1265,7 @@ int pqg_assemble(pqg_ctx* ctx, const uint8_t* d_def_levels, const uint8_t* d_rep
     set_status(st, PQG_ERR_INVALID_ARG, -1, bad, "assembly output capacity");
     return PQG_ERR_INVALID_ARG;
   }
-  bool any_out = false;
-  for (int k = 0; k < depth; k++) any_out = any_out || P.validity[k] || P.offsets[k];
-  if (!any_out) return PQG_OK;  // counts only
+  if (!any_out || one_pass) return PQG_OK;  // counts only, or already emitted
   e = pqg::launch_assemble(s, d > 0 ? d_def_levels : nullptr, r > 0 ? d_rep_levels : nullptr, n_slots, P, counts,
                            n_blocks, totals, 1);
   if (e == hipSuccess && n_blocks == 0)  // no slots: closing offsets only (offsets[0] = 0)

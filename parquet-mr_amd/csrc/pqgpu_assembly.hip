@@ -10,8 +10,9 @@
 // nextLevel[rep] (:284-306). Then, per entry of depth r starting at slot i:
 //   OPTIONAL node k at depth r:   validity = def[i] >= D(k)
 //   REPEATED node at depth r + 1: offsets[entry] = number of depth-(r+1) entries before slot i
-// so every output is a function of per-depth exclusive counts: three passes (block counts,
-// scan of the block counts, emit) over the levels, HBM-bound on the level bytes.
+// so every output is a function of per-depth exclusive counts: three kernels (block counts, scan
+// of the block counts, emit), the level bytes read twice with 16-byte loads, the outputs staged in
+// LDS per block and stored as whole dwords / int64 runs; HBM-bound on the level bytes and outputs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -21,6 +22,7 @@ namespace pqg {
 
 constexpr uint32_t ASM_BLOCK = 4096;  // slots per workgroup (256 threads x 16 slots)
 constexpr uint32_t ASM_PER_THREAD = 16;
+constexpr uint32_t ASM_SCAN_THREADS = 1024;
 
 __device__ __forceinline__ uint32_t asm_entries_mask(const AsmParams& P, uint32_t d, uint32_t r) {
   // bit q: slot begins an entry of depth q
@@ -31,119 +33,161 @@ __device__ __forceinline__ uint32_t asm_entries_mask(const AsmParams& P, uint32_
   return m;
 }
 
+// The 16 level bytes of thread slot range [s0, s0 + 16): one 16-byte load when the range is whole
+// (level arrays from pqg_decode are 256-byte aligned; any other alignment takes bytes), bytes at the tail.
+__device__ __forceinline__ void asm_load16(const uint8_t* __restrict__ a, uint64_t s0, uint64_t n, uint32_t (&w)[4]) {
+  if (!a) {
+    w[0] = w[1] = w[2] = w[3] = 0;
+  } else if (s0 + ASM_PER_THREAD <= n && (((uintptr_t)(a + s0)) & 15u) == 0) {
+    const u32x4 v = __builtin_nontemporal_load((const u32x4*)(a + s0));
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  } else {
+    w[0] = w[1] = w[2] = w[3] = 0;
+    for (uint32_t j = 0; j < ASM_PER_THREAD && s0 + j < n; j++) w[j >> 2] |= (uint32_t)a[s0 + j] << (8 * (j & 3));
+  }
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[4], uint32_t j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; }
+
 __global__ __launch_bounds__(256) void k_asm_count(const uint8_t* __restrict__ def, const uint8_t* __restrict__ rep,
                                                    uint64_t n, AsmParams P, uint64_t* __restrict__ block_counts) {
   __shared__ uint32_t red[4][ASM_MAX_DEPTHS];
   const uint64_t s0 = (uint64_t)blockIdx.x * ASM_BLOCK + (uint64_t)threadIdx.x * ASM_PER_THREAD;
+  uint32_t dw[4], rw[4];
+  asm_load16(def, s0, n, dw);
+  asm_load16(rep, s0, n, rw);
   uint32_t c[ASM_MAX_DEPTHS] = {};
+#pragma unroll
   for (uint32_t j = 0; j < ASM_PER_THREAD; j++) {
-    const uint64_t s = s0 + j;
-    if (s >= n) break;
-    const uint32_t m = asm_entries_mask(P, def ? def[s] : 0u, rep ? rep[s] : 0u);
+    const uint32_t m = s0 + j < n ? asm_entries_mask(P, byte_of(dw, j), byte_of(rw, j)) : 0u;
 #pragma unroll
     for (uint32_t q = 0; q < ASM_MAX_DEPTHS; q++) c[q] += (m >> q) & 1u;
   }
 #pragma unroll
   for (uint32_t q = 0; q < ASM_MAX_DEPTHS; q++) {
     uint32_t v = c[q];
+    if (q <= P.max_rep) {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+      for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    }
     if (lane_id() == 0) red[threadIdx.x >> 6][q] = v;
   }
   __syncthreads();
   if (threadIdx.x < ASM_MAX_DEPTHS) {
     const uint32_t q = threadIdx.x;
-    block_counts[(uint64_t)blockIdx.x * ASM_MAX_DEPTHS + q] = (uint64_t)red[0][q] + red[1][q] + red[2][q] + red[3][q];
+    block_counts[(uint64_t)blockIdx.x * ASM_MAX_DEPTHS + q] =
+        q <= P.max_rep ? (uint64_t)red[0][q] + red[1][q] + red[2][q] + red[3][q] : 0;
   }
 }
 
-// One workgroup: exclusive scan of every depth's block counts (in place); totals[q] = entries
-// of depth q (read by the host, which checks the output capacities before k_asm_emit).
-__global__ __launch_bounds__(256) void k_asm_scan(uint64_t* __restrict__ block_counts, uint32_t n_blocks, AsmParams P,
-                                                  uint64_t* __restrict__ totals) {
-  __shared__ uint64_t wsum[4];
-  __shared__ uint64_t carry;
+// One workgroup of 1024 threads: exclusive scan of every depth's block counts (in place); each
+// thread sums a contiguous segment of blocks, a workgroup scan of the segment sums gives the
+// segment bases, the segment is rewritten. totals[q] = entries of depth q.
+__global__ __launch_bounds__(ASM_SCAN_THREADS) void k_asm_scan(uint64_t* __restrict__ block_counts, uint32_t n_blocks,
+                                                               AsmParams P, uint64_t* __restrict__ totals) {
+  __shared__ uint64_t wsum[ASM_SCAN_THREADS / 64];
+  const uint32_t seg = (n_blocks + ASM_SCAN_THREADS - 1) / ASM_SCAN_THREADS;
+  const uint32_t b0 = min(n_blocks, threadIdx.x * seg), b1 = min(n_blocks, b0 + seg);
   for (uint32_t q = 0; q <= P.max_rep; q++) {
-    if (threadIdx.x == 0) carry = 0;
+    uint64_t v = 0;
+    for (uint32_t b = b0; b < b1; b++) v += block_counts[(uint64_t)b * ASM_MAX_DEPTHS + q];
+    const uint64_t x = wave_incl_scan_u64(v);
+    if (lane_id() == 63) wsum[threadIdx.x >> 6] = x;
     __syncthreads();
-    for (uint32_t b0 = 0; b0 < n_blocks; b0 += 256) {
-      const uint32_t b = b0 + threadIdx.x;
-      const uint64_t v = b < n_blocks ? block_counts[(uint64_t)b * ASM_MAX_DEPTHS + q] : 0;
-      uint64_t x = v;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(x, o);
-        if ((int)lane_id() >= o) x += y;
-      }
-      if (lane_id() == 63) wsum[threadIdx.x >> 6] = x;
-      __syncthreads();
-      uint64_t pre = carry;
-      for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) pre += wsum[w];
-      if (b < n_blocks) block_counts[(uint64_t)b * ASM_MAX_DEPTHS + q] = pre + x - v;
-      __syncthreads();
-      if (threadIdx.x == 255) carry = pre + x;
-      __syncthreads();
+    uint64_t pre = x - v;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) pre += wsum[w];
+    if (threadIdx.x == ASM_SCAN_THREADS - 1) totals[q] = pre + v;
+    for (uint32_t b = b0; b < b1; b++) {
+      const uint64_t c = block_counts[(uint64_t)b * ASM_MAX_DEPTHS + q];
+      block_counts[(uint64_t)b * ASM_MAX_DEPTHS + q] = pre;
+      pre += c;
     }
-    if (threadIdx.x == 0) totals[q] = carry;
     __syncthreads();
   }
 }
 
+// Outputs of one block: per node, the block's entries are a contiguous range of the node's output
+// (entries are numbered in slot order), so every thread writes its entries' values into an LDS image
+// of the range and the workgroup stores the image with wide stores (validity bytes: dwords with byte
+// stores only at the ends shared with the neighbouring blocks; offsets: int64 pairs).
 __global__ __launch_bounds__(256) void k_asm_emit(const uint8_t* __restrict__ def, const uint8_t* __restrict__ rep,
                                                   uint64_t n, AsmParams P, const uint64_t* __restrict__ block_counts,
                                                   const uint64_t* __restrict__ totals) {
   __shared__ uint32_t wsum[4][ASM_MAX_DEPTHS];
+  __shared__ uint64_t img[ASM_BLOCK];  // 32 KiB: one node's entries of this block
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // closing offsets: offsets[n_entries(r - 1)] = n_entries(r)
     for (uint32_t k = 0; k < P.n_nodes; k++)
       if (P.kind[k] == PQG_REPEATED && P.offsets[k]) gst(P.offsets[k] + totals[P.depth[k] - 1], (int64_t)totals[P.depth[k]]);
   }
   const uint64_t s0 = (uint64_t)blockIdx.x * ASM_BLOCK + (uint64_t)threadIdx.x * ASM_PER_THREAD;
-  uint32_t dv[ASM_PER_THREAD], mk[ASM_PER_THREAD];
+  uint32_t dw[4], rw[4];
+  asm_load16(def, s0, n, dw);
+  asm_load16(rep, s0, n, rw);
+  uint32_t mk[ASM_PER_THREAD];
   uint32_t c[ASM_MAX_DEPTHS] = {};
 #pragma unroll
   for (uint32_t j = 0; j < ASM_PER_THREAD; j++) {
-    const uint64_t s = s0 + j;
-    const bool in = s < n;
-    dv[j] = in && def ? def[s] : 0u;
-    mk[j] = in ? asm_entries_mask(P, dv[j], rep ? rep[s] : 0u) : 0u;
+    mk[j] = s0 + j < n ? asm_entries_mask(P, byte_of(dw, j), byte_of(rw, j)) : 0u;
 #pragma unroll
     for (uint32_t q = 0; q < ASM_MAX_DEPTHS; q++) c[q] += (mk[j] >> q) & 1u;
   }
-  // block-exclusive prefix of every depth's count -> the entry index of this thread's first slot
-  uint64_t idx[ASM_MAX_DEPTHS];
+  // block-local exclusive index of this thread's first entry of every depth, block totals
+  uint32_t li[ASM_MAX_DEPTHS], bt[ASM_MAX_DEPTHS];
 #pragma unroll
   for (uint32_t q = 0; q < ASM_MAX_DEPTHS; q++) {
-    uint32_t x = c[q];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o);
-      if ((int)lane_id() >= o) x += y;
-    }
-    if (lane_id() == 63) wsum[threadIdx.x >> 6][q] = x;
-    idx[q] = x - c[q];
+    uint32_t tot = 0;
+    li[q] = q <= P.max_rep ? wave_excl_scan_u32(c[q], &tot) : 0u;
+    if (lane_id() == 0) wsum[threadIdx.x >> 6][q] = tot;
   }
   __syncthreads();
 #pragma unroll
   for (uint32_t q = 0; q < ASM_MAX_DEPTHS; q++) {
-    uint64_t pre = block_counts[(uint64_t)blockIdx.x * ASM_MAX_DEPTHS + q];
+    uint32_t pre = 0;
     for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) pre += wsum[w][q];
-    idx[q] += pre;
+    li[q] += pre;
+    bt[q] = wsum[0][q] + wsum[1][q] + wsum[2][q] + wsum[3][q];
   }
-  for (uint32_t j = 0; j < ASM_PER_THREAD; j++) {
-    const uint32_t m = mk[j];
-    if (m) {
-      for (uint32_t k = 0; k < P.n_nodes; k++) {
-        const uint32_t q = P.depth[k];
-        if (P.kind[k] == PQG_OPTIONAL) {
-          if (((m >> q) & 1u) && P.validity[k]) gst(P.validity[k] + idx[q], (uint8_t)(dv[j] >= P.D[k] ? 1 : 0));
-        } else if (P.kind[k] == PQG_REPEATED) {
-          // one list per entry of the enclosing depth: offsets = entries of this depth before the slot
-          if (((m >> (q - 1)) & 1u) && P.offsets[k]) gst(P.offsets[k] + idx[q - 1], (int64_t)idx[q]);
-        }
-      }
-    }
+  const uint64_t* bc = block_counts + (uint64_t)blockIdx.x * ASM_MAX_DEPTHS;
+  uint8_t* img8 = (uint8_t*)img;
+  for (uint32_t k = 0; k < P.n_nodes; k++) {
+    const uint32_t q = P.depth[k];
+    if (P.kind[k] == PQG_OPTIONAL && P.validity[k]) {
+      const uint32_t Dk = P.D[k];
+      uint32_t l = li[q];
 #pragma unroll
-    for (uint32_t q = 0; q < ASM_MAX_DEPTHS; q++) idx[q] += (m >> q) & 1u;
+      for (uint32_t j = 0; j < ASM_PER_THREAD; j++)
+        if ((mk[j] >> q) & 1u) img8[l++] = byte_of(dw, j) >= Dk ? 1 : 0;
+      __syncthreads();
+      // bytes [B, B + cnt) of validity[k]: aligned dwords inside, bytes at both ends
+      uint8_t* g = P.validity[k] + bc[q];
+      const uint32_t cnt = bt[q];
+      const uint32_t head = (uint32_t)((4u - ((uintptr_t)g & 3u)) & 3u) < cnt ? (uint32_t)((4u - ((uintptr_t)g & 3u)) & 3u) : cnt;
+      const uint32_t nd = (cnt - head) >> 2;
+      for (uint32_t i = threadIdx.x; i < nd; i += 256) {
+        const uint32_t o = head + 4 * i;
+        const uint32_t v = (uint32_t)img8[o] | ((uint32_t)img8[o + 1] << 8) | ((uint32_t)img8[o + 2] << 16) |
+                           ((uint32_t)img8[o + 3] << 24);
+        gst((uint32_t*)(g + o), v);
+      }
+      const uint32_t tail0 = head + 4 * nd;
+      if (threadIdx.x < head) gst(g + threadIdx.x, img8[threadIdx.x]);
+      if (threadIdx.x >= 64 && threadIdx.x - 64 < cnt - tail0) gst(g + tail0 + (threadIdx.x - 64), img8[tail0 + (threadIdx.x - 64)]);
+      __syncthreads();
+    } else if (P.kind[k] == PQG_REPEATED && P.offsets[k]) {
+      // one list per entry of the enclosing depth q - 1: its offset = entries of depth q before the slot
+      uint32_t l = li[q - 1];
+      uint64_t e = bc[q] + li[q];
+#pragma unroll
+      for (uint32_t j = 0; j < ASM_PER_THREAD; j++) {
+        if ((mk[j] >> (q - 1)) & 1u) img[l++] = e;
+        e += (mk[j] >> q) & 1u;
+      }
+      __syncthreads();
+      int64_t* g = P.offsets[k] + bc[q - 1];
+      const uint32_t cnt = bt[q - 1];
+      for (uint32_t i = threadIdx.x; i < cnt; i += 256) gst(g + i, (int64_t)img[i]);
+      __syncthreads();
+    }
   }
 }
 
@@ -151,7 +195,7 @@ hipError_t launch_assemble(hipStream_t st, const uint8_t* def, const uint8_t* re
                            uint64_t* block_counts, uint32_t n_blocks, uint64_t* totals, int phase) {
   if (phase == 0) {
     if (n_blocks) hipLaunchKernelGGL(k_asm_count, dim3(n_blocks), dim3(256), 0, st, def, rep, n, P, block_counts);
-    hipLaunchKernelGGL(k_asm_scan, dim3(1), dim3(256), 0, st, block_counts, n_blocks, P, totals);
+    hipLaunchKernelGGL(k_asm_scan, dim3(1), dim3(ASM_SCAN_THREADS), 0, st, block_counts, n_blocks, P, totals);
   } else if (n_blocks) {
     hipLaunchKernelGGL(k_asm_emit, dim3(n_blocks), dim3(256), 0, st, def, rep, n, P, block_counts, totals);
   }

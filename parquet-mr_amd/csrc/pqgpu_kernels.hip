@@ -1575,7 +1575,14 @@ constexpr uint32_t XT_LDS_BYTES = DICT_LDS_BYTES + WPB * (XT_RUNS * 16 + XT_SEG)
 #ifndef PQG_SPIN_SLEEP
 #define PQG_SPIN_SLEEP 2
 #endif
+#ifdef PQG_FAULT_INJECT
+// Fault-injection build (tests/build/libpqgpu_faultinject.so, tests/test_gpu_timeout.py only; never
+// the product): walker workgroup 0 of every fused launch starts PQG_FAULT_INJECT ticks late, past a
+// spin timeout shortened to 0.1 s, so the expansions waiting for its pages time out.
+constexpr uint64_t SPIN_TIMEOUT_TICKS = 10000000ull;
+#else
 constexpr uint64_t SPIN_TIMEOUT_TICKS = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+#endif
 
 
 
@@ -1946,6 +1953,12 @@ __global__ __launch_bounds__(64 * WPB) PQG_FUSED_ATTR void k_dict_fused(const ui
       if (!walk_wg) break;
     }
   } else if (blockIdx.x < n_walk) {
+#ifdef PQG_FAULT_INJECT
+    if (blockIdx.x == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)PQG_FAULT_INJECT) __builtin_amdgcn_s_sleep(127);
+    }
+#endif
     for (uint32_t g = blockIdx.x; g * WPB < (uint32_t)n_list; g += walk_wg) {
       dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
                         lds, g);

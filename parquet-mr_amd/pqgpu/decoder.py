@@ -83,6 +83,11 @@ class Plan:
     def kernel_count(self):
         return native.lib().pqg_plan_kernel_count(self.handle)
 
+    @property
+    def timeout_fallbacks(self):
+        """Launches re-run in split mode after a fused-kernel wait timed out (pqg_plan_timeout_fallbacks)."""
+        return native.lib().pqg_plan_timeout_fallbacks(self.handle)
+
     def sync(self):
         st = abi.Status()
         rc = native.lib().pqg_sync(self.decoder.ctx, C.byref(st))

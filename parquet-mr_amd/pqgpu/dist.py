@@ -2,17 +2,20 @@
 
 A row group's column chunks decode with no cross-chunk state, so ranks decode
 disjoint row groups with no data-path collective. The only exchange is the final column
-concatenation, when a consumer wants the full column on every rank (all-gather over RCCL):
+concatenation, when a consumer wants the full column on every rank:
 
-  * fixed-width columns: output offsets of each row group are prefix sums of footer row counts,
-    so the decoded slices are all-gathered as they are;
-  * BYTE_ARRAY columns: one all-gather of every rank's byte total, an exclusive scan of them for
-    the ranks' byte bases, then the offsets and value bytes are all-gathered and each row group's
-    offsets rebased onto the concatenated byte buffer.
-
-Reference parallelism being restated: Hadoop InputSplits at row-group granularity
-(parquet-hadoop/src/main/java/org/apache/parquet/hadoop/ParquetInputFormat.java: getSplits :350,
-generateSplits :786).
+  * shards are contiguous runs of row groups in file order, balanced by encoded bytes (the
+    Hadoop split: ParquetInputFormat.generateSplitInfo assigns row groups to splits in file order
+    by compressed size, parquet-hadoop/src/main/java/org/apache/parquet/hadoop/ParquetInputFormat.java
+    :807-841, via getSplits :350 / generateSplits :786), so the full column is the ranks' slices
+    back to back: rank r's rows land at a fixed offset of the output;
+  * fixed-width columns: one all-gather straight into the output (`all_gather_into_tensor` when
+    the slices are equal, otherwise one batch of point-to-point copies, each rank's slice sent once
+    to every peer: on xGMI's fully connected links the peers are direct neighbours), no padding;
+  * BYTE_ARRAY columns: one all-gather of every rank's byte total (one int64 each), their exclusive
+    scan gives every rank's byte base, each rank rebases its own offsets on the device (one add), and
+    the rebased offsets and the value bytes are gathered into the output the same way. No O(rows)
+    host transfer and no per-row-group host loop.
 """
 import numpy as np
 import torch
@@ -20,16 +23,22 @@ import torch.distributed as dist
 
 
 def shard_row_groups(sizes, world):
-    """Greedy longest-processing-time assignment of row groups (by encoded bytes) to ranks.
-    Returns, per rank, the sorted list of its row-group indices."""
-    order = sorted(range(len(sizes)), key=lambda i: (-sizes[i], i))
-    load = [0] * world
+    """Contiguous row-group ranges, one per rank, balanced by encoded bytes: rank r takes the row
+    groups whose byte midpoint falls in [r, r + 1) * total / world (file order kept, as Hadoop's
+    splits keep it). Returns, per rank, its ascending list of row-group indices."""
+    sizes = np.asarray(sizes, dtype=np.float64)
     out = [[] for _ in range(world)]
-    for i in order:
-        r = min(range(world), key=lambda k: (load[k], k))
-        out[r].append(i)
-        load[r] += sizes[i]
-    return [sorted(x) for x in out]
+    if sizes.size == 0:
+        return out
+    total = float(sizes.sum())
+    mid = np.cumsum(sizes) - sizes / 2
+    if total > 0:
+        owner = np.minimum((mid * world / total).astype(np.int64), world - 1)
+    else:
+        owner = np.arange(sizes.size) * world // sizes.size
+    for i, r in enumerate(owner):
+        out[int(r)].append(i)
+    return out
 
 
 def row_group_offsets(row_counts):
@@ -37,52 +46,73 @@ def row_group_offsets(row_counts):
     return np.concatenate([[0], np.cumsum(np.asarray(row_counts, dtype=np.int64))])[:-1]
 
 
+def _check_contiguous(shards):
+    flat = [g for s in shards for g in s]
+    assert flat == list(range(len(flat))), "shards must be contiguous row-group ranges in rank order"
+
+
 def _on_backend(t, group):
     """gloo collectives run on host tensors; RCCL (backend "nccl") on device tensors."""
     return t.cpu() if dist.get_backend(group) == "gloo" else t
 
 
-def _all_gather_padded(t, maxlen, group):
-    """All-gather 1-D tensors of different lengths (each padded to maxlen)."""
+def all_gather_into(out, local, sizes, group=None):
+    """All-gather 1-D slices of per-rank `sizes` (elements) into `out` = the slices back to back in
+    rank order, with no padding: all_gather_into_tensor when every size is equal, otherwise one
+    batch of point-to-point sends / receives (rank r's slice to every peer)."""
     world = dist.get_world_size(group)
-    src = _on_backend(t, group)
-    buf = torch.zeros(maxlen, dtype=src.dtype, device=src.device)
-    buf[: src.numel()] = src
-    out = torch.empty(world * maxlen, dtype=src.dtype, device=src.device)
-    if src.is_cuda:
-        dist.all_gather_into_tensor(out, buf, group=group)
+    rank = dist.get_rank(group)
+    assert local.numel() == sizes[rank] and out.numel() == sum(sizes)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    dst = _on_backend(out, group)
+    src = _on_backend(local, group)
+    if world == 1 or len(set(sizes)) == 1:
+        if world == 1:
+            dst.copy_(src)
+        elif dst.is_cuda:
+            dist.all_gather_into_tensor(dst, src.contiguous(), group=group)
+        else:
+            dist.all_gather(list(dst.view(world, sizes[0]).unbind(0)), src.contiguous(), group=group)
     else:
-        dist.all_gather(list(out.view(world, maxlen).unbind(0)), buf, group=group)
-    return out.view(world, maxlen).to(t.device)
+        dst[int(off[rank]): int(off[rank + 1])].copy_(src)
+        ops = []
+        for peer in range(world):
+            if peer == rank:
+                continue
+            if sizes[rank]:
+                ops.append(dist.P2POp(dist.isend, src.contiguous(), dist.get_global_rank(group, peer)
+                                      if group is not None else peer, group))
+            if sizes[peer]:
+                ops.append(dist.P2POp(dist.irecv, dst[int(off[peer]): int(off[peer + 1])],
+                                      dist.get_global_rank(group, peer) if group is not None else peer, group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+    if dst is not out:
+        out.copy_(dst)
+    return out
 
 
 def gather_column(local, my_rgs, shards, row_counts, group=None):
     """All-gather fixed-width decoded slices into the full column on every rank.
 
     local:  1-D tensor = this rank's row groups (my_rgs, ascending) decoded back to back.
-    shards: every rank's row-group list (shard_row_groups output).
+    shards: every rank's contiguous row-group range (shard_row_groups output).
     Returns the concatenated column (rows of all row groups in row-group order).
     """
+    _check_contiguous(shards)
     counts = np.asarray(row_counts, dtype=np.int64)
     per_rank = [int(counts[s].sum()) for s in shards]
-    assert local.numel() == per_rank[dist.get_rank(group)], (local.numel(), per_rank)
-    parts = _all_gather_padded(local, max(per_rank) if per_rank else 0, group)
-    offs = row_group_offsets(counts)
     full = torch.empty(int(counts.sum()), dtype=local.dtype, device=local.device)
-    for r, rgs in enumerate(shards):
-        pos = 0
-        for rg in rgs:
-            n = int(counts[rg])
-            full[int(offs[rg]): int(offs[rg]) + n] = parts[r][pos: pos + n]
-            pos += n
-    return full
+    return all_gather_into(full, local, per_rank, group)
 
 
 def gather_binary(offsets, data, my_rgs, shards, row_counts, group=None):
     """All-gather a BYTE_ARRAY column (int64 offsets[n + 1] from 0 + value bytes) whose rows are this
     rank's row groups back to back. Returns (offsets[N + 1], data) of the full column in row-group
-    order: one all-gather of the byte totals (int64 per rank), their exclusive scan, then the offsets
-    and the bytes, each row group's offsets rebased onto the concatenated bytes."""
+    order: one all-gather of the byte totals (one int64 per rank); every rank adds its byte base to
+    its own offsets on the device; the rebased offsets and the bytes are gathered into the outputs."""
+    _check_contiguous(shards)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     counts = np.asarray(row_counts, dtype=np.int64)
@@ -90,32 +120,14 @@ def gather_binary(offsets, data, my_rgs, shards, row_counts, group=None):
     n_local = per_rank[rank]
     assert offsets.numel() == n_local + 1, (offsets.numel(), n_local)
     total = offsets[n_local: n_local + 1].to(torch.int64)
-    totals = _all_gather_padded(total, 1, group).view(world).cpu().numpy()
-    byte_base = np.concatenate([[0], np.cumsum(totals)])
-    d_parts = _all_gather_padded(data[: int(totals[rank])], int(totals.max()) if world else 0, group)
-    o_parts = _all_gather_padded(offsets[:n_local], max(per_rank), group)
-    rg_off = row_group_offsets(counts)
-    # bytes of the full column are the ranks' bytes in row-group order; each row group's byte range
-    # inside its rank comes from that rank's own offsets
+    totals_t = torch.empty(world, dtype=torch.int64, device=offsets.device)
+    all_gather_into(totals_t, total, [1] * world, group)
+    totals = [int(x) for x in totals_t.cpu().tolist()]        # world int64s
+    base = int(np.sum(totals[:rank], dtype=np.int64))
+    rebased = offsets[:n_local] + base                       # device rebase onto the full byte buffer
     full_off = torch.empty(int(counts.sum()) + 1, dtype=torch.int64, device=offsets.device)
-    segs = []
-    rg_src = {}
-    for r, rgs in enumerate(shards):
-        pos = 0
-        for rg in rgs:
-            rg_src[rg] = (r, pos)
-            pos += int(counts[rg])
-    o_host = [o_parts[r, : per_rank[r]].cpu().numpy() for r in range(world)]
-    run = 0
-    for rg in range(len(counts)):
-        r, pos = rg_src[rg]
-        n = int(counts[rg])
-        lo = int(o_host[r][pos]) if n else 0
-        hi = int(o_host[r][pos + n]) if pos + n < per_rank[r] else int(totals[r])
-        full_off[int(rg_off[rg]): int(rg_off[rg]) + n] = o_parts[r, pos: pos + n] - lo + run
-        segs.append(d_parts[r, lo:hi])
-        run += hi - lo
-    full_off[-1] = run
-    full_data = torch.cat(segs) if segs else torch.zeros(0, dtype=data.dtype, device=data.device)
-    assert run == int(byte_base[-1])
+    all_gather_into(full_off[:-1], rebased, per_rank, group)
+    full_off[-1] = int(np.sum(totals, dtype=np.int64))
+    full_data = torch.empty(int(np.sum(totals, dtype=np.int64)), dtype=data.dtype, device=data.device)
+    all_gather_into(full_data, data[: totals[rank]], totals, group)
     return full_off, full_data

@@ -33,6 +33,7 @@ def _row_groups():
 
 def _worker(rank, world, port, q):
     import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     from oracle import pqref
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -67,8 +68,47 @@ def _worker(rank, world, port, q):
     allv = [bytes(v) for ch in brgs for v in ch.values]
     exp_off = np.concatenate([[0], np.cumsum([len(v) for v in allv])])
     ok_b = bool(np.array_equal(foff.numpy(), exp_off)) and fdata.numpy().tobytes() == b"".join(allv)
-    q.put((rank, ok and ok_b, [len(s) for s in shards], [len(s) for s in bshards]))
+    ok_c4 = _c4_gather(rank, world)
+    q.put((rank, ok and ok_b and ok_c4, [len(s) for s in shards], [len(s) for s in bshards]))
     dist.destroy_process_group()
+
+
+def _c4_gather(rank, world):
+    """C4 lineitem row groups (small ones: 5 x 20,000 rows) sharded over the ranks, each rank's share
+    decoded (the oracle here; the GPU decode of the same row groups runs in the -m gpu tests), then
+    l_orderkey (int64) and l_comment (BYTE_ARRAY) gathered into the full columns on every rank."""
+    import lineitem as LI
+    from oracle import pqref
+    rgs, base = [], 0
+    for g in range(5):
+        ch, ex, n_ord = LI.make_row_group(20_000, 500 + g, base)
+        base += n_ord
+        rgs.append((ch, ex))
+    sizes = [sum(len(p.body) for c in ch for p in c.pages) for ch, _ in rgs]
+    shards = pdist.shard_row_groups(sizes, world)
+    mine = shards[rank]
+    keys, offs, data = [], [np.zeros(1, np.int64)], []
+    for g in mine:
+        r = pqref.decode_batch(writer.build_batch([rgs[g][0][0], rgs[g][0][15]]))
+        assert r.code == 0
+        keys.append(r.columns[0]["values"])
+        vals = r.columns[1]["values"]
+        offs.append(offs[-1][-1] + np.cumsum([len(v) for v in vals]))
+        data.append(np.frombuffer(b"".join(vals), dtype=np.uint8))
+    counts = [20_000] * 5
+    full = pdist.gather_column(torch.from_numpy(np.concatenate(keys) if keys else np.zeros(0, np.int64)), mine, shards,
+                               counts)
+    ok = np.array_equal(full.numpy(), np.concatenate([ex[0].values for _, ex in rgs]))
+    foff, fdata = pdist.gather_binary(torch.from_numpy(np.concatenate(offs)),
+                                      torch.from_numpy(np.concatenate(data) if data else np.zeros(0, np.uint8)),
+                                      mine, shards, counts)
+    exp_off, exp_data = [np.zeros(1, np.int64)], []
+    for _, ex in rgs:
+        v = ex[15].values
+        exp_off.append(exp_off[-1][-1] + v.offsets[1:])
+        exp_data.append(v.data[: v.offsets[-1]])
+    ok = ok and np.array_equal(foff.numpy(), np.concatenate(exp_off))
+    return bool(ok and np.array_equal(fdata.numpy(), np.concatenate(exp_data)))
 
 
 def _binary_row_groups():
@@ -83,11 +123,18 @@ def _binary_row_groups():
     return rgs
 
 
-def test_shard_row_groups_balanced():
-    sh = pdist.shard_row_groups([10, 9, 8, 1, 1, 1, 7, 3], 3)
-    assert sorted(sum(sh, [])) == list(range(8))
-    loads = [sum([10, 9, 8, 1, 1, 1, 7, 3][i] for i in s) for s in sh]
-    assert max(loads) - min(loads) <= 3
+def test_shard_row_groups_contiguous_and_balanced():
+    sizes = [10, 9, 8, 1, 1, 1, 7, 3]
+    sh = pdist.shard_row_groups(sizes, 3)
+    assert sum(sh, []) == list(range(8))               # contiguous ranges in file order, rank order
+    loads = [sum(sizes[i] for i in s) for s in sh]
+    assert max(loads) - min(loads) <= max(sizes)        # balanced within one row group
+    # the configured C4 shard: 1,000 near-equal row groups over 8 ranks -> 125 each
+    rng = np.random.default_rng(0)
+    sh8 = pdist.shard_row_groups(75_330_000 + rng.integers(-20_000, 20_000, size=1000), 8)
+    assert [len(s) for s in sh8] == [125] * 8
+    assert pdist.shard_row_groups([], 4) == [[], [], [], []]
+    assert sum(pdist.shard_row_groups([5, 5], 4), []) == [0, 1]
 
 
 def test_row_group_offsets():

@@ -139,3 +139,37 @@ def test_c4_lineitem_row_groups(decoder):
     assert rc == 0, st.message
     WL.verify(cols, work, "plan")
     plan.close()
+
+
+def poison(cols, byte=0xA5):
+    for c in cols:
+        for t in (c.values, c.def_levels, c.rep_levels, c.binary_data):
+            if t is not None:
+                t.fill_(byte)
+
+
+def test_c4_configured_shard(decoder):
+    """C4 at its configured per-GPU size: 1 B rows / 8 GPUs = 125 M rows = 125 row groups of 1 M rows,
+    100,000 pages, 636 pqg columns (BASELINE configs[3]; the row-group split of
+    ParquetInputFormat.java:350,786 as pqgpu.dist.shard_row_groups makes it for rank 0 of 8 with the
+    1 B-row table). An oracle sample of every column first; then the FIRST launch of a fresh plan
+    into poisoned outputs must give every row group x column slice == its generated values, and
+    again after more launches."""
+    import lineitem as LI
+    shard = LI.Shard(1_000_000_000, world=8, rank=0)
+    assert len(shard.mine) == 125 and shard.batch.n_pages == 100_000
+    oracle_sample(WL.Workload("c4 rg0", shard.templates[0][0], shard.templates[0][1]), 5)
+    dbatch = decoder.upload(shard.batch)
+    cols, st = decoder.decode(dbatch)          # sizes the BYTE_ARRAY buffers
+    poison(cols)
+    plan = decoder.plan(dbatch, cols)
+    plan.launch()                              # first launch of a fresh plan
+    rc, st = plan.sync()
+    assert rc == 0, st.message
+    shard.verify(cols, decoder.device, "first launch")
+    for _ in range(3):
+        plan.launch()
+    rc, st = plan.sync()
+    assert rc == 0, st.message
+    shard.verify(cols, decoder.device, "after 4 launches")
+    plan.close()

@@ -9,7 +9,8 @@ bench.py prints the ONE headline line (C2). This suite times the other configs a
   c3_mixed       C3: 8 optional columns (2 int32 + 2 int64 DELTA_BINARY_PACKED, 2 double PLAIN,
                  2 BYTE_ARRAY PLAIN of 4-32 bytes), 10 % nulls, RLE def levels, V2 pages
   c5_levels      C5: LIST<int64> records (Poisson(3) lengths, 10 % null lists / elements),
-                 rep + def levels and values (record assembly is the next row)
+                 rep + def levels and values, then record assembly (pqg_assemble_schema: list
+                 validity + offsets, element validity) in every timed step
   str_plain / str_dict / str_dlba / str_dba   BYTE_ARRAY encodings, 4-32 byte strings
   bss_f64        BYTE_STREAM_SPLIT doubles
   delta_i64      DELTA_BINARY_PACKED int64 random walk
@@ -159,6 +160,26 @@ def cpu_sample(chunks, max_pages, budget_s):
             "sample": f"first {max_pages} pages of every column, {reps} reps, {dt:.1f} s{label}"}
 
 
+C5_SCHEMA = [(-1, abi.OPTIONAL), (0, abi.REPEATED), (1, abi.OPTIONAL)]  # optional group list (repeated element: optional int64)
+
+
+def c5_assemble(dec, cols, batch):
+    """Record assembly of the C5 column (RecordReaderImplementation.read's records in columnar form)."""
+    return dec.assemble_schema(C5_SCHEMA, [(2, cols[0].def_levels, cols[0].rep_levels, batch.column_slots[0])])
+
+
+def c5_verify_assembly(got, work, dev):
+    import torch
+    lens, null_list = work.lists["lens"], work.lists["null_list"]
+    assert got["records"] == lens.size
+    assert torch.equal(got["nodes"][0]["validity"], torch.from_numpy((~null_list).astype(np.uint8)).to(dev)), "list validity"
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)).to(dev)
+    assert torch.equal(got["nodes"][1]["offsets"], offs), "list offsets"
+    dl = work.expect[0].def_levels
+    assert torch.equal(got["nodes"][2]["validity"], torch.from_numpy((dl[dl >= 2] == 3).astype(np.uint8)).to(dev)), \
+        "element validity"
+
+
 def run(name, rows, steps, warmup, cpu_budget):
     import torch
     from pqgpu import decoder as D
@@ -185,17 +206,39 @@ def run(name, rows, steps, warmup, cpu_budget):
         plan.launch()
     rc, st = plan.sync()
     assert rc == 0, st.message
+    assemble = name == "c5_levels"
+    if assemble:
+        c5_verify_assembly(c5_assemble(dec, cols, batch), work, dec.device)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     torch.cuda.synchronize()
     ev[0].record(dec.stream)
     for k in range(steps):
         dec.decompress(dbatch)
         plan.launch()
+        if assemble:  # the step includes the record assembly (synchronous: levels must be decoded)
+            got = c5_assemble(dec, cols, batch)
         ev[k + 1].record(dec.stream)
     torch.cuda.synchronize()
     rc, st = plan.sync()
     assert rc == 0, st.message
     WL.verify(cols, work, "after the timed launches")
+    asm = None
+    if assemble:
+        c5_verify_assembly(got, work, dec.device)
+        ea = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        torch.cuda.synchronize()
+        ea[0].record(dec.stream)
+        for _ in range(steps):
+            got = c5_assemble(dec, cols, batch)
+        ea[1].record(dec.stream)
+        torch.cuda.synchronize()
+        a_ms = ea[0].elapsed_time(ea[1]) / steps
+        n_sl = batch.column_slots[0]
+        out_b = sum(int(x["validity"].numel()) if x["validity"] is not None else 8 * int(x["offsets"].numel())
+                    for x in got["nodes"])
+        asm = {"assembly_ms": a_ms, "records": got["records"], "records_per_s": got["records"] / (a_ms / 1e3),
+               "assembly_bytes": 2 * n_sl + out_b, "assembly_gbps": (2 * n_sl + out_b) / (a_ms / 1e3) / 1e9,
+               "verified": "list validity / offsets and element validity == the generated list structure"}
     ms = float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(steps)]))
     nvals = sum(c.n_values for c in cols)
     nslots = sum(batch.column_slots)
@@ -206,6 +249,12 @@ def run(name, rows, steps, warmup, cpu_budget):
            "encoded_bytes": enc, "output_bytes": out, "gbps": gbps, "hbm_frac": gbps / HBM_PEAK_GBS,
            "kernels_per_launch": plan.kernel_count, "input_gen_s": t_gen,
            "verified": "decoded columns == generated values (decode, first plan launch, after the timed launches)"}
+    if asm:
+        res["step"] = "plan launch (levels + values) + pqg_assemble_schema"
+        res["records_per_s"] = asm["records"] / (ms / 1e3)
+        res["assembly"] = asm
+        res["gbps"] = (enc + out + asm["assembly_bytes"]) / (ms / 1e3) / 1e9
+        res["hbm_frac"] = res["gbps"] / HBM_PEAK_GBS
     if compressed:
         comp = sum(len(p.body) for ch in chunks for p in ch.pages) + sum(len(ch.dict_page or b"") for ch in chunks)
         ev2 = [torch.cuda.Event(enable_timing=True) for _ in range(2)]

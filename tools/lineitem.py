@@ -131,3 +131,79 @@ def make_c4(rows, rg_rows=1_000_000, seed=1000):
         chunks += c
         exp += e
     return Workload("c4_lineitem", chunks, exp)
+
+
+class Shard:
+    """One rank's share of the C4 table: `rows` rows in total in row groups of `rg_rows`, split over
+    `world` ranks by encoded bytes (pqgpu.dist.shard_row_groups, the Hadoop row-group split,
+    ParquetInputFormat.java:350,786). T distinct synthetic row groups are laid out repeatedly (row
+    group g = template g mod T): every copy's pages are decoded, none is skipped. Dictionary columns
+    are one pqg column per row group (each row group has its own dictionary); the other columns
+    decode every row group of the rank into one rank-wide column, back to back."""
+
+    def __init__(self, rows, world=1, rank=0, templates=4, rg_rows=1_000_000):
+        import copy
+
+        from pqgpu import dist as pdist
+        self.rg_rows = rg_rows
+        self.n_rg = max(1, rows // rg_rows)
+        self.T = min(templates, self.n_rg)
+        self.templates, base = [], 0
+        for t in range(self.T):
+            ch, ex, n_ord = make_row_group(rg_rows, 1000 + t, base)
+            base += n_ord
+            self.templates.append((ch, ex))
+        tsize = [sum(len(p.body) for c in ch for p in c.pages) for ch, _ in self.templates]
+        self.shards = pdist.shard_row_groups([tsize[g % self.T] for g in range(self.n_rg)], world)
+        self.mine = self.shards[rank]
+        self.chunks = []
+        for g in self.mine:
+            for k, c in enumerate(self.templates[g % self.T][0]):
+                cc = copy.copy(c)
+                cc.column_index = (k, g) if c.dict_page is not None else (k, -1)
+                self.chunks.append(cc)
+        self.batch = writer.build_batch(self.chunks)
+        self.col_of = {}
+        for c in self.chunks:
+            self.col_of.setdefault(c.column_index, len(self.col_of))
+
+    def column(self, k, g):
+        """pqg column index of lineitem column k in row group g, and whether it is rank-wide."""
+        merged = (k, -1) in self.col_of
+        return (self.col_of[(k, -1)] if merged else self.col_of[(k, g)]), merged
+
+    def verify(self, cols, device, what):
+        """Every row group x column slice of the decoded columns == its template's generated values
+        (compared on the device)."""
+        import torch
+        exp_dev = {}
+        pos = {k: 0 for k in range(16)}
+        n = self.rg_rows
+        for g in self.mine:
+            t = g % self.T
+            for k in range(16):
+                ci, merged = self.column(k, g)
+                col = cols[ci]
+                ex = self.templates[t][1][k]
+                if (t, k) not in exp_dev:
+                    if isinstance(ex.values, writer.BinaryValues):
+                        exp_dev[(t, k)] = (torch.from_numpy(ex.values.offsets).to(device),
+                                           torch.from_numpy(ex.values.data).to(device))
+                    else:
+                        exp_dev[(t, k)] = torch.from_numpy(np.ascontiguousarray(ex.values).view(np.uint8)).to(device)
+                e = exp_dev[(t, k)]
+                r0 = pos[k] if merged else 0
+                if isinstance(e, tuple):
+                    offs = col.offsets()[r0:r0 + n + 1]
+                    b0 = int(offs[0].item())
+                    assert torch.equal(offs - b0, e[0]), f"{what}: row group {g} column {k} offsets"
+                    assert torch.equal(col.binary_data[b0:b0 + e[1].numel()], e[1]), f"{what}: rg {g} col {k} bytes"
+                else:
+                    w = e.numel() // n
+                    assert torch.equal(col.values[r0 * w:(r0 + n) * w], e), f"{what}: row group {g} column {k}"
+                if merged:
+                    pos[k] += n
+        for k in range(16):  # every rank-wide column holds exactly its row groups' values
+            ci, merged = self.column(k, self.mine[0]) if self.mine else (None, False)
+            if merged:
+                assert cols[ci].n_values == len(self.mine) * n, f"{what}: column {k} value count"
