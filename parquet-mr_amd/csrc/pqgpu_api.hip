@@ -125,7 +125,6 @@ struct pqg_plan {
   bool dict_fused = true;
   uint32_t chunk_off[N_DICT_CLS] = {0, 0, 0}, chunk_n[N_DICT_CLS] = {0, 0, 0};  // ranges in `chunks`
   // fused dictionary kernel: persistent walker / tile workgroup counts (0: one page / 4 chunks per WG)
-  uint32_t dict_walk_wg = 0, dict_tile_wg = 0, dict_walk_pg = 0;
   // BYTE_ARRAY / fixed-width-dictionary scratch (ColumnDev::blen, bsrc, dict_len, dict_src, block_sums,
   // bin_total), dictionary walks, post-passes, offset-scan blocks, copy chunks
   DevBuf bscratch, bin_lists, bin_blocks, bin_chunks, dba_chunks;
@@ -494,7 +493,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
         continue;
       }
       if (k == C_IDS) bind.push_back(p);
-      const uint32_t nch = (w.num_slots + pqg::BIN_CHUNK - 1) / pqg::BIN_CHUNK;
+      const uint32_t nch = (w.num_slots + pqg::CP_CHUNK_VALUES - 1) / pqg::CP_CHUNK_VALUES;
       for (uint32_t j = 0; j < nch; j++) bin_chunks.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
     }
   // ---- DELTA_BYTE_ARRAY pages: BIN_CHUNK-value chunks (upper bound from the slot count)
@@ -576,15 +575,6 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
             P->pstat.ensure(sizeof(uint64_t) * (size_t)std::max(n_pages, 1)) == hipSuccess &&
             P->flags.ensure(sizeof(uint32_t) * (size_t)std::max(n_pages, 1)) == hipSuccess;
   ok = ok && hipMemsetAsync(P->flags.p, 0, sizeof(uint32_t) * (size_t)std::max(n_pages, 1), s) == hipSuccess;
-  {
-    const char* e = getenv("PQG_DICT_SPLIT");  // A/B switch: walk and tiles as two launches
-    P->dict_fused = !(e && e[0] == '1');
-    // persistent walker / tile workgroups of the fused kernel (A/B knobs; 0 = one unit per WG)
-    if (const char* w = getenv("PQG_DICT_WALK_WG")) P->dict_walk_wg = (uint32_t)std::max(0, atoi(w));
-    if (const char* t = getenv("PQG_DICT_TILE_WG")) P->dict_tile_wg = (uint32_t)std::max(0, atoi(t));
-    // dictionary walk: one workgroup per page (dict_page_wg, 1) or one wave per page (0)
-    if (const char* g = getenv("PQG_DICT_WALK_PG")) P->dict_walk_pg = (uint32_t)std::max(0, atoi(g));
-  }
   {
     uint8_t* scb = (uint8_t*)P->bscratch.p;
     auto at = [&](uint64_t o) -> void* { return o == ~0ull ? nullptr : (void*)(scb + o); };
@@ -685,16 +675,14 @@ int pqg_plan_launch(pqg_plan* P) {
         const int i = k - C_DICT4;
         e = pqg::launch_dict(k == C_DICT8 ? 8 : 4, s, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
                              (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->chunk_off[i], P->chunk_n[i],
-                             (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused,
-                             P->dict_walk_wg, P->dict_tile_wg, P->dict_walk_pg, err, ecount);
+                             (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused, err, ecount);
         break;
       }
       case C_IDS: {
         const int i = k - C_DICT4;
         e = pqg::launch_dict_ids(s, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
                                  (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->chunk_off[i],
-                                 P->chunk_n[i], (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused,
-                                 P->dict_walk_wg, P->dict_tile_wg, P->dict_walk_pg, err, ecount);
+                                 P->chunk_n[i], (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused, err, ecount);
         break;
       }
       case C_BSS: e = pqg::launch_bss(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;

@@ -116,43 +116,27 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
 //      almost always larger than the section) is resolved by a search for succ(i) in the list.
 // So the per-value work is parallel; the serial steps are one per 64 values plus one per
 // false candidate that sits between two true ones.
-#ifndef PQG_BW_WIN
-#define PQG_BW_WIN 2048
-#endif
-#ifndef PQG_BW_AHEAD
-#define PQG_BW_AHEAD 1
-#endif
-#ifndef PQG_BW_COMPACT_LOOP
-#define PQG_BW_COMPACT_LOOP 1
-#endif
-#ifndef PQG_BW_LIFT
-#define PQG_BW_LIFT 1
-#endif
-#ifndef PQG_COPY_REL32
-#define PQG_COPY_REL32 1
-#endif
-#ifndef PQG_COPY_BTAB
-#define PQG_COPY_BTAB 1
-#endif
-#if PQG_COPY_BTAB
 constexpr uint32_t COPY_BTAB = 320;  // block table entries per wave (chunks of up to 5 KiB)
-#endif
-#ifndef PQG_COPY_PERM
-#define PQG_COPY_PERM 1
-#endif
-#ifndef PQG_COPY_COMPOSE
-#define PQG_COPY_COMPOSE 1
-#endif
-constexpr uint32_t BW_WIN = PQG_BW_WIN;    // window bytes
+constexpr uint32_t BW_WIN = 2048;    // window bytes
 constexpr uint32_t BW_Q = BW_WIN / 64;     // positions per lane (16 or 32)
 constexpr uint32_t BW_CAP = BW_WIN / 4;    // candidates per pass over a tile (more: the tile is taken in parts)
 static_assert(BW_Q == 16 || BW_Q == 32, "window of 1 or 2 KiB");
 
 struct BinWalkLds {
   uint2 pn[BW_CAP];       // candidate positions (ascending; bit 31: accepted) and successors (p + 4 + len)
-  uint16_t idx[BW_WIN];   // window offset -> candidate index (valid where pos[idx] matches)
+  uint2 mr[WAVE];         // lane l: candidate mask of window offsets [BW_Q l, BW_Q l + BW_Q), index of its first
   uint32_t cut;           // position of candidate BW_CAP (the end of this pass) when there are more
 };
+static_assert(BW_Q == 32, "window offset -> candidate index through one 32-bit mask per lane");
+
+// Candidate index of window offset so (< BW_WIN), or 0xFFFF when no candidate starts there: the
+// owning lane's mask and first index (4.6 KB of LDS per wave instead of a 2,048-entry index table,
+// so 6 walking waves fit a SIMD where 4 did).
+__device__ __forceinline__ uint32_t bw_index(const BinWalkLds& L, uint32_t so) {
+  const uint2 e = L.mr[so >> 5];
+  const uint32_t bit = so & 31u;
+  return (e.x >> bit) & 1u ? e.y + (uint32_t)__builtin_popcount(e.x & ((1u << bit) - 1u)) : 0xFFFFu;
+}
 
 // Window bytes of one lane: [B + BW_Q * lane, + BW_Q + 4) as BW_Q / 4 + 1 dwords.
 struct BwBytes {
@@ -186,18 +170,12 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
   const uint32_t lane = lane_id();
   uint32_t pos = uni(beg), produced = 0;
   int code = 0;
-  // fixed BW_WIN tiles of the page; the PQG_BW_AHEAD tiles after the current one are in flight
+  // fixed BW_WIN tiles of the page; the tile after the current one is in flight
   // (a page is one wave's serial chain: with few pages per CU the tile latency is not hidden by
   // other waves, so the wave itself keeps several tiles in flight)
   uint32_t B = pos & ~(BW_WIN - 1u);
   BwBytes cur_b = bw_load(rs, B);
   BwBytes nxt_b = bw_load(rs, B + BW_WIN);
-#if PQG_BW_AHEAD >= 2
-  BwBytes nxt2_b = bw_load(rs, B + 2u * BW_WIN);
-#endif
-#if PQG_BW_AHEAD >= 3
-  BwBytes nxt3_b = bw_load(rs, B + 3u * BW_WIN);
-#endif
   while (true) {
     pos = uni(pos);
     produced = uni(produced);
@@ -226,7 +204,6 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
     if (base < pos) m &= pos - base >= BW_Q ? 0u : ~((1u << (pos - base)) - 1u);
     uint32_t total;
     const uint32_t rank = wave_excl_scan_u32((uint32_t)__builtin_popcount(m), &total);
-#if PQG_BW_COMPACT_LOOP
     // one iteration per candidate of this lane (about BW_Q / average value size), not one per
     // position: the per-position form spent most of the walk's scalar and vector instructions
     // on exec-mask branches (profiles/r02/final1/strpmc)
@@ -247,27 +224,13 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
           }
           const uint32_t nx = base + q + 4u + __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
           *(uint64_t*)&L.pn[r] = (uint64_t)(base + q) | ((uint64_t)nx << 32);
-          L.idx[BW_Q * lane + q] = (uint16_t)r;
         } else if (r == BW_CAP) {
           L.cut = base + q;
         }
         r++;
       }
     }
-#else
-#pragma unroll
-    for (uint32_t q = 0; q < BW_Q; q++)
-      if ((m >> q) & 1u) {
-        const uint32_t r = rank + (uint32_t)__builtin_popcount(m & ((1u << q) - 1u));
-        if (r < BW_CAP) {
-          const uint32_t nx = base + q + 4u + __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
-          *(uint64_t*)&L.pn[r] = (uint64_t)(base + q) | ((uint64_t)nx << 32);
-          L.idx[BW_Q * lane + q] = (uint16_t)r;
-        } else if (r == BW_CAP) {
-          L.cut = base + q;
-        }
-      }
-#endif
+    L.mr[lane] = uint2{m, rank};
     wave_sync();
     total = uni(total);
     // this pass covers [pos, eff_end): the whole tile, or up to the first candidate past the cap
@@ -291,8 +254,8 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
       const uint32_t k = i0 + lane;
       const uint32_t s = k < total ? L.pn[k].y : 0xFFFFFFFFu;
       const uint32_t so = s - B;
-      const uint32_t t = so < BW_WIN ? L.idx[so] : 0xFFFFu;
-      const bool hit = t < total && t > k && t - i0 < WAVE && L.pn[t < total ? t : 0].x == s;
+      const uint32_t t = so < BW_WIN ? bw_index(L, so) : 0xFFFFu;
+      const bool hit = t < total && t > k && t - i0 < WAVE;
       const uint32_t J = hit ? t - i0 : WAVE;
       uint64_t mask = 0;
       uint32_t last = 0;
@@ -303,7 +266,6 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
       const uint32_t run = ~next1 ? (uint32_t)__builtin_ctzll(~next1) : WAVE - 1u;
       last = run;
       mask = last == WAVE - 1u ? ~0ull : ((1ull << (last + 1u)) - 1ull);
-#if PQG_BW_LIFT
       if (rdl(J, last) < WAVE) {
         // the chain goes on past a false candidate (e.g. the byte before a length prefix, whose
         // shifted "length" fits the page): successors increase, so lane l is on the chain from
@@ -324,12 +286,6 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
         mask = __ballot(x == lane);
         last = 63u - (uint32_t)__builtin_clzll(mask);
       }
-#else
-      for (uint32_t j = rdl(J, last); j < WAVE; j = rdl(J, j)) {
-        mask |= 1ull << j;
-        last = j;
-      }
-#endif
       const uint32_t n_acc = (uint32_t)__builtin_popcountll(mask);
       const uint32_t room = N - produced - got;
       const uint32_t take = uni(n_acc < room ? n_acc : room);
@@ -340,8 +296,8 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
       const uint32_t cur = rdl(s, last);  // true successor of the last value of the batch
       pos = cur;
       if (cur >= eff_end) { leave = true; break; }
-      const uint32_t a = uni((uint32_t)L.idx[cur - B]);
-      if (a >= total || L.pn[a].x != cur || a <= i0 + last) {  // every position of the window was tested
+      const uint32_t a = uni(bw_index(L, cur - B));
+      if (a >= total || a <= i0 + last) {  // every position of the window was tested
         code = bin_value_error(rs, cur, end, dict);
         break;
       }
@@ -355,26 +311,10 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
     if (leave && nB != B) {
       if (nB == B + BW_WIN) {
         cur_b = nxt_b;
-#if PQG_BW_AHEAD >= 2
-        nxt_b = nxt2_b;
-#if PQG_BW_AHEAD >= 3
-        nxt2_b = nxt3_b;
-        nxt3_b = bw_load(rs, nB + 3u * BW_WIN);
-#else
-        nxt2_b = bw_load(rs, nB + 2u * BW_WIN);
-#endif
-#else
         nxt_b = bw_load(rs, nB + BW_WIN);
-#endif
       } else {  // a value longer than a tile: the prefetch missed
         cur_b = bw_load(rs, nB);
         nxt_b = bw_load(rs, nB + BW_WIN);
-#if PQG_BW_AHEAD >= 2
-        nxt2_b = bw_load(rs, nB + 2u * BW_WIN);
-#endif
-#if PQG_BW_AHEAD >= 3
-        nxt3_b = bw_load(rs, nB + 3u * BW_WIN);
-#endif
       }
       B = nB;
     }
@@ -404,7 +344,7 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
 // page's value offset). dict_walk = 1: `list` holds column indices of BYTE_ARRAY dictionaries;
 // the dictionary page's entries -> dict_len / dict_src; an error is recorded on the column's
 // pseudo page (n_pages + column) as an init error.
-__global__ __launch_bounds__(64 * WPB) void k_bin_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) void k_bin_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                        const PageWork* __restrict__ work,
                                                        const ColumnDev* __restrict__ cols,
                                                        const int32_t* __restrict__ list, int n_list, int dict_walk,
@@ -665,39 +605,34 @@ __device__ __forceinline__ void store_block16(uint8_t* dst, uint64_t a, uint64_t
   }
 }
 
-// Value bytes. One wave per chunk of BIN_CHUNK values of one page (chunks[c] = page | j << 32).
-// The chunk's offsets and sources are staged in LDS; every lane owns output dwords of the
-// chunk's byte range and finds the value of its first byte by binary search (then walks
-// forward). A dword inside one value is one unaligned 4-byte source read; a dword that straddles
-// values (or the chunk ends, which other waves share) is assembled and stored byte by byte.
+// Value bytes of values [i_lo, i_hi) of one page, by one wave (the per-wave path of k_bin_copy,
+// for chunks whose source does not fit the workgroup's LDS staging: long values, large
+// dictionaries). The offsets and sources are staged in LDS; every lane owns output dwords of the
+// range and finds the value of its first byte by binary search (then walks forward). A dword
+// inside one value is one unaligned 4-byte source read; a dword that straddles values (or the
+// range ends, which other waves share) is assembled and stored byte by byte.
 // DELTA_LENGTH_BYTE_ARRAY sources are the page's value bytes (PageWork::aux) + the in-page offset;
 // a value running past the page is the reference's "Failed to read N bytes" (EOF) at that value.
-__global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                                       const PageWork* __restrict__ work,
-                                                       const ColumnDev* __restrict__ cols,
-                                                       const uint64_t* __restrict__ chunks, uint32_t n_chunks,
-                                                       uint64_t* err, ErrCount err_count) {
-  __shared__ uint64_t off_all[WPB][BIN_CHUNK + 1];
-  __shared__ uint32_t src_all[WPB][BIN_CHUNK];
-  __shared__ uint32_t rel_all[WPB][BIN_CHUNK + 1];
-#if PQG_COPY_BTAB
-  __shared__ uint32_t bt_all[WPB][COPY_BTAB];
-#endif
-  const uint32_t c = blockIdx.x * WPB + wave_id();
-  if (c >= n_chunks) return;
-  uint64_t* off = off_all[wave_id()];
-  uint32_t* src = src_all[wave_id()];
-  uint32_t* rel = rel_all[wave_id()];
+constexpr uint32_t CP_VALUES = 512;            // values per workgroup chunk of k_bin_copy
+constexpr uint32_t CP_WAVE = CP_VALUES / WPB;  // values per wave on the per-wave path
+constexpr uint32_t CP_SRC = 24576;             // LDS bytes of staged source per workgroup
+static_assert(CP_VALUES == CP_CHUNK_VALUES, "host chunking (pqgpu_internal.h)");
+
+struct CopyWaveLds {
+  uint64_t off[CP_WAVE + 1];
+  uint32_t src[CP_WAVE];
+  uint32_t rel[CP_WAVE + 1];
+  uint32_t bt[COPY_BTAB];
+};
+
+__device__ __forceinline__ void bin_copy_wave(const uint8_t* __restrict__ bytes, uint64_t n_bytes, const PageWork& pw,
+                                              const ColumnDev& cd, int page, uint32_t i_lo, uint32_t i_hi,
+                                              CopyWaveLds& W, uint64_t* err, ErrCount err_count) {
+  uint64_t* off = W.off;
+  uint32_t* src = W.src;
+  uint32_t* rel = W.rel;
   const uint32_t lane = lane_id();
-  const uint64_t ch = chunks[c];
-  const int page = (int)(uint32_t)ch;
-  const uint32_t j = (uint32_t)(ch >> 32);
-  const PageWork& pw = work[page];
-  const ColumnDev& cd = cols[pw.column];
-  const uint32_t nv = uni(pw.n_values);
-  const uint32_t i_lo = j * BIN_CHUNK;
-  if (i_lo >= nv) return;
-  const uint32_t i_hi = i_lo + BIN_CHUNK < nv ? i_lo + BIN_CHUNK : nv;
+  if (i_lo >= i_hi) return;
   const uint32_t n = i_hi - i_lo;
   const int64_t* offs = (const int64_t*)cd.values + pw.out_offset;
   const bool dlba = uni(pw.bin_kind) == BIN_DLBA;
@@ -708,14 +643,10 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
   const uint64_t page0 = (uint64_t)offs[0];
   for (uint32_t k = lane; k <= n; k += WAVE) off[k] = (uint64_t)offs[i_lo + k];
   wave_sync();
-#if PQG_COPY_REL32
   // PLAIN / DLBA sources follow from the offsets (see below): only value 0's is needed
   // (PLAIN only: DELTA_LENGTH sources are computed per value below for the EOF check)
   const bool plain_small = !dlba && !from_dict && off[n] - off[0] < 0x7FFF0000ull - 16u;
   const uint32_t n_src = plain_small ? 1u : n;
-#else
-  const uint32_t n_src = n;
-#endif
   for (uint32_t k = lane; k < n_src; k += WAVE) {
     uint32_t s;
     if (dlba) {
@@ -741,7 +672,6 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
   // Blocks are gathered G at a time before any of them is stored: a source load issued
   // after a store waits for that store (vmcnt counts both), so loads and stores are not interleaved.
   constexpr uint32_t G = 4;
-#if PQG_COPY_REL32
   if (o_hi - a0 < 0x7FFF0000ull) {
     // The usual case: the chunk's bytes span < 2 GiB, so offsets are kept chunk-relative in 32
     // bits (relative to the first 16-byte block a0), and PLAIN / DELTA_LENGTH sources follow from
@@ -753,12 +683,11 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
     const uint32_t src0 = src[0];
     const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
     uint32_t kv = 0;
-#if PQG_COPY_BTAB
     // value of every 16-byte block's first byte, when the chunk spans at most COPY_BTAB blocks:
     // bt[j] = the last value starting at or before byte 16j (a value starting inside block j - 1
     // is entered at index ceil(rel / 16), then a running maximum), instead of a binary search
     // per block
-    uint32_t* bt = bt_all[wave_id()];
+    uint32_t* bt = W.bt;
     const uint32_t nblk = (r_hi + 15u) >> 4;
     const bool btab = nblk <= COPY_BTAB;
     if (btab) {
@@ -783,7 +712,6 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
       }
       wave_sync();
     }
-#endif
     for (uint32_t bg = 16u * lane; bg < r_hi; bg += 16u * WAVE * G) {
       uint32_t wd[G][4];
       uint32_t have[G];
@@ -794,11 +722,9 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
         wd[g][0] = wd[g][1] = wd[g][2] = wd[g][3] = 0;
         if (b >= r_hi) continue;
         const uint32_t b0 = b > r_lo ? b : r_lo;
-#if PQG_COPY_BTAB
         if (btab) {
           kv = bt[b >> 4];
         } else
-#endif
         {
         uint32_t lo = kv, hi = n;
         while (hi - lo > 1) {
@@ -809,7 +735,6 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
         kv = lo;
         }
         const uint32_t bend = b + 16u < r_hi ? b + 16u : r_hi;
-#if PQG_COPY_COMPOSE
         // PLAIN / DLBA: the block's source is one stream with a 4-byte hole (PLAIN) at every value
         // start inside the block; with at most 4 such starts the block is composed without loops:
         // 9 aligned source dwords, the 8 dwords a_t at the block's byte alignment, and per output
@@ -838,7 +763,6 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
 #pragma unroll
           for (uint32_t q = 0; q < 4; q++) {
             uint32_t word = 0;
-#if PQG_COPY_PERM
             // the dword's bytes come from a[q + c0] and, after at most one value start inside
             // it, a[q + c0 + 1]: one v_perm with the byte selector of the start
             const uint32_t cq = (uint32_t)(prof >> (16u * q)) & 0xFFFFu;  // counts of bytes 4q .. 4q+3
@@ -854,7 +778,6 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
               const uint32_t hb = (dn & 1u) | ((dn & 0x10u) << 4) | ((dn & 0x100u) << 8) | ((dn & 0x1000u) << 12);
               word = __builtin_amdgcn_perm(A1, A0, 0x03020100u + 4u * hb);
             } else
-#endif
             {
 #pragma unroll
             for (uint32_t e = 0; e < 4; e++) {
@@ -872,7 +795,6 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
             if (d0 >= r_lo && d0 + 4u <= r_hi) have[g] |= 1u << q;
           }
         } else
-#endif
         {
         uint32_t k = kv;
         uint32_t k_end = rel[k + 1];
@@ -910,7 +832,6 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
     }
     return;
   }
-#endif
   uint32_t kv = 0;  // value of this lane's current byte (monotone across iterations)
   for (uint64_t ag = a0 + 16u * lane; ag < o_hi; ag += 16u * WAVE * G) {
     uint32_t wd[G][4];
@@ -956,6 +877,200 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
       const uint64_t a = ag + 16u * WAVE * g;
       if (a < o_hi) store_block16(dst, a, o_lo, o_hi, wd[g], have[g], dst_al16);
     }
+  }
+}
+
+// LDS of one k_bin_copy workgroup: the chunk's value starts (relative to the chunk's first 16-byte
+// output block) and dictionary sources, and the staged source bytes; or the per-wave path's tables.
+struct CopyWgLds {
+  uint32_t rel[CP_VALUES + 1];
+  uint32_t src[CP_VALUES];
+  uint32_t img[CP_SRC / 4 + 16];  // source bytes [Sa, Sa + CP_SRC) + slack for 9-dword reads
+};
+union CopyLds {
+  CopyWgLds g;
+  CopyWaveLds w[WPB];
+};
+
+// 4 source bytes at staged offset i (any alignment): two aligned LDS dwords and a byte align.
+__device__ __forceinline__ uint32_t img4(const uint32_t* img, uint32_t i) {
+  return __builtin_amdgcn_alignbyte(img[(i >> 2) + 1], img[i >> 2], i & 3u);
+}
+
+// Value bytes. One workgroup per chunk of CP_VALUES values of one page (chunks[c] = page | j << 32).
+// The chunk's source is staged in LDS with coalesced 16-byte loads: the page bytes its values come
+// from (PLAIN: one stream with a 4-byte length prefix before every value; DELTA_LENGTH: the value
+// bytes back to back) or the whole dictionary page (RLE_DICTIONARY: entries in any order). Then
+// every thread composes whole 16-byte output blocks from LDS (a block with at most 4 value starts
+// from 9 aligned dwords and one v_perm per dword, as the per-wave path does from memory; others
+// piece by piece) and stores them: after the staging loads the workgroup issues stores only, so
+// no load waits behind a store (vmcnt counts both). Source bytes are read from HBM once, where
+// the per-wave path read 36 bytes per 16-byte block. A chunk whose source does not fit CP_SRC
+// takes the per-wave path, CP_WAVE values per wave.
+__global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                       const PageWork* __restrict__ work,
+                                                       const ColumnDev* __restrict__ cols,
+                                                       const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                       uint64_t* err, ErrCount err_count) {
+  __shared__ __attribute__((aligned(16))) CopyLds S;
+  if (blockIdx.x >= n_chunks) return;
+  const uint64_t ch = chunks[blockIdx.x];
+  const int page = (int)(uint32_t)ch;
+  const uint32_t J = (uint32_t)(ch >> 32);
+  const PageWork& pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t nv = uni(pw.n_values);
+  const uint32_t i_lo = J * CP_VALUES;
+  if (i_lo >= nv) return;
+  const uint32_t i_hi = i_lo + CP_VALUES < nv ? i_lo + CP_VALUES : nv;
+  const uint32_t n = i_hi - i_lo;
+  const uint32_t t = threadIdx.x;
+  const int64_t* offs = (const int64_t*)cd.values + pw.out_offset;
+  const uint32_t kind = uni(pw.bin_kind);
+  const bool dlba = kind == BIN_DLBA, from_dict = kind == BIN_DICT;
+  const uint64_t page0 = (uint64_t)offs[0];
+  const uint64_t o_lo = (uint64_t)offs[i_lo], o_hi0 = (uint64_t)offs[i_hi];
+  const uint64_t o_hi = o_hi0 < cd.binary_capacity ? o_hi0 : cd.binary_capacity;  // overflow: reported at sync
+  const uint64_t a0 = o_lo & ~15ull;
+  const uint32_t hole = (dlba || from_dict) ? 0u : 4u;
+  // source of the chunk: page-relative (PLAIN, DLBA) or dictionary-relative (DICT) byte range
+  const uint64_t slim = from_dict ? cd.dict_bytes : pw.size;
+  uint64_t s_lo, s_hi;
+  if (from_dict) {
+    s_lo = 0;
+    s_hi = slim;
+  } else {
+    s_lo = dlba ? pw.aux + (o_lo - page0) : (uint64_t)cd.bsrc[pw.out_offset + i_lo];
+    s_hi = s_lo + (o_hi0 - o_lo) + (uint64_t)hole * (n - 1u);
+  }
+  const uint64_t Sa = s_lo & ~15ull;
+  const bool fit = o_hi0 - a0 < 0x7FFF0000ull && s_hi - Sa <= CP_SRC && s_lo <= slim;
+  if (!fit) {
+    // per-wave path: wave w takes values [i_lo + CP_WAVE w, + CP_WAVE)
+    const uint32_t w0 = i_lo + CP_WAVE * wave_id();
+    bin_copy_wave(bytes, n_bytes, pw, cd, page, w0 < i_hi ? w0 : i_hi, w0 + CP_WAVE < i_hi ? w0 + CP_WAVE : i_hi,
+                  S.w[wave_id()], err, err_count);
+    return;
+  }
+  CopyWgLds& L = S.g;
+  const uint64_t sbase = from_dict ? cd.dict_offset : pw.base;
+  const rsrc_t rs = make_rsrc(bytes + sbase, n_bytes - sbase);
+  // ---- staging: source bytes [Sa, s_hi) (bytes at or past slim read as 0), value starts, sources
+  const uint32_t n_st = (uint32_t)(s_hi - Sa);
+  for (uint32_t o = 16u * t; o < n_st; o += 16u * 64u * WPB) {
+    u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(Sa + o), 0, 0);
+    if (Sa + o + 16u > slim) {
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const int64_t keep = (int64_t)slim - (int64_t)(Sa + o + 4u * q);
+        const uint32_t m = keep >= 4 ? 0xFFFFFFFFu : keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
+        v[q] &= m;
+      }
+    }
+    *(u32x4*)&L.img[o >> 2] = v;
+  }
+  for (uint32_t k = t; k <= n; k += 64u * WPB) L.rel[k] = (uint32_t)((uint64_t)offs[i_lo + k] - a0);
+  if (from_dict)
+    for (uint32_t k = t; k < n; k += 64u * WPB) L.src[k] = cd.bsrc[pw.out_offset + i_lo + k];
+  if (dlba)  // DeltaLengthByteArrayValuesReader.readBytes: a value past the page is EOF at that value
+    for (uint32_t k = t; k < n; k += 64u * WPB) {
+      const uint64_t r = (uint64_t)offs[i_lo + k] - page0, len = (uint64_t)offs[i_lo + k + 1] - (uint64_t)offs[i_lo + k];
+      const uint64_t avail = pw.size > pw.aux ? pw.size - pw.aux : 0;
+      if (r + len > avail) report(err, err_count, page, 2, i_lo + k, PQG_ERR_EOF);
+    }
+  __syncthreads();
+  if (o_lo >= o_hi) return;
+  uint8_t* dst = cd.binary_data;
+  const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
+  const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
+  const uint32_t src0 = (uint32_t)(s_lo - Sa);  // staged offset of value 0's first byte (PLAIN, DLBA)
+  const uint32_t* img = L.img;
+  const uint32_t* rel = L.rel;
+  for (uint32_t b = 16u * t; b < r_hi; b += 16u * 64u * WPB) {
+    const uint32_t b0 = b > r_lo ? b : r_lo;
+    uint32_t lo = 0, hi = n;  // value of the block's first byte
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (rel[mid] <= b0) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t kv = lo;
+    const uint32_t bend = b + 16u < r_hi ? b + 16u : r_hi;
+    uint32_t wd[4];
+    uint32_t have = 0;
+    // staged source offset of block byte 0 (PLAIN / DLBA); compose needs it >= 0
+    const int64_t Sg = (int64_t)src0 + (int64_t)b - (int64_t)r_lo + (int64_t)hole * kv;
+    const bool compose = !from_dict && !(kv + 5u < n && rel[kv + 5u] < bend) && Sg >= 0;
+    if (compose) {
+      uint64_t prof = 0;  // nibble i: value starts at or before byte i of the block (PLAIN)
+#pragma unroll
+      for (uint32_t j = 1; j <= 4; j++) {
+        const uint32_t kk = kv + j;
+        const uint32_t pj = kk < n ? rel[kk] : 0xFFFFFFFFu;
+        if (pj < bend && hole) prof += 0x1111111111111111ull << (4u * (pj - b));
+      }
+      const uint32_t Sv = (uint32_t)Sg, A = Sv >> 2, sh = Sv & 3u;
+      uint32_t a[8];
+#pragma unroll
+      for (uint32_t q = 0; q < 8; q++) a[q] = __builtin_amdgcn_alignbyte(img[A + q + 1], img[A + q], sh);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        uint32_t word = 0;
+        const uint32_t cq = (uint32_t)(prof >> (16u * q)) & 0xFFFFu;  // counts of bytes 4q .. 4q+3
+        const uint32_t c0 = cq & 0xFu;
+        const uint32_t dn = cq - c0 * 0x1111u;  // nibbles: 0, or 1 from the start on
+        if (dn <= 0x1111u && (dn & 0xEEEEu) == 0) {
+          uint32_t A0 = a[q], A1 = a[q + 1];
+#pragma unroll
+          for (uint32_t u = 1; u <= 4; u++) {
+            A0 = c0 == u ? a[q + u < 8 ? q + u : 7] : A0;
+            A1 = c0 == u ? a[q + u + 1 < 8 ? q + u + 1 : 7] : A1;
+          }
+          const uint32_t hb = (dn & 1u) | ((dn & 0x10u) << 4) | ((dn & 0x100u) << 8) | ((dn & 0x1000u) << 12);
+          word = __builtin_amdgcn_perm(A1, A0, 0x03020100u + 4u * hb);
+        } else {
+#pragma unroll
+          for (uint32_t e = 0; e < 4; e++) {
+            const uint32_t c = (uint32_t)(prof >> (4u * (4u * q + e))) & 0xFu;  // 0..4
+            uint32_t v = a[q];
+            v = c == 1u ? a[q + 1] : v;
+            v = c == 2u ? a[q + 2] : v;
+            v = c == 3u ? a[q + 3] : v;
+            v = c == 4u ? a[q + 4] : v;
+            word |= v & (0xFFu << (8u * e));
+          }
+        }
+        const uint32_t d0 = b + 4u * q;
+        wd[q] = word;
+        if (d0 >= r_lo && d0 + 4u <= r_hi) have |= 1u << q;
+      }
+    } else {
+      uint32_t k = kv;
+      uint32_t k_end = rel[k + 1];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t d0 = b + 4u * q;
+        const uint32_t x0 = d0 > r_lo ? d0 : r_lo, x1 = d0 + 4u < r_hi ? d0 + 4u : r_hi;
+        uint32_t word = 0;
+        for (uint32_t cur = x0; cur < x1;) {
+          while (k + 1 < n && cur >= k_end) {
+            k++;
+            k_end = rel[k + 1];
+          }
+          const uint32_t seg_end = x1 < k_end ? x1 : k_end;
+          const uint32_t sp = from_dict ? L.src[k] + (cur - rel[k]) : src0 + (rel[k] - r_lo) + hole * k + (cur - rel[k]);
+          const uint32_t v = sp < n_st ? img4(img, sp) : 0u;  // (DICT: sp is the entry's offset in the page)
+          const uint32_t nb = seg_end - cur;
+          const uint32_t msk = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
+          word |= (v & msk) << (8u * (cur - d0));
+          cur = seg_end;
+        }
+        wd[q] = word;
+        if (x0 == d0 && x1 == d0 + 4u) have |= 1u << q;
+      }
+    }
+    if (!dst_al4) have = 0;  // unaligned byte buffer (C ABI caller): byte stores only
+    store_block16(dst, a0 + b, o_lo, o_hi, wd, have, dst_al16);
   }
 }
 
@@ -1464,8 +1579,8 @@ hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
                            const ColumnDev* cols, const uint64_t* chunks, uint32_t n_chunks, uint64_t* err,
                            ErrCount err_count) {
   if (n_chunks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_bin_copy, dim3((n_chunks + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols,
-                     chunks, n_chunks, err, err_count);
+  hipLaunchKernelGGL(k_bin_copy, dim3(n_chunks), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, chunks, n_chunks,
+                     err, err_count);
   return hipGetLastError();
 }
 

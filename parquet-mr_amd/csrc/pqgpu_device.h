@@ -135,14 +135,10 @@ template <class T>
 __device__ __forceinline__ void gst(T* p, T v) {
   PQG_STORE_GUARD *(__attribute__((address_space(1))) T*)p = v;
 }
-// Streaming output stores. PQG_PLAIN_OUTPUT_STORES selects plain stores (A/B builds).
+// Streaming output stores (plain stores measured 15 % slower on C2, round 1).
 template <class T>
 __device__ __forceinline__ void gst_nt(T* p, T v) {
-#ifdef PQG_PLAIN_OUTPUT_STORES
-  PQG_STORE_GUARD *(__attribute__((address_space(1))) T*)p = v;
-#else
   PQG_STORE_GUARD __builtin_nontemporal_store(v, (__attribute__((address_space(1))) T*)p);
-#endif
 }
 
 // Run records, chunk entries and page status are produced and consumed inside one launch

@@ -76,10 +76,7 @@ constexpr uint64_t ERR_KEY_MASK = (1ull << 48) - 1;
 enum BinKind : uint32_t { BIN_PLAIN = 0, BIN_DLBA = 1, BIN_DICT = 2, BIN_DBA = 3 };
 
 // Output chunk of k_dict_expand: CH_TILES x 64 lanes x 16 bytes.
-#ifndef PQG_CHUNK_TILES
-#define PQG_CHUNK_TILES 16
-#endif
-constexpr uint32_t DICT_CHUNK_TILES = PQG_CHUNK_TILES;
+constexpr uint32_t DICT_CHUNK_TILES = 16;
 inline uint32_t dict_chunk_values(int elem_width) { return DICT_CHUNK_TILES * 64u * (16u / (uint32_t)elem_width); }
 // output chunks of a dictionary page of n slots (slots shifted by up to 16 / width - 1 for 16-B alignment)
 inline uint32_t dict_page_chunks(uint32_t n, int elem_width) {
@@ -91,7 +88,7 @@ constexpr int DICT_WPB = 4;  // pages (walkers) / chunks (tiles) per workgroup o
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                        const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                       bool fused, uint32_t walk_wg, uint32_t tile_wg, uint32_t walk_pg, uint64_t* err,
+                       bool fused, uint64_t* err,
                        ErrCount err_count);
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                          const int32_t* list, int n, uint64_t* err, ErrCount err_count);
@@ -106,7 +103,7 @@ hipError_t launch_delta(int width, hipStream_t st, const uint8_t* bytes, uint64_
 hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                            const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
-                           uint32_t epoch, bool fused, uint32_t walk_wg, uint32_t tile_wg, uint32_t walk_pg,
+                           uint32_t epoch, bool fused,
                            uint64_t* err, ErrCount err_count);
 // DELTA_LENGTH_BYTE_ARRAY lengths (k_delta into blen, records PageWork::aux)
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
@@ -134,7 +131,8 @@ hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
                            uint32_t n_chunks, const uint32_t* dba_meta, const int32_t* carry_cols, int n_carry_cols,
                            uint64_t* err, ErrCount err_count);
 // pqgpu_binary.hip
-constexpr uint32_t BIN_CHUNK = 256;     // values per k_bin_copy chunk
+constexpr uint32_t BIN_CHUNK = 256;     // values per DELTA_BYTE_ARRAY copy chunk
+constexpr uint32_t CP_CHUNK_VALUES = 512;  // values per k_bin_copy chunk (one workgroup)
 constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block
 hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                       const int32_t* list, int n, uint64_t* err, ErrCount err_count);

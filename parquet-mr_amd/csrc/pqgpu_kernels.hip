@@ -55,10 +55,7 @@ struct PreWin {
   uint32_t flg;        // byte b: bit0 packed, bit1 slow path, bits 2..4 header length
 };
 
-#ifndef PQG_SEG_BYTES
-#define PQG_SEG_BYTES 3072
-#endif
-constexpr uint32_t SEG_BYTES = PQG_SEG_BYTES;   // LDS page segment per wave of k_dict_runs (5 workgroups per CU)
+constexpr uint32_t SEG_BYTES = 3072;   // LDS page segment per wave of k_dict_runs (5 workgroups per CU)
 
 
 // Fill the wave's LDS segment with page bytes [lo, lo + SEG_BYTES) (lo 16-aligned).
@@ -168,28 +165,6 @@ __device__ __forceinline__ void predecode(PreWin& pw, uint32_t B, int w) {
   pw.flg = flg;
 }
 
-struct RleWalk {
-  uint32_t pos;       // uniform: next header byte (page-relative)
-  uint32_t sec_end;   // uniform
-  uint32_t produced;  // uniform: values covered by the runs walked so far
-  uint32_t N;         // uniform: values wanted
-  int w;              // uniform: bit width
-  // remainder of a bit-packed run split at a batch boundary (multiple of 8 values:
-  // the split point is byte aligned, 8 values = w bytes)
-  uint32_t pend_count;
-  uint32_t pend_lo, pend_hi;
-};
-
-// One batch of up to 64 runs; lane r holds run r.
-struct RunBatch {
-  uint32_t start;   // first value index of the run
-  uint32_t meta;    // 0 = RLE, 1 = PACKED
-  uint32_t lo, hi;  // RLE: lo = raw value; PACKED: [lo, hi) = bytes read for the run
-  uint32_t nr;      // uniform
-  uint32_t first;   // uniform: value index of the batch start
-  uint32_t end;     // uniform: value index after the batch
-};
-
 // Scalar re-decode of one header at `pos` (rare: varints longer than 5 bytes,
 // 0 or >= 2^28 groups). Bytes come through uniform buffer loads.
 __device__ __forceinline__ uint32_t sbyte(rsrc_t rs, uint32_t p) {
@@ -255,100 +230,6 @@ __device__ __forceinline__ uint32_t pick4(const uint32_t (&a)[4], uint32_t b, ui
   }
 }
 
-// Walk up to 64 runs. Returns 0 or an error code; on error s.N is cut to the
-// error's value index (s.produced) so the caller stops after this batch.
-// `cap` > 0 limits the bit-packed values one batch may cover (they are staged in
-// LDS); a packed run that does not fit is split at a multiple of 8 values.
-__device__ __forceinline__ int walk_batch(PreWin& win, RleWalk& s, RunBatch& rb, uint32_t cap = 0) {
-  const uint32_t lane = lane_id();
-  rb.nr = 0;
-  rb.first = s.produced;
-  rb.start = 0xFFFFFFFFu;
-  rb.meta = 0;
-  rb.lo = 0;
-  rb.hi = 0;
-  int code = 0;
-  uint32_t packed = 0;
-  while (true) {
-    // loop-carried scalars re-asserted wave-uniform (readfirstlane): otherwise the divergence
-    // analysis keeps them in VGPRs and the serial chain runs as masked vector code
-    rb.nr = uni(rb.nr);
-    s.produced = uni(s.produced);
-    s.pos = uni(s.pos);
-    s.N = uni(s.N);
-    s.pend_count = uni(s.pend_count);
-    win.B = uni(win.B);
-    packed = uni(packed);
-    if (rb.nr >= 64u || s.produced >= s.N) break;
-    uint64_t count;
-    uint32_t m, lo, hi = 0;
-    if (s.pend_count) {
-      m = 1;
-      count = s.pend_count;
-      lo = s.pend_lo;
-      hi = s.pend_hi;
-      s.pend_count = 0;
-    } else {
-      if (s.pos >= s.sec_end) { code = PQG_ERR_RLE_PAST_END; break; }     // :81
-      const uint32_t k = s.pos - win.B;
-      if (k >= 256u) {
-        predecode(win, s.pos & ~3u, s.w);
-      }
-      const uint32_t kk = s.pos - win.B, l = kk >> 2, b = kk & 3u;
-      const uint32_t f = (rdl(win.flg, l) >> (8u * b)) & 0xFFu;
-      uint32_t hl, nx, vv;
-      if (f & 2u) {
-        code = slow_header(win.rs, s.pos, s.sec_end, s.w, hl, m, count, vv, nx);
-        if (code) break;
-      } else {
-        hl = f >> 2;
-        m = f & 1u;
-        nx = pick4(win.nxt, b, l);
-        vv = pick4(win.val, b, l);
-        count = pick4(win.cnt, b, l);
-        if ((uint64_t)s.pos + hl > s.sec_end) { code = PQG_ERR_EOF; break; }   // EOFException in read()
-      }
-      if (m == 0) {                                                          // RLE :85-89
-        if (nx > s.sec_end) { code = PQG_ERR_EOF; break; }
-        if (count == 0) count = s.N - s.produced;  // Java: currentCount goes negative, value repeats forever
-        lo = vv;
-        s.pos = nx;
-      } else {                                                               // PACKED :90-104
-        const uint32_t rd_end = nx < s.sec_end ? nx : s.sec_end;             // :97-99
-        lo = vv;
-        hi = rd_end;
-        s.pos = rd_end;
-      }
-    }
-    if (m == 1 && cap) {
-      uint64_t left = s.N - s.produced;
-      uint64_t eff = count < left ? count : left;
-      uint32_t room = cap - packed;
-      if (eff > room) {
-        uint32_t take = room & ~7u;
-        s.pend_count = (uint32_t)(count - take);
-        s.pend_lo = lo + (take >> 3) * (uint32_t)s.w;
-        s.pend_hi = hi;
-        if (take == 0) break;
-        count = take;
-        eff = take;
-      }
-      packed += (uint32_t)eff;
-    }
-    const bool me = lane == rb.nr;
-    rb.start = me ? s.produced : rb.start;
-    rb.meta = me ? m : rb.meta;
-    rb.lo = me ? lo : rb.lo;
-    rb.hi = me ? hi : rb.hi;
-    rb.nr++;
-    uint64_t np = (uint64_t)s.produced + count;
-    s.produced = np < s.N ? (uint32_t)np : s.N;
-  }
-  if (code) s.N = s.produced;
-  rb.end = s.produced;
-  return code;
-}
-
 // Value of element i (page-relative) of a PACKED run [lo, hi) starting at s_r.
 __device__ __forceinline__ uint32_t packed_elem(rsrc_t rs, uint32_t lo, uint32_t hi, uint32_t s_r, uint32_t i, int w) {
   if (w == 0) return 0;
@@ -362,51 +243,6 @@ __device__ __forceinline__ uint32_t packed_elem(rsrc_t rs, uint32_t lo, uint32_t
   }
   x >>= (byte - a) * 8u + (uint32_t)(bit & 7u);
   return w == 32 ? (uint32_t)x : (uint32_t)x & ((1u << w) - 1u);
-}
-
-// packed_elem reading the LDS segment when the 8 bytes are there.
-template <bool LDS_ONLY = false>
-__device__ __forceinline__ uint32_t packed_elem_w(const PreWin& pw, uint32_t lo, uint32_t hi, uint32_t j, int w) {
-  if (w == 0) return 0;
-  const uint64_t bit = (uint64_t)j * (uint32_t)w;
-  const uint32_t byte = lo + (uint32_t)(bit >> 3);
-  const uint32_t a = byte & ~3u;
-  uint64_t x;
-  if (LDS_ONLY || seg_has(pw, a, 8)) x = (uint64_t)seg32(pw, a) | ((uint64_t)seg32(pw, a + 4) << 32);
-  else x = (uint64_t)ld32(pw.rs, a) | ((uint64_t)ld32(pw.rs, a + 4) << 32);
-  if (a + 8u > hi) {
-    const int64_t keep = (int64_t)hi - (int64_t)a;
-    x = keep <= 0 ? 0 : (x & ((1ull << (8 * keep)) - 1ull));
-  }
-  x >>= (byte - a) * 8u + (uint32_t)(bit & 7u);
-  return w == 32 ? (uint32_t)x : (uint32_t)x & ((1u << w) - 1u);
-}
-
-// For lane element index i, select the run (among `mask`) covering it.
-struct Sel {
-  uint32_t s, meta, lo, hi;
-};
-
-__device__ __forceinline__ void select_runs(const RunBatch& rb, uint64_t mask, const uint32_t* idx, Sel* sel, int E) {
-  while (mask) {
-    uint32_t r = (uint32_t)__builtin_ctzll(mask);
-    mask &= mask - 1;
-    uint32_t s = rdl(rb.start, r), m = rdl(rb.meta, r), lo = rdl(rb.lo, r), hi = rdl(rb.hi, r);
-#pragma unroll
-    for (int k = 0; k < E; k++) {
-      bool t = idx[k] >= s;
-      sel[k].s = t ? s : sel[k].s;
-      sel[k].meta = t ? m : sel[k].meta;
-      sel[k].lo = t ? lo : sel[k].lo;
-      sel[k].hi = t ? hi : sel[k].hi;
-    }
-  }
-}
-
-// Runs of the batch that overlap value range [c_lo, c_hi).
-__device__ __forceinline__ uint64_t overlap_mask(const RunBatch& rb, uint32_t run_end, uint32_t c_lo, uint32_t c_hi) {
-  bool ov = lane_id() < rb.nr && rb.start < c_hi && run_end > c_lo;
-  return __ballot(ov);
 }
 
 // ---------------------------------------------------------------------------
@@ -430,8 +266,6 @@ __device__ __forceinline__ typename DictVal<W>::T load_dict(rsrc_t d, uint32_t i
 }
 
 constexpr uint32_t DICT_LDS_BYTES = 8192;   // dictionary staged in LDS per workgroup when it fits
-constexpr uint32_t RT_MAX = 64;             // runs per expansion batch (lane r holds run r)
-constexpr uint32_t NX_SENTINEL = 0xFFFFFFFFu;
 
 // Per-wave LDS of k_dict.
 struct DictWaveLds {
@@ -439,18 +273,6 @@ struct DictWaveLds {
   uint64_t ent[256];       // window position k: next header position | (count | packed << 31) << 32
   uint32_t val[256];       // window position k: RLE raw value, or packed data start
 };
-
-// Exclusive prefix sum over the wave (u32); *total = sum over all lanes.
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t y = __shfl_up(x, o);
-    if ((int)lane_id() >= o) x += y;
-  }
-  *total = rdl(x, 63);
-  return x - v;
-}
 
 // ---------------------------------------------------------------------------
 // Dictionary pages in two launches.
@@ -469,110 +291,6 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) 
 constexpr uint32_t CH_TILES = DICT_CHUNK_TILES;
 
 __device__ __forceinline__ uint32_t chunk_values(uint32_t E) { return CH_TILES * WAVE * E; }
-
-template <int W, bool SMALL>
-__device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg, uint32_t sec_end,
-                                          int w, uint64_t* rec, uint32_t* chunk_run, uint32_t CH, uint32_t sh, int page,
-                                          uint64_t* err, ErrCount err_count, uint32_t& n_rec, uint32_t& n_ok) {
-  const uint32_t lane = lane_id();
-  uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
-  uint32_t produced = 0;       // values covered by the runs read so far
-  uint32_t B = pos - 260u;     // current window: none yet (pos - B >= 256 forces a pre-decode)
-  uint32_t k = 0;              // records written
-  while (true) {
-    // loop-carried scalars re-asserted wave-uniform (readfirstlane): without this the
-    // divergence analysis keeps them in VGPRs and runs the chain as masked vector code
-    produced = uni(produced);
-    N = uni(N);
-    pos = uni(pos);
-    B = uni(B);
-    k = uni(k);
-    if (produced >= N) break;
-    // ---- chain: read runs; run r's record lands in lane r (start, payload)
-    uint32_t nrun = 0;
-    int code = 0;
-    uint32_t r_start = 0, r_pl = 0;
-    while (true) {
-      produced = uni(produced);
-      pos = uni(pos);
-      nrun = uni(nrun);
-      B = uni(B);
-      if (produced >= N || nrun >= RT_MAX) break;
-      if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }           // readNext :81
-      if (pos - B >= 256u) {
-        // new window: pre-decode 256 positions into LDS
-        B = pos & ~3u;
-        predecode<SMALL>(win, B, w);
-#pragma unroll
-        for (uint32_t bb = 0; bb < 4; bb++) {
-          const uint32_t p = B + 4u * lane + bb;
-          const uint32_t f = (win.flg >> (8u * bb)) & 0xFFu;
-          const uint32_t hl = f >> 2;
-          uint32_t nx = win.nxt[bb];
-          // the slow scalar path handles: long varints, 0 / huge group counts, and any
-          // header or RLE value that crosses the section end (EOF semantics)
-          const bool slow = (f & 2u) || p + hl > sec_end || (!(f & 1u) && nx > sec_end);
-          if (slow) nx = NX_SENTINEL;
-          L.ent[4u * lane + bb] = (uint64_t)nx | ((uint64_t)(win.cnt[bb] | ((f & 1u) << 31)) << 32);
-          L.val[4u * lane + bb] = win.val[bb];
-        }
-        wave_sync();
-      }
-      const uint32_t kk = pos - B;
-      const uint64_t e = L.ent[kk];
-      uint32_t nx = uni((uint32_t)e);
-      uint32_t cw = uni((uint32_t)(e >> 32));
-      uint32_t v = uni(L.val[kk]);
-      if (nx == NX_SENTINEL) {
-        uint32_t hl, m, nxs, vv;
-        uint64_t cnt64;
-        if constexpr (SMALL)
-          code = slow_header_g([&](uint32_t p) { return uni((seg32(win, p & ~3u) >> ((p & 3u) * 8u)) & 0xFFu); }, pos,
-                               sec_end, w, hl, m, cnt64, vv, nxs);
-        else
-          code = slow_header(win.rs, pos, sec_end, w, hl, m, cnt64, vv, nxs);
-        if (code) break;
-        if (m == 0 && nxs > sec_end) { code = PQG_ERR_EOF; break; }
-        nx = nxs;
-        v = vv;
-        cw = (uint32_t)(cnt64 > 0x7FFFFFFFull ? 0x7FFFFFFFu : cnt64) | (m << 31);
-      }
-      const uint32_t packed = cw >> 31;
-      uint64_t cnt = cw & 0x7FFFFFFFu;
-      uint32_t payload;
-      if (!packed) {
-        if (cnt == 0) cnt = N - produced;  // Java: currentCount goes negative, value repeats forever
-        payload = v > 0x7FFFFFFFu ? 0x7FFFFFFFu : v;  // ids >= 2^31 are out of range anyway
-        pos = nx;
-      } else {
-        payload = 0x80000000u | v;
-        pos = nx < sec_end ? nx : sec_end;  // truncated final group: readFully of what is left
-      }
-      const bool me = lane == nrun;
-      r_start = me ? produced : r_start;
-      r_pl = me ? payload : r_pl;
-      nrun++;
-      const uint64_t np = (uint64_t)produced + cnt;
-      produced = np < N ? (uint32_t)np : N;
-    }
-    if (code) {
-      if (lane == 0) report(err, err_count, page, 2, produced, code);
-      N = produced;
-    }
-    // ---- records, and the record holding each chunk's first value
-    // (chunk j covers output slots [j*CH, (j+1)*CH); its first value is max(0, j*CH - sh))
-    const uint32_t r_end_n = __shfl_down(r_start, 1);
-    if (lane < nrun) {
-      const uint32_t r_end = lane + 1 < nrun ? r_end_n : produced;
-      sst(rec + k + lane, (uint64_t)r_start | ((uint64_t)r_pl << 32));
-      uint32_t j = r_start == 0 ? 0 : (r_start + sh + CH - 1) / CH;
-      for (; j * CH < r_end + sh; j++) sst(chunk_run + j, k + lane);
-    }
-    k += nrun;
-  }
-  n_rec = k;
-  n_ok = N;
-}
 
 // Walk -> expansion hand-off inside one launch (walkers and expansion waves on any CU / XCD).
 //
@@ -593,315 +311,19 @@ __device__ __forceinline__ void dict_walk(DictWaveLds& L, PreWin& win, uint32_t 
 // vmcnt(0) before its flag, the polling wave loads only after its poll matched), which needs no
 // agent-scope fence. The memory model's fences (buffer_wbl2 sc1 on release, buffer_inv sc1 on
 // acquire) write back / invalidate the caches for the expansion's own traffic too; measured on C2
-// (PQG_HANDOFF = 1 release store: 1.30x the time, 2 acquire fence: 2.45x, 3 both: 2.8x;
+// (tried in round 2: a release store 1.30x the time, an acquire fence 2.45x, both 2.8x;
 // profiles/r02/r02_b/ab).
-#ifndef PQG_HANDOFF
-#define PQG_HANDOFF 0
-#endif
-#ifndef PQG_WALK_CHAIN
-#define PQG_WALK_CHAIN 1
-#endif
-#ifndef PQG_WALK_PRIO
-#define PQG_WALK_PRIO 0
-#endif
-#ifndef PQG_PJ_LARGE
-#define PQG_PJ_LARGE 1
-#endif
-// early partial hand-off after the walker's first window (off: C2 181.5 vs 172.6 us per launch,
-// profiles/r02/early_ab — the extra wait on the walker's stores costs more than early chunks gain)
-#ifndef PQG_LEVELS_BITS
-#define PQG_LEVELS_BITS 1
-#endif
-#ifndef PQG_EARLY
-#define PQG_EARLY 0
-#endif
-// list walk (dict_walk_ls) instead of the mark-word chain of dict_walk_pj
-#ifndef PQG_WALK_LIST
-#define PQG_WALK_LIST 1
-#endif
-// list walk: two chain steps per iteration (successor-of-successor table, PQG_WALK_J2) and the
-// branch-free 4-byte header parse (PQG_PRE_FAST)
-#ifndef PQG_WALK_J2
-#define PQG_WALK_J2 0
-#endif
-#ifndef PQG_PRE_FAST
-#define PQG_PRE_FAST 0
-#endif
-// list walk: the chain followed by the vector unit (ds_bpermute per run) instead of v_readlane + SALU
-// (measured equal on C2 and 1 % slower on Zipf(2.0): profiles/r02/walk_ls/vchain; off)
-#ifndef PQG_WALK_VCHAIN
-#define PQG_WALK_VCHAIN 0
-#endif
+// Variants measured and removed (git history, profiles/r02): an early partial hand-off after the
+// walker's first window (C2 181.5 vs 172.6 us per launch, profiles/r02/early_ab: the extra wait on
+// the walker's stores costs more than the early chunks gain); the mark-word chain of the window walk
+// (the list walk dict_walk_ls replaced it); two chain steps per iteration through a
+// successor-of-successor table, a branch-free 4-byte header parse, and the chain on the vector unit
+// (ds_bpermute per run): all within +-1 % (profiles/r02/walk_ls/variants, vchain).
 __device__ __forceinline__ void handoff_release() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a compiler barrier too (invisible to the waitcnt pass)
 }
 __device__ __forceinline__ void handoff_acquire() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#if PQG_HANDOFF & 2
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-}
-
-// Pointer-jumping walk (SMALL pages: the whole data section sits in the LDS segment).
-//
-// The serial part of the hybrid decoder — each header's position depends on the previous
-// header — is replaced per 256-byte window by list ranking: every position p of the window
-// gets its successor J(p) (the next header position if a run header started at p; 256 if it
-// leaves the window or needs the scalar slow path), and 8 rounds of pointer doubling mark
-// the positions reachable from the chain start. The marked positions, in order, are the
-// window's runs; a saturating prefix sum of their counts gives each run's first value.
-// Cost per window is fixed (~8 LDS round trips) instead of one round trip per run.
-template <int W, bool SMALL = true>
-__device__ __forceinline__ void dict_walk_pj(DictWaveLds& L, PreWin& win, uint32_t N, uint32_t sec_beg,
-                                             uint32_t sec_end, int w, uint64_t* rec, uint32_t* chunk_run,
-                                             uint32_t CH, uint32_t sh, int page, uint64_t* err, ErrCount err_count,
-                                             uint32_t& n_rec, uint32_t& n_ok, uint64_t* prog, uint32_t* pflag,
-                                             uint32_t pepoch) {
-  const uint32_t lane = lane_id();
-#if PQG_EARLY
-  bool first = true;
-#endif
-  // successor table (256 x u16) and reached flags (256 x u8) over L.ent; every access goes
-  // through may_alias types (u16 gathers vs u64 row writes must not be reordered)
-#if !PQG_WALK_CHAIN
-  typedef uint16_t __attribute__((may_alias)) u16a;
-  typedef uint32_t __attribute__((may_alias)) u32a;
-  typedef uint64_t __attribute__((may_alias)) u64a;
-  u16a* Jt = (u16a*)L.ent;
-  uint8_t* Rt = (uint8_t*)L.ent + 512;
-#endif
-  uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
-  uint32_t produced = 0, k = 0;
-  int code = 0;
-#ifdef PQG_DIAG
-  uint64_t d_pre = 0, d_dbl = 0, d_emit = 0, d_win = 0;
-  const uint64_t d_start = __builtin_amdgcn_s_memtime();
-#endif
-  // one record at lane 0 (the scalar slow path) and the chunk entries it owns
-  auto put_record = [&](uint32_t start, uint32_t end, uint32_t payload) {
-    if (lane == 0) {
-      sst(rec + k, (uint64_t)start | ((uint64_t)payload << 32));
-      uint32_t j = start == 0 ? 0 : (start + sh + CH - 1) / CH;
-      for (; j * CH < end + sh; j++) sst(chunk_run + j, k);
-    }
-    k++;
-  };
-  while (true) {
-    pos = uni(pos);
-    produced = uni(produced);
-    k = uni(k);
-    if (produced >= N) break;
-    if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
-    const uint32_t B = pos & ~3u;
-    DIAG_T(t_pre);
-    predecode<SMALL>(win, B, w);  // !SMALL: the segment is refilled when the window leaves it
-    // successors of this lane's 4 positions
-    uint32_t jv[4], nn[4], slowm = 0, inm = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      const uint32_t p = B + 4u * lane + b;
-      const uint32_t f = (win.flg >> (8u * b)) & 0xFFu;
-      const uint32_t hl = f >> 2;
-      const uint32_t nx = win.nxt[b];
-      const bool in = p < sec_end;
-      // slow: long varints, 0 / huge group counts, a header or RLE value crossing the end
-      const bool slow = in && ((f & 2u) || p + hl > sec_end || (!(f & 1u) && nx > sec_end));
-      nn[b] = (f & 1u) ? (nx < sec_end ? nx : sec_end) : nx;  // packed: readFully of what is left
-      jv[b] = (!in || slow || nn[b] - B >= 256u) ? 256u : nn[b] - B;
-      slowm |= (slow ? 1u : 0u) << b;
-      inm |= (in ? 1u : 0u) << b;
-    }
-    DIAG_ADD(d_pre, t_pre);
-    DIAG_T(t_dbl);
-#if PQG_WALK_CHAIN
-    // the chain of run headers from pos, followed with one v_readlane per run (the successors
-    // stay in registers): ~20 dependent scalar steps per window on C2 pages, cheaper than the
-    // ~8 LDS rounds of pointer doubling (#else) unless a window holds very many runs
-    const uint32_t s0 = pos - B;
-    uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
-    uint32_t q = s0, q_last = s0;
-    while (q < 256u) {
-      q = uni(q);
-      q_last = q;
-      const uint32_t ql = q >> 2, qb = q & 3u;
-      const uint64_t bit = 1ull << ql;
-      uint32_t nq;
-      switch (qb) {
-        case 0: m0 |= bit; nq = rdl(jv[0], ql); break;
-        case 1: m1 |= bit; nq = rdl(jv[1], ql); break;
-        case 2: m2 |= bit; nq = rdl(jv[2], ql); break;
-        default: m3 |= bit; nq = rdl(jv[3], ql); break;
-      }
-      q = nq;
-    }
-    DIAG_ADD(d_dbl, t_dbl);
-    DIAG_T(t_emit);
-    const uint32_t mk = (uint32_t)((m0 >> lane) & 1u) | ((uint32_t)((m1 >> lane) & 1u) << 1) |
-                        ((uint32_t)((m2 >> lane) & 1u) << 2) | ((uint32_t)((m3 >> lane) & 1u) << 3);
-#else
-    const uint32_t s0 = pos - B;
-    *(u64a*)(Jt + 4u * lane) =
-        (uint64_t)jv[0] | ((uint64_t)jv[1] << 16) | ((uint64_t)jv[2] << 32) | ((uint64_t)jv[3] << 48);
-    *(u32a*)(Rt + 4u * lane) = (4u * lane <= s0 && s0 < 4u * lane + 4u) ? (1u << (8u * (s0 & 3u))) : 0u;
-    // pointer doubling: after round r the positions reached within 2^(r+1) steps are marked
-#pragma unroll 1
-    for (int r = 0; r < 8; r++) {
-      const uint32_t r4 = *(const u32a*)(Rt + 4u * lane);
-      uint32_t jn[4];
-#pragma unroll
-      for (uint32_t b = 0; b < 4; b++) {
-        if (((r4 >> (8u * b)) & 1u) && jv[b] < 256u) Rt[jv[b]] = 1;
-        jn[b] = jv[b] < 256u ? Jt[jv[b]] : 256u;
-      }
-#pragma unroll
-      for (uint32_t b = 0; b < 4; b++) jv[b] = jn[b];
-      *(u64a*)(Jt + 4u * lane) =
-          (uint64_t)jv[0] | ((uint64_t)jv[1] << 16) | ((uint64_t)jv[2] << 32) | ((uint64_t)jv[3] << 48);
-      // done when no marked position can still reach further (all its jumps are terminal);
-      // positions marked in this round have not been examined yet, so look at them too
-      const uint32_t r4n = *(const u32a*)(Rt + 4u * lane);
-      bool more = false;
-#pragma unroll
-      for (uint32_t b = 0; b < 4; b++) more |= ((r4n >> (8u * b)) & 1u) && jv[b] < 256u;
-      if (!__ballot(more)) break;
-    }
-    const uint32_t r4 = *(const u32a*)(Rt + 4u * lane);
-    DIAG_ADD(d_dbl, t_dbl);
-    DIAG_T(t_emit);
-    uint32_t mk = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) mk |= ((r4 >> (8u * b)) & 1u) << b;
-    // last chain position of the window (its successor is terminal)
-    uint32_t q_last = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      const uint64_t m = __ballot((mk >> b) & 1u);
-      if (m) {
-        const uint32_t q = 4u * (63u - (uint32_t)__builtin_clzll(m)) + b;
-        q_last = q > q_last ? q : q_last;
-      }
-    }
-#endif
-    q_last = uni(q_last);
-    // runs of the window: marked, inside the section, fast-path headers
-    const uint32_t cap = N - produced;
-    uint32_t cc[4], lsum = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      const bool v = ((mk & inm & ~slowm) >> b) & 1u;
-      const bool pk = (win.flg >> (8u * b)) & 1u;
-      uint32_t c = win.cnt[b];
-      if (!pk && c == 0) c = cap;  // Java: currentCount goes negative, the value repeats forever
-      c = v ? (c < cap ? c : cap) : 0u;
-      cc[b] = c;
-      lsum = lsum + c < cap ? lsum + c : cap;
-    }
-    // saturating inclusive scan of the lane sums
-    uint32_t inc = lsum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o);
-      if ((int)lane >= o) inc = inc + y < cap ? inc + y : cap;
-    }
-    uint32_t st = __shfl_up(inc, 1);
-    if (lane == 0) st = 0;
-    const uint32_t total = uni(rdl(inc, WAVE - 1));
-    // record index of each emitted run (emitted: a run that starts before the cap)
-    uint32_t em = 0, stb[4];
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      stb[b] = st;
-      if (cc[b] && st < cap) em |= 1u << b;
-      st = st + cc[b] < cap ? st + cc[b] : cap;
-    }
-    uint32_t base = 0, n_em = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      const uint64_t m = __ballot((em >> b) & 1u);
-      base += (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
-      n_em += (uint32_t)__builtin_popcountll(m);
-    }
-    uint32_t idx = base;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      if ((em >> b) & 1u) {
-        const bool pk = (win.flg >> (8u * b)) & 1u;
-        const uint32_t vv = win.val[b];
-        const uint32_t payload = pk ? (0x80000000u | vv) : (vv > 0x7FFFFFFFu ? 0x7FFFFFFFu : vv);
-        const uint32_t s_abs = produced + stb[b];
-        const uint32_t e_abs = produced + (stb[b] + cc[b] < cap ? stb[b] + cc[b] : cap);
-        sst(rec + k + idx, (uint64_t)s_abs | ((uint64_t)payload << 32));
-        uint32_t j = s_abs == 0 ? 0 : (s_abs + sh + CH - 1) / CH;
-        for (; j * CH < e_abs + sh; j++) sst(chunk_run + j, k + idx);
-        idx++;
-      }
-    }
-    k += uni(n_em);
-    produced += total;
-#if PQG_EARLY
-    // early hand-off after the first window: records [0, k) cover values [0, produced); the page's
-    // flag goes to epoch - 1 (odd: never a full epoch, never the zeroed initial flag) with that
-    // partial status, so the expansion chunks inside [0, produced) start before the walk ends
-    if (first && pflag && produced < N) {
-      handoff_release();
-      if (lane == 0) {
-        sst(prog, (uint64_t)k | ((uint64_t)produced << 32));
-        handoff_release();
-        sst(pflag, pepoch - 1u);
-      }
-    }
-    first = false;
-#endif
-    DIAG_ADD(d_emit, t_emit);
-#ifdef PQG_DIAG
-    d_win++;
-#endif
-    if (produced >= N) break;
-    // continue after the window's last chain position
-    const uint32_t ql = q_last >> 2, qb = q_last & 3u;
-    const uint32_t q_slow = (rdl(slowm, ql) >> qb) & 1u;
-    const uint32_t q_in = (rdl(inm, ql) >> qb) & 1u;
-    if (!q_in) {
-      pos = B + q_last;  // at or past the section end: RLE_PAST_END on the next iteration
-    } else if (!q_slow) {
-      pos = pick4(nn, qb, ql);  // leaves the window
-    } else {
-      // scalar re-decode of the header at q_last (readNext :80-109)
-      pos = B + q_last;
-      uint32_t hl, m, nxs, vv;
-      uint64_t cnt64;
-      code = SMALL ? slow_header_g([&](uint32_t p) { return uni((seg32(win, p & ~3u) >> ((p & 3u) * 8u)) & 0xFFu); },
-                                   pos, sec_end, w, hl, m, cnt64, vv, nxs)
-                   : slow_header_g([&](uint32_t p) { return wbyte(win, p); }, pos, sec_end, w, hl, m, cnt64, vv, nxs);
-      if (code) break;
-      if (m == 0 && nxs > sec_end) { code = PQG_ERR_EOF; break; }
-      uint64_t cnt = cnt64;
-      const uint32_t left = N - produced;
-      if (m == 0 && cnt == 0) cnt = left;
-      const uint32_t take = cnt < left ? (uint32_t)cnt : left;
-      put_record(produced, produced + take, m ? (0x80000000u | vv) : (vv > 0x7FFFFFFFu ? 0x7FFFFFFFu : vv));
-      produced += take;
-      pos = m ? (nxs < sec_end ? nxs : sec_end) : nxs;
-    }
-  }
-  if (code) {
-    if (lane == 0) report(err, err_count, page, 2, produced, code);
-    N = produced;
-  }
-  n_rec = k;
-  n_ok = N;
-#ifdef PQG_DIAG
-  if (lane == 0 && pqg_diag_buf) {
-    uint64_t* d = pqg_diag_buf + 8 * (uint64_t)page;
-    d[0] = d_start;
-    d[1] = __builtin_amdgcn_s_memtime();
-    d[2] = d_pre;
-    d[3] = d_dbl;
-    d[4] = d_emit;
-    d[5] = d_win;
-    d[6] = k;
-  }
-#endif
 }
 
 // Saturating inclusive scan over the wave: lane l gets min(v_0 + ... + v_l, cap) (every v <= cap <
@@ -962,7 +384,7 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
     if (produced >= N) break;
     if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
     const uint32_t B = pos & ~3u;
-    predecode<SMALL, (bool)PQG_PRE_FAST>(win, B, w);
+    predecode<SMALL, (bool)0>(win, B, w);
     uint32_t js = 0, nn[4], slowm = 0, inm = 0;
     uint64_t ent[4];
 #pragma unroll
@@ -984,55 +406,9 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
     ((u64x2a*)L.ent)[2u * lane] = u64x2{ent[0], ent[1]};
     ((u64x2a*)L.ent)[2u * lane + 1u] = u64x2{ent[2], ent[3]};
     wave_sync();
-#if PQG_WALK_J2
-    // successor of the successor of each position (0: the chain stops within two steps)
-    uint32_t js2 = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      const uint32_t j = (js >> (8u * b)) & 0xFFu;
-      const uint32_t src = (uint32_t)__shfl((int)js, (int)(j >> 2));
-      js2 |= (j ? (src >> ((j & 3u) << 3)) & 0xFFu : 0u) << (8u * b);
-    }
-#endif
     uint32_t q = pos - B, nq = 0;
     while (true) {  // batches of at most 64 chain positions
       uint32_t t = 0, lst = 0;
-#if PQG_WALK_J2
-      while (true) {  // two positions per step: q and its successor n1
-        q = uni(q);
-        t = uni(t);
-        const uint32_t l = q >> 2, sb = (q & 3u) << 3;
-        const uint32_t n1 = (rdl(js, l) >> sb) & 0xFFu;
-        const uint32_t n2 = (rdl(js2, l) >> sb) & 0xFFu;
-        lst = lane == t ? q : lst;
-        lst = lane == t + 1u ? n1 : lst;  // past the batch when n1 == 0 (not read)
-        if (n1 == 0u) { t += 1u; nq = 0u; break; }
-        if (n2 == 0u) { t += 2u; q = n1; nq = 0u; break; }
-        t += 2u;
-        if (t == (uint32_t)WAVE) { q = n1; nq = n2; break; }
-        q = n2;
-      }
-#elif PQG_WALK_VCHAIN
-      {
-        // the chain on the vector unit: q stays in a VGPR (the same value in every lane) and each
-        // step is one ds_bpermute broadcast of the successor dword + a byte extract. The scalar
-        // form (v_readlane + ~15 SALU per run) made Zipf(2.0) walks (~40 runs per window)
-        // scalar-issue bound: the CU's walkers share one scalar unit
-        uint32_t qv = q, tv = 0, nqv = 0;
-        asm volatile("" : "+v"(qv));
-        while (true) {
-          lst = lane == tv ? qv : lst;
-          const uint32_t src = (uint32_t)__shfl((int)js, (int)(qv >> 2));
-          nqv = (src >> ((qv & 3u) << 3)) & 0xFFu;
-          tv++;
-          if (nqv == 0u || tv == (uint32_t)WAVE) break;
-          qv = nqv;
-        }
-        q = uni(qv);
-        t = uni(tv);
-        nq = uni(nqv);
-      }
-#else
       while (true) {
         q = uni(q);
         lst = lane == t ? q : lst;  // v_cmp + v_cndmask
@@ -1041,7 +417,6 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
         if (nq == 0u || t == (uint32_t)WAVE) break;
         q = nq;
       }
-#endif
       t = uni(t);
       nq = uni(nq);
       // the batch's last position q ends the chain here (nq == 0): a run only when it is a
@@ -1115,320 +490,6 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
   n_ok = N;
 }
 
-// ---- One WORKGROUP per page: the page's run headers ranked over 2048-byte super-windows.
-//
-// The same list ranking as dict_walk_pj, with the 256 threads of the workgroup sharing one page:
-// every byte position of a super-window (8 per thread) is parsed as a possible run header, its
-// successor goes to an LDS table, and pointer doubling over the whole super-window (<= 12 rounds,
-// workgroup barriers between them) marks the chain of headers from the window's first header. A
-// page's data section is then walked in ceil(bytes / ~2 KB) serial steps instead of one per 256
-// bytes (dict_walk_pj) or one per run (dict_walk): on Zipf(2.0) pages (~8.7 KB, ~1,500 headers) the
-// per-wave walk took ~140 us, the serial part the expansion waits for.
-constexpr uint32_t PW_SW = 2048;                   // header positions per super-window
-constexpr uint32_t PW_PER_T = PW_SW / (64u * WPB);  // positions per thread (8)
-constexpr uint32_t PW_SEG = PW_SW + 128;            // staged bytes: 16-aligned start + parse slack
-
-struct PageWgLds {
-  uint8_t seg[PW_SEG];    // section bytes [A0, A0 + PW_SEG), A0 = super-window start & ~15
-  uint16_t J[PW_SW];      // successor (window-relative; PW_SW: leaves the window / chain end / slow)
-  uint8_t M[PW_SW];       // on the chain from the window's first header
-  uint32_t red[2][WPB];   // per-wave partials of the workgroup scans / maxima
-};
-
-struct HdrAt {
-  uint32_t nx, cnt, val, flg;  // next header, values, RLE value or packed data start, pk | slow << 1 | hl << 2
-};
-
-// Run header at page position p (LDS offset o of the staged segment): the parse of predecode.
-__device__ __forceinline__ HdrAt hdr_parse(const uint8_t* seg, uint32_t o, uint32_t p, int w) {
-  typedef uint32_t __attribute__((may_alias)) u32a;
-  const uint32_t a = o & ~3u, s = o & 3u;
-  const uint32_t d0 = *(const u32a*)(seg + a), d1 = *(const u32a*)(seg + a + 4), d2 = *(const u32a*)(seg + a + 8),
-                 d3 = *(const u32a*)(seg + a + 12);
-  const uint64_t x = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) |
-                     ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
-  const uint32_t hi8 = __builtin_amdgcn_alignbyte(d3, d2, s);  // bytes p + 8 .. p + 11
-  const uint32_t b0 = (uint32_t)x & 0xFFu, b1 = (uint32_t)(x >> 8) & 0xFFu, b2 = (uint32_t)(x >> 16) & 0xFFu,
-                 b3 = (uint32_t)(x >> 24) & 0xFFu, b4 = (uint32_t)(x >> 32) & 0xFFu;
-  uint32_t v = b0 & 0x7Fu, hl = 1, slow = 0;
-  if (b0 & 0x80u) {
-    v |= (b1 & 0x7Fu) << 7; hl = 2;
-    if (b1 & 0x80u) {
-      v |= (b2 & 0x7Fu) << 14; hl = 3;
-      if (b2 & 0x80u) {
-        v |= (b3 & 0x7Fu) << 21; hl = 4;
-        if (b3 & 0x80u) {
-          v |= b4 << 28; hl = 5;
-          if (b4 & 0x80u) slow = 1;
-        }
-      }
-    }
-  }
-  HdrAt h;
-  const uint32_t nb = ((uint32_t)w + 7u) >> 3;
-  if ((v & 1u) == 0) {
-    const uint32_t shb = 8u * hl;
-    const uint64_t y = (x >> shb) | ((uint64_t)hi8 << (64u - shb));
-    h.val = nb == 4 ? (uint32_t)y : (uint32_t)y & ((1u << (8u * nb)) - 1u);
-    h.cnt = v >> 1;
-    h.nx = p + hl + nb;
-    h.flg = (slow << 1) | (hl << 2);
-  } else {
-    const uint32_t groups = v >> 1;
-    if (groups == 0 || groups >= (1u << 28)) slow = 1;
-    h.cnt = groups * 8u;
-    h.val = p + hl;
-    const uint64_t e = (uint64_t)p + hl + (uint64_t)groups * (uint32_t)w;
-    h.nx = e > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)e;
-    h.flg = 1u | (slow << 1) | (hl << 2);
-  }
-  return h;
-}
-
-// Workgroup exclusive prefix of v saturated at cap (min(sum, cap)); *total = the saturated sum.
-__device__ __forceinline__ uint32_t wg_excl_sat(uint32_t v, uint32_t cap, uint32_t* red, uint32_t* total) {
-  const uint32_t lane = lane_id(), wv = wave_id();
-  uint32_t inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(inc, o);
-    if ((int)lane >= o) inc = inc + y < cap ? inc + y : cap;
-  }
-  uint32_t ex = __shfl_up(inc, 1);
-  if (lane == 0) ex = 0;
-  if (lane == WAVE - 1) red[wv] = inc;
-  __syncthreads();
-  uint32_t before = 0, tot = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < WPB; q++) {
-    const uint32_t sq = red[q];
-    if (q < wv) before = before + sq < cap ? before + sq : cap;
-    tot = tot + sq < cap ? tot + sq : cap;
-  }
-  __syncthreads();
-  *total = tot;
-  return before + ex < cap ? before + ex : cap;
-}
-
-__device__ __forceinline__ uint32_t wg_max(uint32_t v, uint32_t* red) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const uint32_t y = __shfl_xor(v, o);
-    v = y > v ? y : v;
-  }
-  if (lane_id() == 0) red[wave_id()] = v;
-  __syncthreads();
-  uint32_t m = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < WPB; q++) m = red[q] > m ? red[q] : m;
-  __syncthreads();
-  return m;
-}
-
-template <int W>
-__device__ void dict_page_wg(PageWgLds& L, rsrc_t rs, uint32_t N, uint32_t sec_beg, uint32_t sec_end, int w, uint64_t* rec,
-                             uint32_t* chunk_run, uint32_t CH, uint32_t sh, int page, uint64_t* err, ErrCount err_count,
-                             uint32_t& n_rec, uint32_t& n_ok) {
-  const uint32_t t = threadIdx.x;
-  uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position (after the bit width)
-  uint32_t produced = 0, k = 0;
-  int code = 0;
-  // a record written by one thread (the scalar slow path) and the chunk entries it owns
-  auto put_record = [&](uint32_t start, uint32_t end, uint32_t payload) {
-    if (t == 0) {
-      sst(rec + k, (uint64_t)start | ((uint64_t)payload << 32));
-      uint32_t j = start == 0 ? 0 : (start + sh + CH - 1) / CH;
-      for (; j * CH < end + sh; j++) sst(chunk_run + j, k);
-    }
-    k++;
-  };
-  while (true) {
-    // every quantity of this loop is workgroup-uniform
-    if (produced >= N) break;
-    if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
-    const uint32_t P0 = pos, A0 = P0 & ~15u;
-    __syncthreads();  // the previous super-window's LDS reads are done
-    for (uint32_t o = 16u * t; o < PW_SEG; o += 16u * 64u * WPB)
-      *(u32x4*)(L.seg + o) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(A0 + o), 0, 0);
-    __syncthreads();
-    uint32_t jv[PW_PER_T], slowm = 0, inm = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < PW_PER_T; b++) {
-      const uint32_t rel = PW_PER_T * t + b, p = P0 + rel;
-      const HdrAt h = hdr_parse(L.seg, p - A0, p, w);
-      const bool pk = h.flg & 1u, in = p < sec_end;
-      const uint32_t hl = h.flg >> 2;
-      // slow: long varints, 0 / huge group counts, a header or RLE value crossing the end
-      const bool slow = in && ((h.flg & 2u) || p + hl > sec_end || (!pk && h.nx > sec_end));
-      const uint32_t nn = pk ? (h.nx < sec_end ? h.nx : sec_end) : h.nx;
-      jv[b] = (!in || slow || nn - P0 >= PW_SW) ? PW_SW : nn - P0;
-      L.J[rel] = (uint16_t)jv[b];
-      L.M[rel] = rel == 0 ? 1 : 0;
-      slowm |= (slow ? 1u : 0u) << b;
-      inm |= (in ? 1u : 0u) << b;
-    }
-    __syncthreads();
-    // pointer doubling: after round r every chain position within 2^(r+1) steps is marked
-#pragma unroll 1
-    for (int r = 0; r < 12; r++) {
-      uint32_t jn[PW_PER_T];
-#pragma unroll
-      for (uint32_t b = 0; b < PW_PER_T; b++) {
-        const uint32_t rel = PW_PER_T * t + b;
-        if (jv[b] < PW_SW && L.M[rel]) L.M[jv[b]] = 1;
-        jn[b] = jv[b] < PW_SW ? L.J[jv[b]] : PW_SW;
-      }
-      __syncthreads();
-      bool more = false;
-#pragma unroll
-      for (uint32_t b = 0; b < PW_PER_T; b++) {
-        jv[b] = jn[b];
-        L.J[PW_PER_T * t + b] = (uint16_t)jn[b];
-      }
-      __syncthreads();
-#pragma unroll
-      for (uint32_t b = 0; b < PW_PER_T; b++) more |= jv[b] < PW_SW && L.M[PW_PER_T * t + b];
-      if (!__syncthreads_or(more)) break;
-    }
-    // the chain: marked positions in order (thread-major = position order)
-    uint32_t mk = 0, hi_rel = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < PW_PER_T; b++)
-      if (L.M[PW_PER_T * t + b]) {
-        mk |= 1u << b;
-        hi_rel = PW_PER_T * t + b;
-      }
-    const uint32_t q_last = wg_max(hi_rel, L.red[0]);
-    const uint32_t cap = N - produced;
-    uint32_t cc[PW_PER_T], pl[PW_PER_T], lsum = 0, n_run = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < PW_PER_T; b++) {
-      cc[b] = 0;
-      pl[b] = 0;
-      if (((mk & inm & ~slowm) >> b) & 1u) {
-        const uint32_t rel = PW_PER_T * t + b, p = P0 + rel;
-        const HdrAt h = hdr_parse(L.seg, p - A0, p, w);
-        uint32_t c = h.cnt;
-        if (!(h.flg & 1u) && c == 0) c = cap;  // Java: currentCount goes negative, the value repeats forever
-        cc[b] = c < cap ? c : cap;
-        pl[b] = (h.flg & 1u) ? (0x80000000u | h.val) : (h.val > 0x7FFFFFFFu ? 0x7FFFFFFFu : h.val);
-        lsum = lsum + cc[b] < cap ? lsum + cc[b] : cap;
-      }
-    }
-    uint32_t total;
-    uint32_t st = wg_excl_sat(lsum, cap, L.red[0], &total);
-    // emitted: a run that starts before the cap
-    uint32_t em = 0, stb[PW_PER_T];
-#pragma unroll
-    for (uint32_t b = 0; b < PW_PER_T; b++) {
-      stb[b] = st;
-      if (cc[b] && st < cap) em |= 1u << b;
-      st = st + cc[b] < cap ? st + cc[b] : cap;
-    }
-    n_run = (uint32_t)__builtin_popcount(em);
-    uint32_t n_em;
-    uint32_t idx = wg_excl_sat(n_run, 0xFFFFFFFFu, L.red[1], &n_em);
-#pragma unroll
-    for (uint32_t b = 0; b < PW_PER_T; b++) {
-      if ((em >> b) & 1u) {
-        const uint32_t s_abs = produced + stb[b];
-        const uint32_t e_abs = produced + (stb[b] + cc[b] < cap ? stb[b] + cc[b] : cap);
-        sst(rec + k + idx, (uint64_t)s_abs | ((uint64_t)pl[b] << 32));
-        uint32_t j = s_abs == 0 ? 0 : (s_abs + sh + CH - 1) / CH;
-        for (; j * CH < e_abs + sh; j++) sst(chunk_run + j, k + idx);
-        idx++;
-      }
-    }
-    k += n_em;
-    produced += total;
-    if (produced >= N) break;
-    // continue after the chain's last position (every thread parses it from LDS)
-    const uint32_t pq = P0 + q_last;
-    const HdrAt hq = hdr_parse(L.seg, pq - A0, pq, w);
-    const bool q_in = pq < sec_end;
-    const uint32_t q_hl = hq.flg >> 2;
-    const bool q_pk = hq.flg & 1u;
-    const bool q_slow = q_in && ((hq.flg & 2u) || pq + q_hl > sec_end || (!q_pk && hq.nx > sec_end));
-    if (!q_in) {
-      pos = pq;  // at the section end: RLE_PAST_END on the next step
-    } else if (!q_slow) {
-      pos = q_pk ? (hq.nx < sec_end ? hq.nx : sec_end) : hq.nx;  // leaves the super-window
-    } else {
-      // scalar re-decode of the header at pq (readNext :80-109), identical in every thread
-      uint32_t hl, m, nxs, vv;
-      uint64_t cnt64;
-      code = slow_header_g([&](uint32_t p) { return sbyte(rs, p); }, pq, sec_end, w, hl, m, cnt64, vv, nxs);
-      if (code) break;
-      if (m == 0 && nxs > sec_end) { code = PQG_ERR_EOF; break; }
-      uint64_t cnt = cnt64;
-      const uint32_t left = N - produced;
-      if (m == 0 && cnt == 0) cnt = left;
-      const uint32_t take = cnt < left ? (uint32_t)cnt : left;
-      put_record(produced, produced + take, m ? (0x80000000u | vv) : (vv > 0x7FFFFFFFu ? 0x7FFFFFFFu : vv));
-      produced += take;
-      pos = m ? (nxs < sec_end ? nxs : sec_end) : nxs;
-    }
-  }
-  if (code) {
-    if (t == 0) report(err, err_count, page, 2, produced, code);
-    N = produced;
-  }
-  n_rec = k;
-  n_ok = N;
-}
-
-// Walker workgroup for ONE page (dict_page_wg); publishes like dict_runs_body.
-template <int W>
-__device__ __forceinline__ void dict_runs_body_wg(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                                  const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
-                                                  const int32_t* __restrict__ list, int n_list, uint64_t* rec,
-                                                  uint32_t* chunk_run, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                                                  uint64_t* err, ErrCount err_count, uint8_t* lds, uint32_t i_page) {
-  PageWgLds& L = *(PageWgLds*)lds;
-  if (i_page >= (uint32_t)n_list) return;
-  const int page = list[i_page];
-#ifdef PQG_DIAG
-  const uint64_t rt_w0 = __builtin_amdgcn_s_memrealtime();
-#endif
-  const PageWork pw = work[page];
-  uint32_t N = uni(pw.n_values);
-  const uint32_t sec_beg = uni(pw.data_begin), sec_end = uni(pw.size);
-  constexpr uint32_t E = 16u / W;
-  const uint32_t CH = chunk_values(E);
-  const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
-  uint32_t n_rec = 0, n_ok = 0;
-  if (N > 0) {
-    const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
-    if (sec_beg >= sec_end) {
-      // empty data section: every read throws "Attempt to read from empty page"
-      if (threadIdx.x == 0) report(err, err_count, page, 2 /*value*/, 0, PQG_ERR_EMPTY_PAGE);
-    } else {
-      const uint32_t bw = sbyte(rs, sec_beg);
-      if (bw > 32u) {  // RunLengthBitPackingHybridDecoder ctor :55 (thrown at initFromPage)
-        if (threadIdx.x == 0) report(err, err_count, page, 0 /*init*/, 2, PQG_ERR_BIT_WIDTH);
-      } else {
-        dict_page_wg<W>(L, rs, N, sec_beg, sec_end, (int)bw, rec + pw.rec_base, chunk_run + pw.chunk_base, CH, sh, page,
-                        err, err_count, n_rec, n_ok);
-      }
-    }
-  }
-  // Publish (see handoff_release): every wave's record / chunk-entry stores are complete before the
-  // barrier, then thread 0 writes the status and the flag
-  handoff_release();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    sst(pstat + page, (uint64_t)n_rec | ((uint64_t)n_ok << 32));
-    handoff_release();
-    sst(flags + page, epoch);
-#ifdef PQG_DIAG
-    if (pqg_diag_wrt) {
-      pqg_diag_wrt[2 * page] = rt_w0;
-      pqg_diag_wrt[2 * page + 1] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
-  }
-}
-
 // One wave per page (4 per workgroup): the run records of RLE_DICTIONARY / PLAIN_DICTIONARY
 // pages (DictionaryValuesReader.initFromPage :48-64 + RunLengthBitPackingHybridDecoder.readNext
 // :80-109). The page section is staged in LDS; a 256-byte window is pre-decoded in parallel
@@ -1447,11 +508,6 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
   const int page = list[i_page];
 #ifdef PQG_DIAG
   const uint64_t rt_w0 = __builtin_amdgcn_s_memrealtime();
-#endif
-#if PQG_WALK_PRIO
-  // the walk is one serial chain per page that the page's expansion waits for: issue its
-  // instructions ahead of the expansion waves sharing the SIMD
-  __builtin_amdgcn_s_setprio(PQG_WALK_PRIO);
 #endif
   const uint32_t lane = lane_id();
   const PageWork pw = work[page];
@@ -1479,29 +535,11 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
         uint64_t* prec = rec + pw.rec_base;
         uint32_t* pcr = chunk_run + pw.chunk_base;
         // SMALL: the whole data section sits in the LDS segment: the walk has no global load
-#if PQG_WALK_LIST && !PQG_EARLY
         if (sec_end - win.seg_lo + 264u <= SEG_BYTES)  // every window inside the segment
           dict_walk_ls<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
         else
           dict_walk_ls<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec,
                                  n_ok);
-#else
-        if (sec_end - win.seg_lo + 264u <= SEG_BYTES)  // every window inside the segment
-          dict_walk_pj<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok,
-                          pstat + page, flags + page, epoch);
-#if PQG_PJ_LARGE
-        // larger sections: the same window walk, the LDS segment refilled as the chain advances
-        // (windows inside long bit-packed runs are jumped over, not pre-decoded)
-        else
-          dict_walk_pj<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec,
-                                 n_ok, pstat + page, flags + page, epoch);
-#else
-        else if (sec_end - win.seg_lo <= SEG_BYTES)
-          dict_walk<W, true>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
-        else
-          dict_walk<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
-#endif
-#endif
       }
     }
   }
@@ -1512,11 +550,7 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
   if (lane == 0) {
     sst(pstat + page, (uint64_t)n_rec | ((uint64_t)n_ok << 32));
     handoff_release();
-#if PQG_HANDOFF & 1
-    __hip_atomic_store(flags + page, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-#else
     sst(flags + page, epoch);
-#endif
 #ifdef PQG_DIAG
     if (pqg_diag_wrt) {
       pqg_diag_wrt[2 * page] = rt_w0;
@@ -1524,9 +558,6 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
     }
 #endif
   }
-#if PQG_WALK_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 template <int W>
@@ -1535,16 +566,10 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_runs(const uint8_t* __restric
                                                         const ColumnDev* __restrict__ cols,
                                                         const int32_t* __restrict__ list, int n_list, uint64_t* rec,
                                                         uint32_t* chunk_run, uint64_t* pstat, uint32_t* flags,
-                                                        uint32_t epoch, uint32_t walk_pg, uint64_t* err,
-                                                        ErrCount err_count) {
+                                                        uint32_t epoch, uint64_t* err, ErrCount err_count) {
   __shared__ __attribute__((aligned(16))) DictWaveLds wl_all[WPB];
-  static_assert(sizeof(DictWaveLds) * WPB >= sizeof(PageWgLds), "walker LDS");
-  if (walk_pg)
-    dict_runs_body_wg<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
-                         (uint8_t*)wl_all, blockIdx.x);
-  else
-    dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
-                      (uint8_t*)wl_all, blockIdx.x);
+  dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
+                    (uint8_t*)wl_all, blockIdx.x);
 }
 
 template <int W>
@@ -1562,19 +587,10 @@ __device__ __forceinline__ typename DictVal<W>::T dict_get_g(bool in_lds, const 
 //   tile sweep  every lane tracks the run holding its element: per tile it advances past
 //               the run starts it crossed (usually none), reads the value (RLE) or unpacks
 //               the id and gathers (packed), and the wave stores one full 1 KB tile.
-#ifndef PQG_XT_RUNS
-#define PQG_XT_RUNS 128
-#endif
-#ifndef PQG_XT_SEG
-#define PQG_XT_SEG 2560
-#endif
-constexpr uint32_t XT_RUNS = PQG_XT_RUNS;  // run table entries per wave
-constexpr uint32_t XT_SEG = PQG_XT_SEG;    // LDS bytes for the packed data of one round
+constexpr uint32_t XT_RUNS = 128;  // run table entries per wave
+constexpr uint32_t XT_SEG = 2560;    // LDS bytes for the packed data of one round
 
 constexpr uint32_t XT_LDS_BYTES = DICT_LDS_BYTES + WPB * (XT_RUNS * 16 + XT_SEG);
-#ifndef PQG_SPIN_SLEEP
-#define PQG_SPIN_SLEEP 2
-#endif
 #ifdef PQG_FAULT_INJECT
 // Fault-injection build (tests/build/libpqgpu_faultinject.so, tests/test_gpu_timeout.py only; never
 // the product): walker workgroup 0 of every fused launch starts PQG_FAULT_INJECT ticks late, past a
@@ -1598,8 +614,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
                                                 const uint64_t* rec, const uint32_t* chunk_run,
                                                 const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                 const uint64_t* pstat, const uint32_t* flags, uint32_t epoch,
-                                                uint64_t* err, ErrCount err_count, uint8_t* lds, uint32_t group,
-                                                uint32_t tile_stride = 0) {
+                                                uint64_t* err, ErrCount err_count, uint8_t* lds, uint32_t group) {
   typedef typename DictVal<W>::T T;
   constexpr uint32_t E = 16 / W;
   constexpr uint32_t TV = WAVE * E;  // values per tile
@@ -1633,14 +648,10 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
     if (dict_in_lds) {
       rsrc_t d0 = make_rsrc(bytes + cd0.dict_offset, cd0.dict_bytes);
       for (uint32_t o = 16u * threadIdx.x; o < (uint32_t)need; o += 16u * 64u * WPB)
-#ifdef PQG_DICT_STAGE_DWORDS
-        *(u32x4*)(dict_lds + o) = u32x4{ld4_any(d0, o), ld4_any(d0, o + 4), ld4_any(d0, o + 8), ld4_any(d0, o + 12)};
-#else
         *(u32x4*)(dict_lds + o) =  // any byte alignment; the piece at the buffer's end dword by dword
             o + 16u <= cd0.dict_bytes
                 ? __builtin_amdgcn_raw_buffer_load_b128(d0, (int)o, 0, 0)
                 : u32x4{ld4_any(d0, o), ld4_any(d0, o + 4), ld4_any(d0, o + 8), ld4_any(d0, o + 12)};
-#endif
     }
   }
   __syncthreads();
@@ -1692,24 +703,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
           pst = uni64(sld(pstat + page));
           break;
         }
-#if PQG_EARLY
-        // the walker's partial status (flag epoch - 1): go when it covers this chunk's values;
-        // the status may already be the final one (stored before the final flag), never an older one
-        if (uni(sld(flags + page)) == epoch - 1u) {
-          const uint32_t sh0 = (uint32_t)(pw.out_offset % (uint64_t)E), nv = uni(pw.n_values);
-          const uint32_t need = ((j + 1) * CH < nv + sh0 ? (j + 1) * CH : nv + sh0) - sh0;
-          handoff_acquire();
-          const uint64_t pp = uni64(sld(pstat + page));
-          if ((uint32_t)(pp >> 32) >= need) {
-#ifdef PQG_DIAG
-            rt_x1 = __builtin_amdgcn_s_memrealtime();
-#endif
-            pst = pp;
-            break;
-          }
-        }
-#endif
-        __builtin_amdgcn_s_sleep(PQG_SPIN_SLEEP);
+        __builtin_amdgcn_s_sleep(2);
         // wall-clock bound (s_memrealtime: constant 100 MHz): a walker that never publishes
         // (descheduled, starved) turns into PQG_ERR_TIMEOUT after SPIN_TIMEOUT_TICKS, not a hang
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -1819,9 +813,6 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       auto sweep = [&](auto fast_tag) {
         constexpr bool FAST = decltype(fast_tag)::value;
         auto value = [&](uint32_t ci, uint32_t i, const u32x4& q) -> T {
-#ifdef PQG_XT_NOVALUE  // A/B diagnostic: the sweep's loop and stores without the value computation
-          return (T)i;
-#endif
           if (!(q.y & 0x80000000u)) return (T)(((uint64_t)q.w << 32) | q.z);
           const uint64_t bit = (uint64_t)(i - q.x) * (uint32_t)w;
           const uint32_t byte = (q.y & 0x7FFFFFFFu) + (uint32_t)(bit >> 3);
@@ -1904,11 +895,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
     }
     return true;
   };
-  // tile_stride == 0: one chunk per wave; else persistent: this wave's chunks c, c + 4 * stride, ...
-  // (chunks in page order, so a wave's next chunk is a page walked later)
-  for (uint32_t cc = c; cc < n_chunks; cc += WPB * tile_stride) {
-    if (!one_chunk(cc) || !tile_stride) break;
-  }
+  if (c < n_chunks) one_chunk(c);  // one chunk per wave
 }
 
 template <int W, bool IDS = false>
@@ -1925,48 +912,30 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_tiles(const uint8_t* __restri
 
 // Walkers and tiles in one grid: workgroups [0, n_walk) walk pages, the rest expand chunks
 // as soon as their page is published, so the expansion overlaps the walk.
-#ifdef PQG_WAVES_PER_EU
-#define PQG_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(PQG_WAVES_PER_EU, PQG_WAVES_PER_EU)))
-#else
-#define PQG_FUSED_ATTR
-#endif
 template <int W, bool IDS = false>
-__global__ __launch_bounds__(64 * WPB) PQG_FUSED_ATTR void k_dict_fused(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                          const PageWork* __restrict__ work,
                                                          const ColumnDev* __restrict__ cols,
                                                          const int32_t* __restrict__ list, int n_list,
                                                          uint32_t n_walk, uint64_t* rec, uint32_t* chunk_run,
                                                          const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                          uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                                                         uint32_t walk_wg, uint32_t tile_wg, uint32_t walk_pg, uint64_t* err,
-                                                         ErrCount err_count) {
+                                                         uint64_t* err, ErrCount err_count) {
   constexpr uint32_t LB = sizeof(DictWaveLds) * WPB > XT_LDS_BYTES ? sizeof(DictWaveLds) * WPB : XT_LDS_BYTES;
-  static_assert(LB >= sizeof(PageWgLds), "walker LDS");
   __shared__ __attribute__((aligned(16))) uint8_t lds[LB];
-  // workgroups [0, n_walk) walk, the rest expand. walk_wg / tile_wg > 0: persistent workgroups
-  // that take every walk_wg-th group of 4 pages / every tile_wg-th group of 4 chunks, in page order.
-  // walk_pg: a walker workgroup walks ONE page with all its threads (dict_page_wg)
-  if (blockIdx.x < n_walk && walk_pg) {
-    for (uint32_t g = blockIdx.x; g < (uint32_t)n_list; g += walk_wg) {
-      dict_runs_body_wg<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err,
-                           err_count, lds, g);
-      if (!walk_wg) break;
-    }
-  } else if (blockIdx.x < n_walk) {
+  // workgroups [0, n_walk) walk (4 pages each), the rest expand (4 chunks each)
+  if (blockIdx.x < n_walk) {
 #ifdef PQG_FAULT_INJECT
     if (blockIdx.x == 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)PQG_FAULT_INJECT) __builtin_amdgcn_s_sleep(127);
     }
 #endif
-    for (uint32_t g = blockIdx.x; g * WPB < (uint32_t)n_list; g += walk_wg) {
-      dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
-                        lds, g);
-      if (!walk_wg) break;
-    }
+    dict_runs_body<W>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
+                      lds, blockIdx.x);
   } else {
     dict_tiles_body<W, true, IDS>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch,
-                                  err, err_count, lds, blockIdx.x - n_walk, tile_wg);
+                                  err, err_count, lds, blockIdx.x - n_walk);
   }
 }
 
@@ -2034,23 +1003,10 @@ __device__ __forceinline__ uint32_t tile_byte_mask(int32_t jb, int32_t je, int32
 }
 
 // Run holding slot lo_s: the largest a < n_run (<= 256) with r_start[a] <= lo_s (r_start ascending,
-// r_start[0] <= lo_s). PQG_LEVELS_FIXED_SEARCH: eight fixed steps with unconditional LDS reads
-// instead of the divergent bisection loop (whose exec bookkeeping runs on the scalar unit):
-// measured C3 10.01 -> 10.10 ms, C5 2.17 -> 2.19 ms (profiles/r02/lv_ab), so off.
-#ifndef PQG_LEVELS_FIXED_SEARCH
-#define PQG_LEVELS_FIXED_SEARCH 0
-#endif
+// r_start[0] <= lo_s). Eight fixed steps with unconditional LDS reads instead of this divergent
+// bisection loop (whose exec bookkeeping runs on the scalar unit) measured C3 10.01 -> 10.10 ms,
+// C5 2.17 -> 2.19 ms (profiles/r02/lv_ab) and were removed.
 __device__ __forceinline__ uint32_t level_run_of(const LevelWaveLds& L, uint32_t n_run, uint32_t lo_s) {
-#if PQG_LEVELS_FIXED_SEARCH
-  uint32_t a = 0;
-#pragma unroll
-  for (uint32_t step = 128; step >= 1; step >>= 1) {
-    const uint32_t i = a + step;
-    const uint32_t v = L.r_start[i < n_run ? i : n_run - 1u];
-    a = (i < n_run && v <= lo_s) ? i : a;
-  }
-  return a;
-#else
   uint32_t a = 0, b = n_run;
   while (b - a > 1) {
     const uint32_t mid = (a + b) >> 1;
@@ -2058,7 +1014,6 @@ __device__ __forceinline__ uint32_t level_run_of(const LevelWaveLds& L, uint32_t
     else b = mid;
   }
   return a;
-#endif
 }
 
 // Bit width WB (1..8) specialisation of expand_level_runs: per tile piece (the part of one run
@@ -2072,7 +1027,6 @@ __device__ __forceinline__ void expand_level_tiles(const LevelWaveLds& L, const 
   const rsrc_t rs = win.rs;
   const uint32_t lane = lane_id();
   const int64_t mis = out ? (int64_t)((uintptr_t)out & 15u) : 0;
-#if PQG_LEVELS_BITS
   // width 1 with every RLE value 0 or 1 (the usual flat optional column): the tile's 16 levels
   // are built as a 16-bit mask (3 operations per piece) and spread to bytes once per tile
   bool bits_ok = false;
@@ -2084,7 +1038,6 @@ __device__ __forceinline__ void expand_level_tiles(const LevelWaveLds& L, const 
     }
     bits_ok = !__ballot(bad);
   }
-#endif
   for (int64_t t = (((int64_t)s_lo + mis) & ~(int64_t)15) - mis; t < (int64_t)s_hi; t += 16 * WAVE) {
     const int64_t s0 = t + 16 * (int64_t)lane;
     if (s0 + 16 <= (int64_t)s_lo || s0 >= (int64_t)s_hi) continue;
@@ -2093,7 +1046,6 @@ __device__ __forceinline__ void expand_level_tiles(const LevelWaveLds& L, const 
     const uint32_t a = level_run_of(L, n_run, lo_s);
     uint32_t acc[4] = {0u, 0u, 0u, 0u};
     uint32_t cur = lo_s, k = a;
-#if PQG_LEVELS_BITS
     if (WB == 1 && bits_ok) {
       uint32_t m = 0;  // bit j: level of tile slot j
       while (cur < hi_s) {
@@ -2144,7 +1096,6 @@ __device__ __forceinline__ void expand_level_tiles(const LevelWaveLds& L, const 
       }
       continue;
     }
-#endif
     while (cur < hi_s) {
       const uint32_t st = L.r_start[k], pay = L.r_pay[k];
       const uint32_t re = k + 1 < n_run ? L.r_start[k + 1] : s_hi;
@@ -2487,124 +1438,6 @@ __device__ __forceinline__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs,
   return code ? produced : N;
 }
 
-// Decode one level section into out[slot_base + i], i < N. Returns the number of
-// slots decoded before an error (N when none) and sets *err_code.
-__device__ uint32_t decode_levels(rsrc_t rs, uint32_t beg, uint32_t end, int w, uint32_t N, uint8_t* out,
-                                  uint32_t max_def, bool count_nonnull, uint32_t* nonnull, int* err_code) {
-  const uint32_t lane = lane_id();
-  RleWalk s;
-  s.pos = beg;
-  s.sec_end = end;
-  s.produced = 0;
-  s.pend_count = 0;
-  s.N = N;
-  s.w = w;
-  PreWin win;
-  win.rs = rs;
-  win.seg = nullptr;
-  win.seg_lo = 0;
-  if (N) predecode(win, beg & ~3u, w);
-  uint32_t cnt = 0;
-  int first_err = 0;
-  uint32_t done = N;
-  while (s.produced < s.N) {
-    RunBatch rb;
-    int code = walk_batch(win, s, rb);
-    if (code && !first_err) { first_err = code; done = rb.end; }
-    if (lane < rb.nr && rb.meta == 0) rb.lo = rb.lo > 255u ? 255u : rb.lo;  // saturate (pqgpu.h)
-    const uint32_t nxt_start = (uint32_t)__shfl_down((int)rb.start, 1);  // convergent: every lane
-    const uint32_t run_end = (lane + 1 < rb.nr) ? nxt_start : rb.end;
-    const uint32_t nr = uni(rb.nr), first = uni(rb.first), endv = uni(rb.end);
-#ifdef PQG_ABLATE_LVL_EXPAND
-    if (endv != 0xFFFFFFFFu) continue;  // diagnostic ablation: walk only
-#endif
-    // tiles of 64 lanes x 16 slots; tile boundaries where out + slot is 16-byte aligned
-    const int64_t mis = out ? (int64_t)((uintptr_t)out & 15u) : 0;
-    for (int64_t t = (((int64_t)first + mis) & ~(int64_t)15) - mis; t < (int64_t)endv; t += 16 * WAVE) {
-      const int64_t s0 = t + 16 * (int64_t)lane;
-      const uint32_t lo_s = (uint32_t)(s0 > (int64_t)first ? s0 : (int64_t)first);
-      const uint32_t hi_s = (uint32_t)(s0 + 16 < (int64_t)endv ? s0 + 16 : (int64_t)endv);
-      const bool act = s0 + 16 > (int64_t)first && s0 < (int64_t)endv;
-      // run holding the lane's first slot: largest r < nr with start[r] <= lo_s
-      uint32_t r = 0;
-#pragma unroll
-      for (uint32_t step = 32; step >= 1; step >>= 1) {
-        const uint32_t c = r + step;
-        const uint32_t v = (uint32_t)__shfl((int)rb.start, (int)(c & 63u));
-        if (c < nr && v <= lo_s) r = c;
-      }
-      uint64_t wlo = 0, whi = 0;  // the lane's 16 level bytes
-      uint32_t cur = act ? lo_s : hi_s;
-      while (__ballot(cur < hi_s)) {  // one run of each lane per pass (usually one pass)
-        const uint32_t st = (uint32_t)__shfl((int)rb.start, (int)r), m = (uint32_t)__shfl((int)rb.meta, (int)r);
-        const uint32_t rlo = (uint32_t)__shfl((int)rb.lo, (int)r), rhi = (uint32_t)__shfl((int)rb.hi, (int)r);
-        const uint32_t re = (uint32_t)__shfl((int)run_end, (int)r);
-        if (cur < hi_s) {
-          const uint32_t stop = hi_s < re ? hi_s : re;
-          if (m == 0) {
-            for (uint32_t q = cur; q < stop; q++) {
-              const uint32_t j = q - (uint32_t)s0;
-              if (j < 8) wlo |= (uint64_t)rlo << (8 * j);
-              else whi |= (uint64_t)rlo << (8 * (j - 8));
-            }
-          } else if (w > 0) {
-            // bits [(cur - st) * w, (stop - st) * w) of the run's bytes [rlo, rhi); past rhi: 0
-            const uint64_t bit0 = (uint64_t)(cur - st) * (uint32_t)w;
-            const uint32_t a0 = rlo + (uint32_t)(bit0 >> 3);
-            uint64_t x[3];
-#pragma unroll
-            for (uint32_t c = 0; c < 3; c++) {
-              const uint32_t ac = a0 + 8u * c;
-              uint64_t v = ld8_any(win.rs, ac);
-              const int64_t keep = (int64_t)rhi - (int64_t)ac;
-              x[c] = keep >= 8 ? v : (keep <= 0 ? 0 : (v & ((1ull << (8 * keep)) - 1ull)));
-            }
-            const uint32_t wmask = w >= 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
-            for (uint32_t q = cur; q < stop; q++) {
-              const uint32_t sh = (uint32_t)(bit0 & 7u) + (q - cur) * (uint32_t)w;  // < 8 + 15 * 32
-              const uint32_t c = sh >> 6, o = sh & 63u;
-              const uint64_t lo64 = c == 0 ? x[0] : (c == 1 ? x[1] : x[2]);
-              const uint64_t hi64 = c == 0 ? x[1] : (c == 1 ? x[2] : 0ull);
-              const uint64_t f = o ? ((lo64 >> o) | (hi64 << (64u - o))) : lo64;
-              uint32_t v = (uint32_t)f & wmask;
-              v = v > 255u ? 255u : v;
-              const uint32_t j = q - (uint32_t)s0;
-              if (j < 8) wlo |= (uint64_t)v << (8 * j);
-              else whi |= (uint64_t)v << (8 * (j - 8));
-            }
-          }
-          cur = stop;
-          r++;
-        }
-      }
-      if (act) {
-        const uint32_t j0 = lo_s - (uint32_t)s0, j1 = hi_s - (uint32_t)s0;
-        if (count_nonnull) {
-          for (uint32_t j = j0; j < j1; j++) {
-            const uint32_t v = (uint32_t)((j < 8 ? wlo >> (8 * j) : whi >> (8 * (j - 8))) & 0xFFu);
-            cnt += v == max_def ? 1u : 0u;
-          }
-        }
-        if (out) {
-          uint8_t* o = out + s0;
-          if (j0 == 0 && j1 == 16) {
-            typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-            gst((v2*)o, v2{wlo, whi});
-          } else {
-            for (uint32_t j = j0; j < j1; j++)
-              gst(o + j, (uint8_t)((j < 8 ? wlo >> (8 * j) : whi >> (8 * (j - 8))) & 0xFFu));
-          }
-        }
-      }
-    }
-  }
-  // wave reduce
-  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-  if (nonnull) *nonnull = cnt;
-  *err_code = first_err;
-  return done;
-}
-
 // decode_levels_pj with the tile expansion specialised for the section's bit width.
 __device__ __forceinline__ uint32_t decode_levels_w(LevelWaveLds& L, rsrc_t rs, uint32_t beg, uint32_t end, int w,
                                                     uint32_t N, uint8_t* out, uint32_t max_def, bool count_nonnull,
@@ -2908,13 +1741,7 @@ __global__ __launch_bounds__(64 * WPB) void k_rle_bool(const uint8_t* __restrict
 // a full store drain per block (vmcnt counts stores on CDNA).
 constexpr uint32_t DSEG = 8192;
 // segment expansion (delta_expand_seg) for miniblocks of a multiple of 16 deltas
-#ifndef PQG_DELTA_SEG
-#define PQG_DELTA_SEG 1
-#endif
 // block headers parsed by the vector unit (delta_hdr_v)
-#ifndef PQG_DELTA_VHDR
-#define PQG_DELTA_VHDR 1
-#endif
 
 struct DSeg {
   rsrc_t rs;
@@ -3390,7 +2217,6 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
       if (nb >= 64u || buffered >= total) break;
       if (p >= end) return PQG_ERR_EOF;
       if (!S.has(p, HDR_SPAN)) break;  // nb > 0 here: the batch ends, the next one refills
-#if PQG_DELTA_VHDR
       {
         DeltaHdr h;
         if (delta_hdr_v(S, p, end, mbn, mbs, buffered, total, h)) {
@@ -3409,7 +2235,6 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
           continue;
         }
       }
-#endif
       const uint64_t mraw = seg_uvar<false>(S, p, end - p, len);  // loadNewBlockToBuffer :122-126
       if ((uint64_t)p + len > end) return PQG_ERR_EOF;
       const int64_t mind = zigzag64(mraw);
@@ -3441,7 +2266,6 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
       nb++;
     }
     if (nb == 0) return PQG_ERR_CORRUPT;  // unreachable: the first block of a batch always fits
-#if PQG_DELTA_VHDR
     // min deltas of the blocks delta_hdr_v walked, one lane per block (the segment holds them: it is
     // refilled only at a batch start)
     if (b_mv) {
@@ -3449,12 +2273,11 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
       b_lo = (uint32_t)md;
       b_hi = (uint32_t)(md >> 32);
     }
-#endif
     // ---- expand the walked blocks (every read from the LDS segment)
     // (the segment path stores 16-value runs per lane: only where they are 16-byte aligned; a
     // page of a nullable column starts at any value offset, and per-element stores of lane-private
     // runs measured slower than delta_expand's lane-interleaved ones)
-    if (PQG_DELTA_SEG && !NEG && (mbs % 16u) == 0 && ((uintptr_t)out % 16u) == 0 && ((uint64_t)block * W) % 16u == 0)
+    if (!NEG && (mbs % 16u) == 0 && ((uintptr_t)out % 16u) == 0 && ((uint64_t)block * W) % 16u == 0)
       delta_expand_seg<W>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out);
     else if (E == 1) delta_expand<W, NEG, 1>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else if (E == 2) delta_expand<W, NEG, 2>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
@@ -3661,31 +2484,29 @@ namespace pqg {
 hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                        const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                        const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
-                       bool fused, uint32_t walk_wg, uint32_t tile_wg, uint32_t walk_pg, uint64_t* err,
-                       ErrCount err_count) {
+                       bool fused, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
-  uint32_t n_walk = walk_pg ? (uint32_t)n : (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
-  if (fused && walk_wg && walk_wg < n_walk) n_walk = walk_wg; else walk_wg = fused && walk_wg ? n_walk : walk_wg;
-  if (fused && tile_wg && tile_wg < n_tile) n_tile = tile_wg; else tile_wg = fused && tile_wg ? n_tile : tile_wg;
+  const uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
   const dim3 blk(64 * WPB);
   if (fused) {
     if (width == 8)
       hipLaunchKernelGGL(k_dict_fused<8>, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n, n_walk,
-                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, walk_pg, err, err_count);
+                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count);
     else
       hipLaunchKernelGGL(k_dict_fused<4>, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n, n_walk,
-                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, walk_pg, err, err_count);
+                         rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count);
     return hipGetLastError();
   }
+  // split mode (pqg_sync's re-run after a fused-kernel timeout): walk, then expand, two launches
   if (width == 8) {
     hipLaunchKernelGGL(k_dict_runs<8>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,
-                       pstat, flags, epoch, walk_pg, err, err_count);
+                       pstat, flags, epoch, err, err_count);
     if (n_tile)
       hipLaunchKernelGGL(k_dict_tiles<8>, dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks,
                          n_chunks, pstat, err, err_count);
   } else {
     hipLaunchKernelGGL(k_dict_runs<4>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,
-                       pstat, flags, epoch, walk_pg, err, err_count);
+                       pstat, flags, epoch, err, err_count);
     if (n_tile)
       hipLaunchKernelGGL(k_dict_tiles<4>, dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks,
                          n_chunks, pstat, err, err_count);
@@ -3696,20 +2517,17 @@ hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t
 hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                            const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
-                           uint32_t epoch, bool fused, uint32_t walk_wg, uint32_t tile_wg, uint32_t walk_pg,
-                           uint64_t* err, ErrCount err_count) {
+                           uint32_t epoch, bool fused, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
-  uint32_t n_walk = walk_pg ? (uint32_t)n : (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
-  if (fused && walk_wg && walk_wg < n_walk) n_walk = walk_wg; else walk_wg = fused && walk_wg ? n_walk : walk_wg;
-  if (fused && tile_wg && tile_wg < n_tile) n_tile = tile_wg; else tile_wg = fused && tile_wg ? n_tile : tile_wg;
+  const uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
   const dim3 blk(64 * WPB);
   if (fused) {
     hipLaunchKernelGGL((k_dict_fused<4, true>), dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n,
-                       n_walk, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, walk_wg, tile_wg, walk_pg, err, err_count);
+                       n_walk, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_dict_runs<4>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,
-                     pstat, flags, epoch, walk_pg, err, err_count);
+                     pstat, flags, epoch, err, err_count);
   if (n_tile)
     hipLaunchKernelGGL((k_dict_tiles<4, true>), dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run,
                        chunks, n_chunks, pstat, err, err_count);

@@ -57,17 +57,10 @@ __device__ __forceinline__ int zhigh(uint32_t v) { return v ? 31 - __builtin_clz
 
 // Reads of bytes this wave stored earlier (literal buffer, output), after the s_waitcnt that
 // completed the stores: system-scope loads (L1 and L2 bypassed). A workgroup-scope load
-// (PQG_ZSTD_SLD=0) measured the same (71.7 ms on 100 M int64 PLAIN pages, profiles/r02/zstd_ab):
+// measured the same (71.7 ms on 100 M int64 PLAIN pages, profiles/r02/zstd_ab):
 // the kernel is not bound by these round trips.
-#ifndef PQG_ZSTD_SLD
-#define PQG_ZSTD_SLD 1
-#endif
 __device__ __forceinline__ uint32_t zld(const uint32_t* p) {
-#if PQG_ZSTD_SLD
   return sld(p);
-#else
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
 }
 
 // one input byte at `o` of the job's input (uniform reads: every lane loads the same dword)
