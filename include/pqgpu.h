@@ -359,7 +359,9 @@ int pqg_snappy_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_statu
  * dst_size bytes at d_dst + dst_offset. Frames that end before dst_size -> PQG_ERR_EOF; a malformed
  * frame, a frame content size or content checksum (XXH64) that does not match -> PQG_ERR_CORRUPT;
  * dictionaries are not supported (a frame naming one -> CORRUPT). Asynchronous on the context's
- * stream; the context keeps 128 KiB of device scratch per job. pqg_zstd_sync reports the first
+ * stream; the context keeps 128 KiB of device scratch per decoding wave (at most 4,096 waves, each
+ * looping over the jobs: 512 MiB at most, whatever the number of pages); the output is read back
+ * only inside each job's [dst_offset, dst_offset + dst_size) (no padding needed). pqg_zstd_sync reports the first
  * failing job (st->page = job index). */
 typedef pqg_snappy_job pqg_zstd_job;
 

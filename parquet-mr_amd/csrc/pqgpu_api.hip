@@ -149,6 +149,9 @@ struct pqg_plan {
   std::vector<uint64_t> col_required_values;
   std::vector<HostErr> host_errs;
   int kernels = 0;
+  DevBuf segs;                        // PLAIN BYTE_ARRAY segments (k_bin_walk_seg): page | s << 32 | last << 63
+  uint32_t n_segs = 0;
+  uint64_t seg_status_off = 0, seg_tmp_off = 0;  // in bscratch: status words + ticket (cleared per launch), scratch
   int timeout_fallbacks = 0;           // launches re-run in split mode after PQG_ERR_TIMEOUT (pqg_sync)
 };
 
@@ -163,7 +166,7 @@ struct pqg_ctx {
   DevBuf host_bytes, host_out, host_counts, host_runs;
   DevBuf asm_scratch;                // pqg_assemble: block counts + totals
   hipStream_t copy_stream = nullptr; // pqg_decode_host: second D2H queue (odd output chunks)
-  DevBuf zstd_scratch;               // pqg_zstd_decompress: literal buffers, ZSTD_LIT_SCRATCH per job
+  DevBuf zstd_scratch;               // pqg_zstd_decompress: literal buffers, ZSTD_LIT_SCRATCH per grid wave
 };
 
 extern "C" {
@@ -458,12 +461,28 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   auto take = [&](uint64_t bytes) { uint64_t o = sc; sc = (sc + bytes + 255) & ~uint64_t(255); return o; };
   std::vector<uint8_t> needs_ids((size_t)std::max(n_cols, 1), 0);
   for (int p : cls_lists[C_IDS]) needs_ids[(size_t)P->h_work[(size_t)p].column] = 1;
+  // PLAIN BYTE_ARRAY pages walked in segments when there are few of them (k_bin_walk_seg)
+  std::vector<uint64_t> segs;
+  std::vector<uint8_t> seg_page((size_t)std::max(n_pages, 1), 0);
+  if (!cls_lists[C_BINP].empty() && cls_lists[C_BINP].size() < pqg::BW_SEG_MAX_PAGES) {
+    for (int p : cls_lists[C_BINP]) {
+      const PageWork& w = P->h_work[(size_t)p];
+      const uint32_t nseg = (w.size + pqg::BW_SEG_BYTES - 1) / pqg::BW_SEG_BYTES + 1;  // + 1: tile alignment of the start
+      if (nseg < 3) continue;
+      seg_page[(size_t)p] = 1;
+      for (uint32_t k = 0; k < nseg; k++)
+        segs.push_back((uint64_t)(uint32_t)p | ((uint64_t)k << 32) | (k + 1 == nseg ? (1ull << 63) : 0ull));
+    }
+  }
   for (int i = 0; i < n_cols; i++) {  // blen first: the part cleared before every launch
     if (ids_mode(cols[i])) continue;  // ids go straight to the column's values
     if (bin_out(cols[i]) || needs_ids[(size_t)i] || dba_fixed[(size_t)i])
       blen_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
   }
+  if (!segs.empty()) P->seg_status_off = take(8 * (segs.size() + 1));  // + the ticket counter
   P->blen_bytes = sc;
+  if (!segs.empty()) P->seg_tmp_off = take(4 * 2 * (uint64_t)pqg::BW_SEG_CAP * segs.size());
+  P->n_segs = (uint32_t)segs.size();
   for (int i = 0; i < n_cols; i++) {
     if (dba_fixed[(size_t)i]) bsrc_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));  // prefix lengths
     if (dba_carry[(size_t)i]) carry_cols.push_back(i);
@@ -496,6 +515,12 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       const uint32_t nch = (w.num_slots + pqg::CP_CHUNK_VALUES - 1) / pqg::CP_CHUNK_VALUES;
       for (uint32_t j = 0; j < nch; j++) bin_chunks.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
     }
+  if (!segs.empty()) {  // walked by k_bin_walk_seg instead of the one-wave-per-page walk
+    std::vector<int> keep;
+    for (int p : cls_lists[C_BINP])
+      if (!seg_page[(size_t)p]) keep.push_back(p);
+    cls_lists[C_BINP].swap(keep);
+  }
   // ---- DELTA_BYTE_ARRAY pages: BIN_CHUNK-value chunks (upper bound from the slot count)
   std::vector<uint64_t> dba_chunks;
   for (int p : cls_lists[C_DBA]) {
@@ -525,6 +550,11 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       for (uint32_t j = 0; j < nch; j++) chunk_list.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
       chunk_total += nch;
     }
+#ifdef PQG_AB_ORDER
+    std::stable_sort(chunk_list.begin() + P->chunk_off[k - C_DICT4], chunk_list.end(), [&](uint64_t a, uint64_t b) {
+      return P->h_work[(size_t)(uint32_t)a].size < P->h_work[(size_t)(uint32_t)b].size;
+    });
+#endif
     P->chunk_n[k - C_DICT4] = (uint32_t)chunk_list.size() - P->chunk_off[k - C_DICT4];
   }
   // ---- flatten lists: [levels][class 0]...[class n]
@@ -568,6 +598,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
             P->bin_blocks.ensure(sizeof(uint64_t) * std::max<size_t>(bin_blocks.size(), 1)) == hipSuccess &&
             P->bin_chunks.ensure(sizeof(uint64_t) * std::max<size_t>(bin_chunks.size(), 1)) == hipSuccess &&
             P->dba_chunks.ensure(sizeof(uint64_t) * std::max<size_t>(dba_chunks.size(), 1)) == hipSuccess &&
+            P->segs.ensure(sizeof(uint64_t) * std::max<size_t>(segs.size(), 1)) == hipSuccess &&
 
             P->rec.ensure(sizeof(uint64_t) * (rec_total + 16)) == hipSuccess &&  // k_dict_fill reads 9 ahead
             P->chunk_run.ensure(sizeof(uint32_t) * std::max<uint32_t>(chunk_total, 1)) == hipSuccess &&
@@ -599,6 +630,8 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     ok = ok && hipMemcpyAsync(P->bin_blocks.p, bin_blocks.data(), sizeof(uint64_t) * bin_blocks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   if (!bin_chunks.empty())
     ok = ok && hipMemcpyAsync(P->bin_chunks.p, bin_chunks.data(), sizeof(uint64_t) * bin_chunks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!segs.empty())
+    ok = ok && hipMemcpyAsync(P->segs.p, segs.data(), sizeof(uint64_t) * segs.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   if (!dba_chunks.empty())
     ok = ok && hipMemcpyAsync(P->dba_chunks.p, dba_chunks.data(), sizeof(uint64_t) * dba_chunks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   if (!chunk_list.empty())
@@ -619,7 +652,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   for (int k = 0; k < C_NCLS; k++) P->kernels += P->cls_n[(size_t)k] ? 1 : 0;
   P->kernels += (P->n_dict_walk ? 1 : 0) + (P->n_bind ? 1 : 0) + (P->n_fixd ? 1 : 0) + (P->n_bin_blocks ? 3 : 0) +
                 (P->n_bin_chunks ? 1 : 0) + (P->cls_n[C_DBA] ? (P->n_dba_chunks ? 4 : 1) : 0) +
-                (P->n_carry ? 1 : 0);
+                (P->n_carry ? 1 : 0) + (P->n_segs ? 1 : 0);
   *out = P;
   return PQG_OK;
 }
@@ -700,6 +733,12 @@ int pqg_plan_launch(pqg_plan* P) {
       case C_DELTA8: e = pqg::launch_delta(8, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
     }
   }
+  if (e == hipSuccess && P->n_segs) {  // PLAIN BYTE_ARRAY pages in segments (status + ticket cleared above)
+    uint8_t* scb = (uint8_t*)P->bscratch.p;
+    e = pqg::launch_bin_walk_seg(s, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->segs.p, P->n_segs,
+                                 (uint64_t*)(scb + P->seg_status_off), (uint32_t*)(scb + P->seg_status_off) + 2u * P->n_segs,
+                                 (uint32_t*)(scb + P->seg_tmp_off), err, ecount);
+  }
   // post-passes: dictionary ids -> BYTE_ARRAY entries / fixed-width entries; offsets; value bytes
   if (e == hipSuccess && P->n_bind) e = pqg::launch_bin_dict_map(s, work, cols, bl + P->off_bind, P->n_bind);
   if (e == hipSuccess && P->n_fixd)
@@ -741,6 +780,7 @@ int pqg_plan_destroy(pqg_plan* P) {
   P->bin_blocks.release();
   P->bin_chunks.release();
   P->dba_chunks.release();
+  P->segs.release();
   delete P;
   return PQG_OK;
 }
@@ -1217,28 +1257,38 @@ int pqg_assemble(pqg_ctx* ctx, const uint8_t* d_def_levels, const uint8_t* d_rep
   const uint32_t n_blocks = (uint32_t)((n_slots + 4095) / 4096);
   const size_t cnt_bytes = sizeof(uint64_t) * pqg::ASM_MAX_DEPTHS * (size_t)std::max<uint32_t>(n_blocks, 1);
   if (ctx->asm_scratch.ensure(cnt_bytes + 256) != hipSuccess || ctx->pin_err.ensure(256) != hipSuccess) return PQG_ERR_HIP;
-  uint64_t* counts = (uint64_t*)ctx->asm_scratch.p;
+  uint64_t* counts = (uint64_t*)ctx->asm_scratch.p;  // block counts (count pass) / look-back status words
   uint64_t* totals = (uint64_t*)((uint8_t*)ctx->asm_scratch.p + cnt_bytes);
+  uint32_t* ticket = (uint32_t*)(totals + pqg::ASM_MAX_DEPTHS);
   bool any_out = false, bounded = true;
   for (int k = 0; k < depth; k++) {
     any_out = any_out || P.validity[k] || P.offsets[k];
     // entries of any depth <= n_slots: outputs sized for that bound need no count round trip
     if ((P.validity[k] && path[k].capacity < n_slots) || (P.offsets[k] && path[k].capacity < n_slots + 1)) bounded = false;
   }
+  const uint8_t* dl = d > 0 ? d_def_levels : nullptr;
+  const uint8_t* rl = r > 0 ? d_rep_levels : nullptr;
+  // the single pass: status words, totals and the ticket zeroed, then one kernel (outputs + totals)
+  auto emit = [&]() -> hipError_t {
+    hipError_t e2 = hipMemsetAsync(ctx->asm_scratch.p, 0, cnt_bytes + sizeof(uint64_t) * pqg::ASM_MAX_DEPTHS + 16, s);
+    if (e2 == hipSuccess) e2 = pqg::launch_assemble(s, dl, rl, n_slots, P, counts, n_blocks, totals, ticket, 1);
+    if (e2 == hipSuccess && n_blocks == 0)  // no slots: closing offsets only (offsets[0] = 0)
+      for (int k = 0; k < depth && e2 == hipSuccess; k++)
+        if (P.kind[k] == PQG_REPEATED && P.offsets[k]) e2 = hipMemsetAsync(P.offsets[k], 0, sizeof(int64_t), s);
+    return e2;
+  };
   const bool one_pass = any_out && bounded;
-  hipError_t e = pqg::launch_assemble(s, d > 0 ? d_def_levels : nullptr, r > 0 ? d_rep_levels : nullptr, n_slots, P,
-                                      counts, n_blocks, totals, 0);
-  if (e == hipSuccess && one_pass) e = pqg::launch_assemble(s, d > 0 ? d_def_levels : nullptr, r > 0 ? d_rep_levels : nullptr,
-                                                            n_slots, P, counts, n_blocks, totals, 1);
+  hipError_t e = one_pass ? emit() : pqg::launch_assemble(s, dl, rl, n_slots, P, counts, n_blocks, totals, ticket, 0);
   uint64_t* h_tot = (uint64_t*)ctx->pin_err.p;
   if (e == hipSuccess) e = hipMemcpyAsync(h_tot, totals, sizeof(uint64_t) * pqg::ASM_MAX_DEPTHS, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess && one_pass && n_blocks == 0)  // no slots: closing offsets only (offsets[0] = 0)
-    for (int k = 0; k < depth && e == hipSuccess; k++)
-      if (P.kind[k] == PQG_REPEATED && P.offsets[k]) e = hipMemsetAsync(P.offsets[k], 0, sizeof(int64_t), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     set_status(st, PQG_ERR_HIP, -1, -1, hipGetErrorString(e));
     return PQG_ERR_HIP;
+  }
+  if (h_tot[pqg::ASM_MAX_DEPTHS - 1] == ~0ull) {  // a look-back wait timed out (k_asm_onepass)
+    set_status(st, PQG_ERR_TIMEOUT, -1, -1, "assembly look-back");
+    return PQG_ERR_TIMEOUT;
   }
   if (n_records) *n_records = h_tot[0];
   int bad = -1;
@@ -1254,11 +1304,7 @@ int pqg_assemble(pqg_ctx* ctx, const uint8_t* d_def_levels, const uint8_t* d_rep
     return PQG_ERR_INVALID_ARG;
   }
   if (!any_out || one_pass) return PQG_OK;  // counts only, or already emitted
-  e = pqg::launch_assemble(s, d > 0 ? d_def_levels : nullptr, r > 0 ? d_rep_levels : nullptr, n_slots, P, counts,
-                           n_blocks, totals, 1);
-  if (e == hipSuccess && n_blocks == 0)  // no slots: closing offsets only (offsets[0] = 0)
-    for (int k = 0; k < depth && e == hipSuccess; k++)
-      if (P.kind[k] == PQG_REPEATED && P.offsets[k]) e = hipMemsetAsync(P.offsets[k], 0, sizeof(int64_t), s);
+  e = emit();
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     set_status(st, PQG_ERR_HIP, -1, -1, hipGetErrorString(e));
@@ -1387,9 +1433,11 @@ int pqg_zstd_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, 
   if (!d_src || !d_dst || !d_jobs) return PQG_ERR_INVALID_ARG;
   if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
   // the scratch may be in use by a previous call still queued on the stream: grow only after it
-  if (ctx->zstd_scratch.cap < pqg::ZSTD_LIT_SCRATCH * (uint64_t)n_jobs) {
+  // one literal buffer per wave of the (bounded) grid, not per job
+  const uint64_t slots = (uint64_t)std::min<int>(n_jobs, (int)pqg::ZSTD_GRID);
+  if (ctx->zstd_scratch.cap < pqg::ZSTD_LIT_SCRATCH * slots) {
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) return PQG_ERR_HIP;
-    if (ctx->zstd_scratch.ensure(pqg::ZSTD_LIT_SCRATCH * (uint64_t)n_jobs) != hipSuccess) return PQG_ERR_HIP;
+    if (ctx->zstd_scratch.ensure(pqg::ZSTD_LIT_SCRATCH * slots) != hipSuccess) return PQG_ERR_HIP;
   }
   const hipError_t e = pqg::launch_zstd(ctx->stream, d_src, src_bytes, d_dst, dst_bytes, d_jobs, n_jobs, d_status,
                                         (uint8_t*)ctx->zstd_scratch.p);

@@ -47,6 +47,13 @@ __device__ __forceinline__ void asm_load16(const uint8_t* __restrict__ a, uint64
   }
 }
 
+__device__ __forceinline__ uint32_t bt_at(const uint32_t (&bt)[ASM_MAX_DEPTHS], uint32_t q) {
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t d = 0; d < ASM_MAX_DEPTHS; d++) v = d == q ? bt[d] : v;
+  return v;
+}
+
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[4], uint32_t j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu; }
 
 __global__ __launch_bounds__(256) void k_asm_count(const uint8_t* __restrict__ def, const uint8_t* __restrict__ rep,
@@ -106,20 +113,30 @@ __global__ __launch_bounds__(ASM_SCAN_THREADS) void k_asm_scan(uint64_t* __restr
   }
 }
 
-// Outputs of one block: per node, the block's entries are a contiguous range of the node's output
-// (entries are numbered in slot order), so every thread writes its entries' values into an LDS image
-// of the range and the workgroup stores the image with wide stores (validity bytes: dwords with byte
-// stores only at the ends shared with the neighbouring blocks; offsets: int64 pairs).
-__global__ __launch_bounds__(256) void k_asm_emit(const uint8_t* __restrict__ def, const uint8_t* __restrict__ rep,
-                                                  uint64_t n, AsmParams P, const uint64_t* __restrict__ block_counts,
-                                                  const uint64_t* __restrict__ totals) {
+// Single pass (outputs): the entry counts before a block come from a decoupled look-back over the
+// blocks before it instead of a separate count kernel and scan, so the levels are read once.
+// Block order is the order in which workgroups take a ticket (atomicAdd), so every block a
+// workgroup waits for is held by a running or finished workgroup: the look-back always ends.
+// status[b * ASM_MAX_DEPTHS + q] (zeroed before the launch): ASM_AGG | the block's entry count of
+// depth q, then ASM_INC | the inclusive count of blocks 0..b; written and read system-scope (the
+// blocks may run on different XCDs, whose L2s are not coherent), the value and its flag in one word.
+// Outputs: per node, the block's entries are a contiguous range of the node's output (entries are
+// numbered in slot order), so every thread writes its entries' values into an LDS image of the range
+// and the workgroup stores the image with wide stores (validity bytes: dwords with byte stores only at
+// the ends shared with the neighbouring blocks; offsets: int64 runs).
+constexpr uint64_t ASM_AGG = 1ull << 62, ASM_INC = 2ull << 62, ASM_VAL = (1ull << 62) - 1ull;
+
+__global__ __launch_bounds__(256) void k_asm_onepass(const uint8_t* __restrict__ def, const uint8_t* __restrict__ rep,
+                                                     uint64_t n, AsmParams P, uint64_t* status, uint32_t* ticket,
+                                                     uint64_t* __restrict__ totals, uint32_t n_blocks) {
   __shared__ uint32_t wsum[4][ASM_MAX_DEPTHS];
+  __shared__ uint64_t bc[ASM_MAX_DEPTHS];
+  __shared__ uint32_t blk_s;
   __shared__ uint64_t img[ASM_BLOCK];  // 32 KiB: one node's entries of this block
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // closing offsets: offsets[n_entries(r - 1)] = n_entries(r)
-    for (uint32_t k = 0; k < P.n_nodes; k++)
-      if (P.kind[k] == PQG_REPEATED && P.offsets[k]) gst(P.offsets[k] + totals[P.depth[k] - 1], (int64_t)totals[P.depth[k]]);
-  }
-  const uint64_t s0 = (uint64_t)blockIdx.x * ASM_BLOCK + (uint64_t)threadIdx.x * ASM_PER_THREAD;
+  if (threadIdx.x == 0) blk_s = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint32_t blk = blk_s;
+  const uint64_t s0 = (uint64_t)blk * ASM_BLOCK + (uint64_t)threadIdx.x * ASM_PER_THREAD;
   uint32_t dw[4], rw[4];
   asm_load16(def, s0, n, dw);
   asm_load16(rep, s0, n, rw);
@@ -147,7 +164,56 @@ __global__ __launch_bounds__(256) void k_asm_emit(const uint8_t* __restrict__ de
     li[q] += pre;
     bt[q] = wsum[0][q] + wsum[1][q] + wsum[2][q] + wsum[3][q];
   }
-  const uint64_t* bc = block_counts + (uint64_t)blockIdx.x * ASM_MAX_DEPTHS;
+  // publish this block's counts, then look back (wave 0): per depth, 64 predecessors per step, one
+  // lane each; the nearest one holding an inclusive count ends the look-back, the aggregates of those
+  // nearer are added (the decoupled look-back of a single-pass scan; a step is one round trip to
+  // memory for 64 blocks, where one predecessor per step made the block chain a serial walk)
+  if (threadIdx.x <= P.max_rep)
+    sst(status + (uint64_t)blk * ASM_MAX_DEPTHS + threadIdx.x, (blk == 0 ? ASM_INC : ASM_AGG) | (uint64_t)bt_at(bt, threadIdx.x));
+  if (threadIdx.x < WAVE) {
+    const uint32_t lane = lane_id();
+    for (uint32_t q = 0; q <= P.max_rep; q++) {
+      uint64_t excl = 0;
+      int64_t j0 = (int64_t)blk - 1;  // nearest predecessor of the current step
+      const uint64_t t_wait = __builtin_amdgcn_s_memrealtime();
+      while (j0 >= 0) {
+        const int64_t j = j0 - (int64_t)lane;
+        const uint64_t v = j >= 0 ? sld(status + (uint64_t)j * ASM_MAX_DEPTHS + q) : ASM_INC;
+        const uint64_t inc = __ballot((v & ASM_INC) != 0);
+        const uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : WAVE;  // nearest inclusive (lane)
+        const uint64_t upto = first == WAVE ? ~0ull : ((2ull << first) - 1ull);
+        if (__ballot(v == 0) & upto) {  // a block up to it has not published yet: read the window again
+          __builtin_amdgcn_s_sleep(1);
+          // bounded (2 s of s_memrealtime): a block that never publishes leaves a wrong count, not a hang
+          if (__builtin_amdgcn_s_memrealtime() - t_wait > 200000000ull) {
+            if (lane == 0) totals[ASM_MAX_DEPTHS - 1] = ~0ull;  // flagged to the host as a timeout
+            break;
+          }
+          continue;
+        }
+        uint64_t x = lane <= first || first == WAVE ? (v & ASM_VAL) : 0ull;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+        excl += x;
+        if (first < WAVE) break;
+        j0 -= WAVE;
+      }
+      if (lane == 0) {
+        const uint32_t agg = bt_at(bt, q);
+        if (blk > 0) sst(status + (uint64_t)blk * ASM_MAX_DEPTHS + q, ASM_INC | (excl + agg));
+        bc[q] = excl;
+        if (blk == n_blocks - 1u) totals[q] = excl + agg;
+      }
+    }
+  }
+  __syncthreads();
+  if (blk == n_blocks - 1u && threadIdx.x == 0) {  // closing offsets: offsets[n_entries(r - 1)] = n_entries(r)
+    for (uint32_t k = 0; k < P.n_nodes; k++)
+      if (P.kind[k] == PQG_REPEATED && P.offsets[k]) {
+        const uint32_t d = P.depth[k];
+        gst(P.offsets[k] + bc[d - 1] + bt_at(bt, d - 1), (int64_t)(bc[d] + bt_at(bt, d)));
+      }
+  }
   uint8_t* img8 = (uint8_t*)img;
   for (uint32_t k = 0; k < P.n_nodes; k++) {
     const uint32_t q = P.depth[k];
@@ -160,8 +226,9 @@ __global__ __launch_bounds__(256) void k_asm_emit(const uint8_t* __restrict__ de
       __syncthreads();
       // bytes [B, B + cnt) of validity[k]: aligned dwords inside, bytes at both ends
       uint8_t* g = P.validity[k] + bc[q];
-      const uint32_t cnt = bt[q];
-      const uint32_t head = (uint32_t)((4u - ((uintptr_t)g & 3u)) & 3u) < cnt ? (uint32_t)((4u - ((uintptr_t)g & 3u)) & 3u) : cnt;
+      const uint32_t cnt = bt_at(bt, q);
+      const uint32_t mis = (uint32_t)((4u - ((uintptr_t)g & 3u)) & 3u);
+      const uint32_t head = mis < cnt ? mis : cnt;
       const uint32_t nd = (cnt - head) >> 2;
       for (uint32_t i = threadIdx.x; i < nd; i += 256) {
         const uint32_t o = head + 4 * i;
@@ -184,7 +251,7 @@ __global__ __launch_bounds__(256) void k_asm_emit(const uint8_t* __restrict__ de
       }
       __syncthreads();
       int64_t* g = P.offsets[k] + bc[q - 1];
-      const uint32_t cnt = bt[q - 1];
+      const uint32_t cnt = bt_at(bt, q - 1);
       for (uint32_t i = threadIdx.x; i < cnt; i += 256) gst(g + i, (int64_t)img[i]);
       __syncthreads();
     }
@@ -192,12 +259,13 @@ __global__ __launch_bounds__(256) void k_asm_emit(const uint8_t* __restrict__ de
 }
 
 hipError_t launch_assemble(hipStream_t st, const uint8_t* def, const uint8_t* rep, uint64_t n, const AsmParams& P,
-                           uint64_t* block_counts, uint32_t n_blocks, uint64_t* totals, int phase) {
-  if (phase == 0) {
+                           uint64_t* block_counts, uint32_t n_blocks, uint64_t* totals, uint32_t* ticket, int phase) {
+  if (phase == 0) {  // entry counts only
     if (n_blocks) hipLaunchKernelGGL(k_asm_count, dim3(n_blocks), dim3(256), 0, st, def, rep, n, P, block_counts);
     hipLaunchKernelGGL(k_asm_scan, dim3(1), dim3(ASM_SCAN_THREADS), 0, st, block_counts, n_blocks, P, totals);
-  } else if (n_blocks) {
-    hipLaunchKernelGGL(k_asm_emit, dim3(n_blocks), dim3(256), 0, st, def, rep, n, P, block_counts, totals);
+  } else if (n_blocks) {  // outputs (and totals) in one pass; block_counts = zeroed status words, ticket = 0
+    hipLaunchKernelGGL(k_asm_onepass, dim3(n_blocks), dim3(256), 0, st, def, rep, n, P, block_counts, ticket, totals,
+                       n_blocks);
   }
   return hipGetLastError();
 }

@@ -165,8 +165,18 @@ __device__ __forceinline__ int bin_value_error(rsrc_t rs, uint32_t p, uint32_t e
 // and stored after it, once the next window's bytes have been requested: a load issued after
 // stores would wait for them (vmcnt counts stores), so every window costs one memory latency,
 // not two.
-__device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, uint32_t N, uint32_t* out_len,
-                         uint32_t* out_src, bool dict, int page, int kind, uint64_t* err, ErrCount err_count) {
+// Result of a walk: where the chain left it (the next value's position), the values produced, and
+// the error that stopped it (0: none).
+struct BinWalkEnd {
+  uint32_t pos, produced;
+  int code;
+};
+
+// The walk from `beg` until N values are produced, an error, or (stop, tile-aligned) the chain
+// reaches `stop`; values go to out_len / out_src [0, produced).
+__device__ __forceinline__ BinWalkEnd bin_walk_core(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, uint32_t N,
+                                                    uint32_t* out_len, uint32_t* out_src, bool dict,
+                                                    uint32_t stop = 0xFFFFFFFFu) {
   const uint32_t lane = lane_id();
   uint32_t pos = uni(beg), produced = 0;
   int code = 0;
@@ -180,7 +190,7 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
     pos = uni(pos);
     produced = uni(produced);
     B = uni(B);
-    if (produced >= N) break;
+    if (produced >= N || pos >= stop) break;
     if ((uint64_t)pos + 4u > end) { code = PQG_ERR_EOF; break; }
     // ---- candidates of the tile [B, B + BW_WIN) holding pos (its bytes are in cur_b)
     const uint32_t base = B + BW_Q * lane;
@@ -337,7 +347,13 @@ __device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg,
     if (code || !leave) break;
     wave_sync();  // the next window overwrites the list
   }
-  if (code && lane == 0) report(err, err_count, page, kind, produced, code);
+  return BinWalkEnd{uni(pos), uni(produced), code};
+}
+
+__device__ __forceinline__ void bin_walk(BinWalkLds& L, rsrc_t rs, uint32_t beg, uint32_t end, uint32_t N, uint32_t* out_len,
+                                         uint32_t* out_src, bool dict, int page, int kind, uint64_t* err, ErrCount err_count) {
+  const BinWalkEnd r = bin_walk_core(L, rs, beg, end, N, out_len, out_src, dict);
+  if (r.code && lane_id() == 0) report(err, err_count, page, kind, r.produced, r.code);
 }
 
 // One wave per page. dict_walk = 0: PLAIN BYTE_ARRAY data pages (values -> blen / bsrc at the
@@ -365,6 +381,134 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) v
   const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
   bin_walk(L, rs, uni(pw.data_begin), uni(pw.size), uni(pw.n_values), cd.blen + pw.out_offset,
            cd.bsrc + pw.out_offset, false, item, 2, err, err_count);
+}
+
+// ---- PLAIN BYTE_ARRAY pages walked in segments (plans with few such pages: one wave per page leaves
+// most of the chip idle while every page's chain is followed tile after tile).
+//
+// A page's data section is cut into SEG_B-byte segments (tile-aligned), one wave each, in the order
+// the waves take tickets (so a segment's predecessor is always held by a running or finished wave).
+// Segment 0 starts at the section start. Segment s > 0 guesses its first value start: the first
+// position of its first tile from which SEG_LINKS consecutive length prefixes each land on a
+// possible value start (a false start — e.g. the byte before a length prefix, read as a length —
+// jumps kilobytes ahead onto string bytes and is rejected within a link or two). Every segment walks
+// from its guess to the segment end with the page walk (bin_walk_core), writing its values to its
+// own scratch, then waits for its predecessor's publication {where the chain left it, values before
+// it}: if that position is not its guess (misspeculation, or no guess), it walks again from there.
+// It then publishes its own exit and count and moves its values to their place in the column. Only
+// the publication chain is serial (one round trip per segment); errors are reported only when they
+// fall inside the page's value count, at the index the one-wave walk would report.
+constexpr uint32_t SEG_B = 8 * BW_WIN;       // section bytes per segment
+constexpr uint32_t SEG_CAP = SEG_B / 4 + 2;  // values that can start in a segment (each takes >= 4 bytes)
+constexpr uint32_t SEG_LINKS = 6;
+constexpr uint64_t SG_OK = 1ull << 62, SG_STOP = 2ull << 62;
+static_assert(SEG_B == BW_SEG_BYTES && SEG_CAP == BW_SEG_CAP, "host segmentation (pqgpu_internal.h)");
+
+// a value could start at p: its 4 length bytes and its bytes inside the section
+__device__ __forceinline__ bool seg_candidate(rsrc_t rs, uint32_t p, uint32_t end) {
+  if ((uint64_t)p + 4u > end) return false;
+  return ld4_any(rs, p) <= end - 4u - p;
+}
+
+__device__ uint32_t seg_guess(rsrc_t rs, uint32_t S0, uint32_t end) {
+  const uint32_t lim = S0 + BW_WIN < end ? S0 + BW_WIN : end;
+  for (uint32_t b = S0; b < lim; b += WAVE) {
+    const uint32_t p = b + lane_id();
+    bool ok = p < lim && seg_candidate(rs, p, end);
+    uint32_t q = p;
+    for (uint32_t k = 0; k < SEG_LINKS && ok; k++) {
+      q = q + 4u + ld4_any(rs, q);
+      if (q >= end) break;  // the chain reaches the section end: nothing contradicts it
+      ok = seg_candidate(rs, q, end);
+    }
+    const uint64_t m = __ballot(ok);
+    if (m) return b + (uint32_t)__builtin_ctzll(m);
+  }
+  return 0xFFFFFFFFu;
+}
+
+__global__ __launch_bounds__(64 * WPB) void k_bin_walk_seg(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                           const PageWork* __restrict__ work,
+                                                           const ColumnDev* __restrict__ cols,
+                                                           const uint64_t* __restrict__ segs, uint32_t n_segs,
+                                                           uint64_t* status, uint32_t* ticket, uint32_t* tmp,
+                                                           uint64_t* err, ErrCount err_count) {
+  __shared__ BinWalkLds lds_all[WPB];
+  __shared__ uint32_t tk[WPB];
+  const uint32_t lane = lane_id();
+  if (lane == 0) tk[wave_id()] = atomicAdd(ticket, 1u);
+  wave_sync();
+  const uint32_t t = uni(tk[wave_id()]);
+  if (t >= n_segs) return;
+  BinWalkLds& L = lds_all[wave_id()];
+  const uint64_t sg = segs[t];
+  const int page = (int)(uint32_t)sg;
+  const uint32_t s = (uint32_t)(sg >> 32) & 0x7FFFFFFFu;
+  const bool last = (sg >> 63) != 0;
+  const PageWork& pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t beg = uni(pw.data_begin), end = uni(pw.size), N = uni(pw.n_values);
+  const uint32_t A0 = beg & ~(BW_WIN - 1u);
+  const uint64_t S0l = s == 0 ? beg : (uint64_t)A0 + (uint64_t)s * SEG_B;
+  const uint32_t S0 = S0l < end ? (uint32_t)S0l : end;
+  const uint32_t stop = last ? 0xFFFFFFFFu : (uint32_t)((uint64_t)A0 + (uint64_t)(s + 1) * SEG_B < end
+                                                             ? (uint64_t)A0 + (uint64_t)(s + 1) * SEG_B : end);
+  uint32_t* tl = tmp + (uint64_t)t * 2u * SEG_CAP;
+  uint32_t* ts = tl + SEG_CAP;
+  const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  const uint32_t guess = s == 0 ? beg : (S0 < end ? uni(seg_guess(rs, S0, end)) : 0xFFFFFFFFu);
+  BinWalkEnd r{guess, 0, 0};
+  if (guess != 0xFFFFFFFFu && N > 0) r = bin_walk_core(L, rs, guess, end, SEG_CAP, tl, ts, false, stop);
+  // the predecessor's publication: where the chain enters this segment, values before it
+  uint32_t entry = beg, before = 0;
+  bool stopped = N == 0;
+  if (s > 0) {
+    uint64_t v = 0;
+    const uint64_t t_wait = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      v = uni64(sld(status + t - 1));
+      if (v) break;
+      __builtin_amdgcn_s_sleep(2);
+      // bounded (s_memrealtime: 100 MHz): a predecessor that never publishes is PQG_ERR_TIMEOUT, not a hang
+      if (__builtin_amdgcn_s_memrealtime() - t_wait > 200000000ull) {
+        if (lane == 0) {
+          report(err, err_count, page, 2, 0, PQG_ERR_TIMEOUT);
+          sst(status + t, SG_STOP);
+        }
+        return;
+      }
+    }
+    if (v & SG_STOP) {
+      stopped = true;
+    } else {
+      entry = (uint32_t)(v >> 31) & 0x7FFFFFFFu;
+      before = (uint32_t)v & 0x7FFFFFFFu;
+    }
+  }
+  if (stopped || before >= N) {
+    if (lane == 0) sst(status + t, SG_STOP);
+    return;
+  }
+  if (s > 0 && guess != entry) {  // misspeculated (or no guess): the walk again from the true entry
+    wave_sync();
+    r = bin_walk_core(L, rs, entry, end, SEG_CAP, tl, ts, false, stop);
+  }
+  const uint32_t room = N - before;
+  const uint32_t take = r.produced < room ? r.produced : room;
+  bool done = r.produced >= room;
+  if (r.code && r.produced < room) {  // an error before the page's values are complete
+    if (lane == 0) report(err, err_count, page, 2, before + r.produced, r.code);
+    done = true;
+  }
+  if (lane == 0) sst(status + t, done ? SG_STOP : (SG_OK | ((uint64_t)(r.pos & 0x7FFFFFFFu) << 31) | (uint64_t)(before + r.produced)));
+  // this segment's values to their place: read back what this wave stored (completed first)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint32_t* out_len = cd.blen + pw.out_offset + before;
+  uint32_t* out_src = cd.bsrc + pw.out_offset + before;
+  for (uint32_t i = lane; i < take; i += WAVE) {
+    gst(out_len + i, sld(tl + i));
+    gst(out_src + i, sld(ts + i));
+  }
 }
 
 // RLE_DICTIONARY BYTE_ARRAY pages: ids (in blen, written by the dictionary kernel) -> entry
@@ -613,9 +757,9 @@ __device__ __forceinline__ void store_block16(uint8_t* dst, uint64_t a, uint64_t
 // range ends, which other waves share) is assembled and stored byte by byte.
 // DELTA_LENGTH_BYTE_ARRAY sources are the page's value bytes (PageWork::aux) + the in-page offset;
 // a value running past the page is the reference's "Failed to read N bytes" (EOF) at that value.
-constexpr uint32_t CP_VALUES = 512;            // values per workgroup chunk of k_bin_copy
+constexpr uint32_t CP_VALUES = CP_CHUNK_VALUES;  // values per workgroup chunk of k_bin_copy
 constexpr uint32_t CP_WAVE = CP_VALUES / WPB;  // values per wave on the per-wave path
-constexpr uint32_t CP_SRC = 24576;             // LDS bytes of staged source per workgroup
+constexpr uint32_t CP_SRC = 48u * CP_VALUES;     // LDS bytes of staged source per workgroup
 static_assert(CP_VALUES == CP_CHUNK_VALUES, "host chunking (pqgpu_internal.h)");
 
 struct CopyWaveLds {
@@ -882,9 +1026,12 @@ __device__ __forceinline__ void bin_copy_wave(const uint8_t* __restrict__ bytes,
 
 // LDS of one k_bin_copy workgroup: the chunk's value starts (relative to the chunk's first 16-byte
 // output block) and dictionary sources, and the staged source bytes; or the per-wave path's tables.
+constexpr uint32_t CP_BLOCKS = CP_SRC / 16 + 2;  // 16-byte output blocks of a staged chunk (output <= source)
 struct CopyWgLds {
   uint32_t rel[CP_VALUES + 1];
   uint32_t src[CP_VALUES];
+  uint16_t bt[CP_BLOCKS];         // output block -> the last value starting at or before its first byte
+  uint32_t wmax[WPB];
   uint32_t img[CP_SRC / 4 + 16];  // source bytes [Sa, Sa + CP_SRC) + slack for 9-dword reads
 };
 union CopyLds {
@@ -944,7 +1091,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
     s_hi = s_lo + (o_hi0 - o_lo) + (uint64_t)hole * (n - 1u);
   }
   const uint64_t Sa = s_lo & ~15ull;
-  const bool fit = o_hi0 - a0 < 0x7FFF0000ull && s_hi - Sa <= CP_SRC && s_lo <= slim;
+  const bool fit = o_hi0 - a0 < 0x7FFF0000ull && s_hi - Sa <= CP_SRC && s_lo <= slim && o_hi0 - a0 <= 16ull * (CP_BLOCKS - 1);
   if (!fit) {
     // per-wave path: wave w takes values [i_lo + CP_WAVE w, + CP_WAVE)
     const uint32_t w0 = i_lo + CP_WAVE * wave_id();
@@ -978,6 +1125,38 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
       const uint64_t avail = pw.size > pw.aux ? pw.size - pw.aux : 0;
       if (r + len > avail) report(err, err_count, page, 2, i_lo + k, PQG_ERR_EOF);
     }
+  const uint32_t nblk = (uint32_t)((o_hi0 - a0 + 15u) >> 4);
+  for (uint32_t i = t; i < nblk; i += 64u * WPB) L.bt[i] = 0;
+  __syncthreads();
+  // block table: value k enters at block ceil(rel / 16) (the last value entering a block writes it:
+  // one writer per block), then a running maximum over the blocks
+  for (uint32_t k = t; k < n; k += 64u * WPB) {
+    const uint32_t blk = (L.rel[k] + 15u) >> 4;
+    if (blk < nblk && (k + 1u == n || ((L.rel[k + 1] + 15u) >> 4) != blk)) L.bt[blk] = (uint16_t)k;
+  }
+  __syncthreads();
+  {
+    // running maximum over nblk entries: each thread a run of consecutive blocks, then the runs
+    const uint32_t per = (nblk + 64u * WPB - 1u) / (64u * WPB);
+    const uint32_t i0 = t * per, i1 = i0 + per < nblk ? i0 + per : nblk;
+    uint32_t mx = 0;
+    for (uint32_t i = i0; i < i1; i++) mx = L.bt[i] > mx ? L.bt[i] : mx;
+    uint32_t inc = mx;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if ((int)lane_id() >= o) inc = y > inc ? y : inc;
+    }
+    if (lane_id() == 63) L.wmax[wave_id()] = inc;
+    __syncthreads();
+    uint32_t run = (uint32_t)__shfl_up(inc, 1);
+    if (lane_id() == 0) run = 0;
+    for (uint32_t w = 0; w < wave_id(); w++) run = L.wmax[w] > run ? L.wmax[w] : run;
+    for (uint32_t i = i0; i < i1; i++) {
+      run = L.bt[i] > run ? L.bt[i] : run;
+      L.bt[i] = (uint16_t)run;
+    }
+  }
   __syncthreads();
   if (o_lo >= o_hi) return;
   uint8_t* dst = cd.binary_data;
@@ -987,14 +1166,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
   const uint32_t* img = L.img;
   const uint32_t* rel = L.rel;
   for (uint32_t b = 16u * t; b < r_hi; b += 16u * 64u * WPB) {
-    const uint32_t b0 = b > r_lo ? b : r_lo;
-    uint32_t lo = 0, hi = n;  // value of the block's first byte
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (rel[mid] <= b0) lo = mid;
-      else hi = mid;
-    }
-    const uint32_t kv = lo;
+    const uint32_t kv = L.bt[b >> 4];  // value of the block's first byte
     const uint32_t bend = b + 16u < r_hi ? b + 16u : r_hi;
     uint32_t wd[4];
     uint32_t have = 0;
@@ -1531,6 +1703,15 @@ hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_bin_walk, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, list, n,
                      dict_walk, n_pages, err, err_count);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin_walk_seg(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                               const ColumnDev* cols, const uint64_t* segs, uint32_t n_segs, uint64_t* status,
+                               uint32_t* ticket, uint32_t* tmp, uint64_t* err, ErrCount err_count) {
+  if (n_segs == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bin_walk_seg, dim3((n_segs + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols,
+                     segs, n_segs, status, ticket, tmp, err, err_count);
   return hipGetLastError();
 }
 

@@ -109,8 +109,10 @@ hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 // pqgpu_snappy.hip: one wave per raw Snappy block (jobs: pqg_snappy_job, device array)
-// ZSTD frames per job (pqgpu_zstd.hip); scratch = n_jobs x ZSTD_LIT_SCRATCH bytes of literal buffers
+// ZSTD frames per job (pqgpu_zstd.hip): a grid of at most ZSTD_GRID one-wave workgroups loops over
+// the jobs; scratch = min(n_jobs, ZSTD_GRID) x ZSTD_LIT_SCRATCH bytes of literal buffers (<= 512 MiB)
 constexpr uint64_t ZSTD_LIT_SCRATCH = 131072;
+constexpr uint32_t ZSTD_GRID = 4096;
 hipError_t launch_zstd(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
                        const pqg_snappy_job* jobs, int n_jobs, int32_t* status, uint8_t* scratch);
 hipError_t launch_snappy(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
@@ -132,13 +134,23 @@ hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
                            uint64_t* err, ErrCount err_count);
 // pqgpu_binary.hip
 constexpr uint32_t BIN_CHUNK = 256;     // values per DELTA_BYTE_ARRAY copy chunk
-constexpr uint32_t CP_CHUNK_VALUES = 512;  // values per k_bin_copy chunk (one workgroup)
+// values per k_bin_copy chunk (one workgroup); A/B on C3 / str_plain / str_dict / C4 (profiles/r03/copy_ab):
+// 512 beats 256 (C3 copy 3.65 vs 4.21 ms) and 1,024 (C3 5.73 ms, str_dict 0.80 vs 0.44 ms)
+constexpr uint32_t CP_CHUNK_VALUES = 512;
+// PLAIN BYTE_ARRAY pages walked in segments of BW_SEG_BYTES (k_bin_walk_seg) when a plan has fewer
+// than BW_SEG_MAX_PAGES such pages; BW_SEG_CAP values of scratch per segment (len + src)
+constexpr uint32_t BW_SEG_BYTES = 16384;
+constexpr uint32_t BW_SEG_CAP = BW_SEG_BYTES / 4 + 2;
+constexpr uint32_t BW_SEG_MAX_PAGES = 4096;
 constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block
 hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                       const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, int dict_walk, int n_pages,
                            uint64_t* err, ErrCount err_count);
+hipError_t launch_bin_walk_seg(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                               const ColumnDev* cols, const uint64_t* segs, uint32_t n_segs, uint64_t* status,
+                               uint32_t* ticket, uint32_t* tmp, uint64_t* err, ErrCount err_count);
 hipError_t launch_bin_dict_map(hipStream_t st, PageWork* work, const ColumnDev* cols, const int32_t* list, int n);
 hipError_t launch_gather_fixed(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n);
@@ -161,7 +173,7 @@ struct AsmParams {
   int64_t* offsets[ASM_MAX_NODES];
 };
 hipError_t launch_assemble(hipStream_t st, const uint8_t* def, const uint8_t* rep, uint64_t n, const AsmParams& P,
-                           uint64_t* block_counts, uint32_t n_blocks, uint64_t* totals, int phase);
+                           uint64_t* block_counts, uint32_t n_blocks, uint64_t* totals, uint32_t* ticket, int phase);
 hipError_t launch_unpack_runs(hipStream_t st, int w, const uint8_t* in, uint64_t in_bytes, const uint64_t* in_off,
                               const uint32_t* counts, const uint64_t* out_off, int32_t* out, int n_runs,
                               uint32_t max_count);

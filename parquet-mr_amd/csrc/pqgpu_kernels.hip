@@ -505,6 +505,9 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
   DictWaveLds& L = ((DictWaveLds*)lds)[wave_id()];
   const int i_page = (int)(group * WPB + wave_id());
   if (i_page >= n_list) return;
+#ifdef PQG_AB_PRIO
+  __builtin_amdgcn_s_setprio(3);
+#endif
   const int page = list[i_page];
 #ifdef PQG_DIAG
   const uint64_t rt_w0 = __builtin_amdgcn_s_memrealtime();
@@ -519,6 +522,9 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
   const uint32_t sh = (uint32_t)(pw.out_offset % (uint64_t)E);
   uint32_t n_rec = 0, n_ok = 0;
   (void)cd;
+#ifdef PQG_DIAG
+  uint64_t rt_w1 = 0, rt_w2 = 0;
+#endif
   if (N > 0) {
     PreWin win;
     win.rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
@@ -529,6 +535,9 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
     } else {
       seg_fill(win, sec_beg & ~15u);
       const uint32_t bw = wbyte(win, sec_beg);
+#ifdef PQG_DIAG
+      rt_w1 = __builtin_amdgcn_s_memrealtime() + (bw > 999u ? 1u : 0u);  // after the staging load
+#endif
       if (bw > 32u) {  // RunLengthBitPackingHybridDecoder ctor :55 (thrown at initFromPage)
         if (lane == 0) report(err, err_count, page, 0 /*init*/, 2, PQG_ERR_BIT_WIDTH);
       } else {
@@ -545,6 +554,9 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
   }
   // Publish (see handoff_release): every lane's record / chunk-entry stores, then lane 0's
   // status, then the flag.
+#ifdef PQG_DIAG
+  rt_w2 = __builtin_amdgcn_s_memrealtime() + (n_rec > 0xFFFFFFF0u ? 1u : 0u);
+#endif
   wave_sync();
   handoff_release();
   if (lane == 0) {
@@ -553,8 +565,10 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
     sst(flags + page, epoch);
 #ifdef PQG_DIAG
     if (pqg_diag_wrt) {
-      pqg_diag_wrt[2 * page] = rt_w0;
-      pqg_diag_wrt[2 * page + 1] = __builtin_amdgcn_s_memrealtime();
+      pqg_diag_wrt[4 * page] = rt_w0;
+      pqg_diag_wrt[4 * page + 1] = __builtin_amdgcn_s_memrealtime();
+      pqg_diag_wrt[4 * page + 2] = rt_w1;
+      pqg_diag_wrt[4 * page + 3] = rt_w2;
     }
 #endif
   }

@@ -26,6 +26,10 @@ constexpr uint32_t ZS_RING = 4096;    // LDS mirror of the most recent output
 constexpr uint32_t ZS_WIN = 1024;     // LDS window of the sequence bitstream
 constexpr uint32_t ZS_HWIN = 256;     // LDS window per Huffman stream
 constexpr uint32_t ZS_LIT_MAX = 131072;
+constexpr uint32_t ZS_SB = 64;        // sequences per execution batch (lane k: sequence k)
+constexpr uint32_t ZS_CAP = 512;      // output bytes per execution batch
+constexpr uint32_t ZS_LIT = 0x80000000u;  // byte source tag: a literal of the batch (| its index)
+constexpr uint32_t ZS_FLUSH = 1024;   // ring bytes written to HBM once this many are pending
 
 struct ZWaveLds {
   uint32_t ll[512], ml[512], of[256];  // FSE decoding entries: sym | nb << 8 | base << 16
@@ -38,7 +42,30 @@ struct ZWaveLds {
   uint8_t wts[256];
   uint16_t nxt[256];
   uint32_t flag;
+  uint32_t sq_ll[ZS_SB + 1], sq_ml[ZS_SB + 1], sq_of[ZS_SB + 1];  // decoded sequences of one batch (+ the carried one)
+  uint32_t src[ZS_CAP];               // batch output byte -> literal index (| ZS_LIT) or output position
+  uint8_t lseg[ZS_CAP + 16];          // the batch's literal bytes
+  uint32_t llcode[36], mlcode[53];     // literal / match length codes: baseline | extra bits << 24
+#ifdef PQG_DIAG
+  uint64_t diag[8];                   // diagnostic build: cycles per phase of the current job
+#endif
 };
+
+#ifdef PQG_DIAG
+// Diagnostic build only (tools/diag_zstd.py): per job 8 u64 = cycles in literals (Huffman), sequence
+// tables, sequence decode, batch execution, long sequences, whole job; sequences; literal bytes.
+static __device__ uint64_t* pqg_zdiag;
+extern "C" int pqg_diag_zstd_set(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(pqg_zdiag), &p, sizeof(p)) == hipSuccess ? 0 : 3;
+}
+#define ZD_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define ZD_ADD(L, i, t0) ((L).diag[i] += __builtin_amdgcn_s_memtime() - (t0))
+#define ZD_CNT(L, i, n) ((L).diag[i] += (n))
+#else
+#define ZD_T(v)
+#define ZD_ADD(L, i, t0)
+#define ZD_CNT(L, i, n)
+#endif
 
 __constant__ int16_t ZLL_DEF[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
 __constant__ int16_t ZML_DEF[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
@@ -84,16 +111,23 @@ struct FwdBits {
   }
 };
 
-// Backward bitstream (RFC 8878 §4.1) whose bytes [0, n) start at input offset `base`; read through
-// an LDS window (wave-uniform use: the whole wave refills it).
+// Backward bitstream (RFC 8878 §4.1) whose bytes [0, n) start at input offset `base` (wave-uniform).
+// Reads come from a 64-bit register container holding stream bits [cbit, cbit + 64), refilled with 8
+// bytes from an LDS window of the stream (the whole wave refills the window): most reads are a
+// shift and a mask, where reading every field from LDS put an LDS round trip on the sequence
+// decoder's serial chain per field (6 per sequence).
 struct BackBits {
   rsrc_t rs;
   uint32_t base, n;
   int64_t bits;      // unread bits
   uint32_t wlo;      // window covers stream bytes [wlo, wlo + ZS_WIN)
   uint8_t* win;
+  uint64_t c;        // container: stream bits [cbit, cbit + 64)
+  int64_t cbit;
   __device__ bool init(rsrc_t r, uint32_t b, uint32_t len, uint8_t* w) {
     rs = r; base = b; n = len; win = w; wlo = 0xFFFFFFFFu;
+    cbit = INT64_MAX;
+    c = 0;
     if (len == 0) return false;
     const uint32_t last = zbyte(rs, base + len - 1);
     if (!last) return false;
@@ -108,6 +142,20 @@ struct BackBits {
                                ld4_any(rs, base + lo + o + 8), ld4_any(rs, base + lo + o + 12)};
     wave_sync();
   }
+  // container for reads ending at bit `end` (exclusive): bits [ceil8(end) - 64, ceil8(end)), from 0
+  __device__ void fill(int64_t end) {
+    const int64_t e8 = (end + 7) & ~7ll;
+    cbit = e8 > 64 ? e8 - 64 : 0;
+    const uint32_t b0 = (uint32_t)(cbit >> 3), b1 = b0 + 8u < n ? b0 + 8u : n;  // bytes [b0, b1)
+    if (wlo == 0xFFFFFFFFu || b0 < wlo || b1 > wlo + ZS_WIN) refill(b1 + 8u < n ? b1 + 8u : n);
+    typedef uint32_t __attribute__((may_alias)) u32a;
+    const uint32_t rel = b0 - wlo, r4 = rel & ~3u, sft = rel & 3u;
+    const uint32_t d0 = *(const u32a*)(win + r4), d1 = *(const u32a*)(win + r4 + 4), d2 = *(const u32a*)(win + r4 + 8);
+    uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sft) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sft) << 32);
+    const uint32_t nb = b1 - b0;  // bytes past the stream's end read as 0
+    if (nb < 8u) v &= (1ull << (8u * nb)) - 1ull;
+    c = uni64(v);
+  }
   // k <= 32 bits; bits below the stream start read as 0 (overflow: bits < 0 afterwards)
   __device__ uint32_t read(int k) {
     if (k == 0) return 0;
@@ -117,25 +165,21 @@ struct BackBits {
     if (a < 0) { sh = (int)-a; a = 0; }
     const int kk = k - sh;
     if (kk <= 0) return 0;
-    const uint32_t b0 = (uint32_t)(a >> 3), b1 = (uint32_t)((a + kk + 7) >> 3);  // bytes [b0, b1)
-    if (wlo == 0xFFFFFFFFu || b0 < wlo || b1 > wlo + ZS_WIN) refill(b1 < n ? b1 : n);
-    uint64_t w = 0;
-    const uint32_t rel = b0 - wlo;
-    typedef uint32_t __attribute__((may_alias)) u32a;
-    const uint32_t r4 = rel & ~3u;
-    const uint32_t d0 = *(const u32a*)(win + r4), d1 = *(const u32a*)(win + r4 + 4), d2 = *(const u32a*)(win + r4 + 8);
-    const uint32_t s = rel & 3u;
-    w = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
-    const uint32_t v = (uint32_t)((w >> (a & 7)) & ((1ull << kk) - 1ull));
+    if (a < cbit || a + kk > cbit + 64) fill(a + kk);
+    const uint32_t v = (uint32_t)((c >> (uint32_t)(a - cbit)) & ((1ull << kk) - 1ull));
     return v << sh;
   }
 };
 
-// Per-lane backward bitstream for one Huffman stream, its own LDS window (lane-private use).
+// Per-lane backward bitstream for one Huffman stream: its own LDS window (lane-private use) and a
+// 64-bit register container of stream bits [cbit, cbit + 64), so a symbol costs one LDS access (its
+// decoding entry) instead of two dependent ones.
 struct LaneBits {
   uint32_t base, n, wlo;
   int64_t bits;
   uint8_t* win;
+  uint64_t c;
+  int64_t cbit;
   __device__ void refill(rsrc_t rs, uint32_t need_end) {
     const uint32_t lo = need_end > ZS_HWIN ? need_end - ZS_HWIN : 0;
     wlo = lo;
@@ -143,20 +187,27 @@ struct LaneBits {
       *(u32x4*)(win + o) = u32x4{ld4_any(rs, base + lo + o), ld4_any(rs, base + lo + o + 4),
                                  ld4_any(rs, base + lo + o + 8), ld4_any(rs, base + lo + o + 12)};
   }
+  __device__ void fill(rsrc_t rs, int64_t end) {
+    const int64_t e8 = (end + 7) & ~7ll;
+    cbit = e8 > 64 ? e8 - 64 : 0;
+    const uint32_t b0 = (uint32_t)(cbit >> 3), b1 = b0 + 8u < n ? b0 + 8u : n;
+    if (wlo == 0xFFFFFFFFu || b0 < wlo || b1 > wlo + ZS_HWIN) refill(rs, b1 + 8u < n ? b1 + 8u : n);
+    typedef uint32_t __attribute__((may_alias)) u32a;
+    const uint32_t rel = b0 - wlo, r4 = rel & ~3u, sft = rel & 3u;
+    const uint32_t d0 = *(const u32a*)(win + r4), d1 = *(const u32a*)(win + r4 + 4), d2 = *(const u32a*)(win + r4 + 8);
+    uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sft) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sft) << 32);
+    const uint32_t nb = b1 - b0;
+    if (nb < 8u) v &= (1ull << (8u * nb)) - 1ull;
+    c = v;
+  }
   __device__ uint32_t peek(rsrc_t rs, int k) {  // the next k bits without consuming (zeros past the start)
     int64_t a = bits - k;
     int sh = 0;
     if (a < 0) { sh = (int)-a; a = 0; }
     const int kk = k - sh;
     if (kk <= 0) return 0;
-    const uint32_t b0 = (uint32_t)(a >> 3), b1 = (uint32_t)((a + kk + 7) >> 3);
-    if (wlo == 0xFFFFFFFFu || b0 < wlo || b1 > wlo + ZS_HWIN) refill(rs, b1 < n ? b1 : n);
-    const uint32_t rel = b0 - wlo;
-    typedef uint32_t __attribute__((may_alias)) u32a;
-    const uint32_t r4 = rel & ~3u, s = rel & 3u;
-    const uint32_t d0 = *(const u32a*)(win + r4), d1 = *(const u32a*)(win + r4 + 4);
-    const uint32_t w = __builtin_amdgcn_alignbyte(d1, d0, s);
-    return ((w >> (a & 7)) & ((1u << kk) - 1u)) << sh;
+    if (a < cbit || a + kk > cbit + 64) fill(rs, a + kk);
+    return (uint32_t)((c >> (uint32_t)(a - cbit)) & ((1ull << kk) - 1ull)) << sh;
   }
 };
 
@@ -351,14 +402,48 @@ __device__ int zhuf_tree(ZWaveLds& L, rsrc_t rs, uint32_t& q, uint32_t lim) {
 struct ZOut {
   uint8_t* dst;
   uint32_t cap;        // job's output size: bytes past it are dropped (the page reader stops there)
-  uint32_t pos;        // bytes produced
+  uint32_t pos;        // bytes produced (the newest ZS_RING of them are in the LDS ring)
   uint32_t frame0;     // output position of the current frame's start
   uint32_t drained;    // every store below this position has completed
+  uint32_t flushed;    // output below this position has been stored from the ring to HBM
 };
 
+// Output bytes are produced into the LDS ring and stored to HBM from there ZS_FLUSH bytes at a time,
+// as dwords aligned to the destination (byte stores only at the ends): one store instruction moves
+// 256 bytes, where a byte store per output byte moved at most 64 (and usually 8: one match).
 __device__ __forceinline__ void zput(ZOut& O, ZWaveLds& L, uint32_t p, uint32_t v) {
+  (void)O;
   L.ring[p & (ZS_RING - 1u)] = (uint8_t)v;
-  if (p < O.cap) gst(O.dst + p, (uint8_t)v);
+}
+
+__device__ __forceinline__ void zflush(ZOut& O, ZWaveLds& L) {
+  const uint32_t a = O.flushed, e = O.pos < O.cap ? O.pos : O.cap;
+  O.flushed = O.pos;
+  if (a >= e) return;
+  typedef uint32_t __attribute__((may_alias)) u32a;
+  const u32a* ring32 = (const u32a*)L.ring;
+  const uint32_t oal = (uint32_t)(uintptr_t)O.dst & 3u;
+  const uint32_t base = ((a + oal) & ~3u) - oal;  // dst + base is dword aligned (base <= a, may wrap)
+  const uint32_t skip = a - base, span = e - base;
+  for (uint32_t d0 = 0; d0 < span; d0 += 4u * WAVE) {
+    const uint32_t d = d0 + 4u * lane_id();
+    if (d < span) {
+      const uint32_t t = base + d, r = t & (ZS_RING - 1u) & ~3u;
+      const uint32_t v = __builtin_amdgcn_alignbyte(ring32[((r + 4u) & (ZS_RING - 1u)) >> 2], ring32[r >> 2], t & 3u);
+      if (d >= skip && d + 4u <= span) {
+        gst((uint32_t*)(O.dst + t), v);
+      } else {
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; j++)
+          if (d + j >= skip && d + j < span) gst(O.dst + (t + j), (uint8_t)(v >> (8u * j)));
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void zmaybe_flush(ZOut& O, ZWaveLds& L) {
+  wave_sync();
+  if (O.pos - O.flushed >= ZS_FLUSH) zflush(O, L);
 }
 
 // output byte q (< pos): from the ring when recent, else from memory (system-scope load after a
@@ -370,52 +455,139 @@ __device__ __forceinline__ uint32_t zget(const ZOut& O, const ZWaveLds& L, uint3
   return (w >> ((q & 3u) * 8u)) & 0xFFu;
 }
 
-__device__ __forceinline__ void zdrain(ZOut& O) {
+// every output byte produced so far stored and complete in HBM
+__device__ __forceinline__ void zdrain(ZOut& O, ZWaveLds& L) {
+  zflush(O, L);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   O.drained = O.pos;
 }
 
-// copy n literal bytes: from the input (raw literals), a single byte (RLE) or the literal buffer
-__device__ void zcopy_lits(ZOut& O, ZWaveLds& L, int kind, rsrc_t rs, uint32_t src, const uint8_t* litbuf,
+// literal byte k of the block's literals: from the input at src + k (raw), the single byte `src`
+// (RLE) or the literal buffer at src + k (Huffman-decoded)
+__device__ __forceinline__ uint32_t zlit(int kind, rsrc_t rs, uint32_t src, const uint8_t* litbuf, uint32_t k) {
+  if (kind == 0) return zbyte(rs, src + k);
+  if (kind == 1) return src;
+  const uint32_t a = src + k;
+  return (zld((const uint32_t*)(litbuf + (a & ~3u))) >> ((a & 3u) * 8u)) & 0xFFu;
+}
+
+// copy n literal bytes (see zlit) to the output, 64 per round through the ring
+__device__ __forceinline__ void zcopy_lits(ZOut& O, ZWaveLds& L, int kind, rsrc_t rs, uint32_t src, const uint8_t* litbuf,
                            uint32_t n) {
+  const uint32_t p0 = O.pos;
   for (uint32_t k0 = 0; k0 < n; k0 += WAVE) {
     const uint32_t k = k0 + lane_id();
-    if (k < n) {
-      uint32_t v;
-      if (kind == 0) v = zbyte(rs, src + k);
-      else if (kind == 1) v = src;
-      else v = (zld((const uint32_t*)(litbuf + ((src + k) & ~3u))) >> (((src + k) & 3u) * 8u)) & 0xFFu;
-      zput(O, L, O.pos + k, v);
+    if (k < n) zput(O, L, p0 + k, zlit(kind, rs, src, litbuf, k));
+    wave_sync();
+    const uint32_t done = p0 + (k0 + WAVE < n ? k0 + WAVE : n);
+    if (done - O.flushed >= ZS_FLUSH) {  // keep the unflushed part well inside the ring
+      O.pos = done;
+      zflush(O, L);
     }
   }
-  O.pos += n;
-  wave_sync();
-  if (O.pos - O.drained >= 2048u) zdrain(O);
+  O.pos = p0 + n;
+  zmaybe_flush(O, L);
 }
 
 // match: n bytes from `off` back; in rounds of min(off, 64) so a round only reads finished bytes
-__device__ void zcopy_match(ZOut& O, ZWaveLds& L, uint32_t off, uint32_t n) {
+__device__ __forceinline__ void zcopy_match(ZOut& O, ZWaveLds& L, uint32_t off, uint32_t n) {
   const uint32_t step = off < WAVE ? off : WAVE;
+  const uint32_t p0 = O.pos;
   for (uint32_t k0 = 0; k0 < n; k0 += step) {
-    const uint32_t cur = O.pos + k0;
+    const uint32_t cur = p0 + k0;
     // a far match reads memory: every byte this round reads must have been stored
     if (off > ZS_RING - WAVE && cur + step - off > O.drained) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      O.drained = cur;
+      O.pos = cur;
+      zdrain(O, L);
     }
     const uint32_t k = k0 + lane_id();
-    if (lane_id() < step && k < n) {
-      const uint32_t q = O.pos + k - off;
-      zput(O, L, O.pos + k, zget(O, L, q, O.pos + k0));
-    }
+    if (lane_id() < step && k < n) zput(O, L, p0 + k, zget(O, L, p0 + k - off, cur));
     wave_sync();
+    if (cur + step - O.flushed >= ZS_FLUSH) {  // keep the unflushed part well inside the ring
+      O.pos = k0 + step < n ? cur + step : p0 + n;
+      zflush(O, L);
+    }
   }
-  O.pos += n;
-  if (O.pos - O.drained >= 2048u) zdrain(O);
+  O.pos = p0 + n;
+  zmaybe_flush(O, L);
+}
+
+// One batch of m decoded sequences (L.sq_*, lane k: sequence k) producing T <= ZS_CAP bytes: every
+// output byte gets its source (a literal of the batch, or the output position it copies), pointer
+// jumping follows in-batch copies of copies until every source is a literal or lies before the
+// batch, then the bytes are gathered from the literal segment / the ring / HBM (older than the
+// ring) at once. Sequences are dependent chains (a match of 8 bytes at offset 8 after 2 literals,
+// again and again, in int64 data): they resolve in log2(depth) rounds instead of one at a time.
+__device__ void zexec_batch(ZOut& O, ZWaveLds& L, uint32_t m, int lit_kind, rsrc_t rs, uint32_t lit_src,
+                            const uint8_t* litbuf, uint32_t lit_pos) {
+  const uint32_t lane = lane_id();
+  const uint32_t ll = lane < m ? L.sq_ll[lane] : 0u, ml = lane < m ? L.sq_ml[lane] : 0u, of = lane < m ? L.sq_of[lane] : 0u;
+  uint32_t T, LT;
+  const uint32_t ob = wave_excl_scan_u32(ll + ml, &T);
+  const uint32_t lb = wave_excl_scan_u32(ll, &LT);
+  T = uni(T);
+  LT = uni(LT);
+  // the batch's literals [lit_pos, lit_pos + LT)
+  for (uint32_t i = lane; i < LT; i += WAVE)
+    L.lseg[i] = (uint8_t)zlit(lit_kind, rs, lit_src, litbuf, lit_pos + i);
+  const uint32_t op = O.pos;
+  for (uint32_t i = 0; i < ll; i++) L.src[ob + i] = ZS_LIT | (lb + i);
+  for (uint32_t i = 0; i < ml; i++) L.src[ob + ll + i] = op + ob + ll + i - of;
+  wave_sync();
+  constexpr uint32_t NB = ZS_CAP / WAVE;
+  uint32_t sv[NB];
+#pragma unroll
+  for (uint32_t j = 0; j < NB; j++) {
+    const uint32_t b = lane + WAVE * j;
+    sv[j] = b < T ? L.src[b] : ZS_LIT;
+  }
+#pragma unroll 1
+  for (uint32_t r = 0; r < 12u; r++) {  // branch-free rounds (the index is clamped to the table)
+    bool more = false, hop = false;
+#pragma unroll
+    for (uint32_t j = 0; j < NB; j++) {
+      const bool inb = !(sv[j] & ZS_LIT) && sv[j] >= op;
+      const uint32_t nv = L.src[(sv[j] - op) & (ZS_CAP - 1u)];
+      sv[j] = inb ? nv : sv[j];
+      hop |= inb;
+      more |= inb && !(nv & ZS_LIT) && nv >= op;
+    }
+    if (!__ballot(hop)) break;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t j = 0; j < NB; j++) L.src[lane + WAVE * j] = sv[j];  // entries >= T hold ZS_LIT
+    wave_sync();
+    if (!__ballot(more)) break;
+  }
+  // bytes: literals from the segment, earlier output from the ring or, older, from HBM
+  uint32_t bv[NB];
+  bool far = false;
+#pragma unroll
+  for (uint32_t j = 0; j < NB; j++) {
+    const uint32_t v = sv[j];
+    bv[j] = (v & ZS_LIT) ? L.lseg[v & (ZS_CAP - 1u)] : L.ring[v & (ZS_RING - 1u)];
+    far |= lane + WAVE * j < T && !(v & ZS_LIT) && v + ZS_RING < op + WAVE;
+  }
+  if (__ballot(far)) {
+    zdrain(O, L);
+#pragma unroll
+    for (uint32_t j = 0; j < NB; j++) {
+      const uint32_t v = sv[j];
+      if (lane + WAVE * j < T && !(v & ZS_LIT) && v + ZS_RING < op + WAVE) bv[j] = zget(O, L, v, 0xFFFFFFFFu);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (uint32_t j = 0; j < NB; j++) {
+    const uint32_t b = lane + WAVE * j;
+    if (b < T) L.ring[(op + b) & (ZS_RING - 1u)] = (uint8_t)bv[j];
+  }
+  O.pos = op + T;
+  zmaybe_flush(O, L);
 }
 
 // One compressed block [q, q + bs) of the job's input. Returns 0 or an error code.
-__device__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t q, uint32_t bs, uint8_t* litbuf, bool& have_huf,
+__device__ __forceinline__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t q, uint32_t bs, uint8_t* litbuf, bool& have_huf,
                       int& huf_bits, bool* have_tab, int* tlog, uint32_t* rep) {
   const uint32_t lim = q + bs;
   if (bs < 1) return PQG_ERR_CORRUPT;
@@ -434,6 +606,7 @@ __device__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t q, uint32_t bs, 
   }
   if (q + hl > lim || regen > ZS_LIT_MAX) return PQG_ERR_CORRUPT;
   uint32_t p = q + hl;
+  ZD_T(t_lit);
   int lit_kind;          // 0 raw (input at lit_src), 1 RLE (byte lit_src), 2 decoded into litbuf
   uint32_t lit_src = 0;
   if (lt == 0) {
@@ -479,7 +652,7 @@ __device__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t q, uint32_t bs, 
 #pragma unroll
       for (int i = 0; i < 4; i++)
         if ((int)lane == i) { mb = sb[i]; mn = sn[i]; mc = cnt[i]; md = dst0[i]; }
-      LaneBits lb{mb, mn, 0xFFFFFFFFu, 0, L.hwin[lane]};
+      LaneBits lb{mb, mn, 0xFFFFFFFFu, 0, L.hwin[lane], 0, INT64_MAX};
       const uint32_t last = mn ? zbyte(rs, mb + mn - 1) : 0u;
       if (!last) {
         bad = 1;
@@ -493,7 +666,11 @@ __device__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t q, uint32_t bs, 
           const uint32_t o = md + i;
           acc |= (e & 0xFFu) << ((o & 3u) * 8u);
           if ((o & 3u) == 3u || i + 1 == mc) {  // flush a (partial) dword: byte stores keep neighbours
-            for (uint32_t j = (o & ~3u) > md ? (o & ~3u) : md; j <= o; j++) gst(litbuf + j, (uint8_t)(acc >> ((j & 3u) * 8u)));
+            if ((o & 3u) == 3u && (o & ~3u) >= md) {
+              gst((uint32_t*)(litbuf + (o & ~3u)), acc);  // a whole dword of this stream
+            } else {
+              for (uint32_t j = (o & ~3u) > md ? (o & ~3u) : md; j <= o; j++) gst(litbuf + j, (uint8_t)(acc >> ((j & 3u) * 8u)));
+            }
             acc = 0;
           }
         }
@@ -505,6 +682,8 @@ __device__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t q, uint32_t bs, 
     lit_kind = 2;
     p += comp;
   }
+  ZD_ADD(L, 0, t_lit);
+  ZD_CNT(L, 7, regen);
   // ---- sequences
   if (p >= lim) return PQG_ERR_CORRUPT;
   uint32_t nseq = zbyte(rs, p);
@@ -517,6 +696,7 @@ __device__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t q, uint32_t bs, 
   else if (nseq < 255) { nseq = ((nseq - 128) << 8) + zbyte(rs, p + 1); p += 2; }
   else { nseq = zbyte(rs, p + 1) + (zbyte(rs, p + 2) << 8) + 0x7F00u; p += 3; }
   if (p >= lim) return PQG_ERR_CORRUPT;
+  ZD_T(t_tab);
   const uint32_t modes = zbyte(rs, p++);
   if (modes & 3u) return PQG_ERR_CORRUPT;
   if (!zseq_table(L, L.ll, &tlog[0], have_tab[0], (int)(modes >> 6), rs, p, lim, ZLL_DEF, 36, 6, 9, 35)) return PQG_ERR_CORRUPT;
@@ -525,14 +705,35 @@ __device__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t q, uint32_t bs, 
   BackBits b;
   if (!b.init(rs, p, lim - p, L.win)) return PQG_ERR_CORRUPT;
   uint32_t sl = b.read(tlog[0]), so = b.read(tlog[1]), sm = b.read(tlog[2]);
-  uint32_t lit_pos = 0;
+  ZD_ADD(L, 1, t_tab);
+  ZD_CNT(L, 6, nseq);
+  ZD_T(t_seq);
+  // Sequences are decoded one after another (the three FSE states and the backward bitstream are
+  // serial), up to ZS_SB of them and ZS_CAP output bytes into LDS, and executed as a batch
+  // (zexec_batch); a sequence longer than ZS_CAP runs on its own through the ring.
+  uint32_t lit_pos = 0;     // literals consumed by executed batches
+  uint32_t m = 0, T = 0;    // sequences / output bytes of the pending batch
+  uint32_t blit = 0;        // literals of the pending batch
+  uint32_t outp = O.pos;    // output position after the pending batch
+  auto run_batch = [&]() {
+    if (m == 0) return;
+    wave_sync();
+    ZD_T(t_ex);
+    zexec_batch(O, L, m, lit_kind, rs, lit_src, litbuf, lit_pos);
+    ZD_ADD(L, 3, t_ex);
+    lit_pos += blit;
+    m = 0; T = 0; blit = 0;
+  };
   for (uint32_t i = 0; i < nseq; i++) {
     const uint32_t el = L.ll[sl], eo = L.of[so], em = L.ml[sm];
     const uint32_t llc = el & 0xFFu, ofc = eo & 0xFFu, mlc = em & 0xFFu;
     if (llc > 35 || mlc > 52 || ofc > 31) return PQG_ERR_CORRUPT;
-    const uint64_t ofv = (1ull << ofc) + (ofc ? b.read((int)ofc) : 0u);
-    const uint32_t ml = ZML_BASE[mlc] + (ZML_BITS[mlc] ? b.read(ZML_BITS[mlc]) : 0u);
-    const uint32_t ll = ZLL_BASE[llc] + (ZLL_BITS[llc] ? b.read(ZLL_BITS[llc]) : 0u);
+    // length codes from LDS: an indexed __constant__ table is a vector memory load here, and its
+    // vmcnt wait also waited for every output store in flight, once per sequence
+    const uint32_t mle = L.mlcode[mlc], lle = L.llcode[llc];
+    const uint64_t ofv = (1ull << ofc) + b.read((int)ofc);
+    const uint32_t ml = (mle & 0xFFFFFFu) + b.read((int)(mle >> 24));
+    const uint32_t ll = (lle & 0xFFFFFFu) + b.read((int)(lle >> 24));
     uint32_t off;
     if (ofv > 3) {
       off = (uint32_t)(ofv - 3);
@@ -558,12 +759,31 @@ __device__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t q, uint32_t bs, 
       sm = (em >> 16) + b.read((int)((em >> 8) & 0xFFu));
       so = (eo >> 16) + b.read((int)((eo >> 8) & 0xFFu));
     }
-    if (b.bits < 0 || lit_pos + ll > regen) return PQG_ERR_CORRUPT;
-    if (ll) zcopy_lits(O, L, lit_kind, rs, lit_kind == 1 ? lit_src : lit_src + lit_pos, litbuf, ll);
-    lit_pos += ll;
-    if (off == 0 || off > O.pos - O.frame0) return PQG_ERR_CORRUPT;
-    zcopy_match(O, L, off, ml);
+    if (b.bits < 0 || lit_pos + blit + ll > regen) return PQG_ERR_CORRUPT;
+    if (off == 0 || off > outp + ll - O.frame0) return PQG_ERR_CORRUPT;
+    if ((uint64_t)ll + ml > ZS_CAP) {  // a long sequence: the batch before it, then itself through the ring
+      run_batch();
+      ZD_T(t_long);
+      if (ll) zcopy_lits(O, L, lit_kind, rs, lit_kind == 1 ? lit_src : lit_src + lit_pos, litbuf, ll);
+      lit_pos += ll;
+      zcopy_match(O, L, off, ml);
+      ZD_ADD(L, 4, t_long);
+      outp = O.pos;
+      continue;
+    }
+    if (T + ll + ml > ZS_CAP || m == ZS_SB) run_batch();
+    if (lane_id() == 0) {
+      L.sq_ll[m] = ll;
+      L.sq_ml[m] = ml;
+      L.sq_of[m] = off;
+    }
+    m++;
+    T += ll + ml;
+    blit += ll;
+    outp += ll + ml;
   }
+  run_batch();
+  ZD_ADD(L, 2, t_seq);
   if (b.bits != 0) return PQG_ERR_CORRUPT;
   if (regen > lit_pos) zcopy_lits(O, L, lit_kind, rs, lit_kind == 1 ? lit_src : lit_src + lit_pos, litbuf, regen - lit_pos);
   return 0;
@@ -577,9 +797,11 @@ __device__ uint64_t zxxh64(const uint8_t* p, uint32_t n) {
   auto rotl = [](uint64_t x, int r) { return (x << r) | (x >> (64 - r)); };
   const uint32_t mis = (uint32_t)(uintptr_t)p & 3u;
   const uint32_t* base = (const uint32_t*)(p - mis);
+  const uint32_t last_w = n ? (n - 1u + mis) >> 2 : 0u;  // the output's last dword: nothing past it is read
   auto rd = [&](uint32_t o, int bytes) {  // little-endian bytes [o, o + bytes) of the output, bytes <= 8
     const uint32_t a = o + mis, w = a >> 2, s = a & 3u;
-    const uint32_t d0 = zld(base + w), d1 = zld(base + w + 1), d2 = s ? zld(base + w + 2) : 0u;
+    const uint32_t d0 = zld(base + w), d1 = w + 1u <= last_w ? zld(base + w + 1) : 0u,
+                   d2 = s && w + 2u <= last_w ? zld(base + w + 2) : 0u;
     uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, s) << 32);
     return bytes == 8 ? v : v & ((1ull << (8 * bytes)) - 1ull);
   };
@@ -604,18 +826,37 @@ __device__ uint64_t zxxh64(const uint8_t* p, uint32_t n) {
   return h;
 }
 
-// One wave per job: the frames of src[job] -> dst[job] (exactly dst_size bytes kept).
+// One wave per job: the frames of src[job] -> dst[job] (exactly dst_size bytes kept). The grid is at
+// most ZS_GRID waves; wave w takes jobs w, w + grid, ... and owns literal scratch slot w, so the
+// scratch is bounded whatever the number of pages.
+__device__ __forceinline__ void zstd_job(ZWaveLds& L, const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
+                         uint64_t dst_bytes, const pqg_snappy_job& jb, int j, int32_t* status, uint8_t* litbuf);
+
 __global__ __launch_bounds__(64) void k_zstd(const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
                                              uint64_t dst_bytes, const pqg_snappy_job* __restrict__ jobs, int n_jobs,
                                              int32_t* status, uint8_t* scratch, uint64_t lit_stride) {
   __shared__ __attribute__((aligned(16))) ZWaveLds L;
-  const int j = (int)blockIdx.x;
-  if (j >= n_jobs) return;
-  const pqg_snappy_job jb = jobs[j];
+  uint8_t* litbuf = scratch + (uint64_t)blockIdx.x * lit_stride;
+  for (uint32_t i = lane_id(); i < 53u; i += WAVE) {
+    if (i < 36u) L.llcode[i] = ZLL_BASE[i] | (uint32_t)ZLL_BITS[i] << 24;
+    L.mlcode[i] = ZML_BASE[i] | (uint32_t)ZML_BITS[i] << 24;
+  }
+  wave_sync();
+  for (int j = (int)blockIdx.x; j < n_jobs; j += (int)gridDim.x) {
+    zstd_job(L, src, src_bytes, dst, dst_bytes, jobs[j], j, status, litbuf);
+    wave_sync();
+  }
+}
+
+__device__ __forceinline__ void zstd_job(ZWaveLds& L, const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
+                         uint64_t dst_bytes, const pqg_snappy_job& jb, int j, int32_t* status, uint8_t* litbuf) {
   const rsrc_t rs = make_rsrc(src + jb.src_offset, src_bytes - jb.src_offset);
   const uint32_t n = uni(jb.src_size);
-  uint8_t* litbuf = scratch + (uint64_t)j * lit_stride;
-  ZOut O{dst + jb.dst_offset, uni(jb.dst_size), 0, 0, 0};
+#ifdef PQG_DIAG
+  for (int i = 0; i < 8; i++) L.diag[i] = 0;
+  ZD_T(t_job);
+#endif
+  ZOut O{dst + jb.dst_offset, uni(jb.dst_size), 0, 0, 0, 0};
   int code = 0;
   uint32_t p = 0;
   if (jb.dst_offset + jb.dst_size > dst_bytes || jb.src_offset + jb.src_size > src_bytes) code = PQG_ERR_INVALID_ARG;
@@ -662,12 +903,8 @@ __global__ __launch_bounds__(64) void k_zstd(const uint8_t* __restrict__ src, ui
       if (type == 3) { code = PQG_ERR_CORRUPT; break; }
       if (type == 1) {
         if (p + 1 > n) { code = PQG_ERR_CORRUPT; break; }
-        const uint32_t v = zbyte(rs, p);
-        for (uint32_t k0 = 0; k0 < bs; k0 += WAVE)
-          if (k0 + lane_id() < bs) zput(O, L, O.pos + k0 + lane_id(), v);
-        O.pos += bs;
+        zcopy_lits(O, L, 1, rs, zbyte(rs, p), litbuf, bs);
         p += 1;
-        wave_sync();
       } else if (type == 0) {
         if (p + bs > n) { code = PQG_ERR_CORRUPT; break; }
         zcopy_lits(O, L, 0, rs, p, litbuf, bs);
@@ -679,7 +916,6 @@ __global__ __launch_bounds__(64) void k_zstd(const uint8_t* __restrict__ src, ui
         if (!code && O.pos - before > ZS_LIT_MAX) code = PQG_ERR_CORRUPT;
         p += bs;
       }
-      if (O.pos - O.drained >= 2048u) zdrain(O);
       if (last) break;
     }
     if (code || cut) break;
@@ -689,12 +925,17 @@ __global__ __launch_bounds__(64) void k_zstd(const uint8_t* __restrict__ src, ui
       const uint32_t want = ld4_any(rs, p);
       p += 4;
       if (O.pos <= O.cap) {
-        zdrain(O);
+        zdrain(O, L);
         const uint32_t got = (uint32_t)zxxh64(O.dst + O.frame0, O.pos - O.frame0);
         if (uni(got) != want) { code = PQG_ERR_CORRUPT; break; }
       }
     }
   }
+  zflush(O, L);
+#ifdef PQG_DIAG
+  L.diag[5] = __builtin_amdgcn_s_memtime() - t_job;
+  if (pqg_zdiag && lane_id() < 8) pqg_zdiag[8 * (uint64_t)j + lane_id()] = L.diag[lane_id()];
+#endif
   if (!code && O.pos < O.cap) code = PQG_ERR_EOF;  // the frames end before the page's size
   if (lane_id() == 0 && status) status[j] = code;
 }
@@ -702,8 +943,8 @@ __global__ __launch_bounds__(64) void k_zstd(const uint8_t* __restrict__ src, ui
 hipError_t launch_zstd(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
                        const pqg_snappy_job* jobs, int n_jobs, int32_t* status, uint8_t* scratch) {
   if (n_jobs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_zstd, dim3(n_jobs), dim3(64), 0, st, src, src_bytes, dst, dst_bytes, jobs, n_jobs, status,
-                     scratch, (uint64_t)ZS_LIT_MAX);
+  hipLaunchKernelGGL(k_zstd, dim3(n_jobs < (int)ZSTD_GRID ? n_jobs : (int)ZSTD_GRID), dim3(64), 0, st, src, src_bytes,
+                     dst, dst_bytes, jobs, n_jobs, status, scratch, (uint64_t)ZS_LIT_MAX);
   return hipGetLastError();
 }
 

@@ -224,3 +224,52 @@ def test_delta_byte_array_error_mid_page(decoder, at):
     ch = make(abi.BYTE_ARRAY, vals, abi.DELTA_BYTE_ARRAY)
     ch.pages[0].body = W.delta_encode(np.array(pre, dtype=np.int32), abi.INT32) + W.dlba_encode(suf)
     run_both(decoder, [ch], expect_error=True)
+
+
+# ---- PLAIN BYTE_ARRAY pages walked in 16 KiB segments (k_bin_walk_seg: plans with few such pages) ----
+
+@pytest.mark.parametrize("kind", ["ascii", "empty", "zeros", "smallints", "random", "long"])
+@pytest.mark.parametrize("version", [1, 2])
+def test_binary_plain_segmented(decoder, kind, version):
+    """Pages of 100-900 KB (many segments each): every kind of value bytes, including ones whose
+    bytes read as small lengths (the speculative segment starts then fail and are walked again), and
+    nullable V1 / V2 pages (the data section starts after the levels, at any alignment)."""
+    n = 2000 if kind == "long" else 60_000
+    vals = _binary_vals(kind, n, seed=11 + len(kind))
+    dl = nulls(n + n // 9, 0.1, seed=5)
+    vals = vals[: int(dl.sum())]
+    run_both(decoder, [make(abi.BYTE_ARRAY, vals, abi.PLAIN, def_levels=dl, max_def=1, version=version,
+                            page_rows=len(dl) // 2 + 1)])
+    run_both(decoder, [make(abi.BYTE_ARRAY, vals, abi.PLAIN, page_rows=len(vals) // 2 + 3)])
+
+
+@pytest.mark.parametrize("where", [0.0, 0.1, 0.5, 0.93, 0.999])
+@pytest.mark.parametrize("how", ["negative", "overrun", "truncate"])
+def test_binary_plain_segmented_errors(decoder, where, how):
+    """An error at any point of a large page (in its first, a middle or the last segment): the
+    status equals the oracle's (page, value index, code); nothing past the error is required."""
+    vals = _strings(30_000, 7, 0, 40)
+    ch = make(abi.BYTE_ARRAY, vals, abi.PLAIN, page_rows=30_000)
+    body = bytearray(ch.pages[0].body)
+    k = int(where * (len(vals) - 1))
+    pos = sum(4 + len(v) for v in vals[:k])
+    if how == "negative":
+        body[pos:pos + 4] = (0x80000001).to_bytes(4, "little")
+    elif how == "overrun":
+        body[pos:pos + 4] = (len(body) * 2).to_bytes(4, "little")
+    else:
+        body = body[:pos + 2]
+    ch.pages[0].body = bytes(body)
+    run_both(decoder, [ch], expect_error=True)
+
+
+def test_binary_plain_segmented_trailing_bytes(decoder):
+    """A page whose header counts fewer values than its bytes hold: the walk stops at the count
+    (the rest is never read, garbage included), in whichever segment the count ends."""
+    vals = _strings(40_000, 8, 0, 30)
+    ch = make(abi.BYTE_ARRAY, vals, abi.PLAIN, page_rows=40_000)
+    ch.pages[0].body = ch.pages[0].body + bytes(np.random.default_rng(1).integers(0, 256, 50_000, dtype=np.uint8))
+    for nv in (1, 777, 23_456, 40_000):
+        ch.pages[0].num_values = nv
+        ch.values = vals[:nv]
+        run_both(decoder, [ch])

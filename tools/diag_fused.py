@@ -26,7 +26,7 @@ dec = D.Decoder(0)
 plan = dec.plan(dec.upload(batch))
 n_pages = batch.n_pages
 max_chunks = n_pages * 16
-wrt = torch.zeros(n_pages * 2, dtype=torch.int64, device="cuda")
+wrt = torch.zeros(n_pages * 4, dtype=torch.int64, device="cuda")
 xrt = torch.zeros(max_chunks * 4, dtype=torch.int64, device="cuda")
 L = native.lib()
 L.pqg_diag_rt_set.argtypes = [C.c_void_p, C.c_void_p]
@@ -42,7 +42,7 @@ for rep in range(3):
     plan.launch()
     torch.cuda.synchronize()
     assert L.pqg_diag_rt_set(None, None) == 0
-    w = wrt.view(-1, 2).cpu().numpy().astype(np.float64)
+    w = wrt.view(-1, 4).cpu().numpy().astype(np.float64)
     x = xrt.view(-1, 4).cpu().numpy()
     x = x[x[:, 0] != 0]
     xt = x[:, :3].astype(np.float64)
@@ -61,6 +61,9 @@ for rep in range(3):
     r = {"kernel_us": end, "chunks": int(len(xt)),
          "walk_start_us": np.percentile(w[:, 0], pct).tolist(), "walk_pub_us": np.percentile(w[:, 1], pct).tolist(),
          "walk_dur_us": np.percentile(w[:, 1] - w[:, 0], pct).tolist(),
+         "walk_stage_us": np.percentile(w[:, 2] - w[:, 0], pct).tolist(),
+         "walk_chain_us": np.percentile(w[:, 3] - w[:, 2], pct).tolist(),
+         "walk_release_us": np.percentile(w[:, 1] - w[:, 3], pct).tolist(),
          "chunk_start_us": np.percentile(xt[:, 0], pct).tolist(), "chunk_spin_us": np.percentile(spin, pct).tolist(),
          "chunk_body_us": np.percentile(body, pct).tolist(), "chunk_end_us": np.percentile(xt[:, 2], pct).tolist(),
          "bucket_us": 5.0, "walking": walking, "spinning": spinning, "storing": storing}

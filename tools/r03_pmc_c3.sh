@@ -1,0 +1,18 @@
+#!/bin/bash
+# SQ + traffic counters per kernel of one suite workload (separate --pmc passes; each pass its own limit)
+set -euo pipefail
+TAG=$1; WL=$2
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
+           "SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  timeout -s KILL 400 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pass$i" -o run -- \
+    python3 tools/bench_suite.py $WL --steps 3 --warmup 1 --cpu-budget 0 > "$OUT/pass$i.log" 2>&1 \
+    || { tail -20 "$OUT/pass$i.log"; exit 1; }
+  i=$((i+1))
+done
+python3 tools/pmc_kernels.py "$OUT" > "$OUT/summary.txt" || true
+cat "$OUT/summary.txt"

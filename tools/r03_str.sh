@@ -9,10 +9,11 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_binary.py \
   tests/test_dba_carry.py tests/test_gpu_fixtures.py tests/test_c_harness.py \
   "tests/test_gpu_fullsize.py::test_c3_full" "tests/test_gpu_fullsize.py::test_c4_lineitem_row_groups" \
-  "tests/test_gpu_fullsize.py::test_c4_configured_shard" -m gpu > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
+  "tests/test_gpu_fullsize.py::test_c4_configured_shard" tests/test_gpu_assembly.py tests/test_assembly_schema.py \
+  "tests/test_gpu_fullsize.py::test_c5_full_with_assembly" -m gpu > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
 tail -2 "$OUT/pytest.log"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-  python3 tools/bench_suite.py c3_mixed str_plain str_dict str_dlba str_dba c4_lineitem --cpu-budget 0 \
+  python3 tools/bench_suite.py c3_mixed c5_levels str_plain str_dict str_dlba str_dba c4_lineitem --cpu-budget 0 \
   > "$OUT/suite.jsonl" 2> "$OUT/suite.err" || { tail -30 "$OUT/suite.err"; exit 1; }
 cat "$OUT/suite.jsonl"
 python3 tools/kstats.py "$OUT/prof"
