@@ -550,11 +550,6 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       for (uint32_t j = 0; j < nch; j++) chunk_list.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
       chunk_total += nch;
     }
-#ifdef PQG_AB_ORDER
-    std::stable_sort(chunk_list.begin() + P->chunk_off[k - C_DICT4], chunk_list.end(), [&](uint64_t a, uint64_t b) {
-      return P->h_work[(size_t)(uint32_t)a].size < P->h_work[(size_t)(uint32_t)b].size;
-    });
-#endif
     P->chunk_n[k - C_DICT4] = (uint32_t)chunk_list.size() - P->chunk_off[k - C_DICT4];
   }
   // ---- flatten lists: [levels][class 0]...[class n]

@@ -369,6 +369,20 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
   uint32_t pos = sec_beg + 1;  // RunLengthBitPackingHybridDecoder stream position
   uint32_t produced = 0, k = 0;
   int code = 0;
+#ifdef PQG_DIAG
+  uint64_t dg_pre = 0, dg_chain = 0, dg_emit = 0, dg_win = 0, dg_bat = 0;
+  struct DgOut {
+    uint64_t *a, *b, *c, *d, *e;
+    uint32_t* k;
+    int page;
+    __device__ ~DgOut() {
+      if (pqg_diag_wph && lane_id() == 0) {
+        uint64_t* o = pqg_diag_wph + 8 * (uint64_t)page;
+        o[0] = *a; o[1] = *b; o[2] = *c; o[3] = *d; o[4] = *e; o[5] = *k;
+      }
+    }
+  } dg_out{&dg_pre, &dg_chain, &dg_emit, &dg_win, &dg_bat, &k, page};
+#endif
   auto put_record = [&](uint32_t start, uint32_t end, uint32_t payload) {
     if (lane == 0) {
       sst(rec + k, (uint64_t)start | ((uint64_t)payload << 32));
@@ -384,6 +398,10 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
     if (produced >= N) break;
     if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
     const uint32_t B = pos & ~3u;
+    DIAG_T(dg_t0);
+#ifdef PQG_DIAG
+    dg_win++;
+#endif
     predecode<SMALL, (bool)0>(win, B, w);
     uint32_t js = 0, nn[4], slowm = 0, inm = 0;
     uint64_t ent[4];
@@ -406,9 +424,14 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
     ((u64x2a*)L.ent)[2u * lane] = u64x2{ent[0], ent[1]};
     ((u64x2a*)L.ent)[2u * lane + 1u] = u64x2{ent[2], ent[3]};
     wave_sync();
+    DIAG_ADD(dg_pre, dg_t0);
     uint32_t q = pos - B, nq = 0;
     while (true) {  // batches of at most 64 chain positions
       uint32_t t = 0, lst = 0;
+      DIAG_T(dg_t1);
+#ifdef PQG_DIAG
+      dg_bat++;
+#endif
       while (true) {
         q = uni(q);
         lst = lane == t ? q : lst;  // v_cmp + v_cndmask
@@ -419,6 +442,8 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
       }
       t = uni(t);
       nq = uni(nq);
+      DIAG_ADD(dg_chain, dg_t1);
+      DIAG_T(dg_t2);
       // the batch's last position q ends the chain here (nq == 0): a run only when it is a
       // fast-path header inside the section (otherwise the scalar path below takes it)
       const uint32_t ql = q >> 2, qb = q & 3u;
@@ -451,6 +476,7 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
       }
       k = uni(k + n_em);
       produced = uni(produced + total);
+      DIAG_ADD(dg_emit, dg_t2);
       if (produced >= N || nq == 0u) break;
       q = nq;  // the chain goes on inside this window: next batch
     }
@@ -505,9 +531,6 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
   DictWaveLds& L = ((DictWaveLds*)lds)[wave_id()];
   const int i_page = (int)(group * WPB + wave_id());
   if (i_page >= n_list) return;
-#ifdef PQG_AB_PRIO
-  __builtin_amdgcn_s_setprio(3);
-#endif
   const int page = list[i_page];
 #ifdef PQG_DIAG
   const uint64_t rt_w0 = __builtin_amdgcn_s_memrealtime();
@@ -691,7 +714,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
     } xstamp{rt_x0, &rt_x1, c};
 #endif
     const int page = (int)(uint32_t)chunks[c];
-      const uint32_t j = (uint32_t)(chunks[c] >> 32);
+    const uint32_t j = (uint32_t)(chunks[c] >> 32);
     // page / column facts and the page's bit width do not depend on the walk: loaded before the
     // hand-off, so the compiler barrier there does not serialize them behind the flag
     const PageWork pw = work[page];
@@ -2480,6 +2503,9 @@ extern "C" int pqg_diag_nostore_set(int v) {
 }
 extern "C" int pqg_diag_set(void* p) {
   return hipMemcpyToSymbol(HIP_SYMBOL(pqg::pqg_diag_buf), &p, sizeof(p)) == hipSuccess ? 0 : 3;
+}
+extern "C" int pqg_diag_wph_set(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(pqg::pqg_diag_wph), &p, sizeof(p)) == hipSuccess ? 0 : 3;
 }
 extern "C" int pqg_diag_rt_set(void* walk, void* chunk) {
   return hipMemcpyToSymbol(HIP_SYMBOL(pqg::pqg_diag_wrt), &walk, sizeof(walk)) == hipSuccess &&

@@ -119,19 +119,19 @@ struct FwdBits {
 struct BackBits {
   rsrc_t rs;
   uint32_t base, n;
-  int64_t bits;      // unread bits
+  int32_t bits;      // unread bits
   uint32_t wlo;      // window covers stream bytes [wlo, wlo + ZS_WIN)
   uint8_t* win;
   uint64_t c;        // container: stream bits [cbit, cbit + 64)
-  int64_t cbit;
+  int32_t cbit;
   __device__ bool init(rsrc_t r, uint32_t b, uint32_t len, uint8_t* w) {
     rs = r; base = b; n = len; win = w; wlo = 0xFFFFFFFFu;
-    cbit = INT64_MAX;
+    cbit = INT32_MAX;
     c = 0;
     if (len == 0) return false;
     const uint32_t last = zbyte(rs, base + len - 1);
     if (!last) return false;
-    bits = (int64_t)(len - 1) * 8 + zhigh(last);
+    bits = (int32_t)(len - 1) * 8 + zhigh(last);
     return true;
   }
   __device__ void refill(uint32_t need_end) {  // window ending at stream byte need_end
@@ -143,10 +143,10 @@ struct BackBits {
     wave_sync();
   }
   // container for reads ending at bit `end` (exclusive): bits [ceil8(end) - 64, ceil8(end)), from 0
-  __device__ void fill(int64_t end) {
-    const int64_t e8 = (end + 7) & ~7ll;
+  __device__ void fill(int32_t end) {
+    const int32_t e8 = (end + 7) & ~7;
     cbit = e8 > 64 ? e8 - 64 : 0;
-    const uint32_t b0 = (uint32_t)(cbit >> 3), b1 = b0 + 8u < n ? b0 + 8u : n;  // bytes [b0, b1)
+    const uint32_t b0 = (uint32_t)cbit >> 3, b1 = b0 + 8u < n ? b0 + 8u : n;  // bytes [b0, b1)
     if (wlo == 0xFFFFFFFFu || b0 < wlo || b1 > wlo + ZS_WIN) refill(b1 + 8u < n ? b1 + 8u : n);
     typedef uint32_t __attribute__((may_alias)) u32a;
     const uint32_t rel = b0 - wlo, r4 = rel & ~3u, sft = rel & 3u;
@@ -160,14 +160,25 @@ struct BackBits {
   __device__ uint32_t read(int k) {
     if (k == 0) return 0;
     bits -= k;
-    int64_t a = bits;
+    int32_t a = bits;
     int sh = 0;
-    if (a < 0) { sh = (int)-a; a = 0; }
+    if (a < 0) { sh = -a; a = 0; }
     const int kk = k - sh;
     if (kk <= 0) return 0;
     if (a < cbit || a + kk > cbit + 64) fill(a + kk);
     const uint32_t v = (uint32_t)((c >> (uint32_t)(a - cbit)) & ((1ull << kk) - 1ull));
     return v << sh;
+  }
+  // Sequence decoding (one container check per group of fields instead of one per field):
+  // need(n) makes n <= 57 unread bits available in the container (all that is left near the
+  // stream start); get(n), n <= 31, then reads them. Reading past the start gives garbage and
+  // leaves bits < 0, which the caller reports as corrupt before the values are used.
+  __device__ __forceinline__ void need(int32_t k) {
+    if (bits - cbit < k && cbit > 0) fill(bits);
+  }
+  __device__ __forceinline__ uint32_t get(int32_t k) {
+    bits -= k;
+    return (uint32_t)(c >> ((uint32_t)(bits - cbit) & 63u)) & ((1u << k) - 1u);
   }
 };
 
@@ -704,7 +715,10 @@ __device__ __forceinline__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t 
   if (!zseq_table(L, L.ml, &tlog[2], have_tab[2], (int)((modes >> 2) & 3u), rs, p, lim, ZML_DEF, 53, 6, 9, 52)) return PQG_ERR_CORRUPT;
   BackBits b;
   if (!b.init(rs, p, lim - p, L.win)) return PQG_ERR_CORRUPT;
-  uint32_t sl = b.read(tlog[0]), so = b.read(tlog[1]), sm = b.read(tlog[2]);
+  b.need(tlog[0] + tlog[1] + tlog[2]);  // <= 27 bits
+  uint32_t sl = b.get(tlog[0]);
+  uint32_t so = b.get(tlog[1]);
+  uint32_t sm = b.get(tlog[2]);
   ZD_ADD(L, 1, t_tab);
   ZD_CNT(L, 6, nseq);
   ZD_T(t_seq);
@@ -725,15 +739,18 @@ __device__ __forceinline__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t 
     m = 0; T = 0; blit = 0;
   };
   for (uint32_t i = 0; i < nseq; i++) {
-    const uint32_t el = L.ll[sl], eo = L.of[so], em = L.ml[sm];
+    const uint32_t el = uni(L.ll[sl]), eo = uni(L.of[so]), em = uni(L.ml[sm]);
     const uint32_t llc = el & 0xFFu, ofc = eo & 0xFFu, mlc = em & 0xFFu;
     if (llc > 35 || mlc > 52 || ofc > 31) return PQG_ERR_CORRUPT;
     // length codes from LDS: an indexed __constant__ table is a vector memory load here, and its
     // vmcnt wait also waited for every output store in flight, once per sequence
-    const uint32_t mle = L.mlcode[mlc], lle = L.llcode[llc];
-    const uint64_t ofv = (1ull << ofc) + b.read((int)ofc);
-    const uint32_t ml = (mle & 0xFFFFFFu) + b.read((int)(mle >> 24));
-    const uint32_t ll = (lle & 0xFFFFFFu) + b.read((int)(lle >> 24));
+    const uint32_t mle = uni(L.mlcode[mlc]), lle = uni(L.llcode[llc]);
+    const int32_t mlb = (int32_t)(mle >> 24), llb = (int32_t)(lle >> 24);
+    b.need((int32_t)ofc);  // offset, match length, literal length extra bits (RFC 8878 §3.1.1.3.2.1.2)
+    const uint32_t ofv = (1u << ofc) + b.get((int32_t)ofc);
+    b.need(mlb + llb);
+    const uint32_t ml = (mle & 0xFFFFFFu) + b.get(mlb);
+    const uint32_t ll = (lle & 0xFFFFFFu) + b.get(llb);
     uint32_t off;
     if (ofv > 3) {
       off = (uint32_t)(ofv - 3);
@@ -754,10 +771,12 @@ __device__ __forceinline__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t 
         rep[0] = off;
       }
     }
-    if (i + 1 < nseq) {
-      sl = (el >> 16) + b.read((int)((el >> 8) & 0xFFu));
-      sm = (em >> 16) + b.read((int)((em >> 8) & 0xFFu));
-      so = (eo >> 16) + b.read((int)((eo >> 8) & 0xFFu));
+    if (i + 1 < nseq) {  // state updates: literal length, match length, offset
+      const int32_t nl = (int32_t)((el >> 8) & 0xFFu), nm = (int32_t)((em >> 8) & 0xFFu), no = (int32_t)((eo >> 8) & 0xFFu);
+      b.need(nl + nm + no);  // <= 26 bits
+      sl = (el >> 16) + b.get(nl);
+      sm = (em >> 16) + b.get(nm);
+      so = (eo >> 16) + b.get(no);
     }
     if (b.bits < 0 || lit_pos + blit + ll > regen) return PQG_ERR_CORRUPT;
     if (off == 0 || off > outp + ll - O.frame0) return PQG_ERR_CORRUPT;

@@ -28,8 +28,10 @@ n_pages = batch.n_pages
 max_chunks = n_pages * 16
 wrt = torch.zeros(n_pages * 4, dtype=torch.int64, device="cuda")
 xrt = torch.zeros(max_chunks * 4, dtype=torch.int64, device="cuda")
+wph = torch.zeros(n_pages * 8, dtype=torch.int64, device="cuda")
 L = native.lib()
 L.pqg_diag_rt_set.argtypes = [C.c_void_p, C.c_void_p]
+L.pqg_diag_wph_set.argtypes = [C.c_void_p]
 for _ in range(3):
     plan.launch()
 torch.cuda.synchronize()
@@ -39,9 +41,12 @@ for rep in range(3):
     xrt.zero_()
     torch.cuda.synchronize()
     assert L.pqg_diag_rt_set(wrt.data_ptr(), xrt.data_ptr()) == 0
+    assert L.pqg_diag_wph_set(C.c_void_p(wph.data_ptr())) == 0
     plan.launch()
     torch.cuda.synchronize()
     assert L.pqg_diag_rt_set(None, None) == 0
+    assert L.pqg_diag_wph_set(None) == 0
+    ph = wph.view(-1, 8).cpu().numpy().astype(np.float64)
     w = wrt.view(-1, 4).cpu().numpy().astype(np.float64)
     x = xrt.view(-1, 4).cpu().numpy()
     x = x[x[:, 0] != 0]
@@ -66,6 +71,8 @@ for rep in range(3):
          "walk_release_us": np.percentile(w[:, 1] - w[:, 3], pct).tolist(),
          "chunk_start_us": np.percentile(xt[:, 0], pct).tolist(), "chunk_spin_us": np.percentile(spin, pct).tolist(),
          "chunk_body_us": np.percentile(body, pct).tolist(), "chunk_end_us": np.percentile(xt[:, 2], pct).tolist(),
+         "list_walk_kcyc_pre_chain_emit_mean": (ph[:, :3].mean(0) / 1e3).tolist(),
+         "list_walk_windows_batches_runs_mean": ph[:, 3:6].mean(0).tolist(),
          "bucket_us": 5.0, "walking": walking, "spinning": spinning, "storing": storing}
     res["runs"].append(r)
     print(json.dumps({k: (np.round(v, 1).tolist() if isinstance(v, list) else v) for k, v in r.items()}), flush=True)
