@@ -236,6 +236,13 @@ int pqg_plan_kernel_count(pqg_plan* plan);
  * walk and the expansion as two launches; the plan keeps that mode and the caller sees the normal
  * result. Returns how many launches of the plan were re-run that way. */
 int pqg_plan_timeout_fallbacks(pqg_plan* plan);
+/* BYTE_ARRAY columns whose pages are all PLAIN decode in one pass per 2 KiB tile of the pages (walk,
+ * offsets and value bytes together), which takes each page's values to fill its data section, as
+ * every writer lays them out. A page with bytes after its num_values values (which the reader
+ * ignores) is detected on the device, and pqg_sync re-runs the plan on the per-value path (value
+ * walk, offset scan, byte copy), which reads exactly num_values values; the plan keeps that path.
+ * Returns how many launches of the plan were re-run that way. */
+int pqg_plan_plain_fallbacks(pqg_plan* plan);
 int pqg_plan_destroy(pqg_plan* plan);
 
 /* ---- host-buffer decode (the JNI shim's entry: file bytes in, arrays out) --

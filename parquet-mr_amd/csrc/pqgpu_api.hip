@@ -153,6 +153,18 @@ struct pqg_plan {
   uint32_t n_segs = 0;
   uint64_t seg_status_off = 0, seg_tmp_off = 0;  // in bscratch: status words + ticket (cleared per launch), scratch
   int timeout_fallbacks = 0;           // launches re-run in split mode after PQG_ERR_TIMEOUT (pqg_sync)
+  // PLAIN-only BYTE_ARRAY columns in one pass (k_bin_bases + k_bin_plain); the per-value path's lists
+  // hold those columns' entries last, so plain_fused launches skip them (pqg_sync turns plain_fused
+  // off when a page's values do not fill its data section)
+  bool plain_fused = false;
+  int plain_fallbacks = 0;
+  DevBuf psegs, pstatus, pcol_pages, pcol_start;  // tiles (page | tile << 32); aggw + incw per tile; column page lists
+  uint32_t n_psegs = 0, pseg_epoch = 0;
+  int n_pcols = 0;
+  uint64_t pticket_off = 0, pflag_off = 0;  // in bscratch: ticket (cleared per launch), inexact flag (epoch-tagged)
+  uint64_t blen_bytes_nf = 0;               // cleared part of bscratch when plain_fused
+  int n_binp_fused = 0, n_bin_cols_nf = 0;  // tails of cls_lists[C_BINP] / bin_cols that belong to those columns
+  uint32_t n_bin_blocks_nf = 0, n_bin_chunks_nf = 0;
 };
 
 struct pqg_ctx {
@@ -251,6 +263,21 @@ int pqg_ctx_destroy(pqg_ctx* c) {
 
 // valid_bytes: the caller's data ends there (page and dictionary extents are checked against it); the
 // kernels may read up to n_bytes (pqg_decode_host's zero padding past the caller's bytes)
+// Kernels one launch of the plan runs (in its current modes).
+static int count_kernels(const pqg_plan* P) {
+  const bool pf = P->plain_fused;
+  int k = (P->levels_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
+  for (int c = 0; c < C_NCLS; c++) {
+    const int n = P->cls_n[(size_t)c] - (c == C_BINP && pf ? P->n_binp_fused : 0);
+    if (n) k += (c == C_DICT4 || c == C_DICT8 || c == C_IDS) && !P->dict_fused ? 2 : 1;
+  }
+  k += (P->n_dict_walk ? 1 : 0) + (P->n_bind ? 1 : 0) + (P->n_fixd ? 1 : 0) +
+       ((pf ? P->n_bin_blocks_nf : P->n_bin_blocks) ? 3 : 0) + ((pf ? P->n_bin_chunks_nf : P->n_bin_chunks) ? 1 : 0) +
+       (P->cls_n[C_DBA] ? (P->n_dba_chunks ? 4 : 1) : 0) + (P->n_carry ? 1 : 0) + (P->n_segs ? 1 : 0) +
+       (pf ? 2 : 0);
+  return k;
+}
+
 static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, uint64_t valid_bytes,
                             const pqg_column_desc* cols, int n_cols, const pqg_page_desc* pages, int n_pages,
                             pqg_plan** out, pqg_status* st) {
@@ -461,12 +488,45 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   auto take = [&](uint64_t bytes) { uint64_t o = sc; sc = (sc + bytes + 255) & ~uint64_t(255); return o; };
   std::vector<uint8_t> needs_ids((size_t)std::max(n_cols, 1), 0);
   for (int p : cls_lists[C_IDS]) needs_ids[(size_t)P->h_work[(size_t)p].column] = 1;
+  // PLAIN-only BYTE_ARRAY columns (every page PLAIN, no descriptor error, < 2^24 - 1 slots per page):
+  // one pass (k_bin_bases + k_bin_plain) over 2 KiB tiles of their pages, when the plan has fewer than
+  // BW_SEG_MAX_PAGES PLAIN pages (with more, one wave per page already fills the chip, and the per-value
+  // path's walk + copy measured faster than the tiles: C3 6.4 vs 10.4 ms, profiles/r03/plain_ab)
+  std::vector<uint8_t> plain_col((size_t)std::max(n_cols, 1), 0);
+  std::vector<uint64_t> psegs;
+  std::vector<int32_t> pcp, pcs(1, 0);
+  {
+    std::vector<int> npg((size_t)std::max(n_cols, 1), 0), nplain((size_t)std::max(n_cols, 1), 0);
+    std::vector<std::vector<int>> cpg((size_t)std::max(n_cols, 1));
+    for (int p = 0; p < n_pages; p++) {
+      const int c = P->h_work[(size_t)p].column;
+      npg[(size_t)c]++;
+      cpg[(size_t)c].push_back(p);
+      if (P->page_cls[(size_t)p] == C_BINP && P->h_work[(size_t)p].num_slots < (1u << 24) - 1u) nplain[(size_t)c]++;
+    }
+    for (int i = 0; i < n_cols; i++) {
+      plain_col[(size_t)i] = bin_out(cols[i]) && !ids_mode(cols[i]) && !col_err[(size_t)i] && !dba_fixed[(size_t)i] &&
+                             npg[(size_t)i] > 0 && nplain[(size_t)i] == npg[(size_t)i] &&
+                             cls_lists[C_BINP].size() < pqg::BW_SEG_MAX_PAGES;
+#ifdef PQG_AB_NOPLAIN  // (A/B builds under abx/ only)
+      plain_col[(size_t)i] = 0;
+#endif
+      if (!plain_col[(size_t)i]) continue;
+      for (int p : cpg[(size_t)i]) {
+        pcp.push_back(p);
+        const uint32_t ntile = std::max<uint32_t>((P->h_work[(size_t)p].size + pqg::BP_TILE - 1) / pqg::BP_TILE, 1u);
+        for (uint32_t k = 0; k < ntile; k++) psegs.push_back((uint64_t)(uint32_t)p | ((uint64_t)k << 32));
+      }
+      pcs.push_back((int32_t)pcp.size());
+    }
+  }
   // PLAIN BYTE_ARRAY pages walked in segments when there are few of them (k_bin_walk_seg)
   std::vector<uint64_t> segs;
   std::vector<uint8_t> seg_page((size_t)std::max(n_pages, 1), 0);
   if (!cls_lists[C_BINP].empty() && cls_lists[C_BINP].size() < pqg::BW_SEG_MAX_PAGES) {
     for (int p : cls_lists[C_BINP]) {
       const PageWork& w = P->h_work[(size_t)p];
+      if (plain_col[(size_t)w.column]) continue;  // one pass (k_bin_plain); the per-value fallback walks per page
       const uint32_t nseg = (w.size + pqg::BW_SEG_BYTES - 1) / pqg::BW_SEG_BYTES + 1;  // + 1: tile alignment of the start
       if (nseg < 3) continue;
       seg_page[(size_t)p] = 1;
@@ -474,21 +534,31 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
         segs.push_back((uint64_t)(uint32_t)p | ((uint64_t)k << 32) | (k + 1 == nseg ? (1ull << 63) : 0ull));
     }
   }
-  for (int i = 0; i < n_cols; i++) {  // blen first: the part cleared before every launch
-    if (ids_mode(cols[i])) continue;  // ids go straight to the column's values
-    if (bin_out(cols[i]) || needs_ids[(size_t)i] || dba_fixed[(size_t)i])
-      blen_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
+  // blen first: the part cleared before every launch (with the one-pass columns' last: not cleared
+  // while they take the one-pass path)
+  for (int pass = 0; pass < 2; pass++) {
+    for (int i = 0; i < n_cols; i++) {
+      if (ids_mode(cols[i]) || (plain_col[(size_t)i] != 0) != (pass == 1)) continue;  // ids go straight to the values
+      if (bin_out(cols[i]) || needs_ids[(size_t)i] || dba_fixed[(size_t)i])
+        blen_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
+    }
+    if (pass == 0) {
+      if (!segs.empty()) P->seg_status_off = take(8 * (segs.size() + 1));  // + the ticket counter
+      if (!psegs.empty()) P->pticket_off = take(8);
+      P->blen_bytes_nf = sc;
+    }
   }
-  if (!segs.empty()) P->seg_status_off = take(8 * (segs.size() + 1));  // + the ticket counter
   P->blen_bytes = sc;
+  if (!psegs.empty()) P->pflag_off = take(8);
   if (!segs.empty()) P->seg_tmp_off = take(4 * 2 * (uint64_t)pqg::BW_SEG_CAP * segs.size());
   P->n_segs = (uint32_t)segs.size();
   for (int i = 0; i < n_cols; i++) {
     if (dba_fixed[(size_t)i]) bsrc_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));  // prefix lengths
     if (dba_carry[(size_t)i]) carry_cols.push_back(i);
   }
-  for (int i = 0; i < n_cols; i++) {
-    if (!bin_out(cols[i])) continue;
+  for (int i0 = 0; i0 < 2 * n_cols; i0++) {  // the one-pass columns last
+    const int i = i0 % n_cols;
+    if (!bin_out(cols[i]) || (plain_col[(size_t)i] != 0) != (i0 >= n_cols)) continue;
     bin_cols.push_back(i);
     P->bin_capacity[(size_t)i] = cols[i].binary_capacity;
     bsrc_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
@@ -503,9 +573,23 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       dsrc_off[(size_t)i] = take(4 * ((uint64_t)cols[i].dict_num_values + 1));
     }
   }
+  {  // bin_cols / bin_blocks of the one-pass columns form the tails
+    int nf = 0;
+    for (int c : bin_cols) nf += plain_col[(size_t)c] ? 0 : 1;
+    P->n_bin_cols_nf = nf;
+    uint32_t nb = 0;
+    for (uint64_t b : bin_blocks) nb += plain_col[(size_t)(b >> 32)] ? 0 : 1;
+    P->n_bin_blocks_nf = nb;
+  }
+  std::vector<uint64_t> plain_chunks;  // copy chunks of the one-pass columns (per-value fallback only)
   for (int k : {C_IDS, C_BINP, C_DLBA})
     for (int p : cls_lists[(size_t)k]) {
       const PageWork& w = P->h_work[(size_t)p];
+      if (k == C_BINP && plain_col[(size_t)w.column]) {
+        const uint32_t nch = (w.num_slots + pqg::CP_CHUNK_VALUES - 1) / pqg::CP_CHUNK_VALUES;
+        for (uint32_t j = 0; j < nch; j++) plain_chunks.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
+        continue;
+      }
       if (k == C_IDS && ids_mode(cols[w.column])) continue;  // the ids are the output
       if (k == C_IDS && cols[w.column].physical_type != PQG_BYTE_ARRAY) {
         fixd.push_back(p);
@@ -515,10 +599,16 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       const uint32_t nch = (w.num_slots + pqg::CP_CHUNK_VALUES - 1) / pqg::CP_CHUNK_VALUES;
       for (uint32_t j = 0; j < nch; j++) bin_chunks.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
     }
-  if (!segs.empty()) {  // walked by k_bin_walk_seg instead of the one-wave-per-page walk
-    std::vector<int> keep;
-    for (int p : cls_lists[C_BINP])
-      if (!seg_page[(size_t)p]) keep.push_back(p);
+  P->n_bin_chunks_nf = (uint32_t)bin_chunks.size();
+  bin_chunks.insert(bin_chunks.end(), plain_chunks.begin(), plain_chunks.end());
+  {  // PLAIN pages: walked by k_bin_walk_seg (not listed), one wave per page, the one-pass columns last
+    std::vector<int> keep, tail;
+    for (int p : cls_lists[C_BINP]) {
+      if (plain_col[(size_t)P->h_work[(size_t)p].column]) tail.push_back(p);
+      else if (!seg_page[(size_t)p]) keep.push_back(p);
+    }
+    P->n_binp_fused = (int)tail.size();
+    keep.insert(keep.end(), tail.begin(), tail.end());
     cls_lists[C_BINP].swap(keep);
   }
   // ---- DELTA_BYTE_ARRAY pages: BIN_CHUNK-value chunks (upper bound from the slot count)
@@ -594,6 +684,10 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
             P->bin_chunks.ensure(sizeof(uint64_t) * std::max<size_t>(bin_chunks.size(), 1)) == hipSuccess &&
             P->dba_chunks.ensure(sizeof(uint64_t) * std::max<size_t>(dba_chunks.size(), 1)) == hipSuccess &&
             P->segs.ensure(sizeof(uint64_t) * std::max<size_t>(segs.size(), 1)) == hipSuccess &&
+            P->psegs.ensure(sizeof(uint64_t) * std::max<size_t>(psegs.size(), 1)) == hipSuccess &&
+            P->pstatus.ensure(2 * sizeof(uint64_t) * std::max<size_t>(psegs.size(), 1)) == hipSuccess &&
+            P->pcol_pages.ensure(sizeof(int32_t) * std::max<size_t>(pcp.size(), 1)) == hipSuccess &&
+            P->pcol_start.ensure(sizeof(int32_t) * pcs.size()) == hipSuccess &&
 
             P->rec.ensure(sizeof(uint64_t) * (rec_total + 16)) == hipSuccess &&  // k_dict_fill reads 9 ahead
             P->chunk_run.ensure(sizeof(uint32_t) * std::max<uint32_t>(chunk_total, 1)) == hipSuccess &&
@@ -627,6 +721,16 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     ok = ok && hipMemcpyAsync(P->bin_chunks.p, bin_chunks.data(), sizeof(uint64_t) * bin_chunks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   if (!segs.empty())
     ok = ok && hipMemcpyAsync(P->segs.p, segs.data(), sizeof(uint64_t) * segs.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!psegs.empty()) {
+    ok = ok && hipMemcpyAsync(P->psegs.p, psegs.data(), sizeof(uint64_t) * psegs.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+    ok = ok && hipMemsetAsync(P->pstatus.p, 0, 2 * sizeof(uint64_t) * psegs.size(), s) == hipSuccess;
+    ok = ok && hipMemcpyAsync(P->pcol_pages.p, pcp.data(), sizeof(int32_t) * pcp.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+    ok = ok && hipMemcpyAsync(P->pcol_start.p, pcs.data(), sizeof(int32_t) * pcs.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+    ok = ok && hipMemsetAsync((uint8_t*)P->bscratch.p + P->pflag_off, 0, 8, s) == hipSuccess;
+  }
+  P->n_psegs = (uint32_t)psegs.size();
+  P->n_pcols = (int)pcs.size() - 1;
+  P->plain_fused = !psegs.empty();
   if (!dba_chunks.empty())
     ok = ok && hipMemcpyAsync(P->dba_chunks.p, dba_chunks.data(), sizeof(uint64_t) * dba_chunks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   if (!chunk_list.empty())
@@ -643,11 +747,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     pqg_plan_destroy(P);
     return PQG_ERR_HIP;
   }
-  P->kernels = (P->levels_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
-  for (int k = 0; k < C_NCLS; k++) P->kernels += P->cls_n[(size_t)k] ? 1 : 0;
-  P->kernels += (P->n_dict_walk ? 1 : 0) + (P->n_bind ? 1 : 0) + (P->n_fixd ? 1 : 0) + (P->n_bin_blocks ? 3 : 0) +
-                (P->n_bin_chunks ? 1 : 0) + (P->cls_n[C_DBA] ? (P->n_dba_chunks ? 4 : 1) : 0) +
-                (P->n_carry ? 1 : 0) + (P->n_segs ? 1 : 0);
+  P->kernels = count_kernels(P);
   *out = P;
   return PQG_OK;
 }
@@ -655,6 +755,8 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
 int pqg_plan_kernel_count(pqg_plan* P) { return P ? P->kernels : 0; }
 
 int pqg_plan_timeout_fallbacks(pqg_plan* P) { return P ? P->timeout_fallbacks : 0; }
+
+int pqg_plan_plain_fallbacks(pqg_plan* P) { return P ? P->plain_fallbacks : 0; }
 
 int pqg_plan_launch(pqg_plan* P) {
   if (!P) return PQG_ERR_INVALID_ARG;
@@ -667,12 +769,19 @@ int pqg_plan_launch(pqg_plan* P) {
   if (++P->err_epoch > pqg::ERR_EPOCH_MAX) {
     P->err_epoch = 1;
     if (hipMemsetAsync(P->err.p, 0, err_bytes + 16, s) != hipSuccess) return PQG_ERR_HIP;
+    if (P->n_psegs && hipMemsetAsync((uint8_t*)P->bscratch.p + P->pflag_off, 0, 8, s) != hipSuccess) return PQG_ERR_HIP;
   }
   const pqg::ErrCount ecount{(uint32_t*)((uint8_t*)P->err.p + err_bytes), P->err_epoch};
   PageWork* work = (PageWork*)P->work.p;
   const ColumnDev* cols = (const ColumnDev*)P->cols.p;
   const int32_t* lists = (const int32_t*)P->lists.p;
-  if (P->blen_bytes && hipMemsetAsync(P->bscratch.p, 0, P->blen_bytes, s) != hipSuccess) return PQG_ERR_HIP;
+  const bool pf = P->plain_fused;
+  const uint64_t clear = pf ? P->blen_bytes_nf : P->blen_bytes;
+  if (clear && hipMemsetAsync(P->bscratch.p, 0, clear, s) != hipSuccess) return PQG_ERR_HIP;
+  if (pf && ++P->pseg_epoch > 255u) {  // k_bin_plain tile words are tagged with 1..255
+    P->pseg_epoch = 1;
+    if (hipMemsetAsync(P->pstatus.p, 0, 2 * sizeof(uint64_t) * P->n_psegs, s) != hipSuccess) return PQG_ERR_HIP;
+  }
   for (void* v : P->empty_bin_values)
     if (hipMemsetAsync(v, 0, sizeof(int64_t), s) != hipSuccess) return PQG_ERR_HIP;
   // page ready flags compare against the launch epoch (even); a walker's early partial status is
@@ -690,11 +799,19 @@ int pqg_plan_launch(pqg_plan* P) {
       e = pqg::launch_scan(s, work, (const int32_t*)P->col_pages.p, (const int32_t*)P->col_page_start.p, P->n_scan_cols);
   }
   const int32_t* bl = (const int32_t*)P->bin_lists.p;
+  if (e == hipSuccess && pf) {  // PLAIN-only BYTE_ARRAY columns: one pass (after the levels: n_values, out_offset)
+    uint8_t* scb = (uint8_t*)P->bscratch.p;
+    uint64_t* ps = (uint64_t*)P->pstatus.p;
+    e = pqg::launch_bin_plain(s, P->d_bytes, P->n_bytes, work, cols, (const int32_t*)P->pcol_pages.p,
+                              (const int32_t*)P->pcol_start.p, P->n_pcols, (const uint64_t*)P->psegs.p, P->n_psegs, ps,
+                              ps + P->n_psegs, (uint32_t*)(scb + P->pticket_off), P->pseg_epoch,
+                              (uint32_t*)(scb + P->pflag_off), P->err_epoch, err, ecount);
+  }
   if (e == hipSuccess && P->n_dict_walk)  // BYTE_ARRAY dictionary entries (PlainBinaryDictionary ctor)
     e = pqg::launch_bin_walk(s, P->d_bytes, P->n_bytes, work, cols, bl + P->off_dict_walk, P->n_dict_walk, 1, P->n_pages,
                              err, ecount);
   for (int k = 0; k < C_NCLS && e == hipSuccess; k++) {
-    int n = P->cls_n[(size_t)k];
+    int n = P->cls_n[(size_t)k] - (k == C_BINP && pf ? P->n_binp_fused : 0);
     if (!n) continue;
     const int32_t* l = lists + P->cls_off[(size_t)k];
     switch (k) {
@@ -738,12 +855,14 @@ int pqg_plan_launch(pqg_plan* P) {
   if (e == hipSuccess && P->n_bind) e = pqg::launch_bin_dict_map(s, work, cols, bl + P->off_bind, P->n_bind);
   if (e == hipSuccess && P->n_fixd)
     e = pqg::launch_gather_fixed(s, P->d_bytes, P->n_bytes, work, cols, bl + P->off_fixd, P->n_fixd);
-  if (e == hipSuccess && P->n_bin_blocks)
-    e = pqg::launch_bin_scan(s, cols, bl + P->off_bin_cols, P->n_bin_cols, (const uint64_t*)P->bin_blocks.p,
-                             P->n_bin_blocks);
-  if (e == hipSuccess && P->n_bin_chunks)
-    e = pqg::launch_bin_copy(s, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->bin_chunks.p, P->n_bin_chunks,
-                             err, ecount);
+  const uint32_t n_blocks = pf ? P->n_bin_blocks_nf : P->n_bin_blocks;
+  if (e == hipSuccess && n_blocks)
+    e = pqg::launch_bin_scan(s, cols, bl + P->off_bin_cols, pf ? P->n_bin_cols_nf : P->n_bin_cols,
+                             (const uint64_t*)P->bin_blocks.p, n_blocks);
+  const uint32_t n_chunks = pf ? P->n_bin_chunks_nf : P->n_bin_chunks;
+  if (e == hipSuccess && n_chunks)
+    e = pqg::launch_bin_copy(s, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->bin_chunks.p, n_chunks, err,
+                             ecount);
   if (e == hipSuccess && P->cls_n[C_DBA])
     e = pqg::launch_dba_copy(s, P->d_bytes, P->n_bytes, work, cols, lists + P->cls_off[C_DBA], P->cls_n[C_DBA],
                              (const uint64_t*)P->dba_chunks.p, P->n_dba_chunks, P->dba_meta(), bl + P->off_carry,
@@ -767,6 +886,10 @@ int pqg_plan_destroy(pqg_plan* P) {
   P->err.release();
   P->rec.release();
   P->chunk_run.release();
+  P->psegs.release();
+  P->pstatus.release();
+  P->pcol_pages.release();
+  P->pcol_start.release();
   P->chunks.release();
   P->pstat.release();
   P->flags.release();
@@ -898,6 +1021,22 @@ int pqg_sync(pqg_ctx* ctx, pqg_status* st) {
   }
   pqg_plan* P = ctx->last_launched;
   if (!P) return PQG_OK;
+  if (P->plain_fused) {
+    // A PLAIN page whose values do not end at its section end (bytes the reader ignores after them)
+    // breaks the one-pass path's byte bases: the launch is re-run on the per-value path (k_bin_walk,
+    // offset scan, k_bin_copy), which reads exactly n_values values per page; the plan keeps that path.
+    uint32_t flag = 0;
+    if (hipMemcpy(&flag, (uint8_t*)P->bscratch.p + P->pflag_off, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess)
+      return PQG_ERR_HIP;
+    if (flag == P->err_epoch) {
+      P->plain_fused = false;
+      P->kernels = count_kernels(P);
+      P->plain_fallbacks++;
+      const int lrc = pqg_plan_launch(P);
+      if (lrc != PQG_OK) return lrc;
+      if (hipStreamSynchronize(ctx->stream) != hipSuccess) return PQG_ERR_HIP;
+    }
+  }
   std::vector<PageWork> work;
   int rc = resolve_errors(P, st, &work);
   if (rc == PQG_ERR_TIMEOUT && P->dict_fused) {
@@ -908,7 +1047,7 @@ int pqg_sync(pqg_ctx* ctx, pqg_status* st) {
     // which have no inter-workgroup waits; the plan keeps that mode. Every output of the re-run is
     // written again, so the result is the same bit for bit.
     P->dict_fused = false;
-    for (int k : {C_DICT4, C_DICT8, C_IDS}) P->kernels += P->cls_n[(size_t)k] ? 1 : 0;
+    P->kernels = count_kernels(P);
     P->timeout_fallbacks++;
     rc = pqg_plan_launch(P);
     if (rc == PQG_OK) {

@@ -403,6 +403,7 @@ constexpr uint32_t SEG_CAP = SEG_B / 4 + 2;  // values that can start in a segme
 constexpr uint32_t SEG_LINKS = 6;
 constexpr uint64_t SG_OK = 1ull << 62, SG_STOP = 2ull << 62;
 static_assert(SEG_B == BW_SEG_BYTES && SEG_CAP == BW_SEG_CAP, "host segmentation (pqgpu_internal.h)");
+static_assert(BW_WIN == BP_TILE, "host tiling of k_bin_plain (pqgpu_internal.h)");
 
 // a value could start at p: its 4 length bytes and its bytes inside the section
 __device__ __forceinline__ bool seg_candidate(rsrc_t rs, uint32_t p, uint32_t end) {
@@ -731,6 +732,21 @@ __global__ __launch_bounds__(256) void k_bin_offsets(const ColumnDev* __restrict
 // Store the 16-byte output block at `a` (dwords wd) clipped to [o_lo, o_hi): one 16-byte store
 // when the block is whole and aligned, dword stores for whole dwords, byte stores at the edges
 // (which neighbouring chunks / pages share). have: bit q = dword q whole (0 for an unaligned dst).
+// c ? y : x per lane, as v_cndmask the optimizer cannot see through: selects among elements of a
+// register array are otherwise turned into an indexed access, which puts the array in scratch (and
+// scratch loads wait for every store in flight)
+__device__ __forceinline__ uint32_t vsel(uint32_t c, uint32_t x, uint32_t y) {
+  uint32_t r;
+  asm("v_cmp_ne_u32 vcc, 0, %3\n\tv_cndmask_b32 %0, %1, %2, vcc" : "=v"(r) : "v"(x), "v"(y), "v"(c) : "vcc");
+  return r;
+}
+// a[i], i < 8: a tree of selects on the bits of i
+__device__ __forceinline__ uint32_t pick8(const uint32_t (&a)[8], uint32_t i) {
+  const uint32_t b0 = i & 1u, b1 = i & 2u, b2 = i & 4u;
+  const uint32_t x0 = vsel(b0, a[0], a[1]), x1 = vsel(b0, a[2], a[3]), x2 = vsel(b0, a[4], a[5]), x3 = vsel(b0, a[6], a[7]);
+  return vsel(b2, vsel(b1, x0, x1), vsel(b1, x2, x3));
+}
+
 __device__ __forceinline__ void store_block16(uint8_t* dst, uint64_t a, uint64_t o_lo, uint64_t o_hi,
                                               const uint32_t (&wd)[4], uint32_t have, bool dst_al16) {
   if (have == 0xFu && dst_al16) {
@@ -913,12 +929,7 @@ __device__ __forceinline__ void bin_copy_wave(const uint8_t* __restrict__ bytes,
             const uint32_t c0 = cq & 0xFu;
             const uint32_t dn = cq - c0 * 0x1111u;  // nibbles: 0, or 1 from the start on
             if (dn <= 0x1111u && (dn & 0xEEEEu) == 0) {
-              uint32_t A0 = a[q], A1 = a[q + 1];
-#pragma unroll
-              for (uint32_t t = 1; t <= 4; t++) {
-                A0 = c0 == t ? a[q + t < 8 ? q + t : 7] : A0;
-                A1 = c0 == t ? a[q + t + 1 < 8 ? q + t + 1 : 7] : A1;
-              }
+              const uint32_t A0 = pick8(a, q + c0 < 7u ? q + c0 : 7u), A1 = pick8(a, q + c0 + 1u < 7u ? q + c0 + 1u : 7u);
               const uint32_t hb = (dn & 1u) | ((dn & 0x10u) << 4) | ((dn & 0x100u) << 8) | ((dn & 0x1000u) << 12);
               word = __builtin_amdgcn_perm(A1, A0, 0x03020100u + 4u * hb);
             } else
@@ -926,12 +937,7 @@ __device__ __forceinline__ void bin_copy_wave(const uint8_t* __restrict__ bytes,
 #pragma unroll
             for (uint32_t e = 0; e < 4; e++) {
               const uint32_t c = (uint32_t)(prof >> (4u * (4u * q + e))) & 0xFu;  // 0..4
-              uint32_t v = a[q];
-              v = c == 1u ? a[q + 1] : v;
-              v = c == 2u ? a[q + 2] : v;
-              v = c == 3u ? a[q + 3] : v;
-              v = c == 4u ? a[q + 4] : v;
-              word |= v & (0xFFu << (8u * e));
+              word |= pick8(a, q + c) & (0xFFu << (8u * e));
             }
             }
             const uint32_t d0 = b + 4u * q;
@@ -1044,7 +1050,36 @@ __device__ __forceinline__ uint32_t img4(const uint32_t* img, uint32_t i) {
   return __builtin_amdgcn_alignbyte(img[(i >> 2) + 1], img[i >> 2], i & 3u);
 }
 
-// Value bytes. One workgroup per chunk of CP_VALUES values of one page (chunks[c] = page | j << 32).
+// One 16-byte output block of length-prefixed values composed from staged source bytes: Sv = staged
+// offset of the block's byte 0 counting no value start inside the block; prof nibble i = the value
+// starts (0..4) at or before byte i, each shifting the source by a 4-byte length prefix. An output
+// dword whose bytes shift by at most one start is one v_perm of two byte-aligned source dwords;
+// others are taken byte by byte. Reads up to staged byte Sv + 39. (The source dwords are read from
+// LDS at the computed offsets: a register array indexed by a start count lands in scratch, whose
+// loads wait for every store in flight.)
+__device__ __forceinline__ void compose_block(const uint32_t* img, uint32_t Sv, uint64_t prof, uint32_t (&wd)[4]) {
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    uint32_t word = 0;
+    const uint32_t cq = (uint32_t)(prof >> (16u * q)) & 0xFFFFu;  // counts of bytes 4q .. 4q+3
+    const uint32_t c0 = cq & 0xFu;
+    const uint32_t dn = cq - c0 * 0x1111u;  // nibbles: 0, or 1 from a start inside the dword on
+    if (dn <= 0x1111u && (dn & 0xEEEEu) == 0) {
+      const uint32_t o = Sv + 4u * (q + c0);
+      const uint32_t hb = (dn & 1u) | ((dn & 0x10u) << 4) | ((dn & 0x100u) << 8) | ((dn & 0x1000u) << 12);
+      word = __builtin_amdgcn_perm(img4(img, o + 4u), img4(img, o), 0x03020100u + 4u * hb);
+    } else {
+#pragma unroll
+      for (uint32_t e = 0; e < 4; e++) {
+        const uint32_t c = (uint32_t)(prof >> (4u * (4u * q + e))) & 0xFu;  // 0..4
+        word |= img4(img, Sv + 4u * (q + c)) & (0xFFu << (8u * e));
+      }
+    }
+    wd[q] = word;
+  }
+}
+
+// Value bytes. Workgroups stride over chunks of CP_VALUES values of one page (chunks[c] = page | j << 32).
 // The chunk's source is staged in LDS with coalesced 16-byte loads: the page bytes its values come
 // from (PLAIN: one stream with a 4-byte length prefix before every value; DELTA_LENGTH: the value
 // bytes back to back) or the whole dictionary page (RLE_DICTIONARY: entries in any order). Then
@@ -1060,15 +1095,17 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
                                                        const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                        uint64_t* err, ErrCount err_count) {
   __shared__ __attribute__((aligned(16))) CopyLds S;
-  if (blockIdx.x >= n_chunks) return;
-  const uint64_t ch = chunks[blockIdx.x];
+  int staged = -1;  // column whose dictionary page is in L.img (kept across this workgroup's chunks)
+  for (uint32_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+  __syncthreads();  // the previous chunk's LDS reads are done
+  const uint64_t ch = chunks[c];
   const int page = (int)(uint32_t)ch;
   const uint32_t J = (uint32_t)(ch >> 32);
   const PageWork& pw = work[page];
   const ColumnDev& cd = cols[pw.column];
   const uint32_t nv = uni(pw.n_values);
   const uint32_t i_lo = J * CP_VALUES;
-  if (i_lo >= nv) return;
+  if (i_lo >= nv) continue;
   const uint32_t i_hi = i_lo + CP_VALUES < nv ? i_lo + CP_VALUES : nv;
   const uint32_t n = i_hi - i_lo;
   const uint32_t t = threadIdx.x;
@@ -1097,14 +1134,17 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
     const uint32_t w0 = i_lo + CP_WAVE * wave_id();
     bin_copy_wave(bytes, n_bytes, pw, cd, page, w0 < i_hi ? w0 : i_hi, w0 + CP_WAVE < i_hi ? w0 + CP_WAVE : i_hi,
                   S.w[wave_id()], err, err_count);
-    return;
+    staged = -1;
+    continue;
   }
   CopyWgLds& L = S.g;
   const uint64_t sbase = from_dict ? cd.dict_offset : pw.base;
   const rsrc_t rs = make_rsrc(bytes + sbase, n_bytes - sbase);
   // ---- staging: source bytes [Sa, s_hi) (bytes at or past slim read as 0), value starts, sources
   const uint32_t n_st = (uint32_t)(s_hi - Sa);
-  for (uint32_t o = 16u * t; o < n_st; o += 16u * 64u * WPB) {
+  const bool restage = !(from_dict && staged == pw.column);  // a dictionary page stays staged
+  staged = from_dict ? pw.column : -1;
+  for (uint32_t o = 16u * t; restage && o < n_st; o += 16u * 64u * WPB) {
     u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(Sa + o), 0, 0);
     if (Sa + o + 16u > slim) {
 #pragma unroll
@@ -1158,7 +1198,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
     }
   }
   __syncthreads();
-  if (o_lo >= o_hi) return;
+  if (o_lo >= o_hi) continue;
   uint8_t* dst = cd.binary_data;
   const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
   const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
@@ -1181,39 +1221,10 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
         const uint32_t pj = kk < n ? rel[kk] : 0xFFFFFFFFu;
         if (pj < bend && hole) prof += 0x1111111111111111ull << (4u * (pj - b));
       }
-      const uint32_t Sv = (uint32_t)Sg, A = Sv >> 2, sh = Sv & 3u;
-      uint32_t a[8];
-#pragma unroll
-      for (uint32_t q = 0; q < 8; q++) a[q] = __builtin_amdgcn_alignbyte(img[A + q + 1], img[A + q], sh);
+      compose_block(img, (uint32_t)Sg, prof, wd);
 #pragma unroll
       for (uint32_t q = 0; q < 4; q++) {
-        uint32_t word = 0;
-        const uint32_t cq = (uint32_t)(prof >> (16u * q)) & 0xFFFFu;  // counts of bytes 4q .. 4q+3
-        const uint32_t c0 = cq & 0xFu;
-        const uint32_t dn = cq - c0 * 0x1111u;  // nibbles: 0, or 1 from the start on
-        if (dn <= 0x1111u && (dn & 0xEEEEu) == 0) {
-          uint32_t A0 = a[q], A1 = a[q + 1];
-#pragma unroll
-          for (uint32_t u = 1; u <= 4; u++) {
-            A0 = c0 == u ? a[q + u < 8 ? q + u : 7] : A0;
-            A1 = c0 == u ? a[q + u + 1 < 8 ? q + u + 1 : 7] : A1;
-          }
-          const uint32_t hb = (dn & 1u) | ((dn & 0x10u) << 4) | ((dn & 0x100u) << 8) | ((dn & 0x1000u) << 12);
-          word = __builtin_amdgcn_perm(A1, A0, 0x03020100u + 4u * hb);
-        } else {
-#pragma unroll
-          for (uint32_t e = 0; e < 4; e++) {
-            const uint32_t c = (uint32_t)(prof >> (4u * (4u * q + e))) & 0xFu;  // 0..4
-            uint32_t v = a[q];
-            v = c == 1u ? a[q + 1] : v;
-            v = c == 2u ? a[q + 2] : v;
-            v = c == 3u ? a[q + 3] : v;
-            v = c == 4u ? a[q + 4] : v;
-            word |= v & (0xFFu << (8u * e));
-          }
-        }
         const uint32_t d0 = b + 4u * q;
-        wd[q] = word;
         if (d0 >= r_lo && d0 + 4u <= r_hi) have |= 1u << q;
       }
     } else {
@@ -1243,6 +1254,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
     }
     if (!dst_al4) have = 0;  // unaligned byte buffer (C ABI caller): byte stores only
     store_block16(dst, a0 + b, o_lo, o_hi, wd, have, dst_al16);
+  }
   }
 }
 
@@ -1686,6 +1698,561 @@ __global__ __launch_bounds__(64) void k_dba_carry(const uint8_t* __restrict__ by
 }
 
 // ---------------------------------------------------------------------------
+// PLAIN BYTE_ARRAY columns in one pass (k_bin_bases + k_bin_plain): the walk, the offsets and the
+// value bytes of every 2 KiB tile of a page by one wave, without the per-value length / source
+// scratch, the offset scan and the copy kernel of the per-value path.
+//
+// A PLAIN data section is N values back to back, each a 4-byte length then its bytes
+// (BinaryPlainValuesReader.readBytes :35-42), so value i of a page lands at
+//   offset_i = base(page) + (P_i - data_begin) - 4 i    (P_i: position of its length prefix)
+// in the column's byte buffer, base(page) = the value bytes of the column's earlier pages. A page
+// whose N values end exactly at the section end holds (size - data_begin - 4 N) value bytes, so
+// base() is a prefix sum known before any walk (k_bin_bases). What a tile still needs is i: the
+// number of values that start in the page before it. Each tile walks its own values (the first
+// tile of the section from the section start; the others from a guessed first value start, see
+// k_bin_walk_seg), publishes that count with the guessed entry and its exit, then looks back over
+// up to 64 earlier tiles of the page at once (decoupled look-back): the nearest tile with an
+// inclusive count plus the counts of the tiles after it, provided each of those tiles' entry is the
+// exit of the tile before it (a misspeculated tile is waited for: it corrects itself). Tiles are
+// taken in ticket order, so the tiles looked back on are running or done. The tile then publishes
+// its inclusive count, writes its offsets, and composes its value bytes from the staged tile in
+// LDS into 16-byte stores.
+// A page whose N-th value does not end at the section end (bytes the reader ignores after the
+// values) breaks the base() assumption: the tile holding that value raises a flag and pqg_sync
+// re-runs the plan on the per-value path (k_bin_walk, offset scan, k_bin_copy), which reads
+// exactly N values. Errors are reported at the index the per-value path reports (values past N are
+// not read by the reference and raise nothing).
+constexpr uint32_t BP_NEXT = 4u * WAVE;         // bytes of the next tile staged too (one dword per lane)
+constexpr uint32_t BP_IMG = BW_WIN + BP_NEXT;    // staged bytes per tile (a value reaching past: from memory)
+constexpr uint32_t BP_BLK = BW_WIN / 16u + 2u;  // output blocks that can hold a value start
+constexpr uint64_t BP_NONE = 0xFFFFFFFFull;     // exit of a tile whose chain stopped (error, section end)
+
+struct BinPlainLds {
+  union {
+    BinWalkLds w;                   // the tile walk (candidate list)
+    uint32_t img[BP_IMG / 4 + 16];  // then: page bytes [B, B + BP_IMG) (+ slack for the compose reads)
+  } u;
+  uint32_t acc[BW_CAP + 1];  // accepted value starts of the tile (page positions), ascending
+  uint16_t bt[BP_BLK + 2];   // output block -> the last value starting at or before its first byte
+};
+
+// Candidates of tile [B, B + BW_WIN) from position pos on (see bin_walk_core); returns their number
+// (at most BW_CAP: eff_end is then the first candidate not listed).
+__device__ __forceinline__ uint32_t bp_candidates(BinWalkLds& W, const BwBytes& cur, uint32_t B, uint32_t pos,
+                                                  uint32_t end, uint32_t& eff_end) {
+  const uint32_t lane = lane_id();
+  const uint32_t base = B + BW_Q * lane;
+  uint32_t d[BW_Q / 4 + 1];
+  d[0] = cur.a.x; d[1] = cur.a.y; d[2] = cur.a.z; d[3] = cur.a.w;
+  d[4] = cur.b.x; d[5] = cur.b.y; d[6] = cur.b.z; d[7] = cur.b.w;
+  d[8] = cur.x;
+  uint32_t m = 0;
+  const int32_t rem0 = (int32_t)(end - 4u - base);
+#pragma unroll
+  for (uint32_t q = 0; q < BW_Q; q++) {
+    const uint32_t len = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
+    const int32_t rem = rem0 - (int32_t)q;
+    m |= (rem >= 0 && len <= (uint32_t)rem ? 1u : 0u) << q;
+  }
+  if (base < pos) m &= pos - base >= BW_Q ? 0u : ~((1u << (pos - base)) - 1u);
+  uint32_t total;
+  const uint32_t rank = wave_excl_scan_u32((uint32_t)__builtin_popcount(m), &total);
+  uint32_t mm = m, r = rank;
+  while (mm) {
+    const uint32_t q = (uint32_t)__builtin_ctz(mm);
+    mm &= mm - 1u;
+    if (r < BW_CAP) {
+      const uint32_t i = q >> 2;
+      uint32_t lo = d[0], hi = d[1];
+#pragma unroll
+      for (uint32_t t = 1; t < BW_Q / 4; t++) {
+        const bool s = i == t;
+        lo = s ? d[t] : lo;
+        hi = s ? d[t + 1] : hi;
+      }
+      const uint32_t nx = base + q + 4u + __builtin_amdgcn_alignbyte(hi, lo, q & 3u);
+      *(uint64_t*)&W.pn[r] = (uint64_t)(base + q) | ((uint64_t)nx << 32);
+    } else if (r == BW_CAP) {
+      W.cut = base + q;
+    }
+    r++;
+  }
+  W.mr[lane] = uint2{m, rank};
+  wave_sync();
+  total = uni(total);
+  eff_end = total > BW_CAP ? uni(W.cut) : B + BW_WIN;
+  return total > BW_CAP ? BW_CAP : total;
+}
+
+struct BpWalk {
+  uint32_t pos, n;  // where the chain left the tile (or stopped), values accepted
+  int code;         // the error that stopped it (PQG_ERR_EOF also at the section end)
+};
+
+struct BpGuess {
+  uint32_t pos, index, total, eff_end;  // guessed start (0xFFFFFFFF: none), its candidate index, the list
+};
+
+// The chain from pos through tile [B, B + BW_WIN): accepted value starts to L.acc[0, n). With
+// list0 < BW_CAP the candidate list of the whole tile is already in LDS (bp_guess) and pos is its
+// candidate list0 (total0 candidates, listed up to eff0).
+__device__ BpWalk bp_walk(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint32_t B, uint32_t pos, uint32_t end,
+                          uint32_t list0 = 0xFFFFFFFFu, uint32_t total0 = 0, uint32_t eff0 = 0) {
+  BinWalkLds& W = L.u.w;
+  const uint32_t lane = lane_id();
+  uint32_t n = 0;
+  int code = 0;
+  const uint32_t tend = B + BW_WIN;
+  bool listed = list0 < BW_CAP;
+  while (true) {
+    pos = uni(pos);
+    n = uni(n);
+    if (pos >= tend) break;
+    if ((uint64_t)pos + 4u > end) { code = PQG_ERR_EOF; break; }
+    uint32_t eff_end, total, i0 = 0;
+    if (listed) {  // the guess's list, from the guessed candidate on
+      total = total0;
+      eff_end = eff0;
+      i0 = list0;
+      listed = false;
+    } else {
+      wave_sync();  // the previous pass's list reads are done
+      total = bp_candidates(W, cur, B, pos, end, eff_end);
+    }
+    if (total == 0 || W.pn[i0].x != pos) {
+      code = bin_value_error(rs, pos, end, false);
+      break;
+    }
+    bool leave = false;
+    while (true) {
+      i0 = uni(i0);
+      n = uni(n);
+      const uint32_t k = i0 + lane;
+      const uint32_t s = k < total ? W.pn[k].y : 0xFFFFFFFFu;
+      const uint32_t so = s - B;
+      const uint32_t t = so < BW_WIN ? bw_index(W, so) : 0xFFFFu;
+      const bool hit = t < total && t > k && t - i0 < WAVE;
+      const uint32_t J = hit ? t - i0 : WAVE;
+      const uint64_t next1 = __ballot(hit && t == k + 1);
+      uint32_t last = ~next1 ? (uint32_t)__builtin_ctzll(~next1) : WAVE - 1u;
+      uint64_t mask = last == WAVE - 1u ? ~0ull : ((1ull << (last + 1u)) - 1ull);
+      if (rdl(J, last) < WAVE) {  // a false candidate inside the batch: binary lifting from lane 0
+        uint32_t P[6];
+        P[0] = J;
+#pragma unroll
+        for (int q = 1; q < 6; q++) {
+          const uint32_t g = (uint32_t)__shfl((int)P[q - 1], (int)(P[q - 1] & (WAVE - 1u)));
+          P[q] = P[q - 1] < WAVE ? g : WAVE;
+        }
+        uint32_t x = 0;
+#pragma unroll
+        for (int q = 5; q >= 0; q--) {
+          const uint32_t y = (uint32_t)__shfl((int)P[q], (int)x);
+          if (y <= lane) x = y;
+        }
+        mask = __ballot(x == lane);
+        last = 63u - (uint32_t)__builtin_clzll(mask);
+      }
+      const uint32_t rank = (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1ull));
+      if ((mask >> lane) & 1ull) L.acc[n + rank] = W.pn[k].x;
+      n += (uint32_t)__builtin_popcountll(mask);
+      const uint32_t nxt = rdl(s, last);  // successor of the batch's last value
+      pos = nxt;
+      if (nxt >= eff_end) { leave = true; break; }
+      const uint32_t a = uni(bw_index(W, nxt - B));
+      if (a >= total || a <= i0 + last) {
+        code = bin_value_error(rs, nxt, end, false);
+        break;
+      }
+      i0 = a;
+    }
+    if (code || !leave) break;
+  }
+  wave_sync();
+  return BpWalk{uni(pos), uni(n), code};
+}
+
+// Guessed first value start of tile [B, B + BW_WIN) (a tile after the one holding the section
+// start). A false candidate (typically the byte before a length prefix, which reads as a length of
+// 256 x the true one) jumps far and lands, by chance, on the true chain about once in 20 tiles: a
+// "first candidate whose links hold" rule picks it then. So every candidate's chain is followed to
+// where it leaves the tile (pointer jumping over the candidate list: 9 rounds for 512 candidates)
+// and the guess is the candidate with the most values on its chain among the first 64 whose chains
+// stay on candidates (the true start's chain holds every true value start of the tile; a false chain
+// that merges into it skips the values it jumps over), ties to the earliest; a chain that leaves the
+// tile within SEG_LINKS links is checked on in memory. 0xFFFFFFFF when no candidate qualifies.
+__device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint32_t B, uint32_t end) {
+  BinWalkLds& W = L.u.w;
+  uint32_t eff_end;
+  const uint32_t total = bp_candidates(W, cur, B, B, end, eff_end);
+  const uint32_t lane = lane_id();
+  // node i: J = successor index, or (last index | 0x8000) once the chain leaves the list, 0xFFFF when
+  // it breaks; D = values on the chain so far (L.acc as scratch: J | D << 16)
+  constexpr uint32_t NP = BW_CAP / WAVE;  // nodes per lane
+  constexpr uint32_t XF = 0x8000u, BAD = 0xFFFFu;
+#pragma unroll
+  for (uint32_t j = 0; j < NP; j++) {
+    const uint32_t i = lane + WAVE * j;
+    uint32_t e = BAD | (1u << 16);
+    if (i < total) {
+      const uint32_t q = W.pn[i].y;
+      const uint32_t t = q < eff_end ? bw_index(W, q - B) : 0xFFFFu;
+      e = (q >= eff_end || q == end ? (i | XF) : (t < total ? t : BAD)) | (1u << 16);  // (end: the last value)
+    }
+    L.acc[i] = e;
+  }
+  wave_sync();
+  for (uint32_t r = 0; r < 9; r++) {
+    uint32_t v[NP];
+#pragma unroll
+    for (uint32_t j = 0; j < NP; j++) {
+      const uint32_t i = lane + WAVE * j;
+      const uint32_t e = L.acc[i];
+      const uint32_t J = e & 0xFFFFu;
+      v[j] = e;
+      if (J < XF) {  // not terminal: jump
+        const uint32_t f = L.acc[J];
+        v[j] = (f & 0xFFFFu) == BAD ? (BAD | (e & 0xFFFF0000u)) : ((f & 0xFFFFu) | ((e >> 16) + (f >> 16)) << 16);
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (uint32_t j = 0; j < NP; j++) L.acc[lane + WAVE * j] = v[j];
+    wave_sync();
+  }
+  const uint32_t e = lane < total ? L.acc[lane] : BAD;
+  const uint32_t J = e & 0xFFFFu;
+  uint32_t d = e >> 16;
+  bool ok = lane < total && J != BAD && (J & XF);
+  uint32_t dmax = ok ? d : 0u;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t y = (uint32_t)__shfl_xor((int)dmax, o);
+    dmax = y > dmax ? y : dmax;
+  }
+  // a chain of SEG_LINKS values inside the tile needs no further check; otherwise (long values) the
+  // chains that leave the tile early are checked on in memory
+  if (uni(dmax) < SEG_LINKS && ok) {
+    uint32_t q = W.pn[J & 0x1FFu].y;
+    for (uint32_t i = d; i < SEG_LINKS && ok; i++) {
+      if (q >= end) break;  // the chain reaches the section end: nothing contradicts it
+      ok = seg_candidate(rs, q, end);
+      q = q + 4u + ld4_any(rs, q);
+    }
+  }
+  // the most values on the chain, ties to the earliest candidate
+  uint32_t key = ok ? (d << 8) | (255u - lane) : 0u;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t y = (uint32_t)__shfl_xor((int)key, o);
+    key = y > key ? y : key;
+  }
+  key = uni(key);
+  const uint32_t gi = 255u - (key & 0xFFu);
+  const uint32_t g = key ? uni(W.pn[gi].x) : 0xFFFFFFFFu;
+  wave_sync();
+  return BpGuess{g, gi, total, eff_end};
+}
+
+__global__ __launch_bounds__(64 * WPB) void k_bin_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                        const PageWork* __restrict__ work,
+                                                        const ColumnDev* __restrict__ cols,
+                                                        const uint64_t* __restrict__ segs, uint32_t n_segs,
+                                                        uint64_t* aggw, uint64_t* incw, uint32_t* ticket,
+                                                        uint32_t epoch, uint32_t* inexact, uint32_t flag_epoch,
+                                                        uint64_t* err, ErrCount err_count) {
+  __shared__ __attribute__((aligned(16))) BinPlainLds lds_all[WPB];
+  const uint32_t lane = lane_id();
+  // Tile t = workgroup order: workgroups are dispatched in index order, so the tiles a tile waits for
+  // hold a slot (one atomic ticket per 2 KiB tile serialized on one address and dominated the kernel).
+  // That order is not promised by the programming model: a wait that times out hands the plan to the
+  // per-value path (the inexact flag) instead of failing the decode.
+  const uint32_t t = blockIdx.x * WPB + wave_id();
+  (void)ticket;
+  if (t >= n_segs) return;
+#ifdef PQG_DIAG
+  const uint64_t dg0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t dg1 = 0, dg2 = 0, dg_polls = 0, dg_guess = 0;
+#endif
+  BinPlainLds& L = lds_all[wave_id()];
+  const uint64_t sg = segs[t];
+  const int page = (int)(uint32_t)sg;
+  const uint32_t s = (uint32_t)(sg >> 32);  // tile of the page: bytes [s BW_WIN, (s + 1) BW_WIN)
+  const PageWork& pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t beg = uni(pw.data_begin), end = uni(pw.size), N = uni(pw.n_values);
+  const uint32_t B = s * BW_WIN;
+  const uint64_t E = (uint64_t)epoch << 56;
+  const uint32_t s0 = beg / BW_WIN;  // the tile holding the section start
+  if (s < s0 || N == 0 || beg >= end || B >= end) {  // no value starts here
+    if (lane == 0) {
+      sst(incw + t, E | BP_NONE);
+      if (s == 0 && N > 0 && beg >= end) report(err, err_count, page, 2, 0, PQG_ERR_EOF);  // no section: value 0
+      if (s == 0 && N == 0 && beg < end) sst(inexact, flag_epoch);  // bytes but no values: base() assumes none
+    }
+    return;
+  }
+  const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  const BwBytes cur = bw_load(rs, B);
+  const uint32_t nxt = ld32(rs, B + BW_WIN + 4u * lane);  // the next tile's first BP_NEXT bytes
+  const bool first = s == s0;
+  const BpGuess gs = first ? BpGuess{beg, 0xFFFFFFFFu, 0, 0} : bp_guess(L, cur, rs, B, end);
+  uint32_t entry = gs.pos;
+#ifdef PQG_DIAG
+  dg_polls = __builtin_amdgcn_s_memrealtime() + (entry == 7u ? 1u : 0u);  // (after the guess; polls below)
+#endif
+  BpWalk r{entry, 0, 0};
+  if (entry != 0xFFFFFFFFu) {
+    r = first ? bp_walk(L, cur, rs, B, entry, end) : bp_walk(L, cur, rs, B, entry, end, gs.index, gs.total, gs.eff_end);
+    if (!first && lane == 0)  // speculative: count, guessed entry, exit, stop
+      sst(aggw + t, E | ((uint64_t)r.n << 46) | ((uint64_t)(entry - B) << 35) | ((uint64_t)(r.code ? 1u : 0u) << 34) |
+                        (uint64_t)r.pos);
+  }
+  uint32_t before = 0;
+  bool stopped = false;
+#ifdef PQG_DIAG
+  dg1 = __builtin_amdgcn_s_memrealtime() + (r.n > 0xFFFFFFF0u ? 1u : 0u);
+#endif
+#ifdef PQG_DIAG_NOLOOKBACK  // diagnostic build only: timing without the look-back (wrong offsets)
+  if (false) {
+#else
+  if (!first) {
+#endif
+    const uint64_t t_wait = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      // lane l: the tile l + 1 before this one (down to the first tile of the section)
+      const bool valid = s >= s0 + 1u + lane;
+      const uint32_t u = t - 1u - lane;
+      const uint64_t iw = valid ? sld(incw + u) : 0ull;
+      const bool inc = valid && (uint32_t)(iw >> 56) == epoch;
+      const uint64_t aw = valid && !inc ? sld(aggw + u) : 0ull;
+      const bool agg = valid && !inc && (uint32_t)(aw >> 56) == epoch;
+      const uint64_t bi = __ballot(inc);
+      const uint32_t F = bi ? (uint32_t)__builtin_ctzll(bi) : WAVE;  // the nearest inclusive count
+      const uint64_t below = F >= WAVE ? ~0ull : ((1ull << F) - 1ull);
+      if (F < WAVE && (__ballot(agg) & below) == below) {
+        const uint32_t ex = inc ? (uint32_t)iw : (uint32_t)aw;
+        const bool stp = inc ? ex == 0xFFFFFFFFu : ((aw >> 34) & 1ull) != 0;
+        const uint32_t cnt = inc ? (uint32_t)(iw >> 32) & 0xFFFFFFu : (uint32_t)(aw >> 46) & 0x3FFu;
+        const uint32_t ent = (s - 1u - lane) * BW_WIN + ((uint32_t)(aw >> 35) & 0x7FFu);
+        // the earliest stopped tile from F on (highest lane): the tiles after it hold no values
+        const uint64_t bs = __ballot(stp && lane <= F);
+        const uint32_t S = bs ? 63u - (uint32_t)__builtin_clzll(bs) : WAVE;
+        const uint32_t lo = S < WAVE ? S : 0u;
+        const uint32_t nex = (uint32_t)__shfl_down((int)ex, 1);  // exit of the tile before this lane's
+        const bool link = lane < lo || lane >= F || ent == nex;
+        if (__ballot(!link) == 0ull) {
+          const uint32_t c = lane >= lo && lane <= F ? cnt : 0u;
+          uint32_t sum = c;
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o);
+          before = uni(sum);
+          if (S < WAVE) {
+            stopped = true;
+          } else {
+            const uint32_t ex0 = uni(rdl(ex, 0));  // where the chain enters this tile
+#ifdef PQG_DIAG
+            dg_guess = ex0 == entry ? 1u : 0u;
+#endif
+            if (ex0 != entry) {                    // misspeculated (or no guess): walk from there
+              entry = ex0;
+              r = ex0 >= B + BW_WIN ? BpWalk{ex0, 0, 0} : bp_walk(L, cur, rs, B, ex0, end);
+            }
+          }
+          break;
+        }
+      }
+      __builtin_amdgcn_s_sleep(2);
+      // bounded (s_memrealtime: 100 MHz): a tile that never publishes sends the plan to the per-value
+      // path (pqg_sync re-runs it), not a hang
+      if (__builtin_amdgcn_s_memrealtime() - t_wait > 200000000ull) {
+        if (lane == 0) {
+          sst(inexact, flag_epoch);
+          sst(incw + t, E | BP_NONE);
+        }
+        return;
+      }
+    }
+  }
+  const uint32_t n = stopped ? 0u : r.n;
+  const uint32_t incl = before + n < 0xFFFFFFu ? before + n : 0xFFFFFFu;
+#ifdef PQG_DIAG
+  dg2 = __builtin_amdgcn_s_memrealtime() + (n > 0xFFFFFFF0u ? 1u : 0u);
+  struct DgBp {
+    uint64_t a, *b, *c, *d, *e;
+    uint32_t t;
+    __device__ ~DgBp() {
+      if (pqg_diag_bp && lane_id() == 0) {
+        uint64_t* o = pqg_diag_bp + 8 * (uint64_t)t;
+        o[0] = a; o[1] = *b; o[2] = *c; o[3] = __builtin_amdgcn_s_memrealtime(); o[4] = *d; o[5] = *e;
+      }
+    }
+  } dg_out{dg0, &dg1, &dg2, &dg_polls, &dg_guess, t};
+#endif
+  if (lane == 0) sst(incw + t, E | ((uint64_t)incl << 32) | (stopped || r.code ? BP_NONE : (uint64_t)r.pos));
+  if (stopped || before >= N) return;
+  if (r.code && before + r.n < N && lane == 0) report(err, err_count, page, 2, before + r.n, r.code);
+  if (before + r.n >= N) {  // the page's last value is here: it must end at the section end
+    const uint32_t q = N - 1u - before;
+    const uint32_t e_last = q + 1u < r.n ? L.acc[q + 1u] : r.pos;
+    if ((q + 1u < r.n || e_last != end) && lane == 0) sst(inexact, flag_epoch);
+  }
+  const uint32_t m = r.n < N - before ? r.n : N - before;
+  if (m == 0) return;
+  // ---- offsets of values before .. before + m (the last one: the end of value m - 1)
+  const uint32_t rpos = r.pos;
+  auto pos_k = [&](uint32_t k) -> uint32_t { return k < r.n ? L.acc[k] : rpos; };
+  int64_t* offs = (int64_t*)cd.values + pw.out_offset + before;
+  const uint64_t bb = pw.bin_base;
+  for (uint32_t k = lane; k <= m; k += WAVE)
+    gst(offs + k, (int64_t)(bb + (uint64_t)(pos_k(k) - beg) - 4ull * (uint64_t)(before + k)));
+  const uint64_t o_lo = bb + (uint64_t)(pos_k(0) - beg) - 4ull * before;
+  const uint64_t o_hi0 = bb + (uint64_t)(pos_k(m) - beg) - 4ull * (uint64_t)(before + m);
+  const uint64_t o_hi = o_hi0 < cd.binary_capacity ? o_hi0 : cd.binary_capacity;  // overflow: reported at sync
+  if (o_lo >= o_hi) return;
+  // ---- value bytes: stage the tile and the start of the next one (the walk's registers), then
+  // compose 16-byte output blocks from LDS (a value reaching further: the rest from memory)
+  wave_sync();  // the walk's candidate list is dead
+  {
+    uint32_t* img = L.u.img;
+    *(u32x4*)&img[8u * lane] = cur.a;
+    *(u32x4*)&img[8u * lane + 4u] = cur.b;
+    img[BW_WIN / 4u + lane] = nxt;
+  }
+  const uint64_t a0 = o_lo & ~15ull;
+  const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
+  const uint32_t P0 = pos_k(0);
+  auto rel = [&](uint32_t k) -> uint32_t { return (pos_k(k) - P0) - 4u * k + r_lo; };  // k <= m
+  for (uint32_t i = lane; i < BP_BLK; i += WAVE) L.bt[i] = 0;
+  wave_sync();
+  for (uint32_t k = lane; k < m; k += WAVE) {
+    const uint32_t blk = (rel(k) + 15u) >> 4;
+    if (blk < BP_BLK && (k + 1u == m || ((rel(k + 1u) + 15u) >> 4) != blk)) L.bt[blk] = (uint16_t)k;
+  }
+  wave_sync();
+  {  // running maximum over the blocks: 3 consecutive entries per lane, then across lanes
+    constexpr uint32_t PER = (BP_BLK + WAVE - 1u) / WAVE;
+    uint32_t v[PER], mx = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t i = PER * lane + j;
+      v[j] = i < BP_BLK ? L.bt[i] : 0u;
+      mx = v[j] > mx ? v[j] : mx;
+    }
+    uint32_t inc = mx;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+      if ((int)lane >= o) inc = y > inc ? y : inc;
+    }
+    uint32_t run = (uint32_t)__shfl_up((int)inc, 1);
+    if (lane == 0) run = 0;
+    wave_sync();
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t i = PER * lane + j;
+      run = v[j] > run ? v[j] : run;
+      if (i < BP_BLK) L.bt[i] = (uint16_t)run;
+    }
+  }
+  wave_sync();
+  uint8_t* dst = cd.binary_data;
+  const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
+  const uint32_t* img = L.u.img;
+  for (uint32_t b = 16u * lane; b < r_hi; b += 16u * WAVE) {
+    const uint32_t kv = (b >> 4) < BP_BLK ? L.bt[b >> 4] : m - 1u;  // value of the block's first byte
+    const uint32_t bend = b + 16u < r_hi ? b + 16u : r_hi;
+    const uint32_t rkv = rel(kv);
+    const int64_t Sg = (int64_t)(pos_k(kv) + 4u - B) + (int64_t)b - (int64_t)rkv;  // staged offset of block byte 0
+    uint32_t wd[4];
+    uint32_t have = 0;
+    const bool compose = !(kv + 5u < m && rel(kv + 5u) < bend) && Sg >= 0 && Sg + 36 <= (int64_t)BP_IMG;
+    if (compose) {
+      uint64_t prof = 0;  // nibble i: value starts at or before byte i of the block
+#pragma unroll
+      for (uint32_t j = 1; j <= 4; j++) {
+        const uint32_t kk = kv + j;
+        const uint32_t pj = kk < m ? rel(kk) : 0xFFFFFFFFu;
+        if (pj < bend) prof += 0x1111111111111111ull << (4u * (pj - b));
+      }
+      compose_block(img, (uint32_t)Sg, prof, wd);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t d0 = b + 4u * q;
+        if (d0 >= r_lo && d0 + 4u <= r_hi) have |= 1u << q;
+      }
+    } else {
+      uint32_t k = kv;
+      uint32_t k_end = rel(k + 1u);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t d0 = b + 4u * q;
+        const uint32_t x0 = d0 > r_lo ? d0 : r_lo, x1 = d0 + 4u < r_hi ? d0 + 4u : r_hi;
+        uint32_t word = 0;
+        for (uint32_t c = x0; c < x1;) {
+          while (k + 1u < m && c >= k_end) {
+            k++;
+            k_end = rel(k + 1u);
+          }
+          const uint32_t seg_end = x1 < k_end ? x1 : k_end;
+          const uint32_t sp = pos_k(k) + 4u - B + (c - rel(k));  // page-relative: B + sp
+          const uint32_t v = sp + 4u <= BP_IMG ? img4(img, sp) : ld4_any(rs, B + sp);
+          const uint32_t nb = seg_end - c;
+          const uint32_t msk = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
+          word |= (v & msk) << (8u * (c - d0));
+          c = seg_end;
+        }
+        wd[q] = word;
+        if (x0 == d0 && x1 == d0 + 4u) have |= 1u << q;
+      }
+    }
+    if (!dst_al4) have = 0;  // unaligned byte buffer (C ABI caller): byte stores only
+    store_block16(dst, a0 + b, o_lo, o_hi, wd, have, dst_al16);
+  }
+}
+
+// base(page) of every page of the PLAIN-only BYTE_ARRAY columns (one workgroup per column, pages in
+// column order): the value bytes of the column's earlier pages, each page taken as filling its data
+// section (size - data_begin - 4 n_values; k_bin_plain checks it); the column total -> bin_total
+// (compared with binary_capacity at sync).
+__global__ __launch_bounds__(256) void k_bin_bases(PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                                   const int32_t* __restrict__ col_pages,
+                                                   const int32_t* __restrict__ col_start) {
+  const int b = col_start[blockIdx.x], e = col_start[blockIdx.x + 1];
+  __shared__ uint64_t wsum[4];
+  __shared__ uint64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = b; base < e; base += 256) {
+    const int i = base + (int)threadIdx.x;
+    uint64_t v = 0;
+    if (i < e) {
+      const PageWork& w = work[col_pages[i]];
+      const uint64_t need = (uint64_t)w.data_begin + 4ull * w.n_values;
+      v = w.size > need ? w.size - need : 0;
+    }
+    uint64_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o);
+      if ((int)lane_id() >= o) x += y;
+    }
+    if (lane_id() == 63) wsum[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint64_t pre = carry;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) pre += wsum[w];
+    if (i < e) gst(&work[col_pages[i]].bin_base, pre + x - v);
+    __syncthreads();
+    if (threadIdx.x == 255) carry = pre + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && e > b) {
+    const ColumnDev& cd = cols[work[col_pages[b]].column];
+    gst(cd.bin_total, carry);
+    gst((int64_t*)cd.values, (int64_t)0);  // offsets[0] (also when the column has no values)
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Launchers
 
 #define PQG_BIN_ARGS bytes, n_bytes, work, cols, list, n, err, err_count
@@ -1712,6 +2279,18 @@ hipError_t launch_bin_walk_seg(hipStream_t st, const uint8_t* bytes, uint64_t n_
   if (n_segs == 0) return hipSuccess;
   hipLaunchKernelGGL(k_bin_walk_seg, dim3((n_segs + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols,
                      segs, n_segs, status, ticket, tmp, err, err_count);
+  return hipGetLastError();
+}
+
+hipError_t launch_bin_plain(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
+                            const int32_t* col_pages, const int32_t* col_start, int n_cols, const uint64_t* segs,
+                            uint32_t n_segs, uint64_t* aggw, uint64_t* incw, uint32_t* ticket, uint32_t epoch,
+                            uint32_t* inexact, uint32_t flag_epoch, uint64_t* err, ErrCount err_count) {
+  if (n_cols <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bin_bases, dim3(n_cols), dim3(256), 0, st, work, cols, col_pages, col_start);
+  if (n_segs)
+    hipLaunchKernelGGL(k_bin_plain, dim3((n_segs + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols,
+                       segs, n_segs, aggw, incw, ticket, epoch, inexact, flag_epoch, err, err_count);
   return hipGetLastError();
 }
 
@@ -1760,9 +2339,19 @@ hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
                            const ColumnDev* cols, const uint64_t* chunks, uint32_t n_chunks, uint64_t* err,
                            ErrCount err_count) {
   if (n_chunks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_bin_copy, dim3(n_chunks), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, chunks, n_chunks,
-                     err, err_count);
+  // one resident round of workgroups (5 per CU at ~31 KiB of LDS each) striding over the chunks: a
+  // dictionary page stays staged across a workgroup's chunks of the same column
+  constexpr uint32_t CP_GRID = 256u * 5u;
+  hipLaunchKernelGGL(k_bin_copy, dim3(n_chunks < CP_GRID ? n_chunks : CP_GRID), dim3(64 * WPB), 0, st, bytes, n_bytes,
+                     work, cols, chunks, n_chunks, err, err_count);
   return hipGetLastError();
 }
 
 }  // namespace pqg
+
+#ifdef PQG_DIAG
+// Diagnostic build only (tools/diag_binplain.py): per k_bin_plain tile, 8 u64 (see pqg_diag_bp).
+extern "C" int pqg_diag_bp_set(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(pqg::pqg_diag_bp), &p, sizeof(p)) == hipSuccess ? 0 : 3;
+}
+#endif

@@ -31,6 +31,7 @@ static __device__ uint64_t* pqg_diag_buf;
 static __device__ uint64_t* pqg_diag_wrt;  // per page: s_memrealtime at walk start / publish
 static __device__ uint64_t* pqg_diag_xrt;  // per chunk: start, flag seen, end, (page | cu << 32)
 static __device__ uint64_t* pqg_diag_wph;  // per page: list-walk cycles (predecode, chain, emit), windows, batches, runs
+static __device__ uint64_t* pqg_diag_bp;   // per k_bin_plain tile: start, walked, looked back, end (s_memrealtime), polls, guess ok
 #define DIAG_T(v) uint64_t v = __builtin_amdgcn_s_memtime()
 #define DIAG_ADD(acc, t0) acc += __builtin_amdgcn_s_memtime() - (t0)
 #else

@@ -59,6 +59,7 @@ struct PageWork {
   uint32_t reserved;    // DELTA_BYTE_ARRAY (set by k_delta): 0 chunk-parallel copy, 1 serial copy, 2 carry chain
   uint32_t pflags;      // pqg_page_desc.flags (PQG_PAGE_DBA_CARRY)
   uint32_t pad0;
+  uint64_t bin_base;    // PLAIN-only BYTE_ARRAY columns (k_bin_bases): value bytes of the column's earlier pages
 };
 
 // Error counter handle passed to every kernel. Error words and the counter are tagged with the
@@ -112,7 +113,11 @@ hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_
 // ZSTD frames per job (pqgpu_zstd.hip): a grid of at most ZSTD_GRID one-wave workgroups loops over
 // the jobs; scratch = min(n_jobs, ZSTD_GRID) x ZSTD_LIT_SCRATCH bytes of literal buffers (<= 512 MiB)
 constexpr uint64_t ZSTD_LIT_SCRATCH = 131072;
+#ifdef PQG_AB_ZGRID  // (A/B builds under abx/ only)
+constexpr uint32_t ZSTD_GRID = PQG_AB_ZGRID;
+#else
 constexpr uint32_t ZSTD_GRID = 4096;
+#endif
 hipError_t launch_zstd(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
                        const pqg_snappy_job* jobs, int n_jobs, int32_t* status, uint8_t* scratch);
 hipError_t launch_snappy(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
@@ -148,6 +153,16 @@ hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, Pa
 hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, int dict_walk, int n_pages,
                            uint64_t* err, ErrCount err_count);
+// PLAIN-only BYTE_ARRAY columns in one pass: k_bin_bases (one workgroup per column, pages in column
+// order in col_pages[col_start[c], col_start[c + 1])) then k_bin_plain over the 2 KiB tiles `segs`
+// (page | tile << 32, in column / page / tile order). aggw / incw: per tile, tagged with `epoch`
+// (1..255; zeroed when it wraps); ticket: zeroed before the launch; inexact: set to flag_epoch when a
+// page's values do not end at its section end (the plan is then re-run on the per-value path).
+constexpr uint32_t BP_TILE = 2048;
+hipError_t launch_bin_plain(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
+                            const int32_t* col_pages, const int32_t* col_start, int n_cols, const uint64_t* segs,
+                            uint32_t n_segs, uint64_t* aggw, uint64_t* incw, uint32_t* ticket, uint32_t epoch,
+                            uint32_t* inexact, uint32_t flag_epoch, uint64_t* err, ErrCount err_count);
 hipError_t launch_bin_walk_seg(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const uint64_t* segs, uint32_t n_segs, uint64_t* status,
                                uint32_t* ticket, uint32_t* tmp, uint64_t* err, ErrCount err_count);

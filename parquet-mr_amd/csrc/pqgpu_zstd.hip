@@ -31,23 +31,51 @@ constexpr uint32_t ZS_CAP = 512;      // output bytes per execution batch
 constexpr uint32_t ZS_LIT = 0x80000000u;  // byte source tag: a literal of the batch (| its index)
 constexpr uint32_t ZS_FLUSH = 1024;   // ring bytes written to HBM once this many are pending
 
-struct ZWaveLds {
-  uint32_t ll[512], ml[512], of[256];  // FSE decoding entries: sym | nb << 8 | base << 16
+// Sequence-section decoder state of the current block, kept in LDS between batches: the decode loop
+// (zseq_decode) is a function of its own, so its state lives in SGPRs without the register pressure
+// of the whole job's code around it (inlined, the loop's state was spilled to VGPR lanes and every
+// uniform test went through the vector unit: ~2,200 cycles per sequence).
+struct ZSeq {
+  uint64_t src, src_len;          // the job's input (the function builds its own buffer resource)
+  uint64_t c;                     // bit container (BackBits)
+  int32_t bits, cbit;
+  uint32_t wlo, base, n;
+  uint32_t sl, so, sm;            // FSE states
+  uint32_t rep0, rep1, rep2;      // repeat offsets
+  uint32_t i, nseq;               // sequences decoded / in the block
+  uint32_t outp, lits, regen, frame0;  // output position and literals after the decoded sequences
+  uint32_t m, T, blit, pend;      // result of a call: batch size, bytes, literals; 1: a sequence is
+                                  // carried to the next batch, 2: it is longer than a batch
+};
+
+// The literal / table-description phase of a block and its sequence execution never overlap, so
+// their scratch shares LDS (18.2 KiB per wave instead of 20.8: 8 waves per CU instead of 7).
+struct ZLitLds {
   uint32_t hw[64];                     // FSE table of compressed Huffman weights (accuracy <= 6)
-  uint16_t huf[2048];                  // Huffman decoding entries: sym | nb << 8
-  uint8_t ring[ZS_RING];
-  uint8_t win[ZS_WIN + 16];
   uint8_t hwin[4][ZS_HWIN + 16];
   int16_t norm[256];
   uint8_t wts[256];
   uint16_t nxt[256];
+};
+struct ZExecLds {
+  uint32_t src[ZS_CAP];                // batch output byte -> literal index (| ZS_LIT) or output position
+  uint8_t lseg[ZS_CAP + 16];           // the batch's literal bytes
+};
+struct ZWaveLds {
+  uint32_t ll[512], ml[512], of[256];  // FSE decoding entries: sym | nb << 8 | base << 16
+  uint16_t huf[2048];                  // Huffman decoding entries: sym | nb << 8 (kept for treeless blocks)
+  uint8_t ring[ZS_RING];
+  uint8_t win[ZS_WIN + 16];
+  union {
+    ZLitLds t;
+    ZExecLds x;
+  } ph;
   uint32_t flag;
   uint32_t sq_ll[ZS_SB + 1], sq_ml[ZS_SB + 1], sq_of[ZS_SB + 1];  // decoded sequences of one batch (+ the carried one)
-  uint32_t src[ZS_CAP];               // batch output byte -> literal index (| ZS_LIT) or output position
-  uint8_t lseg[ZS_CAP + 16];          // the batch's literal bytes
   uint32_t llcode[36], mlcode[53];     // literal / match length codes: baseline | extra bits << 24
+  ZSeq ss;
 #ifdef PQG_DIAG
-  uint64_t diag[8];                   // diagnostic build: cycles per phase of the current job
+  uint64_t diag[12];                  // diagnostic build: cycles per phase of the current job
 #endif
 };
 
@@ -61,7 +89,11 @@ extern "C" int pqg_diag_zstd_set(void* p) {
 #define ZD_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define ZD_ADD(L, i, t0) ((L).diag[i] += __builtin_amdgcn_s_memtime() - (t0))
 #define ZD_CNT(L, i, n) ((L).diag[i] += (n))
+#define ZQ(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define ZQ_ADD(acc, a, b) (acc) += (b) - (a)
 #else
+#define ZQ(v)
+#define ZQ_ADD(acc, a, b)
 #define ZD_T(v)
 #define ZD_ADD(L, i, t0)
 #define ZD_CNT(L, i, n)
@@ -224,8 +256,8 @@ struct LaneBits {
 
 // FSE decoding table from normalized counts (RFC 8878 §4.1.1), wave-uniform; entries in `tab`.
 __device__ bool zfse_build(ZWaveLds& L, uint32_t* tab, int nsym, int log) {
-  int16_t* norm = L.norm;
-  uint16_t* nxt = L.nxt;
+  int16_t* norm = L.ph.t.norm;
+  uint16_t* nxt = L.ph.t.nxt;
   const int size = 1 << log;
   int high = size - 1;
   const uint32_t lane = lane_id();
@@ -295,7 +327,7 @@ __device__ int64_t zread_ncount(rsrc_t rs, uint32_t o, uint32_t lim, int max_log
 __device__ bool zseq_table(ZWaveLds& L, uint32_t* tab, int* tlog, bool& have, int mode, rsrc_t rs, uint32_t& q,
                            uint32_t lim, const int16_t* def, int def_n, int def_log, int max_log, int max_sym) {
   if (mode == 0) {
-    if (lane_id() < (uint32_t)def_n) L.norm[lane_id()] = def[lane_id()];
+    if (lane_id() < (uint32_t)def_n) L.ph.t.norm[lane_id()] = def[lane_id()];
     wave_sync();
     *tlog = def_log;
     have = zfse_build(L, tab, def_n, def_log);
@@ -314,7 +346,7 @@ __device__ bool zseq_table(ZWaveLds& L, uint32_t* tab, int* tlog, bool& have, in
   }
   if (mode == 2) {
     int ns, lg;
-    const int64_t u = zread_ncount(rs, q, lim, max_log, max_sym, L.norm, &ns, &lg);
+    const int64_t u = zread_ncount(rs, q, lim, max_log, max_sym, L.ph.t.norm, &ns, &lg);
     if (u < 0) return false;
     q += (uint32_t)u;
     *tlog = lg;
@@ -324,11 +356,11 @@ __device__ bool zseq_table(ZWaveLds& L, uint32_t* tab, int* tlog, bool& have, in
   return have;  // repeat
 }
 
-// Huffman decoding table from weights L.wts[0, nsym) (+ the implied last weight), RFC 8878 §4.2.1.
+// Huffman decoding table from weights L.ph.t.wts[0, nsym) (+ the implied last weight), RFC 8878 §4.2.1.
 __device__ int zhuf_build(ZWaveLds& L, int nsym) {
   uint32_t total = 0;
   for (int s = 0; s < nsym; s++) {
-    const uint32_t w = L.wts[s];
+    const uint32_t w = L.ph.t.wts[s];
     if (w > 11) return -1;
     if (w) total += 1u << (w - 1);
   }
@@ -336,14 +368,14 @@ __device__ int zhuf_build(ZWaveLds& L, int nsym) {
   const int max_bits = zhigh(total) + 1;
   const uint32_t left = (1u << max_bits) - total;
   if (max_bits > 11 || (left & (left - 1u))) return -1;
-  if (lane_id() == 0) L.wts[nsym] = (uint8_t)(zhigh(left) + 1);
+  if (lane_id() == 0) L.ph.t.wts[nsym] = (uint8_t)(zhigh(left) + 1);
   wave_sync();
   nsym++;
   uint32_t next = 0;
   for (int wt = 1; wt <= max_bits; wt++) {
     const uint32_t nb = (uint32_t)(max_bits + 1 - wt), len = 1u << (wt - 1);
     for (int s = 0; s < nsym; s++) {
-      if (L.wts[s] != wt) continue;
+      if (L.ph.t.wts[s] != wt) continue;
       for (uint32_t e = lane_id(); e < len; e += WAVE) L.huf[next + e] = (uint16_t)(s | (nb << 8));
       next += len;
     }
@@ -363,7 +395,7 @@ __device__ int zhuf_tree(ZWaveLds& L, rsrc_t rs, uint32_t& q, uint32_t lim) {
     if (q + 1 + nb > lim) return -1;
     for (int s = (int)lane_id(); s < nsym; s += WAVE) {
       const uint32_t b = zbyte(rs, q + 1 + (uint32_t)s / 2);
-      L.wts[s] = (uint8_t)((s & 1) ? (b & 15u) : (b >> 4));
+      L.ph.t.wts[s] = (uint8_t)((s & 1) ? (b & 15u) : (b >> 4));
     }
     wave_sync();
     q += 1 + nb;
@@ -371,34 +403,34 @@ __device__ int zhuf_tree(ZWaveLds& L, rsrc_t rs, uint32_t& q, uint32_t lim) {
     const uint32_t cs = hdr;
     if (q + 1 + cs > lim) return -1;
     int ns, lg;
-    const int64_t hb = zread_ncount(rs, q + 1, q + 1 + cs, 6, 255, L.norm, &ns, &lg);
+    const int64_t hb = zread_ncount(rs, q + 1, q + 1 + cs, 6, 255, L.ph.t.norm, &ns, &lg);
     if (hb < 0) return -1;
     // its own table: a later block may repeat the sequence tables (LL / OF / ML mode 3)
-    if (!zfse_build(L, L.hw, ns, lg)) return -1;
+    if (!zfse_build(L, L.ph.t.hw, ns, lg)) return -1;
     BackBits b;
     if (!b.init(rs, q + 1 + (uint32_t)hb, cs - (uint32_t)hb, L.win)) return -1;
     uint32_t s1 = b.read(lg), s2 = b.read(lg);
     // at most 255 decoded weights (libzstd HUF_readStats: FSE output capacity hwSize - 1)
     for (;;) {
       if (nsym >= 255) return -1;
-      uint32_t e = L.hw[s1];
-      if (lane_id() == 0) L.wts[nsym] = (uint8_t)(e & 0xFFu);
+      uint32_t e = L.ph.t.hw[s1];
+      if (lane_id() == 0) L.ph.t.wts[nsym] = (uint8_t)(e & 0xFFu);
       nsym++;
       s1 = (e >> 16) + b.read((int)((e >> 8) & 0xFFu));
       if (b.bits < 0) {
         if (nsym >= 255) return -1;
-        if (lane_id() == 0) L.wts[nsym] = (uint8_t)(L.hw[s2] & 0xFFu);
+        if (lane_id() == 0) L.ph.t.wts[nsym] = (uint8_t)(L.ph.t.hw[s2] & 0xFFu);
         nsym++;
         break;
       }
       if (nsym >= 255) return -1;
-      e = L.hw[s2];
-      if (lane_id() == 0) L.wts[nsym] = (uint8_t)(e & 0xFFu);
+      e = L.ph.t.hw[s2];
+      if (lane_id() == 0) L.ph.t.wts[nsym] = (uint8_t)(e & 0xFFu);
       nsym++;
       s2 = (e >> 16) + b.read((int)((e >> 8) & 0xFFu));
       if (b.bits < 0) {
         if (nsym >= 255) return -1;
-        if (lane_id() == 0) L.wts[nsym] = (uint8_t)(L.hw[s1] & 0xFFu);
+        if (lane_id() == 0) L.ph.t.wts[nsym] = (uint8_t)(L.ph.t.hw[s1] & 0xFFu);
         nsym++;
         break;
       }
@@ -529,7 +561,7 @@ __device__ __forceinline__ void zcopy_match(ZOut& O, ZWaveLds& L, uint32_t off, 
 // batch, then the bytes are gathered from the literal segment / the ring / HBM (older than the
 // ring) at once. Sequences are dependent chains (a match of 8 bytes at offset 8 after 2 literals,
 // again and again, in int64 data): they resolve in log2(depth) rounds instead of one at a time.
-__device__ void zexec_batch(ZOut& O, ZWaveLds& L, uint32_t m, int lit_kind, rsrc_t rs, uint32_t lit_src,
+__device__ __forceinline__ void zexec_batch(ZOut& O, ZWaveLds& L, uint32_t m, int lit_kind, rsrc_t rs, uint32_t lit_src,
                             const uint8_t* litbuf, uint32_t lit_pos) {
   const uint32_t lane = lane_id();
   const uint32_t ll = lane < m ? L.sq_ll[lane] : 0u, ml = lane < m ? L.sq_ml[lane] : 0u, of = lane < m ? L.sq_of[lane] : 0u;
@@ -540,17 +572,17 @@ __device__ void zexec_batch(ZOut& O, ZWaveLds& L, uint32_t m, int lit_kind, rsrc
   LT = uni(LT);
   // the batch's literals [lit_pos, lit_pos + LT)
   for (uint32_t i = lane; i < LT; i += WAVE)
-    L.lseg[i] = (uint8_t)zlit(lit_kind, rs, lit_src, litbuf, lit_pos + i);
+    L.ph.x.lseg[i] = (uint8_t)zlit(lit_kind, rs, lit_src, litbuf, lit_pos + i);
   const uint32_t op = O.pos;
-  for (uint32_t i = 0; i < ll; i++) L.src[ob + i] = ZS_LIT | (lb + i);
-  for (uint32_t i = 0; i < ml; i++) L.src[ob + ll + i] = op + ob + ll + i - of;
+  for (uint32_t i = 0; i < ll; i++) L.ph.x.src[ob + i] = ZS_LIT | (lb + i);
+  for (uint32_t i = 0; i < ml; i++) L.ph.x.src[ob + ll + i] = op + ob + ll + i - of;
   wave_sync();
   constexpr uint32_t NB = ZS_CAP / WAVE;
   uint32_t sv[NB];
 #pragma unroll
   for (uint32_t j = 0; j < NB; j++) {
     const uint32_t b = lane + WAVE * j;
-    sv[j] = b < T ? L.src[b] : ZS_LIT;
+    sv[j] = b < T ? L.ph.x.src[b] : ZS_LIT;
   }
 #pragma unroll 1
   for (uint32_t r = 0; r < 12u; r++) {  // branch-free rounds (the index is clamped to the table)
@@ -558,7 +590,7 @@ __device__ void zexec_batch(ZOut& O, ZWaveLds& L, uint32_t m, int lit_kind, rsrc
 #pragma unroll
     for (uint32_t j = 0; j < NB; j++) {
       const bool inb = !(sv[j] & ZS_LIT) && sv[j] >= op;
-      const uint32_t nv = L.src[(sv[j] - op) & (ZS_CAP - 1u)];
+      const uint32_t nv = L.ph.x.src[(sv[j] - op) & (ZS_CAP - 1u)];
       sv[j] = inb ? nv : sv[j];
       hop |= inb;
       more |= inb && !(nv & ZS_LIT) && nv >= op;
@@ -566,7 +598,7 @@ __device__ void zexec_batch(ZOut& O, ZWaveLds& L, uint32_t m, int lit_kind, rsrc
     if (!__ballot(hop)) break;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (uint32_t j = 0; j < NB; j++) L.src[lane + WAVE * j] = sv[j];  // entries >= T hold ZS_LIT
+    for (uint32_t j = 0; j < NB; j++) L.ph.x.src[lane + WAVE * j] = sv[j];  // entries >= T hold ZS_LIT
     wave_sync();
     if (!__ballot(more)) break;
   }
@@ -576,7 +608,7 @@ __device__ void zexec_batch(ZOut& O, ZWaveLds& L, uint32_t m, int lit_kind, rsrc
 #pragma unroll
   for (uint32_t j = 0; j < NB; j++) {
     const uint32_t v = sv[j];
-    bv[j] = (v & ZS_LIT) ? L.lseg[v & (ZS_CAP - 1u)] : L.ring[v & (ZS_RING - 1u)];
+    bv[j] = (v & ZS_LIT) ? L.ph.x.lseg[v & (ZS_CAP - 1u)] : L.ring[v & (ZS_RING - 1u)];
     far |= lane + WAVE * j < T && !(v & ZS_LIT) && v + ZS_RING < op + WAVE;
   }
   if (__ballot(far)) {
@@ -595,6 +627,113 @@ __device__ void zexec_batch(ZOut& O, ZWaveLds& L, uint32_t m, int lit_kind, rsrc
   }
   O.pos = op + T;
   zmaybe_flush(O, L);
+}
+
+// Decodes the block's next sequences into L.sq_* (RFC 8878 §3.1.1.3.2.1, §3.1.1.5): up to ZS_SB of
+// them and ZS_CAP output bytes, stopping before one that does not fit (carried: pend 1) or after one
+// longer than ZS_CAP (pend 2, in slot ZS_SB); a carried sequence opens the next batch. Returns 0 or
+// PQG_ERR_CORRUPT.
+__device__ __attribute__((noinline)) int zseq_decode(ZWaveLds& L) {
+  ZSeq& S = L.ss;
+  BackBits b;
+  b.rs = make_rsrc((const uint8_t*)uni64(S.src), uni64(S.src_len));  // scalar (an argument would be VGPRs)
+  b.win = L.win;
+  b.base = uni(S.base);
+  b.n = uni(S.n);
+  b.wlo = uni(S.wlo);
+  b.c = uni64(S.c);
+  b.bits = (int32_t)uni((uint32_t)S.bits);
+  b.cbit = (int32_t)uni((uint32_t)S.cbit);
+  uint32_t sl = uni(S.sl), so = uni(S.so), sm = uni(S.sm);
+  uint32_t r0 = uni(S.rep0), r1 = uni(S.rep1), r2 = uni(S.rep2);
+  uint32_t i = uni(S.i);
+  const uint32_t nseq = uni(S.nseq), regen = uni(S.regen), frame0 = uni(S.frame0);
+  uint32_t outp = uni(S.outp), lits = uni(S.lits);
+  const bool lane0 = lane_id() == 0;
+  uint32_t m = 0, T = 0, blit = 0, pend = 0;
+  int code = 0;
+  if (uni(S.pend) == 1u) {  // the sequence carried from the last batch opens this one
+    const uint32_t ll = uni(L.sq_ll[ZS_SB]), ml = uni(L.sq_ml[ZS_SB]);
+    if (lane0) {
+      L.sq_ll[0] = ll;
+      L.sq_ml[0] = ml;
+      L.sq_of[0] = L.sq_of[ZS_SB];
+    }
+    m = 1;
+    T = ll + ml;
+    blit = ll;
+  }
+  while (i < nseq) {
+    const uint32_t el = uni(L.ll[sl]), eo = uni(L.of[so]), em = uni(L.ml[sm]);
+    const uint32_t llc = el & 0xFFu, ofc = eo & 0xFFu, mlc = em & 0xFFu;
+    if (llc > 35 || mlc > 52 || ofc > 31) { code = PQG_ERR_CORRUPT; break; }
+    const uint32_t mle = uni(L.mlcode[mlc]), lle = uni(L.llcode[llc]);
+    const int32_t mlb = (int32_t)(mle >> 24), llb = (int32_t)(lle >> 24);
+    b.need((int32_t)ofc);  // offset, match length, literal length extra bits
+    const uint32_t ofv = (1u << ofc) + b.get((int32_t)ofc);
+    b.need(mlb + llb);
+    const uint32_t ml = (mle & 0xFFFFFFu) + b.get(mlb);
+    const uint32_t ll = (lle & 0xFFFFFFu) + b.get(llb);
+    uint32_t off;
+    if (ofv > 3) {
+      off = ofv - 3u;
+      r2 = r1; r1 = r0; r0 = off;
+    } else {
+      uint32_t idx = ofv - 1u;
+      if (ll == 0) idx++;
+      if (idx == 0) {
+        off = r0;
+      } else if (idx == 3) {
+        off = r0 - 1u;
+        if (off == 0) { code = PQG_ERR_CORRUPT; break; }
+        r2 = r1; r1 = r0; r0 = off;
+      } else {
+        off = idx == 1 ? r1 : r2;
+        if (idx == 2) r2 = r1;
+        r1 = r0;
+        r0 = off;
+      }
+    }
+    i++;
+    if (i < nseq) {  // state updates: literal length, match length, offset
+      const int32_t nl = (int32_t)((el >> 8) & 0xFFu), nm = (int32_t)((em >> 8) & 0xFFu), no = (int32_t)((eo >> 8) & 0xFFu);
+      b.need(nl + nm + no);  // <= 26 bits
+      sl = (el >> 16) + b.get(nl);
+      sm = (em >> 16) + b.get(nm);
+      so = (eo >> 16) + b.get(no);
+    }
+    if (b.bits < 0 || lits + ll > regen) { code = PQG_ERR_CORRUPT; break; }
+    if (off == 0 || off > outp + ll - frame0) { code = PQG_ERR_CORRUPT; break; }
+    lits += ll;
+    outp += ll + ml;
+    const bool big = (uint64_t)ll + ml > ZS_CAP;
+    if (big || T + ll + ml > ZS_CAP || m == ZS_SB) {
+      if (lane0) {
+        L.sq_ll[ZS_SB] = ll;
+        L.sq_ml[ZS_SB] = ml;
+        L.sq_of[ZS_SB] = off;
+      }
+      pend = big ? 2u : 1u;
+      break;
+    }
+    if (lane0) {
+      L.sq_ll[m] = ll;
+      L.sq_ml[m] = ml;
+      L.sq_of[m] = off;
+    }
+    m++;
+    T += ll + ml;
+    blit += ll;
+  }
+  if (lane0) {
+    S.c = b.c; S.bits = b.bits; S.cbit = b.cbit; S.wlo = b.wlo;
+    S.sl = sl; S.so = so; S.sm = sm;
+    S.rep0 = r0; S.rep1 = r1; S.rep2 = r2;
+    S.i = i; S.outp = outp; S.lits = lits;
+    S.m = m; S.T = T; S.blit = blit; S.pend = pend;
+  }
+  wave_sync();
+  return code;
 }
 
 // One compressed block [q, q + bs) of the job's input. Returns 0 or an error code.
@@ -663,7 +802,7 @@ __device__ __forceinline__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t 
 #pragma unroll
       for (int i = 0; i < 4; i++)
         if ((int)lane == i) { mb = sb[i]; mn = sn[i]; mc = cnt[i]; md = dst0[i]; }
-      LaneBits lb{mb, mn, 0xFFFFFFFFu, 0, L.hwin[lane], 0, INT64_MAX};
+      LaneBits lb{mb, mn, 0xFFFFFFFFu, 0, L.ph.t.hwin[lane], 0, INT64_MAX};
       const uint32_t last = mn ? zbyte(rs, mb + mn - 1) : 0u;
       if (!last) {
         bad = 1;
@@ -716,94 +855,52 @@ __device__ __forceinline__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t 
   BackBits b;
   if (!b.init(rs, p, lim - p, L.win)) return PQG_ERR_CORRUPT;
   b.need(tlog[0] + tlog[1] + tlog[2]);  // <= 27 bits
-  uint32_t sl = b.get(tlog[0]);
-  uint32_t so = b.get(tlog[1]);
-  uint32_t sm = b.get(tlog[2]);
+  const uint32_t sl0 = b.get(tlog[0]);
+  const uint32_t so0 = b.get(tlog[1]);
+  const uint32_t sm0 = b.get(tlog[2]);
   ZD_ADD(L, 1, t_tab);
   ZD_CNT(L, 6, nseq);
   ZD_T(t_seq);
   // Sequences are decoded one after another (the three FSE states and the backward bitstream are
-  // serial), up to ZS_SB of them and ZS_CAP output bytes into LDS, and executed as a batch
-  // (zexec_batch); a sequence longer than ZS_CAP runs on its own through the ring.
-  uint32_t lit_pos = 0;     // literals consumed by executed batches
-  uint32_t m = 0, T = 0;    // sequences / output bytes of the pending batch
-  uint32_t blit = 0;        // literals of the pending batch
-  uint32_t outp = O.pos;    // output position after the pending batch
-  auto run_batch = [&]() {
-    if (m == 0) return;
-    wave_sync();
-    ZD_T(t_ex);
-    zexec_batch(O, L, m, lit_kind, rs, lit_src, litbuf, lit_pos);
-    ZD_ADD(L, 3, t_ex);
-    lit_pos += blit;
-    m = 0; T = 0; blit = 0;
-  };
-  for (uint32_t i = 0; i < nseq; i++) {
-    const uint32_t el = uni(L.ll[sl]), eo = uni(L.of[so]), em = uni(L.ml[sm]);
-    const uint32_t llc = el & 0xFFu, ofc = eo & 0xFFu, mlc = em & 0xFFu;
-    if (llc > 35 || mlc > 52 || ofc > 31) return PQG_ERR_CORRUPT;
-    // length codes from LDS: an indexed __constant__ table is a vector memory load here, and its
-    // vmcnt wait also waited for every output store in flight, once per sequence
-    const uint32_t mle = uni(L.mlcode[mlc]), lle = uni(L.llcode[llc]);
-    const int32_t mlb = (int32_t)(mle >> 24), llb = (int32_t)(lle >> 24);
-    b.need((int32_t)ofc);  // offset, match length, literal length extra bits (RFC 8878 §3.1.1.3.2.1.2)
-    const uint32_t ofv = (1u << ofc) + b.get((int32_t)ofc);
-    b.need(mlb + llb);
-    const uint32_t ml = (mle & 0xFFFFFFu) + b.get(mlb);
-    const uint32_t ll = (lle & 0xFFFFFFu) + b.get(llb);
-    uint32_t off;
-    if (ofv > 3) {
-      off = (uint32_t)(ofv - 3);
-      rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = off;
-    } else {
-      uint32_t idx = (uint32_t)ofv - 1u;
-      if (ll == 0) idx++;
-      if (idx == 0) {
-        off = rep[0];
-      } else if (idx == 3) {
-        off = rep[0] - 1u;
-        if (off == 0) return PQG_ERR_CORRUPT;
-        rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = off;
-      } else {
-        off = idx == 1 ? rep[1] : rep[2];
-        if (idx == 2) rep[2] = rep[1];
-        rep[1] = rep[0];
-        rep[0] = off;
-      }
+  // serial) by zseq_decode, a batch at a time (up to ZS_SB sequences, ZS_CAP output bytes, in LDS),
+  // and each batch is executed at once (zexec_batch); a sequence longer than ZS_CAP runs on its own
+  // through the ring.
+  if (lane_id() == 0) {
+    ZSeq& S = L.ss;
+    S.c = b.c; S.bits = b.bits; S.cbit = b.cbit; S.wlo = b.wlo; S.base = b.base; S.n = b.n;
+    S.sl = sl0; S.so = so0; S.sm = sm0;
+    S.rep0 = rep[0]; S.rep1 = rep[1]; S.rep2 = rep[2];
+    S.i = 0; S.nseq = nseq; S.outp = O.pos; S.lits = 0; S.regen = regen; S.frame0 = O.frame0;
+    S.pend = 0;
+  }
+  wave_sync();
+  uint32_t lit_pos = 0;  // literals consumed by executed sequences
+  while (true) {
+    if (zseq_decode(L)) return PQG_ERR_CORRUPT;
+    const uint32_t m = uni(L.ss.m), blit = uni(L.ss.blit), pend = uni(L.ss.pend);
+    if (m) {
+      ZD_T(t_ex);
+      zexec_batch(O, L, m, lit_kind, rs, lit_src, litbuf, lit_pos);
+      ZD_ADD(L, 3, t_ex);
+      lit_pos += blit;
     }
-    if (i + 1 < nseq) {  // state updates: literal length, match length, offset
-      const int32_t nl = (int32_t)((el >> 8) & 0xFFu), nm = (int32_t)((em >> 8) & 0xFFu), no = (int32_t)((eo >> 8) & 0xFFu);
-      b.need(nl + nm + no);  // <= 26 bits
-      sl = (el >> 16) + b.get(nl);
-      sm = (em >> 16) + b.get(nm);
-      so = (eo >> 16) + b.get(no);
-    }
-    if (b.bits < 0 || lit_pos + blit + ll > regen) return PQG_ERR_CORRUPT;
-    if (off == 0 || off > outp + ll - O.frame0) return PQG_ERR_CORRUPT;
-    if ((uint64_t)ll + ml > ZS_CAP) {  // a long sequence: the batch before it, then itself through the ring
-      run_batch();
+    if (pend == 2u) {  // a long sequence: through the ring
       ZD_T(t_long);
+      const uint32_t ll = uni(L.sq_ll[ZS_SB]), ml = uni(L.sq_ml[ZS_SB]), off = uni(L.sq_of[ZS_SB]);
       if (ll) zcopy_lits(O, L, lit_kind, rs, lit_kind == 1 ? lit_src : lit_src + lit_pos, litbuf, ll);
       lit_pos += ll;
       zcopy_match(O, L, off, ml);
+      if (lane_id() == 0) L.ss.pend = 0;
+      wave_sync();
       ZD_ADD(L, 4, t_long);
-      outp = O.pos;
-      continue;
     }
-    if (T + ll + ml > ZS_CAP || m == ZS_SB) run_batch();
-    if (lane_id() == 0) {
-      L.sq_ll[m] = ll;
-      L.sq_ml[m] = ml;
-      L.sq_of[m] = off;
-    }
-    m++;
-    T += ll + ml;
-    blit += ll;
-    outp += ll + ml;
+    if (pend == 0u && uni(L.ss.i) == nseq) break;
   }
-  run_batch();
+  rep[0] = uni(L.ss.rep0);
+  rep[1] = uni(L.ss.rep1);
+  rep[2] = uni(L.ss.rep2);
   ZD_ADD(L, 2, t_seq);
-  if (b.bits != 0) return PQG_ERR_CORRUPT;
+  if ((int32_t)uni((uint32_t)L.ss.bits) != 0) return PQG_ERR_CORRUPT;
   if (regen > lit_pos) zcopy_lits(O, L, lit_kind, rs, lit_kind == 1 ? lit_src : lit_src + lit_pos, litbuf, regen - lit_pos);
   return 0;
 }
@@ -870,9 +967,13 @@ __global__ __launch_bounds__(64) void k_zstd(const uint8_t* __restrict__ src, ui
 __device__ __forceinline__ void zstd_job(ZWaveLds& L, const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
                          uint64_t dst_bytes, const pqg_snappy_job& jb, int j, int32_t* status, uint8_t* litbuf) {
   const rsrc_t rs = make_rsrc(src + jb.src_offset, src_bytes - jb.src_offset);
+  if (lane_id() == 0) {
+    L.ss.src = (uint64_t)(uintptr_t)(src + jb.src_offset);
+    L.ss.src_len = src_bytes - jb.src_offset;
+  }
   const uint32_t n = uni(jb.src_size);
 #ifdef PQG_DIAG
-  for (int i = 0; i < 8; i++) L.diag[i] = 0;
+  for (int i = 0; i < 12; i++) L.diag[i] = 0;
   ZD_T(t_job);
 #endif
   ZOut O{dst + jb.dst_offset, uni(jb.dst_size), 0, 0, 0, 0};
@@ -953,7 +1054,7 @@ __device__ __forceinline__ void zstd_job(ZWaveLds& L, const uint8_t* __restrict_
   zflush(O, L);
 #ifdef PQG_DIAG
   L.diag[5] = __builtin_amdgcn_s_memtime() - t_job;
-  if (pqg_zdiag && lane_id() < 8) pqg_zdiag[8 * (uint64_t)j + lane_id()] = L.diag[lane_id()];
+  if (pqg_zdiag && lane_id() < 12) pqg_zdiag[12 * (uint64_t)j + lane_id()] = L.diag[lane_id()];
 #endif
   if (!code && O.pos < O.cap) code = PQG_ERR_EOF;  // the frames end before the page's size
   if (lane_id() == 0 && status) status[j] = code;

@@ -88,6 +88,12 @@ class Plan:
         """Launches re-run in split mode after a fused-kernel wait timed out (pqg_plan_timeout_fallbacks)."""
         return native.lib().pqg_plan_timeout_fallbacks(self.handle)
 
+    @property
+    def plain_fallbacks(self):
+        """Launches re-run on the per-value BYTE_ARRAY path because a PLAIN page held bytes after its
+        values (pqg_plan_plain_fallbacks)."""
+        return native.lib().pqg_plan_plain_fallbacks(self.handle)
+
     def sync(self):
         st = abi.Status()
         rc = native.lib().pqg_sync(self.decoder.ctx, C.byref(st))

@@ -15,7 +15,7 @@ _LIB = None
 
 EXPORTS = [
     "pqg_abi_version", "pqg_device_count", "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_stream", "pqg_decode",
-    "pqg_sync", "pqg_plan_create", "pqg_plan_launch", "pqg_plan_kernel_count", "pqg_plan_timeout_fallbacks",
+    "pqg_sync", "pqg_plan_create", "pqg_plan_launch", "pqg_plan_kernel_count", "pqg_plan_timeout_fallbacks", "pqg_plan_plain_fallbacks",
     "pqg_plan_destroy",
     "pqg_decode_host", "pqg_unpack_runs", "pqg_router_read", "pqg_error_name", "pqg_assemble", "pqg_assemble_schema",
     "pqg_snappy_decompress", "pqg_snappy_sync", "pqg_zstd_decompress", "pqg_zstd_sync", "pqg_crc32", "pqg_frame_chunk", "pqg_pages_from_headers",
@@ -59,6 +59,7 @@ def lib():
         L.pqg_plan_launch.argtypes = [vp]
         L.pqg_plan_kernel_count.argtypes = [vp]
         L.pqg_plan_timeout_fallbacks.argtypes = [vp]
+        L.pqg_plan_plain_fallbacks.argtypes = [vp]
         L.pqg_plan_destroy.argtypes = [vp]
         L.pqg_decode_host.argtypes = [vp, vp, u64, vp, i32, vp, i32, vp, C.POINTER(abi.Status)]
         L.pqg_unpack_runs.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32]

@@ -10,7 +10,7 @@ from oracle import pqref
 from pqgpu import abi, writer
 
 from helpers import make, nulls, zipf_dict_column
-from test_gpu_parity import run_both
+from test_gpu_parity import assert_same, run_both
 
 pytestmark = pytest.mark.gpu
 
@@ -273,3 +273,63 @@ def test_binary_plain_segmented_trailing_bytes(decoder):
         ch.pages[0].num_values = nv
         ch.values = vals[:nv]
         run_both(decoder, [ch])
+
+
+# ---- PLAIN-only BYTE_ARRAY columns in one pass (k_bin_bases + k_bin_plain, 2 KiB tiles) ----
+
+def _plan_both(decoder, chunks):
+    """Decode through a plan (two launches) and compare with the oracle after each; returns the plan."""
+    batch = writer.build_batch(chunks)
+    ref = pqref.decode_batch(batch)
+    assert ref.code == 0, ref.status
+    plan = decoder.plan(decoder.upload(batch))
+    for _ in range(2):
+        plan.launch()
+        rc, st = plan.sync()
+        assert rc == 0, st.message
+        for i, cd in enumerate(batch.columns):
+            col = plan.columns[i]
+            n = ref.columns[i]["n_values"]
+            assert_same(col.numpy(), ref.columns[i]["values"], cd["physical_type"])
+            if cd["physical_type"] == abi.BYTE_ARRAY:
+                assert np.array_equal(col.offsets().cpu().numpy()[: n + 1], ref.columns[i]["offsets"][: n + 1])
+    return plan
+
+
+def test_binary_plain_one_pass_no_fallback(decoder):
+    """Well-formed PLAIN pages take the one-pass path and never fall back; mixed with a column whose
+    pages are dictionary-encoded (per-value path) in the same plan."""
+    a = make(abi.BYTE_ARRAY, _strings(50_000, 21, 0, 60), abi.PLAIN, page_rows=9000)
+    b = make(abi.BYTE_ARRAY, [_strings(300, 22)[i % 300] for i in range(20_000)], abi.RLE_DICTIONARY, page_rows=7000)
+    plan = _plan_both(decoder, [a, b])
+    assert plan.plain_fallbacks == 0
+
+
+def test_binary_plain_one_pass_fallback(decoder):
+    """Bytes after a page's values (the reader ignores them): the plan falls back to the per-value path
+    once and keeps it; the result equals the oracle on both launches."""
+    vals = _strings(20_000, 23, 0, 30)
+    ch = make(abi.BYTE_ARRAY, vals, abi.PLAIN, page_rows=10_000)
+    ch.pages[0].body = ch.pages[0].body + b"\x07\x00\x00\x00abcdefg" + bytes(300)
+    plan = _plan_both(decoder, [ch])
+    assert plan.plain_fallbacks == 1
+
+
+@pytest.mark.parametrize("lens", ["tile_sized", "tile_minus_4", "spanning", "empty_then_long"])
+def test_binary_plain_tile_edges(decoder, lens):
+    """Values whose boundaries fall on 2 KiB tile edges, values longer than two tiles (a tile with no
+    value start; bytes past the staged tiles), and runs of empty values."""
+    rng = np.random.default_rng(len(lens))
+    if lens == "tile_sized":
+        vals = [bytes(rng.integers(0, 256, 2044, dtype=np.uint8)) for _ in range(40)]
+    elif lens == "tile_minus_4":
+        vals = [bytes(rng.integers(0, 256, int(x), dtype=np.uint8)) for x in rng.integers(2040, 2050, 60)]
+    elif lens == "spanning":
+        vals = [bytes(rng.integers(0, 256, int(x), dtype=np.uint8)) for x in rng.integers(0, 9000, 80)]
+    else:
+        vals = ([b""] * 3000 + [bytes(5000)] + [b"x"] * 700) * 3
+    run_both(decoder, [make(abi.BYTE_ARRAY, vals, abi.PLAIN, page_rows=len(vals) // 3 + 1)])
+    dl = nulls(len(vals) + 50, 0.05, seed=2)
+    nn = int(dl.sum())
+    run_both(decoder, [make(abi.BYTE_ARRAY, (vals * (nn // len(vals) + 1))[:nn], abi.PLAIN, def_levels=dl, max_def=1,
+                            version=1, page_rows=len(dl) // 2 + 1)])

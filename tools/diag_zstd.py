@@ -20,19 +20,20 @@ work = bench_suite.gen("plain_i64_zstd", rows)
 dec = D.Decoder(0)
 db = dec.upload_chunks(work.chunks)
 n_jobs = sum(1 for ch in work.chunks for p in ch.pages if p.codec)
-buf = torch.zeros(max(n_jobs, 1) * 8 + 64, dtype=torch.int64, device="cuda")
+buf = torch.zeros(max(n_jobs, 1) * 12 + 64, dtype=torch.int64, device="cuda")
 L = native.lib()
 L.pqg_diag_zstd_set.argtypes = [C.c_void_p]
 assert L.pqg_diag_zstd_set(buf.data_ptr()) == 0
 dec.decompress(db)
 torch.cuda.synchronize()
-a = buf[: n_jobs * 8].view(n_jobs, 8).cpu().numpy().astype(np.float64)
-names = ["literals", "seq tables", "seq loop", "  batches", "  long seqs", "job", "sequences", "literal bytes"]
+a = buf[: n_jobs * 12].view(n_jobs, 12).cpu().numpy().astype(np.float64)
+names = ["literals", "seq tables", "seq loop", "  batches", "  long seqs", "job", "sequences", "literal bytes",
+         "  state reads", "  extra bits", "  state updates", "  rest"]
 tot = a[:, 5].sum()
 print(f"jobs {n_jobs}, mean job cycles {a[:, 5].mean():.0f}")
 for i, nm in enumerate(names):
     print(f"{nm:14s} sum {a[:, i].sum():16.0f}  per job {a[:, i].mean():12.0f}" +
-          (f"  {100 * a[:, i].sum() / tot:5.1f} %" if i < 6 else ""))
+          (f"  {100 * a[:, i].sum() / tot:5.1f} %" if i < 6 or i >= 8 else ""))
 print(f"cycles per sequence (loop): {a[:, 2].sum() / max(a[:, 6].sum(), 1):.0f}, "
       f"per batch-executed sequence: {a[:, 3].sum() / max(a[:, 6].sum(), 1):.0f}, "
       f"literal cycles per byte: {a[:, 0].sum() / max(a[:, 7].sum(), 1):.1f}")
