@@ -1732,9 +1732,15 @@ struct BinPlainLds {
     BinWalkLds w;                   // the tile walk (candidate list)
     uint32_t img[BP_IMG / 4 + 16];  // then: page bytes [B, B + BP_IMG) (+ slack for the compose reads)
   } u;
-  uint32_t acc[BW_CAP + 1];  // accepted value starts of the tile (page positions), ascending
-  uint16_t bt[BP_BLK + 2];   // output block -> the last value starting at or before its first byte
+  union {
+    uint32_t pj[BW_CAP];  // the guess's pointer jumping over the candidate list
+    struct {
+      uint16_t acc[BW_CAP + 2];  // accepted value starts of the tile (offsets from B), ascending
+      uint16_t bt[BP_BLK + 2];   // output block -> the last value starting at or before its first byte
+    };
+  };
 };
+static_assert(sizeof(BinPlainLds) * WPB <= 160 * 1024 / 6, "6 workgroups of k_bin_plain per CU");
 
 // Candidates of tile [B, B + BW_WIN) from position pos on (see bin_walk_core); returns their number
 // (at most BW_CAP: eff_end is then the first candidate not listed).
@@ -1854,7 +1860,7 @@ __device__ BpWalk bp_walk(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint32_
         last = 63u - (uint32_t)__builtin_clzll(mask);
       }
       const uint32_t rank = (uint32_t)__builtin_popcountll(mask & ((1ull << lane) - 1ull));
-      if ((mask >> lane) & 1ull) L.acc[n + rank] = W.pn[k].x;
+      if ((mask >> lane) & 1ull) L.acc[n + rank] = (uint16_t)(W.pn[k].x - B);
       n += (uint32_t)__builtin_popcountll(mask);
       const uint32_t nxt = rdl(s, last);  // successor of the batch's last value
       pos = nxt;
@@ -1887,7 +1893,7 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
   const uint32_t total = bp_candidates(W, cur, B, B, end, eff_end);
   const uint32_t lane = lane_id();
   // node i: J = successor index, or (last index | 0x8000) once the chain leaves the list, 0xFFFF when
-  // it breaks; D = values on the chain so far (L.acc as scratch: J | D << 16)
+  // it breaks; D = values on the chain so far (L.pj: J | D << 16)
   constexpr uint32_t NP = BW_CAP / WAVE;  // nodes per lane
   constexpr uint32_t XF = 0x8000u, BAD = 0xFFFFu;
 #pragma unroll
@@ -1899,7 +1905,7 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
       const uint32_t t = q < eff_end ? bw_index(W, q - B) : 0xFFFFu;
       e = (q >= eff_end || q == end ? (i | XF) : (t < total ? t : BAD)) | (1u << 16);  // (end: the last value)
     }
-    L.acc[i] = e;
+    L.pj[i] = e;
   }
   wave_sync();
   for (uint32_t r = 0; r < 9; r++) {
@@ -1907,20 +1913,20 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
 #pragma unroll
     for (uint32_t j = 0; j < NP; j++) {
       const uint32_t i = lane + WAVE * j;
-      const uint32_t e = L.acc[i];
+      const uint32_t e = L.pj[i];
       const uint32_t J = e & 0xFFFFu;
       v[j] = e;
       if (J < XF) {  // not terminal: jump
-        const uint32_t f = L.acc[J];
+        const uint32_t f = L.pj[J];
         v[j] = (f & 0xFFFFu) == BAD ? (BAD | (e & 0xFFFF0000u)) : ((f & 0xFFFFu) | ((e >> 16) + (f >> 16)) << 16);
       }
     }
     wave_sync();
 #pragma unroll
-    for (uint32_t j = 0; j < NP; j++) L.acc[lane + WAVE * j] = v[j];
+    for (uint32_t j = 0; j < NP; j++) L.pj[lane + WAVE * j] = v[j];
     wave_sync();
   }
-  const uint32_t e = lane < total ? L.acc[lane] : BAD;
+  const uint32_t e = lane < total ? L.pj[lane] : BAD;
   const uint32_t J = e & 0xFFFFu;
   uint32_t d = e >> 16;
   bool ok = lane < total && J != BAD && (J & XF);
@@ -1954,7 +1960,7 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
   return BpGuess{g, gi, total, eff_end};
 }
 
-__global__ __launch_bounds__(64 * WPB) void k_bin_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) void k_bin_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                         const PageWork* __restrict__ work,
                                                         const ColumnDev* __restrict__ cols,
                                                         const uint64_t* __restrict__ segs, uint32_t n_segs,
@@ -2094,14 +2100,14 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_plain(const uint8_t* __restric
   if (r.code && before + r.n < N && lane == 0) report(err, err_count, page, 2, before + r.n, r.code);
   if (before + r.n >= N) {  // the page's last value is here: it must end at the section end
     const uint32_t q = N - 1u - before;
-    const uint32_t e_last = q + 1u < r.n ? L.acc[q + 1u] : r.pos;
+    const uint32_t e_last = q + 1u < r.n ? B + L.acc[q + 1u] : r.pos;
     if ((q + 1u < r.n || e_last != end) && lane == 0) sst(inexact, flag_epoch);
   }
   const uint32_t m = r.n < N - before ? r.n : N - before;
   if (m == 0) return;
   // ---- offsets of values before .. before + m (the last one: the end of value m - 1)
   const uint32_t rpos = r.pos;
-  auto pos_k = [&](uint32_t k) -> uint32_t { return k < r.n ? L.acc[k] : rpos; };
+  auto pos_k = [&](uint32_t k) -> uint32_t { return k < r.n ? B + L.acc[k] : rpos; };
   int64_t* offs = (int64_t*)cd.values + pw.out_offset + before;
   const uint64_t bb = pw.bin_base;
   for (uint32_t k = lane; k <= m; k += WAVE)
