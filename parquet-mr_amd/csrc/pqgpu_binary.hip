@@ -1893,9 +1893,12 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
   const uint32_t total = bp_candidates(W, cur, B, B, end, eff_end);
   const uint32_t lane = lane_id();
   // node i: J = successor index, or (last index | 0x8000) once the chain leaves the list, 0xFFFF when
-  // it breaks; D = values on the chain so far (L.pj: J | D << 16)
+  // it breaks; D = values on the chain so far (L.pj: J | D << 16). 6 rounds: a chain of more than 64
+  // values is not followed to its end but ranked by where its 64th value lies (the true start's chain
+  // holds every value, so it gets there soonest)
   constexpr uint32_t NP = BW_CAP / WAVE;  // nodes per lane
   constexpr uint32_t XF = 0x8000u, BAD = 0xFFFFu;
+  uint32_t v[NP];
 #pragma unroll
   for (uint32_t j = 0; j < NP; j++) {
     const uint32_t i = lane + WAVE * j;
@@ -1905,17 +1908,15 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
       const uint32_t t = q < eff_end ? bw_index(W, q - B) : 0xFFFFu;
       e = (q >= eff_end || q == end ? (i | XF) : (t < total ? t : BAD)) | (1u << 16);  // (end: the last value)
     }
+    v[j] = e;
     L.pj[i] = e;
   }
   wave_sync();
-  for (uint32_t r = 0; r < 9; r++) {
-    uint32_t v[NP];
+  for (uint32_t r = 0; r < 6; r++) {
 #pragma unroll
     for (uint32_t j = 0; j < NP; j++) {
-      const uint32_t i = lane + WAVE * j;
-      const uint32_t e = L.pj[i];
+      const uint32_t e = v[j];
       const uint32_t J = e & 0xFFFFu;
-      v[j] = e;
       if (J < XF) {  // not terminal: jump
         const uint32_t f = L.pj[J];
         v[j] = (f & 0xFFFFu) == BAD ? (BAD | (e & 0xFFFF0000u)) : ((f & 0xFFFFu) | ((e >> 16) + (f >> 16)) << 16);
@@ -1926,11 +1927,12 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
     for (uint32_t j = 0; j < NP; j++) L.pj[lane + WAVE * j] = v[j];
     wave_sync();
   }
-  const uint32_t e = lane < total ? L.pj[lane] : BAD;
+  const uint32_t e = lane < total ? v[0] : BAD;  // candidate `lane` (one of the first 64)
   const uint32_t J = e & 0xFFFFu;
-  uint32_t d = e >> 16;
-  bool ok = lane < total && J != BAD && (J & XF);
-  uint32_t dmax = ok ? d : 0u;
+  const uint32_t d = e >> 16;
+  const bool term = J != BAD && (J & XF) != 0, lng = J < XF;
+  bool ok = lane < total && (term || lng);
+  uint32_t dmax = ok ? (lng ? 0xFFFFu : d) : 0u;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     const uint32_t y = (uint32_t)__shfl_xor((int)dmax, o);
@@ -1946,8 +1948,10 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
       q = q + 4u + ld4_any(rs, q);
     }
   }
-  // the most values on the chain, ties to the earliest candidate
-  uint32_t key = ok ? (d << 8) | (255u - lane) : 0u;
+  // rank: long chains by where their 64th value lies (sooner first), then chains that leave the tile
+  // by their values; ties to the earliest candidate
+  const uint32_t score = lng ? 0x10000u + (0xFFFFu - (W.pn[J].x - B)) : d;
+  uint32_t key = ok ? (score << 8) | (255u - lane) : 0u;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     const uint32_t y = (uint32_t)__shfl_xor((int)key, o);
