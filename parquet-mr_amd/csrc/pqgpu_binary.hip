@@ -775,7 +775,11 @@ __device__ __forceinline__ void store_block16(uint8_t* dst, uint64_t a, uint64_t
 // a value running past the page is the reference's "Failed to read N bytes" (EOF) at that value.
 constexpr uint32_t CP_VALUES = CP_CHUNK_VALUES;  // values per workgroup chunk of k_bin_copy
 constexpr uint32_t CP_WAVE = CP_VALUES / WPB;  // values per wave on the per-wave path
+#ifdef PQG_AB_CPSRC  // (A/B builds under abx/ only)
+constexpr uint32_t CP_SRC = PQG_AB_CPSRC * CP_VALUES;
+#else
 constexpr uint32_t CP_SRC = 48u * CP_VALUES;     // LDS bytes of staged source per workgroup
+#endif
 static_assert(CP_VALUES == CP_CHUNK_VALUES, "host chunking (pqgpu_internal.h)");
 
 struct CopyWaveLds {
@@ -1089,7 +1093,12 @@ __device__ __forceinline__ void compose_block(const uint32_t* img, uint32_t Sv, 
 // no load waits behind a store (vmcnt counts both). Source bytes are read from HBM once, where
 // the per-wave path read 36 bytes per 16-byte block. A chunk whose source does not fit CP_SRC
 // takes the per-wave path, CP_WAVE values per wave.
-__global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+#ifdef PQG_AB_CPSRC
+#define PQG_COPY_OCC __attribute__((amdgpu_waves_per_eu(7)))
+#else
+#define PQG_COPY_OCC
+#endif
+__global__ __launch_bounds__(64 * WPB) PQG_COPY_OCC void k_bin_copy(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                        const PageWork* __restrict__ work,
                                                        const ColumnDev* __restrict__ cols,
                                                        const uint64_t* __restrict__ chunks, uint32_t n_chunks,
@@ -2349,9 +2358,15 @@ hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
                            const ColumnDev* cols, const uint64_t* chunks, uint32_t n_chunks, uint64_t* err,
                            ErrCount err_count) {
   if (n_chunks == 0) return hipSuccess;
-  // one resident round of workgroups (5 per CU at ~31 KiB of LDS each) striding over the chunks: a
-  // dictionary page stays staged across a workgroup's chunks of the same column
-  constexpr uint32_t CP_GRID = 256u * 5u;
+  // one resident round of workgroups (by LDS: 5 per CU at ~31 KiB each; by VGPRs at most 7) striding
+  // over the chunks: a dictionary page stays staged across a workgroup's chunks of the same column
+#ifdef PQG_AB_CPSRC
+  constexpr uint32_t CP_VGPR_WG = 7u;
+#else
+  constexpr uint32_t CP_VGPR_WG = 5u;  // 95 VGPRs: 5 waves per SIMD
+#endif
+  constexpr uint32_t CP_PER_CU = (160u * 1024u) / (uint32_t)sizeof(CopyLds) < CP_VGPR_WG ? (160u * 1024u) / (uint32_t)sizeof(CopyLds) : CP_VGPR_WG;
+  constexpr uint32_t CP_GRID = 256u * CP_PER_CU;
   hipLaunchKernelGGL(k_bin_copy, dim3(n_chunks < CP_GRID ? n_chunks : CP_GRID), dim3(64 * WPB), 0, st, bytes, n_bytes,
                      work, cols, chunks, n_chunks, err, err_count);
   return hipGetLastError();
