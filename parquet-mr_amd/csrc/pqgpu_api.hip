@@ -157,6 +157,8 @@ struct pqg_plan {
   // hold those columns' entries last, so plain_fused launches skip them (pqg_sync turns plain_fused
   // off when a page's values do not fill its data section)
   bool plain_fused = false;
+  bool plain_pg = false;  // ... through k_bin_plain_pg (one wave per page) instead of the tiles
+  int n_pcp = 0;          // pages of those columns (pcol_pages)
   int plain_fallbacks = 0;
   DevBuf psegs, pstatus, pcol_pages, pcol_start;  // tiles (page | tile << 32); aggw + incw per tile; column page lists
   uint32_t n_psegs = 0, pseg_epoch = 0;
@@ -489,9 +491,15 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   std::vector<uint8_t> needs_ids((size_t)std::max(n_cols, 1), 0);
   for (int p : cls_lists[C_IDS]) needs_ids[(size_t)P->h_work[(size_t)p].column] = 1;
   // PLAIN-only BYTE_ARRAY columns (every page PLAIN, no descriptor error, < 2^24 - 1 slots per page):
-  // one pass (k_bin_bases + k_bin_plain) over 2 KiB tiles of their pages, when the plan has fewer than
-  // BW_SEG_MAX_PAGES PLAIN pages (with more, one wave per page already fills the chip, and the per-value
-  // path's walk + copy measured faster than the tiles: C3 6.4 vs 10.4 ms, profiles/r03/plain_ab)
+  // one pass: k_bin_bases + k_bin_plain over 2 KiB tiles of their pages when the plan has fewer than
+  // BW_SEG_MAX_PAGES PLAIN pages, k_bin_plain_pg (one wave per page, which fills the chip) with more
+  // (there the tiles measured slower than the per-value walk + copy: C3 10.4 vs 6.4 ms, profiles/r03/plain_ab)
+  // PQGPU_PLAIN_PG overrides the choice (tests and A/B): 0 = many-page plans per value, 3 = every plan
+  // one wave per page
+  int plain_mode = 2;
+  if (const char* ev = getenv("PQGPU_PLAIN_PG")) plain_mode = atoi(ev);
+  const bool many_plain = cls_lists[C_BINP].size() >= pqg::BW_SEG_MAX_PAGES || plain_mode == 3;
+  P->plain_pg = many_plain;
   std::vector<uint8_t> plain_col((size_t)std::max(n_cols, 1), 0);
   std::vector<uint64_t> psegs;
   std::vector<int32_t> pcp, pcs(1, 0);
@@ -506,14 +514,14 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     }
     for (int i = 0; i < n_cols; i++) {
       plain_col[(size_t)i] = bin_out(cols[i]) && !ids_mode(cols[i]) && !col_err[(size_t)i] && !dba_fixed[(size_t)i] &&
-                             npg[(size_t)i] > 0 && nplain[(size_t)i] == npg[(size_t)i] &&
-                             cls_lists[C_BINP].size() < pqg::BW_SEG_MAX_PAGES;
+                             npg[(size_t)i] > 0 && nplain[(size_t)i] == npg[(size_t)i] && (!many_plain || plain_mode != 0);
 #ifdef PQG_AB_NOPLAIN  // (A/B builds under abx/ only)
       plain_col[(size_t)i] = 0;
 #endif
       if (!plain_col[(size_t)i]) continue;
       for (int p : cpg[(size_t)i]) {
         pcp.push_back(p);
+        if (many_plain) continue;
         const uint32_t ntile = std::max<uint32_t>((P->h_work[(size_t)p].size + pqg::BP_TILE - 1) / pqg::BP_TILE, 1u);
         for (uint32_t k = 0; k < ntile; k++) psegs.push_back((uint64_t)(uint32_t)p | ((uint64_t)k << 32));
       }
@@ -544,12 +552,12 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     }
     if (pass == 0) {
       if (!segs.empty()) P->seg_status_off = take(8 * (segs.size() + 1));  // + the ticket counter
-      if (!psegs.empty()) P->pticket_off = take(8);
+      if (!pcp.empty()) P->pticket_off = take(8);
       P->blen_bytes_nf = sc;
     }
   }
   P->blen_bytes = sc;
-  if (!psegs.empty()) P->pflag_off = take(8);
+  if (!pcp.empty()) P->pflag_off = take(8);
   if (!segs.empty()) P->seg_tmp_off = take(4 * 2 * (uint64_t)pqg::BW_SEG_CAP * segs.size());
   P->n_segs = (uint32_t)segs.size();
   for (int i = 0; i < n_cols; i++) {
@@ -724,13 +732,16 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   if (!psegs.empty()) {
     ok = ok && hipMemcpyAsync(P->psegs.p, psegs.data(), sizeof(uint64_t) * psegs.size(), hipMemcpyHostToDevice, s) == hipSuccess;
     ok = ok && hipMemsetAsync(P->pstatus.p, 0, 2 * sizeof(uint64_t) * psegs.size(), s) == hipSuccess;
+  }
+  if (!pcp.empty()) {
     ok = ok && hipMemcpyAsync(P->pcol_pages.p, pcp.data(), sizeof(int32_t) * pcp.size(), hipMemcpyHostToDevice, s) == hipSuccess;
     ok = ok && hipMemcpyAsync(P->pcol_start.p, pcs.data(), sizeof(int32_t) * pcs.size(), hipMemcpyHostToDevice, s) == hipSuccess;
     ok = ok && hipMemsetAsync((uint8_t*)P->bscratch.p + P->pflag_off, 0, 8, s) == hipSuccess;
   }
   P->n_psegs = (uint32_t)psegs.size();
   P->n_pcols = (int)pcs.size() - 1;
-  P->plain_fused = !psegs.empty();
+  P->plain_fused = !pcp.empty();
+  P->n_pcp = (int)pcp.size();
   if (!dba_chunks.empty())
     ok = ok && hipMemcpyAsync(P->dba_chunks.p, dba_chunks.data(), sizeof(uint64_t) * dba_chunks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   if (!chunk_list.empty())
@@ -769,7 +780,7 @@ int pqg_plan_launch(pqg_plan* P) {
   if (++P->err_epoch > pqg::ERR_EPOCH_MAX) {
     P->err_epoch = 1;
     if (hipMemsetAsync(P->err.p, 0, err_bytes + 16, s) != hipSuccess) return PQG_ERR_HIP;
-    if (P->n_psegs && hipMemsetAsync((uint8_t*)P->bscratch.p + P->pflag_off, 0, 8, s) != hipSuccess) return PQG_ERR_HIP;
+    if (P->n_pcp && hipMemsetAsync((uint8_t*)P->bscratch.p + P->pflag_off, 0, 8, s) != hipSuccess) return PQG_ERR_HIP;
   }
   const pqg::ErrCount ecount{(uint32_t*)((uint8_t*)P->err.p + err_bytes), P->err_epoch};
   PageWork* work = (PageWork*)P->work.p;
@@ -805,7 +816,7 @@ int pqg_plan_launch(pqg_plan* P) {
     e = pqg::launch_bin_plain(s, P->d_bytes, P->n_bytes, work, cols, (const int32_t*)P->pcol_pages.p,
                               (const int32_t*)P->pcol_start.p, P->n_pcols, (const uint64_t*)P->psegs.p, P->n_psegs, ps,
                               ps + P->n_psegs, (uint32_t*)(scb + P->pticket_off), P->pseg_epoch,
-                              (uint32_t*)(scb + P->pflag_off), P->err_epoch, err, ecount);
+                              (uint32_t*)(scb + P->pflag_off), P->err_epoch, err, ecount, P->plain_pg, P->n_pcp);
   }
   if (e == hipSuccess && P->n_dict_walk)  // BYTE_ARRAY dictionary entries (PlainBinaryDictionary ctor)
     e = pqg::launch_bin_walk(s, P->d_bytes, P->n_bytes, work, cols, bl + P->off_dict_walk, P->n_dict_walk, 1, P->n_pages,

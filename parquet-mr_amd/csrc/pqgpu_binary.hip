@@ -1811,7 +1811,8 @@ struct BpGuess {
 // The chain from pos through tile [B, B + BW_WIN): accepted value starts to L.acc[0, n). With
 // list0 < BW_CAP the candidate list of the whole tile is already in LDS (bp_guess) and pos is its
 // candidate list0 (total0 candidates, listed up to eff0).
-__device__ BpWalk bp_walk(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint32_t B, uint32_t pos, uint32_t end,
+template <class LdsT>
+__device__ BpWalk bp_walk(LdsT& L, const BwBytes& cur, rsrc_t rs, uint32_t B, uint32_t pos, uint32_t end,
                           uint32_t list0 = 0xFFFFFFFFu, uint32_t total0 = 0, uint32_t eff0 = 0) {
   BinWalkLds& W = L.u.w;
   const uint32_t lane = lane_id();
@@ -1973,6 +1974,118 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
   return BpGuess{g, gi, total, eff_end};
 }
 
+// Offsets and value bytes of values [before, before + m) of a page, m <= rn: the rn values the walk
+// accepted in tile [B, B + BW_WIN) start at B + acc[k], the chain left the tile at rpos; img holds the
+// staged page bytes [B, B + img_len) (a value reaching further: the rest from memory). The offsets
+// (offset_k = base(page) + (P_k - data_begin) - 4 k, the last one the end of value m - 1) go to the
+// column's offsets, the value bytes are composed from img into 16-byte output blocks.
+__device__ __forceinline__ void bp_emit(const uint32_t* img, uint32_t img_len, const uint16_t* acc, uint16_t* bt,
+                                        rsrc_t rs, uint32_t B, uint32_t beg, uint32_t rn, uint32_t rpos,
+                                        uint32_t before, uint32_t m, const PageWork& pw, const ColumnDev& cd) {
+  const uint32_t lane = lane_id();
+  // ---- offsets of values before .. before + m (the last one: the end of value m - 1)
+  auto pos_k = [&](uint32_t k) -> uint32_t { return k < rn ? B + acc[k] : rpos; };
+  int64_t* offs = (int64_t*)cd.values + pw.out_offset + before;
+  const uint64_t bb = pw.bin_base;
+  for (uint32_t k = lane; k <= m; k += WAVE)
+    gst(offs + k, (int64_t)(bb + (uint64_t)(pos_k(k) - beg) - 4ull * (uint64_t)(before + k)));
+  const uint64_t o_lo = bb + (uint64_t)(pos_k(0) - beg) - 4ull * before;
+  const uint64_t o_hi0 = bb + (uint64_t)(pos_k(m) - beg) - 4ull * (uint64_t)(before + m);
+  const uint64_t o_hi = o_hi0 < cd.binary_capacity ? o_hi0 : cd.binary_capacity;  // overflow: reported at sync
+  if (o_lo >= o_hi) return;
+  // ---- value bytes: 16-byte output blocks composed from the staged bytes
+  const uint64_t a0 = o_lo & ~15ull;
+  const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
+  const uint32_t P0 = pos_k(0);
+  auto rel = [&](uint32_t k) -> uint32_t { return (pos_k(k) - P0) - 4u * k + r_lo; };  // k <= m
+  for (uint32_t i = lane; i < BP_BLK; i += WAVE) bt[i] = 0;
+  wave_sync();
+  for (uint32_t k = lane; k < m; k += WAVE) {
+    const uint32_t blk = (rel(k) + 15u) >> 4;
+    if (blk < BP_BLK && (k + 1u == m || ((rel(k + 1u) + 15u) >> 4) != blk)) bt[blk] = (uint16_t)k;
+  }
+  wave_sync();
+  {  // running maximum over the blocks: 3 consecutive entries per lane, then across lanes
+    constexpr uint32_t PER = (BP_BLK + WAVE - 1u) / WAVE;
+    uint32_t v[PER], mx = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t i = PER * lane + j;
+      v[j] = i < BP_BLK ? bt[i] : 0u;
+      mx = v[j] > mx ? v[j] : mx;
+    }
+    uint32_t inc = mx;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+      if ((int)lane >= o) inc = y > inc ? y : inc;
+    }
+    uint32_t run = (uint32_t)__shfl_up((int)inc, 1);
+    if (lane == 0) run = 0;
+    wave_sync();
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t i = PER * lane + j;
+      run = v[j] > run ? v[j] : run;
+      if (i < BP_BLK) bt[i] = (uint16_t)run;
+    }
+  }
+  wave_sync();
+  uint8_t* dst = cd.binary_data;
+  const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
+  for (uint32_t b = 16u * lane; b < r_hi; b += 16u * WAVE) {
+    const uint32_t kv = (b >> 4) < BP_BLK ? bt[b >> 4] : m - 1u;  // value of the block's first byte
+    const uint32_t bend = b + 16u < r_hi ? b + 16u : r_hi;
+    const uint32_t rkv = rel(kv);
+    const int64_t Sg = (int64_t)(pos_k(kv) + 4u - B) + (int64_t)b - (int64_t)rkv;  // staged offset of block byte 0
+    uint32_t wd[4];
+    uint32_t have = 0;
+    const bool compose = !(kv + 5u < m && rel(kv + 5u) < bend) && Sg >= 0 && Sg + 36 <= (int64_t)img_len;
+    if (compose) {
+      uint64_t prof = 0;  // nibble i: value starts at or before byte i of the block
+#pragma unroll
+      for (uint32_t j = 1; j <= 4; j++) {
+        const uint32_t kk = kv + j;
+        const uint32_t pj = kk < m ? rel(kk) : 0xFFFFFFFFu;
+        if (pj < bend) prof += 0x1111111111111111ull << (4u * (pj - b));
+      }
+      compose_block(img, (uint32_t)Sg, prof, wd);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t d0 = b + 4u * q;
+        if (d0 >= r_lo && d0 + 4u <= r_hi) have |= 1u << q;
+      }
+    } else {
+      uint32_t k = kv;
+      uint32_t k_end = rel(k + 1u);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t d0 = b + 4u * q;
+        const uint32_t x0 = d0 > r_lo ? d0 : r_lo, x1 = d0 + 4u < r_hi ? d0 + 4u : r_hi;
+        uint32_t word = 0;
+        for (uint32_t c = x0; c < x1;) {
+          while (k + 1u < m && c >= k_end) {
+            k++;
+            k_end = rel(k + 1u);
+          }
+          const uint32_t seg_end = x1 < k_end ? x1 : k_end;
+          const uint32_t sp = pos_k(k) + 4u - B + (c - rel(k));  // page-relative: B + sp
+          const uint32_t v = sp + 4u <= img_len ? img4(img, sp) : ld4_any(rs, B + sp);
+          const uint32_t nb = seg_end - c;
+          const uint32_t msk = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
+          word |= (v & msk) << (8u * (c - d0));
+          c = seg_end;
+        }
+        wd[q] = word;
+        if (x0 == d0 && x1 == d0 + 4u) have |= 1u << q;
+      }
+    }
+    if (!dst_al4) have = 0;  // unaligned byte buffer (C ABI caller): byte stores only
+    store_block16(dst, a0 + b, o_lo, o_hi, wd, have, dst_al16);
+  }
+}
+
+
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) void k_bin_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                         const PageWork* __restrict__ work,
                                                         const ColumnDev* __restrict__ cols,
@@ -2118,115 +2231,95 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) v
   }
   const uint32_t m = r.n < N - before ? r.n : N - before;
   if (m == 0) return;
-  // ---- offsets of values before .. before + m (the last one: the end of value m - 1)
-  const uint32_t rpos = r.pos;
-  auto pos_k = [&](uint32_t k) -> uint32_t { return k < r.n ? B + L.acc[k] : rpos; };
-  int64_t* offs = (int64_t*)cd.values + pw.out_offset + before;
-  const uint64_t bb = pw.bin_base;
-  for (uint32_t k = lane; k <= m; k += WAVE)
-    gst(offs + k, (int64_t)(bb + (uint64_t)(pos_k(k) - beg) - 4ull * (uint64_t)(before + k)));
-  const uint64_t o_lo = bb + (uint64_t)(pos_k(0) - beg) - 4ull * before;
-  const uint64_t o_hi0 = bb + (uint64_t)(pos_k(m) - beg) - 4ull * (uint64_t)(before + m);
-  const uint64_t o_hi = o_hi0 < cd.binary_capacity ? o_hi0 : cd.binary_capacity;  // overflow: reported at sync
-  if (o_lo >= o_hi) return;
-  // ---- value bytes: stage the tile and the start of the next one (the walk's registers), then
-  // compose 16-byte output blocks from LDS (a value reaching further: the rest from memory)
-  wave_sync();  // the walk's candidate list is dead
+  wave_sync();  // the walk's candidate list is dead: stage the tile and the start of the next one
   {
     uint32_t* img = L.u.img;
     *(u32x4*)&img[8u * lane] = cur.a;
     *(u32x4*)&img[8u * lane + 4u] = cur.b;
     img[BW_WIN / 4u + lane] = nxt;
   }
-  const uint64_t a0 = o_lo & ~15ull;
-  const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
-  const uint32_t P0 = pos_k(0);
-  auto rel = [&](uint32_t k) -> uint32_t { return (pos_k(k) - P0) - 4u * k + r_lo; };  // k <= m
-  for (uint32_t i = lane; i < BP_BLK; i += WAVE) L.bt[i] = 0;
   wave_sync();
-  for (uint32_t k = lane; k < m; k += WAVE) {
-    const uint32_t blk = (rel(k) + 15u) >> 4;
-    if (blk < BP_BLK && (k + 1u == m || ((rel(k + 1u) + 15u) >> 4) != blk)) L.bt[blk] = (uint16_t)k;
+  bp_emit(L.u.img, BP_IMG, L.acc, L.bt, rs, B, beg, r.n, r.pos, before, m, pw, cd);
+}
+
+// One-pass PLAIN BYTE_ARRAY for plans with many PLAIN pages (k_bin_plain_pg): one wave per page
+// follows its chain tile after tile from the section start (bp_walk from a known position: no guess,
+// no look-back, the values before a tile are the wave's running count) and emits every tile's offsets
+// and value bytes from the tile and the next one staged in LDS (bp_emit). The next tile's bytes are
+// in registers before the current tile's stores, the one after it is requested before them. With
+// thousands of pages one wave per page fills the chip; the tile kernel (k_bin_plain) spreads few pages
+// over many waves. Same semantics as k_bin_plain: errors at the per-value path's index, a page whose
+// values do not end at its section end raises the inexact flag (pqg_sync re-runs the plan per value).
+struct BinPageLds {
+  union {
+    BinWalkLds w;                         // the tile walk (candidate list)
+    uint32_t img[2u * BW_WIN / 4u + 16];  // then: page bytes [B, B + 2 BW_WIN) (+ slack for the compose reads)
+  } u;
+  uint16_t acc[BW_CAP + 2];  // accepted value starts of the tile (offsets from B), ascending
+  uint16_t bt[BP_BLK + 2];   // output block -> the last value starting at or before its first byte
+};
+static_assert(sizeof(BinPageLds) * WPB <= 160 * 1024 / 6, "6 workgroups of k_bin_plain_pg per CU");
+
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) void k_bin_plain_pg(
+    const uint8_t* __restrict__ bytes, uint64_t n_bytes, const PageWork* __restrict__ work,
+    const ColumnDev* __restrict__ cols, const int32_t* __restrict__ list, int n_list, uint32_t* inexact,
+    uint32_t flag_epoch, uint64_t* err, ErrCount err_count) {
+  __shared__ __attribute__((aligned(16))) BinPageLds lds_all[WPB];
+  const int page = wave_page(list, n_list);
+  if (page < 0) return;
+  BinPageLds& L = lds_all[wave_id()];
+  const uint32_t lane = lane_id();
+  const PageWork& pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t beg = uni(pw.data_begin), end = uni(pw.size), N = uni(pw.n_values);
+  if (N == 0 || beg >= end) {
+    if (lane == 0) {
+      if (N > 0) report(err, err_count, page, 2, 0, PQG_ERR_EOF);  // no section: value 0
+      else if (beg < end) sst(inexact, flag_epoch);                // bytes but no values: base() assumes none
+    }
+    return;
   }
-  wave_sync();
-  {  // running maximum over the blocks: 3 consecutive entries per lane, then across lanes
-    constexpr uint32_t PER = (BP_BLK + WAVE - 1u) / WAVE;
-    uint32_t v[PER], mx = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < PER; j++) {
-      const uint32_t i = PER * lane + j;
-      v[j] = i < BP_BLK ? L.bt[i] : 0u;
-      mx = v[j] > mx ? v[j] : mx;
+  const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
+  uint32_t pos = beg, before = 0;
+  uint32_t B = beg & ~(BW_WIN - 1u);
+  BwBytes cur = bw_load(rs, B), nxt = bw_load(rs, B + BW_WIN);
+  while (true) {
+    pos = uni(pos);
+    before = uni(before);
+    B = uni(B);
+    const BpWalk r = bp_walk(L, cur, rs, B, pos, end);
+    if (r.code && before + r.n < N && lane == 0) report(err, err_count, page, 2, before + r.n, r.code);
+    bool last = r.code != 0;
+    if (before + r.n >= N) {  // the page's last value is here: it must end at the section end
+      const uint32_t q = N - 1u - before;
+      const uint32_t e_last = q + 1u < r.n ? B + L.acc[q + 1u] : r.pos;
+      if ((q + 1u < r.n || e_last != end) && lane == 0) sst(inexact, flag_epoch);
+      last = true;
     }
-    uint32_t inc = mx;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
-      if ((int)lane >= o) inc = y > inc ? y : inc;
+    const uint32_t m = r.n < N - before ? r.n : N - before;
+    wave_sync();  // the walk's candidate list is dead: stage this tile and the next one
+    *(u32x4*)&L.u.img[8u * lane] = cur.a;
+    *(u32x4*)&L.u.img[8u * lane + 4u] = cur.b;
+    *(u32x4*)&L.u.img[BW_WIN / 4u + 8u * lane] = nxt.a;
+    *(u32x4*)&L.u.img[BW_WIN / 4u + 8u * lane + 4u] = nxt.b;
+    // the tile holding the next value (r.pos >= B + BW_WIN: the walk left this tile) and the one after
+    // it, requested before this tile's stores
+    const uint32_t nB = r.pos & ~(BW_WIN - 1u);
+    if (!last) {
+      if (nB == B + BW_WIN) {
+        cur = nxt;
+      } else {  // a value longer than a tile
+        cur = bw_load(rs, nB);
+      }
+      nxt = bw_load(rs, nB + BW_WIN);
     }
-    uint32_t run = (uint32_t)__shfl_up((int)inc, 1);
-    if (lane == 0) run = 0;
     wave_sync();
-#pragma unroll
-    for (uint32_t j = 0; j < PER; j++) {
-      const uint32_t i = PER * lane + j;
-      run = v[j] > run ? v[j] : run;
-      if (i < BP_BLK) L.bt[i] = (uint16_t)run;
-    }
-  }
-  wave_sync();
-  uint8_t* dst = cd.binary_data;
-  const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
-  const uint32_t* img = L.u.img;
-  for (uint32_t b = 16u * lane; b < r_hi; b += 16u * WAVE) {
-    const uint32_t kv = (b >> 4) < BP_BLK ? L.bt[b >> 4] : m - 1u;  // value of the block's first byte
-    const uint32_t bend = b + 16u < r_hi ? b + 16u : r_hi;
-    const uint32_t rkv = rel(kv);
-    const int64_t Sg = (int64_t)(pos_k(kv) + 4u - B) + (int64_t)b - (int64_t)rkv;  // staged offset of block byte 0
-    uint32_t wd[4];
-    uint32_t have = 0;
-    const bool compose = !(kv + 5u < m && rel(kv + 5u) < bend) && Sg >= 0 && Sg + 36 <= (int64_t)BP_IMG;
-    if (compose) {
-      uint64_t prof = 0;  // nibble i: value starts at or before byte i of the block
-#pragma unroll
-      for (uint32_t j = 1; j <= 4; j++) {
-        const uint32_t kk = kv + j;
-        const uint32_t pj = kk < m ? rel(kk) : 0xFFFFFFFFu;
-        if (pj < bend) prof += 0x1111111111111111ull << (4u * (pj - b));
-      }
-      compose_block(img, (uint32_t)Sg, prof, wd);
-#pragma unroll
-      for (uint32_t q = 0; q < 4; q++) {
-        const uint32_t d0 = b + 4u * q;
-        if (d0 >= r_lo && d0 + 4u <= r_hi) have |= 1u << q;
-      }
-    } else {
-      uint32_t k = kv;
-      uint32_t k_end = rel(k + 1u);
-#pragma unroll
-      for (uint32_t q = 0; q < 4; q++) {
-        const uint32_t d0 = b + 4u * q;
-        const uint32_t x0 = d0 > r_lo ? d0 : r_lo, x1 = d0 + 4u < r_hi ? d0 + 4u : r_hi;
-        uint32_t word = 0;
-        for (uint32_t c = x0; c < x1;) {
-          while (k + 1u < m && c >= k_end) {
-            k++;
-            k_end = rel(k + 1u);
-          }
-          const uint32_t seg_end = x1 < k_end ? x1 : k_end;
-          const uint32_t sp = pos_k(k) + 4u - B + (c - rel(k));  // page-relative: B + sp
-          const uint32_t v = sp + 4u <= BP_IMG ? img4(img, sp) : ld4_any(rs, B + sp);
-          const uint32_t nb = seg_end - c;
-          const uint32_t msk = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
-          word |= (v & msk) << (8u * (c - d0));
-          c = seg_end;
-        }
-        wd[q] = word;
-        if (x0 == d0 && x1 == d0 + 4u) have |= 1u << q;
-      }
-    }
-    if (!dst_al4) have = 0;  // unaligned byte buffer (C ABI caller): byte stores only
-    store_block16(dst, a0 + b, o_lo, o_hi, wd, have, dst_al16);
+    if (m) bp_emit(L.u.img, 2u * BW_WIN, L.acc, L.bt, rs, B, beg, r.n, r.pos, before, m, pw, cd);
+    if (last) break;
+    before += r.n;
+    pos = r.pos;
+    B = nB;
+    wave_sync();  // the emit's LDS reads are done before the next walk's list
   }
 }
 
@@ -2304,12 +2397,19 @@ hipError_t launch_bin_walk_seg(hipStream_t st, const uint8_t* bytes, uint64_t n_
 hipError_t launch_bin_plain(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                             const int32_t* col_pages, const int32_t* col_start, int n_cols, const uint64_t* segs,
                             uint32_t n_segs, uint64_t* aggw, uint64_t* incw, uint32_t* ticket, uint32_t epoch,
-                            uint32_t* inexact, uint32_t flag_epoch, uint64_t* err, ErrCount err_count) {
+                            uint32_t* inexact, uint32_t flag_epoch, uint64_t* err, ErrCount err_count,
+                            bool per_page, int n_pages_total) {
   if (n_cols <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_bin_bases, dim3(n_cols), dim3(256), 0, st, work, cols, col_pages, col_start);
-  if (n_segs)
+  if (per_page) {  // one wave per page of col_pages
+    const int n = n_pages_total;
+    if (n > 0)
+      hipLaunchKernelGGL(k_bin_plain_pg, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols,
+                         col_pages, n, inexact, flag_epoch, err, err_count);
+  } else if (n_segs) {
     hipLaunchKernelGGL(k_bin_plain, dim3((n_segs + WPB - 1) / WPB), dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols,
                        segs, n_segs, aggw, incw, ticket, epoch, inexact, flag_epoch, err, err_count);
+  }
   return hipGetLastError();
 }
 

@@ -158,11 +158,14 @@ hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
 // (page | tile << 32, in column / page / tile order). aggw / incw: per tile, tagged with `epoch`
 // (1..255; zeroed when it wraps); ticket: zeroed before the launch; inexact: set to flag_epoch when a
 // page's values do not end at its section end (the plan is then re-run on the per-value path).
+// per_page (plans with BW_SEG_MAX_PAGES or more PLAIN pages): k_bin_plain_pg, one wave per page of
+// col_pages[0, n_pages_total), instead of the tiles.
 constexpr uint32_t BP_TILE = 2048;
 hipError_t launch_bin_plain(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                             const int32_t* col_pages, const int32_t* col_start, int n_cols, const uint64_t* segs,
                             uint32_t n_segs, uint64_t* aggw, uint64_t* incw, uint32_t* ticket, uint32_t epoch,
-                            uint32_t* inexact, uint32_t flag_epoch, uint64_t* err, ErrCount err_count);
+                            uint32_t* inexact, uint32_t flag_epoch, uint64_t* err, ErrCount err_count,
+                            bool per_page, int n_pages_total);
 hipError_t launch_bin_walk_seg(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const uint64_t* segs, uint32_t n_segs, uint64_t* status,
                                uint32_t* ticket, uint32_t* tmp, uint64_t* err, ErrCount err_count);
