@@ -285,6 +285,13 @@ def run_c4(args, world, rank, devi):
             "gb_per_s": total_bytes * args.steps / t_max / 1e9,
             "hbm_frac_per_gpu": total_bytes * args.steps / t_max / 1e9 / world / HBM_PEAK_GBS,
             "kernels_per_launch": plan.kernel_count,
+            # the bound of the whole launch (13 kernels, each HBM-bound integer / byte work): algorithmic
+            # bytes = every column's encoded page bytes read + dense outputs written, per GPU
+            "roofline": {"bound": "hbm", "achieved": total_bytes / world / (t_max / args.steps) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": total_bytes / world / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "whole plan launch (all kernels of the shard)",
+                         "algorithmic_bytes_per_launch": total_bytes / world},
             "verified": None if args.no_verify else "every row group x column slice == its generated values, first launch "
                                                     "of a fresh plan and after the timed launches",
             "cpu_baseline": cpu, "input_gen_s": t_gen,

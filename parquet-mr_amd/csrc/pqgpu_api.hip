@@ -589,6 +589,23 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     for (uint64_t b : bin_blocks) nb += plain_col[(size_t)(b >> 32)] ? 0 : 1;
     P->n_bin_blocks_nf = nb;
   }
+  // dictionary-direct BYTE_ARRAY columns (ColumnDev::dict_direct): required, every data page
+  // dictionary-encoded, the dictionary page small enough to stage in the offset scan
+  std::vector<uint8_t> dict_direct((size_t)std::max(n_cols, 1), 0);
+  {
+    std::vector<int> npg((size_t)std::max(n_cols, 1), 0), nids((size_t)std::max(n_cols, 1), 0);
+    for (int p = 0; p < n_pages; p++) {
+      const int c = P->h_work[(size_t)p].column;
+      npg[(size_t)c]++;
+      if (P->page_cls[(size_t)p] == C_IDS) nids[(size_t)c]++;
+    }
+    for (int i = 0; i < n_cols; i++)
+      dict_direct[(size_t)i] = cols[i].physical_type == PQG_BYTE_ARRAY && bin_out(cols[i]) && !ids_mode(cols[i]) &&
+                               !col_err[(size_t)i] && !dba_fixed[(size_t)i] && !plain_col[(size_t)i] &&
+                               cols[i].max_def == 0 && cols[i].max_rep == 0 && cols[i].dict_offset >= 0 &&
+                               cols[i].dict_size <= pqg::DD_DICT_MAX && npg[(size_t)i] > 0 &&
+                               nids[(size_t)i] == npg[(size_t)i] && getenv("PQGPU_NO_DICT_DIRECT") == nullptr;
+  }
   std::vector<uint64_t> plain_chunks;  // copy chunks of the one-pass columns (per-value fallback only)
   for (int k : {C_IDS, C_BINP, C_DLBA})
     for (int p : cls_lists[(size_t)k]) {
@@ -599,6 +616,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
         continue;
       }
       if (k == C_IDS && ids_mode(cols[w.column])) continue;  // the ids are the output
+      if (k == C_IDS && dict_direct[(size_t)w.column]) continue;  // the offset scan writes the bytes
       if (k == C_IDS && cols[w.column].physical_type != PQG_BYTE_ARRAY) {
         fixd.push_back(p);
         continue;
@@ -715,6 +733,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       d.block_sums = (uint64_t*)at(bsum_off[(size_t)i]);
       d.bin_total = (uint64_t*)at(P->bin_total_off[(size_t)i]);
       d.n_slots = slot_acc[(size_t)i];
+      d.dict_direct = dict_direct[(size_t)i];
       if (dba_fixed[(size_t)i]) {  // DELTA_BYTE_ARRAY values go straight to the fixed-width output
         d.binary_data = (uint8_t*)cols[i].values;
         d.binary_capacity = slot_acc[(size_t)i] * (uint64_t)d.elem_width;
@@ -868,7 +887,7 @@ int pqg_plan_launch(pqg_plan* P) {
     e = pqg::launch_gather_fixed(s, P->d_bytes, P->n_bytes, work, cols, bl + P->off_fixd, P->n_fixd);
   const uint32_t n_blocks = pf ? P->n_bin_blocks_nf : P->n_bin_blocks;
   if (e == hipSuccess && n_blocks)
-    e = pqg::launch_bin_scan(s, cols, bl + P->off_bin_cols, pf ? P->n_bin_cols_nf : P->n_bin_cols,
+    e = pqg::launch_bin_scan(s, P->d_bytes, P->n_bytes, cols, bl + P->off_bin_cols, pf ? P->n_bin_cols_nf : P->n_bin_cols,
                              (const uint64_t*)P->bin_blocks.p, n_blocks);
   const uint32_t n_chunks = pf ? P->n_bin_chunks_nf : P->n_bin_chunks;
   if (e == hipSuccess && n_chunks)

@@ -577,6 +577,32 @@ __global__ __launch_bounds__(256) void k_gather_fixed(const uint8_t* __restrict_
   }
 }
 
+// 4 source bytes at staged offset i (any alignment): two aligned LDS dwords and a byte align.
+__device__ __forceinline__ uint32_t img4(const uint32_t* img, uint32_t i) {
+  return __builtin_amdgcn_alignbyte(img[(i >> 2) + 1], img[i >> 2], i & 3u);
+}
+
+// Store the 16-byte output block at `a` (dwords wd) clipped to [o_lo, o_hi): one 16-byte store
+// when the block is whole and aligned, dword stores for whole dwords, byte stores at the edges
+// (which neighbouring chunks / pages share). have: bit q = dword q whole (0 for an unaligned dst).
+__device__ __forceinline__ void store_block16(uint8_t* dst, uint64_t a, uint64_t o_lo, uint64_t o_hi,
+                                              const uint32_t (&wd)[4], uint32_t have, bool dst_al16) {
+  if (have == 0xFu && dst_al16) {
+    gst_nt((u32x4*)(dst + a), u32x4{wd[0], wd[1], wd[2], wd[3]});
+    return;
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    const uint64_t d0 = a + 4u * q;
+    if ((have >> q) & 1u) {
+      gst((uint32_t*)(dst + d0), wd[q]);
+    } else {
+      for (uint32_t j = 0; j < 4; j++)
+        if (d0 + j >= o_lo && d0 + j < o_hi) gst(dst + d0 + j, (uint8_t)(wd[q] >> (8u * j)));
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Offsets of BYTE_ARRAY columns: exclusive scan of blen over [0, n_slots) (entries past the
 // column's decoded values hold 0: blen is cleared before every launch), written as int64
@@ -605,6 +631,15 @@ __device__ __forceinline__ u32x4 scan_row_load(const uint32_t* blen, uint64_t n_
   return x;
 }
 
+// dict_direct columns: blen holds dictionary ids; the length of value id (0 for an invalid id, which
+// the dictionary kernel reported, as k_bin_dict_map maps it)
+__device__ __forceinline__ u32x4 dd_lengths(const ColumnDev& cd, u32x4 id, uint32_t dn, uint64_t v, uint64_t n_slots) {
+  u32x4 l;
+#pragma unroll
+  for (int k = 0; k < 4; k++) l[k] = id[k] < dn && v + k < n_slots ? cd.dict_len[id[k]] : 0u;
+  return l;
+}
+
 __global__ __launch_bounds__(256) void k_bin_block_sums(const ColumnDev* __restrict__ cols,
                                                         const uint64_t* __restrict__ blocks) {
   __shared__ uint64_t red[4];
@@ -614,6 +649,11 @@ __global__ __launch_bounds__(256) void k_bin_block_sums(const ColumnDev* __restr
   u32x4 x[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) x[i] = scan_row_load(cd.blen, cd.n_slots, v0 + 1024u * i + 4u * threadIdx.x);
+  if (uni(cd.dict_direct)) {
+    const uint32_t dn = uni(cd.dict_n);
+#pragma unroll
+    for (int i = 0; i < 4; i++) x[i] = dd_lengths(cd, x[i], dn, v0 + 1024u * i + 4u * threadIdx.x, cd.n_slots);
+  }
   uint64_t s = 0;
 #pragma unroll
   for (int i = 0; i < 4; i++) s += (uint64_t)x[i][0] + x[i][1] + (uint64_t)x[i][2] + x[i][3];
@@ -667,22 +707,94 @@ __global__ __launch_bounds__(256) void k_bin_block_bases(const ColumnDev* __rest
 // Offsets of one scan block: per row, a wave scan of the threads' 4-length sums and the wave
 // totals through LDS (4 rows scanned side by side: one barrier per block instead of two per
 // 256 lengths); offsets stored as two 16-byte stores per row and thread.
-__global__ __launch_bounds__(256) void k_bin_offsets(const ColumnDev* __restrict__ cols,
+// dict_direct: the dictionary page staged once per workgroup, then per row of 1,024 values an output
+// image of the row's bytes (each value's entry scattered into it, 4 bytes per step) stored as 16-byte
+// blocks; a row whose bytes exceed the image is written with byte stores
+constexpr uint32_t DD_OUT = 16384;
+struct DictDirectLds {
+  uint32_t dict[DD_DICT_MAX / 4 + 4];
+  uint32_t out[DD_OUT / 4 + 4];
+};
+
+__device__ __noinline__ void dd_row_bytes(const ColumnDev& cd, DictDirectLds& D, u32x4 ids, uint64_t v, uint64_t n_slots,
+                                          uint64_t e, uint64_t o_lo, uint64_t o_hi) {
+  const uint32_t t = threadIdx.x;
+  uint8_t* dst = cd.binary_data;
+  const uint32_t dbytes = (uint32_t)cd.dict_bytes, dn = uni(cd.dict_n);
+  const uint64_t a0 = o_lo & ~15ull;
+  const bool img = o_hi - a0 + 16u <= DD_OUT;
+  uint8_t* outb = (uint8_t*)D.out;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t id = ids[k];
+    const bool ok = id < dn && v + k < n_slots;
+    const uint32_t sp = ok ? cd.dict_src[id] : 0u, len = ok ? cd.dict_len[id] : 0u;
+    for (uint32_t j = 0; j < len; j += 4u) {
+      const uint32_t w = sp + j < dbytes ? img4(D.dict, sp + j) : 0u;  // (bytes past the entry: masked)
+#pragma unroll
+      for (uint32_t q = 0; q < 4u; q++) {
+        const uint64_t o = e + j + q;
+        if (j + q < len && o < o_hi) {
+          if (img) outb[o - a0] = (uint8_t)(w >> (8u * q));
+          else gst(dst + o, (uint8_t)(w >> (8u * q)));
+        }
+      }
+    }
+    e += len;
+  }
+  if (!img) return;
+  __syncthreads();
+  const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
+  const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
+  for (uint32_t bb = 16u * t; bb < r_hi; bb += 16u * 256u) {
+    const u32x4 v4 = *(const u32x4*)(outb + bb);
+    uint32_t wd[4] = {v4.x, v4.y, v4.z, v4.w};
+    uint32_t have = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      const uint32_t d0 = bb + 4u * q;
+      if (d0 >= r_lo && d0 + 4u <= r_hi) have |= 1u << q;
+    }
+    if (!dst_al4) have = 0;
+    store_block16(dst, a0 + bb, o_lo, o_hi, wd, have, dst_al16);
+  }
+  __syncthreads();  // the image is reused by the next row
+}
+
+__global__ __launch_bounds__(256) void k_bin_offsets(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                     const ColumnDev* __restrict__ cols,
                                                      const uint64_t* __restrict__ blocks) {
   __shared__ uint64_t wsum[4][4];  // [row][wave]
+  __shared__ uint64_t rowb[5];     // dict_direct: output offset of each row's first value (+ the block end)
+  __shared__ __attribute__((aligned(16))) DictDirectLds D;
   const uint64_t b = blocks[blockIdx.x];
   const ColumnDev& cd = cols[(uint32_t)(b >> 32)];
   const uint64_t v0 = (uint64_t)(uint32_t)b * SCAN_BLOCK;
   const uint64_t n_slots = cd.n_slots;
   int64_t* off = (int64_t*)cd.values;
   const uint32_t t = threadIdx.x, wv = t >> 6, lane = lane_id();
-  u32x4 x[4];
-  uint64_t inc[4];
+  const bool dd = uni(cd.dict_direct) != 0;
+  u32x4 x[4], ids[4];
+  uint64_t inc[4], first[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     x[i] = scan_row_load(cd.blen, n_slots, v0 + 1024u * i + 4u * t);
-    inc[i] = (uint64_t)x[i][0] + x[i][1] + (uint64_t)x[i][2] + x[i][3];
+    ids[i] = x[i];
   }
+  if (dd) {
+    const uint32_t dn = uni(cd.dict_n);
+#pragma unroll
+    for (int i = 0; i < 4; i++) x[i] = dd_lengths(cd, x[i], dn, v0 + 1024u * i + 4u * t, n_slots);
+    // stage the dictionary page (a resource over the rest of the batch: a 16-byte load that crosses
+    // the end of its range returns 0 as a whole, which would drop the page's last bytes; only entry
+    // bytes are ever read from the staged page)
+    const rsrc_t drs = make_rsrc(bytes + cd.dict_offset, n_bytes - cd.dict_offset);
+    const uint32_t nd = (uint32_t)((cd.dict_bytes + 15u) & ~15ull);
+    for (uint32_t o = 16u * t; o < nd; o += 16u * 256u)
+      *(u32x4*)&D.dict[o >> 2] = __builtin_amdgcn_raw_buffer_load_b128(drs, (int)o, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) inc[i] = (uint64_t)x[i][0] + x[i][1] + (uint64_t)x[i][2] + x[i][3];
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
 #pragma unroll
@@ -725,13 +837,22 @@ __global__ __launch_bounds__(256) void k_bin_offsets(const ColumnDev* __restrict
     // the final offset (the column's byte total) after the last slot
     if (v < n_slots && n_slots <= v + 4) gst(off + n_slots, (int64_t)(n_slots - v == 1 ? e1 : n_slots - v == 2 ? e2
                                                                      : n_slots - v == 3 ? e3 : e4));
+    first[i] = e0;
+    if (dd && t == 0) rowb[i] = e0;  // the row's first offset
+    if (dd && i == 3 && t == 255) rowb[4] = e4;
+  }
+  if (!dd) return;
+  // ---- value bytes of the block, row by row (values past n_slots have length 0)
+  __syncthreads();  // rowb, the staged dictionary
+  const uint64_t cap = cd.binary_capacity;
+#pragma unroll 1
+  for (int i = 0; i < 4; i++) {
+    const uint64_t o_lo = rowb[i], o_hi = rowb[i + 1] < cap ? rowb[i + 1] : cap;  // overflow: reported at sync
+    if (o_lo < o_hi) dd_row_bytes(cd, D, ids[i], v0 + 1024u * i + 4u * t, n_slots, first[i], o_lo, o_hi);
   }
 }
 
 // ---------------------------------------------------------------------------
-// Store the 16-byte output block at `a` (dwords wd) clipped to [o_lo, o_hi): one 16-byte store
-// when the block is whole and aligned, dword stores for whole dwords, byte stores at the edges
-// (which neighbouring chunks / pages share). have: bit q = dword q whole (0 for an unaligned dst).
 // c ? y : x per lane, as v_cndmask the optimizer cannot see through: selects among elements of a
 // register array are otherwise turned into an indexed access, which puts the array in scratch (and
 // scratch loads wait for every store in flight)
@@ -747,23 +868,6 @@ __device__ __forceinline__ uint32_t pick8(const uint32_t (&a)[8], uint32_t i) {
   return vsel(b2, vsel(b1, x0, x1), vsel(b1, x2, x3));
 }
 
-__device__ __forceinline__ void store_block16(uint8_t* dst, uint64_t a, uint64_t o_lo, uint64_t o_hi,
-                                              const uint32_t (&wd)[4], uint32_t have, bool dst_al16) {
-  if (have == 0xFu && dst_al16) {
-    gst_nt((u32x4*)(dst + a), u32x4{wd[0], wd[1], wd[2], wd[3]});
-    return;
-  }
-#pragma unroll
-  for (uint32_t q = 0; q < 4; q++) {
-    const uint64_t d0 = a + 4u * q;
-    if ((have >> q) & 1u) {
-      gst((uint32_t*)(dst + d0), wd[q]);
-    } else {
-      for (uint32_t j = 0; j < 4; j++)
-        if (d0 + j >= o_lo && d0 + j < o_hi) gst(dst + d0 + j, (uint8_t)(wd[q] >> (8u * j)));
-    }
-  }
-}
 
 // Value bytes of values [i_lo, i_hi) of one page, by one wave (the per-wave path of k_bin_copy,
 // for chunks whose source does not fit the workgroup's LDS staging: long values, large
@@ -1049,10 +1153,6 @@ union CopyLds {
   CopyWaveLds w[WPB];
 };
 
-// 4 source bytes at staged offset i (any alignment): two aligned LDS dwords and a byte align.
-__device__ __forceinline__ uint32_t img4(const uint32_t* img, uint32_t i) {
-  return __builtin_amdgcn_alignbyte(img[(i >> 2) + 1], img[i >> 2], i & 3u);
-}
 
 // One 16-byte output block of length-prefixed values composed from staged source bytes: Sv = staged
 // offset of the block's byte 0 counting no value start inside the block; prof nibble i = the value
@@ -1174,6 +1274,42 @@ __global__ __launch_bounds__(64 * WPB) PQG_COPY_OCC void k_bin_copy(const uint8_
       const uint64_t avail = pw.size > pw.aux ? pw.size - pw.aux : 0;
       if (r + len > avail) report(err, err_count, page, 2, i_lo + k, PQG_ERR_EOF);
     }
+  // Dictionary chunks of short values (C4's flags and modes: 1-17 bytes): every value's bytes are
+  // scattered from the staged dictionary into an output image after it in LDS (4 bytes per step), then
+  // the image goes out as 16-byte blocks. Composing a 16-byte block that holds many value starts took
+  // one LDS round trip per piece (k_bin_copy 7.5 ms of the C4 125M-row shard for 500 M such values).
+  const uint32_t ob = (n_st + 15u) & ~15u;  // byte offset of the output image in L.img
+  if (from_dict && o_hi0 - a0 <= 16ull * n && ob + (uint32_t)(o_hi0 - a0) + 16u <= CP_SRC) {
+    __syncthreads();  // staged dictionary, rel, src
+    uint8_t* outb = (uint8_t*)L.img + ob;
+    for (uint32_t k = t; k < n; k += 64u * WPB) {
+      const uint32_t r = L.rel[k], len = L.rel[k + 1] - r, sp = L.src[k];
+      for (uint32_t j = 0; j < len; j += 4u) {
+        const uint32_t v = sp + j < n_st ? img4(L.img, sp + j) : 0u;  // (bytes past the value: masked)
+#pragma unroll
+        for (uint32_t e = 0; e < 4u; e++)
+          if (j + e < len) outb[r + j + e] = (uint8_t)(v >> (8u * e));
+      }
+    }
+    __syncthreads();
+    if (o_lo >= o_hi) continue;
+    uint8_t* dst = cd.binary_data;
+    const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
+    const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
+    for (uint32_t b = 16u * t; b < r_hi; b += 16u * 64u * WPB) {
+      const u32x4 v4 = *(const u32x4*)(outb + b);
+      uint32_t wd[4] = {v4.x, v4.y, v4.z, v4.w};
+      uint32_t have = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t d0 = b + 4u * q;
+        if (d0 >= r_lo && d0 + 4u <= r_hi) have |= 1u << q;
+      }
+      if (!dst_al4) have = 0;
+      store_block16(dst, a0 + b, o_lo, o_hi, wd, have, dst_al16);
+    }
+    continue;
+  }
   const uint32_t nblk = (uint32_t)((o_hi0 - a0 + 15u) >> 4);
   for (uint32_t i = t; i < nblk; i += 64u * WPB) L.bt[i] = 0;
   __syncthreads();
@@ -1753,8 +1889,12 @@ static_assert(sizeof(BinPlainLds) * WPB <= 160 * 1024 / 6, "6 workgroups of k_bi
 
 // Candidates of tile [B, B + BW_WIN) from position pos on (see bin_walk_core); returns their number
 // (at most BW_CAP: eff_end is then the first candidate not listed).
+// fast: only lengths below 256 (a value start of a longer value is then missing from the list, and
+// the walk takes the tile again with every length): the byte before a length prefix, read as a
+// length, is 256 x the true one plus a string byte, so short-string pages list (almost) only their
+// true value starts: half the candidates, and batches whose candidates link one to the next.
 __device__ __forceinline__ uint32_t bp_candidates(BinWalkLds& W, const BwBytes& cur, uint32_t B, uint32_t pos,
-                                                  uint32_t end, uint32_t& eff_end) {
+                                                  uint32_t end, uint32_t& eff_end, bool fast = false) {
   const uint32_t lane = lane_id();
   const uint32_t base = B + BW_Q * lane;
   uint32_t d[BW_Q / 4 + 1];
@@ -1763,11 +1903,19 @@ __device__ __forceinline__ uint32_t bp_candidates(BinWalkLds& W, const BwBytes& 
   d[8] = cur.x;
   uint32_t m = 0;
   const int32_t rem0 = (int32_t)(end - 4u - base);
+  if (fast) {
 #pragma unroll
-  for (uint32_t q = 0; q < BW_Q; q++) {
-    const uint32_t len = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
-    const int32_t rem = rem0 - (int32_t)q;
-    m |= (rem >= 0 && len <= (uint32_t)rem ? 1u : 0u) << q;
+    for (uint32_t q = 0; q < BW_Q; q++) {
+      const uint32_t len = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
+      m |= (len < 256u && (int32_t)(len + q) <= rem0 ? 1u : 0u) << q;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t q = 0; q < BW_Q; q++) {
+      const uint32_t len = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
+      const int32_t rem = rem0 - (int32_t)q;
+      m |= (rem >= 0 && len <= (uint32_t)rem ? 1u : 0u) << q;
+    }
   }
   if (base < pos) m &= pos - base >= BW_Q ? 0u : ~((1u << (pos - base)) - 1u);
   uint32_t total;
@@ -1806,36 +1954,45 @@ struct BpWalk {
 
 struct BpGuess {
   uint32_t pos, index, total, eff_end;  // guessed start (0xFFFFFFFF: none), its candidate index, the list
+  bool fast;                            // the list holds short lengths only (bp_candidates fast)
 };
 
 // The chain from pos through tile [B, B + BW_WIN): accepted value starts to L.acc[0, n). With
 // list0 < BW_CAP the candidate list of the whole tile is already in LDS (bp_guess) and pos is its
 // candidate list0 (total0 candidates, listed up to eff0).
-template <class LdsT>
+template <bool FAST, class LdsT>
 __device__ BpWalk bp_walk(LdsT& L, const BwBytes& cur, rsrc_t rs, uint32_t B, uint32_t pos, uint32_t end,
-                          uint32_t list0 = 0xFFFFFFFFu, uint32_t total0 = 0, uint32_t eff0 = 0) {
+                          uint32_t list0 = 0xFFFFFFFFu, uint32_t total0 = 0, uint32_t eff0 = 0, bool list_fast = false) {
   BinWalkLds& W = L.u.w;
   const uint32_t lane = lane_id();
   uint32_t n = 0;
   int code = 0;
   const uint32_t tend = B + BW_WIN;
   bool listed = list0 < BW_CAP;
+  bool fast = listed ? list_fast : FAST;  // short lengths first; every length once a value start is missing
   while (true) {
     pos = uni(pos);
     n = uni(n);
     if (pos >= tend) break;
     if ((uint64_t)pos + 4u > end) { code = PQG_ERR_EOF; break; }
     uint32_t eff_end, total, i0 = 0;
+    bool fast_pass = false;
     if (listed) {  // the guess's list, from the guessed candidate on
       total = total0;
       eff_end = eff0;
       i0 = list0;
       listed = false;
+      fast_pass = fast;
     } else {
       wave_sync();  // the previous pass's list reads are done
-      total = bp_candidates(W, cur, B, pos, end, eff_end);
+      fast_pass = fast;
+      total = bp_candidates(W, cur, B, pos, end, eff_end, fast_pass);
     }
     if (total == 0 || W.pn[i0].x != pos) {
+      if (fast_pass) {  // pos is a longer value's start: list the tile again with every length
+        fast = false;
+        continue;
+      }
       code = bin_value_error(rs, pos, end, false);
       break;
     }
@@ -1877,12 +2034,17 @@ __device__ BpWalk bp_walk(LdsT& L, const BwBytes& cur, rsrc_t rs, uint32_t B, ui
       if (nxt >= eff_end) { leave = true; break; }
       const uint32_t a = uni(bw_index(W, nxt - B));
       if (a >= total || a <= i0 + last) {
+        if (fast_pass) {  // the next value start has a longer length: list the rest again
+          fast = false;
+          break;
+        }
         code = bin_value_error(rs, nxt, end, false);
         break;
       }
       i0 = a;
     }
-    if (code || !leave) break;
+    if (code) break;
+    if (!leave && !(fast_pass && !fast)) break;
   }
   wave_sync();
   return BpWalk{uni(pos), uni(n), code};
@@ -1900,8 +2062,28 @@ __device__ BpWalk bp_walk(LdsT& L, const BwBytes& cur, rsrc_t rs, uint32_t B, ui
 __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint32_t B, uint32_t end) {
   BinWalkLds& W = L.u.w;
   uint32_t eff_end;
-  const uint32_t total = bp_candidates(W, cur, B, B, end, eff_end);
   const uint32_t lane = lane_id();
+  {  // short-length candidates that link one to the next from the first to one leaving the tile: the
+     // first is the guess (no pointer jumping; short-string pages, where false candidates are rare)
+    const uint32_t tf = bp_candidates(W, cur, B, B, end, eff_end, true);
+    bool ok = tf > 0;
+    for (uint32_t k0 = 0; k0 < tf && ok; k0 += WAVE) {
+      const uint32_t k = k0 + lane;
+      bool good = true;
+      if (k < tf) {
+        const uint32_t sc = W.pn[k].y, so = sc - B;
+        good = k + 1u < tf ? (so < BW_WIN && bw_index(W, so) == k + 1u) : sc >= eff_end;
+      }
+      ok = __ballot(!good) == 0ull;
+    }
+    if (ok) {
+      const uint32_t g = uni(W.pn[0].x);
+      wave_sync();
+      return BpGuess{g, 0, tf, eff_end, true};
+    }
+    wave_sync();  // the exact list replaces it
+  }
+  const uint32_t total = bp_candidates(W, cur, B, B, end, eff_end);
   // node i: J = successor index, or (last index | 0x8000) once the chain leaves the list, 0xFFFF when
   // it breaks; D = values on the chain so far (L.pj: J | D << 16). 6 rounds: a chain of more than 64
   // values is not followed to its end but ranked by where its 64th value lies (the true start's chain
@@ -1971,7 +2153,7 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
   const uint32_t gi = 255u - (key & 0xFFu);
   const uint32_t g = key ? uni(W.pn[gi].x) : 0xFFFFFFFFu;
   wave_sync();
-  return BpGuess{g, gi, total, eff_end};
+  return BpGuess{g, gi, total, eff_end, false};
 }
 
 // Offsets and value bytes of values [before, before + m) of a page, m <= rn: the rn values the walk
@@ -1982,7 +2164,11 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
 __device__ __forceinline__ void bp_emit(const uint32_t* img, uint32_t img_len, const uint16_t* acc, uint16_t* bt,
                                         rsrc_t rs, uint32_t B, uint32_t beg, uint32_t rn, uint32_t rpos,
                                         uint32_t before, uint32_t m, const PageWork& pw, const ColumnDev& cd) {
-  const uint32_t lane = lane_id();
+  // the lane index laundered through an empty volatile asm: lane-derived constants are recomputed per
+  // call instead of being hoisted out of the caller's tile loop, where they were spilled to scratch
+  // (a scratch reload waits for every store in flight)
+  uint32_t lane = lane_id();
+  asm volatile("" : "+v"(lane));
   // ---- offsets of values before .. before + m (the last one: the end of value m - 1)
   auto pos_k = [&](uint32_t k) -> uint32_t { return k < rn ? B + acc[k] : rpos; };
   int64_t* offs = (int64_t*)cd.values + pw.out_offset + before;
@@ -2086,7 +2272,10 @@ __device__ __forceinline__ void bp_emit(const uint32_t* img, uint32_t img_len, c
 }
 
 
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) void k_bin_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+#ifndef PQG_BP_WAVES
+#define PQG_BP_WAVES 6
+#endif
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_BP_WAVES))) void k_bin_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                         const PageWork* __restrict__ work,
                                                         const ColumnDev* __restrict__ cols,
                                                         const uint64_t* __restrict__ segs, uint32_t n_segs,
@@ -2128,14 +2317,15 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) v
   const BwBytes cur = bw_load(rs, B);
   const uint32_t nxt = ld32(rs, B + BW_WIN + 4u * lane);  // the next tile's first BP_NEXT bytes
   const bool first = s == s0;
-  const BpGuess gs = first ? BpGuess{beg, 0xFFFFFFFFu, 0, 0} : bp_guess(L, cur, rs, B, end);
+  const BpGuess gs = first ? BpGuess{beg, 0xFFFFFFFFu, 0, 0, false} : bp_guess(L, cur, rs, B, end);
   uint32_t entry = gs.pos;
 #ifdef PQG_DIAG
   dg_polls = __builtin_amdgcn_s_memrealtime() + (entry == 7u ? 1u : 0u);  // (after the guess; polls below)
 #endif
   BpWalk r{entry, 0, 0};
   if (entry != 0xFFFFFFFFu) {
-    r = first ? bp_walk(L, cur, rs, B, entry, end) : bp_walk(L, cur, rs, B, entry, end, gs.index, gs.total, gs.eff_end);
+    r = first ? bp_walk<true>(L, cur, rs, B, entry, end)
+              : bp_walk<true>(L, cur, rs, B, entry, end, gs.index, gs.total, gs.eff_end, gs.fast);
     if (!first && lane == 0)  // speculative: count, guessed entry, exit, stop
       sst(aggw + t, E | ((uint64_t)r.n << 46) | ((uint64_t)(entry - B) << 35) | ((uint64_t)(r.code ? 1u : 0u) << 34) |
                         (uint64_t)r.pos);
@@ -2188,7 +2378,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) v
 #endif
             if (ex0 != entry) {                    // misspeculated (or no guess): walk from there
               entry = ex0;
-              r = ex0 >= B + BW_WIN ? BpWalk{ex0, 0, 0} : bp_walk(L, cur, rs, B, ex0, end);
+              r = ex0 >= B + BW_WIN ? BpWalk{ex0, 0, 0} : bp_walk<true>(L, cur, rs, B, ex0, end);
             }
           }
           break;
@@ -2260,7 +2450,12 @@ struct BinPageLds {
 };
 static_assert(sizeof(BinPageLds) * WPB <= 160 * 1024 / 6, "6 workgroups of k_bin_plain_pg per CU");
 
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) void k_bin_plain_pg(
+// 5 waves per SIMD: 94 VGPRs hold the tile being walked and the next one without spills (at 6, the
+// next tile's registers went to scratch, whose store waited for the prefetch on every tile)
+#ifndef PQG_PG_WAVES
+#define PQG_PG_WAVES 5
+#endif
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_PG_WAVES))) void k_bin_plain_pg(
     const uint8_t* __restrict__ bytes, uint64_t n_bytes, const PageWork* __restrict__ work,
     const ColumnDev* __restrict__ cols, const int32_t* __restrict__ list, int n_list, uint32_t* inexact,
     uint32_t flag_epoch, uint64_t* err, ErrCount err_count) {
@@ -2287,7 +2482,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) v
     pos = uni(pos);
     before = uni(before);
     B = uni(B);
-    const BpWalk r = bp_walk(L, cur, rs, B, pos, end);
+    const BpWalk r = bp_walk<true>(L, cur, rs, B, pos, end);
     if (r.code && before + r.n < N && lane == 0) report(err, err_count, page, 2, before + r.n, r.code);
     bool last = r.code != 0;
     if (before + r.n >= N) {  // the page's last value is here: it must end at the section end
@@ -2427,12 +2622,12 @@ hipError_t launch_gather_fixed(hipStream_t st, const uint8_t* bytes, uint64_t n_
   return hipGetLastError();
 }
 
-hipError_t launch_bin_scan(hipStream_t st, const ColumnDev* cols, const int32_t* bin_cols, int n_bin_cols,
-                           const uint64_t* blocks, uint32_t n_blocks) {
+hipError_t launch_bin_scan(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, const ColumnDev* cols,
+                           const int32_t* bin_cols, int n_bin_cols, const uint64_t* blocks, uint32_t n_blocks) {
   if (n_bin_cols <= 0 || n_blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_bin_block_sums, dim3(n_blocks), dim3(256), 0, st, cols, blocks);
   hipLaunchKernelGGL(k_bin_block_bases, dim3(n_bin_cols), dim3(256), 0, st, cols, bin_cols);
-  hipLaunchKernelGGL(k_bin_offsets, dim3(n_blocks), dim3(256), 0, st, cols, blocks);
+  hipLaunchKernelGGL(k_bin_offsets, dim3(n_blocks), dim3(256), 0, st, bytes, n_bytes, cols, blocks);
   return hipGetLastError();
 }
 

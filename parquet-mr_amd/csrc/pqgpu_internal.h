@@ -33,6 +33,10 @@ struct ColumnDev {
   uint64_t n_slots;        // level slots of the column in the batch (offsets span n_slots + 1)
   uint64_t* block_sums;    // BYTE_ARRAY offset scan: per 4096-value block
   uint64_t* bin_total;     // BYTE_ARRAY: bytes of the decoded values (device, one u64)
+  // 1: a required BYTE_ARRAY column whose data pages are all dictionary-encoded and whose dictionary
+  // page fits DD_DICT_MAX: blen keeps the ids through the offset scan, which maps them to entry
+  // lengths and also writes the value bytes (no k_bin_dict_map, no k_bin_copy for it)
+  uint32_t dict_direct;
 };
 
 // Per page, on the device. The host fills the descriptor facts; for nullable
@@ -148,6 +152,7 @@ constexpr uint32_t BW_SEG_BYTES = 16384;
 constexpr uint32_t BW_SEG_CAP = BW_SEG_BYTES / 4 + 2;
 constexpr uint32_t BW_SEG_MAX_PAGES = 4096;
 constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block
+constexpr uint32_t DD_DICT_MAX = 8192;  // dictionary page bytes staged by the offset scan (dict_direct)
 hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                       const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
@@ -172,7 +177,8 @@ hipError_t launch_bin_walk_seg(hipStream_t st, const uint8_t* bytes, uint64_t n_
 hipError_t launch_bin_dict_map(hipStream_t st, PageWork* work, const ColumnDev* cols, const int32_t* list, int n);
 hipError_t launch_gather_fixed(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n);
-hipError_t launch_bin_scan(hipStream_t st, const ColumnDev* cols, const int32_t* bin_cols, int n_bin_cols,
+hipError_t launch_bin_scan(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, const ColumnDev* cols,
+                           const int32_t* bin_cols, int n_bin_cols,
                            const uint64_t* blocks, uint32_t n_blocks);
 hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const uint64_t* chunks, uint32_t n_chunks, uint64_t* err,

@@ -67,6 +67,17 @@ def test_binary_many_columns_one_batch(decoder):
     run_both(decoder, chunks)
 
 
+@pytest.mark.parametrize("dict_entries,lo,hi", [(3, 1, 1), (7, 3, 7), (60, 0, 40), (330, 16, 32), (500, 10, 30)])
+def test_binary_dictionary_direct(decoder, dict_entries, lo, hi):
+    """Required dictionary-encoded BYTE_ARRAY columns: short entries (C4's flags and modes) take the
+    offset scan's direct path (ids -> lengths -> offsets and bytes), dictionaries past its 8 KiB
+    staging (330 / 500 entries) the per-value path; several pages and scan blocks, empty entries."""
+    words = _strings(dict_entries, seed=dict_entries, lo=lo, hi=hi)
+    ids = np.random.default_rng(dict_entries).integers(0, dict_entries, size=50_000)
+    run_both(decoder, [make(abi.BYTE_ARRAY, [words[i] for i in ids], abi.RLE_DICTIONARY, page_rows=7000),
+                       make(abi.BYTE_ARRAY, [words[i] for i in ids[:9000]], abi.RLE_DICTIONARY, page_rows=3000)])
+
+
 def test_binary_dictionary_expands_past_estimate(decoder):
     """A dictionary of long entries: the decoded bytes exceed the first byte-buffer estimate,
     the status reports the size needed and decode() retries."""
