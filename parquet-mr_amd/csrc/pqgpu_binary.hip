@@ -577,10 +577,18 @@ __global__ __launch_bounds__(256) void k_gather_fixed(const uint8_t* __restrict_
   }
 }
 
-// 4 source bytes at staged offset i (any alignment): two aligned LDS dwords and a byte align.
+// 4 source bytes at staged offset i (any alignment): one unaligned ds_read_b32 (gfx950 runs DS
+// accesses in unaligned mode; 32-bit accesses off their alignment take no replay, unlike b64 / b128)
+#ifdef PQG_AB_IMG4_ALIGNED
 __device__ __forceinline__ uint32_t img4(const uint32_t* img, uint32_t i) {
   return __builtin_amdgcn_alignbyte(img[(i >> 2) + 1], img[i >> 2], i & 3u);
 }
+#else
+__device__ __forceinline__ uint32_t img4(const uint32_t* img, uint32_t i) {
+  typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
+  return *(const u32u*)((const uint8_t*)img + i);
+}
+#endif
 
 // Store the 16-byte output block at `a` (dwords wd) clipped to [o_lo, o_hi): one 16-byte store
 // when the block is whole and aligned, dword stores for whole dwords, byte stores at the edges
@@ -2509,7 +2517,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_PG
       nxt = bw_load(rs, nB + BW_WIN);
     }
     wave_sync();
-    if (m) bp_emit(L.u.img, 2u * BW_WIN, L.acc, L.bt, rs, B, beg, r.n, r.pos, before, m, pw, cd);
+#ifdef PQG_DIAG_PG_NOEMIT  // diagnostic build only (abx/): the walk without the output stage
+    if (false)
+#else
+    if (m)
+#endif
+      bp_emit(L.u.img, 2u * BW_WIN, L.acc, L.bt, rs, B, beg, r.n, r.pos, before, m, pw, cd);
     if (last) break;
     before += r.n;
     pos = r.pos;
