@@ -724,19 +724,19 @@ struct DictDirectLds {
   uint32_t out[DD_OUT / 4 + 4];
 };
 
-__device__ __noinline__ void dd_row_bytes(const ColumnDev& cd, DictDirectLds& D, u32x4 ids, uint64_t v, uint64_t n_slots,
-                                          uint64_t e, uint64_t o_lo, uint64_t o_hi) {
+// lens / srcs: the thread's 4 values' entry lengths and offsets in the dictionary page (gathered
+// before the offset stores: a load issued after them would wait for them, vmcnt counts stores)
+__device__ __noinline__ void dd_row_bytes(const ColumnDev& cd, DictDirectLds& D, u32x4 lens, u32x4 srcs, uint64_t e,
+                                          uint64_t o_lo, uint64_t o_hi) {
   const uint32_t t = threadIdx.x;
   uint8_t* dst = cd.binary_data;
-  const uint32_t dbytes = (uint32_t)cd.dict_bytes, dn = uni(cd.dict_n);
+  const uint32_t dbytes = (uint32_t)cd.dict_bytes;
   const uint64_t a0 = o_lo & ~15ull;
   const bool img = o_hi - a0 + 16u <= DD_OUT;
   uint8_t* outb = (uint8_t*)D.out;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const uint32_t id = ids[k];
-    const bool ok = id < dn && v + k < n_slots;
-    const uint32_t sp = ok ? cd.dict_src[id] : 0u, len = ok ? cd.dict_len[id] : 0u;
+    const uint32_t sp = srcs[k], len = lens[k];
     for (uint32_t j = 0; j < len; j += 4u) {
       const uint32_t w = sp + j < dbytes ? img4(D.dict, sp + j) : 0u;  // (bytes past the entry: masked)
 #pragma unroll
@@ -792,7 +792,15 @@ __global__ __launch_bounds__(256) void k_bin_offsets(const uint8_t* __restrict__
   if (dd) {
     const uint32_t dn = uni(cd.dict_n);
 #pragma unroll
-    for (int i = 0; i < 4; i++) x[i] = dd_lengths(cd, x[i], dn, v0 + 1024u * i + 4u * t, n_slots);
+    for (int i = 0; i < 4; i++) {
+      const uint64_t v = v0 + 1024u * i + 4u * t;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const bool ok = ids[i][k] < dn && v + k < n_slots;
+        x[i][k] = ok ? cd.dict_len[ids[i][k]] : 0u;
+        ids[i][k] = ok ? cd.dict_src[ids[i][k]] : 0u;  // from here on: the entry's offset in the page
+      }
+    }
     // stage the dictionary page (a resource over the rest of the batch: a 16-byte load that crosses
     // the end of its range returns 0 as a whole, which would drop the page's last bytes; only entry
     // bytes are ever read from the staged page)
@@ -856,7 +864,7 @@ __global__ __launch_bounds__(256) void k_bin_offsets(const uint8_t* __restrict__
 #pragma unroll 1
   for (int i = 0; i < 4; i++) {
     const uint64_t o_lo = rowb[i], o_hi = rowb[i + 1] < cap ? rowb[i + 1] : cap;  // overflow: reported at sync
-    if (o_lo < o_hi) dd_row_bytes(cd, D, ids[i], v0 + 1024u * i + 4u * t, n_slots, first[i], o_lo, o_hi);
+    if (o_lo < o_hi) dd_row_bytes(cd, D, x[i], ids[i], first[i], o_lo, o_hi);
   }
 }
 

@@ -624,6 +624,9 @@ __device__ __forceinline__ typename DictVal<W>::T dict_get_g(bool in_lds, const 
 //   tile sweep  every lane tracks the run holding its element: per tile it advances past
 //               the run starts it crossed (usually none), reads the value (RLE) or unpacks
 //               the id and gathers (packed), and the wave stores one full 1 KB tile.
+#ifndef PQG_SPIN_SLEEP
+#define PQG_SPIN_SLEEP 2  // s_sleep units (64 cycles) between two polls of a page's ready flag
+#endif
 constexpr uint32_t XT_RUNS = 128;  // run table entries per wave
 constexpr uint32_t XT_SEG = 2560;    // LDS bytes for the packed data of one round
 
@@ -740,7 +743,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
           pst = uni64(sld(pstat + page));
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(PQG_SPIN_SLEEP);
         // wall-clock bound (s_memrealtime: constant 100 MHz): a walker that never publishes
         // (descheduled, starved) turns into PQG_ERR_TIMEOUT after SPIN_TIMEOUT_TICKS, not a hang
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -1020,7 +1023,10 @@ __device__ uint32_t decode_levels_be(rsrc_t rs, uint32_t beg, uint32_t end, int 
 // Per-wave LDS of the level decoder: the page segment and pre-decode tables of the pointer-
 // jumping walk (as in the dictionary walk) plus the run table of one window.
 struct LevelWaveLds {
-  DictWaveLds w;
+  struct {
+    uint8_t seg[SEG_BYTES];  // page bytes [seg_lo, seg_lo + SEG_BYTES)
+    uint64_t ent[96];        // the window walk's jump table (256 x u16) and chain marks (256 x u8)
+  } w;
   uint32_t r_start[256];  // first slot of run k of the window
   uint32_t r_pay[256];    // RLE: value (saturated to 255); PACKED: 0x80000000 | data byte position
   uint32_t r_end[256];    // PACKED: end of the bytes read for the run (truncated final group)
@@ -1488,7 +1494,11 @@ __device__ __forceinline__ uint32_t decode_levels_w(LevelWaveLds& L, rsrc_t rs, 
   }
 }
 
-__global__ __launch_bounds__(64 * WPB) void k_levels(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+// 5 waves per SIMD (LDS 6.9 KiB per wave, <= 102 VGPRs): 40,000 C3 pages in 8 rounds instead of 10
+#ifndef PQG_LV_WAVES
+#define PQG_LV_WAVES 5
+#endif
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_LV_WAVES))) void k_levels(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                 PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                 const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                                 ErrCount err_count) {
