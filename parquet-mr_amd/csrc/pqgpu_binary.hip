@@ -2172,6 +2172,81 @@ __device__ BpGuess bp_guess(BinPlainLds& L, const BwBytes& cur, rsrc_t rs, uint3
   return BpGuess{g, gi, total, eff_end, false};
 }
 
+// bp_emit for tiles whose values are all at least 4 bytes long, whose output fits 2 KiB and whose
+// sources lie in img (C3's 4-32 byte strings, C4's comments): no block table. Output byte x (relative
+// to the 16-byte aligned a0) of value k comes from img[x + C + 4 k], C = P_0 + 4 - B - r_lo, and k is
+// the number of value starts 1..m-1 at or before x: the starts go into a 2,048-bit LDS bitmap (one
+// dword per lane: lane l owns output bytes [32 l, 32 l + 32)), a wave scan of their popcounts gives
+// each lane its first k, and each of its 8 output dwords is one unaligned LDS read (a start inside the
+// dword: two, and a v_perm). Returns false (nothing written) when the tile does not qualify.
+__device__ __forceinline__ bool bp_emit_fast(uint32_t* bm, const uint32_t* img, uint32_t img_len, const uint16_t* acc,
+                                             uint32_t B, uint32_t beg, uint32_t rn, uint32_t rpos, uint32_t before,
+                                             uint32_t m, const PageWork& pw, const ColumnDev& cd) {
+  uint32_t lane = lane_id();
+  asm volatile("" : "+v"(lane));  // (see bp_emit)
+  auto pos_k = [&](uint32_t k) -> uint32_t { return k < rn ? B + acc[k] : rpos; };
+  const uint64_t bb = pw.bin_base;
+  const uint32_t P0 = uni(pos_k(0)), Pm = uni(pos_k(m));
+  const uint64_t o_lo = bb + (uint64_t)(P0 - beg) - 4ull * before;
+  const uint64_t o_hi0 = bb + (uint64_t)(Pm - beg) - 4ull * (uint64_t)(before + m);
+  const uint64_t o_hi = o_hi0 < cd.binary_capacity ? o_hi0 : cd.binary_capacity;
+  const uint64_t a0 = o_lo & ~15ull;
+#ifdef PQG_AB_NO_FAST_EMIT
+  return false;
+#endif
+  if (o_lo >= o_hi || o_hi - a0 > 2048u || Pm - B + 8u > img_len) return false;
+  bool short_v = false;
+  for (uint32_t k = lane; k < m; k += WAVE) short_v |= pos_k(k + 1u) - pos_k(k) < 8u;  // value bytes < 4
+  if (__ballot(short_v)) return false;
+  const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
+  // offsets of values before .. before + m (the last one: the end of value m - 1)
+  int64_t* offs = (int64_t*)cd.values + pw.out_offset + before;
+  for (uint32_t k = lane; k <= m; k += WAVE)
+    gst(offs + k, (int64_t)(bb + (uint64_t)(pos_k(k) - beg) - 4ull * (uint64_t)(before + k)));
+  // starts of values 1 .. m - 1 (output positions relative to a0; distinct: every value >= 4 bytes)
+  bm[lane] = 0u;
+  wave_sync();
+  for (uint32_t k = lane + 1u; k < m; k += WAVE) {
+    const uint32_t x = (pos_k(k) - P0) - 4u * k + r_lo;
+    if (x < 2048u) __hip_atomic_fetch_or(&bm[x >> 5], 1u << (x & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  wave_sync();
+  const uint32_t bits = bm[lane];
+  uint32_t tot;
+  const uint32_t k0 = wave_excl_scan_u32((uint32_t)__builtin_popcount(bits), &tot);  // starts before the lane's bytes
+  const uint32_t C = P0 + 4u - B - r_lo;
+  uint32_t wd[8];
+#pragma unroll
+  for (uint32_t q = 0; q < 8; q++) {
+    const uint32_t x0 = 32u * lane + 4u * q;
+    const uint32_t k = k0 + (uint32_t)__builtin_popcount(bits & (0xFFFFFFFFu >> (31u - 4u * q)));  // starts <= x0
+    const uint32_t inner = (bits >> (4u * q + 1u)) & 7u;  // a start at x0 + 1 .. x0 + 3 (at most one)
+    const int32_t s0 = (int32_t)(x0 + C + 4u * k);
+    const uint32_t lo = img4(img, s0 > 0 ? (uint32_t)s0 : 0u);
+    const uint32_t hi = img4(img, (uint32_t)(s0 + 4 > 0 ? s0 + 4 : 0));
+    const uint32_t j = inner ? (uint32_t)__builtin_ctz(inner) + 1u : 4u;  // first byte of the next value
+    const uint32_t sel = 0x03020100u + (0x04040404u & ~(j >= 4u ? 0xFFFFFFFFu : (1u << (8u * j)) - 1u));
+    wd[q] = __builtin_amdgcn_perm(hi, lo, sel);
+  }
+  uint8_t* dst = cd.binary_data;
+  const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
+#pragma unroll
+  for (uint32_t g = 0; g < 2; g++) {
+    const uint32_t b = 32u * lane + 16u * g;
+    if (b >= r_hi) break;
+    uint32_t have = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      const uint32_t d0 = b + 4u * q;
+      if (d0 >= r_lo && d0 + 4u <= r_hi) have |= 1u << q;
+    }
+    if (!dst_al4) have = 0;
+    const uint32_t w4[4] = {wd[4 * g], wd[4 * g + 1], wd[4 * g + 2], wd[4 * g + 3]};
+    store_block16(dst, a0 + b, o_lo, o_hi, w4, have, dst_al16);
+  }
+  return true;
+}
+
 // Offsets and value bytes of values [before, before + m) of a page, m <= rn: the rn values the walk
 // accepted in tile [B, B + BW_WIN) start at B + acc[k], the chain left the tile at rpos; img holds the
 // staged page bytes [B, B + img_len) (a value reaching further: the rest from memory). The offsets
@@ -2445,7 +2520,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_BP
     img[BW_WIN / 4u + lane] = nxt;
   }
   wave_sync();
-  bp_emit(L.u.img, BP_IMG, L.acc, L.bt, rs, B, beg, r.n, r.pos, before, m, pw, cd);
+  if (!bp_emit_fast((uint32_t*)L.bt, L.u.img, BP_IMG, L.acc, B, beg, r.n, r.pos, before, m, pw, cd))
+    bp_emit(L.u.img, BP_IMG, L.acc, L.bt, rs, B, beg, r.n, r.pos, before, m, pw, cd);
 }
 
 // One-pass PLAIN BYTE_ARRAY for plans with many PLAIN pages (k_bin_plain_pg): one wave per page
@@ -2530,7 +2606,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_PG
 #else
     if (m)
 #endif
-      bp_emit(L.u.img, 2u * BW_WIN, L.acc, L.bt, rs, B, beg, r.n, r.pos, before, m, pw, cd);
+      if (!bp_emit_fast((uint32_t*)L.bt, L.u.img, 2u * BW_WIN, L.acc, B, beg, r.n, r.pos, before, m, pw, cd))
+        bp_emit(L.u.img, 2u * BW_WIN, L.acc, L.bt, rs, B, beg, r.n, r.pos, before, m, pw, cd);
     if (last) break;
     before += r.n;
     pos = r.pos;
