@@ -2569,8 +2569,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_PG
   const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
   uint32_t pos = beg, before = 0;
   uint32_t B = beg & ~(BW_WIN - 1u);
-  BwBytes cur = bw_load(rs, B), nxt = bw_load(rs, B + BW_WIN);
-  while (true) {
+  // Two tile buffers in ping-pong (the loop body is written for (cur, nxt) = (X, Y), then (Y, X)): a
+  // "cur = nxt" copy made the compiler wait for the freshly issued load of the next tile at once
+  // (its registers were moved into place), a full memory latency per tile.
+  BwBytes X = bw_load(rs, B), Y = bw_load(rs, B + BW_WIN);
+  // one tile; returns true when the page is done
+  auto tile = [&](BwBytes& cur, BwBytes& nxt) __attribute__((always_inline)) -> bool {
     pos = uni(pos);
     before = uni(before);
     B = uni(B);
@@ -2593,12 +2597,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_PG
     // it, requested before this tile's stores
     const uint32_t nB = r.pos & ~(BW_WIN - 1u);
     if (!last) {
-      if (nB == B + BW_WIN) {
-        cur = nxt;
-      } else {  // a value longer than a tile
-        cur = bw_load(rs, nB);
+      if (nB == B + BW_WIN) {  // the next call walks nxt; this buffer takes the tile after it
+        cur = bw_load(rs, nB + BW_WIN);
+      } else {  // a value longer than a tile: both again (next call: nxt = tile nB, cur = the one after)
+        nxt = bw_load(rs, nB);
+        cur = bw_load(rs, nB + BW_WIN);
       }
-      nxt = bw_load(rs, nB + BW_WIN);
     }
     wave_sync();
 #ifdef PQG_DIAG_PG_NOEMIT  // diagnostic build only (abx/): the walk without the output stage
@@ -2608,11 +2612,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_PG
 #endif
       if (!bp_emit_fast((uint32_t*)L.bt, L.u.img, 2u * BW_WIN, L.acc, B, beg, r.n, r.pos, before, m, pw, cd))
         bp_emit(L.u.img, 2u * BW_WIN, L.acc, L.bt, rs, B, beg, r.n, r.pos, before, m, pw, cd);
-    if (last) break;
+    if (last) return true;
     before += r.n;
     pos = r.pos;
     B = nB;
     wave_sync();  // the emit's LDS reads are done before the next walk's list
+    return false;
+  };
+  while (!tile(X, Y) && !tile(Y, X)) {
   }
 }
 
