@@ -494,8 +494,8 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   // one pass: k_bin_bases + k_bin_plain over 2 KiB tiles of their pages when the plan has fewer than
   // BW_SEG_MAX_PAGES PLAIN pages, k_bin_plain_pg (one wave per page, which fills the chip) with more
   // (there the tiles measured slower than the per-value walk + copy: C3 10.4 vs 6.4 ms, profiles/r03/plain_ab)
-  // PQGPU_PLAIN_PG overrides the choice (tests and A/B): 0 = many-page plans per value, 3 = every plan
-  // one wave per page
+  // PQGPU_PLAIN_PG overrides the choice (tests and A/B): 0 = no one-pass path (every plan per value),
+  // 3 = every plan one wave per page
   int plain_mode = 2;
   if (const char* ev = getenv("PQGPU_PLAIN_PG")) plain_mode = atoi(ev);
   const bool many_plain = cls_lists[C_BINP].size() >= pqg::BW_SEG_MAX_PAGES || plain_mode == 3;
@@ -514,10 +514,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     }
     for (int i = 0; i < n_cols; i++) {
       plain_col[(size_t)i] = bin_out(cols[i]) && !ids_mode(cols[i]) && !col_err[(size_t)i] && !dba_fixed[(size_t)i] &&
-                             npg[(size_t)i] > 0 && nplain[(size_t)i] == npg[(size_t)i] && (!many_plain || plain_mode != 0);
-#ifdef PQG_AB_NOPLAIN  // (A/B builds under abx/ only)
-      plain_col[(size_t)i] = 0;
-#endif
+                             npg[(size_t)i] > 0 && nplain[(size_t)i] == npg[(size_t)i] && plain_mode != 0;
       if (!plain_col[(size_t)i]) continue;
       for (int p : cpg[(size_t)i]) {
         pcp.push_back(p);

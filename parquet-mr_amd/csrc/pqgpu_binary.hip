@@ -579,16 +579,11 @@ __global__ __launch_bounds__(256) void k_gather_fixed(const uint8_t* __restrict_
 
 // 4 source bytes at staged offset i (any alignment): one unaligned ds_read_b32 (gfx950 runs DS
 // accesses in unaligned mode; 32-bit accesses off their alignment take no replay, unlike b64 / b128)
-#ifdef PQG_AB_IMG4_ALIGNED
-__device__ __forceinline__ uint32_t img4(const uint32_t* img, uint32_t i) {
-  return __builtin_amdgcn_alignbyte(img[(i >> 2) + 1], img[i >> 2], i & 3u);
-}
-#else
+// (the aligned-pair form, two reads and a v_alignbyte, measured the same or slower: profiles/r03/img4)
 __device__ __forceinline__ uint32_t img4(const uint32_t* img, uint32_t i) {
   typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
   return *(const u32u*)((const uint8_t*)img + i);
 }
-#endif
 
 // Store the 16-byte output block at `a` (dwords wd) clipped to [o_lo, o_hi): one 16-byte store
 // when the block is whole and aligned, dword stores for whole dwords, byte stores at the edges
@@ -895,11 +890,7 @@ __device__ __forceinline__ uint32_t pick8(const uint32_t (&a)[8], uint32_t i) {
 // a value running past the page is the reference's "Failed to read N bytes" (EOF) at that value.
 constexpr uint32_t CP_VALUES = CP_CHUNK_VALUES;  // values per workgroup chunk of k_bin_copy
 constexpr uint32_t CP_WAVE = CP_VALUES / WPB;  // values per wave on the per-wave path
-#ifdef PQG_AB_CPSRC  // (A/B builds under abx/ only)
-constexpr uint32_t CP_SRC = PQG_AB_CPSRC * CP_VALUES;
-#else
 constexpr uint32_t CP_SRC = 48u * CP_VALUES;     // LDS bytes of staged source per workgroup
-#endif
 static_assert(CP_VALUES == CP_CHUNK_VALUES, "host chunking (pqgpu_internal.h)");
 
 struct CopyWaveLds {
@@ -1209,12 +1200,7 @@ __device__ __forceinline__ void compose_block(const uint32_t* img, uint32_t Sv, 
 // no load waits behind a store (vmcnt counts both). Source bytes are read from HBM once, where
 // the per-wave path read 36 bytes per 16-byte block. A chunk whose source does not fit CP_SRC
 // takes the per-wave path, CP_WAVE values per wave.
-#ifdef PQG_AB_CPSRC
-#define PQG_COPY_OCC __attribute__((amdgpu_waves_per_eu(7)))
-#else
-#define PQG_COPY_OCC
-#endif
-__global__ __launch_bounds__(64 * WPB) PQG_COPY_OCC void k_bin_copy(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                        const PageWork* __restrict__ work,
                                                        const ColumnDev* __restrict__ cols,
                                                        const uint64_t* __restrict__ chunks, uint32_t n_chunks,
@@ -2191,9 +2177,6 @@ __device__ __forceinline__ bool bp_emit_fast(uint32_t* bm, const uint32_t* img, 
   const uint64_t o_hi0 = bb + (uint64_t)(Pm - beg) - 4ull * (uint64_t)(before + m);
   const uint64_t o_hi = o_hi0 < cd.binary_capacity ? o_hi0 : cd.binary_capacity;
   const uint64_t a0 = o_lo & ~15ull;
-#ifdef PQG_AB_NO_FAST_EMIT
-  return false;
-#endif
   if (o_lo >= o_hi || o_hi - a0 > 2048u || Pm - B + 8u > img_len) return false;
   bool short_v = false;
   for (uint32_t k = lane; k < m; k += WAVE) short_v |= pos_k(k + 1u) - pos_k(k) < 8u;  // value bytes < 4
@@ -2760,11 +2743,7 @@ hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
   if (n_chunks == 0) return hipSuccess;
   // one resident round of workgroups (by LDS: 5 per CU at ~31 KiB each; by VGPRs at most 7) striding
   // over the chunks: a dictionary page stays staged across a workgroup's chunks of the same column
-#ifdef PQG_AB_CPSRC
-  constexpr uint32_t CP_VGPR_WG = 7u;
-#else
   constexpr uint32_t CP_VGPR_WG = 5u;  // 95 VGPRs: 5 waves per SIMD
-#endif
   constexpr uint32_t CP_PER_CU = (160u * 1024u) / (uint32_t)sizeof(CopyLds) < CP_VGPR_WG ? (160u * 1024u) / (uint32_t)sizeof(CopyLds) : CP_VGPR_WG;
   constexpr uint32_t CP_GRID = 256u * CP_PER_CU;
   hipLaunchKernelGGL(k_bin_copy, dim3(n_chunks < CP_GRID ? n_chunks : CP_GRID), dim3(64 * WPB), 0, st, bytes, n_bytes,

@@ -117,11 +117,7 @@ hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_
 // ZSTD frames per job (pqgpu_zstd.hip): a grid of at most ZSTD_GRID one-wave workgroups loops over
 // the jobs; scratch = min(n_jobs, ZSTD_GRID) x ZSTD_LIT_SCRATCH bytes of literal buffers (<= 512 MiB)
 constexpr uint64_t ZSTD_LIT_SCRATCH = 131072;
-#ifdef PQG_AB_ZGRID  // (A/B builds under abx/ only)
-constexpr uint32_t ZSTD_GRID = PQG_AB_ZGRID;
-#else
 constexpr uint32_t ZSTD_GRID = 4096;
-#endif
 hipError_t launch_zstd(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
                        const pqg_snappy_job* jobs, int n_jobs, int32_t* status, uint8_t* scratch);
 hipError_t launch_snappy(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,

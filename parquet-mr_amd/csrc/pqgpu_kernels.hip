@@ -1030,6 +1030,11 @@ struct LevelWaveLds {
   uint32_t r_start[256];  // first slot of run k of the window
   uint32_t r_pay[256];    // RLE: value (saturated to 255); PACKED: 0x80000000 | data byte position
   uint32_t r_end[256];    // PACKED: end of the bytes read for the run (truncated final group)
+  // the partial 16-slot tile a window's expansion ended on (more windows follow): its levels wait
+  // here for the next window's part instead of going out as byte stores (expand_level_tiles)
+  uint32_t carry[4];
+  int32_t carry_s0;       // tile start (slot index relative to the output base)
+  uint32_t carry_j;       // valid bytes [carry_j & 255, carry_j >> 8); 0: none
 };
 
 // Levels of the runs rs[0 .. n_run) covering slots [s_lo, s_hi) -> out (u8), 16 slots per lane
@@ -1049,6 +1054,54 @@ __device__ __forceinline__ uint32_t tile_byte_mask(int32_t jb, int32_t je, int32
 // r_start[0] <= lo_s). Eight fixed steps with unconditional LDS reads instead of this divergent
 // bisection loop (whose exec bookkeeping runs on the scalar unit) measured C3 10.01 -> 10.10 ms,
 // C5 2.17 -> 2.19 ms (profiles/r02/lv_ab) and were removed.
+// Store one tile's levels [j0, j1) (out + s0 is 16-byte aligned): the first tile of a window range merges
+// the carried part of the same tile (the previous window ended inside it, so carry_j's end is j0); a tile
+// the range ends inside, with more windows to come, becomes the carry; whole tiles go out as one
+// 16-byte store, the tiles at the page's edges byte by byte (other pages own the rest).
+__device__ __forceinline__ void level_tile_out(LevelWaveLds& L, uint8_t* out, int64_t s0, uint32_t (&acc)[4], int32_t j0,
+                                               int32_t j1, uint32_t s_lo, uint32_t s_hi, bool more) {
+  if (s0 + j0 == (int64_t)s_lo && j0 > 0) {
+    const uint32_t cj = L.carry_j;
+    if (cj && L.carry_s0 == (int32_t)s0 && (int32_t)(cj >> 8) == j0) {
+#pragma unroll
+      for (int32_t c = 0; c < 4; c++) {
+        const uint32_t mk = tile_byte_mask(j0, 16, c);
+        acc[c] = (acc[c] & mk) | (L.carry[c] & ~mk);
+      }
+      j0 = (int32_t)(cj & 255u);
+      L.carry_j = 0;
+    }
+  }
+  if (more && j1 < 16 && s0 + j1 == (int64_t)s_hi) {
+#pragma unroll
+    for (int32_t c = 0; c < 4; c++) L.carry[c] = acc[c];
+    L.carry_s0 = (int32_t)s0;
+    L.carry_j = (uint32_t)j0 | ((uint32_t)j1 << 8);
+    return;
+  }
+  uint8_t* o = out + s0;
+  if (j0 == 0 && j1 == 16) {
+    gst((u32x4*)o, u32x4{acc[0], acc[1], acc[2], acc[3]});
+  } else {
+#pragma unroll
+    for (int32_t j = 0; j < 16; j++)
+      if (j >= j0 && j < j1) gst(o + j, (uint8_t)(acc[j >> 2] >> (8 * (j & 3))));
+  }
+}
+
+// A carry left when the section's decode stopped early (an error): its levels go out byte by byte.
+__device__ __forceinline__ void level_carry_flush(LevelWaveLds& L, uint8_t* out) {
+  wave_sync();
+  const uint32_t cj = L.carry_j;
+  if (cj && out && lane_id() < 16u) {
+    const uint32_t j = lane_id();
+    if (j >= (cj & 255u) && j < (cj >> 8)) gst(out + L.carry_s0 + (int32_t)j, (uint8_t)(L.carry[j >> 2] >> (8u * (j & 3u))));
+  }
+  wave_sync();
+  if (lane_id() == 0) L.carry_j = 0;
+  wave_sync();
+}
+
 __device__ __forceinline__ uint32_t level_run_of(const LevelWaveLds& L, uint32_t n_run, uint32_t lo_s) {
   uint32_t a = 0, b = n_run;
   while (b - a > 1) {
@@ -1064,9 +1117,9 @@ __device__ __forceinline__ uint32_t level_run_of(const LevelWaveLds& L, uint32_t
 // its value replicated, a packed piece is 24 bytes at the piece's bit offset, shifted once, then
 // 16 bit fields at compile-time positions; a byte mask merges the piece into the tile.
 template <int WB>
-__device__ __forceinline__ void expand_level_tiles(const LevelWaveLds& L, const PreWin& win, uint32_t n_run,
+__device__ __forceinline__ void expand_level_tiles(LevelWaveLds& L, const PreWin& win, uint32_t n_run,
                                                    uint32_t s_lo, uint32_t s_hi, uint8_t* out, uint32_t max_def,
-                                                   bool count_nonnull, uint32_t& cnt) {
+                                                   bool count_nonnull, uint32_t& cnt, bool more) {
   const rsrc_t rs = win.rs;
   const uint32_t lane = lane_id();
   const int64_t mis = out ? (int64_t)((uintptr_t)out & 15u) : 0;
@@ -1127,16 +1180,7 @@ __device__ __forceinline__ void expand_level_tiles(const LevelWaveLds& L, const 
       const uint32_t j0 = lo_s - (uint32_t)s0, j1 = hi_s - (uint32_t)s0;
       const uint32_t jm = ((1u << j1) - 1u) & ~((1u << j0) - 1u);
       if (count_nonnull) cnt += max_def == 1 ? __builtin_popcount(m & jm) : max_def == 0 ? __builtin_popcount(~m & jm) : 0;
-      if (out) {
-        uint8_t* o = out + s0;
-        if (j0 == 0 && j1 == 16) {
-          gst((u32x4*)o, u32x4{acc[0], acc[1], acc[2], acc[3]});
-        } else {
-#pragma unroll
-          for (uint32_t j = 0; j < 16; j++)
-            if (j >= j0 && j < j1) gst(o + j, (uint8_t)(acc[j >> 2] >> (8 * (j & 3))));
-        }
-      }
+      if (out) level_tile_out(L, out, s0, acc, (int32_t)j0, (int32_t)j1, s_lo, s_hi, more);
       continue;
     }
     while (cur < hi_s) {
@@ -1205,16 +1249,7 @@ __device__ __forceinline__ void expand_level_tiles(const LevelWaveLds& L, const 
         cnt += (uint32_t)__builtin_popcount(~nz & 0x80808080u & tile_byte_mask(j0, j1, c));
       }
     }
-    if (out) {
-      uint8_t* o = out + s0;
-      if (j0 == 0 && j1 == 16) {
-        gst((u32x4*)o, u32x4{acc[0], acc[1], acc[2], acc[3]});
-      } else {
-#pragma unroll
-        for (int32_t j = 0; j < 16; j++)
-          if (j >= j0 && j < j1) gst(o + j, (uint8_t)(acc[j >> 2] >> (8 * (j & 3))));
-      }
-    }
+    if (out) level_tile_out(L, out, s0, acc, j0, j1, s_lo, s_hi, more);
   }
 }
 
@@ -1224,10 +1259,10 @@ __device__ __forceinline__ void expand_level_runs_generic(const LevelWaveLds& L,
 
 // WB = 1..4: the specialised tile expansion; WB = 0: any width.
 template <int WB>
-__device__ __forceinline__ void expand_level_runs(const LevelWaveLds& L, const PreWin& win, uint32_t n_run,
+__device__ __forceinline__ void expand_level_runs(LevelWaveLds& L, const PreWin& win, uint32_t n_run,
                                                   uint32_t s_lo, uint32_t s_hi, int w, uint8_t* out,
-                                                  uint32_t max_def, bool count_nonnull, uint32_t& cnt) {
-  if constexpr (WB > 0) expand_level_tiles<WB>(L, win, n_run, s_lo, s_hi, out, max_def, count_nonnull, cnt);
+                                                  uint32_t max_def, bool count_nonnull, uint32_t& cnt, bool more) {
+  if constexpr (WB > 0) expand_level_tiles<WB>(L, win, n_run, s_lo, s_hi, out, max_def, count_nonnull, cnt, more);
   else expand_level_runs_generic(L, win, n_run, s_lo, s_hi, w, out, max_def, count_nonnull, cnt);
 }
 
@@ -1331,6 +1366,8 @@ __device__ __forceinline__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs,
   win.seg_lo = 0xFFFFF000u;  // nothing staged yet
   uint32_t pos = beg, produced = 0, cnt = 0;
   int code = 0;
+  if (lane == 0) L.carry_j = 0;
+  wave_sync();
   while (true) {
     pos = uni(pos);
     produced = uni(produced);
@@ -1440,7 +1477,9 @@ __device__ __forceinline__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs,
       }
     }
     wave_sync();
-    if (n_em) expand_level_runs<WB>(L, win, n_em, produced, produced + total, w, out, max_def, count_nonnull, cnt);
+    if (n_em)
+      expand_level_runs<WB>(L, win, n_em, produced, produced + total, w, out, max_def, count_nonnull, cnt,
+                            produced + total < N);
     produced += total;
     if (produced >= N) break;
     const uint32_t ql = q_last >> 2, qb = q_last & 3u;
@@ -1470,11 +1509,12 @@ __device__ __forceinline__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs,
         L.r_end[0] = rd_end;
       }
       wave_sync();
-      expand_level_runs<WB>(L, win, 1, produced, produced + take, w, out, max_def, count_nonnull, cnt);
+      expand_level_runs<WB>(L, win, 1, produced, produced + take, w, out, max_def, count_nonnull, cnt, produced + take < N);
       produced += take;
       pos = rd_end;
     }
   }
+  if (WB > 0) level_carry_flush(L, out);
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
   if (nonnull) *nonnull = cnt;
   *err_code = code;
