@@ -22,7 +22,13 @@
 
 namespace pqg {
 
-constexpr uint32_t ZS_RING = 4096;    // LDS mirror of the most recent output
+#ifndef PQG_ZS_RING
+#define PQG_ZS_RING 4096
+#endif
+#ifndef PQG_ZS_WAVES
+#define PQG_ZS_WAVES 2
+#endif
+constexpr uint32_t ZS_RING = PQG_ZS_RING;  // LDS mirror of the most recent output
 constexpr uint32_t ZS_WIN = 1024;     // LDS window of the sequence bitstream
 constexpr uint32_t ZS_HWIN = 256;     // LDS window per Huffman stream
 constexpr uint32_t ZS_LIT_MAX = 131072;
@@ -948,7 +954,7 @@ __device__ uint64_t zxxh64(const uint8_t* p, uint32_t n) {
 __device__ __forceinline__ void zstd_job(ZWaveLds& L, const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
                          uint64_t dst_bytes, const pqg_snappy_job& jb, int j, int32_t* status, uint8_t* litbuf);
 
-__global__ __launch_bounds__(64) void k_zstd(const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PQG_ZS_WAVES))) void k_zstd(const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
                                              uint64_t dst_bytes, const pqg_snappy_job* __restrict__ jobs, int n_jobs,
                                              int32_t* status, uint8_t* scratch, uint64_t lit_stride) {
   __shared__ __attribute__((aligned(16))) ZWaveLds L;
