@@ -224,19 +224,20 @@ __global__ __launch_bounds__(256) void k_asm_onepass(const uint8_t* __restrict__
       for (uint32_t j = 0; j < ASM_PER_THREAD; j++)
         if ((mk[j] >> q) & 1u) img8[l++] = byte_of(dw, j) >= Dk ? 1 : 0;
       __syncthreads();
-      // bytes [B, B + cnt) of validity[k]: aligned dwords inside, bytes at both ends
+      // bytes [B, B + cnt) of validity[k]: aligned 16-byte blocks inside (unaligned 32-bit LDS reads of
+      // the image), bytes at both ends
+      typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
       uint8_t* g = P.validity[k] + bc[q];
       const uint32_t cnt = bt_at(bt, q);
-      const uint32_t mis = (uint32_t)((4u - ((uintptr_t)g & 3u)) & 3u);
+      const uint32_t mis = (uint32_t)((16u - ((uintptr_t)g & 15u)) & 15u);
       const uint32_t head = mis < cnt ? mis : cnt;
-      const uint32_t nd = (cnt - head) >> 2;
+      const uint32_t nd = (cnt - head) >> 4;
       for (uint32_t i = threadIdx.x; i < nd; i += 256) {
-        const uint32_t o = head + 4 * i;
-        const uint32_t v = (uint32_t)img8[o] | ((uint32_t)img8[o + 1] << 8) | ((uint32_t)img8[o + 2] << 16) |
-                           ((uint32_t)img8[o + 3] << 24);
-        gst((uint32_t*)(g + o), v);
+        const uint8_t* s = img8 + head + 16u * i;
+        gst((u32x4*)(g + head + 16u * i),
+            u32x4{*(const u32u*)s, *(const u32u*)(s + 4), *(const u32u*)(s + 8), *(const u32u*)(s + 12)});
       }
-      const uint32_t tail0 = head + 4 * nd;
+      const uint32_t tail0 = head + 16u * nd;
       if (threadIdx.x < head) gst(g + threadIdx.x, img8[threadIdx.x]);
       if (threadIdx.x >= 64 && threadIdx.x - 64 < cnt - tail0) gst(g + tail0 + (threadIdx.x - 64), img8[tail0 + (threadIdx.x - 64)]);
       __syncthreads();
@@ -252,7 +253,17 @@ __global__ __launch_bounds__(256) void k_asm_onepass(const uint8_t* __restrict__
       __syncthreads();
       int64_t* g = P.offsets[k] + bc[q - 1];
       const uint32_t cnt = bt_at(bt, q - 1);
-      for (uint32_t i = threadIdx.x; i < cnt; i += 256) gst(g + i, (int64_t)img[i]);
+      // pairs as 16-byte stores from the first 16-byte aligned entry on
+      const bool al8 = ((uintptr_t)g & 7u) == 0;  // (an int64 array off 8-byte alignment: one entry per store)
+      const uint32_t head = (((uintptr_t)g & 15u) != 0 && cnt > 0) ? 1u : 0u;
+      const uint32_t np = al8 ? (cnt - head) >> 1 : 0u;
+      if (!al8)
+        for (uint32_t i = threadIdx.x; i < cnt; i += 256) gst(g + i, (int64_t)img[i]);
+      typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+      for (uint32_t i = threadIdx.x; i < np; i += 256)
+        gst((i64x2*)(g + head + 2u * i), i64x2{(int64_t)img[head + 2u * i], (int64_t)img[head + 2u * i + 1u]});
+      if (al8 && threadIdx.x == 0 && head) gst(g, (int64_t)img[0]);
+      if (al8 && threadIdx.x == 64 && ((cnt - head) & 1u)) gst(g + cnt - 1u, (int64_t)img[cnt - 1u]);
       __syncthreads();
     }
   }
