@@ -113,6 +113,24 @@ def test_binary_errors(decoder, which):
     run_both(decoder, [_err_case(which)], expect_error=True)
 
 
+@pytest.mark.parametrize("case", ["ascii", "empty", "zeros", "smallints", "random", "long", "optional",
+                                  "plain_eof", "plain_negative"])
+def test_binary_plain_per_page(decoder, monkeypatch, case):
+    """The one-wave-per-page one-pass PLAIN kernel (k_bin_plain_pg, normally for plans with 4,096 or
+    more PLAIN pages) on small plans through the PQGPU_PLAIN_PG=3 dispatch override: every value
+    distribution (false candidates, values longer than a tile, empty values), nulls, and the errors."""
+    monkeypatch.setenv("PQGPU_PLAIN_PG", "3")
+    if case in ("plain_eof", "plain_negative"):
+        run_both(decoder, [_err_case(case)], expect_error=True)
+    elif case == "optional":
+        dl = nulls(20_000, 0.3, seed=3)
+        vals = _strings(int(dl.sum()), seed=4, lo=0, hi=48)
+        run_both(decoder, [make(abi.BYTE_ARRAY, vals, abi.PLAIN, def_levels=dl, max_def=1, version=2, page_rows=6000)])
+    else:
+        n = 600 if case == "long" else 30_000
+        run_both(decoder, [make(abi.BYTE_ARRAY, _binary_vals(case, n, seed=len(case)), abi.PLAIN, page_rows=7000)])
+
+
 @pytest.mark.parametrize("ptype,tl", [(abi.FLOAT, 0), (abi.DOUBLE, 0), (abi.INT32, 0), (abi.INT64, 0),
                                       (abi.FIXED_LEN_BYTE_ARRAY, 3), (abi.FIXED_LEN_BYTE_ARRAY, 16)])
 @pytest.mark.parametrize("null_frac", [0.0, 0.2])
@@ -307,7 +325,16 @@ def _plan_both(decoder, chunks):
     return plan
 
 
-def test_binary_plain_one_pass_no_fallback(decoder):
+@pytest.fixture(params=["tiles", "pages"])
+def one_pass_kernel(request, monkeypatch):
+    """The one-pass PLAIN kernel a small plan takes: the tiles (default) or one wave per page (the
+    PQGPU_PLAIN_PG=3 dispatch override; plans with 4,096 or more PLAIN pages take it by default)."""
+    if request.param == "pages":
+        monkeypatch.setenv("PQGPU_PLAIN_PG", "3")
+    return request.param
+
+
+def test_binary_plain_one_pass_no_fallback(decoder, one_pass_kernel):
     """Well-formed PLAIN pages take the one-pass path and never fall back; mixed with a column whose
     pages are dictionary-encoded (per-value path) in the same plan."""
     a = make(abi.BYTE_ARRAY, _strings(50_000, 21, 0, 60), abi.PLAIN, page_rows=9000)
@@ -316,7 +343,7 @@ def test_binary_plain_one_pass_no_fallback(decoder):
     assert plan.plain_fallbacks == 0
 
 
-def test_binary_plain_one_pass_fallback(decoder):
+def test_binary_plain_one_pass_fallback(decoder, one_pass_kernel):
     """Bytes after a page's values (the reader ignores them): the plan falls back to the per-value path
     once and keeps it; the result equals the oracle on both launches."""
     vals = _strings(20_000, 23, 0, 30)
@@ -327,7 +354,7 @@ def test_binary_plain_one_pass_fallback(decoder):
 
 
 @pytest.mark.parametrize("lens", ["tile_sized", "tile_minus_4", "spanning", "empty_then_long"])
-def test_binary_plain_tile_edges(decoder, lens):
+def test_binary_plain_tile_edges(decoder, lens, one_pass_kernel):
     """Values whose boundaries fall on 2 KiB tile edges, values longer than two tiles (a tile with no
     value start; bytes past the staged tiles), and runs of empty values."""
     rng = np.random.default_rng(len(lens))
