@@ -181,6 +181,10 @@ struct pqg_ctx {
   DevBuf asm_scratch;                // pqg_assemble: block counts + totals
   hipStream_t copy_stream = nullptr; // pqg_decode_host: second D2H queue (odd output chunks)
   DevBuf zstd_scratch;               // pqg_zstd_decompress: literal buffers, ZSTD_LIT_SCRATCH per grid wave
+  // pqg_plan_launch: the one-pass PLAIN BYTE_ARRAY kernel runs on a second queue beside the other
+  // columns' kernels (forked after the levels, joined before the launch ends)
+  hipStream_t side_stream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 extern "C" {
@@ -258,6 +262,12 @@ int pqg_ctx_destroy(pqg_ctx* c) {
     (void)hipStreamSynchronize(c->copy_stream);
     (void)hipStreamDestroy(c->copy_stream);
   }
+  if (c->side_stream) {
+    (void)hipStreamSynchronize(c->side_stream);
+    (void)hipStreamDestroy(c->side_stream);
+  }
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return PQG_OK;
@@ -826,13 +836,26 @@ int pqg_plan_launch(pqg_plan* P) {
       e = pqg::launch_scan(s, work, (const int32_t*)P->col_pages.p, (const int32_t*)P->col_page_start.p, P->n_scan_cols);
   }
   const int32_t* bl = (const int32_t*)P->bin_lists.p;
+  // The one-pass PLAIN BYTE_ARRAY kernel is latency / issue bound (~1 TB/s) and independent of the other
+  // columns' kernels (most of them HBM bound): with other pages in the plan it runs on a second queue,
+  // forked after the levels and joined at the end, so the two kinds share the chip.
+  bool fork = false;
+#ifndef PQG_NO_FORK
+  if (e == hipSuccess && pf && P->n_pages > P->n_pcp) {
+    fork = (ctx->side_stream || hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking) == hipSuccess) &&
+           (ctx->ev_fork || hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) == hipSuccess) &&
+           (ctx->ev_join || hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) == hipSuccess) &&
+           hipEventRecord(ctx->ev_fork, s) == hipSuccess && hipStreamWaitEvent(ctx->side_stream, ctx->ev_fork, 0) == hipSuccess;
+  }
+#endif
   if (e == hipSuccess && pf) {  // PLAIN-only BYTE_ARRAY columns: one pass (after the levels: n_values, out_offset)
     uint8_t* scb = (uint8_t*)P->bscratch.p;
     uint64_t* ps = (uint64_t*)P->pstatus.p;
-    e = pqg::launch_bin_plain(s, P->d_bytes, P->n_bytes, work, cols, (const int32_t*)P->pcol_pages.p,
+    e = pqg::launch_bin_plain(fork ? ctx->side_stream : s, P->d_bytes, P->n_bytes, work, cols, (const int32_t*)P->pcol_pages.p,
                               (const int32_t*)P->pcol_start.p, P->n_pcols, (const uint64_t*)P->psegs.p, P->n_psegs, ps,
                               ps + P->n_psegs, (uint32_t*)(scb + P->pticket_off), P->pseg_epoch,
                               (uint32_t*)(scb + P->pflag_off), P->err_epoch, err, ecount, P->plain_pg, P->n_pcp);
+    if (fork && hipEventRecord(ctx->ev_join, ctx->side_stream) != hipSuccess) e = hipErrorUnknown;
   }
   if (e == hipSuccess && P->n_dict_walk)  // BYTE_ARRAY dictionary entries (PlainBinaryDictionary ctor)
     e = pqg::launch_bin_walk(s, P->d_bytes, P->n_bytes, work, cols, bl + P->off_dict_walk, P->n_dict_walk, 1, P->n_pages,
@@ -894,6 +917,7 @@ int pqg_plan_launch(pqg_plan* P) {
     e = pqg::launch_dba_copy(s, P->d_bytes, P->n_bytes, work, cols, lists + P->cls_off[C_DBA], P->cls_n[C_DBA],
                              (const uint64_t*)P->dba_chunks.p, P->n_dba_chunks, P->dba_meta(), bl + P->off_carry,
                              P->n_carry, err, ecount);
+  if (fork && hipStreamWaitEvent(s, ctx->ev_join, 0) != hipSuccess) e = hipErrorUnknown;
   ctx->last_launched = P;
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }
