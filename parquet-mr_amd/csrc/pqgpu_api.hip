@@ -185,6 +185,10 @@ struct pqg_ctx {
   // columns' kernels (forked after the levels, joined before the launch ends)
   hipStream_t side_stream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // ... and the BYTE_ARRAY kernels of the other columns (dictionary walk / ids / map, per-value walks,
+  // offset scan, copies) on a third, beside the fixed-width columns' kernels
+  hipStream_t bin_stream = nullptr;
+  hipEvent_t ev_join_bin = nullptr;
 };
 
 extern "C" {
@@ -266,6 +270,11 @@ int pqg_ctx_destroy(pqg_ctx* c) {
     (void)hipStreamSynchronize(c->side_stream);
     (void)hipStreamDestroy(c->side_stream);
   }
+  if (c->bin_stream) {
+    (void)hipStreamSynchronize(c->bin_stream);
+    (void)hipStreamDestroy(c->bin_stream);
+  }
+  if (c->ev_join_bin) (void)hipEventDestroy(c->ev_join_bin);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -839,13 +848,26 @@ int pqg_plan_launch(pqg_plan* P) {
   // The one-pass PLAIN BYTE_ARRAY kernel is latency / issue bound (~1 TB/s) and independent of the other
   // columns' kernels (most of them HBM bound): with other pages in the plan it runs on a second queue,
   // forked after the levels and joined at the end, so the two kinds share the chip.
-  bool fork = false;
+  // The BYTE_ARRAY kernels of the other columns likewise go to a third queue when fixed-width columns'
+  // kernels (HBM bound) are in the plan to share the chip with.
+  bool fork = false, fork_bin = false;
 #ifndef PQG_NO_FORK
-  if (e == hipSuccess && pf && P->n_pages > P->n_pcp) {
+  const bool has_fixed = P->cls_n[C_DICT4] || P->cls_n[C_DICT8] || P->cls_n[C_PLAIN] || P->cls_n[C_BOOL] ||
+                         P->cls_n[C_RLEBOOL] || P->cls_n[C_DELTA4] || P->cls_n[C_DELTA8] || P->cls_n[C_BSS];
+  const bool has_bin = P->n_dict_walk || P->cls_n[C_IDS] || P->cls_n[C_BINP] - (pf ? P->n_binp_fused : 0) > 0 ||
+                       P->cls_n[C_DLBA] || P->cls_n[C_DBA] || P->n_segs;
+  const bool want = e == hipSuccess && ((pf && (has_fixed || has_bin)) || (has_bin && has_fixed));
+  const bool ev_ok = want && (ctx->ev_fork || hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) == hipSuccess) &&
+                     hipEventRecord(ctx->ev_fork, s) == hipSuccess;
+  if (ev_ok && pf) {
     fork = (ctx->side_stream || hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking) == hipSuccess) &&
-           (ctx->ev_fork || hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) == hipSuccess) &&
            (ctx->ev_join || hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) == hipSuccess) &&
-           hipEventRecord(ctx->ev_fork, s) == hipSuccess && hipStreamWaitEvent(ctx->side_stream, ctx->ev_fork, 0) == hipSuccess;
+           hipStreamWaitEvent(ctx->side_stream, ctx->ev_fork, 0) == hipSuccess;
+  }
+  if (ev_ok && has_bin && has_fixed) {
+    fork_bin = (ctx->bin_stream || hipStreamCreateWithFlags(&ctx->bin_stream, hipStreamNonBlocking) == hipSuccess) &&
+               (ctx->ev_join_bin || hipEventCreateWithFlags(&ctx->ev_join_bin, hipEventDisableTiming) == hipSuccess) &&
+               hipStreamWaitEvent(ctx->bin_stream, ctx->ev_fork, 0) == hipSuccess;
   }
 #endif
   if (e == hipSuccess && pf) {  // PLAIN-only BYTE_ARRAY columns: one pass (after the levels: n_values, out_offset)
@@ -857,8 +879,9 @@ int pqg_plan_launch(pqg_plan* P) {
                               (uint32_t*)(scb + P->pflag_off), P->err_epoch, err, ecount, P->plain_pg, P->n_pcp);
     if (fork && hipEventRecord(ctx->ev_join, ctx->side_stream) != hipSuccess) e = hipErrorUnknown;
   }
+  const hipStream_t sb = fork_bin ? ctx->bin_stream : s;  // BYTE_ARRAY kernels of the other columns
   if (e == hipSuccess && P->n_dict_walk)  // BYTE_ARRAY dictionary entries (PlainBinaryDictionary ctor)
-    e = pqg::launch_bin_walk(s, P->d_bytes, P->n_bytes, work, cols, bl + P->off_dict_walk, P->n_dict_walk, 1, P->n_pages,
+    e = pqg::launch_bin_walk(sb, P->d_bytes, P->n_bytes, work, cols, bl + P->off_dict_walk, P->n_dict_walk, 1, P->n_pages,
                              err, ecount);
   for (int k = 0; k < C_NCLS && e == hipSuccess; k++) {
     int n = P->cls_n[(size_t)k] - (k == C_BINP && pf ? P->n_binp_fused : 0);
@@ -875,18 +898,18 @@ int pqg_plan_launch(pqg_plan* P) {
       }
       case C_IDS: {
         const int i = k - C_DICT4;
-        e = pqg::launch_dict_ids(s, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
+        e = pqg::launch_dict_ids(sb, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
                                  (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->chunk_off[i],
                                  P->chunk_n[i], (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused, err, ecount);
         break;
       }
       case C_BSS: e = pqg::launch_bss(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_BINP:
-        e = pqg::launch_bin_walk(s, P->d_bytes, P->n_bytes, work, cols, l, n, 0, P->n_pages, err, ecount);
+        e = pqg::launch_bin_walk(sb, P->d_bytes, P->n_bytes, work, cols, l, n, 0, P->n_pages, err, ecount);
         break;
-      case C_DLBA: e = pqg::launch_dlba_lengths(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_DLBA: e = pqg::launch_dlba_lengths(sb, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_DBA:
-        e = pqg::launch_dba_lengths(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount, P->dba_meta());
+        e = pqg::launch_dba_lengths(sb, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount, P->dba_meta());
         break;
       case C_PLAIN: e = pqg::launch_plain(0, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_BOOL: e = pqg::launch_plain(1, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
@@ -897,27 +920,30 @@ int pqg_plan_launch(pqg_plan* P) {
   }
   if (e == hipSuccess && P->n_segs) {  // PLAIN BYTE_ARRAY pages in segments (status + ticket cleared above)
     uint8_t* scb = (uint8_t*)P->bscratch.p;
-    e = pqg::launch_bin_walk_seg(s, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->segs.p, P->n_segs,
+    e = pqg::launch_bin_walk_seg(sb, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->segs.p, P->n_segs,
                                  (uint64_t*)(scb + P->seg_status_off), (uint32_t*)(scb + P->seg_status_off) + 2u * P->n_segs,
                                  (uint32_t*)(scb + P->seg_tmp_off), err, ecount);
   }
   // post-passes: dictionary ids -> BYTE_ARRAY entries / fixed-width entries; offsets; value bytes
-  if (e == hipSuccess && P->n_bind) e = pqg::launch_bin_dict_map(s, work, cols, bl + P->off_bind, P->n_bind);
+  if (e == hipSuccess && P->n_bind) e = pqg::launch_bin_dict_map(sb, work, cols, bl + P->off_bind, P->n_bind);
   if (e == hipSuccess && P->n_fixd)
-    e = pqg::launch_gather_fixed(s, P->d_bytes, P->n_bytes, work, cols, bl + P->off_fixd, P->n_fixd);
+    e = pqg::launch_gather_fixed(sb, P->d_bytes, P->n_bytes, work, cols, bl + P->off_fixd, P->n_fixd);
   const uint32_t n_blocks = pf ? P->n_bin_blocks_nf : P->n_bin_blocks;
   if (e == hipSuccess && n_blocks)
-    e = pqg::launch_bin_scan(s, P->d_bytes, P->n_bytes, cols, bl + P->off_bin_cols, pf ? P->n_bin_cols_nf : P->n_bin_cols,
+    e = pqg::launch_bin_scan(sb, P->d_bytes, P->n_bytes, cols, bl + P->off_bin_cols, pf ? P->n_bin_cols_nf : P->n_bin_cols,
                              (const uint64_t*)P->bin_blocks.p, n_blocks);
   const uint32_t n_chunks = pf ? P->n_bin_chunks_nf : P->n_bin_chunks;
   if (e == hipSuccess && n_chunks)
-    e = pqg::launch_bin_copy(s, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->bin_chunks.p, n_chunks, err,
+    e = pqg::launch_bin_copy(sb, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->bin_chunks.p, n_chunks, err,
                              ecount);
   if (e == hipSuccess && P->cls_n[C_DBA])
-    e = pqg::launch_dba_copy(s, P->d_bytes, P->n_bytes, work, cols, lists + P->cls_off[C_DBA], P->cls_n[C_DBA],
+    e = pqg::launch_dba_copy(sb, P->d_bytes, P->n_bytes, work, cols, lists + P->cls_off[C_DBA], P->cls_n[C_DBA],
                              (const uint64_t*)P->dba_chunks.p, P->n_dba_chunks, P->dba_meta(), bl + P->off_carry,
                              P->n_carry, err, ecount);
   if (fork && hipStreamWaitEvent(s, ctx->ev_join, 0) != hipSuccess) e = hipErrorUnknown;
+  if (fork_bin && (hipEventRecord(ctx->ev_join_bin, ctx->bin_stream) != hipSuccess ||
+                   hipStreamWaitEvent(s, ctx->ev_join_bin, 0) != hipSuccess))
+    e = hipErrorUnknown;
   ctx->last_launched = P;
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }
