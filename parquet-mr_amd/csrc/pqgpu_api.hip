@@ -189,6 +189,11 @@ struct pqg_ctx {
   // offset scan, copies) on a third, beside the fixed-width columns' kernels
   hipStream_t bin_stream = nullptr;
   hipEvent_t ev_join_bin = nullptr;
+  // ... and the fixed-width columns' kernels on a fourth. The three are created one after the other
+  // with the context, so that HIP's round-robin puts them on different hardware queues; the caller's
+  // stream only waits while they run (a queue shared with it costs nothing then).
+  hipStream_t fix_stream = nullptr;
+  hipEvent_t ev_join_fix = nullptr;
 };
 
 extern "C" {
@@ -241,6 +246,9 @@ int pqg_ctx_create(int device, void* hip_stream, pqg_ctx** out) {
     }
     c->own_stream = true;
   }
+  if (hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking) != hipSuccess) c->side_stream = nullptr;
+  if (hipStreamCreateWithFlags(&c->bin_stream, hipStreamNonBlocking) != hipSuccess) c->bin_stream = nullptr;
+  if (hipStreamCreateWithFlags(&c->fix_stream, hipStreamNonBlocking) != hipSuccess) c->fix_stream = nullptr;
   *out = c;
   return PQG_OK;
 }
@@ -275,6 +283,11 @@ int pqg_ctx_destroy(pqg_ctx* c) {
     (void)hipStreamDestroy(c->bin_stream);
   }
   if (c->ev_join_bin) (void)hipEventDestroy(c->ev_join_bin);
+  if (c->fix_stream) {
+    (void)hipStreamSynchronize(c->fix_stream);
+    (void)hipStreamDestroy(c->fix_stream);
+  }
+  if (c->ev_join_fix) (void)hipEventDestroy(c->ev_join_fix);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -869,6 +882,11 @@ int pqg_plan_launch(pqg_plan* P) {
                (ctx->ev_join_bin || hipEventCreateWithFlags(&ctx->ev_join_bin, hipEventDisableTiming) == hipSuccess) &&
                hipStreamWaitEvent(ctx->bin_stream, ctx->ev_fork, 0) == hipSuccess;
   }
+  bool fork_fix = false;
+  if ((fork || fork_bin) && has_fixed)
+    fork_fix = (ctx->fix_stream || hipStreamCreateWithFlags(&ctx->fix_stream, hipStreamNonBlocking) == hipSuccess) &&
+               (ctx->ev_join_fix || hipEventCreateWithFlags(&ctx->ev_join_fix, hipEventDisableTiming) == hipSuccess) &&
+               hipStreamWaitEvent(ctx->fix_stream, ctx->ev_fork, 0) == hipSuccess;
 #endif
   if (e == hipSuccess && pf) {  // PLAIN-only BYTE_ARRAY columns: one pass (after the levels: n_values, out_offset)
     uint8_t* scb = (uint8_t*)P->bscratch.p;
@@ -880,6 +898,7 @@ int pqg_plan_launch(pqg_plan* P) {
     if (fork && hipEventRecord(ctx->ev_join, ctx->side_stream) != hipSuccess) e = hipErrorUnknown;
   }
   const hipStream_t sb = fork_bin ? ctx->bin_stream : s;  // BYTE_ARRAY kernels of the other columns
+  const hipStream_t sf = fork_fix ? ctx->fix_stream : s;  // fixed-width columns
   if (e == hipSuccess && P->n_dict_walk)  // BYTE_ARRAY dictionary entries (PlainBinaryDictionary ctor)
     e = pqg::launch_bin_walk(sb, P->d_bytes, P->n_bytes, work, cols, bl + P->off_dict_walk, P->n_dict_walk, 1, P->n_pages,
                              err, ecount);
@@ -891,7 +910,7 @@ int pqg_plan_launch(pqg_plan* P) {
       case C_DICT4:
       case C_DICT8: {
         const int i = k - C_DICT4;
-        e = pqg::launch_dict(k == C_DICT8 ? 8 : 4, s, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
+        e = pqg::launch_dict(k == C_DICT8 ? 8 : 4, sf, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
                              (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->chunk_off[i], P->chunk_n[i],
                              (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused, err, ecount);
         break;
@@ -903,7 +922,7 @@ int pqg_plan_launch(pqg_plan* P) {
                                  P->chunk_n[i], (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused, err, ecount);
         break;
       }
-      case C_BSS: e = pqg::launch_bss(s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_BSS: e = pqg::launch_bss(sf, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_BINP:
         e = pqg::launch_bin_walk(sb, P->d_bytes, P->n_bytes, work, cols, l, n, 0, P->n_pages, err, ecount);
         break;
@@ -911,11 +930,11 @@ int pqg_plan_launch(pqg_plan* P) {
       case C_DBA:
         e = pqg::launch_dba_lengths(sb, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount, P->dba_meta());
         break;
-      case C_PLAIN: e = pqg::launch_plain(0, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
-      case C_BOOL: e = pqg::launch_plain(1, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
-      case C_RLEBOOL: e = pqg::launch_plain(2, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
-      case C_DELTA4: e = pqg::launch_delta(4, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
-      case C_DELTA8: e = pqg::launch_delta(8, s, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_PLAIN: e = pqg::launch_plain(0, sf, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_BOOL: e = pqg::launch_plain(1, sf, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_RLEBOOL: e = pqg::launch_plain(2, sf, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_DELTA4: e = pqg::launch_delta(4, sf, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
+      case C_DELTA8: e = pqg::launch_delta(8, sf, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
     }
   }
   if (e == hipSuccess && P->n_segs) {  // PLAIN BYTE_ARRAY pages in segments (status + ticket cleared above)
@@ -943,6 +962,9 @@ int pqg_plan_launch(pqg_plan* P) {
   if (fork && hipStreamWaitEvent(s, ctx->ev_join, 0) != hipSuccess) e = hipErrorUnknown;
   if (fork_bin && (hipEventRecord(ctx->ev_join_bin, ctx->bin_stream) != hipSuccess ||
                    hipStreamWaitEvent(s, ctx->ev_join_bin, 0) != hipSuccess))
+    e = hipErrorUnknown;
+  if (fork_fix && (hipEventRecord(ctx->ev_join_fix, ctx->fix_stream) != hipSuccess ||
+                   hipStreamWaitEvent(s, ctx->ev_join_fix, 0) != hipSuccess))
     e = hipErrorUnknown;
   ctx->last_launched = P;
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
