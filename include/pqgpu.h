@@ -23,8 +23,11 @@
  * Threading: a pqg_ctx owns one HIP stream and its device scratch; it is not
  * shared between threads (one ctx per thread per GPU), like a ValuesReader.
  * All pqg_decode / pqg_plan_launch work is asynchronous on the ctx stream
- * until pqg_sync. No exception crosses this ABI: every function returns a
- * pqg_error code and fills an optional pqg_status.
+ * until pqg_sync (a launch may fan out to three internal queues of the ctx
+ * and joins them back into the ctx stream before it returns, so events and
+ * synchronization on the ctx stream cover all of it). No exception crosses
+ * this ABI: every function returns a pqg_error code and fills an optional
+ * pqg_status.
  */
 #ifndef PQGPU_H
 #define PQGPU_H
