@@ -81,7 +81,10 @@ constexpr uint64_t ERR_KEY_MASK = (1ull << 48) - 1;
 enum BinKind : uint32_t { BIN_PLAIN = 0, BIN_DLBA = 1, BIN_DICT = 2, BIN_DBA = 3 };
 
 // Output chunk of k_dict_expand: CH_TILES x 64 lanes x 16 bytes.
-constexpr uint32_t DICT_CHUNK_TILES = 16;
+#ifndef PQG_DICT_CHUNK_TILES
+#define PQG_DICT_CHUNK_TILES 16
+#endif
+constexpr uint32_t DICT_CHUNK_TILES = PQG_DICT_CHUNK_TILES;
 inline uint32_t dict_chunk_values(int elem_width) { return DICT_CHUNK_TILES * 64u * (16u / (uint32_t)elem_width); }
 // output chunks of a dictionary page of n slots (slots shifted by up to 16 / width - 1 for 16-B alignment)
 inline uint32_t dict_page_chunks(uint32_t n, int elem_width) {
