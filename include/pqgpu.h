@@ -24,10 +24,20 @@
  * shared between threads (one ctx per thread per GPU), like a ValuesReader.
  * All pqg_decode / pqg_plan_launch work is asynchronous on the ctx stream
  * until pqg_sync (a launch may fan out to three internal queues of the ctx
- * and joins them back into the ctx stream before it returns, so events and
- * synchronization on the ctx stream cover all of it). No exception crosses
- * this ABI: every function returns a pqg_error code and fills an optional
- * pqg_status.
+ * and joins them back into the ctx stream before it returns). Outputs are
+ * valid only after pqg_sync returns: two rare cases are repaired by pqg_sync
+ * itself with a host-driven re-launch (a PLAIN BYTE_ARRAY page with bytes
+ * after its values, pqg_plan_plain_fallbacks; a fused-kernel timeout,
+ * pqg_plan_timeout_fallbacks), so work ordered after a launch on the ctx
+ * stream by events alone may see outputs that pqg_sync later rewrites.
+ * No exception crosses this ABI: every function returns a pqg_error code and
+ * fills an optional pqg_status.
+ *
+ * ABI 3 (this version): per-page errors (pqg_page_errors) so that a failure
+ * surfaces in its own column only; the staged host path (pqg_host_input /
+ * pqg_decode_staged / pqg_staged_column) for callers that must not hold host
+ * arrays across device work (JNI critical regions); the host batch of router
+ * runs (pqg_router_read_runs); levels readers (pqgpu_reader.h).
  */
 #ifndef PQGPU_H
 #define PQGPU_H
@@ -39,7 +49,7 @@
 extern "C" {
 #endif
 
-#define PQG_ABI_VERSION 2
+#define PQG_ABI_VERSION 3
 
 /* parquet-format `Type` values (parquet.thrift). */
 enum pqg_physical_type {
@@ -220,9 +230,50 @@ int pqg_decode(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes,
                uint32_t* d_page_value_counts, pqg_status* st);
 
 /* Wait for all work on the ctx stream; returns the first decode error of the
- * calls since the previous pqg_sync and fills cols[i].values_written for the
- * most recent pqg_decode / plan launch. */
+ * calls since the previous pqg_sync (every plan launched since then, in launch
+ * order, is checked and repaired as described above) and fills
+ * cols[i].values_written for the most recent pqg_decode. */
 int pqg_sync(pqg_ctx* ctx, pqg_status* st);
+
+/* ---- per-page errors ---------------------------------------------------------
+ * pqg_status names the batch's first failing page. A column reader in the
+ * reference fails on its own (ColumnReaderBase.readPage / checkRead /
+ * readValue, ColumnReaderBase.java:590-676, 738-771): the other columns of the
+ * row group stay readable. pqg_page_errors gives every page's own first error
+ * in the reference's read order of that page:
+ *   DICTIONARY  the column's dictionary page (ColumnReaderBase ctor :448-472; set on the column's
+ *               first page of the batch)
+ *   RL_INIT / DL_INIT / DATA_INIT   rlReader / dlReader / data reader initFromPage (readPageV1
+ *               :738-758; a V2 page's level lengths past the page: RL_INIT)
+ *   RL_READ / DL_READ   repetitionLevelColumn / definitionLevelColumn .nextInt() of slot `index`
+ *               (checkRead :650-676 reads rl then dl per slot)
+ *   VALUE       the read of value `index` of the page (readValue :584-626)
+ * Values are decoded only for slots before a level error, and a page's value count
+ * (page_value_counts) stops there. A caller serving the pages of one column in
+ * order stops at that column's first failing page (pqgpu_reader.h does). */
+enum pqg_phase {
+  PQG_PHASE_NONE = 0,
+  PQG_PHASE_DICTIONARY = 1,
+  PQG_PHASE_RL_INIT = 2,
+  PQG_PHASE_DL_INIT = 3,
+  PQG_PHASE_DATA_INIT = 4,
+  PQG_PHASE_RL_READ = 5,
+  PQG_PHASE_DL_READ = 6,
+  PQG_PHASE_VALUE = 7
+};
+
+typedef struct pqg_page_error {
+  int32_t code;     /* pqg_error; PQG_OK when the page decoded cleanly */
+  int32_t phase;    /* pqg_phase */
+  int64_t index;    /* RL_READ / DL_READ: slot in the page; VALUE: value in the page; else -1 */
+} pqg_page_error;
+
+/* Every page's error of the most recent pqg_decode / pqg_decode_host / pqg_decode_staged on the
+ * ctx, after its pqg_sync (the host calls sync themselves). `n_pages` must equal that call's page
+ * count. API / device failures (no page) are not listed: they are the call's return code. */
+int pqg_page_errors(pqg_ctx* ctx, pqg_page_error* out, int n_pages);
+/* The same for a plan's most recent launch, after pqg_sync. */
+int pqg_plan_page_errors(pqg_plan* plan, pqg_page_error* out, int n_pages);
 
 /* ---- prepared plans (bench / steady-state) --------------------------------
  * A plan uploads descriptors once; pqg_plan_launch re-runs the decode of the
@@ -257,6 +308,39 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes,
                     const pqg_page_desc* pages, int n_pages,
                     uint32_t* h_page_value_counts, pqg_status* st);
 
+/* ---- staged host path -------------------------------------------------------
+ * pqg_decode_host reads and writes the caller's host arrays while the device works, which a JNI
+ * caller may not allow (a Get*ArrayCritical region must not span blocking calls). The staged path
+ * keeps the caller's arrays out of device work: the library owns the pinned input and output
+ * buffers, and the caller copies in before and out after.
+ *   1. pqg_host_input(ctx, n_bytes, &p): pinned buffer of at least n_bytes (+ padding, zeroed by the
+ *      decode); the caller writes the page bytes to p[0 .. n_bytes) (JNI: GetByteArrayRegion, or a
+ *      memcpy from a direct buffer). Valid until the next pqg_host_input / host call on ctx.
+ *   2. pqg_decode_staged(ctx, n_bytes, cols, ...): as pqg_decode_host over those bytes. The output
+ *      fields of `cols` (pointers and capacities) are ignored: the values of every column and the
+ *      levels of every column with max_def / max_rep > 0 are produced into library memory, sized by
+ *      the library. Returns after the outputs are in pinned host memory.
+ *   3. pqg_staged_column(ctx, col, &out): where column `col`'s outputs are in that memory; valid
+ *      until the next host call on ctx. Copy them out with any memcpy (JNI: Set<Type>ArrayRegion,
+ *      or pqg_copy_out inside a short critical region: a plain multi-threaded memcpy, no device call).
+ * Codes, statuses and per-page errors as pqg_decode_host. */
+typedef struct pqg_staged_output {
+  const void* values;        /* n_values elements (BYTE_ARRAY: int64 offsets[n_values + 1]) */
+  const uint8_t* def_levels; /* n_slots bytes, NULL if not wanted / max_def == 0 */
+  const uint8_t* rep_levels; /* n_slots bytes, NULL if not wanted / max_rep == 0 */
+  const uint8_t* binary;     /* BYTE_ARRAY: n_binary value bytes */
+  uint64_t n_values;
+  uint64_t n_slots;
+  uint64_t n_binary;
+} pqg_staged_output;
+
+int pqg_host_input(pqg_ctx* ctx, uint64_t n_bytes, uint8_t** buf);
+int pqg_decode_staged(pqg_ctx* ctx, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
+                      const pqg_page_desc* pages, int n_pages, uint32_t* h_page_value_counts, pqg_status* st);
+int pqg_staged_column(pqg_ctx* ctx, int col, pqg_staged_output* out);
+/* memcpy of n bytes spread over up to 8 host threads (large copies out of pinned memory). */
+void pqg_copy_out(void* dst, const void* src, uint64_t n);
+
 /* ---- ParquetReadRouter boundary --------------------------------------------
  * Batch of bit-packed runs on the device: run r unpacks counts[r] (multiple of 8)
  * LSB-first values of `bit_width` bits from d_in + in_offsets[r] into
@@ -274,6 +358,16 @@ int pqg_unpack_runs(pqg_ctx* ctx, int bit_width, const uint8_t* d_in,
  * (device buffers) or decode whole pages with pqg_decode. */
 int pqg_router_read(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_len,
                     int count, int32_t* out);
+
+/* Many router reads in one round trip (host buffers): run r is ParquetReadRouter.read(bit_width,
+ * in positioned at in_offsets[r], counts[r], ...) and its counts[r] ints go to out + (sum of the
+ * earlier counts). One H2D of the bytes the runs cover, one kernel, one D2H, one synchronisation
+ * for the whole batch (a page's bit-packed runs, say). counts[r] must be a multiple of 8 (a
+ * bit-packed run's currentCount); a run whose counts[r] * bit_width / 8 bytes pass in_len ->
+ * PQG_ERR_EOF with nothing written (SingleBufferInputStream.slice throws EOFException before the
+ * unpack). Synchronous. */
+int pqg_router_read_runs(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_len,
+                         const uint64_t* in_offsets, const uint32_t* counts, int n_runs, int32_t* out);
 
 /* ---- record assembly ---------------------------------------------------------
  * Dremel assembly of ONE leaf column into the columnar form of its records: the

@@ -868,16 +868,17 @@ int pqr_decode(const uint8_t* bytes, uint64_t n_bytes, pqg_column_desc* cols, in
       jstream rls = {page.buf, 0, pg->rl_byte_length};
       jstream dls = {page.buf, pg->rl_byte_length, (int64_t)pg->rl_byte_length + pg->dl_byte_length};
       jstream data = {page.buf, (int64_t)pg->rl_byte_length + pg->dl_byte_length, pg->size};
-      if ((e = lreader_init_v2(&rl, c->max_rep, rls)) || (e = lreader_init_v2(&dl, c->max_def, dls))) {
-        rc = e; set_status(st, rc, p, 0, "level init"); break;
-      }
+      if ((e = lreader_init_v2(&rl, c->max_rep, rls))) { rc = e; set_status(st, rc, p, 0, "rl init"); break; }
+      if ((e = lreader_init_v2(&dl, c->max_def, dls))) { rc = e; set_status(st, rc, p, 0, "dl init"); break; }
       if ((e = vreader_init(&vr, pg, C, &data, nv))) {
         rc = e; set_status(st, rc, p, 0, "data init"); vreader_free(&vr); break;
       }
     } else {
-      if ((e = lreader_init_v1(&rl, pg->rl_encoding, c->max_rep, &page, nv)) ||
-          (e = lreader_init_v1(&dl, pg->dl_encoding, c->max_def, &page, nv))) {
-        rc = e; set_status(st, rc, p, 0, "level init"); break;
+      if ((e = lreader_init_v1(&rl, pg->rl_encoding, c->max_rep, &page, nv))) {
+        rc = e; set_status(st, rc, p, 0, "rl init"); break;
+      }
+      if ((e = lreader_init_v1(&dl, pg->dl_encoding, c->max_def, &page, nv))) {
+        rc = e; set_status(st, rc, p, 0, "dl init"); break;
       }
       if ((e = vreader_init(&vr, pg, C, &page, nv))) {
         rc = e; set_status(st, rc, p, 0, "data init"); vreader_free(&vr); break;
@@ -886,9 +887,8 @@ int pqr_decode(const uint8_t* bytes, uint64_t n_bytes, pqg_column_desc* cols, in
     uint64_t before = C->n_values;
     for (int32_t slot = 0; slot < nv; slot++) {
       int32_t r, d;
-      if ((e = lreader_next(&rl, &r)) || (e = lreader_next(&dl, &d))) {
-        rc = e; set_status(st, rc, p, slot, "level decode"); break;
-      }
+      if ((e = lreader_next(&rl, &r))) { rc = e; set_status(st, rc, p, slot, "rl decode"); break; }
+      if ((e = lreader_next(&dl, &d))) { rc = e; set_status(st, rc, p, slot, "dl decode"); break; }
       if (C->n_slots >= c->levels_capacity && (c->def_levels || c->rep_levels)) {
         rc = PQG_ERR_INVALID_ARG; set_status(st, rc, p, slot, "levels capacity"); break;
       }

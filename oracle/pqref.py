@@ -110,12 +110,20 @@ def delta_decode(data, cap=1 << 22):
     return out[:n].copy(), cons.value
 
 
+# pqg_phase of the oracle's first error, from the reader that raised it (pqr_decode's messages)
+PHASE_OF_MESSAGE = {"dictionary page": abi.PHASE_DICTIONARY, "V2 level lengths": abi.PHASE_RL_INIT,
+                    "rl init": abi.PHASE_RL_INIT, "dl init": abi.PHASE_DL_INIT, "data init": abi.PHASE_DATA_INIT,
+                    "rl decode": abi.PHASE_RL_READ, "dl decode": abi.PHASE_DL_READ, "value decode": abi.PHASE_VALUE}
+
+
 class OracleResult:
-    def __init__(self, code, status, columns, page_value_counts):
+    def __init__(self, code, status, columns, page_value_counts, message=""):
         self.code = code
         self.status = status
         self.columns = columns
         self.page_value_counts = page_value_counts
+        self.message = message
+        self.phase = PHASE_OF_MESSAGE.get(message.split(":")[0], abi.PHASE_NONE) if code else abi.PHASE_NONE
 
 
 def decode_batch(batch, binary_capacity=None):
@@ -177,7 +185,7 @@ def _decode_batch(batch, binary_capacity):
         res["def_levels"] = dl[:batch.column_slots[i]].copy() if cd["max_def"] > 0 else None
         res["rep_levels"] = rl[:batch.column_slots[i]].copy() if cd["max_rep"] > 0 else None
         out.append(res)
-    return OracleResult(rc, st.as_tuple(), out, counts[:batch.n_pages].copy())
+    return OracleResult(rc, st.as_tuple(), out, counts[:batch.n_pages].copy(), st.message.decode(errors="replace"))
 
 
 def snappy_decompress(data, uncompressed_size):

@@ -148,6 +148,7 @@ struct pqg_plan {
   std::vector<uint8_t> col_nullable;
   std::vector<uint64_t> col_required_values;
   std::vector<HostErr> host_errs;
+  std::vector<pqg_page_error> page_errs;  // per page, resolved by pqg_sync (pqg_page_errors)
   int kernels = 0;
   DevBuf segs;                        // PLAIN BYTE_ARRAY segments (k_bin_walk_seg): page | s << 32 | last << 63
   uint32_t n_segs = 0;
@@ -175,6 +176,8 @@ struct pqg_ctx {
   bool own_stream = false;
   pqg_plan* last = nullptr;          // plan of the most recent pqg_decode (owned)
   pqg_plan* last_launched = nullptr; // plan of the most recent launch (decode or plan_launch)
+  std::vector<pqg_plan*> unsynced;   // plans launched since the last pqg_sync, in launch order
+  std::vector<pqg_staged_output> staged;  // pqg_decode_staged: where each column's outputs are in pin_out
   pqg_column_desc* last_cols = nullptr;
   PinnedBuf pin_in, pin_out, pin_err;
   DevBuf host_bytes, host_out, host_counts, host_runs;
@@ -967,6 +970,7 @@ int pqg_plan_launch(pqg_plan* P) {
                    hipStreamWaitEvent(s, ctx->ev_join_fix, 0) != hipSuccess))
     e = hipErrorUnknown;
   ctx->last_launched = P;
+  if (std::find(ctx->unsynced.begin(), ctx->unsynced.end(), P) == ctx->unsynced.end()) ctx->unsynced.push_back(P);
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }
 
@@ -976,6 +980,8 @@ int pqg_plan_destroy(pqg_plan* P) {
     (void)hipStreamSynchronize(P->ctx->stream);
     if (P->ctx->last_launched == P) P->ctx->last_launched = nullptr;
     if (P->ctx->last == P) P->ctx->last = nullptr;
+    auto& u = P->ctx->unsynced;
+    u.erase(std::remove(u.begin(), u.end(), P), u.end());
   }
   P->work.release();
   P->cols.release();
@@ -1061,65 +1067,61 @@ int resolve_errors(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work_out)
 }
 
 int resolve_page_errors(pqg_plan* P, pqg_status* st, const std::vector<uint64_t>& errs) {
+  // every page's own first error (pqg_page_errors), then the batch's first in page order (st)
+  P->page_errs.assign((size_t)P->n_pages, pqg_page_error{PQG_OK, PQG_PHASE_NONE, -1});
   if (P->host_errs.empty() && errs.empty()) return PQG_OK;
   std::vector<const HostErr*> herr((size_t)std::max(P->n_pages, 1), nullptr);
   for (const HostErr& h : P->host_errs)
     if (!herr[(size_t)h.page]) herr[(size_t)h.page] = &h;
+  int first = -1;
   for (int p = 0; p < P->n_pages; p++) {
+    pqg_page_error& pe = P->page_errs[(size_t)p];
     const HostErr* h = herr[(size_t)p];
     // device-detected dictionary page errors (BYTE_ARRAY dictionary walk, pseudo page n_pages + column):
     // the ColumnReaderBase ctor reads the dictionary before the column's first page
     const int col = P->h_work[(size_t)p].column;
-    if (!errs.empty() && col >= 0 && col < P->n_cols && P->col_first_page[(size_t)col] == p) {
-      const uint64_t d = errs[3 * (size_t)(P->n_pages + col)];
-      if (d != ~0ull) {
-        set_status(st, (int)(d & 0xFF), p, -1, "dictionary page");
-        return (int)(d & 0xFF);
-      }
-    }
+    const uint64_t d = (!errs.empty() && col >= 0 && col < P->n_cols && P->col_first_page[(size_t)col] == p)
+                           ? errs[3 * (size_t)(P->n_pages + col)] : ~0ull;
     uint64_t init = errs.empty() ? ~0ull : errs[3 * (size_t)p];
     uint64_t lvl = errs.empty() ? ~0ull : errs[3 * (size_t)p + 1];
     uint64_t val = errs.empty() ? ~0ull : errs[3 * (size_t)p + 2];
-    // host-detected errors are init-phase (descriptor) errors of this page
-    if (h && h->index == -1) {  // dictionary page: before any page is read
-      set_status(st, h->code, p, -1, "dictionary page");
-      return h->code;
+    if (d != ~0ull) {
+      pe = {(int32_t)(d & 0xFF), PQG_PHASE_DICTIONARY, -1};
+    } else if (h && h->index == -1) {  // host-detected dictionary page error: before any page is read
+      pe = {h->code, PQG_PHASE_DICTIONARY, -1};
+    } else if (h || init != ~0ull) {   // init-phase errors: key = phase (0 rl, 1 dl, 2 data) << 8 | code
+      const uint64_t hkey = h ? (((uint64_t)h->index << 8) | (uint64_t)h->code) : ~0ull;
+      const uint64_t k = std::min(hkey, init);
+      const int ph = (int)(k >> 8);
+      pe = {(int32_t)(k & 0xFF), ph == 0 ? PQG_PHASE_RL_INIT : ph == 1 ? PQG_PHASE_DL_INIT : PQG_PHASE_DATA_INIT, -1};
+    } else if (val != ~0ull) {
+      // values are decoded only for slots before a level error: a value error comes first
+      pe = {(int32_t)(val & 0xFF), PQG_PHASE_VALUE, (int64_t)(val >> 8)};
+    } else if (lvl != ~0ull) {         // key = (slot << 1 | 0 rl / 1 dl) << 8 | code
+      pe = {(int32_t)(lvl & 0xFF), ((lvl >> 8) & 1) ? PQG_PHASE_DL_READ : PQG_PHASE_RL_READ, (int64_t)(lvl >> 9)};
     }
-    if (h || init != ~0ull) {
-      uint64_t hkey = h ? (((uint64_t)h->index << 8) | (uint64_t)h->code) : ~0ull;
-      uint64_t k = std::min(hkey, init);
-      int code = (int)(k & 0xFF);
-      set_status(st, code, p, 0, (k >> 8) == 2 ? "data init" : "level init");
-      return code;
-    }
-    if (val != ~0ull) {
-      int code = (int)(val & 0xFF);
-      set_status(st, code, p, (int64_t)(val >> 8), "value decode");
-      return code;
-    }
-    if (lvl != ~0ull) {
-      int code = (int)(lvl & 0xFF);
-      set_status(st, code, p, (int64_t)(lvl >> 9), "level decode");
-      return code;
-    }
+    if (pe.code != PQG_OK && first < 0) first = p;
   }
-  return PQG_OK;
+  if (first < 0) return PQG_OK;
+  const pqg_page_error& pe = P->page_errs[(size_t)first];
+  switch (pe.phase) {
+    case PQG_PHASE_DICTIONARY: set_status(st, pe.code, first, -1, "dictionary page"); break;
+    case PQG_PHASE_DATA_INIT: set_status(st, pe.code, first, 0, "data init"); break;
+    case PQG_PHASE_RL_INIT: case PQG_PHASE_DL_INIT: set_status(st, pe.code, first, 0, "level init"); break;
+    case PQG_PHASE_VALUE: set_status(st, pe.code, first, pe.index, "value decode"); break;
+    default: set_status(st, pe.code, first, pe.index, "level decode"); break;
+  }
+  return pe.code;
 }
 
 }  // namespace
 
-extern "C" {
+namespace {
 
-int pqg_sync(pqg_ctx* ctx, pqg_status* st) {
-  if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
-  if (!ctx) return PQG_ERR_INVALID_ARG;
-  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
-  if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
-    set_status(st, PQG_ERR_HIP, -1, -1, hipGetErrorString(hipGetLastError()));
-    return PQG_ERR_HIP;
-  }
-  pqg_plan* P = ctx->last_launched;
-  if (!P) return PQG_OK;
+// pqg_sync for one launched plan: the PLAIN one-pass re-run, error resolution, the fused-kernel
+// timeout re-run. `work` receives the plan's PageWork (nullable columns' value counts).
+int sync_plan(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work) {
+  pqg_ctx* ctx = P->ctx;
   if (P->plain_fused) {
     // A PLAIN page whose values do not end at its section end (bytes the reader ignores after them)
     // breaks the one-pass path's byte bases: the launch is re-run on the per-value path (k_bin_walk,
@@ -1136,8 +1138,7 @@ int pqg_sync(pqg_ctx* ctx, pqg_status* st) {
       if (hipStreamSynchronize(ctx->stream) != hipSuccess) return PQG_ERR_HIP;
     }
   }
-  std::vector<PageWork> work;
-  int rc = resolve_errors(P, st, &work);
+  int rc = resolve_errors(P, st, work);
   if (rc == PQG_ERR_TIMEOUT && P->dict_fused) {
     // The fused dictionary kernel's hand-off relies on the walker workgroups being dispatched before
     // the expansion workgroups that wait for them, which HIP does not promise. A launch in which an
@@ -1151,22 +1152,65 @@ int pqg_sync(pqg_ctx* ctx, pqg_status* st) {
     rc = pqg_plan_launch(P);
     if (rc == PQG_OK) {
       if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
-      work.clear();
-      rc = resolve_errors(P, st, &work);
-    }
-  }
-  if (ctx->last_cols && P == ctx->last) {
-    for (int i = 0; i < P->n_cols; i++) {
-      uint64_t n = P->col_required_values[(size_t)i];
-      if (P->col_nullable[(size_t)i] && !work.empty()) {
-        n = 0;
-        for (int p = 0; p < P->n_pages; p++)
-          if (work[(size_t)p].column == i) n += work[(size_t)p].n_values;
-      }
-      ctx->last_cols[i].values_written = n;
+      work->clear();
+      rc = resolve_errors(P, st, work);
     }
   }
   return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pqg_sync(pqg_ctx* ctx, pqg_status* st) {
+  if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
+  if (!ctx) return PQG_ERR_INVALID_ARG;
+  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    set_status(st, PQG_ERR_HIP, -1, -1, hipGetErrorString(hipGetLastError()));
+    return PQG_ERR_HIP;
+  }
+  // every plan launched since the last sync, in launch order (re-runs inside sync_plan append the
+  // plan again; the list is taken first and cleared at the end)
+  std::vector<pqg_plan*> plans;
+  plans.swap(ctx->unsynced);
+  int rc = PQG_OK;
+  for (pqg_plan* P : plans) {
+    pqg_status pst;
+    std::vector<PageWork> work;
+    const int prc = sync_plan(P, &pst, &work);
+    if (prc != PQG_OK && rc == PQG_OK) {
+      rc = prc;
+      if (st) *st = pst;
+    }
+    if (prc == PQG_ERR_HIP) break;
+    if (ctx->last_cols && P == ctx->last) {
+      for (int i = 0; i < P->n_cols; i++) {
+        uint64_t n = P->col_required_values[(size_t)i];
+        if (P->col_nullable[(size_t)i] && !work.empty()) {
+          n = 0;
+          for (int p = 0; p < P->n_pages; p++)
+            if (work[(size_t)p].column == i) n += work[(size_t)p].n_values;
+        }
+        ctx->last_cols[i].values_written = n;
+      }
+    }
+  }
+  ctx->unsynced.clear();
+  return rc;
+}
+
+int pqg_plan_page_errors(pqg_plan* P, pqg_page_error* out, int n_pages) {
+  if (!P || n_pages != P->n_pages || (n_pages && !out)) return PQG_ERR_INVALID_ARG;
+  for (int p = 0; p < n_pages; p++)
+    out[p] = (size_t)p < P->page_errs.size() ? P->page_errs[(size_t)p] : pqg_page_error{PQG_OK, PQG_PHASE_NONE, -1};
+  return PQG_OK;
+}
+
+int pqg_page_errors(pqg_ctx* ctx, pqg_page_error* out, int n_pages) {
+  if (!ctx || !ctx->last) return PQG_ERR_INVALID_ARG;
+  return pqg_plan_page_errors(ctx->last, out, n_pages);
 }
 
 int pqg_plan_create(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, const pqg_column_desc* cols, int n_cols,
@@ -1255,10 +1299,15 @@ void par_memcpy(void* dst, const void* src, uint64_t n) {
 }
 }  // namespace
 
-int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
-                    const pqg_page_desc* pages, int n_pages, uint32_t* h_page_value_counts, pqg_status* st) {
+// The host path. h_bytes == nullptr: staged (pqg_decode_staged) — the bytes are already in ctx->pin_in,
+// the outputs stay in ctx->pin_out and ctx->staged describes them; otherwise the caller's arrays.
+static int host_path(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
+                     const pqg_page_desc* pages, int n_pages, uint32_t* h_page_value_counts, pqg_status* st) {
   if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
-  if (!ctx || (n_bytes && !h_bytes) || n_cols < 0 || n_pages < 0) return PQG_ERR_INVALID_ARG;
+  const bool staged = h_bytes == nullptr;
+  if (!ctx || n_cols < 0 || n_pages < 0 || (n_cols && !cols) || (n_pages && !pages)) return PQG_ERR_INVALID_ARG;
+  if (staged && ctx->pin_in.cap < n_bytes + 1024) return PQG_ERR_INVALID_ARG;  // pqg_host_input first
+  ctx->staged.clear();
   if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
   hipStream_t s = ctx->stream;
   // PQG_HOST_TIMING=1: phase times of this call on stderr (diagnostics)
@@ -1290,15 +1339,20 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
     set_status(st, PQG_ERR_HIP, -1, -1, "device buffers");
     return PQG_ERR_HIP;
   }
-  // host -> pinned -> device (the JNI shim hands heap bytes; the copy into pinned
-  // memory is what a production shim does with direct ByteBuffers too)
-  par_memcpy(ctx->pin_in.p, h_bytes, n_bytes);
+  // host -> pinned -> device (staged: the caller wrote the bytes into pin_in)
+  if (!staged) par_memcpy(ctx->pin_in.p, h_bytes, n_bytes);
   std::memset((uint8_t*)ctx->pin_in.p + n_bytes, 0, pad);
   phase("stage-in");
   if (hipMemcpyAsync(ctx->host_bytes.p, ctx->pin_in.p, n_bytes + pad, hipMemcpyHostToDevice, s) != hipSuccess) return PQG_ERR_HIP;
   auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
   std::vector<uint64_t> off_v(nc), off_d(nc), off_r(nc), off_b(nc);
   std::vector<pqg_column_desc> dcols(cols, cols + n_cols);
+  // levels wanted: staged -> every column with a max level > 0; else where the caller gave an array
+  std::vector<uint8_t> want_d(nc, 0), want_r(nc, 0);
+  for (int i = 0; i < n_cols; i++) {
+    want_d[(size_t)i] = cols[i].max_def > 0 && (staged || cols[i].def_levels);
+    want_r[(size_t)i] = cols[i].max_rep > 0 && (staged || cols[i].rep_levels);
+  }
   uint64_t total = 0;
   int rc = PQG_OK;
   pqg_status st2;
@@ -1312,9 +1366,9 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
       off_v[(size_t)i] = total;
       total = al(total + (slots[(size_t)i] + (bin ? 1 : 0)) * (uint64_t)w);
       off_d[(size_t)i] = total;
-      if (cols[i].max_def > 0 && cols[i].def_levels) total = al(total + slots[(size_t)i]);
+      if (want_d[(size_t)i]) total = al(total + slots[(size_t)i]);
       off_r[(size_t)i] = total;
-      if (cols[i].max_rep > 0 && cols[i].rep_levels) total = al(total + slots[(size_t)i]);
+      if (want_r[(size_t)i]) total = al(total + slots[(size_t)i]);
       off_b[(size_t)i] = total;
       if (bin) total = al(total + bin_cap[(size_t)i]);
     }
@@ -1327,8 +1381,8 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
       const bool bin = bin_out(cols[i]);
       dcols[(size_t)i].values = dout + off_v[(size_t)i];
       dcols[(size_t)i].values_capacity = slots[(size_t)i] + (bin ? 1 : 0);
-      dcols[(size_t)i].def_levels = (cols[i].max_def > 0 && cols[i].def_levels) ? dout + off_d[(size_t)i] : nullptr;
-      dcols[(size_t)i].rep_levels = (cols[i].max_rep > 0 && cols[i].rep_levels) ? dout + off_r[(size_t)i] : nullptr;
+      dcols[(size_t)i].def_levels = want_d[(size_t)i] ? dout + off_d[(size_t)i] : nullptr;
+      dcols[(size_t)i].rep_levels = want_r[(size_t)i] ? dout + off_r[(size_t)i] : nullptr;
       dcols[(size_t)i].levels_capacity = slots[(size_t)i];
       dcols[(size_t)i].binary_data = bin ? dout + off_b[(size_t)i] : nullptr;
       dcols[(size_t)i].binary_capacity = bin_cap[(size_t)i];
@@ -1360,7 +1414,7 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   uint8_t* dout = (uint8_t*)ctx->host_out.p;
   const uint8_t* po = (const uint8_t*)ctx->pin_out.p;
   std::vector<HostCopy> jobs;
-  for (int i = 0; i < n_cols; i++) {
+  for (int i = 0; i < n_cols && !staged; i++) {
     const int w = out_width(cols[i]);
     const uint64_t n = std::min<uint64_t>(cols[i].values_written, cols[i].values_capacity);
     if (!bin_out(cols[i]) && cols[i].values && n)
@@ -1414,6 +1468,34 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   if (dec_done) (void)hipEventDestroy(dec_done);
   if (!ok || hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
   phase("d2h+copy");
+  if (staged) {
+    // outputs stay in pin_out: describe them (pqg_staged_column)
+    ctx->staged.resize(nc);
+    for (int i = 0; i < n_cols; i++) {
+      pqg_staged_output& o = ctx->staged[(size_t)i];
+      o.values = po + off_v[(size_t)i];
+      o.def_levels = want_d[(size_t)i] ? po + off_d[(size_t)i] : nullptr;
+      o.rep_levels = want_r[(size_t)i] ? po + off_r[(size_t)i] : nullptr;
+      o.n_values = std::min<uint64_t>(cols[i].values_written, slots[(size_t)i]);
+      o.n_slots = slots[(size_t)i];
+      o.binary = nullptr;
+      o.n_binary = 0;
+      if (bin_out(cols[i])) {
+        const uint64_t nb = (uint64_t)((const int64_t*)o.values)[o.n_values];
+        if (nb > bin_cap[(size_t)i]) {  // the device's count did not fit even after the resize
+          if (rc == PQG_OK) {
+            rc = PQG_ERR_INVALID_ARG;
+            set_status(st, rc, -1, (int64_t)nb, "binary capacity");
+          }
+        } else {
+          o.binary = po + off_b[(size_t)i];
+          o.n_binary = nb;
+        }
+      }
+    }
+    if (h_page_value_counts && n_pages) std::memcpy(h_page_value_counts, counts.data(), sizeof(uint32_t) * (size_t)n_pages);
+    return rc;
+  }
   for (int i = 0; i < n_cols; i++) {
     if (!bin_out(cols[i])) continue;
     // offsets[n + 1] and the bytes they span
@@ -1439,6 +1521,42 @@ int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_
   if (h_page_value_counts && n_pages) std::memcpy(h_page_value_counts, counts.data(), sizeof(uint32_t) * (size_t)n_pages);
   phase("binary");
   return rc;
+}
+
+int pqg_decode_host(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
+                    const pqg_page_desc* pages, int n_pages, uint32_t* h_page_value_counts, pqg_status* st) {
+  static const uint8_t empty = 0;
+  if (n_bytes && !h_bytes) {
+    if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
+    return PQG_ERR_INVALID_ARG;
+  }
+  return host_path(ctx, h_bytes ? h_bytes : &empty, n_bytes, cols, n_cols, pages, n_pages, h_page_value_counts, st);
+}
+
+int pqg_host_input(pqg_ctx* ctx, uint64_t n_bytes, uint8_t** buf) {
+  if (!ctx || !buf) return PQG_ERR_INVALID_ARG;
+  *buf = nullptr;
+  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
+  // the decode pads with 1,024 zero bytes after n_bytes (host_path's `pad`)
+  if (ctx->pin_in.ensure(n_bytes + 1024) != hipSuccess) return PQG_ERR_HIP;
+  ctx->staged.clear();
+  *buf = (uint8_t*)ctx->pin_in.p;
+  return PQG_OK;
+}
+
+int pqg_decode_staged(pqg_ctx* ctx, uint64_t n_bytes, pqg_column_desc* cols, int n_cols, const pqg_page_desc* pages,
+                      int n_pages, uint32_t* h_page_value_counts, pqg_status* st) {
+  return host_path(ctx, nullptr, n_bytes, cols, n_cols, pages, n_pages, h_page_value_counts, st);
+}
+
+int pqg_staged_column(pqg_ctx* ctx, int col, pqg_staged_output* out) {
+  if (!ctx || !out || col < 0 || (size_t)col >= ctx->staged.size()) return PQG_ERR_INVALID_ARG;
+  *out = ctx->staged[(size_t)col];
+  return PQG_OK;
+}
+
+void pqg_copy_out(void* dst, const void* src, uint64_t n) {
+  if (n && dst && src) par_memcpy(dst, src, n);
 }
 
 int pqg_assemble(pqg_ctx* ctx, const uint8_t* d_def_levels, const uint8_t* d_rep_levels, uint64_t n_slots,
@@ -1726,4 +1844,65 @@ int pqg_router_read(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_le
   return PQG_OK;
 }
 
+int pqg_router_read_runs(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_len, const uint64_t* in_offsets,
+                         const uint32_t* counts, int n_runs, int32_t* out) {
+  if (!ctx || bit_width < 0 || bit_width > 32 || n_runs < 0) return PQG_ERR_INVALID_ARG;
+  if (n_runs == 0) return PQG_OK;
+  if (!in_offsets || !counts || !out) return PQG_ERR_INVALID_ARG;
+  // every run's slice first (SingleBufferInputStream.slice throws before any unpack)
+  uint64_t n_bytes = 0, n_vals = 0;
+  uint32_t max_count = 0;
+  for (int r = 0; r < n_runs; r++) {
+    if (counts[r] % 8u != 0) return PQG_ERR_INVALID_ARG;
+    const uint64_t need = (uint64_t)counts[r] * (uint64_t)bit_width / 8u;
+    if (in_offsets[r] > in_len || need > in_len - in_offsets[r]) return PQG_ERR_EOF;
+    if (need && !in) return PQG_ERR_INVALID_ARG;
+    n_bytes += (need + 15) & ~uint64_t(15);
+    n_vals += counts[r];
+    max_count = std::max(max_count, counts[r]);
+  }
+  if (n_vals == 0) return PQG_OK;
+  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
+  hipStream_t s = ctx->stream;
+  // pinned image: [run bytes, each 16-B aligned][in_off u64 x n][out_off u64 x n][counts u32 x n]
+  auto al = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+  const uint64_t o_in = al(n_bytes + 16), o_out = o_in + 8ull * (uint64_t)n_runs, o_cnt = o_out + 8ull * (uint64_t)n_runs;
+  const uint64_t img = al(o_cnt + 4ull * (uint64_t)n_runs);
+  if (ctx->pin_in.ensure(img) != hipSuccess || ctx->pin_out.ensure(4 * n_vals) != hipSuccess ||
+      ctx->host_runs.ensure(img + 4 * n_vals + 256) != hipSuccess)
+    return PQG_ERR_HIP;
+  uint8_t* pin = (uint8_t*)ctx->pin_in.p;
+  uint64_t* pin_in_off = (uint64_t*)(pin + o_in);
+  uint64_t* pin_out_off = (uint64_t*)(pin + o_out);
+  uint32_t* pin_cnt = (uint32_t*)(pin + o_cnt);
+  uint64_t b = 0, v = 0;
+  for (int r = 0; r < n_runs; r++) {
+    const uint64_t need = (uint64_t)counts[r] * (uint64_t)bit_width / 8u;
+    if (need) std::memcpy(pin + b, in + in_offsets[r], need);
+    const uint64_t padded = (need + 15) & ~uint64_t(15);
+    std::memset(pin + b + need, 0, padded - need);
+    pin_in_off[r] = b;
+    pin_out_off[r] = v;
+    pin_cnt[r] = counts[r];
+    b += padded;
+    v += counts[r];
+  }
+  std::memset(pin + n_bytes, 0, o_in - n_bytes);
+  uint8_t* d = (uint8_t*)ctx->host_runs.p;
+  int32_t* dout = (int32_t*)(d + img);
+  if (hipMemcpyAsync(d, pin, img, hipMemcpyHostToDevice, s) != hipSuccess) return PQG_ERR_HIP;
+  for (int r0 = 0; r0 < n_runs; r0 += 65535) {  // grid.y holds the run index
+    const int nr = std::min(n_runs - r0, 65535);
+    const hipError_t e = pqg::launch_unpack_runs(s, bit_width, d, n_bytes + 16, (const uint64_t*)(d + o_in) + r0,
+                                                 (const uint32_t*)(d + o_cnt) + r0, (const uint64_t*)(d + o_out) + r0,
+                                                 dout, nr, max_count);
+    if (e != hipSuccess) return PQG_ERR_HIP;
+  }
+  if (hipMemcpyAsync(ctx->pin_out.p, dout, (size_t)(4 * n_vals), hipMemcpyDeviceToHost, s) != hipSuccess) return PQG_ERR_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
+  std::memcpy(out, ctx->pin_out.p, (size_t)(4 * n_vals));
+  return PQG_OK;
+}
+
 }  // extern "C"
+

@@ -1020,16 +1020,19 @@ __device__ uint32_t decode_levels_be(rsrc_t rs, uint32_t beg, uint32_t end, int 
   return N;
 }
 
-// Per-wave LDS of the level decoder: the page segment and pre-decode tables of the pointer-
-// jumping walk (as in the dictionary walk) plus the run table of one window.
+// Per-wave LDS of the level decoder: the page segment, the binary-lifting tables of one 256-byte
+// window's header chain, the window's pre-decoded headers, and the window's run table.
+// A run of a level section takes at least 2 bytes (w >= 1: header + value byte, or header + >= 1
+// group byte), so a window's chain holds at most 128 runs.
+constexpr uint32_t LV_RUNS = 128;
 struct LevelWaveLds {
-  struct {
-    uint8_t seg[SEG_BYTES];  // page bytes [seg_lo, seg_lo + SEG_BYTES)
-    uint64_t ent[96];        // the window walk's jump table (256 x u16) and chain marks (256 x u8)
-  } w;
-  uint32_t r_start[256];  // first slot of run k of the window
-  uint32_t r_pay[256];    // RLE: value (saturated to 255); PACKED: 0x80000000 | data byte position
-  uint32_t r_end[256];    // PACKED: end of the bytes read for the run (truncated final group)
+  uint8_t seg[SEG_BYTES];     // page bytes [seg_lo, seg_lo + SEG_BYTES)
+  uint8_t J[6][256];          // J[r][p]: window offset of the 2^r-th header after p; 0: the chain stops first
+  uint32_t ecnt[256];         // position p as a header: run count | packed << 31
+  uint16_t eval[256];         // RLE: value (saturated to 255); PACKED: data start - window start
+  uint32_t r_start[LV_RUNS];  // first slot of run k of the window
+  uint32_t r_pay[LV_RUNS];    // RLE: value (saturated to 255); PACKED: 0x80000000 | data byte position
+  uint32_t r_end[LV_RUNS];    // PACKED: end of the bytes read for the run (truncated final group)
   // the partial 16-slot tile a window's expansion ended on (more windows follow): its levels wait
   // here for the next window's part instead of going out as byte stores (expand_level_tiles)
   uint32_t carry[4];
@@ -1346,23 +1349,30 @@ __device__ __forceinline__ void expand_level_runs_generic(const LevelWaveLds& L,
 }
 
 // RLE / bit-packed level section [beg, end) (RunLengthBitPackingHybridDecoder over the section)
-// -> out[0 .. N): the pointer-jumping walk of the dictionary path (one 256-byte window at a time:
-// every byte position pre-decoded as a run header, 8 rounds of pointer doubling mark the chain),
-// the window's runs in an LDS table, then tile expansion of the slots they cover.
+// -> out[0 .. N), one 256-byte window at a time:
+//   1. pre-decode: every lane parses a run header at each of its 4 byte positions as if one started
+//      there (count, value / data start, successor position; branch-free up to 4-byte varints);
+//   2. binary lifting: J[0][p] = the successor of p inside the window (0: the chain leaves the window
+//      or p is not a fast-path header), J[r+1] = J[r] o J[r] — built only until the chain from the
+//      window's entry position ends (J[r][entry] == 0), at most 5 rounds of 4 LDS byte gathers per lane;
+//   3. lane t takes the chain's t-th header directly, c_t = J^t(entry), from the bits of t (one LDS
+//      gather per bit): no per-position marks, no compaction; a chain of more than 64 headers is taken
+//      64 at a time;
+//   4. lane t reads its header's pre-decoded count / payload, a saturating DPP scan gives the runs'
+//      first slots, lane t writes run t of the window's run table, and the tile expansion writes
+//      the slots the window's runs cover.
+// Replaced (round 4) the pointer doubling over all 256 positions with a scatter of chain marks per
+// round and a ballot compaction of the marked headers (C3: ~15 VALU + 7 SALU per run, 1.05 ms).
 // Returns the slots decoded before an error (N when none) and sets *err_code.
 template <int WB>
-__device__ __forceinline__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs, uint32_t beg, uint32_t end, int w, uint32_t N,
-                                     uint8_t* out, uint32_t max_def, bool count_nonnull, uint32_t* nonnull,
-                                     int* err_code) {
+__device__ __forceinline__ uint32_t decode_levels_bl(LevelWaveLds& L, rsrc_t rs, uint32_t beg, uint32_t end, int w,
+                                                     uint32_t N, uint8_t* out, uint32_t max_def, bool count_nonnull,
+                                                     uint32_t* nonnull, int* err_code) {
   const uint32_t lane = lane_id();
-  typedef uint16_t __attribute__((may_alias)) u16a;
   typedef uint32_t __attribute__((may_alias)) u32a;
-  typedef uint64_t __attribute__((may_alias)) u64a;
-  u16a* Jt = (u16a*)L.w.ent;
-  uint8_t* Rt = (uint8_t*)L.w.ent + 512;
   PreWin win;
   win.rs = rs;
-  win.seg = L.w.seg;
+  win.seg = L.seg;
   win.seg_lo = 0xFFFFF000u;  // nothing staged yet
   uint32_t pos = beg, produced = 0, cnt = 0;
   int code = 0;
@@ -1374,8 +1384,8 @@ __device__ __forceinline__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs,
     if (produced >= N) break;
     if (pos >= end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
     const uint32_t B = pos & ~3u;
-    predecode<false>(win, B, w);  // stages [B, B + 264) in the segment when needed
-    uint32_t jv[4], nn[4], slowm = 0, inm = 0;
+    predecode<false, true>(win, B, w);  // stages [B, B + 264) in the segment when needed
+    uint32_t js = 0, nn[4], slowm = 0, inm = 0, ec[4], ev[4];
 #pragma unroll
     for (uint32_t b = 0; b < 4; b++) {
       const uint32_t p = B + 4u * lane + b;
@@ -1385,113 +1395,111 @@ __device__ __forceinline__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs,
       const bool in = p < end;
       const bool slow = in && ((f & 2u) || p + hl > end || (!(f & 1u) && nx > end));
       nn[b] = (f & 1u) ? (nx < end ? nx : end) : nx;  // packed: readFully of what is left
-      jv[b] = (!in || slow || nn[b] - B >= 256u) ? 256u : nn[b] - B;
+      const uint32_t j = (!in || slow || nn[b] - B >= 256u) ? 0u : nn[b] - B;
+      js |= j << (8u * b);
       slowm |= (slow ? 1u : 0u) << b;
       inm |= (in ? 1u : 0u) << b;
+      ec[b] = win.cnt[b] | ((f & 1u) << 31);
+      ev[b] = (f & 1u) ? ((win.val[b] - B) & 0xFFFFu) : (win.val[b] > 255u ? 255u : win.val[b]);
     }
-    const uint32_t s0 = pos - B;
-    *(u64a*)(Jt + 4u * lane) =
-        (uint64_t)jv[0] | ((uint64_t)jv[1] << 16) | ((uint64_t)jv[2] << 32) | ((uint64_t)jv[3] << 48);
-    *(u32a*)(Rt + 4u * lane) = (4u * lane <= s0 && s0 < 4u * lane + 4u) ? (1u << (8u * (s0 & 3u))) : 0u;
+    wave_sync();  // the previous window's chain / expansion reads are done
+    ((u32a*)L.J[0])[lane] = js;
+    *(u32x4*)(L.ecnt + 4u * lane) = u32x4{ec[0], ec[1], ec[2], ec[3]};
+    ((u32a*)L.eval)[2u * lane] = ev[0] | (ev[1] << 16);
+    ((u32a*)L.eval)[2u * lane + 1u] = ev[2] | (ev[3] << 16);
+    wave_sync();
+    // J[r + 1] = J[r] o J[r] until the 2^r-th successor of the entry is missing (chain <= 2^r)
+    uint32_t s = pos - B;  // chain entry (window offset)
+    uint32_t nt = 1;       // tables built
+    {
+      uint32_t cur = js;
 #pragma unroll 1
-    for (int r = 0; r < 8; r++) {
-      const uint32_t r4 = *(const u32a*)(Rt + 4u * lane);
-      uint32_t jn[4];
+      for (uint32_t r = 0; r < 5u; r++) {
+        if (uni((uint32_t)L.J[r][s]) == 0u) break;
+        uint32_t nx2 = 0;
 #pragma unroll
-      for (uint32_t b = 0; b < 4; b++) {
-        if (((r4 >> (8u * b)) & 1u) && jv[b] < 256u) Rt[jv[b]] = 1;
-        jn[b] = jv[b] < 256u ? Jt[jv[b]] : 256u;
-      }
-#pragma unroll
-      for (uint32_t b = 0; b < 4; b++) jv[b] = jn[b];
-      *(u64a*)(Jt + 4u * lane) =
-          (uint64_t)jv[0] | ((uint64_t)jv[1] << 16) | ((uint64_t)jv[2] << 32) | ((uint64_t)jv[3] << 48);
-      const uint32_t r4n = *(const u32a*)(Rt + 4u * lane);
-      bool more = false;
-#pragma unroll
-      for (uint32_t b = 0; b < 4; b++) more |= ((r4n >> (8u * b)) & 1u) && jv[b] < 256u;
-      if (!__ballot(more)) break;
-    }
-    const uint32_t r4 = *(const u32a*)(Rt + 4u * lane);
-    uint32_t mk = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) mk |= ((r4 >> (8u * b)) & 1u) << b;
-    uint32_t q_last = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      const uint64_t m = __ballot((mk >> b) & 1u);
-      if (m) {
-        const uint32_t q = 4u * (63u - (uint32_t)__builtin_clzll(m)) + b;
-        q_last = q > q_last ? q : q_last;
+        for (uint32_t b = 0; b < 4; b++) {
+          const uint32_t j = (cur >> (8u * b)) & 0xFFu;
+          const uint32_t jj = L.J[r][j];
+          nx2 |= (j ? jj : 0u) << (8u * b);
+        }
+        ((u32a*)L.J[r + 1])[lane] = nx2;
+        cur = nx2;
+        nt = r + 2;
+        wave_sync();
       }
     }
-    q_last = uni(q_last);
-    // runs of the window: marked, inside the section, fast-path headers; counts capped at N
-    const uint32_t cap = N - produced;
-    uint32_t cc[4], lsum = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      const bool v = ((mk & inm & ~slowm) >> b) & 1u;
-      const bool pk = (win.flg >> (8u * b)) & 1u;
-      uint32_t c = win.cnt[b];
-      if (!pk && c == 0) c = cap;  // Java: currentCount goes negative, the value repeats forever
-      c = v ? (c < cap ? c : cap) : 0u;
-      cc[b] = c;
-      lsum = lsum + c < cap ? lsum + c : cap;
-    }
-    uint32_t inc = lsum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o);
-      if ((int)lane >= o) inc = inc + y < cap ? inc + y : cap;
-    }
-    uint32_t st = __shfl_up(inc, 1);
-    if (lane == 0) st = 0;
-    const uint32_t total = uni(rdl(inc, WAVE - 1));
-    uint32_t em = 0, stb[4];
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      stb[b] = st;
-      if (cc[b] && st < cap) em |= 1u << b;
-      st = st + cc[b] < cap ? st + cc[b] : cap;
-    }
-    uint32_t base = 0, n_em = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      const uint64_t m = __ballot((em >> b) & 1u);
-      base += (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
-      n_em += (uint32_t)__builtin_popcountll(m);
-    }
-    n_em = uni(n_em);
-    wave_sync();  // the previous window's expansion read the run table
-    uint32_t idx = base;
-#pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      if ((em >> b) & 1u) {
-        const bool pk = (win.flg >> (8u * b)) & 1u;
-        const uint32_t vv = win.val[b];
-        L.r_start[idx] = produced + stb[b];
-        L.r_pay[idx] = pk ? (0x80000000u | vv) : (vv > 255u ? 255u : vv);
-        L.r_end[idx] = nn[b];
-        idx++;
+    nt = uni(nt);
+    const uint32_t w0 = produced;
+    uint32_t n_runs = 0, q = s;
+    while (true) {  // batches of at most 64 chain headers
+      // lane t: c_t = J^t(s)
+      uint32_t c = s;
+      bool ok = true;
+#pragma unroll 1
+      for (uint32_t r = 0; r < nt; r++) {
+        const uint32_t x = L.J[r][c];
+        const bool take = (lane >> r) & 1u;
+        ok = ok && (!take || x != 0u);
+        c = take ? x : c;
       }
+      ok = ok && lane < (1u << nt);  // nt == 6: every lane
+      const uint64_t vm = __ballot(ok);
+      const uint32_t n = uni((uint32_t)__builtin_popcountll(vm));  // a prefix of the lanes
+      q = uni(rdl(c, n - 1u));
+      const uint32_t nq = uni((uint32_t)L.J[0][q]);
+      // the batch's last header q: a run unless the chain stops at it (slow / past the section)
+      const uint32_t ql = q >> 2, qb = q & 3u;
+      const bool last_run = nq != 0u || (!((rdl(slowm, ql) >> qb) & 1u) && ((rdl(inm, ql) >> qb) & 1u));
+      const uint32_t n_v = last_run ? n : n - 1u;
+      const uint32_t cap = N - produced;
+      uint32_t cc = 0, payload = 0, rend = 0;
+      if (lane < n_v) {
+        const uint32_t e = L.ecnt[c], v = L.eval[c];
+        const bool pk = e >> 31;
+        const uint32_t raw = e & 0x7FFFFFFFu;
+        cc = (!pk && raw == 0u) ? cap : raw;  // Java: currentCount goes negative, the value repeats forever
+        cc = cc < cap ? cc : cap;
+        if (pk) {
+          const uint32_t d = B + v;  // data start
+          const uint64_t e2 = (uint64_t)d + (uint64_t)(raw >> 3) * (uint32_t)w;
+          rend = e2 < (uint64_t)end ? (uint32_t)e2 : end;
+          payload = 0x80000000u | d;
+        } else {
+          payload = v;
+        }
+      }
+      const uint32_t inc = wave_incl_scan_sat(cc, cap);
+      uint32_t st = __shfl_up(inc, 1);
+      if (lane == 0) st = 0;
+      const uint32_t total = uni(rdl(inc, WAVE - 1));
+      const bool em = cc > 0u && st < cap;
+      const uint32_t n_em = uni((uint32_t)__builtin_popcountll(__ballot(em)));
+      if (em) {
+        const uint32_t k = n_runs + lane;
+        L.r_start[k] = produced + st;
+        L.r_pay[k] = payload;
+        L.r_end[k] = rend;
+      }
+      n_runs = uni(n_runs + n_em);
+      produced = uni(produced + total);
+      if (produced >= N || nq == 0u) break;
+      s = nq;  // the chain goes on inside this window: next batch
     }
     wave_sync();
-    if (n_em)
-      expand_level_runs<WB>(L, win, n_em, produced, produced + total, w, out, max_def, count_nonnull, cnt,
-                            produced + total < N);
-    produced += total;
+    if (n_runs) expand_level_runs<WB>(L, win, n_runs, w0, produced, w, out, max_def, count_nonnull, cnt, produced < N);
     if (produced >= N) break;
-    const uint32_t ql = q_last >> 2, qb = q_last & 3u;
+    // continue after the window's last chain header q
+    const uint32_t ql = q >> 2, qb = q & 3u;
     const uint32_t q_slow = (rdl(slowm, ql) >> qb) & 1u;
     const uint32_t q_in = (rdl(inm, ql) >> qb) & 1u;
     if (!q_in) {
-      pos = B + q_last;  // at or past the section end: RLE_PAST_END next
+      pos = B + q;  // at or past the section end: RLE_PAST_END next
     } else if (!q_slow) {
       pos = pick4(nn, qb, ql);  // leaves the window
     } else {
-      // scalar re-decode of the header at q_last (readNext :80-109)
-      pos = B + q_last;
+      // scalar re-decode of the header at q (readNext :80-109)
+      pos = B + q;
       uint32_t hl, m, nxs, vv;
       uint64_t cnt64;
       code = slow_header_g([&](uint32_t p) { return wbyte(win, p); }, pos, end, w, hl, m, cnt64, vv, nxs);
@@ -1521,16 +1529,16 @@ __device__ __forceinline__ uint32_t decode_levels_pj(LevelWaveLds& L, rsrc_t rs,
   return code ? produced : N;
 }
 
-// decode_levels_pj with the tile expansion specialised for the section's bit width.
+// decode_levels_bl with the tile expansion specialised for the section's bit width.
 __device__ __forceinline__ uint32_t decode_levels_w(LevelWaveLds& L, rsrc_t rs, uint32_t beg, uint32_t end, int w,
                                                     uint32_t N, uint8_t* out, uint32_t max_def, bool count_nonnull,
                                                     uint32_t* nonnull, int* err_code) {
   switch (w) {
-    case 1: return decode_levels_pj<1>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 2: return decode_levels_pj<2>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 3: return decode_levels_pj<3>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 4: return decode_levels_pj<4>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
-    default: return decode_levels_pj<0>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
+    case 1: return decode_levels_bl<1>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
+    case 2: return decode_levels_bl<2>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
+    case 3: return decode_levels_bl<3>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
+    case 4: return decode_levels_bl<4>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
+    default: return decode_levels_bl<0>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
   }
 }
 

@@ -1,11 +1,14 @@
 // pqgpu_reader.cpp — the ValuesReader contract over a decoded page batch (include/pqgpu_reader.h).
 //
-// Host code of libpqgpu.so; what the JNI shim's GpuValuesReader does per call. Reference:
+// Host code of libpqgpu.so; what the JNI shim's GpuValuesReader / GpuLevelsReader do per call. Reference:
 // ValuesReader (parquet-column/src/main/java/org/apache/parquet/column/values/ValuesReader.java:36-203)
 // and the readers it dispatches to (PlainValuesReader, BooleanPlainValuesReader,
 // BinaryPlainValuesReader, FixedLenByteArrayPlainValuesReader, DictionaryValuesReader,
 // DeltaBinaryPackingValuesReader, ...): each supports only the read of its type and throws
-// UnsupportedOperationException for the others.
+// UnsupportedOperationException for the others. Level readers: ColumnReaderBase.readPageV1 / readPageV2 /
+// newRLEIterator (parquet-column/src/main/java/org/apache/parquet/column/impl/ColumnReaderBase.java:738-789),
+// RunLengthBitPackingHybridValuesReader (.../values/rle/RunLengthBitPackingHybridValuesReader.java:40-65),
+// ZeroIntegerValuesReader.
 #include <cstdint>
 #include <cstring>
 
@@ -24,8 +27,6 @@ int elem_width(int t, int tl) {
   }
 }
 
-bool starts_with(const char* s, const char* p) { return std::strncmp(s, p, std::strlen(p)) == 0; }
-
 // the next value's index, or the error raised at it
 int take(pqg_values_reader* r, uint64_t* i) {
   if (r->error_code && r->pos >= r->error_at) return r->error_code;
@@ -41,8 +42,8 @@ int take(pqg_values_reader* r, uint64_t* i) {
 extern "C" {
 
 int pqg_vr_init_from_page(pqg_values_reader* r, const pqg_column_desc* col, const pqg_page_desc* pages,
-                          const uint32_t* page_value_counts, int n_pages, int page, int decode_rc,
-                          const pqg_status* decode_status) {
+                          const uint32_t* page_value_counts, int n_pages, int page,
+                          const pqg_page_error* page_errors) {
   if (!r || !col || !pages || !page_value_counts || page < 0 || page >= n_pages) return PQG_ERR_INVALID_ARG;
   std::memset(r, 0, sizeof(*r));
   r->physical_type = col->physical_type;
@@ -53,29 +54,93 @@ int pqg_vr_init_from_page(pqg_values_reader* r, const pqg_column_desc* col, cons
   const int column = pages[page].column;
   uint64_t first = 0;
   for (int p = 0; p < page; p++)
-    if (pages[p].column == column) first += page_value_counts[p];
+    if (pages[p].column == column) {
+      // the column reader threw on an earlier page and reads no further
+      if (page_errors && page_errors[p].code) return page_errors[p].code;
+      first += page_value_counts[p];
+    }
   r->pos = first;
   r->end = first + page_value_counts[page];
-  if (decode_rc != PQG_OK) {
-    const int fp = decode_status ? decode_status->page : -1;
-    // not page-specific (API / device failure), or a page after the batch's first failure: the
-    // batch's outputs beyond that point are not served
-    if (fp < 0 || page > fp) return decode_rc;
-    if (page == fp) {
-      const char* m = decode_status->message;
-      if (starts_with(m, "value decode")) {
+  if (page_errors && page_errors[page].code) {
+    const pqg_page_error& e = page_errors[page];
+    switch (e.phase) {
+      case PQG_PHASE_VALUE:
         // DictionaryValuesReader / DeltaBinaryPackingValuesReader / ...: the reads before the
         // failing value succeed, the failing read throws
-        r->error_code = decode_rc;
-        r->error_at = first + (uint64_t)decode_status->value_index;
-      } else {
-        // "data init" / "level init" / "dictionary page": initFromPage / the dictionary read throws;
-        // "level decode": the column reader throws reading this page's levels
-        return decode_rc;
-      }
+        r->error_code = e.code;
+        r->error_at = first + (uint64_t)e.index;
+        break;
+      case PQG_PHASE_RL_READ:
+      case PQG_PHASE_DL_READ:
+        // the page's values stop at the slots before the level error (page_value_counts)
+        break;
+      default:  // the dictionary (ColumnReaderBase ctor) or an initFromPage threw
+        return e.code;
     }
   }
   return PQG_OK;
+}
+
+int pqg_lr_init_from_page(pqg_levels_reader* r, const pqg_column_desc* col, int kind, const pqg_page_desc* pages,
+                          int n_pages, int page, const pqg_page_error* page_errors) {
+  if (!r || !col || !pages || page < 0 || page >= n_pages || (kind != PQG_LEVELS_REP && kind != PQG_LEVELS_DEF))
+    return PQG_ERR_INVALID_ARG;
+  std::memset(r, 0, sizeof(*r));
+  const bool rep = kind == PQG_LEVELS_REP;
+  r->max_level = rep ? col->max_rep : col->max_def;
+  r->levels = r->max_level > 0 ? (rep ? col->rep_levels : col->def_levels) : nullptr;
+  if (r->max_level > 0 && !r->levels) return PQG_ERR_INVALID_ARG;
+  const int column = pages[page].column;
+  uint64_t first = 0;
+  for (int p = 0; p < page; p++)
+    if (pages[p].column == column) {
+      if (page_errors && page_errors[p].code) return page_errors[p].code;
+      first += pages[p].num_values;
+    }
+  r->pos = first;
+  r->end = first + pages[page].num_values;
+  if (page_errors && page_errors[page].code) {
+    const pqg_page_error& e = page_errors[page];
+    switch (e.phase) {
+      case PQG_PHASE_DICTIONARY:
+      case PQG_PHASE_RL_INIT:  // readPageV1: rl init throws before the dl reader exists
+        return e.code;
+      case PQG_PHASE_DL_INIT:  // rl initialised, dl init throws
+        if (!rep) return e.code;
+        break;
+      case PQG_PHASE_RL_READ:  // rl(s) throws; checkRead never reads dl(s)
+        r->error_code = e.code;
+        r->error_at = first + (uint64_t)e.index;
+        break;
+      case PQG_PHASE_DL_READ:  // rl(s) was read, dl(s) throws
+        r->error_code = e.code;
+        r->error_at = first + (uint64_t)e.index + (rep ? 1u : 0u);
+        break;
+      default:  // DATA_INIT (after both level readers) / VALUE: the levels are served
+        break;
+    }
+  }
+  return PQG_OK;
+}
+
+uint64_t pqg_lr_remaining(const pqg_levels_reader* r) { return r && r->end > r->pos ? r->end - r->pos : 0; }
+
+int pqg_lr_read_integer(pqg_levels_reader* r, int32_t* out) {
+  if (!r || !out) return PQG_ERR_INVALID_ARG;
+  if (r->error_code && r->pos >= r->error_at) return r->error_code;
+  if (r->max_level == 0) {  // ZeroIntegerValuesReader.readInteger / NullIntIterator.nextInt: 0, forever
+    *out = 0;
+    r->pos++;
+    return PQG_OK;
+  }
+  if (r->pos >= r->end) return PQG_ERR_EOF;
+  *out = r->levels[r->pos++];
+  return PQG_OK;
+}
+
+int pqg_lr_skip(pqg_levels_reader* r) {
+  int32_t v;
+  return pqg_lr_read_integer(r, &v);
 }
 
 uint64_t pqg_vr_remaining(const pqg_values_reader* r) { return r && r->end > r->pos ? r->end - r->pos : 0; }

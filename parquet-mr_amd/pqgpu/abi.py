@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # parquet-format Type
 BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY = range(8)
@@ -132,6 +132,24 @@ class Status(C.Structure):
 
     def as_tuple(self):
         return (int(self.code), int(self.page), int(self.value_index))
+
+
+class PageError(C.Structure):
+    """pqg_page_error (pqg_page_errors: every page's own first error)."""
+    _fields_ = [("code", C.c_int32), ("phase", C.c_int32), ("index", C.c_int64)]
+
+
+# pqg_phase
+(PHASE_NONE, PHASE_DICTIONARY, PHASE_RL_INIT, PHASE_DL_INIT, PHASE_DATA_INIT, PHASE_RL_READ, PHASE_DL_READ,
+ PHASE_VALUE) = range(8)
+LEVELS_REP, LEVELS_DEF = 0, 1  # pqg_levels_kind
+
+
+class StagedOutput(C.Structure):
+    """pqg_staged_output."""
+    _fields_ = [("values", C.c_void_p), ("def_levels", C.c_void_p), ("rep_levels", C.c_void_p),
+                ("binary", C.c_void_p), ("n_values", C.c_uint64), ("n_slots", C.c_uint64),
+                ("n_binary", C.c_uint64)]
 
 
 # FieldRepetitionType (pqg_repetition)

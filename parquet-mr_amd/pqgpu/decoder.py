@@ -454,6 +454,58 @@ class Decoder:
             res.append(r)
         return rc, st, res, counts[:batch.n_pages], need
 
+    def page_errors(self, n_pages):
+        """Every page's own first error of the last host / device decode (pqg_page_errors):
+        list of (code, phase, index)."""
+        pe = (abi.PageError * max(1, n_pages))()
+        native.check(native.lib().pqg_page_errors(self.ctx, pe, n_pages), what="pqg_page_errors")
+        return [(int(e.code), int(e.phase), int(e.index)) for e in pe[:n_pages]]
+
+    def decode_staged(self, batch):
+        """The staged host path (pqg_host_input, pqg_decode_staged, pqg_staged_column): the page
+        bytes are written into the library's pinned input, the outputs are read from its pinned
+        output. Returns (rc, status, per-column dict like decode_host, page counts)."""
+        L = native.lib()
+        buf = C.c_void_p()
+        native.check(L.pqg_host_input(self.ctx, batch.data.size, C.byref(buf)), what="pqg_host_input")
+        C.memmove(buf, batch.data.ctypes.data, batch.data.size)
+        descs = (abi.ColumnDesc * max(1, len(batch.columns)))()
+        for i, cd in enumerate(batch.columns):
+            for k, v in cd.items():
+                setattr(descs[i], k, v)
+        counts = np.zeros(max(1, batch.n_pages), dtype=np.uint32)
+        pages = np.ascontiguousarray(batch.pages)
+        st = abi.Status()
+        rc = L.pqg_decode_staged(self.ctx, batch.data.size, C.addressof(descs), len(batch.columns),
+                                 pages.ctypes.data if len(pages) else None, len(pages), counts.ctypes.data, C.byref(st))
+        res = []
+        for i, cd in enumerate(batch.columns):
+            o = abi.StagedOutput()
+            native.check(L.pqg_staged_column(self.ctx, i, C.byref(o)), what="pqg_staged_column")
+            n, ns = int(o.n_values), int(o.n_slots)
+            dt = abi.numpy_dtype(cd["physical_type"], cd["type_length"])
+            if descs[i].flags & abi.COLUMN_DICTIONARY_IDS:
+                dt = np.dtype(np.uint32)
+            binary = cd["physical_type"] == abi.BYTE_ARRAY and dt != np.uint32
+
+            def grab(ptr, count, dtype):
+                a = np.empty(count, dtype=dtype)
+                if count:
+                    L.pqg_copy_out(a.ctypes.data, ptr, a.nbytes)
+                return a
+            r = {"n_values": n,
+                 "def_levels": grab(o.def_levels, ns, np.uint8) if o.def_levels else None,
+                 "rep_levels": grab(o.rep_levels, ns, np.uint8) if o.rep_levels else None}
+            if binary:
+                offs = grab(o.values, n + 1, np.int64)
+                data = grab(o.binary, int(o.n_binary), np.uint8) if o.binary else np.zeros(0, np.uint8)
+                r["offsets"] = offs
+                r["values"] = [data[offs[k]:offs[k + 1]].tobytes() for k in range(n)] if o.binary else []
+            else:
+                r["values"] = grab(o.values, n, dt)
+            res.append(r)
+        return rc, st, res, counts[:batch.n_pages]
+
     # -- record assembly -------------------------------------------------------------
     def assemble(self, path, n_slots, def_levels=None, rep_levels=None):
         """Dremel record assembly of one leaf column (pqg_assemble): `path` = repetitions of the
@@ -566,6 +618,19 @@ class Decoder:
                                           out.ctypes.data)
         native.check(rc, what="pqg_router_read")
         return out[:count]
+
+    def router_read_runs(self, bit_width, data, in_offsets, counts):
+        """Many ParquetReadRouter.read calls in one round trip (pqg_router_read_runs): run r reads
+        counts[r] values at byte in_offsets[r] of `data`; the runs' values back to back."""
+        a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        offs = np.ascontiguousarray(in_offsets, dtype=np.uint64)
+        cnts = np.ascontiguousarray(counts, dtype=np.uint32)
+        out = np.zeros(max(int(cnts.sum()), 1), dtype=np.int32)
+        rc = native.lib().pqg_router_read_runs(self.ctx, bit_width, a.ctypes.data if a.size else None, a.size,
+                                               offs.ctypes.data, cnts.ctypes.data, len(cnts), out.ctypes.data)
+        native.check(rc, what="pqg_router_read_runs")
+        return out[:int(cnts.sum())]
 
     def unpack_runs(self, bit_width, d_in, in_offsets, counts, out_offsets, d_out):
         """Batch of bit-packed runs, all device tensors (pqg_unpack_runs)."""

@@ -17,12 +17,15 @@ EXPORTS = [
     "pqg_abi_version", "pqg_device_count", "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_stream", "pqg_decode",
     "pqg_sync", "pqg_plan_create", "pqg_plan_launch", "pqg_plan_kernel_count", "pqg_plan_timeout_fallbacks", "pqg_plan_plain_fallbacks",
     "pqg_plan_destroy",
-    "pqg_decode_host", "pqg_unpack_runs", "pqg_router_read", "pqg_error_name", "pqg_assemble", "pqg_assemble_schema",
+    "pqg_decode_host", "pqg_unpack_runs", "pqg_router_read", "pqg_router_read_runs", "pqg_error_name",
+    "pqg_page_errors", "pqg_plan_page_errors", "pqg_host_input", "pqg_decode_staged", "pqg_staged_column",
+    "pqg_copy_out", "pqg_assemble", "pqg_assemble_schema",
     "pqg_snappy_decompress", "pqg_snappy_sync", "pqg_zstd_decompress", "pqg_zstd_sync", "pqg_crc32", "pqg_frame_chunk", "pqg_pages_from_headers",
     # include/pqgpu_reader.h (the ValuesReader contract over a decoded batch)
     "pqg_vr_init_from_page", "pqg_vr_remaining", "pqg_vr_read_dictionary_id", "pqg_vr_read_boolean",
     "pqg_vr_read_integer", "pqg_vr_read_long", "pqg_vr_read_float", "pqg_vr_read_double", "pqg_vr_read_bytes",
-    "pqg_vr_skip", "pqg_vr_skip_n", "pqg_java_exception",
+    "pqg_vr_skip", "pqg_vr_skip_n", "pqg_lr_init_from_page", "pqg_lr_remaining", "pqg_lr_read_integer",
+    "pqg_lr_skip", "pqg_java_exception",
 ]
 
 
@@ -64,6 +67,14 @@ def lib():
         L.pqg_decode_host.argtypes = [vp, vp, u64, vp, i32, vp, i32, vp, C.POINTER(abi.Status)]
         L.pqg_unpack_runs.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32]
         L.pqg_router_read.argtypes = [vp, i32, vp, C.c_size_t, i32, vp]
+        L.pqg_router_read_runs.argtypes = [vp, i32, vp, C.c_size_t, vp, vp, i32, vp]
+        L.pqg_page_errors.argtypes = [vp, vp, i32]
+        L.pqg_plan_page_errors.argtypes = [vp, vp, i32]
+        L.pqg_host_input.argtypes = [vp, u64, C.POINTER(vp)]
+        L.pqg_decode_staged.argtypes = [vp, u64, vp, i32, vp, i32, vp, C.POINTER(abi.Status)]
+        L.pqg_staged_column.argtypes = [vp, i32, C.POINTER(abi.StagedOutput)]
+        L.pqg_copy_out.argtypes = [vp, vp, u64]
+        L.pqg_copy_out.restype = None
         L.pqg_assemble.argtypes = [vp, vp, vp, u64, vp, i32, C.POINTER(u64), C.POINTER(abi.Status)]
         L.pqg_assemble_schema.argtypes = [vp, vp, i32, vp, i32, C.POINTER(u64), C.POINTER(abi.Status)]
         L.pqg_snappy_decompress.argtypes = [vp, vp, u64, vp, u64, vp, i32, vp]

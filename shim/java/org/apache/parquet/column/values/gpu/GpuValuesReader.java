@@ -22,16 +22,18 @@ public final class GpuValuesReader extends ValuesReader {
   private final int type;
   private final boolean ids;
   private final long end;
+  private final int errorCode;
   private final long errorAt;
   private long pos;
 
-  GpuValuesReader(GpuPageBatch batch, int column, long first, long end, long errorAt) {
+  GpuValuesReader(GpuPageBatch batch, int column, long first, long end, int errorCode, long errorAt) {
     this.batch = batch;
     this.column = column;
     this.type = batch.physicalType[column];
     this.ids = (batch.flags[column] & PqGpu.COLUMN_DICTIONARY_IDS) != 0;
     this.pos = first;
     this.end = end;
+    this.errorCode = errorCode;
     this.errorAt = errorAt;
   }
 
@@ -46,7 +48,7 @@ public final class GpuValuesReader extends ValuesReader {
   }
 
   private int next() {
-    if (errorAt >= 0 && pos >= errorAt) throw batch.exception(batch.code, "value " + pos + " of column " + column);
+    if (errorAt >= 0 && pos >= errorAt) throw batch.exception(errorCode, "value " + pos + " of column " + column);
     if (pos >= end) throw new ParquetDecodingException("no more values in the page (column " + column + ")");
     return (int) pos++;
   }

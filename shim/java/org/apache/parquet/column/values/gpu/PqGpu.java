@@ -86,14 +86,17 @@ public final class PqGpu {
   }
 
   /**
-   * Decode every page of a batch in one call (pqg_decode_host); pageBytes[position, limit) holds
-   * the bytes the descriptors' offsets refer to. values[i]: long[] / int[] / float[] / double[] /
-   * byte[] (BOOLEAN, FIXED_LEN_BYTE_ARRAY, INT96 row-major) or long[] offsets (n + 1) for BYTE_ARRAY
-   * (binary[i] receives the bytes), int[] for COLUMN_DICTIONARY_IDS columns of any type;
-   * defLevels / repLevels may hold null. pageCounts receives each page's value count. Returns {code,
-   * page, value_index, kind (0 none, 1 value error: lazily at that read, 2 page error: at
-   * initFromPage), values_written[0..nCols)}. Decode errors are returned, not thrown: the readers
-   * throw them where the reference readers would.
+   * Decode every page of a batch in one call (the staged host path: pqg_host_input,
+   * pqg_decode_staged, pqg_staged_column; no Java array is held while the device works);
+   * pageBytes[position, limit) holds the bytes the descriptors' offsets refer to. values[i]: long[] /
+   * int[] / float[] / double[] / byte[] (BOOLEAN, FIXED_LEN_BYTE_ARRAY, INT96 row-major) or long[]
+   * offsets (n + 1) for BYTE_ARRAY (binary[i] receives the bytes), int[] for COLUMN_DICTIONARY_IDS
+   * columns of any type; defLevels[i] / repLevels[i] receive the levels of columns with max level > 0.
+   * An element that is null or too short is replaced by a new array of the exact decoded size (a
+   * wrong element type throws IllegalArgumentException). pageCounts receives each page's value count.
+   * Returns {code, page, value_index, 0, values_written[0..nCols), then per page (code, phase, index)
+   * (pqg_page_errors)}. Decode errors are returned, not thrown: the readers throw them where the
+   * reference readers would (GpuPageBatch).
    */
   public static long[] decodeHost(long ctx, ByteBuffer pageBytes, byte[] pageDescs, byte[] columnDescs, Object[] values,
       byte[][] defLevels, byte[][] repLevels, byte[][] binary, int[] pageCounts) {
@@ -123,6 +126,23 @@ public final class PqGpu {
     routerReadArray(ctx, bitWidth, a, off, in.remaining(), count, out);
   }
 
+  /**
+   * A page's bit-packed runs in one call (pqg_router_read_runs): run r is ParquetReadRouter.read(bitWidth,
+   * in positioned at position() + runOffsets[r], runCounts[r], ...), its values go to out after the
+   * earlier runs' values. One PCIe round trip for the whole batch instead of one per run; a run whose
+   * runCounts[r] * bitWidth / 8 bytes pass the buffer's limit -> EOFException before anything is written.
+   */
+  public static void routerReadBatch(long ctx, int bitWidth, ByteBuffer in, long[] runOffsets, int[] runCounts,
+      int nRuns, int[] out) throws java.io.EOFException {
+    if (in.isDirect()) {
+      routerReadBatchDirect(ctx, bitWidth, in, in.position(), in.remaining(), runOffsets, runCounts, nRuns, out);
+      return;
+    }
+    byte[] a = heapBytes(in);
+    int off = in.hasArray() && !in.isReadOnly() ? in.arrayOffset() + in.position() : 0;
+    routerReadBatchArray(ctx, bitWidth, a, off, in.remaining(), runOffsets, runCounts, nRuns, out);
+  }
+
   /** The backing array of a heap buffer, or a copy of [position, limit) of a read-only one. */
   private static byte[] heapBytes(ByteBuffer b) {
     if (b.hasArray() && !b.isReadOnly()) return b.array();
@@ -149,4 +169,10 @@ public final class PqGpu {
 
   private static native void routerReadArray(long ctx, int bitWidth, byte[] in, int offset, int length, int count,
       int[] out);
+
+  private static native void routerReadBatchDirect(long ctx, int bitWidth, ByteBuffer in, int offset, int length,
+      long[] runOffsets, int[] runCounts, int nRuns, int[] out);
+
+  private static native void routerReadBatchArray(long ctx, int bitWidth, byte[] in, int offset, int length,
+      long[] runOffsets, int[] runCounts, int nRuns, int[] out);
 }

@@ -49,7 +49,7 @@ JNIEXPORT jstring JNICALL Java_org_apache_parquet_column_values_gpu_PqGpu_except
   return c ? (*env)->NewStringUTF(env, c) : NULL;
 }
 
-/* Input bytes of a call: a direct buffer's address, or a byte[] pinned for the call's duration.
+/* Input bytes of a host-only call: a direct buffer's address, or a byte[] pinned for its duration.
  * [offset, offset + length) is what the Java side passes (the buffer's position() .. limit()). */
 typedef struct {
   jbyteArray array;
@@ -67,7 +67,8 @@ static int in_check(JNIEnv* env, jobject direct, jbyteArray array, jint offset, 
   return 1;
 }
 
-/* Pin (array) or address (direct) the input; no other JNI call may follow until in_release. */
+/* Pin (array) or address (direct) the input; no other JNI call may follow until in_release. Used
+ * only around host-side parsing (pqg_frame_chunk: no device call, no waiting). */
 static const uint8_t* in_acquire(JNIEnv* env, jobject direct, jbyteArray array, jint offset, in_bytes* ib) {
   ib->array = array;
   ib->pinned = NULL;
@@ -156,9 +157,63 @@ JNIEXPORT jbyteArray JNICALL Java_org_apache_parquet_column_values_gpu_PqGpu_fra
   return frame_chunk(env, NULL, chunk, offset, length, value_count, verify_crc, codec, chunk_offset, column, dict_info);
 }
 
-/* The output arrays (and a heap input array) stay pinned (GetPrimitiveArrayCritical) for the one
- * pqg_decode_host call: it stages the input into pinned host memory and copies the decoded values
- * straight into the outputs; no JNI call is made while they are pinned. */
+/* Copy the input bytes (direct buffer address or a heap array region) into `dst` without holding
+ * the array: GetByteArrayRegion copies, no critical region. */
+static int copy_in(JNIEnv* env, jobject direct, jbyteArray array, jint offset, jint length, uint8_t* dst) {
+  if (length == 0) return 1;
+  if (direct) {
+    const uint8_t* base = (const uint8_t*)(*env)->GetDirectBufferAddress(env, direct);
+    if (!base) return 0;
+    memcpy(dst, base + offset, (size_t)length);
+    return 1;
+  }
+  (*env)->GetByteArrayRegion(env, array, offset, length, (jbyte*)dst);
+  return !(*env)->ExceptionCheck(env);
+}
+
+/* `arrays[i]` as a primitive array of at least `n` elements of `kind` ('J' long, 'I' int, 'F' float,
+ * 'D' double, 'B' byte): the caller's array when it is long enough, else a new one of exactly n
+ * stored back into arrays[i]. NULL with an exception pending on failure. */
+static jarray out_array(JNIEnv* env, jobjectArray arrays, jsize i, char kind, jsize n) {
+  jarray a = (jarray)(*env)->GetObjectArrayElement(env, arrays, i);
+  if (a) {
+    const char* sig = kind == 'J' ? "[J" : kind == 'I' ? "[I" : kind == 'F' ? "[F" : kind == 'D' ? "[D" : "[B";
+    jclass want = (*env)->FindClass(env, sig);
+    if (!want) return NULL;
+    const jboolean ok = (*env)->IsInstanceOf(env, a, want);
+    (*env)->DeleteLocalRef(env, want);
+    if (!ok) {
+      (*env)->DeleteLocalRef(env, a);
+      throw_code(env, PQG_ERR_INVALID_ARG, "decodeHost: an output array has the wrong element type");
+      return NULL;
+    }
+    if ((*env)->GetArrayLength(env, a) >= n) return a;
+    (*env)->DeleteLocalRef(env, a);
+  }
+  switch (kind) {
+    case 'J': a = (*env)->NewLongArray(env, n); break;
+    case 'I': a = (*env)->NewIntArray(env, n); break;
+    case 'F': a = (*env)->NewFloatArray(env, n); break;
+    case 'D': a = (*env)->NewDoubleArray(env, n); break;
+    default: a = (*env)->NewByteArray(env, n); break;
+  }
+  if (a) (*env)->SetObjectArrayElement(env, arrays, i, a);
+  return a;
+}
+
+/* Copy `bytes` bytes of pinned library memory into a Java array: a critical region around a plain
+ * (multi-threaded) memcpy only — no JNI call, no device call, no waiting inside it. */
+static void copy_out(JNIEnv* env, jarray a, const void* src, uint64_t bytes) {
+  if (!bytes) return;
+  void* dst = (*env)->GetPrimitiveArrayCritical(env, a, NULL);
+  if (!dst) return; /* OutOfMemoryError pending */
+  pqg_copy_out(dst, src, bytes);
+  (*env)->ReleasePrimitiveArrayCritical(env, a, dst, 0);
+}
+
+/* Decode a batch through the staged path: the page bytes are copied into the library's pinned input
+ * (no Java array is held while the device works), decoded, and each output is copied from the
+ * library's pinned output into its Java array afterwards. */
 static jlongArray decode_host(JNIEnv* env, jlong ctx, jobject direct, jbyteArray array, jint offset, jint length,
                               jbyteArray page_descs, jbyteArray column_descs, jobjectArray values,
                               jobjectArray def_levels, jobjectArray rep_levels, jobjectArray binary,
@@ -172,70 +227,96 @@ static jlongArray decode_host(JNIEnv* env, jlong ctx, jobject direct, jbyteArray
     throw_code(env, PQG_ERR_INVALID_ARG, "decodeHost: array arguments shorter than the descriptors");
     return NULL;
   }
-  if ((*env)->EnsureLocalCapacity(env, n_cols * 4 + 16) != 0) return NULL; /* OutOfMemoryError pending */
   pqg_page_desc* pd = (pqg_page_desc*)malloc(sizeof(pqg_page_desc) * (size_t)(n_pages + 1));
   pqg_column_desc* cd = (pqg_column_desc*)malloc(sizeof(pqg_column_desc) * (size_t)(n_cols + 1));
   uint32_t* counts = (uint32_t*)calloc((size_t)n_pages + 1, sizeof(uint32_t));
-  jobject* pinned = (jobject*)calloc((size_t)n_cols * 4 + 1, sizeof(jobject));
-  void** ptrs = (void**)calloc((size_t)n_cols * 4 + 1, sizeof(void*));
-  jlong* res = (jlong*)calloc((size_t)n_cols + 4, sizeof(jlong));
-  if (!pd || !cd || !counts || !pinned || !ptrs || !res) {
-    free(pd); free(cd); free(counts); free(pinned); free(ptrs); free(res);
+  pqg_page_error* pe = (pqg_page_error*)calloc((size_t)n_pages + 1, sizeof(pqg_page_error));
+  const jsize n_res = 4 + n_cols + 3 * n_pages;
+  jlong* res = (jlong*)calloc((size_t)n_res, sizeof(jlong));
+  jlongArray out = NULL;
+  if (!pd || !cd || !counts || !pe || !res) {
     throw_code(env, PQG_ERR_INVALID_ARG, "out of memory");
-    return NULL;
+    goto done;
   }
   (*env)->GetByteArrayRegion(env, page_descs, 0, n_pages * (jsize)sizeof(pqg_page_desc), (jbyte*)pd);
   (*env)->GetByteArrayRegion(env, column_descs, 0, n_cols * (jsize)sizeof(pqg_column_desc), (jbyte*)cd);
-  /* element counts first (GetArrayLength is not allowed inside a critical region) */
-  for (jsize i = 0; i < n_cols; i++) {
-    jobject arrs[4] = {(*env)->GetObjectArrayElement(env, values, i), (*env)->GetObjectArrayElement(env, def_levels, i),
-                       (*env)->GetObjectArrayElement(env, rep_levels, i), (*env)->GetObjectArrayElement(env, binary, i)};
-    for (int a = 0; a < 4; a++) pinned[4 * i + a] = arrs[a];
-    const jsize nv = arrs[0] ? (*env)->GetArrayLength(env, (jarray)arrs[0]) : 0;
-    const jsize nd = arrs[1] ? (*env)->GetArrayLength(env, (jarray)arrs[1]) : 0;
-    const jsize nr = arrs[2] ? (*env)->GetArrayLength(env, (jarray)arrs[2]) : 0;
-    const jsize nb = arrs[3] ? (*env)->GetArrayLength(env, (jarray)arrs[3]) : 0;
-    /* capacity in elements of the output: an ids column's int[] holds one uint32 id per value
-     * whatever the physical type; only the byte[] of FIXED_LEN_BYTE_ARRAY / INT96 values holds
-     * type-length bytes per value */
-    const int ids = (cd[i].flags & PQG_COLUMN_DICTIONARY_IDS) != 0;
-    const int fixed_bytes = !ids && (cd[i].physical_type == PQG_FIXED_LEN_BYTE_ARRAY || cd[i].physical_type == PQG_INT96);
-    const int w = cd[i].physical_type == PQG_INT96 ? 12 : cd[i].type_length;
-    cd[i].values_capacity = fixed_bytes ? (w > 0 ? (uint64_t)nv / (uint64_t)w : 0) : (uint64_t)nv;
-    cd[i].levels_capacity = (uint64_t)(nd > nr ? nd : nr);
-    cd[i].binary_capacity = (uint64_t)nb;
-  }
-  for (jsize j = 0; j < n_cols * 4; j++)
-    ptrs[j] = pinned[j] ? (*env)->GetPrimitiveArrayCritical(env, (jarray)pinned[j], NULL) : NULL;
-  for (jsize i = 0; i < n_cols; i++) {
-    cd[i].values = ptrs[4 * i];
-    cd[i].def_levels = (uint8_t*)ptrs[4 * i + 1];
-    cd[i].rep_levels = (uint8_t*)ptrs[4 * i + 2];
-    cd[i].binary_data = (uint8_t*)ptrs[4 * i + 3];
-  }
+  pqg_ctx* c = (pqg_ctx*)(intptr_t)ctx;
+  uint8_t* in = NULL;
   pqg_status st;
   memset(&st, 0, sizeof(st));
-  in_bytes ib;
-  const uint8_t* bytes = in_acquire(env, direct, array, offset, &ib);
-  const int rc = bytes ? pqg_decode_host((pqg_ctx*)(intptr_t)ctx, bytes, (uint64_t)length, cd, n_cols, pd, n_pages,
-                                         counts, &st)
-                       : PQG_ERR_INVALID_ARG;
-  in_release(env, &ib);
-  for (jsize j = n_cols * 4 - 1; j >= 0; j--)
-    if (ptrs[j]) (*env)->ReleasePrimitiveArrayCritical(env, (jarray)pinned[j], ptrs[j], 0);
+  int rc = pqg_host_input(c, (uint64_t)length, &in);
+  if (rc) {
+    throw_code(env, rc, "pqg_host_input failed");
+    goto done;
+  }
+  if (!copy_in(env, direct, array, offset, length, in)) goto done;
+  rc = pqg_decode_staged(c, (uint64_t)length, cd, n_cols, pd, n_pages, counts, &st);
+  if (rc == PQG_ERR_HIP || rc == PQG_ERR_NO_DEVICE || rc == PQG_ERR_TIMEOUT || (rc == PQG_ERR_INVALID_ARG && st.page == -1)) {
+    throw_code(env, rc, st.message); /* the backend failed or the call was malformed: not a decode error */
+    goto done;
+  }
+  if (rc && pqg_page_errors(c, pe, n_pages) != PQG_OK) {
+    throw_code(env, PQG_ERR_INVALID_ARG, "pqg_page_errors failed");
+    goto done;
+  }
+  for (jsize i = 0; i < n_cols; i++) {
+    pqg_staged_output o;
+    if (pqg_staged_column(c, i, &o) != PQG_OK) {
+      throw_code(env, PQG_ERR_INVALID_ARG, "pqg_staged_column failed");
+      goto done;
+    }
+    const int ids = (cd[i].flags & PQG_COLUMN_DICTIONARY_IDS) != 0;
+    const int t = cd[i].physical_type;
+    char kind = 'B';
+    uint64_t n = o.n_values, w = 1;
+    if (ids) { kind = 'I'; w = 4; }
+    else if (t == PQG_INT32) { kind = 'I'; w = 4; }
+    else if (t == PQG_INT64) { kind = 'J'; w = 8; }
+    else if (t == PQG_FLOAT) { kind = 'F'; w = 4; }
+    else if (t == PQG_DOUBLE) { kind = 'D'; w = 8; }
+    else if (t == PQG_BYTE_ARRAY) { kind = 'J'; w = 8; n = o.n_values + 1; }  /* offsets[n + 1] */
+    else if (t == PQG_INT96) { n = o.n_values * 12; }
+    else if (t == PQG_FIXED_LEN_BYTE_ARRAY) { n = o.n_values * (uint64_t)cd[i].type_length; }
+    if (n > 0x7fffffffull || o.n_slots > 0x7fffffffull || o.n_binary > 0x7fffffffull) {
+      throw_code(env, PQG_ERR_INVALID_ARG, "decodeHost: a column exceeds a Java array");
+      goto done;
+    }
+    jarray a = out_array(env, values, i, kind, (jsize)n);
+    if (!a) goto done;
+    copy_out(env, a, o.values, n * w);
+    (*env)->DeleteLocalRef(env, a);
+    if (o.def_levels) {
+      if (!(a = out_array(env, def_levels, i, 'B', (jsize)o.n_slots))) goto done;
+      copy_out(env, a, o.def_levels, o.n_slots);
+      (*env)->DeleteLocalRef(env, a);
+    }
+    if (o.rep_levels) {
+      if (!(a = out_array(env, rep_levels, i, 'B', (jsize)o.n_slots))) goto done;
+      copy_out(env, a, o.rep_levels, o.n_slots);
+      (*env)->DeleteLocalRef(env, a);
+    }
+    if (o.binary) {
+      if (!(a = out_array(env, binary, i, 'B', (jsize)o.n_binary))) goto done;
+      copy_out(env, a, o.binary, o.n_binary);
+      (*env)->DeleteLocalRef(env, a);
+    }
+    res[4 + i] = (jlong)o.n_values;
+    if ((*env)->ExceptionCheck(env)) goto done;
+  }
   (*env)->SetIntArrayRegion(env, page_counts, 0, n_pages, (const jint*)counts);
-  /* {code, page, value_index, kind, values_written...}: kind 1 = a value error raised lazily at its
-   * read, 2 = a page error raised at initFromPage (pqg_vr_init_from_page's rule) */
+  /* {code, page, value_index, 0, values_written[n_cols], (code, phase, index) per page} */
   res[0] = rc;
   res[1] = rc ? st.page : -1;
   res[2] = rc ? st.value_index : -1;
-  res[3] = rc == 0 ? 0 : strncmp(st.message, "value decode", 12) == 0 ? 1 : 2;
-  for (jsize i = 0; i < n_cols; i++) res[4 + i] = (jlong)cd[i].values_written;
-  jlongArray out = (*env)->NewLongArray(env, n_cols + 4);
-  if (out) (*env)->SetLongArrayRegion(env, out, 0, n_cols + 4, res);
-  if (rc == PQG_ERR_INVALID_ARG && st.page == -1) throw_code(env, rc, st.message); /* capacity: API misuse */
-  else if (rc == PQG_ERR_HIP || rc == PQG_ERR_NO_DEVICE || rc == PQG_ERR_TIMEOUT) throw_code(env, rc, st.message);
-  free(res); free(pd); free(cd); free(counts); free(pinned); free(ptrs);
+  for (jsize p = 0; p < n_pages; p++) {
+    res[4 + n_cols + 3 * p] = pe[p].code;
+    res[4 + n_cols + 3 * p + 1] = pe[p].phase;
+    res[4 + n_cols + 3 * p + 2] = pe[p].index;
+  }
+  out = (*env)->NewLongArray(env, n_res);
+  if (out) (*env)->SetLongArrayRegion(env, out, 0, n_res, res);
+done:
+  free(res); free(pd); free(cd); free(counts); free(pe);
   return out;
 }
 
@@ -257,29 +338,81 @@ JNIEXPORT jlongArray JNICALL Java_org_apache_parquet_column_values_gpu_PqGpu_dec
                      rep_levels, binary, page_counts);
 }
 
-static void router_read(JNIEnv* env, jlong ctx, jint bit_width, jobject direct, jbyteArray array, jint offset,
-                        jint length, jint count, jintArray out) {
-  if (!in_check(env, direct, array, offset, length, "routerRead: bad buffer range")) return;
-  if (count < 0 || (*env)->GetArrayLength(env, out) < count) {
-    throw_code(env, PQG_ERR_INVALID_ARG, "routerRead arguments");
+/* Router reads copy their input in (GetByteArrayRegion / direct address) and their output out
+ * (SetIntArrayRegion): no Java array is held while the device works. */
+static void router_runs(JNIEnv* env, jlong ctx, jint bit_width, jobject direct, jbyteArray array, jint offset,
+                        jint length, const uint64_t* offs, const uint32_t* counts, jint n_runs, jintArray out) {
+  uint64_t total = 0;
+  for (jint r = 0; r < n_runs; r++) total += counts[r];
+  if ((*env)->GetArrayLength(env, out) < (jlong)total) {
+    throw_code(env, PQG_ERR_INVALID_ARG, "routerRead: output array too short");
     return;
   }
-  int32_t* dst = (int32_t*)(*env)->GetPrimitiveArrayCritical(env, out, NULL);
-  in_bytes ib;
-  const uint8_t* bytes = dst ? in_acquire(env, direct, array, offset, &ib) : NULL;
-  const int rc = bytes ? pqg_router_read((pqg_ctx*)(intptr_t)ctx, bit_width, bytes, (size_t)length, count, dst)
-                       : PQG_ERR_INVALID_ARG;
-  if (dst) {
-    in_release(env, &ib);
-    (*env)->ReleasePrimitiveArrayCritical(env, out, dst, 0);
-  }
+  uint8_t* in = (uint8_t*)malloc((size_t)length + 1);
+  int32_t* dst = (int32_t*)malloc(4 * (size_t)total + 4);
+  int rc = in && dst ? PQG_OK : PQG_ERR_INVALID_ARG;
+  if (!rc && !copy_in(env, direct, array, offset, length, in)) rc = -1; /* exception pending */
+  if (!rc) rc = pqg_router_read_runs((pqg_ctx*)(intptr_t)ctx, bit_width, in, (size_t)length, offs, counts, n_runs, dst);
+  if (!rc && total) (*env)->SetIntArrayRegion(env, out, 0, (jsize)total, (const jint*)dst);
+  free(in);
+  free(dst);
   /* SingleBufferInputStream.slice past the end: EOFException; the router declares IOException */
   if (rc == PQG_ERR_EOF) {
     jclass c = (*env)->FindClass(env, "java/io/EOFException");
     if (c) (*env)->ThrowNew(env, c, "routerRead: input shorter than count * bitWidth / 8 bytes");
-  } else if (rc) {
-    throw_code(env, rc, "pqg_router_read failed");
+  } else if (rc > 0) {
+    throw_code(env, rc, "pqg_router_read_runs failed");
   }
+}
+
+static void router_read(JNIEnv* env, jlong ctx, jint bit_width, jobject direct, jbyteArray array, jint offset,
+                        jint length, jint count, jintArray out) {
+  if (!in_check(env, direct, array, offset, length, "routerRead: bad buffer range")) return;
+  if (count < 0) {
+    throw_code(env, PQG_ERR_INVALID_ARG, "routerRead arguments");
+    return;
+  }
+  const uint64_t off0 = 0;
+  const uint32_t cnt = (uint32_t)count;
+  router_runs(env, ctx, bit_width, direct, array, offset, length, &off0, &cnt, 1, out);
+}
+
+static void router_read_batch(JNIEnv* env, jlong ctx, jint bit_width, jobject direct, jbyteArray array, jint offset,
+                              jint length, jlongArray run_offsets, jintArray run_counts, jint n_runs, jintArray out) {
+  if (!in_check(env, direct, array, offset, length, "routerReadBatch: bad buffer range")) return;
+  if (n_runs < 0 || (*env)->GetArrayLength(env, run_offsets) < n_runs ||
+      (*env)->GetArrayLength(env, run_counts) < n_runs) {
+    throw_code(env, PQG_ERR_INVALID_ARG, "routerReadBatch arguments");
+    return;
+  }
+  uint64_t* offs = (uint64_t*)malloc(8 * (size_t)n_runs + 8);
+  uint32_t* counts = (uint32_t*)malloc(4 * (size_t)n_runs + 4);
+  if (offs && counts) {
+    (*env)->GetLongArrayRegion(env, run_offsets, 0, n_runs, (jlong*)offs);
+    (*env)->GetIntArrayRegion(env, run_counts, 0, n_runs, (jint*)counts);
+    int bad = 0;
+    for (jint r = 0; r < n_runs; r++) bad |= (int64_t)offs[r] < 0 || (int32_t)counts[r] < 0;
+    if (bad) throw_code(env, PQG_ERR_INVALID_ARG, "routerReadBatch: negative offset or count");
+    else router_runs(env, ctx, bit_width, direct, array, offset, length, offs, counts, n_runs, out);
+  } else {
+    throw_code(env, PQG_ERR_INVALID_ARG, "out of memory");
+  }
+  free(offs);
+  free(counts);
+}
+
+JNIEXPORT void JNICALL Java_org_apache_parquet_column_values_gpu_PqGpu_routerReadBatchDirect(
+    JNIEnv* env, jclass k, jlong ctx, jint bit_width, jobject in, jint offset, jint length, jlongArray run_offsets,
+    jintArray run_counts, jint n_runs, jintArray out) {
+  (void)k;
+  router_read_batch(env, ctx, bit_width, in, NULL, offset, length, run_offsets, run_counts, n_runs, out);
+}
+
+JNIEXPORT void JNICALL Java_org_apache_parquet_column_values_gpu_PqGpu_routerReadBatchArray(
+    JNIEnv* env, jclass k, jlong ctx, jint bit_width, jbyteArray in, jint offset, jint length, jlongArray run_offsets,
+    jintArray run_counts, jint n_runs, jintArray out) {
+  (void)k;
+  router_read_batch(env, ctx, bit_width, NULL, in, offset, length, run_offsets, run_counts, n_runs, out);
 }
 
 JNIEXPORT void JNICALL Java_org_apache_parquet_column_values_gpu_PqGpu_routerReadDirect(

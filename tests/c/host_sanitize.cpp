@@ -91,25 +91,42 @@ static void read_pages(const pqg_column_desc& col0, const pqg_page_desc* pages, 
   col.binary_data = binary;
   col.binary_capacity = nbin;
   col.values_written = total;
-  pqg_status st;
-  std::memset(&st, 0, sizeof(st));
-  int rc = 0;
+  // exactly-sized level arrays (one byte per slot) for the level readers
+  uint8_t* dl = (uint8_t*)std::malloc(total ? total : 1);
+  uint8_t* rl = (uint8_t*)std::malloc(total ? total : 1);
+  for (uint64_t i = 0; i < total; i++) dl[i] = rl[i] = (uint8_t)(i % 3);
+  col.max_def = col.max_def > 0 ? col.max_def : 2;
+  col.max_rep = col.max_rep > 0 ? col.max_rep : 1;
+  col.def_levels = dl;
+  col.rep_levels = rl;
+  std::vector<pqg_page_error> pe((size_t)np + 1, pqg_page_error{PQG_OK, PQG_PHASE_NONE, -1});
   if (mode == 1 && np > 0) {  // a value error in the middle page
-    rc = PQG_ERR_DICT_ID;
-    st.code = rc;
-    st.page = np / 2;
-    st.value_index = pages[np / 2].num_values / 2;
-    std::snprintf(st.message, sizeof(st.message), "value decode");
+    pe[(size_t)np / 2] = {PQG_ERR_DICT_ID, PQG_PHASE_VALUE, (int64_t)pages[np / 2].num_values / 2};
   } else if (mode == 2 && np > 0) {  // an init error in the last page
-    rc = PQG_ERR_CORRUPT;
-    st.code = rc;
-    st.page = np - 1;
-    st.value_index = 0;
-    std::snprintf(st.message, sizeof(st.message), "data init");
+    pe[(size_t)np - 1] = {PQG_ERR_CORRUPT, PQG_PHASE_DATA_INIT, -1};
+  } else if (mode == 3 && np > 0) {  // a level error in the first page
+    pe[0] = {PQG_ERR_RLE_PAST_END, PQG_PHASE_DL_READ, (int64_t)pages[0].num_values / 3};
   }
+  const pqg_page_error* perr = mode ? pe.data() : nullptr;
   for (int p = 0; p < np; p++) {
+    pqg_levels_reader lr[2];
+    for (int kind = 0; kind < 2; kind++) {
+      if (pqg_lr_init_from_page(&lr[kind], &col, kind, pages, np, p, perr)) {
+        (*errs)++;
+        continue;
+      }
+      for (;;) {  // reads past the page's slots end in EOF
+        int32_t v;
+        if (pqg_lr_read_integer(&lr[kind], &v)) {
+          (*errs)++;
+          break;
+        }
+        (*reads)++;
+      }
+      (void)pqg_lr_remaining(&lr[kind]);
+    }
     pqg_values_reader r;
-    const int irc = pqg_vr_init_from_page(&r, &col, pages, counts.data(), np, p, rc, rc ? &st : nullptr);
+    const int irc = pqg_vr_init_from_page(&r, &col, pages, counts.data(), np, p, perr);
     if (irc) {
       (*errs)++;
       continue;
@@ -127,6 +144,8 @@ static void read_pages(const pqg_column_desc& col0, const pqg_page_desc* pages, 
     (void)pqg_vr_remaining(&r);
     (void)pqg_java_exception(read_one(&r));
   }
+  std::free(dl);
+  std::free(rl);
   std::free(values);
   std::free(binary);
 }
@@ -174,7 +193,7 @@ int main(int argc, char** argv) {
         prc = pqg_pages_from_headers(h, n, hdr[0], 0, 0, &col, pages, pcap, &np, &st);
       }
       if (prc == PQG_OK)
-        for (int mode = 0; mode < 3; mode++) read_pages(col, pages, np, mode, &reads, &errs);
+        for (int mode = 0; mode < 4; mode++) read_pages(col, pages, np, mode, &reads, &errs);
       std::free(pages);
     }
     std::printf("%s frame=%d pages=%d n=%d reads=%" PRIu64 " errs=%" PRIu64 "\n", argv[a], frc, prc, np, reads, errs);

@@ -89,3 +89,37 @@ def test_no_device_fails_loudly():
     from pqgpu import decoder
     with pytest.raises(native.PqgError):
         decoder.Decoder(0)
+
+
+# ---- the JNI glue (shim/) against the C ABI: no JDK in the image, so a compile check and a name check --------
+
+SHIM = os.path.join(REPO, "shim")
+
+
+def test_jni_glue_compiles_against_the_abi():
+    """shim/jni/pqgpu_jni.c compiles warning-free against include/ and a declaration-only jni.h
+    (tests/c/jni_stub/jni.h: the JNI functions the glue calls, with the specification's signatures)."""
+    subprocess.run(["gcc", "-std=c11", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-I",
+                    os.path.join(REPO, "tests", "c", "jni_stub"), "-I", os.path.join(REPO, "include"),
+                    os.path.join(SHIM, "jni", "pqgpu_jni.c")], check=True)
+
+
+def test_every_java_native_has_its_jni_symbol():
+    """Each `native` method of PqGpu.java has the JNIEXPORT function the JVM binds it to
+    (Java_<package>_<class>_<method>), and the glue exports nothing else."""
+    java = open(os.path.join(SHIM, "java", "org", "apache", "parquet", "column", "values", "gpu", "PqGpu.java")).read()
+    natives = set(re.findall(r"\bstatic\s+native\s+[\w\[\]]+\s+(\w+)\s*\(", java))
+    glue = open(os.path.join(SHIM, "jni", "pqgpu_jni.c")).read()
+    exported = set(re.findall(r"Java_org_apache_parquet_column_values_gpu_PqGpu_(\w+)\s*\(", glue))
+    assert natives and natives == exported, (natives ^ exported)
+
+
+def test_java_readers_use_only_declared_batch_members():
+    """The readers call GpuPageBatch members that exist (a name check of the Java sources, which cannot be
+    compiled here)."""
+    d = os.path.join(SHIM, "java", "org", "apache", "parquet", "column", "values", "gpu")
+    batch = open(os.path.join(d, "GpuPageBatch.java")).read()
+    for f in ("GpuValuesReader.java", "GpuLevelsReader.java"):
+        src = open(os.path.join(d, f)).read()
+        for m in set(re.findall(r"\bbatch\.(\w+)", src)):
+            assert re.search(r"\b" + m + r"\b\s*[;(=\[]", batch), (f, m)

@@ -18,36 +18,52 @@ from pqgpu import abi, native, writer
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS_SRC = os.path.join(REPO, "tests", "c", "harness.c")
+ROUTER_SRC = os.path.join(REPO, "tests", "c", "router.c")
+
+
+def _build(tmp_path_factory, src, name):
+    exe = str(tmp_path_factory.mktemp(name) / name)
+    libdir = os.path.dirname(native.LIB_PATH)
+    subprocess.run(["gcc", "-std=c11", "-O1", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(REPO, "include"),
+                    src, "-o", exe, "-L", libdir, "-l:libpqgpu.so", f"-Wl,-rpath,{libdir}"], check=True)
+    return exe
 
 
 @pytest.fixture(scope="module")
 def harness(tmp_path_factory):
-    exe = str(tmp_path_factory.mktemp("harness") / "harness")
-    libdir = os.path.dirname(native.LIB_PATH)
-    subprocess.run(["gcc", "-std=c11", "-O1", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(REPO, "include"),
-                    HARNESS_SRC, "-o", exe, "-L", libdir, "-l:libpqgpu.so", f"-Wl,-rpath,{libdir}"], check=True)
-    return exe
+    return _build(tmp_path_factory, HARNESS_SRC, "harness")
 
 
-def case_file(tmp_path, raw, ptype, num_values, type_length=0, max_def=0, max_rep=0, flags=0, codec=0):
-    p = tmp_path / "case.bin"
+@pytest.fixture(scope="module")
+def router(tmp_path_factory):
+    return _build(tmp_path_factory, ROUTER_SRC, "router")
+
+
+def case_file(tmp_path, raw, ptype, num_values, type_length=0, max_def=0, max_rep=0, flags=0, codec=0, name="case.bin"):
+    p = tmp_path / name
     p.write_bytes(b"PQGC" + struct.pack("<6i", ptype, type_length, max_def, max_rep, flags, codec) +
                   struct.pack("<qQ", num_values, len(raw)) + raw)
     return str(p)
 
 
-def run(harness, case, mode="all"):
-    out = subprocess.run([harness, case, mode], capture_output=True, text=True, timeout=120)
+def run(harness, case, mode="all", more=()):
+    out = subprocess.run([harness, case, mode, *more], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     return out.stdout.splitlines()
 
 
 def parse(lines):
     """-> dict: frame / decode / per-page values / page ends / init errors."""
-    res = {"values": {}, "ends": {}, "init": {}, "pages": {}}
+    res = {"values": {}, "ends": {}, "init": {}, "pages": {}, "levels": {}, "perr": {}, "pagecol": {}}
     for ln in lines:
         f = ln.split()
-        if f[0] == "V":
+        if f[0] == "L":
+            res["levels"].setdefault(int(f[1]), []).append((int(f[2]), int(f[3]), int(f[4])))
+        elif f[0] == "PERR":
+            res["perr"][int(f[1])] = (int(f[2]), int(f[3]), int(f[4]))
+        elif f[0] == "PAGECOL":
+            res["pagecol"][int(f[1])] = int(f[2])
+        elif f[0] == "V":
             res["values"].setdefault(int(f[1]), []).append((int(f[2]), f[3]))
         elif f[0] == "END":
             res["ends"][int(f[1])] = (int(f[2]), f[3])
@@ -129,7 +145,7 @@ def test_exception_mapping():
 # ---- GPU: values through the C reader -----------------------------------------------------
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["all", "skip"])
+@pytest.mark.parametrize("mode", ["all", "skip", "staged"])
 @pytest.mark.parametrize("name,c", required_cases(), ids=lambda x: x if isinstance(x, str) else x["key"])
 def test_harness_reads_fixture_values(harness, tmp_path, name, c, mode):
     ch, expected = fixtures.load_chunk(name, c)
@@ -277,3 +293,224 @@ def test_codec_uncompressed_pages_decode(harness, tmp_path, version):
         assert r["DECODE"][0] == "0"
         got = [int(v) for p in sorted(r["values"]) for _, v in r["values"][p]]
         assert got == vals.tolist()
+
+
+# ---- levels through the boundary (pqg_lr_*), per-column error scoping, the staged path ------------
+
+def _c5_chunk(recs=3000, page_rows=1000, version=1, seed=7):
+    """C5's shape (LIST<optional int64>: rep + def levels, Poisson(3) lists, 10 % null lists /
+    elements), small: the values and the levels the writer wrote."""
+    rng = np.random.default_rng(seed)
+    lens = rng.poisson(3, size=recs)
+    null_list = rng.random(recs) < 0.1
+    slots = np.where(null_list | (lens == 0), 1, lens)
+    starts = np.concatenate([[0], np.cumsum(slots)[:-1]])
+    rl = np.ones(int(slots.sum()), dtype=np.uint8)
+    rl[starts] = 0
+    dl = np.full(rl.size, 3, dtype=np.uint8)
+    dl[rng.random(rl.size) < 0.1] = 2
+    dl[starts[null_list]] = 0
+    dl[starts[~null_list & (lens == 0)]] = 1
+    vals = rng.integers(-2**40, 2**40, size=int((dl == 3).sum()))
+    ch = writer.write_column_chunk(abi.INT64, vals, abi.PLAIN, def_levels=dl, rep_levels=rl, max_def=3, max_rep=1,
+                                   page_rows=page_rows, version=version)
+    return ch, vals, dl, rl
+
+
+def _level_stream(r, pages):
+    """(rep, def) per slot and the values read, in page order, from a levels-mode run."""
+    reps, defs, vals = [], [], []
+    for p in pages:
+        for _, rv, dv in r["levels"].get(p, []):
+            reps.append(rv)
+            defs.append(dv)
+        vals += [v for _, v in r["values"].get(p, [])]
+    return np.array(reps, dtype=np.int64), np.array(defs, dtype=np.int64), vals
+
+
+def _oracle(ch):
+    from oracle import pqref
+    return pqref.decode_batch(writer.build_batch([ch]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key", ["rg0_c2", "rg0_c4", "rg0_c5", "rg1_c4", "rg1_c5"])
+def test_harness_levels_nested_fixture(harness, tmp_path, key):
+    """checkRead's per-slot sequence (rl, dl, the value when dl == maxDl) through the C level and
+    value readers on parquet-mr 1.9.0's nested fixture (phoneNumbers.phone.number / .kind: max
+    rep 1, max def 2 / 3) equals the oracle's levels and values."""
+    name = "test-file-with-no-column-indexes-1"
+    c = next(c for n, c in fixtures.chunk_cases() if n == name and c["key"] == key)
+    ch, expected = fixtures.load_chunk(name, c)
+    ref = _oracle(ch)
+    assert ref.code == 0
+    r = parse(run(harness, case_file(tmp_path, raw_chunk(name, c), ch.physical_type, c["num_values"],
+                                     type_length=ch.type_length, max_def=c["max_def"], max_rep=c["max_rep"]),
+                  "levels"))
+    assert r["DECODE"][0] == "0"
+    reps, defs, vals = _level_stream(r, sorted(r["pages"]))
+    want_d = ref.columns[0]["def_levels"]
+    want_r = ref.columns[0]["rep_levels"]
+    assert np.array_equal(defs, want_d)
+    assert np.array_equal(reps, want_r if want_r is not None else np.zeros_like(defs))
+    assert vals == [fmt(v, ch.physical_type) for v in expected]
+    assert all(e == (0, "-") for e in r["ends"].values())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("version", [1, 2])
+def test_harness_levels_c5_shape(harness, tmp_path, version):
+    ch, vals, dl, rl = _c5_chunk(version=version)
+    r = parse(run(harness, case_file(tmp_path, thrift_compact.chunk_bytes(ch), abi.INT64, int(dl.size),
+                                     max_def=3, max_rep=1), "levels"))
+    assert r["DECODE"][0] == "0"
+    reps, defs, got = _level_stream(r, sorted(r["pages"]))
+    assert np.array_equal(reps, rl) and np.array_equal(defs, dl)
+    assert got == [str(int(v)) for v in vals]
+
+
+def _corrupt_prefix(ch, page, section, cut):
+    """Damage a V1 page's level section (0: rl, 1: dl). dl: its 4-byte length prefix shortened by
+    `cut` (the stream ends early, the data section starts inside it). rl: its last `cut` bytes
+    dropped and the prefix fixed up, so the dl section and the data stay intact behind it."""
+    import copy
+    bad = copy.deepcopy(ch)
+    body = bytearray(bad.pages[page].body)
+    at = 0
+    if section == 1 and bad.max_rep > 0:
+        at = 4 + struct.unpack_from("<i", body, 0)[0]
+    n = struct.unpack_from("<i", body, at)[0]
+    if section == 0:
+        k = max(0, n - cut)
+        body = body[:4 + k] + body[4 + n:]
+        struct.pack_into("<i", body, 0, k)
+    else:
+        struct.pack_into("<i", body, at, max(0, n - cut))
+    bad.pages[page].body = bytes(body)
+    return bad
+
+
+def _find_error(ch, page, section, phases):
+    """A corruption of `page`'s level section for which the oracle fails inside `page` with a
+    phase in `phases`."""
+    for cut in range(1, 64):
+        bad = _corrupt_prefix(ch, page, section, cut)
+        ref = _oracle(bad)
+        if ref.code and ref.status[1] == page and ref.phase in phases:
+            return bad, ref
+    pytest.fail("no corruption found")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("section,phases", [(1, (abi.PHASE_DL_READ,)), (0, (abi.PHASE_RL_READ,))])
+def test_harness_level_error_at_the_oracles_slot(harness, tmp_path, section, phases):
+    """A damaged level section (shortened length prefix) fails at the slot, reader and code where
+    the oracle's checkRead fails; the slots and values before it are served, the column's later
+    pages are not."""
+    ch, vals, dl, rl = _c5_chunk(recs=4000, page_rows=1500)
+    bad, ref = _find_error(ch, 1, section, phases)
+    code, page, idx = ref.status
+    r = parse(run(harness, case_file(tmp_path, thrift_compact.chunk_bytes(bad), abi.INT64, int(dl.size),
+                                     max_def=3, max_rep=1), "levels"))
+    assert r["DECODE"][:3] == [str(code), abi_exc(code), str(page)]
+    assert r["perr"][page][:2] == (code, ref.phase)
+    if ref.phase in (abi.PHASE_RL_READ, abi.PHASE_DL_READ):
+        assert r["perr"][page][2] == idx
+        # slots before the failing one are read, and their values; the failing read raises the code
+        got = r["levels"].get(page, [])
+        assert [s for s, _, _ in got] == list(range(idx))
+        assert r["ends"][page][0] == code
+        first = sum(len(pg_levels) for p, pg_levels in r["levels"].items() if p < page)
+        assert [d for _, _, d in got] == dl[first:first + idx].tolist()
+    else:
+        assert r["init"][page][0] == code
+    for p in range(page + 1, len(bad.pages)):
+        assert r["init"][p][0] == code
+    for p in range(page):
+        assert r["ends"][p] == (0, "-")
+
+
+def abi_exc(code):
+    import ctypes as C
+    L = native.lib()
+    L.pqg_java_exception.restype = C.c_char_p
+    L.pqg_java_exception.argtypes = [C.c_int]
+    e = L.pqg_java_exception(code)
+    return e.decode() if e else "-"
+
+
+@pytest.mark.gpu
+def test_harness_error_stays_in_its_column(harness, tmp_path):
+    """Two columns in one batch: an invalid dictionary id in column 0 fails column 0's readers at
+    that value (and its later pages), column 1 (nested levels + values) reads completely — a
+    ColumnReader fails on its own (ColumnReaderBase.java:590-623)."""
+    rng = np.random.default_rng(9)
+    vals = rng.integers(0, 40, size=30000).astype(np.int64)
+    ch0 = writer.write_column_chunk(abi.INT64, vals, abi.RLE_DICTIONARY, page_rows=10000)
+    ids, _ = writer.dictionary_encode(vals)
+    bad = int(np.argmax(ids >= 35))
+    case0 = case_file(tmp_path, thrift_compact.chunk_bytes(ch0, dict_num_values=35), abi.INT64, len(vals), name="c0")
+    ch1, v1, dl1, rl1 = _c5_chunk(recs=3000, page_rows=1000)
+    case1 = case_file(tmp_path, thrift_compact.chunk_bytes(ch1), abi.INT64, int(dl1.size), max_def=3, max_rep=1,
+                      name="c1")
+    r = parse(run(harness, case0, "levels", [case1]))
+    page, idx = bad // 10000, bad % 10000
+    assert r["DECODE"][:4] == [str(abi.ERR_DICT_ID), "java/lang/ArrayIndexOutOfBoundsException", str(page), str(idx)]
+    col0 = sorted(p for p, c in r["pagecol"].items() if c == 0)
+    col1 = sorted(p for p, c in r["pagecol"].items() if c == 1)
+    assert r["perr"][col0[page]] == (abi.ERR_DICT_ID, abi.PHASE_VALUE, idx)
+    got = r["values"].get(col0[page], [])
+    assert len(got) == idx and all(v == str(int(vals[page * 10000 + k])) for k, v in got)
+    assert r["ends"][col0[page]][0] == abi.ERR_DICT_ID
+    for p in col0[page + 1:]:
+        assert r["init"][p][0] == abi.ERR_DICT_ID
+    reps, defs, got1 = _level_stream(r, col1)
+    assert np.array_equal(reps, rl1) and np.array_equal(defs, dl1)
+    assert got1 == [str(int(v)) for v in v1]
+    assert all(r["ends"][p] == (0, "-") for p in col1)
+
+
+# ---- ParquetReadRouter: a page's runs in one call (pqg_router_read_runs) ----------------------------
+
+def _router_case(tmp_path, w, data, offs, counts):
+    p = tmp_path / "router.bin"
+    p.write_bytes(b"PQGR" + struct.pack("<iiQ", w, len(counts), len(data)) +
+                  np.asarray(offs, dtype="<u8").tobytes() + np.asarray(counts, dtype="<u4").tobytes() + bytes(data))
+    return str(p)
+
+
+def _run_router(router, case, tmp_path):
+    outf = tmp_path / "router.out"
+    out = subprocess.run([router, case, str(outf)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    f = out.stdout.split()
+    return int(f[1]), np.fromfile(str(outf), dtype="<i4")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w", list(range(33)))
+def test_router_batch_matches_oracle(router, tmp_path, w):
+    """Many bit-packed runs of one width in one call, each bit-exact with the oracle's
+    ParquetReadRouter.readBatch (pqr_router_read_batch) at the same position."""
+    from oracle import pqref
+    rng = np.random.default_rng(100 + w)
+    counts = (rng.integers(1, 64, size=60) * 8).astype(np.uint32)
+    gaps = rng.integers(0, 5, size=60)
+    offs, pos = [], 0
+    for c, g in zip(counts, gaps):
+        pos += int(g)
+        offs.append(pos)
+        pos += int(c) * w // 8
+    data = rng.integers(0, 256, size=pos + 3, dtype=np.uint8).tobytes()
+    rc, got = _run_router(router, _router_case(tmp_path, w, data, offs, counts), tmp_path)
+    assert rc == 0
+    want = np.concatenate([pqref.router_read(w, data[o:], int(c))[0] for o, c in zip(offs, counts)])
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_router_batch_eof_writes_nothing(router, tmp_path):
+    """A run whose slice passes the input -> EOF (SingleBufferInputStream.slice) before any unpack."""
+    data = bytes(range(100))
+    rc, _ = _run_router(router, _router_case(tmp_path, 7, data, [0, 60], [8, 48]), tmp_path)
+    assert rc == abi.ERR_EOF

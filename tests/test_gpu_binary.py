@@ -181,6 +181,57 @@ def test_host_path_binary(decoder):
         assert res[i]["values"] == ref.columns[i]["values"]
 
 
+def test_staged_path_equals_host_path(decoder):
+    """The staged host path (library-owned pinned input / output: what the JNI glue uses so that no
+    Java array is held across device work) returns what pqg_decode_host returns: BYTE_ARRAY PLAIN and
+    an expanding dictionary column, an optional int64 DELTA column with levels, and a nested column;
+    then a batch with a value error gives the same status and per-page errors on both paths."""
+    words = [bytes([97 + i % 26]) * (100 + i) for i in range(50)]
+    dl = nulls(30000, 0.2, seed=4)
+    walk = np.cumsum(np.random.default_rng(5).integers(-9, 99, size=int(dl.sum()))).astype(np.int64)
+    rng = np.random.default_rng(6)
+    rl = (rng.random(25000) < 0.7).astype(np.uint8)
+    rl[0] = 0
+    dl2 = np.where(rng.random(25000) < 0.1, 1, 2).astype(np.uint8)
+    chunks = [make(abi.BYTE_ARRAY, _strings(20000, 7), abi.PLAIN),
+              make(abi.BYTE_ARRAY, [words[i % 50] for i in range(20000)], abi.RLE_DICTIONARY),
+              make(abi.INT64, walk, abi.DELTA_BINARY_PACKED, def_levels=dl, max_def=1, version=2, page_rows=7000),
+              make(abi.DOUBLE, rng.standard_normal(int((dl2 == 2).sum())), abi.PLAIN, def_levels=dl2, rep_levels=rl,
+                   max_def=2, max_rep=1, page_rows=6000)]
+    batch = writer.build_batch(chunks)
+    rc, st, res, counts = decoder.decode_host(batch)
+    assert rc == 0, st.message
+    rc2, st2, res2, counts2 = decoder.decode_staged(batch)
+    assert rc2 == 0, st2.message
+    assert np.array_equal(counts, counts2)
+    for a, b, cd in zip(res, res2, batch.columns):
+        assert a["n_values"] == b["n_values"]
+        if cd["physical_type"] == abi.BYTE_ARRAY:
+            assert a["values"] == b["values"] and np.array_equal(a["offsets"], b["offsets"])
+        else:
+            assert np.array_equal(np.asarray(a["values"]).view(np.uint8), np.asarray(b["values"]).view(np.uint8))
+        for k in ("def_levels", "rep_levels"):
+            assert (a[k] is None) == (b[k] is None) and (a[k] is None or np.array_equal(a[k], b[k]))
+    # an invalid dictionary id in the dictionary column's second page: same status, same page errors
+    vals = np.random.default_rng(9).integers(0, 40, size=30000).astype(np.int64)
+    bad = make(abi.INT64, vals, abi.RLE_DICTIONARY, page_rows=10000)
+    bad.dict_num_values = 35
+    ids, _ = writer.dictionary_encode(vals)
+    first_bad = int(np.argmax(ids >= 35))
+    batch = writer.build_batch([chunks[2], bad])
+    rc, st, _, _ = decoder.decode_host(batch)
+    pe = decoder.page_errors(batch.n_pages)
+    rc2, st2, _, _ = decoder.decode_staged(batch)
+    pe2 = decoder.page_errors(batch.n_pages)
+    assert rc == rc2 == abi.ERR_DICT_ID and (st.page, st.value_index) == (st2.page, st2.value_index)
+    assert pe == pe2
+    bad_pages = [p for p, e in enumerate(pe) if e[0]]
+    col_pages = [p for p in range(batch.n_pages) if batch.pages[p]["column"] == 1]
+    assert bad_pages[0] == col_pages[first_bad // 10000]
+    assert pe[bad_pages[0]] == (abi.ERR_DICT_ID, abi.PHASE_VALUE, first_bad % 10000)
+    assert all(pe[p][0] == 0 for p in range(batch.n_pages) if batch.pages[p]["column"] == 0)
+
+
 # ---- DELTA_BYTE_ARRAY (DeltaByteArrayReader) -----------------------------------------------------------------
 
 def _dba_vals(kind, n, seed):
@@ -351,6 +402,29 @@ def test_binary_plain_one_pass_fallback(decoder, one_pass_kernel):
     ch.pages[0].body = ch.pages[0].body + b"\x07\x00\x00\x00abcdefg" + bytes(300)
     plan = _plan_both(decoder, [ch])
     assert plan.plain_fallbacks == 1
+
+
+def test_binary_plain_fallback_two_plans_one_sync(decoder, one_pass_kernel):
+    """pqg_sync checks and repairs every plan launched since the previous sync, not only the last
+    one: plan A (a page with bytes after its values) and plan B launched back to back, one sync."""
+    vals = _strings(20_000, 23, 0, 30)
+    a = make(abi.BYTE_ARRAY, vals, abi.PLAIN, page_rows=10_000)
+    a.pages[0].body = a.pages[0].body + b"\x07\x00\x00\x00abcdefg" + bytes(300)
+    b = make(abi.BYTE_ARRAY, _strings(30_000, 24, 0, 40), abi.PLAIN, page_rows=8000)
+    batches = [writer.build_batch([a]), writer.build_batch([b])]
+    refs = [pqref.decode_batch(x) for x in batches]
+    plans = [decoder.plan(decoder.upload(x)) for x in batches]
+    for p in plans:
+        p.launch()
+    rc, st = plans[1].sync()
+    assert rc == 0, st.message
+    for p, ref in zip(plans, refs):
+        n = ref.columns[0]["n_values"]
+        assert np.array_equal(p.columns[0].offsets().cpu().numpy()[: n + 1], ref.columns[0]["offsets"][: n + 1])
+        assert_same(p.columns[0].numpy(), ref.columns[0]["values"], abi.BYTE_ARRAY)
+    assert plans[0].plain_fallbacks == 1 and plans[1].plain_fallbacks == 0
+    for p in plans:
+        p.close()
 
 
 @pytest.mark.parametrize("lens", ["tile_sized", "tile_minus_4", "spanning", "empty_then_long"])

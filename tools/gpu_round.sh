@@ -3,7 +3,10 @@
 # then separate PMC passes for HBM traffic. Every GPU step has its own time limit and
 # the script stops at the first failure (no retries).
 # Usage (from the repo root, via gpurun): bash tools/gpu_round.sh <tag> [steps...]
-#   steps: tests smoke bench e2e bench2 suite suiteprof prof pmc   (default: tests smoke bench prof pmc)
+#   steps: tests smoke bench e2e bench2 suite suiteprof prof pmc c4 c4prof wlpmc
+#   (default: tests smoke bench prof pmc)
+#   env: SUITE="c3_mixed c5_levels" restricts suite / suiteprof / wlpmc to those workloads;
+#        TESTS="tests/test_x.py ..." restricts the tests step.
 set -euo pipefail
 TAG=${1:-run}; shift || true
 STEPS=${*:-tests smoke bench prof pmc}
@@ -13,7 +16,7 @@ export TMPDIR=/tmp
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+      timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 120 --timeout-method thread \
         > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
       tail -3 "$OUT/pytest_gpu.log" ;;
     smoke)
@@ -33,12 +36,18 @@ for s in $STEPS; do
         || { tail -30 "$OUT/bench_zipf2.err"; exit 1; }
       cat "$OUT/bench_zipf2.json" ;;
     suite)
-      timeout -k 10 900 python -u tools/bench_suite.py > "$OUT/suite.jsonl" 2> "$OUT/suite.err" \
+      timeout -k 10 900 python -u tools/bench_suite.py ${SUITE:-} --cpu-budget 0 > "$OUT/suite.jsonl" 2> "$OUT/suite.err" \
         || { tail -30 "$OUT/suite.err"; exit 1; }
-      cat "$OUT/suite.jsonl" ;;
+      python3 - "$OUT/suite.jsonl" <<'PY'
+import json, sys
+for l in open(sys.argv[1]):
+    d = json.loads(l)
+    print(d["workload"], round(d["ms_per_launch"], 4), "ms", round(d.get("hbm_frac", 0), 3))
+PY
+      ;;
     suiteprof)
       timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/suiteprof" -o run -- \
-        python3 tools/bench_suite.py --cpu-budget 0 > "$OUT/suiteprof.jsonl" 2> "$OUT/suiteprof.err" \
+        python3 tools/bench_suite.py ${SUITE:-} --cpu-budget 0 > "$OUT/suiteprof.jsonl" 2> "$OUT/suiteprof.err" \
         || { tail -30 "$OUT/suiteprof.err"; exit 1; }
       python3 tools/kstats.py "$OUT/suiteprof" ;;
     prof)
@@ -57,9 +66,18 @@ for s in $STEPS; do
         i=$((i+1))
       done
       python3 tools/pmc_summary.py "$OUT/pmc" || true ;;
-    strpmc)
-      # SQ counters per kernel of the string-heavy workloads (separate --pmc passes, 8 SQ each)
-      for wl in str_plain c3_mixed; do
+    c4)
+      timeout -k 10 600 python3 bench.py --workload c4 --rows 125000000 --steps 10 --warmup 2 > "$OUT/bench_c4.json" \
+        2> "$OUT/bench_c4.err" || { tail -30 "$OUT/bench_c4.err"; exit 1; }
+      cat "$OUT/bench_c4.json" ;;
+    c4prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c4prof" -o run -- \
+        python3 bench.py --workload c4 --rows 125000000 --steps 5 --warmup 1 --no-cpu > "$OUT/c4prof.json" \
+        2> "$OUT/c4prof.err" || { tail -30 "$OUT/c4prof.err"; exit 1; }
+      python3 tools/kstats.py "$OUT/c4prof" ;;
+    wlpmc|strpmc)
+      # SQ counters per kernel of the named workloads (separate --pmc passes, 8 SQ each)
+      for wl in ${SUITE:-str_plain c3_mixed}; do
         i=0
         mkdir -p "$OUT/strpmc/$wl"
         for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
