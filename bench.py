@@ -63,7 +63,7 @@ def cpu_baseline_mt(chunk, n_values, threads, budget_s):
     required dictionary column are independent once the dictionary is read; ctypes releases the
     GIL during the C decode)."""
     from concurrent.futures import ThreadPoolExecutor
-    from pqgpu import writer
+    from tools.synth import writer
     sys.path.insert(0, REPO)
     from oracle import pqref
     groups = np.array_split(np.arange(len(chunk.pages)), threads)
@@ -164,7 +164,8 @@ def run_c4(args, world, rank, devi):
     import torch
     import torch.distributed as dist
     import lineitem as LI
-    from pqgpu import abi, decoder as D, dist as pdist, writer
+    from pqgpu import abi, decoder as D, dist as pdist
+    from tools.synth import writer
 
     t_gen = time.perf_counter()
     shard = LI.Shard(args.rows, world, rank, args.c4_templates)
@@ -329,7 +330,8 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from pqgpu import decoder as D, writer
+    from pqgpu import decoder as D
+    from tools.synth import writer
 
     world, rank, local, devi = init_ranks(args)
     if args.workload == "c4":

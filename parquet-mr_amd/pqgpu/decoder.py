@@ -2,7 +2,7 @@
 
 `Decoder` owns one pqg_ctx (one HIP stream) per GPU — the analogue of one
 ColumnReader per thread in parquet-mr (ColumnReaderBase is not thread-safe).
-A `PageBatch` (writer.build_batch, or any caller that lays page bodies out in
+A `PageBatch` (batch.build_batch, or any caller that lays page bodies out in
 one buffer) is uploaded once (`upload`) and decoded into dense device columns:
 values of the non-null slots in slot order plus u8 def / rep levels per slot —
 the same sequence the reference's ValuesReader / ColumnReader return
@@ -16,7 +16,7 @@ import time
 import numpy as np
 import torch
 
-from . import abi, native, writer
+from . import abi, batch, native
 
 
 class DeviceBatch:
@@ -140,14 +140,14 @@ class Decoder:
     def upload(self, batch):
         return DeviceBatch(batch, self.device)
 
-    _CODEC_FN = {writer.SNAPPY: ("pqg_snappy_decompress", "pqg_snappy_sync", "snappy block"),
-                 writer.ZSTD: ("pqg_zstd_decompress", "pqg_zstd_sync", "zstd frame")}
+    _CODEC_FN = {batch.SNAPPY: ("pqg_snappy_decompress", "pqg_snappy_sync", "snappy block"),
+                 batch.ZSTD: ("pqg_zstd_decompress", "pqg_zstd_sync", "zstd frame")}
 
     def upload_chunks(self, chunks):
         """Column chunks whose pages may be SNAPPY- or ZSTD-compressed -> a DeviceBatch of
         uncompressed pages.
 
-        The batch is laid out for the uncompressed pages (writer.build_batch over placeholders of
+        The batch is laid out for the uncompressed pages (batch.build_batch over placeholders of
         the uncompressed sizes), the compressed blocks are uploaded once, and
         pqg_snappy_decompress / pqg_zstd_decompress write every block straight into its page's
         place in the batch on the GPU (ColumnChunkPageReadStore.readPage's decompress step).
@@ -159,7 +159,7 @@ class Decoder:
         for ch in chunks:
             ph = copy.copy(ch)
             ph.pages = []
-            if ch.dict_page is not None and ch.dict_codec != writer.UNCOMPRESSED:
+            if ch.dict_page is not None and ch.dict_codec != batch.UNCOMPRESSED:
                 if ch.dict_codec not in self._CODEC_FN:
                     raise native.PqgError(abi.ERR_UNSUPPORTED, what=f"dictionary page codec {ch.dict_codec}")
                 ph.dict_page = bytes(ch.dict_uncompressed_size)
@@ -170,12 +170,12 @@ class Decoder:
                     lv = pg.rl_byte_length + pg.dl_byte_length if pg.version == 2 else 0
                     q.body = pg.body[:lv] + bytes(pg.uncompressed_size - lv)
                     blocks.append((pg.codec, pg.body[lv:], ("page", n_page), lv))
-                elif pg.codec != writer.UNCOMPRESSED:
+                elif pg.codec != batch.UNCOMPRESSED:
                     raise native.PqgError(abi.ERR_UNSUPPORTED, what=f"page codec {pg.codec}")
                 ph.pages.append(q)
                 n_page += 1
             placeholders.append(ph)
-        batch = writer.build_batch(placeholders)
+        batch = batch.build_batch(placeholders)
         dbatch = DeviceBatch(batch, self.device)
         if not blocks:
             return dbatch

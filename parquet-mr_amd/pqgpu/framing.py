@@ -7,7 +7,7 @@ Thrift TCompactProtocol). Chunks are UNCOMPRESSED, SNAPPY or ZSTD (ColumnMetaDat
 compressed pages keep their compressed bodies (codec / uncompressed_size on the Page) and are
 decompressed on the GPU by Decoder.upload_chunks (pqg_snappy_decompress / pqg_zstd_decompress).
 The C-ABI form of the same walk is pqg_frame_chunk (frame_chunk_native below). The result is a
-writer.ColumnChunk whose pages feed writer.build_batch -> the device decoder.
+batch.ColumnChunk whose pages feed batch.build_batch -> the device decoder.
 
 This is host-side metadata handling (headers, offsets); no page data is decoded
 here.
@@ -15,7 +15,7 @@ here.
 import struct
 
 from . import abi
-from .writer import ColumnChunk, Page
+from .batch import ColumnChunk, Page
 
 # PageType (parquet.thrift)
 DATA_PAGE, INDEX_PAGE, DICTIONARY_PAGE, DATA_PAGE_V2 = 0, 1, 2, 3

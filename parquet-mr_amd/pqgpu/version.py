@@ -5,7 +5,7 @@ Restates parquet-mr's CorruptDeltaByteArrays.requiresSequentialReads
 VersionParser.parse (parquet-common/src/main/java/org/apache/parquet/VersionParser.java, FORMAT) and
 SemanticVersion.parse / compareTo (parquet-common/.../SemanticVersion.java:39-160). A True answer means
 the chunk's DELTA_BYTE_ARRAY pages after its first are flagged PQG_PAGE_DBA_CARRY
-(writer.ColumnChunk.dba_carry)."""
+(batch.ColumnChunk.dba_carry)."""
 import re
 
 from . import abi

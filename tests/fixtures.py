@@ -4,7 +4,8 @@ import os
 
 import numpy as np
 
-from pqgpu import abi, framing, writer
+from pqgpu import abi, framing
+from tools.synth import writer
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 

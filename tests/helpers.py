@@ -1,7 +1,8 @@
 """Shared test-input builders (synthetic columns in the shapes of BASELINE.json's configs)."""
 import numpy as np
 
-from pqgpu import abi, writer
+from pqgpu import abi
+from tools.synth import writer
 
 
 def zipf_dict_column(n, card=1000, a=1.5, seed=0, physical_type=abi.INT64, max_run=4096):

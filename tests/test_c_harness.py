@@ -14,7 +14,8 @@ import pytest
 
 import fixtures
 import thrift_compact
-from pqgpu import abi, native, writer
+from pqgpu import abi, native
+from tools.synth import writer
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS_SRC = os.path.join(REPO, "tests", "c", "harness.c")

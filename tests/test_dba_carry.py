@@ -12,7 +12,8 @@ import numpy as np
 import pytest
 
 from oracle import pqref
-from pqgpu import abi, writer
+from pqgpu import abi
+from tools.synth import writer
 from pqgpu.version import requires_sequential_reads
 
 from helpers import assert_same

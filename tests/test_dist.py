@@ -10,7 +10,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from pqgpu import abi, dist as pdist, writer
+from pqgpu import abi, dist as pdist
+from tools.synth import writer
 
 
 def _free_port():

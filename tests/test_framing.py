@@ -12,7 +12,8 @@ import numpy as np
 import pytest
 
 import fixtures
-from pqgpu import abi, framing, native, writer
+from pqgpu import abi, framing, native
+from tools.synth import writer
 from thrift_compact import page_header
 
 

@@ -7,7 +7,8 @@ import torch
 
 from oracle import assembly as A
 from oracle import pqref
-from pqgpu import abi, writer
+from pqgpu import abi
+from tools.synth import writer
 
 from test_oracle_assembly import PAPER, stripes
 

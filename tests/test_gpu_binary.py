@@ -7,7 +7,8 @@ import numpy as np
 import pytest
 
 from oracle import pqref
-from pqgpu import abi, writer
+from pqgpu import abi
+from tools.synth import writer
 
 from helpers import make, nulls, zipf_dict_column
 from test_gpu_parity import assert_same, run_both
@@ -264,7 +265,7 @@ def test_delta_byte_array_optional(decoder, version, null_frac):
 
 
 def _dba_err(which):
-    from pqgpu import writer as W
+    from tools.synth import writer as W
     if which == "prefix_too_long":   # prefix > previous.length (arraycopy IndexOutOfBounds)
         body = W.delta_encode(np.array([0, 9], dtype=np.int32), abi.INT32) + W.dlba_encode([b"abc", b"x"])
     elif which == "suffix_short":    # suffix bytes missing: "Failed to read N bytes"
@@ -296,7 +297,7 @@ def test_delta_byte_array_mixed_pages(decoder):
 def test_delta_byte_array_error_mid_page(decoder, at):
     """An invalid prefix length (longer than the previous value) inside a page of several
     256-value chunks: values before it decode, the error is reported at its index."""
-    from pqgpu import writer as W
+    from tools.synth import writer as W
     vals = _dba_vals("urls", 1280, 9)
     pre = [0] + [len(os.path.commonprefix([vals[i - 1], vals[i]])) for i in range(1, len(vals))]
     pre[at] = len(vals[at - 1]) + 5

@@ -12,7 +12,8 @@ import pytest
 import torch
 
 from oracle import pqref
-from pqgpu import abi, writer
+from pqgpu import abi
+from tools.synth import writer
 
 from helpers import make, zipf_dict_column
 

@@ -56,7 +56,8 @@ def test_gpu_decodes_raw_chunk_bytes(decoder):
     import os
 
     import fixtures
-    from pqgpu import framing, native, writer
+    from pqgpu import framing, native
+    from tools.synth import writer
     L = native.lib()
     pieces, descs, columns, slots, exp, ptypes = [], [], [], [], [], []
     pos = 0

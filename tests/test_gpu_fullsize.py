@@ -22,7 +22,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 
 import workloads as WL  # noqa: E402
-from pqgpu import abi, writer  # noqa: E402
+from pqgpu import abi  # noqa: E402
+from tools.synth import writer  # noqa: E402
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
 

@@ -8,7 +8,8 @@ import numpy as np
 import pytest
 
 from oracle import pqref
-from pqgpu import abi, writer
+from pqgpu import abi
+from tools.synth import writer
 
 from helpers import assert_same, make, nulls, zipf_dict_column
 

@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 
 from oracle import pqref
-from pqgpu import abi, writer
+from pqgpu import abi
+from tools.synth import writer
 
 from fixtures import batch_of, chunk_cases, decompressed_on_host, is_compressed, load_chunk
 from helpers import assert_same

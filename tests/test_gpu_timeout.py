@@ -24,7 +24,8 @@ import json, sys
 import numpy as np, torch
 sys.path[:0] = [sys.argv[1] + "/parquet-mr_amd", sys.argv[1] + "/tools", sys.argv[1]]
 import workloads as WL
-from pqgpu import decoder as D, native, writer
+from pqgpu import decoder as D, native
+from tools.synth import writer
 assert native.LIB_PATH.endswith("libpqgpu_faultinject.so"), native.LIB_PATH
 out = {}
 chunk, dict_vals, ids = WL.make_c2(2_000_000, 42, 43, 1.5, 1000, 4096, 20000)

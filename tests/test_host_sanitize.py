@@ -17,7 +17,8 @@ import numpy as np
 
 import fixtures
 import thrift_compact
-from pqgpu import abi, writer
+from pqgpu import abi
+from tools.synth import writer
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "parquet-mr_amd", "csrc")

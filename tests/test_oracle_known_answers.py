@@ -9,7 +9,8 @@ import pytest
 
 from javarandom import JavaRandom
 from oracle import pqref
-from pqgpu import abi, writer
+from pqgpu import abi
+from tools.synth import writer
 
 
 def uvarint(v):

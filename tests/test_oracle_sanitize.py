@@ -11,7 +11,8 @@ import numpy as np
 import pytest
 
 import fixtures
-from pqgpu import abi, writer
+from pqgpu import abi
+from tools.synth import writer
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE = os.path.join(REPO, "oracle")

@@ -31,7 +31,8 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "parquet-mr_amd"), REPO]
 
-from pqgpu import abi, writer  # noqa: E402
+from pqgpu import abi  # noqa: E402
+from tools.synth import writer  # noqa: E402
 
 sys.path.insert(0, os.path.join(REPO, "tools"))
 import workloads as WL  # noqa: E402

@@ -1,7 +1,8 @@
 import sys, numpy as np
 sys.path.insert(0,"tests"); sys.path.insert(0,"parquet-mr_amd"); sys.path.insert(0,".")
 from fixtures import chunk_cases, load_chunk
-from pqgpu import abi, writer, decoder as D
+from pqgpu import abi, decoder as D
+from tools.synth import writer
 CASES=list(chunk_cases())
 chunks=[];exps=[];names=[]
 for name,c in CASES:

@@ -9,7 +9,8 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "parquet-mr_amd"), REPO]
 import torch  # noqa: E402
-from pqgpu import abi, decoder as D, writer  # noqa: E402
+from pqgpu import abi, decoder as D  # noqa: E402
+from tools.synth import writer  # noqa: E402
 
 dec = D.Decoder(0)
 for (lo, hi, rows, page_rows) in [(0, 0, 4_000_000, 20000), (4, 32, 4_000_000, 20000), (100, 200, 1_000_000, 5000),

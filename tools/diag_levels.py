@@ -8,7 +8,8 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "parquet-mr_amd"), REPO]
 import torch  # noqa: E402
-from pqgpu import abi, decoder as D, writer  # noqa: E402
+from pqgpu import abi, decoder as D  # noqa: E402
+from tools.synth import writer  # noqa: E402
 
 dec = D.Decoder(0)
 rows = 20_000_000

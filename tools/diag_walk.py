@@ -14,7 +14,8 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from pqgpu import decoder as D, native, writer  # noqa: E402
+from pqgpu import decoder as D, native  # noqa: E402
+from tools.synth import writer  # noqa: E402
 
 zipf = float(sys.argv[1]) if len(sys.argv) > 1 else 1.5
 out = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/diag_walk.json"

@@ -25,7 +25,8 @@ row groups and lay them out repeatedly (the decode of each copy is independent w
 """
 import numpy as np
 
-from pqgpu import abi, writer
+from pqgpu import abi
+from tools.synth import writer
 from workloads import Expected, Workload, binary_take
 
 COLUMNS = [

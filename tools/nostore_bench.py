@@ -10,7 +10,8 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from pqgpu import decoder as D, native, writer  # noqa: E402
+from pqgpu import decoder as D, native  # noqa: E402
+from tools.synth import writer  # noqa: E402
 
 nostore = len(sys.argv) > 1 and sys.argv[1] == "nostore"
 chunk, dv, ids = bench.make_c2(100_000_000)

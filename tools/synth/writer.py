@@ -15,7 +15,8 @@ way parquet-mr's column writers do:
     RLE/bit-packed ids (DictionaryValuesWriter.getBytes :159-186); dictionary
     page = PLAIN values.
 
-The writer is input synthesis only; it is not part of the decode path.
+The writer is input synthesis only; it is not part of the decode path (the page-batch layout the
+decoder uploads is pqgpu.batch, re-exported here for the tests and tools).
 """
 import ctypes as C
 import os
@@ -24,7 +25,9 @@ from typing import List, Optional
 
 import numpy as np
 
-from . import abi
+from pqgpu import abi
+from pqgpu.batch import (ALIGN, PAD, SNAPPY, UNCOMPRESSED, ZSTD, ColumnChunk, Page, PageBatch,  # noqa: F401
+                          build_batch)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
@@ -34,7 +37,7 @@ def _lib():
     global _LIB
     if _LIB is None:
         # input synthesis only (the restated parquet-mr encoders), built outside the product package
-        path = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "tools", "synth", "libpqwriter.so")
+        path = os.path.join(_HERE, "libpqwriter.so")
         if not os.path.exists(path):
             raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
         lib = C.CDLL(path)
@@ -224,51 +227,6 @@ def dictionary_encode(values):
     return ids, uniq[order]
 
 
-@dataclass
-class Page:
-    body: bytes
-    num_values: int
-    encoding: int
-    version: int = 1
-    rl_encoding: int = abi.RLE
-    dl_encoding: int = abi.RLE
-    rl_byte_length: int = 0
-    dl_byte_length: int = 0
-    num_nulls: int = 0
-    num_rows: int = 0
-    # page codec (parquet CompressionCodec: 0 UNCOMPRESSED, 1 SNAPPY). A compressed V1 body is
-    # one Snappy block of the whole page; a compressed V2 body is the level sections as they
-    # are, then one Snappy block of the data section. uncompressed_size: the header's
-    # uncompressed_page_size (V2: levels included).
-    codec: int = 0
-    uncompressed_size: int = 0
-
-
-@dataclass
-class ColumnChunk:
-    physical_type: int
-    max_rep: int = 0
-    max_def: int = 0
-    type_length: int = 0
-    pages: List[Page] = field(default_factory=list)
-    dict_page: Optional[bytes] = None
-    dict_num_values: int = 0
-    dict_encoding: int = abi.PLAIN
-    dict_codec: int = 0               # codec of the dictionary page (its uncompressed size below)
-    dict_uncompressed_size: int = 0
-    # expected decode (what the reference reader returns), for tests
-    values: Optional[object] = None
-    def_levels: Optional[np.ndarray] = None
-    rep_levels: Optional[np.ndarray] = None
-    # CorruptDeltaByteArrays.requiresSequentialReads(created_by, DELTA_BYTE_ARRAY): build_batch flags
-    # the chunk's DELTA_BYTE_ARRAY pages after its first page PQG_PAGE_DBA_CARRY
-    dba_carry: bool = False
-
-    @property
-    def num_slots(self):
-        return sum(p.num_values for p in self.pages)
-
-
 def be_pack(values, bit_width):
     """Deprecated BIT_PACKED level encoding (BitPacking / Packer.BIG_ENDIAN): MSB-first bit
     stream, ceil(n * w / 8) bytes."""
@@ -405,93 +363,6 @@ def first_appearance_ids(ids):
     remap = np.empty(int(ids.max()) + 1 if ids.size else 1, dtype=np.int32)
     remap[order] = np.arange(order.size, dtype=np.int32)
     return remap[ids], order
-
-
-@dataclass
-class PageBatch:
-    """All pages of several column chunks in one byte buffer + descriptor tables."""
-    data: np.ndarray            # uint8, padded
-    pages: np.ndarray           # PAGE_DTYPE
-    columns: List[dict]         # pqg_column_desc fields without output pointers
-    chunks: List[ColumnChunk]
-    page_slot_offsets: np.ndarray  # per page: first slot within its column
-    column_slots: List[int]
-    column_values: List[int]
-
-    @property
-    def n_pages(self):
-        return len(self.pages)
-
-
-ALIGN = 16
-PAD = 256
-
-
-def build_batch(chunks, align=ALIGN):
-    """Lay chunks out in one buffer (each page 16-B aligned), build the descriptor tables.
-
-    Several chunks may belong to the same output column (row groups of one column):
-    pass `column_of` on the chunk objects via attribute `column_index` to merge.
-    """
-    pieces = []
-    pos = 0
-
-    def place(b):
-        nonlocal pos
-        off = (pos + align - 1) // align * align
-        pieces.append((off, b))
-        pos = off + len(b)
-        return off
-
-    # output columns: chunks with the same column_index share one output column
-    col_index = []
-    columns = []
-    seen = {}
-    for i, ch in enumerate(chunks):
-        key = getattr(ch, "column_index", i)
-        if key not in seen:
-            seen[key] = len(columns)
-            columns.append(None)
-        col_index.append(seen[key])
-    page_rows = []
-    slot_off = []
-    col_slots = [0] * len(columns)
-    col_vals = [0] * len(columns)
-    dict_info = {}
-    for ci, ch in enumerate(chunks):
-        oc = col_index[ci]
-        doff = -1
-        if ch.dict_page is not None:
-            doff = place(ch.dict_page)
-        dict_info.setdefault(oc, []).append(doff)
-        if columns[oc] is None:
-            columns[oc] = dict(physical_type=ch.physical_type, type_length=ch.type_length, max_rep=ch.max_rep,
-                               max_def=ch.max_def, dict_offset=doff,
-                               dict_size=len(ch.dict_page) if ch.dict_page is not None else 0,
-                               dict_num_values=ch.dict_num_values, dict_encoding=ch.dict_encoding)
-        elif ch.dict_page is not None:
-            raise ValueError("a pqg_column_desc has one dictionary: decode row groups with separate "
-                             "dictionaries as separate columns (one per row group)")
-        for k, pg in enumerate(ch.pages):
-            off = place(pg.body)
-            carry = abi.PAGE_DBA_CARRY if (getattr(ch, "dba_carry", False) and k > 0 and
-                                           pg.encoding == abi.DELTA_BYTE_ARRAY) else 0
-            page_rows.append((off, len(pg.body), pg.num_values, oc, pg.version, pg.encoding, pg.rl_encoding,
-                              pg.dl_encoding, pg.rl_byte_length, pg.dl_byte_length, carry))
-            slot_off.append(col_slots[oc])
-            col_slots[oc] += pg.num_values
-        col_vals[oc] += len(ch.values) if ch.values is not None else getattr(ch, "n_values_hint", 0)
-    total = pos + PAD
-    data = np.zeros((total + align - 1) // align * align, dtype=np.uint8)
-    for off, b in pieces:
-        data[off:off + len(b)] = np.frombuffer(b, dtype=np.uint8)
-    pages = np.array(page_rows, dtype=abi.PAGE_DTYPE) if page_rows else np.zeros(0, dtype=abi.PAGE_DTYPE)
-    return PageBatch(data=data, pages=pages, columns=columns, chunks=list(chunks),
-                     page_slot_offsets=np.array(slot_off, dtype=np.int64), column_slots=col_slots,
-                     column_values=col_vals)
-
-
-UNCOMPRESSED, SNAPPY, ZSTD = 0, 1, 6   # parquet.thrift CompressionCodec
 
 
 def snappy_chunk(chunk):

@@ -25,7 +25,8 @@ for _p in (os.path.join(REPO, "parquet-mr_amd"), REPO):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-from pqgpu import abi, writer  # noqa: E402
+from pqgpu import abi  # noqa: E402
+from tools.synth import writer  # noqa: E402
 
 
 @dataclass
