@@ -214,6 +214,20 @@ int pqg_ctx_destroy(pqg_ctx* ctx);
 /* The hipStream_t the ctx launches on. */
 void* pqg_ctx_stream(pqg_ctx* ctx);
 
+/* Kernel-choice overrides for plans created on the ctx afterwards (tests and A/B measurements;
+ * the defaults are the measured choices). Decoded results are the same under every setting.
+ *   PQG_DISPATCH_PLAIN_ONE_PASS  PLAIN-only BYTE_ARRAY columns: 0 = per-value path (walk, offset
+ *                                scan, copy), 2 = one pass, tiles below 4,096 PLAIN pages and one
+ *                                wave per page from there (default), 3 = one pass, one wave per page
+ *   PQG_DISPATCH_DICT_DIRECT     dictionary BYTE_ARRAY columns with small dictionaries: 1 = ids
+ *                                mapped straight to lengths and bytes (default), 0 = ids, then map
+ * Returns PQG_ERR_INVALID_ARG for an unknown key or value. Not thread-safe (like the ctx). */
+enum pqg_dispatch {
+  PQG_DISPATCH_PLAIN_ONE_PASS = 1,
+  PQG_DISPATCH_DICT_DIRECT = 2
+};
+int pqg_ctx_set_dispatch(pqg_ctx* ctx, int key, int value);
+
 /* ---- device-resident batch decode ----------------------------------------
  * `d_bytes` is a 4-byte aligned DEVICE buffer holding every page body (and
  * dictionary page) the descriptors refer to, padded by at least 64 readable

@@ -197,6 +197,9 @@ struct pqg_ctx {
   // stream only waits while they run (a queue shared with it costs nothing then).
   hipStream_t fix_stream = nullptr;
   hipEvent_t ev_join_fix = nullptr;
+  // pqg_ctx_set_dispatch: kernel-choice overrides for the plans created on this ctx
+  int plain_mode = 2;       // PQG_DISPATCH_PLAIN_ONE_PASS
+  bool dict_direct = true;  // PQG_DISPATCH_DICT_DIRECT
 };
 
 extern "C" {
@@ -257,6 +260,21 @@ int pqg_ctx_create(int device, void* hip_stream, pqg_ctx** out) {
 }
 
 void* pqg_ctx_stream(pqg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int pqg_ctx_set_dispatch(pqg_ctx* ctx, int key, int value) {
+  if (!ctx) return PQG_ERR_INVALID_ARG;
+  switch (key) {
+    case PQG_DISPATCH_PLAIN_ONE_PASS:
+      if (value != 0 && value != 2 && value != 3) return PQG_ERR_INVALID_ARG;
+      ctx->plain_mode = value;
+      return PQG_OK;
+    case PQG_DISPATCH_DICT_DIRECT:
+      if (value != 0 && value != 1) return PQG_ERR_INVALID_ARG;
+      ctx->dict_direct = value != 0;
+      return PQG_OK;
+    default: return PQG_ERR_INVALID_ARG;
+  }
+}
 
 int pqg_plan_destroy(pqg_plan* p);
 
@@ -529,10 +547,9 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   // one pass: k_bin_bases + k_bin_plain over 2 KiB tiles of their pages when the plan has fewer than
   // BW_SEG_MAX_PAGES PLAIN pages, k_bin_plain_pg (one wave per page, which fills the chip) with more
   // (there the tiles measured slower than the per-value walk + copy: C3 10.4 vs 6.4 ms, profiles/r03/plain_ab)
-  // PQGPU_PLAIN_PG overrides the choice (tests and A/B): 0 = no one-pass path (every plan per value),
-  // 3 = every plan one wave per page
-  int plain_mode = 2;
-  if (const char* ev = getenv("PQGPU_PLAIN_PG")) plain_mode = atoi(ev);
+  // pqg_ctx_set_dispatch(PQG_DISPATCH_PLAIN_ONE_PASS) overrides the choice (tests and A/B): 0 = no
+  // one-pass path (every plan per value), 3 = every plan one wave per page
+  const int plain_mode = ctx->plain_mode;
   const bool many_plain = cls_lists[C_BINP].size() >= pqg::BW_SEG_MAX_PAGES || plain_mode == 3;
   P->plain_pg = many_plain;
   std::vector<uint8_t> plain_col((size_t)std::max(n_cols, 1), 0);
@@ -636,7 +653,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
                                !col_err[(size_t)i] && !dba_fixed[(size_t)i] && !plain_col[(size_t)i] &&
                                cols[i].max_def == 0 && cols[i].max_rep == 0 && cols[i].dict_offset >= 0 &&
                                cols[i].dict_size <= pqg::DD_DICT_MAX && npg[(size_t)i] > 0 &&
-                               nids[(size_t)i] == npg[(size_t)i] && getenv("PQGPU_NO_DICT_DIRECT") == nullptr;
+                               nids[(size_t)i] == npg[(size_t)i] && ctx->dict_direct;
   }
   std::vector<uint64_t> plain_chunks;  // copy chunks of the one-pass columns (per-value fallback only)
   for (int k : {C_IDS, C_BINP, C_DLBA})

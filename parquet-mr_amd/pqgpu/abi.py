@@ -212,3 +212,7 @@ def numpy_dtype(physical_type, type_length=0):
     if physical_type == BYTE_ARRAY:
         return np.dtype("<i8")  # offsets
     return np.dtype((np.void, elem_width(physical_type, type_length)))
+
+# pqg_ctx_set_dispatch keys (include/pqgpu.h enum pqg_dispatch)
+DISPATCH_PLAIN_ONE_PASS = 1
+DISPATCH_DICT_DIRECT = 2

@@ -125,6 +125,10 @@ class Decoder:
         native.check(L.pqg_ctx_create(device, C.c_void_p(stream.cuda_stream), C.byref(h)), what="pqg_ctx_create")
         self.ctx = h
 
+    def set_dispatch(self, key, value):
+        """pqg_ctx_set_dispatch: kernel-choice override for plans created afterwards (abi.DISPATCH_*)."""
+        native.check(native.lib().pqg_ctx_set_dispatch(self.ctx, int(key), int(value)), what="pqg_ctx_set_dispatch")
+
     def close(self):
         if self.ctx:
             native.lib().pqg_ctx_destroy(self.ctx)

@@ -14,7 +14,8 @@ LIB_PATH = os.environ.get("PQGPU_LIB") or os.path.join(_HERE, "libpqgpu.so")
 _LIB = None
 
 EXPORTS = [
-    "pqg_abi_version", "pqg_device_count", "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_stream", "pqg_decode",
+    "pqg_abi_version", "pqg_device_count", "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_stream", "pqg_ctx_set_dispatch",
+    "pqg_decode",
     "pqg_sync", "pqg_plan_create", "pqg_plan_launch", "pqg_plan_kernel_count", "pqg_plan_timeout_fallbacks", "pqg_plan_plain_fallbacks",
     "pqg_plan_destroy",
     "pqg_decode_host", "pqg_unpack_runs", "pqg_router_read", "pqg_router_read_runs", "pqg_error_name",
@@ -56,6 +57,7 @@ def lib():
         L.pqg_ctx_destroy.argtypes = [vp]
         L.pqg_ctx_stream.argtypes = [vp]
         L.pqg_ctx_stream.restype = vp
+        L.pqg_ctx_set_dispatch.argtypes = [vp, i32, i32]
         L.pqg_decode.argtypes = [vp, vp, u64, vp, i32, vp, i32, vp, C.POINTER(abi.Status)]
         L.pqg_sync.argtypes = [vp, C.POINTER(abi.Status)]
         L.pqg_plan_create.argtypes = [vp, vp, u64, vp, i32, vp, i32, C.POINTER(vp), C.POINTER(abi.Status)]

@@ -116,11 +116,10 @@ def test_binary_errors(decoder, which):
 
 @pytest.mark.parametrize("case", ["ascii", "empty", "zeros", "smallints", "random", "long", "optional",
                                   "plain_eof", "plain_negative"])
-def test_binary_plain_per_page(decoder, monkeypatch, case):
+def test_binary_plain_per_page(decoder, per_page_dispatch, case):
     """The one-wave-per-page one-pass PLAIN kernel (k_bin_plain_pg, normally for plans with 4,096 or
-    more PLAIN pages) on small plans through the PQGPU_PLAIN_PG=3 dispatch override: every value
+    more PLAIN pages) on small plans through the PQG_DISPATCH_PLAIN_ONE_PASS = 3 override: every value
     distribution (false candidates, values longer than a tile, empty values), nulls, and the errors."""
-    monkeypatch.setenv("PQGPU_PLAIN_PG", "3")
     if case in ("plain_eof", "plain_negative"):
         run_both(decoder, [_err_case(case)], expect_error=True)
     elif case == "optional":
@@ -378,12 +377,20 @@ def _plan_both(decoder, chunks):
 
 
 @pytest.fixture(params=["tiles", "pages"])
-def one_pass_kernel(request, monkeypatch):
+def one_pass_kernel(request, decoder):
     """The one-pass PLAIN kernel a small plan takes: the tiles (default) or one wave per page (the
-    PQGPU_PLAIN_PG=3 dispatch override; plans with 4,096 or more PLAIN pages take it by default)."""
+    PQG_DISPATCH_PLAIN_ONE_PASS = 3 override; plans with 4,096 or more PLAIN pages take it by default)."""
     if request.param == "pages":
-        monkeypatch.setenv("PQGPU_PLAIN_PG", "3")
-    return request.param
+        decoder.set_dispatch(abi.DISPATCH_PLAIN_ONE_PASS, 3)
+    yield request.param
+    decoder.set_dispatch(abi.DISPATCH_PLAIN_ONE_PASS, 2)
+
+
+@pytest.fixture
+def per_page_dispatch(decoder):
+    decoder.set_dispatch(abi.DISPATCH_PLAIN_ONE_PASS, 3)
+    yield
+    decoder.set_dispatch(abi.DISPATCH_PLAIN_ONE_PASS, 2)
 
 
 def test_binary_plain_one_pass_no_fallback(decoder, one_pass_kernel):
