@@ -764,7 +764,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
             P->pcol_pages.ensure(sizeof(int32_t) * std::max<size_t>(pcp.size(), 1)) == hipSuccess &&
             P->pcol_start.ensure(sizeof(int32_t) * pcs.size()) == hipSuccess &&
 
-            P->rec.ensure(sizeof(uint64_t) * (rec_total + 16)) == hipSuccess &&  // k_dict_fill reads 9 ahead
+            P->rec.ensure(sizeof(uint64_t) * (rec_total + 2 * 64 + 16)) == hipSuccess &&  // the expansion prefetches a page's first 128
             P->chunk_run.ensure(sizeof(uint32_t) * std::max<uint32_t>(chunk_total, 1)) == hipSuccess &&
             P->chunks.ensure(sizeof(uint64_t) * std::max<size_t>(chunk_list.size(), 1)) == hipSuccess &&
             P->pstat.ensure(sizeof(uint64_t) * (size_t)std::max(n_pages, 1)) == hipSuccess &&

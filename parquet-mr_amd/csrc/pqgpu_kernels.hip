@@ -784,6 +784,9 @@ __device__ __forceinline__ typename DictVal<W>::T dict_get_g(bool in_lds, const 
 //   tile sweep  every lane tracks the run holding its element: per tile it advances past
 //               the run starts it crossed (usually none), reads the value (RLE) or unpacks
 //               the id and gathers (packed), and the wave stores one full 1 KB tile.
+#ifndef PQG_XT_RECPF
+#define PQG_XT_RECPF 1  // 0: run records loaded after the chunk's first-run entry only (A/B builds)
+#endif
 #ifndef PQG_XT_EARLY
 #define PQG_XT_EARLY 1  // 0: packed bytes loaded after the records only (A/B builds)
 #endif
@@ -871,6 +874,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
   uint32_t j = 0, dict_n = 0, sec_end = 0, db = 0, N = 0, sh = 0, v_lo = 0, v_hi = 0, n_rec = 0, k = 0;
   uint32_t pre_lo = 0xFFFFFFFFu, pre_hi = 0;  // section bytes staged in xseg ahead of the records
   int w = 0;
+  uint64_t pf0 = 0, pf1 = 0;  // PQG_XT_RECPF: records [0, 128) of the page (lane l: l and 64 + l)
   PageWork pw{};
   rsrc_t drs = make_rsrc(bytes, 0), prs = drs;
 #ifdef PQG_DIAG
@@ -946,6 +950,10 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       // the page status and the chunk's first run in one round trip
       pst = sld(pstat + cpage);
       k = sld(chunk_run + pw.chunk_base + j);
+      if (PQG_XT_RECPF) {  // the page's first 2 x 64 run records in the same round trip
+        pf0 = sld(rec + pw.rec_base + lane);
+        pf1 = sld(rec + pw.rec_base + WAVE + lane);
+      }
       pst = uni64(pst);
       k = uni(k);
       N = (uint32_t)(pst >> 32);  // values covered before a walk error
@@ -986,10 +994,24 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       for (uint32_t t0 = 0; t0 < XT_RUNS; t0 += WAVE) {
         const uint32_t r = k + t0 + lane;
         const bool has = r < n_rec && t0 + lane < XT_RUNS - 1;  // a run of this round
-        const uint64_t rr = r < n_rec ? sld(prec + r) : 0;
+        uint64_t rr;
+        if (PQG_XT_RECPF) {  // records the hand-off prefetched come from the lanes holding them
+          const int src = (int)(r & (WAVE - 1u));
+          const uint64_t a0 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pf0 >> 32), src) << 32) |
+                              (uint32_t)__shfl((int)(uint32_t)pf0, src);
+          const uint64_t a1 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pf1 >> 32), src) << 32) |
+                              (uint32_t)__shfl((int)(uint32_t)pf1, src);
+          rr = r >= n_rec ? 0 : (r < WAVE ? a0 : (r < 2u * WAVE ? a1 : sld(prec + r)));
+        } else {
+          rr = r < n_rec ? sld(prec + r) : 0;
+        }
         const uint32_t st = r < n_rec ? (uint32_t)rr : N;        // (past the runs: end sentinel)
         const uint32_t pl = (uint32_t)(rr >> 32);
-        const uint32_t nx63 = uni(k + t0 + WAVE < n_rec ? (uint32_t)sld(prec + k + t0 + WAVE) : N);
+        const uint32_t q63 = k + t0 + WAVE;
+        const uint32_t nx63 = uni(q63 >= n_rec ? N
+                                  : (PQG_XT_RECPF && q63 < 2u * WAVE
+                                         ? rdl((uint32_t)(q63 < WAVE ? pf0 : pf1), q63 & (WAVE - 1u))
+                                         : (uint32_t)sld(prec + q63)));
         const uint32_t en_n = __shfl_down(st, 1);
         const uint32_t en = lane == WAVE - 1 ? nx63 : en_n;  // end of this lane's run
         const bool live = has && st < v_hi;
