@@ -158,6 +158,7 @@ struct pqg_plan {
   // hold those columns' entries last, so plain_fused launches skip them (pqg_sync turns plain_fused
   // off when a page's values do not fill its data section)
   bool plain_fused = false;
+  bool any_dict_direct = false;  // a dictionary-direct BYTE_ARRAY column: the offset scan stages dictionaries
   bool plain_pg = false;  // ... through k_bin_plain_pg (one wave per page) instead of the tiles
   int n_pcp = 0;          // pages of those columns (pcol_pages)
   int plain_fallbacks = 0;
@@ -783,6 +784,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       d.bin_total = (uint64_t*)at(P->bin_total_off[(size_t)i]);
       d.n_slots = slot_acc[(size_t)i];
       d.dict_direct = dict_direct[(size_t)i];
+      P->any_dict_direct = P->any_dict_direct || dict_direct[(size_t)i];
       if (dba_fixed[(size_t)i]) {  // DELTA_BYTE_ARRAY values go straight to the fixed-width output
         d.binary_data = (uint8_t*)cols[i].values;
         d.binary_capacity = slot_acc[(size_t)i] * (uint64_t)d.elem_width;
@@ -970,7 +972,7 @@ int pqg_plan_launch(pqg_plan* P) {
   const uint32_t n_blocks = pf ? P->n_bin_blocks_nf : P->n_bin_blocks;
   if (e == hipSuccess && n_blocks)
     e = pqg::launch_bin_scan(sb, P->d_bytes, P->n_bytes, cols, bl + P->off_bin_cols, pf ? P->n_bin_cols_nf : P->n_bin_cols,
-                             (const uint64_t*)P->bin_blocks.p, n_blocks);
+                             (const uint64_t*)P->bin_blocks.p, n_blocks, P->any_dict_direct);
   const uint32_t n_chunks = pf ? P->n_bin_chunks_nf : P->n_bin_chunks;
   if (e == hipSuccess && n_chunks)
     e = pqg::launch_bin_copy(sb, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->bin_chunks.p, n_chunks, err,
@@ -1156,7 +1158,11 @@ int sync_plan(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work) {
     }
   }
   int rc = resolve_errors(P, st, work);
-  if (rc == PQG_ERR_TIMEOUT && P->dict_fused) {
+  // only a timeout of the fused dictionary kernel's hand-off is re-run in split mode (a PLAIN
+  // BYTE_ARRAY segment walk that timed out waiting for its predecessor reaches the caller)
+  const int tpage = st ? (int)st->page : -1;
+  const int tcls = tpage >= 0 && tpage < P->n_pages ? P->page_cls[(size_t)tpage] : -1;
+  if (rc == PQG_ERR_TIMEOUT && P->dict_fused && (tcls == C_DICT4 || tcls == C_DICT8 || tcls == C_IDS)) {
     // The fused dictionary kernel's hand-off relies on the walker workgroups being dispatched before
     // the expansion workgroups that wait for them, which HIP does not promise. A launch in which an
     // expansion waited past SPIN_TIMEOUT_TICKS (it then stops and reports PQG_ERR_TIMEOUT; the walkers

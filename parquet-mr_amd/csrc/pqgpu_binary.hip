@@ -769,7 +769,10 @@ __global__ __launch_bounds__(256) void k_bin_offsets(const uint8_t* __restrict__
                                                      const uint64_t* __restrict__ blocks) {
   __shared__ uint64_t wsum[4][4];  // [row][wave]
   __shared__ uint64_t rowb[5];     // dict_direct: output offset of each row's first value (+ the block end)
-  __shared__ __attribute__((aligned(16))) DictDirectLds D;
+  // dict_direct staging: dynamic LDS, allocated only by launches of plans with dictionary-direct
+  // columns (the other offset scans keep the occupancy of ~0.2 KiB of LDS per workgroup)
+  extern __shared__ __attribute__((aligned(16))) uint8_t dd_lds[];
+  DictDirectLds& D = *(DictDirectLds*)dd_lds;
   const uint64_t b = blocks[blockIdx.x];
   const ColumnDev& cd = cols[(uint32_t)(b >> 32)];
   const uint64_t v0 = (uint64_t)(uint32_t)b * SCAN_BLOCK;
@@ -2711,11 +2714,13 @@ hipError_t launch_gather_fixed(hipStream_t st, const uint8_t* bytes, uint64_t n_
 }
 
 hipError_t launch_bin_scan(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, const ColumnDev* cols,
-                           const int32_t* bin_cols, int n_bin_cols, const uint64_t* blocks, uint32_t n_blocks) {
+                           const int32_t* bin_cols, int n_bin_cols, const uint64_t* blocks, uint32_t n_blocks,
+                           bool dict_direct) {
   if (n_bin_cols <= 0 || n_blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_bin_block_sums, dim3(n_blocks), dim3(256), 0, st, cols, blocks);
   hipLaunchKernelGGL(k_bin_block_bases, dim3(n_bin_cols), dim3(256), 0, st, cols, bin_cols);
-  hipLaunchKernelGGL(k_bin_offsets, dim3(n_blocks), dim3(256), 0, st, bytes, n_bytes, cols, blocks);
+  hipLaunchKernelGGL(k_bin_offsets, dim3(n_blocks), dim3(256), dict_direct ? sizeof(DictDirectLds) : 0, st, bytes,
+                     n_bytes, cols, blocks);
   return hipGetLastError();
 }
 

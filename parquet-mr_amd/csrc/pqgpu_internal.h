@@ -178,7 +178,8 @@ hipError_t launch_gather_fixed(hipStream_t st, const uint8_t* bytes, uint64_t n_
                                const ColumnDev* cols, const int32_t* list, int n);
 hipError_t launch_bin_scan(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, const ColumnDev* cols,
                            const int32_t* bin_cols, int n_bin_cols,
-                           const uint64_t* blocks, uint32_t n_blocks);
+                           const uint64_t* blocks, uint32_t n_blocks,
+                           bool dict_direct);
 hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const uint64_t* chunks, uint32_t n_chunks, uint64_t* err,
                            ErrCount err_count);
