@@ -710,46 +710,61 @@ __global__ __launch_bounds__(256) void k_bin_block_bases(const ColumnDev* __rest
 // Offsets of one scan block: per row, a wave scan of the threads' 4-length sums and the wave
 // totals through LDS (4 rows scanned side by side: one barrier per block instead of two per
 // 256 lengths); offsets stored as two 16-byte stores per row and thread.
-// dict_direct: the dictionary page staged once per workgroup, then per row of 1,024 values an output
-// image of the row's bytes (each value's entry scattered into it, 4 bytes per step) stored as 16-byte
-// blocks; a row whose bytes exceed the image is written with byte stores
-constexpr uint32_t DD_OUT = 16384;
+// dict_direct: the dictionary page staged once per workgroup, then per row each wave builds an output
+// image of its 256 values' bytes in its own LDS image (whole dwords as unaligned 4-byte writes, the
+// last 1-3 bytes of a value as a 2- and a 1-byte write, so no write leaves the value's own bytes) and
+// stores it as 16-byte blocks: no workgroup barrier per row (the wave's bytes are contiguous; the
+// blocks it shares with its neighbours at both ends are stored byte-exact); a quarter row whose bytes
+// exceed the image is written with byte stores
+constexpr uint32_t DD_WIMG = 6144;  // output image per wave (a quarter row: 256 values of up to 24 bytes)
 struct DictDirectLds {
   uint32_t dict[DD_DICT_MAX / 4 + 4];
-  uint32_t out[DD_OUT / 4 + 4];
+  uint32_t img[WPB][DD_WIMG / 4 + 4];
 };
 
 // lens / srcs: the thread's 4 values' entry lengths and offsets in the dictionary page (gathered
-// before the offset stores: a load issued after them would wait for them, vmcnt counts stores)
-__device__ __noinline__ void dd_row_bytes(const ColumnDev& cd, DictDirectLds& D, u32x4 lens, u32x4 srcs, uint64_t e,
-                                          uint64_t o_lo, uint64_t o_hi) {
-  const uint32_t t = threadIdx.x;
+// before the offset stores: a load issued after them would wait for them, vmcnt counts stores);
+// e: output offset of the thread's first value; [o_lo, o_hi): the wave's bytes (clipped to the
+// capacity), w_hi: their unclipped end
+__device__ __noinline__ void dd_wave_bytes(const ColumnDev& cd, const uint32_t* dict, uint32_t* img, u32x4 lens,
+                                           u32x4 srcs, uint64_t e, uint64_t o_lo, uint64_t o_hi, uint64_t w_hi) {
+  typedef uint16_t __attribute__((aligned(1), may_alias)) u16u;
+  typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
   uint8_t* dst = cd.binary_data;
   const uint32_t dbytes = (uint32_t)cd.dict_bytes;
   const uint64_t a0 = o_lo & ~15ull;
-  const bool img = o_hi - a0 + 16u <= DD_OUT;
-  uint8_t* outb = (uint8_t*)D.out;
+  const bool in_img = w_hi - a0 + 16u <= DD_WIMG;
+  uint8_t* outb = (uint8_t*)img;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t sp = srcs[k], len = lens[k];
-    for (uint32_t j = 0; j < len; j += 4u) {
-      const uint32_t w = sp + j < dbytes ? img4(D.dict, sp + j) : 0u;  // (bytes past the entry: masked)
+    if (in_img) {
+      uint8_t* ob = outb + (e - a0);
+      uint32_t j = 0;
+      for (; j + 4u <= len; j += 4u) *(u32u*)(ob + j) = img4(dict, sp + j);
+      if (j < len) {  // 1-3 bytes left (bytes past the dictionary page: never part of an entry)
+        const uint32_t w = sp + j < dbytes ? img4(dict, sp + j) : 0u;
+        const uint32_t r = len - j;
+        if (r & 2u) *(u16u*)(ob + j) = (uint16_t)w;
+        if (r & 1u) ob[j + (r & 2u)] = (uint8_t)(w >> (8u * (r & 2u)));
+      }
+    } else {
+      for (uint32_t j = 0; j < len; j += 4u) {
+        const uint32_t w = sp + j < dbytes ? img4(dict, sp + j) : 0u;
 #pragma unroll
-      for (uint32_t q = 0; q < 4u; q++) {
-        const uint64_t o = e + j + q;
-        if (j + q < len && o < o_hi) {
-          if (img) outb[o - a0] = (uint8_t)(w >> (8u * q));
-          else gst(dst + o, (uint8_t)(w >> (8u * q)));
+        for (uint32_t q = 0; q < 4u; q++) {
+          const uint64_t o = e + j + q;
+          if (j + q < len && o < o_hi) gst(dst + o, (uint8_t)(w >> (8u * q)));
         }
       }
     }
     e += len;
   }
-  if (!img) return;
-  __syncthreads();
+  if (!in_img) return;
+  wave_sync();
   const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
   const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
-  for (uint32_t bb = 16u * t; bb < r_hi; bb += 16u * 256u) {
+  for (uint32_t bb = 16u * lane_id(); bb < r_hi; bb += 16u * WAVE) {
     const u32x4 v4 = *(const u32x4*)(outb + bb);
     uint32_t wd[4] = {v4.x, v4.y, v4.z, v4.w};
     uint32_t have = 0;
@@ -761,14 +776,13 @@ __device__ __noinline__ void dd_row_bytes(const ColumnDev& cd, DictDirectLds& D,
     if (!dst_al4) have = 0;
     store_block16(dst, a0 + bb, o_lo, o_hi, wd, have, dst_al16);
   }
-  __syncthreads();  // the image is reused by the next row
+  wave_sync();  // the image is reused by the next row
 }
 
 __global__ __launch_bounds__(256) void k_bin_offsets(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                      const ColumnDev* __restrict__ cols,
                                                      const uint64_t* __restrict__ blocks) {
   __shared__ uint64_t wsum[4][4];  // [row][wave]
-  __shared__ uint64_t rowb[5];     // dict_direct: output offset of each row's first value (+ the block end)
   // dict_direct staging: dynamic LDS, allocated only by launches of plans with dictionary-direct
   // columns (the other offset scans keep the occupancy of ~0.2 KiB of LDS per workgroup)
   extern __shared__ __attribute__((aligned(16))) uint8_t dd_lds[];
@@ -781,7 +795,7 @@ __global__ __launch_bounds__(256) void k_bin_offsets(const uint8_t* __restrict__
   const uint32_t t = threadIdx.x, wv = t >> 6, lane = lane_id();
   const bool dd = uni(cd.dict_direct) != 0;
   u32x4 x[4], ids[4];
-  uint64_t inc[4], first[4];
+  uint64_t inc[4], first[4], last[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     x[i] = scan_row_load(cd.blen, n_slots, v0 + 1024u * i + 4u * t);
@@ -852,17 +866,18 @@ __global__ __launch_bounds__(256) void k_bin_offsets(const uint8_t* __restrict__
     if (v < n_slots && n_slots <= v + 4) gst(off + n_slots, (int64_t)(n_slots - v == 1 ? e1 : n_slots - v == 2 ? e2
                                                                      : n_slots - v == 3 ? e3 : e4));
     first[i] = e0;
-    if (dd && t == 0) rowb[i] = e0;  // the row's first offset
-    if (dd && i == 3 && t == 255) rowb[4] = e4;
+    last[i] = e4;
   }
   if (!dd) return;
-  // ---- value bytes of the block, row by row (values past n_slots have length 0)
-  __syncthreads();  // rowb, the staged dictionary
+  // ---- value bytes of the block: each wave its quarter of every row (values past n_slots have length 0)
+  __syncthreads();  // the staged dictionary
   const uint64_t cap = cd.binary_capacity;
 #pragma unroll 1
   for (int i = 0; i < 4; i++) {
-    const uint64_t o_lo = rowb[i], o_hi = rowb[i + 1] < cap ? rowb[i + 1] : cap;  // overflow: reported at sync
-    if (o_lo < o_hi) dd_row_bytes(cd, D, x[i], ids[i], first[i], o_lo, o_hi);
+    const uint64_t w_lo = ((uint64_t)rdl((uint32_t)(first[i] >> 32), 0) << 32) | rdl((uint32_t)first[i], 0);
+    const uint64_t w_hi = ((uint64_t)rdl((uint32_t)(last[i] >> 32), 63) << 32) | rdl((uint32_t)last[i], 63);
+    const uint64_t o_hi = w_hi < cap ? w_hi : cap;  // overflow: reported at sync
+    if (w_lo < o_hi) dd_wave_bytes(cd, D.dict, D.img[wv], x[i], ids[i], first[i], w_lo, o_hi, w_hi);
   }
 }
 
