@@ -3,7 +3,7 @@
 # then separate PMC passes for HBM traffic. Every GPU step has its own time limit and
 # the script stops at the first failure (no retries).
 # Usage (from the repo root, via gpurun): bash tools/gpu_round.sh <tag> [steps...]
-#   steps: tests smoke bench e2e bench2 suite suiteprof prof pmc c4 c4prof wlpmc
+#   steps: tests smoke bench e2e bench2 suite suiteprof prof pmc c4 c4prof wlpmc router diag
 #   (default: tests smoke bench prof pmc)
 #   env: SUITE="c3_mixed c5_levels" restricts suite / suiteprof / wlpmc to those workloads;
 #        TESTS="tests/test_x.py ..." restricts the tests step.
@@ -65,11 +65,20 @@ PY
           || { tail -20 "$OUT/pmc/pass$i.log"; exit 1; }
         i=$((i+1))
       done
-      python3 tools/pmc_summary.py "$OUT/pmc" || true ;;
+      python3 tools/pmc_summary.py "$OUT/pmc" --json "$OUT/traffic.json" || true ;;
     c4)
       timeout -k 10 600 python3 bench.py --workload c4 --rows 125000000 --steps 10 --warmup 2 > "$OUT/bench_c4.json" \
         2> "$OUT/bench_c4.err" || { tail -30 "$OUT/bench_c4.err"; exit 1; }
       cat "$OUT/bench_c4.json" ;;
+    router)
+      timeout -k 10 120 python3 tools/router_latency.py > "$OUT/router_latency.jsonl" 2> "$OUT/router.err" \
+        || { tail -20 "$OUT/router.err"; exit 1; }
+      cat "$OUT/router_latency.jsonl" ;;
+    diag)
+      # walk / hand-off / expansion timeline of one C2 launch (diagnostic build abx/libdiag.so)
+      PQGPU_LIB=$PWD/abx/libdiag.so timeout -k 10 300 python3 tools/diag_fused.py 1.5 "$OUT/diag_fused.json" \
+        > "$OUT/diag_fused.log" 2>&1 || { tail -20 "$OUT/diag_fused.log"; exit 1; }
+      tail -30 "$OUT/diag_fused.log" ;;
     c4prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c4prof" -o run -- \
         python3 bench.py --workload c4 --rows 125000000 --steps 5 --warmup 1 --no-cpu > "$OUT/c4prof.json" \
