@@ -158,7 +158,7 @@ struct pqg_plan {
   // hold those columns' entries last, so plain_fused launches skip them (pqg_sync turns plain_fused
   // off when a page's values do not fill its data section)
   bool plain_fused = false;
-  bool any_dict_direct = false;  // a dictionary-direct BYTE_ARRAY column: the offset scan stages dictionaries
+  uint32_t dd_dict_bytes = 0;  // largest dictionary-direct dictionary page (the offset scan stages it)
   bool plain_pg = false;  // ... through k_bin_plain_pg (one wave per page) instead of the tiles
   int n_pcp = 0;          // pages of those columns (pcol_pages)
   int plain_fallbacks = 0;
@@ -784,7 +784,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       d.bin_total = (uint64_t*)at(P->bin_total_off[(size_t)i]);
       d.n_slots = slot_acc[(size_t)i];
       d.dict_direct = dict_direct[(size_t)i];
-      P->any_dict_direct = P->any_dict_direct || dict_direct[(size_t)i];
+      if (dict_direct[(size_t)i]) P->dd_dict_bytes = std::max<uint32_t>(P->dd_dict_bytes, std::max<uint32_t>((uint32_t)cols[i].dict_size, 16u));
       if (dba_fixed[(size_t)i]) {  // DELTA_BYTE_ARRAY values go straight to the fixed-width output
         d.binary_data = (uint8_t*)cols[i].values;
         d.binary_capacity = slot_acc[(size_t)i] * (uint64_t)d.elem_width;
@@ -972,7 +972,7 @@ int pqg_plan_launch(pqg_plan* P) {
   const uint32_t n_blocks = pf ? P->n_bin_blocks_nf : P->n_bin_blocks;
   if (e == hipSuccess && n_blocks)
     e = pqg::launch_bin_scan(sb, P->d_bytes, P->n_bytes, cols, bl + P->off_bin_cols, pf ? P->n_bin_cols_nf : P->n_bin_cols,
-                             (const uint64_t*)P->bin_blocks.p, n_blocks, P->any_dict_direct);
+                             (const uint64_t*)P->bin_blocks.p, n_blocks, P->dd_dict_bytes);
   const uint32_t n_chunks = pf ? P->n_bin_chunks_nf : P->n_bin_chunks;
   if (e == hipSuccess && n_chunks)
     e = pqg::launch_bin_copy(sb, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->bin_chunks.p, n_chunks, err,

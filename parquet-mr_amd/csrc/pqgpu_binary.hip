@@ -718,9 +718,10 @@ __global__ __launch_bounds__(256) void k_bin_block_bases(const ColumnDev* __rest
 // exceed the image is written with byte stores
 constexpr uint32_t DD_WIMG = 6144;  // output image per wave (a quarter row: 256 values of up to 24 bytes)
 struct DictDirectLds {
-  uint32_t dict[DD_DICT_MAX / 4 + 4];
   uint32_t img[WPB][DD_WIMG / 4 + 4];
+  uint32_t dict[DD_DICT_MAX / 4 + 4];  // (the launch allocates only the plan's largest dictionary)
 };
+constexpr uint32_t DD_LDS_FIXED = sizeof(uint32_t) * WPB * (DD_WIMG / 4 + 4);
 
 // lens / srcs: the thread's 4 values' entry lengths and offsets in the dictionary page (gathered
 // before the offset stores: a load issued after them would wait for them, vmcnt counts stores);
@@ -2730,12 +2731,13 @@ hipError_t launch_gather_fixed(hipStream_t st, const uint8_t* bytes, uint64_t n_
 
 hipError_t launch_bin_scan(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, const ColumnDev* cols,
                            const int32_t* bin_cols, int n_bin_cols, const uint64_t* blocks, uint32_t n_blocks,
-                           bool dict_direct) {
+                           uint32_t dd_dict_bytes) {
   if (n_bin_cols <= 0 || n_blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_bin_block_sums, dim3(n_blocks), dim3(256), 0, st, cols, blocks);
   hipLaunchKernelGGL(k_bin_block_bases, dim3(n_bin_cols), dim3(256), 0, st, cols, bin_cols);
-  hipLaunchKernelGGL(k_bin_offsets, dim3(n_blocks), dim3(256), dict_direct ? sizeof(DictDirectLds) : 0, st, bytes,
-                     n_bytes, cols, blocks);
+  // dynamic LDS: the wave images and the plan's largest dictionary-direct dictionary (none: 0 bytes)
+  const uint32_t dyn = dd_dict_bytes ? DD_LDS_FIXED + ((dd_dict_bytes + 15u) & ~15u) + 16u : 0u;
+  hipLaunchKernelGGL(k_bin_offsets, dim3(n_blocks), dim3(256), dyn, st, bytes, n_bytes, cols, blocks);
   return hipGetLastError();
 }
 

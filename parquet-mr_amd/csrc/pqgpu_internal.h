@@ -151,7 +151,10 @@ constexpr uint32_t BW_SEG_BYTES = 16384;
 constexpr uint32_t BW_SEG_CAP = BW_SEG_BYTES / 4 + 2;
 constexpr uint32_t BW_SEG_MAX_PAGES = 4096;
 constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block
-constexpr uint32_t DD_DICT_MAX = 8192;  // dictionary page bytes staged by the offset scan (dict_direct)
+#ifndef PQG_DD_DICT_MAX
+#define PQG_DD_DICT_MAX 8192
+#endif
+constexpr uint32_t DD_DICT_MAX = PQG_DD_DICT_MAX;  // dictionary page bytes staged by the offset scan (dict_direct)
 hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                       const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
@@ -179,7 +182,7 @@ hipError_t launch_gather_fixed(hipStream_t st, const uint8_t* bytes, uint64_t n_
 hipError_t launch_bin_scan(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, const ColumnDev* cols,
                            const int32_t* bin_cols, int n_bin_cols,
                            const uint64_t* blocks, uint32_t n_blocks,
-                           bool dict_direct);
+                           uint32_t dd_dict_bytes);
 hipError_t launch_bin_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const uint64_t* chunks, uint32_t n_chunks, uint64_t* err,
                            ErrCount err_count);
