@@ -487,6 +487,18 @@ int pqg_zstd_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, 
                         const pqg_zstd_job* d_jobs, int n_jobs, int32_t* d_status);
 int pqg_zstd_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_status* st);
 
+/* LZ4_RAW pages (ColumnChunkPageReadStore.readPage -> Lz4RawDecompressor, parquet-hadoop/.../hadoop/
+ * codec/Lz4RawDecompressor.java:26-50, aircompressor's Lz4Decompressor underneath): every job is one
+ * raw LZ4 block (lz4 block format) decompressed into exactly dst_size bytes (the header's
+ * uncompressed size; another length, or a malformed block -> PQG_ERR_CORRUPT in the job's status).
+ * Same job table and calling sequence as pqg_snappy_decompress; pqg_lz4_raw_sync reports the first
+ * failing job (st->page = job index). */
+typedef pqg_snappy_job pqg_lz4_job;
+
+int pqg_lz4_raw_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, uint8_t* d_dst, uint64_t dst_bytes,
+                           const pqg_lz4_job* d_jobs, int n_jobs, int32_t* d_status);
+int pqg_lz4_raw_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_status* st);
+
 /* ---- page framing (host) ----------------------------------------------------
  * File bytes in: the page headers of one raw column chunk, as
  * ParquetFileReader.Chunk.readAllPages reads them

@@ -1026,3 +1026,59 @@ int pqr_snappy_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t e
   *out_len = op;
   return 0;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * LZ4 raw block decompression (ORACLE). parquet-mr decompresses an LZ4_RAW page with
+ * Lz4RawDecompressor (parquet-hadoop/.../hadoop/codec/Lz4RawDecompressor.java:26-50, a
+ * NonBlockedDecompressor over a buffer of the header's uncompressed size), which calls
+ * io.airlift.compress.lz4.Lz4Decompressor (aircompressor, a third-party library absent here, pinned
+ * in parquet-mr's pom as io.airlift:aircompressor). This restates the published LZ4 block format
+ * (lz4/lz4 doc/lz4_Block_format.md): a sequence is a token (literal length in the high nibble,
+ * match length - 4 in the low nibble; 15 continues with bytes added while they are 255), the
+ * literals, a 2-byte little-endian offset (0 is invalid) and the match, which may overlap its own
+ * output; the block ends with a sequence of literals only, at the end of the input. An empty
+ * output is the single byte 0. Returns 0 and *out_len, or PQG_ERR_CORRUPT for malformed input or an
+ * output length different from `expect`.
+ * ------------------------------------------------------------------------------------------ */
+int pqr_lz4_raw_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expect, int64_t* out_len) {
+  if (n <= 0) return PQG_ERR_CORRUPT;
+  int64_t p = 0, op = 0;
+  for (;;) {
+    if (p >= n) return PQG_ERR_CORRUPT;
+    const uint32_t token = src[p++];
+    int64_t ll = token >> 4;
+    if (ll == 15) {
+      uint32_t b;
+      do {
+        if (p >= n) return PQG_ERR_CORRUPT;
+        b = src[p++];
+        ll += b;
+      } while (b == 255);
+    }
+    if (p + ll > n || op + ll > expect) return PQG_ERR_CORRUPT;
+    memcpy(dst + op, src + p, (size_t)ll);
+    p += ll;
+    op += ll;
+    if (p == n) break;  /* the last sequence: literals only */
+    if (p + 2 > n) return PQG_ERR_CORRUPT;
+    const int64_t off = (int64_t)src[p] | ((int64_t)src[p + 1] << 8);
+    p += 2;
+    if (off == 0 || off > op) return PQG_ERR_CORRUPT;
+    int64_t ml = token & 15;
+    if (ml == 15) {
+      uint32_t b;
+      do {
+        if (p >= n) return PQG_ERR_CORRUPT;
+        b = src[p++];
+        ml += b;
+      } while (b == 255);
+    }
+    ml += 4;
+    if (op + ml > expect) return PQG_ERR_CORRUPT;
+    for (int64_t i = 0; i < ml; i++) dst[op + i] = dst[op - off + i];
+    op += ml;
+  }
+  if (op != expect) return PQG_ERR_CORRUPT;
+  *out_len = op;
+  return 0;
+}

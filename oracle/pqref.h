@@ -19,6 +19,8 @@ int64_t pqr_delta_decode(const uint8_t* buf, int64_t len, int64_t* out, int64_t 
 int pqr_snappy_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expect, int64_t* out_len);
 /* Zstandard (RFC 8878) frames -> dst (zstd_ref.c); XXH64 of the content checksum */
 int pqr_zstd_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expect, int64_t* out_len);
+/* LZ4 raw block (Lz4RawDecompressor; LZ4 block format restated): 0, or PQG_ERR_CORRUPT. */
+int pqr_lz4_raw_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expect, int64_t* out_len);
 uint64_t pqr_xxh64(const uint8_t* p, uint64_t n, uint64_t seed);
 int pqr_decode(const uint8_t* bytes, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
                const pqg_page_desc* pages, int n_pages, uint32_t* page_value_counts, pqg_status* st);

@@ -44,6 +44,8 @@ def lib():
         L.pqr_snappy_decompress.restype = C.c_int
         L.pqr_zstd_decompress.argtypes = [vp, i64, vp, i64, C.POINTER(i64)]
         L.pqr_zstd_decompress.restype = C.c_int
+        L.pqr_lz4_raw_decompress.argtypes = [vp, i64, vp, i64, C.POINTER(i64)]
+        L.pqr_lz4_raw_decompress.restype = C.c_int
         L.pqr_xxh64.argtypes = [vp, C.c_uint64, C.c_uint64]
         L.pqr_xxh64.restype = C.c_uint64
         L.pqr_delta_decode.restype = i64
@@ -197,6 +199,18 @@ def snappy_decompress(data, uncompressed_size):
     rc = lib().pqr_snappy_decompress(src.ctypes.data, len(data), out.ctypes.data, int(uncompressed_size), C.byref(n))
     if rc:
         raise ValueError(f"snappy: error {rc}")
+    return out[:n.value].tobytes()
+
+
+def lz4_raw_decompress(data, uncompressed_size):
+    """LZ4 raw block -> bytes (ORACLE; pqr_lz4_raw_decompress, the LZ4 block format restated).
+    Raises ValueError(code) when malformed or of another length."""
+    src = np.frombuffer(bytes(data), dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    out = np.zeros(max(int(uncompressed_size), 1), dtype=np.uint8)
+    n = C.c_int64(0)
+    rc = lib().pqr_lz4_raw_decompress(src.ctypes.data, len(data), out.ctypes.data, int(uncompressed_size), C.byref(n))
+    if rc:
+        raise ValueError(f"lz4_raw: error {rc}")
     return out[:n.value].tobytes()
 
 

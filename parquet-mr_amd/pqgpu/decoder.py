@@ -145,10 +145,11 @@ class Decoder:
         return DeviceBatch(batch, self.device)
 
     _CODEC_FN = {batch.SNAPPY: ("pqg_snappy_decompress", "pqg_snappy_sync", "snappy block"),
-                 batch.ZSTD: ("pqg_zstd_decompress", "pqg_zstd_sync", "zstd frame")}
+                 batch.ZSTD: ("pqg_zstd_decompress", "pqg_zstd_sync", "zstd frame"),
+                 batch.LZ4_RAW: ("pqg_lz4_raw_decompress", "pqg_lz4_raw_sync", "lz4_raw block")}
 
     def upload_chunks(self, chunks):
-        """Column chunks whose pages may be SNAPPY- or ZSTD-compressed -> a DeviceBatch of
+        """Column chunks whose pages may be SNAPPY-, ZSTD- or LZ4_RAW-compressed -> a DeviceBatch of
         uncompressed pages.
 
         The batch is laid out for the uncompressed pages (batch.build_batch over placeholders of
@@ -258,6 +259,13 @@ class Decoder:
         """Raw Snappy blocks (host bytes) -> device tensor of the concatenated outputs (each at a
         16-byte aligned offset, or with skew=True at offsets of every residue mod 16) + the
         offsets, decompressed by pqg_snappy_decompress. Returns (out_tensor, offsets, status_codes)."""
+        return self._block_jobs("pqg_snappy_decompress", "pqg_snappy_sync", blocks, sizes, skew)
+
+    def lz4_raw_decompress(self, blocks, sizes, skew=False):
+        """Raw LZ4 blocks (host bytes) -> as snappy_decompress, by pqg_lz4_raw_decompress."""
+        return self._block_jobs("pqg_lz4_raw_decompress", "pqg_lz4_raw_sync", blocks, sizes, skew)
+
+    def _block_jobs(self, fn, fn_sync, blocks, sizes, skew):
         src, soff, pos = [], [], 0
         for b in blocks:
             soff.append(pos)
@@ -276,11 +284,10 @@ class Decoder:
         d_status = torch.full((max(len(blocks), 1),), -1, dtype=torch.int32, device=self.device)
         torch.cuda.current_stream(self.device).synchronize()
         L = native.lib()
-        native.check(L.pqg_snappy_decompress(self.ctx, d_src.data_ptr(), d_src.numel(), d_dst.data_ptr(), d_dst.numel(),
-                                             d_jobs.data_ptr(), len(blocks), d_status.data_ptr()),
-                     what="pqg_snappy_decompress")
+        native.check(getattr(L, fn)(self.ctx, d_src.data_ptr(), d_src.numel(), d_dst.data_ptr(), d_dst.numel(),
+                                    d_jobs.data_ptr(), len(blocks), d_status.data_ptr()), what=fn)
         st = abi.Status()
-        L.pqg_snappy_sync(self.ctx, d_status.data_ptr(), len(blocks), C.byref(st))
+        getattr(L, fn_sync)(self.ctx, d_status.data_ptr(), len(blocks), C.byref(st))
         return d_dst, doff, d_status[:len(blocks)].cpu().numpy()
 
     @staticmethod

@@ -25,7 +25,9 @@ def chunk_cases():
 def load_chunk(name, c):
     buf = np.fromfile(os.path.join(GOLDEN, name + ".parquet"), dtype=np.uint8)
     ptype = framing.TYPE_BY_NAME[c["physical_type"]]
-    codec = {"SNAPPY": writer.SNAPPY, "ZSTD": writer.ZSTD}.get(c.get("compression"), writer.UNCOMPRESSED)
+    # (pyarrow names the LZ4_RAW codec it writes "LZ4")
+    codec = {"SNAPPY": writer.SNAPPY, "ZSTD": writer.ZSTD, "LZ4": writer.LZ4_RAW,
+             "LZ4_RAW": writer.LZ4_RAW}.get(c.get("compression"), writer.UNCOMPRESSED)
     ch = framing.read_column_chunk(buf, c["start"], c["length"], ptype, max_def=c["max_def"], max_rep=c["max_rep"],
                                    type_length=c["type_length"], num_values=c["num_values"], codec=codec)
     exp = np.load(os.path.join(GOLDEN, name + ".npz"))
@@ -49,19 +51,21 @@ def is_compressed(ch):
 
 
 def decompressed_on_host(ch):
-    """The chunk with every SNAPPY / ZSTD page decompressed by the ORACLE (test infrastructure)."""
+    """The chunk with every SNAPPY / ZSTD / LZ4_RAW page decompressed by the ORACLE (test infrastructure)."""
     import copy
 
     from oracle import pqref
+    unzs = {writer.ZSTD: pqref.zstd_decompress, writer.SNAPPY: pqref.snappy_decompress,
+            writer.LZ4_RAW: pqref.lz4_raw_decompress}
     out = copy.deepcopy(ch)
     if out.dict_codec:
-        unz = pqref.zstd_decompress if out.dict_codec == writer.ZSTD else pqref.snappy_decompress
+        unz = unzs[out.dict_codec]
         out.dict_page = unz(out.dict_page, out.dict_uncompressed_size)
         out.dict_codec = writer.UNCOMPRESSED
     for p in out.pages:
         if p.codec:
             lv = p.rl_byte_length + p.dl_byte_length if p.version == 2 else 0
-            unz = pqref.zstd_decompress if p.codec == writer.ZSTD else pqref.snappy_decompress
+            unz = unzs[p.codec]
             p.body = p.body[:lv] + unz(p.body[lv:], p.uncompressed_size - lv)
             p.codec = writer.UNCOMPRESSED
     return out

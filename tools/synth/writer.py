@@ -26,8 +26,8 @@ from typing import List, Optional
 import numpy as np
 
 from pqgpu import abi
-from pqgpu.batch import (ALIGN, PAD, SNAPPY, UNCOMPRESSED, ZSTD, ColumnChunk, Page, PageBatch,  # noqa: F401
-                          build_batch)
+from pqgpu.batch import (ALIGN, LZ4_RAW, PAD, SNAPPY, UNCOMPRESSED, ZSTD, ColumnChunk, Page,  # noqa: F401
+                          PageBatch, build_batch)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
@@ -403,4 +403,26 @@ def zstd_chunk(chunk, level=3):
         lv = pg.rl_byte_length + pg.dl_byte_length if pg.version == 2 else 0
         pg.body = pg.body[:lv] + codec.compress(pg.body[lv:], asbytes=True)
         pg.codec = ZSTD
+    return out
+
+
+def lz4_raw_chunk(chunk):
+    """A copy of `chunk` with every page (and the dictionary page) LZ4_RAW-compressed the way
+    parquet-mr writes LZ4_RAW column chunks (Lz4RawCompressor, one raw LZ4 block per page; V1: the
+    whole body; V2: the data section after the level sections). Compression by pyarrow's liblz4
+    (test-data synthesis only)."""
+    import copy
+
+    import pyarrow as pa
+    codec = pa.Codec("lz4_raw")
+    out = copy.deepcopy(chunk)
+    if out.dict_page is not None:
+        out.dict_uncompressed_size = len(out.dict_page)
+        out.dict_page = codec.compress(out.dict_page, asbytes=True)
+        out.dict_codec = LZ4_RAW
+    for pg in out.pages:
+        pg.uncompressed_size = len(pg.body)
+        lv = pg.rl_byte_length + pg.dl_byte_length if pg.version == 2 else 0
+        pg.body = pg.body[:lv] + codec.compress(pg.body[lv:], asbytes=True)
+        pg.codec = LZ4_RAW
     return out
