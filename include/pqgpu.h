@@ -499,6 +499,19 @@ int pqg_lz4_raw_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_byte
                            const pqg_lz4_job* d_jobs, int n_jobs, int32_t* d_status);
 int pqg_lz4_raw_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_status* st);
 
+/* GZIP pages (ColumnChunkPageReadStore.readPage -> CodecFactory.HeapBytesDecompressor.decompress,
+ * parquet-hadoop/.../hadoop/CodecFactory.java:155-182, Hadoop's GzipCodec stream read for exactly the
+ * page's size): every job is gzip members (RFC 1952) of DEFLATE data (RFC 1951) read until dst_size
+ * bytes are produced. The member completing the page has its trailer unread; an earlier member's ISIZE
+ * is checked (its CRC-32 is not recomputed on the device). Fewer bytes than dst_size -> PQG_ERR_EOF,
+ * malformed data -> PQG_ERR_CORRUPT in the job's status. Same job table and calling sequence as
+ * pqg_snappy_decompress; pqg_gzip_sync reports the first failing job (st->page = job index). */
+typedef pqg_snappy_job pqg_gzip_job;
+
+int pqg_gzip_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, uint8_t* d_dst, uint64_t dst_bytes,
+                        const pqg_gzip_job* d_jobs, int n_jobs, int32_t* d_status);
+int pqg_gzip_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_status* st);
+
 /* ---- page framing (host) ----------------------------------------------------
  * File bytes in: the page headers of one raw column chunk, as
  * ParquetFileReader.Chunk.readAllPages reads them

@@ -21,6 +21,8 @@ int pqr_snappy_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t e
 int pqr_zstd_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expect, int64_t* out_len);
 /* LZ4 raw block (Lz4RawDecompressor; LZ4 block format restated): 0, or PQG_ERR_CORRUPT. */
 int pqr_lz4_raw_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expect, int64_t* out_len);
+/* GZIP members (RFC 1952 / 1951 restated, gzip_ref.c): 0, PQG_ERR_EOF (short) or PQG_ERR_CORRUPT. */
+int pqr_gzip_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expect, int64_t* out_len);
 uint64_t pqr_xxh64(const uint8_t* p, uint64_t n, uint64_t seed);
 int pqr_decode(const uint8_t* bytes, uint64_t n_bytes, pqg_column_desc* cols, int n_cols,
                const pqg_page_desc* pages, int n_pages, uint32_t* page_value_counts, pqg_status* st);

@@ -46,6 +46,8 @@ def lib():
         L.pqr_zstd_decompress.restype = C.c_int
         L.pqr_lz4_raw_decompress.argtypes = [vp, i64, vp, i64, C.POINTER(i64)]
         L.pqr_lz4_raw_decompress.restype = C.c_int
+        L.pqr_gzip_decompress.argtypes = [vp, i64, vp, i64, C.POINTER(i64)]
+        L.pqr_gzip_decompress.restype = C.c_int
         L.pqr_xxh64.argtypes = [vp, C.c_uint64, C.c_uint64]
         L.pqr_xxh64.restype = C.c_uint64
         L.pqr_delta_decode.restype = i64
@@ -212,6 +214,18 @@ def lz4_raw_decompress(data, uncompressed_size):
     if rc:
         raise ValueError(f"lz4_raw: error {rc}")
     return out[:n.value].tobytes()
+
+
+def gzip_decompress(data, uncompressed_size):
+    """GZIP members -> the first `uncompressed_size` bytes (ORACLE; pqr_gzip_decompress, RFC 1952 /
+    1951 restated). Raises ValueError(code) when malformed (CORRUPT) or short (EOF)."""
+    src = np.frombuffer(bytes(data), dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    out = np.zeros(max(int(uncompressed_size), 1), dtype=np.uint8)
+    n = C.c_int64(0)
+    rc = lib().pqr_gzip_decompress(src.ctypes.data, len(data), out.ctypes.data, int(uncompressed_size), C.byref(n))
+    if rc:
+        raise ValueError(f"gzip: error {rc}")
+    return out[:int(uncompressed_size)].tobytes()
 
 
 def zstd_decompress(data, uncompressed_size):

@@ -1826,6 +1826,32 @@ int pqg_lz4_raw_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_stat
   return PQG_OK;
 }
 
+int pqg_gzip_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, uint8_t* d_dst, uint64_t dst_bytes,
+                        const pqg_gzip_job* d_jobs, int n_jobs, int32_t* d_status) {
+  if (!ctx || n_jobs < 0) return PQG_ERR_INVALID_ARG;
+  if (n_jobs == 0) return PQG_OK;
+  if (!d_src || !d_dst || !d_jobs) return PQG_ERR_INVALID_ARG;
+  if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
+  const hipError_t e = pqg::launch_gzip(ctx->stream, d_src, src_bytes, d_dst, dst_bytes, d_jobs, n_jobs, d_status);
+  return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
+}
+
+int pqg_gzip_sync(pqg_ctx* ctx, const int32_t* d_status, int n_jobs, pqg_status* st) {
+  if (!ctx || n_jobs < 0) return PQG_ERR_INVALID_ARG;
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return PQG_ERR_HIP;
+  if (st) set_status(st, PQG_OK, -1, -1, "gzip");
+  if (!d_status || n_jobs == 0) return PQG_OK;
+  std::vector<int32_t> h((size_t)n_jobs);
+  if (hipMemcpy(h.data(), d_status, sizeof(int32_t) * (size_t)n_jobs, hipMemcpyDeviceToHost) != hipSuccess)
+    return PQG_ERR_HIP;
+  for (int j = 0; j < n_jobs; j++)
+    if (h[(size_t)j]) {
+      set_status(st, h[(size_t)j], j, -1, "gzip block");
+      return h[(size_t)j];
+    }
+  return PQG_OK;
+}
+
 int pqg_zstd_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, uint8_t* d_dst, uint64_t dst_bytes,
                         const pqg_zstd_job* d_jobs, int n_jobs, int32_t* d_status) {
   if (!ctx || n_jobs < 0) return PQG_ERR_INVALID_ARG;

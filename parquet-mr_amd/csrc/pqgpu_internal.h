@@ -127,6 +127,8 @@ hipError_t launch_snappy(hipStream_t st, const uint8_t* src, uint64_t src_bytes,
                          const void* jobs, int n_jobs, int32_t* status);
 hipError_t launch_lz4raw(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
                          const void* jobs, int n_jobs, int32_t* status);
+hipError_t launch_gzip(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
+                       const void* jobs, int n_jobs, int32_t* status);
 // DELTA_BYTE_ARRAY prefix / suffix lengths (k_delta MODE 2: bsrc = prefix, blen = value length, aux;
 // dba_meta: per BIN_CHUNK-value chunk {suffix bytes before it, smallest prefix in it};
 // PageWork::reserved = 1 when a value is longer than DBA_VB: that page takes the serial copy)

@@ -20,16 +20,9 @@
 #include <stdint.h>
 
 #include "pqgpu_device.h"
+#include "pqgpu_lzexec.h"
 
 namespace pqg {
-
-constexpr uint32_t LZ_RING = 4096;  // LDS window of the most recent output bytes
-constexpr uint32_t LZ_RMASK = LZ_RING - 1;
-constexpr uint32_t LZ_SEG = 2048;   // LDS segment of the compressed block
-constexpr uint32_t LZ_CAP = 256;    // output bytes per batch
-constexpr uint32_t LZ_EL = 64;      // elements per batch
-constexpr uint32_t LZ_PIECE = 64;   // bytes per element at most
-constexpr uint32_t LZ_LIT = 0x80000000u;  // source tag of a literal byte (| its segment offset)
 
 struct Lz4JobDev {  // = pqg_snappy_job
   uint64_t src_offset;
@@ -69,32 +62,6 @@ __global__ __launch_bounds__(WAVE) void k_lz4raw(const uint8_t* __restrict__ src
     wave_sync();
   };
   auto in_seg = [&](uint32_t q) { return q >= lo && q < lo + LZ_SEG; };
-  typedef uint32_t __attribute__((may_alias)) u32a;
-  const u32a* ring32 = (const u32a*)ring;
-  auto ring4 = [&](uint32_t t) -> uint32_t {  // ring bytes of output positions t .. t + 3 (the ring wraps)
-    const uint32_t r = t & LZ_RMASK & ~3u;
-    return __builtin_amdgcn_alignbyte(ring32[((r + 4u) & LZ_RMASK) >> 2], ring32[r >> 2], t & 3u);
-  };
-  // output [a, e) (all in the ring) to HBM: aligned dwords, bytes at the ends
-  const uint32_t oal = (uint32_t)(uintptr_t)out & 3u;
-  auto flush = [&](uint32_t a, uint32_t e) {
-    const uint32_t base = ((a + oal) & ~3u) - oal;
-    const uint32_t skip = a - base, span = e - base;
-    for (uint32_t d0 = 0; d0 < span; d0 += 4u * WAVE) {
-      const uint32_t d = d0 + 4u * lane;
-      if (d < span) {
-        const uint32_t t = base + d, v = ring4(t);
-        if (d >= skip && d + 4u <= span) {
-          gst((uint32_t*)(out + t), v);
-        } else {
-#pragma unroll
-          for (uint32_t j = 0; j < 4u; j++)
-            if (d + j >= skip && d + j < span) gst(out + (t + j), (uint8_t)(v >> (8u * j)));
-        }
-      }
-    }
-  };
-
   int code = n == 0u ? PQG_ERR_CORRUPT : 0;  // an empty output is the single byte 0, never no bytes
   // byte q of the block (uniform q): from the segment, else a buffer load (rare: header bytes past the
   // segment inside a batch, whose literal elements still point into the segment)
@@ -198,65 +165,7 @@ __global__ __launch_bounds__(WAVE) void k_lz4raw(const uint8_t* __restrict__ src
     T = uni(T);
     wave_sync();
     if (m) {
-      // ---- the source of every output byte of the batch
-      const uint32_t es = lane < m ? e_src[lane] : 0u, el = lane < m ? e_len[lane] : 0u;
-      uint32_t tot;
-      const uint32_t eo = wave_excl_scan_u32(el, &tot);
-      for (uint32_t i = 0; i < el; i++) sS[eo + i] = es + i;  // literal: segment byte; copy: output position
-      wave_sync();
-      constexpr uint32_t NB = LZ_CAP / WAVE;
-      uint32_t sv[NB];
-#pragma unroll
-      for (uint32_t j = 0; j < NB; j++) {
-        const uint32_t b = lane + WAVE * j;
-        sv[j] = b < T ? sS[b] : LZ_LIT;
-      }
-#pragma unroll 1
-      for (uint32_t r = 0; r < 12u; r++) {  // copies of copies inside the batch
-        bool more = false, hop = false;
-#pragma unroll
-        for (uint32_t j = 0; j < NB; j++) {
-          const bool inb = !(sv[j] & LZ_LIT) && sv[j] >= op;
-          const uint32_t nv = sS[(sv[j] - op) & (LZ_CAP - 1u)];
-          sv[j] = inb ? nv : sv[j];
-          hop |= inb;
-          more |= inb && !(nv & LZ_LIT) && nv >= op;
-        }
-        if (!__ballot(hop)) break;
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (uint32_t j = 0; j < NB; j++) sS[lane + WAVE * j] = sv[j];
-        wave_sync();
-        if (!__ballot(more)) break;
-      }
-      uint32_t bv[NB];
-      bool far = false;
-#pragma unroll
-      for (uint32_t j = 0; j < NB; j++) {
-        const uint32_t v = sv[j];
-        const uint32_t lit = seg[v & (LZ_SEG - 1u)], rg = ring[v & LZ_RMASK];
-        bv[j] = (v & LZ_LIT) ? lit : rg;
-        far |= lane + WAVE * j < T && !(v & LZ_LIT) && v + LZ_RING < op + T + WAVE;
-      }
-      if (__ballot(far)) {  // older than the ring: from HBM, after this wave's stores completed
-        __builtin_amdgcn_s_waitcnt(0);
-#pragma unroll
-        for (uint32_t j = 0; j < NB; j++) {
-          const uint32_t v = sv[j];
-          if (lane + WAVE * j < T && !(v & LZ_LIT) && v + LZ_RING < op + T + WAVE) {
-            const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(ro, (int)(v & ~3u), 0, 0);
-            bv[j] = (w >> ((v & 3u) * 8u)) & 0xFFu;
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (uint32_t j = 0; j < NB; j++) {
-        const uint32_t b = lane + WAVE * j;
-        if (b < T) ring[(op + b) & LZ_RMASK] = (uint8_t)bv[j];
-      }
-      wave_sync();
-      flush(op, op + T);
+      lz_exec_batch(ring, seg, sS, e_src, e_len, m, T, op, out, ro);
       op += T;
     }
     if (done && !lit_left && !match_left) break;

@@ -142,4 +142,4 @@ def build_batch(chunks, align=ALIGN):
                      column_values=col_vals)
 
 
-UNCOMPRESSED, SNAPPY, ZSTD, LZ4_RAW = 0, 1, 6, 7   # parquet.thrift CompressionCodec
+UNCOMPRESSED, SNAPPY, GZIP, ZSTD, LZ4_RAW = 0, 1, 2, 6, 7   # parquet.thrift CompressionCodec

@@ -146,10 +146,11 @@ class Decoder:
 
     _CODEC_FN = {batch.SNAPPY: ("pqg_snappy_decompress", "pqg_snappy_sync", "snappy block"),
                  batch.ZSTD: ("pqg_zstd_decompress", "pqg_zstd_sync", "zstd frame"),
-                 batch.LZ4_RAW: ("pqg_lz4_raw_decompress", "pqg_lz4_raw_sync", "lz4_raw block")}
+                 batch.LZ4_RAW: ("pqg_lz4_raw_decompress", "pqg_lz4_raw_sync", "lz4_raw block"),
+                 batch.GZIP: ("pqg_gzip_decompress", "pqg_gzip_sync", "gzip stream")}
 
     def upload_chunks(self, chunks):
-        """Column chunks whose pages may be SNAPPY-, ZSTD- or LZ4_RAW-compressed -> a DeviceBatch of
+        """Column chunks whose pages may be SNAPPY-, GZIP-, ZSTD- or LZ4_RAW-compressed -> a DeviceBatch of
         uncompressed pages.
 
         The batch is laid out for the uncompressed pages (batch.build_batch over placeholders of
@@ -264,6 +265,10 @@ class Decoder:
     def lz4_raw_decompress(self, blocks, sizes, skew=False):
         """Raw LZ4 blocks (host bytes) -> as snappy_decompress, by pqg_lz4_raw_decompress."""
         return self._block_jobs("pqg_lz4_raw_decompress", "pqg_lz4_raw_sync", blocks, sizes, skew)
+
+    def gzip_decompress(self, blocks, sizes, skew=False):
+        """GZIP streams (host bytes) -> as snappy_decompress, by pqg_gzip_decompress."""
+        return self._block_jobs("pqg_gzip_decompress", "pqg_gzip_sync", blocks, sizes, skew)
 
     def _block_jobs(self, fn, fn_sync, blocks, sizes, skew):
         src, soff, pos = [], [], 0

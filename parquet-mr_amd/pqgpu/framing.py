@@ -3,7 +3,7 @@
 Restates what parquet-mr's ParquetFileReader.Chunk.readAllPages does for one
 column chunk (parquet-hadoop/.../ParquetFileReader.java:1824-1979) with the
 header read by Util.readPageHeader (parquet-format-structures/.../Util.java:127-131,
-Thrift TCompactProtocol). Chunks are UNCOMPRESSED, SNAPPY, ZSTD or LZ4_RAW (ColumnMetaData.codec):
+Thrift TCompactProtocol). Chunks are UNCOMPRESSED, SNAPPY, GZIP, ZSTD or LZ4_RAW (ColumnMetaData.codec):
 compressed pages keep their compressed bodies (codec / uncompressed_size on the Page) and are
 decompressed on the GPU by Decoder.upload_chunks (pqg_snappy_decompress / pqg_zstd_decompress).
 The C-ABI form of the same walk is pqg_frame_chunk (frame_chunk_native below). The result is a
@@ -169,8 +169,8 @@ def read_column_chunk(buf, start, length, physical_type, max_def=0, max_rep=0, t
         h, body = read_page_header(buf, pos)
         size = h["compressed_page_size"]
         usize = h.get("uncompressed_page_size", size)
-        if codec not in (0, 1, 6, 7):
-            raise ThriftError(f"codec {codec} is not supported (UNCOMPRESSED, SNAPPY, ZSTD and LZ4_RAW are)")
+        if codec not in (0, 1, 2, 6, 7):
+            raise ThriftError(f"codec {codec} is not supported (UNCOMPRESSED, SNAPPY, GZIP, ZSTD and LZ4_RAW are)")
         # UNCOMPRESSED: CodecFactory.NO_OP_DECOMPRESSOR hands the page bytes on as they are, whatever
         # uncompressed_page_size says (CodecFactory.java:60-83); the codec alone decides (pqg_pages_from_headers)
         data = bytes(buf[body:body + size])

@@ -22,7 +22,7 @@ EXPORTS = [
     "pqg_page_errors", "pqg_plan_page_errors", "pqg_host_input", "pqg_decode_staged", "pqg_staged_column",
     "pqg_copy_out", "pqg_assemble", "pqg_assemble_schema",
     "pqg_snappy_decompress", "pqg_snappy_sync", "pqg_zstd_decompress", "pqg_zstd_sync",
-    "pqg_lz4_raw_decompress", "pqg_lz4_raw_sync", "pqg_crc32", "pqg_frame_chunk", "pqg_pages_from_headers",
+    "pqg_lz4_raw_decompress", "pqg_lz4_raw_sync", "pqg_gzip_decompress", "pqg_gzip_sync", "pqg_crc32", "pqg_frame_chunk", "pqg_pages_from_headers",
     # include/pqgpu_reader.h (the ValuesReader contract over a decoded batch)
     "pqg_vr_init_from_page", "pqg_vr_remaining", "pqg_vr_read_dictionary_id", "pqg_vr_read_boolean",
     "pqg_vr_read_integer", "pqg_vr_read_long", "pqg_vr_read_float", "pqg_vr_read_double", "pqg_vr_read_bytes",
@@ -86,6 +86,8 @@ def lib():
         L.pqg_zstd_sync.argtypes = [vp, vp, i32, C.POINTER(abi.Status)]
         L.pqg_lz4_raw_decompress.argtypes = [vp, vp, u64, vp, u64, vp, i32, vp]
         L.pqg_lz4_raw_sync.argtypes = [vp, vp, i32, C.POINTER(abi.Status)]
+        L.pqg_gzip_decompress.argtypes = [vp, vp, u64, vp, u64, vp, i32, vp]
+        L.pqg_gzip_sync.argtypes = [vp, vp, i32, C.POINTER(abi.Status)]
         L.pqg_crc32.argtypes = [C.c_uint32, vp, u64]
         L.pqg_crc32.restype = C.c_uint32
         L.pqg_frame_chunk.argtypes = [vp, u64, C.c_int64, i32, vp, i32, C.POINTER(i32), C.POINTER(abi.Status)]

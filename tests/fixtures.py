@@ -26,8 +26,8 @@ def load_chunk(name, c):
     buf = np.fromfile(os.path.join(GOLDEN, name + ".parquet"), dtype=np.uint8)
     ptype = framing.TYPE_BY_NAME[c["physical_type"]]
     # (pyarrow names the LZ4_RAW codec it writes "LZ4")
-    codec = {"SNAPPY": writer.SNAPPY, "ZSTD": writer.ZSTD, "LZ4": writer.LZ4_RAW,
-             "LZ4_RAW": writer.LZ4_RAW}.get(c.get("compression"), writer.UNCOMPRESSED)
+    codec = {"SNAPPY": writer.SNAPPY, "ZSTD": writer.ZSTD, "LZ4": writer.LZ4_RAW, "LZ4_RAW": writer.LZ4_RAW,
+             "GZIP": writer.GZIP}.get(c.get("compression"), writer.UNCOMPRESSED)
     ch = framing.read_column_chunk(buf, c["start"], c["length"], ptype, max_def=c["max_def"], max_rep=c["max_rep"],
                                    type_length=c["type_length"], num_values=c["num_values"], codec=codec)
     exp = np.load(os.path.join(GOLDEN, name + ".npz"))
@@ -51,12 +51,12 @@ def is_compressed(ch):
 
 
 def decompressed_on_host(ch):
-    """The chunk with every SNAPPY / ZSTD / LZ4_RAW page decompressed by the ORACLE (test infrastructure)."""
+    """The chunk with every SNAPPY / ZSTD / LZ4_RAW / GZIP page decompressed by the ORACLE (test infrastructure)."""
     import copy
 
     from oracle import pqref
     unzs = {writer.ZSTD: pqref.zstd_decompress, writer.SNAPPY: pqref.snappy_decompress,
-            writer.LZ4_RAW: pqref.lz4_raw_decompress}
+            writer.LZ4_RAW: pqref.lz4_raw_decompress, writer.GZIP: pqref.gzip_decompress}
     out = copy.deepcopy(ch)
     if out.dict_codec:
         unz = unzs[out.dict_codec]

@@ -278,6 +278,35 @@ def write_arrow_lz4_fixtures():
     return out
 
 
+def write_arrow_gzip_fixtures():
+    """GZIP-compressed chunks (parquet-mr's GZIP codec: Hadoop GzipCodec, gzip members): the LZ4_RAW
+    fixtures' table, V1 and V2 pages, through the device GZIP decoder."""
+    rng = np.random.default_rng(80)
+    n = 12000
+    runs = np.minimum(rng.zipf(1.6, size=n), 200)
+    ids = np.repeat(rng.integers(0, 300, size=n), runs)[:n]
+    valid = rng.random(n) > 0.15
+    words = [f"w{i:04d}-{'x' * (i % 17)}" for i in range(300)]
+    t = pa.table({
+        "dict_i64": pa.array(rng.integers(-2**60, 2**60, size=300)[ids], type=pa.int64()),
+        "opt_plain_f64": pa.array(rng.standard_normal(n), mask=~valid),
+        "delta_i64": pa.array(np.cumsum(rng.integers(-50, 5000, size=n)).astype(np.int64)),
+        "dict_str": pa.array([words[i] for i in ids]),
+        "opt_plain_str": pa.array([words[i][: 3 + i % 9] for i in rng.integers(0, 300, size=n)], mask=~valid),
+        "plain_i64": pa.array(np.cumsum(rng.integers(-100, 1000, size=n)).astype(np.int64)),
+    })
+    out = []
+    for ver in ("1.0", "2.0"):
+        name = f"arrow_gzip_v{ver[0]}"
+        pq.write_table(t, os.path.join(HERE, name + ".parquet"), data_page_version=ver, compression="GZIP",
+                       use_dictionary=["dict_i64", "dict_str"],
+                       column_encoding={"opt_plain_f64": "PLAIN", "delta_i64": "DELTA_BINARY_PACKED",
+                                        "opt_plain_str": "PLAIN", "plain_i64": "PLAIN"},
+                       data_page_size=8 * 1024, row_group_size=n, write_page_index=False)
+        out.append(name)
+    return out
+
+
 def write_arrow_bool_rle_fixtures():
     """BOOLEAN values with the RLE encoding (4-byte length + width-1 hybrid stream; what
     parquet-mr's V2 writer emits for booleans, DefaultV2ValuesWriterFactory.getBooleanValuesWriter):
@@ -326,7 +355,8 @@ def main():
         shutil.copyfile(src, dst)
         manifest[name] = {"source": f"reference:{rel}", "chunks": describe(dst, name, None)}
     for name in (write_arrow_fixtures() + write_arrow_binary_fixtures() + write_arrow_snappy_fixtures() +
-                 write_arrow_bool_rle_fixtures() + write_arrow_zstd_fixtures() + write_arrow_lz4_fixtures()):
+                 write_arrow_bool_rle_fixtures() + write_arrow_zstd_fixtures() + write_arrow_lz4_fixtures() +
+                 write_arrow_gzip_fixtures()):
         manifest[name] = {"source": "pyarrow " + pa.__version__, "chunks": describe(os.path.join(HERE, name + ".parquet"),
                                                                                    name, None)}
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
@@ -339,6 +369,8 @@ if __name__ == "__main__":
         sys.exit(add_fixtures(write_arrow_snappy_fixtures))
     if "--zstd" in sys.argv:
         sys.exit(add_fixtures(write_arrow_zstd_fixtures))
+    if "--gzip" in sys.argv:
+        sys.exit(add_fixtures(write_arrow_gzip_fixtures))
     if "--lz4" in sys.argv:
         sys.exit(add_fixtures(write_arrow_lz4_fixtures))
     if "--bool-rle" in sys.argv:

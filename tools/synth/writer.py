@@ -26,8 +26,8 @@ from typing import List, Optional
 import numpy as np
 
 from pqgpu import abi
-from pqgpu.batch import (ALIGN, LZ4_RAW, PAD, SNAPPY, UNCOMPRESSED, ZSTD, ColumnChunk, Page,  # noqa: F401
-                          PageBatch, build_batch)
+from pqgpu.batch import (ALIGN, GZIP, LZ4_RAW, PAD, SNAPPY, UNCOMPRESSED, ZSTD, ColumnChunk,  # noqa: F401
+                          Page, PageBatch, build_batch)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
@@ -425,4 +425,24 @@ def lz4_raw_chunk(chunk):
         lv = pg.rl_byte_length + pg.dl_byte_length if pg.version == 2 else 0
         pg.body = pg.body[:lv] + codec.compress(pg.body[lv:], asbytes=True)
         pg.codec = LZ4_RAW
+    return out
+
+
+def gzip_chunk(chunk, level=6):
+    """A copy of `chunk` with every page (and the dictionary page) GZIP-compressed the way
+    parquet-mr writes GZIP column chunks (Hadoop GzipCodec: one gzip member per page; V1: the whole
+    body; V2: the data section). Compression by Python's zlib (test-data synthesis only)."""
+    import copy
+    import gzip
+
+    out = copy.deepcopy(chunk)
+    if out.dict_page is not None:
+        out.dict_uncompressed_size = len(out.dict_page)
+        out.dict_page = gzip.compress(out.dict_page, compresslevel=level)
+        out.dict_codec = GZIP
+    for pg in out.pages:
+        pg.uncompressed_size = len(pg.body)
+        lv = pg.rl_byte_length + pg.dl_byte_length if pg.version == 2 else 0
+        pg.body = pg.body[:lv] + gzip.compress(pg.body[lv:], compresslevel=level)
+        pg.codec = GZIP
     return out
