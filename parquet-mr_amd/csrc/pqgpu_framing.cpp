@@ -313,11 +313,11 @@ int pqg_pages_from_headers(const pqg_page_header* headers, int n_headers, int co
     // page (readDictionaryPage :313-316) always do; a V2 page only when is_compressed (:218, :232,
     // :253). UNCOMPRESSED is CodecFactory.NO_OP_DECOMPRESSOR (CodecFactory.java:60-83), whose
     // BytesInput form returns the bytes as they are. A compressed page must be decompressed first
-    // (pqg_snappy_decompress / pqg_zstd_decompress) into a layout of its own.
+    // (pqg_snappy / zstd / lz4_raw / gzip_decompress) into a layout of its own.
     const bool compressed = codec != PQG_CODEC_UNCOMPRESSED && (h.type != PQG_DATA_PAGE_V2 || h.is_compressed);
     if (compressed && (h.type == PQG_DICTIONARY_PAGE || h.type == PQG_DATA_PAGE || h.type == PQG_DATA_PAGE_V2)) {
       pqg_set_status(st, PQG_ERR_UNSUPPORTED, i, -1,
-                     "compressed page: decompress the chunk (pqg_snappy_decompress / pqg_zstd_decompress) and "
+                     "compressed page: decompress the chunk (pqg_snappy / zstd / lz4_raw / gzip_decompress) and "
                      "describe the decompressed pages");
       return PQG_ERR_UNSUPPORTED;
     }

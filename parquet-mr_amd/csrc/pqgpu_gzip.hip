@@ -28,17 +28,36 @@
 namespace pqg {
 
 constexpr uint32_t GZ_FAST = 9;  // first-level table bits
-constexpr uint16_t GZ_SLOW = 0xFFFFu;
+constexpr uint32_t GZ_SLOW = 0xFFFFFFFFu;
+
+// First-level table entry (codes of <= 9 bits; longer: GZ_SLOW): symbol | code length << 9, and for a
+// length symbol its base << 13 | extra bits << 22, for a distance symbol base << 13 | extra bits << 28
+// (no dependent table lookup between a symbol and its extra bits).
+__device__ __forceinline__ uint32_t gz_ent_sym(uint32_t e) { return e & 511u; }
+__device__ __forceinline__ uint32_t gz_ent_len(uint32_t e) { return (e >> 9) & 15u; }
+
+// Symbol-loop state between calls of gz_symbols (LDS; SGPRs inside the call)
+struct GzState {
+  uint64_t src, src_len;  // the job's input
+  uint64_t bb;            // bit container: bc bits, LSB first; p = next input byte to load
+  uint32_t bc, p, lo, n;  // lo: the LDS segment holds input [lo, lo + LZ_SEG)
+  uint32_t at, ulen, mstart;  // output position of the batch, page size, member's first output byte
+  uint32_t cdist, clen, cfull;  // a match carried into the next batch (cfull: it completes the page)
+  uint32_t m, T, res;     // result: elements, bytes; 0 batch full, 1 end of block, 2 page complete, 3 corrupt
+};
 
 struct GzLds {
   uint8_t ring[LZ_RING];
   uint8_t lits[LZ_SEG];
-  uint8_t seg[LZ_SEG];  // compressed bytes [lo, lo + LZ_SEG)
+  uint8_t seg[LZ_SEG + 16];  // compressed bytes [lo, lo + LZ_SEG)
   uint32_t sS[LZ_CAP];
   uint32_t e_src[LZ_EL], e_len[LZ_EL];
-  uint16_t lfast[1u << GZ_FAST], dfast[1u << GZ_FAST];  // symbol | length << 9
+  uint32_t lfast[1u << GZ_FAST], dfast[1u << GZ_FAST];
+  uint32_t lentab[32], disttab[32];  // base | extra bits << 16 (length symbols 257.., distance symbols)
   int16_t lcount[16], lsym[320], dcount[16], dsym[32], ccount[16], csym[32];
   uint8_t lens[320 + 32];
+  uint8_t ord[20];
+  GzState st;
 };
 
 __constant__ uint16_t GZ_LBASE[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
@@ -50,9 +69,11 @@ __constant__ uint8_t GZ_DEXT[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
 __constant__ uint8_t GZ_ORD[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // Canonical Huffman tables of lens[0 .. n) (RFC 1951 3.2.2): counts, symbols in canonical order and,
-// when `fast`, the first-level table (bit-reversed codes of <= 9 bits -> symbol | length << 9).
-// Returns left (0: complete, > 0: incomplete) or -1 (over-subscribed). All lanes.
-__device__ int gz_build(const uint8_t* lens, int n, int16_t* count, int16_t* sym, uint16_t* fast) {
+// when `fast`, the first-level table (bit-reversed codes of <= 9 bits). kind 0: literal / length
+// table (ext = lentab), 1: distance table (ext = disttab). Returns left (0: complete, > 0: incomplete)
+// or -1 (over-subscribed). All lanes.
+__device__ int gz_build(const uint8_t* lens, int n, int16_t* count, int16_t* sym, uint32_t* fast, int kind,
+                        const uint32_t* ext) {
   const uint32_t lane = lane_id();
   uint32_t cnt[16];
 #pragma unroll
@@ -104,14 +125,200 @@ __device__ int gz_build(const uint8_t* lens, int n, int16_t* count, int16_t* sym
     if (s < n && l) {
       sym[base_o + rank] = (int16_t)s;
       if (fast && l <= GZ_FAST) {
-        const uint32_t c = base_c + rank;                    // MSB-first code
+        uint32_t e = (uint32_t)s | (l << 9);
+        if (kind == 0 && s > 256 && s < 286) {
+          const uint32_t t = ext[s - 257];
+          e |= ((t & 0x1FFu) << 13) | ((t >> 16) << 22);
+        } else if (kind == 1 && s < 30) {
+          const uint32_t t = ext[s];
+          e |= ((t & 0x7FFFu) << 13) | ((t >> 16) << 28);
+        }
+        const uint32_t c = base_c + rank;                            // MSB-first code
         const uint32_t rv = __builtin_bitreverse32(c) >> (32u - l);  // as the LSB-first reader sees it
-        for (uint32_t k = 0; k < (1u << (GZ_FAST - l)); k++) fast[rv | (k << l)] = (uint16_t)(s | (l << 9));
+        for (uint32_t k = 0; k < (1u << (GZ_FAST - l)); k++) fast[rv | (k << l)] = e;
       }
     }
   }
   wave_sync();
   return left;
+}
+
+// Input segment: bytes [q & ~15, + LZ_SEG) of the job's input into LDS (all lanes).
+__device__ __forceinline__ uint32_t gz_fill(GzLds& L, rsrc_t rs, uint32_t q) {
+  const uint32_t lo = uni(q & ~15u);
+#pragma unroll
+  for (uint32_t i = 0; i < LZ_SEG; i += 16u * WAVE) {
+    const uint32_t o = i + 16u * lane_id();
+    *(u32x4*)(L.seg + o) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lo + o), 0, 0);
+  }
+  wave_sync();
+  return lo;
+}
+
+// The symbols of a Huffman block, one batch (<= LZ_EL elements, <= LZ_CAP bytes) per call, into
+// L.e_src / e_len / lits; L.st.res says why it returned. A function of its own so that its state
+// stays in SGPRs (the ZSTD sequence loop's lesson: inlined into the job's code, the uniform state
+// was spilled to VGPR lanes). Elements and literal bytes are staged in VGPRs (lane k: element k,
+// literal byte k + 64 j) and written to LDS once per batch.
+__device__ __attribute__((noinline)) void gz_symbols(GzLds& L) {
+  GzState& S = L.st;
+  const uint32_t lane = lane_id();
+  const rsrc_t rs = make_rsrc((const uint8_t*)uni64(S.src), uni64(S.src_len));
+  uint64_t bb = uni64(S.bb);
+  uint32_t bc = uni(S.bc), p = uni(S.p), lo = uni(S.lo);
+  const uint32_t n = uni(S.n), ulen = uni(S.ulen), mstart = uni(S.mstart), op = uni(S.at);
+  const uint64_t nbits = (uint64_t)n * 8u;
+  typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
+  uint32_t m = 0, T = 0, res = 0, run = 0;  // run: bytes of the open literal element
+  uint32_t es = 0, el = 0, lv0 = 0, lv1 = 0, lv2 = 0, lv3 = 0;
+  uint32_t cdist = 0, clen = 0, cfull = 0;
+  auto refill = [&]() {
+    if (bc <= 32u) {
+      if (p < lo || p + 4u > lo + LZ_SEG) lo = gz_fill(L, rs, p);
+      uint32_t w = uni(*(const u32u*)(L.seg + (p - lo)));
+      if (p + 4u > n) w = p >= n ? 0u : w & (0xFFFFFFFFu >> (8u * (p + 4u - n)));
+      bb |= (uint64_t)w << bc;
+      bc += 32u;
+      p += 4u;
+    }
+  };
+  auto take_bits = [&](uint32_t k) -> uint32_t {  // k <= 15, after a refill
+    const uint32_t v = (uint32_t)bb & ((1u << k) - 1u);
+    bb >>= k;
+    bc -= k;
+    return v;
+  };
+  auto slow = [&](const int16_t* count, const int16_t* sym) -> int {  // codes of 10-15 bits
+    int c = 0, first = 0, index = 0;
+    for (int l = 1; l < 16; l++) {
+      c |= (int)take_bits(1);
+      const int k = (int)uni((uint32_t)(int32_t)count[l]);
+      if (c - k < first) return (int)uni((uint32_t)(int32_t)sym[index + (c - first)]);
+      index += k;
+      first = (first + k) << 1;
+      c <<= 1;
+    }
+    return -1;
+  };
+  auto close = [&]() {
+    if (run) {
+      es = lane == m ? (LZ_LIT | (T - run)) : es;
+      el = lane == m ? run : el;
+      m++;
+      run = 0;
+    }
+  };
+  // a back-reference in pieces of <= LZ_PIECE bytes, as many as the batch holds; returns the rest
+  auto put_match = [&](uint32_t dist, uint32_t len) -> uint32_t {
+    close();
+    while (len && m < LZ_EL && T < LZ_CAP) {
+      uint32_t t = len < LZ_PIECE ? len : LZ_PIECE;
+      t = t < LZ_CAP - T ? t : LZ_CAP - T;
+      es = lane == m ? op + T - dist : es;
+      el = lane == m ? t : el;
+      m++;
+      T += t;
+      len -= t;
+    }
+    return len;
+  };
+  // (literal bytes sit at their batch offset: lits[T] for the byte of output op + T)
+  if (uni(S.clen)) {
+    const uint32_t d = uni(S.cdist), f = uni(S.cfull);
+    const uint32_t rest = put_match(d, uni(S.clen));
+    if (rest) {
+      cdist = d;
+      clen = rest;
+      cfull = f;
+    } else if (f) {
+      res = 2;
+    }
+  }
+  if (!clen && res == 0) {
+    while (true) {
+      if (m + (run ? 1u : 0u) >= LZ_EL || T >= LZ_CAP) break;  // batch full
+      refill();
+      uint32_t e = uni(L.lfast[(uint32_t)bb & ((1u << GZ_FAST) - 1u)]);
+      uint32_t sym;
+      if (e != GZ_SLOW) {
+        const uint32_t l = gz_ent_len(e);
+        bb >>= l;
+        bc -= l;
+        sym = gz_ent_sym(e);
+      } else {
+        refill();
+        const int s = slow(L.lcount, L.lsym);
+        if (s < 0) { res = 3; break; }
+        sym = (uint32_t)s;
+        e = sym < 257u || sym > 285u ? sym : sym | ((uni(L.lentab[sym - 257u]) & 0x1FFu) << 13) |
+                                                   ((uni(L.lentab[sym - 257u]) >> 16) << 22);
+      }
+      if ((uint64_t)p * 8u - bc > nbits) { res = 3; break; }
+      if (sym < 256u) {
+        if (op + T >= ulen) { res = 2; break; }
+        if (run == LZ_PIECE) close();
+        const uint32_t j = T >> 6;
+        const bool me = lane == (T & 63u);
+        lv0 = me && j == 0 ? sym : lv0;
+        lv1 = me && j == 1 ? sym : lv1;
+        lv2 = me && j == 2 ? sym : lv2;
+        lv3 = me && j == 3 ? sym : lv3;
+        T++;
+        run++;
+        continue;
+      }
+      if (sym == 256u) { res = 1; break; }
+      if (sym > 285u) { res = 3; break; }
+      refill();
+      uint32_t len = ((e >> 13) & 0x1FFu) + take_bits((e >> 22) & 7u);
+      uint32_t d = uni(L.dfast[(uint32_t)bb & ((1u << GZ_FAST) - 1u)]);
+      if (d != GZ_SLOW) {
+        const uint32_t l = gz_ent_len(d);
+        bb >>= l;
+        bc -= l;
+      } else {
+        const int s = slow(L.dcount, L.dsym);
+        if (s < 0 || s >= 30) { res = 3; break; }
+        const uint32_t t = uni(L.disttab[s]);
+        d = (uint32_t)s | ((t & 0x7FFFu) << 13) | ((t >> 16) << 28);
+      }
+      if (gz_ent_sym(d) >= 30u) { res = 3; break; }
+      refill();
+      const uint32_t dist = ((d >> 13) & 0x7FFFu) + take_bits(d >> 28);
+      if ((uint64_t)p * 8u - bc > nbits) { res = 3; break; }
+      const uint32_t at = op + T;
+      if (dist > at - mstart) { res = 3; break; }
+      uint32_t full = 0;
+      if (len > ulen - at) {  // the page completes inside this match
+        len = ulen - at;
+        full = 1;
+      }
+      const uint32_t rest = len ? put_match(dist, len) : 0u;
+      if (rest) {
+        cdist = dist;
+        clen = rest;
+        cfull = full;
+        break;
+      }
+      if (full) { res = 2; break; }
+    }
+  }
+  close();
+  // literal bytes at their batch offsets, elements in lanes
+  if (lane < T) L.lits[lane] = (uint8_t)lv0;
+  if (lane + 64u < T) L.lits[lane + 64u] = (uint8_t)lv1;
+  if (lane + 128u < T) L.lits[lane + 128u] = (uint8_t)lv2;
+  if (lane + 192u < T) L.lits[lane + 192u] = (uint8_t)lv3;
+  if (lane < m) {
+    L.e_src[lane] = es;
+    L.e_len[lane] = el;
+  }
+  if (lane == 0) {
+    S.bb = bb; S.bc = bc; S.p = p; S.lo = lo;
+    S.cdist = cdist; S.clen = clen; S.cfull = cfull;
+    S.m = m; S.T = T; S.res = res;
+  }
+  wave_sync();
 }
 
 struct GzJobDev {  // = pqg_snappy_job
@@ -138,29 +345,31 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
   const rsrc_t rs = make_rsrc(src + J.src_offset, src_bytes - J.src_offset);
   const rsrc_t ro = make_rsrc(dst + J.dst_offset, dst_bytes - J.dst_offset);
   uint8_t* out = dst + J.dst_offset;
-  typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
   const uint64_t nbits = (uint64_t)n * 8u;
-  uint32_t lo = 0x80000000u;  // segment = member bytes [lo, lo + LZ_SEG)
-  auto fill = [&](uint32_t q) {
-    lo = uni(q & ~15u);
-#pragma unroll
-    for (uint32_t i = 0; i < LZ_SEG; i += 16u * WAVE) {
-      const uint32_t o = i + 16u * lane;
-      *(u32x4*)(L.seg + o) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lo + o), 0, 0);
-    }
-    wave_sync();
-  };
+  // length / distance bases and extra bits, and the code-length order, in LDS (a __constant__
+  // table indexed per symbol is a vector memory load whose wait also waits for the output stores)
+  if (lane < 29u) L.lentab[lane] = GZ_LBASE[lane] | ((uint32_t)GZ_LEXT[lane] << 16);
+  if (lane < 30u) L.disttab[lane] = GZ_DBASE[lane] | ((uint32_t)GZ_DEXT[lane] << 16);
+  if (lane < 19u) L.ord[lane] = GZ_ORD[lane];
+  if (lane == 0) {
+    L.st.src = (uint64_t)(uintptr_t)(src + J.src_offset);
+    L.st.src_len = src_bytes - J.src_offset;
+    L.st.n = n;
+    L.st.ulen = ulen;
+  }
+  wave_sync();
+  uint32_t lo = 0x80000000u;  // segment = input bytes [lo, lo + LZ_SEG)
   auto byte_at = [&](uint32_t q) -> uint32_t {  // byte q of the input (0 past its end)
     return q < n ? uni((ld32(rs, q & ~3u) >> ((q & 3u) * 8u)) & 0xFFu) : 0u;
   };
-  // bit reader: the container bb holds bc bits; p = next byte to load. Bytes past n read as 0 (the
-  // buffer resource returns 0 past the job's range only at the end of `src`, so they are masked):
-  // reading past the input shows as consumed() > nbits, checked after every symbol.
+  // bit reader of the block headers and code lengths (the symbol loop has its own, in gz_symbols):
+  // bytes past n read as 0; reading past the input shows as consumed() > nbits
   uint32_t p = 0, bc = 0;
   uint64_t bb = 0;
+  typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
   auto refill = [&]() {
     while (bc <= 32u) {
-      if (p < lo || p + 4u > lo + LZ_SEG) fill(p);
+      if (p < lo || p + 4u > lo + LZ_SEG) lo = gz_fill(L, rs, p);
       uint32_t w = uni(*(const u32u*)(L.seg + (p - lo)));
       if (p + 4u > n) w = p >= n ? 0u : w & (0xFFFFFFFFu >> (8u * (p + 4u - n)));
       bb |= (uint64_t)w << bc;
@@ -181,7 +390,6 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
     bb = 0;
     bc = 0;
   };
-  // canonical decode (RFC 1951 3.2.2 order): the code read bit by bit, MSB first
   auto decode_slow = [&](const int16_t* count, const int16_t* sym) -> int {
     int c = 0, first = 0, index = 0;
     for (int l = 1; l < 16; l++) {
@@ -194,69 +402,18 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
     }
     return -1;
   };
-  auto decode = [&](const uint16_t* fast, const int16_t* count, const int16_t* sym) -> int {
-    refill();
-    const uint32_t e = uni((uint32_t)fast[bb & ((1u << GZ_FAST) - 1u)]);
-    if (e != GZ_SLOW) {
-      const uint32_t l = e >> 9;
-      bb >>= l;
-      bc -= l;
-      return (int)(e & 511u);
-    }
-    return decode_slow(count, sym);
-  };
 
-  // ---- output batches (pqgpu_lzexec.h)
-  uint32_t op = 0;                // output bytes executed
-  uint32_t m = 0, T = 0, nl = 0;  // batch: elements, output bytes, literal bytes
-  bool open = false;              // the batch's last element is a literal run still growing
-  auto exec = [&]() {
+  uint32_t op = 0;  // output bytes written
+  auto exec = [&](uint32_t m, uint32_t T) {
     if (m) {
-      wave_sync();
       lz_exec_batch(L.ring, L.lits, L.sS, L.e_src, L.e_len, m, T, op, out, ro);
       op += T;
     }
-    m = 0;
-    T = 0;
-    nl = 0;
-    open = false;
   };
-  auto put_lit = [&](uint32_t b) {
-    if (m >= LZ_EL || T >= LZ_CAP) exec();
-    if (lane == 0) {
-      L.lits[nl] = (uint8_t)b;
-      if (open) {
-        L.e_len[m - 1u] += 1u;
-      } else {
-        L.e_src[m] = LZ_LIT | nl;
-        L.e_len[m] = 1u;
-      }
-    }
-    if (!open) m++;
-    nl++;
-    T++;
-    open = (T & (LZ_PIECE - 1u)) != 0u;  // literal elements end at 64-byte steps of the batch
-  };
-  auto put_match = [&](uint32_t dist, uint32_t len) {
-    open = false;
-    while (len) {
-      if (m >= LZ_EL || T >= LZ_CAP) exec();
-      uint32_t take = len < LZ_PIECE ? len : LZ_PIECE;
-      take = take < LZ_CAP - T ? take : LZ_CAP - T;
-      if (lane == 0) {
-        L.e_src[m] = op + T - dist;
-        L.e_len[m] = take;
-      }
-      m++;
-      T += take;
-      len -= take;
-    }
-  };
-
   int code = 0;
   bool full = false;  // a symbol past the page's size was decoded: reading stops there
   uint32_t q = 0;     // byte position of the next member
-  while (!code && op + T < ulen) {
+  while (!code && op < ulen) {
     // ---- member header (RFC 1952 2.3)
     if (q >= n) { code = PQG_ERR_EOF; break; }  // the stream ends before the page's size
     if (q + 10u > n) { code = PQG_ERR_CORRUPT; break; }
@@ -275,7 +432,7 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
     if (flg & 2u) q += 2u;
     if (q > n) { code = PQG_ERR_CORRUPT; break; }
     restart(q);
-    const uint32_t member_start = op + T;
+    const uint32_t member_start = op;
     // ---- DEFLATE blocks (RFC 1951 3.2.3)
     uint32_t last = 0;
     do {
@@ -289,7 +446,6 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
         if (len != (~nlen & 0xFFFFu) || at + 4u + len > n) { code = PQG_ERR_CORRUPT; break; }
         uint32_t s = at + 4u, left = len;
         while (left) {  // up to 256 bytes a batch, straight into the literal buffer
-          exec();
           if (op >= ulen) { full = true; break; }
           uint32_t take = left < LZ_CAP ? left : LZ_CAP;
           take = take < ulen - op ? take : ulen - op;
@@ -297,13 +453,13 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
             const uint32_t b = s + i;
             L.lits[i] = (uint8_t)(ld32(rs, b & ~3u) >> ((b & 3u) * 8u));
           }
-          if (lane < (take + LZ_PIECE - 1u) / LZ_PIECE) {
+          const uint32_t m = (take + LZ_PIECE - 1u) / LZ_PIECE;
+          if (lane < m) {
             L.e_src[lane] = LZ_LIT | (lane * LZ_PIECE);
             L.e_len[lane] = take - lane * LZ_PIECE < LZ_PIECE ? take - lane * LZ_PIECE : LZ_PIECE;
           }
-          m = (take + LZ_PIECE - 1u) / LZ_PIECE;
-          T = take;
-          exec();
+          wave_sync();
+          exec(m, take);
           s += take;
           left -= take;
         }
@@ -315,8 +471,8 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
         for (uint32_t s = lane; s < 288u + 30u; s += WAVE)
           L.lens[s] = s < 144u ? 8 : s < 256u ? 9 : s < 280u ? 7 : s < 288u ? 8 : 5;
         wave_sync();
-        gz_build(L.lens, 288, L.lcount, L.lsym, L.lfast);
-        gz_build(L.lens + 288, 30, L.dcount, L.dsym, L.dfast);
+        gz_build(L.lens, 288, L.lcount, L.lsym, L.lfast, 0, L.lentab);
+        gz_build(L.lens + 288, 30, L.dcount, L.dsym, L.dfast, 1, L.disttab);
       } else {  // dynamic codes (RFC 1951 3.2.7)
         const uint32_t nlen = bits(5) + 257u, ndist = bits(5) + 1u, ncode = bits(4) + 4u;
         if (nlen > 286u || ndist > 30u) { code = PQG_ERR_CORRUPT; break; }
@@ -324,10 +480,13 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
         wave_sync();
         for (uint32_t i = 0; i < ncode; i++) {
           const uint32_t v = bits(3);
-          if (lane == 0) L.lens[GZ_ORD[i]] = (uint8_t)v;
+          if (lane == 0) L.lens[L.ord[i]] = (uint8_t)v;
         }
         wave_sync();
-        if (consumed() > nbits || gz_build(L.lens, 19, L.ccount, L.csym, nullptr) != 0) { code = PQG_ERR_CORRUPT; break; }
+        if (consumed() > nbits || gz_build(L.lens, 19, L.ccount, L.csym, nullptr, 0, nullptr) != 0) {
+          code = PQG_ERR_CORRUPT;
+          break;
+        }
         // the literal / length and distance code lengths (lens[0 .. 19) is free again: the
         // code-length code lives in ccount / csym)
         uint32_t idx = 0;
@@ -364,52 +523,43 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
         if (lane < 32u) L.lens[288u + lane] = (uint8_t)dl;
         wave_sync();
         // incomplete codes only when a single symbol is used (zlib's rule; pqr_gzip_decompress)
-        const int e1 = gz_build(L.lens, (int)nlen, L.lcount, L.lsym, L.lfast);
+        const int e1 = gz_build(L.lens, (int)nlen, L.lcount, L.lsym, L.lfast, 0, L.lentab);
         uint32_t used = 0;
         for (int l = 1; l < 16; l++) used += uni((uint32_t)(int32_t)L.lcount[l]);
         if (e1 < 0 || (e1 > 0 && used != 1u)) { code = PQG_ERR_CORRUPT; break; }
-        const int e2 = gz_build(L.lens + 288, (int)ndist, L.dcount, L.dsym, L.dfast);
+        const int e2 = gz_build(L.lens + 288, (int)ndist, L.dcount, L.dsym, L.dfast, 1, L.disttab);
         used = 0;
         for (int l = 1; l < 16; l++) used += uni((uint32_t)(int32_t)L.dcount[l]);
         if (e2 < 0 || (e2 > 0 && used > 1u)) { code = PQG_ERR_CORRUPT; break; }
       }
-      // ---- the block's symbols
-      while (true) {
-        const int sym = decode(L.lfast, L.lcount, L.lsym);
-        if (sym < 0 || consumed() > nbits) { code = PQG_ERR_CORRUPT; break; }
-        if (sym < 256) {
-          if (op + T >= ulen) { full = true; break; }
-          put_lit((uint32_t)sym);
-        } else if (sym == 256) {
-          break;
-        } else {
-          const uint32_t li = (uint32_t)sym - 257u;
-          if (li >= 29u) { code = PQG_ERR_CORRUPT; break; }
-          uint32_t len = GZ_LBASE[li] + bits(GZ_LEXT[li]);
-          const int ds = decode(L.dfast, L.dcount, L.dsym);
-          if (ds < 0 || ds >= 30) { code = PQG_ERR_CORRUPT; break; }
-          const uint32_t dist = GZ_DBASE[ds] + bits(GZ_DEXT[ds]);
-          if (consumed() > nbits) { code = PQG_ERR_CORRUPT; break; }
-          const uint32_t at = op + T;
-          if (dist > at - member_start) { code = PQG_ERR_CORRUPT; break; }
-          if (len > ulen - at) {  // the page completes inside this match
-            len = ulen - at;
-            full = true;
-          }
-          if (len) put_match(dist, len);
-          if (full) break;
-        }
+      // ---- the block's symbols, a batch per gz_symbols call
+      if (lane == 0) {
+        L.st.bb = bb; L.st.bc = bc; L.st.p = p; L.st.lo = lo;
+        L.st.mstart = member_start; L.st.clen = 0;
       }
+      uint32_t res = 0;
+      do {
+        if (lane == 0) L.st.at = op;
+        wave_sync();
+        gz_symbols(L);
+        res = uni(L.st.res);
+        if (res == 3u) { code = PQG_ERR_CORRUPT; break; }
+        exec(uni(L.st.m), uni(L.st.T));
+      } while (res == 0u);
+      bb = uni64(L.st.bb);
+      bc = uni(L.st.bc);
+      p = uni(L.st.p);
+      lo = uni(L.st.lo);
+      if (res == 2u) full = true;
     } while (!code && !full && !last);
-    if (code || full || op + T >= ulen) break;  // complete: the trailer is not read
+    if (code || full || op >= ulen) break;  // complete: the trailer is not read
     // ---- trailer of a member that ends before the page is complete: ISIZE (CRC-32 not recomputed)
     const uint32_t at = (uint32_t)((consumed() + 7u) >> 3);
     if (at + 8u > n) { code = PQG_ERR_CORRUPT; break; }
     const uint32_t isz = byte_at(at + 4u) | (byte_at(at + 5u) << 8) | (byte_at(at + 6u) << 16) | (byte_at(at + 7u) << 24);
-    if (isz != op + T - member_start) { code = PQG_ERR_CORRUPT; break; }
+    if (isz != op - member_start) { code = PQG_ERR_CORRUPT; break; }
     q = at + 8u;
   }
-  if (!code) exec();
   if (!code && op != ulen) code = PQG_ERR_EOF;
   if (lane == 0 && status) status[jb] = code;
 }

@@ -155,7 +155,7 @@ class Decoder:
 
         The batch is laid out for the uncompressed pages (batch.build_batch over placeholders of
         the uncompressed sizes), the compressed blocks are uploaded once, and
-        pqg_snappy_decompress / pqg_zstd_decompress write every block straight into its page's
+        the codec kernels (pqg_snappy / zstd / lz4_raw / gzip_decompress) write every block straight into its page's
         place in the batch on the GPU (ColumnChunkPageReadStore.readPage's decompress step).
         Raises PqgError(CORRUPT / EOF) with the failing block when a block is malformed or its
         length differs from the header."""

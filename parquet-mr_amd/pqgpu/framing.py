@@ -5,7 +5,7 @@ column chunk (parquet-hadoop/.../ParquetFileReader.java:1824-1979) with the
 header read by Util.readPageHeader (parquet-format-structures/.../Util.java:127-131,
 Thrift TCompactProtocol). Chunks are UNCOMPRESSED, SNAPPY, GZIP, ZSTD or LZ4_RAW (ColumnMetaData.codec):
 compressed pages keep their compressed bodies (codec / uncompressed_size on the Page) and are
-decompressed on the GPU by Decoder.upload_chunks (pqg_snappy_decompress / pqg_zstd_decompress).
+decompressed on the GPU by Decoder.upload_chunks (pqg_snappy / zstd / lz4_raw / gzip_decompress).
 The C-ABI form of the same walk is pqg_frame_chunk (frame_chunk_native below). The result is a
 batch.ColumnChunk whose pages feed batch.build_batch -> the device decoder.
 

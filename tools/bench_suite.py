@@ -15,6 +15,8 @@ bench.py prints the ONE headline line (C2). This suite times the other configs a
   bss_f64        BYTE_STREAM_SPLIT doubles
   delta_i64      DELTA_BINARY_PACKED int64 random walk
   delta_i64_2048 the same values with 2048-value blocks of 8 miniblocks (DuckDB's writer; the block-by-block path)
+  (on request) c2_snappy / c2_zstd / c2_lz4 / c2_gzip and plain_i64_{snappy,zstd,lz4,gzip}: the headline
+                 pages or an int64 random walk compressed with each codec (decompression timed alone too)
 
 value = non-null values decoded per second; gbps = algorithmic bytes (encoded page bytes read +
 decoded values / offsets / bytes written + level bytes written) / launch time. cpu = the oracle
@@ -88,6 +90,18 @@ def gen(name, rows):
     if name == "plain_i64_zstd":  # int64 random walk, PLAIN pages, ZSTD level 3
         walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
         return WL.Workload(name, [writer.zstd_chunk(writer.write_column_chunk(abi.INT64, walk, abi.PLAIN))], [E(walk)])
+    if name == "plain_i64_lz4":  # int64 random walk, PLAIN pages, LZ4_RAW
+        walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
+        return WL.Workload(name, [writer.lz4_raw_chunk(writer.write_column_chunk(abi.INT64, walk, abi.PLAIN))], [E(walk)])
+    if name == "c2_lz4":
+        w = WL.c2(rows)
+        return WL.Workload(name, [writer.lz4_raw_chunk(w.chunks[0])], w.expect)
+    if name == "plain_i64_gzip":  # int64 random walk, PLAIN pages, GZIP (zlib level 6, Hadoop's default)
+        walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
+        return WL.Workload(name, [writer.gzip_chunk(writer.write_column_chunk(abi.INT64, walk, abi.PLAIN))], [E(walk)])
+    if name == "c2_gzip":
+        w = WL.c2(rows)
+        return WL.Workload(name, [writer.gzip_chunk(w.chunks[0])], w.expect)
     if name == "delta_i64":
         walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
         return WL.Workload(name, [writer.write_column_chunk(abi.INT64, walk, abi.DELTA_BINARY_PACKED)], [E(walk)])
@@ -122,10 +136,11 @@ def cpu_sample(chunks, max_pages, budget_s):
         sub.append(c)
     t_unz, label = 0.0, ""
     if any(p.codec for c in sub for p in c.pages):
-        # SNAPPY / ZSTD: the oracle decompresses the pages (C restatements of the formats), timed too
+        # SNAPPY / ZSTD / LZ4_RAW / GZIP: the oracle decompresses the pages (C restatements of the formats), timed too
         import copy
-        fns = {writer.SNAPPY: pqref.snappy_decompress, writer.ZSTD: pqref.zstd_decompress}
-        codec_name = {writer.SNAPPY: "Snappy", writer.ZSTD: "ZSTD"}[next(p.codec for c in sub for p in c.pages if p.codec)]
+        fns = {writer.SNAPPY: pqref.snappy_decompress, writer.ZSTD: pqref.zstd_decompress,
+               writer.LZ4_RAW: pqref.lz4_raw_decompress, writer.GZIP: pqref.gzip_decompress}
+        codec_name = {writer.SNAPPY: "Snappy", writer.ZSTD: "ZSTD", writer.LZ4_RAW: "LZ4_RAW", writer.GZIP: "GZIP"}[next(p.codec for c in sub for p in c.pages if p.codec)]
 
         def unz(c):
             c = copy.deepcopy(c)
@@ -269,7 +284,7 @@ def run(name, rows, steps, warmup, cpu_budget, check=True):
         ev2[1].record(dec.stream)
         torch.cuda.synchronize()
         sms = ev2[0].elapsed_time(ev2[1]) / steps
-        codec = {writer.SNAPPY: "snappy", writer.ZSTD: "zstd"}[next(p.codec for ch in chunks for p in ch.pages if p.codec)]
+        codec = {writer.SNAPPY: "snappy", writer.ZSTD: "zstd", writer.LZ4_RAW: "lz4_raw", writer.GZIP: "gzip"}[next(p.codec for ch in chunks for p in ch.pages if p.codec)]
         res.update({"compressed_bytes": comp, f"{codec}_ms": sms,
                     f"{codec}_gbps_uncompressed": enc / (sms / 1e3) / 1e9})
     if name == "c1_plain_i32":
@@ -303,6 +318,8 @@ def main():
                     "delta_i64_2048": 100_000_000,
                     "c2_snappy": 100_000_000, "plain_i64_snappy": 100_000_000,
                     "c2_zstd": 100_000_000, "plain_i64_zstd": 100_000_000,
+                    "c2_lz4": 100_000_000, "plain_i64_lz4": 100_000_000,
+                    "c2_gzip": 100_000_000, "plain_i64_gzip": 100_000_000,
                     "c4_lineitem": 8_000_000}
     for w in args.workloads:
         rows = args.rows or default_rows[w]
