@@ -185,6 +185,7 @@ struct pqg_ctx {
   DevBuf asm_scratch;                // pqg_assemble: block counts + totals
   hipStream_t copy_stream = nullptr; // pqg_decode_host: second D2H queue (odd output chunks)
   DevBuf zstd_scratch;               // pqg_zstd_decompress: literal buffers, ZSTD_LIT_SCRATCH per grid wave
+  DevBuf zstd_seqs, zstd_mode;       // pqg_zstd_decompress: sequence records of the lane-per-page pre-pass, per-job mode
   // pqg_plan_launch: the one-pass PLAIN BYTE_ARRAY kernel runs on a second queue beside the other
   // columns' kernels (forked after the levels, joined before the launch ends)
   hipStream_t side_stream = nullptr;
@@ -292,6 +293,9 @@ int pqg_ctx_destroy(pqg_ctx* c) {
   c->host_counts.release();
   c->host_runs.release();
   c->asm_scratch.release();
+  c->zstd_scratch.release();
+  c->zstd_seqs.release();
+  c->zstd_mode.release();
   if (c->copy_stream) {
     (void)hipStreamSynchronize(c->copy_stream);
     (void)hipStreamDestroy(c->copy_stream);
@@ -1865,8 +1869,29 @@ int pqg_zstd_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, 
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) return PQG_ERR_HIP;
     if (ctx->zstd_scratch.ensure(pqg::ZSTD_LIT_SCRATCH * slots) != hipSuccess) return PQG_ERR_HIP;
   }
+  // sequence pre-pass scratch: dst_bytes / 5 + 1 eight-byte records (a job's records start at its
+  // dst_offset / 5) and one mode word per job; without it every job takes the inline decoder
+  uint64_t* seqs = nullptr;
+  int32_t* mode = nullptr;
+#if PQG_ZSTD_2P
+  {
+    const size_t need_s = 8u * (size_t)(dst_bytes / 5u + 2u), need_m = 4u * (size_t)n_jobs;
+    if (ctx->zstd_seqs.cap < need_s || ctx->zstd_mode.cap < need_m) {
+      if (hipStreamSynchronize(ctx->stream) != hipSuccess) return PQG_ERR_HIP;
+      if (ctx->zstd_seqs.ensure(need_s) != hipSuccess || ctx->zstd_mode.ensure(need_m) != hipSuccess) {
+        (void)hipGetLastError();
+        ctx->zstd_seqs.release();
+        ctx->zstd_mode.release();
+      }
+    }
+    if (ctx->zstd_seqs.cap >= need_s && ctx->zstd_mode.cap >= need_m) {
+      seqs = (uint64_t*)ctx->zstd_seqs.p;
+      mode = (int32_t*)ctx->zstd_mode.p;
+    }
+  }
+#endif
   const hipError_t e = pqg::launch_zstd(ctx->stream, d_src, src_bytes, d_dst, dst_bytes, d_jobs, n_jobs, d_status,
-                                        (uint8_t*)ctx->zstd_scratch.p);
+                                        (uint8_t*)ctx->zstd_scratch.p, seqs, mode);
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }
 

@@ -120,9 +120,16 @@ hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_
 // ZSTD frames per job (pqgpu_zstd.hip): a grid of at most ZSTD_GRID one-wave workgroups loops over
 // the jobs; scratch = min(n_jobs, ZSTD_GRID) x ZSTD_LIT_SCRATCH bytes of literal buffers (<= 512 MiB)
 constexpr uint64_t ZSTD_LIT_SCRATCH = 131072;
+#ifndef PQG_ZSTD_2P
+#define PQG_ZSTD_2P 1  // sequence pre-pass (k_zstd_seq) + replay; 0: inline decoder only (A/B builds)
+#endif
 constexpr uint32_t ZSTD_GRID = 4096;
+// With seqs / mode (both non-null) the sequences are first decoded one lane per job by k_zstd_seq into
+// seqs (8-byte records; job j at dst_offset / 5, so seqs holds dst_bytes / 5 + 1 records) and
+// replayed by k_zstd; mode[j] (n_jobs int32) says which jobs the pre-pass left to the inline decoder.
 hipError_t launch_zstd(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
-                       const pqg_snappy_job* jobs, int n_jobs, int32_t* status, uint8_t* scratch);
+                       const pqg_snappy_job* jobs, int n_jobs, int32_t* status, uint8_t* scratch, uint64_t* seqs,
+                       int32_t* mode);
 hipError_t launch_snappy(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
                          const void* jobs, int n_jobs, int32_t* status);
 hipError_t launch_lz4raw(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,

@@ -744,7 +744,7 @@ __device__ __attribute__((noinline)) int zseq_decode(ZWaveLds& L) {
 
 // One compressed block [q, q + bs) of the job's input. Returns 0 or an error code.
 __device__ __forceinline__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t q, uint32_t bs, uint8_t* litbuf, bool& have_huf,
-                      int& huf_bits, bool* have_tab, int* tlog, uint32_t* rep) {
+                      int& huf_bits, bool* have_tab, int* tlog, uint32_t* rep, const uint64_t* rec, uint32_t& rc) {
   const uint32_t lim = q + bs;
   if (bs < 1) return PQG_ERR_CORRUPT;
   const uint32_t b0 = zbyte(rs, q);
@@ -852,6 +852,46 @@ __device__ __forceinline__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t 
   else if (nseq < 255) { nseq = ((nseq - 128) << 8) + zbyte(rs, p + 1); p += 2; }
   else { nseq = zbyte(rs, p + 1) + (zbyte(rs, p + 2) << 8) + 0x7F00u; p += 3; }
   if (p >= lim) return PQG_ERR_CORRUPT;
+  if (rec) {  // replay: k_zstd_seq decoded (and checked) this block's sequences
+    ZD_T(t_rep);
+    const uint32_t lane = lane_id();
+    uint32_t i = 0, lit_pos = 0;
+    while (i < nseq) {
+      const uint32_t k = i + lane;
+      const uint64_t r = k < nseq ? rec[rc + k] : 0ull;
+      const uint32_t ll = (uint32_t)r & 0x3FFFFu, ml = (uint32_t)(r >> 18) & 0x3FFFFu, off = (uint32_t)(r >> 36);
+      const uint32_t tot = ll + ml;
+      const bool big = tot > ZS_CAP;
+      const uint32_t cum = (uint32_t)wave_incl_scan_u64(big ? (uint64_t)ZS_CAP + 1u : tot);
+      const uint64_t stop = __ballot(k >= nseq || big || cum > ZS_CAP);
+      const uint32_t m = stop ? (uint32_t)__builtin_ctzll(stop) : WAVE;
+      if (lane < m) {
+        L.sq_ll[lane] = ll;
+        L.sq_ml[lane] = ml;
+        L.sq_of[lane] = off;
+      }
+      uint32_t blit;
+      (void)wave_excl_scan_u32(lane < m ? ll : 0u, &blit);
+      blit = uni(blit);
+      wave_sync();
+      if (m) {
+        zexec_batch(O, L, m, lit_kind, rs, lit_src, litbuf, lit_pos);
+        lit_pos += blit;
+      }
+      i += m;
+      if (m < WAVE && i < nseq && uni(rdl(big ? 1u : 0u, m))) {  // a sequence longer than a batch: through the ring
+        const uint32_t bll = uni(rdl(ll, m)), bml = uni(rdl(ml, m)), bof = uni(rdl(off, m));
+        if (bll) zcopy_lits(O, L, lit_kind, rs, lit_kind == 1 ? lit_src : lit_src + lit_pos, litbuf, bll);
+        lit_pos += bll;
+        zcopy_match(O, L, bof, bml);
+        i++;
+      }
+    }
+    rc += nseq;
+    ZD_ADD(L, 2, t_rep);
+    if (regen > lit_pos) zcopy_lits(O, L, lit_kind, rs, lit_kind == 1 ? lit_src : lit_src + lit_pos, litbuf, regen - lit_pos);
+    return 0;
+  }
   ZD_T(t_tab);
   const uint32_t modes = zbyte(rs, p++);
   if (modes & 3u) return PQG_ERR_CORRUPT;
@@ -948,15 +988,378 @@ __device__ uint64_t zxxh64(const uint8_t* p, uint32_t n) {
   return h;
 }
 
+// ---- Sequence pre-pass (k_zstd_seq): one LANE per job ------------------------------------------------
+// The sequence section is a serial chain per block (three FSE states and one backward bitstream), and
+// decoded by a wave's scalar unit it costs ~150 scalar instructions per sequence, which the CU's one
+// scalar unit issues for all of its waves: 100 M int64 PLAIN pages took 44 ms, scalar-issue bound.
+// Here every lane decodes the sequences of its own job (page) with vector instructions — one
+// instruction advances 16 pages — and writes them as 8-byte records {ll:18, ml:18, offset:28} in
+// stream order to `seqs` (job j's records at dst_offset / 5, capacity (dst_offset + dst_size) / 5 -
+// dst_offset / 5: disjoint because the jobs' outputs are). k_zstd then replays them (literals, match
+// execution, checksums) instead of decoding. The pre-pass checks everything the inline decoder
+// checks in the sequence section; anything it does not take (a malformed or unusual stream, a page
+// of >= 2^28 bytes, more sequences than its capacity) marks the job for the inline path, which then
+// reports exactly what it always did. Per lane: its FSE tables (next-state base | bits << 12 in
+// u16, symbol in u8: 3.75 KiB for LL 512 + ML 512 + OF 256 states) and a 256-byte LDS window of
+// its bitstream, refilled 256 bytes at a time.
+#ifndef PQG_ZQ_JOBS
+#define PQG_ZQ_JOBS 16
+#endif
+constexpr uint32_t ZQ_JOBS = PQG_ZQ_JOBS;  // lanes (jobs) per workgroup
+constexpr uint32_t ZQ_WIN = 256;
+constexpr uint32_t ZQ_LL = 0, ZQ_ML = 512, ZQ_OF = 1024;  // table regions (entries)
+constexpr int32_t ZQ_REPLAY = 0, ZQ_INLINE = 1;
+
+struct ZqLane {
+  uint8_t win[ZQ_WIN + 16];  // bitstream bytes [wlo, wlo + ZQ_WIN) of the job's input (absolute offsets)
+  uint16_t e[1280];          // FSE entries: next-state base | nb << 12
+  uint8_t s[1280];           // their symbols
+  int16_t norm[56];
+  uint16_t nxt[56];
+};
+struct ZqLds {
+  ZqLane l[ZQ_JOBS];
+  uint32_t llcode[36], mlcode[53];
+  int16_t def_ll[36], def_ml[53], def_of[29];
+};
+
+// FSE decoding table of `nsym` normalized counts (T.norm) with accuracy `log` into region `r`.
+__device__ bool zq_build(ZqLane& T, uint32_t r, int nsym, int log) {
+  const int size = 1 << log, mask = size - 1;
+  int high = size - 1;
+  for (int s = 0; s < nsym; s++) {
+    if (T.norm[s] == -1) {
+      T.s[r + high--] = (uint8_t)s;
+      T.nxt[s] = 1;
+    } else {
+      T.nxt[s] = (uint16_t)T.norm[s];
+    }
+  }
+  const int step = (size >> 1) + (size >> 3) + 3;
+  int pos = 0;
+  for (int s = 0; s < nsym; s++)
+    for (int i = 0; i < T.norm[s]; i++) {
+      T.s[r + pos] = (uint8_t)s;
+      do { pos = (pos + step) & mask; } while (pos > high);
+    }
+  if (pos != 0) return false;
+  for (int u = 0; u < size; u++) {
+    const uint32_t sy = T.s[r + u];
+    const uint32_t ns = T.nxt[sy]++;
+    const int nb = log - zhigh(ns);
+    T.e[r + u] = (uint16_t)(((ns << nb) - (uint32_t)size) | ((uint32_t)nb << 12));
+  }
+  return true;
+}
+
+// Normalized counts at input offset o (absolute) into T.norm; returns bytes read or -1.
+__device__ int64_t zq_ncount(ZqLane& T, rsrc_t rs, uint32_t o, uint32_t lim, int max_log, int max_sym, int* nsym, int* log) {
+  FwdBits f{rs, lim, (uint64_t)o * 8u, false};
+  const int accuracy = 5 + (int)f.get(4);
+  if (accuracy > max_log) return -1;
+  *log = accuracy;
+  int remaining = (1 << accuracy) + 1, sym = 0;
+  while (remaining > 1 && sym <= max_sym && !f.bad) {
+    const int nbits = zhigh((uint32_t)remaining) + 1;
+    const uint32_t maxv = (1u << nbits) - 1u - (uint32_t)remaining;
+    uint32_t v = f.get(nbits - 1);
+    if (v >= maxv) {
+      v |= f.get(1) << (nbits - 1);
+      if (v >= (1u << (nbits - 1))) v -= maxv;
+    }
+    const int prob = (int)v - 1;
+    T.norm[sym] = (int16_t)prob;
+    sym++;
+    remaining -= prob < 0 ? -prob : prob;
+    if (prob == 0 && sym <= max_sym) {
+      uint32_t rep;
+      do {
+        rep = f.get(2);
+        for (uint32_t r = 0; r < rep && sym <= max_sym; r++) T.norm[sym++] = 0;
+      } while (rep == 3 && !f.bad);
+    }
+  }
+  if (f.bad || remaining != 1 || sym > max_sym + 1) return -1;
+  *nsym = sym;
+  return (int64_t)((f.bitpos + 7) >> 3) - o;
+}
+
+// One sequence table (mode: predefined / RLE / FSE-compressed / repeat), as zseq_table.
+__device__ bool zq_table(ZqLane& T, uint32_t r, int* tlog, bool& have, int mode, rsrc_t rs, uint32_t& q, uint32_t lim,
+                         const int16_t* def, int def_n, int def_log, int max_log, int max_sym) {
+  if (mode == 0) {
+    for (int i = 0; i < def_n; i++) T.norm[i] = def[i];
+    *tlog = def_log;
+    have = zq_build(T, r, def_n, def_log);
+    return have;
+  }
+  if (mode == 1) {
+    if (q >= lim) return false;
+    const uint32_t sy = zbyte(rs, q);
+    q++;
+    if ((int)sy > max_sym) return false;
+    T.s[r] = (uint8_t)sy;
+    T.e[r] = 0;
+    *tlog = 0;
+    have = true;
+    return true;
+  }
+  if (mode == 2) {
+    int ns, lg;
+    const int64_t u = zq_ncount(T, rs, q, lim, max_log, max_sym, &ns, &lg);
+    if (u < 0) return false;
+    q += (uint32_t)u;
+    *tlog = lg;
+    have = zq_build(T, r, ns, lg);
+    return have;
+  }
+  return have;
+}
+
+// The sequences of one compressed block's sequence section [q, lim) (absolute input offsets). Returns
+// false for anything the inline path must handle.
+__device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32_t lim, uint32_t regen, uint32_t& outp,
+                              uint32_t frame0, uint32_t* rep, bool* have_tab, int* tlog, uint64_t* rec, uint32_t& cnt,
+                              uint32_t cap) {
+  if (q >= lim) return false;
+  uint32_t nseq = zbyte(rs, q);
+  if (nseq == 0) {
+    outp += regen;
+    return q + 1u == lim;
+  }
+  if (nseq < 128) { q += 1; }
+  else if (nseq < 255) { nseq = ((nseq - 128) << 8) + zbyte(rs, q + 1); q += 2; }
+  else { nseq = zbyte(rs, q + 1) + (zbyte(rs, q + 2) << 8) + 0x7F00u; q += 3; }
+  if (q >= lim) return false;
+  const uint32_t modes = zbyte(rs, q++);
+  if (modes & 3u) return false;
+  if (!zq_table(T, ZQ_LL, &tlog[0], have_tab[0], (int)(modes >> 6), rs, q, lim, L.def_ll, 36, 6, 9, 35)) return false;
+  if (!zq_table(T, ZQ_OF, &tlog[1], have_tab[1], (int)((modes >> 4) & 3u), rs, q, lim, L.def_of, 29, 5, 8, 31)) return false;
+  if (!zq_table(T, ZQ_ML, &tlog[2], have_tab[2], (int)((modes >> 2) & 3u), rs, q, lim, L.def_ml, 53, 6, 9, 52)) return false;
+  // backward bitstream [q, lim): container c = stream bits [cbit, cbit + 64), from the LDS window
+  const uint32_t sb = q, sn = lim - q;
+  if (sn == 0) return false;
+  const uint32_t lastb = zbyte(rs, sb + sn - 1u);
+  if (!lastb) return false;
+  int32_t bits = (int32_t)(sn - 1u) * 8 + zhigh(lastb), cbit = 0;
+  uint32_t wlo = 0xFFFFFFFFu;
+  uint64_t c = 0;
+  typedef uint32_t __attribute__((may_alias)) u32a;
+  auto fill = [&](int32_t end) {
+    const int32_t e8 = (end + 7) & ~7;
+    cbit = e8 > 64 ? e8 - 64 : 0;
+    const uint32_t b0 = sb + ((uint32_t)cbit >> 3);  // absolute
+    const uint32_t b1 = b0 + 8u < sb + sn ? b0 + 8u : sb + sn;
+    if (wlo == 0xFFFFFFFFu || b0 < wlo || b0 + 12u > wlo + ZQ_WIN) {
+      const uint32_t top = (b0 + 16u) & ~15u;
+      wlo = top >= ZQ_WIN - 16u ? top - (ZQ_WIN - 16u) : 0u;
+#pragma unroll
+      for (uint32_t o = 0; o < ZQ_WIN; o += 16)
+        *(u32x4*)(T.win + o) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(wlo + o), 0, 0);
+    }
+    const uint32_t rel = b0 - wlo, r4 = rel & ~3u, sft = rel & 3u;
+    const uint32_t d0 = *(const u32a*)(T.win + r4), d1 = *(const u32a*)(T.win + r4 + 4), d2 = *(const u32a*)(T.win + r4 + 8);
+    uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sft) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sft) << 32);
+    const uint32_t nb = b1 - b0;
+    if (nb < 8u) v &= (1ull << (8u * nb)) - 1ull;
+    c = v;
+  };
+  auto need = [&](int32_t k) {
+    if (bits - cbit < k && cbit > 0) fill(bits);
+  };
+  auto get = [&](int32_t k) -> uint32_t {
+    bits -= k;
+    return (uint32_t)(c >> ((uint32_t)(bits - cbit) & 63u)) & ((1u << k) - 1u);
+  };
+  fill(bits);
+  need(tlog[0] + tlog[1] + tlog[2]);
+  uint32_t sl = get(tlog[0]), so = get(tlog[1]), sm = get(tlog[2]);
+  uint32_t r0 = rep[0], r1 = rep[1], r2 = rep[2], lits = 0;
+  for (uint32_t i = 0; i < nseq; i++) {
+    const uint32_t el = T.e[ZQ_LL + sl], eo = T.e[ZQ_OF + so], em = T.e[ZQ_ML + sm];
+    const uint32_t llc = T.s[ZQ_LL + sl], ofc = T.s[ZQ_OF + so], mlc = T.s[ZQ_ML + sm];
+    if (llc > 35 || mlc > 52 || ofc > 31) return false;
+    const uint32_t mle = L.mlcode[mlc], lle = L.llcode[llc];
+    const int32_t mlb = (int32_t)(mle >> 24), llb = (int32_t)(lle >> 24);
+    need((int32_t)ofc);
+    const uint32_t ofv = (1u << ofc) + get((int32_t)ofc);
+    need(mlb + llb);
+    const uint32_t ml = (mle & 0xFFFFFFu) + get(mlb);
+    const uint32_t ll = (lle & 0xFFFFFFu) + get(llb);
+    uint32_t off;
+    if (ofv > 3) {
+      off = ofv - 3u;
+      r2 = r1; r1 = r0; r0 = off;
+    } else {
+      uint32_t idx = ofv - 1u;
+      if (ll == 0) idx++;
+      if (idx == 0) {
+        off = r0;
+      } else if (idx == 3) {
+        off = r0 - 1u;
+        if (off == 0) return false;
+        r2 = r1; r1 = r0; r0 = off;
+      } else {
+        off = idx == 1 ? r1 : r2;
+        if (idx == 2) r2 = r1;
+        r1 = r0;
+        r0 = off;
+      }
+    }
+    if (i + 1u < nseq) {
+      const int32_t nl = (int32_t)(el >> 12), nm = (int32_t)(em >> 12), no = (int32_t)(eo >> 12);
+      need(nl + nm + no);
+      sl = (el & 0xFFFu) + get(nl);
+      sm = (em & 0xFFFu) + get(nm);
+      so = (eo & 0xFFFu) + get(no);
+    }
+    if (bits < 0 || lits + ll > regen) return false;
+    if (off == 0 || off > outp + ll - frame0) return false;
+    if (ll >= (1u << 18) || ml >= (1u << 18) || off >= (1u << 28) || cnt >= cap) return false;
+    gst(rec + cnt, (uint64_t)ll | ((uint64_t)ml << 18) | ((uint64_t)off << 36));
+    cnt++;
+    lits += ll;
+    outp += ll + ml;
+  }
+  if (bits != 0) return false;
+  rep[0] = r0;
+  rep[1] = r1;
+  rep[2] = r2;
+  outp += regen - lits;
+  return true;
+}
+
+// The sequence pre-pass of one job (lane): frames and blocks as zstd_job walks them, stopping where
+// it stops (the block that reaches the page's size is still decoded whole). Returns ZQ_REPLAY or
+// ZQ_INLINE.
+__device__ int32_t zq_job(ZqLds& L, ZqLane& T, rsrc_t rs, const pqg_snappy_job& jb, uint64_t* seqs) {
+  const uint64_t so64 = jb.src_offset, n = jb.src_size;
+  if (so64 + n >= 0xFFFFFF00ull || jb.dst_size >= (1u << 27)) return ZQ_INLINE;
+  const uint32_t so = (uint32_t)so64, cap = jb.dst_size;
+  const uint64_t base = jb.dst_offset / 5u;
+  const uint32_t rcap = (uint32_t)((jb.dst_offset + jb.dst_size) / 5u - base);
+  uint64_t* rec = seqs + base;
+  uint32_t cnt = 0, outp = 0, p = so;
+  const uint32_t end = so + (uint32_t)n;
+  while (p < end && outp < cap) {
+    if (end - p < 4) return ZQ_INLINE;
+    const uint32_t magic = ld4_any(rs, p);
+    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {
+      if (end - p < 8) return ZQ_INLINE;
+      const uint32_t sz = ld4_any(rs, p + 4);
+      if (sz > end - p - 8) return ZQ_INLINE;
+      p += 8 + sz;
+      continue;
+    }
+    if (magic != 0xFD2FB528u) return ZQ_INLINE;
+    p += 4;
+    if (p >= end) return ZQ_INLINE;
+    const uint32_t fhd = zbyte(rs, p++);
+    const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1u, checksum = (fhd >> 2) & 1u, did_flag = fhd & 3u;
+    if (fhd & 8u) return ZQ_INLINE;
+    if (!single) p++;
+    const uint32_t did_sz = did_flag == 3 ? 4u : did_flag;
+    uint32_t did = 0;
+    for (uint32_t i = 0; i < did_sz; i++) did |= zbyte(rs, p + i) << (8 * i);
+    p += did_sz;
+    if (did) return ZQ_INLINE;
+    const uint32_t fcs_sz = fcs_flag == 0 ? single : (fcs_flag == 1 ? 2u : fcs_flag == 2 ? 4u : 8u);
+    if (p + fcs_sz > end) return ZQ_INLINE;
+    uint64_t fcs = 0;
+    for (uint32_t i = 0; i < fcs_sz; i++) fcs |= (uint64_t)zbyte(rs, p + i) << (8 * i);
+    if (fcs_sz == 2) fcs += 256;
+    p += fcs_sz;
+    const uint32_t frame0 = outp;
+    uint32_t rep[3] = {1, 4, 8};
+    bool have_tab[3] = {false, false, false};
+    int tlog[3] = {0, 0, 0};
+    bool cut = false;
+    while (true) {
+      if (outp >= cap) { cut = true; break; }
+      if (p + 3 > end) return ZQ_INLINE;
+      const uint32_t bh = zbyte(rs, p) | (zbyte(rs, p + 1) << 8) | (zbyte(rs, p + 2) << 16);
+      p += 3;
+      const uint32_t last = bh & 1u, type = (bh >> 1) & 3u, bs = bh >> 3;
+      if (type == 3) return ZQ_INLINE;
+      if (type == 1) {
+        if (p + 1 > end) return ZQ_INLINE;
+        outp += bs;
+        p += 1;
+      } else if (type == 0) {
+        if (p + bs > end) return ZQ_INLINE;
+        outp += bs;
+        p += bs;
+      } else {
+        if (p + bs > end || bs < 1) return ZQ_INLINE;
+        const uint32_t lim = p + bs, before = outp;
+        // literals section header (the literals themselves are k_zstd's)
+        const uint32_t b0 = zbyte(rs, p);
+        const int lt = (int)(b0 & 3u), sf = (int)((b0 >> 2) & 3u);
+        uint32_t regen = 0, comp = 0, hl = 0;
+        if (lt <= 1) {
+          if (sf == 0 || sf == 2) { regen = b0 >> 3; hl = 1; }
+          else if (sf == 1) { regen = (b0 >> 4) + (zbyte(rs, p + 1) << 4); hl = 2; }
+          else { regen = (b0 >> 4) + (zbyte(rs, p + 1) << 4) + (zbyte(rs, p + 2) << 12); hl = 3; }
+        } else {
+          const uint64_t v = ld8_any(rs, p);
+          if (sf <= 1) { regen = (uint32_t)(v >> 4) & 0x3FFu; comp = (uint32_t)(v >> 14) & 0x3FFu; hl = 3; }
+          else if (sf == 2) { regen = (uint32_t)(v >> 4) & 0x3FFFu; comp = (uint32_t)(v >> 18) & 0x3FFFu; hl = 4; }
+          else { regen = (uint32_t)(v >> 4) & 0x3FFFFu; comp = (uint32_t)(v >> 22) & 0x3FFFFu; hl = 5; }
+        }
+        if (p + hl > lim || regen > ZS_LIT_MAX) return ZQ_INLINE;
+        uint32_t q = p + hl;
+        const uint32_t lsz = lt == 0 ? regen : lt == 1 ? 1u : comp;
+        if (q + lsz > lim) return ZQ_INLINE;
+        q += lsz;
+        if (!zq_block_seqs(L, T, rs, q, lim, regen, outp, frame0, rep, have_tab, tlog, rec, cnt, rcap)) return ZQ_INLINE;
+        if (outp - before > ZS_LIT_MAX) return ZQ_INLINE;
+        p += bs;
+      }
+      if (last) break;
+    }
+    if (cut) break;
+    if ((fcs_flag || single) && (uint64_t)(outp - frame0) != fcs) return ZQ_INLINE;
+    if (checksum) {
+      if (p + 4 > end) return ZQ_INLINE;
+      p += 4;
+    }
+  }
+  return ZQ_REPLAY;
+}
+
+__global__ __launch_bounds__(64) void k_zstd_seq(const uint8_t* __restrict__ src, uint64_t src_bytes,
+                                                 const pqg_snappy_job* __restrict__ jobs, int n_jobs,
+                                                 uint64_t* __restrict__ seqs, int32_t* __restrict__ mode) {
+  __shared__ __attribute__((aligned(16))) ZqLds L;
+  const uint32_t lane = lane_id();
+  for (uint32_t i = lane; i < 53u; i += WAVE) {
+    if (i < 36u) {
+      L.llcode[i] = ZLL_BASE[i] | (uint32_t)ZLL_BITS[i] << 24;
+      L.def_ll[i] = ZLL_DEF[i];
+    }
+    if (i < 29u) L.def_of[i] = ZOF_DEF[i];
+    L.mlcode[i] = ZML_BASE[i] | (uint32_t)ZML_BITS[i] << 24;
+    L.def_ml[i] = ZML_DEF[i];
+  }
+  wave_sync();
+  const int j = (int)(blockIdx.x * ZQ_JOBS + lane);
+  if (lane >= ZQ_JOBS || j >= n_jobs) return;  // (no cross-lane operation follows)
+  const rsrc_t rs = make_rsrc(src, src_bytes);
+  const pqg_snappy_job jb = jobs[j];
+  mode[j] = zq_job(L, L.l[lane], rs, jb, seqs);
+}
+
 // One wave per job: the frames of src[job] -> dst[job] (exactly dst_size bytes kept). The grid is at
 // most ZS_GRID waves; wave w takes jobs w, w + grid, ... and owns literal scratch slot w, so the
 // scratch is bounded whatever the number of pages.
 __device__ __forceinline__ void zstd_job(ZWaveLds& L, const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
-                         uint64_t dst_bytes, const pqg_snappy_job& jb, int j, int32_t* status, uint8_t* litbuf);
+                         uint64_t dst_bytes, const pqg_snappy_job& jb, int j, int32_t* status, uint8_t* litbuf,
+                         const uint64_t* rec);
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PQG_ZS_WAVES))) void k_zstd(const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
                                              uint64_t dst_bytes, const pqg_snappy_job* __restrict__ jobs, int n_jobs,
-                                             int32_t* status, uint8_t* scratch, uint64_t lit_stride) {
+                                             int32_t* status, uint8_t* scratch, uint64_t lit_stride,
+                                             const uint64_t* __restrict__ seqs, const int32_t* __restrict__ mode) {
   __shared__ __attribute__((aligned(16))) ZWaveLds L;
   uint8_t* litbuf = scratch + (uint64_t)blockIdx.x * lit_stride;
   for (uint32_t i = lane_id(); i < 53u; i += WAVE) {
@@ -965,13 +1368,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PQG_ZS_WAVES
   }
   wave_sync();
   for (int j = (int)blockIdx.x; j < n_jobs; j += (int)gridDim.x) {
-    zstd_job(L, src, src_bytes, dst, dst_bytes, jobs[j], j, status, litbuf);
+    const pqg_snappy_job jb = jobs[j];
+    const bool replay = seqs && (int32_t)uni((uint32_t)mode[j]) == ZQ_REPLAY;
+    zstd_job(L, src, src_bytes, dst, dst_bytes, jb, j, status, litbuf, replay ? seqs + jb.dst_offset / 5u : nullptr);
     wave_sync();
   }
 }
 
 __device__ __forceinline__ void zstd_job(ZWaveLds& L, const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
-                         uint64_t dst_bytes, const pqg_snappy_job& jb, int j, int32_t* status, uint8_t* litbuf) {
+                         uint64_t dst_bytes, const pqg_snappy_job& jb, int j, int32_t* status, uint8_t* litbuf,
+                         const uint64_t* rec) {
   const rsrc_t rs = make_rsrc(src + jb.src_offset, src_bytes - jb.src_offset);
   if (lane_id() == 0) {
     L.ss.src = (uint64_t)(uintptr_t)(src + jb.src_offset);
@@ -984,7 +1390,7 @@ __device__ __forceinline__ void zstd_job(ZWaveLds& L, const uint8_t* __restrict_
 #endif
   ZOut O{dst + jb.dst_offset, uni(jb.dst_size), 0, 0, 0, 0};
   int code = 0;
-  uint32_t p = 0;
+  uint32_t p = 0, rc = 0;  // rc: replayed sequences so far
   if (jb.dst_offset + jb.dst_size > dst_bytes || jb.src_offset + jb.src_size > src_bytes) code = PQG_ERR_INVALID_ARG;
   while (!code && p < n && O.pos < O.cap) {
     p = uni(p);
@@ -1038,7 +1444,7 @@ __device__ __forceinline__ void zstd_job(ZWaveLds& L, const uint8_t* __restrict_
       } else {
         if (p + bs > n) { code = PQG_ERR_CORRUPT; break; }
         const uint32_t before = O.pos;
-        code = zblock(L, O, rs, p, bs, litbuf, have_huf, huf_bits, have_tab, tlog, rep);
+        code = zblock(L, O, rs, p, bs, litbuf, have_huf, huf_bits, have_tab, tlog, rep, rec, rc);
         if (!code && O.pos - before > ZS_LIT_MAX) code = PQG_ERR_CORRUPT;
         p += bs;
       }
@@ -1067,10 +1473,18 @@ __device__ __forceinline__ void zstd_job(ZWaveLds& L, const uint8_t* __restrict_
 }
 
 hipError_t launch_zstd(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
-                       const pqg_snappy_job* jobs, int n_jobs, int32_t* status, uint8_t* scratch) {
+                       const pqg_snappy_job* jobs, int n_jobs, int32_t* status, uint8_t* scratch, uint64_t* seqs,
+                       int32_t* mode) {
   if (n_jobs <= 0) return hipSuccess;
+  if (seqs && mode) {
+    hipLaunchKernelGGL(k_zstd_seq, dim3((n_jobs + (int)ZQ_JOBS - 1) / (int)ZQ_JOBS), dim3(64), 0, st, src, src_bytes,
+                       jobs, n_jobs, seqs, mode);
+  } else {
+    seqs = nullptr;
+    mode = nullptr;
+  }
   hipLaunchKernelGGL(k_zstd, dim3(n_jobs < (int)ZSTD_GRID ? n_jobs : (int)ZSTD_GRID), dim3(64), 0, st, src, src_bytes,
-                     dst, dst_bytes, jobs, n_jobs, status, scratch, (uint64_t)ZS_LIT_MAX);
+                     dst, dst_bytes, jobs, n_jobs, status, scratch, (uint64_t)ZS_LIT_MAX, seqs, mode);
   return hipGetLastError();
 }
 
