@@ -181,8 +181,8 @@ class Decoder:
                 ph.pages.append(q)
                 n_page += 1
             placeholders.append(ph)
-        batch = batch.build_batch(placeholders)
-        dbatch = DeviceBatch(batch, self.device)
+        hb = batch.build_batch(placeholders)
+        dbatch = DeviceBatch(hb, self.device)
         if not blocks:
             return dbatch
         col_of_chunk = []
@@ -198,11 +198,11 @@ class Decoder:
                                                         ("src_size", "<u4"), ("dst_size", "<u4")]))
             for j, (_, payload, (kind, idx), prefix) in enumerate(mine):
                 if kind == "dict":
-                    dst = int(batch.columns[col_of_chunk[idx]]["dict_offset"])
-                    n_out = int(batch.columns[col_of_chunk[idx]]["dict_size"])
+                    dst = int(hb.columns[col_of_chunk[idx]]["dict_offset"])
+                    n_out = int(hb.columns[col_of_chunk[idx]]["dict_size"])
                 else:
-                    dst = int(batch.pages["offset"][idx]) + prefix
-                    n_out = int(batch.pages["size"][idx]) - prefix
+                    dst = int(hb.pages["offset"][idx]) + prefix
+                    n_out = int(hb.pages["size"][idx]) - prefix
                 table[j] = (pos, dst, len(payload), n_out)
                 src.append(payload + bytes((-len(payload)) % 16))
                 pos += len(src[-1])

@@ -158,7 +158,7 @@ def test_harness_reads_fixture_values(harness, tmp_path, name, c, mode):
     for p in sorted(r["pages"]):
         n = r["pages"][p]
         got = r["values"].get(p, [])
-        want_idx = list(range(n)) if mode == "all" else [k for k in range(n) if k % 5 >= 3]
+        want_idx = list(range(n)) if mode in ("all", "staged") else [k for k in range(n) if k % 5 >= 3]
         assert [k for k, _ in got] == want_idx
         for k, v in got:
             assert v == fmt(expected[pos + k], ch.physical_type), (p, k)

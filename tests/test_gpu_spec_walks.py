@@ -144,10 +144,11 @@ def run_both(decoder, chunks):
 
 # ---- level sections -------------------------------------------------------------------------------
 
-@pytest.mark.parametrize("max_def", [1, 3, 5, 15, 31, 63, 127, 255])
+@pytest.mark.parametrize("max_def", [1, 3, 5, 15, 31, 63, 127, 254])
 @pytest.mark.parametrize("shape", ["long_packed", "long_rle", "mixed"])
 def test_levels_hand_built_runs(decoder, max_def, shape):
-    """Packed runs of up to 300 groups (a 255-level page: 2,400 data bytes in one run), RLE runs of
+    """Packed runs of up to 300 groups (an 8-bit-level page: 2,400 data bytes in one run; max_def 254 is the
+    device limit, pqg_plan_create: 255 is UNSUPPORTED), RLE runs of
     up to 5,000 slots, pages of 30,000-60,000 slots, every width 1..8."""
     w = int(max_def).bit_length()
     rng = np.random.default_rng(max_def * 3 + len(shape))
