@@ -668,7 +668,7 @@ __device__ bool dict_walk_sp(uint8_t* seg, rsrc_t rs, uint32_t N, uint32_t sec_b
 }
 
 #ifndef PQG_DICT_SP
-#define PQG_DICT_SP 1  // 0: every dictionary page through dict_walk_ls (A/B builds)
+#define PQG_DICT_SP 0  // 1: pages through the speculative-piece walk (measured slower on C2 / Zipf(2.0): A/B builds only)
 #endif
 
 // One wave per page (4 per workgroup): the run records of RLE_DICTIONARY / PLAIN_DICTIONARY
@@ -2134,7 +2134,7 @@ __device__ uint32_t decode_levels_sp(LevelSpLds& L, rsrc_t rs, uint32_t beg, uin
 }
 
 #ifndef PQG_LV_SP
-#define PQG_LV_SP 1  // 0: every RLE level section through the window walk (A/B builds)
+#define PQG_LV_SP 0  // 1: RLE level sections through the speculative-piece decoder (measured 2.2x slower: A/B builds only)
 #endif
 
 template <int W>
