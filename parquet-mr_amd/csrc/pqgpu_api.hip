@@ -889,7 +889,7 @@ int pqg_plan_launch(pqg_plan* P) {
   // forked after the levels and joined at the end, so the two kinds share the chip.
   // The BYTE_ARRAY kernels of the other columns likewise go to a third queue when fixed-width columns'
   // kernels (HBM bound) are in the plan to share the chip with.
-  bool fork = false, fork_bin = false;
+  bool fork = false, fork_bin = false, fork_fix = false;
 #ifndef PQG_NO_FORK
   const bool has_fixed = P->cls_n[C_DICT4] || P->cls_n[C_DICT8] || P->cls_n[C_PLAIN] || P->cls_n[C_BOOL] ||
                          P->cls_n[C_RLEBOOL] || P->cls_n[C_DELTA4] || P->cls_n[C_DELTA8] || P->cls_n[C_BSS];
@@ -908,7 +908,6 @@ int pqg_plan_launch(pqg_plan* P) {
                (ctx->ev_join_bin || hipEventCreateWithFlags(&ctx->ev_join_bin, hipEventDisableTiming) == hipSuccess) &&
                hipStreamWaitEvent(ctx->bin_stream, ctx->ev_fork, 0) == hipSuccess;
   }
-  bool fork_fix = false;
   if ((fork || fork_bin) && has_fixed)
     fork_fix = (ctx->fix_stream || hipStreamCreateWithFlags(&ctx->fix_stream, hipStreamNonBlocking) == hipSuccess) &&
                (ctx->ev_join_fix || hipEventCreateWithFlags(&ctx->ev_join_fix, hipEventDisableTiming) == hipSuccess) &&

@@ -568,7 +568,7 @@ __device__ __forceinline__ void zcopy_match(ZOut& O, ZWaveLds& L, uint32_t off, 
 // ring) at once. Sequences are dependent chains (a match of 8 bytes at offset 8 after 2 literals,
 // again and again, in int64 data): they resolve in log2(depth) rounds instead of one at a time.
 __device__ __forceinline__ void zexec_batch(ZOut& O, ZWaveLds& L, uint32_t m, int lit_kind, rsrc_t rs, uint32_t lit_src,
-                            const uint8_t* litbuf, uint32_t lit_pos) {
+                            const uint8_t* litbuf, uint32_t lit_pos, int32_t lw_rel = -1) {
   const uint32_t lane = lane_id();
   const uint32_t ll = lane < m ? L.sq_ll[lane] : 0u, ml = lane < m ? L.sq_ml[lane] : 0u, of = lane < m ? L.sq_of[lane] : 0u;
   uint32_t T, LT;
@@ -578,7 +578,8 @@ __device__ __forceinline__ void zexec_batch(ZOut& O, ZWaveLds& L, uint32_t m, in
   LT = uni(LT);
   // the batch's literals [lit_pos, lit_pos + LT)
   for (uint32_t i = lane; i < LT; i += WAVE)
-    L.ph.x.lseg[i] = (uint8_t)zlit(lit_kind, rs, lit_src, litbuf, lit_pos + i);
+    L.ph.x.lseg[i] = lw_rel >= 0 ? L.win[(uint32_t)lw_rel + i]  // staged (replay): see zblock
+                                 : (uint8_t)zlit(lit_kind, rs, lit_src, litbuf, lit_pos + i);
   const uint32_t op = O.pos;
   for (uint32_t i = 0; i < ll; i++) L.ph.x.src[ob + i] = ZS_LIT | (lb + i);
   for (uint32_t i = 0; i < ml; i++) L.ph.x.src[ob + ll + i] = op + ob + ll + i - of;
@@ -856,9 +857,44 @@ __device__ __forceinline__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t 
     ZD_T(t_rep);
     const uint32_t lane = lane_id();
     uint32_t i = 0, lit_pos = 0;
+    // record queue: records [qb, qe) of the block, lane l of q_j holding record qb + 64 j + l (one
+    // load round per 256 records instead of one per batch)
+    uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+    uint32_t qb = 0, qe = 0;
+    // raw / Huffman-decoded literals staged ZS_WIN bytes at a time in L.win (free in replay: no
+    // bitstream): one load round per ~1 KiB of literals instead of one per batch. Source address of
+    // literal k: lit_src + k in the input (raw), k in litbuf (decoded); window [lw, lw + ZS_WIN).
+    uint32_t lw = 0xFFFFFFFFu;
+    const uint32_t sa0 = lit_kind == 0 ? lit_src : 0u;
+    auto stage = [&](uint32_t k) {
+      lw = (sa0 + k) & ~3u;
+      for (uint32_t j = lane; j < ZS_WIN / 4u; j += WAVE) {
+        const uint32_t a = lw + 4u * j;
+        const uint32_t v = lit_kind == 0 ? ld32(rs, a) : zld((const uint32_t*)(litbuf + a));
+        *(uint32_t*)(L.win + 4u * j) = v;
+      }
+      wave_sync();
+    };
+    auto shfl64 = [](uint64_t v, uint32_t l) -> uint64_t {
+      return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, (int)l) | ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)l) << 32);
+    };
     while (i < nseq) {
+      if (i + WAVE > qe && qe < nseq) {
+        qb = i;
+        qe = i + 4u * WAVE < nseq ? i + 4u * WAVE : nseq;
+        const uint32_t b = i + lane;
+        q0 = b < nseq ? rec[rc + b] : 0ull;
+        q1 = b + WAVE < nseq ? rec[rc + b + WAVE] : 0ull;
+        q2 = b + 2u * WAVE < nseq ? rec[rc + b + 2u * WAVE] : 0ull;
+        q3 = b + 3u * WAVE < nseq ? rec[rc + b + 3u * WAVE] : 0ull;
+      }
       const uint32_t k = i + lane;
-      const uint64_t r = k < nseq ? rec[rc + k] : 0ull;
+      const uint32_t d = uni(i - qb), s0 = d >> 6, l = (d + lane) & (WAVE - 1u);
+      const bool upper = (d & (WAVE - 1u)) + lane >= WAVE;  // the lane's record sits in slot s0 + 1
+      const uint64_t A = s0 == 0 ? q0 : s0 == 1 ? q1 : s0 == 2 ? q2 : q3;
+      const uint64_t Bq = s0 == 0 ? q1 : s0 == 1 ? q2 : s0 == 2 ? q3 : 0ull;
+      const uint64_t ra = shfl64(A, l), rb = shfl64(Bq, l);
+      const uint64_t r = k < nseq ? (upper ? rb : ra) : 0ull;
       const uint32_t ll = (uint32_t)r & 0x3FFFFu, ml = (uint32_t)(r >> 18) & 0x3FFFFu, off = (uint32_t)(r >> 36);
       const uint32_t tot = ll + ml;
       const bool big = tot > ZS_CAP;
@@ -875,7 +911,12 @@ __device__ __forceinline__ int zblock(ZWaveLds& L, ZOut& O, rsrc_t rs, uint32_t 
       blit = uni(blit);
       wave_sync();
       if (m) {
-        zexec_batch(O, L, m, lit_kind, rs, lit_src, litbuf, lit_pos);
+        int32_t rel = -1;
+        if (lit_kind != 1 && blit) {
+          if (lw == 0xFFFFFFFFu || sa0 + lit_pos < lw || sa0 + lit_pos + blit > lw + ZS_WIN) stage(lit_pos);
+          rel = (int32_t)(sa0 + lit_pos - lw);
+        }
+        zexec_batch(O, L, m, lit_kind, rs, lit_src, litbuf, lit_pos, rel);
         lit_pos += blit;
       }
       i += m;
@@ -1000,13 +1041,32 @@ __device__ uint64_t zxxh64(const uint8_t* p, uint32_t n) {
 // checks in the sequence section; anything it does not take (a malformed or unusual stream, a page
 // of >= 2^28 bytes, more sequences than its capacity) marks the job for the inline path, which then
 // reports exactly what it always did. Per lane: its FSE tables (next-state base | bits << 12 in
-// u16, symbol in u8: 3.75 KiB for LL 512 + ML 512 + OF 256 states) and a 256-byte LDS window of
-// its bitstream, refilled 256 bytes at a time.
+// u16, symbol in u8: 3.75 KiB for LL 512 + ML 512 + OF 256 states) and a 512-byte LDS window of
+// its bitstream. Window refills are collective: when any lane of the sequence loop could read below
+// its window in the next sequence, every lane in the loop re-centres its window at its position, so
+// the wave waits for one round of loads per ~150 sequences instead of once per lane's refill
+// (measured: per-lane refills at uncorrelated times stalled the wave every few sequences).
 #ifndef PQG_ZQ_JOBS
 #define PQG_ZQ_JOBS 16
 #endif
 constexpr uint32_t ZQ_JOBS = PQG_ZQ_JOBS;  // lanes (jobs) per workgroup
-constexpr uint32_t ZQ_WIN = 256;
+#ifdef PQG_DIAG
+// Diagnostic build only (tools/diag_zstd.py): per job 6 u64 = pre-pass cycles (whole job, tables,
+// sequence loops), sequences, window re-centrings, compressed blocks.
+static __device__ uint64_t* pqg_zqdiag;
+extern "C" int pqg_diag_zq_set(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(pqg_zqdiag), &p, sizeof(p)) == hipSuccess ? 0 : 3;
+}
+struct ZqDiag {
+  uint64_t tab, loop, seqs, rec, blocks;
+};
+#define ZQD_ARG , ZqDiag& zd
+#define ZQD_PASS , zd
+#else
+#define ZQD_ARG
+#define ZQD_PASS
+#endif
+constexpr uint32_t ZQ_WIN = 512;
 constexpr uint32_t ZQ_LL = 0, ZQ_ML = 512, ZQ_OF = 1024;  // table regions (entries)
 constexpr int32_t ZQ_REPLAY = 0, ZQ_INLINE = 1;
 
@@ -1120,7 +1180,7 @@ __device__ bool zq_table(ZqLane& T, uint32_t r, int* tlog, bool& have, int mode,
 // false for anything the inline path must handle.
 __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32_t lim, uint32_t regen, uint32_t& outp,
                               uint32_t frame0, uint32_t* rep, bool* have_tab, int* tlog, uint64_t* rec, uint32_t& cnt,
-                              uint32_t cap) {
+                              uint32_t cap ZQD_ARG) {
   if (q >= lim) return false;
   uint32_t nseq = zbyte(rs, q);
   if (nseq == 0) {
@@ -1133,6 +1193,10 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
   if (q >= lim) return false;
   const uint32_t modes = zbyte(rs, q++);
   if (modes & 3u) return false;
+#ifdef PQG_DIAG
+  const uint64_t zt0 = __builtin_amdgcn_s_memtime();
+  zd.blocks++;
+#endif
   if (!zq_table(T, ZQ_LL, &tlog[0], have_tab[0], (int)(modes >> 6), rs, q, lim, L.def_ll, 36, 6, 9, 35)) return false;
   if (!zq_table(T, ZQ_OF, &tlog[1], have_tab[1], (int)((modes >> 4) & 3u), rs, q, lim, L.def_of, 29, 5, 8, 31)) return false;
   if (!zq_table(T, ZQ_ML, &tlog[2], have_tab[2], (int)((modes >> 2) & 3u), rs, q, lim, L.def_ml, 53, 6, 9, 52)) return false;
@@ -1145,18 +1209,19 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
   uint32_t wlo = 0xFFFFFFFFu;
   uint64_t c = 0;
   typedef uint32_t __attribute__((may_alias)) u32a;
+  auto recenter = [&](uint32_t b0) {  // window [wlo, wlo + ZQ_WIN) with b0 16-32 bytes below its top
+    const uint32_t top = (b0 + 16u) & ~15u;
+    wlo = top >= ZQ_WIN - 16u ? top - (ZQ_WIN - 16u) : 0u;
+#pragma unroll
+    for (uint32_t o = 0; o < ZQ_WIN; o += 16)
+      *(u32x4*)(T.win + o) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(wlo + o), 0, 0);
+  };
   auto fill = [&](int32_t end) {
     const int32_t e8 = (end + 7) & ~7;
     cbit = e8 > 64 ? e8 - 64 : 0;
     const uint32_t b0 = sb + ((uint32_t)cbit >> 3);  // absolute
     const uint32_t b1 = b0 + 8u < sb + sn ? b0 + 8u : sb + sn;
-    if (wlo == 0xFFFFFFFFu || b0 < wlo || b0 + 12u > wlo + ZQ_WIN) {
-      const uint32_t top = (b0 + 16u) & ~15u;
-      wlo = top >= ZQ_WIN - 16u ? top - (ZQ_WIN - 16u) : 0u;
-#pragma unroll
-      for (uint32_t o = 0; o < ZQ_WIN; o += 16)
-        *(u32x4*)(T.win + o) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(wlo + o), 0, 0);
-    }
+    if (wlo == 0xFFFFFFFFu || b0 < wlo || b0 + 12u > wlo + ZQ_WIN) recenter(b0);
     const uint32_t rel = b0 - wlo, r4 = rel & ~3u, sft = rel & 3u;
     const uint32_t d0 = *(const u32a*)(T.win + r4), d1 = *(const u32a*)(T.win + r4 + 4), d2 = *(const u32a*)(T.win + r4 + 8);
     uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sft) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sft) << 32);
@@ -1172,55 +1237,97 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
     return (uint32_t)(c >> ((uint32_t)(bits - cbit) & 63u)) & ((1u << k) - 1u);
   };
   fill(bits);
+#ifdef PQG_DIAG
+  const uint64_t zt1 = __builtin_amdgcn_s_memtime();
+  zd.tab += zt1 - zt0;
+#endif
   need(tlog[0] + tlog[1] + tlog[2]);
   uint32_t sl = get(tlog[0]), so = get(tlog[1]), sm = get(tlog[2]);
   uint32_t r0 = rep[0], r1 = rep[1], r2 = rep[2], lits = 0;
+  // One sequence = one pass with no data-dependent branch on the common path: the table entries and
+  // 20 window bytes at the read position are loaded together; the sequence's bits (offset, match and
+  // literal length extras, then the LL / ML / OF state bits: T <= 64 of them, else the inline path
+  // takes the job) come out of one 64-bit funnel shift; repeat offsets are selects.
   for (uint32_t i = 0; i < nseq; i++) {
-    const uint32_t el = T.e[ZQ_LL + sl], eo = T.e[ZQ_OF + so], em = T.e[ZQ_ML + sm];
-    const uint32_t llc = T.s[ZQ_LL + sl], ofc = T.s[ZQ_OF + so], mlc = T.s[ZQ_ML + sm];
-    if (llc > 35 || mlc > 52 || ofc > 31) return false;
-    const uint32_t mle = L.mlcode[mlc], lle = L.llcode[llc];
-    const int32_t mlb = (int32_t)(mle >> 24), llb = (int32_t)(lle >> 24);
-    need((int32_t)ofc);
-    const uint32_t ofv = (1u << ofc) + get((int32_t)ofc);
-    need(mlb + llb);
-    const uint32_t ml = (mle & 0xFFFFFFu) + get(mlb);
-    const uint32_t ll = (lle & 0xFFFFFFu) + get(llb);
-    uint32_t off;
-    if (ofv > 3) {
-      off = ofv - 3u;
-      r2 = r1; r1 = r0; r0 = off;
-    } else {
-      uint32_t idx = ofv - 1u;
-      if (ll == 0) idx++;
-      if (idx == 0) {
-        off = r0;
-      } else if (idx == 3) {
-        off = r0 - 1u;
-        if (off == 0) return false;
-        r2 = r1; r1 = r0; r0 = off;
-      } else {
-        off = idx == 1 ? r1 : r2;
-        if (idx == 2) r2 = r1;
-        r1 = r0;
-        r0 = off;
+    {  // a sequence reads at most 64 bits below `bits`: re-centre every window of the loop together
+      const int32_t lowbit = bits - 160 > 0 ? bits - 160 : 0;
+      const bool want = sb + ((uint32_t)lowbit >> 3) < wlo;
+      if (__ballot(want)) {
+        recenter(sb + ((uint32_t)(bits > 0 ? bits : 0) >> 3));
+#ifdef PQG_DIAG
+        zd.rec++;
+#endif
       }
     }
-    if (i + 1u < nseq) {
-      const int32_t nl = (int32_t)(el >> 12), nm = (int32_t)(em >> 12), no = (int32_t)(eo >> 12);
-      need(nl + nm + no);
-      sl = (el & 0xFFFu) + get(nl);
-      sm = (em & 0xFFFu) + get(nm);
-      so = (eo & 0xFFFu) + get(no);
+    // every load of the step first (table entries, window bytes), one exit test at the end: an early
+    // return per check sinks the loads below it and costs an exec-mask region each
+    const uint32_t el = T.e[ZQ_LL + sl], eo = T.e[ZQ_OF + so], em = T.e[ZQ_ML + sm];
+    const uint32_t llc = T.s[ZQ_LL + sl], ofc0 = T.s[ZQ_OF + so], mlc = T.s[ZQ_ML + sm];
+    // stream bits [cb, cb + 160) from the window: cb <= bits - 64 < cb + 32
+    const int32_t lowbit = bits - 64 > 0 ? bits - 64 : 0;
+    const uint32_t a = (sb + ((uint32_t)lowbit >> 3)) & ~3u;
+    const int32_t cb = ((int32_t)a - (int32_t)sb) * 8;
+    const uint32_t rel = a - wlo;
+    const uint32_t d0 = *(const u32a*)(T.win + rel), d1 = *(const u32a*)(T.win + rel + 4),
+                   d2 = *(const u32a*)(T.win + rel + 8), d3 = *(const u32a*)(T.win + rel + 12),
+                   d4 = *(const u32a*)(T.win + rel + 16);
+    bool bad = llc > 35 || mlc > 52 || ofc0 > 31;
+    const uint32_t ofc = ofc0 & 31u;
+    const uint32_t mle = L.mlcode[mlc < 52u ? mlc : 52u], lle = L.llcode[llc < 35u ? llc : 35u];
+    const uint32_t mlb = mle >> 24, llb = lle >> 24;
+    const bool more = i + 1u < nseq;
+    const uint32_t nl = more ? el >> 12 : 0u, nm = more ? em >> 12 : 0u, no = more ? eo >> 12 : 0u;
+    uint32_t tt = ofc + mlb + llb + nl + nm + no;
+    bad |= tt > 64u;
+    tt = tt > 64u ? 64u : tt;
+    bits -= (int32_t)tt;
+    const int32_t off = bits - cb;  // in [0, 96) unless the stream is overrun (bits < 0: failed below)
+    const uint32_t ix = (uint32_t)off >> 5, sh = (uint32_t)off & 31u;
+    const uint32_t x0 = ix == 0 ? d0 : ix == 1 ? d1 : d2;
+    const uint32_t x1 = ix == 0 ? d1 : ix == 1 ? d2 : d3;
+    const uint32_t x2 = ix == 0 ? d2 : ix == 1 ? d3 : d4;
+    const uint64_t Y = (uint64_t)__builtin_amdgcn_alignbit(x1, x0, sh) |
+                       ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, sh) << 32);  // stream bits [bits, bits + 64)
+    uint32_t t = tt;
+    auto fld = [&](uint32_t k) -> uint32_t {  // the next k <= 31 bits, from the top of Y down
+      t -= k;
+      return (uint32_t)(Y >> t) & ((1u << k) - 1u);
+    };
+    const uint32_t ofv = (1u << ofc) + fld(ofc);
+    const uint32_t ml = (mle & 0xFFFFFFu) + fld(mlb);
+    const uint32_t ll = (lle & 0xFFFFFFu) + fld(llb);
+    const uint32_t nsl = (el & 0xFFFu) + fld(nl);
+    const uint32_t nsm = (em & 0xFFFu) + fld(nm);
+    const uint32_t nso = (eo & 0xFFFu) + fld(no);
+    // repeat offsets (RFC 8878 3.1.1.5)
+    const bool big = ofv > 3u;
+    const uint32_t ri = ofv - 1u + (ll == 0u ? 1u : 0u);
+    uint32_t roff = r0;  // a chain of selects (nested conditionals compile to exec-mask branches)
+    roff = ri == 1u ? r1 : roff;
+    roff = ri == 2u ? r2 : roff;
+    roff = ri == 3u ? r0 - 1u : roff;
+    roff = big ? ofv - 3u : roff;
+    const uint32_t n2 = (big || ri >= 2u) ? r1 : r2, n1 = (big || ri >= 1u) ? r0 : r1;
+    r2 = n2;
+    r1 = n1;
+    r0 = roff;
+    if (more) {
+      sl = nsl;
+      sm = nsm;
+      so = nso;
     }
-    if (bits < 0 || lits + ll > regen) return false;
-    if (off == 0 || off > outp + ll - frame0) return false;
-    if (ll >= (1u << 18) || ml >= (1u << 18) || off >= (1u << 28) || cnt >= cap) return false;
-    gst(rec + cnt, (uint64_t)ll | ((uint64_t)ml << 18) | ((uint64_t)off << 36));
+    bad |= bits < 0 || lits + ll > regen || roff == 0 || roff > outp + ll - frame0;
+    bad |= ll >= (1u << 18) || ml >= (1u << 18) || roff >= (1u << 28) || cnt >= cap;
+    if (bad) return false;
+    gst(rec + cnt, (uint64_t)ll | ((uint64_t)ml << 18) | ((uint64_t)roff << 36));
     cnt++;
     lits += ll;
     outp += ll + ml;
   }
+#ifdef PQG_DIAG
+  zd.loop += __builtin_amdgcn_s_memtime() - zt1;
+  zd.seqs += nseq;
+#endif
   if (bits != 0) return false;
   rep[0] = r0;
   rep[1] = r1;
@@ -1232,7 +1339,7 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
 // The sequence pre-pass of one job (lane): frames and blocks as zstd_job walks them, stopping where
 // it stops (the block that reaches the page's size is still decoded whole). Returns ZQ_REPLAY or
 // ZQ_INLINE.
-__device__ int32_t zq_job(ZqLds& L, ZqLane& T, rsrc_t rs, const pqg_snappy_job& jb, uint64_t* seqs) {
+__device__ int32_t zq_job(ZqLds& L, ZqLane& T, rsrc_t rs, const pqg_snappy_job& jb, uint64_t* seqs ZQD_ARG) {
   const uint64_t so64 = jb.src_offset, n = jb.src_size;
   if (so64 + n >= 0xFFFFFF00ull || jb.dst_size >= (1u << 27)) return ZQ_INLINE;
   const uint32_t so = (uint32_t)so64, cap = jb.dst_size;
@@ -1311,7 +1418,8 @@ __device__ int32_t zq_job(ZqLds& L, ZqLane& T, rsrc_t rs, const pqg_snappy_job& 
         const uint32_t lsz = lt == 0 ? regen : lt == 1 ? 1u : comp;
         if (q + lsz > lim) return ZQ_INLINE;
         q += lsz;
-        if (!zq_block_seqs(L, T, rs, q, lim, regen, outp, frame0, rep, have_tab, tlog, rec, cnt, rcap)) return ZQ_INLINE;
+        if (!zq_block_seqs(L, T, rs, q, lim, regen, outp, frame0, rep, have_tab, tlog, rec, cnt, rcap ZQD_PASS))
+          return ZQ_INLINE;
         if (outp - before > ZS_LIT_MAX) return ZQ_INLINE;
         p += bs;
       }
@@ -1346,7 +1454,22 @@ __global__ __launch_bounds__(64) void k_zstd_seq(const uint8_t* __restrict__ src
   if (lane >= ZQ_JOBS || j >= n_jobs) return;  // (no cross-lane operation follows)
   const rsrc_t rs = make_rsrc(src, src_bytes);
   const pqg_snappy_job jb = jobs[j];
+#ifdef PQG_DIAG
+  ZqDiag zd{0, 0, 0, 0, 0};
+  const uint64_t zj0 = __builtin_amdgcn_s_memtime();
+  mode[j] = zq_job(L, L.l[lane], rs, jb, seqs, zd);
+  if (pqg_zqdiag) {
+    uint64_t* o = pqg_zqdiag + 6 * (uint64_t)j;
+    o[0] = __builtin_amdgcn_s_memtime() - zj0;
+    o[1] = zd.tab;
+    o[2] = zd.loop;
+    o[3] = zd.seqs;
+    o[4] = zd.rec;
+    o[5] = zd.blocks;
+  }
+#else
   mode[j] = zq_job(L, L.l[lane], rs, jb, seqs);
+#endif
 }
 
 // One wave per job: the frames of src[job] -> dst[job] (exactly dst_size bytes kept). The grid is at

@@ -24,8 +24,17 @@ buf = torch.zeros(max(n_jobs, 1) * 12 + 64, dtype=torch.int64, device="cuda")
 L = native.lib()
 L.pqg_diag_zstd_set.argtypes = [C.c_void_p]
 assert L.pqg_diag_zstd_set(buf.data_ptr()) == 0
+zq = torch.zeros(max(n_jobs, 1) * 6 + 64, dtype=torch.int64, device="cuda")
+if hasattr(L, "pqg_diag_zq_set"):
+    L.pqg_diag_zq_set.argtypes = [C.c_void_p]
+    assert L.pqg_diag_zq_set(zq.data_ptr()) == 0
 dec.decompress(db)
 torch.cuda.synchronize()
+q = zq[: n_jobs * 6].view(n_jobs, 6).cpu().numpy().astype(np.float64)
+if q[:, 0].sum():
+    print(f"pre-pass (k_zstd_seq, one lane per job): mean job cycles {q[:, 0].mean():.0f}, tables {q[:, 1].mean():.0f}, "
+          f"sequence loops {q[:, 2].mean():.0f}; sequences {q[:, 3].mean():.0f}, re-centrings {q[:, 4].mean():.1f}, "
+          f"blocks {q[:, 5].mean():.1f}; loop cycles per sequence {q[:, 2].sum() / max(q[:, 3].sum(), 1):.0f}")
 a = buf[: n_jobs * 12].view(n_jobs, 12).cpu().numpy().astype(np.float64)
 names = ["literals", "seq tables", "seq loop", "  batches", "  long seqs", "job", "sequences", "literal bytes",
          "  state reads", "  extra bits", "  state updates", "  rest"]
