@@ -1040,14 +1040,15 @@ __device__ uint64_t zxxh64(const uint8_t* p, uint32_t n) {
 // execution, checksums) instead of decoding. The pre-pass checks everything the inline decoder
 // checks in the sequence section; anything it does not take (a malformed or unusual stream, a page
 // of >= 2^28 bytes, more sequences than its capacity) marks the job for the inline path, which then
-// reports exactly what it always did. Per lane: its FSE tables (next-state base | bits << 12 in
-// u16, symbol in u8: 3.75 KiB for LL 512 + ML 512 + OF 256 states) and a 512-byte LDS window of
+// reports exactly what it always did. Per lane: its FSE tables (one u32 per state: next-state base,
+// state bits, the symbol's extra bits and baseline: 5 KiB for LL 512 + ML 512 + OF 256 states; 12
+// lanes per workgroup, 2 workgroups per CU) and a 512-byte LDS window of
 // its bitstream. Window refills are collective: when any lane of the sequence loop could read below
 // its window in the next sequence, every lane in the loop re-centres its window at its position, so
 // the wave waits for one round of loads per ~150 sequences instead of once per lane's refill
 // (measured: per-lane refills at uncorrelated times stalled the wave every few sequences).
 #ifndef PQG_ZQ_JOBS
-#define PQG_ZQ_JOBS 16
+#define PQG_ZQ_JOBS 12
 #endif
 constexpr uint32_t ZQ_JOBS = PQG_ZQ_JOBS;  // lanes (jobs) per workgroup
 #ifdef PQG_DIAG
@@ -1072,8 +1073,7 @@ constexpr int32_t ZQ_REPLAY = 0, ZQ_INLINE = 1;
 
 struct ZqLane {
   uint8_t win[ZQ_WIN + 16];  // bitstream bytes [wlo, wlo + ZQ_WIN) of the job's input (absolute offsets)
-  uint16_t e[1280];          // FSE entries: next-state base | nb << 12
-  uint8_t s[1280];           // their symbols
+  uint32_t e[1280];          // FSE entries (zq_entry): next-state base, state bits, the symbol's extra bits and baseline
   int16_t norm[56];
   uint16_t nxt[56];
 };
@@ -1083,13 +1083,31 @@ struct ZqLds {
   int16_t def_ll[36], def_ml[53], def_of[29];
 };
 
-// FSE decoding table of `nsym` normalized counts (T.norm) with accuracy `log` into region `r`.
-__device__ bool zq_build(ZqLane& T, uint32_t r, int nsym, int log) {
+// A decoding entry carries what the sequence step needs from its symbol, so a state costs one LDS
+// read: next-state base (bits 0-8) | state bits << 9 | the symbol's extra bits << 13 | its baseline
+// << 18 (0x3FFF: a baseline of >= 16,383, which for every such code is (1 << extra bits) + ZQ_ADD:
+// LL codes 33-35, ML codes 50-52 (+3), offset codes >= 14).
+constexpr uint32_t ZQ_BIG = 0x3FFFu;
+__device__ __forceinline__ uint32_t zq_sym_entry(const ZqLds& L, int kind, uint32_t sy) {
+  uint32_t xb, bl;
+  if (kind == 0) { xb = L.llcode[sy] >> 24; bl = L.llcode[sy] & 0xFFFFFFu; }
+  else if (kind == 1) { xb = L.mlcode[sy] >> 24; bl = L.mlcode[sy] & 0xFFFFFFu; }
+  else { xb = sy; bl = 1u << sy; }
+  return (xb << 13) | ((bl >= ZQ_BIG ? ZQ_BIG : bl) << 18);
+}
+__device__ __forceinline__ uint32_t zq_baseline(uint32_t e, uint32_t add) {
+  const uint32_t bl = e >> 18;
+  return bl != ZQ_BIG ? bl : (1u << ((e >> 13) & 31u)) + add;
+}
+
+// FSE decoding table of `nsym` normalized counts (T.norm) with accuracy `log` into region `r`
+// (kind 0 LL, 1 ML, 2 OF: which code table the symbols index).
+__device__ bool zq_build(const ZqLds& L, ZqLane& T, uint32_t r, int nsym, int log, int kind) {
   const int size = 1 << log, mask = size - 1;
   int high = size - 1;
   for (int s = 0; s < nsym; s++) {
     if (T.norm[s] == -1) {
-      T.s[r + high--] = (uint8_t)s;
+      T.e[r + high--] = (uint32_t)s;
       T.nxt[s] = 1;
     } else {
       T.nxt[s] = (uint16_t)T.norm[s];
@@ -1099,15 +1117,15 @@ __device__ bool zq_build(ZqLane& T, uint32_t r, int nsym, int log) {
   int pos = 0;
   for (int s = 0; s < nsym; s++)
     for (int i = 0; i < T.norm[s]; i++) {
-      T.s[r + pos] = (uint8_t)s;
+      T.e[r + pos] = (uint32_t)s;
       do { pos = (pos + step) & mask; } while (pos > high);
     }
   if (pos != 0) return false;
   for (int u = 0; u < size; u++) {
-    const uint32_t sy = T.s[r + u];
+    const uint32_t sy = T.e[r + u];
     const uint32_t ns = T.nxt[sy]++;
     const int nb = log - zhigh(ns);
-    T.e[r + u] = (uint16_t)(((ns << nb) - (uint32_t)size) | ((uint32_t)nb << 12));
+    T.e[r + u] = ((ns << nb) - (uint32_t)size) | ((uint32_t)nb << 9) | zq_sym_entry(L, kind, sy);
   }
   return true;
 }
@@ -1145,12 +1163,13 @@ __device__ int64_t zq_ncount(ZqLane& T, rsrc_t rs, uint32_t o, uint32_t lim, int
 }
 
 // One sequence table (mode: predefined / RLE / FSE-compressed / repeat), as zseq_table.
-__device__ bool zq_table(ZqLane& T, uint32_t r, int* tlog, bool& have, int mode, rsrc_t rs, uint32_t& q, uint32_t lim,
+__device__ bool zq_table(const ZqLds& L, int kind, ZqLane& T, uint32_t r, int* tlog, bool& have, int mode, rsrc_t rs,
+                         uint32_t& q, uint32_t lim,
                          const int16_t* def, int def_n, int def_log, int max_log, int max_sym) {
   if (mode == 0) {
     for (int i = 0; i < def_n; i++) T.norm[i] = def[i];
     *tlog = def_log;
-    have = zq_build(T, r, def_n, def_log);
+    have = zq_build(L, T, r, def_n, def_log, kind);
     return have;
   }
   if (mode == 1) {
@@ -1158,8 +1177,7 @@ __device__ bool zq_table(ZqLane& T, uint32_t r, int* tlog, bool& have, int mode,
     const uint32_t sy = zbyte(rs, q);
     q++;
     if ((int)sy > max_sym) return false;
-    T.s[r] = (uint8_t)sy;
-    T.e[r] = 0;
+    T.e[r] = zq_sym_entry(L, kind, sy);
     *tlog = 0;
     have = true;
     return true;
@@ -1170,7 +1188,7 @@ __device__ bool zq_table(ZqLane& T, uint32_t r, int* tlog, bool& have, int mode,
     if (u < 0) return false;
     q += (uint32_t)u;
     *tlog = lg;
-    have = zq_build(T, r, ns, lg);
+    have = zq_build(L, T, r, ns, lg, kind);
     return have;
   }
   return have;
@@ -1197,9 +1215,11 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
   const uint64_t zt0 = __builtin_amdgcn_s_memtime();
   zd.blocks++;
 #endif
-  if (!zq_table(T, ZQ_LL, &tlog[0], have_tab[0], (int)(modes >> 6), rs, q, lim, L.def_ll, 36, 6, 9, 35)) return false;
-  if (!zq_table(T, ZQ_OF, &tlog[1], have_tab[1], (int)((modes >> 4) & 3u), rs, q, lim, L.def_of, 29, 5, 8, 31)) return false;
-  if (!zq_table(T, ZQ_ML, &tlog[2], have_tab[2], (int)((modes >> 2) & 3u), rs, q, lim, L.def_ml, 53, 6, 9, 52)) return false;
+  if (!zq_table(L, 0, T, ZQ_LL, &tlog[0], have_tab[0], (int)(modes >> 6), rs, q, lim, L.def_ll, 36, 6, 9, 35)) return false;
+  if (!zq_table(L, 2, T, ZQ_OF, &tlog[1], have_tab[1], (int)((modes >> 4) & 3u), rs, q, lim, L.def_of, 29, 5, 8, 31))
+    return false;
+  if (!zq_table(L, 1, T, ZQ_ML, &tlog[2], have_tab[2], (int)((modes >> 2) & 3u), rs, q, lim, L.def_ml, 53, 6, 9, 52))
+    return false;
   // backward bitstream [q, lim): container c = stream bits [cbit, cbit + 64), from the LDS window
   const uint32_t sb = q, sn = lim - q;
   if (sn == 0) return false;
@@ -1262,7 +1282,6 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
     // every load of the step first (table entries, window bytes), one exit test at the end: an early
     // return per check sinks the loads below it and costs an exec-mask region each
     const uint32_t el = T.e[ZQ_LL + sl], eo = T.e[ZQ_OF + so], em = T.e[ZQ_ML + sm];
-    const uint32_t llc = T.s[ZQ_LL + sl], ofc0 = T.s[ZQ_OF + so], mlc = T.s[ZQ_ML + sm];
     // stream bits [cb, cb + 160) from the window: cb <= bits - 64 < cb + 32
     const int32_t lowbit = bits - 64 > 0 ? bits - 64 : 0;
     const uint32_t a = (sb + ((uint32_t)lowbit >> 3)) & ~3u;
@@ -1271,12 +1290,10 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
     const uint32_t d0 = *(const u32a*)(T.win + rel), d1 = *(const u32a*)(T.win + rel + 4),
                    d2 = *(const u32a*)(T.win + rel + 8), d3 = *(const u32a*)(T.win + rel + 12),
                    d4 = *(const u32a*)(T.win + rel + 16);
-    bool bad = llc > 35 || mlc > 52 || ofc0 > 31;
-    const uint32_t ofc = ofc0 & 31u;
-    const uint32_t mle = L.mlcode[mlc < 52u ? mlc : 52u], lle = L.llcode[llc < 35u ? llc : 35u];
-    const uint32_t mlb = mle >> 24, llb = lle >> 24;
+    bool bad = false;  // (the tables hold valid symbols only: zq_ncount / zq_table check them)
+    const uint32_t ofc = (eo >> 13) & 31u, mlb = (em >> 13) & 31u, llb = (el >> 13) & 31u;
     const bool more = i + 1u < nseq;
-    const uint32_t nl = more ? el >> 12 : 0u, nm = more ? em >> 12 : 0u, no = more ? eo >> 12 : 0u;
+    const uint32_t nl = more ? (el >> 9) & 15u : 0u, nm = more ? (em >> 9) & 15u : 0u, no = more ? (eo >> 9) & 15u : 0u;
     uint32_t tt = ofc + mlb + llb + nl + nm + no;
     bad |= tt > 64u;
     tt = tt > 64u ? 64u : tt;
@@ -1293,12 +1310,12 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
       t -= k;
       return (uint32_t)(Y >> t) & ((1u << k) - 1u);
     };
-    const uint32_t ofv = (1u << ofc) + fld(ofc);
-    const uint32_t ml = (mle & 0xFFFFFFu) + fld(mlb);
-    const uint32_t ll = (lle & 0xFFFFFFu) + fld(llb);
-    const uint32_t nsl = (el & 0xFFFu) + fld(nl);
-    const uint32_t nsm = (em & 0xFFFu) + fld(nm);
-    const uint32_t nso = (eo & 0xFFFu) + fld(no);
+    const uint32_t ofv = zq_baseline(eo, 0u) + fld(ofc);
+    const uint32_t ml = zq_baseline(em, 3u) + fld(mlb);
+    const uint32_t ll = zq_baseline(el, 0u) + fld(llb);
+    const uint32_t nsl = (el & 0x1FFu) + fld(nl);
+    const uint32_t nsm = (em & 0x1FFu) + fld(nm);
+    const uint32_t nso = (eo & 0x1FFu) + fld(no);
     // repeat offsets (RFC 8878 3.1.1.5)
     const bool big = ofv > 3u;
     const uint32_t ri = ofv - 1u + (ll == 0u ? 1u : 0u);
