@@ -52,17 +52,13 @@ __device__ __forceinline__ void lz_flush(const uint8_t* ring, uint8_t* out, uint
   }
 }
 
-// Execute elements [0, m) producing output [op, op + T): ring + HBM. `lits` is the literal buffer
-// (LZ_SEG bytes), ro a buffer resource over the output (far copies read it back).
-__device__ __forceinline__ void lz_exec_batch(uint8_t* ring, const uint8_t* lits, uint32_t* sS, const uint32_t* e_src,
-                                              const uint32_t* e_len, uint32_t m, uint32_t T, uint32_t op,
-                                              uint8_t* out, rsrc_t ro) {
+// Output [op, op + T) from its byte sources sS[0, T) (LZ_LIT | offset in the literal buffer `lits`
+// of LMASK + 1 bytes, or the output position copied): ring + HBM. ro: a buffer resource over the
+// output (far copies read it back).
+template <uint32_t LMASK = LZ_SEG - 1u>
+__device__ __forceinline__ void lz_exec_sources(uint8_t* ring, const uint8_t* lits, uint32_t* sS, uint32_t T,
+                                                uint32_t op, uint8_t* out, rsrc_t ro) {
   const uint32_t lane = lane_id();
-  const uint32_t es = lane < m ? e_src[lane] : 0u, el = lane < m ? e_len[lane] : 0u;
-  uint32_t tot;
-  const uint32_t eo = wave_excl_scan_u32(el, &tot);
-  for (uint32_t i = 0; i < el; i++) sS[eo + i] = es + i;  // literal: buffer byte; copy: output position
-  wave_sync();
   constexpr uint32_t NB = LZ_CAP / WAVE;
   uint32_t sv[NB];
 #pragma unroll
@@ -93,7 +89,7 @@ __device__ __forceinline__ void lz_exec_batch(uint8_t* ring, const uint8_t* lits
 #pragma unroll
   for (uint32_t j = 0; j < NB; j++) {
     const uint32_t v = sv[j];
-    const uint32_t lit = lits[v & (LZ_SEG - 1u)], rg = ring[v & LZ_RMASK];
+    const uint32_t lit = lits[v & LMASK], rg = ring[v & LZ_RMASK];
     bv[j] = (v & LZ_LIT) ? lit : rg;
     far |= lane + WAVE * j < T && !(v & LZ_LIT) && v + LZ_RING < op + T + WAVE;
   }
@@ -116,6 +112,21 @@ __device__ __forceinline__ void lz_exec_batch(uint8_t* ring, const uint8_t* lits
   }
   wave_sync();
   lz_flush(ring, out, op, op + T);
+}
+
+// Execute elements [0, m) producing output [op, op + T): ring + HBM. `lits` is the literal buffer
+// (LZ_SEG bytes).
+template <uint32_t LMASK = LZ_SEG - 1u>
+__device__ __forceinline__ void lz_exec_batch(uint8_t* ring, const uint8_t* lits, uint32_t* sS, const uint32_t* e_src,
+                                              const uint32_t* e_len, uint32_t m, uint32_t T, uint32_t op,
+                                              uint8_t* out, rsrc_t ro) {
+  const uint32_t lane = lane_id();
+  const uint32_t es = lane < m ? e_src[lane] : 0u, el = lane < m ? e_len[lane] : 0u;
+  uint32_t tot;
+  const uint32_t eo = wave_excl_scan_u32(el, &tot);
+  for (uint32_t i = 0; i < el; i++) sS[eo + i] = es + i;  // literal: buffer byte; copy: output position
+  wave_sync();
+  lz_exec_sources<LMASK>(ring, lits, sS, T, op, out, ro);
 }
 
 }  // namespace pqg
