@@ -186,6 +186,7 @@ struct pqg_ctx {
   hipStream_t copy_stream = nullptr; // pqg_decode_host: second D2H queue (odd output chunks)
   DevBuf zstd_scratch;               // pqg_zstd_decompress: literal buffers, ZSTD_LIT_SCRATCH per grid wave
   DevBuf zstd_seqs, zstd_mode;       // pqg_zstd_decompress: sequence records of the lane-per-page pre-pass, per-job mode
+  DevBuf gzip_recs, gzip_mode;       // pqg_gzip_decompress: back-reference records of the token pre-pass, per-job count
   // pqg_plan_launch: the one-pass PLAIN BYTE_ARRAY kernel runs on a second queue beside the other
   // columns' kernels (forked after the levels, joined before the launch ends)
   hipStream_t side_stream = nullptr;
@@ -296,6 +297,8 @@ int pqg_ctx_destroy(pqg_ctx* c) {
   c->zstd_scratch.release();
   c->zstd_seqs.release();
   c->zstd_mode.release();
+  c->gzip_recs.release();
+  c->gzip_mode.release();
   if (c->copy_stream) {
     (void)hipStreamSynchronize(c->copy_stream);
     (void)hipStreamDestroy(c->copy_stream);
@@ -1835,7 +1838,27 @@ int pqg_gzip_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, 
   if (n_jobs == 0) return PQG_OK;
   if (!d_src || !d_dst || !d_jobs) return PQG_ERR_INVALID_ARG;
   if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
-  const hipError_t e = pqg::launch_gzip(ctx->stream, d_src, src_bytes, d_dst, dst_bytes, d_jobs, n_jobs, d_status);
+  // token pre-pass scratch: dst_bytes / 3 + 2 eight-byte records and one word per job; without it
+  // every job takes the scalar decoder
+  uint64_t* recs = nullptr;
+  int32_t* mode = nullptr;
+  {
+    const size_t need_r = 8u * (size_t)(dst_bytes / 3u + 2u), need_m = 4u * (size_t)n_jobs;
+    if (ctx->gzip_recs.cap < need_r || ctx->gzip_mode.cap < need_m) {
+      if (hipStreamSynchronize(ctx->stream) != hipSuccess) return PQG_ERR_HIP;
+      if (ctx->gzip_recs.ensure(need_r) != hipSuccess || ctx->gzip_mode.ensure(need_m) != hipSuccess) {
+        (void)hipGetLastError();
+        ctx->gzip_recs.release();
+        ctx->gzip_mode.release();
+      }
+    }
+    if (ctx->gzip_recs.cap >= need_r && ctx->gzip_mode.cap >= need_m) {
+      recs = (uint64_t*)ctx->gzip_recs.p;
+      mode = (int32_t*)ctx->gzip_mode.p;
+    }
+  }
+  const hipError_t e = pqg::launch_gzip(ctx->stream, d_src, src_bytes, d_dst, dst_bytes, d_jobs, n_jobs, d_status,
+                                        recs, mode);
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }
 

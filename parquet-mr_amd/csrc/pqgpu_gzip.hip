@@ -331,10 +331,11 @@ struct GzJobDev {  // = pqg_snappy_job
 __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, uint64_t src_bytes,
                                                uint8_t* __restrict__ dst, uint64_t dst_bytes,
                                                const GzJobDev* __restrict__ jobs, int n_jobs,
-                                               int32_t* __restrict__ status) {
+                                               int32_t* __restrict__ status, const int32_t* __restrict__ mode) {
   __shared__ __attribute__((aligned(16))) GzLds L;
   const int jb = (int)blockIdx.x;
   if (jb >= n_jobs) return;
+  if (mode && mode[jb] >= 0) return;  // decoded by the token pre-pass (k_gzip_seq + k_gzip_replay)
   const uint32_t lane = lane_id();
   const GzJobDev J = jobs[jb];
   const uint32_t n = uni(J.src_size), ulen = uni(J.dst_size);
@@ -564,11 +565,374 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
   if (lane == 0 && status) status[jb] = code;
 }
 
+// ---- Token pre-pass (k_gzip_seq): one LANE per page ------------------------------------------------
+// The symbol loop above is a serial scalar chain per page whose issue the CU's one scalar unit shares
+// among its waves (the round-3 ZSTD diagnosis). Here every lane decodes the DEFLATE tokens of its own
+// page with vector instructions (12 pages per workgroup): Huffman tables per block in the lane's LDS
+// slice (first-level table of 512 entries carrying length / distance bases and extra bits, canonical
+// counts for longer codes), the input through a 512-byte LDS window re-centred collectively (all lanes
+// of the token loop together), literal bytes stored straight to their output positions, and each
+// back-reference as an 8-byte record {output position:32, distance:16, length:16} (job j's records at
+// dst_offset / 3). k_gzip_replay then executes the records in 189-byte output windows with the shared
+// executor (literal bytes read back from the output). Anything else — a malformed stream, a page that
+// completes inside a member, more records than the job's range, a stream past 4 GiB — is left to
+// k_gzip, which reports exactly what it always did.
+#ifndef PQG_GZ_2P
+#define PQG_GZ_2P 1
+#endif
+constexpr uint32_t GQ_JOBS = 12;
+constexpr uint32_t GQ_WIN = 512;
+constexpr int32_t GQ_INLINE = -1;  // mode[j]: -1 = k_gzip decodes job j, else its record count
+constexpr uint32_t GQ_OUTW = 189;  // replay output window (<= 63 records of >= 3 bytes + one from before)
+
+struct GqLane {
+  uint8_t win[GQ_WIN + 16];  // input bytes [wlo, wlo + GQ_WIN) (offsets into src)
+  uint32_t lfast[1u << GZ_FAST], dfast[1u << GZ_FAST];
+  int16_t lcount[16], lsym[288], dcount[16], dsym[32];
+  uint16_t offs[16], next[16];
+  uint8_t lens[320 + 32];
+};
+struct GqLds {
+  GqLane l[GQ_JOBS];
+  uint32_t lentab[32], disttab[32];
+  uint8_t ord[20];
+};
+
+// Canonical tables of lens[0 .. n) for one lane (serial): as gz_build, returns left (0 complete,
+// > 0 incomplete) or -1 (over-subscribed)
+__device__ int gq_build(GqLane& T, const uint8_t* lens, int n, int16_t* count, int16_t* sym, uint32_t* fast, int kind,
+                        const uint32_t* ext) {
+  for (int l = 0; l < 16; l++) count[l] = 0;
+  for (int s = 0; s < n; s++) count[lens[s]]++;
+  count[0] = 0;
+  int left = 1;
+  T.offs[1] = 0;
+  T.next[1] = 0;
+  for (int l = 1; l < 16; l++) {
+    left = (left << 1) - count[l];
+    if (left < 0) return -1;
+    if (l < 15) {
+      T.offs[l + 1] = (uint16_t)(T.offs[l] + count[l]);
+      T.next[l + 1] = (uint16_t)((T.next[l] + count[l]) << 1);
+    }
+  }
+  for (uint32_t i = 0; i < (1u << GZ_FAST); i++) fast[i] = GZ_SLOW;
+  for (int s = 0; s < n; s++) {
+    const uint32_t l = lens[s];
+    if (!l) continue;
+    sym[T.offs[l]++] = (int16_t)s;
+    const uint32_t c = T.next[l]++;
+    if (l <= GZ_FAST) {
+      uint32_t e = (uint32_t)s | (l << 9);
+      if (kind == 0 && s > 256 && s < 286) {
+        const uint32_t t = ext[s - 257];
+        e |= ((t & 0x1FFu) << 13) | ((t >> 16) << 22);
+      } else if (kind == 1 && s < 30) {
+        const uint32_t t = ext[s];
+        e |= ((t & 0x7FFFu) << 13) | ((t >> 16) << 28);
+      }
+      const uint32_t rv = __builtin_bitreverse32(c) >> (32u - l);
+      for (uint32_t k = 0; k < (1u << (GZ_FAST - l)); k++) fast[rv | (k << l)] = e;
+    }
+  }
+  return left;
+}
+
+// canonical decode of the code at the bottom of x (LSB first, MSB-first code); returns the symbol
+// (its length in *len) or -1
+__device__ __forceinline__ int gq_slow(uint64_t x, const int16_t* count, const int16_t* sym, uint32_t* len) {
+  int c = 0, first = 0, index = 0;
+  for (int l = 1; l < 16; l++) {
+    c |= (int)((x >> (l - 1)) & 1u);
+    const int k = count[l];
+    if (c - k < first) {
+      *len = (uint32_t)l;
+      return sym[index + (c - first)];
+    }
+    index += k;
+    first = (first + k) << 1;
+    c <<= 1;
+  }
+  return -1;
+}
+
+__device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uint8_t* dst, uint64_t* recs) {
+  if (J.src_offset + J.src_size + 16u >= 0xFFFFFF00ull || J.dst_size == 0u || J.dst_size >= (1u << 31))
+    return GQ_INLINE;
+  const uint32_t so = (uint32_t)J.src_offset, n = J.src_size, ulen = J.dst_size;
+  const uint64_t endbit = ((uint64_t)so + n) * 8u;
+  uint8_t* out = dst + J.dst_offset;
+  const uint64_t rbase = J.dst_offset / 3u;
+  const uint32_t rcap = (uint32_t)((J.dst_offset + J.dst_size) / 3u - rbase);
+  uint64_t* rec = recs + rbase;
+  typedef uint32_t __attribute__((may_alias)) u32a;
+  uint32_t wlo = 0xFFFFFFFFu;
+  auto recenter = [&](uint32_t byte) {
+    wlo = byte & ~15u;
+#pragma unroll
+    for (uint32_t o = 0; o < GQ_WIN; o += 16)
+      *(u32x4*)(T.win + o) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(wlo + o), 0, 0);
+  };
+  auto peek = [&](uint64_t b) -> uint64_t {  // 64 input bits from bit b (window must hold them)
+    const uint32_t byte = (uint32_t)(b >> 3);
+    const uint32_t rel = byte - wlo, r4 = rel & ~3u, sh = (rel & 3u) * 8u + (uint32_t)(b & 7u);
+    const uint32_t d0 = *(const u32a*)(T.win + r4), d1 = *(const u32a*)(T.win + r4 + 4), d2 = *(const u32a*)(T.win + r4 + 8);
+    return (uint64_t)__builtin_amdgcn_alignbit(d1, d0, sh) | ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32);
+  };
+  auto ensure = [&](uint64_t b) {  // the window holds the 8 bytes from bit b (single lane)
+    const uint32_t byte = (uint32_t)(b >> 3);
+    if (wlo == 0xFFFFFFFFu || byte < wlo || byte + 12u > wlo + GQ_WIN) recenter(byte);
+  };
+  uint64_t bp = 0;
+  auto bits = [&](uint32_t k) -> uint32_t {  // k <= 32
+    ensure(bp);
+    const uint32_t v = (uint32_t)(peek(bp) & ((1ull << k) - 1ull));
+    bp += k;
+    return v;
+  };
+  auto byte_at = [&](uint32_t q) -> uint32_t {  // byte q of the job's input (absolute offset so + q)
+    return (ld32(rs, (so + q) & ~3u) >> (((so + q) & 3u) * 8u)) & 0xFFu;
+  };
+  uint32_t op = 0, cnt = 0, q = 0;
+  while (op < ulen) {
+    // member header (RFC 1952 2.3)
+    if (q + 10u > n) return GQ_INLINE;
+    const uint32_t flg = byte_at(q + 3u);
+    if (byte_at(q) != 0x1fu || byte_at(q + 1u) != 0x8bu || byte_at(q + 2u) != 8u || (flg & 0xE0u)) return GQ_INLINE;
+    q += 10u;
+    if (flg & 4u) {
+      if (q + 2u > n) return GQ_INLINE;
+      q += 2u + (byte_at(q) | (byte_at(q + 1u) << 8));
+    }
+    if (flg & 8u) { while (q < n && byte_at(q)) q++; q++; }
+    if (flg & 16u) { while (q < n && byte_at(q)) q++; q++; }
+    if (flg & 2u) q += 2u;
+    if (q > n) return GQ_INLINE;
+    bp = ((uint64_t)so + q) * 8u;
+    const uint32_t mstart = op;
+    uint32_t last = 0;
+    do {
+      last = bits(1);
+      const uint32_t type = bits(2);
+      if (bp > endbit || type == 3u) return GQ_INLINE;
+      if (type == 0u) {  // stored
+        bp = (bp + 7u) & ~7ull;
+        const uint32_t len = bits(16), nlen = bits(16);
+        const uint32_t at = (uint32_t)(bp >> 3) - so;
+        if (len != (~nlen & 0xFFFFu) || at + len > n || op + len > ulen) return GQ_INLINE;
+        for (uint32_t i = 0; i < len; i++) gst(out + op + i, (uint8_t)byte_at(at + i));
+        op += len;
+        bp += 8ull * len;
+        continue;
+      }
+      if (type == 1u) {
+        for (uint32_t s = 0; s < 288u + 30u; s++) T.lens[s] = s < 144u ? 8 : s < 256u ? 9 : s < 280u ? 7 : s < 288u ? 8 : 5;
+        gq_build(T, T.lens, 288, T.lcount, T.lsym, T.lfast, 0, L.lentab);
+        gq_build(T, T.lens + 288, 30, T.dcount, T.dsym, T.dfast, 1, L.disttab);
+      } else {
+        const uint32_t nlen = bits(5) + 257u, ndist = bits(5) + 1u, ncode = bits(4) + 4u;
+        if (nlen > 286u || ndist > 30u) return GQ_INLINE;
+        for (uint32_t s = 0; s < 19u; s++) T.lens[s] = 0;
+        for (uint32_t i = 0; i < ncode; i++) T.lens[L.ord[i]] = (uint8_t)bits(3);
+        // the code-length code: canonical tables in dcount / dsym (rebuilt below)
+        if (gq_build(T, T.lens, 19, T.dcount, T.dsym, T.dfast, 2, nullptr) != 0) return GQ_INLINE;
+        uint32_t idx = 0;
+        while (idx < nlen + ndist) {
+          ensure(bp);
+          uint32_t cl = 0;
+          const int sym = gq_slow(peek(bp), T.dcount, T.dsym, &cl);
+          if (sym < 0) return GQ_INLINE;
+          bp += cl;
+          if (sym < 16) {
+            T.lens[idx++] = (uint8_t)sym;
+          } else {
+            uint32_t rep, val = 0;
+            if (sym == 16) {
+              if (idx == 0) return GQ_INLINE;
+              val = T.lens[idx - 1u];
+              rep = 3u + bits(2);
+            } else if (sym == 17) {
+              rep = 3u + bits(3);
+            } else {
+              rep = 11u + bits(7);
+            }
+            if (idx + rep > nlen + ndist) return GQ_INLINE;
+            for (uint32_t k = 0; k < rep; k++) T.lens[idx + k] = (uint8_t)val;
+            idx += rep;
+          }
+        }
+        if (bp > endbit || T.lens[256] == 0u) return GQ_INLINE;
+        // (descending: position 288 + k is read as nlen + k' for a larger k' when nlen > 258)
+        for (int k = 31; k >= 0; k--) T.lens[288 + k] = (uint32_t)k < ndist ? T.lens[nlen + (uint32_t)k] : 0;
+        const int e1 = gq_build(T, T.lens, (int)nlen, T.lcount, T.lsym, T.lfast, 0, L.lentab);
+        if (e1 != 0) return GQ_INLINE;  // (incomplete single-code tables: the inline path)
+        const int e2 = gq_build(T, T.lens + 288, (int)ndist, T.dcount, T.dsym, T.dfast, 1, L.disttab);
+        if (e2 != 0) return GQ_INLINE;
+      }
+      // ---- the block's tokens
+      while (true) {
+        {  // re-centre every window of the loop together when one could leave its window
+          const bool want = (uint32_t)(bp >> 3) + 24u > wlo + GQ_WIN || (uint32_t)(bp >> 3) < wlo;
+          if (__ballot(want)) recenter((uint32_t)(bp >> 3));
+        }
+        const uint64_t x = peek(bp);
+        uint32_t e = T.lfast[(uint32_t)x & ((1u << GZ_FAST) - 1u)];
+        uint32_t l;
+        if (e == GZ_SLOW) {
+          const int s2 = gq_slow(x, T.lcount, T.lsym, &l);
+          if (s2 < 0) return GQ_INLINE;
+          e = (uint32_t)s2;
+          if (s2 > 256 && s2 < 286) {
+            const uint32_t t = L.lentab[s2 - 257];
+            e |= ((t & 0x1FFu) << 13) | ((t >> 16) << 22);
+          }
+        } else {
+          l = gz_ent_len(e);
+        }
+        const uint32_t sym = gz_ent_sym(e);
+        if (sym < 256u) {
+          if (op >= ulen || bp + l > endbit) return GQ_INLINE;
+          gst(out + op, (uint8_t)sym);
+          op++;
+          bp += l;
+          continue;
+        }
+        if (sym == 256u) {
+          bp += l;
+          if (bp > endbit) return GQ_INLINE;
+          break;
+        }
+        if (sym > 285u) return GQ_INLINE;
+        const uint32_t lext = (e >> 22) & 7u;
+        const uint32_t len = ((e >> 13) & 0x1FFu) + (uint32_t)((x >> l) & ((1u << lext) - 1u));
+        const uint64_t y = x >> (l + lext);
+        uint32_t d = T.dfast[(uint32_t)y & ((1u << GZ_FAST) - 1u)];
+        uint32_t dl;
+        if (d == GZ_SLOW) {
+          const int s3 = gq_slow(y, T.dcount, T.dsym, &dl);
+          if (s3 < 0 || s3 >= 30) return GQ_INLINE;
+          const uint32_t t = L.disttab[s3];
+          d = (uint32_t)s3 | ((t & 0x7FFFu) << 13) | ((t >> 16) << 28);
+        } else {
+          dl = gz_ent_len(d);
+        }
+        if (gz_ent_sym(d) >= 30u) return GQ_INLINE;
+        const uint32_t dext = d >> 28;
+        const uint32_t dist = ((d >> 13) & 0x7FFFu) + (uint32_t)((y >> dl) & ((1u << dext) - 1u));
+        const uint32_t tb = l + lext + dl + dext;
+        if (bp + tb > endbit || dist > op - mstart || op + len > ulen || cnt >= rcap) return GQ_INLINE;
+        gst(rec + cnt, (uint64_t)op | ((uint64_t)dist << 32) | ((uint64_t)len << 48));
+        cnt++;
+        op += len;
+        bp += tb;
+      }
+    } while (!last);
+    if (op >= ulen) break;  // complete: the trailer is not read
+    // a member that ends before the page: ISIZE, then the next member
+    const uint32_t at = (uint32_t)((bp + 7u) >> 3) - so;
+    if (at + 8u > n) return GQ_INLINE;
+    const uint32_t isz = byte_at(at + 4u) | (byte_at(at + 5u) << 8) | (byte_at(at + 6u) << 16) | (byte_at(at + 7u) << 24);
+    if (isz != op - mstart) return GQ_INLINE;
+    q = at + 8u;
+  }
+  return op == ulen ? (int32_t)cnt : GQ_INLINE;
+}
+
+__global__ __launch_bounds__(64) void k_gzip_seq(const uint8_t* __restrict__ src, uint64_t src_bytes,
+                                                 uint8_t* __restrict__ dst, uint64_t dst_bytes,
+                                                 const GzJobDev* __restrict__ jobs, int n_jobs,
+                                                 uint64_t* __restrict__ recs, int32_t* __restrict__ mode) {
+  __shared__ __attribute__((aligned(16))) GqLds L;
+  const uint32_t lane = lane_id();
+  if (lane < 29u) L.lentab[lane] = GZ_LBASE[lane] | ((uint32_t)GZ_LEXT[lane] << 16);
+  if (lane < 30u) L.disttab[lane] = GZ_DBASE[lane] | ((uint32_t)GZ_DEXT[lane] << 16);
+  if (lane < 19u) L.ord[lane] = GZ_ORD[lane];
+  wave_sync();
+  const int j = (int)(blockIdx.x * GQ_JOBS + lane);
+  if (lane >= GQ_JOBS || j >= n_jobs) return;  // (no cross-lane operation follows)
+  const GzJobDev J = jobs[j];
+  if (J.src_offset + J.src_size > src_bytes || J.dst_offset + J.dst_size > dst_bytes) {
+    mode[j] = GQ_INLINE;
+    return;
+  }
+  const rsrc_t rs = make_rsrc(src, src_bytes);
+  mode[j] = gq_job(L, L.l[lane], rs, J, dst, recs);
+}
+
+// Replay: the records of a pre-passed page in 189-byte output windows. Every byte of a window gets its
+// source — itself (a literal the pre-pass stored, read back into LDS) or the output position its
+// back-reference copies — and the window is resolved by the shared executor.
+__global__ __launch_bounds__(WAVE) void k_gzip_replay(uint8_t* __restrict__ dst, uint64_t dst_bytes,
+                                                      const GzJobDev* __restrict__ jobs, int n_jobs,
+                                                      const uint64_t* __restrict__ recs,
+                                                      const int32_t* __restrict__ mode, int32_t* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[LZ_RING];
+  __shared__ __attribute__((aligned(16))) uint8_t lits[256];
+  __shared__ uint32_t sS[LZ_CAP];
+  __shared__ uint64_t rq[256];  // records [rq0, rq0 + 256)
+  const int jb = (int)blockIdx.x;
+  if (jb >= n_jobs || mode[jb] < 0) return;
+  const uint32_t nrec = (uint32_t)mode[jb];
+  const uint32_t lane = lane_id();
+  const GzJobDev J = jobs[jb];
+  const uint32_t ulen = uni(J.dst_size);
+  uint8_t* out = dst + J.dst_offset;
+  const rsrc_t ro = make_rsrc(out, dst_bytes - J.dst_offset);
+  const uint64_t* rec = recs + J.dst_offset / 3u;
+  uint32_t ri = 0, rq0 = 0, rqn = 0;  // next record; queue [rq0, rq0 + rqn)
+  bool more = true;                   // records past the queue may exist
+  for (uint32_t A = 0; A < ulen; A += GQ_OUTW) {
+    const uint32_t T = ulen - A < GQ_OUTW ? ulen - A : GQ_OUTW;
+    const uint32_t Bend = A + T;
+    if (more && ri + WAVE > rq0 + rqn) {  // refill the queue from ri
+      rq0 = ri;
+      for (uint32_t k = lane; k < 256u; k += WAVE) {
+        const uint32_t i = rq0 + k;
+        rq[k] = i < nrec ? rec[i] : ~0ull;
+      }
+      rqn = rq0 + 256u <= nrec ? 256u : nrec - rq0;
+      more = rq0 + rqn < nrec;
+      wave_sync();
+    }
+    // the literal bytes of the window, and every byte's default source: itself
+    for (uint32_t i = lane; i < T; i += WAVE) {
+      const uint32_t a = A + i;
+      lits[i] = (uint8_t)(__builtin_amdgcn_raw_buffer_load_b32(ro, (int)(a & ~3u), 0, 0) >> ((a & 3u) * 8u));
+      sS[i] = LZ_LIT | i;
+    }
+    // records overlapping the window: a prefix of the queue from ri (output positions ascending)
+    const uint32_t k = ri + lane;
+    const uint64_t r = k < rq0 + rqn ? rq[k - rq0] : ~0ull;
+    const uint32_t at = (uint32_t)r, dist = (uint32_t)(r >> 32) & 0xFFFFu, len = (uint32_t)(r >> 48);
+    const bool valid = k < rq0 + rqn && at < Bend;  // (a queued record ends past A: ri moves past finished ones)
+    const uint64_t stop = __ballot(!valid);
+    const uint32_t m = stop ? (uint32_t)__builtin_ctzll(stop) : WAVE;
+    wave_sync();
+    if (lane < m) {
+      const uint32_t b0 = at > A ? at : A, b1 = at + len < Bend ? at + len : Bend;
+      for (uint32_t q = b0; q < b1; q++) sS[q - A] = q - dist;
+    }
+    wave_sync();
+    lz_exec_sources<255u>(ring, lits, sS, T, A, out, ro);
+    // records that end inside the window are done
+    const uint64_t done = __ballot(lane < m && at + len <= Bend);
+    ri += (uint32_t)__builtin_popcountll(done);
+  }
+  if (lane == 0 && status) status[jb] = 0;
+}
+
 hipError_t launch_gzip(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
-                       const void* jobs, int n_jobs, int32_t* status) {
+                       const void* jobs, int n_jobs, int32_t* status, uint64_t* recs, int32_t* mode) {
   if (n_jobs <= 0) return hipSuccess;
+  if (!(recs && mode && PQG_GZ_2P)) mode = nullptr;
+  if (mode) {
+    hipLaunchKernelGGL(k_gzip_seq, dim3((n_jobs + (int)GQ_JOBS - 1) / (int)GQ_JOBS), dim3(64), 0, st, src, src_bytes,
+                       dst, dst_bytes, (const GzJobDev*)jobs, n_jobs, recs, mode);
+    hipLaunchKernelGGL(k_gzip_replay, dim3(n_jobs), dim3(WAVE), 0, st, dst, dst_bytes, (const GzJobDev*)jobs, n_jobs,
+                       (const uint64_t*)recs, (const int32_t*)mode, status);
+  }
   hipLaunchKernelGGL(k_gzip, dim3(n_jobs), dim3(WAVE), 0, st, src, src_bytes, dst, dst_bytes,
-                     (const GzJobDev*)jobs, n_jobs, status);
+                     (const GzJobDev*)jobs, n_jobs, status, (const int32_t*)mode);
   return hipGetLastError();
 }
 

@@ -399,6 +399,22 @@ def test_many_zlib_streams(decoder, skew):
 
 
 @pytest.mark.gpu
+def test_large_pages(decoder):
+    """Pages of 160 KB (parquet-mr's int64 pages of 20,000 values, text-like rows) at zlib levels 1, 6
+    and 9: dynamic blocks with 259+ literal/length codes, 30 distance codes and 32 KiB distances,
+    many blocks per page, tens of thousands of back-references (the token pre-pass's common case)."""
+    rng = np.random.default_rng(11)
+    raws = []
+    for lvl in (1, 6, 9):
+        raws.append(np.cumsum(rng.integers(-100, 1000, size=20000)).astype(np.int64).tobytes())
+        raws.append(b"".join(f"{int(v)},row-{int(v) % 977};".encode() for v in rng.integers(0, 1 << 30, size=9000)))
+    streams = [gzip.compress(r, compresslevel=[1, 1, 6, 6, 9, 9][i]) for i, r in enumerate(raws)]
+    got, status = _run(decoder, streams, [len(r) for r in raws])
+    assert list(status) == [0] * len(raws)
+    assert got == raws
+
+
+@pytest.mark.gpu
 def test_malformed_streams(decoder):
     cases = _corrupt_cases()
     good = gzip.compress(b"abc")
