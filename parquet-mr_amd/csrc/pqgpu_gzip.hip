@@ -769,7 +769,9 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
         const int e2 = gq_build(T, T.lens + 288, (int)ndist, T.dcount, T.dsym, T.dfast, 1, L.disttab);
         if (e2 != 0) return GQ_INLINE;
       }
-      // ---- the block's tokens
+      // ---- the block's tokens: one step per token with the literal and back-reference forms
+      // computed side by side (selects, both table reads issued together) and one exit test; codes
+      // longer than the first-level tables take a rare branch
       while (true) {
         {  // re-centre every window of the loop together when one could leave its window
           const bool want = (uint32_t)(bp >> 3) + 24u > wlo + GQ_WIN || (uint32_t)(bp >> 3) < wlo;
@@ -777,54 +779,46 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
         }
         const uint64_t x = peek(bp);
         uint32_t e = T.lfast[(uint32_t)x & ((1u << GZ_FAST) - 1u)];
-        uint32_t l;
+        bool bad = false;
+        uint32_t l = gz_ent_len(e);
         if (e == GZ_SLOW) {
           const int s2 = gq_slow(x, T.lcount, T.lsym, &l);
-          if (s2 < 0) return GQ_INLINE;
-          e = (uint32_t)s2;
+          bad = s2 < 0;
+          e = s2 < 0 ? 0u : (uint32_t)s2;
           if (s2 > 256 && s2 < 286) {
             const uint32_t t = L.lentab[s2 - 257];
             e |= ((t & 0x1FFu) << 13) | ((t >> 16) << 22);
           }
-        } else {
-          l = gz_ent_len(e);
         }
         const uint32_t sym = gz_ent_sym(e);
-        if (sym < 256u) {
-          if (op >= ulen || bp + l > endbit) return GQ_INLINE;
-          gst(out + op, (uint8_t)sym);
-          op++;
-          bp += l;
-          continue;
-        }
-        if (sym == 256u) {
-          bp += l;
-          if (bp > endbit) return GQ_INLINE;
-          break;
-        }
-        if (sym > 285u) return GQ_INLINE;
-        const uint32_t lext = (e >> 22) & 7u;
-        const uint32_t len = ((e >> 13) & 0x1FFu) + (uint32_t)((x >> l) & ((1u << lext) - 1u));
+        const bool lit = sym < 256u, eob = sym == 256u;
+        const uint32_t lext = lit || eob ? 0u : (e >> 22) & 7u;
+        const uint32_t len = lit ? 1u : ((e >> 13) & 0x1FFu) + (uint32_t)((x >> l) & ((1u << lext) - 1u));
         const uint64_t y = x >> (l + lext);
         uint32_t d = T.dfast[(uint32_t)y & ((1u << GZ_FAST) - 1u)];
-        uint32_t dl;
-        if (d == GZ_SLOW) {
+        uint32_t dl = gz_ent_len(d);
+        if (!lit && !eob && d == GZ_SLOW) {
           const int s3 = gq_slow(y, T.dcount, T.dsym, &dl);
-          if (s3 < 0 || s3 >= 30) return GQ_INLINE;
-          const uint32_t t = L.disttab[s3];
-          d = (uint32_t)s3 | ((t & 0x7FFFu) << 13) | ((t >> 16) << 28);
-        } else {
-          dl = gz_ent_len(d);
+          bad |= s3 < 0 || s3 >= 30;
+          const uint32_t t = L.disttab[s3 < 0 || s3 >= 30 ? 0 : s3];
+          d = (uint32_t)(s3 < 0 ? 0 : s3) | ((t & 0x7FFFu) << 13) | ((t >> 16) << 28);
         }
-        if (gz_ent_sym(d) >= 30u) return GQ_INLINE;
         const uint32_t dext = d >> 28;
         const uint32_t dist = ((d >> 13) & 0x7FFFu) + (uint32_t)((y >> dl) & ((1u << dext) - 1u));
-        const uint32_t tb = l + lext + dl + dext;
-        if (bp + tb > endbit || dist > op - mstart || op + len > ulen || cnt >= rcap) return GQ_INLINE;
-        gst(rec + cnt, (uint64_t)op | ((uint64_t)dist << 32) | ((uint64_t)len << 48));
-        cnt++;
-        op += len;
+        const uint32_t tb = lit || eob ? l : l + lext + dl + dext;
+        bad |= bp + tb > endbit || sym > 285u;
+        if (!lit && !eob) bad |= gz_ent_sym(d) >= 30u || dist > op - mstart || cnt >= rcap;
+        if (!eob) bad |= op + len > ulen;  // (a page completing inside the member: the scalar decoder)
+        if (bad) return GQ_INLINE;
         bp += tb;
+        if (eob) break;
+        if (lit) {
+          gst(out + op, (uint8_t)sym);
+        } else {
+          gst(rec + cnt, (uint64_t)op | ((uint64_t)dist << 32) | ((uint64_t)len << 48));
+          cnt++;
+        }
+        op += len;
       }
     } while (!last);
     if (op >= ulen) break;  // complete: the trailer is not read
@@ -835,7 +829,9 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
     if (isz != op - mstart) return GQ_INLINE;
     q = at + 8u;
   }
-  return op == ulen ? (int32_t)cnt : GQ_INLINE;
+  // pages of long back-references (over 48 output bytes per record on average: few tokens, mostly
+  // copying) are cheaper for the scalar decoder than for 189-byte replay windows
+  return op == ulen && (cnt == 0u || ulen / cnt <= 48u) ? (int32_t)cnt : GQ_INLINE;
 }
 
 __global__ __launch_bounds__(64) void k_gzip_seq(const uint8_t* __restrict__ src, uint64_t src_bytes,
@@ -873,6 +869,10 @@ __global__ __launch_bounds__(WAVE) void k_gzip_replay(uint8_t* __restrict__ dst,
   const int jb = (int)blockIdx.x;
   if (jb >= n_jobs || mode[jb] < 0) return;
   const uint32_t nrec = (uint32_t)mode[jb];
+  if (nrec == 0u) {  // literals only: the pre-pass wrote the whole page
+    if (lane_id() == 0 && status) status[jb] = 0;
+    return;
+  }
   const uint32_t lane = lane_id();
   const GzJobDev J = jobs[jb];
   const uint32_t ulen = uni(J.dst_size);
