@@ -693,7 +693,7 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
   auto byte_at = [&](uint32_t q) -> uint32_t {  // byte q of the job's input (absolute offset so + q)
     return (ld32(rs, (so + q) & ~3u) >> (((so + q) & 3u) * 8u)) & 0xFFu;
   };
-  uint32_t op = 0, cnt = 0, q = 0;
+  uint32_t op = 0, cnt = 0, q = 0, ntok = 0;
   while (op < ulen) {
     // member header (RFC 1952 2.3)
     if (q + 10u > n) return GQ_INLINE;
@@ -739,10 +739,11 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
         uint32_t idx = 0;
         while (idx < nlen + ndist) {
           ensure(bp);
-          uint32_t cl = 0;
-          const int sym = gq_slow(peek(bp), T.dcount, T.dsym, &cl);
-          if (sym < 0) return GQ_INLINE;
-          bp += cl;
+          // the code-length code is complete with codes of <= 7 bits: one first-level lookup
+          const uint32_t ce = T.dfast[(uint32_t)peek(bp) & ((1u << GZ_FAST) - 1u)];
+          if (ce == GZ_SLOW) return GQ_INLINE;
+          const int sym = (int)gz_ent_sym(ce);
+          bp += gz_ent_len(ce);
           if (sym < 16) {
             T.lens[idx++] = (uint8_t)sym;
           } else {
@@ -819,6 +820,7 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
           cnt++;
         }
         op += len;
+        if (++ntok == 64u && op > 48u * 64u) return GQ_INLINE;  // long back-references: see below
       }
     } while (!last);
     if (op >= ulen) break;  // complete: the trailer is not read
