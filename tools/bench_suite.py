@@ -44,7 +44,7 @@ HBM_PEAK_GBS = 8000.0
 
 def gen(name, rows):
     """-> workloads.Workload (column chunks + the values written, for verification)."""
-    if name in ("c2_zipf2", "c3_mixed", "c5_levels", "c4_lineitem"):
+    if name in ("c2_zipf2", "c3_mixed", "c5_levels", "c4_lineitem") or name in WL.C3_PARTS:
         return WL.generate(name, rows)
     rng = np.random.default_rng(7)
     E = WL.Expected
@@ -320,7 +320,8 @@ def main():
                     "c2_zstd": 100_000_000, "plain_i64_zstd": 100_000_000,
                     "c2_lz4": 100_000_000, "plain_i64_lz4": 100_000_000,
                     "c2_gzip": 100_000_000, "plain_i64_gzip": 100_000_000,
-                    "c4_lineitem": 8_000_000}
+                    "c4_lineitem": 8_000_000, "c3_delta": 100_000_000, "c3_double": 100_000_000,
+                    "c3_strings": 100_000_000}
     for w in args.workloads:
         rows = args.rows or default_rows[w]
         if args.gen_only:

@@ -107,6 +107,9 @@ def c3_mixed(rows, log=True):
     return Workload("c3_mixed", out, exp)
 
 
+C3_PARTS = {"c3_delta": (0, 1, 4, 5), "c3_double": (2, 6), "c3_strings": (3, 7)}
+
+
 def c5_levels(recs):
     rng = np.random.default_rng(7)
     lens = rng.poisson(3, size=recs)
@@ -168,6 +171,10 @@ def generate(name, rows):
         return c2(rows, a=2.0)
     if name == "c3_mixed":
         return c3_mixed(rows)
+    if name in C3_PARTS:  # C3's columns of one kind alone (kernel times without the other columns' overlap)
+        w = c3_mixed(rows)
+        keep = C3_PARTS[name]
+        return Workload(name, [w.chunks[i] for i in keep], [w.expect[i] for i in keep])
     if name == "c5_levels":
         return c5_levels(rows)
     if name == "c4_lineitem":
