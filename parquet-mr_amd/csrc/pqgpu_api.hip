@@ -203,6 +203,7 @@ struct pqg_ctx {
   // pqg_ctx_set_dispatch: kernel-choice overrides for the plans created on this ctx
   int plain_mode = 2;       // PQG_DISPATCH_PLAIN_ONE_PASS
   bool dict_direct = true;  // PQG_DISPATCH_DICT_DIRECT
+  uint32_t gz_prepass_min = pqg::GZ_PREPASS_MIN;  // PQG_DISPATCH_GZIP_PREPASS_MIN
 };
 
 extern "C" {
@@ -274,6 +275,10 @@ int pqg_ctx_set_dispatch(pqg_ctx* ctx, int key, int value) {
     case PQG_DISPATCH_DICT_DIRECT:
       if (value != 0 && value != 1) return PQG_ERR_INVALID_ARG;
       ctx->dict_direct = value != 0;
+      return PQG_OK;
+    case PQG_DISPATCH_GZIP_PREPASS_MIN:
+      if (value < 0) return PQG_ERR_INVALID_ARG;
+      ctx->gz_prepass_min = (uint32_t)value;
       return PQG_OK;
     default: return PQG_ERR_INVALID_ARG;
   }
@@ -1858,7 +1863,7 @@ int pqg_gzip_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, 
     }
   }
   const hipError_t e = pqg::launch_gzip(ctx->stream, d_src, src_bytes, d_dst, dst_bytes, d_jobs, n_jobs, d_status,
-                                        recs, mode);
+                                        recs, mode, ctx->gz_prepass_min);
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
 }
 

@@ -585,6 +585,7 @@ constexpr uint32_t GQ_WIN = 512;
 constexpr int32_t GQ_INLINE = -1;  // mode[j]: -1 = k_gzip decodes job j, else its record count
 constexpr uint32_t GQ_OUTW = 189;  // replay output window (<= 63 records of >= 3 bytes + one from before)
 
+
 struct GqLane {
   uint8_t win[GQ_WIN + 16];  // input bytes [wlo, wlo + GQ_WIN) (offsets into src)
   uint32_t lfast[1u << GZ_FAST], dfast[1u << GZ_FAST];
@@ -839,7 +840,8 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
 __global__ __launch_bounds__(64) void k_gzip_seq(const uint8_t* __restrict__ src, uint64_t src_bytes,
                                                  uint8_t* __restrict__ dst, uint64_t dst_bytes,
                                                  const GzJobDev* __restrict__ jobs, int n_jobs,
-                                                 uint64_t* __restrict__ recs, int32_t* __restrict__ mode) {
+                                                 uint64_t* __restrict__ recs, int32_t* __restrict__ mode,
+                                                 uint32_t min_out) {
   __shared__ __attribute__((aligned(16))) GqLds L;
   const uint32_t lane = lane_id();
   if (lane < 29u) L.lentab[lane] = GZ_LBASE[lane] | ((uint32_t)GZ_LEXT[lane] << 16);
@@ -849,7 +851,7 @@ __global__ __launch_bounds__(64) void k_gzip_seq(const uint8_t* __restrict__ src
   const int j = (int)(blockIdx.x * GQ_JOBS + lane);
   if (lane >= GQ_JOBS || j >= n_jobs) return;  // (no cross-lane operation follows)
   const GzJobDev J = jobs[j];
-  if (J.src_offset + J.src_size > src_bytes || J.dst_offset + J.dst_size > dst_bytes) {
+  if (J.src_offset + J.src_size > src_bytes || J.dst_offset + J.dst_size > dst_bytes || J.dst_size < min_out) {  // (small pages: k_gzip)
     mode[j] = GQ_INLINE;
     return;
   }
@@ -924,12 +926,13 @@ __global__ __launch_bounds__(WAVE) void k_gzip_replay(uint8_t* __restrict__ dst,
 }
 
 hipError_t launch_gzip(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
-                       const void* jobs, int n_jobs, int32_t* status, uint64_t* recs, int32_t* mode) {
+                       const void* jobs, int n_jobs, int32_t* status, uint64_t* recs, int32_t* mode,
+                       uint32_t prepass_min) {
   if (n_jobs <= 0) return hipSuccess;
   if (!(recs && mode && PQG_GZ_2P)) mode = nullptr;
   if (mode) {
     hipLaunchKernelGGL(k_gzip_seq, dim3((n_jobs + (int)GQ_JOBS - 1) / (int)GQ_JOBS), dim3(64), 0, st, src, src_bytes,
-                       dst, dst_bytes, (const GzJobDev*)jobs, n_jobs, recs, mode);
+                       dst, dst_bytes, (const GzJobDev*)jobs, n_jobs, recs, mode, prepass_min);
     hipLaunchKernelGGL(k_gzip_replay, dim3(n_jobs), dim3(WAVE), 0, st, dst, dst_bytes, (const GzJobDev*)jobs, n_jobs,
                        (const uint64_t*)recs, (const int32_t*)mode, status);
   }

@@ -138,8 +138,13 @@ hipError_t launch_lz4raw(hipStream_t st, const uint8_t* src, uint64_t src_bytes,
 // (literals stored in place, back-references as 8-byte records at dst_offset / 3: recs holds
 // dst_bytes / 3 + 2 of them) and replayed by k_gzip_replay; mode[j] (n_jobs int32) = the job's record
 // count, or -1 for the jobs left to k_gzip.
+// Pages of fewer output bytes than prepass_min skip the token pre-pass (one lane builds a dynamic block's
+// Huffman tables serially there; k_gzip's wave builds them in parallel, which small pages, with few
+// tokens to share the cost, need): PQG_DISPATCH_GZIP_PREPASS_MIN, default GZ_PREPASS_MIN.
+constexpr uint32_t GZ_PREPASS_MIN = 16384;
 hipError_t launch_gzip(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
-                       const void* jobs, int n_jobs, int32_t* status, uint64_t* recs, int32_t* mode);
+                       const void* jobs, int n_jobs, int32_t* status, uint64_t* recs, int32_t* mode,
+                       uint32_t prepass_min = GZ_PREPASS_MIN);
 // DELTA_BYTE_ARRAY prefix / suffix lengths (k_delta MODE 2: bsrc = prefix, blen = value length, aux;
 // dba_meta: per BIN_CHUNK-value chunk {suffix bytes before it, smallest prefix in it};
 // PageWork::reserved = 1 when a value is longer than DBA_VB: that page takes the serial copy)

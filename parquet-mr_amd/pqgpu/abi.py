@@ -216,3 +216,4 @@ def numpy_dtype(physical_type, type_length=0):
 # pqg_ctx_set_dispatch keys (include/pqgpu.h enum pqg_dispatch)
 DISPATCH_PLAIN_ONE_PASS = 1
 DISPATCH_DICT_DIRECT = 2
+DISPATCH_GZIP_PREPASS_MIN = 3  # pqg_gzip_decompress: smallest page (output bytes) for the token pre-pass

@@ -373,6 +373,17 @@ def test_gzip_fixtures_hold_compressed_pages():
 
 # ---- GPU --------------------------------------------------------------------------------------------
 
+@pytest.fixture(params=["small_pages_wave", "every_page_prepass"])
+def prepass(decoder, request):
+    """Pages below PQG_DISPATCH_GZIP_PREPASS_MIN (default 16384 output bytes) go to the one-wave
+    decoder; with 0 every page takes the token pre-pass (and, for what it hands back, the wave decoder),
+    so both paths see every case."""
+    if request.param == "every_page_prepass":
+        decoder.set_dispatch(abi.DISPATCH_GZIP_PREPASS_MIN, 0)
+    yield request.param
+    decoder.set_dispatch(abi.DISPATCH_GZIP_PREPASS_MIN, 16384)
+
+
 def _run(decoder, streams, sizes, skew=False):
     out, offs, status = decoder.gzip_decompress(streams, sizes, skew=skew)
     host = out.cpu().numpy()
@@ -381,7 +392,7 @@ def _run(decoder, streams, sizes, skew=False):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("skew", [False, True])
-def test_handmade_streams(decoder, skew):
+def test_handmade_streams(decoder, skew, prepass):
     cases = _handmade()
     got, status = _run(decoder, [c[0] for c in cases], [c[1] for c in cases], skew=skew)
     assert list(status) == [0] * len(cases)
@@ -391,7 +402,7 @@ def test_handmade_streams(decoder, skew):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("skew", [False, True])
-def test_many_zlib_streams(decoder, skew):
+def test_many_zlib_streams(decoder, skew, prepass):
     raws, streams = _zlib_streams()
     got, status = _run(decoder, streams, [len(r) for r in raws], skew=skew)
     assert list(status) == [0] * len(raws)
@@ -415,7 +426,7 @@ def test_large_pages(decoder):
 
 
 @pytest.mark.gpu
-def test_malformed_streams(decoder):
+def test_malformed_streams(decoder, prepass):
     cases = _corrupt_cases()
     good = gzip.compress(b"abc")
     streams, sizes = [good], [3]
