@@ -694,7 +694,7 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
   auto byte_at = [&](uint32_t q) -> uint32_t {  // byte q of the job's input (absolute offset so + q)
     return (ld32(rs, (so + q) & ~3u) >> (((so + q) & 3u) * 8u)) & 0xFFu;
   };
-  uint32_t op = 0, cnt = 0, q = 0, ntok = 0;
+  uint32_t op = 0, cnt = 0, q = 0;
   while (op < ulen) {
     // member header (RFC 1952 2.3)
     if (q + 10u > n) return GQ_INLINE;
@@ -821,7 +821,6 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
           cnt++;
         }
         op += len;
-        if (++ntok == 64u && op > 48u * 64u) return GQ_INLINE;  // long back-references: see below
       }
     } while (!last);
     if (op >= ulen) break;  // complete: the trailer is not read
