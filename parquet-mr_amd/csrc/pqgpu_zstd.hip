@@ -1194,6 +1194,9 @@ __device__ bool zq_table(const ZqLds& L, int kind, ZqLane& T, uint32_t r, int* t
   return have;
 }
 
+#ifndef PQG_ZQ_LEAN
+#define PQG_ZQ_LEAN 1  // 0: every record bound checked per sequence (A/B builds)
+#endif
 // The sequences of one compressed block's sequence section [q, lim) (absolute input offsets). Returns
 // false for anything the inline path must handle.
 __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32_t lim, uint32_t regen, uint32_t& outp,
@@ -1264,6 +1267,11 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
   need(tlog[0] + tlog[1] + tlog[2]);
   uint32_t sl = get(tlog[0]), so = get(tlog[1]), sm = get(tlog[2]);
   uint32_t r0 = rep[0], r1 = rep[1], r2 = rep[2], lits = 0;
+  // record room for the block's sequences, checked once. The record fields need no check per sequence:
+  // literal and match lengths stay below 2^17 (LL code 35: 65536 + 16 extra bits; ML code 52: 65539 +
+  // 16 bits; the tables hold valid codes only), and an offset that passes the window check is at most
+  // the output so far (< 2^27 + 2^18: jobs of < 2^27 bytes)
+  if (PQG_ZQ_LEAN && cnt + nseq > cap) return false;
   // One sequence = one pass with no data-dependent branch on the common path: the table entries and
   // 20 window bytes at the read position are loaded together; the sequence's bits (offset, match and
   // literal length extras, then the LL / ML / OF state bits: T <= 64 of them, else the inline path
@@ -1334,7 +1342,9 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
       so = nso;
     }
     bad |= bits < 0 || lits + ll > regen || roff == 0 || roff > outp + ll - frame0;
+#if !PQG_ZQ_LEAN
     bad |= ll >= (1u << 18) || ml >= (1u << 18) || roff >= (1u << 28) || cnt >= cap;
+#endif
     if (bad) return false;
     gst(rec + cnt, (uint64_t)ll | ((uint64_t)ml << 18) | ((uint64_t)roff << 36));
     cnt++;
