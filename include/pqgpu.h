@@ -306,7 +306,10 @@ int pqg_plan_kernel_count(pqg_plan* plan);
  * page's walk). Should an expansion wait longer than 2 s (the GPU did not dispatch the walker it
  * waits for), that launch reports PQG_ERR_TIMEOUT internally and pqg_sync re-runs the plan with the
  * walk and the expansion as two launches; the plan keeps that mode and the caller sees the normal
- * result. Returns how many launches of the plan were re-run that way. */
+ * result. The same holds for a segment of a segmented PLAIN BYTE_ARRAY page walk (per-value path,
+ * few large pages) whose predecessor segment did not publish within 2 s: the plan re-runs with those
+ * pages walked one wave each, and keeps that mode. Returns how many launches of the plan were re-run
+ * either way. */
 int pqg_plan_timeout_fallbacks(pqg_plan* plan);
 /* BYTE_ARRAY columns whose pages are all PLAIN decode in one pass per 2 KiB tile of the pages (walk,
  * offsets and value bytes together), which takes each page's values to fill its data section, as

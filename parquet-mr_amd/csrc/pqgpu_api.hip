@@ -168,6 +168,10 @@ struct pqg_plan {
   uint64_t pticket_off = 0, pflag_off = 0;  // in bscratch: ticket (cleared per launch), inexact flag (epoch-tagged)
   uint64_t blen_bytes_nf = 0;               // cleared part of bscratch when plain_fused
   int n_binp_fused = 0, n_bin_cols_nf = 0;  // tails of cls_lists[C_BINP] / bin_cols that belong to those columns
+  // pages k_bin_walk_seg walks (the last n_binp_seg of cls_lists[C_BINP], after the one-pass columns'
+  // pages); seg_walk false: one wave per page instead (pqg_sync's re-run after a segment wait timed out)
+  int n_binp_seg = 0;
+  bool seg_walk = true;
   uint32_t n_bin_blocks_nf = 0, n_bin_chunks_nf = 0;
 };
 
@@ -336,7 +340,7 @@ static int count_kernels(const pqg_plan* P) {
   const bool pf = P->plain_fused;
   int k = (P->levels_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
   for (int c = 0; c < C_NCLS; c++) {
-    const int n = P->cls_n[(size_t)c] - (c == C_BINP && pf ? P->n_binp_fused : 0);
+    const int n = P->cls_n[(size_t)c] - (c == C_BINP ? P->n_binp_seg + (pf ? P->n_binp_fused : 0) : 0);
     if (n) k += (c == C_DICT4 || c == C_DICT8 || c == C_IDS) && !P->dict_fused ? 2 : 1;
   }
   k += (P->n_dict_walk ? 1 : 0) + (P->n_bind ? 1 : 0) + (P->n_fixd ? 1 : 0) +
@@ -690,13 +694,16 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   P->n_bin_chunks_nf = (uint32_t)bin_chunks.size();
   bin_chunks.insert(bin_chunks.end(), plain_chunks.begin(), plain_chunks.end());
   {  // PLAIN pages: walked by k_bin_walk_seg (not listed), one wave per page, the one-pass columns last
-    std::vector<int> keep, tail;
+    std::vector<int> keep, tail, seg;
     for (int p : cls_lists[C_BINP]) {
       if (plain_col[(size_t)P->h_work[(size_t)p].column]) tail.push_back(p);
       else if (!seg_page[(size_t)p]) keep.push_back(p);
+      else seg.push_back(p);
     }
     P->n_binp_fused = (int)tail.size();
+    P->n_binp_seg = (int)seg.size();
     keep.insert(keep.end(), tail.begin(), tail.end());
+    keep.insert(keep.end(), seg.begin(), seg.end());
     cls_lists[C_BINP].swap(keep);
   }
   // ---- DELTA_BYTE_ARRAY pages: BIN_CHUNK-value chunks (upper bound from the slot count)
@@ -901,7 +908,7 @@ int pqg_plan_launch(pqg_plan* P) {
 #ifndef PQG_NO_FORK
   const bool has_fixed = P->cls_n[C_DICT4] || P->cls_n[C_DICT8] || P->cls_n[C_PLAIN] || P->cls_n[C_BOOL] ||
                          P->cls_n[C_RLEBOOL] || P->cls_n[C_DELTA4] || P->cls_n[C_DELTA8] || P->cls_n[C_BSS];
-  const bool has_bin = P->n_dict_walk || P->cls_n[C_IDS] || P->cls_n[C_BINP] - (pf ? P->n_binp_fused : 0) > 0 ||
+  const bool has_bin = P->n_dict_walk || P->cls_n[C_IDS] || P->cls_n[C_BINP] - P->n_binp_seg - (pf ? P->n_binp_fused : 0) > 0 ||
                        P->cls_n[C_DLBA] || P->cls_n[C_DBA] || P->n_segs;
   const bool want = e == hipSuccess && ((pf && (has_fixed || has_bin)) || (has_bin && has_fixed));
   const bool ev_ok = want && (ctx->ev_fork || hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) == hipSuccess) &&
@@ -936,7 +943,7 @@ int pqg_plan_launch(pqg_plan* P) {
     e = pqg::launch_bin_walk(sb, P->d_bytes, P->n_bytes, work, cols, bl + P->off_dict_walk, P->n_dict_walk, 1, P->n_pages,
                              err, ecount);
   for (int k = 0; k < C_NCLS && e == hipSuccess; k++) {
-    int n = P->cls_n[(size_t)k] - (k == C_BINP && pf ? P->n_binp_fused : 0);
+    int n = P->cls_n[(size_t)k] - (k == C_BINP ? P->n_binp_seg + (pf ? P->n_binp_fused : 0) : 0);
     if (!n) continue;
     const int32_t* l = lists + P->cls_off[(size_t)k];
     switch (k) {
@@ -970,7 +977,11 @@ int pqg_plan_launch(pqg_plan* P) {
       case C_DELTA8: e = pqg::launch_delta(8, sf, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
     }
   }
-  if (e == hipSuccess && P->n_segs) {  // PLAIN BYTE_ARRAY pages in segments (status + ticket cleared above)
+  if (e == hipSuccess && P->n_segs && !P->seg_walk)  // the segmented pages one wave each (after a timeout)
+    e = pqg::launch_bin_walk(sb, P->d_bytes, P->n_bytes, work, cols,
+                             lists + P->cls_off[C_BINP] + (P->cls_n[C_BINP] - P->n_binp_seg), P->n_binp_seg, 0,
+                             P->n_pages, err, ecount);
+  if (e == hipSuccess && P->n_segs && P->seg_walk) {  // PLAIN BYTE_ARRAY pages in segments (status + ticket cleared above)
     uint8_t* scb = (uint8_t*)P->bscratch.p;
     e = pqg::launch_bin_walk_seg(sb, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->segs.p, P->n_segs,
                                  (uint64_t*)(scb + P->seg_status_off), (uint32_t*)(scb + P->seg_status_off) + 2u * P->n_segs,
@@ -1181,6 +1192,22 @@ int sync_plan(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work) {
     // which have no inter-workgroup waits; the plan keeps that mode. Every output of the re-run is
     // written again, so the result is the same bit for bit.
     P->dict_fused = false;
+    P->kernels = count_kernels(P);
+    P->timeout_fallbacks++;
+    rc = pqg_plan_launch(P);
+    if (rc == PQG_OK) {
+      if (st) { std::memset(st, 0, sizeof(*st)); st->page = -1; }
+      work->clear();
+      rc = resolve_errors(P, st, work);
+    }
+  }
+  // likewise a segment of a segmented PLAIN BYTE_ARRAY page that waited past its bound for its
+  // predecessor's publication (k_bin_walk_seg; the predecessor always holds an earlier ticket, so this
+  // needs a starved wave): the plan re-runs with those pages one wave each and keeps that mode
+  const int tpage2 = st ? (int)st->page : -1;
+  const int tcls2 = tpage2 >= 0 && tpage2 < P->n_pages ? P->page_cls[(size_t)tpage2] : -1;
+  if (rc == PQG_ERR_TIMEOUT && P->n_segs && P->seg_walk && tcls2 == C_BINP) {
+    P->seg_walk = false;
     P->kernels = count_kernels(P);
     P->timeout_fallbacks++;
     rc = pqg_plan_launch(P);

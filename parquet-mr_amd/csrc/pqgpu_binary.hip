@@ -402,6 +402,14 @@ constexpr uint32_t SEG_B = 8 * BW_WIN;       // section bytes per segment
 constexpr uint32_t SEG_CAP = SEG_B / 4 + 2;  // values that can start in a segment (each takes >= 4 bytes)
 constexpr uint32_t SEG_LINKS = 6;
 constexpr uint64_t SG_OK = 1ull << 62, SG_STOP = 2ull << 62;
+#ifdef PQG_FAULT_INJECT
+// Fault-injection build (tests/build/libpqgpu_faultinject.so, tests/test_gpu_timeout.py only; never the
+// product): the wave holding ticket 0 publishes PQG_FAULT_INJECT ticks late, past a wait bound
+// shortened to 0.1 s, so the segments after it time out
+constexpr uint64_t SEG_TIMEOUT_TICKS = 10000000ull;
+#else
+constexpr uint64_t SEG_TIMEOUT_TICKS = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+#endif
 static_assert(SEG_B == BW_SEG_BYTES && SEG_CAP == BW_SEG_CAP, "host segmentation (pqgpu_internal.h)");
 static_assert(BW_WIN == BP_TILE, "host tiling of k_bin_plain (pqgpu_internal.h)");
 
@@ -471,7 +479,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_walk_seg(const uint8_t* __rest
       if (v) break;
       __builtin_amdgcn_s_sleep(2);
       // bounded (s_memrealtime: 100 MHz): a predecessor that never publishes is PQG_ERR_TIMEOUT, not a hang
-      if (__builtin_amdgcn_s_memrealtime() - t_wait > 200000000ull) {
+      if (__builtin_amdgcn_s_memrealtime() - t_wait > SEG_TIMEOUT_TICKS) {
         if (lane == 0) {
           report(err, err_count, page, 2, 0, PQG_ERR_TIMEOUT);
           sst(status + t, SG_STOP);
@@ -494,6 +502,12 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_walk_seg(const uint8_t* __rest
     wave_sync();
     r = bin_walk_core(L, rs, entry, end, SEG_CAP, tl, ts, false, stop);
   }
+#ifdef PQG_FAULT_INJECT
+  if (t == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)PQG_FAULT_INJECT) __builtin_amdgcn_s_sleep(127);
+  }
+#endif
   const uint32_t room = N - before;
   const uint32_t take = r.produced < room ? r.produced : room;
   bool done = r.produced >= room;

@@ -70,3 +70,61 @@ def test_timed_out_fused_launch_is_rerun_split_and_bit_exact(tmp_path):
     s = res["second"]
     assert s["rc"] == 0 and s["equal"] and s["fallbacks"] == 1, res  # split mode stays: no further timeout
     assert res["decode"]["equal"], res
+
+
+CHILD_SEG = r"""
+import json, sys
+import numpy as np, torch
+sys.path[:0] = [sys.argv[1] + "/parquet-mr_amd", sys.argv[1] + "/tools", sys.argv[1]]
+from pqgpu import abi, decoder as D, native
+from tools.synth import writer
+assert native.LIB_PATH.endswith("libpqgpu_faultinject.so"), native.LIB_PATH
+vals = writer.BinaryValues.random(60_000, 4, 32, seed=5)
+chunk = writer.write_column_chunk(abi.BYTE_ARRAY, vals, abi.PLAIN)  # 3 pages of ~440 KB: segmented
+batch = writer.build_batch([chunk])
+exp_off = torch.from_numpy(vals.offsets)
+exp_data = torch.from_numpy(vals.data[: int(vals.offsets[-1])].copy())
+dec = D.Decoder(0, poison=0xA5)
+dec.set_dispatch(abi.DISPATCH_PLAIN_ONE_PASS, 0)  # the per-value path: k_bin_walk_seg for few large pages
+dbatch = dec.upload(batch)
+cols = dec.alloc_columns(batch)
+plan = dec.plan(dbatch, cols)
+k0 = plan.kernel_count
+def same(c):
+    off = c.offsets().cpu()
+    return bool(torch.equal(off, exp_off)) and bool(torch.equal(c.binary_data[: int(off[-1])].cpu(), exp_data))
+out = {}
+plan.launch()
+rc, st = plan.sync()
+out["first"] = {"rc": rc, "fallbacks": plan.timeout_fallbacks, "kernels": plan.kernel_count, "kernels_before": k0,
+                "equal": same(cols[0])}
+cols[0].binary_data.fill_(0xA5)
+plan.launch()
+rc, st = plan.sync()
+out["second"] = {"rc": rc, "fallbacks": plan.timeout_fallbacks, "equal": same(cols[0])}
+plan.close()
+dec.close()
+print("RESULT " + json.dumps(out))
+"""
+
+
+@pytest.mark.gpu
+def test_timed_out_segment_walk_is_rerun_per_page_and_bit_exact(tmp_path):
+    """The segmented PLAIN BYTE_ARRAY walk (k_bin_walk_seg): a segment whose predecessor publishes past
+    the wait bound reports PQG_ERR_TIMEOUT; pqg_sync re-runs the plan with those pages one wave each
+    (k_bin_walk) and the caller sees the normal, bit-exact result. Injected as above: the wave holding
+    the first ticket publishes 0.5 s late, the bound is 0.1 s."""
+    assert os.path.exists(INJECT_LIB), "build() makes the fault-injection library"
+    script = tmp_path / "child_seg.py"
+    script.write_text(CHILD_SEG)
+    env = dict(os.environ, PQGPU_LIB=INJECT_LIB)
+    r = subprocess.run([sys.executable, str(script), REPO], env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1]
+    res = json.loads(line[7:])
+    f = res["first"]
+    assert f["rc"] == 0 and f["equal"], res
+    assert f["fallbacks"] == 1, res                  # the injected delay did time the segment walk out
+    assert f["kernels"] == f["kernels_before"], res  # k_bin_walk_seg replaced by one k_bin_walk launch
+    s = res["second"]
+    assert s["rc"] == 0 and s["equal"] and s["fallbacks"] == 1, res  # per-page mode stays: no further timeout
