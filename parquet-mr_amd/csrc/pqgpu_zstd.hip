@@ -1194,6 +1194,9 @@ __device__ bool zq_table(const ZqLds& L, int kind, ZqLane& T, uint32_t r, int* t
   return have;
 }
 
+#ifndef PQG_ZQ_THR
+#define PQG_ZQ_THR 1  // 0: the re-centring test recomputed from the window base every sequence (A/B builds)
+#endif
 #ifndef PQG_ZQ_LEAN
 #define PQG_ZQ_LEAN 1  // 0: every record bound checked per sequence (A/B builds)
 #endif
@@ -1276,12 +1279,20 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
   // 20 window bytes at the read position are loaded together; the sequence's bits (offset, match and
   // literal length extras, then the LL / ML / OF state bits: T <= 64 of them, else the inline path
   // takes the job) come out of one 64-bit funnel shift; repeat offsets are selects.
+  // re-centring threshold: the window holds stream bits [bits - 160, bits) while bits >= rthr
+  // (sb + max(bits - 160, 0) / 8 >= wlo), recomputed when the window moves
+  int32_t rthr = wlo > sb ? (int32_t)(wlo - sb) * 8 + 160 : INT32_MIN;
   for (uint32_t i = 0; i < nseq; i++) {
     {  // a sequence reads at most 64 bits below `bits`: re-centre every window of the loop together
+#if PQG_ZQ_THR
+      const bool want = bits < rthr;
+#else
       const int32_t lowbit = bits - 160 > 0 ? bits - 160 : 0;
       const bool want = sb + ((uint32_t)lowbit >> 3) < wlo;
+#endif
       if (__ballot(want)) {
         recenter(sb + ((uint32_t)(bits > 0 ? bits : 0) >> 3));
+        rthr = wlo > sb ? (int32_t)(wlo - sb) * 8 + 160 : INT32_MIN;
 #ifdef PQG_DIAG
         zd.rec++;
 #endif
