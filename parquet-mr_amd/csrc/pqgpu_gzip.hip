@@ -582,6 +582,9 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
 #endif
 constexpr uint32_t GQ_JOBS = 12;
 constexpr uint32_t GQ_WIN = 512;
+#ifndef PQG_GQ_THR
+#define PQG_GQ_THR 1  // 0: the token loop's window test from wlo every token (A/B builds)
+#endif
 constexpr int32_t GQ_INLINE = -1;  // mode[j]: -1 = k_gzip decodes job j, else its record count
 constexpr uint32_t GQ_OUTW = 189;  // replay output window (<= 63 records of >= 3 bytes + one from before)
 
@@ -668,8 +671,12 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
   uint64_t* rec = recs + rbase;
   typedef uint32_t __attribute__((may_alias)) u32a;
   uint32_t wlo = 0xFFFFFFFFu;
+  // the token loop re-centres once bp >= rthr (fewer than 24 window bytes left above bp; bp only
+  // grows and every window starts at or below the position it was centred for)
+  uint64_t rthr = 0;
   auto recenter = [&](uint32_t byte) {
     wlo = byte & ~15u;
+    rthr = ((uint64_t)wlo + GQ_WIN - 23u) * 8u;
 #pragma unroll
     for (uint32_t o = 0; o < GQ_WIN; o += 16)
       *(u32x4*)(T.win + o) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(wlo + o), 0, 0);
@@ -776,7 +783,11 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
       // longer than the first-level tables take a rare branch
       while (true) {
         {  // re-centre every window of the loop together when one could leave its window
+#if PQG_GQ_THR
+          const bool want = bp >= rthr;
+#else
           const bool want = (uint32_t)(bp >> 3) + 24u > wlo + GQ_WIN || (uint32_t)(bp >> 3) < wlo;
+#endif
           if (__ballot(want)) recenter((uint32_t)(bp >> 3));
         }
         const uint64_t x = peek(bp);
