@@ -582,11 +582,14 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
 #endif
 constexpr uint32_t GQ_JOBS = 12;
 constexpr uint32_t GQ_WIN = 512;
+#ifndef PQG_GQ_ADAPT
+#define PQG_GQ_ADAPT 1  // 0: fixed 189-byte replay windows (A/B builds)
+#endif
 #ifndef PQG_GQ_THR
 #define PQG_GQ_THR 1  // 0: the token loop's window test from wlo every token (A/B builds)
 #endif
 constexpr int32_t GQ_INLINE = -1;  // mode[j]: -1 = k_gzip decodes job j, else its record count
-constexpr uint32_t GQ_OUTW = 189;  // replay output window (<= 63 records of >= 3 bytes + one from before)
+[[maybe_unused]] constexpr uint32_t GQ_OUTW = 189;  // fixed replay window (PQG_GQ_ADAPT=0: <= 63 records of >= 3 bytes + one from before)
 
 
 struct GqLane {
@@ -895,9 +898,7 @@ __global__ __launch_bounds__(WAVE) void k_gzip_replay(uint8_t* __restrict__ dst,
   const uint64_t* rec = recs + J.dst_offset / 3u;
   uint32_t ri = 0, rq0 = 0, rqn = 0;  // next record; queue [rq0, rq0 + rqn)
   bool more = true;                   // records past the queue may exist
-  for (uint32_t A = 0; A < ulen; A += GQ_OUTW) {
-    const uint32_t T = ulen - A < GQ_OUTW ? ulen - A : GQ_OUTW;
-    const uint32_t Bend = A + T;
+  for (uint32_t A = 0; A < ulen;) {
     if (more && ri + WAVE > rq0 + rqn) {  // refill the queue from ri
       rq0 = ri;
       for (uint32_t k = lane; k < 256u; k += WAVE) {
@@ -908,6 +909,19 @@ __global__ __launch_bounds__(WAVE) void k_gzip_replay(uint8_t* __restrict__ dst,
       more = rq0 + rqn < nrec;
       wave_sync();
     }
+#if PQG_GQ_ADAPT
+    // the window: up to LZ_CAP bytes, ending where the 64th record from ri starts (records are
+    // disjoint and ascending and record ri ends past A, so that start lies past A and at most 63
+    // records reach into the window, one per lane)
+    uint32_t T = ulen - A < LZ_CAP ? ulen - A : LZ_CAP;
+    if (ri + (WAVE - 1u) < rq0 + rqn) {
+      const uint32_t at63 = uni((uint32_t)rq[ri + (WAVE - 1u) - rq0]);
+      T = at63 - A < T ? at63 - A : T;
+    }
+#else
+    const uint32_t T = ulen - A < GQ_OUTW ? ulen - A : GQ_OUTW;
+#endif
+    const uint32_t Bend = A + T;
     // the literal bytes of the window, and every byte's default source: itself
     for (uint32_t i = lane; i < T; i += WAVE) {
       const uint32_t a = A + i;
@@ -931,6 +945,7 @@ __global__ __launch_bounds__(WAVE) void k_gzip_replay(uint8_t* __restrict__ dst,
     // records that end inside the window are done
     const uint64_t done = __ballot(lane < m && at + len <= Bend);
     ri += (uint32_t)__builtin_popcountll(done);
+    A += T;
   }
   if (lane == 0 && status) status[jb] = 0;
 }
