@@ -390,6 +390,31 @@ int pqg_router_read(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_le
 int pqg_router_read_runs(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_len,
                          const uint64_t* in_offsets, const uint32_t* counts, int n_runs, int32_t* out);
 
+/* ParquetReadRouter.read (parquet-plugins/parquet-encoding-vector/.../ParquetReadRouter.java:57-66)
+ * with its contract kept — out[0 .. count) holds the run's values when the call returns — at one
+ * device round trip per page instead of per run. `in` is the caller's stream at the run's data start
+ * and `stream_left` the bytes left in that stream (ByteBufferInputStream.available(): the run's bytes
+ * and everything after them). On a miss the hybrid stream after the run is walked on the host
+ * (RunLengthBitPackingHybridDecoder.readNext header forms), this run and every later bit-packed run
+ * found are unpacked in one pqg_router_read_runs call, and the results are kept in the context; a
+ * later call for a walked run (same width, count, position from the end, and bytes) is served from
+ * host memory with no device work. The caller advances its stream by count*bit_width/8 bytes, as
+ * after readBatch. Errors as pqg_router_read: count not a multiple of 8 -> INVALID_ARG; the run's
+ * bytes past stream_left -> PQG_ERR_EOF (SingleBufferInputStream.slice) with nothing written. */
+int pqg_router_read_page(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t stream_left, int count,
+                         int32_t* out);
+
+/* The cache probe of pqg_router_read_page alone (host only, never a device call): needs only the
+ * run's count*bit_width/8 bytes at `run`. *hit = 1 with out filled, or 0 with nothing written (then
+ * call pqg_router_read_page with the whole stream tail). For callers whose stream tail costs a copy
+ * (the JNI shim's heap arrays). */
+int pqg_router_cache_lookup(pqg_ctx* ctx, int bit_width, const uint8_t* run, size_t stream_left, int count,
+                            int32_t* out, int* hit);
+
+/* Reads served from the page cache (hits) and device round trips (misses) since the context was
+ * created. */
+int pqg_router_cache_stats(pqg_ctx* ctx, uint64_t* hits, uint64_t* misses);
+
 /* ---- record assembly ---------------------------------------------------------
  * Dremel assembly of ONE leaf column into the columnar form of its records: the
  * Arrow-style equivalent of the converter events parquet-mr's automaton emits

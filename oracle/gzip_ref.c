@@ -13,7 +13,15 @@
  * bytes are produced (readFully of the page size: neither output beyond it nor the trailer of the
  * member that completes the page is read); a member that ends before the page is complete has its
  * CRC-32 and ISIZE checked before the next member's header; fewer than `expect` bytes -> PQG_ERR_EOF
- * (EOFException); malformed data -> PQG_ERR_CORRUPT (ZipException / IOException). */
+ * (EOFException); malformed data -> PQG_ERR_CORRUPT (ZipException / IOException).
+ *
+ * Credit: the inflate part (gz_build's canonical-code construction with its over-subscription /
+ * incomplete-code checks, gz_decode's bit-at-a-time canonical decode, the length / distance base and
+ * extra-bit tables, the code-length-code order and the dynamic-block header checks) follows the
+ * structure of puff.c, Mark Adler's reference inflate in zlib's contrib/puff (Copyright (C) 2002-2013
+ * Mark Adler, zlib license). This file is an altered version of that code: restated in this
+ * repository's style, with gzip member framing, page-size truncation and this oracle's error codes
+ * added. It is the test checker only; nothing in the product uses it. */
 #include <stdint.h>
 #include <string.h>
 

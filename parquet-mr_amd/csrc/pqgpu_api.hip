@@ -175,6 +175,20 @@ struct pqg_plan {
   uint32_t n_bin_blocks_nf = 0, n_bin_chunks_nf = 0;
 };
 
+// pqg_router_read_page: the bit-packed runs of a hybrid stream's tail, walked on the host at the first
+// read of a page, unpacked on the device in one round trip and served from host memory by the later
+// reads (ParquetReadRouter.read: the values are in the caller's buffer when the call returns).
+struct RouterCache {
+  int w = -1;
+  uint64_t tail_len = 0;        // bytes from the walked tail's start to the stream's end
+  std::vector<uint8_t> bytes;   // the tail (a cached run is served only when its bytes equal the request's)
+  std::vector<uint64_t> off;    // run data start, relative to the tail start (ascending)
+  std::vector<uint32_t> cnt;    // values of the run
+  std::vector<uint64_t> vo;     // first value of the run in vals
+  std::vector<int32_t> vals;
+  uint64_t hits = 0, misses = 0;
+};
+
 struct pqg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -208,6 +222,7 @@ struct pqg_ctx {
   int plain_mode = 2;       // PQG_DISPATCH_PLAIN_ONE_PASS
   bool dict_direct = true;  // PQG_DISPATCH_DICT_DIRECT
   uint32_t gz_prepass_min = pqg::GZ_PREPASS_MIN;  // PQG_DISPATCH_GZIP_PREPASS_MIN
+  RouterCache router;  // pqg_router_read_page
 };
 
 extern "C" {
@@ -905,7 +920,6 @@ int pqg_plan_launch(pqg_plan* P) {
   // The BYTE_ARRAY kernels of the other columns likewise go to a third queue when fixed-width columns'
   // kernels (HBM bound) are in the plan to share the chip with.
   bool fork = false, fork_bin = false, fork_fix = false;
-#ifndef PQG_NO_FORK
   const bool has_fixed = P->cls_n[C_DICT4] || P->cls_n[C_DICT8] || P->cls_n[C_PLAIN] || P->cls_n[C_BOOL] ||
                          P->cls_n[C_RLEBOOL] || P->cls_n[C_DELTA4] || P->cls_n[C_DELTA8] || P->cls_n[C_BSS];
   const bool has_bin = P->n_dict_walk || P->cls_n[C_IDS] || P->cls_n[C_BINP] - P->n_binp_seg - (pf ? P->n_binp_fused : 0) > 0 ||
@@ -927,7 +941,6 @@ int pqg_plan_launch(pqg_plan* P) {
     fork_fix = (ctx->fix_stream || hipStreamCreateWithFlags(&ctx->fix_stream, hipStreamNonBlocking) == hipSuccess) &&
                (ctx->ev_join_fix || hipEventCreateWithFlags(&ctx->ev_join_fix, hipEventDisableTiming) == hipSuccess) &&
                hipStreamWaitEvent(ctx->fix_stream, ctx->ev_fork, 0) == hipSuccess;
-#endif
   if (e == hipSuccess && pf) {  // PLAIN-only BYTE_ARRAY columns: one pass (after the levels: n_values, out_offset)
     uint8_t* scb = (uint8_t*)P->bscratch.p;
     uint64_t* ps = (uint64_t*)P->pstatus.p;
@@ -1238,9 +1251,14 @@ int pqg_sync(pqg_ctx* ctx, pqg_status* st) {
   plans.swap(ctx->unsynced);
   int rc = PQG_OK;
   for (pqg_plan* P : plans) {
+    // sync_plan can return PQG_ERR_HIP before anything sets the status: start from "no error"
     pqg_status pst;
+    std::memset(&pst, 0, sizeof(pst));
+    pst.page = -1;
     std::vector<PageWork> work;
     const int prc = sync_plan(P, &pst, &work);
+    if (prc != PQG_OK && pst.code == 0 && pst.message[0] == '\0')
+      set_status(&pst, prc, -1, -1, prc == PQG_ERR_HIP ? hipGetErrorString(hipGetLastError()) : "plan sync failed");
     if (prc != PQG_OK && rc == PQG_OK) {
       rc = prc;
       if (st) *st = pst;
@@ -1927,7 +1945,6 @@ int pqg_zstd_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, 
   // dst_offset / 5) and one mode word per job; without it every job takes the inline decoder
   uint64_t* seqs = nullptr;
   int32_t* mode = nullptr;
-#if PQG_ZSTD_2P
   {
     const size_t need_s = 8u * (size_t)(dst_bytes / 5u + 2u), need_m = 4u * (size_t)n_jobs;
     if (ctx->zstd_seqs.cap < need_s || ctx->zstd_mode.cap < need_m) {
@@ -1943,7 +1960,6 @@ int pqg_zstd_decompress(pqg_ctx* ctx, const uint8_t* d_src, uint64_t src_bytes, 
       mode = (int32_t*)ctx->zstd_mode.p;
     }
   }
-#endif
   const hipError_t e = pqg::launch_zstd(ctx->stream, d_src, src_bytes, d_dst, dst_bytes, d_jobs, n_jobs, d_status,
                                         (uint8_t*)ctx->zstd_scratch.p, seqs, mode);
   return e == hipSuccess ? PQG_OK : PQG_ERR_HIP;
@@ -1971,6 +1987,7 @@ int pqg_router_read(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t in_le
   const uint64_t need = (uint64_t)count * (uint64_t)bit_width / 8u;
   if (need > in_len) return PQG_ERR_EOF;  // in.slice(count * bitWidth / 8) -> EOFException
   if (count == 0) return PQG_OK;
+  ctx->staged.clear();  // pin_in / pin_out are reused: an earlier staged decode's outputs are gone
   if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
   hipStream_t s = ctx->stream;
   const uint64_t in_al = (need + 16 + 255) & ~uint64_t(255);
@@ -2016,6 +2033,7 @@ int pqg_router_read_runs(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t 
     max_count = std::max(max_count, counts[r]);
   }
   if (n_vals == 0) return PQG_OK;
+  ctx->staged.clear();  // pin_in / pin_out are reused: an earlier staged decode's outputs are gone
   if (hipSetDevice(ctx->device) != hipSuccess) return PQG_ERR_HIP;
   hipStream_t s = ctx->stream;
   // pinned image: [run bytes, each 16-B aligned][in_off u64 x n][out_off u64 x n][counts u32 x n]
@@ -2055,6 +2073,123 @@ int pqg_router_read_runs(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t 
   if (hipMemcpyAsync(ctx->pin_out.p, dout, (size_t)(4 * n_vals), hipMemcpyDeviceToHost, s) != hipSuccess) return PQG_ERR_HIP;
   if (hipStreamSynchronize(s) != hipSuccess) return PQG_ERR_HIP;
   std::memcpy(out, ctx->pin_out.p, (size_t)(4 * n_vals));
+  return PQG_OK;
+}
+
+}  // extern "C"
+
+// ---- ParquetReadRouter.read with the page's runs cached --------------------------------------------
+
+namespace {
+
+// Bounds of one walk: what a miss decodes in its single round trip.
+constexpr uint64_t ROUTER_MAX_VALUES = 1u << 22;
+constexpr size_t ROUTER_MAX_RUNS = 1u << 16;
+
+// Served from the cache when the run at this stream position (stream_left bytes before the end) was
+// walked, with the same width and count, and its bytes are the ones unpacked then.
+bool router_hit(RouterCache& c, int w, const uint8_t* in, uint64_t need, uint64_t stream_left, int count,
+                int32_t* out) {
+  if (c.w != w || stream_left > c.tail_len || c.off.empty()) return false;
+  const uint64_t pos = c.tail_len - stream_left;
+  const auto it = std::lower_bound(c.off.begin(), c.off.end(), pos);
+  if (it == c.off.end() || *it != pos) return false;
+  const size_t r = (size_t)(it - c.off.begin());
+  if (c.cnt[r] != (uint32_t)count) return false;
+  if (need && std::memcmp(in, c.bytes.data() + pos, need) != 0) return false;
+  std::memcpy(out, c.vals.data() + c.vo[r], (size_t)count * 4);
+  c.hits++;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pqg_router_cache_lookup(pqg_ctx* ctx, int bit_width, const uint8_t* run, size_t stream_left, int count,
+                            int32_t* out, int* hit) {
+  if (!ctx || !hit || bit_width < 0 || bit_width > 32 || count < 0 || count % 8 != 0 || (count && !out))
+    return PQG_ERR_INVALID_ARG;
+  *hit = 0;
+  const uint64_t need = (uint64_t)count * (uint64_t)bit_width / 8u;
+  if (need > stream_left) return PQG_ERR_EOF;
+  if (need && !run) return PQG_ERR_INVALID_ARG;
+  if (count == 0) {
+    *hit = 1;
+    return PQG_OK;
+  }
+  *hit = router_hit(ctx->router, bit_width, run, need, stream_left, count, out) ? 1 : 0;
+  return PQG_OK;
+}
+
+int pqg_router_read_page(pqg_ctx* ctx, int bit_width, const uint8_t* in, size_t stream_left, int count, int32_t* out) {
+  int hit = 0;
+  const int lrc = pqg_router_cache_lookup(ctx, bit_width, in, stream_left, count, out, &hit);
+  if (lrc != PQG_OK || hit) return lrc;
+  if (!in) return PQG_ERR_INVALID_ARG;
+  RouterCache& c = ctx->router;
+  const uint64_t L = stream_left, need = (uint64_t)count * (uint64_t)bit_width / 8u;
+  // Walk the hybrid stream after this run (RunLengthBitPackingHybridDecoder.readNext :80-109 header
+  // forms; BytesUtils.readUnsignedVarInt :202-211) and list every bit-packed run whose bytes are in the
+  // stream. The walk is a prediction of the caller's next reads: bytes past the hybrid stream (data the
+  // caller reads otherwise) may parse as runs, which are decoded and never served; a header that cannot
+  // be a run ends the walk. Runs the walk missed are served by a later miss.
+  c.w = -1;
+  c.off.clear();
+  c.cnt.clear();
+  c.vo.clear();
+  c.off.push_back(0);
+  c.cnt.push_back((uint32_t)count);
+  c.vo.push_back(0);
+  uint64_t total = (uint64_t)count, q = need;
+  const uint32_t nb_rle = ((uint32_t)bit_width + 7u) / 8u;
+  while (q < L && c.off.size() < ROUTER_MAX_RUNS) {
+    uint32_t hdr = 0, sh = 0, b = 0;
+    uint64_t k = q;
+    bool ok = true;
+    while (true) {
+      if (k >= L || sh > 28) { ok = false; break; }
+      b = in[k++];
+      if (!(b & 0x80u)) break;
+      hdr |= (b & 0x7Fu) << sh;
+      sh += 7;
+    }
+    if (!ok) break;
+    hdr |= b << sh;
+    if (!(hdr & 1u)) {  // RLE run: count, then the value in ceil(w / 8) bytes
+      q = k + nb_rle;
+      continue;
+    }
+    const uint64_t groups = hdr >> 1, vals = groups * 8u, bytes = groups * (uint64_t)bit_width;
+    if (vals > 0x7FFFFFF8u || k + bytes > L || total + vals > ROUTER_MAX_VALUES) break;
+    if (vals) {
+      c.off.push_back(k);
+      c.cnt.push_back((uint32_t)vals);
+      c.vo.push_back(total);
+      total += vals;
+    }
+    q = k + bytes;
+  }
+  c.vals.resize(total);
+  const uint64_t keep = c.off.size() > 1 ? c.off.back() + (uint64_t)c.cnt.back() * (uint64_t)bit_width / 8u : need;
+  c.bytes.assign(in, in + keep);
+  c.tail_len = L;
+  c.misses++;
+  const int rc = pqg_router_read_runs(ctx, bit_width, in, (size_t)L, c.off.data(), c.cnt.data(), (int)c.off.size(),
+                                      c.vals.data());
+  if (rc != PQG_OK) {
+    c.off.clear();
+    return rc;
+  }
+  c.w = bit_width;
+  std::memcpy(out, c.vals.data(), (size_t)count * 4);
+  return PQG_OK;
+}
+
+int pqg_router_cache_stats(pqg_ctx* ctx, uint64_t* hits, uint64_t* misses) {
+  if (!ctx) return PQG_ERR_INVALID_ARG;
+  if (hits) *hits = ctx->router.hits;
+  if (misses) *misses = ctx->router.misses;
   return PQG_OK;
 }
 

@@ -2379,10 +2379,7 @@ __device__ __forceinline__ void bp_emit(const uint32_t* img, uint32_t img_len, c
 }
 
 
-#ifndef PQG_BP_WAVES
-#define PQG_BP_WAVES 6
-#endif
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_BP_WAVES))) void k_bin_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6))) void k_bin_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                         const PageWork* __restrict__ work,
                                                         const ColumnDev* __restrict__ cols,
                                                         const uint64_t* __restrict__ segs, uint32_t n_segs,
@@ -2442,11 +2439,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_BP
 #ifdef PQG_DIAG
   dg1 = __builtin_amdgcn_s_memrealtime() + (r.n > 0xFFFFFFF0u ? 1u : 0u);
 #endif
-#ifdef PQG_DIAG_NOLOOKBACK  // diagnostic build only: timing without the look-back (wrong offsets)
-  if (false) {
-#else
   if (!first) {
-#endif
     const uint64_t t_wait = __builtin_amdgcn_s_memrealtime();
     while (true) {
       // lane l: the tile l + 1 before this one (down to the first tile of the section)
@@ -2560,10 +2553,7 @@ static_assert(sizeof(BinPageLds) * WPB <= 160 * 1024 / 6, "6 workgroups of k_bin
 
 // 5 waves per SIMD: 94 VGPRs hold the tile being walked and the next one without spills (at 6, the
 // next tile's registers went to scratch, whose store waited for the prefetch on every tile)
-#ifndef PQG_PG_WAVES
-#define PQG_PG_WAVES 5
-#endif
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_PG_WAVES))) void k_bin_plain_pg(
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5))) void k_bin_plain_pg(
     const uint8_t* __restrict__ bytes, uint64_t n_bytes, const PageWork* __restrict__ work,
     const ColumnDev* __restrict__ cols, const int32_t* __restrict__ list, int n_list, uint32_t* inexact,
     uint32_t flag_epoch, uint64_t* err, ErrCount err_count) {
@@ -2621,11 +2611,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_PG
       }
     }
     wave_sync();
-#ifdef PQG_DIAG_PG_NOEMIT  // diagnostic build only (abx/): the walk without the output stage
-    if (false)
-#else
     if (m)
-#endif
       if (!bp_emit_fast((uint32_t*)L.bt, L.u.img, 2u * BW_WIN, L.acc, B, beg, r.n, r.pos, before, m, pw, cd))
         bp_emit(L.u.img, 2u * BW_WIN, L.acc, L.bt, rs, B, beg, r.n, r.pos, before, m, pw, cd);
     if (last) return true;

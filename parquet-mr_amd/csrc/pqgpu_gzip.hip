@@ -577,19 +577,9 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
 // executor (literal bytes read back from the output). Anything else — a malformed stream, a page that
 // completes inside a member, more records than the job's range, a stream past 4 GiB — is left to
 // k_gzip, which reports exactly what it always did.
-#ifndef PQG_GZ_2P
-#define PQG_GZ_2P 1
-#endif
 constexpr uint32_t GQ_JOBS = 12;
 constexpr uint32_t GQ_WIN = 512;
-#ifndef PQG_GQ_ADAPT
-#define PQG_GQ_ADAPT 1  // 0: fixed 189-byte replay windows (A/B builds)
-#endif
-#ifndef PQG_GQ_THR
-#define PQG_GQ_THR 1  // 0: the token loop's window test from wlo every token (A/B builds)
-#endif
 constexpr int32_t GQ_INLINE = -1;  // mode[j]: -1 = k_gzip decodes job j, else its record count
-[[maybe_unused]] constexpr uint32_t GQ_OUTW = 189;  // fixed replay window (PQG_GQ_ADAPT=0: <= 63 records of >= 3 bytes + one from before)
 
 
 struct GqLane {
@@ -786,11 +776,7 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
       // longer than the first-level tables take a rare branch
       while (true) {
         {  // re-centre every window of the loop together when one could leave its window
-#if PQG_GQ_THR
           const bool want = bp >= rthr;
-#else
-          const bool want = (uint32_t)(bp >> 3) + 24u > wlo + GQ_WIN || (uint32_t)(bp >> 3) < wlo;
-#endif
           if (__ballot(want)) recenter((uint32_t)(bp >> 3));
         }
         const uint64_t x = peek(bp);
@@ -909,7 +895,6 @@ __global__ __launch_bounds__(WAVE) void k_gzip_replay(uint8_t* __restrict__ dst,
       more = rq0 + rqn < nrec;
       wave_sync();
     }
-#if PQG_GQ_ADAPT
     // the window: up to LZ_CAP bytes, ending where the 64th record from ri starts (records are
     // disjoint and ascending and record ri ends past A, so that start lies past A and at most 63
     // records reach into the window, one per lane)
@@ -918,9 +903,6 @@ __global__ __launch_bounds__(WAVE) void k_gzip_replay(uint8_t* __restrict__ dst,
       const uint32_t at63 = uni((uint32_t)rq[ri + (WAVE - 1u) - rq0]);
       T = at63 - A < T ? at63 - A : T;
     }
-#else
-    const uint32_t T = ulen - A < GQ_OUTW ? ulen - A : GQ_OUTW;
-#endif
     const uint32_t Bend = A + T;
     // the literal bytes of the window, and every byte's default source: itself
     for (uint32_t i = lane; i < T; i += WAVE) {
@@ -954,7 +936,7 @@ hipError_t launch_gzip(hipStream_t st, const uint8_t* src, uint64_t src_bytes, u
                        const void* jobs, int n_jobs, int32_t* status, uint64_t* recs, int32_t* mode,
                        uint32_t prepass_min) {
   if (n_jobs <= 0) return hipSuccess;
-  if (!(recs && mode && PQG_GZ_2P)) mode = nullptr;
+  if (!(recs && mode)) mode = nullptr;
   if (mode) {
     hipLaunchKernelGGL(k_gzip_seq, dim3((n_jobs + (int)GQ_JOBS - 1) / (int)GQ_JOBS), dim3(64), 0, st, src, src_bytes,
                        dst, dst_bytes, (const GzJobDev*)jobs, n_jobs, recs, mode, prepass_min);

@@ -81,10 +81,7 @@ constexpr uint64_t ERR_KEY_MASK = (1ull << 48) - 1;
 enum BinKind : uint32_t { BIN_PLAIN = 0, BIN_DLBA = 1, BIN_DICT = 2, BIN_DBA = 3 };
 
 // Output chunk of k_dict_expand: CH_TILES x 64 lanes x 16 bytes.
-#ifndef PQG_DICT_CHUNK_TILES
-#define PQG_DICT_CHUNK_TILES 16
-#endif
-constexpr uint32_t DICT_CHUNK_TILES = PQG_DICT_CHUNK_TILES;
+constexpr uint32_t DICT_CHUNK_TILES = 16;
 inline uint32_t dict_chunk_values(int elem_width) { return DICT_CHUNK_TILES * 64u * (16u / (uint32_t)elem_width); }
 // output chunks of a dictionary page of n slots (slots shifted by up to 16 / width - 1 for 16-B alignment)
 inline uint32_t dict_page_chunks(uint32_t n, int elem_width) {
@@ -120,9 +117,6 @@ hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_
 // ZSTD frames per job (pqgpu_zstd.hip): a grid of at most ZSTD_GRID one-wave workgroups loops over
 // the jobs; scratch = min(n_jobs, ZSTD_GRID) x ZSTD_LIT_SCRATCH bytes of literal buffers (<= 512 MiB)
 constexpr uint64_t ZSTD_LIT_SCRATCH = 131072;
-#ifndef PQG_ZSTD_2P
-#define PQG_ZSTD_2P 1  // sequence pre-pass (k_zstd_seq) + replay; 0: inline decoder only (A/B builds)
-#endif
 constexpr uint32_t ZSTD_GRID = 4096;
 // With seqs / mode (both non-null) the sequences are first decoded one lane per job by k_zstd_seq into
 // seqs (8-byte records; job j at dst_offset / 5, so seqs holds dst_bytes / 5 + 1 records) and
@@ -171,10 +165,7 @@ constexpr uint32_t BW_SEG_BYTES = 16384;
 constexpr uint32_t BW_SEG_CAP = BW_SEG_BYTES / 4 + 2;
 constexpr uint32_t BW_SEG_MAX_PAGES = 4096;
 constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block
-#ifndef PQG_DD_DICT_MAX
-#define PQG_DD_DICT_MAX 8192
-#endif
-constexpr uint32_t DD_DICT_MAX = PQG_DD_DICT_MAX;  // dictionary page bytes staged by the offset scan (dict_direct)
+constexpr uint32_t DD_DICT_MAX = 8192;  // dictionary page bytes staged by the offset scan (dict_direct)
 hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                       const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,

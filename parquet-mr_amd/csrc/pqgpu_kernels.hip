@@ -516,161 +516,6 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
   n_ok = N;
 }
 
-// ---------------------------------------------------------------------------
-// Speculative-piece walk of a dictionary-id section (round 4): the run records of dict_walk_ls from
-// the scheme of decode_levels_sp (below, with the levels): one 32-byte piece of a 2 KiB super-window
-// per lane, a speculative walk from each piece's first byte, the scalar unit's pass over the pieces
-// on the chain, a re-walk of any piece whose true entry it did not visit; then every piece on the
-// chain counts its runs and values, two scans give each piece's first record and first value, and
-// each piece stores its own records and chunk entries. A C2 page (~870 bytes, ~86 runs) is one
-// super-window of ~28 pieces of ~3 runs each, where the window walk takes ~4 windows of fixed work.
-// Returns false (nothing published yet, the caller walks the page again with dict_walk_ls) on any
-// header outside the common case: varints over 4 bytes, 0-group packed runs, 0-count RLE runs (the
-// reader repeats their value forever), headers or RLE values crossing the section end, a chain
-// that ends before the page's values do.
-constexpr uint32_t SPD_SW = 32u * WAVE;    // section bytes per super-window (32 per lane)
-constexpr uint32_t SPD_SEG = SPD_SW + 32;  // headers only: the super-window + alignment + 8-byte reads
-
-struct SpIdRun {
-  uint32_t next, cnt, val;  // val: raw RLE id; PACKED: data start
-  bool pk, bad;
-};
-
-__device__ __forceinline__ SpIdRun sp_parse_id(const uint8_t* seg, uint32_t lo, uint32_t p, uint32_t end, uint32_t w) {
-  typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
-  const uint32_t o = p - lo;
-  const uint32_t d = *(const u32u*)(seg + o), d1 = *(const u32u*)(seg + o + 4u);
-  const uint32_t stop = ~d & 0x80808080u;
-  const uint32_t hl = stop ? ((uint32_t)__builtin_ctz(stop) >> 3) + 1u : 4u;
-  const uint32_t dm = d & (0xFFFFFFFFu >> (32u - 8u * hl));
-  const uint32_t v = (dm & 0x7Fu) | ((dm >> 1) & 0x3F80u) | ((dm >> 2) & 0x1FC000u) | ((dm >> 3) & 0xFE00000u);
-  SpIdRun r;
-  bool bad = stop == 0u || p + hl > end;
-  if (!(v & 1u)) {
-    const uint32_t nb = (w + 7u) >> 3;
-    const uint64_t x = ((uint64_t)d1 << 32 | d) >> (8u * hl);
-    r.val = nb >= 4u ? (uint32_t)x : (uint32_t)x & ((1u << (8u * nb)) - 1u);
-    r.cnt = v >> 1;
-    r.pk = false;
-    r.next = p + hl + nb;
-    bad |= r.cnt == 0u || r.next > end;
-  } else {
-    const uint32_t g = v >> 1;
-    r.cnt = g * 8u;
-    r.val = p + hl;
-    r.pk = true;
-    const uint64_t e = (uint64_t)p + hl + (uint64_t)g * w;
-    r.next = e > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)e;
-    bad |= g == 0u;
-  }
-  r.bad = bad;
-  return r;
-}
-
-__device__ __forceinline__ void sp_walk_id(const uint8_t* seg, uint32_t lo, uint32_t s, uint32_t bk, uint32_t end,
-                                           uint32_t w, uint32_t& X, uint32_t& V, bool& stop) {
-  const uint32_t pe = bk + 32u;
-  uint32_t p = s, vm = 0;
-  bool st = false;
-  while (p < pe && p < end) {
-    const SpIdRun r = sp_parse_id(seg, lo, p, end, w);
-    vm |= 1u << (p - bk);
-    if (r.bad) { st = true; break; }
-    p = r.next;
-  }
-  X = p;
-  V = vm;
-  stop = st;
-}
-
-__device__ bool dict_walk_sp(uint8_t* seg, rsrc_t rs, uint32_t N, uint32_t sec_beg, uint32_t sec_end, uint32_t w,
-                             uint64_t* rec, uint32_t* chunk_run, uint32_t CH, uint32_t sh, uint32_t& n_rec) {
-  const uint32_t lane = lane_id();
-  uint32_t pos = sec_beg + 1u, produced = 0, k = 0;
-  while (produced < N) {
-    pos = uni(pos);
-    if (pos >= sec_end) return false;
-    const uint32_t lo = pos & ~15u;
-    wave_sync();
-    for (uint32_t i = 16u * lane; i < SPD_SEG; i += 16u * WAVE)
-      *(u32x4*)(seg + i) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lo + i), 0, 0);
-    wave_sync();
-    const uint32_t bk = pos + 32u * lane;
-    uint32_t X, V;
-    bool stop;
-    sp_walk_id(seg, lo, bk, bk, sec_end, w, X, V, stop);
-    uint32_t E = 0, last = 0;
-    uint64_t R = 0;
-    for (uint32_t it = 0;; it++) {
-      const uint32_t nl = (stop || X >= sec_end || X - pos >= SPD_SW) ? 64u : (X - pos) >> 5;
-      R = 0;
-      E = 0;
-      uint32_t q = 0, e = pos;
-      while (q < 64u) {
-        R |= 1ull << q;
-        E = lane == q ? e : E;
-        last = q;
-        e = uni(rdl(X, q));
-        q = uni(rdl(nl, q));
-      }
-      const bool on = (R >> lane) & 1ull;
-      const uint32_t off = E - bk;
-      const bool ok = !on || (off < 32u && ((V >> off) & 1u));
-      if (!__ballot(!ok)) break;
-      if (it >= 64u) return false;
-      if (!ok) sp_walk_id(seg, lo, E, bk, sec_end, w, X, V, stop);
-    }
-    const bool on = (R >> lane) & 1ull;
-    const uint32_t cap = N - produced;
-    uint32_t c = 0, nr = 0;
-    if (on) {
-      for (uint32_t p = E; p < X;) {
-        const SpIdRun r = sp_parse_id(seg, lo, p, sec_end, w);
-        c = r.cnt < cap - c ? c + r.cnt : cap;
-        nr++;
-        p = r.next;
-      }
-    }
-    const uint32_t inc = wave_incl_scan_sat(c, cap);
-    uint32_t ex = __shfl_up(inc, 1);
-    if (lane == 0) ex = 0;
-    const uint32_t total = uni(rdl(inc, WAVE - 1));
-    uint32_t nr_all;
-    const uint32_t rex = wave_excl_scan_u32(nr, &nr_all);
-    const uint32_t x_last = uni(rdl(X, last));
-    const bool stop_last = uni(rdl((uint32_t)stop, last)) != 0u;
-    if (total < cap && (stop_last || x_last >= sec_end)) return false;
-    // each piece stores its records: first value | payload << 32 (dict_walk_ls's format), and the
-    // chunk entries of the chunks whose first value it holds
-    uint32_t em = 0;
-    if (on) {
-      uint32_t s = produced + ex, idx = k + rex;
-      for (uint32_t p = E; p < X && s < N;) {
-        const SpIdRun r = sp_parse_id(seg, lo, p, sec_end, w);
-        const uint32_t e = r.cnt < N - s ? s + r.cnt : N;
-        const uint32_t payload = r.pk ? (0x80000000u | r.val) : (r.val > 0x7FFFFFFFu ? 0x7FFFFFFFu : r.val);
-        sst(rec + idx, (uint64_t)s | ((uint64_t)payload << 32));
-        for (uint32_t j = s == 0 ? 0 : (s + sh + CH - 1) / CH; j * CH < e + sh; j++) sst(chunk_run + j, idx);
-        idx++;
-        em++;
-        s = e;
-        p = r.next;
-      }
-    }
-    for (int o = 32; o > 0; o >>= 1) em += __shfl_xor(em, o);
-    k = uni(k + em);
-    produced = uni(produced + total);
-    pos = x_last;
-    (void)nr_all;
-  }
-  n_rec = k;
-  return true;
-}
-
-#ifndef PQG_DICT_SP
-#define PQG_DICT_SP 0  // 1: pages through the speculative-piece walk (measured slower on C2 / Zipf(2.0): A/B builds only)
-#endif
-
 // One wave per page (4 per workgroup): the run records of RLE_DICTIONARY / PLAIN_DICTIONARY
 // pages (DictionaryValuesReader.initFromPage :48-64 + RunLengthBitPackingHybridDecoder.readNext
 // :80-109). The page section is staged in LDS; a 256-byte window is pre-decoded in parallel
@@ -721,17 +566,12 @@ __device__ __forceinline__ void dict_runs_body(const uint8_t* __restrict__ bytes
       } else {
         uint64_t* prec = rec + pw.rec_base;
         uint32_t* pcr = chunk_run + pw.chunk_base;
-        if (PQG_DICT_SP && dict_walk_sp(L.seg, win.rs, N, sec_beg, sec_end, bw, prec, pcr, CH, sh, n_rec)) {
-          n_ok = N;
-        } else {
-          if (PQG_DICT_SP) seg_fill(win, sec_beg & ~15u);  // the speculative walk restaged the segment
         // SMALL: the whole data section sits in the LDS segment: the walk has no global load
         if (sec_end - win.seg_lo + 264u <= SEG_BYTES)  // every window inside the segment
           dict_walk_ls<W>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec, n_ok);
         else
           dict_walk_ls<W, false>(L, win, N, sec_beg, sec_end, (int)bw, prec, pcr, CH, sh, page, err, err_count, n_rec,
                                  n_ok);
-        }
       }
     }
   }
@@ -784,15 +624,7 @@ __device__ __forceinline__ typename DictVal<W>::T dict_get_g(bool in_lds, const 
 //   tile sweep  every lane tracks the run holding its element: per tile it advances past
 //               the run starts it crossed (usually none), reads the value (RLE) or unpacks
 //               the id and gathers (packed), and the wave stores one full 1 KB tile.
-#ifndef PQG_XT_RECPF
-#define PQG_XT_RECPF 1  // 0: run records loaded after the chunk's first-run entry only (A/B builds)
-#endif
-#ifndef PQG_XT_EARLY
-#define PQG_XT_EARLY 1  // 0: packed bytes loaded after the records only (A/B builds)
-#endif
-#ifndef PQG_SPIN_SLEEP
-#define PQG_SPIN_SLEEP 2  // s_sleep units (64 cycles) between two polls of a page's ready flag
-#endif
+constexpr int SPIN_SLEEP = 2;  // s_sleep units (64 cycles) between two polls of a page's ready flag
 constexpr uint32_t XT_RUNS = 128;  // run table entries per wave
 constexpr uint32_t XT_SEG = 2560;    // LDS bytes for the packed data of one round
 
@@ -874,7 +706,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
   uint32_t j = 0, dict_n = 0, sec_end = 0, db = 0, N = 0, sh = 0, v_lo = 0, v_hi = 0, n_rec = 0, k = 0;
   uint32_t pre_lo = 0xFFFFFFFFu, pre_hi = 0;  // section bytes staged in xseg ahead of the records
   int w = 0;
-  uint64_t pf0 = 0, pf1 = 0;  // PQG_XT_RECPF: records [0, 128) of the page (lane l: l and 64 + l)
+  uint64_t pf0 = 0, pf1 = 0;  // records [0, 128) of the page (lane l: l and 64 + l)
   PageWork pw{};
   rsrc_t drs = make_rsrc(bytes, 0), prs = drs;
 #ifdef PQG_DIAG
@@ -911,7 +743,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
     w = (int)uni((ld32(prs, db & ~3u) >> ((db & 3u) * 8u)) & 0xFFu);
     // a data section that fits xseg is staged whole now (input bytes: no hand-off needed), so the
     // packed bytes of its runs need no load after the records
-    if (PQG_XT_EARLY && sec_end > db && sec_end + 8u - (db & ~15u) <= XT_SEG) {
+    if (sec_end > db && sec_end + 8u - (db & ~15u) <= XT_SEG) {
       pre_lo = db & ~15u;
       pre_hi = sec_end + 8u;
 #pragma unroll
@@ -934,7 +766,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
 #endif
           break;
         }
-        __builtin_amdgcn_s_sleep(PQG_SPIN_SLEEP);
+        __builtin_amdgcn_s_sleep(SPIN_SLEEP);
         // wall-clock bound (s_memrealtime: constant 100 MHz): a walker that never publishes
         // (descheduled, starved) turns into PQG_ERR_TIMEOUT after SPIN_TIMEOUT_TICKS, not a hang
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -950,7 +782,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       // the page status and the chunk's first run in one round trip
       pst = sld(pstat + cpage);
       k = sld(chunk_run + pw.chunk_base + j);
-      if (PQG_XT_RECPF) {  // the page's first 2 x 64 run records in the same round trip
+      {  // the page's first 2 x 64 run records in the same round trip
         pf0 = sld(rec + pw.rec_base + lane);
         pf1 = sld(rec + pw.rec_base + WAVE + lane);
       }
@@ -994,22 +826,18 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       for (uint32_t t0 = 0; t0 < XT_RUNS; t0 += WAVE) {
         const uint32_t r = k + t0 + lane;
         const bool has = r < n_rec && t0 + lane < XT_RUNS - 1;  // a run of this round
-        uint64_t rr;
-        if (PQG_XT_RECPF) {  // records the hand-off prefetched come from the lanes holding them
-          const int src = (int)(r & (WAVE - 1u));
-          const uint64_t a0 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pf0 >> 32), src) << 32) |
-                              (uint32_t)__shfl((int)(uint32_t)pf0, src);
-          const uint64_t a1 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pf1 >> 32), src) << 32) |
-                              (uint32_t)__shfl((int)(uint32_t)pf1, src);
-          rr = r >= n_rec ? 0 : (r < WAVE ? a0 : (r < 2u * WAVE ? a1 : sld(prec + r)));
-        } else {
-          rr = r < n_rec ? sld(prec + r) : 0;
-        }
+        // records the hand-off prefetched come from the lanes holding them
+        const int src = (int)(r & (WAVE - 1u));
+        const uint64_t a0 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pf0 >> 32), src) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)pf0, src);
+        const uint64_t a1 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pf1 >> 32), src) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)pf1, src);
+        const uint64_t rr = r >= n_rec ? 0 : (r < WAVE ? a0 : (r < 2u * WAVE ? a1 : sld(prec + r)));
         const uint32_t st = r < n_rec ? (uint32_t)rr : N;        // (past the runs: end sentinel)
         const uint32_t pl = (uint32_t)(rr >> 32);
         const uint32_t q63 = k + t0 + WAVE;
         const uint32_t nx63 = uni(q63 >= n_rec ? N
-                                  : (PQG_XT_RECPF && q63 < 2u * WAVE
+                                  : (q63 < 2u * WAVE
                                          ? rdl((uint32_t)(q63 < WAVE ? pf0 : pf1), q63 & (WAVE - 1u))
                                          : (uint32_t)sld(prec + q63)));
         const uint32_t en_n = __shfl_down(st, 1);
@@ -1772,416 +1600,15 @@ __device__ __forceinline__ uint32_t decode_levels_w(LevelWaveLds& L, rsrc_t rs, 
   }
 }
 
-// ---------------------------------------------------------------------------
-// Level sections of width 1..8 by speculative pieces (round 4; the window walk above stays as the
-// general path). The window walk spends a fixed ~500 VALU + ~200 SALU wave-instructions per 256
-// section bytes (pre-decode of every position, lifting tables, a tile expansion with a run search
-// per 16 slots) whatever the runs look like. Here one wave takes a super-window of 2 KiB of the
-// section, one 32-byte piece per lane:
-//   1. speculate: lane k walks the header chain from the first byte of its piece as if a header
-//      started there, until it leaves the piece, and records the positions it visited (one bit per
-//      piece byte) and its exit. Chains of the hybrid encoding re-synchronise within a few headers,
-//      so the true chain almost always enters piece k at a position lane k visited;
-//   2. resolve: from lane 0 (the true position) the scalar unit follows exit -> piece of the exit
-//      (one v_readlane pair per piece); a piece whose true entry it did not visit is walked again
-//      from that entry, until every piece on the chain is consistent;
-//   3. count: each piece on the chain re-walks from its entry to its exit summing run counts; a
-//      saturating DPP scan gives the first slot of every piece;
-//   4. emit: each piece writes its runs into an LDS image of the page's levels packed at the
-//      section's own width (RLE runs as replicated values, packed runs as shifted copies of their
-//      bytes) with ds_or, so pieces never order their writes; RLE runs longer than 8 dwords are
-//      filled by the whole wave;
-//   5. expand (per 32 Ki-bit image, once per page for C3 / C5 pages): 16 slots per lane from 2w
-//      image bytes, one aligned 16-byte store, the non-null count as a byte compare / popcount.
-// Anything outside the common case — a header that is malformed, too long (5-byte varint), an RLE
-// count of 0, an RLE value wider than the section, a chain that ends before the page's slots do —
-// makes the page fall back to the window walk, which raises the reference's error at its slot.
-constexpr uint32_t SP_P = 32;                // section bytes per lane piece
-constexpr uint32_t SP_SW = SP_P * WAVE;      // section bytes per super-window
-constexpr uint32_t SP_SEG = 2624;            // staged: super-window + 16 (alignment) + 512 (packed data) + slack
-constexpr uint32_t SP_BUFW = 1024;           // level image: 32 Ki bits
-struct LevelSpLds {
-  uint8_t seg[SP_SEG];                       // section bytes [lo, lo + SP_SEG)
-  uint32_t buf[SP_BUFW + 4];                 // level image (+ slack for the expansion's 16-byte reads)
-};
-union LevelLds {
-  LevelWaveLds a;
-  LevelSpLds b;
-};
-
-typedef uint32_t __attribute__((aligned(1), may_alias)) u32_un;
-
-struct SpRun {
-  uint32_t next, cnt, val;  // val: RLE value; PACKED: data start
-  bool pk, bad;
-};
-
-// Run header at section byte p (staged): branch-free varint of at most 4 bytes
-// (RunLengthBitPackingHybridDecoder.readNext :80-109 for width W <= 8: a 1-byte RLE value).
-template <int W>
-__device__ __forceinline__ SpRun sp_parse(const uint8_t* seg, uint32_t lo, uint32_t p, uint32_t end) {
-  const uint32_t o = p - lo;
-  const uint32_t d = *(const u32_un*)(seg + o), d1 = *(const u32_un*)(seg + o + 4u);
-  const uint32_t stop = ~d & 0x80808080u;
-  const uint32_t hl = stop ? ((uint32_t)__builtin_ctz(stop) >> 3) + 1u : 4u;
-  const uint32_t dm = d & (0xFFFFFFFFu >> (32u - 8u * hl));
-  const uint32_t v = (dm & 0x7Fu) | ((dm >> 1) & 0x3F80u) | ((dm >> 2) & 0x1FC000u) | ((dm >> 3) & 0xFE00000u);
-  SpRun r;
-  bool bad = stop == 0u || p + hl > end;
-  if (!(v & 1u)) {
-    const uint32_t val = (hl == 4u ? d1 : __builtin_amdgcn_alignbyte(d1, d, hl)) & 0xFFu;
-    r.cnt = v >> 1;
-    r.val = val;
-    r.pk = false;
-    r.next = p + hl + 1u;
-    bad |= r.cnt == 0u || r.next > end || val > (uint32_t)((1 << W) - 1);
-  } else {
-    const uint32_t g = v >> 1;
-    r.cnt = g * 8u;
-    r.val = p + hl;
-    r.pk = true;
-    r.next = p + hl + g * (uint32_t)W;
-    bad |= g == 0u;
-  }
-  r.bad = bad;
-  return r;
-}
-
-// Walk from s inside the piece [bk, bk + SP_P): visited positions -> V (bit p - bk), exit -> X
-// (first chain position past the piece or the section; a malformed header: its position, stop).
-template <int W>
-__device__ __forceinline__ void sp_walk(const uint8_t* seg, uint32_t lo, uint32_t s, uint32_t bk, uint32_t end,
-                                        uint32_t& X, uint32_t& V, bool& stop) {
-  const uint32_t pe = bk + SP_P;
-  uint32_t p = s, vm = 0;
-  bool st = false;
-  while (p < pe && p < end) {
-    const SpRun r = sp_parse<W>(seg, lo, p, end);
-    vm |= 1u << (p - bk);
-    if (r.bad) { st = true; break; }
-    p = r.next;
-  }
-  X = p;
-  V = vm;
-  stop = st;
-}
-
-// 8 section bytes at byte a (staged, else a buffer load), bytes at or past the section end 0
-// (readNext :96-99: the final group reads what is left).
-__device__ __forceinline__ uint64_t sp_read8(const uint8_t* seg, uint32_t lo, rsrc_t rs, uint32_t a, uint32_t end) {
-  uint64_t x;
-  if (a - lo + 8u <= SP_SEG) {
-    const uint8_t* q = seg + (a - lo);
-    x = (uint64_t)*(const u32_un*)q | ((uint64_t)*(const u32_un*)(q + 4) << 32);
-  } else {
-    x = ld8_any(rs, a);
-  }
-  const int32_t k = (int32_t)(end - a);
-  return k >= 8 ? x : (k <= 0 ? 0ull : (x & ((1ull << (8 * k)) - 1ull)));
-}
-
-// Dword i of the image filled with value `val` (fields at multiples of W from bit 0).
-template <int W>
-__device__ __forceinline__ uint32_t sp_pattern(uint32_t val, uint32_t i) {
-  constexpr uint32_t NC = 64u / W;
-  uint64_t rep = 0;
-#pragma unroll
-  for (uint32_t c = 0; c < NC; c++) rep |= 1ull << (c * W);
-  const uint64_t r = (uint64_t)val * rep;
-  if constexpr ((W & (W - 1)) == 0) return (uint32_t)r;
-  else return (uint32_t)(r >> ((32u * i) % (uint32_t)W));
-}
-
-// OR the level bits [b0, b1) of an RLE run into dwords [i0, i1] (by the calling lanes).
-__device__ __forceinline__ uint32_t sp_word_mask(uint32_t b0, uint32_t b1, uint32_t i) {
-  const uint32_t lo = b0 > 32u * i ? b0 - 32u * i : 0u;
-  const uint32_t hi = b1 - 32u * i >= 32u ? 32u : b1 - 32u * i;
-  const uint32_t mh = hi >= 32u ? 0xFFFFFFFFu : (1u << hi) - 1u;
-  return mh & ~((1u << lo) - 1u);
-}
-
-// Expand image slots [sbase, x_hi) (out + sbase is 16-byte aligned; slots outside [0, N) are not
-// stored): 16 slots per lane -> one 16-byte store; returns this lane's count of levels == max_def.
-template <int W>
-__device__ __forceinline__ uint32_t sp_expand(const LevelSpLds& L, uint8_t* out, int64_t sbase, int64_t x_hi,
-                                              uint32_t N, uint32_t max_def, bool count_nonnull) {
-  uint32_t cnt = 0;
-  const int64_t lo = sbase > 0 ? sbase : 0;
-  if (x_hi <= lo) return 0;
-  const uint32_t ntiles = (uint32_t)((x_hi - sbase + 15) >> 4);
-  const uint8_t* img = (const uint8_t*)L.buf;
-  for (uint32_t i = lane_id(); i < ntiles; i += WAVE) {
-    const int64_t t0 = sbase + 16 * (int64_t)i;
-    uint32_t acc[4];
-    uint32_t m1 = 0;
-    if constexpr (W == 1) {
-      m1 = *(const uint16_t*)(img + 2u * i);
-#pragma unroll
-      for (uint32_t c = 0; c < 4; c++) acc[c] = (((m1 >> (4u * c)) & 0xFu) * 0x204081u) & 0x01010101u;
-    } else if constexpr (W == 2) {
-      const uint32_t x = L.buf[i];
-#pragma unroll
-      for (uint32_t c = 0; c < 4; c++) {
-        const uint32_t y = (x >> (8u * c)) & 0xFFu;
-        acc[c] = (y & 3u) | ((y & 0xCu) << 6) | ((y & 0x30u) << 12) | ((y & 0xC0u) << 18);
-      }
-    } else if constexpr (W == 4) {
-      const uint32_t x0 = L.buf[2u * i], x1 = L.buf[2u * i + 1u];
-#pragma unroll
-      for (uint32_t c = 0; c < 4; c++) {
-        const uint32_t y = ((c < 2 ? x0 : x1) >> (16u * (c & 1u))) & 0xFFFFu;
-        acc[c] = (y & 0xFu) | ((y & 0xF0u) << 4) | ((y & 0xF00u) << 8) | ((y & 0xF000u) << 12);
-      }
-    } else if constexpr (W == 8) {
-      const u32x4 x = *(const u32x4*)(img + 16u * i);
-      acc[0] = x[0]; acc[1] = x[1]; acc[2] = x[2]; acc[3] = x[3];
-    } else {
-      const uint8_t* q = img + 2u * W * i;
-      const uint64_t a0 = (uint64_t)*(const u32_un*)q | ((uint64_t)*(const u32_un*)(q + 4) << 32);
-      const uint64_t a1 = (uint64_t)*(const u32_un*)(q + 8) | ((uint64_t)*(const u32_un*)(q + 12) << 32);
-      constexpr uint32_t M = (1u << W) - 1u;
-#pragma unroll
-      for (uint32_t c = 0; c < 4; c++) acc[c] = 0;
-#pragma unroll
-      for (uint32_t qd = 0; qd < 16; qd++) {
-        const uint32_t bp = qd * W;
-        const uint32_t f = (uint32_t)(bp + W <= 64u ? (a0 >> bp) : (bp >= 64u ? (a1 >> (bp - 64u)) : ((a0 >> bp) | (a1 << (64u - bp))))) & M;
-        acc[qd >> 2] |= f << (8u * (qd & 3u));
-      }
-    }
-    const int32_t j0 = t0 < 0 ? (int32_t)(-t0) : 0;
-    const int64_t e = x_hi < (int64_t)N ? x_hi : (int64_t)N;
-    const int32_t j1 = e - t0 >= 16 ? 16 : (int32_t)(e - t0);
-    if (j1 <= j0) continue;
-    if (count_nonnull) {
-      if (W == 1 && max_def <= 1u) {
-        const uint32_t jm = ((j1 >= 32 ? 0xFFFFFFFFu : (1u << j1) - 1u)) & ~((1u << j0) - 1u);
-        cnt += (uint32_t)__builtin_popcount((max_def ? m1 : ~m1) & jm);
-      } else {
-        const uint32_t rep = max_def * 0x01010101u;
-#pragma unroll
-        for (int32_t c = 0; c < 4; c++) {
-          const uint32_t y = acc[c] ^ rep;
-          const uint32_t nz = ((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y;
-          cnt += (uint32_t)__builtin_popcount(~nz & 0x80808080u & tile_byte_mask(j0, j1, c));
-        }
-      }
-    }
-    if (out) {
-      uint8_t* o = out + t0;
-      if (j0 == 0 && j1 == 16) {
-        gst((u32x4*)o, u32x4{acc[0], acc[1], acc[2], acc[3]});
-      } else {
-#pragma unroll
-        for (int32_t j = 0; j < 16; j++)
-          if (j >= j0 && j < j1) gst(o + j, (uint8_t)(acc[j >> 2] >> (8 * (j & 3))));
-      }
-    }
-  }
-  return cnt;
-}
-
-__device__ __forceinline__ void sp_zero(LevelSpLds& L) {
-  for (uint32_t i = 4u * lane_id(); i < SP_BUFW + 4u; i += 4u * WAVE) *(u32x4*)(L.buf + i) = u32x4{0u, 0u, 0u, 0u};
-}
-
-// Emit the runs of each lane's piece on the chain (entry E, exit X, first slot S) that fall in
-// slots [c_lo, c_hi) into the image (slot sbase = image bit 0).
-template <int W>
-__device__ __forceinline__ void sp_emit(LevelSpLds& L, uint32_t lo, rsrc_t rs, uint32_t end, bool on, uint32_t E,
-                                        uint32_t X, uint32_t S, int64_t sbase, uint32_t c_lo, uint32_t c_hi) {
-  uint32_t p = on ? E : X, s = S;
-  for (;;) {
-    const bool act = p < X && s < c_hi;
-    if (!__ballot(act)) break;
-    bool lng = false;
-    uint32_t a = 0, b = 0, val = 0;
-    if (act) {
-      const SpRun r = sp_parse<W>(L.seg, lo, p, end);
-      const uint32_t e = r.cnt < c_hi - s ? s + r.cnt : c_hi;
-      a = s > c_lo ? s : c_lo;
-      b = e;
-      if (a < b) {
-        const uint32_t b0 = (uint32_t)((int64_t)a - sbase) * W, b1 = (uint32_t)((int64_t)b - sbase) * W;
-        if (!r.pk) {
-          val = r.val;
-          if (val) {
-            const uint32_t i0 = b0 >> 5, i1 = (b1 - 1u) >> 5;
-            if (i1 - i0 >= 8u) {
-              lng = true;
-            } else {
-              for (uint32_t i = i0; i <= i1; i++) atomicOr(&L.buf[i], sp_pattern<W>(val, i) & sp_word_mask(b0, b1, i));
-            }
-          }
-        } else {
-          const uint32_t sb = (a - s) * W;  // bit of slot a in the run's data
-          const uint32_t nbits = b1 - b0;
-          for (uint32_t t = 0; t < nbits; t += 32u) {
-            const uint32_t q = sb + t;
-            uint32_t x = (uint32_t)(sp_read8(L.seg, lo, rs, r.val + (q >> 3), end) >> (q & 7u));
-            const uint32_t nb = nbits - t;
-            if (nb < 32u) x &= (1u << nb) - 1u;
-            const uint32_t o = b0 + t, wi = o >> 5, sh = o & 31u;
-            atomicOr(&L.buf[wi], x << sh);
-            if (sh && nb > 32u - sh) atomicOr(&L.buf[wi + 1u], x >> (32u - sh));
-          }
-        }
-      }
-      s = e;
-      p = r.next;
-    }
-    // long RLE runs: the whole wave fills them
-    uint64_t lm = __ballot(lng);
-    while (lm) {
-      const uint32_t l = (uint32_t)__builtin_ctzll(lm);
-      lm &= lm - 1ull;
-      const uint32_t la = uni(rdl(a, l)), lb = uni(rdl(b, l)), lv = uni(rdl(val, l));
-      const uint32_t b0 = (uint32_t)((int64_t)la - sbase) * W, b1 = (uint32_t)((int64_t)lb - sbase) * W;
-      for (uint32_t i = (b0 >> 5) + lane_id(); i <= ((b1 - 1u) >> 5); i += WAVE)
-        atomicOr(&L.buf[i], sp_pattern<W>(lv, i) & sp_word_mask(b0, b1, i));
-    }
-  }
-}
-
-// Returns the slots decoded (N) and the non-null count, or sets *fallback (nothing reported: the
-// caller re-decodes the section with decode_levels_w, which raises any error at its slot).
-template <int W>
-__device__ uint32_t decode_levels_sp(LevelSpLds& L, rsrc_t rs, uint32_t beg, uint32_t end, uint32_t N, uint8_t* out,
-                                     uint32_t max_def, bool count_nonnull, uint32_t* nonnull, bool* fallback) {
-  constexpr uint32_t CAPS = (SP_BUFW * 32u / W) & ~15u;  // slots per image
-  const uint32_t lane = lane_id();
-  const int64_t mis = out ? (int64_t)((uintptr_t)out & 15u) : 0;
-  int64_t sbase = -mis;
-  uint32_t pos = beg, produced = 0, cnt = 0;
-  *fallback = false;
-  sp_zero(L);
-  while (produced < N) {
-    pos = uni(pos);
-    if (pos >= end) { *fallback = true; return 0; }  // readNext :81 (the general path reports it)
-    const uint32_t lo = pos & ~15u;
-    wave_sync();
-    for (uint32_t i = 16u * lane; i < SP_SEG; i += 16u * WAVE)
-      *(u32x4*)(L.seg + i) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lo + i), 0, 0);
-    wave_sync();
-    const uint32_t bk = pos + SP_P * lane;
-    uint32_t X, V;
-    bool stop;
-    sp_walk<W>(L.seg, lo, bk, bk, end, X, V, stop);
-    uint32_t E = 0, last = 0;
-    uint64_t R = 0;
-    for (uint32_t it = 0;; it++) {
-      const uint32_t nl = (stop || X >= end || X - pos >= SP_SW) ? 64u : (X - pos) / SP_P;
-      R = 0;
-      E = 0;
-      uint32_t k = 0, e = pos;
-      while (k < 64u) {
-        R |= 1ull << k;
-        E = lane == k ? e : E;
-        last = k;
-        e = uni(rdl(X, k));
-        k = uni(rdl(nl, k));
-      }
-      const bool on = (R >> lane) & 1ull;
-      const uint32_t off = E - bk;
-      const bool ok = !on || (off < SP_P && ((V >> off) & 1u));
-      if (!__ballot(!ok)) break;
-      if (it >= 64u) { *fallback = true; return 0; }
-      if (!ok) sp_walk<W>(L.seg, lo, E, bk, end, X, V, stop);
-    }
-    const bool on = (R >> lane) & 1ull;
-    // runs counted from the entry to the exit
-    const uint32_t cap = N - produced;
-    uint32_t c = 0;
-    if (on) {
-      for (uint32_t p = E; p < X;) {
-        const SpRun r = sp_parse<W>(L.seg, lo, p, end);
-        c = r.cnt < cap - c ? c + r.cnt : cap;
-        p = r.next;
-      }
-    }
-    const uint32_t inc = wave_incl_scan_sat(c, cap);
-    uint32_t ex = __shfl_up(inc, 1);
-    if (lane == 0) ex = 0;
-    const uint32_t total = uni(rdl(inc, WAVE - 1));
-    const uint32_t x_last = uni(rdl(X, last));
-    const bool stop_last = uni(rdl((uint32_t)stop, last)) != 0u;
-    if (total < cap && (stop_last || x_last >= end)) { *fallback = true; return 0; }  // a malformed header / the section ends first
-    // emit into the image; an image that fills up is expanded and the super-window's remaining
-    // runs go to the next one (a run keeps its slots: each emit re-walks and clips)
-    const uint32_t hi = produced + total;
-    uint32_t c_lo = produced;
-    for (;;) {
-      const int64_t whi = sbase + (int64_t)CAPS;
-      const uint32_t c_hi = (int64_t)hi < whi ? hi : (uint32_t)whi;
-      wave_sync();
-      sp_emit<W>(L, lo, rs, end, on, E, X, produced + ex, sbase, c_lo, c_hi);
-      if ((int64_t)hi <= whi) break;
-      wave_sync();
-      cnt += sp_expand<W>(L, out, sbase, whi, N, max_def, count_nonnull);
-      wave_sync();
-      sp_zero(L);
-      sbase = whi;
-      c_lo = (uint32_t)whi;
-    }
-    produced = hi;
-    pos = x_last;
-  }
-  wave_sync();
-  cnt += sp_expand<W>(L, out, sbase, (int64_t)N, N, max_def, count_nonnull);
-  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-  if (nonnull) *nonnull = cnt;
-  return N;
-}
-
-#ifndef PQG_LV_SP
-#define PQG_LV_SP 0  // 1: RLE level sections through the speculative-piece decoder (measured 2.2x slower: A/B builds only)
-#endif
-
-template <int W>
-__device__ __forceinline__ uint32_t decode_levels_sp_or_w(LevelLds& L, rsrc_t rs, uint32_t beg, uint32_t end, uint32_t N,
-                                                          uint8_t* out, uint32_t max_def, bool count_nonnull,
-                                                          uint32_t* nonnull, int* err_code) {
-  bool fb = true;
-  uint32_t r = 0;
-  if (PQG_LV_SP) r = decode_levels_sp<W>(L.b, rs, beg, end, N, out, max_def, count_nonnull, nonnull, &fb);
-  if (!fb) {
-    *err_code = 0;
-    return r;
-  }
-  wave_sync();
-  return decode_levels_w(L.a, rs, beg, end, W, N, out, max_def, count_nonnull, nonnull, err_code);
-}
-
-// RLE / bit-packed level section of width w: the speculative-piece decoder for w <= 8, the window
-// walk for wider sections and for the sections it hands back.
-__device__ __forceinline__ uint32_t decode_levels_any(LevelLds& L, rsrc_t rs, uint32_t beg, uint32_t end, int w,
-                                                      uint32_t N, uint8_t* out, uint32_t max_def, bool count_nonnull,
-                                                      uint32_t* nonnull, int* err_code) {
-  switch (w) {
-    case 1: return decode_levels_sp_or_w<1>(L, rs, beg, end, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 2: return decode_levels_sp_or_w<2>(L, rs, beg, end, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 3: return decode_levels_sp_or_w<3>(L, rs, beg, end, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 4: return decode_levels_sp_or_w<4>(L, rs, beg, end, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 5: return decode_levels_sp_or_w<5>(L, rs, beg, end, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 6: return decode_levels_sp_or_w<6>(L, rs, beg, end, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 7: return decode_levels_sp_or_w<7>(L, rs, beg, end, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 8: return decode_levels_sp_or_w<8>(L, rs, beg, end, N, out, max_def, count_nonnull, nonnull, err_code);
-    default: return decode_levels_w(L.a, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
-  }
-}
-
 // 5 waves per SIMD (LDS 6.9 KiB per wave, <= 102 VGPRs): 40,000 C3 pages in 8 rounds instead of 10
-#ifndef PQG_LV_WAVES
-#define PQG_LV_WAVES 5
-#endif
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_LV_WAVES))) void k_levels(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5))) void k_levels(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                 PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                 const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                                 ErrCount err_count) {
-  __shared__ __attribute__((aligned(16))) LevelLds lvl_lds[WPB];
+  __shared__ __attribute__((aligned(16))) LevelWaveLds lvl_lds[WPB];
   const int page = wave_page(list, n_list);
   if (page < 0) return;
-  LevelLds& LL = lvl_lds[wave_id()];
+  LevelWaveLds& LL = lvl_lds[wave_id()];
   PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
   const uint32_t lane = lane_id();
@@ -2254,7 +1681,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_LV
   uint64_t lvl_err_key = ~0ull;
   if (wr > 0) {
     uint32_t done = rl_be ? decode_levels_be(win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code)
-                          : decode_levels_any(LL, win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code);
+                          : decode_levels_w(LL, win.rs, rl_beg, rl_end, wr, nslots, rep_out, 0, false, nullptr, &code);
     if (code) {
       limit = done;
       lvl_err_key = ((uint64_t)done << 1) << 8 | (uint64_t)code;
@@ -2267,7 +1694,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(PQG_LV
     int code2 = 0;
     uint32_t done = dl_be ? decode_levels_be(win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true,
                                              &nonnull, &code2)
-                          : decode_levels_any(LL, win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true,
+                          : decode_levels_w(LL, win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true,
                                              &nonnull, &code2);
     if (code2) {
       uint64_t key = (((uint64_t)done << 1) | 1ull) << 8 | (uint64_t)code2;
@@ -2631,9 +2058,6 @@ __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_
 // past the count and are not stored) and the store layout are those of delta_expand: lane l stores
 // the 16 values ending one delta earlier (the first from lane l - 1 / the carry), as wide stores
 // when the run is aligned. Not for NEG streams (DELTA_LENGTH lengths check every value).
-#ifndef PQG_DELTA_SEG_ANY
-#define PQG_DELTA_SEG_ANY 2  // 1: the segment expansion for 16-byte aligned pages only (A/B builds)
-#endif
 template <int W>
 __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uint32_t b_data, uint32_t b_wpos,
                                                  uint32_t b_lo, uint32_t b_hi, uint32_t b_nmb, uint32_t blk_first,
@@ -3032,8 +2456,7 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     // ---- expand the walked blocks (every read from the LDS segment)
     // (the segment path stores 16-value runs per lane, shifted to 16-byte alignment: pages of
     // nullable columns, which start at any value offset, take it too)
-    if (PQG_DELTA_SEG_ANY && !NEG && (mbs % 16u) == 0 && ((uint64_t)block * W) % 16u == 0 &&
-        (PQG_DELTA_SEG_ANY > 1 || ((uintptr_t)out % 16u) == 0))
+    if (!NEG && (mbs % 16u) == 0 && ((uint64_t)block * W) % 16u == 0)
       delta_expand_seg<W>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out);
     else if (E == 1) delta_expand<W, NEG, 1>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else if (E == 2) delta_expand<W, NEG, 2>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);

@@ -22,13 +22,7 @@
 
 namespace pqg {
 
-#ifndef PQG_ZS_RING
-#define PQG_ZS_RING 4096
-#endif
-#ifndef PQG_ZS_WAVES
-#define PQG_ZS_WAVES 2
-#endif
-constexpr uint32_t ZS_RING = PQG_ZS_RING;  // LDS mirror of the most recent output
+constexpr uint32_t ZS_RING = 4096;  // LDS mirror of the most recent output
 constexpr uint32_t ZS_WIN = 1024;     // LDS window of the sequence bitstream
 constexpr uint32_t ZS_HWIN = 256;     // LDS window per Huffman stream
 constexpr uint32_t ZS_LIT_MAX = 131072;
@@ -1047,10 +1041,7 @@ __device__ uint64_t zxxh64(const uint8_t* p, uint32_t n) {
 // its window in the next sequence, every lane in the loop re-centres its window at its position, so
 // the wave waits for one round of loads per ~150 sequences instead of once per lane's refill
 // (measured: per-lane refills at uncorrelated times stalled the wave every few sequences).
-#ifndef PQG_ZQ_JOBS
-#define PQG_ZQ_JOBS 12
-#endif
-constexpr uint32_t ZQ_JOBS = PQG_ZQ_JOBS;  // lanes (jobs) per workgroup
+constexpr uint32_t ZQ_JOBS = 12;  // lanes (jobs) per workgroup
 #ifdef PQG_DIAG
 // Diagnostic build only (tools/diag_zstd.py): per job 6 u64 = pre-pass cycles (whole job, tables,
 // sequence loops), sequences, window re-centrings, compressed blocks.
@@ -1194,12 +1185,6 @@ __device__ bool zq_table(const ZqLds& L, int kind, ZqLane& T, uint32_t r, int* t
   return have;
 }
 
-#ifndef PQG_ZQ_THR
-#define PQG_ZQ_THR 1  // 0: the re-centring test recomputed from the window base every sequence (A/B builds)
-#endif
-#ifndef PQG_ZQ_LEAN
-#define PQG_ZQ_LEAN 1  // 0: every record bound checked per sequence (A/B builds)
-#endif
 // The sequences of one compressed block's sequence section [q, lim) (absolute input offsets). Returns
 // false for anything the inline path must handle.
 __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32_t lim, uint32_t regen, uint32_t& outp,
@@ -1274,7 +1259,7 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
   // literal and match lengths stay below 2^17 (LL code 35: 65536 + 16 extra bits; ML code 52: 65539 +
   // 16 bits; the tables hold valid codes only), and an offset that passes the window check is at most
   // the output so far (< 2^27 + 2^18: jobs of < 2^27 bytes)
-  if (PQG_ZQ_LEAN && cnt + nseq > cap) return false;
+  if (cnt + nseq > cap) return false;
   // One sequence = one pass with no data-dependent branch on the common path: the table entries and
   // 20 window bytes at the read position are loaded together; the sequence's bits (offset, match and
   // literal length extras, then the LL / ML / OF state bits: T <= 64 of them, else the inline path
@@ -1284,12 +1269,7 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
   int32_t rthr = wlo > sb ? (int32_t)(wlo - sb) * 8 + 160 : INT32_MIN;
   for (uint32_t i = 0; i < nseq; i++) {
     {  // a sequence reads at most 64 bits below `bits`: re-centre every window of the loop together
-#if PQG_ZQ_THR
       const bool want = bits < rthr;
-#else
-      const int32_t lowbit = bits - 160 > 0 ? bits - 160 : 0;
-      const bool want = sb + ((uint32_t)lowbit >> 3) < wlo;
-#endif
       if (__ballot(want)) {
         recenter(sb + ((uint32_t)(bits > 0 ? bits : 0) >> 3));
         rthr = wlo > sb ? (int32_t)(wlo - sb) * 8 + 160 : INT32_MIN;
@@ -1353,9 +1333,6 @@ __device__ bool zq_block_seqs(ZqLds& L, ZqLane& T, rsrc_t rs, uint32_t q, uint32
       so = nso;
     }
     bad |= bits < 0 || lits + ll > regen || roff == 0 || roff > outp + ll - frame0;
-#if !PQG_ZQ_LEAN
-    bad |= ll >= (1u << 18) || ml >= (1u << 18) || roff >= (1u << 28) || cnt >= cap;
-#endif
     if (bad) return false;
     gst(rec + cnt, (uint64_t)ll | ((uint64_t)ml << 18) | ((uint64_t)roff << 36));
     cnt++;
@@ -1517,7 +1494,7 @@ __device__ __forceinline__ void zstd_job(ZWaveLds& L, const uint8_t* __restrict_
                          uint64_t dst_bytes, const pqg_snappy_job& jb, int j, int32_t* status, uint8_t* litbuf,
                          const uint64_t* rec);
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PQG_ZS_WAVES))) void k_zstd(const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_zstd(const uint8_t* __restrict__ src, uint64_t src_bytes, uint8_t* dst,
                                              uint64_t dst_bytes, const pqg_snappy_job* __restrict__ jobs, int n_jobs,
                                              int32_t* status, uint8_t* scratch, uint64_t lit_stride,
                                              const uint64_t* __restrict__ seqs, const int32_t* __restrict__ mode) {

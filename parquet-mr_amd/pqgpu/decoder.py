@@ -494,6 +494,10 @@ class Decoder:
         st = abi.Status()
         rc = L.pqg_decode_staged(self.ctx, batch.data.size, C.addressof(descs), len(batch.columns),
                                  pages.ctypes.data if len(pages) else None, len(pages), counts.ctypes.data, C.byref(st))
+        if rc != abi.OK and batch.columns:
+            probe = abi.StagedOutput()
+            if L.pqg_staged_column(self.ctx, 0, C.byref(probe)) != abi.OK:
+                native.check(rc, st, what="pqg_decode_staged")  # no plan was made: the call's own status
         res = []
         for i, cd in enumerate(batch.columns):
             o = abi.StagedOutput()
@@ -647,6 +651,26 @@ class Decoder:
                                                offs.ctypes.data, cnts.ctypes.data, len(cnts), out.ctypes.data)
         native.check(rc, what="pqg_router_read_runs")
         return out[:int(cnts.sum())]
+
+    def router_read_page(self, bit_width, stream, pos, count, out=None):
+        """ParquetReadRouter.read through the page cache (pqg_router_read_page): `stream` is the
+        caller's whole stream (a uint8 array) positioned at byte `pos`, the run's data start; returns
+        the run's `count` values (into `out` when given)."""
+        a = stream
+        left = a.size - pos
+        if out is None:
+            out = np.zeros(max(count, 1), dtype=np.int32)
+        ptr = a.ctypes.data + pos if left > 0 else None
+        rc = native.lib().pqg_router_read_page(self.ctx, bit_width, ptr, left, count, out.ctypes.data)
+        native.check(rc, what="pqg_router_read_page")
+        return out[:count]
+
+    def router_cache_stats(self):
+        """(hits, misses) of pqg_router_read_page on this context."""
+        import ctypes as C
+        h, m = C.c_uint64(), C.c_uint64()
+        native.check(native.lib().pqg_router_cache_stats(self.ctx, C.byref(h), C.byref(m)), what="pqg_router_cache_stats")
+        return int(h.value), int(m.value)
 
     def unpack_runs(self, bit_width, d_in, in_offsets, counts, out_offsets, d_out):
         """Batch of bit-packed runs, all device tensors (pqg_unpack_runs)."""

@@ -18,7 +18,8 @@ EXPORTS = [
     "pqg_decode",
     "pqg_sync", "pqg_plan_create", "pqg_plan_launch", "pqg_plan_kernel_count", "pqg_plan_timeout_fallbacks", "pqg_plan_plain_fallbacks",
     "pqg_plan_destroy",
-    "pqg_decode_host", "pqg_unpack_runs", "pqg_router_read", "pqg_router_read_runs", "pqg_error_name",
+    "pqg_decode_host", "pqg_unpack_runs", "pqg_router_read", "pqg_router_read_runs", "pqg_router_read_page",
+    "pqg_router_cache_lookup", "pqg_router_cache_stats", "pqg_error_name",
     "pqg_page_errors", "pqg_plan_page_errors", "pqg_host_input", "pqg_decode_staged", "pqg_staged_column",
     "pqg_copy_out", "pqg_assemble", "pqg_assemble_schema",
     "pqg_snappy_decompress", "pqg_snappy_sync", "pqg_zstd_decompress", "pqg_zstd_sync",
@@ -71,6 +72,9 @@ def lib():
         L.pqg_unpack_runs.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32]
         L.pqg_router_read.argtypes = [vp, i32, vp, C.c_size_t, i32, vp]
         L.pqg_router_read_runs.argtypes = [vp, i32, vp, C.c_size_t, vp, vp, i32, vp]
+        L.pqg_router_read_page.argtypes = [vp, i32, vp, C.c_size_t, i32, vp]
+        L.pqg_router_cache_lookup.argtypes = [vp, i32, vp, C.c_size_t, i32, vp, C.POINTER(i32)]
+        L.pqg_router_cache_stats.argtypes = [vp, C.POINTER(u64), C.POINTER(u64)]
         L.pqg_page_errors.argtypes = [vp, vp, i32]
         L.pqg_plan_page_errors.argtypes = [vp, vp, i32]
         L.pqg_host_input.argtypes = [vp, u64, C.POINTER(vp)]

@@ -143,6 +143,25 @@ public final class PqGpu {
     routerReadBatchArray(ctx, bitWidth, a, off, in.remaining(), runOffsets, runCounts, nRuns, out);
   }
 
+  /**
+   * ParquetReadRouter.read with its contract kept (the run's values are in out[0..count) when the call
+   * returns) at one device round trip per page (pqg_router_read_page). `tail` holds the caller's stream
+   * from the run's data start to the stream's end in [position, limit): the first read of a page also
+   * unpacks every later bit-packed run of the stream, and the reads of those runs are served from the
+   * library's cache with no device work. The caller advances its own stream by count * bitWidth / 8
+   * bytes; fewer bytes than that in `tail` -> EOFException with nothing written.
+   */
+  public static void routerReadPage(long ctx, int bitWidth, ByteBuffer tail, int count, int[] out)
+      throws java.io.EOFException {
+    if (tail.isDirect()) {
+      routerReadPageDirect(ctx, bitWidth, tail, tail.position(), tail.remaining(), count, out);
+      return;
+    }
+    byte[] a = heapBytes(tail);
+    int off = tail.hasArray() && !tail.isReadOnly() ? tail.arrayOffset() + tail.position() : 0;
+    routerReadPageArray(ctx, bitWidth, a, off, tail.remaining(), count, out);
+  }
+
   /** The backing array of a heap buffer, or a copy of [position, limit) of a read-only one. */
   private static byte[] heapBytes(ByteBuffer b) {
     if (b.hasArray() && !b.isReadOnly()) return b.array();
@@ -169,6 +188,12 @@ public final class PqGpu {
 
   private static native void routerReadArray(long ctx, int bitWidth, byte[] in, int offset, int length, int count,
       int[] out);
+
+  private static native void routerReadPageDirect(long ctx, int bitWidth, ByteBuffer tail, int offset, int length,
+      int count, int[] out);
+
+  private static native void routerReadPageArray(long ctx, int bitWidth, byte[] tail, int offset, int length,
+      int count, int[] out);
 
   private static native void routerReadBatchDirect(long ctx, int bitWidth, ByteBuffer in, int offset, int length,
       long[] runOffsets, int[] runCounts, int nRuns, int[] out);

@@ -256,7 +256,8 @@ static jlongArray decode_host(JNIEnv* env, jlong ctx, jobject direct, jbyteArray
     goto done;
   }
   if (rc && pqg_page_errors(c, pe, n_pages) != PQG_OK) {
-    throw_code(env, PQG_ERR_INVALID_ARG, "pqg_page_errors failed");
+    /* no plan was made (a descriptor refused before the launch): the call's own status is the error */
+    throw_code(env, rc, st.message);
     goto done;
   }
   for (jsize i = 0; i < n_cols; i++) {
@@ -338,6 +339,16 @@ JNIEXPORT jlongArray JNICALL Java_org_apache_parquet_column_values_gpu_PqGpu_dec
                      rep_levels, binary, page_counts);
 }
 
+static void throw_router(JNIEnv* env, int rc, const char* what) {
+  /* SingleBufferInputStream.slice past the end: EOFException; the router declares IOException */
+  if (rc == PQG_ERR_EOF) {
+    jclass c = (*env)->FindClass(env, "java/io/EOFException");
+    if (c) (*env)->ThrowNew(env, c, "routerRead: input shorter than count * bitWidth / 8 bytes");
+  } else if (rc > 0) {
+    throw_code(env, rc, what);
+  }
+}
+
 /* Router reads copy their input in (GetByteArrayRegion / direct address) and their output out
  * (SetIntArrayRegion): no Java array is held while the device works. */
 static void router_runs(JNIEnv* env, jlong ctx, jint bit_width, jobject direct, jbyteArray array, jint offset,
@@ -356,13 +367,7 @@ static void router_runs(JNIEnv* env, jlong ctx, jint bit_width, jobject direct, 
   if (!rc && total) (*env)->SetIntArrayRegion(env, out, 0, (jsize)total, (const jint*)dst);
   free(in);
   free(dst);
-  /* SingleBufferInputStream.slice past the end: EOFException; the router declares IOException */
-  if (rc == PQG_ERR_EOF) {
-    jclass c = (*env)->FindClass(env, "java/io/EOFException");
-    if (c) (*env)->ThrowNew(env, c, "routerRead: input shorter than count * bitWidth / 8 bytes");
-  } else if (rc > 0) {
-    throw_code(env, rc, "pqg_router_read_runs failed");
-  }
+  throw_router(env, rc, "pqg_router_read_runs failed");
 }
 
 static void router_read(JNIEnv* env, jlong ctx, jint bit_width, jobject direct, jbyteArray array, jint offset,
@@ -399,6 +404,60 @@ static void router_read_batch(JNIEnv* env, jlong ctx, jint bit_width, jobject di
   }
   free(offs);
   free(counts);
+}
+
+/* ParquetReadRouter.read with the contract kept (values in `out` on return), one device round trip per
+ * page (pqg_router_read_page). [offset, offset + length) is the caller's stream from the run's data start
+ * to its end. A direct buffer is read in place; a heap array is probed with the run's bytes only
+ * (pqg_router_cache_lookup: a host-only copy of count * bitWidth / 8 bytes) and copied whole only on a
+ * miss. No Java array is held while the device works. */
+static void router_page(JNIEnv* env, jlong ctx, jint bit_width, jobject direct, jbyteArray array, jint offset,
+                        jint length, jint count, jintArray out) {
+  if (!in_check(env, direct, array, offset, length, "routerReadPage: bad buffer range")) return;
+  if (count < 0 || bit_width < 0 || bit_width > 32 || (*env)->GetArrayLength(env, out) < count) {
+    throw_code(env, PQG_ERR_INVALID_ARG, "routerReadPage arguments");
+    return;
+  }
+  pqg_ctx* c = (pqg_ctx*)(intptr_t)ctx;
+  const uint64_t need = (uint64_t)count * (uint64_t)bit_width / 8u;
+  int32_t* dst = (int32_t*)malloc(4 * (size_t)count + 4);
+  int rc = dst ? PQG_OK : PQG_ERR_INVALID_ARG;
+  if (!rc && direct) {
+    const uint8_t* base = (const uint8_t*)(*env)->GetDirectBufferAddress(env, direct);
+    rc = pqg_router_read_page(c, bit_width, base + offset, (size_t)length, count, dst);
+  } else if (!rc) {
+    int hit = 0;
+    if (need <= (uint64_t)length) {
+      uint8_t* run = (uint8_t*)malloc((size_t)need + 1);
+      rc = run ? PQG_OK : PQG_ERR_INVALID_ARG;
+      if (!rc && !copy_in(env, NULL, array, offset, (jint)need, run)) rc = -1; /* exception pending */
+      if (!rc) rc = pqg_router_cache_lookup(c, bit_width, run, (size_t)length, count, dst, &hit);
+      free(run);
+    }
+    if (!rc && !hit) {
+      uint8_t* tail = (uint8_t*)malloc((size_t)length + 1);
+      rc = tail ? PQG_OK : PQG_ERR_INVALID_ARG;
+      if (!rc && !copy_in(env, NULL, array, offset, length, tail)) rc = -1;
+      if (!rc) rc = pqg_router_read_page(c, bit_width, tail, (size_t)length, count, dst);
+      free(tail);
+    }
+  }
+  if (!rc && count) (*env)->SetIntArrayRegion(env, out, 0, count, (const jint*)dst);
+  free(dst);
+  throw_router(env, rc, "pqg_router_read_page failed");
+}
+
+JNIEXPORT void JNICALL Java_org_apache_parquet_column_values_gpu_PqGpu_routerReadPageDirect(
+    JNIEnv* env, jclass k, jlong ctx, jint bit_width, jobject in, jint offset, jint length, jint count, jintArray out) {
+  (void)k;
+  router_page(env, ctx, bit_width, in, NULL, offset, length, count, out);
+}
+
+JNIEXPORT void JNICALL Java_org_apache_parquet_column_values_gpu_PqGpu_routerReadPageArray(
+    JNIEnv* env, jclass k, jlong ctx, jint bit_width, jbyteArray in, jint offset, jint length, jint count,
+    jintArray out) {
+  (void)k;
+  router_page(env, ctx, bit_width, NULL, in, offset, length, count, out);
 }
 
 JNIEXPORT void JNICALL Java_org_apache_parquet_column_values_gpu_PqGpu_routerReadBatchDirect(

@@ -515,3 +515,168 @@ def test_router_batch_eof_writes_nothing(router, tmp_path):
     data = bytes(range(100))
     rc, _ = _run_router(router, _router_case(tmp_path, 7, data, [0, 60], [8, 48]), tmp_path)
     assert rc == abi.ERR_EOF
+
+
+# ---- ParquetReadRouter with its contract: a Spark-style caller loop (pqg_router_read_page) ---------------
+
+REPLAY_SRC = os.path.join(REPO, "tests", "c", "router_replay.c")
+
+
+@pytest.fixture(scope="module")
+def router_replay(tmp_path_factory):
+    return _build(tmp_path_factory, REPLAY_SRC, "router_replay")
+
+
+def _v1_streams(ch):
+    """Per V1 page of a chunk: its hybrid sections as (bit_width, n, section bytes, rest of the page
+    from the section start): rl / dl level sections (4-byte length prefix) and a dictionary-encoded
+    data section (1-byte bit width + ids to the page end)."""
+    out = []
+    for pg in ch.pages:
+        assert pg.version == 1
+        b, at = pg.body, 0
+        for maxl in (ch.max_rep, ch.max_def):
+            if maxl == 0:
+                continue
+            ln = struct.unpack_from("<i", b, at)[0]
+            out.append((writer.width_from_max_int(maxl), pg.num_values, b[at + 4:at + 4 + ln], b[at + 4:]))
+            at += 4 + ln
+        if pg.encoding in (abi.RLE_DICTIONARY, abi.PLAIN_DICTIONARY) and at < len(b):
+            # values count: the slots with d == max_def (the oracle's levels tell; here all for required)
+            out.append((b[at], None, b[at + 1:], b[at + 1:]))
+    return out
+
+
+def _replay(router_replay, tmp_path, streams, tail):
+    """streams: (w, n, section, page rest). Returns (calls, per-stream (code, decoded), stats)."""
+    p = tmp_path / "replay.bin"
+    blob = [b"PQGS", struct.pack("<i", len(streams))]
+    for w, n, sec, rest in streams:
+        s = rest if tail else sec
+        blob.append(struct.pack("<iqQQ", w, n, len(sec), len(s)) + bytes(s))
+    p.write_bytes(b"".join(blob))
+    outf = tmp_path / "replay.out"
+    r = subprocess.run([router_replay, str(p), str(outf)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    vals = np.fromfile(str(outf), dtype="<i4")
+    calls, res, stats, at = [], [], None, 0
+    for ln in r.stdout.splitlines():
+        f = ln.split()
+        if f[0] == "CALL":
+            s, pos, cnt = int(f[1]), int(f[2]), int(f[3])
+            calls.append((s, pos, cnt, vals[at:at + cnt]))
+            at += cnt
+        elif f[0] == "STREAM":
+            n = int(f[3])
+            res.append((int(f[2]), vals[at:at + n]))
+            at += n
+        elif f[0] == "STATS":
+            stats = (int(f[1]), int(f[2]))
+        else:
+            pytest.fail(ln)
+    return calls, res, stats
+
+
+def _check_replay(streams, calls, res, stats):
+    """Every read's buffer on return == the oracle's ParquetReadRouter.readBatch at that position;
+    each stream's values == the oracle's RunLengthBitPackingHybridDecoder; one device round trip per
+    stream that has bit-packed runs."""
+    from oracle import pqref
+    for s, pos, cnt, got in calls:
+        w, _, sec, _ = streams[s]
+        want, _ = pqref.router_read(w, bytes(sec[pos:]), cnt)
+        assert np.array_equal(got, want), (s, pos, cnt)
+    for s, (code, got) in enumerate(res):
+        w, n, sec, _ = streams[s]
+        want, rc, _, _ = pqref.rle_decode(w, bytes(sec), n)
+        assert code == 0 and rc == 0
+        assert np.array_equal(got, want), s
+    with_packed = len({s for s, _, _, _ in calls})
+    assert stats[1] == with_packed and stats[0] == len(calls) - with_packed
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tail", [False, True], ids=["section", "page_rest"])
+@pytest.mark.parametrize("zipf", [1.5, 2.0])
+def test_router_replay_c2_pages(router_replay, tmp_path, zipf, tail):
+    """C2's shape (Zipf runs of ids, w = 10, 20,000-value V1 pages as parquet-mr writes them), read the
+    way Spark's readNextGroup reads: header -> ParquetReadRouter.read -> consume currentBuffer at once."""
+    from tools import workloads
+    ch, _, _ = workloads.make_c2(120_000, a=zipf)
+    streams = [(w, pg.num_values, sec, rest) for (w, _, sec, rest), pg in zip(_v1_streams(ch), ch.pages)]
+    calls, res, stats = _replay(router_replay, tmp_path, streams, tail)
+    assert len(calls) > 10
+    _check_replay(streams, calls, res, stats)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tail", [False, True], ids=["section", "page_rest"])
+def test_router_replay_nested_fixture(router_replay, tmp_path, tail):
+    """parquet-mr 1.9.0's nested fixture: every rl / dl level section and dictionary id section through
+    the caller loop (with page_rest the caller's stream runs on into the page's later sections, which the
+    walk parses as if they were runs: those are unpacked and never served)."""
+    from oracle import pqref
+    name = "test-file-with-no-column-indexes-1"
+    streams = []
+    for n, c in fixtures.chunk_cases():
+        if n != name:
+            continue
+        ch, _ = fixtures.load_chunk(name, c)
+        ref = pqref.decode_batch(writer.build_batch([ch]))
+        dl = ref.columns[0]["def_levels"]
+        at = 0
+        # per page: level streams, then the data stream with n = non-null slots of the page
+        for pg in ch.pages:
+            ss = _v1_streams(type(ch)(ch.physical_type, ch.max_rep, ch.max_def, ch.type_length, [pg]))
+            nn = int((dl[at:at + pg.num_values] == ch.max_def).sum()) if dl is not None else pg.num_values
+            streams += [(w, cnt if cnt is not None else nn, sec, rest) for w, cnt, sec, rest in ss]
+            at += pg.num_values
+    assert len(streams) >= 10
+    calls, res, stats = _replay(router_replay, tmp_path, streams, tail)
+    _check_replay(streams, calls, res, stats)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w", [1, 2, 3, 7, 8, 10, 13, 16, 20, 24, 31, 32])
+def test_router_replay_widths(router_replay, tmp_path, w):
+    """Hybrid streams as parquet-mr's encoder writes them (RunLengthBitPackingHybridEncoder: packed runs
+    of up to 504 values, RLE runs of repeats), every width class, several streams back to back (the cache
+    moves from stream to stream)."""
+    rng = np.random.default_rng(500 + w)
+    streams = []
+    for k in range(4):
+        n = int(rng.integers(2000, 9000))
+        runs = np.minimum(rng.zipf(1.8, size=n), 300)
+        v = np.repeat(rng.integers(0, 1 << min(w, 31), size=runs.size, dtype=np.int64), runs)[:n].astype(np.uint32)
+        sec = writer.rle_encode(v, w)
+        streams.append((w, n, sec, sec + bytes(rng.integers(0, 256, size=64, dtype=np.uint8))))
+    calls, res, stats = _replay(router_replay, tmp_path, streams, True)
+    assert calls
+    _check_replay(streams, calls, res, stats)
+
+
+@pytest.mark.gpu
+def test_router_page_cache_serves_only_matching_bytes(tmp_path):
+    """A cached run is served only for the same width, count, position from the stream end and bytes:
+    a different buffer of the same length whose run bytes differ is a miss and decodes its own bytes."""
+    from oracle import pqref
+    from pqgpu import decoder as D
+    dec = D.Decoder(0)
+    rng = np.random.default_rng(77)
+    v = rng.integers(0, 1 << 9, size=4000).astype(np.uint32)
+    sec = np.frombuffer(writer.rle_encode(v, 9), dtype=np.uint8).copy()
+    hdr_len = 1 if sec[0] < 0x80 else 2
+    count = ((int(sec[0]) & 0x7F) | ((int(sec[1]) & 0x7F) << 7 if hdr_len == 2 else 0)) >> 1
+    count *= 8
+    got = dec.router_read_page(9, sec, hdr_len, count)
+    assert np.array_equal(got, pqref.router_read(9, sec[hdr_len:].tobytes(), count)[0])
+    h0, m0 = dec.router_cache_stats()
+    other = sec.copy()
+    other[hdr_len + 3] ^= 0x5A
+    got2 = dec.router_read_page(9, other, hdr_len, count)
+    assert np.array_equal(got2, pqref.router_read(9, other[hdr_len:].tobytes(), count)[0])
+    h1, m1 = dec.router_cache_stats()
+    assert (h1, m1) == (h0, m0 + 1)
+    with pytest.raises(native.PqgError) as e:  # the run's bytes past the stream: EOF, nothing written
+        dec.router_read_page(9, sec[:hdr_len + 10].copy(), hdr_len, count)
+    assert e.value.code == abi.ERR_EOF

@@ -1,18 +1,17 @@
-"""GPU parity for the speculative-piece walks (round 4): level sections (decode_levels_sp) and
-dictionary-id sections (dict_walk_sp), on hand-built RLE / bit-packed hybrid sections that the
-parquet-mr writer never produces but the reader accepts (RunLengthBitPackingHybridDecoder.readNext,
+"""GPU parity of the window walks (decode_levels_bl for level sections, dict_walk_ls for dictionary
+ids) on hand-built RLE / bit-packed hybrid sections that the parquet-mr writer never produces but the
+reader accepts (RunLengthBitPackingHybridDecoder.readNext,
 parquet-column/.../rle/RunLengthBitPackingHybridDecoder.java:80-109):
 
   * bit-packed runs longer than 63 groups (other writers; runs whose data passes the walk's staged
     bytes), RLE runs of hundreds of thousands of values (one header for a whole page), pages larger
-    than one level image, widths 1..8 for levels and 0..32 for dictionary ids;
-  * the cases the fast path hands back to the window walk: an RLE level value wider than the width
-    (read unmasked), an RLE run of count 0 (the reader repeats its value for the rest of the page),
-    a section that ends before the page's slots / values do.
+    than the walk's LDS segment, widths 1..8 for levels and 0..32 for dictionary ids;
+  * the headers outside the walks' branch-free pre-decode (scalar slow path): an RLE level value wider
+    than the width (read unmasked), an RLE run of count 0 (the reader repeats its value for the rest of
+    the page), a section that ends before the page's slots / values do.
 
 Every case is compared with the oracle (values bit for bit, levels, per-page counts, first error).
-"""
-import numpy as np
+"""import numpy as np
 import pytest
 
 from oracle import pqref
@@ -191,8 +190,8 @@ def test_levels_large_random_page(decoder):
 
 
 @pytest.mark.parametrize("case", ["wide_rle_value", "zero_count_rle", "short_section", "truncated_group"])
-def test_levels_handed_back(decoder, case):
-    """Sections the speculative decoder hands to the window walk: its result (levels, counts, error
+def test_levels_slow_path_headers(decoder, case):
+    """Sections with headers outside the pre-decode's fast path: its result (levels, counts, error
     at the oracle's slot) must be the same."""
     rng = np.random.default_rng(len(case))
     w, max_def = 2, 3
