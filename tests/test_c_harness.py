@@ -577,10 +577,11 @@ def _replay(router_replay, tmp_path, streams, tail):
     return calls, res, stats
 
 
-def _check_replay(streams, calls, res, stats):
+def _check_replay(streams, calls, res, stats, strict=True):
     """Every read's buffer on return == the oracle's ParquetReadRouter.readBatch at that position;
     each stream's values == the oracle's RunLengthBitPackingHybridDecoder; one device round trip per
-    stream that has bit-packed runs."""
+    stream that has bit-packed runs (strict; otherwise at most one: a stream whose first run has the
+    bytes, width, count and distance to the stream end of a cached run is served from the cache)."""
     from oracle import pqref
     for s, pos, cnt, got in calls:
         w, _, sec, _ = streams[s]
@@ -592,7 +593,8 @@ def _check_replay(streams, calls, res, stats):
         assert code == 0 and rc == 0
         assert np.array_equal(got, want), s
     with_packed = len({s for s, _, _, _ in calls})
-    assert stats[1] == with_packed and stats[0] == len(calls) - with_packed
+    assert stats[0] + stats[1] == len(calls)
+    assert stats[1] == with_packed if strict else 1 <= stats[1] <= with_packed
 
 
 @pytest.mark.gpu
@@ -633,7 +635,8 @@ def test_router_replay_nested_fixture(router_replay, tmp_path, tail):
             at += pg.num_values
     assert len(streams) >= 10
     calls, res, stats = _replay(router_replay, tmp_path, streams, tail)
-    _check_replay(streams, calls, res, stats)
+    # (the fixture's two leaves of one repeated group have equal level sections: the second is a hit)
+    _check_replay(streams, calls, res, stats, strict=False)
 
 
 @pytest.mark.gpu

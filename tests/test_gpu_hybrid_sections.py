@@ -11,7 +11,8 @@ parquet-column/.../rle/RunLengthBitPackingHybridDecoder.java:80-109):
     the page), a section that ends before the page's slots / values do.
 
 Every case is compared with the oracle (values bit for bit, levels, per-page counts, first error).
-"""import numpy as np
+"""
+import numpy as np
 import pytest
 
 from oracle import pqref

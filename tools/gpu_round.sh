@@ -71,7 +71,7 @@ PY
         2> "$OUT/bench_c4.err" || { tail -30 "$OUT/bench_c4.err"; exit 1; }
       cat "$OUT/bench_c4.json" ;;
     router)
-      timeout -k 10 120 python3 tools/router_latency.py > "$OUT/router_latency.jsonl" 2> "$OUT/router.err" \
+      timeout -k 10 300 python3 tools/router_latency.py > "$OUT/router_latency.jsonl" 2> "$OUT/router.err" \
         || { tail -20 "$OUT/router.err"; exit 1; }
       cat "$OUT/router_latency.jsonl" ;;
     diag)
