@@ -112,6 +112,31 @@ def pyarrow_baseline(values, budget_s, threads):
             "sample": f"pyarrow {pa.__version__} read_table of the same 100M values (its own pages), {reps} reps"}
 
 
+def link_ceiling(out_bytes, in_bytes, device, reps=5):
+    """The PCIe link alone on this box: one pinned hipMemcpyAsync of the decoded column's size
+    (device -> host) and of the encoded pages' size (host -> device), best of `reps`, in GB/s."""
+    import torch
+    res = {}
+    s = torch.cuda.Stream(device)
+    for name, n, d2h in (("d2h_pinned_gbs", out_bytes, True), ("h2d_pinned_gbs", in_bytes, False)):
+        dev_t = torch.empty(n, dtype=torch.uint8, device=device)
+        host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        host.fill_(1)
+        best = None
+        for _ in range(reps):
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            with torch.cuda.stream(s):
+                (host.copy_(dev_t, non_blocking=True) if d2h else dev_t.copy_(host, non_blocking=True))
+            s.synchronize()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        res[name] = n / best / 1e9
+        del dev_t, host
+    res["bytes"] = {"d2h": out_bytes, "h2d": in_bytes}
+    return res
+
+
 def launch_ranks(n):
     """`--gpus N` run without a launcher: start N ranks under torch.distributed.run (one process per
     GPU, rendezvous on 127.0.0.1) as a CHILD process and exit with its code. Nothing here touches
@@ -168,7 +193,9 @@ def run_c4(args, world, rank, devi):
     from tools.synth import writer
 
     t_gen = time.perf_counter()
-    shard = LI.Shard(args.rows, world, rank, args.c4_templates)
+    keep = [int(k) for k in args.c4_cols.split(",")] if args.c4_cols else None
+    shard = LI.Shard(args.rows, world, rank, args.c4_templates, keep=keep)
+    n_keep = len(shard.keep)
     rg_rows, n_rg, T, templates, shards, mine = shard.rg_rows, shard.n_rg, shard.T, shard.templates, shard.shards, shard.mine
     batch, col_of = shard.batch, shard.col_of
     t_gen = time.perf_counter() - t_gen
@@ -259,7 +286,7 @@ def run_c4(args, world, rank, devi):
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, REPO)
         from oracle import pqref
-        b1 = writer.build_batch(templates[0][0])
+        b1 = writer.build_batch([templates[0][0][k] for k in shard.keep])
         t1, reps = time.perf_counter(), 0
         while True:
             r = pqref.decode_batch(b1)
@@ -268,10 +295,10 @@ def run_c4(args, world, rank, devi):
             if time.perf_counter() - t1 >= args.cpu_budget:
                 break
         dt = time.perf_counter() - t1
-        cpu = {"value": reps * rg_rows * 16 / dt, "unit": "values/s", "cores": 1, "kind": "port",
-               "sample": f"{reps} x one 1M-row, 16-column row group, oracle/pqref.c single thread, {dt:.1f} s"}
+        cpu = {"value": reps * rg_rows * n_keep / dt, "unit": "values/s", "cores": 1, "kind": "port",
+               "sample": f"{reps} x one 1M-row, {n_keep}-column row group, oracle/pqref.c single thread, {dt:.1f} s"}
     if rank == 0:
-        value = total_rows * 16 * args.steps / t_max
+        value = total_rows * n_keep * args.steps / t_max
         out = {
             "metric": "decoded values/s, device-resident C4 lineitem 16 columns",
             "value": value, "unit": "values/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -282,7 +309,8 @@ def run_c4(args, world, rank, devi):
                                    "pages of 20,000 values, uncompressed, 1M-row row groups sharded over ranks",
                        "rows_total": int(total_rows), "row_groups_total": n_rg, "row_groups_this_rank": len(mine),
                        "distinct_row_groups": T, "pages_this_rank": batch.n_pages,
-                       "pqg_columns_this_rank": len(batch.columns), "parallelism": f"row-group shard x{world}"},
+                       "pqg_columns_this_rank": len(batch.columns), "parallelism": f"row-group shard x{world}",
+                       "lineitem_columns": shard.keep},
             "gb_per_s": total_bytes * args.steps / t_max / 1e9,
             "hbm_frac_per_gpu": total_bytes * args.steps / t_max / 1e9 / world / HBM_PEAK_GBS,
             "kernels_per_launch": plan.kernel_count,
@@ -315,6 +343,8 @@ def main():
                     help="c2: the headline (BASELINE metric); c4: lineitem 16 columns, strong scaling")
     ap.add_argument("--rows", type=int, default=None, help="c2: rows per GPU (100M); c4: rows in total (1B)")
     ap.add_argument("--c4-templates", type=int, default=4, help="c4: distinct synthetic row groups")
+    ap.add_argument("--c4-cols", default=None,
+                    help="c4 diagnostics: comma-separated lineitem columns to decode (default: all 16)")
     ap.add_argument("--zipf", type=float, default=1.5)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -436,7 +466,12 @@ def main():
             native_s.append(dec.last_native_s)
             assert rc2 == 0
         e2e_s = min(native_s)
+        link = link_ceiling(n * 8, data_bytes, dec.device)
+        # the link's share of the host path: the output's D2H at the measured pinned ceiling
+        d2h_floor_s = n * 8 / (link["d2h_pinned_gbs"] * 1e9)
         e2e = {"values_per_s": n / e2e_s, "seconds": e2e_s, "native_call_s": native_s,
+               "output_gb_per_s": n * 8 / e2e_s / 1e9, "link": link,
+               "frac_of_d2h_ceiling": d2h_floor_s / e2e_s,
                "with_python_alloc_s": times,
                "path": "pqg_decode_host (one C call: host page bytes -> pinned -> H2D, plan, decode, sync, "
                        "chunked D2H -> caller's int64 array); output array allocated and touched beforehand"}

@@ -99,7 +99,10 @@ size_t err_region_bytes(int n_pages, int n_cols) {
 //   C_IDS   dictionary pages whose values are not 4 / 8 bytes (BYTE_ARRAY, FLBA, INT96): ids first
 //   C_BINP  PLAIN BYTE_ARRAY          C_DLBA  DELTA_LENGTH_BYTE_ARRAY      C_BSS  BYTE_STREAM_SPLIT
 //   C_DBA   DELTA_BYTE_ARRAY (lengths here; values by k_dba_copy after the offset scan)
-enum Cls { C_DICT4 = 0, C_DICT8, C_IDS, C_PLAIN, C_BOOL, C_DELTA4, C_DELTA8, C_BSS, C_BINP, C_DLBA, C_DBA, C_RLEBOOL, C_NCLS };
+//   C_DD    dictionary pages of dictionary-direct BYTE_ARRAY columns (ColumnDev::dict_direct): walk + chunk
+//           byte sums, per-column scan, offsets + value bytes (launch_dict_dd), no ids stored
+enum Cls { C_DICT4 = 0, C_DICT8, C_IDS, C_PLAIN, C_BOOL, C_DELTA4, C_DELTA8, C_BSS, C_BINP, C_DLBA, C_DBA, C_RLEBOOL, C_DD,
+           C_NCLS };
 constexpr int N_DICT_CLS = 3;  // C_DICT4, C_DICT8, C_IDS: run-record walk + chunk expansion
 
 struct HostErr {
@@ -124,6 +127,12 @@ struct pqg_plan {
   uint32_t err_epoch = pqg::ERR_EPOCH_MAX;  // error-word epoch of the last launch (first launch wraps: zeroes the region)
   bool dict_fused = true;
   uint32_t chunk_off[N_DICT_CLS] = {0, 0, 0}, chunk_n[N_DICT_CLS] = {0, 0, 0};  // ranges in `chunks`
+  // C_DD: its chunks in `chunks` (per column in page order, each column's first at a multiple of 4:
+  // padding entries of page 0xFFFFFFFF between columns), the per-chunk byte sums / first bytes in
+  // bscratch, the columns and their chunk ranges in bin_lists, the LDS of the staged dictionaries
+  uint32_t dd_chunk_off = 0, dd_chunk_n = 0, dd_region = 16;
+  uint64_t dd_sums_off = ~0ull;
+  int n_dd_cols = 0, off_dd_cols = 0, off_dd_start = 0;
   // fused dictionary kernel: persistent walker / tile workgroup counts (0: one page / 4 chunks per WG)
   // BYTE_ARRAY / fixed-width-dictionary scratch (ColumnDev::blen, bsrc, dict_len, dict_src, block_sums,
   // bin_total), dictionary walks, post-passes, offset-scan blocks, copy chunks
@@ -158,7 +167,6 @@ struct pqg_plan {
   // hold those columns' entries last, so plain_fused launches skip them (pqg_sync turns plain_fused
   // off when a page's values do not fill its data section)
   bool plain_fused = false;
-  uint32_t dd_dict_bytes = 0;  // largest dictionary-direct dictionary page (the offset scan stages it)
   bool plain_pg = false;  // ... through k_bin_plain_pg (one wave per page) instead of the tiles
   int n_pcp = 0;          // pages of those columns (pcol_pages)
   int plain_fallbacks = 0;
@@ -356,7 +364,8 @@ static int count_kernels(const pqg_plan* P) {
   int k = (P->levels_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
   for (int c = 0; c < C_NCLS; c++) {
     const int n = P->cls_n[(size_t)c] - (c == C_BINP ? P->n_binp_seg + (pf ? P->n_binp_fused : 0) : 0);
-    if (n) k += (c == C_DICT4 || c == C_DICT8 || c == C_IDS) && !P->dict_fused ? 2 : 1;
+    if (n && c == C_DD) k += P->dict_fused ? 3 : 4;
+    else if (n) k += (c == C_DICT4 || c == C_DICT8 || c == C_IDS) && !P->dict_fused ? 2 : 1;
   }
   k += (P->n_dict_walk ? 1 : 0) + (P->n_bind ? 1 : 0) + (P->n_fixd ? 1 : 0) +
        ((pf ? P->n_bin_blocks_nf : P->n_bin_blocks) ? 3 : 0) + ((pf ? P->n_bin_chunks_nf : P->n_bin_chunks) ? 1 : 0) +
@@ -609,6 +618,30 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       pcs.push_back((int32_t)pcp.size());
     }
   }
+  // dictionary-direct BYTE_ARRAY columns (ColumnDev::dict_direct): required, every data page
+  // dictionary-encoded, the dictionary page small enough to stage (DD_DICT_MAX bytes, at most 2,048
+  // entries): their pages leave C_IDS for C_DD (no ids stored, no offset scan or copy of their own)
+  std::vector<uint8_t> dict_direct((size_t)std::max(n_cols, 1), 0);
+  {
+    std::vector<int> npg((size_t)std::max(n_cols, 1), 0), nids((size_t)std::max(n_cols, 1), 0);
+    for (int p = 0; p < n_pages; p++) {
+      const int c = P->h_work[(size_t)p].column;
+      npg[(size_t)c]++;
+      if (P->page_cls[(size_t)p] == C_IDS) nids[(size_t)c]++;
+    }
+    for (int i = 0; i < n_cols; i++)
+      dict_direct[(size_t)i] = cols[i].physical_type == PQG_BYTE_ARRAY && bin_out(cols[i]) && !ids_mode(cols[i]) &&
+                               !col_err[(size_t)i] && !dba_fixed[(size_t)i] && !plain_col[(size_t)i] &&
+                               cols[i].max_def == 0 && cols[i].max_rep == 0 && cols[i].dict_offset >= 0 &&
+                               cols[i].dict_size <= pqg::DD_DICT_MAX && cols[i].dict_num_values <= 2048 &&
+                               npg[(size_t)i] > 0 && nids[(size_t)i] == npg[(size_t)i] && ctx->dict_direct;
+    std::vector<int> keep, dd;
+    for (int p : cls_lists[C_IDS]) (dict_direct[(size_t)P->h_work[(size_t)p].column] ? dd : keep).push_back(p);
+    std::stable_sort(dd.begin(), dd.end(), [&](int a, int b) { return P->h_work[(size_t)a].column < P->h_work[(size_t)b].column; });
+    for (int p : dd) P->page_cls[(size_t)p] = C_DD;
+    cls_lists[C_IDS].swap(keep);
+    cls_lists[C_DD].swap(dd);
+  }
   // PLAIN BYTE_ARRAY pages walked in segments when there are few of them (k_bin_walk_seg)
   std::vector<uint64_t> segs;
   std::vector<uint8_t> seg_page((size_t)std::max(n_pages, 1), 0);
@@ -627,7 +660,8 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   // while they take the one-pass path)
   for (int pass = 0; pass < 2; pass++) {
     for (int i = 0; i < n_cols; i++) {
-      if (ids_mode(cols[i]) || (plain_col[(size_t)i] != 0) != (pass == 1)) continue;  // ids go straight to the values
+      if (ids_mode(cols[i]) || dict_direct[(size_t)i] || (plain_col[(size_t)i] != 0) != (pass == 1))
+        continue;  // ids go straight to the values; dictionary-direct columns store none
       if (bin_out(cols[i]) || needs_ids[(size_t)i] || dba_fixed[(size_t)i])
         blen_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
     }
@@ -648,8 +682,15 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   for (int i0 = 0; i0 < 2 * n_cols; i0++) {  // the one-pass columns last
     const int i = i0 % n_cols;
     if (!bin_out(cols[i]) || (plain_col[(size_t)i] != 0) != (i0 >= n_cols)) continue;
-    bin_cols.push_back(i);
     P->bin_capacity[(size_t)i] = cols[i].binary_capacity;
+    if (dict_direct[(size_t)i]) {  // the byte total (k_dd_bases) and the dictionary's entries only
+      P->bin_total_off[(size_t)i] = take(8);
+      dict_walk.push_back(i);
+      dlen_off[(size_t)i] = take(4 * ((uint64_t)cols[i].dict_num_values + 1));
+      dsrc_off[(size_t)i] = take(4 * ((uint64_t)cols[i].dict_num_values + 1));
+      continue;
+    }
+    bin_cols.push_back(i);
     bsrc_off[(size_t)i] = take(4 * (slot_acc[(size_t)i] + 1));
     const uint64_t nb = (slot_acc[(size_t)i] + pqg::SCAN_BLOCK - 1) / pqg::SCAN_BLOCK;
     bsum_off[(size_t)i] = take(8 * (nb + 1));
@@ -669,23 +710,6 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     uint32_t nb = 0;
     for (uint64_t b : bin_blocks) nb += plain_col[(size_t)(b >> 32)] ? 0 : 1;
     P->n_bin_blocks_nf = nb;
-  }
-  // dictionary-direct BYTE_ARRAY columns (ColumnDev::dict_direct): required, every data page
-  // dictionary-encoded, the dictionary page small enough to stage in the offset scan
-  std::vector<uint8_t> dict_direct((size_t)std::max(n_cols, 1), 0);
-  {
-    std::vector<int> npg((size_t)std::max(n_cols, 1), 0), nids((size_t)std::max(n_cols, 1), 0);
-    for (int p = 0; p < n_pages; p++) {
-      const int c = P->h_work[(size_t)p].column;
-      npg[(size_t)c]++;
-      if (P->page_cls[(size_t)p] == C_IDS) nids[(size_t)c]++;
-    }
-    for (int i = 0; i < n_cols; i++)
-      dict_direct[(size_t)i] = cols[i].physical_type == PQG_BYTE_ARRAY && bin_out(cols[i]) && !ids_mode(cols[i]) &&
-                               !col_err[(size_t)i] && !dba_fixed[(size_t)i] && !plain_col[(size_t)i] &&
-                               cols[i].max_def == 0 && cols[i].max_rep == 0 && cols[i].dict_offset >= 0 &&
-                               cols[i].dict_size <= pqg::DD_DICT_MAX && npg[(size_t)i] > 0 &&
-                               nids[(size_t)i] == npg[(size_t)i] && ctx->dict_direct;
   }
   std::vector<uint64_t> plain_chunks;  // copy chunks of the one-pass columns (per-value fallback only)
   for (int k : {C_IDS, C_BINP, C_DLBA})
@@ -752,6 +776,34 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     }
     P->chunk_n[k - C_DICT4] = (uint32_t)chunk_list.size() - P->chunk_off[k - C_DICT4];
   }
+  std::vector<int32_t> dd_cols, dd_start;
+  P->dd_chunk_off = (uint32_t)chunk_list.size();
+  for (int p : cls_lists[C_DD]) {  // (sorted by column)
+    PageWork& w = P->h_work[(size_t)p];
+    if (dd_cols.empty() || dd_cols.back() != w.column) {  // dd_start: [begin, end) of each column's chunks
+      if (!dd_cols.empty()) dd_start.push_back((int32_t)(chunk_list.size() - P->dd_chunk_off));
+      while ((chunk_list.size() - P->dd_chunk_off) % (uint32_t)pqg::DICT_WPB) {  // whole workgroups per column
+        chunk_list.push_back(0xFFFFFFFFull);
+        chunk_total++;
+      }
+      dd_cols.push_back(w.column);
+      dd_start.push_back((int32_t)(chunk_list.size() - P->dd_chunk_off));
+      const pqg_column_desc& cc = cols[w.column];
+      P->dd_region = std::max<uint32_t>(P->dd_region, (uint32_t)(((uint64_t)cc.dict_size + 15u) & ~15ull) +
+                                                          4u * (uint32_t)cc.dict_num_values);
+    }
+    const uint32_t ch = pqg::dict_chunk_values(4);
+    w.rec_base = rec_total;
+    rec_total += (uint64_t)std::min<uint32_t>(w.num_slots, w.size) + 1;
+    w.chunk_base = chunk_total;
+    const uint32_t nch = (uint32_t)(((uint64_t)w.num_slots + 3u + ch - 1) / ch);
+    for (uint32_t j = 0; j < nch; j++) chunk_list.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
+    chunk_total += nch;
+  }
+  if (!dd_cols.empty()) dd_start.push_back((int32_t)(chunk_list.size() - P->dd_chunk_off));
+  P->dd_chunk_n = (uint32_t)chunk_list.size() - P->dd_chunk_off;
+  P->n_dd_cols = (int)dd_cols.size();
+  if (P->dd_chunk_n) P->dd_sums_off = take(8 * (uint64_t)P->dd_chunk_n);
   // ---- flatten lists: [levels][class 0]...[class n]
   std::vector<int32_t> flat(lvl_list.begin(), lvl_list.end());
   P->levels_off = 0;
@@ -778,6 +830,8 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   P->off_fixd = (int)bl.size(); P->n_fixd = (int)fixd.size(); bl.insert(bl.end(), fixd.begin(), fixd.end());
   P->off_bin_cols = (int)bl.size(); P->n_bin_cols = (int)bin_cols.size(); bl.insert(bl.end(), bin_cols.begin(), bin_cols.end());
   P->off_carry = (int)bl.size(); P->n_carry = (int)carry_cols.size(); bl.insert(bl.end(), carry_cols.begin(), carry_cols.end());
+  P->off_dd_cols = (int)bl.size(); bl.insert(bl.end(), dd_cols.begin(), dd_cols.end());
+  P->off_dd_start = (int)bl.size(); bl.insert(bl.end(), dd_start.begin(), dd_start.end());
   P->n_bin_blocks = (uint32_t)bin_blocks.size();
   P->n_bin_chunks = (uint32_t)bin_chunks.size();
   // ---- upload
@@ -818,7 +872,6 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       d.bin_total = (uint64_t*)at(P->bin_total_off[(size_t)i]);
       d.n_slots = slot_acc[(size_t)i];
       d.dict_direct = dict_direct[(size_t)i];
-      if (dict_direct[(size_t)i]) P->dd_dict_bytes = std::max<uint32_t>(P->dd_dict_bytes, std::max<uint32_t>((uint32_t)cols[i].dict_size, 16u));
       if (dba_fixed[(size_t)i]) {  // DELTA_BYTE_ARRAY values go straight to the fixed-width output
         d.binary_data = (uint8_t*)cols[i].values;
         d.binary_capacity = slot_acc[(size_t)i] * (uint64_t)d.elem_width;
@@ -922,7 +975,7 @@ int pqg_plan_launch(pqg_plan* P) {
   bool fork = false, fork_bin = false, fork_fix = false;
   const bool has_fixed = P->cls_n[C_DICT4] || P->cls_n[C_DICT8] || P->cls_n[C_PLAIN] || P->cls_n[C_BOOL] ||
                          P->cls_n[C_RLEBOOL] || P->cls_n[C_DELTA4] || P->cls_n[C_DELTA8] || P->cls_n[C_BSS];
-  const bool has_bin = P->n_dict_walk || P->cls_n[C_IDS] || P->cls_n[C_BINP] - P->n_binp_seg - (pf ? P->n_binp_fused : 0) > 0 ||
+  const bool has_bin = P->n_dict_walk || P->cls_n[C_IDS] || P->cls_n[C_DD] || P->cls_n[C_BINP] - P->n_binp_seg - (pf ? P->n_binp_fused : 0) > 0 ||
                        P->cls_n[C_DLBA] || P->cls_n[C_DBA] || P->n_segs;
   const bool want = e == hipSuccess && ((pf && (has_fixed || has_bin)) || (has_bin && has_fixed));
   const bool ev_ok = want && (ctx->ev_fork || hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) == hipSuccess) &&
@@ -975,6 +1028,13 @@ int pqg_plan_launch(pqg_plan* P) {
                                  P->chunk_n[i], (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused, err, ecount);
         break;
       }
+      case C_DD:
+        e = pqg::launch_dict_dd(sb, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
+                                (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->dd_chunk_off, P->dd_chunk_n,
+                                (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused, err, ecount,
+                                (uint64_t*)((uint8_t*)P->bscratch.p + P->dd_sums_off), bl + P->off_dd_cols,
+                                bl + P->off_dd_start, P->n_dd_cols, P->dd_region);
+        break;
       case C_BSS: e = pqg::launch_bss(sf, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_BINP:
         e = pqg::launch_bin_walk(sb, P->d_bytes, P->n_bytes, work, cols, l, n, 0, P->n_pages, err, ecount);
@@ -1007,7 +1067,7 @@ int pqg_plan_launch(pqg_plan* P) {
   const uint32_t n_blocks = pf ? P->n_bin_blocks_nf : P->n_bin_blocks;
   if (e == hipSuccess && n_blocks)
     e = pqg::launch_bin_scan(sb, P->d_bytes, P->n_bytes, cols, bl + P->off_bin_cols, pf ? P->n_bin_cols_nf : P->n_bin_cols,
-                             (const uint64_t*)P->bin_blocks.p, n_blocks, P->dd_dict_bytes);
+                             (const uint64_t*)P->bin_blocks.p, n_blocks);
   const uint32_t n_chunks = pf ? P->n_bin_chunks_nf : P->n_bin_chunks;
   if (e == hipSuccess && n_chunks)
     e = pqg::launch_bin_copy(sb, P->d_bytes, P->n_bytes, work, cols, (const uint64_t*)P->bin_chunks.p, n_chunks, err,
@@ -1197,7 +1257,7 @@ int sync_plan(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work) {
   // BYTE_ARRAY segment walk that timed out waiting for its predecessor reaches the caller)
   const int tpage = st ? (int)st->page : -1;
   const int tcls = tpage >= 0 && tpage < P->n_pages ? P->page_cls[(size_t)tpage] : -1;
-  if (rc == PQG_ERR_TIMEOUT && P->dict_fused && (tcls == C_DICT4 || tcls == C_DICT8 || tcls == C_IDS)) {
+  if (rc == PQG_ERR_TIMEOUT && P->dict_fused && (tcls == C_DICT4 || tcls == C_DICT8 || tcls == C_IDS || tcls == C_DD)) {
     // The fused dictionary kernel's hand-off relies on the walker workgroups being dispatched before
     // the expansion workgroups that wait for them, which HIP does not promise. A launch in which an
     // expansion waited past SPIN_TIMEOUT_TICKS (it then stops and reports PQG_ERR_TIMEOUT; the walkers

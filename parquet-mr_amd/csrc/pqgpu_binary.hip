@@ -599,27 +599,6 @@ __device__ __forceinline__ uint32_t img4(const uint32_t* img, uint32_t i) {
   return *(const u32u*)((const uint8_t*)img + i);
 }
 
-// Store the 16-byte output block at `a` (dwords wd) clipped to [o_lo, o_hi): one 16-byte store
-// when the block is whole and aligned, dword stores for whole dwords, byte stores at the edges
-// (which neighbouring chunks / pages share). have: bit q = dword q whole (0 for an unaligned dst).
-__device__ __forceinline__ void store_block16(uint8_t* dst, uint64_t a, uint64_t o_lo, uint64_t o_hi,
-                                              const uint32_t (&wd)[4], uint32_t have, bool dst_al16) {
-  if (have == 0xFu && dst_al16) {
-    gst_nt((u32x4*)(dst + a), u32x4{wd[0], wd[1], wd[2], wd[3]});
-    return;
-  }
-#pragma unroll
-  for (uint32_t q = 0; q < 4; q++) {
-    const uint64_t d0 = a + 4u * q;
-    if ((have >> q) & 1u) {
-      gst((uint32_t*)(dst + d0), wd[q]);
-    } else {
-      for (uint32_t j = 0; j < 4; j++)
-        if (d0 + j >= o_lo && d0 + j < o_hi) gst(dst + d0 + j, (uint8_t)(wd[q] >> (8u * j)));
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Offsets of BYTE_ARRAY columns: exclusive scan of blen over [0, n_slots) (entries past the
 // column's decoded values hold 0: blen is cleared before every launch), written as int64
@@ -648,15 +627,6 @@ __device__ __forceinline__ u32x4 scan_row_load(const uint32_t* blen, uint64_t n_
   return x;
 }
 
-// dict_direct columns: blen holds dictionary ids; the length of value id (0 for an invalid id, which
-// the dictionary kernel reported, as k_bin_dict_map maps it)
-__device__ __forceinline__ u32x4 dd_lengths(const ColumnDev& cd, u32x4 id, uint32_t dn, uint64_t v, uint64_t n_slots) {
-  u32x4 l;
-#pragma unroll
-  for (int k = 0; k < 4; k++) l[k] = id[k] < dn && v + k < n_slots ? cd.dict_len[id[k]] : 0u;
-  return l;
-}
-
 __global__ __launch_bounds__(256) void k_bin_block_sums(const ColumnDev* __restrict__ cols,
                                                         const uint64_t* __restrict__ blocks) {
   __shared__ uint64_t red[4];
@@ -666,11 +636,6 @@ __global__ __launch_bounds__(256) void k_bin_block_sums(const ColumnDev* __restr
   u32x4 x[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) x[i] = scan_row_load(cd.blen, cd.n_slots, v0 + 1024u * i + 4u * threadIdx.x);
-  if (uni(cd.dict_direct)) {
-    const uint32_t dn = uni(cd.dict_n);
-#pragma unroll
-    for (int i = 0; i < 4; i++) x[i] = dd_lengths(cd, x[i], dn, v0 + 1024u * i + 4u * threadIdx.x, cd.n_slots);
-  }
   uint64_t s = 0;
 #pragma unroll
   for (int i = 0; i < 4; i++) s += (uint64_t)x[i][0] + x[i][1] + (uint64_t)x[i][2] + x[i][3];
@@ -724,118 +689,20 @@ __global__ __launch_bounds__(256) void k_bin_block_bases(const ColumnDev* __rest
 // Offsets of one scan block: per row, a wave scan of the threads' 4-length sums and the wave
 // totals through LDS (4 rows scanned side by side: one barrier per block instead of two per
 // 256 lengths); offsets stored as two 16-byte stores per row and thread.
-// dict_direct: the dictionary page staged once per workgroup, then per row each wave builds an output
-// image of its 256 values' bytes in its own LDS image (whole dwords as unaligned 4-byte writes, the
-// last 1-3 bytes of a value as a 2- and a 1-byte write, so no write leaves the value's own bytes) and
-// stores it as 16-byte blocks: no workgroup barrier per row (the wave's bytes are contiguous; the
-// blocks it shares with its neighbours at both ends are stored byte-exact); a quarter row whose bytes
-// exceed the image is written with byte stores
-constexpr uint32_t DD_WIMG = 6144;  // output image per wave (a quarter row: 256 values of up to 24 bytes)
-struct DictDirectLds {
-  uint32_t img[WPB][DD_WIMG / 4 + 4];
-  uint32_t dict[DD_DICT_MAX / 4 + 4];  // (the launch allocates only the plan's largest dictionary)
-};
-constexpr uint32_t DD_LDS_FIXED = sizeof(uint32_t) * WPB * (DD_WIMG / 4 + 4);
-
-// lens / srcs: the thread's 4 values' entry lengths and offsets in the dictionary page (gathered
-// before the offset stores: a load issued after them would wait for them, vmcnt counts stores);
-// e: output offset of the thread's first value; [o_lo, o_hi): the wave's bytes (clipped to the
-// capacity), w_hi: their unclipped end
-__device__ __noinline__ void dd_wave_bytes(const ColumnDev& cd, const uint32_t* dict, uint32_t* img, u32x4 lens,
-                                           u32x4 srcs, uint64_t e, uint64_t o_lo, uint64_t o_hi, uint64_t w_hi) {
-  typedef uint16_t __attribute__((aligned(1), may_alias)) u16u;
-  typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
-  uint8_t* dst = cd.binary_data;
-  const uint32_t dbytes = (uint32_t)cd.dict_bytes;
-  const uint64_t a0 = o_lo & ~15ull;
-  const bool in_img = w_hi - a0 + 16u <= DD_WIMG;
-  uint8_t* outb = (uint8_t*)img;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const uint32_t sp = srcs[k], len = lens[k];
-    if (in_img) {
-      uint8_t* ob = outb + (e - a0);
-      uint32_t j = 0;
-      for (; j + 4u <= len; j += 4u) *(u32u*)(ob + j) = img4(dict, sp + j);
-      if (j < len) {  // 1-3 bytes left (bytes past the dictionary page: never part of an entry)
-        const uint32_t w = sp + j < dbytes ? img4(dict, sp + j) : 0u;
-        const uint32_t r = len - j;
-        if (r & 2u) *(u16u*)(ob + j) = (uint16_t)w;
-        if (r & 1u) ob[j + (r & 2u)] = (uint8_t)(w >> (8u * (r & 2u)));
-      }
-    } else {
-      for (uint32_t j = 0; j < len; j += 4u) {
-        const uint32_t w = sp + j < dbytes ? img4(dict, sp + j) : 0u;
-#pragma unroll
-        for (uint32_t q = 0; q < 4u; q++) {
-          const uint64_t o = e + j + q;
-          if (j + q < len && o < o_hi) gst(dst + o, (uint8_t)(w >> (8u * q)));
-        }
-      }
-    }
-    e += len;
-  }
-  if (!in_img) return;
-  wave_sync();
-  const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
-  const uint32_t r_lo = (uint32_t)(o_lo - a0), r_hi = (uint32_t)(o_hi - a0);
-  for (uint32_t bb = 16u * lane_id(); bb < r_hi; bb += 16u * WAVE) {
-    const u32x4 v4 = *(const u32x4*)(outb + bb);
-    uint32_t wd[4] = {v4.x, v4.y, v4.z, v4.w};
-    uint32_t have = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < 4; q++) {
-      const uint32_t d0 = bb + 4u * q;
-      if (d0 >= r_lo && d0 + 4u <= r_hi) have |= 1u << q;
-    }
-    if (!dst_al4) have = 0;
-    store_block16(dst, a0 + bb, o_lo, o_hi, wd, have, dst_al16);
-  }
-  wave_sync();  // the image is reused by the next row
-}
-
 __global__ __launch_bounds__(256) void k_bin_offsets(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                      const ColumnDev* __restrict__ cols,
                                                      const uint64_t* __restrict__ blocks) {
   __shared__ uint64_t wsum[4][4];  // [row][wave]
-  // dict_direct staging: dynamic LDS, allocated only by launches of plans with dictionary-direct
-  // columns (the other offset scans keep the occupancy of ~0.2 KiB of LDS per workgroup)
-  extern __shared__ __attribute__((aligned(16))) uint8_t dd_lds[];
-  DictDirectLds& D = *(DictDirectLds*)dd_lds;
   const uint64_t b = blocks[blockIdx.x];
   const ColumnDev& cd = cols[(uint32_t)(b >> 32)];
   const uint64_t v0 = (uint64_t)(uint32_t)b * SCAN_BLOCK;
   const uint64_t n_slots = cd.n_slots;
   int64_t* off = (int64_t*)cd.values;
   const uint32_t t = threadIdx.x, wv = t >> 6, lane = lane_id();
-  const bool dd = uni(cd.dict_direct) != 0;
-  u32x4 x[4], ids[4];
-  uint64_t inc[4], first[4], last[4];
+  u32x4 x[4];
+  uint64_t inc[4];
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    x[i] = scan_row_load(cd.blen, n_slots, v0 + 1024u * i + 4u * t);
-    ids[i] = x[i];
-  }
-  if (dd) {
-    const uint32_t dn = uni(cd.dict_n);
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const uint64_t v = v0 + 1024u * i + 4u * t;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const bool ok = ids[i][k] < dn && v + k < n_slots;
-        x[i][k] = ok ? cd.dict_len[ids[i][k]] : 0u;
-        ids[i][k] = ok ? cd.dict_src[ids[i][k]] : 0u;  // from here on: the entry's offset in the page
-      }
-    }
-    // stage the dictionary page (a resource over the rest of the batch: a 16-byte load that crosses
-    // the end of its range returns 0 as a whole, which would drop the page's last bytes; only entry
-    // bytes are ever read from the staged page)
-    const rsrc_t drs = make_rsrc(bytes + cd.dict_offset, n_bytes - cd.dict_offset);
-    const uint32_t nd = (uint32_t)((cd.dict_bytes + 15u) & ~15ull);
-    for (uint32_t o = 16u * t; o < nd; o += 16u * 256u)
-      *(u32x4*)&D.dict[o >> 2] = __builtin_amdgcn_raw_buffer_load_b128(drs, (int)o, 0, 0);
-  }
+  for (int i = 0; i < 4; i++) x[i] = scan_row_load(cd.blen, n_slots, v0 + 1024u * i + 4u * t);
 #pragma unroll
   for (int i = 0; i < 4; i++) inc[i] = (uint64_t)x[i][0] + x[i][1] + (uint64_t)x[i][2] + x[i][3];
 #pragma unroll
@@ -880,19 +747,6 @@ __global__ __launch_bounds__(256) void k_bin_offsets(const uint8_t* __restrict__
     // the final offset (the column's byte total) after the last slot
     if (v < n_slots && n_slots <= v + 4) gst(off + n_slots, (int64_t)(n_slots - v == 1 ? e1 : n_slots - v == 2 ? e2
                                                                      : n_slots - v == 3 ? e3 : e4));
-    first[i] = e0;
-    last[i] = e4;
-  }
-  if (!dd) return;
-  // ---- value bytes of the block: each wave its quarter of every row (values past n_slots have length 0)
-  __syncthreads();  // the staged dictionary
-  const uint64_t cap = cd.binary_capacity;
-#pragma unroll 1
-  for (int i = 0; i < 4; i++) {
-    const uint64_t w_lo = ((uint64_t)rdl((uint32_t)(first[i] >> 32), 0) << 32) | rdl((uint32_t)first[i], 0);
-    const uint64_t w_hi = ((uint64_t)rdl((uint32_t)(last[i] >> 32), 63) << 32) | rdl((uint32_t)last[i], 63);
-    const uint64_t o_hi = w_hi < cap ? w_hi : cap;  // overflow: reported at sync
-    if (w_lo < o_hi) dd_wave_bytes(cd, D.dict, D.img[wv], x[i], ids[i], first[i], w_lo, o_hi, w_hi);
   }
 }
 
@@ -2730,14 +2584,11 @@ hipError_t launch_gather_fixed(hipStream_t st, const uint8_t* bytes, uint64_t n_
 }
 
 hipError_t launch_bin_scan(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, const ColumnDev* cols,
-                           const int32_t* bin_cols, int n_bin_cols, const uint64_t* blocks, uint32_t n_blocks,
-                           uint32_t dd_dict_bytes) {
+                           const int32_t* bin_cols, int n_bin_cols, const uint64_t* blocks, uint32_t n_blocks) {
   if (n_bin_cols <= 0 || n_blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_bin_block_sums, dim3(n_blocks), dim3(256), 0, st, cols, blocks);
   hipLaunchKernelGGL(k_bin_block_bases, dim3(n_bin_cols), dim3(256), 0, st, cols, bin_cols);
-  // dynamic LDS: the wave images and the plan's largest dictionary-direct dictionary (none: 0 bytes)
-  const uint32_t dyn = dd_dict_bytes ? DD_LDS_FIXED + ((dd_dict_bytes + 15u) & ~15u) + 16u : 0u;
-  hipLaunchKernelGGL(k_bin_offsets, dim3(n_blocks), dim3(256), dyn, st, bytes, n_bytes, cols, blocks);
+  hipLaunchKernelGGL(k_bin_offsets, dim3(n_blocks), dim3(256), 0, st, bytes, n_bytes, cols, blocks);
   return hipGetLastError();
 }
 

@@ -143,6 +143,27 @@ __device__ __forceinline__ void gst_nt(T* p, T v) {
   PQG_STORE_GUARD __builtin_nontemporal_store(v, (__attribute__((address_space(1))) T*)p);
 }
 
+// Store the 16-byte output block at `a` (dwords wd) clipped to [o_lo, o_hi): one 16-byte store
+// when the block is whole and aligned, dword stores for whole dwords, byte stores at the edges
+// (which neighbouring chunks / pages share). have: bit q = dword q whole (0 for an unaligned dst).
+__device__ __forceinline__ void store_block16(uint8_t* dst, uint64_t a, uint64_t o_lo, uint64_t o_hi,
+                                              const uint32_t (&wd)[4], uint32_t have, bool dst_al16) {
+  if (have == 0xFu && dst_al16) {
+    gst_nt((u32x4*)(dst + a), u32x4{wd[0], wd[1], wd[2], wd[3]});
+    return;
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    const uint64_t d0 = a + 4u * q;
+    if ((have >> q) & 1u) {
+      gst((uint32_t*)(dst + d0), wd[q]);
+    } else {
+      for (uint32_t j = 0; j < 4; j++)
+        if (d0 + j >= o_lo && d0 + j < o_hi) gst(dst + d0 + j, (uint8_t)(wd[q] >> (8u * j)));
+    }
+  }
+}
+
 // Run records, chunk entries and page status are produced and consumed inside one launch
 // by the fused dictionary kernel (different CUs, possibly different XCDs, whose L2s are not
 // coherent): they are written and read with system-scope relaxed accesses (sc0 sc1: through

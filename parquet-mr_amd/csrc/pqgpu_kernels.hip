@@ -646,22 +646,53 @@ constexpr uint64_t SPIN_TIMEOUT_TICKS = 200000000ull;  // 2 s of s_memrealtime (
 // IDS: the expansion writes the dictionary ids themselves (u32, into ColumnDev::blen) instead
 // of dictionary values: BYTE_ARRAY / FIXED_LEN_BYTE_ARRAY / INT96 dictionaries, whose values
 // are materialized by later kernels (k_bin_dict_map + k_bin_copy, k_gather_fixed).
-template <int W, bool FUSED, bool IDS = false>
+// DD (dictionary-direct BYTE_ARRAY columns, ColumnDev::dict_direct; IDS, W = 4):
+//   DD_SUMS  the chunk's value bytes: sum of the entry lengths of its ids -> dd[chunk] (no id stores);
+//   DD_STR   offsets and value bytes from the ids, the chunk's first byte at dd[chunk] (the sums
+//            scanned per column by k_dd_bases): int64 offsets as 16-byte stores, the bytes composed
+//            from the staged dictionary page in a per-wave LDS image and stored as 16-byte blocks.
+//   Slots of a page past a walk error (pstat's value count) are empty values (length 0).
+// dd_region (DD_STR): LDS bytes before the run tables: the dictionary page, then one u32 entry per id
+// (source offset << 16 | length); sized per launch (dynamic LDS).
+constexpr int DD_NONE = 0, DD_SUMS = 1, DD_STR = 2;
+constexpr uint32_t DD_IMG = 6144;     // DD_STR: output image per wave (a tile of 256 values of <= 23 bytes)
+constexpr uint32_t DD_ENT_MAX = 2048; // entries of a dictionary page of at most DD_DICT_MAX bytes (4-byte lengths)
+
+// Inclusive prefix sum over the wave (u32) with DPP row shifts / broadcasts; all 64 lanes active.
+__device__ __forceinline__ uint32_t wave_incl_scan_u32_dpp(uint32_t x) {
+#define PQG_DPP_ADD(ctrl, rmask) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, ctrl, rmask, 0xf, true);
+  PQG_DPP_ADD(0x111, 0xf)  // row_shr:1
+  PQG_DPP_ADD(0x112, 0xf)  // row_shr:2
+  PQG_DPP_ADD(0x114, 0xf)  // row_shr:4
+  PQG_DPP_ADD(0x118, 0xf)  // row_shr:8
+  PQG_DPP_ADD(0x142, 0xa)  // row_bcast:15 -> rows 1, 3
+  PQG_DPP_ADD(0x143, 0xc)  // row_bcast:31 -> rows 2, 3
+#undef PQG_DPP_ADD
+  return x;
+}
+
+template <int W, bool FUSED, bool IDS = false, int DD = DD_NONE>
 __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                 const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                 const uint64_t* rec, const uint32_t* chunk_run,
                                                 const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                 const uint64_t* pstat, const uint32_t* flags, uint32_t epoch,
-                                                uint64_t* err, ErrCount err_count, uint8_t* lds, uint32_t group) {
+                                                uint64_t* err, ErrCount err_count, uint8_t* lds, uint32_t group,
+                                                uint64_t* dd = nullptr, uint32_t dd_region = 0) {
   typedef typename DictVal<W>::T T;
+  static_assert(DD == DD_NONE || (IDS && W == 4), "dictionary-direct modes take the ids of a 4-byte expansion");
   constexpr uint32_t E = 16 / W;
   constexpr uint32_t TV = WAVE * E;  // values per tile
   constexpr uint32_t CH = CH_TILES * TV;
+  const uint32_t DL = DD == DD_STR ? dd_region : DICT_LDS_BYTES;  // bytes of the dictionary region
   uint8_t* dict_lds = lds;
-  u32x4* tab = (u32x4*)(lds + DICT_LDS_BYTES) + wave_id() * XT_RUNS;
-  uint8_t* xseg = lds + DICT_LDS_BYTES + WPB * XT_RUNS * 16 + wave_id() * XT_SEG;
+  u32x4* tab = (u32x4*)(lds + DL) + wave_id() * XT_RUNS;
+  uint8_t* xseg = lds + DL + WPB * XT_RUNS * 16 + wave_id() * XT_SEG;
+  uint8_t* img = lds + DL + WPB * (XT_RUNS * 16 + XT_SEG) + wave_id() * (DD_IMG + 16);  // DD_STR
   const uint32_t lane = lane_id();
   const uint32_t c = group * WPB + wave_id();
+  // (a chunk list entry of page 0xFFFFFFFF is padding: the host aligns each dictionary-direct column's
+  // chunks to whole workgroups, so a workgroup's waves share one dictionary)
   const int page = c < n_chunks ? (int)(uint32_t)chunks[c] : -1;
   // the workgroup's dictionary in LDS when its chunks share one that fits
   int* wg_col = (int*)dict_lds;
@@ -728,8 +759,9 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
     }
   } xstamp{rt_x0, &rt_x1, c, c < n_chunks};
 #endif
-  if (c < n_chunks) {
-    cpage = (int)(uint32_t)chunks[c];
+  uint32_t NF = 0;  // DD: the page's values (pstat's N stops at a walk error)
+  if (page >= 0) {
+    cpage = page;
     j = (uint32_t)(chunks[c] >> 32);
     // page / column facts and the page's bit width do not depend on the walk: loaded before the
     // hand-off, so the compiler barrier there does not serialize them behind the flag
@@ -789,9 +821,10 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       pst = uni64(pst);
       k = uni(k);
       N = (uint32_t)(pst >> 32);  // values covered before a walk error
+      NF = DD != DD_NONE ? uni(pw.n_values) : N;
       sh = (uint32_t)(pw.out_offset % (uint64_t)E);
       const uint32_t s_lo = j * CH > sh ? j * CH : sh;
-      const uint32_t s_hi = (j + 1) * CH < N + sh ? (j + 1) * CH : N + sh;
+      const uint32_t s_hi = (j + 1) * CH < NF + sh ? (j + 1) * CH : NF + sh;
       go = s_lo < s_hi;
       v_lo = s_lo - sh;
       v_hi = s_hi - sh;
@@ -805,6 +838,28 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       if (o < need) *(u32x4*)(dict_lds + o) = dreg[r];
     }
   }
+  // DD: the entry table (DD_SUMS: lengths; DD_STR: source << 16 | length, after the staged page)
+  uint32_t dd_ent_off = 0;
+  if constexpr (DD != DD_NONE) {
+    if (same && c0 >= 0) {
+      const ColumnDev& cd0 = cols[c0];
+      const uint32_t dn = uni(cd0.dict_n);
+      const uint32_t pg16 = (uint32_t)((cd0.dict_bytes + 15u) & ~15ull);
+      dd_ent_off = DD == DD_STR ? pg16 : 0u;
+      dict_in_lds = dn <= DD_ENT_MAX && cd0.dict_bytes <= DD_DICT_MAX && (DD == DD_SUMS || pg16 + 4u * dn <= DL);
+      if (dict_in_lds) {
+        uint32_t* ent = (uint32_t*)(dict_lds + dd_ent_off);
+        for (uint32_t i = threadIdx.x; i < dn; i += 64u * WPB)
+          ent[i] = DD == DD_STR ? (cd0.dict_src[i] << 16) | cd0.dict_len[i] : cd0.dict_len[i];
+        if constexpr (DD == DD_STR) {  // (a resource over the rest of the batch: a 16-byte load crossing
+          // the end of its range would return 0 as a whole; only entry bytes are ever read from it)
+          const rsrc_t d0 = make_rsrc(bytes + cd0.dict_offset, n_bytes - cd0.dict_offset);
+          for (uint32_t o = 16u * threadIdx.x; o < pg16; o += 16u * 64u * WPB)
+            *(u32x4*)(dict_lds + o) = __builtin_amdgcn_raw_buffer_load_b128(d0, (int)o, 0, 0);
+        }
+      }
+    }
+  }
   __syncthreads();
   // ---- part 2: the chunk's run tables and tile sweeps
   auto one_chunk = [&]() {
@@ -816,13 +871,140 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
     T* const pag = out_base + (pw.out_offset - sh);  // slot 0 of the page
     const bool out16 = ((uintptr_t)out_base & 15u) == 0;
     const uint32_t wmask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
+    // the walked part of the chunk (DD: slots past a walk error follow as empty values)
+    const uint32_t r_hi = DD != DD_NONE ? (v_hi < N ? v_hi : N) : v_hi;
+    // DD state: DD_SUMS the lane's byte sum; DD_STR the running first byte of the next value, the
+    // output image's 16-byte aligned start (bytes [ia, run_base) are composed, not yet stored) and the
+    // first byte this chunk owns (the block at its start is shared with the previous chunk's wave)
+    uint32_t dd_acc = 0;
+    uint64_t run_base = 0, ia = 0, own_lo = 0, cap = 0;
+    int64_t* opag = nullptr;
+    bool o16 = false;
+    const uint32_t* ent_l = (const uint32_t*)(dict_lds + dd_ent_off);
+    if constexpr (DD == DD_STR) {
+      run_base = uni64(dd[c]);
+      ia = run_base & ~15ull;
+      own_lo = run_base;
+      cap = cd.binary_capacity;
+      opag = (int64_t*)cd.values + (pw.out_offset - sh);
+      o16 = ((uintptr_t)cd.values & 15u) == 0;
+    }
+    // DD: entry of id (DD_SUMS: its length; DD_STR: source << 16 | length); 0 past the dictionary
+    auto dd_entry = [&](uint32_t id) -> uint32_t {
+      if (id >= dict_n) return 0u;
+      if (own_dict) return ent_l[id];
+      return DD == DD_STR ? (cd.dict_src[id] << 16) | cd.dict_len[id] : cd.dict_len[id];
+    };
+
+    // DD_STR: the composed bytes [ia, run_base) that are still in the image (at most one partial block)
+    auto dd_flush = [&]() {
+      const uint64_t lo = own_lo > ia ? own_lo : ia;
+      const uint64_t hi = run_base < cap ? run_base : cap;
+      if (lane < 16u && ia + lane >= lo && ia + lane < hi) gst(cd.binary_data + ia + lane, img[lane]);
+      wave_sync();
+    };
+    // DD_STR: one tile's values (ids v, slots outside [lo_u, hi_u) skipped): offsets, then the bytes
+    auto dd_tile = [&](uint32_t ts, uint32_t lo_u, uint32_t hi_u, const T (&v)[E]) {
+      typedef uint16_t __attribute__((aligned(1), may_alias)) u16u;
+      typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
+      uint32_t ln[E], sr[E], ls = 0;
+  #pragma unroll
+      for (uint32_t e = 0; e < E; e++) {
+        const uint32_t sl = ts + E * lane + e;
+        const uint32_t en = sl >= lo_u && sl < hi_u ? dd_entry((uint32_t)v[e]) : 0u;
+        ln[e] = en & 0xFFFFu;
+        sr[e] = en >> 16;
+        ls += ln[e];
+      }
+      const uint32_t inc = wave_incl_scan_u32_dpp(ls);
+      const uint32_t tot = uni(rdl(inc, WAVE - 1));
+      const uint32_t ex = inc - ls;
+      // offsets (BinaryPlainValuesReader / DictionaryValuesReader.readBytes order: value i starts where
+      // value i - 1 ends)
+      uint64_t o[E];
+      o[0] = run_base + ex;
+  #pragma unroll
+      for (uint32_t e = 1; e < E; e++) o[e] = o[e - 1] + ln[e - 1];
+      int64_t* op = opag + ts + E * lane;
+      if (o16 && ts >= lo_u && ts + TV <= hi_u) {
+        typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+        gst_nt((i64x2*)op, i64x2{(int64_t)o[0], (int64_t)o[1]});
+        gst_nt((i64x2*)(op + 2), i64x2{(int64_t)o[2], (int64_t)o[3]});
+      } else {
+  #pragma unroll
+        for (uint32_t e = 0; e < E; e++)
+          if (ts + E * lane + e >= lo_u && ts + E * lane + e < hi_u) gst(op + e, (int64_t)o[e]);
+      }
+      if (tot == 0) return;
+      uint8_t* const dst = cd.binary_data;
+      const uint64_t end = run_base + tot;
+      const bool dst16 = ((uintptr_t)dst & 15u) == 0, dst4 = ((uintptr_t)dst & 3u) == 0;
+      auto dword_at = [&](uint32_t sp) -> uint32_t {  // 4 dictionary-page bytes at sp
+        return own_dict ? *(const u32u*)(dict_lds + sp) : ld4_any(drs, sp);
+      };
+      if (own_dict && end - ia <= DD_IMG) {
+        // compose: each value's whole dwords as unaligned 4-byte writes, its last 1-3 bytes as a 2- and a
+        // 1-byte write, so no write leaves the value's own bytes (other lanes write around it)
+        uint8_t* ob = img + (uint32_t)(run_base - ia) + ex;
+  #pragma unroll
+        for (uint32_t e = 0; e < E; e++) {
+          uint32_t q = 0;
+          for (; q + 4u <= ln[e]; q += 4u) *(u32u*)(ob + q) = dword_at(sr[e] + q);
+          if (q < ln[e]) {
+            const uint32_t x = dword_at(sr[e] + q), r = ln[e] - q;
+            if (r & 2u) *(u16u*)(ob + q) = (uint16_t)x;
+            if (r & 1u) ob[q + (r & 2u)] = (uint8_t)(x >> (8u * (r & 2u)));
+          }
+          ob += ln[e];
+        }
+        wave_sync();
+        // whole 16-byte blocks go out; the partial last block stays in the image for the next tile
+        const uint32_t nfull = (uint32_t)((end - ia) >> 4);
+        const uint64_t o_hi = end < cap ? end : cap;
+        for (uint32_t bb = lane; bb < nfull; bb += WAVE) {
+          const u32x4 x4 = *(const u32x4*)(img + 16u * bb);
+          const uint32_t wd[4] = {x4.x, x4.y, x4.z, x4.w};
+          const uint64_t a = ia + 16u * bb;
+          uint32_t have = 0;
+  #pragma unroll
+          for (uint32_t q = 0; q < 4; q++) have |= (a + 4u * q >= own_lo && a + 4u * q + 4u <= o_hi ? 1u : 0u) << q;
+          if (!dst4) have = 0;
+          if (a + 16u > own_lo && a < o_hi) store_block16(dst, a, own_lo, o_hi, wd, have, dst16);
+        }
+        const uint32_t tail = (uint32_t)(end - ia) & 15u;
+        uint32_t keep = 0;
+        if (lane < 4u) keep = *(const uint32_t*)(img + 16u * nfull + 4u * lane);
+        wave_sync();
+        if (lane < 4u && tail) *(uint32_t*)(img + 4u * lane) = keep;
+        wave_sync();
+        ia += 16ull * nfull;
+      } else {
+        // the tile's bytes do not fit the image (or the dictionary is not staged): the composed
+        // partial block goes out first, then every lane writes its values' bytes itself
+        dd_flush();
+        uint64_t ob = run_base + ex;
+  #pragma unroll
+        for (uint32_t e = 0; e < E; e++) {
+          for (uint32_t q = 0; q < ln[e]; q += 4u) {
+            const uint32_t x = dword_at(sr[e] + q);
+  #pragma unroll
+            for (uint32_t b = 0; b < 4u; b++)
+              if (q + b < ln[e] && ob + q + b < cap) gst(dst + ob + q + b, (uint8_t)(x >> (8u * b)));
+          }
+          ob += ln[e];
+        }
+        ia = end & ~15ull;
+        own_lo = end;
+      }
+      run_base = end;
+    };
 
     uint32_t b_lo = v_lo;
-    while (true) {
+    while (v_lo < r_hi) {
       k = uni(k);
       b_lo = uni(b_lo);
       // ---- load phase: runs k .. k + n_tab - 1 into the table (entry n_tab: end sentinel)
-      uint32_t n_tab = 0, b_hi = v_hi, px_lo = 0xFFFFFFFFu, px_hi = 0;
+      uint32_t n_tab = 0, b_hi = r_hi, px_lo = 0xFFFFFFFFu, px_hi = 0;
       for (uint32_t t0 = 0; t0 < XT_RUNS; t0 += WAVE) {
         const uint32_t r = k + t0 + lane;
         const bool has = r < n_rec && t0 + lane < XT_RUNS - 1;  // a run of this round
@@ -842,7 +1024,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
                                          : (uint32_t)sld(prec + q63)));
         const uint32_t en_n = __shfl_down(st, 1);
         const uint32_t en = lane == WAVE - 1 ? nx63 : en_n;  // end of this lane's run
-        const bool live = has && st < v_hi;
+        const bool live = has && st < r_hi;
         uint32_t vlo = 0, vhi = 0;
         if (live && !(pl & 0x80000000u)) {
           if (pl < dict_n) {
@@ -860,12 +1042,12 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
         if (live && (pl & 0x80000000u)) {
           const uint32_t e_run = en;
           const uint32_t lo = (pl & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)((st > b_lo ? st : b_lo) - st) * (uint32_t)w) >> 3);
-          const uint32_t hi_v = (e_run < v_hi ? e_run : v_hi);
+          const uint32_t hi_v = (e_run < r_hi ? e_run : r_hi);
           const uint32_t hi = (pl & 0x7FFFFFFFu) + (uint32_t)(((uint64_t)(hi_v > st ? hi_v - st : 0) * (uint32_t)w + 7) >> 3) + 8u;
           px_lo = lo < px_lo ? lo : px_lo;
           px_hi = hi > px_hi ? hi : px_hi;
         }
-        const uint64_t inb = __ballot(has && st < v_hi);
+        const uint64_t inb = __ballot(has && st < r_hi);
         n_tab += (uint32_t)__builtin_popcountll(inb);
         if (!(inb >> 63)) break;  // this batch ends the round
       }
@@ -882,7 +1064,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       // round end: the start of the first run not in the table
       if (n_tab >= XT_RUNS - 1) {
         const u32x4 q = tab[XT_RUNS - 1];
-        b_hi = uni(q.x) < v_hi ? uni(q.x) : v_hi;
+        b_hi = uni(q.x) < r_hi ? uni(q.x) : r_hi;
       }
       bool x_lds = true;
       if (px_hi > px_lo && px_lo >= pre_lo && px_hi <= pre_hi) {
@@ -946,6 +1128,8 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
           if (ci + step < n_tab && tab[ci + step].x <= pe) ci += step;
         u32x4 cq = tab[ci];
         uint32_t ce = tab[ci + 1].x;
+        // the round's slot range, uniform: the whole-tile store test below is a scalar compare
+        const uint32_t lo_u = uni(b_lo + sh), hi_u = uni(b_hi + sh);
         for (uint32_t t = t_beg; t < t_end; t++) {
           t = uni(t);
           const uint32_t ts = t * TV;  // first slot of the tile
@@ -958,42 +1142,74 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
           }
           // elements outside [b_lo, b_hi) are not stored; they are evaluated at a clamped index
           T v[E];
-          v[0] = value(ci, pe, cq);
+          const uint32_t pl = p0 + (E - 1);
+          const uint32_t il = pl < b_lo || pl > 0x7FFFFFFFu ? b_lo : (pl >= b_hi ? b_hi - 1 : pl);
+          // The common tile (C2: runs of ~100 values, 128 per tile): every lane's E elements lie in its
+          // current run and that run is RLE, so each element is the run's value — one wave-uniform test
+          // instead of E divergent run / packed branches, whose exec-mask bookkeeping ran on the scalar
+          // unit (~40 SALU per tile) that the walkers on the CU share.
+          if (!__ballot((cq.y & 0x80000000u) || il >= ce)) {
+            const T rv = (T)(((uint64_t)cq.w << 32) | cq.z);
   #pragma unroll
-          for (uint32_t e = 1; e < E; e++) {
-            const uint32_t x = p0 + e;  // value index of element e (wraps below 0)
-            const uint32_t i = x < b_lo || x > 0x7FFFFFFFu ? b_lo : (x >= b_hi ? b_hi - 1 : x);
-            if (i < ce) {
-              v[e] = value(ci, i, cq);
-            } else {  // the element starts a later run
-              uint32_t cj = ci + 1;
-              while (cj + 1 < n_tab && tab[cj + 1].x <= i) cj++;
-              v[e] = value(cj, i, tab[cj]);
+            for (uint32_t e = 0; e < E; e++) v[e] = rv;
+          } else {
+            v[0] = value(ci, pe, cq);
+  #pragma unroll
+            for (uint32_t e = 1; e < E; e++) {
+              const uint32_t x = p0 + e;  // value index of element e (wraps below 0)
+              const uint32_t i = x < b_lo || x > 0x7FFFFFFFu ? b_lo : (x >= b_hi ? b_hi - 1 : x);
+              if (i < ce) {
+                v[e] = value(ci, i, cq);
+              } else {  // the element starts a later run
+                uint32_t cj = ci + 1;
+                while (cj + 1 < n_tab && tab[cj + 1].x <= i) cj++;
+                v[e] = value(cj, i, tab[cj]);
+              }
             }
           }
-          T* tp = pag + ts + E * lane;
-          if (out16 && ts >= b_lo + sh && ts + TV <= b_hi + sh) {
-            if constexpr (W == 8) {
-              typedef uint64_t v2 __attribute__((ext_vector_type(2)));
-              gst_nt((v2*)tp, v2{v[0], v[1]});
-            } else {
-              gst_nt((u32x4*)tp, u32x4{v[0], v[1], v[2], v[3]});
-            }
-          } else {
+          if constexpr (DD == DD_SUMS) {
   #pragma unroll
-            for (uint32_t e = 0; e < E; e++)
-              if (ts + E * lane + e >= b_lo + sh && ts + E * lane + e < b_hi + sh) gst(tp + e, v[e]);
+            for (uint32_t e = 0; e < E; e++) {
+              const uint32_t sl = ts + E * lane + e;
+              dd_acc += sl >= lo_u && sl < hi_u ? dd_entry((uint32_t)v[e]) : 0u;
+            }
+          } else if constexpr (DD == DD_STR) {
+            dd_tile(ts, lo_u, hi_u, v);
+          } else {
+            T* tp = pag + ts + E * lane;
+            if (out16 && ts >= lo_u && ts + TV <= hi_u) {
+              if constexpr (W == 8) {
+                typedef uint64_t v2 __attribute__((ext_vector_type(2)));
+                gst_nt((v2*)tp, v2{v[0], v[1]});
+              } else {
+                gst_nt((u32x4*)tp, u32x4{v[0], v[1], v[2], v[3]});
+              }
+            } else {
+  #pragma unroll
+              for (uint32_t e = 0; e < E; e++)
+                if (ts + E * lane + e >= lo_u && ts + E * lane + e < hi_u) gst(tp + e, v[e]);
+            }
           }
         }
       };
       if ((IDS || own_dict) && x_lds) sweep(std::true_type{});
       else sweep(std::false_type{});
-      if (b_hi >= v_hi) break;
+      if (b_hi >= r_hi) break;
       k += XT_RUNS - 1;
       b_lo = b_hi;
     }
+    if constexpr (DD == DD_SUMS) {
+      for (int o = 32; o >= 1; o >>= 1) dd_acc += __shfl_xor(dd_acc, o);
+      if (lane == 0) gst(dd + c, (uint64_t)dd_acc);
+    } else if constexpr (DD == DD_STR) {
+      // slots past a walk error: empty values (the reader threw before them)
+      const uint32_t t_lo = v_lo > r_hi ? v_lo : r_hi;
+      for (uint32_t i = t_lo + lane; i < v_hi; i += WAVE) gst(opag + sh + i, (int64_t)run_base);
+      dd_flush();
+    }
   };
   if (go) one_chunk();  // one chunk per wave
+  else if (DD == DD_SUMS && page >= 0 && lane == 0) gst(dd + c, (uint64_t)0);
 }
 
 template <int W, bool IDS = false>
@@ -1037,6 +1253,97 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restri
   }
 }
 
+
+// Dictionary-direct BYTE_ARRAY columns (ColumnDev::dict_direct: required, every data page
+// dictionary-encoded, the dictionary page at most DD_DICT_MAX bytes): the ids are never stored.
+//   k_dict_fused_dd  walkers + DD_SUMS expansion: per output chunk the bytes of its values
+//                    (PlainBinaryDictionary entry lengths, PlainValuesDictionary.java:58-134)
+//   k_dd_bases       per column: exclusive scan of its chunks' sums (chunks in page order) -> each chunk's
+//                    first byte; the total -> bin_total and offsets[n_slots]
+//   k_dict_str       DD_STR expansion over the walkers' run records: offsets and value bytes
+// (DictionaryValuesReader.readBytes, DictionaryValuesReader.java:75-82, per value: the id's entry)
+__global__ __launch_bounds__(64 * WPB) void k_dict_fused_dd(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                            const PageWork* __restrict__ work,
+                                                            const ColumnDev* __restrict__ cols,
+                                                            const int32_t* __restrict__ list, int n_list,
+                                                            uint32_t n_walk, uint64_t* rec, uint32_t* chunk_run,
+                                                            const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                            uint64_t* pstat, uint32_t* flags, uint32_t epoch,
+                                                            uint64_t* err, ErrCount err_count, uint64_t* sums) {
+  constexpr uint32_t LB = sizeof(DictWaveLds) * WPB > XT_LDS_BYTES ? sizeof(DictWaveLds) * WPB : XT_LDS_BYTES;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LB];
+  if (blockIdx.x < n_walk) {
+#ifdef PQG_FAULT_INJECT
+    if (blockIdx.x == 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)PQG_FAULT_INJECT) __builtin_amdgcn_s_sleep(127);
+    }
+#endif
+    dict_runs_body<4>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
+                      lds, blockIdx.x);
+  } else {
+    dict_tiles_body<4, true, true, DD_SUMS>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, flags,
+                                            epoch, err, err_count, lds, blockIdx.x - n_walk, sums);
+  }
+}
+
+// split mode (pqg_sync's re-run after a fused-kernel timeout): the DD_SUMS expansion after the walk
+__global__ __launch_bounds__(64 * WPB) void k_dict_tiles_dd(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                            const PageWork* __restrict__ work,
+                                                            const ColumnDev* __restrict__ cols, const uint64_t* rec,
+                                                            const uint32_t* chunk_run,
+                                                            const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                            const uint64_t* pstat, uint64_t* err, ErrCount err_count,
+                                                            uint64_t* sums) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[XT_LDS_BYTES];
+  dict_tiles_body<4, false, true, DD_SUMS>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat,
+                                           nullptr, 0, err, err_count, lds, blockIdx.x, sums);
+}
+
+// One workgroup per dictionary-direct column: its chunks are sums[start[2i] .. start[2i + 1]) in page order.
+__global__ __launch_bounds__(256) void k_dd_bases(const ColumnDev* __restrict__ cols, const int32_t* __restrict__ dd_cols,
+                                                  const int32_t* __restrict__ start, uint64_t* sums) {
+  __shared__ uint64_t wsum[4];
+  const ColumnDev& cd = cols[dd_cols[blockIdx.x]];
+  const uint32_t b = (uint32_t)start[2 * blockIdx.x], e = (uint32_t)start[2 * blockIdx.x + 1];
+  uint64_t carry = 0;
+  for (uint32_t c0 = b; c0 < e; c0 += 256u) {
+    const uint32_t i = c0 + threadIdx.x;
+    const uint64_t v = i < e ? sums[i] : 0;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o);
+      if ((int)lane_id() >= o) x += y;
+    }
+    if (lane_id() == 63) wsum[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint64_t pre = carry, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; w++) {
+      pre += w < (threadIdx.x >> 6) ? wsum[w] : 0;
+      tot += wsum[w];
+    }
+    if (i < e) sums[i] = pre + x - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *cd.bin_total = carry;
+    gst((int64_t*)cd.values + cd.n_slots, (int64_t)carry);
+  }
+}
+
+__global__ __launch_bounds__(64 * WPB) void k_dict_str(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                       const PageWork* __restrict__ work,
+                                                       const ColumnDev* __restrict__ cols, const uint64_t* rec,
+                                                       const uint32_t* chunk_run, const uint64_t* __restrict__ chunks,
+                                                       uint32_t n_chunks, const uint64_t* pstat, uint64_t* err,
+                                                       ErrCount err_count, uint64_t* bases, uint32_t dd_region) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dd_lds[];
+  dict_tiles_body<4, false, true, DD_STR>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, nullptr,
+                                          0, err, err_count, dd_lds, blockIdx.x, bases, dd_region);
+}
 
 // ---------------------------------------------------------------------------
 // Levels (def/rep) of nullable columns: ColumnReaderBase.readPageV1/readPageV2,
@@ -2713,6 +3020,35 @@ hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
   if (n_tile)
     hipLaunchKernelGGL((k_dict_tiles<4, true>), dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run,
                        chunks, n_chunks, pstat, err, err_count);
+  return hipGetLastError();
+}
+
+hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
+                          const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
+                          const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
+                          uint32_t epoch, bool fused, uint64_t* err, ErrCount err_count, uint64_t* sums,
+                          const int32_t* dd_cols, const int32_t* dd_start, int n_dd_cols, uint32_t dd_region) {
+  if (n <= 0) return hipSuccess;
+  const uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
+  const dim3 blk(64 * WPB);
+  if (fused) {
+    hipLaunchKernelGGL(k_dict_fused_dd, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n, n_walk,
+                       rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count, sums);
+  } else {
+    hipLaunchKernelGGL(k_dict_runs<4>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,
+                       pstat, flags, epoch, err, err_count);
+    if (n_tile)
+      hipLaunchKernelGGL(k_dict_tiles_dd, dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks,
+                         n_chunks, pstat, err, err_count, sums);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_dd_bases, dim3(n_dd_cols), dim3(256), 0, st, cols, dd_cols, dd_start, sums);
+  e = hipGetLastError();
+  if (e != hipSuccess || !n_tile) return e;
+  const size_t lds = (size_t)dd_region + WPB * (XT_RUNS * 16 + XT_SEG + DD_IMG + 16);
+  hipLaunchKernelGGL(k_dict_str, dim3(n_tile), blk, lds, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks,
+                     n_chunks, pstat, err, err_count, sums, dd_region);
   return hipGetLastError();
 }
 

@@ -453,3 +453,91 @@ def test_binary_plain_tile_edges(decoder, lens, one_pass_kernel):
     nn = int(dl.sum())
     run_both(decoder, [make(abi.BYTE_ARRAY, (vals * (nn // len(vals) + 1))[:nn], abi.PLAIN, def_levels=dl, max_def=1,
                             version=1, page_rows=len(dl) // 2 + 1)])
+
+
+# ---- dictionary-direct BYTE_ARRAY columns (launch_dict_dd: walk + chunk byte sums, per-column scan,
+# offsets and value bytes from the ids in registers) ------------------------------------------------------
+
+def _lineitem_words():
+    return [b"DELIVER IN PERSON", b"COLLECT COD", b"NONE", b"TAKE BACK RETURN", b"R", b"A", b"N", b"", b"AIR"]
+
+
+@pytest.mark.parametrize("dict_direct", [1, 0])
+def test_dictionary_direct_interleaved_columns(decoder, dict_direct):
+    """Several dictionary-direct columns whose pages are interleaved in the page table (the plan sorts
+    their chunks by column and pads each column to whole workgroups), beside a column of another kind;
+    PQG_DISPATCH_DICT_DIRECT = 0 sends the same columns through ids -> map -> copy: equal results."""
+    words = _lineitem_words()
+    rng = np.random.default_rng(17)
+    chunks = []
+    for k, (n, card, rows) in enumerate([(47_000, 3, 20000), (30_001, 9, 7000), (8_191, 2, 1000), (25_000, 7, 4096)]):
+        w = words[k: k + card] if k + card <= len(words) else words[:card]
+        ids = rng.integers(0, card, size=n)
+        chunks.append(make(abi.BYTE_ARRAY, [w[i] for i in ids], abi.RLE_DICTIONARY, page_rows=rows))
+    chunks.append(make(abi.INT64, zipf_dict_column(20_000, card=40, seed=5), abi.RLE_DICTIONARY, page_rows=3000))
+    batch = writer.build_batch(chunks)
+    order = np.argsort(np.arange(batch.n_pages) % 5, kind="stable")
+    cols = batch.pages["column"][order]
+    for c in range(len(chunks)):  # keep each column's page order
+        idx = np.nonzero(cols == c)[0]
+        order[idx] = np.sort(order[idx])
+    batch.pages = batch.pages[order]
+    batch.page_slot_offsets = batch.page_slot_offsets[order]
+    ref = pqref.decode_batch(batch)
+    assert ref.code == 0
+    decoder.set_dispatch(abi.DISPATCH_DICT_DIRECT, dict_direct)
+    try:
+        dcols, st = decoder.decode(decoder.upload(batch), check=False)
+    finally:
+        decoder.set_dispatch(abi.DISPATCH_DICT_DIRECT, 1)
+    assert st.code == 0, st.message
+    for i, cd in enumerate(batch.columns):
+        assert_same(dcols[i].numpy(), ref.columns[i]["values"], cd["physical_type"])
+        if cd["physical_type"] == abi.BYTE_ARRAY:
+            n = ref.columns[i]["n_values"]
+            assert np.array_equal(dcols[i].offsets().cpu().numpy(), ref.columns[i]["offsets"][: n + 1])
+
+
+@pytest.mark.parametrize("lens", [(0, 0), (1, 4000), (2000, 2000, 2000), (0, 1, 23, 24, 64)])
+def test_dictionary_direct_entry_lengths(decoder, lens):
+    """Entry lengths around the kernel's per-wave image (6 KiB per 256-value tile): empty entries only,
+    tiles whose bytes overflow the image (written value by value), and mixes of both in one chunk."""
+    rng = np.random.default_rng(len(lens))
+    words = [bytes(rng.integers(65, 91, size=n, dtype=np.uint8)) for n in lens]
+    ids = rng.integers(0, len(words), size=9000)
+    ids[:600] = 0  # an RLE run of the first entry, then mixed runs
+    run_both(decoder, [make(abi.BYTE_ARRAY, [words[i] for i in ids], abi.RLE_DICTIONARY, page_rows=3500)])
+
+
+def test_dictionary_direct_expands_past_estimate(decoder):
+    """A dictionary-direct column whose bytes exceed the first byte-buffer estimate: the byte total
+    (k_dd_bases) reports the size needed and decode() retries."""
+    words = [bytes([66 + i]) * 2600 for i in range(3)]  # 7.8 KB dictionary page: dictionary-direct
+    vals = [words[i % 3] for i in range(6000)]
+    batch, ref, dcols = run_both(decoder, [make(abi.BYTE_ARRAY, vals, abi.RLE_DICTIONARY, page_rows=2000)])
+    assert dcols[0].binary_data.numel() >= 6000 * 2600
+
+
+def test_dictionary_direct_error_stays_in_its_column(decoder):
+    """An id past the dictionary in one dictionary-direct column: the oracle's status, and the other
+    dictionary-direct column of the batch decodes completely."""
+    words = _lineitem_words()
+    rng = np.random.default_rng(23)
+    good_ids = rng.integers(0, 7, size=30_000)
+    good = make(abi.BYTE_ARRAY, [words[i] for i in good_ids], abi.RLE_DICTIONARY, page_rows=9000)
+    bad = make(abi.BYTE_ARRAY, [words[i] for i in rng.integers(0, 6, size=30_000)], abi.RLE_DICTIONARY,
+               page_rows=9000)
+    bad.dict_num_values = 4
+    batch = writer.build_batch([bad, good])
+    ref = pqref.decode_batch(batch)
+    dcols, st = decoder.decode(decoder.upload(batch), check=False)
+    assert ref.code != 0 and (int(st.code), int(st.page), int(st.value_index)) == ref.status
+    assert_same(dcols[1].numpy(), [words[i] for i in good_ids], abi.BYTE_ARRAY)
+
+
+def test_dictionary_direct_plan_relaunch(decoder):
+    """A plan launched twice: the chunk sums and bases are rewritten per launch (nothing stale)."""
+    words = _lineitem_words()
+    ids = np.random.default_rng(29).integers(0, 9, size=40_000)
+    _plan_both(decoder, [make(abi.BYTE_ARRAY, [words[i] for i in ids], abi.RLE_DICTIONARY, page_rows=20000),
+                         make(abi.BYTE_ARRAY, [words[i] for i in ids[::-1]], abi.RLE_DICTIONARY, page_rows=6000)])

@@ -28,7 +28,7 @@ for s in $STEPS; do
         || { tail -30 "$OUT/bench.err"; exit 1; }
       cat "$OUT/bench.json" ;;
     e2e)
-      timeout -k 10 400 python -u bench.py --no-cpu --e2e --steps 5 > "$OUT/bench_e2e.json" 2> "$OUT/bench_e2e.err" \
+      PQG_HOST_TIMING=1 timeout -k 10 400 python -u bench.py --no-cpu --e2e --steps 5 > "$OUT/bench_e2e.json" 2> "$OUT/bench_e2e.err" \
         || { tail -30 "$OUT/bench_e2e.err"; exit 1; }
       cat "$OUT/bench_e2e.json" ;;
     bench2)

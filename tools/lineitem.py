@@ -142,7 +142,7 @@ class Shard:
     are one pqg column per row group (each row group has its own dictionary); the other columns
     decode every row group of the rank into one rank-wide column, back to back."""
 
-    def __init__(self, rows, world=1, rank=0, templates=4, rg_rows=1_000_000):
+    def __init__(self, rows, world=1, rank=0, templates=4, rg_rows=1_000_000, keep=None):
         import copy
 
         from pqgpu import dist as pdist
@@ -157,9 +157,13 @@ class Shard:
         tsize = [sum(len(p.body) for c in ch for p in c.pages) for ch, _ in self.templates]
         self.shards = pdist.shard_row_groups([tsize[g % self.T] for g in range(self.n_rg)], world)
         self.mine = self.shards[rank]
+        # keep: the lineitem columns decoded (diagnostics: a subset's kernels without the others' overlap)
+        self.keep = list(range(16)) if keep is None else sorted(keep)
         self.chunks = []
         for g in self.mine:
             for k, c in enumerate(self.templates[g % self.T][0]):
+                if k not in self.keep:
+                    continue
                 cc = copy.copy(c)
                 cc.column_index = (k, g) if c.dict_page is not None else (k, -1)
                 self.chunks.append(cc)
@@ -178,11 +182,11 @@ class Shard:
         (compared on the device)."""
         import torch
         exp_dev = {}
-        pos = {k: 0 for k in range(16)}
+        pos = {k: 0 for k in self.keep}
         n = self.rg_rows
         for g in self.mine:
             t = g % self.T
-            for k in range(16):
+            for k in self.keep:
                 ci, merged = self.column(k, g)
                 col = cols[ci]
                 ex = self.templates[t][1][k]
@@ -204,7 +208,7 @@ class Shard:
                     assert torch.equal(col.values[r0 * w:(r0 + n) * w], e), f"{what}: row group {g} column {k}"
                 if merged:
                     pos[k] += n
-        for k in range(16):  # every rank-wide column holds exactly its row groups' values
+        for k in self.keep:  # every rank-wide column holds exactly its row groups' values
             ci, merged = self.column(k, self.mine[0]) if self.mine else (None, False)
             if merged:
                 assert cols[ci].n_values == len(self.mine) * n, f"{what}: column {k} value count"
