@@ -202,6 +202,8 @@ def run_c4(args, world, rank, devi):
     enc_bytes = int(batch.pages["size"].sum()) + sum(int(c["dict_size"]) for c in batch.columns if c["dict_offset"] >= 0)
 
     dec = D.Decoder(devi, poison=0xA5)
+    if args.dict_split:
+        dec.set_dispatch(abi.DISPATCH_DICT_FUSED, 0)
     dbatch = dec.upload(batch)
     cols, st = dec.decode(dbatch)  # sizes the BYTE_ARRAY buffers
     for c in cols:  # poison: the plan's first launch must write every element itself
@@ -343,6 +345,8 @@ def main():
                     help="c2: the headline (BASELINE metric); c4: lineitem 16 columns, strong scaling")
     ap.add_argument("--rows", type=int, default=None, help="c2: rows per GPU (100M); c4: rows in total (1B)")
     ap.add_argument("--c4-templates", type=int, default=4, help="c4: distinct synthetic row groups")
+    ap.add_argument("--dict-split", action="store_true",
+                    help="diagnostics: dictionary walk and expansion as two launches (PQG_DISPATCH_DICT_FUSED = 0)")
     ap.add_argument("--c4-cols", default=None,
                     help="c4 diagnostics: comma-separated lineitem columns to decode (default: all 16)")
     ap.add_argument("--zipf", type=float, default=1.5)
@@ -377,6 +381,9 @@ def main():
     data_bytes = int(sum(len(p.body) for p in chunk.pages))
 
     dec = D.Decoder(devi, poison=0xA5)
+    if args.dict_split:
+        from pqgpu import abi
+        dec.set_dispatch(abi.DISPATCH_DICT_FUSED, 0)
     dbatch = dec.upload(batch)
     cols = dec.alloc_columns(batch)  # poisoned: an element no launch writes cannot pass the check
     plan = dec.plan(dbatch, cols)

@@ -221,6 +221,8 @@ void* pqg_ctx_stream(pqg_ctx* ctx);
  *                                wave per page from there (default), 3 = one pass, one wave per page
  *   PQG_DISPATCH_DICT_DIRECT     dictionary BYTE_ARRAY columns with small dictionaries: 1 = ids
  *                                mapped straight to lengths and bytes (default), 0 = ids, then map
+ *   PQG_DISPATCH_DICT_FUSED      dictionary pages: 1 = walk and expansion in one launch (default),
+ *                                0 = two launches (the mode a fused launch that timed out re-runs in)
  *   PQG_DISPATCH_GZIP_PREPASS_MIN pqg_gzip_decompress: pages of at least `value` output bytes take the
  *                                token pre-pass + replay, smaller ones the one-wave decoder (default
  *                                16384; 0 = every page); applies to later pqg_gzip_decompress calls
@@ -228,7 +230,8 @@ void* pqg_ctx_stream(pqg_ctx* ctx);
 enum pqg_dispatch {
   PQG_DISPATCH_PLAIN_ONE_PASS = 1,
   PQG_DISPATCH_DICT_DIRECT = 2,
-  PQG_DISPATCH_GZIP_PREPASS_MIN = 3
+  PQG_DISPATCH_GZIP_PREPASS_MIN = 3,
+  PQG_DISPATCH_DICT_FUSED = 4
 };
 int pqg_ctx_set_dispatch(pqg_ctx* ctx, int key, int value);
 

@@ -229,6 +229,7 @@ struct pqg_ctx {
   // pqg_ctx_set_dispatch: kernel-choice overrides for the plans created on this ctx
   int plain_mode = 2;       // PQG_DISPATCH_PLAIN_ONE_PASS
   bool dict_direct = true;  // PQG_DISPATCH_DICT_DIRECT
+  bool dict_fused = true;   // PQG_DISPATCH_DICT_FUSED
   uint32_t gz_prepass_min = pqg::GZ_PREPASS_MIN;  // PQG_DISPATCH_GZIP_PREPASS_MIN
   RouterCache router;  // pqg_router_read_page
 };
@@ -306,6 +307,10 @@ int pqg_ctx_set_dispatch(pqg_ctx* ctx, int key, int value) {
     case PQG_DISPATCH_GZIP_PREPASS_MIN:
       if (value < 0) return PQG_ERR_INVALID_ARG;
       ctx->gz_prepass_min = (uint32_t)value;
+      return PQG_OK;
+    case PQG_DISPATCH_DICT_FUSED:
+      if (value != 0 && value != 1) return PQG_ERR_INVALID_ARG;
+      ctx->dict_fused = value != 0;
       return PQG_OK;
     default: return PQG_ERR_INVALID_ARG;
   }
@@ -387,6 +392,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   pqg_plan* P = new (std::nothrow) pqg_plan();
   if (!P) return PQG_ERR_INVALID_ARG;
   P->ctx = ctx;
+  P->dict_fused = ctx->dict_fused;
   P->d_bytes = d_bytes;
   P->n_bytes = n_bytes;
   P->n_pages = n_pages;
@@ -672,6 +678,11 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     }
   }
   P->blen_bytes = sc;
+  // dictionary-direct columns: compact ids (u8 for dictionaries of at most 256 entries, else u16), written
+  // by k_dict_fused_dd for every slot k_dd_str reads (not cleared; padded: k_dd_str reads whole dwords)
+  for (int i = 0; i < n_cols; i++)
+    if (dict_direct[(size_t)i])
+      blen_off[(size_t)i] = take((cols[i].dict_num_values <= 256 ? 1u : 2u) * (slot_acc[(size_t)i] + 16));
   if (!pcp.empty()) P->pflag_off = take(8);
   if (!segs.empty()) P->seg_tmp_off = take(4 * 2 * (uint64_t)pqg::BW_SEG_CAP * segs.size());
   P->n_segs = (uint32_t)segs.size();
@@ -871,7 +882,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       d.block_sums = (uint64_t*)at(bsum_off[(size_t)i]);
       d.bin_total = (uint64_t*)at(P->bin_total_off[(size_t)i]);
       d.n_slots = slot_acc[(size_t)i];
-      d.dict_direct = dict_direct[(size_t)i];
+      d.dict_direct = dict_direct[(size_t)i] ? (cols[i].dict_num_values <= 256 ? 1u : 2u) : 0u;  // id bytes
       if (dba_fixed[(size_t)i]) {  // DELTA_BYTE_ARRAY values go straight to the fixed-width output
         d.binary_data = (uint8_t*)cols[i].values;
         d.binary_capacity = slot_acc[(size_t)i] * (uint64_t)d.elem_width;

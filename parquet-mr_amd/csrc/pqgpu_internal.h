@@ -33,9 +33,9 @@ struct ColumnDev {
   uint64_t n_slots;        // level slots of the column in the batch (offsets span n_slots + 1)
   uint64_t* block_sums;    // BYTE_ARRAY offset scan: per 4096-value block
   uint64_t* bin_total;     // BYTE_ARRAY: bytes of the decoded values (device, one u64)
-  // 1: a required BYTE_ARRAY column whose data pages are all dictionary-encoded and whose dictionary
-  // page fits DD_DICT_MAX: its pages take launch_dict_dd (chunk byte sums, scan, offsets + bytes from
-  // the ids in registers); no blen, no offset scan blocks, no k_bin_dict_map / k_bin_copy
+  // A required BYTE_ARRAY column whose data pages are all dictionary-encoded and whose dictionary page
+  // fits DD_DICT_MAX: its pages take launch_dict_dd (compact ids + chunk byte sums, scan, offsets and
+  // bytes); dict_direct = the bytes of its ids in blen (1: u8, 2: u16), 0 for every other column
   uint32_t dict_direct;
 };
 
@@ -113,7 +113,7 @@ hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
 // dictionary-direct BYTE_ARRAY columns (ColumnDev::dict_direct): the walk + per-chunk byte sums
 // (k_dict_fused_dd, or k_dict_runs + k_dict_tiles_dd in split mode), the per-column scan of the sums
 // (k_dd_bases: chunks of column i are sums[dd_start[2i] .. dd_start[2i + 1])), then offsets and value
-// bytes (k_dict_str; dd_region = LDS bytes of the staged dictionary page + its u32 entry table)
+// bytes (k_dd_str; dd_region = LDS bytes of the staged dictionary page + its u32 entry table)
 hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                           const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                           const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
@@ -174,7 +174,7 @@ constexpr uint32_t BW_SEG_BYTES = 16384;
 constexpr uint32_t BW_SEG_CAP = BW_SEG_BYTES / 4 + 2;
 constexpr uint32_t BW_SEG_MAX_PAGES = 4096;
 constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block
-constexpr uint32_t DD_DICT_MAX = 8192;  // dictionary page bytes staged by k_dict_str (dict_direct)
+constexpr uint32_t DD_DICT_MAX = 8192;  // dictionary page bytes staged by k_dd_str (dict_direct)
 hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                       const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,

@@ -397,6 +397,27 @@ __device__ __forceinline__ void dict_walk_ls(DictWaveLds& L, PreWin& win, uint32
     k = uni(k);
     if (produced >= N) break;
     if (pos >= sec_end) { code = PQG_ERR_RLE_PAST_END; break; }  // readNext :81
+    // A bit-packed run of at least 32 data bytes is taken on the scalar unit, without pre-decoding a
+    // 256-byte window that holds at most eight headers (few-entry dictionaries of random ids — C4's
+    // flag and mode columns, runs of 504 values at w = 1..3 — have one or two per window). The header
+    // test reads one byte; an RLE header (C2's usual one) goes straight to the window.
+    {
+      if (!SMALL && !seg_has(win, pos & ~3u, 8u)) seg_fill(win, pos & ~15u);
+      const uint32_t b0 = uni((seg32(win, pos & ~3u) >> ((pos & 3u) * 8u)) & 0xFFu);
+      if (b0 & 1u) {
+        uint32_t hl, m, nxs, vv;
+        uint64_t cnt64;
+        const int c2 = slow_header_g([&](uint32_t p) { return wbyte(win, p); }, pos, sec_end, w, hl, m, cnt64, vv, nxs);
+        if (c2 == 0 && m && (cnt64 >> 3) * (uint32_t)w >= 32u) {
+          const uint32_t left = N - produced;
+          const uint32_t take = cnt64 < left ? (uint32_t)cnt64 : left;
+          put_record(produced, produced + take, 0x80000000u | vv);
+          produced += take;
+          pos = nxs < sec_end ? nxs : sec_end;  // readFully of what is left
+          continue;
+        }
+      }
+    }
     const uint32_t B = pos & ~3u;
     DIAG_T(dg_t0);
 #ifdef PQG_DIAG
@@ -646,16 +667,11 @@ constexpr uint64_t SPIN_TIMEOUT_TICKS = 200000000ull;  // 2 s of s_memrealtime (
 // IDS: the expansion writes the dictionary ids themselves (u32, into ColumnDev::blen) instead
 // of dictionary values: BYTE_ARRAY / FIXED_LEN_BYTE_ARRAY / INT96 dictionaries, whose values
 // are materialized by later kernels (k_bin_dict_map + k_bin_copy, k_gather_fixed).
-// DD (dictionary-direct BYTE_ARRAY columns, ColumnDev::dict_direct; IDS, W = 4):
-//   DD_SUMS  the chunk's value bytes: sum of the entry lengths of its ids -> dd[chunk] (no id stores);
-//   DD_STR   offsets and value bytes from the ids, the chunk's first byte at dd[chunk] (the sums
-//            scanned per column by k_dd_bases): int64 offsets as 16-byte stores, the bytes composed
-//            from the staged dictionary page in a per-wave LDS image and stored as 16-byte blocks.
-//   Slots of a page past a walk error (pstat's value count) are empty values (length 0).
-// dd_region (DD_STR): LDS bytes before the run tables: the dictionary page, then one u32 entry per id
-// (source offset << 16 | length); sized per launch (dynamic LDS).
-constexpr int DD_NONE = 0, DD_SUMS = 1, DD_STR = 2;
-constexpr uint32_t DD_IMG = 6144;     // DD_STR: output image per wave (a tile of 256 values of <= 23 bytes)
+// DD_SUMS (dictionary-direct BYTE_ARRAY columns, ColumnDev::dict_direct; IDS, W = 4): the expansion
+// stores the ids compactly (ColumnDev::blen as u8 ids for dict_direct 1, u16 for 2: a quarter / half of
+// the u32 id traffic) and the chunk's value bytes, the sum of its ids' entry lengths, to dd[chunk].
+// Slots of a page past a walk error (pstat's value count) are left to k_dd_str (empty values).
+constexpr int DD_NONE = 0, DD_SUMS = 1;
 constexpr uint32_t DD_ENT_MAX = 2048; // entries of a dictionary page of at most DD_DICT_MAX bytes (4-byte lengths)
 
 // Inclusive prefix sum over the wave (u32) with DPP row shifts / broadcasts; all 64 lanes active.
@@ -678,17 +694,15 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
                                                 const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                 const uint64_t* pstat, const uint32_t* flags, uint32_t epoch,
                                                 uint64_t* err, ErrCount err_count, uint8_t* lds, uint32_t group,
-                                                uint64_t* dd = nullptr, uint32_t dd_region = 0) {
+                                                uint64_t* dd = nullptr) {
   typedef typename DictVal<W>::T T;
   static_assert(DD == DD_NONE || (IDS && W == 4), "dictionary-direct modes take the ids of a 4-byte expansion");
   constexpr uint32_t E = 16 / W;
   constexpr uint32_t TV = WAVE * E;  // values per tile
   constexpr uint32_t CH = CH_TILES * TV;
-  const uint32_t DL = DD == DD_STR ? dd_region : DICT_LDS_BYTES;  // bytes of the dictionary region
   uint8_t* dict_lds = lds;
-  u32x4* tab = (u32x4*)(lds + DL) + wave_id() * XT_RUNS;
-  uint8_t* xseg = lds + DL + WPB * XT_RUNS * 16 + wave_id() * XT_SEG;
-  uint8_t* img = lds + DL + WPB * (XT_RUNS * 16 + XT_SEG) + wave_id() * (DD_IMG + 16);  // DD_STR
+  u32x4* tab = (u32x4*)(lds + DICT_LDS_BYTES) + wave_id() * XT_RUNS;
+  uint8_t* xseg = lds + DICT_LDS_BYTES + WPB * XT_RUNS * 16 + wave_id() * XT_SEG;
   const uint32_t lane = lane_id();
   const uint32_t c = group * WPB + wave_id();
   // (a chunk list entry of page 0xFFFFFFFF is padding: the host aligns each dictionary-direct column's
@@ -838,25 +852,15 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       if (o < need) *(u32x4*)(dict_lds + o) = dreg[r];
     }
   }
-  // DD: the entry table (DD_SUMS: lengths; DD_STR: source << 16 | length, after the staged page)
-  uint32_t dd_ent_off = 0;
+  // DD_SUMS: the entry lengths
   if constexpr (DD != DD_NONE) {
     if (same && c0 >= 0) {
       const ColumnDev& cd0 = cols[c0];
       const uint32_t dn = uni(cd0.dict_n);
-      const uint32_t pg16 = (uint32_t)((cd0.dict_bytes + 15u) & ~15ull);
-      dd_ent_off = DD == DD_STR ? pg16 : 0u;
-      dict_in_lds = dn <= DD_ENT_MAX && cd0.dict_bytes <= DD_DICT_MAX && (DD == DD_SUMS || pg16 + 4u * dn <= DL);
+      dict_in_lds = dn <= DD_ENT_MAX && cd0.dict_bytes <= DD_DICT_MAX;
       if (dict_in_lds) {
-        uint32_t* ent = (uint32_t*)(dict_lds + dd_ent_off);
-        for (uint32_t i = threadIdx.x; i < dn; i += 64u * WPB)
-          ent[i] = DD == DD_STR ? (cd0.dict_src[i] << 16) | cd0.dict_len[i] : cd0.dict_len[i];
-        if constexpr (DD == DD_STR) {  // (a resource over the rest of the batch: a 16-byte load crossing
-          // the end of its range would return 0 as a whole; only entry bytes are ever read from it)
-          const rsrc_t d0 = make_rsrc(bytes + cd0.dict_offset, n_bytes - cd0.dict_offset);
-          for (uint32_t o = 16u * threadIdx.x; o < pg16; o += 16u * 64u * WPB)
-            *(u32x4*)(dict_lds + o) = __builtin_amdgcn_raw_buffer_load_b128(d0, (int)o, 0, 0);
-        }
+        uint32_t* ent = (uint32_t*)dict_lds;
+        for (uint32_t i = threadIdx.x; i < dn; i += 64u * WPB) ent[i] = cd0.dict_len[i];
       }
     }
   }
@@ -873,131 +877,14 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
     const uint32_t wmask = w == 32 ? 0xFFFFFFFFu : (1u << w) - 1u;
     // the walked part of the chunk (DD: slots past a walk error follow as empty values)
     const uint32_t r_hi = DD != DD_NONE ? (v_hi < N ? v_hi : N) : v_hi;
-    // DD state: DD_SUMS the lane's byte sum; DD_STR the running first byte of the next value, the
-    // output image's 16-byte aligned start (bytes [ia, run_base) are composed, not yet stored) and the
-    // first byte this chunk owns (the block at its start is shared with the previous chunk's wave)
+    // DD_SUMS: the lane's byte sum, the column's compact ids (slot 0 of the page), their width
     uint32_t dd_acc = 0;
-    uint64_t run_base = 0, ia = 0, own_lo = 0, cap = 0;
-    int64_t* opag = nullptr;
-    bool o16 = false;
-    const uint32_t* ent_l = (const uint32_t*)(dict_lds + dd_ent_off);
-    if constexpr (DD == DD_STR) {
-      run_base = uni64(dd[c]);
-      ia = run_base & ~15ull;
-      own_lo = run_base;
-      cap = cd.binary_capacity;
-      opag = (int64_t*)cd.values + (pw.out_offset - sh);
-      o16 = ((uintptr_t)cd.values & 15u) == 0;
-    }
-    // DD: entry of id (DD_SUMS: its length; DD_STR: source << 16 | length); 0 past the dictionary
-    auto dd_entry = [&](uint32_t id) -> uint32_t {
-      if (id >= dict_n) return 0u;
-      if (own_dict) return ent_l[id];
-      return DD == DD_STR ? (cd.dict_src[id] << 16) | cd.dict_len[id] : cd.dict_len[id];
-    };
-
-    // DD_STR: the composed bytes [ia, run_base) that are still in the image (at most one partial block)
-    auto dd_flush = [&]() {
-      const uint64_t lo = own_lo > ia ? own_lo : ia;
-      const uint64_t hi = run_base < cap ? run_base : cap;
-      if (lane < 16u && ia + lane >= lo && ia + lane < hi) gst(cd.binary_data + ia + lane, img[lane]);
-      wave_sync();
-    };
-    // DD_STR: one tile's values (ids v, slots outside [lo_u, hi_u) skipped): offsets, then the bytes
-    auto dd_tile = [&](uint32_t ts, uint32_t lo_u, uint32_t hi_u, const T (&v)[E]) {
-      typedef uint16_t __attribute__((aligned(1), may_alias)) u16u;
-      typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
-      uint32_t ln[E], sr[E], ls = 0;
-  #pragma unroll
-      for (uint32_t e = 0; e < E; e++) {
-        const uint32_t sl = ts + E * lane + e;
-        const uint32_t en = sl >= lo_u && sl < hi_u ? dd_entry((uint32_t)v[e]) : 0u;
-        ln[e] = en & 0xFFFFu;
-        sr[e] = en >> 16;
-        ls += ln[e];
-      }
-      const uint32_t inc = wave_incl_scan_u32_dpp(ls);
-      const uint32_t tot = uni(rdl(inc, WAVE - 1));
-      const uint32_t ex = inc - ls;
-      // offsets (BinaryPlainValuesReader / DictionaryValuesReader.readBytes order: value i starts where
-      // value i - 1 ends)
-      uint64_t o[E];
-      o[0] = run_base + ex;
-  #pragma unroll
-      for (uint32_t e = 1; e < E; e++) o[e] = o[e - 1] + ln[e - 1];
-      int64_t* op = opag + ts + E * lane;
-      if (o16 && ts >= lo_u && ts + TV <= hi_u) {
-        typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
-        gst_nt((i64x2*)op, i64x2{(int64_t)o[0], (int64_t)o[1]});
-        gst_nt((i64x2*)(op + 2), i64x2{(int64_t)o[2], (int64_t)o[3]});
-      } else {
-  #pragma unroll
-        for (uint32_t e = 0; e < E; e++)
-          if (ts + E * lane + e >= lo_u && ts + E * lane + e < hi_u) gst(op + e, (int64_t)o[e]);
-      }
-      if (tot == 0) return;
-      uint8_t* const dst = cd.binary_data;
-      const uint64_t end = run_base + tot;
-      const bool dst16 = ((uintptr_t)dst & 15u) == 0, dst4 = ((uintptr_t)dst & 3u) == 0;
-      auto dword_at = [&](uint32_t sp) -> uint32_t {  // 4 dictionary-page bytes at sp
-        return own_dict ? *(const u32u*)(dict_lds + sp) : ld4_any(drs, sp);
-      };
-      if (own_dict && end - ia <= DD_IMG) {
-        // compose: each value's whole dwords as unaligned 4-byte writes, its last 1-3 bytes as a 2- and a
-        // 1-byte write, so no write leaves the value's own bytes (other lanes write around it)
-        uint8_t* ob = img + (uint32_t)(run_base - ia) + ex;
-  #pragma unroll
-        for (uint32_t e = 0; e < E; e++) {
-          uint32_t q = 0;
-          for (; q + 4u <= ln[e]; q += 4u) *(u32u*)(ob + q) = dword_at(sr[e] + q);
-          if (q < ln[e]) {
-            const uint32_t x = dword_at(sr[e] + q), r = ln[e] - q;
-            if (r & 2u) *(u16u*)(ob + q) = (uint16_t)x;
-            if (r & 1u) ob[q + (r & 2u)] = (uint8_t)(x >> (8u * (r & 2u)));
-          }
-          ob += ln[e];
-        }
-        wave_sync();
-        // whole 16-byte blocks go out; the partial last block stays in the image for the next tile
-        const uint32_t nfull = (uint32_t)((end - ia) >> 4);
-        const uint64_t o_hi = end < cap ? end : cap;
-        for (uint32_t bb = lane; bb < nfull; bb += WAVE) {
-          const u32x4 x4 = *(const u32x4*)(img + 16u * bb);
-          const uint32_t wd[4] = {x4.x, x4.y, x4.z, x4.w};
-          const uint64_t a = ia + 16u * bb;
-          uint32_t have = 0;
-  #pragma unroll
-          for (uint32_t q = 0; q < 4; q++) have |= (a + 4u * q >= own_lo && a + 4u * q + 4u <= o_hi ? 1u : 0u) << q;
-          if (!dst4) have = 0;
-          if (a + 16u > own_lo && a < o_hi) store_block16(dst, a, own_lo, o_hi, wd, have, dst16);
-        }
-        const uint32_t tail = (uint32_t)(end - ia) & 15u;
-        uint32_t keep = 0;
-        if (lane < 4u) keep = *(const uint32_t*)(img + 16u * nfull + 4u * lane);
-        wave_sync();
-        if (lane < 4u && tail) *(uint32_t*)(img + 4u * lane) = keep;
-        wave_sync();
-        ia += 16ull * nfull;
-      } else {
-        // the tile's bytes do not fit the image (or the dictionary is not staged): the composed
-        // partial block goes out first, then every lane writes its values' bytes itself
-        dd_flush();
-        uint64_t ob = run_base + ex;
-  #pragma unroll
-        for (uint32_t e = 0; e < E; e++) {
-          for (uint32_t q = 0; q < ln[e]; q += 4u) {
-            const uint32_t x = dword_at(sr[e] + q);
-  #pragma unroll
-            for (uint32_t b = 0; b < 4u; b++)
-              if (q + b < ln[e] && ob + q + b < cap) gst(dst + ob + q + b, (uint8_t)(x >> (8u * b)));
-          }
-          ob += ln[e];
-        }
-        ia = end & ~15ull;
-        own_lo = end;
-      }
-      run_base = end;
-    };
+    const uint32_t* ent_l = (const uint32_t*)dict_lds;
+    uint8_t* const idpag = (uint8_t*)cd.blen + (pw.out_offset - sh) * (uint64_t)cd.dict_direct;
+    // DD: length of id's entry, 0 past the dictionary. Always from LDS: the plan gives a dictionary-direct
+    // column whole workgroups and dictionaries that fit (a global load in the tile loop would make every
+    // later wait a vmcnt(0), draining the stores)
+    auto dd_entry = [&](uint32_t id) -> uint32_t { return id < dict_n ? ent_l[id] : 0u; };
 
     uint32_t b_lo = v_lo;
     while (v_lo < r_hi) {
@@ -1128,8 +1015,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
           if (ci + step < n_tab && tab[ci + step].x <= pe) ci += step;
         u32x4 cq = tab[ci];
         uint32_t ce = tab[ci + 1].x;
-        // the round's slot range, uniform: the whole-tile store test below is a scalar compare
-        const uint32_t lo_u = uni(b_lo + sh), hi_u = uni(b_hi + sh);
+        const uint32_t lo_u = b_lo + sh, hi_u = b_hi + sh;  // the round's slot range
         for (uint32_t t = t_beg; t < t_end; t++) {
           t = uni(t);
           const uint32_t ts = t * TV;  // first slot of the tile
@@ -1142,39 +1028,38 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
           }
           // elements outside [b_lo, b_hi) are not stored; they are evaluated at a clamped index
           T v[E];
-          const uint32_t pl = p0 + (E - 1);
-          const uint32_t il = pl < b_lo || pl > 0x7FFFFFFFu ? b_lo : (pl >= b_hi ? b_hi - 1 : pl);
-          // The common tile (C2: runs of ~100 values, 128 per tile): every lane's E elements lie in its
-          // current run and that run is RLE, so each element is the run's value — one wave-uniform test
-          // instead of E divergent run / packed branches, whose exec-mask bookkeeping ran on the scalar
-          // unit (~40 SALU per tile) that the walkers on the CU share.
-          if (!__ballot((cq.y & 0x80000000u) || il >= ce)) {
-            const T rv = (T)(((uint64_t)cq.w << 32) | cq.z);
+          v[0] = value(ci, pe, cq);
   #pragma unroll
-            for (uint32_t e = 0; e < E; e++) v[e] = rv;
-          } else {
-            v[0] = value(ci, pe, cq);
-  #pragma unroll
-            for (uint32_t e = 1; e < E; e++) {
-              const uint32_t x = p0 + e;  // value index of element e (wraps below 0)
-              const uint32_t i = x < b_lo || x > 0x7FFFFFFFu ? b_lo : (x >= b_hi ? b_hi - 1 : x);
-              if (i < ce) {
-                v[e] = value(ci, i, cq);
-              } else {  // the element starts a later run
-                uint32_t cj = ci + 1;
-                while (cj + 1 < n_tab && tab[cj + 1].x <= i) cj++;
-                v[e] = value(cj, i, tab[cj]);
-              }
+          for (uint32_t e = 1; e < E; e++) {
+            const uint32_t x = p0 + e;  // value index of element e (wraps below 0)
+            const uint32_t i = x < b_lo || x > 0x7FFFFFFFu ? b_lo : (x >= b_hi ? b_hi - 1 : x);
+            if (i < ce) {
+              v[e] = value(ci, i, cq);
+            } else {  // the element starts a later run
+              uint32_t cj = ci + 1;
+              while (cj + 1 < n_tab && tab[cj + 1].x <= i) cj++;
+              v[e] = value(cj, i, tab[cj]);
             }
           }
           if constexpr (DD == DD_SUMS) {
+            const bool whole = ts >= lo_u && ts + TV <= hi_u;
+            uint8_t* ip = idpag + (uint64_t)(ts + E * lane) * cd.dict_direct;
+            if (cd.dict_direct == 1u) {
+              if (whole) gst((uint32_t*)ip, (v[0] & 0xFFu) | (v[1] & 0xFFu) << 8 | (v[2] & 0xFFu) << 16 | v[3] << 24);
+            } else if (whole) {
+              typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+              gst((u32x2*)ip, u32x2{(v[0] & 0xFFFFu) | v[1] << 16, (v[2] & 0xFFFFu) | v[3] << 16});
+            }
   #pragma unroll
             for (uint32_t e = 0; e < E; e++) {
               const uint32_t sl = ts + E * lane + e;
-              dd_acc += sl >= lo_u && sl < hi_u ? dd_entry((uint32_t)v[e]) : 0u;
+              const bool in = sl >= lo_u && sl < hi_u;
+              dd_acc += in ? dd_entry((uint32_t)v[e]) : 0u;
+              if (in && !whole) {
+                if (cd.dict_direct == 1u) gst(ip + e, (uint8_t)v[e]);
+                else gst((uint16_t*)ip + e, (uint16_t)v[e]);
+              }
             }
-          } else if constexpr (DD == DD_STR) {
-            dd_tile(ts, lo_u, hi_u, v);
           } else {
             T* tp = pag + ts + E * lane;
             if (out16 && ts >= lo_u && ts + TV <= hi_u) {
@@ -1201,13 +1086,14 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
     if constexpr (DD == DD_SUMS) {
       for (int o = 32; o >= 1; o >>= 1) dd_acc += __shfl_xor(dd_acc, o);
       if (lane == 0) gst(dd + c, (uint64_t)dd_acc);
-    } else if constexpr (DD == DD_STR) {
-      // slots past a walk error: empty values (the reader threw before them)
-      const uint32_t t_lo = v_lo > r_hi ? v_lo : r_hi;
-      for (uint32_t i = t_lo + lane; i < v_hi; i += WAVE) gst(opag + sh + i, (int64_t)run_base);
-      dd_flush();
     }
   };
+  if (DD != DD_NONE && go && !(dict_in_lds && pw.column == c0)) {
+    // (never with the plan's layout: whole workgroups per column, dictionaries within DD_DICT_MAX / 2,048
+    // entries)
+    if (lane == 0) report(err, err_count, cpage, 2, v_lo, PQG_ERR_INVALID_ARG);
+    go = false;
+  }
   if (go) one_chunk();  // one chunk per wave
   else if (DD == DD_SUMS && page >= 0 && lane == 0) gst(dd + c, (uint64_t)0);
 }
@@ -1256,11 +1142,11 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restri
 
 // Dictionary-direct BYTE_ARRAY columns (ColumnDev::dict_direct: required, every data page
 // dictionary-encoded, the dictionary page at most DD_DICT_MAX bytes): the ids are never stored.
-//   k_dict_fused_dd  walkers + DD_SUMS expansion: per output chunk the bytes of its values
-//                    (PlainBinaryDictionary entry lengths, PlainValuesDictionary.java:58-134)
+//   k_dict_fused_dd  walkers + DD_SUMS expansion: per output chunk its compact ids and the bytes of its
+//                    values (PlainBinaryDictionary entry lengths, PlainValuesDictionary.java:58-134)
 //   k_dd_bases       per column: exclusive scan of its chunks' sums (chunks in page order) -> each chunk's
 //                    first byte; the total -> bin_total and offsets[n_slots]
-//   k_dict_str       DD_STR expansion over the walkers' run records: offsets and value bytes
+//   k_dd_str         per output chunk: the compact ids -> int64 offsets and the value bytes
 // (DictionaryValuesReader.readBytes, DictionaryValuesReader.java:75-82, per value: the id's entry)
 __global__ __launch_bounds__(64 * WPB) void k_dict_fused_dd(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                             const PageWork* __restrict__ work,
@@ -1334,15 +1220,152 @@ __global__ __launch_bounds__(256) void k_dd_bases(const ColumnDev* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(64 * WPB) void k_dict_str(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                                       const PageWork* __restrict__ work,
-                                                       const ColumnDev* __restrict__ cols, const uint64_t* rec,
-                                                       const uint32_t* chunk_run, const uint64_t* __restrict__ chunks,
-                                                       uint32_t n_chunks, const uint64_t* pstat, uint64_t* err,
-                                                       ErrCount err_count, uint64_t* bases, uint32_t dd_region) {
+// One wave per output chunk of k_dict_fused_dd (chunks of one column per workgroup: the plan pads the
+// chunk list). The chunk's ids are loaded first, all of them (one dword per tile per lane for u8 ids,
+// two for u16: no load after the first store, whose wait would drain the stores), then per 256-value
+// tile: the entries from the staged table, a wave scan of the lanes' byte counts, the offsets as two
+// 16-byte stores per lane, and each value's bytes from the staged dictionary page as unaligned dword
+// stores plus a 2- and a 1-byte store for its last 1-3 bytes (no store leaves the value's own bytes).
+// Slots of a page past a walk error (pstat) are empty values. dd_region: LDS bytes of the staged page
+// (16-byte rounded) + its u32 entry table (source << 16 | length).
+__global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                     const PageWork* __restrict__ work,
+                                                     const ColumnDev* __restrict__ cols,
+                                                     const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                     const uint64_t* pstat, const uint64_t* __restrict__ bases,
+                                                     uint64_t* err, ErrCount err_count, uint32_t dd_region) {
+  typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
+  typedef uint32_t __attribute__((aligned(1), may_alias, address_space(1))) g32u;
+  typedef uint16_t __attribute__((aligned(1), may_alias, address_space(1))) g16u;
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+  constexpr uint32_t E = 4, TV = WAVE * E, CH = CH_TILES * TV;
   extern __shared__ __attribute__((aligned(16))) uint8_t dd_lds[];
-  dict_tiles_body<4, false, true, DD_STR>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, nullptr,
-                                          0, err, err_count, dd_lds, blockIdx.x, bases, dd_region);
+  __shared__ int wg_col[WPB];
+  const uint32_t lane = lane_id();
+  const uint32_t c = blockIdx.x * WPB + wave_id();
+  const int page = c < n_chunks ? (int)(uint32_t)chunks[c] : -1;
+  if (lane == 0) wg_col[wave_id()] = page >= 0 ? work[page].column : -1;
+  __syncthreads();
+  int c0 = -1;
+  bool same = true;
+#pragma unroll
+  for (int q = 0; q < WPB; q++) {
+    const int cq = wg_col[q];
+    if (cq >= 0) {
+      if (c0 < 0) c0 = cq;
+      else if (cq != c0) same = false;
+    }
+  }
+  uint32_t ent_off = 0;
+  bool staged = false;
+  if (same && c0 >= 0) {  // the dictionary page, then the entry table
+    const ColumnDev& cd0 = cols[c0];
+    const uint32_t dn = uni(cd0.dict_n);
+    ent_off = (uint32_t)((cd0.dict_bytes + 15u) & ~15ull);
+    staged = dn <= DD_ENT_MAX && cd0.dict_bytes <= DD_DICT_MAX && ent_off + 4u * dn <= dd_region;
+    if (staged) {
+      uint32_t* ent = (uint32_t*)(dd_lds + ent_off);
+      for (uint32_t i = threadIdx.x; i < dn; i += 64u * WPB) ent[i] = (cd0.dict_src[i] << 16) | cd0.dict_len[i];
+      // (a resource over the rest of the batch: a 16-byte load crossing the end of its range would
+      // return 0 as a whole; only entry bytes are ever read from the staged page)
+      const rsrc_t d0 = make_rsrc(bytes + cd0.dict_offset, n_bytes - cd0.dict_offset);
+      for (uint32_t o = 16u * threadIdx.x; o < ent_off; o += 16u * 64u * WPB)
+        *(u32x4*)(dd_lds + o) = __builtin_amdgcn_raw_buffer_load_b128(d0, (int)o, 0, 0);
+    }
+  }
+  __syncthreads();
+  if (page < 0) return;
+  const PageWork pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t j = (uint32_t)(chunks[c] >> 32);
+  if (!staged || pw.column != c0) {
+    // (never with the plan's layout: whole workgroups per column, dictionaries within DD_DICT_MAX /
+    // 2,048 entries and within the launch's dd_region)
+    if (lane == 0) report(err, err_count, page, 2, 0, PQG_ERR_INVALID_ARG);
+    return;
+  }
+  const uint32_t dict_n = uni(cd.dict_n), idw = uni(cd.dict_direct);
+  const uint32_t NF = uni(pw.n_values);
+  const uint32_t nok = uni((uint32_t)(sld(pstat + page) >> 32));  // values before a walk error
+  const uint32_t sh = (uint32_t)(pw.out_offset % E);
+  const uint32_t s_lo = j * CH > sh ? j * CH : sh;
+  const uint32_t s_hi = (j + 1) * CH < NF + sh ? (j + 1) * CH : NF + sh;
+  if (s_lo >= s_hi) return;
+  const uint32_t ok_hi = (nok < NF ? nok : NF) + sh;  // slots [ok_hi, s_hi): empty values
+  // the chunk's ids: tile t -> lane's 4 ids (u8: dword t; u16: dwords 2t, 2t + 1)
+  const uint8_t* idpag = (const uint8_t*)cd.blen + (pw.out_offset - sh) * (uint64_t)idw;
+  uint32_t idr[2 * CH_TILES];
+#pragma unroll
+  for (uint32_t t = 0; t < CH_TILES; t++) {
+    const uint32_t ts = j * CH + t * TV;
+    const uint8_t* ip = idpag + (uint64_t)(ts + E * lane) * idw;
+    const bool any = ts + E * lane < s_hi;  // (the id array is padded: the ids after a lane's first are readable)
+    if (idw == 1u) {
+      idr[2 * t] = any ? *(const __attribute__((address_space(1))) uint32_t*)ip : 0u;
+      idr[2 * t + 1] = 0u;
+    } else {
+      const u32x2 x = any ? *(const __attribute__((address_space(1))) u32x2*)ip : u32x2{0u, 0u};
+      idr[2 * t] = x.x;
+      idr[2 * t + 1] = x.y;
+    }
+  }
+  const uint32_t* ent = (const uint32_t*)(dd_lds + ent_off);
+  uint8_t* const dst = cd.binary_data;
+  const uint64_t cap = cd.binary_capacity;
+  int64_t* const opag = (int64_t*)cd.values + (pw.out_offset - sh);  // offsets of the page's slot 0
+  const bool o16 = ((uintptr_t)cd.values & 15u) == 0;
+  uint64_t run_base = uni64(bases[c]);
+#pragma unroll 1
+  for (uint32_t t = 0; t < CH_TILES; t++) {
+    const uint32_t ts = uni(j * CH + t * TV);
+    if (ts >= s_hi) break;
+    uint32_t ln[E], sr[E], ls = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < E; e++) {
+      const uint32_t sl = ts + E * lane + e;
+      const uint32_t id = idw == 1u ? (idr[2 * t] >> (8u * e)) & 0xFFu
+                                    : (idr[2 * t + (e >> 1)] >> (16u * (e & 1u))) & 0xFFFFu;
+      const uint32_t en = sl >= s_lo && sl < ok_hi && id < dict_n ? ent[id] : 0u;
+      ln[e] = en & 0xFFFFu;
+      sr[e] = en >> 16;
+      ls += ln[e];
+    }
+    const uint32_t inc = wave_incl_scan_u32_dpp(ls);
+    const uint32_t tot = uni(rdl(inc, WAVE - 1));
+    uint64_t o[E];
+    o[0] = run_base + (inc - ls);
+#pragma unroll
+    for (uint32_t e = 1; e < E; e++) o[e] = o[e - 1] + ln[e - 1];
+    int64_t* op = opag + ts + E * lane;
+    if (o16 && ts >= s_lo && ts + TV <= s_hi) {
+      gst_nt((i64x2*)op, i64x2{(int64_t)o[0], (int64_t)o[1]});
+      gst_nt((i64x2*)(op + 2), i64x2{(int64_t)o[2], (int64_t)o[3]});
+    } else {
+#pragma unroll
+      for (uint32_t e = 0; e < E; e++)
+        if (ts + E * lane + e >= s_lo && ts + E * lane + e < s_hi) gst(op + e, (int64_t)o[e]);
+    }
+    run_base += tot;
+    if (run_base <= cap) {
+#pragma unroll
+      for (uint32_t e = 0; e < E; e++) {
+        uint8_t* ob = dst + o[e];
+        uint32_t q = 0;
+        for (; q + 4u <= ln[e]; q += 4u) *(g32u*)(ob + q) = *(const u32u*)(dd_lds + sr[e] + q);
+        if (q < ln[e]) {
+          const uint32_t x = *(const u32u*)(dd_lds + sr[e] + q), r = ln[e] - q;
+          if (r & 2u) *(g16u*)(ob + q) = (uint16_t)x;
+          if (r & 1u) gst(ob + q + (r & 2u), (uint8_t)(x >> (8u * (r & 2u))));
+        }
+      }
+    } else {  // past the capacity (reported at sync with the size needed): the bytes that fit
+#pragma unroll
+      for (uint32_t e = 0; e < E; e++)
+        for (uint32_t q = 0; q < ln[e]; q++)
+          if (o[e] + q < cap) gst(dst + o[e] + q, dd_lds[sr[e] + q]);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -3046,9 +3069,8 @@ hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes
   hipLaunchKernelGGL(k_dd_bases, dim3(n_dd_cols), dim3(256), 0, st, cols, dd_cols, dd_start, sums);
   e = hipGetLastError();
   if (e != hipSuccess || !n_tile) return e;
-  const size_t lds = (size_t)dd_region + WPB * (XT_RUNS * 16 + XT_SEG + DD_IMG + 16);
-  hipLaunchKernelGGL(k_dict_str, dim3(n_tile), blk, lds, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks,
-                     n_chunks, pstat, err, err_count, sums, dd_region);
+  hipLaunchKernelGGL(k_dd_str, dim3(n_tile), blk, dd_region, st, bytes, n_bytes, work, cols, chunks, n_chunks, pstat,
+                     sums, err, err_count, dd_region);
   return hipGetLastError();
 }
 
