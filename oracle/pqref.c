@@ -1038,7 +1038,9 @@ int pqr_snappy_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t e
  * literals, a 2-byte little-endian offset (0 is invalid) and the match, which may overlap its own
  * output; the block ends with a sequence of literals only, at the end of the input. An empty
  * output is the single byte 0. Returns 0 and *out_len, or PQG_ERR_CORRUPT for malformed input or an
- * output length different from `expect`.
+ * output length different from `expect`. Parity unpinned for blocks that break the format's
+ * end-of-block rules (last 5 bytes literals, last match >= 12 bytes before the end): they are not
+ * checked here (nor by k_lz4raw), while aircompressor may reject them.
  * ------------------------------------------------------------------------------------------ */
 int pqr_lz4_raw_decompress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t expect, int64_t* out_len) {
   if (n <= 0) return PQG_ERR_CORRUPT;

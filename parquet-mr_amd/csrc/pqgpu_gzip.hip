@@ -9,8 +9,8 @@
 // pqr_gzip_decompress (oracle/gzip_ref.c), whose semantics this follows: members one after the other,
 // reading stops once the page's bytes are produced (the trailer of the member that completes the page
 // is not read), a member that ends earlier has its ISIZE checked before the next header.
-// (Its CRC-32 is not recomputed on the device: a corrupted non-final member whose DEFLATE data still
-// decodes to its ISIZE is accepted here and rejected by the oracle.)
+// A non-final member's CRC-32 is recomputed from the output (gz_member_crc; the token pre-pass hands
+// multi-member pages to k_gzip).
 //
 // One wave per page. The scalar unit runs the bit reader (a 64-bit container refilled 4 bytes at a
 // time from an LDS segment of the member) and decodes symbols through 512-entry first-level tables in
@@ -328,6 +328,46 @@ struct GzJobDev {  // = pqg_snappy_job
   uint32_t dst_size;
 };
 
+// CRC-32 (RFC 1952 8; reflected polynomial 0xEDB88320) of output bytes [b, e) through `ro`, after this
+// wave's stores: lane l takes a contiguous piece bit by bit, the pieces are joined in order with
+// crc(A B) = (crc(A) * x^(8|B|) mod P) ^ crc(B) (GF(2) arithmetic of zlib's crc32_combine). Only for
+// members that end before the page (rare: multi-member pages), so plain loops.
+__device__ __forceinline__ uint32_t gz_mulmodp(uint32_t a, uint32_t b) {
+  uint32_t pr = 0;
+  for (uint32_t m = 1u << 31; m; m >>= 1) {
+    if (a & m) pr ^= b;
+    b = (b & 1u) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+  }
+  return pr;
+}
+__device__ __forceinline__ uint32_t gz_x8n(uint32_t n) {  // x^(8n) mod P
+  uint32_t r = 1u << 31, pw = 1u << 23;                    // x^0, x^8
+  for (; n; n >>= 1) {
+    if (n & 1u) r = gz_mulmodp(pw, r);
+    pw = gz_mulmodp(pw, pw);
+  }
+  return r;
+}
+__device__ uint32_t gz_member_crc(rsrc_t ro, uint32_t b, uint32_t e) {
+  __builtin_amdgcn_s_waitcnt(0);
+  const uint32_t lane = lane_id(), len = e - b, S = (len + WAVE - 1u) / WAVE;
+  const uint32_t lb = b + (lane * S < len ? lane * S : len), le = b + ((lane + 1u) * S < len ? (lane + 1u) * S : len);
+  uint32_t c = 0xFFFFFFFFu;
+  for (uint32_t q = lb; q < le; q++) {
+    c ^= (__builtin_amdgcn_raw_buffer_load_b32(ro, (int)(q & ~3u), 0, 0) >> ((q & 3u) * 8u)) & 0xFFu;
+    for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+  }
+  c ^= 0xFFFFFFFFu;
+  uint32_t tot = 0;
+  const uint32_t xs = gz_x8n(S);
+  for (uint32_t l = 0; l < WAVE; l++) {
+    const uint32_t cl = uni(__builtin_amdgcn_readlane(c, l));
+    const uint32_t n_l = l * S < len ? ((l + 1u) * S < len ? S : len - l * S) : 0u;
+    if (n_l) tot = gz_mulmodp(n_l == S ? xs : gz_x8n(n_l), tot) ^ cl;
+  }
+  return tot;
+}
+
 __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, uint64_t src_bytes,
                                                uint8_t* __restrict__ dst, uint64_t dst_bytes,
                                                const GzJobDev* __restrict__ jobs, int n_jobs,
@@ -554,11 +594,13 @@ __global__ __launch_bounds__(WAVE) void k_gzip(const uint8_t* __restrict__ src, 
       if (res == 2u) full = true;
     } while (!code && !full && !last);
     if (code || full || op >= ulen) break;  // complete: the trailer is not read
-    // ---- trailer of a member that ends before the page is complete: ISIZE (CRC-32 not recomputed)
+    // ---- trailer of a member that ends before the page is complete: CRC-32 and ISIZE
     const uint32_t at = (uint32_t)((consumed() + 7u) >> 3);
     if (at + 8u > n) { code = PQG_ERR_CORRUPT; break; }
+    const uint32_t crc = byte_at(at) | (byte_at(at + 1u) << 8) | (byte_at(at + 2u) << 16) | (byte_at(at + 3u) << 24);
     const uint32_t isz = byte_at(at + 4u) | (byte_at(at + 5u) << 8) | (byte_at(at + 6u) << 16) | (byte_at(at + 7u) << 24);
     if (isz != op - member_start) { code = PQG_ERR_CORRUPT; break; }
+    if (gz_member_crc(ro, member_start, op) != crc) { code = PQG_ERR_CORRUPT; break; }
     q = at + 8u;
   }
   if (!code && op != ulen) code = PQG_ERR_EOF;
@@ -824,12 +866,8 @@ __device__ int32_t gq_job(GqLds& L, GqLane& T, rsrc_t rs, const GzJobDev& J, uin
       }
     } while (!last);
     if (op >= ulen) break;  // complete: the trailer is not read
-    // a member that ends before the page: ISIZE, then the next member
-    const uint32_t at = (uint32_t)((bp + 7u) >> 3) - so;
-    if (at + 8u > n) return GQ_INLINE;
-    const uint32_t isz = byte_at(at + 4u) | (byte_at(at + 5u) << 8) | (byte_at(at + 6u) << 16) | (byte_at(at + 7u) << 24);
-    if (isz != op - mstart) return GQ_INLINE;
-    q = at + 8u;
+    // a member that ends before the page (its CRC-32 is checked by k_gzip)
+    return GQ_INLINE;
   }
   // pages of long back-references (over 48 output bytes per record on average: few tokens, mostly
   // copying) are cheaper for the scalar decoder than for 189-byte replay windows

@@ -1755,9 +1755,15 @@ __device__ __forceinline__ void expand_level_runs_generic(const LevelWaveLds& L,
 template <int WB>
 __device__ __forceinline__ uint32_t decode_levels_bl(LevelWaveLds& L, rsrc_t rs, uint32_t beg, uint32_t end, int w,
                                                      uint32_t N, uint8_t* out, uint32_t max_def, bool count_nonnull,
-                                                     uint32_t* nonnull, int* err_code) {
+                                                     uint32_t* nonnull, int* err_code, uint64_t* diag = nullptr) {
   const uint32_t lane = lane_id();
   typedef uint32_t __attribute__((may_alias)) u32a;
+#ifdef PQG_DIAG
+  uint64_t dt[5] = {0, 0, 0, 0, 0}, dm = __builtin_amdgcn_s_memtime();
+#define LV_TICK(k) do { if (diag) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); dt[k] += t_ - dm; dm = t_; } } while (0)
+#else
+#define LV_TICK(k) do { } while (0)
+#endif
   PreWin win;
   win.rs = rs;
   win.seg = L.seg;
@@ -1792,6 +1798,7 @@ __device__ __forceinline__ uint32_t decode_levels_bl(LevelWaveLds& L, rsrc_t rs,
     }
     wave_sync();  // the previous window's chain / expansion reads are done
     ((u32a*)L.J[0])[lane] = js;
+    LV_TICK(0);
     *(u32x4*)(L.ecnt + 4u * lane) = u32x4{ec[0], ec[1], ec[2], ec[3]};
     ((u32a*)L.eval)[2u * lane] = ev[0] | (ev[1] << 16);
     ((u32a*)L.eval)[2u * lane + 1u] = ev[2] | (ev[3] << 16);
@@ -1818,6 +1825,7 @@ __device__ __forceinline__ uint32_t decode_levels_bl(LevelWaveLds& L, rsrc_t rs,
       }
     }
     nt = uni(nt);
+    LV_TICK(1);
     const uint32_t w0 = produced;
     uint32_t n_runs = 0, q = s;
     while (true) {  // batches of at most 64 chain headers
@@ -1875,7 +1883,12 @@ __device__ __forceinline__ uint32_t decode_levels_bl(LevelWaveLds& L, rsrc_t rs,
       s = nq;  // the chain goes on inside this window: next batch
     }
     wave_sync();
+    LV_TICK(2);
     if (n_runs) expand_level_runs<WB>(L, win, n_runs, w0, produced, w, out, max_def, count_nonnull, cnt, produced < N);
+    LV_TICK(3);
+#ifdef PQG_DIAG
+    dt[4] += 1;
+#endif
     if (produced >= N) break;
     // continue after the window's last chain header q
     const uint32_t ql = q >> 2, qb = q & 3u;
@@ -1911,6 +1924,11 @@ __device__ __forceinline__ uint32_t decode_levels_bl(LevelWaveLds& L, rsrc_t rs,
     }
   }
   if (WB > 0) level_carry_flush(L, out);
+#ifdef PQG_DIAG
+  if (diag && lane == 0)
+    for (int k = 0; k < 5; k++) diag[k] = dt[k];
+#endif
+#undef LV_TICK
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
   if (nonnull) *nonnull = cnt;
   *err_code = code;
@@ -1920,13 +1938,13 @@ __device__ __forceinline__ uint32_t decode_levels_bl(LevelWaveLds& L, rsrc_t rs,
 // decode_levels_bl with the tile expansion specialised for the section's bit width.
 __device__ __forceinline__ uint32_t decode_levels_w(LevelWaveLds& L, rsrc_t rs, uint32_t beg, uint32_t end, int w,
                                                     uint32_t N, uint8_t* out, uint32_t max_def, bool count_nonnull,
-                                                    uint32_t* nonnull, int* err_code) {
+                                                    uint32_t* nonnull, int* err_code, uint64_t* diag = nullptr) {
   switch (w) {
-    case 1: return decode_levels_bl<1>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 2: return decode_levels_bl<2>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 3: return decode_levels_bl<3>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
-    case 4: return decode_levels_bl<4>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
-    default: return decode_levels_bl<0>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code);
+    case 1: return decode_levels_bl<1>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code, diag);
+    case 2: return decode_levels_bl<2>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code, diag);
+    case 3: return decode_levels_bl<3>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code, diag);
+    case 4: return decode_levels_bl<4>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code, diag);
+    default: return decode_levels_bl<0>(L, rs, beg, end, w, N, out, max_def, count_nonnull, nonnull, err_code, diag);
   }
 }
 
@@ -2025,7 +2043,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5))) v
     uint32_t done = dl_be ? decode_levels_be(win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true,
                                              &nonnull, &code2)
                           : decode_levels_w(LL, win.rs, dl_beg, dl_end, wd, limit, def_out, (uint32_t)cd.max_def, true,
-                                             &nonnull, &code2);
+                                             &nonnull, &code2,
+#ifdef PQG_DIAG
+                                            pqg_diag_wph ? pqg_diag_wph + 8 * (uint64_t)page : nullptr
+#else
+                                            nullptr
+#endif
+                                             );
     if (code2) {
       uint64_t key = (((uint64_t)done << 1) | 1ull) << 8 | (uint64_t)code2;
       if (key < lvl_err_key) lvl_err_key = key;

@@ -439,6 +439,33 @@ def test_malformed_streams(decoder, prepass):
 
 
 @pytest.mark.gpu
+def test_crc_of_non_final_members(decoder, prepass):
+    """A member that ends before the page has its CRC-32 recomputed on the device (as the oracle and
+    Hadoop's GzipCodec stream do): one flipped CRC bit -> CORRUPT; the completing member's trailer is
+    not read. Members of 3 KB, 40 KB (stored + compressed) and 0 bytes."""
+    rng = np.random.default_rng(5)
+    parts = [b"abc" * 1000, rng.integers(0, 40, size=40000, dtype=np.uint8).tobytes(), b""]
+    streams, sizes, want = [], [], []
+    for raw in parts:
+        for lvl in (0, 6):
+            for flip in (0, 1, 1 << 31):
+                first = member(raw_deflate(raw, level=lvl), raw, crc=zlib.crc32(raw) ^ flip)
+                tail = b"tail" * 5000
+                streams.append(first + gzip.compress(tail))
+                sizes.append(len(raw) + len(tail))
+                want.append(abi.ERR_CORRUPT if flip else 0)
+                bad_last = member(raw_deflate(raw, level=lvl), raw, crc=zlib.crc32(raw) ^ 1)
+                streams.append(gzip.compress(tail) + bad_last)
+                sizes.append(len(raw) + len(tail))
+                want.append(0)  # the completing member's trailer is not read
+    got, status = _run(decoder, streams, sizes)
+    assert list(status) == want
+    for g, s, n, w in zip(got, streams, sizes, want):
+        if w == 0:
+            assert g == pqref.gzip_decompress(s, n)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,c", GZIP_CASES, ids=[f"{n}:{c['key']}" for n, c in GZIP_CASES])
 def test_gzip_fixture_end_to_end(decoder, name, c):
     """File bytes of a GZIP chunk -> GPU decompression into the batch -> GPU decode; the batch equals
