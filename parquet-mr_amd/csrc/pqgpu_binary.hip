@@ -1792,7 +1792,20 @@ __device__ __forceinline__ uint32_t bp_candidates(BinWalkLds& W, const BwBytes& 
   d[8] = cur.x;
   uint32_t m = 0;
   const int32_t rem0 = (int32_t)(end - 4u - base);
-  if (fast) {
+  if (fast && rem0 >= (int32_t)(BW_Q - 1u + 255u)) {
+    // len < 256 <=> the prefix's bytes 1..3 are zero (every such length fits the section here): a
+    // zero-byte SWAR per dword (bit 7 of byte k: byte k == 0), then per dword the AND of the flags
+    // shifted by 1, 2 and 3 bytes, its 4 bits packed by one multiply
+    uint32_t z[BW_Q / 4 + 1];
+#pragma unroll
+    for (uint32_t j = 0; j <= BW_Q / 4; j++) z[j] = ~((((d[j] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d[j])) & 0x80808080u;
+#pragma unroll
+    for (uint32_t j = 0; j < BW_Q / 4; j++) {
+      const uint32_t c = __builtin_amdgcn_alignbit(z[j + 1], z[j], 8u) & __builtin_amdgcn_alignbit(z[j + 1], z[j], 16u) &
+                         __builtin_amdgcn_alignbit(z[j + 1], z[j], 24u);
+      m |= ((((c >> 7) * 0x00204081u) >> 21) & 0xFu) << (4u * j);
+    }
+  } else if (fast) {
 #pragma unroll
     for (uint32_t q = 0; q < BW_Q; q++) {
       const uint32_t len = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);

@@ -1220,6 +1220,37 @@ __global__ __launch_bounds__(256) void k_dd_bases(const ColumnDev* __restrict__ 
   }
 }
 
+// Value bytes of the lane's E values (entry e: ln[e] bytes at LDS dd_lds + sr[e]), bytes [q0, q0 + 4 MD)
+// of each: all MD dwords of every value and its tail dword are read first, then the stores (whole
+// dwords, then a 2- and a 1-byte store for the last 1-3 bytes inside the range). Reads past an entry
+// stay inside the workgroup's LDS or return 0; no store leaves the value's own bytes.
+template <uint32_t MD>
+__device__ __forceinline__ void dd_put(uint8_t* dst, const uint64_t (&o)[4], const uint32_t (&ln)[4],
+                                       const uint32_t (&sr)[4], const uint8_t* dd_lds, uint32_t q0 = 0) {
+  typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
+  typedef uint32_t __attribute__((aligned(1), may_alias, address_space(1))) g32u;
+  typedef uint16_t __attribute__((aligned(1), may_alias, address_space(1))) g16u;
+  uint32_t x[4][MD], tl[4];
+#pragma unroll
+  for (uint32_t e = 0; e < 4; e++) {
+#pragma unroll
+    for (uint32_t k = 0; k < MD; k++) x[e][k] = *(const u32u*)(dd_lds + sr[e] + q0 + 4u * k);
+    tl[e] = *(const u32u*)(dd_lds + sr[e] + (ln[e] & ~3u));
+  }
+#pragma unroll
+  for (uint32_t e = 0; e < 4; e++) {
+    uint8_t* ob = dst + o[e];
+#pragma unroll
+    for (uint32_t k = 0; k < MD; k++)
+      if (q0 + 4u * k + 4u <= ln[e]) *(g32u*)(ob + q0 + 4u * k) = x[e][k];
+    const uint32_t q = ln[e] & ~3u, r = ln[e] & 3u;
+    if (r && q >= q0 && q < q0 + 4u * MD) {
+      if (r & 2u) *(g16u*)(ob + q) = (uint16_t)tl[e];
+      if (r & 1u) gst(ob + q + (r & 2u), (uint8_t)(tl[e] >> (8u * (r & 2u))));
+    }
+  }
+}
+
 // One wave per output chunk of k_dict_fused_dd (chunks of one column per workgroup: the plan pads the
 // chunk list). The chunk's ids are loaded first, all of them (one dword per tile per lane for u8 ids,
 // two for u16: no load after the first store, whose wait would drain the stores), then per 256-value
@@ -1286,6 +1317,21 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
     return;
   }
   const uint32_t dict_n = uni(cd.dict_n), idw = uni(cd.dict_direct);
+  // longest entry (its bytes decide the store shapes below) and whether every entry is 1 byte long
+  uint32_t md = 0, mn = 0xFFFFu;
+  for (uint32_t i = lane; i < dict_n; i += WAVE) {
+    const uint32_t l = ((const uint32_t*)(dd_lds + ent_off))[i] & 0xFFFFu;
+    md = l > md ? l : md;
+    mn = l < mn ? l : mn;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t a = (uint32_t)__shfl_xor((int)md, o), b = (uint32_t)__shfl_xor((int)mn, o);
+    md = a > md ? a : md;
+    mn = b < mn ? b : mn;
+  }
+  md = uni(md);
+  const bool one = uni(mn) == 1u && md == 1u;
   const uint32_t NF = uni(pw.n_values);
   const uint32_t nok = uni((uint32_t)(sld(pstat + page) >> 32));  // values before a walk error
   const uint32_t sh = (uint32_t)(pw.out_offset % E);
@@ -1348,16 +1394,19 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
     }
     run_base += tot;
     if (run_base <= cap) {
+      if (one && ls == E) {  // 1-byte entries, the lane's 4 values in range: one dword
+        uint32_t x = 0;
 #pragma unroll
-      for (uint32_t e = 0; e < E; e++) {
-        uint8_t* ob = dst + o[e];
-        uint32_t q = 0;
-        for (; q + 4u <= ln[e]; q += 4u) *(g32u*)(ob + q) = *(const u32u*)(dd_lds + sr[e] + q);
-        if (q < ln[e]) {
-          const uint32_t x = *(const u32u*)(dd_lds + sr[e] + q), r = ln[e] - q;
-          if (r & 2u) *(g16u*)(ob + q) = (uint16_t)x;
-          if (r & 1u) gst(ob + q + (r & 2u), (uint8_t)(x >> (8u * (r & 2u))));
-        }
+        for (uint32_t e = 0; e < E; e++) x |= (uint32_t)dd_lds[sr[e]] << (8u * e);
+        *(g32u*)(dst + o[0]) = x;
+      } else if (md <= 4u) {
+        dd_put<1>(dst, o, ln, sr, dd_lds);
+      } else if (md <= 8u) {
+        dd_put<2>(dst, o, ln, sr, dd_lds);
+      } else {
+        // 16 bytes per value a round: every LDS read of a round before its stores (a read per store
+        // waited for the LDS latency once per dword)
+        for (uint32_t q0 = 0; q0 < md; q0 += 16u) dd_put<4>(dst, o, ln, sr, dd_lds, q0);
       }
     } else {  // past the capacity (reported at sync with the size needed): the bytes that fit
 #pragma unroll
