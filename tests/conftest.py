@@ -37,3 +37,14 @@ def decoder():
     dec = D.Decoder(0, poison=0xA5)  # unwritten output elements show up as 0xA5A5...
     yield dec
     dec.close()
+
+
+@pytest.fixture(params=["wave_per_page", "lane_per_page"])
+def level_kernel(decoder, request):
+    """Level sections through both level kernels: k_levels (one wave per page, the default below
+    PQG_DISPATCH_LEVELS_LANE_MIN pages) and k_levels_lane (one lane per page; forced with 0)."""
+    from pqgpu import abi
+    if request.param == "lane_per_page":
+        decoder.set_dispatch(abi.DISPATCH_LEVELS_LANE_MIN, 0)
+    yield request.param
+    decoder.set_dispatch(abi.DISPATCH_LEVELS_LANE_MIN, 2048)
