@@ -226,16 +226,12 @@ void* pqg_ctx_stream(pqg_ctx* ctx);
  *   PQG_DISPATCH_GZIP_PREPASS_MIN pqg_gzip_decompress: pages of at least `value` output bytes take the
  *                                token pre-pass + replay, smaller ones the one-wave decoder (default
  *                                16384; 0 = every page); applies to later pqg_gzip_decompress calls
- *   PQG_DISPATCH_LEVELS_LANE_MIN nullable columns' level sections: from `value` pages with RLE level
- *                                sections on (default 2048; 0 = always), one GPU lane walks each page's
- *                                hybrid stream; fewer pages: one wave per page
  * Returns PQG_ERR_INVALID_ARG for an unknown key or value. Not thread-safe (like the ctx). */
 enum pqg_dispatch {
   PQG_DISPATCH_PLAIN_ONE_PASS = 1,
   PQG_DISPATCH_DICT_DIRECT = 2,
   PQG_DISPATCH_GZIP_PREPASS_MIN = 3,
-  PQG_DISPATCH_DICT_FUSED = 4,
-  PQG_DISPATCH_LEVELS_LANE_MIN = 5
+  PQG_DISPATCH_DICT_FUSED = 4
 };
 int pqg_ctx_set_dispatch(pqg_ctx* ctx, int key, int value);
 

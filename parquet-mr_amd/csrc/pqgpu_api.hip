@@ -152,7 +152,6 @@ struct pqg_plan {
   std::vector<PageWork> h_work;
   std::vector<int> cls_off, cls_n;  // into lists
   int levels_off = 0, levels_n = 0;
-  int lvlane_off = 0, lvlane_n = 0;  // pages of k_levels_lane (one lane per page)
   int n_scan_cols = 0;
   std::vector<int> page_cls;        // -1 if not launched
   std::vector<uint8_t> col_nullable;
@@ -232,7 +231,6 @@ struct pqg_ctx {
   bool dict_direct = true;  // PQG_DISPATCH_DICT_DIRECT
   bool dict_fused = true;   // PQG_DISPATCH_DICT_FUSED
   uint32_t gz_prepass_min = pqg::GZ_PREPASS_MIN;  // PQG_DISPATCH_GZIP_PREPASS_MIN
-  uint32_t lane_levels_min = pqg::LANE_LEVELS_MIN;  // PQG_DISPATCH_LEVELS_LANE_MIN
   RouterCache router;  // pqg_router_read_page
 };
 
@@ -314,10 +312,6 @@ int pqg_ctx_set_dispatch(pqg_ctx* ctx, int key, int value) {
       if (value != 0 && value != 1) return PQG_ERR_INVALID_ARG;
       ctx->dict_fused = value != 0;
       return PQG_OK;
-    case PQG_DISPATCH_LEVELS_LANE_MIN:
-      if (value < 0) return PQG_ERR_INVALID_ARG;
-      ctx->lane_levels_min = (uint32_t)value;
-      return PQG_OK;
     default: return PQG_ERR_INVALID_ARG;
   }
 }
@@ -372,7 +366,7 @@ int pqg_ctx_destroy(pqg_ctx* c) {
 // Kernels one launch of the plan runs (in its current modes).
 static int count_kernels(const pqg_plan* P) {
   const bool pf = P->plain_fused;
-  int k = (P->levels_n ? 1 : 0) + (P->lvlane_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
+  int k = (P->levels_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
   for (int c = 0; c < C_NCLS; c++) {
     const int n = P->cls_n[(size_t)c] - (c == C_BINP ? P->n_binp_seg + (pf ? P->n_binp_fused : 0) : 0);
     if (n && c == C_DD) k += P->dict_fused ? 3 : 4;
@@ -821,43 +815,10 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   P->dd_chunk_n = (uint32_t)chunk_list.size() - P->dd_chunk_off;
   P->n_dd_cols = (int)dd_cols.size();
   if (P->dd_chunk_n) P->dd_sums_off = take(8 * (uint64_t)P->dd_chunk_n);
-  // ---- level pages: one lane per page (k_levels_lane) for RLE sections of width <= 8 when there are
-  // enough of them to fill waves, one wave per page (k_levels) for the rest; a wave of lane pages
-  // spans at most 2 GiB of the batch (its buffer offsets are 32-bit)
-  std::vector<int> lane_list, wave_list;
-  {
-    std::vector<int> elig;
-    for (int p : lvl_list) {
-      const PageWork& w = P->h_work[(size_t)p];
-      const pqg_column_desc& c = cols[w.column];
-      const bool bp = w.version == 1 && ((c.max_rep > 0 && w.rl_encoding == PQG_BIT_PACKED) ||
-                                         (c.max_def > 0 && w.dl_encoding == PQG_BIT_PACKED));
-      if (!bp && c.max_rep <= 255 && c.max_def <= 255) elig.push_back(p);
-      else wave_list.push_back(p);
-    }
-    if (elig.size() >= (size_t)ctx->lane_levels_min && !elig.empty()) {
-      for (size_t g = 0; g < elig.size(); g += 64) {
-        const size_t e = std::min(elig.size(), g + 64);
-        uint64_t lo = ~0ull, hi = 0;
-        for (size_t k = g; k < e; k++) {
-          const PageWork& w = P->h_work[(size_t)elig[k]];
-          lo = std::min(lo, w.base);
-          hi = std::max(hi, w.base + w.size);
-        }
-        auto& dst = hi - lo < (1ull << 31) ? lane_list : wave_list;
-        dst.insert(dst.end(), elig.begin() + (long)g, elig.begin() + (long)e);
-      }
-    } else {
-      wave_list.insert(wave_list.end(), elig.begin(), elig.end());
-    }
-  }
-  // ---- flatten lists: [levels][lane levels][class 0]...[class n]
-  std::vector<int32_t> flat(wave_list.begin(), wave_list.end());
+  // ---- flatten lists: [levels][class 0]...[class n]
+  std::vector<int32_t> flat(lvl_list.begin(), lvl_list.end());
   P->levels_off = 0;
-  P->levels_n = (int)wave_list.size();
-  P->lvlane_off = (int)flat.size();
-  P->lvlane_n = (int)lane_list.size();
-  flat.insert(flat.end(), lane_list.begin(), lane_list.end());
+  P->levels_n = (int)lvl_list.size();
   P->cls_off.assign(C_NCLS, 0);
   P->cls_n.assign(C_NCLS, 0);
   for (int k = 0; k < C_NCLS; k++) {
@@ -1011,11 +972,8 @@ int pqg_plan_launch(pqg_plan* P) {
       return PQG_ERR_HIP;
   }
   hipError_t e = hipSuccess;
-  if (P->levels_n || P->lvlane_n) {
+  if (P->levels_n) {
     e = pqg::launch_levels(s, P->d_bytes, P->n_bytes, work, cols, lists + P->levels_off, P->levels_n, err, ecount);
-    if (e == hipSuccess)
-      e = pqg::launch_levels_lane(s, P->d_bytes, P->n_bytes, work, cols, lists + P->lvlane_off, P->lvlane_n, err,
-                                  ecount);
     if (e == hipSuccess)
       e = pqg::launch_scan(s, work, (const int32_t*)P->col_pages.p, (const int32_t*)P->col_page_start.p, P->n_scan_cols);
   }

@@ -97,8 +97,6 @@ hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t
                        ErrCount err_count);
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                          const int32_t* list, int n, uint64_t* err, ErrCount err_count);
-hipError_t launch_levels_lane(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
-                         const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_scan(hipStream_t st, PageWork* work, const int32_t* col_pages, const int32_t* col_page_start,
                        int n_cols);
 hipError_t launch_plain(int kind, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
@@ -147,9 +145,6 @@ hipError_t launch_lz4raw(hipStream_t st, const uint8_t* src, uint64_t src_bytes,
 // Huffman tables serially there; k_gzip's wave builds them in parallel, which small pages, with few
 // tokens to share the cost, need): PQG_DISPATCH_GZIP_PREPASS_MIN, default GZ_PREPASS_MIN.
 constexpr uint32_t GZ_PREPASS_MIN = 16384;
-// Level pages: one lane per page (k_levels_lane) from this many eligible pages on
-// (PQG_DISPATCH_LEVELS_LANE_MIN), one wave per page below.
-constexpr uint32_t LANE_LEVELS_MIN = 2048;
 hipError_t launch_gzip(hipStream_t st, const uint8_t* src, uint64_t src_bytes, uint8_t* dst, uint64_t dst_bytes,
                        const void* jobs, int n_jobs, int32_t* status, uint64_t* recs, int32_t* mode,
                        uint32_t prepass_min = GZ_PREPASS_MIN);

@@ -2116,319 +2116,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5))) v
   }
 }
 
-// ---------------------------------------------------------------------------
-// k_levels_lane: the level sections of many pages, one LANE per page. The hybrid stream of one page
-// is a serial chain (RunLengthBitPackingHybridDecoder.readNext, :80-109: header, then its run), so a
-// wave that walks one page spends its vector instructions on every byte position of every window
-// (k_levels' pre-decode: ~1,200 VALU per 256 section bytes) to find one header in three; here each
-// lane follows its own page's chain header by header, exactly as the reference decoder does, and 64
-// pages share every instruction. The lane's page bytes come through its own LDS window (96 bytes,
-// refilled forward by 16-byte buffer loads), its levels are gathered in a 16-byte register group
-// aligned to the output address and stored whole (byte stores only at the page's first and last
-// group, which neighbouring pages share). Same results and errors as k_levels; the host sends it the
-// pages with RLE level sections of width <= 8 when there are enough of them (lane_level_pages).
-constexpr uint32_t LL_WIN = 96;  // LDS window bytes per lane
-
-struct LaneLvl {
-  uint8_t* buf;     // the lane's LDS window: page bytes [lo, lo + LL_WIN)
-  rsrc_t rs;        // wave resource (from the wave's lowest page base)
-  uint32_t pb;      // page base relative to the resource
-  uint32_t lo;      // window start (page-relative, 16-aligned); 0xFFFFFFFF: empty
-  // output group: levels of slots [16 cg - mis, + 16) in acc, bytes [jv, jh) written
-  uint8_t* out;
-  uint32_t mis;
-  int32_t cg;
-  uint32_t jv, jh;
-  uint32_t acc[4];
-  uint32_t cnt, max_def;
-  bool count;
-
-  __device__ __forceinline__ void fill(uint32_t p) {  // window from (p - 16) on
-    lo = (p >= 16u ? p - 16u : 0u) & ~15u;
-    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (uint32_t q = 0; q < LL_WIN; q += 16u)
-      *(u32x4v*)(buf + q) = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(pb + lo + q), 0, 0);
-  }
-  // dword of page bytes [p, p + 4) (p >= lo after ensure); bytes past the batch read 0
-  __device__ __forceinline__ void ensure(uint32_t p, uint32_t n) {
-    if (lo == 0xFFFFFFFFu || p < lo || p + n > lo + LL_WIN) fill(p);
-  }
-  __device__ __forceinline__ uint32_t rd4(uint32_t p) const {
-    typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
-    return *(const u32u*)(buf + (p - lo));
-  }
-  __device__ __forceinline__ void flush() {
-    if (cg < 0) return;
-    const int64_t s0 = 16 * (int64_t)cg - (int64_t)mis;
-    if (count) {  // bytes == max_def inside [jv, jh)
-      const uint32_t rep = max_def * 0x01010101u;
-#pragma unroll
-      for (uint32_t c = 0; c < 4; c++) {
-        const uint32_t y = acc[c] ^ rep;
-        const uint32_t nz = ((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y;
-        cnt += (uint32_t)__builtin_popcount(~nz & 0x80808080u & tile_byte_mask((int32_t)jv, (int32_t)jh, (int32_t)c));
-      }
-    }
-    if (out) {
-      uint8_t* o = out + s0;
-      if (jv == 0 && jh == 16) {
-        gst((u32x4*)o, u32x4{acc[0], acc[1], acc[2], acc[3]});
-      } else {
-#pragma unroll
-        for (uint32_t c = 0; c < 4; c++) {  // (o is 16-byte aligned)
-          const uint32_t m = tile_byte_mask((int32_t)jv, (int32_t)jh, (int32_t)c);
-          if (m == 0xFFFFFFFFu) {
-            gst((uint32_t*)(o + 4u * c), acc[c]);
-          } else if (m) {
-#pragma unroll
-            for (uint32_t b = 0; b < 4; b++)
-              if ((m >> (8u * b)) & 1u) gst(o + 4u * c + b, (uint8_t)(acc[c] >> (8u * b)));
-          }
-        }
-      }
-    }
-    cg = -1;
-  }
-  // levels v (group-aligned bytes of the group holding slot s) for slots [s, min(e, group end)):
-  // returns the next slot
-  __device__ __forceinline__ uint32_t put(uint32_t s, uint32_t e, const uint32_t (&v)[4]) {
-    const uint32_t g = (s + mis) >> 4, j0 = (s + mis) & 15u;
-    const uint32_t ge = 16u * g - mis + 16u;
-    const uint32_t j1 = e < ge ? e + mis - 16u * g : 16u;
-    if ((int32_t)g != cg) {
-      flush();
-      cg = (int32_t)g;
-      jv = j0;
-      acc[0] = acc[1] = acc[2] = acc[3] = 0u;
-    }
-#pragma unroll
-    for (uint32_t c = 0; c < 4; c++) {
-      const uint32_t m = tile_byte_mask((int32_t)j0, (int32_t)j1, (int32_t)c);
-      acc[c] = (acc[c] & ~m) | (v[c] & m);
-    }
-    jh = j1;
-    if (j1 == 16u) flush();
-    return 16u * g - mis + j1;
-  }
-};
-
-// One level section [beg, end) of width w (1..8) -> slots [0, N) (readNext :80-109 per header; RLE
-// values saturate at 255, as k_levels). Returns the slots decoded before an error (N when none).
-__device__ __forceinline__ uint32_t lane_levels(LaneLvl& L, uint32_t beg, uint32_t end, uint32_t w, uint32_t N, int* err_code) {
-  uint32_t pos = beg, produced = 0;
-  int code = 0;
-  const uint32_t nb = (w + 7u) >> 3;
-  while (produced < N) {
-    if (pos >= end) { code = PQG_ERR_RLE_PAST_END; break; }
-    // readUnsignedVarInt (BytesUtils.java), as slow_header_g
-    uint32_t value = 0, i = 0, k = 0, bb;
-    L.ensure(pos, 8u);
-    for (;;) {
-      if (pos + k >= end) { code = PQG_ERR_EOF; break; }
-      if (k >= 8u) L.ensure(pos + k, 4u);
-      bb = L.rd4(pos + k) & 0xFFu;
-      if (!(bb & 0x80u)) break;
-      value |= (bb & 0x7Fu) << (i & 31u);
-      i += 7;
-      k++;
-    }
-    if (code) break;
-    const uint32_t header = value | (bb << (i & 31u)), hl = k + 1u;
-    const uint32_t left = N - produced;
-    if ((header & 1u) == 0u) {  // RLE: count, then ceil(w / 8) value bytes
-      if ((uint64_t)pos + hl + nb > end) { code = PQG_ERR_EOF; break; }
-      L.ensure(pos + hl, 4u);
-      const uint32_t vv = L.rd4(pos + hl) & 0xFFu;  // nb == 1 (w <= 8)
-      const uint32_t c = header >> 1;
-      const uint32_t take = c == 0u || c > left ? left : c;  // 0: the value repeats (Java's negative count)
-      const uint32_t rep = vv * 0x01010101u;
-      const uint32_t v[4] = {rep, rep, rep, rep};
-      const uint32_t e = produced + take;
-      for (uint32_t s = produced; s < e;) s = L.put(s, e, v);
-      produced = e;
-      pos = pos + hl + nb;
-    } else {  // PACKED: groups of 8 values, groups * w bytes (readFully of what is left)
-      const uint32_t groups = header >> 1;
-      if (groups == 0u) { code = PQG_ERR_EMPTY_PACKED_RUN; break; }
-      if (groups >= (1u << 28)) { code = PQG_ERR_CORRUPT; break; }
-      const uint32_t rlo = pos + hl;
-      const uint64_t nx = (uint64_t)rlo + (uint64_t)groups * w;
-      const uint32_t rhi = nx < (uint64_t)end ? (uint32_t)nx : end;
-      const uint32_t c = groups * 8u;
-      const uint32_t take = c < left ? c : left;
-      const uint32_t st = produced, e = produced + take;
-      for (uint32_t s = st; s < e;) {
-        const uint32_t j0 = (s + L.mis) & 15u;
-        // bit offset of the group's slot 0 from the run's data (negative: slots before the run, masked)
-        const int32_t base = ((int32_t)(s - st) - (int32_t)j0) * (int32_t)w;
-        const int32_t byte0 = (int32_t)rlo + (base >> 3);
-        const uint32_t bsh = (uint32_t)base & 7u;
-        const int32_t a4 = byte0 & ~3;
-        const uint32_t sb = (uint32_t)(byte0 - a4);
-        const uint32_t a4c = a4 > 0 ? (uint32_t)a4 : 0u;
-        L.ensure(a4c, 24u);
-        uint32_t y[6];
-#pragma unroll
-        for (uint32_t q = 0; q < 6; q++) {
-          const int32_t aq = a4 + 4 * (int32_t)q;
-          const uint32_t x = aq >= 0 ? L.rd4((uint32_t)aq) : 0u;
-          const int32_t kp = (int32_t)rhi - aq;  // bytes at or past the read end are 0 (readNext :96-99)
-          y[q] = x & (kp >= 4 ? 0xFFFFFFFFu : (kp <= 0 ? 0u : (1u << (8 * kp)) - 1u));
-        }
-        uint32_t z[5], D[5];
-#pragma unroll
-        for (uint32_t q = 0; q < 5; q++) z[q] = __builtin_amdgcn_alignbyte(y[q + 1], y[q], sb);
-#pragma unroll
-        for (uint32_t q = 0; q < 4; q++) D[q] = __builtin_amdgcn_alignbit(z[q + 1], z[q], bsh);
-        D[4] = z[4] >> bsh;
-        uint32_t v[4];
-        if (w == 1u) {
-#pragma unroll
-          for (uint32_t q = 0; q < 4; q++) v[q] = (((D[0] >> (4u * q)) & 0xFu) * 0x204081u) & 0x01010101u;
-        } else {
-          // dword q: slots 4q .. 4q + 3 = bits [4 q w, 4 q w + 4 w) of D (4 w <= 32)
-          const uint32_t m = (1u << w) - 1u;
-#pragma unroll
-          for (uint32_t q = 0; q < 4; q++) {
-            const uint32_t P = 4u * q * w, wi = P >> 5, bo = P & 31u;
-            const uint32_t lo = wi == 0 ? D[0] : wi == 1 ? D[1] : wi == 2 ? D[2] : D[3];
-            const uint32_t hi = wi == 0 ? D[1] : wi == 1 ? D[2] : wi == 2 ? D[3] : D[4];
-            const uint32_t t = __builtin_amdgcn_alignbit(hi, lo, bo);
-            v[q] = (t & m) | (((t >> w) & m) << 8) | (((t >> (2u * w)) & m) << 16) | (((t >> (3u * w)) & m) << 24);
-          }
-        }
-        s = L.put(s, e, v);
-      }
-      produced = e;
-      pos = rhi;
-    }
-  }
-  L.flush();
-  *err_code = code;
-  return code ? produced : N;
-}
-
-__global__ __launch_bounds__(64 * WPB) void k_levels_lane(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
-                                                           PageWork* __restrict__ work,
-                                                           const ColumnDev* __restrict__ cols,
-                                                           const int32_t* __restrict__ list, int n_list,
-                                                           uint64_t* err, ErrCount err_count) {
-  __shared__ __attribute__((aligned(16))) uint8_t lwin[64 * WPB * LL_WIN];
-  const uint32_t i = blockIdx.x * 64u * WPB + threadIdx.x;
-  const int page = i < (uint32_t)n_list ? list[i] : -1;
-  // the wave's resource starts at its lowest page base (the host keeps a wave's pages within 2 GiB)
-  uint64_t b = page >= 0 ? work[page].base : ~0ull;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const uint64_t y = __shfl_xor(b, o);
-    b = y < b ? y : b;
-  }
-  b = uni64(b);
-  if (b == ~0ull) return;
-  if (page < 0) return;  // (no cross-lane operation follows)
-  const PageWork pw = work[page];
-  const ColumnDev& cd = cols[pw.column];
-  LaneLvl L;
-  L.buf = lwin + threadIdx.x * LL_WIN;
-  L.rs = make_rsrc(bytes + b, n_bytes - b);
-  L.pb = (uint32_t)(pw.base - b);
-  L.lo = 0xFFFFFFFFu;
-  const uint32_t size = pw.size, nslots = pw.num_slots;
-  const uint32_t max_rep = (uint32_t)cd.max_rep, max_def = (uint32_t)cd.max_def;
-  const uint32_t wr = max_rep ? 32u - __builtin_clz(max_rep) : 0u;
-  const uint32_t wd = max_def ? 32u - __builtin_clz(max_def) : 0u;
-  uint32_t rl_beg = 0, rl_end = 0, dl_beg = 0, dl_end = 0, data_beg = 0;
-  int init_err = 0, init_phase = 0;
-  if (pw.version == 2) {
-    rl_end = pw.rl_len;
-    dl_beg = rl_end;
-    dl_end = rl_end + pw.dl_len;
-    data_beg = dl_end;
-    if ((uint64_t)pw.rl_len + pw.dl_len > size) init_err = PQG_ERR_CORRUPT;
-  } else {  // V1: RLE sections with a 4-byte length prefix (the host sends BIT_PACKED pages to k_levels)
-    uint32_t p = 0;
-    for (int which = 0; which < 2 && !init_err; which++) {
-      const uint32_t maxl = which == 0 ? max_rep : max_def;
-      const int enc = which == 0 ? pw.rl_encoding : pw.dl_encoding;
-      uint32_t bgn = p, en = p;
-      if (maxl > 0) {
-        if (enc != PQG_RLE) { init_err = PQG_ERR_UNSUPPORTED; init_phase = which; break; }
-        if (p + 4u > size) { init_err = PQG_ERR_EOF; init_phase = which; break; }
-        L.ensure(p, 4u);
-        const int32_t len = (int32_t)L.rd4(p);
-        if (len < 0) { init_err = PQG_ERR_CORRUPT; init_phase = which; break; }
-        if ((uint64_t)p + 4u + (uint32_t)len > size) { init_err = PQG_ERR_EOF; init_phase = which; break; }
-        bgn = p + 4u;
-        en = bgn + (uint32_t)len;
-        p = en;
-      } else if (enc != PQG_RLE && enc != PQG_BIT_PACKED) {
-        init_err = PQG_ERR_UNSUPPORTED;
-        init_phase = which;
-        break;
-      }
-      if (which == 0) { rl_beg = bgn; rl_end = en; } else { dl_beg = bgn; dl_end = en; }
-    }
-    data_beg = p;
-  }
-  if (init_err) {
-    report(err, err_count, page, 0, (uint64_t)init_phase, init_err);
-    work[page].n_values = 0;
-    work[page].data_begin = size;
-    return;
-  }
-  uint8_t* rep_out = cd.rep_levels ? cd.rep_levels + pw.slot_offset : nullptr;
-  uint8_t* def_out = cd.def_levels ? cd.def_levels + pw.slot_offset : nullptr;
-  uint32_t limit = nslots;
-  uint64_t key = ~0ull;
-  const uint32_t zero[4] = {0u, 0u, 0u, 0u};
-  L.cnt = 0;
-  L.count = false;
-  L.cg = -1;
-  if (wr > 0 || rep_out) {
-    L.out = rep_out;
-    L.mis = rep_out ? (uint32_t)((uintptr_t)rep_out & 15u) : 0u;
-    L.max_def = 0;
-    if (wr > 0) {
-      int code = 0;
-      const uint32_t done = lane_levels(L, rl_beg, rl_end, wr, nslots, &code);
-      if (code) {
-        limit = done;
-        key = ((uint64_t)done << 1) << 8 | (uint64_t)code;
-      }
-    } else {
-      for (uint32_t s = 0; s < nslots;) s = L.put(s, nslots, zero);
-      L.flush();
-    }
-  }
-  uint32_t nonnull;
-  L.out = def_out;
-  L.mis = def_out ? (uint32_t)((uintptr_t)def_out & 15u) : 0u;
-  L.cg = -1;
-  if (wd > 0) {
-    L.cnt = 0;
-    L.count = true;
-    L.max_def = max_def;
-    int code = 0;
-    const uint32_t done = lane_levels(L, dl_beg, dl_end, wd, limit, &code);
-    if (code) {
-      const uint64_t k2 = (((uint64_t)done << 1) | 1ull) << 8 | (uint64_t)code;
-      key = k2 < key ? k2 : key;
-    }
-    nonnull = L.cnt;
-  } else {
-    nonnull = limit;
-    if (def_out) {
-      L.count = false;
-      for (uint32_t s = 0; s < limit;) s = L.put(s, limit, zero);
-      L.flush();
-    }
-  }
-  if (key != ~0ull) report_key(&err[3 * (uint64_t)page + 1], err_count, key);
-  work[page].n_values = nonnull;
-  work[page].data_begin = data_beg;
-}
-
 // Exclusive scan of non-null counts per column (one workgroup per column).
 __global__ __launch_bounds__(256) void k_scan_offsets(PageWork* __restrict__ work, const int32_t* __restrict__ col_pages,
                                                       const int32_t* __restrict__ col_page_start, int n_cols) {
@@ -3462,13 +3149,6 @@ hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes,
                          const int32_t* list, int n, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_levels, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
-  return hipGetLastError();
-}
-
-hipError_t launch_levels_lane(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
-                              const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_levels_lane, dim3((n + 64 * WPB - 1) / (64 * WPB)), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   return hipGetLastError();
 }
 

@@ -218,4 +218,3 @@ DISPATCH_PLAIN_ONE_PASS = 1
 DISPATCH_DICT_DIRECT = 2
 DISPATCH_GZIP_PREPASS_MIN = 3  # pqg_gzip_decompress: smallest page (output bytes) for the token pre-pass
 DISPATCH_DICT_FUSED = 4  # dictionary pages: 1 = walk + expansion in one launch, 0 = two launches
-DISPATCH_LEVELS_LANE_MIN = 5  # level pages: one lane per page from this many pages on (default 2048)

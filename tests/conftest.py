@@ -38,13 +38,3 @@ def decoder():
     yield dec
     dec.close()
 
-
-@pytest.fixture(params=["wave_per_page", "lane_per_page"])
-def level_kernel(decoder, request):
-    """Level sections through both level kernels: k_levels (one wave per page, the default below
-    PQG_DISPATCH_LEVELS_LANE_MIN pages) and k_levels_lane (one lane per page; forced with 0)."""
-    from pqgpu import abi
-    if request.param == "lane_per_page":
-        decoder.set_dispatch(abi.DISPATCH_LEVELS_LANE_MIN, 0)
-    yield request.param
-    decoder.set_dispatch(abi.DISPATCH_LEVELS_LANE_MIN, 2048)

@@ -15,7 +15,7 @@ GPU_DBA = True  # DELTA_BYTE_ARRAY on the device
 
 
 @pytest.mark.parametrize("name,c", CASES, ids=[f"{n}:{c['key']}:{c['path']}" for n, c in CASES])
-def test_gpu_decodes_fixture(decoder, level_kernel, name, c):
+def test_gpu_decodes_fixture(decoder, name, c):
     ch, expected = load_chunk(name, c)
     batch = batch_of(ch)
     cols, st = decoder.decode(decoder.upload(batch), check=False)
@@ -33,7 +33,7 @@ def test_gpu_decodes_fixture(decoder, level_kernel, name, c):
         assert np.array_equal(cols[0].rep_levels[:batch.column_slots[0]].cpu().numpy(), ref.columns[0]["rep_levels"])
 
 
-def test_gpu_all_fixtures_one_batch(decoder, level_kernel):
+def test_gpu_all_fixtures_one_batch(decoder):
     """Every fixture chunk decoded in ONE pqg_decode call (many columns, mixed encodings)."""
     chunks, exp = [], []
     for name, c in CASES:

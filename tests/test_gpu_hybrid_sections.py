@@ -146,7 +146,7 @@ def run_both(decoder, chunks):
 
 @pytest.mark.parametrize("max_def", [1, 3, 5, 15, 31, 63, 127, 254])
 @pytest.mark.parametrize("shape", ["long_packed", "long_rle", "mixed"])
-def test_levels_hand_built_runs(decoder, level_kernel, max_def, shape):
+def test_levels_hand_built_runs(decoder, max_def, shape):
     """Packed runs of up to 300 groups (an 8-bit-level page: 2,400 data bytes in one run; max_def 254 is the
     device limit, pqg_plan_create: 255 is UNSUPPORTED), RLE runs of
     up to 5,000 slots, pages of 30,000-60,000 slots, every width 1..8."""
@@ -167,7 +167,7 @@ def test_levels_hand_built_runs(decoder, level_kernel, max_def, shape):
 
 
 @pytest.mark.parametrize("max_def", [1, 3])
-def test_levels_one_rle_run_per_page(decoder, level_kernel, max_def):
+def test_levels_one_rle_run_per_page(decoder, max_def):
     """Pages without nulls: one RLE header for 300,000 slots (the whole wave fills the level image,
     several images per page)."""
     w = int(max_def).bit_length()
@@ -181,7 +181,7 @@ def test_levels_one_rle_run_per_page(decoder, level_kernel, max_def):
     run_both(decoder, [level_chunk(secs, max_def)])
 
 
-def test_levels_large_random_page(decoder, level_kernel):
+def test_levels_large_random_page(decoder):
     """200,000 random 2-bit levels in one page (mostly bit-packed): many level images and
     super-windows per page."""
     rng = np.random.default_rng(5)
@@ -191,7 +191,7 @@ def test_levels_large_random_page(decoder, level_kernel):
 
 
 @pytest.mark.parametrize("case", ["wide_rle_value", "zero_count_rle", "short_section", "truncated_group"])
-def test_levels_slow_path_headers(decoder, level_kernel, case):
+def test_levels_slow_path_headers(decoder, case):
     """Sections with headers outside the pre-decode's fast path: its result (levels, counts, error
     at the oracle's slot) must be the same."""
     rng = np.random.default_rng(len(case))

@@ -98,7 +98,7 @@ def test_dict_known_answer_pages(decoder):
                                        (abi.PLAIN, abi.INT32), (abi.DELTA_BINARY_PACKED, abi.INT64),
                                        (abi.DELTA_BINARY_PACKED, abi.INT32), (abi.PLAIN, abi.BOOLEAN)])
 @pytest.mark.parametrize("null_frac", [0.0, 0.1, 0.9, 1.0])
-def test_optional_columns(decoder, level_kernel, version, enc, ptype, null_frac):
+def test_optional_columns(decoder, version, enc, ptype, null_frac):
     n_slots = 50_000
     dl = nulls(n_slots, null_frac, seed=5)
     n = int(dl.sum())
@@ -118,7 +118,7 @@ def test_optional_columns(decoder, level_kernel, version, enc, ptype, null_frac)
 
 
 @pytest.mark.parametrize("version", [1, 2])
-def test_nested_list_levels(decoder, level_kernel, version):
+def test_nested_list_levels(decoder, version):
     """Config 5 shape: optional group (LIST) { repeated group list { optional int64 element } }:
     max_rep 1, max_def 3. Lists ~ Poisson(3), 10% null lists, 10% null elements."""
     rng = np.random.default_rng(11)
@@ -325,11 +325,10 @@ def test_error_missing_dictionary(decoder):
 
 
 @pytest.mark.parametrize("seed", range(16))
-def test_error_level_sections_corrupted(decoder, level_kernel, seed):
+def test_error_level_sections_corrupted(decoder, seed):
     """Level sections with bytes overwritten at random, or cut short (V2: the section lengths of the
     header kept, V1: the length prefix kept): the first error (code, page, slot) or, with none, the
-    levels and values equal the oracle's, through both level kernels. Nested (rep + def) columns for
-    odd seeds."""
+    levels and values equal the oracle's. Nested (rep + def) columns for seeds 2, 3 mod 4."""
     rng = np.random.default_rng(seed)
     version = 1 + seed % 2
     n = 8000
@@ -364,7 +363,7 @@ def test_error_level_sections_corrupted(decoder, level_kernel, seed):
     run_both(decoder, [ch], expect_error=ref.code != 0)
 
 
-def test_error_level_section_length(decoder, level_kernel):
+def test_error_level_section_length(decoder):
     dl = nulls(4000, 0.2, seed=1)
     ch = make(abi.DOUBLE, np.random.default_rng(0).standard_normal(int(dl.sum())), abi.PLAIN, def_levels=dl,
               max_def=1, version=1, page_rows=1000)
@@ -424,7 +423,7 @@ def test_host_path_extent_past_buffer(decoder, what, over):
 @pytest.mark.parametrize("max_def", [1, 2, 5, 12, 20, 40])
 @pytest.mark.parametrize("shape", ["random", "runs"])
 @pytest.mark.parametrize("version", [1, 2])
-def test_rle_level_widths(decoder, level_kernel, max_def, shape, version):
+def test_rle_level_widths(decoder, max_def, shape, version):
     """RLE / bit-packed hybrid definition levels of bit widths 1..6 (the level expansion is
     specialised per width up to 4), random (mostly bit-packed) and run-heavy (mostly RLE with
     short bit-packed stretches) sequences."""
@@ -443,7 +442,7 @@ def test_rle_level_widths(decoder, level_kernel, max_def, shape, version):
 
 
 @pytest.mark.parametrize("max_def,max_rep", [(1, 0), (2, 0), (3, 1), (7, 0)])
-def test_v1_bit_packed_levels(decoder, level_kernel, max_def, max_rep):
+def test_v1_bit_packed_levels(decoder, max_def, max_rep):
     """Deprecated BIT_PACKED (big-endian) level sections of old parquet-mr V1 pages
     (ByteBitPackingValuesReader(maxLevel, BIG_ENDIAN))."""
     rng = np.random.default_rng(max_def * 10 + max_rep)
