@@ -1695,7 +1695,8 @@ __device__ __forceinline__ void expand_level_runs_generic(const LevelWaveLds& L,
                                                           uint32_t s_lo, uint32_t s_hi, int w, uint8_t* out,
                                                           uint32_t max_def, bool count_nonnull, uint32_t& cnt);
 
-// WB = 1..4: the specialised tile expansion; WB = 0: any width.
+// WB = 1..4: the specialised tile expansion; WB = 0: any width. (A level image in LDS written one run
+// per lane, then read 16 slots per lane, measured no faster on C3: 0.990 vs 0.981 ms, profiles/r05/lv_image.)
 template <int WB>
 __device__ __forceinline__ void expand_level_runs(LevelWaveLds& L, const PreWin& win, uint32_t n_run,
                                                   uint32_t s_lo, uint32_t s_hi, int w, uint8_t* out,

@@ -1,6 +1,6 @@
 set -e
-O=gpurun_out/r05r; mkdir -p $O
-bash tools/ab_c4prof.sh r05r_dd 8,9,13,14 abx/libnb.so abx/libno.so abx/libnone.so
-export TMPDIR=/tmp
-PQGPU_LIB=$PWD/abx/liblw.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/lw -o run -- python3 -u tools/bench_suite.py c3_mixed --cpu-budget 0 --steps 5 --warmup 1 --no-verify > $O/lw.jsonl 2> $O/lw.err || { tail -20 $O/lw.err; exit 1; }
-python3 tools/kstats.py $O/lw | head -8
+O=gpurun_out/r05s; mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_hybrid_sections.py tests/test_gpu_fixtures.py tests/test_gpu_fullsize.py tests/test_gpu_assembly.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+bash tools/ab_suite_prof.sh r05s_lv "c3_mixed c5_levels" abx/libbase.so parquet-mr_amd/pqgpu/libpqgpu.so
+bash tools/c4_pmc_group.sh r05s 8,9,13,14
