@@ -113,25 +113,49 @@ def pyarrow_baseline(values, budget_s, threads):
 
 
 def link_ceiling(out_bytes, in_bytes, device, reps=5):
-    """The PCIe link alone on this box: one pinned hipMemcpyAsync of the decoded column's size
-    (device -> host) and of the encoded pages' size (host -> device), best of `reps`, in GB/s."""
+    """The PCIe link alone on this box, best of `reps`, in GB/s: one pinned hipMemcpyAsync of the
+    decoded column's size (device -> host) and of the encoded pages' size (host -> device); the
+    decoded size as 32 MiB pieces alternating over two streams (two DMA engines, as pqg_decode_host
+    issues it); and the host's own copy of that size from pinned into a touched pageable array
+    (torch's threaded CPU copy), the last stage of pqg_decode_host."""
     import torch
     res = {}
     s = torch.cuda.Stream(device)
-    for name, n, d2h in (("d2h_pinned_gbs", out_bytes, True), ("h2d_pinned_gbs", in_bytes, False)):
-        dev_t = torch.empty(n, dtype=torch.uint8, device=device)
-        host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
-        host.fill_(1)
+    s2 = torch.cuda.Stream(device)
+
+    def best_of(fn, sync):
         best = None
         for _ in range(reps):
             torch.cuda.synchronize(device)
             t0 = time.perf_counter()
-            with torch.cuda.stream(s):
-                (host.copy_(dev_t, non_blocking=True) if d2h else dev_t.copy_(host, non_blocking=True))
-            s.synchronize()
+            fn()
+            sync()
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
-        res[name] = n / best / 1e9
+        return best
+
+    for name, n, d2h in (("d2h_pinned_gbs", out_bytes, True), ("h2d_pinned_gbs", in_bytes, False)):
+        dev_t = torch.empty(n, dtype=torch.uint8, device=device)
+        host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        host.fill_(1)
+
+        def one():
+            with torch.cuda.stream(s):
+                (host.copy_(dev_t, non_blocking=True) if d2h else dev_t.copy_(host, non_blocking=True))
+        res[name] = n / best_of(one, s.synchronize) / 1e9
+        if d2h:
+            piece = 32 << 20
+
+            def two():
+                for k, a in enumerate(range(0, n, piece)):
+                    with torch.cuda.stream(s2 if k & 1 else s):
+                        host[a:a + piece].copy_(dev_t[a:a + piece], non_blocking=True)
+            res["d2h_pinned_2streams_gbs"] = n / best_of(two, lambda: (s.synchronize(), s2.synchronize())) / 1e9
+            page = torch.empty(n, dtype=torch.uint8)
+            page.fill_(0)
+            res["host_pinned_to_pageable_gbs"] = n / best_of(lambda: page.copy_(host), lambda: None) / 1e9
+            res["host_copy_threads"] = torch.get_num_threads()
+            del page
         del dev_t, host
     res["bytes"] = {"d2h": out_bytes, "h2d": in_bytes}
     return res
@@ -473,15 +497,27 @@ def main():
             native_s.append(dec.last_native_s)
             assert rc2 == 0
         e2e_s = min(native_s)
+        staged_s = []
+        for _ in range(3):  # the staged path: outputs stay in the library's pinned buffer (no host copy)
+            rc3, _, res3, _ = dec.decode_staged(batch)
+            staged_s.append(dec.last_native_s)
+            assert rc3 == 0 and res3[0]["n_values"] == n
         link = link_ceiling(n * 8, data_bytes, dec.device)
-        # the link's share of the host path: the output's D2H at the measured pinned ceiling
+        # the link's share of the host path: the output's D2H at the measured pinned ceilings
         d2h_floor_s = n * 8 / (link["d2h_pinned_gbs"] * 1e9)
+        d2h2_floor_s = n * 8 / (link["d2h_pinned_2streams_gbs"] * 1e9)
         e2e = {"values_per_s": n / e2e_s, "seconds": e2e_s, "native_call_s": native_s,
                "output_gb_per_s": n * 8 / e2e_s / 1e9, "link": link,
                "frac_of_d2h_ceiling": d2h_floor_s / e2e_s,
+               "frac_of_d2h_2streams_ceiling": d2h2_floor_s / e2e_s,
                "with_python_alloc_s": times,
                "path": "pqg_decode_host (one C call: host page bytes -> pinned -> H2D, plan, decode, sync, "
-                       "chunked D2H -> caller's int64 array); output array allocated and touched beforehand"}
+                       "chunked D2H -> caller's int64 array); output array allocated and touched beforehand",
+               "staged": {"seconds": min(staged_s), "native_call_s": staged_s,
+                          "output_gb_per_s": n * 8 / min(staged_s) / 1e9,
+                          "frac_of_d2h_2streams_ceiling": d2h2_floor_s / min(staged_s),
+                          "path": "pqg_decode_staged (page bytes already in the pinned input; outputs left in "
+                                  "the pinned output for the caller to read in place)"}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

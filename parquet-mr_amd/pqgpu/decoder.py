@@ -480,7 +480,8 @@ class Decoder:
     def decode_staged(self, batch):
         """The staged host path (pqg_host_input, pqg_decode_staged, pqg_staged_column): the page
         bytes are written into the library's pinned input, the outputs are read from its pinned
-        output. Returns (rc, status, per-column dict like decode_host, page counts)."""
+        output. Returns (rc, status, per-column dict like decode_host, page counts);
+        self.last_native_s = seconds inside pqg_decode_staged."""
         L = native.lib()
         buf = C.c_void_p()
         native.check(L.pqg_host_input(self.ctx, batch.data.size, C.byref(buf)), what="pqg_host_input")
@@ -492,8 +493,10 @@ class Decoder:
         counts = np.zeros(max(1, batch.n_pages), dtype=np.uint32)
         pages = np.ascontiguousarray(batch.pages)
         st = abi.Status()
+        t0 = time.perf_counter()
         rc = L.pqg_decode_staged(self.ctx, batch.data.size, C.addressof(descs), len(batch.columns),
                                  pages.ctypes.data if len(pages) else None, len(pages), counts.ctypes.data, C.byref(st))
+        self.last_native_s = time.perf_counter() - t0
         if rc != abi.OK and batch.columns:
             probe = abi.StagedOutput()
             if L.pqg_staged_column(self.ctx, 0, C.byref(probe)) != abi.OK:
