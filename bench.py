@@ -228,6 +228,8 @@ def run_c4(args, world, rank, devi):
     dec = D.Decoder(devi, poison=0xA5)
     if args.dict_split:
         dec.set_dispatch(abi.DISPATCH_DICT_FUSED, 0)
+    if args.plain_mode is not None:
+        dec.set_dispatch(abi.DISPATCH_PLAIN_ONE_PASS, args.plain_mode)
     dbatch = dec.upload(batch)
     cols, st = dec.decode(dbatch)  # sizes the BYTE_ARRAY buffers
     for c in cols:  # poison: the plan's first launch must write every element itself
@@ -369,6 +371,8 @@ def main():
                     help="c2: the headline (BASELINE metric); c4: lineitem 16 columns, strong scaling")
     ap.add_argument("--rows", type=int, default=None, help="c2: rows per GPU (100M); c4: rows in total (1B)")
     ap.add_argument("--c4-templates", type=int, default=4, help="c4: distinct synthetic row groups")
+    ap.add_argument("--plain-mode", type=int, default=None,
+                    help="PQG_DISPATCH_PLAIN_ONE_PASS override (A/B of the PLAIN BYTE_ARRAY kernels)")
     ap.add_argument("--dict-split", action="store_true",
                     help="diagnostics: dictionary walk and expansion as two launches (PQG_DISPATCH_DICT_FUSED = 0)")
     ap.add_argument("--c4-cols", default=None,

@@ -217,8 +217,9 @@ void* pqg_ctx_stream(pqg_ctx* ctx);
 /* Kernel-choice overrides for plans created on the ctx afterwards (tests and A/B measurements;
  * the defaults are the measured choices). Decoded results are the same under every setting.
  *   PQG_DISPATCH_PLAIN_ONE_PASS  PLAIN-only BYTE_ARRAY columns: 0 = per-value path (walk, offset
- *                                scan, copy), 2 = one pass, tiles below 4,096 PLAIN pages and one
- *                                wave per page from there (default), 3 = one pass, one wave per page
+ *                                scan, copy), 1 = one pass, tiles, 2 = one pass, tiles below 4,096
+ *                                PLAIN pages and one wave per page from there (default), 3 = one
+ *                                pass, one wave per page
  *   PQG_DISPATCH_DICT_DIRECT     dictionary BYTE_ARRAY columns with small dictionaries: 1 = ids
  *                                mapped straight to lengths and bytes (default), 0 = ids, then map
  *   PQG_DISPATCH_DICT_FUSED      dictionary pages: 1 = walk and expansion in one launch (default),

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -297,7 +298,7 @@ int pqg_ctx_set_dispatch(pqg_ctx* ctx, int key, int value) {
   if (!ctx) return PQG_ERR_INVALID_ARG;
   switch (key) {
     case PQG_DISPATCH_PLAIN_ONE_PASS:
-      if (value != 0 && value != 2 && value != 3) return PQG_ERR_INVALID_ARG;
+      if (value < 0 || value > 3) return PQG_ERR_INVALID_ARG;
       ctx->plain_mode = value;
       return PQG_OK;
     case PQG_DISPATCH_DICT_DIRECT:
@@ -597,7 +598,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   // pqg_ctx_set_dispatch(PQG_DISPATCH_PLAIN_ONE_PASS) overrides the choice (tests and A/B): 0 = no
   // one-pass path (every plan per value), 3 = every plan one wave per page
   const int plain_mode = ctx->plain_mode;
-  const bool many_plain = cls_lists[C_BINP].size() >= pqg::BW_SEG_MAX_PAGES || plain_mode == 3;
+  const bool many_plain = (cls_lists[C_BINP].size() >= pqg::BW_SEG_MAX_PAGES && plain_mode != 1) || plain_mode == 3;
   P->plain_pg = many_plain;
   std::vector<uint8_t> plain_col((size_t)std::max(n_cols, 1), 0);
   std::vector<uint64_t> psegs;
@@ -1423,7 +1424,9 @@ struct HostCopy {
   uint64_t src;  // offset in the pinned buffer
   uint64_t len;
 };
-constexpr uint64_t HOST_CHUNK = 32ull << 20;
+// D2H piece: each is copied out by one thread as soon as it lands, so the copy of the last piece is the
+// tail after the link (32 MiB pieces: d2h+copy 21-24 ms for 800 MB against 14 ms of link, r05u)
+constexpr uint64_t HOST_CHUNK = 8ull << 20;
 inline int host_threads(uint64_t bytes) {
   const unsigned hw = std::thread::hardware_concurrency();
   const uint64_t want = bytes / (8ull << 20) + 1;
@@ -1588,38 +1591,43 @@ static int host_path(pqg_ctx* ctx, const uint8_t* h_bytes, uint64_t n_bytes, pqg
         hipEventRecord(dec_done, s) == hipSuccess && hipStreamWaitEvent(ctx->copy_stream, dec_done, 0) == hipSuccess)
       s2 = ctx->copy_stream;
   }
-  for (uint64_t k = 0; k < n_chunks && ok; k++) {
+  // The copy threads start first and take each piece once it is queued and its event has completed:
+  // hipMemcpyAsync into pinned memory measured blocking here (its events had all completed when the
+  // threads started, r05w), so a queue-then-copy order ran the host copies after the whole D2H.
+  std::vector<std::atomic<int>> queued((size_t)n_chunks);
+  for (auto& q : queued) q.store(0, std::memory_order_relaxed);
+  const int T = std::max(1, std::min<int>(host_threads(total), (int)n_chunks));
+  std::vector<int> wok((size_t)T, 1);
+  std::vector<std::thread> th;
+  std::vector<double> t_dma((size_t)n_chunks, 0.0);  // (PQG_HOST_TIMING: when each piece was seen landed)
+  const auto t_d0 = std::chrono::steady_clock::now();
+  for (int t = 0; t < T && !staged; t++)
+    th.emplace_back([&, t] {
+      if (hipSetDevice(ctx->device) != hipSuccess) { wok[(size_t)t] = 0; return; }
+      for (uint64_t k = (uint64_t)t; k < n_chunks; k += (uint64_t)T) {
+        int q;
+        while ((q = queued[(size_t)k].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+        if (q < 0 || hipEventSynchronize(ev[(size_t)k]) != hipSuccess) { wok[(size_t)t] = 0; return; }
+        if (timing) t_dma[(size_t)k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_d0).count();
+        copy_range(jobs, po, k * HOST_CHUNK, std::min(total, (k + 1) * HOST_CHUNK));
+      }
+    });
+  for (uint64_t k = 0; k < n_chunks; k++) {
     const uint64_t a = k * HOST_CHUNK, len = std::min(HOST_CHUNK, total - a);
     hipStream_t sk = (k & 1) ? s2 : s;
-    ok = hipMemcpyAsync((uint8_t*)ctx->pin_out.p + a, dout + a, len, hipMemcpyDeviceToHost, sk) == hipSuccess &&
+    ok = ok && hipMemcpyAsync((uint8_t*)ctx->pin_out.p + a, dout + a, len, hipMemcpyDeviceToHost, sk) == hipSuccess &&
          hipEventCreateWithFlags(&ev[(size_t)k], hipEventDisableTiming) == hipSuccess &&
          hipEventRecord(ev[(size_t)k], sk) == hipSuccess;
+    queued[(size_t)k].store(ok ? 1 : -1, std::memory_order_release);  // (-1: the threads stop)
   }
   std::vector<uint32_t> counts((size_t)std::max(n_pages, 1));
   if (ok && n_pages)
     ok = hipMemcpyAsync(counts.data(), ctx->host_counts.p, sizeof(uint32_t) * (size_t)n_pages, hipMemcpyDeviceToHost, s) == hipSuccess;
-  if (ok) {
-    const int T = std::max(1, std::min<int>(host_threads(total), (int)n_chunks));
-    std::vector<int> wok((size_t)T, 1);
-    std::vector<std::thread> th;
-    // (PQG_HOST_TIMING: when the last chunk's D2H completed, against the end of the copies)
-    std::vector<double> t_dma((size_t)n_chunks, 0.0);
-    const auto t_d0 = std::chrono::steady_clock::now();
-    for (int t = 0; t < T; t++)
-      th.emplace_back([&, t] {
-        if (hipSetDevice(ctx->device) != hipSuccess) { wok[(size_t)t] = 0; return; }
-        for (uint64_t k = (uint64_t)t; k < n_chunks; k += (uint64_t)T) {
-          if (hipEventSynchronize(ev[(size_t)k]) != hipSuccess) { wok[(size_t)t] = 0; return; }
-          if (timing) t_dma[(size_t)k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_d0).count();
-          copy_range(jobs, po, k * HOST_CHUNK, std::min(total, (k + 1) * HOST_CHUNK));
-        }
-      });
-    for (auto& x : th) x.join();
-    for (int v : wok) ok = ok && v;
-    if (timing && n_chunks)
-      std::fprintf(stderr, "pqg_decode_host   last D2H chunk landed %.3f ms after the first was queued (%d copy threads)\n",
-                   *std::max_element(t_dma.begin(), t_dma.end()), T);
-  }
+  for (auto& x : th) x.join();
+  for (int v : wok) ok = ok && v;
+  if (timing && n_chunks && !staged)
+    std::fprintf(stderr, "pqg_decode_host   last D2H piece seen landed %.3f ms after the copy threads started (%d threads)\n",
+                 *std::max_element(t_dma.begin(), t_dma.end()), T);
   if (s2 != s && hipStreamSynchronize(s2) != hipSuccess) ok = false;
   for (hipEvent_t e : ev)
     if (e) (void)hipEventDestroy(e);
