@@ -327,6 +327,16 @@ def run_c4(args, world, rank, devi):
                "sample": f"{reps} x one 1M-row, {n_keep}-column row group, oracle/pqref.c single thread, {dt:.1f} s"}
     if rank == 0:
         value = total_rows * n_keep * args.steps / t_max
+        # HBM traffic of one launch (every kernel's PMC FETCH_SIZE x 2 + WRITE_SIZE per dispatch, summed;
+        # tools/c4_traffic.sh) when it was measured on this workload
+        c4_traffic, c4_traffic_bytes, c4_traffic_src = None, None, None
+        tj_path = os.path.join(REPO, "profiles", "traffic_c4_latest.json")
+        if os.path.exists(tj_path) and world == 1:
+            tj = json.load(open(tj_path))
+            if tj.get("rows") == int(total_rows) and tj.get("columns") == list(shard.keep):
+                c4_traffic_bytes = tj["traffic_bytes_per_launch"]
+                c4_traffic = c4_traffic_bytes / (t_max / args.steps) / 1e9
+                c4_traffic_src = os.path.relpath(tj_path, REPO)
         out = {
             "metric": "decoded values/s, device-resident C4 lineitem 16 columns",
             "value": value, "unit": "values/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -346,7 +356,9 @@ def run_c4(args, world, rank, devi):
             # bytes = every column's encoded page bytes read + dense outputs written, per GPU
             "roofline": {"bound": "hbm", "achieved": total_bytes / world / (t_max / args.steps) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": total_bytes / world / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "frac": total_bytes / world / (t_max / args.steps) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": c4_traffic, "traffic_bytes_per_launch": c4_traffic_bytes,
+                         "traffic_source": c4_traffic_src,
                          "kernel": "whole plan launch (all kernels of the shard)",
                          "algorithmic_bytes_per_launch": total_bytes / world},
             "verified": None if args.no_verify else "every row group x column slice == its generated values, first launch "

@@ -1792,20 +1792,9 @@ __device__ __forceinline__ uint32_t bp_candidates(BinWalkLds& W, const BwBytes& 
   d[8] = cur.x;
   uint32_t m = 0;
   const int32_t rem0 = (int32_t)(end - 4u - base);
-  if (fast && rem0 >= (int32_t)(BW_Q - 1u + 255u)) {
-    // len < 256 <=> the prefix's bytes 1..3 are zero (every such length fits the section here): a
-    // zero-byte SWAR per dword (bit 7 of byte k: byte k == 0), then per dword the AND of the flags
-    // shifted by 1, 2 and 3 bytes, its 4 bits packed by one multiply
-    uint32_t z[BW_Q / 4 + 1];
-#pragma unroll
-    for (uint32_t j = 0; j <= BW_Q / 4; j++) z[j] = ~((((d[j] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d[j])) & 0x80808080u;
-#pragma unroll
-    for (uint32_t j = 0; j < BW_Q / 4; j++) {
-      const uint32_t c = __builtin_amdgcn_alignbit(z[j + 1], z[j], 8u) & __builtin_amdgcn_alignbit(z[j + 1], z[j], 16u) &
-                         __builtin_amdgcn_alignbit(z[j + 1], z[j], 24u);
-      m |= ((((c >> 7) * 0x00204081u) >> 21) & 0xFu) << (4u * j);
-    }
-  } else if (fast) {
+  // (a zero-byte SWAR form of the short-length test, 9 dwords per lane, measured slower on C4's comment
+  // column: 5.16 vs 5.00 ms, profiles/r05/binplain_swar)
+  if (fast) {
 #pragma unroll
     for (uint32_t q = 0; q < BW_Q; q++) {
       const uint32_t len = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
@@ -2094,29 +2083,35 @@ __device__ __forceinline__ bool bp_emit_fast(uint32_t* bm, const uint32_t* img, 
     if (x < 2048u) __hip_atomic_fetch_or(&bm[x >> 5], 1u << (x & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   wave_sync();
-  const uint32_t bits = bm[lane];
+  // starts before each 32-byte word of the output (lane w: word w), then lane l composes output blocks
+  // l and 64 + l (bytes [16 l, + 16) and [1024 + 16 l, + 16)): each store instruction covers 1 KiB
+  // of consecutive output (two blocks per lane side by side left every instruction's lines half
+  // written: C4's comment column wrote 7.3 GB for 4.4 GB of output, profiles/r05/c4)
   uint32_t tot;
-  const uint32_t k0 = wave_excl_scan_u32((uint32_t)__builtin_popcount(bits), &tot);  // starts before the lane's bytes
+  const uint32_t kw = wave_excl_scan_u32((uint32_t)__builtin_popcount(bm[lane]), &tot);
   const uint32_t C = P0 + 4u - B - r_lo;
-  uint32_t wd[8];
-#pragma unroll
-  for (uint32_t q = 0; q < 8; q++) {
-    const uint32_t x0 = 32u * lane + 4u * q;
-    const uint32_t k = k0 + (uint32_t)__builtin_popcount(bits & (0xFFFFFFFFu >> (31u - 4u * q)));  // starts <= x0
-    const uint32_t inner = (bits >> (4u * q + 1u)) & 7u;  // a start at x0 + 1 .. x0 + 3 (at most one)
-    const int32_t s0 = (int32_t)(x0 + C + 4u * k);
-    const uint32_t lo = img4(img, s0 > 0 ? (uint32_t)s0 : 0u);
-    const uint32_t hi = img4(img, (uint32_t)(s0 + 4 > 0 ? s0 + 4 : 0));
-    const uint32_t j = inner ? (uint32_t)__builtin_ctz(inner) + 1u : 4u;  // first byte of the next value
-    const uint32_t sel = 0x03020100u + (0x04040404u & ~(j >= 4u ? 0xFFFFFFFFu : (1u << (8u * j)) - 1u));
-    wd[q] = __builtin_amdgcn_perm(hi, lo, sel);
-  }
   uint8_t* dst = cd.binary_data;
   const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
 #pragma unroll
   for (uint32_t g = 0; g < 2; g++) {
-    const uint32_t b = 32u * lane + 16u * g;
-    if (b >= r_hi) break;
+    const uint32_t blk = 64u * g + lane, w = blk >> 1, half = 16u * (blk & 1u);
+    const uint32_t bits = bm[w];
+    const uint32_t k0 = (uint32_t)__shfl((int)kw, (int)w);  // starts before word w
+    const uint32_t b = 16u * blk;
+    uint32_t wd[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      const uint32_t bo = half + 4u * q, x0 = b + 4u * q;
+      const uint32_t k = k0 + (uint32_t)__builtin_popcount(bits & (0xFFFFFFFFu >> (31u - bo)));  // starts <= x0
+      const uint32_t inner = (bits >> (bo + 1u)) & 7u;  // a start at x0 + 1 .. x0 + 3 (at most one)
+      const int32_t s0 = (int32_t)(x0 + C + 4u * k);
+      const uint32_t lo = img4(img, s0 > 0 ? (uint32_t)s0 : 0u);
+      const uint32_t hi = img4(img, (uint32_t)(s0 + 4 > 0 ? s0 + 4 : 0));
+      const uint32_t j = inner ? (uint32_t)__builtin_ctz(inner) + 1u : 4u;  // first byte of the next value
+      const uint32_t sel = 0x03020100u + (0x04040404u & ~(j >= 4u ? 0xFFFFFFFFu : (1u << (8u * j)) - 1u));
+      wd[q] = __builtin_amdgcn_perm(hi, lo, sel);
+    }
+    if (b >= r_hi) continue;
     uint32_t have = 0;
 #pragma unroll
     for (uint32_t q = 0; q < 4; q++) {
@@ -2124,8 +2119,7 @@ __device__ __forceinline__ bool bp_emit_fast(uint32_t* bm, const uint32_t* img, 
       if (d0 >= r_lo && d0 + 4u <= r_hi) have |= 1u << q;
     }
     if (!dst_al4) have = 0;
-    const uint32_t w4[4] = {wd[4 * g], wd[4 * g + 1], wd[4 * g + 2], wd[4 * g + 3]};
-    store_block16(dst, a0 + b, o_lo, o_hi, w4, have, dst_al16);
+    store_block16(dst, a0 + b, o_lo, o_hi, wd, have, dst_al16);
   }
   return true;
 }

@@ -1,16 +1,10 @@
 set -e
-O=gpurun_out/r05v; mkdir -p $O
+O=gpurun_out/r05ab; mkdir -p $O
 export TMPDIR=/tmp
-PQG_HOST_TIMING=1 timeout -k 10 400 python -u bench.py --no-cpu --e2e --steps 5 > $O/e2e.json 2> $O/e2e.err || { tail -30 $O/e2e.err; exit 1; }
-python3 -c "
-import json
-d=json.load(open('$O/e2e.json'))['e2e_host_path']
-print(json.dumps({k:v for k,v in d.items() if k not in ('path','native_call_s','with_python_alloc_s')}))"
-for m in 1 2; do
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pm$m -o run -- python3 bench.py --workload c4 --rows 125000000 --steps 5 --warmup 1 --no-cpu --no-verify --c4-cols 15 --plain-mode $m > $O/pm$m.json 2> $O/pm$m.err || { tail -20 $O/pm$m.err; exit 1; }
-echo "== plain mode $m"; python3 tools/kstats.py $O/pm$m | head -6
+bash tools/ab_suite_prof.sh r05ab_s "c3_strings" abx/libprev.so parquet-mr_amd/pqgpu/libpqgpu.so
+for L in abx/libprev.so parquet-mr_amd/pqgpu/libpqgpu.so; do
+PQGPU_LIB=$PWD/$L timeout -k 10 600 python3 bench.py --workload c4 --rows 125000000 --steps 10 --warmup 2 --no-cpu > $O/c4.json 2> $O/c4.err || { tail -30 $O/c4.err; exit 1; }
+python3 -c "import json; print('C4 $L', json.load(open('$O/c4.json'))['ms_per_step'])"
 done
-for m in 1 2; do
-timeout -k 10 600 python3 bench.py --workload c4 --rows 125000000 --steps 10 --warmup 2 --no-cpu --plain-mode $m > $O/c4_pm$m.json 2> $O/c4_pm$m.err || { tail -30 $O/c4_pm$m.err; exit 1; }
-python3 -c "import json; print('C4 plain mode $m', json.load(open('$O/c4_pm$m.json'))['ms_per_step'])"
-done
+SUITE="c3_mixed" timeout -k 10 900 python -u tools/bench_suite.py c3_mixed --cpu-budget 0 > $O/c3.jsonl 2> $O/c3.err && cat $O/c3.jsonl | python3 -c "import json,sys; [print(json.loads(l)['workload'], json.loads(l)['ms_per_launch']) for l in sys.stdin]"
+PQGPU_LIB=$PWD/abx/libprev.so timeout -k 10 900 python -u tools/bench_suite.py c3_mixed --cpu-budget 0 > $O/c3p.jsonl 2> $O/c3p.err && cat $O/c3p.jsonl | python3 -c "import json,sys; [print('prev', json.loads(l)['workload'], json.loads(l)['ms_per_launch']) for l in sys.stdin]"
