@@ -1251,6 +1251,24 @@ __device__ __forceinline__ void dd_put(uint8_t* dst, const uint64_t (&o)[4], con
   }
 }
 
+// Block gather of k_dd_str (entries of 2 .. DDG_MD_MAX bytes): per tile, each wave writes its values'
+// tile-relative starts and entries to LDS and, for every 16-byte output block, the value holding the
+// block's first byte (each value marks the blocks whose first byte it holds); then every lane composes
+// whole blocks from the staged dictionary page (a 16-byte unaligned LDS read per value piece, masked and
+// shifted into the block) and stores them as one aligned 16-byte store: 64 KB of value bytes per 4,096
+// store instructions, where storing each value's own bytes (dd_put) scattered dword / short / byte stores
+// at lane strides (C4: 24.7 M store instructions per launch, the kernel's bound).
+constexpr uint32_t DDG_MD_MAX = 32;
+constexpr uint32_t DDG_FV = (WAVE * 4u * DDG_MD_MAX) / 16u + 2u;
+struct DdgLds {
+  uint32_t vo[WAVE * 4];  // tile-relative first byte of value v
+  uint32_t ve[WAVE * 4];  // entry: source << 16 | length (0: empty / out of range)
+  uint16_t fv[DDG_FV];    // block b: the value holding its first byte
+};
+constexpr uint32_t DDG_WAVE_BYTES = (sizeof(DdgLds) + 15u) & ~15u;
+// 0xFF in byte i of the result for each bit i of x (x < 16)
+__device__ __forceinline__ uint32_t spread_bytes4(uint32_t x) { return ((x * 0x00204081u) & 0x01010101u) * 0xFFu; }
+
 // One wave per output chunk of k_dict_fused_dd (chunks of one column per workgroup: the plan pads the
 // chunk list). The chunk's ids are loaded first, all of them (one dword per tile per lane for u8 ids,
 // two for u16: no load after the first store, whose wait would drain the stores), then per 256-value
@@ -1269,7 +1287,9 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
   typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
   constexpr uint32_t E = 4, TV = WAVE * E, CH = CH_TILES * TV;
-  extern __shared__ __attribute__((aligned(16))) uint8_t dd_lds[];
+  // the staged dictionary page at dd_raw + 16 (16 bytes of slack before it for the block gather's reads)
+  extern __shared__ __attribute__((aligned(16))) uint8_t dd_raw[];
+  uint8_t* const dd_lds = dd_raw + 16;
   __shared__ int wg_col[WPB];
   const uint32_t lane = lane_id();
   const uint32_t c = blockIdx.x * WPB + wave_id();
@@ -1359,6 +1379,14 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
   const uint64_t cap = cd.binary_capacity;
   int64_t* const opag = (int64_t*)cd.values + (pw.out_offset - sh);  // offsets of the page's slot 0
   const bool o16 = ((uintptr_t)cd.values & 15u) == 0;
+  // block gather: entries of 2 .. DDG_MD_MAX bytes into a 16-byte aligned value buffer
+  const bool gather = !one && md <= DDG_MD_MAX && ((uintptr_t)dst & 15u) == 0;
+  DdgLds& G = *(DdgLds*)(dd_lds + ((dd_region + 15u) & ~15u) + wave_id() * DDG_WAVE_BYTES);
+  // a tile's partial last block, finished by the next tile (uniform): bytes [cb_lo, cb_hi) of the block
+  // at cb_tal; cx / cxlo: the carrying lane's copy
+  bool cb_on = false;
+  uint32_t cb_w[4] = {0, 0, 0, 0}, cb_lo = 0, cb_hi = 0, cx[4] = {0, 0, 0, 0}, cxlo = 0;
+  uint64_t cb_tal = 0;
   uint64_t run_base = uni64(bases[c]);
 #pragma unroll 1
   for (uint32_t t = 0; t < CH_TILES; t++) {
@@ -1390,8 +1418,92 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
       for (uint32_t e = 0; e < E; e++)
         if (ts + E * lane + e >= s_lo && ts + E * lane + e < s_hi) gst(op + e, (int64_t)o[e]);
     }
+    const uint64_t tb = run_base;  // the tile's first byte
     run_base += tot;
-    if (run_base <= cap) {
+    if (run_base <= cap && gather) {
+      wave_sync();  // the previous tile's gather reads are done
+      // positions relative to the tile's first 16-byte block (32-bit): bytes [rb, re)
+      const uint64_t tal = tb & ~15ull;
+      const uint32_t rb = (uint32_t)(tb - tal), re = rb + tot;
+#pragma unroll
+      for (uint32_t e = 0; e < E; e++) {
+        G.vo[E * lane + e] = rb + (uint32_t)(o[e] - tb);
+        G.ve[E * lane + e] = (sr[e] << 16) | ln[e];
+      }
+      const uint32_t nblk = (re + 15u) >> 4;
+#pragma unroll
+      for (uint32_t e = 0; e < E; e++) {
+        if (!ln[e]) continue;
+        // the blocks whose first byte (16 b, or rb for the tile's first block) this value holds
+        const uint32_t g = rb + (uint32_t)(o[e] - tb);
+        for (uint32_t b = g == rb ? (g >> 4) : ((g + 15u) >> 4); (b << 4) < g + ln[e]; b++) G.fv[b] = (uint16_t)(E * lane + e);
+      }
+      wave_sync();
+      // the tile's last block, when partial, is finished by the next tile of the chunk (same wave)
+      const bool next_tile = t + 1 < CH_TILES && ts + TV < s_hi;
+      for (uint32_t b = lane; b < nblk; b += WAVE) {
+        const uint32_t gb = b << 4;
+        uint32_t bs = gb > rb ? gb : rb;
+        const uint32_t be = gb + 16u < re ? gb + 16u : re;
+        uint32_t v = G.fv[b];
+        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        if (b == 0 && cb_on) {  // the previous tile's partial last block (uniform carry)
+          a0 = cb_w[0]; a1 = cb_w[1]; a2 = cb_w[2]; a3 = cb_w[3];
+          bs = cb_lo;
+        }
+        uint32_t pos = gb > rb ? gb : rb;
+        while (pos < be) {
+          const uint32_t g = G.vo[v], ev = G.ve[v];
+          const uint32_t ge = g + (ev & 0xFFFFu);
+          if (pos < ge) {  // (empty values hold no byte)
+            const uint32_t n = (ge < be ? ge : be) - pos;  // bytes of this piece
+            const uint32_t k = pos - gb;                    // their place in the block
+            // the 16 page bytes that line up with the block: page offset (source of pos) - k, read
+            // through the 16 bytes of slack before the staged page
+            const uint32_t base = 16u + (ev >> 16) + (pos - g) - k;
+            const uint32_t q = base & ~3u, r = base & 3u;
+            const uint32_t* w = (const uint32_t*)(dd_raw + q);
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+            const uint32_t m16 = ((1u << (k + n)) - 1u) & ~((1u << k) - 1u);  // block bytes [k, k + n)
+            a0 |= __builtin_amdgcn_alignbyte(w1, w0, r) & spread_bytes4(m16 & 15u);
+            a1 |= __builtin_amdgcn_alignbyte(w2, w1, r) & spread_bytes4((m16 >> 4) & 15u);
+            a2 |= __builtin_amdgcn_alignbyte(w3, w2, r) & spread_bytes4((m16 >> 8) & 15u);
+            a3 |= __builtin_amdgcn_alignbyte(w4, w3, r) & spread_bytes4(m16 >> 12);
+            pos += n;
+          }
+          v++;
+        }
+        const uint32_t wd[4] = {a0, a1, a2, a3};
+        if (b == nblk - 1u && be < gb + 16u && next_tile) {  // carried: the lane's values go to the next tile
+          cx[0] = a0; cx[1] = a1; cx[2] = a2; cx[3] = a3;
+          cxlo = bs - gb;
+        } else {
+          uint32_t have = 0;
+#pragma unroll
+          for (uint32_t d = 0; d < 4; d++) have |= (gb + 4u * d >= bs && gb + 4u * d + 4u <= be ? 1u : 0u) << d;
+          store_block16(dst, tal + gb, tal + bs, tal + be, wd, have, true);
+        }
+      }
+      // the partial last block of this tile (lane (nblk - 1) % 64) as uniform values for the next tile,
+      // whose block 0 is the same 16 bytes (its first byte continues this tile's last)
+      const bool carried = nblk && next_tile && (re & 15u) != 0u;
+      if (carried) {
+        const uint32_t cl = (nblk - 1u) & (WAVE - 1u);
+#pragma unroll
+        for (uint32_t d = 0; d < 4; d++) cb_w[d] = rdl(cx[d], cl);
+        cb_lo = rdl(cxlo, cl);
+      } else if (cb_on && nblk == 0) {  // (a tile without bytes: the carried block is stored as is)
+        if (lane == 0) {
+          uint32_t have = 0;
+#pragma unroll
+          for (uint32_t d = 0; d < 4; d++) have |= (4u * d >= cb_lo && 4u * d + 4u <= cb_hi ? 1u : 0u) << d;
+          store_block16(dst, cb_tal, cb_tal + cb_lo, cb_tal + cb_hi, cb_w, have, true);
+        }
+      }
+      cb_on = carried;
+      cb_hi = re & 15u;
+      cb_tal = tal + ((uint64_t)(nblk ? nblk - 1u : 0u) << 4);
+    } else if (run_base <= cap) {
       if (one && ls == E) {  // 1-byte entries, the lane's 4 values in range: one dword
         uint32_t x = 0;
 #pragma unroll
@@ -3141,8 +3253,8 @@ hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes
   hipLaunchKernelGGL(k_dd_bases, dim3(n_dd_cols), dim3(256), 0, st, cols, dd_cols, dd_start, sums);
   e = hipGetLastError();
   if (e != hipSuccess || !n_tile) return e;
-  hipLaunchKernelGGL(k_dd_str, dim3(n_tile), blk, dd_region, st, bytes, n_bytes, work, cols, chunks, n_chunks, pstat,
-                     sums, err, err_count, dd_region);
+  hipLaunchKernelGGL(k_dd_str, dim3(n_tile), blk, 16u + ((dd_region + 15u) & ~15u) + WPB * DDG_WAVE_BYTES, st, bytes, n_bytes,
+                     work, cols, chunks, n_chunks, pstat, sums, err, err_count, dd_region);
   return hipGetLastError();
 }
 

@@ -498,10 +498,13 @@ def test_dictionary_direct_interleaved_columns(decoder, dict_direct):
             assert np.array_equal(dcols[i].offsets().cpu().numpy(), ref.columns[i]["offsets"][: n + 1])
 
 
-@pytest.mark.parametrize("lens", [(0, 0), (1, 4000), (2000, 2000, 2000), (0, 1, 23, 24, 64)])
+@pytest.mark.parametrize("lens", [(0, 0), (1, 4000), (2000, 2000, 2000), (0, 1, 23, 24, 64),
+                                  (2, 3), (0, 2, 17, 32), (17, 11, 4, 16), (7, 3, 4, 4, 5, 4, 3), (16,), (32, 32, 1)])
 def test_dictionary_direct_entry_lengths(decoder, lens):
-    """Entry lengths around the kernel's per-wave image (6 KiB per 256-value tile): empty entries only,
-    tiles whose bytes overflow the image (written value by value), and mixes of both in one chunk."""
+    """Entry lengths around the kernel's byte paths: empty entries only, 1-byte entries, entries of 2..32
+    bytes (composed into whole 16-byte output blocks: C4's ship instruct / mode shapes, blocks that start
+    inside, at the start of and between entries, 16-byte entries, empty entries between), longer ones
+    (written value by value), and mixes in one chunk."""
     rng = np.random.default_rng(len(lens))
     words = [bytes(rng.integers(65, 91, size=n, dtype=np.uint8)) for n in lens]
     ids = rng.integers(0, len(words), size=9000)
