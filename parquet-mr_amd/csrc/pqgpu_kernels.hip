@@ -1266,8 +1266,6 @@ struct DdgLds {
   uint16_t fv[DDG_FV];    // block b: the value holding its first byte
 };
 constexpr uint32_t DDG_WAVE_BYTES = (sizeof(DdgLds) + 15u) & ~15u;
-// 0xFF in byte i of the result for each bit i of x (x < 16)
-__device__ __forceinline__ uint32_t spread_bytes4(uint32_t x) { return ((x * 0x00204081u) & 0x01010101u) * 0xFFu; }
 
 // One wave per output chunk of k_dict_fused_dd (chunks of one column per workgroup: the plan pads the
 // chunk list). The chunk's ids are loaded first, all of them (one dword per tile per lane for u8 ids,
@@ -1291,6 +1289,16 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
   extern __shared__ __attribute__((aligned(16))) uint8_t dd_raw[];
   uint8_t* const dd_lds = dd_raw + 16;
   __shared__ int wg_col[WPB];
+  // block gather: v_perm selectors taking bytes k .. 15 of a block from the source, the rest from the
+  // accumulated block (dd_sel[k], dword d: byte j <- source when 4 d + j >= k)
+  __shared__ u32x4 dd_sel[16];
+  if (threadIdx.x < 64u) {
+    const uint32_t k = threadIdx.x >> 2, d = threadIdx.x & 3u;
+    uint32_t sel = 0;
+#pragma unroll
+    for (uint32_t jb = 0; jb < 4; jb++) sel |= (4u * d + jb >= k ? 4u + jb : jb) << (8u * jb);
+    ((uint32_t*)dd_sel)[threadIdx.x] = sel;
+  }
   const uint32_t lane = lane_id();
   const uint32_t c = blockIdx.x * WPB + wave_id();
   const int page = c < n_chunks ? (int)(uint32_t)chunks[c] : -1;
@@ -1464,11 +1472,13 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
             const uint32_t q = base & ~3u, r = base & 3u;
             const uint32_t* w = (const uint32_t*)(dd_raw + q);
             const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
-            const uint32_t m16 = ((1u << (k + n)) - 1u) & ~((1u << k) - 1u);  // block bytes [k, k + n)
-            a0 |= __builtin_amdgcn_alignbyte(w1, w0, r) & spread_bytes4(m16 & 15u);
-            a1 |= __builtin_amdgcn_alignbyte(w2, w1, r) & spread_bytes4((m16 >> 4) & 15u);
-            a2 |= __builtin_amdgcn_alignbyte(w3, w2, r) & spread_bytes4((m16 >> 8) & 15u);
-            a3 |= __builtin_amdgcn_alignbyte(w4, w3, r) & spread_bytes4(m16 >> 12);
+            // block bytes k .. 15 from the source (a later piece overwrites from its own k on; bytes
+            // past the block's end are not stored)
+            const u32x4 sl = dd_sel[k];
+            a0 = __builtin_amdgcn_perm(__builtin_amdgcn_alignbyte(w1, w0, r), a0, sl.x);
+            a1 = __builtin_amdgcn_perm(__builtin_amdgcn_alignbyte(w2, w1, r), a1, sl.y);
+            a2 = __builtin_amdgcn_perm(__builtin_amdgcn_alignbyte(w3, w2, r), a2, sl.z);
+            a3 = __builtin_amdgcn_perm(__builtin_amdgcn_alignbyte(w4, w3, r), a3, sl.w);
             pos += n;
           }
           v++;
@@ -2970,12 +2980,15 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     // ---- expand the walked blocks (every read from the LDS segment)
     // (the segment path stores 16-value runs per lane, shifted to 16-byte alignment: pages of
     // nullable columns, which start at any value offset, take it too)
+#ifndef PQG_DELTA_NOEXP  // (diagnostic build: the header walk alone)
     if (!NEG && (mbs % 16u) == 0 && ((uint64_t)block * W) % 16u == 0)
       delta_expand_seg<W>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out);
-    else if (E == 1) delta_expand<W, NEG, 1>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
+    else if (E == 1)
+      delta_expand<W, NEG, 1>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else if (E == 2) delta_expand<W, NEG, 2>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else if (E == 4) delta_expand<W, NEG, 4>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else delta_expand<W, NEG, 8>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
+#endif
     n_blocks += nb;
   }
   // the value after the last delta of the last block (the expansion stores values up to the one
