@@ -2619,39 +2619,70 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
     const uint32_t blo = m >= 4u ? wlo : (m ? wlo & ((1u << (8u * m)) - 1u) : 0u);
     const uint32_t bhi = m <= 4u ? 0u : whi & ((1u << (8u * (m - 4u))) - 1u);
     const uint32_t dbase = data + (__builtin_amdgcn_sad_u8(blo, 0u, 0u) + __builtin_amdgcn_sad_u8(bhi, 0u, 0u)) * mb_bytes;
-    const uint64_t mask = wl == 64 ? ~0ull : ((1ull << wl) - 1ull);
-    const bool narrow = !__ballot(lane_in && wl > 32u);  // every width <= 32: two dwords per delta
-    uint64_t loc[L];
-    uint64_t sum = 0;
-    uint32_t bit = jm * wl;
-#pragma unroll
-    for (uint32_t q = 0; q < L; q++) {
-      uint64_t d = 0;
-      if (wl) {
-        const uint32_t byte = dbase + (bit >> 3);
-        const uint32_t a = byte & ~3u;
-        const uint32_t sh = (byte - a) * 8u + (bit & 7u);  // < 32
-        const uint64_t lo64 = (uint64_t)S.w32(a) | ((uint64_t)S.w32(a + 4) << 32);
-        if (narrow) {
-          d = (lo64 >> sh) & mask;
-        } else {
-          const uint32_t x2 = S.w32(a + 8);
-          d = (sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)))) & mask;
-        }
-      }
-      sum += lane_in ? d + mind : 0ull;
-      loc[q] = sum;
-      bit += wl;
-    }
-    const uint64_t x = wave_incl_scan_u64(sum);
-    const uint64_t base_v = carry + (x - sum);
-    const uint64_t last = base_v + loc[L - 1];
-    const uint32_t plo = (uint32_t)__shfl_up((int)(uint32_t)last, 1), phi = (uint32_t)__shfl_up((int)(uint32_t)(last >> 32), 1);
-    const uint64_t prev = lane == 0 ? carry : (((uint64_t)phi << 32) | plo);
-    const uint64_t k0 = (uint64_t)blk_first - 1u + (uint64_t)bb * block + j0;  // index of the run's first value
     T u[L + 3];
+    uint64_t x;  // the wave scan of the lanes' sums (its last lane: the batch's total)
+    if constexpr (W == 4) {
+      // 4-byte values: the reader keeps long sums and casts them to int, whose low 32 bits depend on
+      // the low 32 bits of every delta and of minDelta only: 32-bit unpack (one v_alignbit from the
+      // dword pair holding the delta's first bit), sums and scan
+      const uint32_t mask = wl >= 32u ? 0xFFFFFFFFu : (1u << wl) - 1u;
+      const uint32_t mind32 = (uint32_t)mind;
+      uint32_t loc[L];
+      uint32_t sum = 0;
+      uint32_t ab = dbase * 8u + jm * wl;  // bit position in the page
 #pragma unroll
-    for (uint32_t q = 0; q < L + 1; q++) u[q] = (T)(q == 0 ? prev : base_v + loc[q - 1]);
+      for (uint32_t q = 0; q < L; q++) {
+        uint32_t d = 0;
+        if (wl) {
+          const uint32_t a = (ab >> 5) << 2;
+          d = __builtin_amdgcn_alignbit(S.w32(a + 4), S.w32(a), ab & 31u) & mask;
+        }
+        sum += lane_in ? d + mind32 : 0u;
+        loc[q] = sum;
+        ab += wl;
+      }
+      const uint32_t x32 = wave_incl_scan_u32_dpp(sum);
+      const uint32_t base_v = (uint32_t)carry + (x32 - sum);
+      // (the shuffle outside the select: a lane left out of it would hand its neighbour a 0)
+      const uint32_t up = (uint32_t)__shfl_up((int)(base_v + loc[L - 1]), 1);
+      const uint32_t prev = lane == 0 ? (uint32_t)carry : up;
+#pragma unroll
+      for (uint32_t q = 0; q < L + 1; q++) u[q] = (T)(q == 0 ? prev : base_v + loc[q - 1]);
+      x = x32;
+    } else {
+      const uint64_t mask = wl == 64 ? ~0ull : ((1ull << wl) - 1ull);
+      const bool narrow = !__ballot(lane_in && wl > 32u);  // every width <= 32: two dwords per delta
+      uint64_t loc[L];
+      uint64_t sum = 0;
+      uint32_t bit = jm * wl;
+#pragma unroll
+      for (uint32_t q = 0; q < L; q++) {
+        uint64_t d = 0;
+        if (wl) {
+          const uint32_t byte = dbase + (bit >> 3);
+          const uint32_t a = byte & ~3u;
+          const uint32_t sh = (byte - a) * 8u + (bit & 7u);  // < 32
+          const uint64_t lo64 = (uint64_t)S.w32(a) | ((uint64_t)S.w32(a + 4) << 32);
+          if (narrow) {
+            d = (lo64 >> sh) & mask;
+          } else {
+            const uint32_t x2 = S.w32(a + 8);
+            d = (sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)))) & mask;
+          }
+        }
+        sum += lane_in ? d + mind : 0ull;
+        loc[q] = sum;
+        bit += wl;
+      }
+      x = wave_incl_scan_u64(sum);
+      const uint64_t base_v = carry + (x - sum);
+      const uint64_t last = base_v + loc[L - 1];
+      const uint32_t plo = (uint32_t)__shfl_up((int)(uint32_t)last, 1), phi = (uint32_t)__shfl_up((int)(uint32_t)(last >> 32), 1);
+      const uint64_t prev = lane == 0 ? carry : (((uint64_t)phi << 32) | plo);
+#pragma unroll
+      for (uint32_t q = 0; q < L + 1; q++) u[q] = (T)(q == 0 ? prev : base_v + loc[q - 1]);
+    }
+    const uint64_t k0 = (uint64_t)blk_first - 1u + (uint64_t)bb * block + j0;  // index of the run's first value
     // values 17, 18 of the lane's window: lane l + 1's u[1], u[2] (only for 4-byte values: sft <= 3)
     if constexpr (VPC > 2) {
       u[L + 1] = (T)(uint32_t)__shfl_down((int)(uint32_t)u[1], 1);
@@ -2666,15 +2697,20 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
           if (q < sft && k0 + q < n_out) gst(out + k0 + q, u[q]);
       const uint64_t a = k0 + sft;
       if (wide && !last_lane && a + L <= n_out) {
-        T v[L];
+        // v[q] = u[sft + q]: sft is uniform, so a branch per value of it picks the registers statically
+        auto put = [&](auto s_tag) {
+          constexpr uint32_t SF = decltype(s_tag)::value;
+          T v[L];
 #pragma unroll
-        for (uint32_t q = 0; q < L; q++) {  // v[q] = u[sft + q]
-          T y = u[q];
-#pragma unroll
-          for (uint32_t t = 1; t < VPC; t++) y = sft == t ? u[q + t] : y;
-          v[q] = y;
+          for (uint32_t q = 0; q < L; q++) v[q] = u[q + SF];
+          store_run<T, L>(out + a, v);
+        };
+        if (sft == 0) put(std::integral_constant<uint32_t, 0>{});
+        else if (sft == 1) put(std::integral_constant<uint32_t, 1>{});
+        else if constexpr (VPC > 2) {
+          if (sft == 2) put(std::integral_constant<uint32_t, 2>{});
+          else put(std::integral_constant<uint32_t, 3>{});
         }
-        store_run<T, L>(out + a, v);
       } else {
         const uint64_t e = last_lane ? k0 + L : a + L;  // the last lane: its own values only
 #pragma unroll
@@ -2684,7 +2720,8 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
         }
       }
     }
-    carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
+    if constexpr (W == 4) carry += rdl((uint32_t)x, 63);  // (only its low 32 bits are ever stored)
+    else carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
   }
 }
 
