@@ -797,6 +797,9 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
         const uint32_t o = i + 16u * lane;
         if (o < pre_hi - pre_lo) *(u32x4*)(xseg + o) = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(pre_lo + o), 0, 0);
       }
+      // bytes past the section read as 0 (the truncated final group, :96-99): zeroed once here, so
+      // the tile sweep's unpack needs no per-value check
+      if (lane < 8u) xseg[sec_end - pre_lo + lane] = 0;
     }
     uint64_t pst = 0;
     bool ok = true;
@@ -965,6 +968,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
             const uint32_t o = i + 16u * lane;
             if (o < px_hi - px_lo) *(u32x4*)(xseg + o) = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(px_lo + o), 0, 0);
           }
+          for (uint32_t o = (sec_end > px_lo ? sec_end - px_lo : 0u) + lane; o < px_hi - px_lo; o += WAVE) xseg[o] = 0;
         }
       }
       // DICT_ID: RLE runs of the round with an id past the dictionary (reported at the first
@@ -982,21 +986,27 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
         constexpr bool FAST = decltype(fast_tag)::value;
         auto value = [&](uint32_t ci, uint32_t i, const u32x4& q) -> T {
           if (!(q.y & 0x80000000u)) return (T)(((uint64_t)q.w << 32) | q.z);
-          const uint64_t bit = (uint64_t)(i - q.x) * (uint32_t)w;
-          const uint32_t byte = (q.y & 0x7FFFFFFFu) + (uint32_t)(bit >> 3);
-          const uint32_t a4 = byte & ~3u;
-          uint64_t y;
-          if (FAST)
-            y = (uint64_t)*(const u32_alias*)(xseg + (a4 - px_lo)) |
-                ((uint64_t)*(const u32_alias*)(xseg + (a4 - px_lo) + 4) << 32);
-          else
-            y = (uint64_t)ld32(prs, a4) | ((uint64_t)ld32(prs, a4 + 4) << 32);
-          if (a4 + 8u > sec_end) {  // truncated final group: bytes past the section are 0 (:96-99)
-            const int64_t keep = (int64_t)sec_end - (int64_t)a4;
-            y = keep <= 0 ? 0 : (y & ((1ull << (8 * keep)) - 1ull));
+          uint32_t id;
+          if (FAST) {
+            // staged bytes (zeroed past the section end), page value counts below 2^27: 32-bit bit
+            // positions and one v_alignbit from the dword pair holding the id's first bit
+            const uint32_t bit = (i - q.x) * (uint32_t)w;
+            const uint32_t byte = (q.y & 0x7FFFFFFFu) + (bit >> 3);
+            const uint32_t o = (byte & ~3u) - px_lo;
+            id = __builtin_amdgcn_alignbit(*(const u32_alias*)(xseg + o + 4), *(const u32_alias*)(xseg + o),
+                                           ((byte & 3u) << 3) + (bit & 7u)) & wmask;
+          } else {
+            const uint64_t bit = (uint64_t)(i - q.x) * (uint32_t)w;
+            const uint32_t byte = (q.y & 0x7FFFFFFFu) + (uint32_t)(bit >> 3);
+            const uint32_t a4 = byte & ~3u;
+            uint64_t y = (uint64_t)ld32(prs, a4) | ((uint64_t)ld32(prs, a4 + 4) << 32);
+            if (a4 + 8u > sec_end) {  // truncated final group: bytes past the section are 0 (:96-99)
+              const int64_t keep = (int64_t)sec_end - (int64_t)a4;
+              y = keep <= 0 ? 0 : (y & ((1ull << (8 * keep)) - 1ull));
+            }
+            y >>= (byte - a4) * 8u + (uint32_t)(bit & 7u);
+            id = w == 0 ? 0u : (uint32_t)y & wmask;
           }
-          y >>= (byte - a4) * 8u + (uint32_t)(bit & 7u);
-          const uint32_t id = w == 0 ? 0u : (uint32_t)y & wmask;
           if (id >= dict_n) {
             report(err, err_count, page, 2, i, PQG_ERR_DICT_ID);
             return 0;
@@ -1077,7 +1087,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
           }
         }
       };
-      if ((IDS || own_dict) && x_lds) sweep(std::true_type{});
+      if ((IDS || own_dict) && x_lds && N < (1u << 27)) sweep(std::true_type{});
       else sweep(std::false_type{});
       if (b_hi >= r_hi) break;
       k += XT_RUNS - 1;
