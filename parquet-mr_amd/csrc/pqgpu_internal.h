@@ -174,7 +174,10 @@ constexpr uint32_t BW_SEG_BYTES = 16384;
 constexpr uint32_t BW_SEG_CAP = BW_SEG_BYTES / 4 + 2;
 constexpr uint32_t BW_SEG_MAX_PAGES = 4096;
 constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block
-constexpr uint32_t DD_DICT_MAX = 8192;  // dictionary page bytes staged by k_dd_str (dict_direct)
+// dictionary page bytes staged by k_dd_str (dict_direct): 32 KiB since round 5 (8 KiB before; the suite's
+// str_dict dictionary, 1,000 entries of 4-32 bytes in 22 KB, then took the per-value path: 0.667 ms, now
+// 0.347 ms, profiles/r05/dd32k; k_dd_str's LDS at 32 KiB + the entry table: 4 workgroups per CU)
+constexpr uint32_t DD_DICT_MAX = 32768;
 hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                       const int32_t* list, int n, uint64_t* err, ErrCount err_count);
 hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
