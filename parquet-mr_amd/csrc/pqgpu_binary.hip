@@ -186,6 +186,11 @@ __device__ __forceinline__ BinWalkEnd bin_walk_core(BinWalkLds& L, rsrc_t rs, ui
   uint32_t B = pos & ~(BW_WIN - 1u);
   BwBytes cur_b = bw_load(rs, B);
   BwBytes nxt_b = bw_load(rs, B + BW_WIN);
+  // Short lengths first (< 256, the usual string): the byte before a length prefix then never reads
+  // as a candidate (it is 256 x the true length plus a string byte), so a tile's candidates link one
+  // to the next and the binary lifting below is not needed. A value start the short pass does not
+  // list (a longer value) sends the tile through the pass with every length.
+  bool fast = true;
   while (true) {
     pos = uni(pos);
     produced = uni(produced);
@@ -208,7 +213,7 @@ __device__ __forceinline__ BinWalkEnd bin_walk_core(BinWalkLds& L, rsrc_t rs, ui
     for (uint32_t q = 0; q < BW_Q; q++) {
       const uint32_t len = __builtin_amdgcn_alignbyte(d[(q >> 2) + 1], d[q >> 2], q & 3u);
       const int32_t rem = rem0 - (int32_t)q;
-      const bool c = rem >= 0 && len <= (uint32_t)rem;
+      const bool c = rem >= 0 && len <= (uint32_t)rem && (!fast || len < 256u);
       m |= (c ? 1u : 0u) << q;
     }
     if (base < pos) m &= pos - base >= BW_Q ? 0u : ~((1u << (pos - base)) - 1u);
@@ -247,6 +252,11 @@ __device__ __forceinline__ BinWalkEnd bin_walk_core(BinWalkLds& L, rsrc_t rs, ui
     const uint32_t eff_end = total > BW_CAP ? uni(L.cut) : B + BW_WIN;
     if (total > BW_CAP) total = BW_CAP;
     if (total == 0 || L.pn[0].x != pos) {  // the current position cannot hold a value
+      if (fast) {  // (or a longer one: the tile again with every length)
+        fast = false;
+        wave_sync();
+        continue;
+      }
       code = bin_value_error(rs, pos, end, dict);
       break;
     }
@@ -258,6 +268,7 @@ __device__ __forceinline__ BinWalkEnd bin_walk_core(BinWalkLds& L, rsrc_t rs, ui
     // read from a shifted prefix, e.g. the byte before a small length — are never reached).
     uint32_t i0 = 0, got = 0;
     bool leave = false;  // next position lies past the window
+    bool retry = false;  // the short pass missed a value start: this tile again with every length
     while (true) {
       i0 = uni(i0);
       got = uni(got);
@@ -308,6 +319,12 @@ __device__ __forceinline__ BinWalkEnd bin_walk_core(BinWalkLds& L, rsrc_t rs, ui
       if (cur >= eff_end) { leave = true; break; }
       const uint32_t a = uni(bw_index(L, cur - B));
       if (a >= total || a <= i0 + last) {  // every position of the window was tested
+        if (fast) {  // a longer value: the rest of the tile with every length
+          fast = false;
+          leave = false;
+          retry = true;
+          break;
+        }
         code = bin_value_error(rs, cur, end, dict);
         break;
       }
@@ -344,6 +361,11 @@ __device__ __forceinline__ BinWalkEnd bin_walk_core(BinWalkLds& L, rsrc_t rs, ui
       done += (uint32_t)__builtin_popcountll(am);
     }
     produced += got;
+    if (retry) {  // (pos: the value the short pass could not follow; its tile again, every length)
+      wave_sync();
+      continue;
+    }
+    fast = true;
     if (code || !leave) break;
     wave_sync();  // the next window overwrites the list
   }
