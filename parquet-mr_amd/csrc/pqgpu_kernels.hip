@@ -1282,6 +1282,7 @@ __device__ __forceinline__ void dd_put(uint8_t* dst, const uint64_t (&o)[4], con
 // store instructions, where storing each value's own bytes (dd_put) scattered dword / short / byte stores
 // at lane strides (C4: 24.7 M store instructions per launch, the kernel's bound).
 constexpr uint32_t DDG_MD_MAX = 32;
+constexpr uint32_t DD_SPLIT_MAX_CHUNKS = 16384;  // k_dd_str: a workgroup per chunk up to this many chunks
 constexpr uint32_t DDG_FV = (WAVE * 4u * DDG_MD_MAX) / 16u + 2u;
 struct DdgLds {
   uint32_t vo[WAVE * 4];  // tile-relative first byte of value v
@@ -1298,6 +1299,7 @@ constexpr uint32_t DDG_WAVE_BYTES = (sizeof(DdgLds) + 15u) & ~15u;
 // stores plus a 2- and a 1-byte store for its last 1-3 bytes (no store leaves the value's own bytes).
 // Slots of a page past a walk error (pstat) are empty values. dd_region: LDS bytes of the staged page
 // (16-byte rounded) + its u32 entry table (source << 16 | length).
+template <uint32_t TPW>
 __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                      const PageWork* __restrict__ work,
                                                      const ColumnDev* __restrict__ cols,
@@ -1323,7 +1325,15 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
     ((uint32_t*)dd_sel)[threadIdx.x] = sel;
   }
   const uint32_t lane = lane_id();
-  const uint32_t c = blockIdx.x * WPB + wave_id();
+  // TPW = CH_TILES: one chunk per wave. TPW = CH_TILES / WPB: one workgroup per chunk, wave w takes tiles
+  // [T0, T1) of it (4x the workgroups: str_dict's 4,883 chunks filled 1.2 rounds of the chip's workgroup
+  // slots, the second one a fifth: 0.321 -> 0.274 ms; C4's 122 k chunks keep a chunk per wave, 10.50 vs
+  // 10.63 ms; profiles/r05/dd_split)
+  static_assert(TPW == CH_TILES || TPW * WPB == CH_TILES, "a chunk per wave or per workgroup");
+  constexpr bool SPLIT = TPW < CH_TILES;
+  const uint32_t c = SPLIT ? blockIdx.x : blockIdx.x * WPB + wave_id();
+  const uint32_t T0 = SPLIT ? wave_id() * TPW : 0u, T1 = T0 + TPW;
+  __shared__ uint32_t wsum[WPB];
   const int page = c < n_chunks ? (int)(uint32_t)chunks[c] : -1;
   if (lane == 0) wg_col[wave_id()] = page >= 0 ? work[page].column : -1;
   __syncthreads();
@@ -1388,12 +1398,12 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
   const uint32_t s_hi = (j + 1) * CH < NF + sh ? (j + 1) * CH : NF + sh;
   if (s_lo >= s_hi) return;
   const uint32_t ok_hi = (nok < NF ? nok : NF) + sh;  // slots [ok_hi, s_hi): empty values
-  // the chunk's ids: tile t -> lane's 4 ids (u8: dword t; u16: dwords 2t, 2t + 1)
+  // the wave's ids: tile T0 + t -> lane's 4 ids (u8: dword t; u16: dwords 2t, 2t + 1)
   const uint8_t* idpag = (const uint8_t*)cd.blen + (pw.out_offset - sh) * (uint64_t)idw;
-  uint32_t idr[2 * CH_TILES];
+  uint32_t idr[2 * TPW];
 #pragma unroll
-  for (uint32_t t = 0; t < CH_TILES; t++) {
-    const uint32_t ts = j * CH + t * TV;
+  for (uint32_t t = 0; t < TPW; t++) {
+    const uint32_t ts = j * CH + (T0 + t) * TV;
     const uint8_t* ip = idpag + (uint64_t)(ts + E * lane) * idw;
     const bool any = ts + E * lane < s_hi;  // (the id array is padded: the ids after a lane's first are readable)
     if (idw == 1u) {
@@ -1418,17 +1428,41 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
   bool cb_on = false;
   uint32_t cb_w[4] = {0, 0, 0, 0}, cb_lo = 0, cb_hi = 0, cx[4] = {0, 0, 0, 0}, cxlo = 0;
   uint64_t cb_tal = 0;
+  // the wave's first byte: the chunk's plus the bytes of the lower waves' tiles (SPLIT; the waves of a
+  // workgroup then share its chunk, so none of them has returned above)
+  if constexpr (SPLIT) {
+    uint32_t ws = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < TPW; t++) {
+      const uint32_t ts = j * CH + (T0 + t) * TV;
+#pragma unroll
+      for (uint32_t e = 0; e < E; e++) {
+        const uint32_t sl = ts + E * lane + e;
+        const uint32_t id = idw == 1u ? (idr[2 * t] >> (8u * e)) & 0xFFu
+                                      : (idr[2 * t + (e >> 1)] >> (16u * (e & 1u))) & 0xFFFFu;
+        ws += sl >= s_lo && sl < ok_hi && id < dict_n ? ent[id] & 0xFFFFu : 0u;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ws += (uint32_t)__shfl_xor((int)ws, o);
+    if (lane == 0) wsum[wave_id()] = ws;
+    __syncthreads();
+  }
   uint64_t run_base = uni64(bases[c]);
+  if constexpr (SPLIT) {
+    for (uint32_t w = 0; w < wave_id(); w++) run_base += wsum[w];
+    run_base = uni64(run_base);
+  }
 #pragma unroll 1
-  for (uint32_t t = 0; t < CH_TILES; t++) {
+  for (uint32_t t = T0; t < T1; t++) {
     const uint32_t ts = uni(j * CH + t * TV);
     if (ts >= s_hi) break;
     uint32_t ln[E], sr[E], ls = 0;
 #pragma unroll
     for (uint32_t e = 0; e < E; e++) {
       const uint32_t sl = ts + E * lane + e;
-      const uint32_t id = idw == 1u ? (idr[2 * t] >> (8u * e)) & 0xFFu
-                                    : (idr[2 * t + (e >> 1)] >> (16u * (e & 1u))) & 0xFFFFu;
+      const uint32_t id = idw == 1u ? (idr[2 * (t - T0)] >> (8u * e)) & 0xFFu
+                                    : (idr[2 * (t - T0) + (e >> 1)] >> (16u * (e & 1u))) & 0xFFFFu;
       const uint32_t en = sl >= s_lo && sl < ok_hi && id < dict_n ? ent[id] : 0u;
       ln[e] = en & 0xFFFFu;
       sr[e] = en >> 16;
@@ -1471,7 +1505,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
       }
       wave_sync();
       // the tile's last block, when partial, is finished by the next tile of the chunk (same wave)
-      const bool next_tile = t + 1 < CH_TILES && ts + TV < s_hi;
+      const bool next_tile = t + 1 < T1 && ts + TV < s_hi;
       for (uint32_t b = lane; b < nblk; b += WAVE) {
         const uint32_t gb = b << 4;
         uint32_t bs = gb > rb ? gb : rb;
@@ -3326,8 +3360,13 @@ hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes
   hipLaunchKernelGGL(k_dd_bases, dim3(n_dd_cols), dim3(256), 0, st, cols, dd_cols, dd_start, sums);
   e = hipGetLastError();
   if (e != hipSuccess || !n_tile) return e;
-  hipLaunchKernelGGL(k_dd_str, dim3(n_tile), blk, 16u + ((dd_region + 15u) & ~15u) + WPB * DDG_WAVE_BYTES, st, bytes, n_bytes,
-                     work, cols, chunks, n_chunks, pstat, sums, err, err_count, dd_region);
+  const uint32_t dd_lds_bytes = 16u + ((dd_region + 15u) & ~15u) + WPB * DDG_WAVE_BYTES;
+  if (n_chunks <= DD_SPLIT_MAX_CHUNKS)  // few chunks: a workgroup per chunk
+    hipLaunchKernelGGL(k_dd_str<CH_TILES / WPB>, dim3(n_chunks), blk, dd_lds_bytes, st, bytes, n_bytes, work, cols, chunks,
+                       n_chunks, pstat, sums, err, err_count, dd_region);
+  else
+    hipLaunchKernelGGL(k_dd_str<CH_TILES>, dim3(n_tile), blk, dd_lds_bytes, st, bytes, n_bytes, work, cols, chunks, n_chunks,
+                       pstat, sums, err, err_count, dd_region);
   return hipGetLastError();
 }
 
