@@ -3074,7 +3074,6 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     // ---- expand the walked blocks (every read from the LDS segment)
     // (the segment path stores 16-value runs per lane, shifted to 16-byte alignment: pages of
     // nullable columns, which start at any value offset, take it too)
-#ifndef PQG_DELTA_NOEXP  // (diagnostic build: the header walk alone)
     if (!NEG && (mbs % 16u) == 0 && ((uint64_t)block * W) % 16u == 0)
       delta_expand_seg<W>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out);
     else if (E == 1)
@@ -3082,7 +3081,6 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     else if (E == 2) delta_expand<W, NEG, 2>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else if (E == 4) delta_expand<W, NEG, 4>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else delta_expand<W, NEG, 8>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
-#endif
     n_blocks += nb;
   }
   // the value after the last delta of the last block (the expansion stores values up to the one
