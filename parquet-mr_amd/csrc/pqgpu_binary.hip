@@ -2515,31 +2515,49 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5))) v
 __global__ __launch_bounds__(256) void k_bin_bases(PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                    const int32_t* __restrict__ col_pages,
                                                    const int32_t* __restrict__ col_start) {
+  // thread t takes BB_PER consecutive pages per round: all their loads issued before any use (two
+  // dependent round trips per round: the page list, then the pages' facts), a register scan, one
+  // workgroup scan of the threads' totals. (The previous 256-page rounds paid both round trips and
+  // three barriers per 256 pages: C3's two columns of 5,000 pages took 290-640 us on the strings'
+  // queue, ahead of k_bin_plain_pg.)
+  constexpr int BB_PER = 16;
   const int b = col_start[blockIdx.x], e = col_start[blockIdx.x + 1];
   __shared__ uint64_t wsum[4];
-  __shared__ uint64_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int base = b; base < e; base += 256) {
-    const int i = base + (int)threadIdx.x;
-    uint64_t v = 0;
-    if (i < e) {
-      const PageWork& w = work[col_pages[i]];
-      const uint64_t need = (uint64_t)w.data_begin + 4ull * w.n_values;
-      v = w.size > need ? w.size - need : 0;
+  uint64_t carry = 0;
+  for (int r0 = b; r0 < e; r0 += 256 * BB_PER) {
+    const int i0 = r0 + (int)threadIdx.x * BB_PER;
+    int pg[BB_PER];
+#pragma unroll
+    for (int q = 0; q < BB_PER; q++) pg[q] = i0 + q < e ? col_pages[i0 + q] : -1;
+    uint64_t v[BB_PER], own = 0;
+#pragma unroll
+    for (int q = 0; q < BB_PER; q++) {
+      v[q] = 0;
+      if (pg[q] >= 0) {
+        const PageWork& w = work[pg[q]];
+        const uint64_t need = (uint64_t)w.data_begin + 4ull * w.n_values;
+        v[q] = w.size > need ? w.size - need : 0;
+      }
+      own += v[q];
     }
-    uint64_t x = v;
+    uint64_t x = own;
     for (int o = 1; o < 64; o <<= 1) {
       const uint64_t y = __shfl_up(x, o);
       if ((int)lane_id() >= o) x += y;
     }
     if (lane_id() == 63) wsum[threadIdx.x >> 6] = x;
     __syncthreads();
-    uint64_t pre = carry;
-    for (int w = 0; w < (int)(threadIdx.x >> 6); w++) pre += wsum[w];
-    if (i < e) gst(&work[col_pages[i]].bin_base, pre + x - v);
-    __syncthreads();
-    if (threadIdx.x == 255) carry = pre + x;
+    uint64_t pre = carry + x - own, tot = 0;
+    for (int w = 0; w < 4; w++) {
+      pre += w < (int)(threadIdx.x >> 6) ? wsum[w] : 0;
+      tot += wsum[w];
+    }
+#pragma unroll
+    for (int q = 0; q < BB_PER; q++) {
+      if (pg[q] >= 0) gst(&work[pg[q]].bin_base, pre);
+      pre += v[q];
+    }
+    carry += tot;
     __syncthreads();
   }
   if (threadIdx.x == 0 && e > b) {

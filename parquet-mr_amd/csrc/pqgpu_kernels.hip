@@ -2299,28 +2299,42 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5))) v
 // Exclusive scan of non-null counts per column (one workgroup per column).
 __global__ __launch_bounds__(256) void k_scan_offsets(PageWork* __restrict__ work, const int32_t* __restrict__ col_pages,
                                                       const int32_t* __restrict__ col_page_start, int n_cols) {
+  // thread t takes SO_PER consecutive pages per round, all loads issued first (two dependent round
+  // trips per round instead of per 256 pages), one workgroup scan of the threads' totals
+  constexpr int SO_PER = 16;
   const int c = blockIdx.x;
   const int b = col_page_start[c], e = col_page_start[c + 1];
   __shared__ uint64_t warp_sums[4];
-  __shared__ uint64_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int base = b; base < e; base += 256) {
-    int i = base + (int)threadIdx.x;
-    uint64_t v = i < e ? work[col_pages[i]].n_values : 0;
-    // inclusive wave scan
-    uint64_t x = v;
+  uint64_t carry = 0;
+  for (int r0 = b; r0 < e; r0 += 256 * SO_PER) {
+    const int i0 = r0 + (int)threadIdx.x * SO_PER;
+    int pg[SO_PER];
+#pragma unroll
+    for (int q = 0; q < SO_PER; q++) pg[q] = i0 + q < e ? col_pages[i0 + q] : -1;
+    uint64_t v[SO_PER], own = 0;
+#pragma unroll
+    for (int q = 0; q < SO_PER; q++) {
+      v[q] = pg[q] >= 0 ? work[pg[q]].n_values : 0;
+      own += v[q];
+    }
+    uint64_t x = own;
     for (int o = 1; o < 64; o <<= 1) {
-      uint64_t y = __shfl_up(x, o);
+      const uint64_t y = __shfl_up(x, o);
       if ((int)lane_id() >= o) x += y;
     }
     if (lane_id() == 63) warp_sums[threadIdx.x >> 6] = x;
     __syncthreads();
-    uint64_t pre = carry;
-    for (int wv = 0; wv < (int)(threadIdx.x >> 6); wv++) pre += warp_sums[wv];
-    if (i < e) gst(&work[col_pages[i]].out_offset, (uint64_t)(pre + x - v));
-    __syncthreads();
-    if (threadIdx.x == 255) carry = pre + x;
+    uint64_t pre = carry + x - own, tot = 0;
+    for (int wv = 0; wv < 4; wv++) {
+      pre += wv < (int)(threadIdx.x >> 6) ? warp_sums[wv] : 0;
+      tot += warp_sums[wv];
+    }
+#pragma unroll
+    for (int q = 0; q < SO_PER; q++) {
+      if (pg[q] >= 0) gst(&work[pg[q]].out_offset, pre);
+      pre += v[q];
+    }
+    carry += tot;
     __syncthreads();
   }
 }
