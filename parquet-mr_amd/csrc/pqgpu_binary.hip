@@ -1356,6 +1356,80 @@ __device__ __forceinline__ uint64_t dba_off(const ColumnDev& cd, uint64_t v) {
                                                       : (uint64_t)((const int64_t*)cd.values)[v];
 }
 
+// One batch of <= 64 values assembled in LDS and stored (the byte-parallel path): lane k holds value
+// k's length L, prefix length P (<= L), suffix offset sx in the staging sb8 and output offset lx in
+// the batch (ltot bytes in all, <= DBA_OB; every L <= DBA_VB); prevb is the value before the batch,
+// the batch's last value goes to vlast; o_lo: output offset of the batch's first byte.
+__device__ __forceinline__ void dba_batch(DbaPar* par, const uint8_t* sb8, const uint8_t* prevb, uint8_t* vlast, bool in,
+                                          uint32_t L, uint32_t P, uint32_t sx, uint32_t lx, uint32_t ltot, uint32_t nb,
+                                          uint64_t o_lo, uint8_t* dst, uint64_t cap) {
+  const uint32_t lane = lane_id();
+  uint32_t mv = in ? P : 0xFFFFFFFFu;
+#pragma unroll
+  for (uint32_t st = 0; st < 6; st++) {
+    if (st) {
+      const uint32_t y = __shfl_up(mv, 1u << (st - 1));
+      if (lane >= (1u << (st - 1))) mv = y < mv ? y : mv;
+    }
+    par->pmin[st][lane] = mv;
+  }
+  par->sx[lane] = sx;
+  wave_sync();
+  uint32_t ps = 255u;
+  if (in && P > 0) {  // max{y < lane : P_y <= P - 1}
+    int y = (int)lane - 1;
+    const uint32_t th = P - 1u;
+#pragma unroll
+    for (int st = 5; st >= 0; st--)
+      if (y >= (1 << st) - 1 && par->pmin[st][y] > th) y -= 1 << st;
+    ps = y < 0 ? 255u : (uint32_t)y;
+  }
+  par->pse[lane] = (uint8_t)ps;
+  wave_sync();
+  uint8_t* obuf = par->obuf_raw + 16;
+  if (in) {
+    uint8_t* ob = obuf + lx;
+    uint32_t y = lane, hi = L, lo = P, sxy = sx;
+    while (true) {
+      for (uint32_t b = lo; b < hi; b++) ob[b] = sb8[sxy + (b - lo)];  // suffix of y
+      if (lo == 0) break;
+      hi = lo;
+      y = par->pse[y];
+      if (y == 255u) {  // inherited from before the batch
+        for (uint32_t b = 0; b < hi; b++) ob[b] = prevb[b];
+        break;
+      }
+      lo = par->pmin[0][y];
+      sxy = par->sx[y];
+    }
+  }
+  wave_sync();
+  // the batch's bytes -> output, 16-byte blocks (edges shared with the neighbouring
+  // batches / chunks are stored bytewise)
+  const uint64_t o_end = o_lo + ltot;
+  const uint64_t o_hi = o_end < cap ? o_end : cap;
+  const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
+  typedef uint32_t __attribute__((may_alias)) u32a;
+  for (uint64_t a = (o_lo & ~15ull) + 16u * lane; a < o_hi; a += 16u * WAVE) {
+    const int32_t rel = (int32_t)(int64_t)(a - o_lo);  // >= -15
+    const int32_t rb = rel & ~3;
+    const uint32_t sb = (uint32_t)rel & 3u;
+    uint32_t w[5], wd[4], have = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < 5; c++) w[c] = *(const u32a*)(obuf + rb + 4 * (int32_t)c);
+#pragma unroll
+    for (uint32_t c = 0; c < 4; c++) {
+      wd[c] = __builtin_amdgcn_alignbyte(w[c + 1], w[c], sb);
+      const uint64_t d0 = a + 4u * c;
+      if (d0 >= o_lo && d0 + 4u <= o_hi) have |= 1u << c;
+    }
+    store_block16(dst, a, o_lo, o_hi, wd, dst_al4 ? have : 0u, dst_al16);
+  }
+  // the batch's last value becomes the previous value
+  const uint32_t ll = rdl(L, nb - 1), lxl = rdl(lx, nb - 1);
+  for (uint32_t b = lane; b < ll; b += WAVE) vlast[b] = obuf[lxl + b];
+}
+
 // Values [i_beg, i_end) of a page, in order. The previous value is in vbuf[cur ^ 1] when
 // prev_lds; otherwise at output offset prev_off. sp: page-relative position of value i_beg's suffix.
 __device__ __forceinline__ void dba_values(const ColumnDev& cd, uint64_t v0, rsrc_t rs, uint32_t i_beg, uint32_t i_end,
@@ -1391,72 +1465,8 @@ __device__ __forceinline__ void dba_values(const ColumnDev& cd, uint64_t v0, rsr
       const uint32_t lx = wave_excl_scan_u32(L, &ltot);
       ltot = uni(ltot);
       if (lmax <= DBA_VB && ltot <= DBA_OB) {
-        uint32_t mv = in ? P : 0xFFFFFFFFu;
-#pragma unroll
-        for (uint32_t st = 0; st < 6; st++) {
-          if (st) {
-            const uint32_t y = __shfl_up(mv, 1u << (st - 1));
-            if (lane >= (1u << (st - 1))) mv = y < mv ? y : mv;
-          }
-          par->pmin[st][lane] = mv;
-        }
-        par->sx[lane] = sx;
-        wave_sync();
-        uint32_t ps = 255u;
-        if (in && P > 0) {  // max{y < lane : P_y <= P - 1}
-          int y = (int)lane - 1;
-          const uint32_t th = P - 1u;
-#pragma unroll
-          for (int st = 5; st >= 0; st--)
-            if (y >= (1 << st) - 1 && par->pmin[st][y] > th) y -= 1 << st;
-          ps = y < 0 ? 255u : (uint32_t)y;
-        }
-        par->pse[lane] = (uint8_t)ps;
-        wave_sync();
-        uint8_t* obuf = par->obuf_raw + 16;
-        const uint8_t* prevb = vbuf[cur ^ 1];
-        if (in) {
-          uint8_t* ob = obuf + lx;
-          uint32_t y = lane, hi = L, lo = P, sxy = sx;
-          while (true) {
-            for (uint32_t b = lo; b < hi; b++) ob[b] = sb8[sxy + (b - lo)];  // suffix of y
-            if (lo == 0) break;
-            hi = lo;
-            y = par->pse[y];
-            if (y == 255u) {  // inherited from before the batch
-              for (uint32_t b = 0; b < hi; b++) ob[b] = prevb[b];
-              break;
-            }
-            lo = par->pmin[0][y];
-            sxy = par->sx[y];
-          }
-        }
-        wave_sync();
-        // the batch's bytes -> output, 16-byte blocks (edges shared with the neighbouring
-        // batches / chunks are stored bytewise)
         const uint64_t o_lo = ((uint64_t)rdl((uint32_t)(off >> 32), 0) << 32) | rdl((uint32_t)off, 0);
-        const uint64_t o_end = o_lo + ltot;
-        const uint64_t o_hi = o_end < cap ? o_end : cap;
-        const bool dst_al16 = ((uintptr_t)dst & 15u) == 0, dst_al4 = ((uintptr_t)dst & 3u) == 0;
-        typedef uint32_t __attribute__((may_alias)) u32a;
-        for (uint64_t a = (o_lo & ~15ull) + 16u * lane; a < o_hi; a += 16u * WAVE) {
-          const int32_t rel = (int32_t)(int64_t)(a - o_lo);  // >= -15
-          const int32_t rb = rel & ~3;
-          const uint32_t sb = (uint32_t)rel & 3u;
-          uint32_t w[5], wd[4], have = 0;
-#pragma unroll
-          for (uint32_t c = 0; c < 5; c++) w[c] = *(const u32a*)(obuf + rb + 4 * (int32_t)c);
-#pragma unroll
-          for (uint32_t c = 0; c < 4; c++) {
-            wd[c] = __builtin_amdgcn_alignbyte(w[c + 1], w[c], sb);
-            const uint64_t d0 = a + 4u * c;
-            if (d0 >= o_lo && d0 + 4u <= o_hi) have |= 1u << c;
-          }
-          store_block16(dst, a, o_lo, o_hi, wd, dst_al4 ? have : 0u, dst_al16);
-        }
-        // the batch's last value becomes the previous value
-        const uint32_t ll = rdl(L, nb - 1), lxl = rdl(lx, nb - 1);
-        for (uint32_t b = lane; b < ll; b += WAVE) vbuf[cur][b] = obuf[lxl + b];
+        dba_batch(par, sb8, vbuf[cur ^ 1], vbuf[cur], in, L, P, sx, lx, ltot, nb, o_lo, dst, cap);
         cur ^= 1;
         sp += stot;
         wave_sync();  // the next batch overwrites the staging buffers
@@ -1681,15 +1691,61 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chunks(const uint8_t* __restri
   const uint32_t lane = lane_id();
   const uint64_t v0 = pw.out_offset;
   uint8_t(*vbuf)[DBA_VB] = vbuf_all[wave_id()];
-  if (i_lo) {  // previous value -> vbuf[1]
-    const uint32_t lp = uni(cd.blen[v0 + i_lo - 1]);
-    const uint64_t o = dba_off(cd, v0 + i_lo - 1);
-    for (uint32_t b = lane; b < lp; b += WAVE) vbuf[1][b] = o + b < cd.binary_capacity ? cd.binary_data[o + b] : 0;
-    wave_sync();
-  }
+  uint32_t* sbuf = sbuf_all[wave_id()];
+  uint8_t* dst = cd.binary_data;
+  const uint64_t cap = cd.binary_capacity;
   const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
-  const uint32_t sp = uni(pw.aux) + meta[2u * ((uint64_t)pw.chunk_base + j)];
-  dba_values(cd, v0, rs, i_lo, i_hi, uni(sp), vbuf, sbuf_all[wave_id()], 0, true, 0, &par_all[wave_id()]);
+  // every load of the chunk at once, so that the chunk costs two memory round trips (these, then its
+  // suffix bytes and previous value) instead of two per 64-value batch: lengths and prefix lengths
+  // (lane: values 64 q + lane), each batch's output offset, the previous value's length and offset
+  static_assert(BIN_CHUNK == 4 * WAVE, "a chunk is 4 batches of 64 values");
+  const uint32_t n = i_hi - i_lo;
+  uint32_t Lq[4], Pq[4];
+  uint64_t oq[4];
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    const uint32_t i = WAVE * q + lane;
+    const bool in = i < n;
+    Lq[q] = in ? cd.blen[v0 + i_lo + i] : 0u;
+    Pq[q] = in ? cd.bsrc[v0 + i_lo + i] : 0u;
+    oq[q] = WAVE * q < n ? dba_off(cd, v0 + i_lo + WAVE * q) : 0;
+  }
+  const uint32_t lp = i_lo ? uni(cd.blen[v0 + i_lo - 1]) : 0u;
+  const uint64_t po = i_lo ? dba_off(cd, v0 + i_lo - 1) : 0;
+  const uint32_t sp = uni(uni(pw.aux) + meta[2u * ((uint64_t)pw.chunk_base + j)]);
+  uint32_t sxq[4], lxq[4], ltq[4], sbase = 0;
+  bool fits = true;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    Pq[q] = Pq[q] < Lq[q] ? Pq[q] : Lq[q];
+    uint32_t st, lt;
+    sxq[q] = sbase + wave_excl_scan_u32(Lq[q] - Pq[q], &st);
+    lxq[q] = wave_excl_scan_u32(Lq[q], &lt);
+    sbase += uni(st);
+    ltq[q] = uni(lt);
+    fits = fits && ltq[q] <= DBA_OB;
+  }
+  fits = fits && sbase <= DBA_SB;
+  // the chunk's suffix bytes and the previous value (-> vbuf[1])
+  if (fits)
+    for (uint32_t o = 4u * lane; o < sbase; o += 4u * WAVE) sbuf[o >> 2] = ld4_any(rs, sp + o);
+  for (uint32_t b = lane; b < lp; b += WAVE) vbuf[1][b] = po + b < cap ? dst[po + b] : 0;
+  __builtin_amdgcn_s_waitcnt(0);
+  wave_sync();
+  if (!fits) {  // batch by batch, with the per-value path for batches past the LDS buffers
+    dba_values(cd, v0, rs, i_lo, i_hi, sp, vbuf, sbuf, 0, true, 0, &par_all[wave_id()]);
+    return;
+  }
+  uint32_t cur = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    if (WAVE * q >= n) break;
+    const uint32_t nb = n - WAVE * q < WAVE ? n - WAVE * q : WAVE;
+    dba_batch(&par_all[wave_id()], (const uint8_t*)sbuf, vbuf[cur ^ 1], vbuf[cur], WAVE * q + lane < n, Lq[q], Pq[q],
+              sxq[q], lxq[q], ltq[q], nb, oq[q], dst, cap);
+    cur ^= 1;
+    wave_sync();  // the next batch overwrites the batch tables and reads the value just copied
+  }
 }
 
 // PQG_PAGE_DBA_CARRY pages (PARQUET-246): one wave per column walks the column's DELTA_BYTE_ARRAY
