@@ -1334,7 +1334,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
 // A page with a value longer than DBA_VB (PageWork::reserved, set by k_delta) is copied by
 // k_dba_copy, the same per-value loop over the whole page with long previous values read back
 // from the output.
-constexpr uint32_t DBA_SB = 4096;  // LDS suffix staging bytes per batch
+constexpr uint32_t DBA_SB = 3072;  // LDS suffix staging bytes per batch (a chunk, in k_dba_chunks)
 constexpr uint32_t DBA_OB = 4096;  // LDS output bytes of a byte-parallel batch
 
 // LDS of the byte-parallel batch (k_dba_chunks): the batch's values are assembled in obuf, lane
@@ -1344,8 +1344,8 @@ constexpr uint32_t DBA_OB = 4096;  // LDS output bytes of a byte-parallel batch
 // batch's last value.
 struct DbaPar {
   uint8_t obuf_raw[16 + DBA_OB + 32];  // obuf = obuf_raw + 16 (slack for unaligned dword reads)
-  uint32_t pmin[6][WAVE];              // pmin[s][x] = min prefix length over values (x - 2^s, x]
-  uint32_t sx[WAVE];                   // suffix offset of value x in the staging buffer
+  uint16_t pmin[6][WAVE];              // pmin[s][x] = min prefix length over values (x - 2^s, x] (<= DBA_VB)
+  uint16_t sx[WAVE];                   // suffix offset of value x in the staging buffer (<= DBA_SB)
   uint8_t pse[WAVE];                   // previous value with a smaller prefix length (255: none)
 };
 
@@ -1371,9 +1371,9 @@ __device__ __forceinline__ void dba_batch(DbaPar* par, const uint8_t* sb8, const
       const uint32_t y = __shfl_up(mv, 1u << (st - 1));
       if (lane >= (1u << (st - 1))) mv = y < mv ? y : mv;
     }
-    par->pmin[st][lane] = mv;
+    par->pmin[st][lane] = (uint16_t)(mv < 0xFFFFu ? mv : 0xFFFFu);
   }
-  par->sx[lane] = sx;
+  par->sx[lane] = (uint16_t)sx;
   wave_sync();
   uint32_t ps = 255u;
   if (in && P > 0) {  // max{y < lane : P_y <= P - 1}
@@ -1433,8 +1433,9 @@ __device__ __forceinline__ void dba_batch(DbaPar* par, const uint8_t* sb8, const
 // Values [i_beg, i_end) of a page, in order. The previous value is in vbuf[cur ^ 1] when
 // prev_lds; otherwise at output offset prev_off. sp: page-relative position of value i_beg's suffix.
 __device__ __forceinline__ void dba_values(const ColumnDev& cd, uint64_t v0, rsrc_t rs, uint32_t i_beg, uint32_t i_end,
-                                           uint32_t sp, uint8_t (*vbuf)[DBA_VB], uint32_t* sbuf, uint32_t cur,
+                                           uint32_t sp, uint8_t* vb0, uint8_t* vb1, uint32_t* sbuf, uint32_t cur,
                                            bool prev_lds, uint64_t prev_off, DbaPar* par = nullptr) {
+  uint8_t* vbuf[2] = {vb0, vb1};  // value buffers (DBA_VB bytes; one may be par's assembly buffer)
   const uint32_t lane = lane_id();
   uint8_t* dst = cd.binary_data;
   const uint64_t cap = cd.binary_capacity;
@@ -1466,8 +1467,13 @@ __device__ __forceinline__ void dba_values(const ColumnDev& cd, uint64_t v0, rsr
       ltot = uni(ltot);
       if (lmax <= DBA_VB && ltot <= DBA_OB) {
         const uint64_t o_lo = ((uint64_t)rdl((uint32_t)(off >> 32), 0) << 32) | rdl((uint32_t)off, 0);
-        dba_batch(par, sb8, vbuf[cur ^ 1], vbuf[cur], in, L, P, sx, lx, ltot, nb, o_lo, dst, cap);
-        cur ^= 1;
+        if (vbuf[cur ^ 1] == par->obuf_raw + 16) {  // the previous value sits in the assembly buffer
+          for (uint32_t b = lane; b < DBA_VB; b += WAVE) vbuf[cur][b] = vbuf[cur ^ 1][b];
+          wave_sync();
+          cur ^= 1;
+        }
+        // the batch's last value replaces the previous one in the same buffer
+        dba_batch(par, sb8, vbuf[cur ^ 1], vbuf[cur ^ 1], in, L, P, sx, lx, ltot, nb, o_lo, dst, cap);
         sp += stot;
         wave_sync();  // the next batch overwrites the staging buffers
         continue;
@@ -1522,7 +1528,8 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_copy(const uint8_t* __restrict
   if (uni(pw.reserved) != 1u) return;
   const ColumnDev& cd = cols[pw.column];
   const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
-  dba_values(cd, pw.out_offset, rs, 0, uni(pw.n_values), uni(pw.aux), vbuf_all[wave_id()], sbuf_all[wave_id()], 0,
+  dba_values(cd, pw.out_offset, rs, 0, uni(pw.n_values), uni(pw.aux), vbuf_all[wave_id()][0], vbuf_all[wave_id()][1],
+             sbuf_all[wave_id()], 0,
              true, 0);
 }
 
@@ -1678,7 +1685,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chunks(const uint8_t* __restri
                                                          const ColumnDev* __restrict__ cols,
                                                          const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                          const uint32_t* __restrict__ meta) {
-  __shared__ uint8_t vbuf_all[WPB][2][DBA_VB];
+  __shared__ uint8_t vbuf_all[WPB][DBA_VB];  // the previous value (one buffer: 4 waves per SIMD)
   __shared__ uint32_t sbuf_all[WPB][DBA_SB / 4 + 1];
   __shared__ __attribute__((aligned(16))) DbaPar par_all[WPB];
   const uint32_t c = blockIdx.x * WPB + wave_id();
@@ -1690,7 +1697,8 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chunks(const uint8_t* __restri
   const ColumnDev& cd = cols[pw.column];
   const uint32_t lane = lane_id();
   const uint64_t v0 = pw.out_offset;
-  uint8_t(*vbuf)[DBA_VB] = vbuf_all[wave_id()];
+  uint8_t* vb = vbuf_all[wave_id()];
+  DbaPar* par = &par_all[wave_id()];
   uint32_t* sbuf = sbuf_all[wave_id()];
   uint8_t* dst = cd.binary_data;
   const uint64_t cap = cd.binary_capacity;
@@ -1726,24 +1734,24 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chunks(const uint8_t* __restri
     fits = fits && ltq[q] <= DBA_OB;
   }
   fits = fits && sbase <= DBA_SB;
-  // the chunk's suffix bytes and the previous value (-> vbuf[1])
+  // the chunk's suffix bytes and the previous value (-> vb)
   if (fits)
     for (uint32_t o = 4u * lane; o < sbase; o += 4u * WAVE) sbuf[o >> 2] = ld4_any(rs, sp + o);
-  for (uint32_t b = lane; b < lp; b += WAVE) vbuf[1][b] = po + b < cap ? dst[po + b] : 0;
+  for (uint32_t b = lane; b < lp; b += WAVE) vb[b] = po + b < cap ? dst[po + b] : 0;
   __builtin_amdgcn_s_waitcnt(0);
   wave_sync();
   if (!fits) {  // batch by batch, with the per-value path for batches past the LDS buffers
-    dba_values(cd, v0, rs, i_lo, i_hi, sp, vbuf, sbuf, 0, true, 0, &par_all[wave_id()]);
+    // (the assembly buffer is the per-value path's second value buffer: previous value in vb = vbuf[cur ^ 1])
+    dba_values(cd, v0, rs, i_lo, i_hi, sp, par->obuf_raw + 16, vb, sbuf, 0, true, 0, par);
     return;
   }
-  uint32_t cur = 0;
 #pragma unroll
   for (uint32_t q = 0; q < 4; q++) {
     if (WAVE * q >= n) break;
     const uint32_t nb = n - WAVE * q < WAVE ? n - WAVE * q : WAVE;
-    dba_batch(&par_all[wave_id()], (const uint8_t*)sbuf, vbuf[cur ^ 1], vbuf[cur], WAVE * q + lane < n, Lq[q], Pq[q],
-              sxq[q], lxq[q], ltq[q], nb, oq[q], dst, cap);
-    cur ^= 1;
+    // the batch's last value replaces the previous one in vb (read only during the assembly)
+    dba_batch(par, (const uint8_t*)sbuf, vb, vb, WAVE * q + lane < n, Lq[q], Pq[q], sxq[q], lxq[q], ltq[q], nb, oq[q],
+              dst, cap);
     wave_sync();  // the next batch overwrites the batch tables and reads the value just copied
   }
 }
@@ -1805,7 +1813,7 @@ __global__ __launch_bounds__(64) void k_dba_carry(const uint8_t* __restrict__ by
       }
     }
     const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
-    dba_values(cd, v0, rs, 0, nv, uni(pw.aux), vbuf, sbuf, 0, prev_lds, prev_off);
+    dba_values(cd, v0, rs, 0, nv, uni(pw.aux), vbuf[0], vbuf[1], sbuf, 0, prev_lds, prev_off);
   }
 }
 
