@@ -112,6 +112,28 @@ def pyarrow_baseline(values, budget_s, threads):
             "sample": f"pyarrow {pa.__version__} read_table of the same 100M values (its own pages), {reps} reps"}
 
 
+def store_ceiling(nbytes, device, stream, reps=10):
+    """Write-only HBM rate of this box for the headline's output size, in GB/s: torch's fill_ of an
+    nbytes int64 buffer on the decode stream (the expansion's stores alone, without its reads or walks),
+    best of `reps`, timed with HIP events on that stream. The decode's achieved rate is reported against
+    both this and the nominal 8 TB/s."""
+    import torch
+    buf = torch.empty(nbytes // 8, dtype=torch.int64, device=device)
+    best = None
+    with torch.cuda.stream(stream):
+        buf.fill_(0)
+        for r in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            buf.fill_(r)
+            e1.record(stream)
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None or ms < best else best
+    del buf
+    return nbytes / (best / 1e3) / 1e9
+
+
 def link_ceiling(out_bytes, in_bytes, device, reps=5):
     """The PCIe link alone on this box, best of `reps`, in GB/s: one pinned hipMemcpyAsync of the
     decoded column's size (device -> host) and of the encoded pages' size (host -> device); the
@@ -502,6 +524,7 @@ def main():
     avg_launch_s = float(np.mean(per_launch_ms)) / 1e3
     algo_bytes = n * 8 + data_bytes  # per launch: int64 out + encoded data-page bytes read
     achieved = algo_bytes / avg_launch_s / 1e9
+    st_ceil = store_ceiling(n * 8, cols[0].typed().device, stream)
 
     e2e = None
     if args.e2e and rank == 0:
@@ -580,7 +603,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_bytes_per_launch": traffic_bytes, "traffic_source": traffic_src,
                          "kernel": "pqg::k_dict_fused<8> (avg_launch_ms: whole plan launch, one dispatch, incl. the ~6 us dispatch-to-dispatch gap)", "algorithmic_bytes_per_launch": algo_bytes,
-                         "avg_launch_ms": avg_launch_s * 1e3},
+                         "avg_launch_ms": avg_launch_s * 1e3,
+                         "store_ceiling": st_ceil, "frac_of_store_ceiling": achieved / st_ceil,
+                         "store_ceiling_note": "GB/s of a torch fill_ of the 800 MB output on the same stream, "
+                                               "best of 10 (write-only; measured live in this run)"},
             "cpu_baseline": cpu,
             "input_gen_s": t_gen,
         }

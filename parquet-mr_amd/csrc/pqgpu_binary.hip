@@ -1327,8 +1327,9 @@ __global__ __launch_bounds__(64 * WPB) void k_bin_copy(const uint8_t* __restrict
 // come from chunk c's own suffixes. So:
 //   k_dba_tail    (one wave per chunk)  writes the own bytes [m_c, |T_c|) of T_c into the output:
 //                 value y of the chunk supplies bytes [P_y, min P_{y+1..last}) (suffix minimum);
-//   k_dba_chain   (one wave per page)   follows T_0, T_1, ... with T in LDS and writes the
-//                 inherited bytes [0, m_c) of every T_c: one short step per chunk;
+//   k_dba_chain_par (one wave per chunk) writes the inherited bytes [0, m_c) of every T_c, each
+//                 copied from the last earlier T whose own bytes hold it (k_dba_chain: pages of more
+//                 than DCP chunks follow T_0, T_1, ... in LDS, one short step per chunk);
 //   k_dba_chunks  (one wave per chunk)  with T_{c-1} read back as the previous value, assembles
 //                 the chunk's values one after another (LDS, byte-parallel per value).
 // A page with a value longer than DBA_VB (PageWork::reserved, set by k_delta) is copied by
@@ -1549,12 +1550,19 @@ __device__ __forceinline__ bool dba_chunk(const PageWork* work, const uint64_t* 
 }
 
 // Own bytes of the chunk's last value: value y supplies bytes [P_y, R_y), R_y = min(P_{y+1..last})
-// (R_last = its length); those intervals tile [m_c, L_last).
+// (R_last = its length); those intervals tile [m_c, L_last). Byte b's supplier is therefore
+// y(b) = max{y : P_y <= b}, found per byte by a descent over a prefix-min table of the chunk's P (the
+// batch assembly's previous-smaller search): one lane per byte, every byte's load in flight at once
+// (a lane walking its values' byte ranges waited for one load per byte).
 __global__ __launch_bounds__(64 * WPB) void k_dba_tail(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                        const PageWork* __restrict__ work,
                                                        const ColumnDev* __restrict__ cols,
                                                        const uint64_t* __restrict__ chunks, uint32_t n_chunks,
                                                        const uint32_t* __restrict__ meta) {
+  static_assert(BIN_CHUNK == 4 * WAVE, "a chunk is 4 values per lane");
+  constexpr uint32_t LV = 8;                        // table levels: windows of 1 .. 128 values
+  __shared__ uint16_t pm_all[WPB][LV][BIN_CHUNK];   // pm[s][x] = min P over values (x - 2^s, x] (<= DBA_VB)
+  __shared__ uint32_t sx_all[WPB][BIN_CHUNK];       // suffix offset of value x in the chunk
   const uint32_t c = blockIdx.x * WPB + wave_id();
   if (c >= n_chunks) return;
   int page;
@@ -1565,58 +1573,147 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_tail(const uint8_t* __restrict
   const uint32_t lane = lane_id();
   const uint64_t v0 = pw.out_offset;
   const uint32_t n = i_hi - i_lo;
+  const uint32_t last = n - 1;
+  uint16_t(*pm)[BIN_CHUNK] = pm_all[wave_id()];
+  uint32_t* sxa = sx_all[wave_id()];
   // lane holds values y = 4 * lane + q of the chunk
-  uint32_t Lq[4], Pq[4], Sq[4], s_lane = 0, m_lane = 0xFFFFFFFFu;
+  uint32_t Lq[4], Pq[4], s_lane = 0;
 #pragma unroll
   for (uint32_t q = 0; q < 4; q++) {
     const uint32_t y = 4u * lane + q;
     const bool in = y < n;
     Lq[q] = in ? cd.blen[v0 + i_lo + y] : 0u;
-    const uint32_t p = in ? cd.bsrc[v0 + i_lo + y] : 0u;
-    Pq[q] = in ? (p < Lq[q] ? p : Lq[q]) : 0xFFFFFFFFu;
-    Sq[q] = in ? Lq[q] - Pq[q] : 0u;
-    s_lane += Sq[q];
+    Pq[q] = in ? cd.bsrc[v0 + i_lo + y] : 0u;
   }
-  const uint32_t last = n - 1;
   const uint32_t L_last = uni(cd.blen[v0 + i_lo + last]);
-  if (L_last == 0) return;
-  uint32_t stot;
-  const uint32_t sx_lane = wave_excl_scan_u32(s_lane, &stot);
-  // suffix minimum of P over the following values: within the lane, then over the later lanes
-#pragma unroll
-  for (uint32_t q = 0; q < 4; q++) m_lane = Pq[q] < m_lane ? Pq[q] : m_lane;
-  uint32_t after = 0xFFFFFFFFu;  // min over lanes > this lane
-  {
-    uint32_t x = m_lane;  // inclusive suffix min over lanes >= this one
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_down(x, o);
-      if ((int)lane + o < 64) x = y < x ? y : x;
-    }
-    after = __shfl_down(x, 1);
-    if (lane == 63) after = 0xFFFFFFFFu;
-  }
+  const uint64_t o_last = dba_off(cd, v0 + i_lo + last);
   const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
   const uint32_t sp = uni(pw.aux) + meta[2u * ((uint64_t)pw.chunk_base + j)];
-  const uint64_t o_last = dba_off(cd, v0 + i_lo + last);
+  if (L_last == 0) return;  // (an error in the chunk leaves its last value empty)
+  uint32_t pmin_l = 0xFFFFu;
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    const uint32_t y = 4u * lane + q;
+    const uint32_t P = y < n ? (Pq[q] < Lq[q] ? Pq[q] : Lq[q]) : 0xFFFFu;
+    s_lane += y < n ? Lq[q] - P : 0u;
+    pm[0][y] = (uint16_t)P;
+  }
+  uint32_t stot;
+  uint32_t sx = wave_excl_scan_u32(s_lane, &stot);
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) {
+    const uint32_t y = 4u * lane + q;
+    sxa[y] = sx;
+    const uint32_t P = pm[0][y];
+    pmin_l = P < pmin_l ? P : pmin_l;
+    sx += y < n ? Lq[q] - P : 0u;
+  }
+  const uint32_t m_c = uni(wave_min_u32(pmin_l));
+  wave_sync();
+  for (uint32_t sl = 1; sl < LV; sl++) {
+    const uint32_t h = 1u << (sl - 1);
+    uint32_t v[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+      const uint32_t x = 4u * lane + q;
+      const uint32_t a = pm[sl - 1][x], b = x >= h ? pm[sl - 1][x - h] : 0xFFFFu;
+      v[q] = a < b ? a : b;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) pm[sl][4u * lane + q] = (uint16_t)v[q];
+    wave_sync();
+  }
   uint8_t* dst = cd.binary_data;
   const uint64_t cap = cd.binary_capacity;
-  uint32_t R = after, sx = sx_lane;
-  uint32_t sxq[4];
+  for (uint32_t b0 = m_c; b0 < L_last; b0 += WAVE) {
+    const uint32_t b = b0 + lane;
+    if (b < L_last) {
+      int y = (int)last;
 #pragma unroll
-  for (uint32_t q = 0; q < 4; q++) { sxq[q] = sx; sx += Sq[q]; }
+      for (int sl = LV - 1; sl >= 0; sl--)
+        if (y >= (1 << sl) - 1 && (uint32_t)pm[sl][y] > b) y -= 1 << sl;
+      y = y < 0 ? 0 : y;  // (b >= m_c: found)
+      const uint32_t a = sp + sxa[y] + (b - pm[0][y]);
+      const uint32_t v = (ld32(rs, a & ~3u) >> ((a & 3u) * 8u)) & 0xFFu;
+      if (o_last + b < cap) gst(dst + o_last + b, (uint8_t)v);
+    }
+  }
+}
+
+// Inherited bytes of every chunk's last value, all chunks at once (pages of at most DCP chunks; the
+// serial k_dba_chain below takes the others). With k_c = min(m_c, |T_c|) the bytes T_c inherits (k_0 =
+// 0: T_0 is all own bytes), T_c[b] = T_{c-1}[b] for b < k_c unrolls to T_c[b] = T_{c*}[b] with
+// c* = max{c' < c : k_{c'} <= b}: an own byte of T_{c*}, written by k_dba_tail (an earlier launch). One
+// wave per chunk finds c* per byte by a descent over a min table of the page's k (the previous-smaller
+// search of the batch assembly, over chunks), then copies the bytes: no per-page serial step.
+constexpr uint32_t DCP = 256;     // chunks per page of the parallel chain
+constexpr uint32_t DCP_LV = 8;    // table levels: windows of 1 .. 2^(DCP_LV - 1) chunks (descent reach 2^DCP_LV - 1)
+__global__ __launch_bounds__(64 * WPB) void k_dba_chain_par(const PageWork* __restrict__ work,
+                                                            const ColumnDev* __restrict__ cols,
+                                                            const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                            const uint32_t* __restrict__ meta) {
+  __shared__ uint16_t mk_all[WPB][DCP_LV][DCP];  // mk[s][x] = min k over chunks (x - 2^s, x]
+  const uint32_t cid = blockIdx.x * WPB + wave_id();
+  if (cid >= n_chunks) return;
+  int page;
+  uint32_t j, i_lo, i_hi;
+  if (!dba_chunk(work, chunks, cid, page, j, i_lo, i_hi) || j == 0) return;
+  const PageWork& pw = work[page];
+  const uint32_t nv = uni(pw.n_values);
+  const uint32_t nch = (nv + BIN_CHUNK - 1) / BIN_CHUNK;
+  if (nch > DCP) return;
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t lane = lane_id();
+  const uint64_t v0 = pw.out_offset;
+  uint8_t* dst = cd.binary_data;
+  const uint64_t cap = cd.binary_capacity;
+  const uint32_t* m = meta + 2u * (uint64_t)pw.chunk_base;
+  uint16_t(*mk)[DCP] = mk_all[wave_id()];
+  auto last_of = [&](uint32_t c) __attribute__((always_inline)) {
+    return (c + 1) * BIN_CHUNK < nv ? (c + 1) * BIN_CHUNK - 1 : nv - 1;
+  };
+  // k of chunks 0 .. j (k_j: the bytes this chunk's last value inherits); lengths <= DBA_VB (16 bits)
+  uint32_t kq[DCP / WAVE];
 #pragma unroll
-  for (int q = 3; q >= 0; q--) {
-    const uint32_t y = 4u * lane + (uint32_t)q;
-    if (y < n) {
-      const uint32_t hi = y == last ? L_last : (R < Lq[q] ? R : Lq[q]);
-      for (uint32_t b = Pq[q]; b < hi; b++) {
-        const uint32_t a = sp + sxq[q] + (b - Pq[q]);
-        const uint32_t v = (ld32(rs, a & ~3u) >> ((a & 3u) * 8u)) & 0xFFu;
-        if (o_last + b < cap) gst(dst + o_last + b, (uint8_t)v);
+  for (uint32_t r = 0; r < DCP / WAVE; r++) {
+    const uint32_t c = lane + r * WAVE;
+    uint32_t k = 0;
+    if (c > 0 && c <= j) {
+      const uint32_t Ll = cd.blen[v0 + last_of(c)], mc = m[2u * c + 1u];
+      k = mc < Ll ? mc : Ll;
+    }
+    kq[r] = k;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < DCP / WAVE; r++)
+    if (lane + r * WAVE <= j) mk[0][lane + r * WAVE] = (uint16_t)kq[r];
+  wave_sync();
+  const uint32_t kj = uni((uint32_t)mk[0][j]);
+  if (kj == 0) return;
+  for (uint32_t s = 1; s < DCP_LV; s++) {
+#pragma unroll
+    for (uint32_t r = 0; r < DCP / WAVE; r++) {
+      const uint32_t x = lane + r * WAVE;
+      if (x < j) {
+        const uint32_t h = 1u << (s - 1);
+        const uint32_t a = mk[s - 1][x], b = x >= h ? mk[s - 1][x - h] : 0xFFFFu;
+        mk[s][x] = (uint16_t)(a < b ? a : b);
       }
     }
-    R = Pq[q] < R ? Pq[q] : R;
+    wave_sync();
+  }
+  const uint64_t oj = dba_off(cd, v0 + last_of(j));
+  for (uint32_t b0 = 0; b0 < kj; b0 += WAVE) {
+    const uint32_t b = b0 + lane;
+    if (b >= kj) break;
+    // c* = max{c' <= j - 1 : k_{c'} <= b} (k_0 = 0: always found)
+    int y = (int)j - 1;
+#pragma unroll
+    for (int sl = DCP_LV - 1; sl >= 0; sl--)
+      if (y >= (1 << sl) - 1 && (uint32_t)mk[sl][y] > b) y -= 1 << sl;
+    y = y < 0 ? 0 : y;
+    const uint64_t os = dba_off(cd, v0 + last_of((uint32_t)y));
+    if (os + b < cap && oj + b < cap) gst(dst + oj + b, dst[os + b]);
   }
 }
 
@@ -1635,7 +1732,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dba_chain(const PageWork* __restri
   const uint32_t lane = lane_id();
   const uint32_t nv = uni(pw.n_values);
   const uint32_t nch = (nv + BIN_CHUNK - 1) / BIN_CHUNK;
-  if (nch <= 1) return;
+  if (nch <= 1 || nch <= DCP) return;  // (pages of <= DCP chunks: k_dba_chain_par)
   const uint64_t v0 = pw.out_offset;
   uint8_t* dst = cd.binary_data;
   const uint64_t cap = cd.binary_capacity;
@@ -2711,6 +2808,7 @@ hipError_t launch_dba_copy(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
   if (n_chunks) {
     const dim3 gc((n_chunks + WPB - 1) / WPB);
     hipLaunchKernelGGL(k_dba_tail, gc, dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, chunks, n_chunks, dba_meta);
+    hipLaunchKernelGGL(k_dba_chain_par, gc, dim3(64 * WPB), 0, st, work, cols, chunks, n_chunks, dba_meta);
     hipLaunchKernelGGL(k_dba_chain, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, work, cols, list, n, dba_meta);
     hipLaunchKernelGGL(k_dba_chunks, gc, dim3(64 * WPB), 0, st, bytes, n_bytes, work, cols, chunks, n_chunks, dba_meta);
   }

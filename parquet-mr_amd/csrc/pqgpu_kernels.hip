@@ -3176,61 +3176,90 @@ __global__ __launch_bounds__(64 * WPB) void k_delta(const uint8_t* __restrict__ 
     // per BIN_CHUNK-value chunk of the page, for the chunk-parallel value copy (k_dba_tail /
     // k_dba_chain / k_dba_chunks): suffix bytes before the chunk, smallest prefix length in it
     uint32_t* meta = dba_meta + 2u * (uint64_t)pw.chunk_base;
-    uint32_t cmin = 0xFFFFFFFFu, lmax = 0;
+    uint32_t lmax = 0;
     // the lengths were just stored by this wave: wait for them, then read past the L1 (a line
     // shared with a neighbouring page may sit in this CU's L1 from before those stores)
     __builtin_amdgcn_s_waitcnt(0);
-    // DG batches of lengths are loaded before the stores of any of them (a load issued after
-    // stores waits for them: one drain per DG batches, not per batch)
-    constexpr uint32_t DG = 8;
-    for (uint32_t g0 = 0; g0 < n_chk; g0 += DG * WAVE) {
-    int32_t pre_g[DG], suf_g[DG];
+    // Rounds of DG chunks (BIN_CHUNK = 256 values: lane l holds values 4 l .. 4 l + 3 of a chunk): every
+    // length of a round is loaded before the stores of any of it (a load issued after stores waits for
+    // them), and a chunk costs one wave scan, min, max and ballot for 256 values (the lane's 4 values
+    // are chained in registers), where one per 64 values left the check at half of the kernel.
+    static_assert(BIN_CHUNK == 4 * WAVE, "a chunk is 4 values per lane");
+    constexpr uint32_t DG = 4;
+    for (uint32_t g0 = 0; g0 < n_chk; g0 += DG * BIN_CHUNK) {
+    int32_t pre_g[DG][4], suf_g[DG][4];
 #pragma unroll
-    for (uint32_t q = 0; q < DG; q++) {
-      const uint32_t i = g0 + q * WAVE + lane;
-      pre_g[q] = i < n_chk ? (int32_t)sld(pl + i) : 0;
-      suf_g[q] = i < n_chk ? (int32_t)sld(sl + i) : 0;
-    }
+    for (uint32_t d = 0; d < DG; d++)
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t i = g0 + d * BIN_CHUNK + 4u * lane + q;
+        pre_g[d][q] = i < n_chk ? (int32_t)sld(pl + i) : 0;
+        suf_g[d][q] = i < n_chk ? (int32_t)sld(sl + i) : 0;
+      }
     __builtin_amdgcn_s_waitcnt(0);
 #pragma unroll
-    for (uint32_t q = 0; q < DG; q++) {
-      const uint32_t i0 = g0 + q * WAVE;
-      if (i0 >= n_chk) break;
-      const uint32_t i = i0 + lane;
-      const bool in = i < n_chk;
-      const int32_t pre = pre_g[q];
-      const int32_t suf = suf_g[q];
-      const uint64_t sv = suf > 0 ? (uint64_t)suf : 0;
-      const uint64_t incl = wave_incl_scan_u64(sv);
-      const int32_t full = (int32_t)((uint32_t)pre + (uint32_t)suf);
-      uint32_t prev = __shfl_up((uint32_t)(full < 0 ? 0 : full), 1);
-      if (lane == 0) prev = prev_len;
-      int c = 0;
-      if (in) {
-        if (suf < 0) c = PQG_ERR_CORRUPT;
-        else if (s_carry + incl > avail) c = PQG_ERR_EOF;
-        else if (pre != 0 && (full < 0 || pre < 0 || ((uint32_t)pre > prev && !(carry && i == 0)))) c = PQG_ERR_CORRUPT;
-        else if (fixw && full != fixw) c = PQG_ERR_CORRUPT;
+    for (uint32_t d = 0; d < DG; d++) {
+      const uint32_t c0 = g0 + d * BIN_CHUNK;  // the chunk's first value
+      if (c0 >= n_chk) break;
+      const uint32_t ib = c0 + 4u * lane;       // the lane's first value
+      uint64_t sv_sum = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) sv_sum += suf_g[d][q] > 0 ? (uint64_t)suf_g[d][q] : 0;
+      const uint64_t incl_l = wave_incl_scan_u64(sv_sum);
+      uint64_t run = s_carry + incl_l - sv_sum;  // suffix bytes before the lane's first value
+      // previous value's length (clamped at 0) for the lane's first value: the last of lane - 1
+      const int32_t f3 = (int32_t)((uint32_t)pre_g[d][3] + (uint32_t)suf_g[d][3]);
+      const uint32_t up = __shfl_up((uint32_t)(f3 < 0 ? 0 : f3), 1);
+      uint32_t prev = lane == 0 ? prev_len : up;
+      uint32_t bad_i = 0xFFFFFFFFu;
+      int bad_c = 0;
+      int32_t full[4];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t i = ib + q;
+        const int32_t pre = pre_g[d][q], suf = suf_g[d][q];
+        full[q] = (int32_t)((uint32_t)pre + (uint32_t)suf);
+        run += suf > 0 ? (uint64_t)suf : 0;
+        int c = 0;
+        if (i < n_chk) {
+          if (suf < 0) c = PQG_ERR_CORRUPT;
+          else if (run > avail) c = PQG_ERR_EOF;
+          else if (pre != 0 && (full[q] < 0 || pre < 0 || ((uint32_t)pre > prev && !(carry && i == 0)))) c = PQG_ERR_CORRUPT;
+          else if (fixw && full[q] != fixw) c = PQG_ERR_CORRUPT;
+        }
+        if (c && bad_i == 0xFFFFFFFFu) {
+          bad_i = i;
+          bad_c = c;
+        }
+        prev = full[q] < 0 ? 0u : (uint32_t)full[q];
       }
-      if (c) report(err, err_count, page, 2, i, c);
-      const uint64_t bad = __ballot(c != 0);
-      if (bad && first_bad == 0xFFFFFFFFu) first_bad = i0 + (uint32_t)__builtin_ctzll(bad);
+      // the page's first invalid value (the reference throws there): reported once, every value from
+      // it on gets length 0
+      const uint32_t wb = uni(wave_min_u32(bad_i));
+      if (wb != 0xFFFFFFFFu && first_bad == 0xFFFFFFFFu) {
+        first_bad = wb;
+        if (bad_i == wb) report(err, err_count, page, 2, wb, bad_c);
+      }
       const uint32_t fb = uni(first_bad);
-      const uint32_t Lf = (c || i >= fb) ? 0u : (uint32_t)full;
-      if (in) gst(sl + i, Lf);
-      if ((i0 % BIN_CHUNK) == 0 && lane == 0) gst(meta + 2u * (i0 / BIN_CHUNK), (uint32_t)s_carry);
-      {
-        const uint32_t pf = !in ? 0xFFFFFFFFu : (Lf ? (uint32_t)pre : 0u);  // the copy's prefix: min(prefix, length)
-        const uint32_t mn = wave_min_u32(pf), mx = wave_max_u32(in ? Lf : 0u);
-        cmin = mn < cmin ? mn : cmin;
-        lmax = mx > lmax ? mx : lmax;
+      uint32_t pmn = 0xFFFFFFFFu, lmx = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t i = ib + q;
+        if (i >= n_chk) break;
+        const uint32_t Lf = i >= fb ? 0u : (uint32_t)full[q];
+        gst(sl + i, Lf);
+        const uint32_t pf = Lf ? (uint32_t)pre_g[d][q] : 0u;  // the copy's prefix: min(prefix, length)
+        pmn = pf < pmn ? pf : pmn;
+        lmx = Lf > lmx ? Lf : lmx;
       }
-      if (((i0 + WAVE) % BIN_CHUNK) == 0 || i0 + WAVE >= n_chk) {
-        if (lane == 0) gst(meta + 2u * (i0 / BIN_CHUNK) + 1u, cmin);
-        cmin = 0xFFFFFFFFu;
+      const uint32_t cmin = wave_min_u32(pmn), mx = wave_max_u32(lmx);
+      lmax = mx > lmax ? mx : lmax;
+      if (lane == 0) {
+        gst(meta + 2u * (c0 / BIN_CHUNK), (uint32_t)s_carry);
+        gst(meta + 2u * (c0 / BIN_CHUNK) + 1u, cmin);
       }
-      prev_len = rdl((uint32_t)(full < 0 ? 0 : full), WAVE - 1);
-      s_carry += rdl((uint32_t)incl, WAVE - 1) | ((uint64_t)rdl((uint32_t)(incl >> 32), WAVE - 1) << 32);
+      prev_len = rdl(prev, WAVE - 1);
+      s_carry += rdl((uint32_t)incl_l, WAVE - 1) | ((uint64_t)rdl((uint32_t)(incl_l >> 32), WAVE - 1) << 32);
     }
     }
     // chunks past the checked values hold no bytes

@@ -254,6 +254,12 @@ def test_delta_byte_array(decoder, kind, n):
     run_both(decoder, [make(abi.BYTE_ARRAY, _dba_vals(kind, n, 5), abi.DELTA_BYTE_ARRAY, page_rows=5000)])
 
 
+def test_delta_byte_array_long_pages(decoder):
+    # pages of more than 256 chunks of 256 values: the serial chain (k_dba_chain) beside the per-chunk one
+    vals = _dba_vals("urls", 150_000, 9)
+    run_both(decoder, [make(abi.BYTE_ARRAY, vals, abi.DELTA_BYTE_ARRAY, page_rows=70_000)])
+
+
 @pytest.mark.parametrize("version", [1, 2])
 @pytest.mark.parametrize("null_frac", [0.2, 1.0])
 def test_delta_byte_array_optional(decoder, version, null_frac):
