@@ -10,8 +10,10 @@ one-per-GPU, no data-path collective: weak scaling); value = all ranks' values /
 max-over-ranks time.
 
 Prints ONE JSON line on rank 0. Extra objects: "roofline" (dominant kernel
-k_dict<8>, HBM-bound) and "cpu_baseline" (the oracle's value-at-a-time port of
-the reference reader, 1 thread, bounded sample).
+k_dict<8>, HBM-bound), "cpu_baseline" (the oracle's value-at-a-time port of
+the reference reader, 1 thread, bounded sample) and, at N=1, "e2e_host_path" (the
+PCIe-inclusive pqg_decode_host rate with the pinned D2H link ceiling measured in the
+same run; never `value`).
 """
 import argparse
 import json
@@ -417,7 +419,9 @@ def main():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the timed RCCL all-gather of the column")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default=None)
-    ap.add_argument("--e2e", action="store_true", help="also time the host-bytes-in / host-array-out path")
+    ap.add_argument("--e2e", action="store_true",
+                    help="time the host-bytes-in / host-array-out path (default on at N=1, rank 0)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host path (profiling runs)")
     ap.add_argument("--traffic-json", default=TRAFFIC_JSON,
                     help="rocprofv3 PMC traffic summary of this kernel (tools/pmc_summary.py --json)")
     args = ap.parse_args()
@@ -527,7 +531,7 @@ def main():
     st_ceil = store_ceiling(n * 8, cols[0].typed().device, stream)
 
     e2e = None
-    if args.e2e and rank == 0:
+    if rank == 0 and (args.e2e or (world == 1 and not args.no_e2e)):
         times, native_s = [], []
         for _ in range(3):  # best of 3 (the first call also allocates and pins the staging buffers)
             t1 = time.perf_counter()

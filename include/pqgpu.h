@@ -28,12 +28,15 @@
  * valid only after pqg_sync returns: two rare cases are repaired by pqg_sync
  * itself with a host-driven re-launch (a PLAIN BYTE_ARRAY page with bytes
  * after its values, pqg_plan_plain_fallbacks; a fused-kernel timeout,
- * pqg_plan_timeout_fallbacks), so work ordered after a launch on the ctx
+ * pqg_plan_timeout_fallbacks; a wrong V2 header null count,
+ * pqg_plan_null_hint_fallbacks), so work ordered after a launch on the ctx
  * stream by events alone may see outputs that pqg_sync later rewrites.
  * No exception crosses this ABI: every function returns a pqg_error code and
  * fills an optional pqg_status.
  *
- * ABI 3 (this version): per-page errors (pqg_page_errors) so that a failure
+ * ABI 4 (this version): pqg_page_desc carries the V2 header's num_nulls
+ * (PQG_PAGE_NULL_COUNT, 56-byte descriptor), pqg_plan_null_hint_fallbacks.
+ * ABI 3: per-page errors (pqg_page_errors) so that a failure
  * surfaces in its own column only; the staged host path (pqg_host_input /
  * pqg_decode_staged / pqg_staged_column) for callers that must not hold host
  * arrays across device work (JNI critical regions); the host batch of router
@@ -49,7 +52,7 @@
 extern "C" {
 #endif
 
-#define PQG_ABI_VERSION 3
+#define PQG_ABI_VERSION 4
 
 /* parquet-format `Type` values (parquet.thrift). */
 enum pqg_physical_type {
@@ -129,6 +132,8 @@ typedef struct pqg_page_desc {
   uint32_t rl_byte_length; /* V2 only: repetition_levels_byte_length */
   uint32_t dl_byte_length; /* V2 only: definition_levels_byte_length */
   uint32_t flags;          /* PQG_PAGE_* (0 for a page written by a current writer) */
+  uint32_t num_nulls;      /* V2 only, read when flags has PQG_PAGE_NULL_COUNT: DataPageHeaderV2.num_nulls (ABI 4) */
+  uint32_t reserved;       /* 0 (sizeof(pqg_page_desc) = 56) */
 } pqg_page_desc;
 
 /* pqg_page_desc.flags: PQG_PAGE_DBA_CARRY — a DELTA_BYTE_ARRAY page whose reader takes the previous
@@ -144,6 +149,19 @@ typedef struct pqg_page_desc {
  * reader to DeltaByteArrayReader), otherwise PQG_ERR_UNSUPPORTED. Flagged pages are decoded in page
  * order, one column at a time. */
 #define PQG_PAGE_DBA_CARRY 1
+
+/* pqg_page_desc.flags: PQG_PAGE_NULL_COUNT — `num_nulls` holds the DataPageV2 header's null count
+ * (DataPageV2.getNullCount, parquet-column/src/main/java/org/apache/parquet/column/page/DataPageV2.java:197-199;
+ * pqg_pages_from_headers sets it for every V2 page). The reference never trusts that count: it decodes
+ * the definition levels and reads a value for every slot with dl == max_def (ColumnReaderBase.java:650-676,
+ * readPageV2 :760-771). The decoder uses it as a verified hint: when every page of every nullable column
+ * of a plan is a V2 page carrying it, each page's value count (num_values - num_nulls) and output offset
+ * are known on the host, so the value kernels start at the launch's start beside the level kernel instead
+ * of after it. The level kernel still decodes every level section and compares each page's true count;
+ * a mismatch (or any level / level-init error on such a page) makes pqg_sync re-run the plan with the
+ * counts taken from the levels, as without the hint (pqg_plan_null_hint_fallbacks counts these re-runs),
+ * so results and errors are those of the reference whatever the header says. */
+#define PQG_PAGE_NULL_COUNT 2
 
 /*
  * One column chunk: the ColumnDescriptor facts the decoder needs (physical
@@ -224,6 +242,9 @@ void* pqg_ctx_stream(pqg_ctx* ctx);
  *                                mapped straight to lengths and bytes (default), 0 = ids, then map
  *   PQG_DISPATCH_DICT_FUSED      dictionary pages: 1 = walk and expansion in one launch (default),
  *                                0 = two launches (the mode a fused launch that timed out re-runs in)
+ *   PQG_DISPATCH_NULL_HINTS      nullable columns of V2 pages: 1 = value kernels start from the header
+ *                                null counts beside the level decode, which verifies them (default;
+ *                                PQG_PAGE_NULL_COUNT), 0 = levels first
  *   PQG_DISPATCH_GZIP_PREPASS_MIN pqg_gzip_decompress: pages of at least `value` output bytes take the
  *                                token pre-pass + replay, smaller ones the one-wave decoder (default
  *                                16384; 0 = every page); applies to later pqg_gzip_decompress calls
@@ -232,7 +253,8 @@ enum pqg_dispatch {
   PQG_DISPATCH_PLAIN_ONE_PASS = 1,
   PQG_DISPATCH_DICT_DIRECT = 2,
   PQG_DISPATCH_GZIP_PREPASS_MIN = 3,
-  PQG_DISPATCH_DICT_FUSED = 4
+  PQG_DISPATCH_DICT_FUSED = 4,
+  PQG_DISPATCH_NULL_HINTS = 5
 };
 int pqg_ctx_set_dispatch(pqg_ctx* ctx, int key, int value);
 
@@ -322,6 +344,11 @@ int pqg_plan_timeout_fallbacks(pqg_plan* plan);
  * walk, offset scan, byte copy), which reads exactly num_values values; the plan keeps that path.
  * Returns how many launches of the plan were re-run that way. */
 int pqg_plan_plain_fallbacks(pqg_plan* plan);
+/* Plans whose nullable columns are all V2 pages with PQG_PAGE_NULL_COUNT start their value kernels
+ * from the header null counts (see PQG_PAGE_NULL_COUNT). Returns how many launches of the plan pqg_sync
+ * re-ran with the counts taken from the levels because a header count was wrong (the plan then keeps
+ * the level-first order). */
+int pqg_plan_null_hint_fallbacks(pqg_plan* plan);
 int pqg_plan_destroy(pqg_plan* plan);
 
 /* ---- host-buffer decode (the JNI shim's entry: file bytes in, arrays out) --

@@ -182,6 +182,14 @@ struct pqg_plan {
   int n_binp_seg = 0;
   bool seg_walk = true;
   uint32_t n_bin_blocks_nf = 0, n_bin_chunks_nf = 0;
+  // V2 header null counts (PQG_PAGE_NULL_COUNT): every nullable page of the plan carries one, so the
+  // host filled those pages' n_values / data_begin / out_offset and the value kernels start beside
+  // k_levels, which verifies the counts into the epoch-tagged word at hint_off (bscratch); a mismatch
+  // makes pqg_sync re-run level-first, and the plan keeps that order (null_hints false)
+  bool null_hints = false;
+  uint64_t hint_off = 0;
+  int hint_fallbacks = 0;
+  uint32_t* d_counts = nullptr;  // pqg_decode's d_page_value_counts (refreshed after a re-run)
 };
 
 // pqg_router_read_page: the bit-packed runs of a hybrid stream's tail, walked on the host at the first
@@ -231,6 +239,7 @@ struct pqg_ctx {
   int plain_mode = 2;       // PQG_DISPATCH_PLAIN_ONE_PASS
   bool dict_direct = true;  // PQG_DISPATCH_DICT_DIRECT
   bool dict_fused = true;   // PQG_DISPATCH_DICT_FUSED
+  bool null_hints = true;   // PQG_DISPATCH_NULL_HINTS
   uint32_t gz_prepass_min = pqg::GZ_PREPASS_MIN;  // PQG_DISPATCH_GZIP_PREPASS_MIN
   RouterCache router;  // pqg_router_read_page
 };
@@ -313,6 +322,10 @@ int pqg_ctx_set_dispatch(pqg_ctx* ctx, int key, int value) {
       if (value != 0 && value != 1) return PQG_ERR_INVALID_ARG;
       ctx->dict_fused = value != 0;
       return PQG_OK;
+    case PQG_DISPATCH_NULL_HINTS:
+      if (value != 0 && value != 1) return PQG_ERR_INVALID_ARG;
+      ctx->null_hints = value != 0;
+      return PQG_OK;
     default: return PQG_ERR_INVALID_ARG;
   }
 }
@@ -367,7 +380,7 @@ int pqg_ctx_destroy(pqg_ctx* c) {
 // Kernels one launch of the plan runs (in its current modes).
 static int count_kernels(const pqg_plan* P) {
   const bool pf = P->plain_fused;
-  int k = (P->levels_n ? 1 : 0) + (P->n_scan_cols ? 1 : 0);
+  int k = (P->levels_n ? 1 : 0) + (P->n_scan_cols && !P->null_hints ? 1 : 0);
   for (int c = 0; c < C_NCLS; c++) {
     const int n = P->cls_n[(size_t)c] - (c == C_BINP ? P->n_binp_seg + (pf ? P->n_binp_fused : 0) : 0);
     if (n && c == C_DD) k += P->dict_fused ? 3 : 4;
@@ -579,6 +592,28 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   }
   for (int i = 0; i < n_cols; i++) P->col_required_values[(size_t)i] = val_acc[(size_t)i];
   P->col_first_page = col_first_page;
+  // V2 header null counts as a verified hint (PQG_PAGE_NULL_COUNT): only when every nullable page of the
+  // plan carries a usable one, so that no value kernel has to wait for k_levels
+  if (ctx->null_hints && !lvl_list.empty()) {
+    bool all = true;
+    for (int p : lvl_list) {
+      const pqg_page_desc& g = pages[p];
+      all = all && g.version == 2 && (g.flags & PQG_PAGE_NULL_COUNT) && g.num_nulls <= g.num_values &&
+            (uint64_t)g.rl_byte_length + g.dl_byte_length <= g.size;
+    }
+    if (all) {
+      std::vector<uint64_t> acc((size_t)std::max(n_cols, 1), 0);
+      for (int p : lvl_list) {  // (page order within each column)
+        const pqg_page_desc& g = pages[p];
+        PageWork& w = P->h_work[(size_t)p];
+        w.n_values = g.num_values - g.num_nulls;
+        w.data_begin = g.rl_byte_length + g.dl_byte_length;
+        w.out_offset = acc[(size_t)g.column];
+        acc[(size_t)g.column] += w.n_values;
+      }
+      P->null_hints = true;
+    }
+  }
   // ---- BYTE_ARRAY and fixed-width dictionary columns: scratch layout, dictionary walks,
   // post-passes, offset-scan blocks and copy chunks
   std::vector<int32_t> dict_walk, bind, fixd, bin_cols, carry_cols;
@@ -625,9 +660,11 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       pcs.push_back((int32_t)pcp.size());
     }
   }
-  // dictionary-direct BYTE_ARRAY columns (ColumnDev::dict_direct): required, every data page
-  // dictionary-encoded, the dictionary page small enough to stage (DD_DICT_MAX bytes, at most 2,048
-  // entries): their pages leave C_IDS for C_DD (no ids stored, no offset scan or copy of their own)
+  // dictionary-direct BYTE_ARRAY columns (ColumnDev::dict_direct): every data page dictionary-encoded,
+  // the dictionary page small enough to stage (DD_DICT_MAX bytes, at most 2,048 entries): their pages
+  // leave C_IDS for C_DD (no ids stored, no offset scan or copy of their own). Nullable and nested
+  // columns too (round 6): the walk decodes a page's n_values ids from its data section, which k_levels
+  // (or the V2 header counts) give, and values are indexed by out_offset like every other class
   std::vector<uint8_t> dict_direct((size_t)std::max(n_cols, 1), 0);
   {
     std::vector<int> npg((size_t)std::max(n_cols, 1), 0), nids((size_t)std::max(n_cols, 1), 0);
@@ -639,7 +676,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     for (int i = 0; i < n_cols; i++)
       dict_direct[(size_t)i] = cols[i].physical_type == PQG_BYTE_ARRAY && bin_out(cols[i]) && !ids_mode(cols[i]) &&
                                !col_err[(size_t)i] && !dba_fixed[(size_t)i] && !plain_col[(size_t)i] &&
-                               cols[i].max_def == 0 && cols[i].max_rep == 0 && cols[i].dict_offset >= 0 &&
+                               cols[i].dict_offset >= 0 &&
                                cols[i].dict_size <= pqg::DD_DICT_MAX && cols[i].dict_num_values <= 2048 &&
                                npg[(size_t)i] > 0 && nids[(size_t)i] == npg[(size_t)i] && ctx->dict_direct;
     std::vector<int> keep, dd;
@@ -685,6 +722,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     if (dict_direct[(size_t)i])
       blen_off[(size_t)i] = take((cols[i].dict_num_values <= 256 ? 1u : 2u) * (slot_acc[(size_t)i] + 16));
   if (!pcp.empty()) P->pflag_off = take(8);
+  if (P->null_hints) P->hint_off = take(8);
   if (!segs.empty()) P->seg_tmp_off = take(4 * 2 * (uint64_t)pqg::BW_SEG_CAP * segs.size());
   P->n_segs = (uint32_t)segs.size();
   for (int i = 0; i < n_cols; i++) {
@@ -907,6 +945,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     ok = ok && hipMemcpyAsync(P->pcol_start.p, pcs.data(), sizeof(int32_t) * pcs.size(), hipMemcpyHostToDevice, s) == hipSuccess;
     ok = ok && hipMemsetAsync((uint8_t*)P->bscratch.p + P->pflag_off, 0, 8, s) == hipSuccess;
   }
+  if (P->null_hints) ok = ok && hipMemsetAsync((uint8_t*)P->bscratch.p + P->hint_off, 0, 8, s) == hipSuccess;
   P->n_psegs = (uint32_t)psegs.size();
   P->n_pcols = (int)pcs.size() - 1;
   P->plain_fused = !pcp.empty();
@@ -938,6 +977,8 @@ int pqg_plan_timeout_fallbacks(pqg_plan* P) { return P ? P->timeout_fallbacks : 
 
 int pqg_plan_plain_fallbacks(pqg_plan* P) { return P ? P->plain_fallbacks : 0; }
 
+int pqg_plan_null_hint_fallbacks(pqg_plan* P) { return P ? P->hint_fallbacks : 0; }
+
 int pqg_plan_launch(pqg_plan* P) {
   if (!P) return PQG_ERR_INVALID_ARG;
   pqg_ctx* ctx = P->ctx;
@@ -950,6 +991,7 @@ int pqg_plan_launch(pqg_plan* P) {
     P->err_epoch = 1;
     if (hipMemsetAsync(P->err.p, 0, err_bytes + 16, s) != hipSuccess) return PQG_ERR_HIP;
     if (P->n_pcp && hipMemsetAsync((uint8_t*)P->bscratch.p + P->pflag_off, 0, 8, s) != hipSuccess) return PQG_ERR_HIP;
+    if (P->null_hints && hipMemsetAsync((uint8_t*)P->bscratch.p + P->hint_off, 0, 8, s) != hipSuccess) return PQG_ERR_HIP;
   }
   const pqg::ErrCount ecount{(uint32_t*)((uint8_t*)P->err.p + err_bytes), P->err_epoch};
   PageWork* work = (PageWork*)P->work.p;
@@ -973,8 +1015,12 @@ int pqg_plan_launch(pqg_plan* P) {
       return PQG_ERR_HIP;
   }
   hipError_t e = hipSuccess;
-  if (P->levels_n) {
-    e = pqg::launch_levels(s, P->d_bytes, P->n_bytes, work, cols, lists + P->levels_off, P->levels_n, err, ecount);
+  // level-first order: k_levels + k_scan_offsets give the nullable pages' counts and offsets before any
+  // value kernel; with V2 header null counts (null_hints) the host has them and k_levels only verifies
+  // them, on the caller's stream beside the forked value kernels (launched after the fork below)
+  const bool hints = P->null_hints && P->levels_n;
+  if (P->levels_n && !hints) {
+    e = pqg::launch_levels(s, P->d_bytes, P->n_bytes, work, cols, lists + P->levels_off, P->levels_n, err, ecount, nullptr);
     if (e == hipSuccess)
       e = pqg::launch_scan(s, work, (const int32_t*)P->col_pages.p, (const int32_t*)P->col_page_start.p, P->n_scan_cols);
   }
@@ -989,7 +1035,8 @@ int pqg_plan_launch(pqg_plan* P) {
                          P->cls_n[C_RLEBOOL] || P->cls_n[C_DELTA4] || P->cls_n[C_DELTA8] || P->cls_n[C_BSS];
   const bool has_bin = P->n_dict_walk || P->cls_n[C_IDS] || P->cls_n[C_DD] || P->cls_n[C_BINP] - P->n_binp_seg - (pf ? P->n_binp_fused : 0) > 0 ||
                        P->cls_n[C_DLBA] || P->cls_n[C_DBA] || P->n_segs;
-  const bool want = e == hipSuccess && ((pf && (has_fixed || has_bin)) || (has_bin && has_fixed));
+  const bool want = e == hipSuccess && ((pf && (has_fixed || has_bin)) || (has_bin && has_fixed) ||
+                                        (hints && (pf || has_bin || has_fixed)));
   const bool ev_ok = want && (ctx->ev_fork || hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) == hipSuccess) &&
                      hipEventRecord(ctx->ev_fork, s) == hipSuccess;
   if (ev_ok && pf) {
@@ -997,15 +1044,18 @@ int pqg_plan_launch(pqg_plan* P) {
            (ctx->ev_join || hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) == hipSuccess) &&
            hipStreamWaitEvent(ctx->side_stream, ctx->ev_fork, 0) == hipSuccess;
   }
-  if (ev_ok && has_bin && has_fixed) {
+  if (ev_ok && has_bin && (has_fixed || hints)) {
     fork_bin = (ctx->bin_stream || hipStreamCreateWithFlags(&ctx->bin_stream, hipStreamNonBlocking) == hipSuccess) &&
                (ctx->ev_join_bin || hipEventCreateWithFlags(&ctx->ev_join_bin, hipEventDisableTiming) == hipSuccess) &&
                hipStreamWaitEvent(ctx->bin_stream, ctx->ev_fork, 0) == hipSuccess;
   }
-  if ((fork || fork_bin) && has_fixed)
+  if (ev_ok && (fork || fork_bin || hints) && has_fixed)
     fork_fix = (ctx->fix_stream || hipStreamCreateWithFlags(&ctx->fix_stream, hipStreamNonBlocking) == hipSuccess) &&
                (ctx->ev_join_fix || hipEventCreateWithFlags(&ctx->ev_join_fix, hipEventDisableTiming) == hipSuccess) &&
                hipStreamWaitEvent(ctx->fix_stream, ctx->ev_fork, 0) == hipSuccess;
+  if (e == hipSuccess && hints)  // the level sections, verified against the header counts, beside the value kernels
+    e = pqg::launch_levels(s, P->d_bytes, P->n_bytes, work, cols, lists + P->levels_off, P->levels_n, err, ecount,
+                           (uint32_t*)((uint8_t*)P->bscratch.p + P->hint_off));
   if (e == hipSuccess && pf) {  // PLAIN-only BYTE_ARRAY columns: one pass (after the levels: n_values, out_offset)
     uint8_t* scb = (uint8_t*)P->bscratch.p;
     uint64_t* ps = (uint64_t*)P->pstatus.p;
@@ -1248,6 +1298,28 @@ namespace {
 // timeout re-run. `work` receives the plan's PageWork (nullable columns' value counts).
 int sync_plan(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work) {
   pqg_ctx* ctx = P->ctx;
+  if (P->null_hints && P->levels_n) {
+    // A V2 header null count that disagrees with the page's definition levels (or a level error on such
+    // a page): the value kernels ran on wrong counts / offsets. The reference decodes by the levels
+    // (ColumnReaderBase.java:650-676, 760-771), so the launch is re-run level-first, which rewrites every
+    // output; the plan keeps that order.
+    uint32_t flag = 0;
+    if (hipMemcpy(&flag, (uint8_t*)P->bscratch.p + P->hint_off, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess)
+      return PQG_ERR_HIP;
+    if (flag == P->err_epoch) {
+      P->null_hints = false;
+      P->kernels = count_kernels(P);
+      P->hint_fallbacks++;
+      const int lrc = pqg_plan_launch(P);
+      if (lrc != PQG_OK) return lrc;
+      if (P->d_counts &&  // pqg_decode's per-page counts, copied after the first launch
+          hipMemcpy2DAsync(P->d_counts, sizeof(uint32_t), (const uint8_t*)P->work.p + offsetof(PageWork, n_values),
+                           sizeof(PageWork), sizeof(uint32_t), (size_t)P->n_pages, hipMemcpyDeviceToDevice,
+                           ctx->stream) != hipSuccess)
+        return PQG_ERR_HIP;
+      if (hipStreamSynchronize(ctx->stream) != hipSuccess) return PQG_ERR_HIP;
+    }
+  }
   if (P->plain_fused) {
     // A PLAIN page whose values do not end at its section end (bytes the reader ignores after them)
     // breaks the one-pass path's byte bases: the launch is re-run on the per-value path (k_bin_walk,
@@ -1399,6 +1471,7 @@ static int decode_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_bytes, u
   ctx->last = P;
   ctx->last_cols = cols;
   rc = pqg_plan_launch(P);
+  P->d_counts = n_pages > 0 ? d_page_value_counts : nullptr;
   if (rc == PQG_OK && d_page_value_counts && n_pages > 0) {
     // n_values of every page (strided in PageWork) -> dense uint32 array
     rc = hipMemcpy2DAsync(d_page_value_counts, sizeof(uint32_t), (const uint8_t*)P->work.p + offsetof(PageWork, n_values),

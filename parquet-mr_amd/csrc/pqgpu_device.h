@@ -16,27 +16,6 @@ constexpr int WAVE = 64;
 // waves resident), so pages are packed 4 to a workgroup.
 constexpr int WPB = 4;
 
-// XCD-aware order of workgroups. The dispatcher deals workgroups round-robin over the 8 XCDs
-// (observed, MI355X_MICROARCH.md: block b runs on XCD b % 8; relied on for speed only). Workgroup g
-// of a range of n workgroups whose first one has blockIdx `first` gets index xcd_order(g, n, first & 7)
-// in [0, n): the workgroups of one XCD take one contiguous run of indices, in dispatch order, so each
-// XCD writes one contiguous part of the output at a time. Measured on the expansion's store shape
-// (4 waves x 16 KiB chunks, 800 MB, profiles/r05/store_xcd): 6.23 TB/s against 5.44 with chunks dealt
-// in block order. A bijection of [0, n) for any n and origin (tests/test_xcd_order.py).
-// Not applied to the decoder's kernels: on them the same remap measured neutral or slower (C2 173.3 vs
-// 174.0 us, Zipf(2.0) 0.338 vs 0.318 ms, C4 11.59 vs 11.49 ms; split-mode expansion 152.6 vs 156.0 us,
-// profiles/r05/store_xcd): with chunks of uneven duration the round-robin placement drifts (the same
-// microbenchmark with 0..4 dependent loads per chunk: 5.48 vs 5.07 TB/s), and claiming chunks per
-// HW_REG_XCC_ID from per-XCD counters was slower than block order (4.86 TB/s).
-__host__ __device__ __forceinline__ uint32_t xcd_order(uint32_t g, uint32_t n, uint32_t off) {
-  // blocks u = off + g of the range [0, off + n), classes u % 8; the `off` phantom blocks u < off
-  // (one at the head of each class x < off) are removed from the positions
-  const uint32_t u = g + off, U = n + off, x = u & 7u, j = u >> 3;
-  const uint32_t q = U >> 3, r = U & 7u;
-  const uint32_t base = x * q + (x < r ? x : r);
-  return base + j - (x + 1u < off ? x + 1u : off);
-}
-
 __device__ __forceinline__ uint32_t wave_id() {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 }

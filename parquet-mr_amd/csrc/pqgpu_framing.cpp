@@ -344,6 +344,10 @@ int pqg_pages_from_headers(const pqg_page_header* headers, int n_headers, int co
       p.dl_encoding = h.definition_level_encoding;
       p.rl_byte_length = (uint32_t)h.repetition_levels_byte_length;
       p.dl_byte_length = (uint32_t)h.definition_levels_byte_length;
+      if (p.version == 2 && h.num_nulls >= 0) {  // DataPageV2.getNullCount: a hint the decoder verifies
+        p.flags |= PQG_PAGE_NULL_COUNT;
+        p.num_nulls = (uint32_t)h.num_nulls;
+      }
     }
     n++;
   }

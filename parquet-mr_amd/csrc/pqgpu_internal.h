@@ -40,7 +40,8 @@ struct ColumnDev {
 };
 
 // Per page, on the device. The host fills the descriptor facts; for nullable
-// columns k_levels fills data_begin / n_values and k_scan_offsets fills out_offset.
+// columns k_levels fills data_begin / n_values and k_scan_offsets fills out_offset (or, in a plan
+// running on V2 header null counts, the host fills them too and k_levels verifies them).
 struct PageWork {
   uint64_t base;        // page body offset in the batch
   uint32_t size;        // page body bytes
@@ -95,8 +96,11 @@ hipError_t launch_dict(int width, hipStream_t st, const uint8_t* bytes, uint64_t
                        const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags, uint32_t epoch,
                        bool fused, uint64_t* err,
                        ErrCount err_count);
+// hint_bad: non-null when the plan runs on V2 header null counts (PQG_PAGE_NULL_COUNT): the host filled
+// every listed page's n_values / data_begin / out_offset, k_levels only verifies them and stores
+// err_count.epoch to *hint_bad on a mismatch or a level error (no PageWork write); null: level-first
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
-                         const int32_t* list, int n, uint64_t* err, ErrCount err_count);
+                         const int32_t* list, int n, uint64_t* err, ErrCount err_count, uint32_t* hint_bad);
 hipError_t launch_scan(hipStream_t st, PageWork* work, const int32_t* col_pages, const int32_t* col_page_start,
                        int n_cols);
 hipError_t launch_plain(int kind, hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,

@@ -1201,7 +1201,8 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_tiles_dd(const uint8_t* __res
 // register scan), a workgroup scan of the threads' totals, then each thread writes its bases. (The
 // previous 256-sum rounds with two barriers each took 15 us for str_dict's 4,883 chunks.)
 constexpr uint32_t DDB_PER = 16;
-__global__ __launch_bounds__(256) void k_dd_bases(const ColumnDev* __restrict__ cols, const int32_t* __restrict__ dd_cols,
+__global__ __launch_bounds__(256) void k_dd_bases(const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                                  const uint64_t* __restrict__ chunks, const int32_t* __restrict__ dd_cols,
                                                   const int32_t* __restrict__ start, uint64_t* sums) {
   __shared__ uint64_t wsum[4];
   const ColumnDev& cd = cols[dd_cols[blockIdx.x]];
@@ -1239,7 +1240,15 @@ __global__ __launch_bounds__(256) void k_dd_bases(const ColumnDev* __restrict__ 
   }
   if (threadIdx.x == 0) {
     *cd.bin_total = carry;
-    gst((int64_t*)cd.values + cd.n_slots, (int64_t)carry);
+    // offsets[n]: n = the column's values = the end of its last page's (the last chunk's page: the host
+    // pads before a column's first chunk, never after its last; slots for a required column, the non-null
+    // count of a nullable one)
+    uint64_t n = cd.n_slots;
+    if (e > b) {
+      const PageWork& lp = work[(uint32_t)chunks[e - 1]];
+      n = lp.out_offset + lp.n_values;
+    }
+    gst((int64_t*)cd.values + n, (int64_t)carry);
   }
 }
 
@@ -1586,6 +1595,13 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
         for (uint32_t q0 = 0; q0 < md; q0 += 16u) dd_put<4>(dst, o, ln, sr, dd_lds, q0);
       }
     } else {  // past the capacity (reported at sync with the size needed): the bytes that fit
+      if (cb_on) {  // the previous tile's carried partial block: its bytes below the capacity
+        if (lane == 0) {
+          const uint64_t hi = cb_tal + cb_hi < cap ? cb_tal + cb_hi : cap;
+          store_block16(dst, cb_tal, cb_tal + cb_lo, hi, cb_w, 0u, true);
+        }
+        cb_on = false;
+      }
 #pragma unroll
       for (uint32_t e = 0; e < E; e++)
         for (uint32_t q = 0; q < ln[e]; q++)
@@ -2179,7 +2195,11 @@ __device__ __forceinline__ uint32_t decode_levels_w(LevelWaveLds& L, rsrc_t rs, 
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5))) void k_levels(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                 PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                                 const int32_t* __restrict__ list, int n_list, uint64_t* err,
-                                                ErrCount err_count) {
+                                                ErrCount err_count, uint32_t* hint_bad) {
+  // hint_bad != nullptr: the plan runs on the V2 header null counts (PQG_PAGE_NULL_COUNT), which the
+  // host already put in n_values / data_begin / out_offset and the value kernels are reading beside this
+  // kernel; nothing of the page's work entry is written here, the true count is only compared, and a
+  // mismatch or any level error raises hint_bad (err_count's epoch): pqg_sync then re-runs level-first
   __shared__ __attribute__((aligned(16))) LevelWaveLds lvl_lds[WPB];
   const int page = wave_page(list, n_list);
   if (page < 0) return;
@@ -2243,8 +2263,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5))) v
   if (init_err) {
     if (lane == 0) {
       report(err, err_count, page, 0, (uint64_t)init_phase, init_err);
-      work[page].n_values = 0;
-      work[page].data_begin = size;
+      if (hint_bad) {
+        sst(hint_bad, err_count.epoch);
+      } else {
+        work[page].n_values = 0;
+        work[page].data_begin = size;
+      }
     }
     return;
   }
@@ -2291,8 +2315,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(5))) v
       // level error key: slot << 1 | (0 = rl, 1 = dl) — host decodes it
       report_key(&err[3 * (uint64_t)page + 1], err_count, lvl_err_key);
     }
-    work[page].n_values = nonnull;
-    work[page].data_begin = data_beg;
+    if (hint_bad) {
+      if (lvl_err_key != ~0ull || nonnull != pw.n_values || data_beg != pw.data_begin) sst(hint_bad, err_count.epoch);
+    } else {
+      work[page].n_values = nonnull;
+      work[page].data_begin = data_beg;
+    }
   }
 }
 
@@ -2700,12 +2728,15 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
       const uint32_t mind32 = (uint32_t)mind;
       uint32_t loc[L];
       uint32_t sum = 0;
-      uint32_t ab = dbase * 8u + jm * wl;  // bit position in the page
+      // bit position relative to the dword holding the miniblock data's first byte (a page-absolute
+      // bit position would wrap for data 512 MiB or more into a page)
+      const uint32_t abase = dbase & ~3u;
+      uint32_t ab = (dbase & 3u) * 8u + jm * wl;
 #pragma unroll
       for (uint32_t q = 0; q < L; q++) {
         uint32_t d = 0;
         if (wl) {
-          const uint32_t a = (ab >> 5) << 2;
+          const uint32_t a = abase + ((ab >> 5) << 2);
           d = __builtin_amdgcn_alignbit(S.w32(a + 4), S.w32(a), ab & 31u) & mask;
         }
         sum += lane_in ? d + mind32 : 0u;
@@ -3398,7 +3429,7 @@ hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_dd_bases, dim3(n_dd_cols), dim3(256), 0, st, cols, dd_cols, dd_start, sums);
+  hipLaunchKernelGGL(k_dd_bases, dim3(n_dd_cols), dim3(256), 0, st, work, cols, chunks, dd_cols, dd_start, sums);
   e = hipGetLastError();
   if (e != hipSuccess || !n_tile) return e;
   const uint32_t dd_lds_bytes = 16u + ((dd_region + 15u) & ~15u) + WPB * DDG_WAVE_BYTES;
@@ -3412,9 +3443,9 @@ hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes
 }
 
 hipError_t launch_levels(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
-                         const int32_t* list, int n, uint64_t* err, ErrCount err_count) {
+                         const int32_t* list, int n, uint64_t* err, ErrCount err_count, uint32_t* hint_bad) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_levels, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
+  hipLaunchKernelGGL(k_levels, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS, hint_bad);
   return hipGetLastError();
 }
 

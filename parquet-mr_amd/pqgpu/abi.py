@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # parquet-format Type
 BOOLEAN, INT32, INT64, INT96, FLOAT, DOUBLE, BYTE_ARRAY, FIXED_LEN_BYTE_ARRAY = range(8)
@@ -49,6 +49,7 @@ ERR_CRC = 21
 CODEC_UNCOMPRESSED, CODEC_SNAPPY, CODEC_GZIP, CODEC_LZO, CODEC_BROTLI, CODEC_LZ4, CODEC_ZSTD, CODEC_LZ4_RAW = range(8)
 COLUMN_DICTIONARY_IDS = 1  # pqg_column_desc.flags: values <- uint32 dictionary ids
 PAGE_DBA_CARRY = 1  # pqg_page_desc.flags: DELTA_BYTE_ARRAY page continues the previous page's value (PARQUET-246)
+PAGE_NULL_COUNT = 2  # pqg_page_desc.flags: num_nulls holds the V2 header's null count (a verified hint)
 
 ERROR_NAMES = {
     OK: "OK", ERR_INVALID_ARG: "INVALID_ARG", ERR_UNSUPPORTED: "UNSUPPORTED", ERR_HIP: "HIP",
@@ -61,7 +62,7 @@ ERROR_NAMES = {
 
 
 class PageDesc(C.Structure):
-    """pqg_page_desc (48 bytes)."""
+    """pqg_page_desc (56 bytes)."""
     _fields_ = [
         ("offset", C.c_uint64),
         ("size", C.c_uint32),
@@ -74,15 +75,17 @@ class PageDesc(C.Structure):
         ("rl_byte_length", C.c_uint32),
         ("dl_byte_length", C.c_uint32),
         ("flags", C.c_uint32),
+        ("num_nulls", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 
 PAGE_DTYPE = np.dtype([
     ("offset", "<u8"), ("size", "<u4"), ("num_values", "<u4"), ("column", "<i4"), ("version", "<i4"),
     ("encoding", "<i4"), ("rl_encoding", "<i4"), ("dl_encoding", "<i4"), ("rl_byte_length", "<u4"),
-    ("dl_byte_length", "<u4"), ("flags", "<u4"),
+    ("dl_byte_length", "<u4"), ("flags", "<u4"), ("num_nulls", "<u4"), ("reserved", "<u4"),
 ])
-assert PAGE_DTYPE.itemsize == C.sizeof(PageDesc) == 48
+assert PAGE_DTYPE.itemsize == C.sizeof(PageDesc) == 56
 
 
 class ColumnDesc(C.Structure):
@@ -218,3 +221,4 @@ DISPATCH_PLAIN_ONE_PASS = 1
 DISPATCH_DICT_DIRECT = 2
 DISPATCH_GZIP_PREPASS_MIN = 3  # pqg_gzip_decompress: smallest page (output bytes) for the token pre-pass
 DISPATCH_DICT_FUSED = 4  # dictionary pages: 1 = walk + expansion in one launch, 0 = two launches
+DISPATCH_NULL_HINTS = 5  # V2 nullable columns: 1 = value kernels from the header null counts (verified), 0 = levels first

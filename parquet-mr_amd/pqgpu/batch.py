@@ -127,8 +127,11 @@ def build_batch(chunks, align=ALIGN):
             off = place(pg.body)
             carry = abi.PAGE_DBA_CARRY if (getattr(ch, "dba_carry", False) and k > 0 and
                                            pg.encoding == abi.DELTA_BYTE_ARRAY) else 0
+            # V2 pages carry the header's null count (a hint the decoder verifies against the levels)
+            nulls_flag = abi.PAGE_NULL_COUNT if pg.version == 2 else 0
             page_rows.append((off, len(pg.body), pg.num_values, oc, pg.version, pg.encoding, pg.rl_encoding,
-                              pg.dl_encoding, pg.rl_byte_length, pg.dl_byte_length, carry))
+                              pg.dl_encoding, pg.rl_byte_length, pg.dl_byte_length, carry | nulls_flag,
+                              pg.num_nulls if pg.version == 2 else 0, 0))
             slot_off.append(col_slots[oc])
             col_slots[oc] += pg.num_values
         col_vals[oc] += len(ch.values) if ch.values is not None else getattr(ch, "n_values_hint", 0)

@@ -94,6 +94,12 @@ class Plan:
         values (pqg_plan_plain_fallbacks)."""
         return native.lib().pqg_plan_plain_fallbacks(self.handle)
 
+    @property
+    def null_hint_fallbacks(self):
+        """Launches re-run level-first because a V2 header's num_nulls disagreed with the page's
+        definition levels (pqg_plan_null_hint_fallbacks)."""
+        return native.lib().pqg_plan_null_hint_fallbacks(self.handle)
+
     def sync(self):
         st = abi.Status()
         rc = native.lib().pqg_sync(self.decoder.ctx, C.byref(st))

@@ -17,6 +17,7 @@ EXPORTS = [
     "pqg_abi_version", "pqg_device_count", "pqg_ctx_create", "pqg_ctx_destroy", "pqg_ctx_stream", "pqg_ctx_set_dispatch",
     "pqg_decode",
     "pqg_sync", "pqg_plan_create", "pqg_plan_launch", "pqg_plan_kernel_count", "pqg_plan_timeout_fallbacks", "pqg_plan_plain_fallbacks",
+    "pqg_plan_null_hint_fallbacks",
     "pqg_plan_destroy",
     "pqg_decode_host", "pqg_unpack_runs", "pqg_router_read", "pqg_router_read_runs", "pqg_router_read_page",
     "pqg_router_cache_lookup", "pqg_router_cache_stats", "pqg_error_name",
@@ -67,6 +68,7 @@ def lib():
         L.pqg_plan_kernel_count.argtypes = [vp]
         L.pqg_plan_timeout_fallbacks.argtypes = [vp]
         L.pqg_plan_plain_fallbacks.argtypes = [vp]
+        L.pqg_plan_null_hint_fallbacks.argtypes = [vp]
         L.pqg_plan_destroy.argtypes = [vp]
         L.pqg_decode_host.argtypes = [vp, vp, u64, vp, i32, vp, i32, vp, C.POINTER(abi.Status)]
         L.pqg_unpack_runs.argtypes = [vp, i32, vp, vp, vp, vp, vp, i32]

@@ -23,7 +23,7 @@ public final class PqGpu {
   private PqGpu() {}
 
   /** Size of one packed pqg_page_desc / pqg_column_desc (little endian, C layout). */
-  public static final int PAGE_DESC_BYTES = 48;
+  public static final int PAGE_DESC_BYTES = 56;
   public static final int COLUMN_DESC_BYTES = 104;
   /** pqg_column_desc.flags: decode dictionary ids (readValueDictionaryId) instead of values. */
   public static final int COLUMN_DICTIONARY_IDS = 1;

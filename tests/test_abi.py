@@ -49,6 +49,7 @@ LAYOUT_C = r"""
 int main(void) {
   printf("pqg_page_desc %zu\npqg_column_desc %zu\npqg_status %zu\n", sizeof(pqg_page_desc), sizeof(pqg_column_desc), sizeof(pqg_status));
   O(pqg_page_desc, offset); O(pqg_page_desc, num_values); O(pqg_page_desc, dl_byte_length);
+  O(pqg_page_desc, flags); O(pqg_page_desc, num_nulls);
   O(pqg_column_desc, dict_offset); O(pqg_column_desc, values); O(pqg_column_desc, def_levels);
   O(pqg_column_desc, binary_data); O(pqg_column_desc, values_written);
   O(pqg_status, value_index); O(pqg_status, message);

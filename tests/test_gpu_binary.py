@@ -468,8 +468,17 @@ def _lineitem_words():
     return [b"DELIVER IN PERSON", b"COLLECT COD", b"NONE", b"TAKE BACK RETURN", b"R", b"A", b"N", b"", b"AIR"]
 
 
+@pytest.fixture(params=[1, 0], ids=["fused", "split"])
+def dict_fused(decoder, request):
+    """PQG_DISPATCH_DICT_FUSED: 1 = walk + expansion in one launch (k_dict_fused_dd), 0 = the split
+    launches (k_dict_runs + k_dict_tiles_dd), which are also the timeout re-run of the fused one."""
+    decoder.set_dispatch(abi.DISPATCH_DICT_FUSED, request.param)
+    yield request.param
+    decoder.set_dispatch(abi.DISPATCH_DICT_FUSED, 1)
+
+
 @pytest.mark.parametrize("dict_direct", [1, 0])
-def test_dictionary_direct_interleaved_columns(decoder, dict_direct):
+def test_dictionary_direct_interleaved_columns(decoder, dict_direct, dict_fused):
     """Several dictionary-direct columns whose pages are interleaved in the page table (the plan sorts
     their chunks by column and pads each column to whole workgroups), beside a column of another kind;
     PQG_DISPATCH_DICT_DIRECT = 0 sends the same columns through ids -> map -> copy: equal results."""
@@ -506,7 +515,7 @@ def test_dictionary_direct_interleaved_columns(decoder, dict_direct):
 
 @pytest.mark.parametrize("lens", [(0, 0), (1, 4000), (2000, 2000, 2000), (0, 1, 23, 24, 64),
                                   (2, 3), (0, 2, 17, 32), (17, 11, 4, 16), (7, 3, 4, 4, 5, 4, 3), (16,), (32, 32, 1)])
-def test_dictionary_direct_entry_lengths(decoder, lens):
+def test_dictionary_direct_entry_lengths(decoder, lens, dict_fused):
     """Entry lengths around the kernel's byte paths: empty entries only, 1-byte entries, entries of 2..32
     bytes (composed into whole 16-byte output blocks: C4's ship instruct / mode shapes, blocks that start
     inside, at the start of and between entries, 16-byte entries, empty entries between), longer ones
@@ -544,9 +553,87 @@ def test_dictionary_direct_error_stays_in_its_column(decoder):
     assert_same(dcols[1].numpy(), [words[i] for i in good_ids], abi.BYTE_ARRAY)
 
 
-def test_dictionary_direct_plan_relaunch(decoder):
+def test_dictionary_direct_plan_relaunch(decoder, dict_fused):
     """A plan launched twice: the chunk sums and bases are rewritten per launch (nothing stale)."""
     words = _lineitem_words()
     ids = np.random.default_rng(29).integers(0, 9, size=40_000)
     _plan_both(decoder, [make(abi.BYTE_ARRAY, [words[i] for i in ids], abi.RLE_DICTIONARY, page_rows=20000),
                          make(abi.BYTE_ARRAY, [words[i] for i in ids[::-1]], abi.RLE_DICTIONARY, page_rows=6000)])
+
+
+@pytest.mark.parametrize("short", [0.5, 0.9])
+def test_dictionary_direct_short_buffer_keeps_prefix(decoder, short):
+    """A byte buffer shorter than the column: the call reports the size needed and the bytes below the
+    capacity are the column's (entries of 2..32 bytes: the block gather, whose partial last block of a
+    tile is carried into the next tile; a next tile past the capacity stores it byte-wise)."""
+    rng = np.random.default_rng(int(short * 10))
+    words = _strings(40, seed=31, lo=2, hi=31)
+    ids = rng.integers(0, len(words), size=60_000)
+    batch = writer.build_batch([make(abi.BYTE_ARRAY, [words[i] for i in ids], abi.RLE_DICTIONARY, page_rows=20000)])
+    ref = pqref.decode_batch(batch)
+    assert ref.code == 0
+    want = b"".join(ref.columns[0]["values"])
+    cols = decoder.alloc_columns(batch)
+    cap = int(len(want) * short) + 5
+    import torch
+    cols[0].binary_data = torch.zeros(cap, dtype=torch.uint8, device=decoder.device)
+    rc, st, _ = decoder._decode_once(decoder.upload(batch), cols, None)
+    assert rc == abi.ERR_INVALID_ARG and st.message.startswith(b"binary capacity"), st.message
+    assert int(st.value_index) >= len(want)
+    got = cols[0].binary_data.cpu().numpy().tobytes()
+    assert got == want[:cap]
+
+
+@pytest.mark.parametrize("version", [1, 2])
+@pytest.mark.parametrize("null_frac", [0.0, 0.1, 0.6, 1.0])
+def test_dictionary_direct_optional(decoder, version, null_frac, dict_fused):
+    """Optional dictionary BYTE_ARRAY columns take the dictionary-direct path too (round 6): the walk reads
+    each page's n_values ids (from k_levels, or the V2 header counts), offsets[n] closes at the column's
+    non-null count; all-null pages and all-null columns included."""
+    words = _lineitem_words() + _strings(40, seed=77, lo=2, hi=30)
+    dl = nulls(30_000, null_frac, seed=int(null_frac * 10) + version)
+    n = int(dl.sum())
+    ids = np.random.default_rng(version).integers(0, len(words), size=n)
+    run_both(decoder, [make(abi.BYTE_ARRAY, [words[i] for i in ids], abi.RLE_DICTIONARY, def_levels=dl, max_def=1,
+                            version=version, page_rows=4000),
+                       make(abi.INT64, zipf_dict_column(9000, card=30, seed=2), abi.RLE_DICTIONARY, page_rows=3000)])
+
+
+@pytest.mark.parametrize("version", [1, 2])
+def test_dictionary_direct_nested(decoder, version):
+    """A repeated dictionary BYTE_ARRAY leaf (rep + def levels; LIST<string>): dictionary-direct, equal to the
+    oracle (values, offsets, both level arrays), and equal to the ids -> map -> copy path."""
+    rng = np.random.default_rng(5)
+    rl, dl = [], []
+    for L in rng.poisson(2.5, size=6000):
+        if L == 0:
+            rl.append(0); dl.append(int(rng.integers(0, 2)))
+        for j in range(L):
+            rl.append(0 if j == 0 else 1); dl.append(3 if rng.random() >= 0.15 else 2)
+    rl = np.array(rl, dtype=np.uint8)
+    dl = np.array(dl, dtype=np.uint8)
+    words = _strings(300, seed=8, lo=0, hi=24)
+    vals = [words[i] for i in rng.integers(0, len(words), size=int((dl == 3).sum()))]
+    ch = make(abi.BYTE_ARRAY, vals, abi.RLE_DICTIONARY, def_levels=dl, rep_levels=rl, max_def=3, max_rep=1,
+              version=version, page_rows=2500)
+    batch, ref, a = run_both(decoder, [ch])
+    decoder.set_dispatch(abi.DISPATCH_DICT_DIRECT, 0)
+    try:
+        _, _, b = run_both(decoder, [ch])
+    finally:
+        decoder.set_dispatch(abi.DISPATCH_DICT_DIRECT, 1)
+    assert np.array_equal(a[0].offsets().cpu().numpy(), b[0].offsets().cpu().numpy())
+
+
+def test_dictionary_direct_optional_errors(decoder):
+    """An id past the dictionary on an optional dictionary-direct column (V1 and V2 pages): the oracle's
+    status (page, value index)."""
+    words = _lineitem_words()
+    dl = nulls(20_000, 0.2, seed=3)
+    n = int(dl.sum())
+    ids = np.random.default_rng(4).integers(0, 6, size=n)
+    for version in (1, 2):
+        ch = make(abi.BYTE_ARRAY, [words[i] for i in ids], abi.RLE_DICTIONARY, def_levels=dl, max_def=1,
+                  version=version, page_rows=3000)
+        ch.dict_num_values = 4
+        run_both(decoder, [ch], expect_error=True)

@@ -128,3 +128,60 @@ def test_timed_out_segment_walk_is_rerun_per_page_and_bit_exact(tmp_path):
     assert f["kernels"] == f["kernels_before"], res  # k_bin_walk_seg replaced by one k_bin_walk launch
     s = res["second"]
     assert s["rc"] == 0 and s["equal"] and s["fallbacks"] == 1, res  # per-page mode stays: no further timeout
+
+
+CHILD_DD = r"""
+import json, sys
+import numpy as np, torch
+sys.path[:0] = [sys.argv[1] + "/parquet-mr_amd", sys.argv[1] + "/tools", sys.argv[1]]
+from pqgpu import abi, decoder as D, native
+from tools.synth import writer
+assert native.LIB_PATH.endswith("libpqgpu_faultinject.so"), native.LIB_PATH
+words = [b"DELIVER IN PERSON", b"COLLECT COD", b"NONE", b"TAKE BACK RETURN", b"R", b"", b"AIR", b"MAIL"]
+ids = np.random.default_rng(3).integers(0, len(words), size=400_000)
+vals = [words[i] for i in ids]
+chunk = writer.write_column_chunk(abi.BYTE_ARRAY, vals, abi.RLE_DICTIONARY, page_rows=5000)
+batch = writer.build_batch([chunk])
+lens = np.array([len(v) for v in vals], dtype=np.int64)
+exp_off = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]))
+exp_data = torch.from_numpy(np.frombuffer(b"".join(vals), dtype=np.uint8).copy())
+dec = D.Decoder(0, poison=0xA5)
+dbatch = dec.upload(batch)
+cols = dec.alloc_columns(batch)
+plan = dec.plan(dbatch, cols)
+def same(c):
+    off = c.offsets().cpu()
+    return bool(torch.equal(off, exp_off)) and bool(torch.equal(c.binary_data[: int(off[-1])].cpu(), exp_data))
+out = {}
+plan.launch()
+rc, st = plan.sync()
+out["first"] = {"rc": rc, "fallbacks": plan.timeout_fallbacks, "equal": same(cols[0])}
+cols[0].binary_data.fill_(0xA5)
+cols[0].values.fill_(0xA5)
+plan.launch()
+rc, st = plan.sync()
+out["second"] = {"rc": rc, "fallbacks": plan.timeout_fallbacks, "equal": same(cols[0])}
+plan.close()
+dec.close()
+print("RESULT " + json.dumps(out))
+"""
+
+
+@pytest.mark.gpu
+def test_timed_out_dictionary_direct_launch_is_rerun_split_and_bit_exact(tmp_path):
+    """A dictionary-direct BYTE_ARRAY column (k_dict_fused_dd: walk + compact ids + chunk byte sums in
+    one launch): the injected walker delay times the launch out and pqg_sync re-runs it in split mode
+    (k_dict_runs<4> + k_dict_tiles_dd, then k_dd_bases / k_dd_str); offsets and bytes are bit-exact."""
+    assert os.path.exists(INJECT_LIB), "build() makes the fault-injection library"
+    script = tmp_path / "child_dd.py"
+    script.write_text(CHILD_DD)
+    env = dict(os.environ, PQGPU_LIB=INJECT_LIB)
+    r = subprocess.run([sys.executable, str(script), REPO], env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")][-1]
+    res = json.loads(line[7:])
+    f = res["first"]
+    assert f["rc"] == 0 and f["equal"], res
+    assert f["fallbacks"] == 1, res
+    s = res["second"]
+    assert s["rc"] == 0 and s["equal"] and s["fallbacks"] == 1, res

@@ -12,6 +12,8 @@ bench.py prints the ONE headline line (C2). This suite times the other configs a
                  rep + def levels and values, then record assembly (pqg_assemble_schema: list
                  validity + offsets, element validity) in every timed step
   str_plain / str_dict / str_dlba / str_dba   BYTE_ARRAY encodings, 4-32 byte strings
+  str_dict_opt   str_dict with 10 % nulls (V1 pages: levels first)
+  str_dict_16k   str_dict with a 16,384-entry dictionary (past the LDS-staged dictionary-direct path)
   bss_f64        BYTE_STREAM_SPLIT doubles
   delta_i64      DELTA_BINARY_PACKED int64 random walk
   delta_i64_2048 the same values with 2048-value blocks of 8 miniblocks (DuckDB's writer; the block-by-block path)
@@ -52,18 +54,25 @@ def gen(name, rows):
         v = np.random.default_rng(1).integers(-2**31, 2**31 - 1, size=rows, dtype=np.int64).astype(np.int32)
         return WL.Workload(name, [writer.write_column_chunk(abi.INT32, v, abi.PLAIN)], [E(v)])
     if name.startswith("str_"):
-        enc = {"str_plain": abi.PLAIN, "str_dict": abi.RLE_DICTIONARY, "str_dlba": abi.DELTA_LENGTH_BYTE_ARRAY,
+        enc = {"str_plain": abi.PLAIN, "str_dict": abi.RLE_DICTIONARY, "str_dict_opt": abi.RLE_DICTIONARY,
+               "str_dict_16k": abi.RLE_DICTIONARY, "str_dlba": abi.DELTA_LENGTH_BYTE_ARRAY,
                "str_dba": abi.DELTA_BYTE_ARRAY}[name]
         if enc == abi.RLE_DICTIONARY:
-            words = writer.BinaryValues.random(1000, 4, 32, seed=3)
-            runs = np.minimum(rng.zipf(1.5, size=rows), 4096)
-            ids = np.repeat(rng.integers(0, 1000, size=runs.size), runs)[:rows]
+            # str_dict: 1,000 entries, required; str_dict_opt: the same with 10 % nulls (V1 pages, parquet-mr's
+            # default writer); str_dict_16k: 16,384 entries (past the 2,048-entry / 32 KiB LDS staging)
+            card = 16384 if name == "str_dict_16k" else 1000
+            dl = WL.nulls(rows, 0.1, 9) if name == "str_dict_opt" else None
+            nv = int(dl.sum()) if dl is not None else rows
+            words = writer.BinaryValues.random(card, 4, 32, seed=3)
+            runs = np.minimum(rng.zipf(1.5, size=nv), 4096)
+            ids = np.repeat(rng.integers(0, card, size=runs.size), runs)[:nv]
             ids_fa, order = writer.first_appearance_ids(ids)
             wl = [words[int(o)] for o in order]
             dwords = writer.BinaryValues(np.concatenate([[0], np.cumsum([len(x) for x in wl])]),
                                          np.frombuffer(b"".join(wl), dtype=np.uint8))
-            ch = writer.write_dict_column_from_ids(abi.BYTE_ARRAY, dwords, ids_fa)
-            return WL.Workload(name, [ch], [E(WL.binary_take(wl, ids_fa))])
+            ch = writer.write_dict_column_from_ids(abi.BYTE_ARRAY, dwords, ids_fa, def_levels=dl,
+                                                   max_def=1 if dl is not None else 0)
+            return WL.Workload(name, [ch], [E(WL.binary_take(wl, ids_fa), dl)])
         if enc == abi.DELTA_BYTE_ARRAY:
             # sorted keys with shared prefixes
             keys = np.sort(rng.integers(0, 10**12, size=rows))
@@ -303,7 +312,8 @@ def run(name, rows, steps, warmup, cpu_budget, check=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("workloads", nargs="*", default=["c1_plain_i32", "c2_zipf2", "c3_mixed", "c5_levels", "str_plain",
-                                                     "str_dict", "str_dlba", "str_dba", "bss_f64", "delta_i64",
+                                                     "str_dict", "str_dict_opt", "str_dict_16k", "str_dlba", "str_dba",
+                                                     "bss_f64", "delta_i64",
                                                      "delta_i64_2048"])
     ap.add_argument("--rows", type=int, default=None, help="override the per-workload row count")
     ap.add_argument("--steps", type=int, default=10)
@@ -321,6 +331,7 @@ def main():
                     "c2_lz4": 100_000_000, "plain_i64_lz4": 100_000_000,
                     "c2_gzip": 100_000_000, "plain_i64_gzip": 100_000_000,
                     "c4_lineitem": 8_000_000, "c3_delta": 100_000_000, "c3_double": 100_000_000,
+                    "str_dict_opt": 20_000_000, "str_dict_16k": 20_000_000,
                     "c3_strings": 100_000_000}
     for w in args.workloads:
         rows = args.rows or default_rows[w]

@@ -32,7 +32,7 @@ for s in $STEPS; do
         || { tail -30 "$OUT/bench_e2e.err"; exit 1; }
       cat "$OUT/bench_e2e.json" ;;
     bench2)
-      timeout -k 10 400 python -u bench.py --no-cpu --zipf 2.0 > "$OUT/bench_zipf2.json" 2> "$OUT/bench_zipf2.err" \
+      timeout -k 10 400 python -u bench.py --no-cpu --no-e2e --zipf 2.0 > "$OUT/bench_zipf2.json" 2> "$OUT/bench_zipf2.err" \
         || { tail -30 "$OUT/bench_zipf2.err"; exit 1; }
       cat "$OUT/bench_zipf2.json" ;;
     suite)
@@ -52,7 +52,7 @@ PY
       python3 tools/kstats.py "$OUT/suiteprof" ;;
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-        python3 bench.py --no-cpu > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
+        python3 bench.py --no-cpu --no-e2e > "$OUT/prof_bench.json" 2> "$OUT/prof.err" \
         || { tail -30 "$OUT/prof.err"; exit 1; }
       python3 tools/kstats.py "$OUT/prof" ;;
     pmc)
@@ -61,7 +61,7 @@ PY
       for grp in "FETCH_SIZE" "WRITE_SIZE" \
                  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU"; do
         timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc/pass$i" -o run -- \
-          python3 bench.py --no-cpu --steps 5 --warmup 1 > "$OUT/pmc/pass$i.log" 2>&1 \
+          python3 bench.py --no-cpu --no-e2e --steps 5 --warmup 1 > "$OUT/pmc/pass$i.log" 2>&1 \
           || { tail -20 "$OUT/pmc/pass$i.log"; exit 1; }
         i=$((i+1))
       done

@@ -339,18 +339,35 @@ def write_column_chunk(physical_type, values, encoding, *, def_levels=None, rep_
     return chunk
 
 
-def write_dict_column_from_ids(physical_type, dict_values, ids, page_rows=20000, encoding=abi.RLE_DICTIONARY):
-    """Required dictionary column from ids already numbered in first-appearance order
-    (fast path for large synthetic inputs; same bytes as write_column_chunk)."""
+def write_dict_column_from_ids(physical_type, dict_values, ids, page_rows=20000, encoding=abi.RLE_DICTIONARY,
+                               def_levels=None, max_def=0, version=1):
+    """Dictionary column from ids already numbered in first-appearance order (fast path for large
+    synthetic inputs; same bytes as write_column_chunk). def_levels / max_def: a flat optional column
+    (ids are the non-null values' ids; pages of page_rows slots, V1 or V2 level sections)."""
     ids = np.ascontiguousarray(ids, dtype=np.int32)
     bit_width = width_from_max_int(len(dict_values) - 1)
-    chunk = ColumnChunk(physical_type=physical_type, values=None)
+    chunk = ColumnChunk(physical_type=physical_type, values=None, max_def=max_def if def_levels is not None else 0)
     chunk.dict_page = plain_encode(dict_values, physical_type)
     chunk.dict_num_values = len(dict_values)
-    for s in range(0, max(len(ids), 1), page_rows):
-        e = min(s + page_rows, len(ids))
-        data = bytes([bit_width]) + rle_encode(ids[s:e], bit_width)
-        chunk.pages.append(Page(body=data, num_values=e - s, encoding=encoding, num_rows=e - s))
+    if def_levels is None:
+        for s in range(0, max(len(ids), 1), page_rows):
+            e = min(s + page_rows, len(ids))
+            data = bytes([bit_width]) + rle_encode(ids[s:e], bit_width)
+            chunk.pages.append(Page(body=data, num_values=e - s, encoding=encoding, num_rows=e - s))
+    else:
+        dl = np.ascontiguousarray(def_levels, dtype=np.uint8)
+        value_pos = np.concatenate([[0], np.cumsum(dl == max_def)]).astype(np.int64)
+        assert int(value_pos[-1]) == len(ids)
+        for s in range(0, max(len(dl), 1), page_rows):
+            e = min(s + page_rows, len(dl))
+            v0, v1 = int(value_pos[s]), int(value_pos[e])
+            data = bytes([bit_width]) + rle_encode(ids[v0:v1], bit_width)
+            dls = _level_section(dl[s:e], max_def, version)
+            page = Page(body=dls + data, num_values=e - s, encoding=encoding, version=version,
+                        num_nulls=(e - s) - (v1 - v0), num_rows=e - s)
+            if version == 2:
+                page.dl_byte_length = len(dls)
+            chunk.pages.append(page)
     chunk.n_values_hint = len(ids)
     return chunk
 
