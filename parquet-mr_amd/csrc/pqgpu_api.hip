@@ -102,8 +102,9 @@ size_t err_region_bytes(int n_pages, int n_cols) {
 //   C_DBA   DELTA_BYTE_ARRAY (lengths here; values by k_dba_copy after the offset scan)
 //   C_DD    dictionary pages of dictionary-direct BYTE_ARRAY columns (ColumnDev::dict_direct): walk + chunk
 //           byte sums, per-column scan, offsets + value bytes (launch_dict_dd), no ids stored
+//   C_DDG   the same for dictionary-direct columns whose dictionary is gathered from HBM (ColumnDev::dd_global)
 enum Cls { C_DICT4 = 0, C_DICT8, C_IDS, C_PLAIN, C_BOOL, C_DELTA4, C_DELTA8, C_BSS, C_BINP, C_DLBA, C_DBA, C_RLEBOOL, C_DD,
-           C_NCLS };
+           C_DDG, C_NCLS };
 constexpr int N_DICT_CLS = 3;  // C_DICT4, C_DICT8, C_IDS: run-record walk + chunk expansion
 
 struct HostErr {
@@ -131,15 +132,21 @@ struct pqg_plan {
   // C_DD: its chunks in `chunks` (per column in page order, each column's first at a multiple of 4:
   // padding entries of page 0xFFFFFFFF between columns), the per-chunk byte sums / first bytes in
   // bscratch, the columns and their chunk ranges in bin_lists, the LDS of the staged dictionaries
-  uint32_t dd_chunk_off = 0, dd_chunk_n = 0, dd_region = 16;
-  uint64_t dd_sums_off = ~0ull;
-  int n_dd_cols = 0, off_dd_cols = 0, off_dd_start = 0;
+  // ([0]: C_DD, dictionaries staged in LDS; [1]: C_DDG, dictionaries gathered from HBM)
+  uint32_t dd_chunk_off[2] = {0, 0}, dd_chunk_n[2] = {0, 0}, dd_region = 16;
+  uint64_t dd_sums_off[2] = {~0ull, ~0ull};
+  int n_dd_cols[2] = {0, 0}, off_dd_cols[2] = {0, 0}, off_dd_start[2] = {0, 0};
   // fused dictionary kernel: persistent walker / tile workgroup counts (0: one page / 4 chunks per WG)
   // BYTE_ARRAY / fixed-width-dictionary scratch (ColumnDev::blen, bsrc, dict_len, dict_src, block_sums,
   // bin_total), dictionary walks, post-passes, offset-scan blocks, copy chunks
   DevBuf bscratch, bin_lists, bin_blocks, bin_chunks, dba_chunks;
   uint64_t blen_bytes = 0;            // leading part of bscratch cleared before every launch
   int n_dict_walk = 0, n_bind = 0, n_fixd = 0, n_bin_cols = 0, n_carry = 0;
+  // BYTE_ARRAY dictionary pages of at least DENT_MIN bytes: walked per tile (launch_dict_entries)
+  DevBuf dent_tiles;
+  uint32_t n_dent_tiles = 0;
+  int n_dent_cols = 0, off_dent_cols = 0, off_dent_start = 0;
+  uint64_t dent_rec_off = 0, dent_scr_off = 0, dent_tb_off = 0;
   int off_dict_walk = 0, off_bind = 0, off_fixd = 0, off_bin_cols = 0, off_carry = 0;  // into bin_lists
   uint32_t n_bin_blocks = 0, n_bin_chunks = 0, n_dba_chunks = 0;
   uint64_t dba_meta_off = ~0ull;  // DELTA_BYTE_ARRAY per-chunk {suffix base, smallest prefix} in bscratch
@@ -384,9 +391,10 @@ static int count_kernels(const pqg_plan* P) {
   for (int c = 0; c < C_NCLS; c++) {
     const int n = P->cls_n[(size_t)c] - (c == C_BINP ? P->n_binp_seg + (pf ? P->n_binp_fused : 0) : 0);
     if (n && c == C_DD) k += P->dict_fused ? 3 : 4;
+    else if (n && c == C_DDG) k += P->dict_fused ? 4 : 5;
     else if (n) k += (c == C_DICT4 || c == C_DICT8 || c == C_IDS) && !P->dict_fused ? 2 : 1;
   }
-  k += (P->n_dict_walk ? 1 : 0) + (P->n_bind ? 1 : 0) + (P->n_fixd ? 1 : 0) +
+  k += (P->n_dict_walk ? 1 : 0) + (P->n_dent_tiles ? 3 : 0) + (P->n_bind ? 1 : 0) + (P->n_fixd ? 1 : 0) +
        ((pf ? P->n_bin_blocks_nf : P->n_bin_blocks) ? 3 : 0) + ((pf ? P->n_bin_chunks_nf : P->n_bin_chunks) ? 1 : 0) +
        (P->cls_n[C_DBA] ? (P->n_dba_chunks ? 4 : 1) : 0) + (P->n_carry ? 1 : 0) + (P->n_segs ? 1 : 0) +
        (pf ? 2 : 0);
@@ -616,10 +624,10 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   }
   // ---- BYTE_ARRAY and fixed-width dictionary columns: scratch layout, dictionary walks,
   // post-passes, offset-scan blocks and copy chunks
-  std::vector<int32_t> dict_walk, bind, fixd, bin_cols, carry_cols;
+  std::vector<int32_t> dict_walk, bind, fixd, bin_cols, carry_cols, dent_cols;
   std::vector<uint64_t> bin_blocks, bin_chunks;
   std::vector<uint64_t> blen_off((size_t)std::max(n_cols, 1), ~0ull), bsrc_off = blen_off, dlen_off = blen_off,
-      dsrc_off = blen_off, bsum_off = blen_off;
+      dsrc_off = blen_off, bsum_off = blen_off, dent_off = blen_off;
   P->bin_total_off.assign((size_t)std::max(n_cols, 1), ~0ull);
   P->bin_capacity.assign((size_t)std::max(n_cols, 1), 0);
   uint64_t sc = 0;
@@ -664,8 +672,10 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   // the dictionary page small enough to stage (DD_DICT_MAX bytes, at most 2,048 entries): their pages
   // leave C_IDS for C_DD (no ids stored, no offset scan or copy of their own). Nullable and nested
   // columns too (round 6): the walk decodes a page's n_values ids from its data section, which k_levels
-  // (or the V2 header counts) give, and values are indexed by out_offset like every other class
-  std::vector<uint8_t> dict_direct((size_t)std::max(n_cols, 1), 0);
+  // (or the V2 header counts) give, and values are indexed by out_offset like every other class.
+  // Larger dictionaries (at most 65,536 entries: u16 ids) take C_DDG: their entries and value bytes are
+  // gathered from HBM instead of LDS (k_dd_gsums / k_dd_gstr; round 6)
+  std::vector<uint8_t> dict_direct((size_t)std::max(n_cols, 1), 0), dd_glob((size_t)std::max(n_cols, 1), 0);
   {
     std::vector<int> npg((size_t)std::max(n_cols, 1), 0), nids((size_t)std::max(n_cols, 1), 0);
     for (int p = 0; p < n_pages; p++) {
@@ -676,15 +686,24 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     for (int i = 0; i < n_cols; i++)
       dict_direct[(size_t)i] = cols[i].physical_type == PQG_BYTE_ARRAY && bin_out(cols[i]) && !ids_mode(cols[i]) &&
                                !col_err[(size_t)i] && !dba_fixed[(size_t)i] && !plain_col[(size_t)i] &&
-                               cols[i].dict_offset >= 0 &&
-                               cols[i].dict_size <= pqg::DD_DICT_MAX && cols[i].dict_num_values <= 2048 &&
+                               cols[i].dict_offset >= 0 && cols[i].dict_num_values <= 65536 &&
                                npg[(size_t)i] > 0 && nids[(size_t)i] == npg[(size_t)i] && ctx->dict_direct;
-    std::vector<int> keep, dd;
-    for (int p : cls_lists[C_IDS]) (dict_direct[(size_t)P->h_work[(size_t)p].column] ? dd : keep).push_back(p);
-    std::stable_sort(dd.begin(), dd.end(), [&](int a, int b) { return P->h_work[(size_t)a].column < P->h_work[(size_t)b].column; });
+    for (int i = 0; i < n_cols; i++)
+      dd_glob[(size_t)i] = dict_direct[(size_t)i] &&
+                           (cols[i].dict_size > pqg::DD_DICT_MAX || cols[i].dict_num_values > 2048);
+    std::vector<int> keep, dd, ddg;
+    for (int p : cls_lists[C_IDS]) {
+      const int c = P->h_work[(size_t)p].column;
+      (!dict_direct[(size_t)c] ? keep : dd_glob[(size_t)c] ? ddg : dd).push_back(p);
+    }
+    auto by_col = [&](int a, int b) { return P->h_work[(size_t)a].column < P->h_work[(size_t)b].column; };
+    std::stable_sort(dd.begin(), dd.end(), by_col);
+    std::stable_sort(ddg.begin(), ddg.end(), by_col);
     for (int p : dd) P->page_cls[(size_t)p] = C_DD;
+    for (int p : ddg) P->page_cls[(size_t)p] = C_DDG;
     cls_lists[C_IDS].swap(keep);
     cls_lists[C_DD].swap(dd);
+    cls_lists[C_DDG].swap(ddg);
   }
   // PLAIN BYTE_ARRAY pages walked in segments when there are few of them (k_bin_walk_seg)
   std::vector<uint64_t> segs;
@@ -720,7 +739,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   // by k_dict_fused_dd for every slot k_dd_str reads (not cleared; padded: k_dd_str reads whole dwords)
   for (int i = 0; i < n_cols; i++)
     if (dict_direct[(size_t)i])
-      blen_off[(size_t)i] = take((cols[i].dict_num_values <= 256 ? 1u : 2u) * (slot_acc[(size_t)i] + 16));
+      blen_off[(size_t)i] = take((cols[i].dict_num_values <= 256 && !dd_glob[(size_t)i] ? 1u : 2u) * (slot_acc[(size_t)i] + 16));
   if (!pcp.empty()) P->pflag_off = take(8);
   if (P->null_hints) P->hint_off = take(8);
   if (!segs.empty()) P->seg_tmp_off = take(4 * 2 * (uint64_t)pqg::BW_SEG_CAP * segs.size());
@@ -735,7 +754,10 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     P->bin_capacity[(size_t)i] = cols[i].binary_capacity;
     if (dict_direct[(size_t)i]) {  // the byte total (k_dd_bases) and the dictionary's entries only
       P->bin_total_off[(size_t)i] = take(8);
-      dict_walk.push_back(i);
+      // (dictionaries gathered from HBM: always the tile walk, whose scatter also packs their entries)
+      ((cols[i].dict_size >= pqg::DENT_MIN || dd_glob[(size_t)i]) && cols[i].dict_num_values ? dent_cols : dict_walk)
+          .push_back(i);
+      if (dd_glob[(size_t)i]) dent_off[(size_t)i] = take(8 * ((uint64_t)cols[i].dict_num_values + 1));
       dlen_off[(size_t)i] = take(4 * ((uint64_t)cols[i].dict_num_values + 1));
       dsrc_off[(size_t)i] = take(4 * ((uint64_t)cols[i].dict_num_values + 1));
       continue;
@@ -748,7 +770,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     for (uint64_t b = 0; b < nb; b++) bin_blocks.push_back(((uint64_t)(uint32_t)i << 32) | b);
     if (nb == 0 && cols[i].values) P->empty_bin_values.push_back(cols[i].values);
     if (cols[i].dict_offset >= 0 && !col_err[(size_t)i]) {
-      dict_walk.push_back(i);
+      (cols[i].dict_size >= pqg::DENT_MIN && cols[i].dict_num_values ? dent_cols : dict_walk).push_back(i);
       dlen_off[(size_t)i] = take(4 * ((uint64_t)cols[i].dict_num_values + 1));
       dsrc_off[(size_t)i] = take(4 * ((uint64_t)cols[i].dict_num_values + 1));
     }
@@ -826,34 +848,37 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     }
     P->chunk_n[k - C_DICT4] = (uint32_t)chunk_list.size() - P->chunk_off[k - C_DICT4];
   }
-  std::vector<int32_t> dd_cols, dd_start;
-  P->dd_chunk_off = (uint32_t)chunk_list.size();
-  for (int p : cls_lists[C_DD]) {  // (sorted by column)
-    PageWork& w = P->h_work[(size_t)p];
-    if (dd_cols.empty() || dd_cols.back() != w.column) {  // dd_start: [begin, end) of each column's chunks
-      if (!dd_cols.empty()) dd_start.push_back((int32_t)(chunk_list.size() - P->dd_chunk_off));
-      while ((chunk_list.size() - P->dd_chunk_off) % (uint32_t)pqg::DICT_WPB) {  // whole workgroups per column
-        chunk_list.push_back(0xFFFFFFFFull);
-        chunk_total++;
+  std::vector<int32_t> dd_cols[2], dd_start[2];
+  for (int g = 0; g < 2; g++) {  // C_DD, then C_DDG
+    P->dd_chunk_off[g] = (uint32_t)chunk_list.size();
+    for (int p : cls_lists[g ? C_DDG : C_DD]) {  // (sorted by column)
+      PageWork& w = P->h_work[(size_t)p];
+      if (dd_cols[g].empty() || dd_cols[g].back() != w.column) {  // dd_start: [begin, end) of each column's chunks
+        if (!dd_cols[g].empty()) dd_start[g].push_back((int32_t)(chunk_list.size() - P->dd_chunk_off[g]));
+        while ((chunk_list.size() - P->dd_chunk_off[g]) % (uint32_t)pqg::DICT_WPB) {  // whole workgroups per column
+          chunk_list.push_back(0xFFFFFFFFull);
+          chunk_total++;
+        }
+        dd_cols[g].push_back(w.column);
+        dd_start[g].push_back((int32_t)(chunk_list.size() - P->dd_chunk_off[g]));
+        const pqg_column_desc& cc = cols[w.column];
+        if (!g)
+          P->dd_region = std::max<uint32_t>(P->dd_region, (uint32_t)(((uint64_t)cc.dict_size + 15u) & ~15ull) +
+                                                              4u * (uint32_t)cc.dict_num_values);
       }
-      dd_cols.push_back(w.column);
-      dd_start.push_back((int32_t)(chunk_list.size() - P->dd_chunk_off));
-      const pqg_column_desc& cc = cols[w.column];
-      P->dd_region = std::max<uint32_t>(P->dd_region, (uint32_t)(((uint64_t)cc.dict_size + 15u) & ~15ull) +
-                                                          4u * (uint32_t)cc.dict_num_values);
+      const uint32_t ch = pqg::dict_chunk_values(4);
+      w.rec_base = rec_total;
+      rec_total += (uint64_t)std::min<uint32_t>(w.num_slots, w.size) + 1;
+      w.chunk_base = chunk_total;
+      const uint32_t nch = (uint32_t)(((uint64_t)w.num_slots + 3u + ch - 1) / ch);
+      for (uint32_t j = 0; j < nch; j++) chunk_list.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
+      chunk_total += nch;
     }
-    const uint32_t ch = pqg::dict_chunk_values(4);
-    w.rec_base = rec_total;
-    rec_total += (uint64_t)std::min<uint32_t>(w.num_slots, w.size) + 1;
-    w.chunk_base = chunk_total;
-    const uint32_t nch = (uint32_t)(((uint64_t)w.num_slots + 3u + ch - 1) / ch);
-    for (uint32_t j = 0; j < nch; j++) chunk_list.push_back((uint64_t)(uint32_t)p | ((uint64_t)j << 32));
-    chunk_total += nch;
+    if (!dd_cols[g].empty()) dd_start[g].push_back((int32_t)(chunk_list.size() - P->dd_chunk_off[g]));
+    P->dd_chunk_n[g] = (uint32_t)chunk_list.size() - P->dd_chunk_off[g];
+    P->n_dd_cols[g] = (int)dd_cols[g].size();
+    if (P->dd_chunk_n[g]) P->dd_sums_off[g] = take(8 * (uint64_t)P->dd_chunk_n[g]);
   }
-  if (!dd_cols.empty()) dd_start.push_back((int32_t)(chunk_list.size() - P->dd_chunk_off));
-  P->dd_chunk_n = (uint32_t)chunk_list.size() - P->dd_chunk_off;
-  P->n_dd_cols = (int)dd_cols.size();
-  if (P->dd_chunk_n) P->dd_sums_off = take(8 * (uint64_t)P->dd_chunk_n);
   // ---- flatten lists: [levels][class 0]...[class n]
   std::vector<int32_t> flat(lvl_list.begin(), lvl_list.end());
   P->levels_off = 0;
@@ -880,8 +905,27 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
   P->off_fixd = (int)bl.size(); P->n_fixd = (int)fixd.size(); bl.insert(bl.end(), fixd.begin(), fixd.end());
   P->off_bin_cols = (int)bl.size(); P->n_bin_cols = (int)bin_cols.size(); bl.insert(bl.end(), bin_cols.begin(), bin_cols.end());
   P->off_carry = (int)bl.size(); P->n_carry = (int)carry_cols.size(); bl.insert(bl.end(), carry_cols.begin(), carry_cols.end());
-  P->off_dd_cols = (int)bl.size(); bl.insert(bl.end(), dd_cols.begin(), dd_cols.end());
-  P->off_dd_start = (int)bl.size(); bl.insert(bl.end(), dd_start.begin(), dd_start.end());
+  std::vector<uint64_t> dent_tiles;
+  {  // large BYTE_ARRAY dictionaries: 2 KiB tiles of their pages, per column in dent_cols order
+    std::vector<int32_t> dstart(1, 0);
+    for (int i : dent_cols) {
+      const uint32_t nt = (cols[i].dict_size + pqg::DENT_TILE - 1) / pqg::DENT_TILE;
+      for (uint32_t t = 0; t < nt; t++) dent_tiles.push_back((uint64_t)(uint32_t)i | ((uint64_t)t << 32));
+      dstart.push_back((int32_t)dent_tiles.size());
+    }
+    P->off_dent_cols = (int)bl.size(); P->n_dent_cols = (int)dent_cols.size(); bl.insert(bl.end(), dent_cols.begin(), dent_cols.end());
+    P->off_dent_start = (int)bl.size(); bl.insert(bl.end(), dstart.begin(), dstart.end());
+    P->n_dent_tiles = (uint32_t)dent_tiles.size();
+    if (P->n_dent_tiles) {
+      P->dent_rec_off = take(16ull * P->n_dent_tiles);
+      P->dent_scr_off = take(2ull * pqg::DENT_CAP * P->n_dent_tiles);
+      P->dent_tb_off = take(8ull * P->n_dent_tiles);
+    }
+  }
+  for (int g = 0; g < 2; g++) {
+    P->off_dd_cols[g] = (int)bl.size(); bl.insert(bl.end(), dd_cols[g].begin(), dd_cols[g].end());
+    P->off_dd_start[g] = (int)bl.size(); bl.insert(bl.end(), dd_start[g].begin(), dd_start[g].end());
+  }
   P->n_bin_blocks = (uint32_t)bin_blocks.size();
   P->n_bin_chunks = (uint32_t)bin_chunks.size();
   // ---- upload
@@ -898,6 +942,7 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
             P->bin_chunks.ensure(sizeof(uint64_t) * std::max<size_t>(bin_chunks.size(), 1)) == hipSuccess &&
             P->dba_chunks.ensure(sizeof(uint64_t) * std::max<size_t>(dba_chunks.size(), 1)) == hipSuccess &&
             P->segs.ensure(sizeof(uint64_t) * std::max<size_t>(segs.size(), 1)) == hipSuccess &&
+            P->dent_tiles.ensure(sizeof(uint64_t) * std::max<size_t>(dent_tiles.size(), 1)) == hipSuccess &&
             P->psegs.ensure(sizeof(uint64_t) * std::max<size_t>(psegs.size(), 1)) == hipSuccess &&
             P->pstatus.ensure(2 * sizeof(uint64_t) * std::max<size_t>(psegs.size(), 1)) == hipSuccess &&
             P->pcol_pages.ensure(sizeof(int32_t) * std::max<size_t>(pcp.size(), 1)) == hipSuccess &&
@@ -918,10 +963,12 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
       d.bsrc = (uint32_t*)at(bsrc_off[(size_t)i]);
       d.dict_len = (uint32_t*)at(dlen_off[(size_t)i]);
       d.dict_src = (uint32_t*)at(dsrc_off[(size_t)i]);
+      d.dict_ent = (uint64_t*)at(dent_off[(size_t)i]);
       d.block_sums = (uint64_t*)at(bsum_off[(size_t)i]);
       d.bin_total = (uint64_t*)at(P->bin_total_off[(size_t)i]);
       d.n_slots = slot_acc[(size_t)i];
-      d.dict_direct = dict_direct[(size_t)i] ? (cols[i].dict_num_values <= 256 ? 1u : 2u) : 0u;  // id bytes
+      d.dict_direct = dict_direct[(size_t)i] ? (cols[i].dict_num_values <= 256 && !dd_glob[(size_t)i] ? 1u : 2u) : 0u;  // id bytes
+      d.dd_global = dd_glob[(size_t)i];
       if (dba_fixed[(size_t)i]) {  // DELTA_BYTE_ARRAY values go straight to the fixed-width output
         d.binary_data = (uint8_t*)cols[i].values;
         d.binary_capacity = slot_acc[(size_t)i] * (uint64_t)d.elem_width;
@@ -936,6 +983,9 @@ static int plan_create_impl(pqg_ctx* ctx, const uint8_t* d_bytes, uint64_t n_byt
     ok = ok && hipMemcpyAsync(P->bin_chunks.p, bin_chunks.data(), sizeof(uint64_t) * bin_chunks.size(), hipMemcpyHostToDevice, s) == hipSuccess;
   if (!segs.empty())
     ok = ok && hipMemcpyAsync(P->segs.p, segs.data(), sizeof(uint64_t) * segs.size(), hipMemcpyHostToDevice, s) == hipSuccess;
+  if (!dent_tiles.empty())
+    ok = ok && hipMemcpyAsync(P->dent_tiles.p, dent_tiles.data(), sizeof(uint64_t) * dent_tiles.size(), hipMemcpyHostToDevice,
+                              s) == hipSuccess;
   if (!psegs.empty()) {
     ok = ok && hipMemcpyAsync(P->psegs.p, psegs.data(), sizeof(uint64_t) * psegs.size(), hipMemcpyHostToDevice, s) == hipSuccess;
     ok = ok && hipMemsetAsync(P->pstatus.p, 0, 2 * sizeof(uint64_t) * psegs.size(), s) == hipSuccess;
@@ -1019,12 +1069,26 @@ int pqg_plan_launch(pqg_plan* P) {
   // value kernel; with V2 header null counts (null_hints) the host has them and k_levels only verifies
   // them, on the caller's stream beside the forked value kernels (launched after the fork below)
   const bool hints = P->null_hints && P->levels_n;
-  if (P->levels_n && !hints) {
+  const int32_t* bl = (const int32_t*)P->bin_lists.p;
+  auto launch_dict_walks = [&](hipStream_t st) -> hipError_t {
+    hipError_t r = hipSuccess;
+    if (P->n_dict_walk)  // BYTE_ARRAY dictionary entries (PlainBinaryDictionary ctor)
+      r = pqg::launch_bin_walk(st, P->d_bytes, P->n_bytes, work, cols, bl + P->off_dict_walk, P->n_dict_walk, 1,
+                               P->n_pages, err, ecount);
+    if (r == hipSuccess && P->n_dent_tiles) {  // ... of the large dictionaries, per 2 KiB tile
+      uint8_t* scb = (uint8_t*)P->bscratch.p;
+      r = pqg::launch_dict_entries(st, P->d_bytes, P->n_bytes, cols, (const uint64_t*)P->dent_tiles.p, P->n_dent_tiles,
+                                   bl + P->off_dent_cols, bl + P->off_dent_start, P->n_dent_cols,
+                                   (uint64_t*)(scb + P->dent_rec_off), (uint16_t*)(scb + P->dent_scr_off),
+                                   (uint64_t*)(scb + P->dent_tb_off), P->n_pages, err, ecount);
+    }
+    return r;
+  };
+  if (e == hipSuccess && P->levels_n && !hints) {
     e = pqg::launch_levels(s, P->d_bytes, P->n_bytes, work, cols, lists + P->levels_off, P->levels_n, err, ecount, nullptr);
     if (e == hipSuccess)
       e = pqg::launch_scan(s, work, (const int32_t*)P->col_pages.p, (const int32_t*)P->col_page_start.p, P->n_scan_cols);
   }
-  const int32_t* bl = (const int32_t*)P->bin_lists.p;
   // The one-pass PLAIN BYTE_ARRAY kernel is latency / issue bound (~1 TB/s) and independent of the other
   // columns' kernels (most of them HBM bound): with other pages in the plan it runs on a second queue,
   // forked after the levels and joined at the end, so the two kinds share the chip.
@@ -1033,7 +1097,7 @@ int pqg_plan_launch(pqg_plan* P) {
   bool fork = false, fork_bin = false, fork_fix = false;
   const bool has_fixed = P->cls_n[C_DICT4] || P->cls_n[C_DICT8] || P->cls_n[C_PLAIN] || P->cls_n[C_BOOL] ||
                          P->cls_n[C_RLEBOOL] || P->cls_n[C_DELTA4] || P->cls_n[C_DELTA8] || P->cls_n[C_BSS];
-  const bool has_bin = P->n_dict_walk || P->cls_n[C_IDS] || P->cls_n[C_DD] || P->cls_n[C_BINP] - P->n_binp_seg - (pf ? P->n_binp_fused : 0) > 0 ||
+  const bool has_bin = P->n_dict_walk || P->n_dent_tiles || P->cls_n[C_IDS] || P->cls_n[C_DD] || P->cls_n[C_DDG] || P->cls_n[C_BINP] - P->n_binp_seg - (pf ? P->n_binp_fused : 0) > 0 ||
                        P->cls_n[C_DLBA] || P->cls_n[C_DBA] || P->n_segs;
   const bool want = e == hipSuccess && ((pf && (has_fixed || has_bin)) || (has_bin && has_fixed) ||
                                         (hints && (pf || has_bin || has_fixed)));
@@ -1067,9 +1131,7 @@ int pqg_plan_launch(pqg_plan* P) {
   }
   const hipStream_t sb = fork_bin ? ctx->bin_stream : s;  // BYTE_ARRAY kernels of the other columns
   const hipStream_t sf = fork_fix ? ctx->fix_stream : s;  // fixed-width columns
-  if (e == hipSuccess && P->n_dict_walk)  // BYTE_ARRAY dictionary entries (PlainBinaryDictionary ctor)
-    e = pqg::launch_bin_walk(sb, P->d_bytes, P->n_bytes, work, cols, bl + P->off_dict_walk, P->n_dict_walk, 1, P->n_pages,
-                             err, ecount);
+  if (e == hipSuccess) e = launch_dict_walks(sb);
   for (int k = 0; k < C_NCLS && e == hipSuccess; k++) {
     int n = P->cls_n[(size_t)k] - (k == C_BINP ? P->n_binp_seg + (pf ? P->n_binp_fused : 0) : 0);
     if (!n) continue;
@@ -1091,12 +1153,15 @@ int pqg_plan_launch(pqg_plan* P) {
         break;
       }
       case C_DD:
+      case C_DDG: {
+        const int g = k == C_DDG ? 1 : 0;
         e = pqg::launch_dict_dd(sb, P->d_bytes, P->n_bytes, work, cols, l, n, (uint64_t*)P->rec.p,
-                                (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->dd_chunk_off, P->dd_chunk_n,
-                                (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused, err, ecount,
-                                (uint64_t*)((uint8_t*)P->bscratch.p + P->dd_sums_off), bl + P->off_dd_cols,
-                                bl + P->off_dd_start, P->n_dd_cols, P->dd_region);
+                                (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->dd_chunk_off[g],
+                                P->dd_chunk_n[g], (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused,
+                                err, ecount, (uint64_t*)((uint8_t*)P->bscratch.p + P->dd_sums_off[g]),
+                                bl + P->off_dd_cols[g], bl + P->off_dd_start[g], P->n_dd_cols[g], P->dd_region, g == 1);
         break;
+      }
       case C_BSS: e = pqg::launch_bss(sf, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;
       case C_BINP:
         e = pqg::launch_bin_walk(sb, P->d_bytes, P->n_bytes, work, cols, l, n, 0, P->n_pages, err, ecount);
@@ -1180,6 +1245,7 @@ int pqg_plan_destroy(pqg_plan* P) {
   P->bin_chunks.release();
   P->dba_chunks.release();
   P->segs.release();
+  P->dent_tiles.release();
   delete P;
   return PQG_OK;
 }
@@ -1341,7 +1407,7 @@ int sync_plan(pqg_plan* P, pqg_status* st, std::vector<PageWork>* work) {
   // BYTE_ARRAY segment walk that timed out waiting for its predecessor reaches the caller)
   const int tpage = st ? (int)st->page : -1;
   const int tcls = tpage >= 0 && tpage < P->n_pages ? P->page_cls[(size_t)tpage] : -1;
-  if (rc == PQG_ERR_TIMEOUT && P->dict_fused && (tcls == C_DICT4 || tcls == C_DICT8 || tcls == C_IDS || tcls == C_DD)) {
+  if (rc == PQG_ERR_TIMEOUT && P->dict_fused && (tcls == C_DICT4 || tcls == C_DICT8 || tcls == C_IDS || tcls == C_DD || tcls == C_DDG)) {
     // The fused dictionary kernel's hand-off relies on the walker workgroups being dispatched before
     // the expansion workgroups that wait for them, which HIP does not promise. A launch in which an
     // expansion waited past SPIN_TIMEOUT_TICKS (it then stops and reports PQG_ERR_TIMEOUT; the walkers

@@ -434,6 +434,7 @@ constexpr uint64_t SEG_TIMEOUT_TICKS = 200000000ull;  // 2 s of s_memrealtime (1
 #endif
 static_assert(SEG_B == BW_SEG_BYTES && SEG_CAP == BW_SEG_CAP, "host segmentation (pqgpu_internal.h)");
 static_assert(BW_WIN == BP_TILE, "host tiling of k_bin_plain (pqgpu_internal.h)");
+static_assert(BW_WIN == DENT_TILE && BW_CAP == DENT_CAP, "host tiling of the dictionary entry walk (pqgpu_internal.h)");
 
 // a value could start at p: its 4 length bytes and its bytes inside the section
 __device__ __forceinline__ bool seg_candidate(rsrc_t rs, uint32_t p, uint32_t end) {
@@ -2737,6 +2738,135 @@ hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, Pa
                       const int32_t* list, int n, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_bss, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_BIN_ARGS);
+  return hipGetLastError();
+}
+
+// ---- BYTE_ARRAY dictionary pages of DENT_MIN bytes or more (PlainBinaryDictionary ctor,
+// PlainValuesDictionary.java:58-134: dict_n entries of [u32 length][bytes] read one after the other),
+// walked in parallel. The one-wave walk (k_bin_walk, dict_walk = 1) follows a 360 KB page of 16,384
+// entries tile after tile in ~550 us (profiles/r06); here every 2 KiB tile is walked at once from a
+// guessed first entry, as the one-pass PLAIN tiles do, but without inter-workgroup waits:
+//   k_dent_walk     one wave per tile: bp_guess (tile 0: the page start), the tile's chain (bp_walk), its
+//                   accepted starts (u16 tile offsets) to the tile's scratch, the record {guess, exit, count,
+//                   code}
+//   k_dent_resolve  one wave per dictionary: the true entry of tile t is the exit of tile t - 1; a tile
+//                   whose guess is not that entry (rare) is walked again from it by this wave; tile t's first
+//                   entry index = the counts before it (capped at dict_n); the chain's first error before
+//                   dict_n entries is the dictionary's error (bin_value_error's dictionary codes, as the
+//                   one-wave walk reports them)
+//   k_dent_scatter  one wave per tile: its entries' lengths and sources to dict_len / dict_src
+__global__ __launch_bounds__(64 * WPB) void k_dent_walk(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                       const ColumnDev* __restrict__ cols, const uint64_t* __restrict__ tiles,
+                                                       uint32_t n_tiles, uint64_t* rec, uint16_t* scr) {
+  __shared__ __attribute__((aligned(16))) BinPlainLds lds_all[WPB];
+  const uint32_t t = blockIdx.x * WPB + wave_id();
+  if (t >= n_tiles) return;
+  const uint32_t lane = lane_id();
+  BinPlainLds& L = lds_all[wave_id()];
+  const uint64_t tv = tiles[t];
+  const ColumnDev& cd = cols[(uint32_t)tv];
+  const uint32_t s = (uint32_t)(tv >> 32), B = s * BW_WIN, end = uni((uint32_t)cd.dict_bytes);
+  const rsrc_t rs = make_rsrc(bytes + cd.dict_offset, n_bytes - cd.dict_offset);
+  const BwBytes cur = bw_load(rs, B);
+  const BpGuess gs = s == 0 ? BpGuess{0u, 0xFFFFFFFFu, 0, 0, false} : bp_guess(L, cur, rs, B, end);
+  BpWalk r{gs.pos, 0, 0};
+  if (gs.pos != 0xFFFFFFFFu)
+    r = s == 0 ? bp_walk<true>(L, cur, rs, B, 0u, end)
+               : bp_walk<true>(L, cur, rs, B, gs.pos, end, gs.index, gs.total, gs.eff_end, gs.fast);
+  for (uint32_t k = lane; k < r.n; k += WAVE) gst(scr + (uint64_t)t * BW_CAP + k, L.acc[k]);
+  if (lane == 0) {
+    gst(rec + 2u * t, (uint64_t)gs.pos | ((uint64_t)r.pos << 32));
+    gst(rec + 2u * t + 1u, (uint64_t)r.n | ((uint64_t)(uint32_t)r.code << 32));
+  }
+}
+
+__global__ __launch_bounds__(64) void k_dent_resolve(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                    const ColumnDev* __restrict__ cols, const int32_t* __restrict__ dcols,
+                                                    const int32_t* __restrict__ dstart, const uint64_t* rec, uint16_t* scr,
+                                                    uint64_t* tb, int n_pages, uint64_t* err, ErrCount err_count) {
+  __shared__ __attribute__((aligned(16))) BinPlainLds L;
+  const uint32_t lane = lane_id();
+  const int col = dcols[blockIdx.x];
+  const ColumnDev& cd = cols[col];
+  const uint32_t t0 = (uint32_t)dstart[blockIdx.x], t1 = (uint32_t)dstart[blockIdx.x + 1];
+  const uint32_t N = uni(cd.dict_n), end = uni((uint32_t)cd.dict_bytes);
+  const rsrc_t rs = make_rsrc(bytes + cd.dict_offset, n_bytes - cd.dict_offset);
+  uint32_t entry = 0, before = 0, t = t0;
+  int code = 0;
+  bool done = N == 0;
+  uint64_t r0 = 0, r1 = 0;  // lane l: the records of tile (t - t0) rounded down to 64, + l
+  for (; t < t1 && !done; t++) {
+    const uint32_t s = t - t0, j = s & (WAVE - 1u);
+    if (j == 0) {  // the next 64 records, one per lane
+      const bool in = t + lane < t1;
+      r0 = in ? sld(rec + 2u * (t + lane)) : 0ull;
+      r1 = in ? sld(rec + 2u * (t + lane) + 1u) : 0ull;
+    }
+    const uint32_t B = s * BW_WIN;
+    if (entry >= B + BW_WIN) {  // a value spans the whole tile: no entry starts in it
+      if (lane == 0) gst(tb + t, (uint64_t)before);
+      continue;
+    }
+    const uint32_t guess = uni(rdl((uint32_t)r0, j));
+    uint32_t ex = uni(rdl((uint32_t)(r0 >> 32), j)), cnt = uni(rdl((uint32_t)r1, j));
+    uint32_t cd_code = uni(rdl((uint32_t)(r1 >> 32), j));
+    if (s != 0 && guess != entry) {  // misspeculated (or no guess): this wave walks the tile from its true entry
+      const BwBytes cur = bw_load(rs, B);
+      const BpWalk rr = bp_walk<true>(L, cur, rs, B, entry, end);
+      for (uint32_t k = lane; k < rr.n; k += WAVE) gst(scr + (uint64_t)t * BW_CAP + k, L.acc[k]);
+      ex = rr.pos;
+      cnt = rr.n;
+      cd_code = (uint32_t)rr.code;
+      wave_sync();
+    }
+    const uint32_t take = cnt < N - before ? cnt : N - before;
+    if (lane == 0) gst(tb + t, (uint64_t)before | ((uint64_t)take << 32));
+    before += take;
+    if (before >= N) {
+      done = true;
+    } else if (cd_code) {  // the chain stopped (an error, or the section end) before dict_n entries
+      code = bin_value_error(rs, ex, end, true);
+      done = true;
+    } else {
+      entry = ex;
+    }
+  }
+  if (!done) code = bin_value_error(rs, entry, end, true);  // past the last tile before dict_n entries
+  for (uint32_t u = t + lane; u < t1; u += WAVE) gst(tb + u, (uint64_t)before);  // tiles past the end: none
+  if (code && lane == 0) report(err, err_count, n_pages + col, 0, before, code);
+}
+
+__global__ __launch_bounds__(64 * WPB) void k_dent_scatter(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                          const ColumnDev* __restrict__ cols,
+                                                          const uint64_t* __restrict__ tiles, uint32_t n_tiles,
+                                                          const uint16_t* __restrict__ scr, const uint64_t* __restrict__ tb) {
+  const uint32_t t = blockIdx.x * WPB + wave_id();
+  if (t >= n_tiles) return;
+  const uint64_t tv = tiles[t];
+  const ColumnDev& cd = cols[(uint32_t)tv];
+  const uint32_t B = (uint32_t)(tv >> 32) * BW_WIN;
+  const uint64_t v = tb[t];
+  const uint32_t base = (uint32_t)v, cnt = (uint32_t)(v >> 32);
+  const rsrc_t rs = make_rsrc(bytes + cd.dict_offset, n_bytes - cd.dict_offset);
+  for (uint32_t k = lane_id(); k < cnt; k += WAVE) {
+    const uint32_t p = B + scr[(uint64_t)t * BW_CAP + k];
+    const uint32_t len = ld4_any(rs, p);
+    gst(cd.dict_len + base + k, len);
+    gst(cd.dict_src + base + k, p + 4u);
+    if (cd.dict_ent) gst(cd.dict_ent + base + k, ((uint64_t)(p + 4u) << 32) | len);
+  }
+}
+
+hipError_t launch_dict_entries(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, const ColumnDev* cols,
+                               const uint64_t* tiles, uint32_t n_tiles, const int32_t* dcols, const int32_t* dstart,
+                               int n_dcols, uint64_t* rec, uint16_t* scr, uint64_t* tb, int n_pages, uint64_t* err,
+                               ErrCount err_count) {
+  if (!n_tiles || n_dcols <= 0) return hipSuccess;
+  const dim3 grid((n_tiles + WPB - 1) / WPB), blk(64 * WPB);
+  hipLaunchKernelGGL(k_dent_walk, grid, blk, 0, st, bytes, n_bytes, cols, tiles, n_tiles, rec, scr);
+  hipLaunchKernelGGL(k_dent_resolve, dim3(n_dcols), dim3(64), 0, st, bytes, n_bytes, cols, dcols, dstart, rec, scr, tb,
+                     n_pages, err, err_count);
+  hipLaunchKernelGGL(k_dent_scatter, grid, blk, 0, st, bytes, n_bytes, cols, tiles, n_tiles, scr, tb);
   return hipGetLastError();
 }
 

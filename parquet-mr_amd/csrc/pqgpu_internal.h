@@ -35,8 +35,12 @@ struct ColumnDev {
   uint64_t* bin_total;     // BYTE_ARRAY: bytes of the decoded values (device, one u64)
   // A required BYTE_ARRAY column whose data pages are all dictionary-encoded and whose dictionary page
   // fits DD_DICT_MAX: its pages take launch_dict_dd (compact ids + chunk byte sums, scan, offsets and
-  // bytes); dict_direct = the bytes of its ids in blen (1: u8, 2: u16), 0 for every other column
+  // bytes); dict_direct = the bytes of its ids in blen (1: u8, 2: u16), 0 for every other column.
+  // dd_global: a dictionary too large to stage in LDS (over DD_DICT_MAX bytes or 2,048 entries, at most
+  // 65,536 entries: u16 ids): entries and value bytes are gathered from HBM (k_dd_gsums, k_dd_gstr)
   uint32_t dict_direct;
+  uint32_t dd_global;
+  uint64_t* dict_ent;  // dd_global: entry i = source << 32 | length (k_dent_scatter), one gather per value
 };
 
 // Per page, on the device. The host fills the descriptor facts; for nullable
@@ -118,11 +122,14 @@ hipError_t launch_dict_ids(hipStream_t st, const uint8_t* bytes, uint64_t n_byte
 // (k_dict_fused_dd, or k_dict_runs + k_dict_tiles_dd in split mode), the per-column scan of the sums
 // (k_dd_bases: chunks of column i are sums[dd_start[2i] .. dd_start[2i + 1])), then offsets and value
 // bytes (k_dd_str; dd_region = LDS bytes of the staged dictionary page + its u32 entry table)
+// global: the columns' dictionaries are gathered from HBM (ColumnDev::dd_global): ids only in the walk's
+// expansion, then k_dd_gsums, k_dd_bases, k_dd_gstr
 hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                           const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                           const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
                           uint32_t epoch, bool fused, uint64_t* err, ErrCount err_count, uint64_t* sums,
-                          const int32_t* dd_cols, const int32_t* dd_start, int n_dd_cols, uint32_t dd_region);
+                          const int32_t* dd_cols, const int32_t* dd_start, int n_dd_cols, uint32_t dd_region,
+                          bool global);
 // DELTA_LENGTH_BYTE_ARRAY lengths (k_delta into blen, records PageWork::aux)
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count);
@@ -184,6 +191,17 @@ constexpr uint32_t SCAN_BLOCK = 4096;   // values per offset-scan block
 constexpr uint32_t DD_DICT_MAX = 32768;
 hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                       const int32_t* list, int n, uint64_t* err, ErrCount err_count);
+// BYTE_ARRAY dictionary pages of at least DENT_MIN bytes: entries walked per 2 KiB tile in parallel
+// (k_dent_walk, k_dent_resolve, k_dent_scatter) instead of one wave per page. tiles: column | tile << 32
+// (in column order; dictionary dcols[i]'s tiles are [dstart[i], dstart[i + 1])); scratch per tile: rec
+// 16 bytes, scr BW_CAP u16, tb 8 bytes
+constexpr uint32_t DENT_MIN = 16384;
+constexpr uint32_t DENT_TILE = 2048;
+constexpr uint32_t DENT_CAP = DENT_TILE / 4;
+hipError_t launch_dict_entries(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, const ColumnDev* cols,
+                               const uint64_t* tiles, uint32_t n_tiles, const int32_t* dcols, const int32_t* dstart,
+                               int n_dcols, uint64_t* rec, uint16_t* scr, uint64_t* tb, int n_pages, uint64_t* err,
+                               ErrCount err_count);
 hipError_t launch_bin_walk(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                            const ColumnDev* cols, const int32_t* list, int n, int dict_walk, int n_pages,
                            uint64_t* err, ErrCount err_count);

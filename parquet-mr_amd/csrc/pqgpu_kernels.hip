@@ -671,7 +671,9 @@ constexpr uint64_t SPIN_TIMEOUT_TICKS = 200000000ull;  // 2 s of s_memrealtime (
 // stores the ids compactly (ColumnDev::blen as u8 ids for dict_direct 1, u16 for 2: a quarter / half of
 // the u32 id traffic) and the chunk's value bytes, the sum of its ids' entry lengths, to dd[chunk].
 // Slots of a page past a walk error (pstat's value count) are left to k_dd_str (empty values).
-constexpr int DD_NONE = 0, DD_SUMS = 1;
+// DD_IDS (dictionary-direct columns whose dictionary is too large to stage, ColumnDev::dd_global): the
+// compact u16 ids only; the chunk sums come from k_dd_gsums, which gathers the entry lengths from HBM.
+constexpr int DD_NONE = 0, DD_SUMS = 1, DD_IDS = 2;
 constexpr uint32_t DD_ENT_MAX = 2048; // entries of a dictionary page of at most DD_DICT_MAX bytes (4-byte lengths)
 
 // Inclusive prefix sum over the wave (u32) with DPP row shifts / broadcasts; all 64 lanes active.
@@ -856,7 +858,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
     }
   }
   // DD_SUMS: the entry lengths
-  if constexpr (DD != DD_NONE) {
+  if constexpr (DD == DD_SUMS) {
     if (same && c0 >= 0) {
       const ColumnDev& cd0 = cols[c0];
       const uint32_t dn = uni(cd0.dict_n);
@@ -1051,7 +1053,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
               v[e] = value(cj, i, tab[cj]);
             }
           }
-          if constexpr (DD == DD_SUMS) {
+          if constexpr (DD != DD_NONE) {
             const bool whole = ts >= lo_u && ts + TV <= hi_u;
             uint8_t* ip = idpag + (uint64_t)(ts + E * lane) * cd.dict_direct;
             if (cd.dict_direct == 1u) {
@@ -1064,7 +1066,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
             for (uint32_t e = 0; e < E; e++) {
               const uint32_t sl = ts + E * lane + e;
               const bool in = sl >= lo_u && sl < hi_u;
-              dd_acc += in ? dd_entry((uint32_t)v[e]) : 0u;
+              if constexpr (DD == DD_SUMS) dd_acc += in ? dd_entry((uint32_t)v[e]) : 0u;
               if (in && !whole) {
                 if (cd.dict_direct == 1u) gst(ip + e, (uint8_t)v[e]);
                 else gst((uint16_t*)ip + e, (uint16_t)v[e]);
@@ -1098,7 +1100,7 @@ __device__ __forceinline__ void dict_tiles_body(const uint8_t* __restrict__ byte
       if (lane == 0) gst(dd + c, (uint64_t)dd_acc);
     }
   };
-  if (DD != DD_NONE && go && !(dict_in_lds && pw.column == c0)) {
+  if (DD == DD_SUMS && go && !(dict_in_lds && pw.column == c0)) {
     // (never with the plan's layout: whole workgroups per column, dictionaries within DD_DICT_MAX / 2,048
     // entries)
     if (lane == 0) report(err, err_count, cpage, 2, v_lo, PQG_ERR_INVALID_ARG);
@@ -1158,6 +1160,8 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_fused(const uint8_t* __restri
 //                    first byte; the total -> bin_total and offsets[n_slots]
 //   k_dd_str         per output chunk: the compact ids -> int64 offsets and the value bytes
 // (DictionaryValuesReader.readBytes, DictionaryValuesReader.java:75-82, per value: the id's entry)
+// DDM = DD_SUMS (dictionary staged in LDS) or DD_IDS (large dictionaries: ids only, k_dd_gsums sums)
+template <int DDM>
 __global__ __launch_bounds__(64 * WPB) void k_dict_fused_dd(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                             const PageWork* __restrict__ work,
                                                             const ColumnDev* __restrict__ cols,
@@ -1178,12 +1182,13 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_fused_dd(const uint8_t* __res
     dict_runs_body<4>(bytes, n_bytes, work, cols, list, n_list, rec, chunk_run, pstat, flags, epoch, err, err_count,
                       lds, blockIdx.x);
   } else {
-    dict_tiles_body<4, true, true, DD_SUMS>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, flags,
-                                            epoch, err, err_count, lds, blockIdx.x - n_walk, sums);
+    dict_tiles_body<4, true, true, DDM>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat, flags,
+                                        epoch, err, err_count, lds, blockIdx.x - n_walk, sums);
   }
 }
 
-// split mode (pqg_sync's re-run after a fused-kernel timeout): the DD_SUMS expansion after the walk
+// split mode (pqg_sync's re-run after a fused-kernel timeout): the DD_SUMS / DD_IDS expansion after the walk
+template <int DDM>
 __global__ __launch_bounds__(64 * WPB) void k_dict_tiles_dd(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                             const PageWork* __restrict__ work,
                                                             const ColumnDev* __restrict__ cols, const uint64_t* rec,
@@ -1192,8 +1197,8 @@ __global__ __launch_bounds__(64 * WPB) void k_dict_tiles_dd(const uint8_t* __res
                                                             const uint64_t* pstat, uint64_t* err, ErrCount err_count,
                                                             uint64_t* sums) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[XT_LDS_BYTES];
-  dict_tiles_body<4, false, true, DD_SUMS>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat,
-                                           nullptr, 0, err, err_count, lds, blockIdx.x, sums);
+  dict_tiles_body<4, false, true, DDM>(bytes, n_bytes, work, cols, rec, chunk_run, chunks, n_chunks, pstat,
+                                       nullptr, 0, err, err_count, lds, blockIdx.x, sums);
 }
 
 // One workgroup per dictionary-direct column: its chunks are sums[start[2i] .. start[2i + 1]) in page order.
@@ -1608,6 +1613,270 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_str(const uint8_t* __restrict__
           if (o[e] + q < cap) gst(dst + o[e] + q, dd_lds[sr[e] + q]);
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Dictionary-direct columns whose dictionary page is too large to stage in LDS (ColumnDev::dd_global: over
+// DD_DICT_MAX bytes or 2,048 entries, at most 65,536 entries): the walk's expansion stores the u16 ids only
+// (DD_IDS); the entries (PlainBinaryDictionary, PlainValuesDictionary.java:58-134: dict_len / dict_src from
+// the dictionary walk) and the value bytes are gathered from HBM — a dictionary of a few hundred KB stays
+// in L2 — by the two kernels below, with k_dd_bases between them. Ids past the dictionary and slots past a
+// walk error are empty values (the walk reports the error), as k_dd_str writes them.
+
+// Byte sum of every chunk: one wave per chunk, all its ids loaded first (two dwords per lane per tile),
+// then the walked slots' entry lengths, summed over the wave (no stores but the sum).
+__global__ __launch_bounds__(64 * WPB) void k_dd_gsums(const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                                     const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                     const uint64_t* pstat, uint64_t* sums) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  constexpr uint32_t E = 4, TV = WAVE * E, CH = CH_TILES * TV;
+  const uint32_t lane = lane_id();
+  const uint32_t c = blockIdx.x * WPB + wave_id();
+  if (c >= n_chunks) return;
+  const uint64_t ce = chunks[c];
+  if ((uint32_t)ce == 0xFFFFFFFFu) return;  // padding between columns (never summed)
+  const int page = (int)(uint32_t)ce;
+  const PageWork pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t j = (uint32_t)(ce >> 32);
+  const uint32_t dict_n = uni(cd.dict_n), NF = uni(pw.n_values);
+  const uint32_t nok = uni((uint32_t)(sld(pstat + page) >> 32));  // values before a walk error
+  const uint32_t sh = (uint32_t)(pw.out_offset % E);
+  const uint32_t s_lo = j * CH > sh ? j * CH : sh;
+  const uint32_t s_hi = (j + 1) * CH < NF + sh ? (j + 1) * CH : NF + sh;
+  const uint32_t ok_hi = (nok < NF ? nok : NF) + sh;
+  uint64_t acc = 0;
+  if (s_lo < s_hi) {
+    const uint16_t* idpag = (const uint16_t*)cd.blen + (pw.out_offset - sh);
+    u32x2 idr[CH_TILES];
+#pragma unroll
+    for (uint32_t t = 0; t < CH_TILES; t++) {
+      const uint32_t ts = j * CH + t * TV;
+      idr[t] = ts + E * lane < s_hi ? *(const __attribute__((address_space(1))) u32x2*)(idpag + ts + E * lane)
+                                     : u32x2{0u, 0u};
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < CH_TILES; t++) {
+      const uint32_t ts = j * CH + t * TV;
+#pragma unroll
+      for (uint32_t e = 0; e < E; e++) {
+        const uint32_t sl = ts + E * lane + e;
+        const uint32_t id = ((e < 2 ? idr[t].x : idr[t].y) >> (16u * (e & 1u))) & 0xFFFFu;
+        const bool ok = sl >= s_lo && sl < ok_hi && id < dict_n;
+        acc += ok ? cd.dict_len[ok ? id : 0u] : 0u;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += (uint64_t)__shfl_xor((long long)acc, o);
+  if (lane == 0) gst(sums + c, acc);
+}
+
+// Offsets and value bytes: one workgroup per 4,096-value chunk, wave w its tiles [4 w, 4 w + 4). The
+// wave's ids, then its values' entries (lane: 4 per tile), are loaded before the first store; per tile
+// a wave scan of the lengths gives the offsets (two 16-byte stores per lane), and the value bytes of
+// entries of at most 32 bytes go through LDS: each value's 32 source bytes (two 16-byte loads from the
+// dictionary page, the next tile's requested before this tile's stores) into a staging slot, then every
+// lane composes whole 16-byte output blocks from the slots (k_dd_str's block gather) and stores them
+// aligned, a tile's edge blocks byte-masked. A tile with a longer entry copies bytes one by one.
+constexpr uint32_t DDX_MD = 32;  // longest entry of the block path (= staging bytes per value)
+struct DdxLds {
+  uint8_t pre[16];                               // slack before the staging (the gather reads base - k)
+  uint32_t stg[WAVE * 4 * DDX_MD / 4 + 8];       // lane l's value e: 32 source bytes at 32 (64 e + l) (+ slack)
+  uint32_t vo[WAVE * 4];                         // tile-relative first output byte of value v
+  uint32_t ve[WAVE * 4];                         // staged source << 16 | length
+  uint16_t fv[(WAVE * 4 * DDX_MD) / 16 + 2];     // output block b: the value holding its first byte
+};
+__global__ __launch_bounds__(64 * WPB) void k_dd_gstr(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
+                                                    const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
+                                                    const uint64_t* __restrict__ chunks, uint32_t n_chunks,
+                                                    const uint64_t* pstat, const uint64_t* __restrict__ bases,
+                                                    uint64_t* err, ErrCount err_count) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+  constexpr uint32_t E = 4, TV = WAVE * E, CH = CH_TILES * TV, TPW = CH_TILES / WPB;
+  __shared__ __attribute__((aligned(16))) DdxLds lds_all[WPB];
+  __shared__ u32x4 dd_sel[16];  // (k_dd_str's selectors: block bytes k .. 15 from the source)
+  __shared__ uint32_t wsum[WPB];
+  if (threadIdx.x < 64u) {
+    const uint32_t k = threadIdx.x >> 2, d = threadIdx.x & 3u;
+    uint32_t sel = 0;
+#pragma unroll
+    for (uint32_t jb = 0; jb < 4; jb++) sel |= (4u * d + jb >= k ? 4u + jb : jb) << (8u * jb);
+    ((uint32_t*)dd_sel)[threadIdx.x] = sel;
+  }
+  __syncthreads();
+  const uint32_t lane = lane_id();
+  const uint32_t c = blockIdx.x;  // (the workgroup's waves share the chunk: uniform exits below)
+  if (c >= n_chunks) return;
+  const uint64_t ce = chunks[c];
+  if ((uint32_t)ce == 0xFFFFFFFFu) return;
+  const int page = (int)(uint32_t)ce;
+  const PageWork pw = work[page];
+  const ColumnDev& cd = cols[pw.column];
+  const uint32_t j = (uint32_t)(ce >> 32);
+  const uint32_t dict_n = uni(cd.dict_n), NF = uni(pw.n_values);
+  const uint32_t nok = uni((uint32_t)(sld(pstat + page) >> 32));
+  const uint32_t sh = (uint32_t)(pw.out_offset % E);
+  const uint32_t s_lo = j * CH > sh ? j * CH : sh;
+  const uint32_t s_hi = (j + 1) * CH < NF + sh ? (j + 1) * CH : NF + sh;
+  if (s_lo >= s_hi) return;
+  const uint32_t ok_hi = (nok < NF ? nok : NF) + sh;
+  const uint32_t T0 = wave_id() * TPW;
+  // ids, then entries (all loads before the first store)
+  const uint16_t* idpag = (const uint16_t*)cd.blen + (pw.out_offset - sh);
+  u32x2 idr[TPW];
+#pragma unroll
+  for (uint32_t t = 0; t < TPW; t++) {
+    const uint32_t ts = j * CH + (T0 + t) * TV;
+    idr[t] = ts + E * lane < s_hi ? *(const __attribute__((address_space(1))) u32x2*)(idpag + ts + E * lane)
+                                   : u32x2{0u, 0u};
+  }
+  uint32_t ln[TPW][E], sr[TPW][E], ws = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < TPW; t++) {
+    const uint32_t ts = j * CH + (T0 + t) * TV;
+#pragma unroll
+    for (uint32_t e = 0; e < E; e++) {
+      const uint32_t sl = ts + E * lane + e;
+      const uint32_t id = ((e < 2 ? idr[t].x : idr[t].y) >> (16u * (e & 1u))) & 0xFFFFu;
+      const bool ok = sl >= s_lo && sl < ok_hi && id < dict_n;
+      const uint64_t en = cd.dict_ent[ok ? id : 0u];  // (branch-free: see ld8_any)
+      ln[t][e] = ok ? (uint32_t)en : 0u;
+      sr[t][e] = ok ? (uint32_t)(en >> 32) : 0u;
+      ws += ln[t][e];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ws += (uint32_t)__shfl_xor((int)ws, o);
+  if (lane == 0) wsum[wave_id()] = ws;
+  __syncthreads();
+  uint64_t run_base = uni64(bases[c]);
+  for (uint32_t w = 0; w < wave_id(); w++) run_base += wsum[w];
+  run_base = uni64(run_base);
+  uint8_t* const dst = cd.binary_data;
+  const uint64_t cap = cd.binary_capacity;
+  int64_t* const opag = (int64_t*)cd.values + (pw.out_offset - sh);
+  const bool o16 = ((uintptr_t)cd.values & 15u) == 0, d16 = ((uintptr_t)dst & 15u) == 0;
+  // the dictionary page + the batch's readable slack after it: a load at DDX_OOB is out of range (no access)
+  const rsrc_t drs = make_rsrc(bytes + cd.dict_offset, cd.dict_bytes + 64u);
+  constexpr uint32_t DDX_OOB = 0x7FFFFFF0u;
+  const rsrc_t brs = make_rsrc(bytes + cd.dict_offset, n_bytes - cd.dict_offset);  // (long entries, byte by byte)
+  DdxLds& X = lds_all[wave_id()];
+  const uint8_t* const xb = (const uint8_t*)&X;  // staged source s is at xb + 16 + s
+  // the 32 source bytes of the lane's 4 values of tile t (entries over 32 bytes: the byte path)
+  u32x4 pb[E][2];
+  auto load_tile = [&](uint32_t t) {
+#pragma unroll
+    for (uint32_t e = 0; e < E; e++) {  // (out-of-range offsets for empty values / bytes 16.. of short ones)
+      pb[e][0] = __builtin_amdgcn_raw_buffer_load_b128(drs, (int)(ln[t][e] ? sr[t][e] : DDX_OOB), 0, 0);
+      pb[e][1] = __builtin_amdgcn_raw_buffer_load_b128(drs, (int)(ln[t][e] > 16u ? sr[t][e] + 16u : DDX_OOB), 0, 0);
+    }
+  };
+  load_tile(0);
+#pragma unroll
+  for (uint32_t t = 0; t < TPW; t++) {
+    const uint32_t ts = j * CH + (T0 + t) * TV;
+    if (ts >= s_hi) break;  // (uniform)
+    uint32_t ls = 0, mx = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < E; e++) {
+      ls += ln[t][e];
+      mx = ln[t][e] > mx ? ln[t][e] : mx;
+    }
+    const uint32_t inc = wave_incl_scan_u32_dpp(ls);
+    const uint32_t tot = uni(rdl(inc, WAVE - 1));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const uint32_t y = (uint32_t)__shfl_xor((int)mx, o);
+      mx = y > mx ? y : mx;
+    }
+    mx = uni(mx);
+    uint64_t o[E];
+    o[0] = run_base + (inc - ls);
+#pragma unroll
+    for (uint32_t e = 1; e < E; e++) o[e] = o[e - 1] + ln[t][e - 1];
+    const uint64_t tb = run_base;
+    run_base += tot;
+    const bool gather = mx <= DDX_MD && d16 && run_base <= cap;
+    const uint64_t tal = tb & ~15ull;
+    const uint32_t rb = (uint32_t)(tb - tal), re = rb + tot;
+    if (gather) {
+      wave_sync();  // the previous tile's gather reads are done
+#pragma unroll
+      for (uint32_t e = 0; e < E; e++) {
+        // slots 64 e + lane: consecutive lanes 32 bytes apart (slots 4 lane + e, 128 bytes apart, put a
+        // 16-byte write of every lane on two bank groups)
+        const uint32_t v = E * lane + e, slot = WAVE * e + lane;
+        *(u32x4*)&X.stg[8u * slot] = pb[e][0];
+        *(u32x4*)&X.stg[8u * slot + 4u] = pb[e][1];
+        X.vo[v] = rb + (uint32_t)(o[e] - tb);
+        X.ve[v] = ((DDX_MD * slot) << 16) | ln[t][e];
+      }
+#pragma unroll
+      for (uint32_t e = 0; e < E; e++) {
+        if (!ln[t][e]) continue;
+        // the blocks whose first byte (16 b, or rb for the tile's first block) this value holds
+        const uint32_t g = rb + (uint32_t)(o[e] - tb);
+        for (uint32_t b = g == rb ? (g >> 4) : ((g + 15u) >> 4); (b << 4) < g + ln[t][e]; b++)
+          X.fv[b] = (uint16_t)(E * lane + e);
+      }
+    }
+    // the next tile's source bytes, requested before this tile's stores
+    if (t + 1 < TPW) load_tile(t + 1);
+    int64_t* op = opag + ts + E * lane;
+    if (o16 && ts >= s_lo && ts + TV <= s_hi) {
+      gst_nt((i64x2*)op, i64x2{(int64_t)o[0], (int64_t)o[1]});
+      gst_nt((i64x2*)(op + 2), i64x2{(int64_t)o[2], (int64_t)o[3]});
+    } else {
+#pragma unroll
+      for (uint32_t e = 0; e < E; e++)
+        if (ts + E * lane + e >= s_lo && ts + E * lane + e < s_hi) gst(op + e, (int64_t)o[e]);
+    }
+    if (gather) {
+      wave_sync();
+      const uint32_t nblk = (re + 15u) >> 4;
+      for (uint32_t b = lane; b < nblk; b += WAVE) {
+        const uint32_t gb = b << 4;
+        const uint32_t bs = gb > rb ? gb : rb;
+        const uint32_t be = gb + 16u < re ? gb + 16u : re;
+        uint32_t v = X.fv[b];
+        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        uint32_t pos = bs;
+        while (pos < be) {
+          const uint32_t g = X.vo[v], ev = X.ve[v];
+          const uint32_t ge = g + (ev & 0xFFFFu);
+          if (pos < ge) {  // (empty values hold no byte)
+            const uint32_t n = (ge < be ? ge : be) - pos;
+            const uint32_t k = pos - gb;
+            const uint32_t base = 16u + (ev >> 16) + (pos - g) - k;
+            const uint32_t q = base & ~3u, r = base & 3u;
+            const uint32_t* w = (const uint32_t*)(xb + q);
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+            const u32x4 sl = dd_sel[k];
+            a0 = __builtin_amdgcn_perm(__builtin_amdgcn_alignbyte(w1, w0, r), a0, sl.x);
+            a1 = __builtin_amdgcn_perm(__builtin_amdgcn_alignbyte(w2, w1, r), a1, sl.y);
+            a2 = __builtin_amdgcn_perm(__builtin_amdgcn_alignbyte(w3, w2, r), a2, sl.z);
+            a3 = __builtin_amdgcn_perm(__builtin_amdgcn_alignbyte(w4, w3, r), a3, sl.w);
+            pos += n;
+          }
+          v++;
+        }
+        const uint32_t wd[4] = {a0, a1, a2, a3};
+        uint32_t have = 0;
+#pragma unroll
+        for (uint32_t d = 0; d < 4; d++) have |= (gb + 4u * d >= bs && gb + 4u * d + 4u <= be ? 1u : 0u) << d;
+        store_block16(dst, tal + gb, tal + bs, tal + be, wd, have, true);
+      }
+    } else {  // entries over 32 bytes, an unaligned value buffer, or past the capacity: the bytes that fit
+#pragma unroll
+      for (uint32_t e = 0; e < E; e++)
+        for (uint32_t q = 0; q < ln[t][e]; q++)
+          if (o[e] + q < cap) gst(dst + o[e] + q, (uint8_t)(ld32(brs, (sr[t][e] + q) & ~3u) >> (((sr[t][e] + q) & 3u) * 8u)));
+    }
+  }
+  (void)err;
+  (void)err_count;
 }
 
 // ---------------------------------------------------------------------------
@@ -3413,25 +3682,45 @@ hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes
                           const ColumnDev* cols, const int32_t* list, int n, uint64_t* rec, uint32_t* chunk_run,
                           const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
                           uint32_t epoch, bool fused, uint64_t* err, ErrCount err_count, uint64_t* sums,
-                          const int32_t* dd_cols, const int32_t* dd_start, int n_dd_cols, uint32_t dd_region) {
+                          const int32_t* dd_cols, const int32_t* dd_start, int n_dd_cols, uint32_t dd_region,
+                          bool global) {
   if (n <= 0) return hipSuccess;
   const uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
   const dim3 blk(64 * WPB);
   if (fused) {
-    hipLaunchKernelGGL(k_dict_fused_dd, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n, n_walk,
-                       rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count, sums);
+    if (global)
+      hipLaunchKernelGGL(k_dict_fused_dd<DD_IDS>, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n,
+                         n_walk, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count, sums);
+    else
+      hipLaunchKernelGGL(k_dict_fused_dd<DD_SUMS>, dim3(n_walk + n_tile), blk, 0, st, bytes, n_bytes, work, cols, list, n,
+                         n_walk, rec, chunk_run, chunks, n_chunks, pstat, flags, epoch, err, err_count, sums);
   } else {
     hipLaunchKernelGGL(k_dict_runs<4>, dim3(n_walk), blk, 0, st, bytes, n_bytes, work, cols, list, n, rec, chunk_run,
                        pstat, flags, epoch, err, err_count);
-    if (n_tile)
-      hipLaunchKernelGGL(k_dict_tiles_dd, dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run, chunks,
-                         n_chunks, pstat, err, err_count, sums);
+    if (n_tile) {
+      if (global)
+        hipLaunchKernelGGL(k_dict_tiles_dd<DD_IDS>, dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run,
+                           chunks, n_chunks, pstat, err, err_count, sums);
+      else
+        hipLaunchKernelGGL(k_dict_tiles_dd<DD_SUMS>, dim3(n_tile), blk, 0, st, bytes, n_bytes, work, cols, rec, chunk_run,
+                           chunks, n_chunks, pstat, err, err_count, sums);
+    }
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (global && n_tile) {  // the chunks' byte sums from the stored ids (entry lengths gathered from HBM)
+    hipLaunchKernelGGL(k_dd_gsums, dim3(n_tile), blk, 0, st, work, cols, chunks, n_chunks, pstat, sums);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(k_dd_bases, dim3(n_dd_cols), dim3(256), 0, st, work, cols, chunks, dd_cols, dd_start, sums);
   e = hipGetLastError();
   if (e != hipSuccess || !n_tile) return e;
+  if (global) {  // a workgroup per chunk
+    hipLaunchKernelGGL(k_dd_gstr, dim3(n_chunks), blk, 0, st, bytes, n_bytes, work, cols, chunks, n_chunks, pstat, sums,
+                       err, err_count);
+    return hipGetLastError();
+  }
   const uint32_t dd_lds_bytes = 16u + ((dd_region + 15u) & ~15u) + WPB * DDG_WAVE_BYTES;
   if (n_chunks <= DD_SPLIT_MAX_CHUNKS)  // few chunks: a workgroup per chunk
     hipLaunchKernelGGL(k_dd_str<CH_TILES / WPB>, dim3(n_chunks), blk, dd_lds_bytes, st, bytes, n_bytes, work, cols, chunks,

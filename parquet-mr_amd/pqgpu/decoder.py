@@ -316,6 +316,8 @@ class Decoder:
                 if pos + 4 > len(d):
                     break
                 n = int.from_bytes(d[pos:pos + 4], "little")
+                if pos + 4 + n > len(d):  # a corrupt entry (the decode reports it): no size from it
+                    break
                 longest = max(longest, n)
                 pos += 4 + n
             est = max(est, batch.column_slots[i] * longest + 64)

@@ -637,3 +637,104 @@ def test_dictionary_direct_optional_errors(decoder):
                   version=version, page_rows=3000)
         ch.dict_num_values = 4
         run_both(decoder, [ch], expect_error=True)
+
+
+@pytest.mark.parametrize("shape", ["16k", "3000_short", "2000_over_32k", "long_entries", "mixed_long", "65536"])
+def test_dictionary_direct_large(decoder, shape, dict_fused):
+    """Dictionaries past the LDS staging (over 2,048 entries or 32 KiB; at most 65,536 entries): u16 ids,
+    entries and value bytes gathered from HBM (k_dd_gsums / k_dd_gstr); entries over 32 bytes take the byte
+    path; equal to the oracle and to the ids -> map -> copy path."""
+    card, lo, hi, n = {"16k": (16384, 4, 32, 120_000), "3000_short": (3000, 0, 8, 60_000),
+                       "2000_over_32k": (2000, 20, 40, 60_000), "long_entries": (2500, 33, 90, 30_000),
+                       "mixed_long": (5000, 0, 48, 50_000), "65536": (65536, 1, 6, 200_000)}[shape]
+    words = _strings(card, seed=card, lo=lo, hi=hi)
+    rng = np.random.default_rng(card)
+    runs = np.minimum(rng.zipf(1.6, size=n), 300)
+    ids = np.repeat(rng.integers(0, card, size=runs.size), runs)[:n]
+    if shape == "65536":
+        ids[:card] = np.arange(card)  # every entry used: the dictionary holds all 65,536
+    vals = [words[i] for i in ids]
+    batch, ref, a = run_both(decoder, [make(abi.BYTE_ARRAY, vals, abi.RLE_DICTIONARY, page_rows=9000)])
+    decoder.set_dispatch(abi.DISPATCH_DICT_DIRECT, 0)
+    try:
+        _, _, b = run_both(decoder, [make(abi.BYTE_ARRAY, vals, abi.RLE_DICTIONARY, page_rows=9000)])
+    finally:
+        decoder.set_dispatch(abi.DISPATCH_DICT_DIRECT, 1)
+    assert np.array_equal(a[0].offsets().cpu().numpy(), b[0].offsets().cpu().numpy())
+
+
+@pytest.mark.parametrize("version", [1, 2])
+def test_dictionary_direct_large_optional(decoder, version):
+    """A nullable column with a 10,000-entry dictionary beside a small-dictionary one (both dictionary-direct
+    kinds in one plan), 15 % nulls."""
+    words = _strings(10_000, seed=12, lo=1, hi=28)
+    small = _lineitem_words()
+    dl = nulls(70_000, 0.15, seed=version)
+    n = int(dl.sum())
+    rng = np.random.default_rng(3)
+    run_both(decoder, [make(abi.BYTE_ARRAY, [words[i] for i in rng.integers(0, 10_000, size=n)], abi.RLE_DICTIONARY,
+                            def_levels=dl, max_def=1, version=version, page_rows=8000),
+                       make(abi.BYTE_ARRAY, [small[i] for i in rng.integers(0, len(small), size=40_000)],
+                            abi.RLE_DICTIONARY, page_rows=7000)])
+
+
+def test_dictionary_direct_large_error(decoder):
+    """An id past a large dictionary: the oracle's status."""
+    words = _strings(5000, seed=5, lo=2, hi=20)
+    ids = np.random.default_rng(9).integers(0, 5000, size=40_000)
+    ch = make(abi.BYTE_ARRAY, [words[i] for i in ids], abi.RLE_DICTIONARY, page_rows=6000)
+    ch.dict_num_values = 4000
+    run_both(decoder, [ch], expect_error=True)
+
+
+def test_dictionary_direct_large_short_buffer(decoder):
+    """A byte buffer shorter than the column (large dictionary): the size needed is reported and the bytes
+    below the capacity are the column's."""
+    words = _strings(4000, seed=6, lo=2, hi=31)
+    ids = np.random.default_rng(10).integers(0, 4000, size=50_000)
+    batch = writer.build_batch([make(abi.BYTE_ARRAY, [words[i] for i in ids], abi.RLE_DICTIONARY, page_rows=20000)])
+    ref = pqref.decode_batch(batch)
+    want = b"".join(ref.columns[0]["values"])
+    cols = decoder.alloc_columns(batch)
+    cap = len(want) // 2 + 3
+    import torch
+    cols[0].binary_data = torch.zeros(cap, dtype=torch.uint8, device=decoder.device)
+    rc, st, _ = decoder._decode_once(decoder.upload(batch), cols, None)
+    assert rc == abi.ERR_INVALID_ARG and int(st.value_index) >= len(want)
+    assert cols[0].binary_data.cpu().numpy().tobytes() == want[:cap]
+
+
+@pytest.mark.parametrize("case", ["ok", "cut", "neg_len", "long_len", "more_declared", "fewer_declared", "huge_entry",
+                                  "70k_entries"])
+def test_large_dictionary_page_walk(decoder, case):
+    """Dictionary pages of 16 KiB or more are walked per 2 KiB tile (k_dent_walk / k_dent_resolve /
+    k_dent_scatter): entries, the dictionary's error (PlainBinaryDictionary ctor) and the decoded values equal
+    the oracle's — truncated pages, a negative or oversized length in the middle, more or fewer entries
+    declared than the page holds, an entry longer than a tile, and a dictionary past 65,536 entries (ids ->
+    map -> copy path)."""
+    rng = np.random.default_rng(len(case))
+    card = 70_000 if case == "70k_entries" else 3000
+    words = _strings(card, seed=card, lo=0, hi=20)
+    if case == "huge_entry":
+        words[5] = bytes(rng.integers(65, 91, size=7000, dtype=np.uint8))
+    if case == "70k_entries":  # every entry used: 70,000 distinct values, past the u16 ids
+        ids = np.concatenate([np.arange(card), rng.integers(0, card, size=10_000)])
+    else:
+        ids = rng.integers(0, 2900, size=60_000)
+    ch = make(abi.BYTE_ARRAY, [words[i] for i in ids], abi.RLE_DICTIONARY, page_rows=9000)
+    d = bytearray(ch.dict_page)
+    if case == "cut":
+        ch.dict_page = bytes(d[: len(d) - 37])
+    elif case in ("neg_len", "long_len"):
+        p = 0
+        for _ in range(1500):  # the 1,500th entry's length prefix
+            p += 4 + int.from_bytes(d[p:p + 4], "little")
+        d[p:p + 4] = ((0x80000000 | 5) if case == "neg_len" else len(d) * 3).to_bytes(4, "little")
+        ch.dict_page = bytes(d)
+    elif case == "more_declared":
+        ch.dict_num_values += 2
+    elif case == "fewer_declared":
+        ch.dict_num_values -= 50  # the page's last entries are never read; ids past them are errors
+    batch = writer.build_batch([ch])
+    ref = pqref.decode_batch(batch)
+    run_both(decoder, [ch], expect_error=ref.code != 0)

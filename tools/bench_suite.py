@@ -214,6 +214,10 @@ def run(name, rows, steps, warmup, cpu_budget, check=True):
     compressed = any(p.codec for ch in chunks for p in ch.pages)
     t_gen = time.perf_counter() - t0
     dec = D.Decoder(0)
+    # A/B runs: PQGPU_DISPATCH="key=value,..." (abi.DISPATCH_* keys, e.g. 5=0: levels first for V2 columns)
+    for kv in filter(None, os.environ.get("PQGPU_DISPATCH", "").split(",")):
+        k, v = kv.split("=")
+        dec.set_dispatch(int(k), int(v))
     if compressed:  # SNAPPY / ZSTD: every timed step decompresses on the GPU, then decodes
         dbatch = dec.upload_chunks(chunks)
         batch = dbatch.batch

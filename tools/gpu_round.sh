@@ -89,7 +89,7 @@ PY
       for wl in ${SUITE:-str_plain c3_mixed}; do
         i=0
         mkdir -p "$OUT/strpmc/$wl"
-        for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" \
+        for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE" \
                    "SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM"; do
           timeout -s KILL 400 rocprofv3 --pmc $grp --output-format csv -d "$OUT/strpmc/$wl/pass$i" -o run -- \
             python3 tools/bench_suite.py $wl --steps 3 --warmup 1 --cpu-budget 0 > "$OUT/strpmc/$wl/pass$i.log" 2>&1 \
