@@ -252,6 +252,7 @@ def run_c4(args, world, rank, devi):
     dec = D.Decoder(devi, poison=0xA5)
     if args.dict_split:
         dec.set_dispatch(abi.DISPATCH_DICT_FUSED, 0)
+    _ab_dispatch(dec)
     if args.plain_mode is not None:
         dec.set_dispatch(abi.DISPATCH_PLAIN_ONE_PASS, args.plain_mode)
     dbatch = dec.upload(batch)
@@ -398,6 +399,13 @@ def run_c4(args, world, rank, devi):
         dist.destroy_process_group()
 
 
+def _ab_dispatch(dec):
+    """A/B runs only: PQGPU_DISPATCH="key=value,..." (abi.DISPATCH_* keys) overrides the measured defaults."""
+    for kv in filter(None, os.environ.get("PQGPU_DISPATCH", "").split(",")):
+        k, v = kv.split("=")
+        dec.set_dispatch(int(k), int(v))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -450,6 +458,7 @@ def main():
     if args.dict_split:
         from pqgpu import abi
         dec.set_dispatch(abi.DISPATCH_DICT_FUSED, 0)
+    _ab_dispatch(dec)
     dbatch = dec.upload(batch)
     cols = dec.alloc_columns(batch)  # poisoned: an element no launch writes cannot pass the check
     plan = dec.plan(dbatch, cols)

@@ -242,6 +242,10 @@ struct pqg_ctx {
   // stream only waits while they run (a queue shared with it costs nothing then).
   hipStream_t fix_stream = nullptr;
   hipEvent_t ev_join_fix = nullptr;
+  // ... and the tile walk of large dictionaries beside the id walk of their dictionary-direct pages, whose
+  // ids need no entries (C_DDG: the entries are first read by k_dd_gsums, which waits for ev_dent)
+  hipStream_t dent_stream = nullptr;
+  hipEvent_t ev_dent_fork = nullptr, ev_dent = nullptr;
   // pqg_ctx_set_dispatch: kernel-choice overrides for the plans created on this ctx
   int plain_mode = 2;       // PQG_DISPATCH_PLAIN_ONE_PASS
   bool dict_direct = true;  // PQG_DISPATCH_DICT_DIRECT
@@ -375,6 +379,12 @@ int pqg_ctx_destroy(pqg_ctx* c) {
     (void)hipStreamDestroy(c->fix_stream);
   }
   if (c->ev_join_fix) (void)hipEventDestroy(c->ev_join_fix);
+  if (c->dent_stream) {
+    (void)hipStreamSynchronize(c->dent_stream);
+    (void)hipStreamDestroy(c->dent_stream);
+  }
+  if (c->ev_dent_fork) (void)hipEventDestroy(c->ev_dent_fork);
+  if (c->ev_dent) (void)hipEventDestroy(c->ev_dent);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -1070,18 +1080,33 @@ int pqg_plan_launch(pqg_plan* P) {
   // them, on the caller's stream beside the forked value kernels (launched after the fork below)
   const bool hints = P->null_hints && P->levels_n;
   const int32_t* bl = (const int32_t*)P->bin_lists.p;
+  auto launch_dent = [&](hipStream_t st) -> hipError_t {  // large dictionaries' entries, per 2 KiB tile
+    uint8_t* scb = (uint8_t*)P->bscratch.p;
+    return pqg::launch_dict_entries(st, P->d_bytes, P->n_bytes, cols, (const uint64_t*)P->dent_tiles.p, P->n_dent_tiles,
+                                    bl + P->off_dent_cols, bl + P->off_dent_start, P->n_dent_cols,
+                                    (uint64_t*)(scb + P->dent_rec_off), (uint16_t*)(scb + P->dent_scr_off),
+                                    (uint64_t*)(scb + P->dent_tb_off), P->n_pages, err, ecount);
+  };
+  // every large dictionary's column dictionary-direct with HBM entries (C_DDG only): its tile walk runs
+  // on a queue of its own from the start, beside the levels and the id walk (k_dict_fused_dd<DD_IDS>)
+  bool dent_fork = false;
+  if (e == hipSuccess && P->n_dent_tiles && P->cls_n[C_DDG] && !P->cls_n[C_DD] && !P->cls_n[C_IDS] && !P->n_bind) {
+    dent_fork = (ctx->dent_stream || hipStreamCreateWithFlags(&ctx->dent_stream, hipStreamNonBlocking) == hipSuccess) &&
+                (ctx->ev_dent_fork || hipEventCreateWithFlags(&ctx->ev_dent_fork, hipEventDisableTiming) == hipSuccess) &&
+                (ctx->ev_dent || hipEventCreateWithFlags(&ctx->ev_dent, hipEventDisableTiming) == hipSuccess) &&
+                hipEventRecord(ctx->ev_dent_fork, s) == hipSuccess &&
+                hipStreamWaitEvent(ctx->dent_stream, ctx->ev_dent_fork, 0) == hipSuccess;
+    if (dent_fork) {
+      e = launch_dent(ctx->dent_stream);
+      if (e == hipSuccess && hipEventRecord(ctx->ev_dent, ctx->dent_stream) != hipSuccess) e = hipErrorUnknown;
+    }
+  }
   auto launch_dict_walks = [&](hipStream_t st) -> hipError_t {
     hipError_t r = hipSuccess;
     if (P->n_dict_walk)  // BYTE_ARRAY dictionary entries (PlainBinaryDictionary ctor)
       r = pqg::launch_bin_walk(st, P->d_bytes, P->n_bytes, work, cols, bl + P->off_dict_walk, P->n_dict_walk, 1,
                                P->n_pages, err, ecount);
-    if (r == hipSuccess && P->n_dent_tiles) {  // ... of the large dictionaries, per 2 KiB tile
-      uint8_t* scb = (uint8_t*)P->bscratch.p;
-      r = pqg::launch_dict_entries(st, P->d_bytes, P->n_bytes, cols, (const uint64_t*)P->dent_tiles.p, P->n_dent_tiles,
-                                   bl + P->off_dent_cols, bl + P->off_dent_start, P->n_dent_cols,
-                                   (uint64_t*)(scb + P->dent_rec_off), (uint16_t*)(scb + P->dent_scr_off),
-                                   (uint64_t*)(scb + P->dent_tb_off), P->n_pages, err, ecount);
-    }
+    if (r == hipSuccess && P->n_dent_tiles && !dent_fork) r = launch_dent(st);
     return r;
   };
   if (e == hipSuccess && P->levels_n && !hints) {
@@ -1159,7 +1184,8 @@ int pqg_plan_launch(pqg_plan* P) {
                                 (uint32_t*)P->chunk_run.p, (const uint64_t*)P->chunks.p + P->dd_chunk_off[g],
                                 P->dd_chunk_n[g], (uint64_t*)P->pstat.p, (uint32_t*)P->flags.p, P->epoch, P->dict_fused,
                                 err, ecount, (uint64_t*)((uint8_t*)P->bscratch.p + P->dd_sums_off[g]),
-                                bl + P->off_dd_cols[g], bl + P->off_dd_start[g], P->n_dd_cols[g], P->dd_region, g == 1);
+                                bl + P->off_dd_cols[g], bl + P->off_dd_start[g], P->n_dd_cols[g], P->dd_region, g == 1,
+                                g == 1 && dent_fork ? ctx->ev_dent : nullptr);
         break;
       }
       case C_BSS: e = pqg::launch_bss(sf, P->d_bytes, P->n_bytes, work, cols, l, n, err, ecount); break;

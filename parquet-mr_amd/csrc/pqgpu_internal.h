@@ -129,7 +129,7 @@ hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes
                           const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
                           uint32_t epoch, bool fused, uint64_t* err, ErrCount err_count, uint64_t* sums,
                           const int32_t* dd_cols, const int32_t* dd_start, int n_dd_cols, uint32_t dd_region,
-                          bool global);
+                          bool global, hipEvent_t entries_ready = nullptr);
 // DELTA_LENGTH_BYTE_ARRAY lengths (k_delta into blen, records PageWork::aux)
 hipError_t launch_dlba_lengths(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work,
                                const ColumnDev* cols, const int32_t* list, int n, uint64_t* err, ErrCount err_count);

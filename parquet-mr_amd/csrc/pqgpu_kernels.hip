@@ -3683,7 +3683,7 @@ hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes
                           const uint64_t* chunks, uint32_t n_chunks, uint64_t* pstat, uint32_t* flags,
                           uint32_t epoch, bool fused, uint64_t* err, ErrCount err_count, uint64_t* sums,
                           const int32_t* dd_cols, const int32_t* dd_start, int n_dd_cols, uint32_t dd_region,
-                          bool global) {
+                          bool global, hipEvent_t entries_ready) {
   if (n <= 0) return hipSuccess;
   const uint32_t n_walk = (uint32_t)(n + WPB - 1) / WPB, n_tile = (n_chunks + WPB - 1) / WPB;
   const dim3 blk(64 * WPB);
@@ -3708,6 +3708,8 @@ hipError_t launch_dict_dd(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  // (the entries, walked on another queue: the ids above never read them)
+  if (entries_ready && hipStreamWaitEvent(st, entries_ready, 0) != hipSuccess) return hipErrorUnknown;
   if (global && n_tile) {  // the chunks' byte sums from the stored ids (entry lengths gathered from HBM)
     hipLaunchKernelGGL(k_dd_gsums, dim3(n_tile), blk, 0, st, work, cols, chunks, n_chunks, pstat, sums);
     e = hipGetLastError();

@@ -82,6 +82,31 @@ def test_dict_multiple_columns_interleaved(decoder):
         assert_same(dcols[i].numpy(), ref.columns[i]["values"], batch.columns[i]["physical_type"])
 
 
+@pytest.mark.parametrize("case", ["multi", "many_pages", "id_error", "tiny"])
+def test_dict_columns_of_both_widths(decoder, case):
+    """Several fused dictionary columns of both widths in one launch, a column of fewer chunks than an
+    expansion workgroup, and a dictionary-id error beside a truncated page: values and first error as the
+    oracle's."""
+    if case == "tiny":
+        chunks = [make(abi.INT32, zipf_dict_column(37, card=5, a=1.5, seed=1, physical_type=abi.INT32),
+                       abi.RLE_DICTIONARY, page_rows=10)]
+    elif case == "many_pages":
+        chunks = [make(abi.INT64, zipf_dict_column(300_000, card=900, a=1.2, seed=2), abi.RLE_DICTIONARY,
+                       page_rows=1500)]
+    else:
+        chunks = []
+        for k in range(5):
+            pt = abi.INT64 if k % 2 == 0 else abi.INT32
+            v = zipf_dict_column(40_000 + 9_000 * k, card=3 + k * 300, a=1.4 + 0.3 * k, seed=10 + k, physical_type=pt)
+            chunks.append(make(pt, v, abi.RLE_DICTIONARY, page_rows=3000 + 1000 * k))
+    if case == "id_error":
+        chunks[3].dict_num_values = 600  # ids >= 600 of column 3 out of range; truncated page in column 1
+        chunks[1].pages[5].body = chunks[1].pages[5].body[:-7]
+        run_both(decoder, chunks, expect_error=True)
+    else:
+        run_both(decoder, chunks)
+
+
 def test_dict_known_answer_pages(decoder):
     """TestDictionary.testLongDictionary (:285-317): 1000 x (i % 50), then 2000 descending."""
     v1 = np.arange(1000, dtype=np.int64) % 50
