@@ -1680,12 +1680,13 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_gsums(const PageWork* __restric
 // lane composes whole 16-byte output blocks from the slots (k_dd_str's block gather) and stores them
 // aligned, a tile's edge blocks byte-masked. A tile with a longer entry copies bytes one by one.
 constexpr uint32_t DDX_MD = 32;  // longest entry of the block path (= staging bytes per value)
+// (16-bit offsets and 8-bit block owners: 39.4 KB per workgroup, 4 workgroups per CU instead of 3)
 struct DdxLds {
   uint8_t pre[16];                               // slack before the staging (the gather reads base - k)
   uint32_t stg[WAVE * 4 * DDX_MD / 4 + 8];       // lane l's value e: 32 source bytes at 32 (64 e + l) (+ slack)
-  uint32_t vo[WAVE * 4];                         // tile-relative first output byte of value v
-  uint32_t ve[WAVE * 4];                         // staged source << 16 | length
-  uint16_t fv[(WAVE * 4 * DDX_MD) / 16 + 2];     // output block b: the value holding its first byte
+  uint16_t vo[WAVE * 4];                         // tile-relative first output byte of value v (< 8,208)
+  uint16_t ve[WAVE * 4];                         // staging slot << 6 | length (<= 32)
+  uint8_t fv[(WAVE * 4 * DDX_MD) / 16 + 2];      // output block b: the value (< 256) holding its first byte
 };
 __global__ __launch_bounds__(64 * WPB) void k_dd_gstr(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                                     const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
@@ -1810,8 +1811,8 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_gstr(const uint8_t* __restrict_
         const uint32_t v = E * lane + e, slot = WAVE * e + lane;
         *(u32x4*)&X.stg[8u * slot] = pb[e][0];
         *(u32x4*)&X.stg[8u * slot + 4u] = pb[e][1];
-        X.vo[v] = rb + (uint32_t)(o[e] - tb);
-        X.ve[v] = ((DDX_MD * slot) << 16) | ln[t][e];
+        X.vo[v] = (uint16_t)(rb + (uint32_t)(o[e] - tb));
+        X.ve[v] = (uint16_t)((slot << 6) | ln[t][e]);
       }
 #pragma unroll
       for (uint32_t e = 0; e < E; e++) {
@@ -1819,7 +1820,7 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_gstr(const uint8_t* __restrict_
         // the blocks whose first byte (16 b, or rb for the tile's first block) this value holds
         const uint32_t g = rb + (uint32_t)(o[e] - tb);
         for (uint32_t b = g == rb ? (g >> 4) : ((g + 15u) >> 4); (b << 4) < g + ln[t][e]; b++)
-          X.fv[b] = (uint16_t)(E * lane + e);
+          X.fv[b] = (uint8_t)(E * lane + e);
       }
     }
     // the next tile's source bytes, requested before this tile's stores
@@ -1845,11 +1846,11 @@ __global__ __launch_bounds__(64 * WPB) void k_dd_gstr(const uint8_t* __restrict_
         uint32_t pos = bs;
         while (pos < be) {
           const uint32_t g = X.vo[v], ev = X.ve[v];
-          const uint32_t ge = g + (ev & 0xFFFFu);
+          const uint32_t ge = g + (ev & 63u);
           if (pos < ge) {  // (empty values hold no byte)
             const uint32_t n = (ge < be ? ge : be) - pos;
             const uint32_t k = pos - gb;
-            const uint32_t base = 16u + (ev >> 16) + (pos - g) - k;
+            const uint32_t base = 16u + DDX_MD * (ev >> 6) + (pos - g) - k;
             const uint32_t q = base & ~3u, r = base & 3u;
             const uint32_t* w = (const uint32_t*)(xb + q);
             const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
