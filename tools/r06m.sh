@@ -1,0 +1,12 @@
+set -e
+O=gpurun_out/r06m; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 1100 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+for L in parquet-mr_amd/pqgpu/libpqgpu.so abx/libprev.so parquet-mr_amd/pqgpu/libpqgpu.so abx/libprev.so; do
+  PQGPU_LIB=$PWD/$L timeout -k 10 600 python3 tools/bench_suite.py str_dict_opt str_dict str_dict_16k --cpu-budget 0 > $O/s.jsonl 2> $O/s.err || { tail -20 $O/s.err; exit 1; }
+  python3 -c "
+import json
+for l in open('$O/s.jsonl'):
+    d=json.loads(l); print('$L', d['workload'], round(d['ms_per_launch'],4), round(d.get('hbm_frac', 0) or 0, 3))"
+done
