@@ -3203,8 +3203,9 @@ __device__ int delta_generic(DSeg& S, uint32_t p, uint32_t end, uint32_t block, 
 struct DeltaHdr {
   uint32_t len, wpos, dpos, next, used, dbytes;
 };
-__device__ __forceinline__ bool delta_hdr_v(const DSeg& S, uint32_t p, uint32_t end, uint32_t mbn, uint32_t mbs,
-                                            uint32_t buffered, uint32_t total, DeltaHdr& h) {
+// (per lane: p need not be uniform; `used` miniblocks are read)
+__device__ __forceinline__ bool delta_hdr_parse(const DSeg& S, uint32_t p, uint32_t end, uint32_t mbn, uint32_t mbs,
+                                                uint32_t used, DeltaHdr& h) {
   const uint32_t a = p & ~3u, sb = p & 3u;
   if (!S.has(a, 20)) return false;
   uint32_t d[5];
@@ -3225,9 +3226,6 @@ __device__ __forceinline__ bool delta_hdr_v(const DSeg& S, uint32_t p, uint32_t 
   const uint32_t xb = q == 0 ? x[1] : (q == 1 ? x[2] : x[3]);
   const uint32_t xc = q == 0 ? x[2] : x[3];
   uint32_t wl = __builtin_amdgcn_alignbyte(xb, xa, r), wh = __builtin_amdgcn_alignbyte(xc, xb, r);
-  // miniblocks unpacked while buffered < total (:131-135)
-  const uint32_t rem = total - buffered;  // > 0
-  const uint32_t used = rem >= mbn * mbs ? mbn : (rem + mbs - 1u) / mbs;  // a page's last block only
   wl &= used >= 4u ? 0xFFFFFFFFu : (1u << (8u * used)) - 1u;
   wh &= used <= 4u ? 0u : (used == 8u ? 0xFFFFFFFFu : (1u << (8u * (used - 4u))) - 1u);
   // a used width > 64 (bit 7 set, or low 7 bits >= 65): the scalar walk reports CORRUPT
@@ -3236,7 +3234,14 @@ __device__ __forceinline__ bool delta_hdr_v(const DSeg& S, uint32_t p, uint32_t 
   h.dbytes = (__builtin_amdgcn_sad_u8(wl, 0u, 0u) + __builtin_amdgcn_sad_u8(wh, 0u, 0u)) * (mbs / 8u);
   h.dpos = h.wpos + mbn;
   h.next = h.dpos + h.dbytes;
-  const bool ok = len <= 8u && !bad && (uint64_t)h.dpos + h.dbytes <= end;  // (implies p + len, wpos + mbn <= end)
+  return len <= 8u && !bad && (uint64_t)h.dpos + h.dbytes <= end;  // (implies p + len, wpos + mbn <= end)
+}
+__device__ __forceinline__ bool delta_hdr_v(const DSeg& S, uint32_t p, uint32_t end, uint32_t mbn, uint32_t mbs,
+                                            uint32_t buffered, uint32_t total, DeltaHdr& h) {
+  // miniblocks unpacked while buffered < total (:131-135)
+  const uint32_t rem = total - buffered;  // > 0
+  const uint32_t used = rem >= mbn * mbs ? mbn : (rem + mbs - 1u) / mbs;  // a page's last block only
+  const bool ok = delta_hdr_parse(S, p, end, mbn, mbs, used, h);
   return uni(ok ? 1u : 0u) != 0u;
 }
 
@@ -3323,6 +3328,61 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     uint32_t b_data = 0, b_wpos = 0, b_lo = 0, b_hi = 0, b_nmb = 0, b_mv = 0;
     uint32_t nb = 0;
     const uint32_t blk_first = buffered;
+    // Fast chain over the batch's full blocks (every miniblock read): on the serial path only what the
+    // next header's position needs — the min delta varint's length (stop-bit mask), the width bytes' sum —
+    // while lane b keeps block b's header position; then every check of delta_hdr_v and the staged-data
+    // test, one lane per block, all at once. The batch is cut at the first block that fails them (its
+    // successor, computed from a bad header, is never used): the loop below takes that block (slow
+    // header, error, refill) and the page's last, partial block.
+    {
+      const uint32_t full = mbn * mbs;                   // values of a full block (<= 512)
+      const uint32_t nfull = uni((total - buffered) / full);
+      const uint32_t lim = nfull < 64u ? nfull : 64u;
+      const uint32_t mb8 = mbs / 8u;
+      const uint32_t wml = mbn >= 4u ? 0xFFFFFFFFu : (1u << (8u * mbn)) - 1u;
+      const uint32_t wmh = mbn <= 4u ? 0u : (mbn == 8u ? 0xFFFFFFFFu : (1u << (8u * (mbn - 4u))) - 1u);
+      uint32_t pc = p, b_p = 0, n_c = 0;
+      while (n_c < lim && S.has(pc, HDR_SPAN)) {
+        const uint32_t a = pc & ~3u, sb = pc & 3u;
+        uint32_t d[5];
+#pragma unroll
+        for (int i = 0; i < 5; i++) d[i] = S.w32(a + 4u * i);
+        uint32_t x[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) x[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sb);
+        const uint64_t lo = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+        const uint64_t stop = ~lo & 0x8080808080808080ull;
+        const uint32_t len = stop ? ((uint32_t)__builtin_ctzll(stop) >> 3) + 1u : 9u;
+        const uint32_t q = len >> 2, r = len & 3u;
+        const uint32_t xa = q == 0 ? x[0] : (q == 1 ? x[1] : x[2]);
+        const uint32_t xb = q == 0 ? x[1] : (q == 1 ? x[2] : x[3]);
+        const uint32_t xc = q == 0 ? x[2] : x[3];
+        const uint32_t wl = __builtin_amdgcn_alignbyte(xb, xa, r) & wml, wh = __builtin_amdgcn_alignbyte(xc, xb, r) & wmh;
+        b_p = lane == n_c ? pc : b_p;
+        pc = uni(pc + len + mbn + (__builtin_amdgcn_sad_u8(wl, 0u, 0u) + __builtin_amdgcn_sad_u8(wh, 0u, 0u)) * mb8);
+        n_c = uni(n_c + 1u);
+      }
+      if (n_c) {
+        DeltaHdr h{};
+        bool ok = false;
+        if (lane < n_c)
+          ok = delta_hdr_parse(S, b_p, end, mbn, mbs, mbn, h) && S.has(h.dpos, h.dbytes + 12u);
+        const uint64_t badm = __ballot(lane < n_c && !ok);
+        const uint32_t nk = uni(badm ? (uint32_t)__builtin_ctzll(badm) : n_c);  // blocks kept
+        const bool keep = lane < nk;
+        b_data = keep ? h.dpos : 0u;
+        b_wpos = keep ? h.wpos : 0u;
+        b_lo = keep ? b_p : 0u;  // header position and varint length: the min delta follows below
+        b_hi = keep ? h.len : 0u;
+        b_mv = keep ? 1u : 0u;
+        b_nmb = keep ? mbn : 0u;
+        if (nk) {
+          p = uni(rdl(h.next, nk - 1u));
+          buffered = uni(buffered + nk * full);
+        }
+        nb = nk;
+      }
+    }
     while (true) {
       nb = uni(nb);
       p = uni(p);
