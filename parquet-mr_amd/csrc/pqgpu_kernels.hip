@@ -2943,13 +2943,13 @@ __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_
 
 // Segment expansion of nb walked blocks whose miniblocks hold a multiple of 16 deltas (parquet-mr
 // and Arrow write 128 / 4, i.e. 32 per miniblock): lane l of a step takes segment g = 64 * step + l
-// of the batch — 16 consecutive deltas of one miniblock of block g / (block / 16) — unpacks them
+// of the batch — L = 8 consecutive deltas of one miniblock of block g / (block / L) — unpacks them
 // from the LDS segment at its own bit position, keeps their running sums in registers, and one
-// 64-bit DPP scan of the 64 segment sums gives every segment its base: 1,024 deltas per scan and
+// 64-bit DPP scan of the 64 segment sums gives every segment its base: 512 deltas per scan and
 // per carry step instead of one block (delta_expand: 64 * E). Values, the minDelta addition
 // (loadNewBlockToBuffer :139-142, also for the unread miniblocks of a last block, whose values lie
 // past the count and are not stored) and the store layout are those of delta_expand: lane l stores
-// the 16 values ending one delta earlier (the first from lane l - 1 / the carry), as wide stores
+// the L values ending one delta earlier (the first from lane l - 1 / the carry), as wide stores
 // when the run is aligned. Not for NEG streams (DELTA_LENGTH lengths check every value).
 template <int W>
 __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uint32_t b_data, uint32_t b_wpos,
@@ -2957,15 +2957,18 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
                                                  uint32_t block, uint32_t mbs, uint32_t n_out, uint64_t& carry,
                                                  typename DictVal<W>::T* out) {
   typedef typename DictVal<W>::T T;
-  constexpr uint32_t L = 16;
+  // 8 deltas per lane-step (16 measured slower: its 115 VGPRs left 4 waves per SIMD, and 5,000 pages of
+  // delta_i64 took 1.2 rounds of them; at 98 VGPRs the LDS segments' 5 waves per SIMD hold every page at
+  // once: delta_i64 0.370 -> 0.336 ms, C3 6.68 -> 6.61 ms, C4 10.26 -> 10.12 ms, profiles/r06/delta_l8)
+  constexpr uint32_t L = 8;
   const uint32_t lane = lane_id();
   const uint32_t SB = block / L;  // segments per block
   const uint32_t n_seg = nb * SB;
   const uint32_t mb_bytes = mbs / 8u;  // bytes per bit of width
-  // Runs are stored shifted by `sft` values so that every lane's 16 stored values start 16-byte
+  // Runs are stored shifted by `sft` values so that every lane's L stored values start 16-byte
   // aligned whatever the page's output offset (pages of nullable columns start at any value): lane l
-  // stores values [k0 + sft, k0 + sft + 16), the last sft of them the first values of lane l + 1's
-  // run (its u[1], u[2]: one shuffle each; u[16] is the lane's own last value). The batch's last lane
+  // stores values [k0 + sft, k0 + sft + L), the last sft of them the first values of lane l + 1's
+  // run (its u[1], u[2]: one shuffle each; u[L] is the lane's own last value). The batch's last lane
   // stores only its own values, lane 0 also the sft values before its wide run.
   constexpr uint32_t VPC = 16u / sizeof(T);  // values per 16 bytes
   const uint32_t mis = (uint32_t)((((uintptr_t)out + (uint64_t)(blk_first - 1) * sizeof(T)) % 16u) / sizeof(T));
@@ -3055,7 +3058,7 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
       for (uint32_t q = 0; q < L + 1; q++) u[q] = (T)(q == 0 ? prev : base_v + loc[q - 1]);
     }
     const uint64_t k0 = (uint64_t)blk_first - 1u + (uint64_t)bb * block + j0;  // index of the run's first value
-    // values 17, 18 of the lane's window: lane l + 1's u[1], u[2] (only for 4-byte values: sft <= 3)
+    // values L + 1, L + 2 of the lane's window: lane l + 1's u[1], u[2] (only for 4-byte values: sft <= 3)
     if constexpr (VPC > 2) {
       u[L + 1] = (T)(uint32_t)__shfl_down((int)(uint32_t)u[1], 1);
       u[L + 2] = (T)(uint32_t)__shfl_down((int)(uint32_t)u[2], 1);
