@@ -2951,6 +2951,19 @@ __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_
 // past the count and are not stored) and the store layout are those of delta_expand: lane l stores
 // the L values ending one delta earlier (the first from lane l - 1 / the carry), as wide stores
 // when the run is aligned. Not for NEG streams (DELTA_LENGTH lengths check every value).
+// In-place inclusive prefix of a lane's deltas in two independent halves joined at the end (half the
+// dependent adds of one running sum).
+template <class U, uint32_t N>
+__device__ __forceinline__ void delta_local_prefix(U (&v)[N]) {
+  constexpr uint32_t H = N / 2;
+#pragma unroll
+  for (uint32_t q = 1; q < H; q++) v[q] += v[q - 1];
+#pragma unroll
+  for (uint32_t q = H + 1; q < N; q++) v[q] += v[q - 1];
+#pragma unroll
+  for (uint32_t q = H; q < N; q++) v[q] += v[H - 1];
+}
+
 template <int W>
 __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uint32_t b_data, uint32_t b_wpos,
                                                  uint32_t b_lo, uint32_t b_hi, uint32_t b_nmb, uint32_t blk_first,
@@ -3012,17 +3025,16 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
           const uint32_t a = abase + ((ab >> 5) << 2);
           d = __builtin_amdgcn_alignbit(S.w32(a + 4), S.w32(a), ab & 31u) & mask;
         }
-        sum += lane_in ? d + mind32 : 0u;
-        loc[q] = sum;
+        loc[q] = lane_in ? d + mind32 : 0u;
         ab += wl;
       }
+      delta_local_prefix(loc);
+      sum = loc[L - 1];
       const uint32_t x32 = wave_incl_scan_u32_dpp(sum);
+      // the value before the lane's first delta: the carry plus every earlier lane's sum (= lane l - 1's last)
       const uint32_t base_v = (uint32_t)carry + (x32 - sum);
-      // (the shuffle outside the select: a lane left out of it would hand its neighbour a 0)
-      const uint32_t up = (uint32_t)__shfl_up((int)(base_v + loc[L - 1]), 1);
-      const uint32_t prev = lane == 0 ? (uint32_t)carry : up;
 #pragma unroll
-      for (uint32_t q = 0; q < L + 1; q++) u[q] = (T)(q == 0 ? prev : base_v + loc[q - 1]);
+      for (uint32_t q = 0; q < L + 1; q++) u[q] = (T)(q == 0 ? base_v : base_v + loc[q - 1]);
       x = x32;
     } else {
       const uint64_t mask = wl == 64 ? ~0ull : ((1ull << wl) - 1ull);
@@ -3045,17 +3057,16 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
             d = (sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)))) & mask;
           }
         }
-        sum += lane_in ? d + mind : 0ull;
-        loc[q] = sum;
+        loc[q] = lane_in ? d + mind : 0ull;
         bit += wl;
       }
+      delta_local_prefix(loc);
+      sum = loc[L - 1];
       x = wave_incl_scan_u64(sum);
+      // the value before the lane's first delta: the carry plus every earlier lane's sum (= lane l - 1's last)
       const uint64_t base_v = carry + (x - sum);
-      const uint64_t last = base_v + loc[L - 1];
-      const uint32_t plo = (uint32_t)__shfl_up((int)(uint32_t)last, 1), phi = (uint32_t)__shfl_up((int)(uint32_t)(last >> 32), 1);
-      const uint64_t prev = lane == 0 ? carry : (((uint64_t)phi << 32) | plo);
 #pragma unroll
-      for (uint32_t q = 0; q < L + 1; q++) u[q] = (T)(q == 0 ? prev : base_v + loc[q - 1]);
+      for (uint32_t q = 0; q < L + 1; q++) u[q] = (T)(q == 0 ? base_v : base_v + loc[q - 1]);
     }
     const uint64_t k0 = (uint64_t)blk_first - 1u + (uint64_t)bb * block + j0;  // index of the run's first value
     // values L + 1, L + 2 of the lane's window: lane l + 1's u[1], u[2] (only for 4-byte values: sft <= 3)
