@@ -3017,16 +3017,21 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
       // bit position relative to the dword holding the miniblock data's first byte (a page-absolute
       // bit position would wrap for data 512 MiB or more into a page)
       const uint32_t abase = dbase & ~3u;
-      uint32_t ab = (dbase & 3u) * 8u + jm * wl;
+      const uint32_t ab0 = (dbase & 3u) * 8u + jm * wl;
+      // every dword pair is read unconditionally (a zero width reads the miniblock's first dword, inside
+      // the staged segment, and masks it to 0): a branch per delta put an LDS round trip and its wait
+      // between the deltas, 8 serial trips per step instead of one
+      uint32_t x0[L], x1[L];
 #pragma unroll
       for (uint32_t q = 0; q < L; q++) {
-        uint32_t d = 0;
-        if (wl) {
-          const uint32_t a = abase + ((ab >> 5) << 2);
-          d = __builtin_amdgcn_alignbit(S.w32(a + 4), S.w32(a), ab & 31u) & mask;
-        }
+        const uint32_t a = abase + (((ab0 + q * wl) >> 5) << 2);
+        x0[q] = S.w32(a);
+        x1[q] = S.w32(a + 4);
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < L; q++) {
+        const uint32_t d = __builtin_amdgcn_alignbit(x1[q], x0[q], (ab0 + q * wl) & 31u) & mask;
         loc[q] = lane_in ? d + mind32 : 0u;
-        ab += wl;
       }
       delta_local_prefix(loc);
       sum = loc[L - 1];
@@ -3041,25 +3046,30 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
       const bool narrow = !__ballot(lane_in && wl > 32u);  // every width <= 32: two dwords per delta
       uint64_t loc[L];
       uint64_t sum = 0;
-      uint32_t bit = jm * wl;
+      // all reads of the step first, no branch per delta (see the 4-byte path): a zero width reads the
+      // miniblock's first dwords and masks them to 0
+      const uint32_t bit0 = (dbase & 3u) * 8u + jm * wl;  // relative to the dword holding dbase
+      const uint32_t abase = dbase & ~3u;
+      uint32_t x0[L], x1[L], x2[L];
+      auto unpack = [&](auto wide_tag) {
+        constexpr bool WIDE = decltype(wide_tag)::value;
 #pragma unroll
-      for (uint32_t q = 0; q < L; q++) {
-        uint64_t d = 0;
-        if (wl) {
-          const uint32_t byte = dbase + (bit >> 3);
-          const uint32_t a = byte & ~3u;
-          const uint32_t sh = (byte - a) * 8u + (bit & 7u);  // < 32
-          const uint64_t lo64 = (uint64_t)S.w32(a) | ((uint64_t)S.w32(a + 4) << 32);
-          if (narrow) {
-            d = (lo64 >> sh) & mask;
-          } else {
-            const uint32_t x2 = S.w32(a + 8);
-            d = (sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2 << (64u - sh)))) & mask;
-          }
+        for (uint32_t q = 0; q < L; q++) {
+          const uint32_t a = abase + (((bit0 + q * wl) >> 5) << 2);
+          x0[q] = S.w32(a);
+          x1[q] = S.w32(a + 4);
+          if (WIDE) x2[q] = S.w32(a + 8);
         }
-        loc[q] = lane_in ? d + mind : 0ull;
-        bit += wl;
-      }
+#pragma unroll
+        for (uint32_t q = 0; q < L; q++) {
+          const uint32_t sh = (bit0 + q * wl) & 31u;
+          const uint64_t lo64 = (uint64_t)x0[q] | ((uint64_t)x1[q] << 32);
+          const uint64_t d = (WIDE ? (sh == 0 ? lo64 : ((lo64 >> sh) | ((uint64_t)x2[q] << (64u - sh)))) : (lo64 >> sh)) & mask;
+          loc[q] = lane_in ? d + mind : 0ull;
+        }
+      };
+      if (narrow) unpack(std::false_type{});
+      else unpack(std::true_type{});
       delta_local_prefix(loc);
       sum = loc[L - 1];
       x = wave_incl_scan_u64(sum);
@@ -3075,6 +3085,72 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
       u[L + 2] = (T)(uint32_t)__shfl_down((int)(uint32_t)u[2], 1);
     } else {
       u[L + 1] = u[L + 2] = 0;
+    }
+    // A full step (64 lanes, its 16-byte rows inside the output): the rows are exchanged between lanes so
+    // that every store instruction writes 1 KiB contiguous. Lane-contiguous runs (each lane 64 bytes, four
+    // 16-byte stores 64 bytes apart) store at ~3.6 TB/s (profiles/r02/store_patterns.txt 'lane-contig');
+    // the same step with 1 KiB per instruction took delta_i64 0.335 -> 0.245 ms (profiles/r06/delta_tstore).
+    // Row r of the step holds values [K + sft + VPC r, + VPC); lane l's run is rows NR l .. NR l + NR - 1;
+    // instruction i of lane m stores row 64 i + m. Round a of NR: lane m (r = m % NR) fetches for
+    // instruction (a + r) % NR from lane (64 / NR) * ((a + r) % NR) + m / NR, which offers its row
+    // (c - a) % NR (c = its lane / (64 / NR)): every source is read by one lane per round (ds_bpermute).
+    const uint64_t K = (uint64_t)blk_first - 1u + (uint64_t)L * g0;  // value index of lane 0's u[0]
+    if (wide && g0 + WAVE <= n_seg && K + sft + (uint64_t)WAVE * L <= n_out) {
+      if (lane == 0)  // the sft values before the first row
+        for (uint32_t q = 0; q < VPC - 1u; q++)
+          if (q < sft) gst(out + K + q, u[q]);
+      auto tput = [&](auto s_tag) {
+        constexpr uint32_t SF = decltype(s_tag)::value;
+        constexpr uint32_t NR = L / VPC;  // rows per lane (4 for 8-byte values, 2 for 4-byte)
+        u32x4 row[NR];
+#pragma unroll
+        for (uint32_t j = 0; j < NR; j++) {
+          T v[VPC];
+#pragma unroll
+          for (uint32_t q = 0; q < VPC; q++) v[q] = u[SF + VPC * j + q];
+          __builtin_memcpy(&row[j], v, 16);
+        }
+        const uint32_t c = lane / (WAVE / NR), r = lane % NR;
+        u32x4 st[NR];
+#pragma unroll
+        for (uint32_t a = 0; a < NR; a++) {
+          const uint32_t sel = (c - a) % NR;
+          u32x4 q = row[0];
+#pragma unroll
+          for (uint32_t j = 1; j < NR; j++) q = sel == j ? row[j] : q;
+          const uint32_t ia = (a + r) % NR;
+          const int src = (int)((WAVE / NR) * ia + lane / NR);
+          u32x4 got;
+          got.x = (uint32_t)__shfl((int)q.x, src);
+          got.y = (uint32_t)__shfl((int)q.y, src);
+          got.z = (uint32_t)__shfl((int)q.z, src);
+          got.w = (uint32_t)__shfl((int)q.w, src);
+#pragma unroll
+          for (uint32_t i = 0; i < NR; i++) st[i] = ia == i ? got : st[i];
+        }
+        u32x4* const base = (u32x4*)(out + K + SF);
+#pragma unroll
+        for (uint32_t i = 0; i < NR; i++) {
+          // with 4-byte values and SF >= 2 the step's last row reaches past index K + 64 L (lane 63's last
+          // value): only its values up to there go out here, the rest are the next step's head
+          if (W == 4 && SF >= 2 && i == NR - 1 && lane == WAVE - 1) {
+            const uint32_t* sp = (const uint32_t*)&st[i];
+#pragma unroll
+            for (uint32_t q = 0; q < 5u - SF; q++) gst((uint32_t*)(base + WAVE * i + lane) + q, sp[q]);
+          } else {
+            gst(base + WAVE * i + lane, st[i]);
+          }
+        }
+      };
+      if (sft == 0) tput(std::integral_constant<uint32_t, 0>{});
+      else if (sft == 1) tput(std::integral_constant<uint32_t, 1>{});
+      else if constexpr (VPC > 2) {
+        if (sft == 2) tput(std::integral_constant<uint32_t, 2>{});
+        else tput(std::integral_constant<uint32_t, 3>{});
+      }
+      if constexpr (W == 4) carry += rdl((uint32_t)x, 63);
+      else carry += (uint64_t)rdl((uint32_t)x, 63) | ((uint64_t)rdl((uint32_t)(x >> 32), 63) << 32);
+      continue;
     }
     if (lane_in) {
       const bool last_lane = g + 1u >= n_seg || lane == WAVE - 1u;

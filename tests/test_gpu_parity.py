@@ -213,6 +213,18 @@ def test_delta(decoder, ptype, kind):
     run_both(decoder, [make(ptype, vals, abi.DELTA_BINARY_PACKED, page_rows=20000)])
 
 
+@pytest.mark.parametrize("ptype", [abi.INT32, abi.INT64])
+@pytest.mark.parametrize("page_rows", [20001, 20003, 513, 1023])
+def test_delta_output_shifts(decoder, ptype, page_rows):
+    # pages of an odd value count start at every output offset mod 16 bytes, so the expansion's
+    # transposed 1 KiB rows run at every shift (4-byte values: 0..3, the last row of a step cut at
+    # lane 63's last value for shifts 2 and 3) and pages of ~1 / ~2 full 512-value steps end in partial ones
+    rng = np.random.default_rng(page_rows)
+    n = 8 * page_rows + 77
+    vals = np.cumsum(rng.integers(-50, 1 << 12, size=n)).astype(np.int64 if ptype == abi.INT64 else np.int32)
+    run_both(decoder, [make(ptype, vals, abi.DELTA_BINARY_PACKED, page_rows=page_rows)])
+
+
 @pytest.mark.parametrize("block,mb", [(128, 4), (64, 8), (256, 8), (512, 8), (32, 1), (8, 1),
                                       (192, 3), (24, 3), (320, 5),
                                       # block-by-block path: > 512 values or > 8 miniblocks (DuckDB: 2048 / 8)

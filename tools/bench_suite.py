@@ -16,6 +16,7 @@ bench.py prints the ONE headline line (C2). This suite times the other configs a
   str_dict_16k   str_dict with a 16,384-entry dictionary (past the LDS-staged dictionary-direct path)
   bss_f64        BYTE_STREAM_SPLIT doubles
   delta_i64      DELTA_BINARY_PACKED int64 random walk
+  delta_i32      DELTA_BINARY_PACKED int32 random walk
   delta_i64_2048 the same values with 2048-value blocks of 8 miniblocks (DuckDB's writer; the block-by-block path)
   (on request) c2_snappy / c2_zstd / c2_lz4 / c2_gzip and plain_i64_{snappy,zstd,lz4,gzip}: the headline
                  pages or an int64 random walk compressed with each codec (decompression timed alone too)
@@ -114,6 +115,9 @@ def gen(name, rows):
     if name == "delta_i64":
         walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
         return WL.Workload(name, [writer.write_column_chunk(abi.INT64, walk, abi.DELTA_BINARY_PACKED)], [E(walk)])
+    if name == "delta_i32":  # int32 random walk (the 4-byte DELTA path: 32-bit unpack, sums and scan)
+        walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int32)
+        return WL.Workload(name, [writer.write_column_chunk(abi.INT32, walk, abi.DELTA_BINARY_PACKED)], [E(walk)])
     if name == "delta_i64_2048":  # the same values in DuckDB's DELTA configuration (blocks of 2048, 8 miniblocks)
         walk = np.cumsum(rng.integers(-100, 1000, size=rows)).astype(np.int64)
         return WL.Workload(name, [writer.write_column_chunk(abi.INT64, walk, abi.DELTA_BINARY_PACKED, delta_block=2048,
@@ -317,7 +321,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("workloads", nargs="*", default=["c1_plain_i32", "c2_zipf2", "c3_mixed", "c5_levels", "str_plain",
                                                      "str_dict", "str_dict_opt", "str_dict_16k", "str_dlba", "str_dba",
-                                                     "bss_f64", "delta_i64",
+                                                     "bss_f64", "delta_i64", "delta_i32",
                                                      "delta_i64_2048"])
     ap.add_argument("--rows", type=int, default=None, help="override the per-workload row count")
     ap.add_argument("--steps", type=int, default=10)
@@ -328,7 +332,7 @@ def main():
     args = ap.parse_args()
     default_rows = {"c1_plain_i32": 1_000_000, "c2_zipf2": 100_000_000, "c3_mixed": 100_000_000,
                     "c5_levels": 100_000_000, "str_plain": 20_000_000, "str_dict": 20_000_000,
-                    "str_dlba": 20_000_000, "str_dba": 20_000_000, "bss_f64": 100_000_000, "delta_i64": 100_000_000,
+                    "str_dlba": 20_000_000, "str_dba": 20_000_000, "bss_f64": 100_000_000, "delta_i64": 100_000_000, "delta_i32": 100_000_000,
                     "delta_i64_2048": 100_000_000,
                     "c2_snappy": 100_000_000, "plain_i64_snappy": 100_000_000,
                     "c2_zstd": 100_000_000, "plain_i64_zstd": 100_000_000,
