@@ -14,6 +14,7 @@ bench.py prints the ONE headline line (C2). This suite times the other configs a
   str_plain / str_dict / str_dlba / str_dba   BYTE_ARRAY encodings, 4-32 byte strings
   str_dict_opt   str_dict with 10 % nulls (V1 pages: levels first)
   str_dict_16k   str_dict with a 16,384-entry dictionary (past the LDS-staged dictionary-direct path)
+  plain_f64      PLAIN doubles (required)
   bss_f64        BYTE_STREAM_SPLIT doubles
   delta_i64      DELTA_BINARY_PACKED int64 random walk
   delta_i32      DELTA_BINARY_PACKED int32 random walk
@@ -85,6 +86,9 @@ def gen(name, rows):
             return WL.Workload(name, [writer.write_column_chunk(abi.BYTE_ARRAY, v, enc)], [E(v)])
         v = writer.BinaryValues.random(rows, 4, 32, seed=5)
         return WL.Workload(name, [writer.write_column_chunk(abi.BYTE_ARRAY, v, enc)], [E(v)])
+    if name == "plain_f64":  # PLAIN doubles, required (k_plain's copy)
+        v = rng.standard_normal(rows)
+        return WL.Workload(name, [writer.write_column_chunk(abi.DOUBLE, v, abi.PLAIN)], [E(v)])
     if name == "bss_f64":
         v = rng.standard_normal(rows)
         return WL.Workload(name, [writer.write_column_chunk(abi.DOUBLE, v, abi.BYTE_STREAM_SPLIT)], [E(v)])
@@ -321,7 +325,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("workloads", nargs="*", default=["c1_plain_i32", "c2_zipf2", "c3_mixed", "c5_levels", "str_plain",
                                                      "str_dict", "str_dict_opt", "str_dict_16k", "str_dlba", "str_dba",
-                                                     "bss_f64", "delta_i64", "delta_i32",
+                                                     "plain_f64", "bss_f64", "delta_i64", "delta_i32",
                                                      "delta_i64_2048"])
     ap.add_argument("--rows", type=int, default=None, help="override the per-workload row count")
     ap.add_argument("--steps", type=int, default=10)
@@ -332,7 +336,7 @@ def main():
     args = ap.parse_args()
     default_rows = {"c1_plain_i32": 1_000_000, "c2_zipf2": 100_000_000, "c3_mixed": 100_000_000,
                     "c5_levels": 100_000_000, "str_plain": 20_000_000, "str_dict": 20_000_000,
-                    "str_dlba": 20_000_000, "str_dba": 20_000_000, "bss_f64": 100_000_000, "delta_i64": 100_000_000, "delta_i32": 100_000_000,
+                    "str_dlba": 20_000_000, "str_dba": 20_000_000, "bss_f64": 100_000_000, "plain_f64": 100_000_000, "delta_i64": 100_000_000, "delta_i32": 100_000_000,
                     "delta_i64_2048": 100_000_000,
                     "c2_snappy": 100_000_000, "plain_i64_snappy": 100_000_000,
                     "c2_zstd": 100_000_000, "plain_i64_zstd": 100_000_000,
