@@ -76,7 +76,16 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
         }
       } else {
         uint32_t* o = (uint32_t*)out + 2 * i0;
-        if (i0 + 4 <= n && ((uintptr_t)o & 15u) == 0) {
+        const uint32_t ib = i0 - 4u * lane;  // the wave's first value this step (uniform)
+        if (ib + 4u * WAVE <= n && ((uintptr_t)out & 15u) == 0) {
+          // a full step: the lanes' 32-byte runs exchanged so that each store writes 1 KiB contiguous
+          const u32x4 row[2] = {u32x4{lo[0], hi[0], lo[1], hi[1]}, u32x4{lo[2], hi[2], lo[3], hi[3]}};
+          u32x4 st[2];
+          lane_rows_to_tiles<2>(row, st);
+          u32x4* const base = (u32x4*)((uint32_t*)out + 2 * ib);
+          gst_nt(base + lane, st[0]);
+          gst_nt(base + WAVE + lane, st[1]);
+        } else if (i0 + 4 <= n && ((uintptr_t)o & 15u) == 0) {
           gst_nt((u32x4*)o, u32x4{lo[0], hi[0], lo[1], hi[1]});
           gst_nt((u32x4*)(o + 4), u32x4{lo[2], hi[2], lo[3], hi[3]});
         } else {

@@ -143,6 +143,37 @@ __device__ __forceinline__ void gst_nt(T* p, T v) {
   PQG_STORE_GUARD __builtin_nontemporal_store(v, (__attribute__((address_space(1))) T*)p);
 }
 
+// Lane-contiguous runs -> 1 KiB per store instruction. Lane l holds NR consecutive 16-byte rows of a
+// wave's contiguous output (rows NR l .. NR l + NR - 1); on return st[i] holds row 64 i + l, so store
+// i of the wave writes 1 KiB contiguous. (Each lane writing its own NR rows puts every instruction's 64
+// rows NR * 16 bytes apart: 4 rows per lane stored at ~3.6 TB/s against 5.4-6.2 for 1 KiB per
+// instruction, profiles/r02/store_patterns.txt 'lane-contig'.) Round a of NR: lane m (r = m % NR)
+// fetches for store (a + r) % NR from lane (64 / NR) * ((a + r) % NR) + m / NR, which offers its row
+// (c - a) % NR, c = its lane / (64 / NR): every lane is read by exactly one lane per round
+// (4 ds_bpermute_b32 per round). All 64 lanes must be active.
+template <uint32_t NR>
+__device__ __forceinline__ void lane_rows_to_tiles(const u32x4 (&row)[NR], u32x4 (&st)[NR]) {
+  static_assert(NR == 2 || NR == 4, "2 or 4 rows per lane");
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t c = lane / (64u / NR), r = lane % NR;
+#pragma unroll
+  for (uint32_t a = 0; a < NR; a++) {
+    const uint32_t sel = (c - a) % NR;
+    u32x4 q = row[0];
+#pragma unroll
+    for (uint32_t j = 1; j < NR; j++) q = sel == j ? row[j] : q;
+    const uint32_t ia = (a + r) % NR;
+    const int src = (int)((64u / NR) * ia + lane / NR);
+    u32x4 got;
+    got.x = (uint32_t)__shfl((int)q.x, src);
+    got.y = (uint32_t)__shfl((int)q.y, src);
+    got.z = (uint32_t)__shfl((int)q.z, src);
+    got.w = (uint32_t)__shfl((int)q.w, src);
+#pragma unroll
+    for (uint32_t i = 0; i < NR; i++) st[i] = ia == i ? got : st[i];
+  }
+}
+
 // Store the 16-byte output block at `a` (dwords wd) clipped to [o_lo, o_hi): one 16-byte store
 // when the block is whole and aligned, dword stores for whole dwords, byte stores at the edges
 // (which neighbouring chunks / pages share). have: bit q = dword q whole (0 for an unaligned dst).

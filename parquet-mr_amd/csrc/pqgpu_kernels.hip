@@ -3087,13 +3087,11 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
       u[L + 1] = u[L + 2] = 0;
     }
     // A full step (64 lanes, its 16-byte rows inside the output): the rows are exchanged between lanes so
-    // that every store instruction writes 1 KiB contiguous. Lane-contiguous runs (each lane 64 bytes, four
-    // 16-byte stores 64 bytes apart) store at ~3.6 TB/s (profiles/r02/store_patterns.txt 'lane-contig');
-    // the same step with 1 KiB per instruction took delta_i64 0.335 -> 0.245 ms (profiles/r06/delta_tstore).
-    // Row r of the step holds values [K + sft + VPC r, + VPC); lane l's run is rows NR l .. NR l + NR - 1;
-    // instruction i of lane m stores row 64 i + m. Round a of NR: lane m (r = m % NR) fetches for
-    // instruction (a + r) % NR from lane (64 / NR) * ((a + r) % NR) + m / NR, which offers its row
-    // (c - a) % NR (c = its lane / (64 / NR)): every source is read by one lane per round (ds_bpermute).
+    // that every store instruction writes 1 KiB contiguous (lane_rows_to_tiles). Lane-contiguous runs (each
+    // lane 64 bytes, four 16-byte stores 64 bytes apart) store at ~3.6 TB/s (profiles/r02/store_patterns.txt
+    // 'lane-contig'); the same step with 1 KiB per instruction took delta_i64 0.335 -> 0.245 ms
+    // (profiles/r06/delta_tstore). Row r of the step holds values [K + sft + VPC r, + VPC); lane l's run is
+    // rows NR l .. NR l + NR - 1; store i of lane m writes row 64 i + m.
     const uint64_t K = (uint64_t)blk_first - 1u + (uint64_t)L * g0;  // value index of lane 0's u[0]
     if (wide && g0 + WAVE <= n_seg && K + sft + (uint64_t)WAVE * L <= n_out) {
       if (lane == 0)  // the sft values before the first row
@@ -3110,24 +3108,8 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
           for (uint32_t q = 0; q < VPC; q++) v[q] = u[SF + VPC * j + q];
           __builtin_memcpy(&row[j], v, 16);
         }
-        const uint32_t c = lane / (WAVE / NR), r = lane % NR;
         u32x4 st[NR];
-#pragma unroll
-        for (uint32_t a = 0; a < NR; a++) {
-          const uint32_t sel = (c - a) % NR;
-          u32x4 q = row[0];
-#pragma unroll
-          for (uint32_t j = 1; j < NR; j++) q = sel == j ? row[j] : q;
-          const uint32_t ia = (a + r) % NR;
-          const int src = (int)((WAVE / NR) * ia + lane / NR);
-          u32x4 got;
-          got.x = (uint32_t)__shfl((int)q.x, src);
-          got.y = (uint32_t)__shfl((int)q.y, src);
-          got.z = (uint32_t)__shfl((int)q.z, src);
-          got.w = (uint32_t)__shfl((int)q.w, src);
-#pragma unroll
-          for (uint32_t i = 0; i < NR; i++) st[i] = ia == i ? got : st[i];
-        }
+        lane_rows_to_tiles<NR>(row, st);
         u32x4* const base = (u32x4*)(out + K + SF);
 #pragma unroll
         for (uint32_t i = 0; i < NR; i++) {
