@@ -30,8 +30,10 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
                                                   const ColumnDev* __restrict__ cols,
                                                   const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                                   ErrCount err_count) {
-  const int page = wave_page(list, n_list);
+  // a workgroup per page, its waves interleaved over the page's 256-value steps
+  const int page = (int)blockIdx.x < n_list ? list[blockIdx.x] : -1;
   if (page < 0) return;
+  const uint32_t part = wave_id();
   const PageWork pw = work[page];
   const ColumnDev& cd = cols[pw.column];
   const uint32_t lane = lane_id();
@@ -39,20 +41,20 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
   const uint32_t beg = uni(pw.data_begin), end = uni(pw.size);
   const uint32_t avail = end > beg ? end - beg : 0;
   if (W == 0 || avail % W != 0 || pw.num_slots < avail / W) {
-    if (lane == 0) report(err, err_count, page, 0, 2, PQG_ERR_CORRUPT);
+    if (lane == 0 && part == 0) report(err, err_count, page, 0, 2, PQG_ERR_CORRUPT);
     return;
   }
   const uint32_t count = avail / W;
   uint32_t n = uni(pw.n_values);
   if (n > count) {
-    if (lane == 0) report(err, err_count, page, 2, count, PQG_ERR_EOF);
+    if (lane == 0 && part == 0) report(err, err_count, page, 2, count, PQG_ERR_EOF);
     n = count;
   }
   const rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
   uint8_t* out = (uint8_t*)cd.values + pw.out_offset * W;
   if (W == 4 || W == 8) {
     // lane: values [i0, i0 + 4); stream k -> one dword holding byte k of those 4 values
-    for (uint32_t i0 = 4u * lane; i0 < n; i0 += 4u * WAVE) {
+    for (uint32_t i0 = 4u * (lane + WAVE * part); i0 < n; i0 += 4u * WAVE * WPB) {
       uint32_t d[8];
 #pragma unroll
       for (uint32_t k = 0; k < 8; k++) d[k] = k < W ? ld4_any(rs, beg + k * count + i0) : 0u;
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bss(const uint8_t* __restrict__ by
   } else {
     // FIXED_LEN_BYTE_ARRAY of any width: one output byte per lane and step
     const uint64_t nb = (uint64_t)n * W;
-    for (uint64_t o = lane; o < nb; o += WAVE) {
+    for (uint64_t o = lane + WAVE * part; o < nb; o += WAVE * WPB) {
       const uint32_t i = (uint32_t)(o / W), k = (uint32_t)(o % W);
       const uint32_t a = beg + k * count + i;
       gst(out + o, (uint8_t)(ld32(rs, a & ~3u) >> ((a & 3u) * 8u)));
@@ -2746,7 +2748,7 @@ __global__ __launch_bounds__(256) void k_bin_bases(PageWork* __restrict__ work, 
 hipError_t launch_bss(hipStream_t st, const uint8_t* bytes, uint64_t n_bytes, PageWork* work, const ColumnDev* cols,
                       const int32_t* list, int n, uint64_t* err, ErrCount err_count) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_bss, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_BIN_ARGS);
+  hipLaunchKernelGGL(k_bss, dim3(n), dim3(64 * WPB), 0, st, PQG_BIN_ARGS);  // a workgroup per page
   return hipGetLastError();
 }
 

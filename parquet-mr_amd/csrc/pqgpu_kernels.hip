@@ -2641,12 +2641,16 @@ __global__ __launch_bounds__(256) void k_scan_offsets(PageWork* __restrict__ wor
 // PLAIN fixed width (PlainValuesReader / FixedLenByteArrayPlainValuesReader):
 // byte copy of n_values * W bytes from the data section, EOF at the first
 // value that does not fit.
+// A workgroup per page, its WPB waves interleaved over the page's 1 KiB rows (wave w: rows w, w + WPB, ...):
+// with one wave per page a page of 160 KB was one wave's serial copy (a load, its wait and a 1 KiB store per
+// row), and C5's 14,224 pages took two uneven rounds of the resident waves.
 __global__ __launch_bounds__(64 * WPB) void k_plain(const uint8_t* __restrict__ bytes, uint64_t n_bytes,
                                               const PageWork* __restrict__ work, const ColumnDev* __restrict__ cols,
                                               const int32_t* __restrict__ list, int n_list, uint64_t* err,
                                               ErrCount err_count) {
-  const int page = wave_page(list, n_list);
+  const int page = (int)blockIdx.x < n_list ? list[blockIdx.x] : -1;
   if (page < 0) return;
+  const uint32_t part = wave_id();
   const PageWork pw = work[page];
   const ColumnDev cd = cols[pw.column];
   const uint32_t lane = lane_id();
@@ -2656,7 +2660,7 @@ __global__ __launch_bounds__(64 * WPB) void k_plain(const uint8_t* __restrict__ 
   const uint32_t avail = end > beg ? end - beg : 0;
   if ((uint64_t)n * W > avail) {
     uint32_t fit = avail / W;
-    if (lane == 0) report(err, err_count, page, 2, fit, PQG_ERR_EOF);
+    if (lane == 0 && part == 0) report(err, err_count, page, 2, fit, PQG_ERR_EOF);
     n = fit;
   }
   rsrc_t rs = make_rsrc(bytes + pw.base, n_bytes - pw.base);
@@ -2667,15 +2671,16 @@ __global__ __launch_bounds__(64 * WPB) void k_plain(const uint8_t* __restrict__ 
   const uintptr_t d0 = (uintptr_t)dst, d1 = d0 + nb;
   const uintptr_t a0 = (d0 + 15u) & ~(uintptr_t)15u, a1 = d1 & ~(uintptr_t)15u;
   if (a0 >= a1) {  // tiny: bytewise
-    for (uint64_t i = lane; i < nb; i += WAVE) gst(dst + i, (uint8_t)(ld32(rs, (src0 + (uint32_t)i) & ~3u) >> (((src0 + (uint32_t)i) & 3u) * 8u)));
+    if (part == 0)
+      for (uint64_t i = lane; i < nb; i += WAVE) gst(dst + i, (uint8_t)(ld32(rs, (src0 + (uint32_t)i) & ~3u) >> (((src0 + (uint32_t)i) & 3u) * 8u)));
     return;
   }
   const uint32_t head = (uint32_t)(a0 - d0), tail = (uint32_t)(d1 - a1);
-  if (lane < head) {
+  if (part == 0 && lane < head) {
     uint32_t o = src0 + lane;
     gst(dst + lane, (uint8_t)(ld32(rs, o & ~3u) >> ((o & 3u) * 8u)));
   }
-  if (lane < tail) {
+  if (part == 0 && lane < tail) {
     uint64_t i = (a1 - d0) + lane;
     uint32_t o = src0 + (uint32_t)i;
     gst(dst + i, (uint8_t)(ld32(rs, o & ~3u) >> ((o & 3u) * 8u)));
@@ -2684,7 +2689,7 @@ __global__ __launch_bounds__(64 * WPB) void k_plain(const uint8_t* __restrict__ 
   const uint64_t nchunks = (a1 - a0) >> 4;
   const uint32_t sbase = src0 + head;           // source offset of the first aligned chunk
   const uint32_t mis = sbase & 3u;
-  for (uint64_t c = lane; c < nchunks; c += WAVE) {
+  for (uint64_t c = WAVE * part + lane; c < nchunks; c += WAVE * WPB) {
     uint32_t so = sbase + (uint32_t)(c << 4);
     v4 v;
     if (mis == 0) {
@@ -3885,7 +3890,7 @@ hipError_t launch_plain(int kind, hipStream_t st, const uint8_t* bytes, uint64_t
   if (n <= 0) return hipSuccess;
   if (kind == 1) hipLaunchKernelGGL(k_plain_bool, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
   else if (kind == 2) hipLaunchKernelGGL(k_rle_bool, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
-  else hipLaunchKernelGGL(k_plain, dim3((n + WPB - 1) / WPB), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);
+  else hipLaunchKernelGGL(k_plain, dim3(n), dim3(64 * WPB), 0, st, PQG_LAUNCH_ARGS);  // a workgroup per page
   return hipGetLastError();
 }
 
