@@ -126,83 +126,125 @@ __global__ __launch_bounds__(ASM_SCAN_THREADS) void k_asm_scan(uint64_t* __restr
 // the ends shared with the neighbouring blocks; offsets: int64 runs).
 constexpr uint64_t ASM_AGG = 1ull << 62, ASM_INC = 2ull << 62, ASM_VAL = (1ull << 62) - 1ull;
 
-__global__ __launch_bounds__(256) void k_asm_onepass(const uint8_t* __restrict__ def, const uint8_t* __restrict__ rep,
+// MD: repetition depths the kernel tracks (max_rep + 1 <= MD; 2, 4 or 8): per-thread counts, indexes and the
+// packed per-slot entry masks sized for it, so a flat LIST column (max_rep 1) runs at 8 workgroups per CU;
+// the offsets image holds 32-bit block-relative counts (16 KiB of LDS: the 64-bit image's 32 KiB and 97
+// VGPRs allowed 4 workgroups per CU). The look-back reads every depth's status word of a predecessor in one
+// round trip (one loop over 64 predecessors for all depths, where each depth had its own loop).
+// threads of a one-pass workgroup (8 waves, 8,192 slots): C5 assembly 0.94 ms at 4 waves / 4,096 slots, 0.76 ms
+// here, 1.08 ms at 16 waves / 16,384 slots (profiles/r06/asm_blocks)
+constexpr uint32_t ASM1_THREADS = 512;
+constexpr uint32_t ASM1_BLOCK = ASM1_THREADS * ASM_PER_THREAD;  // slots per one-pass block
+constexpr uint32_t ASM1_WAVES = ASM1_THREADS / 64;
+template <uint32_t MD>
+__global__ __launch_bounds__(ASM1_THREADS) void k_asm_onepass(const uint8_t* __restrict__ def, const uint8_t* __restrict__ rep,
                                                      uint64_t n, AsmParams P, uint64_t* status, uint32_t* ticket,
                                                      uint64_t* __restrict__ totals, uint32_t n_blocks) {
-  __shared__ uint32_t wsum[4][ASM_MAX_DEPTHS];
-  __shared__ uint64_t bc[ASM_MAX_DEPTHS];
+  static_assert(MD == 2 || MD == 4 || MD == 8, "depth classes");
+  constexpr uint32_t MB = MD <= 4 ? 4u : 8u;            // mask bits per slot in the packed masks
+  constexpr uint32_t NMK = (ASM_PER_THREAD * MB) / 64u;  // 64-bit words of packed masks
+  __shared__ uint32_t wsum[ASM1_WAVES][MD];
+  __shared__ uint64_t bc[MD];
   __shared__ uint32_t blk_s;
-  __shared__ uint64_t img[ASM_BLOCK];  // 32 KiB: one node's entries of this block
+  __shared__ uint32_t img[ASM1_BLOCK];  // 32 KiB: one node's entries of this block (validity bytes / relative offsets)
   if (threadIdx.x == 0) blk_s = atomicAdd(ticket, 1u);
   __syncthreads();
   const uint32_t blk = blk_s;
-  const uint64_t s0 = (uint64_t)blk * ASM_BLOCK + (uint64_t)threadIdx.x * ASM_PER_THREAD;
+  const uint32_t max_rep = P.max_rep;
+  const uint64_t s0 = (uint64_t)blk * ASM1_BLOCK + (uint64_t)threadIdx.x * ASM_PER_THREAD;
   uint32_t dw[4], rw[4];
   asm_load16(def, s0, n, dw);
   asm_load16(rep, s0, n, rw);
-  uint32_t mk[ASM_PER_THREAD];
-  uint32_t c[ASM_MAX_DEPTHS] = {};
+  uint64_t mkp[NMK] = {};
+  uint32_t c[MD] = {};
 #pragma unroll
   for (uint32_t j = 0; j < ASM_PER_THREAD; j++) {
-    mk[j] = s0 + j < n ? asm_entries_mask(P, byte_of(dw, j), byte_of(rw, j)) : 0u;
+    const uint32_t m = s0 + j < n ? asm_entries_mask(P, byte_of(dw, j), byte_of(rw, j)) : 0u;
+    mkp[(j * MB) / 64u] |= (uint64_t)m << ((j * MB) % 64u);
 #pragma unroll
-    for (uint32_t q = 0; q < ASM_MAX_DEPTHS; q++) c[q] += (mk[j] >> q) & 1u;
+    for (uint32_t q = 0; q < MD; q++) c[q] += (m >> q) & 1u;
   }
+  auto mk = [&](uint32_t j) -> uint32_t { return (uint32_t)(mkp[(j * MB) / 64u] >> ((j * MB) % 64u)) & ((1u << MB) - 1u); };
   // block-local exclusive index of this thread's first entry of every depth, block totals
-  uint32_t li[ASM_MAX_DEPTHS], bt[ASM_MAX_DEPTHS];
+  uint32_t li[MD], bt[MD];
 #pragma unroll
-  for (uint32_t q = 0; q < ASM_MAX_DEPTHS; q++) {
+  for (uint32_t q = 0; q < MD; q++) {
     uint32_t tot = 0;
-    li[q] = q <= P.max_rep ? wave_excl_scan_u32(c[q], &tot) : 0u;
+    li[q] = q <= max_rep ? wave_excl_scan_u32(c[q], &tot) : 0u;
     if (lane_id() == 0) wsum[threadIdx.x >> 6][q] = tot;
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t q = 0; q < ASM_MAX_DEPTHS; q++) {
+  for (uint32_t q = 0; q < MD; q++) {
     uint32_t pre = 0;
     for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) pre += wsum[w][q];
     li[q] += pre;
-    bt[q] = wsum[0][q] + wsum[1][q] + wsum[2][q] + wsum[3][q];
+    uint32_t t = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < ASM1_WAVES; w++) t += wsum[w][q];
+    bt[q] = t;
   }
-  // publish this block's counts, then look back (wave 0): per depth, 64 predecessors per step, one
-  // lane each; the nearest one holding an inclusive count ends the look-back, the aggregates of those
-  // nearer are added (the decoupled look-back of a single-pass scan; a step is one round trip to
-  // memory for 64 blocks, where one predecessor per step made the block chain a serial walk)
-  if (threadIdx.x <= P.max_rep)
-    sst(status + (uint64_t)blk * ASM_MAX_DEPTHS + threadIdx.x, (blk == 0 ? ASM_INC : ASM_AGG) | (uint64_t)bt_at(bt, threadIdx.x));
+  auto bt_q = [&](uint32_t q) -> uint32_t {
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t d = 0; d < MD; d++) v = d == q ? bt[d] : v;
+    return v;
+  };
+  // publish this block's counts, then look back (wave 0): 64 predecessors per step, one lane each, every
+  // depth's status word of a predecessor loaded in the same round trip; per depth the nearest predecessor
+  // holding an inclusive count ends its look-back, the aggregates of those nearer are added (the decoupled
+  // look-back of a single-pass scan)
+  if (threadIdx.x <= max_rep)
+    sst(status + (uint64_t)blk * ASM_MAX_DEPTHS + threadIdx.x, (blk == 0 ? ASM_INC : ASM_AGG) | (uint64_t)bt_q(threadIdx.x));
   if (threadIdx.x < WAVE) {
     const uint32_t lane = lane_id();
-    for (uint32_t q = 0; q <= P.max_rep; q++) {
-      uint64_t excl = 0;
-      int64_t j0 = (int64_t)blk - 1;  // nearest predecessor of the current step
-      const uint64_t t_wait = __builtin_amdgcn_s_memrealtime();
-      while (j0 >= 0) {
-        const int64_t j = j0 - (int64_t)lane;
-        const uint64_t v = j >= 0 ? sld(status + (uint64_t)j * ASM_MAX_DEPTHS + q) : ASM_INC;
-        const uint64_t inc = __ballot((v & ASM_INC) != 0);
-        const uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : WAVE;  // nearest inclusive (lane)
-        const uint64_t upto = first == WAVE ? ~0ull : ((2ull << first) - 1ull);
-        if (__ballot(v == 0) & upto) {  // a block up to it has not published yet: read the window again
-          __builtin_amdgcn_s_sleep(1);
-          // bounded (2 s of s_memrealtime): a block that never publishes leaves a wrong count, not a hang
-          if (__builtin_amdgcn_s_memrealtime() - t_wait > 200000000ull) {
-            if (lane == 0) totals[ASM_MAX_DEPTHS - 1] = ~0ull;  // flagged to the host as a timeout
-            break;
-          }
-          continue;
+    uint64_t excl[MD] = {};
+    uint32_t open = (1u << (max_rep + 1u)) - 1u;  // depths still looking back (uniform)
+    int64_t j0 = (int64_t)blk - 1;                 // nearest predecessor of the current step
+    const uint64_t t_wait = __builtin_amdgcn_s_memrealtime();
+    while (open && j0 >= 0) {
+      const int64_t j = j0 - (int64_t)lane;
+      uint64_t v[MD];
+#pragma unroll
+      for (uint32_t q = 0; q < MD; q++)
+        v[q] = ((open >> q) & 1u) ? (j >= 0 ? sld(status + (uint64_t)j * ASM_MAX_DEPTHS + q) : ASM_INC) : ASM_INC;
+      bool again = false;
+      uint32_t first[MD];
+#pragma unroll
+      for (uint32_t q = 0; q < MD; q++) {
+        const uint64_t inc = __ballot((v[q] & ASM_INC) != 0);
+        first[q] = inc ? (uint32_t)__builtin_ctzll(inc) : WAVE;  // nearest inclusive (lane)
+        const uint64_t upto = first[q] == WAVE ? ~0ull : ((2ull << first[q]) - 1ull);
+        if (((open >> q) & 1u) && (__ballot(v[q] == 0) & upto)) again = true;  // not published yet
+      }
+      if (again) {  // a block up to a depth's nearest inclusive one has not published: read the window again
+        __builtin_amdgcn_s_sleep(1);
+        // bounded (2 s of s_memrealtime): a block that never publishes leaves a wrong count, not a hang
+        if (__builtin_amdgcn_s_memrealtime() - t_wait > 200000000ull) {
+          if (lane == 0) totals[ASM_MAX_DEPTHS - 1] = ~0ull;  // flagged to the host as a timeout
+          break;
         }
-        uint64_t x = lane <= first || first == WAVE ? (v & ASM_VAL) : 0ull;
+        continue;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < MD; q++) {
+        if (!((open >> q) & 1u)) continue;
+        uint64_t x = lane <= first[q] || first[q] == WAVE ? (v[q] & ASM_VAL) : 0ull;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
-        excl += x;
-        if (first < WAVE) break;
-        j0 -= WAVE;
+        excl[q] += x;
+        if (first[q] < WAVE) open &= ~(1u << q);
       }
-      if (lane == 0) {
-        const uint32_t agg = bt_at(bt, q);
-        if (blk > 0) sst(status + (uint64_t)blk * ASM_MAX_DEPTHS + q, ASM_INC | (excl + agg));
-        bc[q] = excl;
-        if (blk == n_blocks - 1u) totals[q] = excl + agg;
+      j0 -= WAVE;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (uint32_t q = 0; q < MD; q++) {
+        if (q > max_rep) break;
+        const uint32_t agg = bt_q(q);
+        if (blk > 0) sst(status + (uint64_t)blk * ASM_MAX_DEPTHS + q, ASM_INC | (excl[q] + agg));
+        bc[q] = excl[q];
+        if (blk == n_blocks - 1u) totals[q] = excl[q] + agg;
       }
     }
   }
@@ -211,28 +253,34 @@ __global__ __launch_bounds__(256) void k_asm_onepass(const uint8_t* __restrict__
     for (uint32_t k = 0; k < P.n_nodes; k++)
       if (P.kind[k] == PQG_REPEATED && P.offsets[k]) {
         const uint32_t d = P.depth[k];
-        gst(P.offsets[k] + bc[d - 1] + bt_at(bt, d - 1), (int64_t)(bc[d] + bt_at(bt, d)));
+        gst(P.offsets[k] + bc[d - 1] + bt_q(d - 1), (int64_t)(bc[d] + bt_q(d)));
       }
   }
   uint8_t* img8 = (uint8_t*)img;
   for (uint32_t k = 0; k < P.n_nodes; k++) {
     const uint32_t q = P.depth[k];
+    uint32_t li_q = 0, li_p = 0;  // this thread's first entry of depth q (and q - 1)
+#pragma unroll
+    for (uint32_t d = 0; d < MD; d++) {
+      li_q = d == q ? li[d] : li_q;
+      li_p = d + 1u == q ? li[d] : li_p;
+    }
     if (P.kind[k] == PQG_OPTIONAL && P.validity[k]) {
       const uint32_t Dk = P.D[k];
-      uint32_t l = li[q];
+      uint32_t l = li_q;
 #pragma unroll
       for (uint32_t j = 0; j < ASM_PER_THREAD; j++)
-        if ((mk[j] >> q) & 1u) img8[l++] = byte_of(dw, j) >= Dk ? 1 : 0;
+        if ((mk(j) >> q) & 1u) img8[l++] = byte_of(dw, j) >= Dk ? 1 : 0;
       __syncthreads();
       // bytes [B, B + cnt) of validity[k]: aligned 16-byte blocks inside (unaligned 32-bit LDS reads of
       // the image), bytes at both ends
       typedef uint32_t __attribute__((aligned(1), may_alias)) u32u;
       uint8_t* g = P.validity[k] + bc[q];
-      const uint32_t cnt = bt_at(bt, q);
+      const uint32_t cnt = bt_q(q);
       const uint32_t mis = (uint32_t)((16u - ((uintptr_t)g & 15u)) & 15u);
       const uint32_t head = mis < cnt ? mis : cnt;
       const uint32_t nd = (cnt - head) >> 4;
-      for (uint32_t i = threadIdx.x; i < nd; i += 256) {
+      for (uint32_t i = threadIdx.x; i < nd; i += ASM1_THREADS) {
         const uint8_t* s = img8 + head + 16u * i;
         gst((u32x4*)(g + head + 16u * i),
             u32x4{*(const u32u*)s, *(const u32u*)(s + 4), *(const u32u*)(s + 8), *(const u32u*)(s + 12)});
@@ -242,28 +290,31 @@ __global__ __launch_bounds__(256) void k_asm_onepass(const uint8_t* __restrict__
       if (threadIdx.x >= 64 && threadIdx.x - 64 < cnt - tail0) gst(g + tail0 + (threadIdx.x - 64), img8[tail0 + (threadIdx.x - 64)]);
       __syncthreads();
     } else if (P.kind[k] == PQG_REPEATED && P.offsets[k]) {
-      // one list per entry of the enclosing depth q - 1: its offset = entries of depth q before the slot
-      uint32_t l = li[q - 1];
-      uint64_t e = bc[q] + li[q];
+      // one list per entry of the enclosing depth q - 1: its offset = entries of depth q before the slot,
+      // kept relative to the block's first entry of depth q (bc[q]) in the image
+      uint32_t l = li_p;
+      uint32_t e = li_q;
 #pragma unroll
       for (uint32_t j = 0; j < ASM_PER_THREAD; j++) {
-        if ((mk[j] >> (q - 1)) & 1u) img[l++] = e;
-        e += (mk[j] >> q) & 1u;
+        if ((mk(j) >> (q - 1)) & 1u) img[l++] = e;
+        e += (mk(j) >> q) & 1u;
       }
       __syncthreads();
+      const uint64_t base = bc[q];
       int64_t* g = P.offsets[k] + bc[q - 1];
-      const uint32_t cnt = bt_at(bt, q - 1);
+      const uint32_t cnt = bt_q(q - 1);
       // pairs as 16-byte stores from the first 16-byte aligned entry on
       const bool al8 = ((uintptr_t)g & 7u) == 0;  // (an int64 array off 8-byte alignment: one entry per store)
       const uint32_t head = (((uintptr_t)g & 15u) != 0 && cnt > 0) ? 1u : 0u;
       const uint32_t np = al8 ? (cnt - head) >> 1 : 0u;
       if (!al8)
-        for (uint32_t i = threadIdx.x; i < cnt; i += 256) gst(g + i, (int64_t)img[i]);
+        for (uint32_t i = threadIdx.x; i < cnt; i += ASM1_THREADS) gst(g + i, (int64_t)(base + img[i]));
       typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
-      for (uint32_t i = threadIdx.x; i < np; i += 256)
-        gst((i64x2*)(g + head + 2u * i), i64x2{(int64_t)img[head + 2u * i], (int64_t)img[head + 2u * i + 1u]});
-      if (al8 && threadIdx.x == 0 && head) gst(g, (int64_t)img[0]);
-      if (al8 && threadIdx.x == 64 && ((cnt - head) & 1u)) gst(g + cnt - 1u, (int64_t)img[cnt - 1u]);
+      for (uint32_t i = threadIdx.x; i < np; i += ASM1_THREADS)
+        gst((i64x2*)(g + head + 2u * i),
+            i64x2{(int64_t)(base + img[head + 2u * i]), (int64_t)(base + img[head + 2u * i + 1u])});
+      if (al8 && threadIdx.x == 0 && head) gst(g, (int64_t)(base + img[0]));
+      if (al8 && threadIdx.x == 64 && ((cnt - head) & 1u)) gst(g + cnt - 1u, (int64_t)(base + img[cnt - 1u]));
       __syncthreads();
     }
   }
@@ -275,8 +326,17 @@ hipError_t launch_assemble(hipStream_t st, const uint8_t* def, const uint8_t* re
     if (n_blocks) hipLaunchKernelGGL(k_asm_count, dim3(n_blocks), dim3(256), 0, st, def, rep, n, P, block_counts);
     hipLaunchKernelGGL(k_asm_scan, dim3(1), dim3(ASM_SCAN_THREADS), 0, st, block_counts, n_blocks, P, totals);
   } else if (n_blocks) {  // outputs (and totals) in one pass; block_counts = zeroed status words, ticket = 0
-    hipLaunchKernelGGL(k_asm_onepass, dim3(n_blocks), dim3(256), 0, st, def, rep, n, P, block_counts, ticket, totals,
-                       n_blocks);
+    // (blocks of ASM1_BLOCK slots: at most the count pass's n_blocks status words are used)
+    const uint32_t n1 = (uint32_t)((n + ASM1_BLOCK - 1) / ASM1_BLOCK);
+    if (P.max_rep < 2u)
+      hipLaunchKernelGGL(k_asm_onepass<2>, dim3(n1), dim3(ASM1_THREADS), 0, st, def, rep, n, P, block_counts, ticket,
+                         totals, n1);
+    else if (P.max_rep < 4u)
+      hipLaunchKernelGGL(k_asm_onepass<4>, dim3(n1), dim3(ASM1_THREADS), 0, st, def, rep, n, P, block_counts, ticket,
+                         totals, n1);
+    else
+      hipLaunchKernelGGL(k_asm_onepass<8>, dim3(n1), dim3(ASM1_THREADS), 0, st, def, rep, n, P, block_counts, ticket,
+                         totals, n1);
   }
   return hipGetLastError();
 }
