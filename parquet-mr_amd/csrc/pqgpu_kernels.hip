@@ -3185,15 +3185,16 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
 template <int W, bool NEG>
 __device__ int delta_generic(DSeg& S, uint32_t p, uint32_t end, uint32_t block, uint32_t mbn, uint32_t mbs,
                              uint32_t total, uint32_t n_out, uint64_t carry, typename DictVal<W>::T* out, int page,
-                             uint64_t* err, ErrCount err_count, uint32_t* p_end) {
+                             uint64_t* err, ErrCount err_count, uint32_t* p_end, uint32_t buffered0 = 1) {
   typedef typename DictVal<W>::T T;
   const uint32_t lane = lane_id();
   auto byte_at = [&](uint32_t a) -> uint32_t {
     if (!S.has(a & ~3u, 4)) S.fill(a);
     return uni((S.w32(a & ~3u) >> (8u * (a & 3u))) & 0xFFu);
   };
-  uint32_t buffered = 1;
-  uint64_t k_next = 1;  // value index after the next delta
+  // (buffered0 > 1: resumed at a block boundary by the batched path, values before it stored)
+  uint32_t buffered = buffered0;
+  uint64_t k_next = buffered0;  // value index after the next delta
   while (true) {
     p = uni(p);
     buffered = uni(buffered);
@@ -3386,7 +3387,10 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
   }
   // register budget of the batched expansion: block <= 512 values, <= 8 miniblocks (parquet-mr
   // and Arrow write 128 / 4); other configurations take the block-by-block path
-  if (block > 512u || mbn > 8u)
+  // (blocks of up to 2,048 values in at most 8 miniblocks of a multiple of 16 deltas — DuckDB writes 2048 / 8 —
+  // take the batched walk and the segment expansion too, whose per-lane work does not depend on the block)
+  const bool seg_big = !NEG && block <= 2048u && mbn <= 8u && (mbs % 16u) == 0 && ((uint64_t)block * W) % 16u == 0;
+  if ((block > 512u || mbn > 8u) && !seg_big)
     return delta_generic<W, NEG>(S, p, end, block, mbn, mbs, total, n_out, carry, out, page, err, err_count, p_end);
   uint32_t buffered = 1;  // Java valuesBuffered (includes the first value)
   uint32_t n_blocks = 0;
@@ -3515,7 +3519,21 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
       buffered = bufd;
       nb++;
     }
-    if (nb == 0) return PQG_ERR_CORRUPT;  // unreachable: the first block of a batch always fits
+    if (nb == 0) {
+      // a block whose data does not fit the segment (only blocks over 512 values: > 4 KiB of deltas): the rest of
+      // the stream block by block, from this block boundary (the values before it are stored)
+      if (block > 512u) {
+        if (S.lo != uni(p & ~15u)) {  // a fresh segment from the block on, then the batch again
+          S.fill(p);
+          continue;
+        }
+        const uint64_t k = (uint64_t)n_blocks * block;
+        if (n_blocks && k < n_out && lane == 0) gst(out + k, (T)carry);  // the value before this block
+        return delta_generic<W, NEG>(S, p, end, block, mbn, mbs, total, n_out, carry, out, page, err, err_count, p_end,
+                                     buffered);
+      }
+      return PQG_ERR_CORRUPT;  // unreachable: a block of at most 512 values always fits
+    }
     // min deltas of the blocks delta_hdr_v walked, one lane per block (the segment holds them: it is
     // refilled only at a batch start)
     if (b_mv) {

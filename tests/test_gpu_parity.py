@@ -225,6 +225,28 @@ def test_delta_output_shifts(decoder, ptype, page_rows):
     run_both(decoder, [make(ptype, vals, abi.DELTA_BINARY_PACKED, page_rows=page_rows)])
 
 
+@pytest.mark.parametrize("ptype", [abi.INT32, abi.INT64])
+@pytest.mark.parametrize("block,mb", [(2048, 8), (1024, 4), (768, 3)])
+@pytest.mark.parametrize("kind", ["walk", "random", "mixed"])
+def test_delta_big_blocks(decoder, ptype, block, mb, kind):
+    # blocks of 513..2048 values take the batched walk and segment expansion while a block's deltas fit the
+    # LDS segment (8 KiB); 64-bit random deltas (16 KiB per 2048-value block) fall back to the block-by-block
+    # path from that block on ("mixed": small deltas first, random ones after, so one page takes both)
+    rng = np.random.default_rng(block + mb)
+    n = 45_001
+    info = np.iinfo(np.int64 if ptype == abi.INT64 else np.int32)
+    if kind == "walk":
+        vals = np.cumsum(rng.integers(-50, 5000, size=n))
+    elif kind == "random":
+        vals = rng.integers(info.min, info.max, size=n, dtype=np.int64)
+    else:
+        vals = np.concatenate([np.cumsum(rng.integers(-50, 5000, size=n // 2)),
+                               rng.integers(info.min, info.max, size=n - n // 2, dtype=np.int64)])
+    vals = vals.astype(np.int64 if ptype == abi.INT64 else np.int32)
+    run_both(decoder, [make(ptype, vals, abi.DELTA_BINARY_PACKED, delta_block=block, delta_miniblocks=mb,
+                            page_rows=15_000)])
+
+
 @pytest.mark.parametrize("block,mb", [(128, 4), (64, 8), (256, 8), (512, 8), (32, 1), (8, 1),
                                       (192, 3), (24, 3), (320, 5),
                                       # block-by-block path: > 512 values or > 8 miniblocks (DuckDB: 2048 / 8)
