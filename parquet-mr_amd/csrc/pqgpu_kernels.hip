@@ -2955,7 +2955,8 @@ __device__ __forceinline__ void delta_expand(const DSeg& S, uint32_t nb, uint32_
 // (loadNewBlockToBuffer :139-142, also for the unread miniblocks of a last block, whose values lie
 // past the count and are not stored) and the store layout are those of delta_expand: lane l stores
 // the L values ending one delta earlier (the first from lane l - 1 / the carry), as wide stores
-// when the run is aligned. Not for NEG streams (DELTA_LENGTH lengths check every value).
+// when the run is aligned. NEG streams (DELTA_LENGTH lengths) check every value of a step that holds a
+// negative one on the per-lane stores.
 // In-place inclusive prefix of a lane's deltas in two independent halves joined at the end (half the
 // dependent adds of one running sum).
 template <class U, uint32_t N>
@@ -2969,11 +2970,14 @@ __device__ __forceinline__ void delta_local_prefix(U (&v)[N]) {
   for (uint32_t q = H; q < N; q++) v[q] += v[H - 1];
 }
 
-template <int W>
+// NEG (DELTA_LENGTH_BYTE_ARRAY lengths): a negative (int) value is reported as CORRUPT at its index and stored
+// as 0; a step holding one takes the per-lane stores, which check every value.
+template <int W, bool NEG = false>
 __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uint32_t b_data, uint32_t b_wpos,
                                                  uint32_t b_lo, uint32_t b_hi, uint32_t b_nmb, uint32_t blk_first,
                                                  uint32_t block, uint32_t mbs, uint32_t n_out, uint64_t& carry,
-                                                 typename DictVal<W>::T* out) {
+                                                 typename DictVal<W>::T* out, int page = 0, uint64_t* err = nullptr,
+                                                 ErrCount err_count = ErrCount{}) {
   typedef typename DictVal<W>::T T;
   // 8 deltas per lane-step (16 measured slower: its 115 VGPRs left 4 waves per SIMD, and 5,000 pages of
   // delta_i64 took 1.2 rounds of them; at 98 VGPRs the LDS segments' 5 waves per SIMD hold every page at
@@ -3098,7 +3102,14 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
     // (profiles/r06/delta_tstore). Row r of the step holds values [K + sft + VPC r, + VPC); lane l's run is
     // rows NR l .. NR l + NR - 1; store i of lane m writes row 64 i + m.
     const uint64_t K = (uint64_t)blk_first - 1u + (uint64_t)L * g0;  // value index of lane 0's u[0]
-    if (wide && g0 + WAVE <= n_seg && K + sft + (uint64_t)WAVE * L <= n_out) {
+    bool neg_any = false;
+    if constexpr (NEG) {
+      bool ln = false;
+#pragma unroll
+      for (uint32_t q = 0; q < L + VPC - 1u; q++) ln |= (int32_t)(uint32_t)u[q] < 0;
+      neg_any = __ballot(lane_in && ln) != 0;
+    }
+    if (wide && (!NEG || !neg_any) && g0 + WAVE <= n_seg && K + sft + (uint64_t)WAVE * L <= n_out) {
       if (lane == 0)  // the sft values before the first row
         for (uint32_t q = 0; q < VPC - 1u; q++)
           if (q < sft) gst(out + K + q, u[q]);
@@ -3141,11 +3152,26 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
     }
     if (lane_in) {
       const bool last_lane = g + 1u >= n_seg || lane == WAVE - 1u;
+      // a checked store (NEG: a negative length is CORRUPT at its index and written as 0)
+      // (value 0, the stream's first value, was checked and stored by delta_stream: never rewritten here)
+      auto put1 = [&](uint64_t k, T v) {
+        if constexpr (NEG) {
+          if (k == 0) return;
+          if ((int32_t)(uint32_t)v < 0) {
+            report(err, err_count, page, 2, k, PQG_ERR_CORRUPT);
+            v = 0;
+          }
+        }
+        gst(out + k, v);
+      };
       if (lane == 0)  // the sft values before lane 0's shifted run
         for (uint32_t q = 0; q < VPC - 1u; q++)
-          if (q < sft && k0 + q < n_out) gst(out + k0 + q, u[q]);
+          if (q < sft && k0 + q < n_out) {
+            if constexpr (NEG) put1(k0 + q, u[q]);
+            else gst(out + k0 + q, u[q]);
+          }
       const uint64_t a = k0 + sft;
-      if (wide && !last_lane && a + L <= n_out) {
+      if (wide && (!NEG || !neg_any) && !last_lane && a + L <= n_out) {
         // v[q] = u[sft + q]: sft is uniform, so a branch per value of it picks the registers statically
         auto put = [&](auto s_tag) {
           constexpr uint32_t SF = decltype(s_tag)::value;
@@ -3165,7 +3191,10 @@ __device__ __forceinline__ void delta_expand_seg(const DSeg& S, uint32_t nb, uin
 #pragma unroll
         for (uint32_t q = 0; q < L + VPC - 1u; q++) {
           const uint64_t k = k0 + q;
-          if (k >= a && k < e && k < n_out) gst(out + k, u[q]);
+          if (k >= a && k < e && k < n_out) {
+            if constexpr (NEG) put1(k, u[q]);
+            else gst(out + k, u[q]);
+          }
         }
       }
     }
@@ -3389,7 +3418,7 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
   // and Arrow write 128 / 4); other configurations take the block-by-block path
   // (blocks of up to 2,048 values in at most 8 miniblocks of a multiple of 16 deltas — DuckDB writes 2048 / 8 —
   // take the batched walk and the segment expansion too, whose per-lane work does not depend on the block)
-  const bool seg_big = !NEG && block <= 2048u && mbn <= 8u && (mbs % 16u) == 0 && ((uint64_t)block * W) % 16u == 0;
+  const bool seg_big = block <= 2048u && mbn <= 8u && (mbs % 16u) == 0 && ((uint64_t)block * W) % 16u == 0;
   if ((block > 512u || mbn > 8u) && !seg_big)
     return delta_generic<W, NEG>(S, p, end, block, mbn, mbs, total, n_out, carry, out, page, err, err_count, p_end);
   uint32_t buffered = 1;  // Java valuesBuffered (includes the first value)
@@ -3528,7 +3557,14 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
           continue;
         }
         const uint64_t k = (uint64_t)n_blocks * block;
-        if (n_blocks && k < n_out && lane == 0) gst(out + k, (T)carry);  // the value before this block
+        if (n_blocks && k < n_out && lane == 0) {  // the value before this block
+          T v = (T)carry;
+          if (NEG && (int32_t)(uint32_t)v < 0) {
+            report(err, err_count, page, 2, k, PQG_ERR_CORRUPT);
+            v = 0;
+          }
+          gst(out + k, v);
+        }
         return delta_generic<W, NEG>(S, p, end, block, mbn, mbs, total, n_out, carry, out, page, err, err_count, p_end,
                                      buffered);
       }
@@ -3544,8 +3580,14 @@ __device__ int delta_stream(DSeg& S, uint32_t p, uint32_t end, uint32_t want, ty
     // ---- expand the walked blocks (every read from the LDS segment)
     // (the segment path stores 16-value runs per lane, shifted to 16-byte alignment: pages of
     // nullable columns, which start at any value offset, take it too)
-    if (!NEG && (mbs % 16u) == 0 && ((uint64_t)block * W) % 16u == 0)
-      delta_expand_seg<W>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out);
+    if ((mbs % 16u) == 0 && ((uint64_t)block * W) % 16u == 0)
+      {
+        if constexpr (NEG)
+          delta_expand_seg<W, NEG>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page,
+                                   err, err_count);
+        else
+          delta_expand_seg<W>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out);
+      }
     else if (E == 1)
       delta_expand<W, NEG, 1>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);
     else if (E == 2) delta_expand<W, NEG, 2>(S, nb, b_data, b_wpos, b_lo, b_hi, b_nmb, blk_first, block, mbs, n_out, carry, out, page, err, err_count);

@@ -114,6 +114,20 @@ def test_binary_errors(decoder, which):
     run_both(decoder, [_err_case(which)], expect_error=True)
 
 
+@pytest.mark.parametrize("k", [0, 1, 700, 4095, 9999])
+def test_dlba_negative_length(decoder, k):
+    """A negative DELTA_LENGTH_BYTE_ARRAY length (in.slice(negative) in readBytes): CORRUPT at its index, the
+    values before it decoded — in the first value, inside and at the end of a 512-length expansion step, and
+    in the page's last value (the length stream's steps take the segment expansion, whose stores check
+    every length of a step that holds a negative one)."""
+    vals = _strings(10_000, 11, 1, 20)
+    ch = make(abi.BYTE_ARRAY, vals, abi.DELTA_LENGTH_BYTE_ARRAY, page_rows=10_000)
+    lens = np.array([len(v) for v in vals], dtype=np.int32)
+    lens[k] = -5
+    ch.pages[0].body = writer.delta_encode(lens, abi.INT32) + b"".join(vals)
+    run_both(decoder, [ch], expect_error=True)
+
+
 @pytest.mark.parametrize("case", ["ascii", "empty", "zeros", "smallints", "random", "long", "optional",
                                   "plain_eof", "plain_negative"])
 def test_binary_plain_per_page(decoder, per_page_dispatch, case):
